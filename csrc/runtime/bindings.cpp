@@ -1,0 +1,261 @@
+// Python bindings of the host runtime (_native): ONNX reader, CPU executor, tree compiler,
+// risk.v1 wire codec, account index, XXH64.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <memory>
+
+#include "account_index.h"
+#include "executor.h"
+#include "onnx_model.h"
+#include "trees.h"
+#include "wire.h"
+#include "xxh64.h"
+
+namespace py = pybind11;
+using namespace igp;
+
+namespace {
+
+py::object attr_value(const onnx::Attribute& a) {
+  switch (a.type) {
+    case onnx::A_FLOAT: return py::float_(a.f);
+    case onnx::A_INT: return py::int_(a.i);
+    case onnx::A_STRING: return py::str(a.s);
+    case onnx::A_FLOATS: return py::array_t<float>(a.floats.size(), a.floats.data());
+    case onnx::A_INTS: return py::array_t<int64_t>(a.ints.size(), a.ints.data());
+    case onnx::A_STRINGS: {
+      py::list l;
+      for (auto& s : a.strings) l.append(py::str(s));
+      return l;
+    }
+    case onnx::A_TENSOR: {
+      if (!a.t) return py::none();
+      std::vector<py::ssize_t> shape(a.t->dims.begin(), a.t->dims.end());
+      if (a.t->dtype == onnx::FLOAT) return py::array_t<float>(shape, a.t->f.data());
+      return py::array_t<int64_t>(shape, a.t->i.data());
+    }
+    default: return py::none();
+  }
+}
+
+py::array tensor_to_np(const onnx::Tensor& t) {
+  std::vector<py::ssize_t> shape(t.dims.begin(), t.dims.end());
+  if (t.dtype == onnx::FLOAT) return py::array_t<float>(shape, t.f.data());
+  return py::array_t<int64_t>(shape, t.i.data());
+}
+
+onnx::Tensor np_to_tensor(const std::string& name, py::array arr) {
+  onnx::Tensor t;
+  t.name = name;
+  for (py::ssize_t d = 0; d < arr.ndim(); ++d) t.dims.push_back(arr.shape(d));
+  if (py::isinstance<py::array_t<int64_t>>(arr) || arr.dtype().kind() == 'i') {
+    auto a = py::array_t<int64_t, py::array::c_style | py::array::forcecast>(arr);
+    t.dtype = onnx::INT64;
+    t.i.assign(a.data(), a.data() + a.size());
+  } else {
+    auto a = py::array_t<float, py::array::c_style | py::array::forcecast>(arr);
+    t.dtype = onnx::FLOAT;
+    t.f.assign(a.data(), a.data() + a.size());
+  }
+  return t;
+}
+
+py::list value_infos(const std::vector<onnx::ValueInfo>& vs) {
+  py::list l;
+  for (auto& v : vs) l.append(py::make_tuple(v.name, v.elem_type, v.dims, v.params));
+  return l;
+}
+
+template <class T>
+py::array_t<T> vec_np(const std::vector<T>& v) { return py::array_t<T>(v.size(), v.data()); }
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "igaming_platform_amd host runtime (C++)";
+
+  m.def("xxh64", [](py::bytes b, uint64_t seed) {
+    std::string s = b;
+    return xxh64(s.data(), s.size(), seed);
+  });
+  m.def("id_hashes", [](const std::vector<std::string>& ids, uint64_t seed) {
+    py::array_t<uint64_t> out(ids.size());
+    auto* o = out.mutable_data();
+    for (size_t k = 0; k < ids.size(); ++k) o[k] = id_hash(ids[k], seed);
+    return out;
+  });
+
+  py::class_<onnx::Model, std::shared_ptr<onnx::Model>>(m, "OnnxModel")
+      .def_static("from_bytes", [](py::bytes b) { return std::make_shared<onnx::Model>(onnx::parse_model(std::string(b))); })
+      .def_static("load", [](const std::string& p) { return std::make_shared<onnx::Model>(onnx::load_model(p)); })
+      .def_readonly("ir_version", &onnx::Model::ir_version)
+      .def_readonly("producer_name", &onnx::Model::producer_name)
+      .def_readonly("opsets", &onnx::Model::opsets)
+      .def_readonly("metadata", &onnx::Model::metadata)
+      .def("inputs", [](const onnx::Model& mm) { return value_infos(mm.graph.inputs); })
+      .def("outputs", [](const onnx::Model& mm) { return value_infos(mm.graph.outputs); })
+      .def("initializer_names", [](const onnx::Model& mm) {
+        std::vector<std::string> n;
+        for (auto& kv : mm.graph.initializers) n.push_back(kv.first);
+        return n;
+      })
+      .def("initializer", [](const onnx::Model& mm, const std::string& name) {
+        auto it = mm.graph.initializers.find(name);
+        if (it == mm.graph.initializers.end()) throw py::key_error(name);
+        return tensor_to_np(it->second);
+      })
+      .def("nodes", [](const onnx::Model& mm) {
+        py::list l;
+        for (auto& n : mm.graph.nodes) {
+          py::dict d, attrs;
+          d["op_type"] = n.op_type;
+          d["domain"] = n.domain;
+          d["name"] = n.name;
+          d["inputs"] = n.inputs;
+          d["outputs"] = n.outputs;
+          for (auto& kv : n.attrs) attrs[py::str(kv.first)] = attr_value(kv.second);
+          d["attrs"] = attrs;
+          l.append(d);
+        }
+        return l;
+      });
+
+  py::class_<exec::Executor, std::shared_ptr<exec::Executor>>(m, "Executor")
+      .def(py::init([](std::shared_ptr<onnx::Model> mm) { return std::make_shared<exec::Executor>(*mm); }))
+      .def("run", [](const exec::Executor& ex, py::dict inputs) {
+        std::map<std::string, onnx::Tensor> in;
+        for (auto item : inputs) {
+          std::string name = py::str(item.first);
+          in[name] = np_to_tensor(name, py::array::ensure(item.second));
+        }
+        std::map<std::string, onnx::Tensor> out;
+        {
+          py::gil_scoped_release rel;
+          out = ex.run(in);
+        }
+        py::dict res;
+        for (auto& kv : out) res[py::str(kv.first)] = tensor_to_np(kv.second);
+        return res;
+      })
+      .def("tree_complete", [](const exec::Executor& ex, size_t node_index, int32_t limit) {
+        const trees::Ensemble* e = ex.ensemble(node_index);
+        if (!e) throw std::runtime_error("node is not a TreeEnsemble");
+        trees::Complete c = trees::to_complete(*e, limit);
+        const int64_t n_int = (int64_t(1) << c.depth) - 1, n_leaf = int64_t(1) << c.depth;
+        py::dict d;
+        d["depth"] = c.depth;
+        d["n_trees"] = c.n_trees;
+        d["k"] = c.k;
+        d["nodes"] = py::array_t<float>({int64_t(c.n_trees), n_int, int64_t(2)}, c.nodes.data());
+        d["leaves"] = py::array_t<float>({int64_t(c.n_trees), n_leaf, int64_t(c.k)}, c.leaves.data());
+        d["base_values"] = vec_np(e->base_values);
+        d["post"] = e->post;
+        d["aggregate"] = e->aggregate;
+        d["classifier"] = e->classifier;
+        d["binary_case"] = e->binary_case;
+        d["binary_class"] = e->binary_class & 1;
+        d["weights_all_positive"] = !(e->binary_class & 0x100);
+        d["n_outputs"] = e->n_outputs;
+        d["max_feature"] = e->max_feature;
+        d["classlabels"] = vec_np(e->classlabels);
+        return d;
+      }, py::arg("node_index"), py::arg("limit") = 12);
+
+  py::class_<wire::RequestBatch, std::shared_ptr<wire::RequestBatch>>(m, "RequestBatch")
+      .def(py::init<>())
+      .def("parse_batch", [](wire::RequestBatch& b, py::bytes data) {
+        char* p; py::ssize_t n;
+        PYBIND11_BYTES_AS_STRING_AND_SIZE(data.ptr(), &p, &n);
+        py::gil_scoped_release rel;
+        wire::parse_batch(p, size_t(n), b);
+      })
+      .def("parse_tx", [](wire::RequestBatch& b, py::bytes data) {
+        char* p; py::ssize_t n;
+        PYBIND11_BYTES_AS_STRING_AND_SIZE(data.ptr(), &p, &n);
+        wire::parse_tx(p, size_t(n), b);
+      })
+      .def("clear", &wire::RequestBatch::clear)
+      .def("__len__", &wire::RequestBatch::size)
+      .def_readonly("account_id", &wire::RequestBatch::account_id)
+      .def("columns", [](const wire::RequestBatch& b) {
+        py::dict d;
+        d["account_hash"] = vec_np(b.account_hash);
+        d["amount"] = vec_np(b.amount);
+        d["tx_type"] = vec_np(b.tx_type);
+        d["device_hash"] = vec_np(b.device_hash);
+        d["fp_hash"] = vec_np(b.fp_hash);
+        d["ip_hash"] = vec_np(b.ip_hash);
+        return d;
+      });
+
+  m.def("tx_type_id", [](const std::string& s) { return int(wire::tx_type_id(s.data(), s.size())); });
+
+  py::class_<AccountIndex, std::shared_ptr<AccountIndex>>(m, "AccountIndex")
+      .def(py::init<int64_t>())
+      .def("lookup_batch", [](AccountIndex& ix, const wire::RequestBatch& b, bool insert) {
+        py::array_t<int32_t> slots(b.size());
+        py::array_t<uint8_t> fresh(b.size());
+        ix.lookup(b.account_id, b.account_hash, insert, slots.mutable_data(), fresh.mutable_data());
+        return py::make_tuple(slots, fresh);
+      })
+      .def("lookup", [](AccountIndex& ix, const std::vector<std::string>& ids, bool insert) {
+        std::vector<uint64_t> h(ids.size());
+        for (size_t k = 0; k < ids.size(); ++k) h[k] = id_hash(ids[k], SEED_ACCOUNT);
+        py::array_t<int32_t> slots(ids.size());
+        py::array_t<uint8_t> fresh(ids.size());
+        ix.lookup(ids, h, insert, slots.mutable_data(), fresh.mutable_data());
+        return py::make_tuple(slots, fresh);
+      }, py::arg("ids"), py::arg("insert") = false)
+      .def("__len__", &AccountIndex::size)
+      .def_property_readonly("capacity", &AccountIndex::capacity)
+      .def("id_of", &AccountIndex::id_of);
+
+  // results: uint32[n,2] (ResultRec), feats: int32[n,32] (FeatRec) or None, ms: int64[n] or None
+  auto view = [](py::array res, py::object feat, py::object ms, wire::ResultView& v,
+                 py::array& keep_r, py::object& keep_f, py::object& keep_m) {
+    keep_r = py::array_t<uint32_t, py::array::c_style | py::array::forcecast>(res);
+    if (keep_r.ndim() != 2 || keep_r.shape(1) != 2) throw std::runtime_error("results must be [n,2] (ResultRec)");
+    v.n = size_t(keep_r.shape(0));
+    v.res = reinterpret_cast<const ResultRec*>(keep_r.data());
+    v.feat = nullptr;
+    v.response_ms = nullptr;
+    if (!feat.is_none()) {
+      auto f = py::array_t<int32_t, py::array::c_style | py::array::forcecast>(feat);
+      if (f.ndim() != 2 || f.shape(1) != 32 || size_t(f.shape(0)) != v.n) throw std::runtime_error("features must be [n,32] (FeatRec)");
+      keep_f = f;
+      v.feat = reinterpret_cast<const FeatRec*>(f.data());
+    }
+    if (!ms.is_none()) {
+      auto t = py::array_t<int64_t, py::array::c_style | py::array::forcecast>(ms);
+      if (size_t(t.size()) != v.n) throw std::runtime_error("response_ms length mismatch");
+      keep_m = t;
+      v.response_ms = t.data();
+    }
+  };
+  m.def("serialize_batch_response", [view](py::array res, py::object feat, py::object ms) {
+    wire::ResultView v;
+    py::array kr; py::object kf, km;
+    view(res, feat, ms, v, kr, kf, km);
+    std::string out;
+    {
+      py::gil_scoped_release rel;
+      out = wire::serialize_batch_response(v);
+    }
+    return py::bytes(out);
+  }, py::arg("results"), py::arg("features") = py::none(), py::arg("response_ms") = py::none());
+  m.def("serialize_tx_response", [view](py::array res, py::object feat, py::object ms, size_t i) {
+    wire::ResultView v;
+    py::array kr; py::object kf, km;
+    view(res, feat, ms, v, kr, kf, km);
+    if (i >= v.n) throw std::runtime_error("index out of range");
+    return py::bytes(wire::serialize_tx_response(v, i));
+  }, py::arg("results"), py::arg("features") = py::none(), py::arg("response_ms") = py::none(), py::arg("index") = 0);
+  m.def("serialize_feature_vector", [](py::array feat) {
+    auto f = py::array_t<int32_t, py::array::c_style | py::array::forcecast>(feat);
+    if (f.size() != 32) throw std::runtime_error("FeatRec must have 32 int32 words");
+    return py::bytes(wire::serialize_feature_vector(*reinterpret_cast<const FeatRec*>(f.data())));
+  });
+}

@@ -1,0 +1,49 @@
+"""Golden HyperLogLog (p = 8) — the spec for the device HLL update/count kernels.
+
+Replaces Redis PFADD/PFCOUNT on ``features:<id>:devices:24h`` / ``ips:24h``
+(``redis_store.go:80-81, 141-152``). Redis' estimator and hash are not reproduced
+bit-for-bit (not observable by clients); the counts agree with the exact distinct
+count within HLL error, and for the cardinalities the rules look at (<= ~20) the
+linear-counting branch is used, which is exact up to register collisions.
+
+Register update: idx = h & 255, w = h >> 8 (56 bits), rank = clz56(w) + 1 (57 if w == 0),
+reg[idx] = max(reg[idx], rank).
+Estimate: E = alpha * m^2 / sum(2^-reg); if E <= 2.5 m and V (zero registers) > 0,
+E = m * ln(m / V). Count = floor(E + 0.5).
+"""
+from __future__ import annotations
+
+import math
+
+P = 8
+M = 1 << P
+ALPHA = 0.7213 / (1.0 + 1.079 / M)
+
+
+def rank_of(h: int) -> int:
+    w = h >> P
+    if w == 0:
+        return 64 - P + 1
+    return (64 - P) - w.bit_length() + 1
+
+
+def add(regs: bytearray, h: int) -> None:
+    if h == 0:
+        return
+    idx = h & (M - 1)
+    r = rank_of(h)
+    if r > regs[idx]:
+        regs[idx] = r
+
+
+def count(regs) -> int:
+    z = 0.0
+    v = 0
+    for r in regs:
+        z += math.ldexp(1.0, -int(r))
+        if r == 0:
+            v += 1
+    e = ALPHA * M * M / z
+    if e <= 2.5 * M and v > 0:
+        e = M * math.log(M / v)
+    return int(math.floor(e + 0.5))

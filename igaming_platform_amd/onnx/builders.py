@@ -1,0 +1,160 @@
+"""Deterministic random-init ONNX models for the five BASELINE configs.
+
+There is no network for trained checkpoints (BASELINE.json: "random-init model weights"),
+so each config's model is generated from a fixed seed with the architecture the config
+names. Input name ``input`` / primary output ``output`` follow ``onnx_model.go:37-38``.
+
+* cfg1 ``logistic``: input[N,32] -> Gemm -> Sigmoid -> output[N,1]
+* cfg2 ``gbdt``:     input[N,128] -> TreeEnsembleClassifier(100 trees, LOGISTIC)
+                      -> label[N], output[N,2]
+* cfg3 ``stacked``:  input[N,128] -> TreeEnsembleRegressor(100 trees, n_targets=32)
+                      -> Gemm(32x256) -> Relu -> Gemm(256x1) -> Sigmoid -> output[N,1]
+* cfg4 ``ltv_mlp``:  input[N,256] -> (Gemm -> Relu) x4 (width 512) -> Gemm -> output[N,1]
+* cfg5 ``gru``:      input[T=100,N,16] -> GRU(256) -> Squeeze -> GRU(256) -> Y_h
+                      -> Reshape[N,256] -> Gemm -> Sigmoid -> output[N,1]
+"""
+from __future__ import annotations
+
+from typing import Dict, List
+
+import numpy as np
+
+from . import schema as S
+from .writer import ML_DOMAIN, model, node, tensor, tree_attrs, value_info
+
+MODES = ["BRANCH_LEQ", "BRANCH_LT", "BRANCH_GTE", "BRANCH_GT"]
+
+
+def random_complete_tree(rng: np.random.Generator, depth: int, n_features: int, k: int,
+                         leaf_scale: float = 0.1, mixed_modes: bool = False,
+                         feature_lo: int = 0) -> Dict[str, np.ndarray]:
+    """Complete binary tree in BFS order: node i has children 2i+1 (true) / 2i+2 (false)."""
+    n_int = (1 << depth) - 1
+    n = (1 << (depth + 1)) - 1
+    feature = np.full(n, -1, np.int64)
+    feature[:n_int] = rng.integers(feature_lo, n_features, n_int)
+    threshold = np.zeros(n, np.float32)
+    threshold[:n_int] = rng.uniform(0.05, 0.95, n_int).astype(np.float32)
+    left = np.zeros(n, np.int64)
+    right = np.zeros(n, np.int64)
+    left[:n_int] = 2 * np.arange(n_int) + 1
+    right[:n_int] = 2 * np.arange(n_int) + 2
+    if mixed_modes:
+        mode = [MODES[i] for i in rng.integers(0, 4, n)]
+    else:
+        mode = ["BRANCH_LEQ"] * n
+    missing = rng.integers(0, 2, n).astype(np.int64)
+    leaf_values = np.zeros((n, k), np.float32)
+    leaf_values[n_int:] = (rng.standard_normal((n - n_int, k)) * leaf_scale).astype(np.float32)
+    return dict(feature=feature, threshold=threshold, left=left, right=right, mode=mode,
+                missing_true=missing, leaf_values=leaf_values)
+
+
+def logistic(n_features: int = 32, seed: int = 1):
+    rng = np.random.default_rng(seed)
+    w = (rng.standard_normal((n_features, 1)) * 0.5).astype(np.float32)
+    b = np.array([-1.0], np.float32)
+    nodes = [node("Gemm", ["input", "W", "B"], ["logit"]), node("Sigmoid", ["logit"], ["output"])]
+    return model(nodes, [value_info("input", S.FLOAT, ["N", n_features])],
+                 [value_info("output", S.FLOAT, ["N", 1])], [tensor("W", w), tensor("B", b)],
+                 name="fraud_logistic", metadata={"family": "logistic", "features": str(n_features)})
+
+
+def gbdt(n_trees: int = 100, depth: int = 7, n_features: int = 128, seed: int = 2,
+         mixed_modes: bool = False):
+    rng = np.random.default_rng(seed)
+    trees = []
+    for _ in range(n_trees):
+        t = random_complete_tree(rng, depth, n_features, 1, leaf_scale=0.15, mixed_modes=mixed_modes)
+        t["class_offset"] = 1   # weights on class 1 only: ORT's binary case
+        trees.append(t)
+    a = tree_attrs(trees, "class")
+    nodes = [node("TreeEnsembleClassifier", ["input"], ["label", "output"], domain=ML_DOMAIN,
+                  post_transform="LOGISTIC", classlabels_int64s=np.array([0, 1], np.int64),
+                  base_values=np.array([-0.5], np.float32), **a)]
+    return model(nodes, [value_info("input", S.FLOAT, ["N", n_features])],
+                 [value_info("label", S.INT64, ["N"]), value_info("output", S.FLOAT, ["N", 2])],
+                 name="fraud_gbdt",
+                 metadata={"family": "gbdt", "trees": str(n_trees), "depth": str(depth)})
+
+
+def stacked(n_trees: int = 100, depth: int = 7, n_features: int = 128, k: int = 32,
+            hidden: int = 256, seed: int = 3):
+    rng = np.random.default_rng(seed)
+    trees = [random_complete_tree(rng, depth, n_features, k, leaf_scale=0.1) for _ in range(n_trees)]
+    a = tree_attrs(trees, "target")
+    w1 = (rng.standard_normal((k, hidden)) * np.sqrt(2.0 / k)).astype(np.float32)
+    b1 = (rng.standard_normal(hidden) * 0.01).astype(np.float32)
+    w2 = (rng.standard_normal((hidden, 1)) * np.sqrt(1.0 / hidden)).astype(np.float32)
+    b2 = np.array([-0.25], np.float32)
+    nodes = [
+        node("TreeEnsembleRegressor", ["input"], ["emb"], domain=ML_DOMAIN, n_targets=k,
+             aggregate_function="SUM", post_transform="NONE",
+             base_values=np.zeros(k, np.float32), **a),
+        node("Gemm", ["emb", "W1", "B1"], ["h1"]),
+        node("Relu", ["h1"], ["a1"]),
+        node("Gemm", ["a1", "W2", "B2"], ["logit"]),
+        node("Sigmoid", ["logit"], ["output"]),
+    ]
+    return model(nodes, [value_info("input", S.FLOAT, ["N", n_features])],
+                 [value_info("output", S.FLOAT, ["N", 1])],
+                 [tensor("W1", w1), tensor("B1", b1), tensor("W2", w2), tensor("B2", b2)],
+                 name="fraud_stacked",
+                 metadata={"family": "stacked", "trees": str(n_trees), "targets": str(k)})
+
+
+def ltv_mlp(n_features: int = 256, width: int = 512, layers: int = 4, seed: int = 4):
+    rng = np.random.default_rng(seed)
+    nodes, inits = [], []
+    prev, cur = n_features, "input"
+    for i in range(layers):
+        w = (rng.standard_normal((prev, width)) * np.sqrt(2.0 / prev)).astype(np.float32)
+        b = (rng.standard_normal(width) * 0.01).astype(np.float32)
+        inits += [tensor(f"W{i}", w), tensor(f"B{i}", b)]
+        nodes += [node("Gemm", [cur, f"W{i}", f"B{i}"], [f"h{i}"]), node("Relu", [f"h{i}"], [f"a{i}"])]
+        prev, cur = width, f"a{i}"
+    w = (rng.standard_normal((prev, 1)) * np.sqrt(1.0 / prev)).astype(np.float32)
+    inits += [tensor("Wout", w), tensor("Bout", np.array([50.0], np.float32))]
+    nodes.append(node("Gemm", [cur, "Wout", "Bout"], ["output"]))
+    return model(nodes, [value_info("input", S.FLOAT, ["N", n_features])],
+                 [value_info("output", S.FLOAT, ["N", 1])], inits, name="ltv_mlp",
+                 metadata={"family": "mlp", "layers": str(layers), "width": str(width)})
+
+
+def _gru_weights(rng, in_dim: int, hidden: int):
+    s = 1.0 / np.sqrt(hidden)
+    w = rng.uniform(-s, s, (1, 3 * hidden, in_dim)).astype(np.float32)
+    r = rng.uniform(-s, s, (1, 3 * hidden, hidden)).astype(np.float32)
+    b = rng.uniform(-s, s, (1, 6 * hidden)).astype(np.float32)
+    return w, r, b
+
+
+def gru(seq: int = 100, in_dim: int = 16, hidden: int = 256, seed: int = 5):
+    rng = np.random.default_rng(seed)
+    w1, r1, b1 = _gru_weights(rng, in_dim, hidden)
+    w2, r2, b2 = _gru_weights(rng, hidden, hidden)
+    wh = (rng.standard_normal((hidden, 1)) * np.sqrt(1.0 / hidden)).astype(np.float32)
+    bh = np.array([0.0], np.float32)
+    nodes = [
+        node("GRU", ["input", "W1", "R1", "B1"], ["Y1", "Yh1"], hidden_size=hidden,
+             linear_before_reset=1),
+        node("Squeeze", ["Y1", "ax1"], ["X2"]),
+        node("GRU", ["X2", "W2", "R2", "B2"], ["Y2", "Yh2"], hidden_size=hidden,
+             linear_before_reset=1),
+        node("Reshape", ["Yh2", "shp"], ["h"]),
+        node("Gemm", ["h", "Wh", "Bh"], ["logit"]),
+        node("Sigmoid", ["logit"], ["output"]),
+    ]
+    inits = [tensor("W1", w1), tensor("R1", r1), tensor("B1", b1), tensor("W2", w2),
+             tensor("R2", r2), tensor("B2", b2), tensor("Wh", wh), tensor("Bh", bh),
+             tensor("ax1", np.array([1], np.int64)), tensor("shp", np.array([-1, hidden], np.int64))]
+    return model(nodes, [value_info("input", S.FLOAT, [seq, "N", in_dim])],
+                 [value_info("output", S.FLOAT, ["N", 1])], inits, name="abuse_gru",
+                 metadata={"family": "gru", "layers": "2", "hidden": str(hidden), "seq": str(seq)})
+
+
+BUILDERS = {"logistic": logistic, "gbdt": gbdt, "stacked": stacked, "ltv_mlp": ltv_mlp, "gru": gru}
+
+
+def build(kind: str, **kw):
+    return BUILDERS[kind](**kw)
