@@ -60,3 +60,97 @@ static_assert(sizeof(ResultRec) == 8, "ResultRec must be 8 bytes");
 #define IGP_RES_REASONS(p) ((p) >> 20)
 
 }  // namespace igp
+
+namespace igp {
+
+// Per-account real-time scalars (the reference's Redis keys other than the tx ZSET/HLLs),
+// 64 bytes. Times are unix seconds (uint32); a key is alive iff now < its expiry.
+struct AcctRT {
+  uint32_t hll_dev_exp;     // features:<id>:devices:24h TTL
+  uint32_t hll_ip_exp;      // features:<id>:ips:24h TTL
+  uint32_t last_tx;         // features:<id>:last_tx
+  uint32_t last_tx_exp;
+  uint32_t session_start;   // features:<id>:session_start
+  uint32_t session_exp;
+  uint32_t sum_exp;         // features:<id>:tx_sum:1h TTL (compat sum mode)
+  uint32_t last_event_ts;   // previous event time (GRU dt feature)
+  int64_t sum_compat;       // INCRBY running sum (compat mode)
+  int32_t ring_head;        // next tx-ring write position
+  int32_t ev_head;          // next event-ring write position
+  int32_t ev_count;
+  int32_t pad[3];
+};
+static_assert(sizeof(AcctRT) == 64, "AcctRT must be 64 bytes");
+
+// Warehouse batch features (engine.go:127-140), 80 bytes.
+struct AcctBatch {
+  int64_t total_deposits;
+  int64_t total_withdrawals;
+  int64_t total_bets;
+  int64_t total_wins;
+  int64_t account_created_at;
+  int32_t deposit_count;
+  int32_t withdraw_count;
+  int32_t bet_count;
+  int32_t win_count;
+  float avg_bet_size;
+  int32_t bonus_claim_count;
+  float bonus_wager_complete;
+  int32_t present;          // 0 = batch features unavailable (partial features, quirk Q10)
+  int32_t pad[2];
+};
+static_assert(sizeof(AcctBatch) == 80, "AcctBatch must be 80 bytes");
+
+// Scoring configuration block kept in device memory: graphs read it on every replay, so
+// UpdateThresholds never needs a graph re-capture (engine.go:196-228, 246-257).
+struct ScoreCfg {
+  int32_t block_threshold;
+  int32_t review_threshold;
+  int32_t max_tx_per_minute;
+  int32_t new_account_days;
+  int64_t large_deposit_amount;
+  int32_t max_devices_per_day;
+  int32_t max_ips_per_day;
+  double ml_weight;
+  double rule_weight;
+  double ml_high_risk;
+  double ml_error_score;
+  int32_t w_high_velocity, w_new_account_large_tx, w_multiple_devices, w_ip_country_mismatch;
+  int32_t w_vpn, w_rapid_deposit_withdraw, w_bonus_abuse, w_known_fraudster;
+  int32_t model_kind;       // 0 none, 1 heuristic (mockPredict), 2 model output buffer
+  int32_t ml_col;           // column of the model output holding P(fraud)
+  int32_t ml_stride;        // row stride of the model output
+  int32_t log_identity;     // 1 = reference stub log1p(x)=x (quirk Q1)
+  int32_t sum_compat;       // 1 = INCRBY-with-TTL 1h sum (quirk Q8)
+  int32_t session_ttl, last_tx_ttl, hll_ttl, sum_ttl;
+  int32_t bl_mask;          // blacklist table capacity - 1
+  int32_t bl_max_probe;
+  int32_t ip_mask;          // ip-intel table capacity - 1
+  int32_t ip_max_probe;
+  int32_t ext_width;        // feature-vector columns beyond the 30 reference ones
+  int32_t pad[5];
+};
+static_assert(sizeof(ScoreCfg) == 176, "ScoreCfg must be 176 bytes");
+
+// One scoring request / transaction event as shipped host->device (48 bytes). A batch is a
+// contiguous slab [BatchHdr | ReqRec x n]: one H2D copy per micro-batch.
+struct ReqRec {
+  int32_t slot;       // feature-store slot on this GPU (-1 = unknown account)
+  int32_t tx_type;    // TxType
+  int64_t amount;     // cents
+  uint64_t dev_hash;  // XXH64 digests, 0 = absent
+  uint64_t fp_hash;
+  uint64_t ip_hash;
+  int64_t ts;         // event time (unix s) used by feature_update
+};
+static_assert(sizeof(ReqRec) == 48, "ReqRec must be 48 bytes");
+
+// Per-batch header in device memory (written by one H2D copy per batch, read by every
+// kernel of the captured graph): the number of live rows and the scoring clock.
+struct BatchHdr {
+  int32_t n;
+  int32_t pad;
+  int64_t now;
+};
+
+}  // namespace igp

@@ -1,0 +1,168 @@
+// pybind11 launch bindings of the gfx950 kernels (_hipk). Arguments arrive as a dict of
+// device pointers (torch data_ptr()) and sizes; igaming_platform_amd/ops/kernels.py builds
+// the dicts and validates every shape/dtype/device before calling in.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <string>
+
+#include "launch.h"
+
+namespace py = pybind11;
+using namespace igp;
+
+namespace {
+
+template <class T>
+T ptr(const py::dict& d, const char* k) {
+  if (!d.contains(k)) return nullptr;
+  py::object o = d[k];
+  if (o.is_none()) return nullptr;
+  return reinterpret_cast<T>(o.cast<uintptr_t>());
+}
+
+int32_t geti(const py::dict& d, const char* k, int32_t def = 0) {
+  if (!d.contains(k)) return def;
+  return d[k].cast<int32_t>();
+}
+
+hipStream_t stream_of(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+void check(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_hipk, m) {
+  m.doc() = "igaming_platform_amd gfx950 HIP kernels";
+  m.attr("ARCH") = "gfx950";
+  m.attr("SIZEOF_SCORECFG") = (int)sizeof(ScoreCfg);
+  m.attr("SIZEOF_FEATREC") = (int)sizeof(FeatRec);
+  m.attr("SIZEOF_ACCTRT") = (int)sizeof(AcctRT);
+  m.attr("SIZEOF_ACCTBATCH") = (int)sizeof(AcctBatch);
+  m.attr("SIZEOF_REQREC") = (int)sizeof(ReqRec);
+
+  m.def("feature_assemble", [](py::dict d, uintptr_t s) {
+    AssembleArgs a{};
+    a.hdr = ptr<const BatchHdr*>(d, "hdr");
+    a.cfg = ptr<const ScoreCfg*>(d, "cfg");
+    a.req = ptr<const ReqRec*>(d, "req");
+    a.ring_ts = ptr<const uint32_t*>(d, "ring_ts");
+    a.ring_amt = ptr<const int64_t*>(d, "ring_amt");
+    a.hll = ptr<const uint8_t*>(d, "hll");
+    a.rt = ptr<const AcctRT*>(d, "rt");
+    a.batch = ptr<const AcctBatch*>(d, "batch");
+    a.ext = ptr<const float*>(d, "ext");
+    a.bl_keys = ptr<const uint64_t*>(d, "bl_keys");
+    a.bl_exp = ptr<const uint32_t*>(d, "bl_exp");
+    a.ip_keys = ptr<const uint64_t*>(d, "ip_keys");
+    a.ip_flags = ptr<const uint32_t*>(d, "ip_flags");
+    a.X = ptr<float*>(d, "X");
+    a.feat = ptr<FeatRec*>(d, "feat");
+    a.x_stride = geti(d, "x_stride");
+    a.ring_size = geti(d, "ring_size");
+    a.n_rows = geti(d, "n_rows");
+    launch_feature_assemble(a, stream_of(s));
+    check("feature_assemble");
+  });
+
+  m.def("feature_update", [](py::dict d, uintptr_t s) {
+    UpdateArgs a{};
+    a.cfg = ptr<const ScoreCfg*>(d, "cfg");
+    a.n_ptr = ptr<const int32_t*>(d, "n_ptr");
+    a.n = geti(d, "n");
+    a.n_max = geti(d, "n_max");
+    a.req = ptr<const ReqRec*>(d, "req");
+    a.ring_ts = ptr<uint32_t*>(d, "ring_ts");
+    a.ring_amt = ptr<int64_t*>(d, "ring_amt");
+    a.hll = ptr<uint8_t*>(d, "hll");
+    a.rt = ptr<AcctRT*>(d, "rt");
+    a.ev = ptr<uint16_t*>(d, "ev");
+    a.ring_size = geti(d, "ring_size");
+    a.ev_ring = geti(d, "ev_ring");
+    a.ev_dim = geti(d, "ev_dim");
+    a.dcap = geti(d, "dcap");
+    a.dkeys = ptr<int32_t*>(d, "dkeys");
+    a.dfirst = ptr<int32_t*>(d, "dfirst");
+    a.dcount = ptr<int32_t*>(d, "dcount");
+    launch_feature_update(a, stream_of(s));
+    check("feature_update");
+  });
+
+  m.def("tree_ensemble", [](py::dict d, uintptr_t s) {
+    TreeArgs a{};
+    a.hdr = ptr<const BatchHdr*>(d, "hdr");
+    a.X = ptr<const float*>(d, "X");
+    a.nodes = ptr<const float2*>(d, "nodes");
+    a.leaves = ptr<const float*>(d, "leaves");
+    a.base = ptr<const float*>(d, "base");
+    a.out = ptr<float*>(d, "out");
+    a.x_stride = geti(d, "x_stride");
+    a.n_rows = geti(d, "n_rows");
+    a.n_trees = geti(d, "n_trees");
+    a.depth = geti(d, "depth");
+    a.k = geti(d, "k");
+    a.n_out = geti(d, "n_out");
+    a.post = geti(d, "post");
+    a.average = geti(d, "average");
+    a.binary_class = geti(d, "binary_class", -1);
+    a.all_positive = geti(d, "all_positive", 1);
+    const int groups = geti(d, "groups", 1);
+    launch_tree_ensemble_grouped(a, groups, ptr<float*>(d, "partial"), stream_of(s));
+    check("tree_ensemble");
+  });
+
+  auto gemm_args = [](const py::dict& d) {
+    GemmArgs a{};
+    a.X = ptr<const void*>(d, "X");
+    a.W = ptr<const uint16_t*>(d, "W");
+    a.bias = ptr<const float*>(d, "bias");
+    a.Y = ptr<void*>(d, "Y");
+    a.m_ptr = ptr<const int32_t*>(d, "m_ptr");
+    a.M = geti(d, "M");
+    a.N = geti(d, "N");
+    a.K = geti(d, "K");
+    a.ldx = geti(d, "ldx");
+    a.ldy = geti(d, "ldy");
+    a.ldw = geti(d, "ldw");
+    a.x_bf16 = geti(d, "x_bf16");
+    a.y_bf16 = geti(d, "y_bf16");
+    a.act = geti(d, "act");
+    return a;
+  };
+  m.def("gemm", [gemm_args](py::dict d, uintptr_t s) {
+    launch_gemm(gemm_args(d), stream_of(s));
+    check("gemm");
+  });
+  m.def("gemv", [gemm_args](py::dict d, uintptr_t s) {
+    launch_gemv(gemm_args(d), stream_of(s));
+    check("gemv");
+  });
+
+  m.def("ensemble", [](py::dict d, uintptr_t s) {
+    EnsembleArgs a{};
+    a.hdr = ptr<const BatchHdr*>(d, "hdr");
+    a.cfg = ptr<const ScoreCfg*>(d, "cfg");
+    a.feat = ptr<const FeatRec*>(d, "feat");
+    a.X = ptr<const float*>(d, "X");
+    a.x_stride = geti(d, "x_stride");
+    a.ml = ptr<const float*>(d, "ml");
+    a.out = ptr<ResultRec*>(d, "out");
+    a.metrics = ptr<unsigned long long*>(d, "metrics");
+    a.n_rows = geti(d, "n_rows");
+    launch_ensemble(a, stream_of(s));
+    check("ensemble");
+  });
+
+  m.def("ltv", [](py::dict d, uintptr_t s) {
+    LtvArgs a{};
+    a.pf = ptr<const float*>(d, "pf");
+    a.ltv_model = ptr<const float*>(d, "ltv_model");
+    a.out = ptr<float*>(d, "out");
+    a.B = geti(d, "B");
+    launch_ltv(a, stream_of(s));
+    check("ltv");
+  });
+}

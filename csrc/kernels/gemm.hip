@@ -1,0 +1,211 @@
+// K3 dense layers on the CDNA4 matrix cores: Y[M,N] = act(X[M,K] . W^T + b).
+//
+// W is stored bf16 [N_pad][K_pad] (each output column's weights contiguous in K), so both
+// MFMA operand fragments are 16-byte contiguous LDS reads (mfma_f32_16x16x32_bf16:
+// lane l holds A[l&15][8(l>>4)..+8] and B[8(l>>4)..+8][l&15]). X may be f32 (cast to bf16
+// while staging, fusing the producer's dtype conversion) or bf16; accumulation is f32;
+// bias + activation are fused into the epilogue. 4 waves in a 2x2 arrangement, BK = 64,
+// two LDS buffers: tile k+1 is loaded to registers while tile k's MFMAs run.
+#include "common.h"
+#include "launch.h"
+
+namespace igp {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int G_BK = 64;
+constexpr int G_PAD = 8;  // bf16 elements of row padding (144-byte rows)
+
+__device__ __forceinline__ float act_fn(float v, int act) {
+  switch (act) {
+    case 1: return v > 0.f ? v : 0.f;
+    case 2: return 1.f / (1.f + expf(-v));
+    case 3: return tanhf(v);
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
+  constexpr int LDS_ROW = G_BK + G_PAD;
+  constexpr int FM = BM / 32;  // fragments per wave along M (wave covers BM/2 rows)
+  constexpr int FN = BN / 32;
+  __shared__ __attribute__((aligned(16))) uint16_t sA[2][BM * LDS_ROW];
+  __shared__ __attribute__((aligned(16))) uint16_t sB[2][BN * LDS_ROW];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int M = a.m_ptr ? min(*a.m_ptr, a.M) : a.M;
+  // XCD-aware remap (blocks sharing an X row panel land on one XCD's L2)
+  const int nbx = (a.N + BN - 1) / BN;
+  const int row0 = blockIdx.y * BM;
+  const int col0 = blockIdx.x * BN;
+  if (row0 >= M) return;
+  (void)nbx;
+  const int K = a.K;
+  const int k_pad = a.ldw;
+  const int n_kt = (K + G_BK - 1) / G_BK;
+
+  // staging: A tile BM x 64 -> BM*8 chunks of 8 elements; B tile BN x 64 -> BN*8 chunks
+  constexpr int A_CHUNKS = BM * G_BK / 8 / 256;
+  constexpr int B_CHUNKS = BN * G_BK / 8 / 256;
+  uint4 ra[A_CHUNKS], rb[B_CHUNKS];
+
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * G_BK;
+#pragma unroll
+    for (int c = 0; c < A_CHUNKS; ++c) {
+      const int ch = tid + c * 256;
+      const int r = ch >> 3, kc = (ch & 7) * 8;
+      const int row = row0 + r, k = k0 + kc;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (row < M) {
+        if (a.x_bf16) {
+          const uint16_t* src = reinterpret_cast<const uint16_t*>(a.X) + (size_t)row * a.ldx + k;
+          if (k + 8 <= K) {
+            v = *reinterpret_cast<const uint4*>(src);
+          } else {
+            uint16_t t[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) t[j] = (k + j < K) ? src[j] : 0;
+            v = make_uint4(t[0] | (t[1] << 16), t[2] | (t[3] << 16), t[4] | (t[5] << 16), t[6] | (t[7] << 16));
+          }
+        } else {
+          const float* src = reinterpret_cast<const float*>(a.X) + (size_t)row * a.ldx + k;
+          float f[8];
+          if (k + 8 <= K && ((a.ldx & 3) == 0)) {
+            const float4 p = *reinterpret_cast<const float4*>(src);
+            const float4 q = *reinterpret_cast<const float4*>(src + 4);
+            f[0] = p.x; f[1] = p.y; f[2] = p.z; f[3] = p.w; f[4] = q.x; f[5] = q.y; f[6] = q.z; f[7] = q.w;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = (k + j < K) ? src[j] : 0.f;
+          }
+          v = make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
+                         pack_bf16x2(f[6], f[7]));
+        }
+      }
+      ra[c] = v;
+    }
+#pragma unroll
+    for (int c = 0; c < B_CHUNKS; ++c) {
+      const int ch = tid + c * 256;
+      const int r = ch >> 3, kc = (ch & 7) * 8;
+      const int n = col0 + r, k = k0 + kc;
+      // W is zero padded to [N_pad][K_pad] with N_pad a multiple of 128, K_pad of 64
+      rb[c] = (k < k_pad) ? *reinterpret_cast<const uint4*>(a.W + (size_t)n * k_pad + k) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int c = 0; c < A_CHUNKS; ++c) {
+      const int ch = tid + c * 256;
+      *reinterpret_cast<uint4*>(&sA[buf][(ch >> 3) * LDS_ROW + (ch & 7) * 8]) = ra[c];
+    }
+#pragma unroll
+    for (int c = 0; c < B_CHUNKS; ++c) {
+      const int ch = tid + c * 256;
+      *reinterpret_cast<uint4*>(&sB[buf][(ch >> 3) * LDS_ROW + (ch & 7) * 8]) = rb[c];
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < n_kt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < n_kt) load_tile(kt + 1);  // global loads in flight under the MFMAs
+#pragma unroll
+    for (int kk = 0; kk < G_BK / 32; ++kk) {
+      bf16x8 fa[FM], fb[FN];
+      const int kof = kk * 32 + 8 * (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wm * (BM / 2) + i * 16 + (lane & 15);
+        fa[i] = *reinterpret_cast<const bf16x8*>(&sA[cur][r * LDS_ROW + kof]);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int r = wn * (BN / 2) + j * 16 + (lane & 15);
+        fb[j] = *reinterpret_cast<const bf16x8*>(&sB[cur][r * LDS_ROW + kof]);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < n_kt) {
+      store_tile(cur ^ 1);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: bias + activation, f32 or bf16 stores
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = col0 + wn * (BN / 2) + j * 16 + (lane & 15);
+      if (col >= a.N) continue;
+      const float b = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = row0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + q;
+        if (row >= M) continue;
+        const float v = act_fn(acc[i][j][q] + b, a.act);
+        if (a.y_bf16) reinterpret_cast<uint16_t*>(a.Y)[(size_t)row * a.ldy + col] = f32_to_bf16(v);
+        else reinterpret_cast<float*>(a.Y)[(size_t)row * a.ldy + col] = v;
+      }
+    }
+}
+
+// N == 1 heads (logistic / final regression): one wave per row, lanes over K.
+__global__ void __launch_bounds__(256) gemv_kernel(GemmArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int M = a.m_ptr ? min(*a.m_ptr, a.M) : a.M;
+  if (row >= M) return;
+  float s = 0.f;
+  for (int k = lane; k < a.K; k += 64) {
+    const float x = a.x_bf16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(a.X)[(size_t)row * a.ldx + k])
+                             : reinterpret_cast<const float*>(a.X)[(size_t)row * a.ldx + k];
+    s += x * bf16_to_f32(a.W[k]);
+  }
+  s = wave_sum(s);
+  if (lane == 0) {
+    const float v = act_fn(s + (a.bias ? a.bias[0] : 0.f), a.act);
+    if (a.y_bf16) reinterpret_cast<uint16_t*>(a.Y)[(size_t)row * a.ldy] = f32_to_bf16(v);
+    else reinterpret_cast<float*>(a.Y)[(size_t)row * a.ldy] = v;
+  }
+}
+
+void launch_gemm(const GemmArgs& a, hipStream_t st) {
+  if (a.M <= 0) return;
+  const bool big = a.M >= 4096 && a.N >= 128;
+  if (big) {
+    dim3 grid((a.N + 127) / 128, (a.M + 127) / 128);
+    hipLaunchKernelGGL((gemm_kernel<128, 128>), grid, dim3(256), 0, st, a);
+  } else {
+    dim3 grid((a.N + 63) / 64, (a.M + 63) / 64);
+    hipLaunchKernelGGL((gemm_kernel<64, 64>), grid, dim3(256), 0, st, a);
+  }
+}
+
+void launch_gemv(const GemmArgs& a, hipStream_t st) {
+  if (a.M <= 0) return;
+  hipLaunchKernelGGL(gemv_kernel, dim3((a.M + 3) / 4), dim3(256), 0, st, a);
+}
+
+}  // namespace igp

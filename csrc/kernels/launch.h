@@ -1,0 +1,140 @@
+// Kernel argument blocks and host launch entry points of the _hipk extension.
+// Every launch takes an explicit hipStream_t (torch's current stream from Python) and
+// performs no allocation or synchronisation, so all of them are hipGraph-capturable.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../include/records.h"
+
+namespace igp {
+
+struct AssembleArgs {
+  const BatchHdr* hdr;
+  const ScoreCfg* cfg;
+  const ReqRec* req;         // [n_rows]
+  const uint32_t* ring_ts;
+  const int64_t* ring_amt;
+  const uint8_t* hll;       // [C][2][256]
+  const AcctRT* rt;
+  const AcctBatch* batch;
+  const float* ext;         // [C][ext_width]
+  const uint64_t* bl_keys;  // blacklist open-addressing table (nullable)
+  const uint32_t* bl_exp;
+  const uint64_t* ip_keys;  // ip-intel table (nullable)
+  const uint32_t* ip_flags;
+  float* X;                 // [n_rows][x_stride]
+  FeatRec* feat;            // [n_rows]
+  int32_t x_stride;
+  int32_t ring_size;
+  int32_t n_rows;           // rows covered by the launch (graph bucket)
+};
+
+struct UpdateArgs {
+  const ScoreCfg* cfg;
+  const int32_t* n_ptr;     // live event count in device memory (nullable -> n)
+  int32_t n;
+  int32_t n_max;            // grid coverage
+  const ReqRec* req;        // events (ReqRec.ts = event time)
+  uint32_t* ring_ts;
+  int64_t* ring_amt;
+  uint8_t* hll;
+  AcctRT* rt;
+  uint16_t* ev;             // event ring bf16 [C][ev_ring][ev_dim] (nullable)
+  int32_t ring_size;
+  int32_t ev_ring;
+  int32_t ev_dim;
+  int32_t dcap;             // dedup scratch capacity (power of two >= 2 * n_max)
+  int32_t* dkeys;
+  int32_t* dfirst;
+  int32_t* dcount;
+};
+
+void launch_feature_assemble(const AssembleArgs& a, hipStream_t st);
+void launch_feature_update(const UpdateArgs& a, hipStream_t st);
+
+// ---- K2 tree ensemble (complete layout)
+struct TreeArgs {
+  const BatchHdr* hdr;      // nullable: all n_rows live
+  const float* X;           // [n][x_stride]
+  const float2* nodes;      // [T][2^D-1] (threshold, meta bits)
+  const float* leaves;      // [T][2^D][K]
+  const float* base;        // [K] (nullable)
+  float* out;               // [n][n_out]
+  int32_t x_stride;
+  int32_t n_rows;
+  int32_t n_trees;
+  int32_t depth;
+  int32_t k;                // targets per leaf
+  int32_t n_out;            // output columns (2 in the binary-classifier case)
+  int32_t post;             // 0 none, 1 logistic, 2 softmax
+  int32_t average;          // 1 = AVERAGE aggregate
+  int32_t binary_class;     // -1 unless classifier binary case
+  int32_t all_positive;
+};
+void launch_tree_ensemble(const TreeArgs& a, hipStream_t st);
+void launch_tree_ensemble_grouped(const TreeArgs& a, int groups, float* partial, hipStream_t st);
+
+// ---- K3 dense layers: Y = act(X W^T + b)
+struct GemmArgs {
+  const void* X;            // [M][ldx] f32 or bf16
+  const uint16_t* W;        // bf16 [N_pad][K_pad] (row n = output column n)
+  const float* bias;        // [N] nullable
+  void* Y;                  // [M][ldy] f32 or bf16
+  const int32_t* m_ptr;     // live rows in device memory (nullable -> M)
+  int32_t M, N, K;          // logical sizes; K_pad = round_up(K, 32)
+  int32_t ldx, ldy, ldw;
+  int32_t x_bf16, y_bf16;
+  int32_t act;              // 0 none, 1 relu, 2 sigmoid, 3 tanh
+};
+void launch_gemm(const GemmArgs& a, hipStream_t st);
+void launch_gemv(const GemmArgs& a, hipStream_t st);  // N == 1 heads
+
+// ---- K5 ensemble + action + metrics
+struct EnsembleArgs {
+  const BatchHdr* hdr;
+  const ScoreCfg* cfg;
+  const FeatRec* feat;
+  const float* X;           // for the heuristic model
+  int32_t x_stride;
+  const float* ml;          // model output (nullable)
+  ResultRec* out;
+  unsigned long long* metrics;  // [128] score histogram(101) | actions(4) | ml_high | rows (nullable)
+  int32_t n_rows;
+};
+void launch_ensemble(const EnsembleArgs& a, hipStream_t st);
+
+// ---- K4 GRU sequence (recurrent weights resident in VGPRs)
+struct GruArgs {
+  const uint16_t* X;        // bf16 [T][B][I] (I <= 32) when G == nullptr
+  const float* G;           // precomputed input projection f32 [T][B][3H] (nullable)
+  const uint16_t* Wf;       // bf16 input weights fragments [3H][32] (used when G == nullptr)
+  const uint16_t* R;        // bf16 [3H][H]
+  const float* bias;        // [6H] (Wb z,r,h | Rb z,r,h)
+  uint16_t* Y;              // bf16 [T][B][H] (nullable)
+  float* Yh;                // f32 [B][H] (nullable)
+  int32_t T, B, I, H;
+  int32_t linear_before_reset;
+};
+void launch_gru(const GruArgs& a, hipStream_t st);
+
+// ---- event history gather for the GRU: ring -> [T][B][dim] bf16, oldest first
+struct EventGatherArgs {
+  const uint16_t* ev;       // [C][ring][dim]
+  const AcctRT* rt;
+  const int32_t* slot;      // [B]
+  uint16_t* out;            // [T][B][dim_pad]
+  int32_t B, ring, dim, dim_pad;
+};
+void launch_event_gather(const EventGatherArgs& a, hipStream_t st);
+
+// ---- K9 LTV / churn / segment
+struct LtvArgs {
+  const float* pf;          // [B][25] player features (golden.ltv.PLAYER_COLUMNS)
+  const float* ltv_model;   // [B] learned LTV (nullable -> formula)
+  float* out;               // [B][6]: ltv, churn, survival, confidence, segment, nba
+  int32_t B;
+};
+void launch_ltv(const LtvArgs& a, hipStream_t st);
+
+}  // namespace igp

@@ -1,0 +1,227 @@
+// K2 tree_ensemble: ONNX-ML TreeEnsemble{Classifier,Regressor} on the complete-tree layout
+// (csrc/runtime/trees.h). Semantics: CPU executor (csrc/runtime/trees.cpp).
+//
+// Block = 256 threads = 4 waves, 64 samples (lane = sample). The block's 64-row X tile
+// ([64][F+1] f32, +1 pad -> conflict-free column reads) and its tree group's node table
+// (8 B/node) are staged in LDS; the four waves split the group's trees and each lane keeps
+// 4 traversals in flight (independent LDS chains hide the ds_read latency). Leaf vectors
+// are read from L2. Wave partials are reduced through LDS; with several tree groups per
+// sample tile (small batches) partial sums go to a scratch slab and a finisher kernel adds
+// base values and applies the post transform.
+#include "common.h"
+#include "launch.h"
+
+namespace igp {
+
+constexpr int TR_ROWS = 64;
+constexpr int TR_ILP = 4;
+
+__device__ __forceinline__ int tree_step(int i, float x, float2 nd) {
+  const uint32_t m = __float_as_uint(nd.y);
+  const int mode = (m >> 16) & 7;
+  const float t = nd.x;
+  bool c = mode == 0 ? (x <= t) : mode == 1 ? (x < t) : mode == 2 ? (x >= t)
+         : mode == 3 ? (x > t) : mode == 4 ? (x == t) : (x != t);
+  c = c || (((m >> 19) & 1u) && isnan(x));
+  return 2 * i + (c ? 1 : 2);
+}
+
+template <int K>
+__global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_group, int feat_w,
+                                                   int nodes_in_lds, float* partial) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int xs = feat_w + 1;
+  float* sx = reinterpret_cast<float*>(smem);                       // [64][feat_w+1]
+  float2* sn = reinterpret_cast<float2*>(smem + ((TR_ROWS * xs * 4 + 15) & ~15));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row0 = blockIdx.x * TR_ROWS;
+  const int g = blockIdx.y;
+  const int t0 = g * trees_per_group;
+  const int t1 = min(a.n_trees, t0 + trees_per_group);
+  const int n_int = (1 << a.depth) - 1;
+  const int n_leaf = 1 << a.depth;
+
+  // stage X tile
+  for (int e = tid; e < TR_ROWS * feat_w; e += 256) {
+    const int r = e / feat_w, c = e - r * feat_w;
+    const int row = row0 + r;
+    sx[r * xs + c] = row < a.n_rows ? a.X[(size_t)row * a.x_stride + c] : 0.f;
+  }
+  // stage this group's nodes
+  const float2* gn = a.nodes + (size_t)t0 * n_int;
+  const int nn = (t1 - t0) * n_int;
+  if (nodes_in_lds)
+    for (int e = tid; e < nn; e += 256) sn[e] = gn[e];
+  __syncthreads();
+  const float2* nodes = nodes_in_lds ? sn : gn;
+
+  float acc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k] = 0.f;
+  const float* xrow = sx + lane * xs;
+
+  // trees of this wave: t0 + wave + 4j
+  for (int tb = t0 + wave; tb < t1; tb += 4 * TR_ILP) {
+    int idx[TR_ILP];
+    int tt[TR_ILP];
+#pragma unroll
+    for (int q = 0; q < TR_ILP; ++q) {
+      tt[q] = tb + 4 * q;
+      idx[q] = 0;
+    }
+    for (int d = 0; d < a.depth; ++d) {
+#pragma unroll
+      for (int q = 0; q < TR_ILP; ++q) {
+        if (tt[q] < t1) {
+          const float2 nd = nodes[(tt[q] - t0) * n_int + idx[q]];
+          const int f = __float_as_uint(nd.y) & 0xffff;
+          idx[q] = tree_step(idx[q], xrow[f], nd);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < TR_ILP; ++q) {
+      if (tt[q] < t1) {
+        const float* lf = a.leaves + ((size_t)tt[q] * n_leaf + (idx[q] - n_int)) * K;
+        if constexpr (K % 4 == 0) {
+#pragma unroll
+          for (int k = 0; k < K; k += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(lf + k);
+            acc[k] += v.x; acc[k + 1] += v.y; acc[k + 2] += v.z; acc[k + 3] += v.w;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < K; ++k) acc[k] += lf[k];
+        }
+      }
+    }
+  }
+  // reduce the 4 waves through LDS (reuse the X tile region)
+  __syncthreads();
+  float* red = sx;  // [4][64][K]
+#pragma unroll
+  for (int k = 0; k < K; ++k) red[(wave * TR_ROWS + lane) * K + k] = acc[k];
+  __syncthreads();
+  for (int e = tid; e < TR_ROWS * K; e += 256) {
+    const int r = e / K, k = e - r * K;
+    const int row = row0 + r;
+    float v = red[(0 * TR_ROWS + r) * K + k] + red[(1 * TR_ROWS + r) * K + k] +
+              red[(2 * TR_ROWS + r) * K + k] + red[(3 * TR_ROWS + r) * K + k];
+    if (row >= a.n_rows) continue;
+    if (partial) {
+      partial[((size_t)g * a.n_rows + row) * K + k] = v;
+    } else {
+      red[(4 * TR_ROWS + r) * K + k] = v;  // final sums, post-transform below
+    }
+  }
+  if (partial) return;
+  __syncthreads();
+  // post transform, one thread per row
+  for (int r = tid; r < TR_ROWS; r += 256) {
+    const int row = row0 + r;
+    if (row >= a.n_rows) continue;
+    float* o = a.out + (size_t)row * a.n_out;
+    const float* s = red + (4 * TR_ROWS + r) * K;
+    if (a.binary_class >= 0) {
+      float v = s[0];
+      if (a.average) v /= (float)a.n_trees;
+      if (a.base) v += a.base[0];
+      const int c = a.binary_class;
+      if (a.post == 1) {
+        o[c] = 1.f / (1.f + expf(-v));
+        o[1 - c] = 1.f / (1.f + expf(v));
+      } else {
+        o[c] = v;
+        o[1 - c] = a.all_positive ? 1.f - v : -v;
+      }
+      continue;
+    }
+    float mx = -INFINITY;
+    for (int k = 0; k < K; ++k) {
+      float v = s[k];
+      if (a.average) v /= (float)a.n_trees;
+      if (a.base) v += a.base[k];
+      if (a.post == 1) v = 1.f / (1.f + expf(-v));
+      o[k] = v;
+      mx = fmaxf(mx, v);
+    }
+    if (a.post == 2) {
+      float sum = 0.f;
+      for (int k = 0; k < K; ++k) { o[k] = expf(o[k] - mx); sum += o[k]; }
+      for (int k = 0; k < K; ++k) o[k] /= sum;
+    }
+  }
+}
+
+__global__ void tree_finish_kernel(TreeArgs a, const float* partial, int groups) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= a.n_rows) return;
+  const int K = a.k;
+  float* o = a.out + (size_t)row * a.n_out;
+  if (a.binary_class >= 0) {
+    float v = 0.f;
+    for (int g = 0; g < groups; ++g) v += partial[((size_t)g * a.n_rows + row) * K];
+    if (a.average) v /= (float)a.n_trees;
+    if (a.base) v += a.base[0];
+    const int c = a.binary_class;
+    if (a.post == 1) {
+      o[c] = 1.f / (1.f + expf(-v));
+      o[1 - c] = 1.f / (1.f + expf(v));
+    } else {
+      o[c] = v;
+      o[1 - c] = a.all_positive ? 1.f - v : -v;
+    }
+    return;
+  }
+  float mx = -INFINITY;
+  for (int k = 0; k < K; ++k) {
+    float v = 0.f;
+    for (int g = 0; g < groups; ++g) v += partial[((size_t)g * a.n_rows + row) * K + k];
+    if (a.average) v /= (float)a.n_trees;
+    if (a.base) v += a.base[k];
+    if (a.post == 1) v = 1.f / (1.f + expf(-v));
+    o[k] = v;
+    mx = fmaxf(mx, v);
+  }
+  if (a.post == 2) {
+    float sum = 0.f;
+    for (int k = 0; k < K; ++k) { o[k] = expf(o[k] - mx); sum += o[k]; }
+    for (int k = 0; k < K; ++k) o[k] /= sum;
+  }
+}
+
+template <int K>
+static void launch_k(const TreeArgs& a, int groups, float* partial, hipStream_t st) {
+  const int tpg = (a.n_trees + groups - 1) / groups;
+  const int feat_w = a.x_stride;
+  const int n_int = (1 << a.depth) - 1;
+  const size_t x_bytes = ((size_t)TR_ROWS * (feat_w + 1) * 4 + 15) & ~size_t(15);
+  const size_t red_bytes = (size_t)5 * TR_ROWS * K * 4;
+  const size_t node_bytes = (size_t)tpg * n_int * 8;
+  size_t lds = x_bytes > red_bytes ? x_bytes : red_bytes;
+  int in_lds = (lds + node_bytes) <= 96 * 1024;  // keep >= 1 block/CU with headroom
+  if (in_lds) lds = x_bytes + node_bytes > red_bytes ? x_bytes + node_bytes : red_bytes;
+  dim3 grid((a.n_rows + TR_ROWS - 1) / TR_ROWS, groups);
+  hipLaunchKernelGGL((tree_kernel<K>), grid, dim3(256), lds, st, a, tpg, feat_w, in_lds,
+                     groups > 1 ? partial : nullptr);
+  if (groups > 1)
+    hipLaunchKernelGGL(tree_finish_kernel, dim3((a.n_rows + 255) / 256), dim3(256), 0, st, a, partial, groups);
+}
+
+// partial scratch: [groups][n_rows][K] f32, provided by the caller when groups > 1
+void launch_tree_ensemble_grouped(const TreeArgs& a, int groups, float* partial, hipStream_t st) {
+  switch (a.k) {
+    case 1: launch_k<1>(a, groups, partial, st); break;
+    case 2: launch_k<2>(a, groups, partial, st); break;
+    case 4: launch_k<4>(a, groups, partial, st); break;
+    case 8: launch_k<8>(a, groups, partial, st); break;
+    case 16: launch_k<16>(a, groups, partial, st); break;
+    case 32: launch_k<32>(a, groups, partial, st); break;
+    case 64: launch_k<64>(a, groups, partial, st); break;
+    default: break;  // host validates K before launch
+  }
+}
+
+void launch_tree_ensemble(const TreeArgs& a, hipStream_t st) { launch_tree_ensemble_grouped(a, 1, nullptr, st); }
+
+}  // namespace igp

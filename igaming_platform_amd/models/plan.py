@@ -1,0 +1,313 @@
+"""ONNX graph -> device execution plan.
+
+The C++ reader parses the file; this module walks the (single-input) chain from the model
+input to the primary output and lowers it to fused device steps:
+
+* ``TreeStep``   TreeEnsemble{Classifier,Regressor} (+ a following Sigmoid folded into the
+                 post transform) -> K2 ``tree_ensemble`` on the complete-tree layout.
+* ``DenseStep``  Gemm / MatMul(+Add) with a following Relu/Sigmoid/Tanh fused into the
+                 epilogue -> K3 ``gemm`` (MFMA) or ``gemv`` (N == 1).
+* ``GRUStep``    ONNX GRU (forward, layout 0) -> K4 (cfg 5).
+* Identity / Flatten / Squeeze / Reshape to 2-D are folded away.
+
+Anything else raises :class:`PlanError`; the engine then runs that model through the C++
+CPU executor (explicitly, with a warning) rather than silently substituting torch ops.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+
+from ..native import native
+
+ML_DOMAIN = "ai.onnx.ml"
+POST = {0: "NONE", 1: "LOGISTIC", 2: "SOFTMAX", 3: "SOFTMAX_ZERO", 4: "PROBIT"}
+
+
+class PlanError(RuntimeError):
+    pass
+
+
+@dataclass
+class TreeStep:
+    n_trees: int
+    depth: int
+    k: int
+    n_out: int
+    post: int            # kernel post code: 0 none, 1 logistic, 2 softmax
+    average: int
+    binary_class: int    # -1 unless the classifier binary case
+    all_positive: int
+    max_feature: int
+    nodes_np: np.ndarray
+    leaves_np: np.ndarray
+    base_np: Optional[np.ndarray]
+    classifier: bool = False
+    nodes: Any = None
+    leaves: Any = None
+    base: Any = None
+    kind: str = "tree"
+
+    @property
+    def out_width(self) -> int:
+        return self.n_out
+
+
+@dataclass
+class DenseStep:
+    n: int
+    k: int
+    act: str
+    w_np: np.ndarray     # [N, K] float32 (logical)
+    b_np: Optional[np.ndarray]
+    w: Any = None        # bf16 [N_pad, K_pad] device
+    b: Any = None
+    kind: str = "dense"
+
+    @property
+    def out_width(self) -> int:
+        return self.n
+
+
+@dataclass
+class GRUStep:
+    hidden: int
+    in_dim: int
+    linear_before_reset: int
+    w_np: np.ndarray     # [3H, I]
+    r_np: np.ndarray     # [3H, H]
+    b_np: np.ndarray     # [6H]
+    seq: int = 0
+    dev: Dict[str, Any] = field(default_factory=dict)
+    kind: str = "gru"
+
+    @property
+    def out_width(self) -> int:
+        return self.hidden
+
+
+@dataclass
+class Plan:
+    family: str
+    in_width: int
+    steps: List[Any]
+    out_width: int
+    ml_col: int
+    metadata: Dict[str, str]
+    input_name: str
+    output_name: str
+    seq_input: bool = False
+
+    def describe(self) -> str:
+        parts = []
+        for s in self.steps:
+            if s.kind == "tree":
+                parts.append(f"tree(T={s.n_trees},D={s.depth},K={s.k},post={s.post})")
+            elif s.kind == "dense":
+                parts.append(f"dense({s.k}->{s.n},{s.act})")
+            else:
+                parts.append(f"gru(I={s.in_dim},H={s.hidden})")
+        return " -> ".join(parts)
+
+
+def _consumers(nodes, name):
+    return [n for n in nodes if name in n["inputs"]]
+
+
+def compile_onnx(model, input_name: str = "input", output_name: str = "output",
+                 depth_limit: int = 12) -> Plan:
+    """``model``: _native.OnnxModel. Returns a host-side Plan (upload with :func:`to_device`)."""
+    N = native()
+    ex = N.Executor(model)
+    nodes = model.nodes()
+    index = {id(n): i for i, n in enumerate(nodes)}
+    inputs = {v[0]: v for v in model.inputs()}
+    if input_name not in inputs:
+        if len(inputs) == 1:
+            input_name = next(iter(inputs))
+        else:
+            raise PlanError(f"model has no input named {input_name!r}")
+    outs = [v[0] for v in model.outputs()]
+    if output_name not in outs:
+        output_name = outs[-1]
+    in_vi = inputs[input_name]
+    dims = in_vi[2]
+    seq_input = len(dims) == 3
+    in_width = int(dims[-1]) if dims and dims[-1] > 0 else -1
+    inits = set(model.initializer_names())
+
+    def const(name):
+        return model.initializer(name)
+
+    steps: List[Any] = []
+    cur = input_name
+    width = in_width
+    ml_col = 0
+    visited = set()
+    while cur != output_name:
+        cons = [n for n in _consumers(nodes, cur) if id(n) not in visited]
+        if len(cons) != 1:
+            raise PlanError(f"value {cur!r} feeds {len(cons)} nodes; only chains are lowered")
+        n = cons[0]
+        visited.add(id(n))
+        op, a = n["op_type"], n["attrs"]
+        if op in ("TreeEnsembleClassifier", "TreeEnsembleRegressor"):
+            c = ex.tree_complete(index[id(n)], depth_limit)
+            if c["aggregate"] not in (0, 1):
+                raise PlanError("TreeEnsemble aggregate MIN/MAX is CPU-only")
+            post = {0: 0, 1: 1, 2: 2}.get(int(c["post"]))
+            if post is None:
+                raise PlanError(f"TreeEnsemble post_transform {POST[int(c['post'])]} is CPU-only")
+            binary = bool(c["binary_case"])
+            k = int(c["k"])
+            n_out = int(c["n_outputs"]) if c["classifier"] else k
+            base = c["base_values"]
+            if binary:
+                bv = base[:1] if len(base) == 1 else (base[c["binary_class"]:c["binary_class"] + 1]
+                                                      if len(base) == 2 else None)
+                base = bv
+            ts = TreeStep(n_trees=int(c["n_trees"]), depth=int(c["depth"]), k=k, n_out=n_out, post=post,
+                          average=int(c["aggregate"] == 1), binary_class=int(c["binary_class"]) if binary else -1,
+                          all_positive=int(bool(c["weights_all_positive"])), max_feature=int(c["max_feature"]),
+                          nodes_np=np.ascontiguousarray(c["nodes"], np.float32),
+                          leaves_np=np.ascontiguousarray(c["leaves"], np.float32),
+                          base_np=None if base is None or len(base) == 0 else np.asarray(base, np.float32),
+                          classifier=bool(c["classifier"]))
+            steps.append(ts)
+            width = n_out
+            if c["classifier"]:
+                # outputs: (label, probabilities); continue on the probability tensor
+                prob = n["outputs"][1] if len(n["outputs"]) > 1 else n["outputs"][0]
+                ml_col = 1 if n_out == 2 else 0
+                cur = prob
+            else:
+                cur = n["outputs"][0]
+            continue
+        if op in ("Gemm", "MatMul"):
+            w = const(n["inputs"][1]) if n["inputs"][1] in inits else None
+            if w is None:
+                raise PlanError(f"{op}: weight must be an initializer")
+            w = np.asarray(w, np.float32)
+            if op == "Gemm":
+                if int(a.get("transA", 0)):
+                    raise PlanError("Gemm transA=1 is not lowered")
+                if int(a.get("transB", 0)):
+                    w = w.T
+                alpha = float(a.get("alpha", 1.0))
+                beta = float(a.get("beta", 1.0))
+                w = w * alpha
+                b = None
+                if len(n["inputs"]) > 2 and n["inputs"][2]:
+                    b = np.asarray(const(n["inputs"][2]), np.float32).ravel() * beta
+                    if b.size == 1 and w.shape[1] > 1:
+                        b = np.full(w.shape[1], b[0], np.float32)
+            else:
+                b = None
+            out_name = n["outputs"][0]
+            if op == "MatMul":
+                nxt = _consumers(nodes, out_name)
+                if len(nxt) == 1 and nxt[0]["op_type"] == "Add" and id(nxt[0]) not in visited:
+                    other = [i for i in nxt[0]["inputs"] if i != out_name][0]
+                    if other in inits:
+                        b = np.asarray(const(other), np.float32).ravel()
+                        visited.add(id(nxt[0]))
+                        out_name = nxt[0]["outputs"][0]
+            act = "none"
+            nxt = _consumers(nodes, out_name)
+            if len(nxt) == 1 and nxt[0]["op_type"] in ("Relu", "Sigmoid", "Tanh") and id(nxt[0]) not in visited:
+                act = nxt[0]["op_type"].lower()
+                visited.add(id(nxt[0]))
+                out_name = nxt[0]["outputs"][0]
+            if width > 0 and w.shape[0] != width:
+                raise PlanError(f"{op}: weight rows {w.shape[0]} != input width {width}")
+            steps.append(DenseStep(n=int(w.shape[1]), k=int(w.shape[0]), act=act,
+                                   w_np=np.ascontiguousarray(w.T, np.float32), b_np=b))
+            width = int(w.shape[1])
+            ml_col = 0
+            cur = out_name
+            continue
+        if op in ("Relu", "Sigmoid", "Tanh"):
+            last = steps[-1] if steps else None
+            if isinstance(last, DenseStep) and last.act == "none":
+                last.act = op.lower()
+            elif isinstance(last, TreeStep) and op == "Sigmoid" and last.post == 0:
+                last.post = 1
+            else:
+                raise PlanError(f"standalone {op} is not lowered")
+            cur = n["outputs"][0]
+            continue
+        if op in ("Identity", "Flatten"):
+            cur = n["outputs"][0]
+            continue
+        if op in ("Squeeze", "Reshape", "Unsqueeze"):
+            # shape-only between GRU layers / before the head (validated by the CPU executor)
+            cur = n["outputs"][0]
+            continue
+        if op == "GRU":
+            if a.get("direction", "forward") != "forward" or int(a.get("layout", 0)) != 0:
+                raise PlanError("GRU: only forward, layout 0 is lowered")
+            if len(n["inputs"]) > 4 and n["inputs"][4]:
+                raise PlanError("GRU: sequence_lens is not lowered")
+            W = np.asarray(const(n["inputs"][1]), np.float32)[0]
+            R = np.asarray(const(n["inputs"][2]), np.float32)[0]
+            H = int(a.get("hidden_size", R.shape[-1]))
+            B = (np.asarray(const(n["inputs"][3]), np.float32)[0] if len(n["inputs"]) > 3 and n["inputs"][3]
+                 else np.zeros(6 * H, np.float32))
+            steps.append(GRUStep(hidden=H, in_dim=int(W.shape[1]),
+                                 linear_before_reset=int(a.get("linear_before_reset", 0)),
+                                 w_np=W, r_np=R, b_np=B, seq=int(dims[0]) if dims[0] > 0 else 0))
+            width = H
+            # continue on Y (chained GRU) or Y_h (head)
+            y, yh = n["outputs"][0], (n["outputs"][1] if len(n["outputs"]) > 1 else "")
+            y_used = bool(y) and any(id(c) not in visited for c in _consumers(nodes, y))
+            cur = y if y_used else yh
+            continue
+        raise PlanError(f"op {op} is not lowered to the device")
+    fam = model.metadata.get("family", "")
+    if not fam:
+        kinds = [s.kind for s in steps]
+        fam = ("gbdt" if kinds == ["tree"] else "stacked" if kinds and kinds[0] == "tree"
+               else "gru" if "gru" in kinds else "mlp")
+    return Plan(family=fam, in_width=in_width, steps=steps, out_width=width, ml_col=ml_col,
+                metadata=dict(model.metadata), input_name=input_name, output_name=output_name,
+                seq_input=seq_input)
+
+
+def _bf16_padded(w: np.ndarray, n_mult: int = 128, k_mult: int = 64):
+    import torch
+    n, k = w.shape
+    npad = -(-n // n_mult) * n_mult
+    kpad = -(-k // k_mult) * k_mult
+    buf = np.zeros((npad, kpad), np.float32)
+    buf[:n, :k] = w
+    return torch.from_numpy(buf).to(torch.bfloat16)
+
+
+def to_device(plan: Plan, device) -> Plan:
+    import torch
+    for s in plan.steps:
+        if s.kind == "tree":
+            s.nodes = torch.from_numpy(s.nodes_np).to(device)
+            s.leaves = torch.from_numpy(s.leaves_np).to(device)
+            s.base = None if s.base_np is None else torch.from_numpy(s.base_np).to(device)
+        elif s.kind == "dense":
+            s.w = _bf16_padded(s.w_np).to(device)
+            s.b = None if s.b_np is None else torch.from_numpy(np.ascontiguousarray(s.b_np)).to(device)
+        elif s.kind == "gru":
+            s.dev = gru_device_weights(s, device)
+    return plan
+
+
+def gru_device_weights(s: GRUStep, device) -> Dict[str, Any]:
+    import torch
+    H = s.hidden
+    d = {
+        "R": torch.from_numpy(np.ascontiguousarray(s.r_np)).to(torch.bfloat16).to(device),
+        "bias": torch.from_numpy(np.ascontiguousarray(s.b_np, np.float32)).to(device),
+        # input projection as a dense layer [3H, I] (W rows are output columns already)
+        "W": _bf16_padded(np.ascontiguousarray(s.w_np)).to(device),
+        "Wb": torch.from_numpy(np.ascontiguousarray(s.b_np[:3 * H], np.float32)).to(device),
+    }
+    return d

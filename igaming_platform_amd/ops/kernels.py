@@ -1,0 +1,171 @@
+"""Typed launch wrappers for the gfx950 kernels in ``_hipk``.
+
+Every wrapper checks — on the host, before the launch — that operands live on the same GPU,
+are contiguous, have the dtype the kernel reads and are at least as large as the grid will
+index (a kernel fault can reset every GPU of a node, so nothing is left to the device).
+All launches go to the caller's current torch stream and are hipGraph-capturable.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ..native import hipk
+from ..layouts import check_layouts
+
+ACT = {"none": 0, "relu": 1, "sigmoid": 2, "tanh": 3}
+_checked = False
+
+
+def _mod():
+    global _checked
+    m = hipk()
+    if not _checked:
+        check_layouts(m)
+        _checked = True
+    return m
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _need(t: Optional[torch.Tensor], name: str, dtype=None, min_numel: int = 0, device=None):
+    if t is None:
+        raise ValueError(f"{name}: tensor required")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: must be a GPU tensor")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name}: on {t.device}, expected {device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if dtype is not None and t.dtype not in (dtype if isinstance(dtype, tuple) else (dtype,)):
+        raise ValueError(f"{name}: dtype {t.dtype}, expected {dtype}")
+    if t.numel() < min_numel:
+        raise ValueError(f"{name}: {t.numel()} elements < {min_numel} required")
+    return t.data_ptr()
+
+
+def _opt(t: Optional[torch.Tensor], name: str, **kw):
+    return None if t is None else _need(t, name, **kw)
+
+
+# --------------------------------------------------------------------------- K1
+def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch.Tensor,
+                     X: torch.Tensor, feat: torch.Tensor, n_rows: int) -> None:
+    dev = store.device
+    if X.dim() != 2 or X.shape[1] < 30 + store.ext_width:
+        raise ValueError("X must be [rows, >= 30 + ext_width]")
+    d = dict(
+        hdr=_need(hdr, "hdr", torch.int64, 2, dev), cfg=_need(cfg_dev, "cfg", torch.uint8, 176, dev),
+        req=_need(req, "req", torch.uint8, 48 * n_rows, dev),
+        ring_ts=_need(store.ring_ts, "ring_ts", torch.int32), ring_amt=_need(store.ring_amt, "ring_amt", torch.int64),
+        hll=_need(store.hll, "hll", torch.uint8), rt=_need(store.rt, "rt", torch.int32),
+        batch=_need(store.batch, "batch", torch.int32), ext=_need(store.ext, "ext", torch.float32),
+        bl_keys=_need(store.bl_keys, "bl_keys", torch.int64), bl_exp=_need(store.bl_exp, "bl_exp", torch.int32),
+        ip_keys=_need(store.ip_keys, "ip_keys", torch.int64), ip_flags=_need(store.ip_flags, "ip_flags", torch.int32),
+        X=_need(X, "X", torch.float32, X.shape[1] * n_rows, dev),
+        feat=_need(feat, "feat", torch.int32, 32 * n_rows, dev),
+        x_stride=int(X.shape[1]), ring_size=int(store.ring_ts.shape[1]), n_rows=int(n_rows),
+    )
+    _mod().feature_assemble(d, _stream())
+
+
+# --------------------------------------------------------------------------- K6
+def feature_update(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int,
+                   n_ptr: Optional[torch.Tensor] = None, n: int = 0) -> None:
+    dev = store.device
+    if n_max > store.max_events:
+        raise ValueError(f"feature_update: {n_max} events > store.max_events {store.max_events}")
+    d = dict(
+        cfg=_need(cfg_dev, "cfg", torch.uint8, 176, dev), n_ptr=_opt(n_ptr, "n_ptr", dtype=torch.int32),
+        n=int(n), n_max=int(n_max), req=_need(req, "req", torch.uint8, 48 * n_max, dev),
+        ring_ts=_need(store.ring_ts, "ring_ts", torch.int32), ring_amt=_need(store.ring_amt, "ring_amt", torch.int64),
+        hll=_need(store.hll, "hll", torch.uint8), rt=_need(store.rt, "rt", torch.int32),
+        ev=_opt(store.ev, "ev", dtype=torch.int16),
+        ring_size=int(store.ring_ts.shape[1]),
+        ev_ring=int(store.ev.shape[1]) if store.ev is not None else 0,
+        ev_dim=int(store.ev.shape[2]) if store.ev is not None else 0,
+        dcap=int(store.dcap), dkeys=_need(store.dkeys, "dkeys", torch.int32),
+        dfirst=_need(store.dfirst, "dfirst", torch.int32), dcount=_need(store.dcount, "dcount", torch.int32),
+    )
+    if n_ptr is None and n > n_max:
+        raise ValueError("n > n_max")
+    _mod().feature_update(d, _stream())
+
+
+# --------------------------------------------------------------------------- K2
+def tree_ensemble(tp, X: torch.Tensor, out: torch.Tensor, n_rows: int,
+                  partial: Optional[torch.Tensor] = None, groups: int = 1) -> None:
+    """``tp``: models.plan.TreeStep with device tensors."""
+    dev = X.device
+    if tp.k not in (1, 2, 4, 8, 16, 32, 64):
+        raise ValueError(f"tree kernel built for K in 1,2,4,8,16,32,64; got {tp.k}")
+    if X.shape[1] <= tp.max_feature:
+        raise ValueError("X narrower than the ensemble's largest feature id")
+    if groups > 1 and (partial is None or partial.numel() < groups * n_rows * tp.k):
+        raise ValueError("grouped tree launch needs a [groups, rows, K] partial buffer")
+    d = dict(
+        X=_need(X, "X", torch.float32, X.shape[1] * n_rows), nodes=_need(tp.nodes, "nodes", torch.float32, device=dev),
+        leaves=_need(tp.leaves, "leaves", torch.float32, device=dev), base=_opt(tp.base, "base", dtype=torch.float32),
+        out=_need(out, "out", torch.float32, tp.n_out * n_rows, dev), x_stride=int(X.shape[1]),
+        n_rows=int(n_rows), n_trees=tp.n_trees, depth=tp.depth, k=tp.k, n_out=tp.n_out, post=tp.post,
+        average=tp.average, binary_class=tp.binary_class, all_positive=tp.all_positive,
+        groups=int(groups), partial=_opt(partial, "partial", dtype=torch.float32),
+    )
+    if tp.nodes.numel() < tp.n_trees * ((1 << tp.depth) - 1) * 2:
+        raise ValueError("node table smaller than n_trees * (2^depth - 1)")
+    if tp.leaves.numel() < tp.n_trees * (1 << tp.depth) * tp.k:
+        raise ValueError("leaf table smaller than n_trees * 2^depth * K")
+    _mod().tree_ensemble(d, _stream())
+
+
+# --------------------------------------------------------------------------- K3
+def dense(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], Y: torch.Tensor,
+          M: int, N: int, K: int, act: str = "none", m_ptr: Optional[torch.Tensor] = None) -> None:
+    """Y[:M,:N] = act(X[:M,:K] W^T + b); W bf16 [N_pad(128), K_pad(64)] from models.plan."""
+    dev = X.device
+    if X.dtype not in (torch.float32, torch.bfloat16) or Y.dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError("dense: X and Y must be float32 or bfloat16")
+    if W.dtype != torch.bfloat16 or W.dim() != 2:
+        raise ValueError("dense: W must be 2-D bfloat16")
+    if N == 1:
+        if W.shape[1] < K:
+            raise ValueError("dense: W narrower than K")
+    elif W.shape[0] % 128 or W.shape[1] % 64 or W.shape[0] < N or W.shape[1] < K:
+        raise ValueError("dense: W must be padded to [N_pad % 128 == 0, K_pad % 64 == 0]")
+    if X.shape[1] < K or Y.shape[1] < N or X.shape[0] < M or Y.shape[0] < M:
+        raise ValueError("dense: operand shapes smaller than M/N/K")
+    if bias is not None and bias.numel() < N:
+        raise ValueError("dense: bias shorter than N")
+    d = dict(X=_need(X, "X", device=dev), W=_need(W, "W", device=dev), bias=_opt(bias, "bias", dtype=torch.float32),
+             Y=_need(Y, "Y", device=dev), m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32), M=int(M), N=int(N),
+             K=int(K), ldx=int(X.shape[1]), ldy=int(Y.shape[1]), ldw=int(W.shape[1]),
+             x_bf16=int(X.dtype == torch.bfloat16), y_bf16=int(Y.dtype == torch.bfloat16), act=ACT[act])
+    if N == 1:
+        _mod().gemv(d, _stream())
+    else:
+        _mod().gemm(d, _stream())
+
+
+# --------------------------------------------------------------------------- K5 / K10
+def ensemble(hdr, cfg_dev, feat, X, ml: Optional[torch.Tensor], out, n_rows: int,
+             metrics: Optional[torch.Tensor] = None) -> None:
+    dev = feat.device
+    d = dict(hdr=_need(hdr, "hdr", torch.int64, 2, dev), cfg=_need(cfg_dev, "cfg", torch.uint8, 176, dev),
+             feat=_need(feat, "feat", torch.int32, 32 * n_rows, dev),
+             X=_need(X, "X", torch.float32, X.shape[1] * n_rows, dev), x_stride=int(X.shape[1]),
+             ml=_opt(ml, "ml", dtype=torch.float32), out=_need(out, "out", torch.int32, 2 * n_rows, dev),
+             metrics=_opt(metrics, "metrics", dtype=torch.int64, min_numel=128), n_rows=int(n_rows))
+    _mod().ensemble(d, _stream())
+
+
+# --------------------------------------------------------------------------- K9
+def ltv(pf: torch.Tensor, out: torch.Tensor, model_ltv: Optional[torch.Tensor] = None) -> None:
+    B = pf.shape[0]
+    if pf.dim() != 2 or pf.shape[1] != 25:
+        raise ValueError("ltv: player features must be [B, 25]")
+    d = dict(pf=_need(pf, "pf", torch.float32), out=_need(out, "out", torch.float32, 6 * B),
+             ltv_model=_opt(model_ltv, "ltv_model", dtype=torch.float32, min_numel=B), B=int(B))
+    _mod().ltv(d, _stream())

@@ -1,0 +1,83 @@
+"""Shared helpers for golden-vs-device comparisons."""
+from __future__ import annotations
+
+import numpy as np
+
+from igaming_platform_amd.config import Config, TX_TYPE_ID
+from igaming_platform_amd.golden import scoring as GS
+from igaming_platform_amd.golden.features import GoldenFeatureStore, model_input
+from igaming_platform_amd.layouts import FR_BLACKLISTED
+from igaming_platform_amd.utils.synth import make_population, make_requests, to_events
+
+RAW_INT_FIELDS = ["tx_count_1m", "tx_count_5m", "tx_count_1h", "tx_sum_1h", "unique_devices_24h",
+                  "unique_ips_24h", "account_age_days", "total_deposits", "total_withdrawals",
+                  "net_deposit", "deposit_count", "withdraw_count", "time_since_last_tx_sec",
+                  "session_duration_sec", "bonus_claim_count"]
+RAW_F32_FIELDS = ["tx_avg_1h", "avg_bet_size", "win_rate", "bonus_wager_completion_rate"]
+
+
+def build_world(cfg: Config, n_accounts: int, seed: int, now: int, n_hist_batches: int = 6,
+                hist_batch: int = 512, blacklist_every: int = 37, intel_every: int = 29):
+    """Population + golden store (+ the event history to replay on the device)."""
+    ext_w = cfg.features.width - 30
+    pop = make_population(n_accounts, ext_w, seed=seed, now=now)
+    gold = GoldenFeatureStore(cfg.features)
+    for i, aid in enumerate(pop.ids):
+        gold.set_batch(aid, pop.golden_batch(i))
+        gold.set_ext(aid, pop.ext[i] if ext_w > 0 else None)
+    rng = np.random.default_rng(seed + 100)
+    hist = []
+    # history spread over ~2 days, ending just before now; later batches are denser/hotter
+    for b in range(n_hist_batches):
+        t_end = now - (n_hist_batches - 1 - b) * 7200 - 5
+        spread = 86400 if b == 0 else 3000
+        r = make_requests(pop, hist_batch, rng, t_end, spread_s=spread, hot_frac=0.15 if b >= n_hist_batches - 2 else 0.02,
+                          unknown_frac=0.02)
+        hist.append(r)
+        for ev in to_events(pop, r):
+            gold.apply(ev)
+    bl = []
+    for i in range(0, n_accounts, blacklist_every):
+        bl.append(("device", f"dev-{i}-0"))
+    for i in range(3, n_accounts, blacklist_every * 2):
+        bl.append(("ip", f"10.{i % 250}.{i // 250 % 250}.1"))
+    intel = []
+    for i in range(5, n_accounts, intel_every):
+        intel.append((f"10.{i % 250}.{i // 250 % 250}.2", i % 3 == 0, i % 3 == 1, i % 3 == 2))
+    return pop, gold, hist, bl, intel
+
+
+def golden_score(cfg: Config, gold: GoldenFeatureStore, pop, row, now: int, model: str = "heuristic",
+                 ml_override=None):
+    s = int(row["slot"])
+    aid = pop.ids[s] if s >= 0 else "__unknown__"
+    f = gold.raw_features(aid, now, ip_hash=int(row["ip_hash"]))
+    if s < 0:
+        f["_partial"] = True
+    bl = gold.blacklisted([int(row["dev_hash"]), int(row["fp_hash"]), int(row["ip_hash"])], now)
+    amount, tx = int(row["amount"]), int(row["tx_type"])
+    rule, reasons = GS.apply_rules(cfg.scoring, f, amount, tx, bl)
+    ext = gold.accounts[aid].ext if (s >= 0 and aid in gold.accounts) else None
+    x = model_input(f, amount, tx, cfg.features.log_transform, cfg.features.width, ext)
+    if model == "none":
+        ml = None
+    elif model == "heuristic":
+        ml = GS.heuristic_predict(x)
+    else:
+        ml = ml_override
+    score, action, reasons, mlv = GS.ensemble(cfg.scoring, rule, reasons, ml)
+    return dict(features=f, blacklisted=bl, rule=rule, reasons=reasons, score=score, action=action,
+                ml=mlv, x=x)
+
+
+def compare_featrec(fr, g, row_idx: int):
+    f = g["features"]
+    for k in RAW_INT_FIELDS:
+        assert int(fr[k]) == int(f[k]), f"row {row_idx}: {k} device={fr[k]} golden={f[k]}"
+    for k in RAW_F32_FIELDS:
+        assert np.float32(fr[k]) == np.float32(f[k]), f"row {row_idx}: {k} device={fr[k]} golden={f[k]}"
+    flags = int(fr["flags"])
+    assert bool(flags & 1) == f["is_vpn"] and bool(flags & 2) == f["is_proxy"] and bool(flags & 4) == f["is_tor"], row_idx
+    assert bool(flags & 16) == f["bonus_only_player"], row_idx
+    assert bool(flags & FR_BLACKLISTED) == g["blacklisted"], row_idx
+    assert bool(flags & 64) == f["_partial"], row_idx

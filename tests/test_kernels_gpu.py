@@ -1,0 +1,268 @@
+"""Device kernels vs the golden spec / C++ CPU executor / torch fp32 (run on MI355X)."""
+import numpy as np
+import pytest
+
+from igaming_platform_amd.config import Config, REASON_BIT
+from igaming_platform_amd.golden import ltv as GL
+from igaming_platform_amd.layouts import FEATREC, REQREC
+from igaming_platform_amd.utils.hashing import SEED_IP, id_hash
+
+from .helpers import build_world, compare_featrec, golden_score
+
+pytestmark = pytest.mark.gpu
+
+NOW = 1_760_000_000
+
+
+def _store_and_world(cfg, n_acc=300, seed=1):
+    import torch
+    from igaming_platform_amd.features.device_store import DeviceFeatureStore
+    from igaming_platform_amd.ops import kernels as K
+    pop, gold, hist, bl, intel = build_world(cfg, n_acc, seed, NOW)
+    store = DeviceFeatureStore(n_acc, cfg.features, "cuda", events=True, max_events=2048)
+    store.set_batch_features(np.arange(n_acc), pop.batch)
+    if cfg.features.width > 30:
+        store.set_ext(np.arange(n_acc), pop.ext)
+    for t, v in bl:
+        e = store.blacklist.add(t, v, reason="test")
+        gold.blacklist[id_hash(v, {"device": 0x44455649, "ip": SEED_IP}[t])] = e.expires_at
+    for ip, vpn, proxy, tor in intel:
+        store.ipintel.set(ip, vpn, proxy, tor)
+        gold.ip_intel[id_hash(ip, SEED_IP)] = (1 if vpn else 0) | (2 if proxy else 0) | (4 if tor else 0)
+    store.sync_tables()
+    cfg_dev = torch.zeros(176, dtype=torch.uint8, device="cuda")
+    from igaming_platform_amd.layouts import score_cfg
+    cfg_dev.copy_(torch.from_numpy(score_cfg(cfg, 1, **store.table_params()).view(np.uint8).copy()))
+    for r in hist:
+        req = torch.from_numpy(r.view(np.uint8).copy()).cuda()
+        K.feature_update(store, cfg_dev, req, len(r), n=len(r))
+    torch.cuda.synchronize()
+    return pop, gold, store
+
+
+@pytest.mark.parametrize("width,log_mode,sum_mode", [(30, "log1p", "sliding"), (40, "identity", "compat")])
+def test_feature_pipeline_matches_golden(width, log_mode, sum_mode):
+    from igaming_platform_amd.engine.scorer import GpuScorer
+    cfg = Config()
+    cfg.features.width = width
+    cfg.features.log_transform = log_mode
+    cfg.features.sum_mode = sum_mode
+    cfg.gpu.buckets = [64, 256, 1024]
+    pop, gold, store = _store_and_world(cfg)
+    scorer = GpuScorer(cfg, store, plan=None, model="heuristic", update_features=True)
+    rng = np.random.default_rng(7)
+    from igaming_platform_amd.utils.synth import make_requests, to_events
+    for it in range(3):
+        now = NOW + 60 * it
+        req = make_requests(pop, 700, rng, now, hot_frac=0.2, unknown_frac=0.03)
+        req["ts"] = now
+        out = scorer.score(req, now=now, want_features=True)
+        feats = out["features"]
+        for i, row in enumerate(req):
+            g = golden_score(cfg, gold, pop, row, now)
+            compare_featrec(feats[i], g, i)
+            assert out["score"][i] == g["score"], (i, out["score"][i], g["score"])
+            assert out["action"][i] == g["action"], i
+            assert out["rule_score"][i] == g["rule"], i
+            mask = sum(1 << REASON_BIT[r] for r in g["reasons"])
+            assert out["reasons"][i] == mask, (i, out["reasons"][i], g["reasons"])
+            assert np.float32(out["ml"][i]) == np.float32(g["ml"]), i
+        # score-then-update: the golden applies the batch after scoring it
+        for ev in to_events(pop, req):
+            gold.apply(ev)
+
+
+def test_normalized_inputs_match_golden():
+    import torch
+    from igaming_platform_amd.engine.scorer import GpuScorer
+    cfg = Config()
+    cfg.features.width = 40
+    cfg.gpu.buckets = [512]
+    pop, gold, store = _store_and_world(cfg, n_acc=200, seed=3)
+    scorer = GpuScorer(cfg, store, plan=None, model="heuristic", update_features=False, use_graphs=False)
+    rng = np.random.default_rng(9)
+    from igaming_platform_amd.utils.synth import make_requests
+    req = make_requests(pop, 500, rng, NOW, hot_frac=0.1)
+    scorer.score(req, now=NOW)
+    X = scorer.X[:500].cpu().numpy()
+    for i, row in enumerate(req):
+        g = golden_score(cfg, gold, pop, row, NOW)
+        np.testing.assert_allclose(X[i], g["x"], rtol=2e-7, atol=0, err_msg=f"row {i}")
+
+
+def test_graph_replay_equals_eager():
+    from igaming_platform_amd.engine.scorer import GpuScorer
+    cfg = Config()
+    cfg.gpu.buckets = [128, 1024]
+    pop, gold, store = _store_and_world(cfg, n_acc=256, seed=5)
+    sa = GpuScorer(cfg, store, plan=None, model="heuristic", update_features=False, use_graphs=False)
+    sb = GpuScorer(cfg, store, plan=None, model="heuristic", update_features=False, use_graphs=True)
+    sb.capture()
+    from igaming_platform_amd.utils.synth import make_requests
+    rng = np.random.default_rng(11)
+    for n in (1, 77, 128, 900):
+        req = make_requests(pop, n, rng, NOW)
+        a = sa.score(req, now=NOW)
+        b = sb.score(req, now=NOW)
+        for k in ("score", "action", "reasons", "rule_score", "ml"):
+            np.testing.assert_array_equal(a[k], b[k])
+
+
+# ----------------------------------------------------------------------------- trees
+def _tree_case(kind, **kw):
+    import torch
+    from igaming_platform_amd.models.plan import compile_onnx, to_device
+    from igaming_platform_amd.native import native
+    from igaming_platform_amd.onnx import builders
+    N = native()
+    m = N.OnnxModel.from_bytes(builders.build(kind, **kw).SerializeToString())
+    plan = to_device(compile_onnx(m), "cuda")
+    return N, m, plan
+
+
+@pytest.mark.parametrize("kind,kw,groups", [
+    ("gbdt", dict(n_trees=100, depth=7), 1), ("gbdt", dict(n_trees=100, depth=7), 6),
+    ("gbdt", dict(n_trees=37, depth=5, mixed_modes=True), 3),
+])
+def test_tree_kernel_matches_cpu_executor(kind, kw, groups):
+    import torch
+    from igaming_platform_amd.ops import kernels as K
+    N, m, plan = _tree_case(kind, **kw)
+    ts = plan.steps[0]
+    rng = np.random.default_rng(0)
+    for rows in (1, 63, 1000, 4096):
+        X = rng.uniform(0, 1, (rows, 128)).astype(np.float32)
+        X[rng.uniform(0, 1, X.shape) < 0.01] = np.nan
+        X[:, 5] = ts.nodes_np[0, 0, 0] if ts.nodes_np.size else 0.5  # hit a threshold exactly
+        ref = N.Executor(m).run({"input": X})["output"]
+        Xd = torch.from_numpy(X).cuda()
+        out = torch.zeros((rows, ts.n_out), dtype=torch.float32, device="cuda")
+        part = torch.zeros(max(groups, 1) * rows * ts.k, dtype=torch.float32, device="cuda")
+        K.tree_ensemble(ts, Xd, out, rows, partial=part, groups=groups)
+        np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=2e-6)
+
+
+def test_stacked_tree_embedding_matches_cpu():
+    import torch
+    from igaming_platform_amd.ops import kernels as K
+    from igaming_platform_amd.onnx import builders, writer
+    from igaming_platform_amd.native import native
+    N = native()
+    # regressor-only model (the embedding part of cfg 3)
+    full = builders.stacked(n_trees=50, depth=6, k=32)
+    g = full.graph
+    nodes = [g.node[0]]
+    nodes[0].output[0] = "output"
+    reg = writer.model(nodes, [g.input[0]], [writer.value_info("output", 1, ["N", 32])], name="emb")
+    m = N.OnnxModel.from_bytes(reg.SerializeToString())
+    from igaming_platform_amd.models.plan import compile_onnx, to_device
+    plan = to_device(compile_onnx(m), "cuda")
+    ts = plan.steps[0]
+    X = np.random.default_rng(1).uniform(0, 1, (2048, 128)).astype(np.float32)
+    ref = N.Executor(m).run({"input": X})["output"]
+    out = torch.zeros((2048, 32), dtype=torch.float32, device="cuda")
+    part = torch.zeros(4 * 2048 * 32, dtype=torch.float32, device="cuda")
+    for groups in (1, 4):
+        K.tree_ensemble(ts, torch.from_numpy(X).cuda(), out, 2048, partial=part, groups=groups)
+        np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+
+
+# ----------------------------------------------------------------------------- dense / MFMA
+@pytest.mark.parametrize("M,N,Kd,act,xbf", [
+    (1, 32, 32, "relu", False), (37, 256, 32, "relu", False), (4096, 512, 256, "relu", True),
+    (8192, 256, 32, "none", False), (1000, 768, 16, "none", True), (333, 1, 256, "sigmoid", False),
+    (5000, 512, 512, "tanh", True),
+])
+def test_dense_mfma_matches_torch_fp32(M, N, Kd, act, xbf):
+    import torch
+    from igaming_platform_amd.models.plan import _bf16_padded
+    from igaming_platform_amd.ops import kernels as K
+    g = torch.Generator().manual_seed(M + N + Kd)
+    X = torch.randn(M, Kd, generator=g)
+    W = torch.randn(N, Kd, generator=g) / Kd ** 0.5     # [N, K] = output rows
+    b = torch.randn(N, generator=g) * 0.1
+    Xd = (X.to(torch.bfloat16) if xbf else X).cuda()
+    Wd = _bf16_padded(W.numpy()).cuda()
+    Y = torch.zeros(M, N, dtype=torch.float32, device="cuda")
+    K.dense(Xd, Wd, b.cuda(), Y, M, N, Kd, act=act)
+    ref = X.to(torch.bfloat16).float() @ W.to(torch.bfloat16).float().T + b
+    ref = {"relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh, "none": lambda t: t}[act](ref)
+    torch.testing.assert_close(Y.cpu(), ref, rtol=2e-3, atol=2e-3)
+
+
+def test_dense_respects_live_rows():
+    import torch
+    from igaming_platform_amd.models.plan import _bf16_padded
+    from igaming_platform_amd.ops import kernels as K
+    X = torch.randn(256, 64).cuda()
+    Wd = _bf16_padded(np.random.default_rng(0).standard_normal((128, 64)).astype(np.float32)).cuda()
+    Y = torch.full((256, 128), 7.0, device="cuda")
+    m = torch.tensor([100], dtype=torch.int32, device="cuda")
+    K.dense(X, Wd, None, Y, 256, 128, 64, m_ptr=m)
+    assert torch.all(Y[100:] == 7.0)
+    assert not torch.all(Y[:100] == 7.0)
+
+
+# ----------------------------------------------------------------------------- full model plans
+@pytest.mark.parametrize("kind,width", [("logistic", 32), ("gbdt", 128), ("stacked", 128)])
+def test_scorer_with_model_matches_executor_and_golden(kind, width):
+    import torch
+    from igaming_platform_amd.engine.scorer import GpuScorer
+    from igaming_platform_amd.models.plan import compile_onnx, to_device
+    from igaming_platform_amd.native import native
+    from igaming_platform_amd.onnx import builders
+    cfg = Config()
+    cfg.features.width = width
+    cfg.gpu.buckets = [256, 1024]
+    pop, gold, store = _store_and_world(cfg, n_acc=300, seed=2)
+    N = native()
+    m = N.OnnxModel.from_bytes(builders.build(kind).SerializeToString())
+    plan = to_device(compile_onnx(m), "cuda")
+    sc = GpuScorer(cfg, store, plan=plan, model="plan", update_features=False)
+    sc.capture()
+    rng = np.random.default_rng(4)
+    from igaming_platform_amd.utils.synth import make_requests
+    req = make_requests(pop, 1000, rng, NOW, hot_frac=0.1)
+    out = sc.score(req, now=NOW)
+    X = sc.X[:1000].cpu().numpy()
+    ref = N.Executor(m).run({"input": X})["output"]
+    col = plan.ml_col
+    ml_ref = np.clip(ref[:, col], 0, 1)
+    tol = 2e-2 if kind != "gbdt" else 1e-5   # bf16 MFMA head vs fp32 executor
+    np.testing.assert_allclose(out["ml"], ml_ref, atol=tol)
+    # rules/ensemble exact given the device's own ml value
+    for i, row in enumerate(req):
+        g = golden_score(cfg, gold, pop, row, NOW, model="plan", ml_override=float(out["ml"][i]))
+        assert out["score"][i] == g["score"] and out["action"][i] == g["action"], i
+        assert out["reasons"][i] == sum(1 << REASON_BIT[r] for r in g["reasons"]), i
+
+
+# ----------------------------------------------------------------------------- LTV
+def test_ltv_kernel_matches_golden():
+    import torch
+    from igaming_platform_amd.ops import kernels as K
+    rng = np.random.default_rng(3)
+    n = 3000
+    rows = []
+    for i in range(n):
+        f = GL.PlayerFeatures(
+            days_since_registration=int(rng.integers(0, 400)), days_since_last_deposit=int(rng.integers(0, 60)),
+            days_since_last_bet=int(rng.integers(0, 60)), sessions_per_week=float(np.float32(rng.uniform(0, 8))),
+            total_deposits=float(np.float32(rng.uniform(0, 5e4))), total_withdrawals=float(np.float32(rng.uniform(0, 5e4))),
+            net_revenue=float(np.float32(rng.normal(500, 3000))), deposit_frequency=float(np.float32(rng.uniform(0, 6))),
+            bet_count=int(rng.integers(0, 300)), games_played=int(rng.integers(0, 20)),
+            bonuses_claimed=int(rng.integers(0, 6)), bonus_conversion_rate=float(np.float32(rng.uniform(0, 1))),
+            push_enabled=bool(rng.integers(0, 2)), email_opt_in=bool(rng.integers(0, 2)),
+            has_vip_manager=bool(rng.integers(0, 2)), support_tickets=int(rng.integers(0, 6)))
+        rows.append(f)
+    pf = torch.tensor(np.array([f.row() for f in rows], np.float32)).cuda()
+    out = torch.zeros((n, 6), dtype=torch.float32, device="cuda")
+    K.ltv(pf, out)
+    o = out.cpu().numpy()
+    for i, f in enumerate(rows):
+        p = GL.predict(f)
+        assert np.float32(o[i, 0]) == np.float32(p.predicted_ltv), i
+        assert np.float32(o[i, 1]) == np.float32(p.churn_risk), i
+        assert int(o[i, 2]) == p.survival_days and int(o[i, 4]) == p.segment, i
+        assert np.float32(o[i, 3]) == np.float32(p.confidence), i
+        assert GL.NBA_CODES[int(o[i, 5])] == p.next_best_action, i
