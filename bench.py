@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Headline benchmark: fraud scores/sec (whole node) + p99 score latency, MI355X.
+
+BASELINE.json metric "fraud scores/sec (whole node) + p99 score latency at 1/2/4/8 MI355X";
+default config = cfg 3, the data-parallel headline: GBDT+MLP stacked ensemble
+(ONNX TreeEnsembleRegressor(100 trees, depth 7, 128 features, 32 targets) -> Gemm(32x256)
+-> Relu -> Gemm(256x1) -> Sigmoid), micro-batch 8192 per GPU, DP over all GPUs with RCCL.
+
+One timed step per GPU = one full scoring micro-batch, nothing skipped:
+  host: pack 8192 requests (48 B ReqRec) into a pinned slab
+  GPU (one captured hipGraph): H2D slab -> feature_assemble (ring windows, HLL, blacklist,
+      ip-intel, rules) -> tree ensemble -> MFMA dense -> GEMV+sigmoid -> ensemble/action
+      (+metrics) -> feature_update (score-then-update) -> D2H results
+  RCCL: all_gather of the packed results across ranks (+ metrics all_reduce every 16 steps)
+Per-GPU work is fixed as N grows (weak scaling): global batch = 8192 x N per step.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|heuristic]
+For N > 1 run under torchrun (the driver does), or this script launches torchrun itself.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+BASELINE_P99_MS = 50.0  # README.md:58 "< 50ms latency" (the only published number)
+
+CONFIGS = {
+    "cfg3": dict(model="stacked", width=128, batch=8192,
+                 desc="cfg3 GBDT(100 trees,d7,128 feat)+MLP(32-256-1) stacked, TreeEnsembleRegressor->Gemm"),
+    "cfg2": dict(model="gbdt", width=128, batch=1024,
+                 desc="cfg2 GBDT fraud ensemble, 100 trees d7, 128 features, TreeEnsembleClassifier"),
+    "cfg1": dict(model="logistic", width=32, batch=8192, desc="cfg1 32-feature logistic (GPU path)"),
+    "heuristic": dict(model="heuristic", width=30, batch=8192, desc="reference rules + mockPredict heuristic"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU micro-batch (default: the config's)")
+    ap.add_argument("--accounts", type=int, default=1 << 20, help="feature-store accounts per GPU")
+    ap.add_argument("--depth", type=int, default=2, help="pipeline depth (batches in flight)")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-gather", action="store_true", help="skip the per-step RCCL all_gather")
+    ap.add_argument("--json-out", default="")
+    return ap.parse_args()
+
+
+def maybe_launch_torchrun(a) -> None:
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        port = 29500 + (os.getpid() % 1000)
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port)] + sys.argv
+        sys.exit(subprocess.call(cmd))
+
+
+def main():
+    a = parse()
+    maybe_launch_torchrun(a)
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.engine.scorer import GpuScorer
+    from igaming_platform_amd.features.device_store import DeviceFeatureStore
+    from igaming_platform_amd.layouts import REQREC
+    from igaming_platform_amd.models.plan import compile_onnx, to_device
+    from igaming_platform_amd.native import native
+    from igaming_platform_amd.onnx import builders
+    from igaming_platform_amd.ops import kernels as K
+    from igaming_platform_amd.utils.synth import NOW0, make_population, make_requests
+
+    c = CONFIGS[a.config]
+    B = a.batch or c["batch"]
+    cfg = Config()
+    cfg.features.width = c["width"]
+    cfg.gpu.buckets = [B]
+    cfg.gpu.max_batch = B
+    n_acc = a.accounts
+
+    # ---- per-rank shard: population, HBM store, model replica
+    pop = make_population(n_acc, c["width"] - 30, seed=1000 + rank, fast_hash=True)
+    store = DeviceFeatureStore(n_acc, cfg.features, dev, events=True, max_events=B)
+    store.set_batch_features(np.arange(n_acc), pop.batch)
+    if c["width"] > 30:
+        store.set_ext(np.arange(n_acc), pop.ext)
+    for i in range(0, 200):
+        store.blacklist.add("device", f"bad-device-{rank}-{i}")
+    store.sync_tables()
+    plan = None
+    model = "heuristic"
+    if c["model"] != "heuristic":
+        m = native().OnnxModel.from_bytes(builders.build(c["model"]).SerializeToString())
+        plan = to_device(compile_onnx(m), dev)
+        model = "plan"
+    sc = GpuScorer(cfg, store, plan=plan, model=model, device=dev, pipeline_depth=a.depth,
+                   use_graphs=not a.no_graphs)
+    rng = np.random.default_rng(7 + rank)
+    # warm the feature store with ~an hour of history (velocity windows, HLLs, sessions)
+    for h in range(24):
+        r = make_requests(pop, B, rng, NOW0 - 3600 + 150 * h, spread_s=150, hot_frac=0.01)
+        t = torch.from_numpy(r.view(np.uint8).copy()).to(dev)
+        K.feature_update(store, sc.cfg_dev, t, B, n=B)
+    torch.cuda.synchronize(dev)
+    sc.capture()
+    pool = [make_requests(pop, B, rng, NOW0, hot_frac=0.02, unknown_frac=0.001) for _ in range(8)]
+
+    gathered = torch.zeros(world * B * 2, dtype=torch.int32, device=dev) if world > 1 else None
+    met_sum = torch.zeros(128, dtype=torch.int64, device=dev)
+
+    def step(i: int, now: int):
+        slot = sc.next_slot()
+        v = sc.slab_view(slot, B)
+        v[:] = pool[i % len(pool)]
+        v["ts"] = now
+        p = sc.submit_packed(slot, B, now)
+        if world > 1 and not a.no_gather:
+            with torch.cuda.stream(sc.stream):
+                dist.all_gather_into_tensor(gathered, sc.res[:B].reshape(-1))
+                if i % 16 == 15:
+                    met_sum.copy_(sc.metrics)
+                    dist.all_reduce(met_sum)
+                p.event.record(sc.stream)
+        return p
+
+    inflight = []
+    lat = []
+    now = NOW0
+    for i in range(a.warmup):
+        inflight.append(step(i, now + i // 50))
+        if len(inflight) >= a.depth:
+            sc.wait(inflight.pop(0), unpack=False)
+    for p in inflight:
+        sc.wait(p, unpack=False)
+    inflight = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        p = step(a.warmup + i, now + (a.warmup + i) // 50)
+        inflight.append(p)
+        if len(inflight) >= a.depth:
+            q = inflight.pop(0)
+            sc.wait(q, unpack=False)
+            lat.append((time.perf_counter() - q.t_submit) * 1e3)
+    for q in inflight:
+        sc.wait(q, unpack=False)
+        lat.append((time.perf_counter() - q.t_submit) * 1e3)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stats = torch.tensor([elapsed, float(np.percentile(lat, 99)), float(np.percentile(lat, 50))],
+                         dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+    elapsed, p99, p50 = (float(x) for x in stats.cpu())
+    total = world * B * a.steps
+    out = {
+        "metric": "fraud scores/sec (whole node) + p99 score latency",
+        "value": total / elapsed,
+        "unit": "scores/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic",
+        "config": {
+            "model": c["desc"],
+            "global_batch": B * world,
+            "seq_len": 1,
+            "parallelism": f"dp{world}",
+            "per_gpu_batch": B,
+            "accounts_per_gpu": n_acc,
+            "pipeline_depth": a.depth,
+            "graphs": not a.no_graphs,
+            "numerics": "fp32 features+trees, bf16 MFMA MLP (fp32 accumulate), fp64 ensemble",
+        },
+        "p99_latency_ms": p99,
+        "p50_latency_ms": p50,
+        "latency_baseline_ms": BASELINE_P99_MS,
+        "latency_vs_baseline": BASELINE_P99_MS / p99 if p99 > 0 else None,
+    }
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -87,6 +87,13 @@ PYBIND11_MODULE(_hipk, m) {
     a.dkeys = ptr<int32_t*>(d, "dkeys");
     a.dfirst = ptr<int32_t*>(d, "dfirst");
     a.dcount = ptr<int32_t*>(d, "dcount");
+    a.dfill = ptr<int32_t*>(d, "dfill");
+    a.doff = ptr<int32_t*>(d, "doff");
+    a.dlist = ptr<int32_t*>(d, "dlist");
+    a.dtotal = ptr<int32_t*>(d, "dtotal");
+    if (!a.dkeys || !a.dfirst || !a.dcount || !a.dfill || !a.doff || !a.dlist || !a.dtotal)
+      throw std::runtime_error("feature_update: dedup scratch missing");
+    if (a.ev && a.ev_dim != 16) throw std::runtime_error("feature_update: event dim must be 16");
     launch_feature_update(a, stream_of(s));
     check("feature_update");
   });
@@ -139,6 +146,29 @@ PYBIND11_MODULE(_hipk, m) {
   m.def("gemv", [gemm_args](py::dict d, uintptr_t s) {
     launch_gemv(gemm_args(d), stream_of(s));
     check("gemv");
+  });
+
+  m.def("mlp_head", [](py::dict d, uintptr_t s) {
+    HeadArgs a{};
+    a.X = ptr<const void*>(d, "X");
+    a.W1 = ptr<const uint16_t*>(d, "W1");
+    a.b1 = ptr<const float*>(d, "b1");
+    a.w2 = ptr<const float*>(d, "w2");
+    a.b2 = d.contains("b2") ? d["b2"].cast<float>() : 0.f;
+    a.Y = ptr<float*>(d, "Y");
+    a.m_ptr = ptr<const int32_t*>(d, "m_ptr");
+    a.M = geti(d, "M");
+    a.K = geti(d, "K");
+    a.N1 = geti(d, "N1");
+    a.k_pad = geti(d, "k_pad");
+    a.ldx = geti(d, "ldx");
+    a.ldy = geti(d, "ldy");
+    a.x_bf16 = geti(d, "x_bf16");
+    a.act1 = geti(d, "act1");
+    a.act2 = geti(d, "act2");
+    if (a.k_pad % 32 || a.k_pad < a.K) throw std::runtime_error("mlp_head: k_pad must be a multiple of 32 >= K");
+    launch_mlp_head(a, stream_of(s));
+    check("mlp_head");
   });
 
   m.def("ensemble", [](py::dict d, uintptr_t s) {

@@ -212,13 +212,21 @@ __global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs a) {
 }
 
 // ---------------------------------------------------------------------------------- K6
-// Ordered per-account event application. Pass 1 registers each event's slot in a batch
-// scratch hash table (first index + count); pass 2: the first event of each account applies
-// all of that account's events in batch order (exclusive owner, no atomics on the state).
+// Ordered per-account event application without serial scans:
+//   reset   scratch table (keys, first, count, fill, off) + segment allocator
+//   insert  each event registers its slot: first index (atomicMin) and count (atomicAdd)
+//   single  accounts with one event in the batch apply it directly (the common case); the
+//           first event of a multi-event account reserves a segment of `count` list entries
+//   fill    every event of a multi-event account writes its index into that segment
+//   multi   the owner sorts its segment (batch order) and applies the events sequentially
+//           with the account's AcctRT held in registers (one load, one store).
+// The state of an account is only ever written by its single owner thread, so no atomics
+// touch the feature store itself.
 
-__global__ void dedup_reset_kernel(int32_t* keys, int32_t* first, int32_t* count, int cap) {
+__global__ void dedup_reset_kernel(UpdateArgs a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < cap) { keys[i] = -1; first[i] = 0x7fffffff; count[i] = 0; }
+  if (i < a.dcap) { a.dkeys[i] = -1; a.dfirst[i] = 0x7fffffff; a.dcount[i] = 0; a.dfill[i] = 0; }
+  if (i == 0) *a.dtotal = 0;
 }
 
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
@@ -226,10 +234,14 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   return x;
 }
 
+__device__ __forceinline__ int n_events(const UpdateArgs& a) {
+  const int n = a.n_ptr ? *a.n_ptr : a.n;
+  return n < a.n_max ? n : a.n_max;
+}
+
 __global__ void dedup_insert_kernel(UpdateArgs a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int n = a.n_ptr ? *a.n_ptr : a.n;
-  if (i >= n) return;
+  if (i >= n_events(a)) return;
   const int s = a.req[i].slot;
   if (s < 0) return;
   uint32_t h = mix32((uint32_t)s) & (uint32_t)(a.dcap - 1);
@@ -244,18 +256,46 @@ __global__ void dedup_insert_kernel(UpdateArgs a) {
   }
 }
 
-__device__ void apply_event(const UpdateArgs& a, int j) {
-  const ReqRec& ev = a.req[j];
+__device__ __forceinline__ int dedup_find(const UpdateArgs& a, int s) {
+  uint32_t h = mix32((uint32_t)s) & (uint32_t)(a.dcap - 1);
+  for (int p = 0; p < a.dcap; ++p) {
+    const int k = a.dkeys[h];
+    if (k == s) return (int)h;
+    if (k == -1) return -1;
+    h = (h + 1) & (uint32_t)(a.dcap - 1);
+  }
+  return -1;
+}
+
+__device__ __forceinline__ void hll_add(uint8_t* rg, uint32_t& exp, uint64_t h, int64_t now, int ttl,
+                                        bool& changed) {
+  if (now >= (int64_t)exp) {
+    uint4* w = reinterpret_cast<uint4*>(rg);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = make_uint4(0, 0, 0, 0);
+  }
+  const int idx = (int)(h & 255u);
+  const uint64_t wv = h >> 8;
+  const int rank = wv ? (__clzll((long long)wv) - 8 + 1) : 57;
+  if (rank > rg[idx]) {
+    rg[idx] = (uint8_t)rank;
+    changed = true;
+  }
+  exp = (uint32_t)(now + ttl);
+}
+
+// apply one event to an account whose AcctRT `r` the caller holds in registers
+__device__ void apply_event(const UpdateArgs& a, int j, AcctRT& r) {
+  const ReqRec ev = a.req[j];
   const int s = ev.slot;
   const int64_t now = ev.ts;
-  AcctRT r = a.rt[s];
   const ScoreCfg& cfg = *a.cfg;
   const int64_t amt = ev.amount;
   // tx ring (ZADD + trim; here: overwrite the oldest entry)
   const int hd = r.ring_head;
   a.ring_ts[(size_t)s * a.ring_size + hd] = (uint32_t)now;
   a.ring_amt[(size_t)s * a.ring_size + hd] = amt;
-  r.ring_head = (hd + 1) % a.ring_size;
+  r.ring_head = hd + 1 == a.ring_size ? 0 : hd + 1;
   // INCRBY + EXPIRE 1h (compat sum)
   if (now >= (int64_t)r.sum_exp) r.sum_compat = 0;
   r.sum_compat += amt;
@@ -263,26 +303,8 @@ __device__ void apply_event(const UpdateArgs& a, int j) {
   // PFADD + EXPIRE 24h
   bool new_dev = false, new_ip = false;
   uint8_t* regs = a.hll + (size_t)s * 512;
-  const uint64_t hv[2] = {ev.dev_hash, ev.ip_hash};
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const uint64_t h = hv[q];
-    if (!h) continue;
-    uint32_t& exp = q == 0 ? r.hll_dev_exp : r.hll_ip_exp;
-    uint8_t* rg = regs + q * 256;
-    if (now >= (int64_t)exp) {
-      uint4* w = reinterpret_cast<uint4*>(rg);
-      for (int k = 0; k < 16; ++k) w[k] = make_uint4(0, 0, 0, 0);
-    }
-    const int idx = (int)(h & 255u);
-    const uint64_t wv = h >> 8;
-    const int rank = wv ? (__clzll((long long)wv) - 8 + 1) : 57;
-    if (rank > rg[idx]) {
-      rg[idx] = (uint8_t)rank;
-      (q == 0 ? new_dev : new_ip) = true;
-    }
-    exp = (uint32_t)(now + cfg.hll_ttl);
-  }
+  if (ev.dev_hash) hll_add(regs, r.hll_dev_exp, ev.dev_hash, now, cfg.hll_ttl, new_dev);
+  if (ev.ip_hash) hll_add(regs + 256, r.hll_ip_exp, ev.ip_hash, now, cfg.hll_ttl, new_ip);
   // SET last_tx EX 7d; SETNX session_start + EXPIRE 30 min
   r.last_tx = (uint32_t)now;
   r.last_tx_exp = (uint32_t)(now + cfg.last_tx_ttl);
@@ -291,52 +313,78 @@ __device__ void apply_event(const UpdateArgs& a, int j) {
   // event ring for the bonus-abuse GRU (golden.features.encode_event)
   if (a.ev) {
     uint16_t* e = a.ev + ((size_t)s * a.ev_ring + r.ev_head) * a.ev_dim;
-    float v[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = 0.f;
-    v[0] = (float)(log1p((double)(amt > 0 ? amt : 0)) / 16.0);
     const int tt = ev.tx_type;
-    if (tt >= 0 && tt < 6) v[1 + tt] = 1.f;
     const int64_t prev = (int64_t)r.last_event_ts;
     const int64_t dt = (prev > 0 && now >= prev) ? now - prev : 0;
-    v[7] = (float)(log1p((double)dt) / 12.0);
     const double hour = (double)(now % 86400) / 3600.0;
-    v[8] = (float)sin(2.0 * M_PI * hour / 24.0);
-    v[9] = (float)cos(2.0 * M_PI * hour / 24.0);
-    v[10] = new_dev ? 1.f : 0.f;
-    v[11] = new_ip ? 1.f : 0.f;
-    v[12] = amt >= 100000 ? 1.f : 0.f;
-    v[13] = 1.f;
-    for (int k = 0; k < a.ev_dim && k < 16; ++k) e[k] = f32_to_bf16(v[k]);
-    r.ev_head = (r.ev_head + 1) % a.ev_ring;
+    uint32_t w[8];
+    w[0] = (uint32_t)f32_to_bf16((float)(log1p((double)(amt > 0 ? amt : 0)) / 16.0)) |
+           ((uint32_t)f32_to_bf16(tt == 0 ? 1.f : 0.f) << 16);
+    w[1] = (uint32_t)f32_to_bf16(tt == 1 ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(tt == 2 ? 1.f : 0.f) << 16);
+    w[2] = (uint32_t)f32_to_bf16(tt == 3 ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(tt == 4 ? 1.f : 0.f) << 16);
+    w[3] = (uint32_t)f32_to_bf16(tt == 5 ? 1.f : 0.f) |
+           ((uint32_t)f32_to_bf16((float)(log1p((double)dt) / 12.0)) << 16);
+    w[4] = (uint32_t)f32_to_bf16((float)sin(2.0 * M_PI * hour / 24.0)) |
+           ((uint32_t)f32_to_bf16((float)cos(2.0 * M_PI * hour / 24.0)) << 16);
+    w[5] = (uint32_t)f32_to_bf16(new_dev ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(new_ip ? 1.f : 0.f) << 16);
+    w[6] = (uint32_t)f32_to_bf16(amt >= 100000 ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(1.f) << 16);
+    w[7] = 0u;
+    uint4* e4 = reinterpret_cast<uint4*>(e);  // ev_dim == 16 (32 B, 16-B aligned)
+    e4[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    e4[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    r.ev_head = r.ev_head + 1 == a.ev_ring ? 0 : r.ev_head + 1;
     r.ev_count = r.ev_count + 1 > a.ev_ring ? a.ev_ring : r.ev_count + 1;
   }
   r.last_event_ts = (uint32_t)now;
-  a.rt[s] = r;
 }
 
-__global__ void feature_update_kernel(UpdateArgs a) {
+__global__ void update_single_kernel(UpdateArgs a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int n = a.n_ptr ? *a.n_ptr : a.n;
-  if (i >= n) return;
+  if (i >= n_events(a)) return;
   const int s = a.req[i].slot;
   if (s < 0) return;
-  uint32_t h = mix32((uint32_t)s) & (uint32_t)(a.dcap - 1);
-  int first = -1, count = 0;
-  for (int p = 0; p < a.dcap; ++p) {
-    if (a.dkeys[h] == s) { first = a.dfirst[h]; count = a.dcount[h]; break; }
-    h = (h + 1) & (uint32_t)(a.dcap - 1);
+  const int h = dedup_find(a, s);
+  if (h < 0 || a.dfirst[h] != i) return;
+  const int c = a.dcount[h];
+  if (c == 1) {
+    AcctRT r = a.rt[s];
+    apply_event(a, i, r);
+    a.rt[s] = r;
+  } else {
+    a.doff[h] = atomicAdd(a.dtotal, c);
   }
-  if (first != i) return;
-  if (count == 1) {
-    apply_event(a, i);
-    return;
+}
+
+__global__ void update_fill_kernel(UpdateArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_events(a)) return;
+  const int s = a.req[i].slot;
+  if (s < 0) return;
+  const int h = dedup_find(a, s);
+  if (h < 0 || a.dcount[h] < 2) return;
+  const int pos = atomicAdd(&a.dfill[h], 1);
+  a.dlist[a.doff[h] + pos] = i;
+}
+
+__global__ void update_multi_kernel(UpdateArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_events(a)) return;
+  const int s = a.req[i].slot;
+  if (s < 0) return;
+  const int h = dedup_find(a, s);
+  if (h < 0 || a.dfirst[h] != i) return;
+  const int c = a.dcount[h];
+  if (c < 2) return;
+  int* lst = a.dlist + a.doff[h];
+  for (int x = 1; x < c; ++x) {  // insertion sort: batch order (segments are short)
+    const int v = lst[x];
+    int y = x - 1;
+    while (y >= 0 && lst[y] > v) { lst[y + 1] = lst[y]; --y; }
+    lst[y + 1] = v;
   }
-  for (int j = i; j < n && count > 0; ++j) {
-    if (a.req[j].slot != s) continue;
-    apply_event(a, j);
-    --count;
-  }
+  AcctRT r = a.rt[s];
+  for (int x = 0; x < c; ++x) apply_event(a, lst[x], r);
+  a.rt[s] = r;
 }
 
 // ---------------------------------------------------------------------------------- launch
@@ -346,13 +394,13 @@ void launch_feature_assemble(const AssembleArgs& a, hipStream_t st) {
 }
 
 void launch_feature_update(const UpdateArgs& a, hipStream_t st) {
-  const int cap = a.dcap;
-  hipLaunchKernelGGL(dedup_reset_kernel, dim3((cap + 255) / 256), dim3(256), 0, st, a.dkeys, a.dfirst,
-                     a.dcount, cap);
   if (a.n_max <= 0) return;
+  hipLaunchKernelGGL(dedup_reset_kernel, dim3((a.dcap + 255) / 256), dim3(256), 0, st, a);
   const int g = (a.n_max + 255) / 256;
   hipLaunchKernelGGL(dedup_insert_kernel, dim3(g), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(feature_update_kernel, dim3(g), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(update_single_kernel, dim3(g), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(update_fill_kernel, dim3(g), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(update_multi_kernel, dim3(g), dim3(256), 0, st, a);
 }
 
 }  // namespace igp

@@ -191,6 +191,120 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs a) {
   }
 }
 
+// Fused dense + N==1 head: y[r] = act2( sum_n act1(x[r] . W1[n] + b1[n]) * w2[n] + b2 ).
+// 64 rows per block; the block's A tile (64 x K_pad bf16) is staged in LDS once, W1 fragments
+// stream from L2 (W1 is tiny and shared by every block); the 64 x N1 hidden tile lives only
+// in accumulators: bias + act1 + w2-weighting happen in registers, rows are reduced across
+// lanes (xor shuffles) and across the two column-waves through LDS.
+__global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int kp = a.k_pad;
+  const int lds_row = kp + G_PAD;
+  uint16_t* sA = reinterpret_cast<uint16_t*>(smem);
+  float* sred = reinterpret_cast<float*>(smem + (((size_t)64 * lds_row * 2 + 15) & ~size_t(15)));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int M = a.m_ptr ? min(*a.m_ptr, a.M) : a.M;
+  const int row0 = blockIdx.x * 64;
+  if (row0 >= M) return;
+  // stage A: 64 rows x kp (f32 or bf16 -> bf16), zero-padded past K and M
+  for (int ch = tid; ch < 64 * (kp / 8); ch += 256) {
+    const int r = ch / (kp / 8), kc = (ch % (kp / 8)) * 8;
+    const int row = row0 + r;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row < M) {
+      if (a.x_bf16) {
+        const uint16_t* src = reinterpret_cast<const uint16_t*>(a.X) + (size_t)row * a.ldx + kc;
+        uint16_t t[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] = (kc + j < a.K) ? src[j] : 0;
+        v = make_uint4(t[0] | (t[1] << 16), t[2] | (t[3] << 16), t[4] | (t[5] << 16), t[6] | (t[7] << 16));
+      } else {
+        const float* src = reinterpret_cast<const float*>(a.X) + (size_t)row * a.ldx + kc;
+        float f[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (kc + j < a.K) ? src[j] : 0.f;
+        v = make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
+                       pack_bf16x2(f[6], f[7]));
+      }
+    }
+    *reinterpret_cast<uint4*>(&sA[r * lds_row + kc]) = v;
+  }
+  __syncthreads();
+  float part[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) part[i][q] = 0.f;
+  for (int c0 = 0; c0 < a.N1; c0 += 64) {
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < kp; k0 += 32) {
+      const int kof = k0 + 8 * (lane >> 4);
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(&sA[(wm * 32 + i * 16 + (lane & 15)) * lds_row + kof]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = c0 + wn * 32 + j * 16 + (lane & 15);
+        fb[j] = *reinterpret_cast<const bf16x8*>(a.W1 + (size_t)n * kp + kof);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = c0 + wn * 32 + j * 16 + (lane & 15);
+      const bool ok = col < a.N1;
+      const float b1 = ok && a.b1 ? a.b1[col] : 0.f;
+      const float w2 = ok ? a.w2[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) part[i][q] += act_fn(acc[i][j][q] + b1, a.act1) * w2;
+    }
+  }
+  // reduce over the 16 lanes that share rows (lane & 15 differs)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v = part[i][q];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      part[i][q] = v;
+    }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sred[wn * 64 + wm * 32 + i * 16 + (lane >> 4) * 4 + q] = part[i][q];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int row = row0 + tid;
+    if (row < M) {
+      const float v = act_fn(sred[tid] + sred[64 + tid] + a.b2, a.act2);
+      a.Y[(size_t)row * a.ldy] = v;
+    }
+  }
+}
+
+void launch_mlp_head(const HeadArgs& a, hipStream_t st) {
+  if (a.M <= 0) return;
+  const size_t lds = (((size_t)64 * (a.k_pad + G_PAD) * 2 + 15) & ~size_t(15)) + 128 * sizeof(float);
+  hipLaunchKernelGGL(mlp_head_kernel, dim3((a.M + 63) / 64), dim3(256), lds, st, a);
+}
+
 void launch_gemm(const GemmArgs& a, hipStream_t st) {
   if (a.M <= 0) return;
   const bool big = a.M >= 4096 && a.N >= 128;

@@ -48,6 +48,10 @@ struct UpdateArgs {
   int32_t* dkeys;
   int32_t* dfirst;
   int32_t* dcount;
+  int32_t* dfill;
+  int32_t* doff;
+  int32_t* dlist;           // [n_max] segment lists of multi-event accounts
+  int32_t* dtotal;          // segment allocator
 };
 
 void launch_feature_assemble(const AssembleArgs& a, hipStream_t st);
@@ -89,6 +93,22 @@ struct GemmArgs {
 };
 void launch_gemm(const GemmArgs& a, hipStream_t st);
 void launch_gemv(const GemmArgs& a, hipStream_t st);  // N == 1 heads
+
+// dense(N1) + act1 + dense(N1 -> 1) + act2 fused; W1 bf16 [N1_pad(64)][k_pad(32)]
+struct HeadArgs {
+  const void* X;
+  const uint16_t* W1;
+  const float* b1;          // [N1] nullable
+  const float* w2;          // [N1] f32
+  float b2;
+  float* Y;                 // [M][ldy] f32 (column 0)
+  const int32_t* m_ptr;
+  int32_t M, K, N1, k_pad;
+  int32_t ldx, ldy;
+  int32_t x_bf16;
+  int32_t act1, act2;
+};
+void launch_mlp_head(const HeadArgs& a, hipStream_t st);
 
 // ---- K5 ensemble + action + metrics
 struct EnsembleArgs {

@@ -190,6 +190,20 @@ __global__ void tree_finish_kernel(TreeArgs a, const float* partial, int groups)
   }
 }
 
+// regressor / multi-output without a row-wise post transform: one thread per (row, target)
+__global__ void tree_finish_elem_kernel(TreeArgs a, const float* partial, int groups) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int K = a.k;
+  if (e >= a.n_rows * K) return;
+  const int k = e % K;
+  float v = 0.f;
+  for (int g = 0; g < groups; ++g) v += partial[(size_t)g * a.n_rows * K + e];
+  if (a.average) v /= (float)a.n_trees;
+  if (a.base) v += a.base[k];
+  if (a.post == 1) v = 1.f / (1.f + expf(-v));
+  a.out[e] = v;  // n_out == K
+}
+
 template <int K>
 static void launch_k(const TreeArgs& a, int groups, float* partial, hipStream_t st) {
   const int tpg = (a.n_trees + groups - 1) / groups;
@@ -204,8 +218,13 @@ static void launch_k(const TreeArgs& a, int groups, float* partial, hipStream_t 
   dim3 grid((a.n_rows + TR_ROWS - 1) / TR_ROWS, groups);
   hipLaunchKernelGGL((tree_kernel<K>), grid, dim3(256), lds, st, a, tpg, feat_w, in_lds,
                      groups > 1 ? partial : nullptr);
-  if (groups > 1)
-    hipLaunchKernelGGL(tree_finish_kernel, dim3((a.n_rows + 255) / 256), dim3(256), 0, st, a, partial, groups);
+  if (groups > 1) {
+    if (a.binary_class < 0 && a.post != 2 && a.n_out == K)
+      hipLaunchKernelGGL(tree_finish_elem_kernel, dim3((a.n_rows * K + 255) / 256), dim3(256), 0, st, a,
+                         partial, groups);
+    else
+      hipLaunchKernelGGL(tree_finish_kernel, dim3((a.n_rows + 255) / 256), dim3(256), 0, st, a, partial, groups);
+  }
 }
 
 // partial scratch: [groups][n_rows][K] f32, provided by the caller when groups > 1

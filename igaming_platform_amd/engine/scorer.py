@@ -102,8 +102,8 @@ class GpuScorer:
         steps = self.plan.steps
         for i, s in enumerate(steps):
             last = i == len(steps) - 1
-            feeds_dense = (not last) and steps[i + 1].kind == "dense"
-            dt = torch.bfloat16 if (s.kind == "dense" and feeds_dense and steps[i + 1].n > 1) else torch.float32
+            feeds_mma = (not last) and steps[i + 1].kind in ("dense", "head")
+            dt = torch.bfloat16 if (s.kind == "dense" and feeds_mma) else torch.float32
             self.step_out.append(torch.zeros((B, s.out_width), dtype=dt, device=dev))
             if s.kind == "tree":
                 need = 0
@@ -143,6 +143,8 @@ class GpuScorer:
                     K.tree_ensemble(s, cur, out, bucket, partial=self.tree_partial, groups=g)
                 elif s.kind == "dense":
                     K.dense(cur, s.w, s.b, out, bucket, s.n, s.k, act=s.act, m_ptr=self.n_ptr)
+                elif s.kind == "head":
+                    K.mlp_head(s, cur, out, bucket, m_ptr=self.n_ptr)
                 cur = out
         K.ensemble(self.hdr, self.cfg_dev, self.feat, self.X, self.ml, self.res, bucket, self.metrics)
         if self.update_features:

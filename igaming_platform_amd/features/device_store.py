@@ -75,6 +75,10 @@ class DeviceFeatureStore:
         self.dkeys = torch.empty(self.dcap, dtype=torch.int32, **z)
         self.dfirst = torch.empty(self.dcap, dtype=torch.int32, **z)
         self.dcount = torch.empty(self.dcap, dtype=torch.int32, **z)
+        self.dfill = torch.empty(self.dcap, dtype=torch.int32, **z)
+        self.doff = torch.empty(self.dcap, dtype=torch.int32, **z)
+        self.dlist = torch.empty(self.max_events, dtype=torch.int32, **z)
+        self.dtotal = torch.zeros(1, dtype=torch.int32, **z)
 
     # ------------------------------------------------------------------ sizing
     def bytes_per_account(self) -> int:

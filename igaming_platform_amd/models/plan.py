@@ -72,6 +72,27 @@ class DenseStep:
 
 
 @dataclass
+class HeadStep:
+    """dense(K -> N1, act1) + dense(N1 -> 1, act2) fused into one kernel (K3 mlp_head)."""
+    n1: int
+    k: int
+    act1: str
+    act2: str
+    w1_np: np.ndarray    # [N1, K]
+    b1_np: Optional[np.ndarray]
+    w2_np: np.ndarray    # [N1]
+    b2: float
+    w1: Any = None
+    b1: Any = None
+    w2: Any = None
+    kind: str = "head"
+
+    @property
+    def out_width(self) -> int:
+        return 1
+
+
+@dataclass
 class GRUStep:
     hidden: int
     in_dim: int
@@ -107,6 +128,8 @@ class Plan:
                 parts.append(f"tree(T={s.n_trees},D={s.depth},K={s.k},post={s.post})")
             elif s.kind == "dense":
                 parts.append(f"dense({s.k}->{s.n},{s.act})")
+            elif s.kind == "head":
+                parts.append(f"head({s.k}->{s.n1},{s.act1}->1,{s.act2})")
             else:
                 parts.append(f"gru(I={s.in_dim},H={s.hidden})")
         return " -> ".join(parts)
@@ -117,7 +140,7 @@ def _consumers(nodes, name):
 
 
 def compile_onnx(model, input_name: str = "input", output_name: str = "output",
-                 depth_limit: int = 12) -> Plan:
+                 depth_limit: int = 12, fuse_heads: bool = True) -> Plan:
     """``model``: _native.OnnxModel. Returns a host-side Plan (upload with :func:`to_device`)."""
     N = native()
     ex = N.Executor(model)
@@ -270,9 +293,31 @@ def compile_onnx(model, input_name: str = "input", output_name: str = "output",
         kinds = [s.kind for s in steps]
         fam = ("gbdt" if kinds == ["tree"] else "stacked" if kinds and kinds[0] == "tree"
                else "gru" if "gru" in kinds else "mlp")
-    return Plan(family=fam, in_width=in_width, steps=steps, out_width=width, ml_col=ml_col,
+    plan = Plan(family=fam, in_width=in_width, steps=steps, out_width=width, ml_col=ml_col,
                 metadata=dict(model.metadata), input_name=input_name, output_name=output_name,
                 seq_input=seq_input)
+    return fuse(plan) if fuse_heads else plan
+
+
+def fuse(plan: Plan) -> Plan:
+    """Fusion pass: dense(N>1) followed by dense(N=1) -> HeadStep (no hidden tensor in HBM)."""
+    out = []
+    i = 0
+    st = plan.steps
+    while i < len(st):
+        s = st[i]
+        if (s.kind == "dense" and s.n > 1 and i + 1 < len(st) and st[i + 1].kind == "dense"
+                and st[i + 1].n == 1 and s.n <= 4096 and s.k <= 1024):
+            t = st[i + 1]
+            out.append(HeadStep(n1=s.n, k=s.k, act1=s.act, act2=t.act, w1_np=s.w_np, b1_np=s.b_np,
+                                w2_np=np.ascontiguousarray(t.w_np[0], np.float32),
+                                b2=float(t.b_np[0]) if t.b_np is not None else 0.0))
+            i += 2
+            continue
+        out.append(s)
+        i += 1
+    plan.steps = out
+    return plan
 
 
 def _bf16_padded(w: np.ndarray, n_mult: int = 128, k_mult: int = 64):
@@ -295,6 +340,10 @@ def to_device(plan: Plan, device) -> Plan:
         elif s.kind == "dense":
             s.w = _bf16_padded(s.w_np).to(device)
             s.b = None if s.b_np is None else torch.from_numpy(np.ascontiguousarray(s.b_np)).to(device)
+        elif s.kind == "head":
+            s.w1 = _bf16_padded(s.w1_np).to(device)
+            s.b1 = None if s.b1_np is None else torch.from_numpy(np.ascontiguousarray(s.b1_np)).to(device)
+            s.w2 = torch.from_numpy(s.w2_np).to(device)
         elif s.kind == "gru":
             s.dev = gru_device_weights(s, device)
     return plan

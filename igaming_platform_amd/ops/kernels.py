@@ -89,7 +89,11 @@ def feature_update(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int,
         ev_dim=int(store.ev.shape[2]) if store.ev is not None else 0,
         dcap=int(store.dcap), dkeys=_need(store.dkeys, "dkeys", torch.int32),
         dfirst=_need(store.dfirst, "dfirst", torch.int32), dcount=_need(store.dcount, "dcount", torch.int32),
+        dfill=_need(store.dfill, "dfill", torch.int32), doff=_need(store.doff, "doff", torch.int32),
+        dlist=_need(store.dlist, "dlist", torch.int32, n_max), dtotal=_need(store.dtotal, "dtotal", torch.int32),
     )
+    if store.ev is not None and store.ev.shape[2] != 16:
+        raise ValueError("event ring dim must be 16")
     if n_ptr is None and n > n_max:
         raise ValueError("n > n_max")
     _mod().feature_update(d, _stream())
@@ -147,6 +151,24 @@ def dense(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], Y: tor
         _mod().gemv(d, _stream())
     else:
         _mod().gemm(d, _stream())
+
+
+def mlp_head(hs, X: torch.Tensor, Y: torch.Tensor, M: int, m_ptr: Optional[torch.Tensor] = None) -> None:
+    """``hs``: models.plan.HeadStep. Y[:M, 0] = act2(act1(X W1^T + b1) . w2 + b2)."""
+    dev = X.device
+    if X.dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError("mlp_head: X must be float32 or bfloat16")
+    if X.shape[1] < hs.k or X.shape[0] < M or Y.shape[0] < M or Y.dtype != torch.float32:
+        raise ValueError("mlp_head: operand shapes/dtypes")
+    if hs.w1.shape[0] < -(-hs.n1 // 64) * 64 or hs.w1.shape[1] % 32 or hs.w1.shape[1] < hs.k:
+        raise ValueError("mlp_head: W1 padding")
+    d = dict(X=_need(X, "X", device=dev), W1=_need(hs.w1, "W1", torch.bfloat16, device=dev),
+             b1=_opt(hs.b1, "b1", dtype=torch.float32, min_numel=hs.n1),
+             w2=_need(hs.w2, "w2", torch.float32, hs.n1, dev), b2=float(hs.b2),
+             Y=_need(Y, "Y", torch.float32, M, dev), m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32),
+             M=int(M), K=int(hs.k), N1=int(hs.n1), k_pad=int(hs.w1.shape[1]), ldx=int(X.shape[1]),
+             ldy=int(Y.shape[1]), x_bf16=int(X.dtype == torch.bfloat16), act1=ACT[hs.act1], act2=ACT[hs.act2])
+    _mod().mlp_head(d, _stream())
 
 
 # --------------------------------------------------------------------------- K5 / K10

@@ -266,3 +266,26 @@ def test_ltv_kernel_matches_golden():
         assert int(o[i, 2]) == p.survival_days and int(o[i, 4]) == p.segment, i
         assert np.float32(o[i, 3]) == np.float32(p.confidence), i
         assert GL.NBA_CODES[int(o[i, 5])] == p.next_best_action, i
+
+
+@pytest.mark.parametrize("M,K,N1,act1,act2,xbf", [
+    (8192, 32, 256, "relu", "sigmoid", False), (100, 512, 512, "relu", "none", True),
+    (1, 64, 64, "tanh", "sigmoid", False), (4097, 256, 130, "relu", "sigmoid", True),
+])
+def test_mlp_head_matches_torch_fp32(M, K, N1, act1, act2, xbf):
+    import torch
+    from igaming_platform_amd.models.plan import HeadStep, to_device, Plan
+    from igaming_platform_amd.ops import kernels as K_
+    g = torch.Generator().manual_seed(M + K + N1)
+    X = torch.randn(M, K, generator=g)
+    W1 = torch.randn(N1, K, generator=g) / K ** 0.5
+    b1 = torch.randn(N1, generator=g) * 0.1
+    w2 = torch.randn(N1, generator=g) / N1 ** 0.5
+    hs = HeadStep(n1=N1, k=K, act1=act1, act2=act2, w1_np=W1.numpy(), b1_np=b1.numpy(), w2_np=w2.numpy(), b2=0.3)
+    to_device(Plan("t", K, [hs], 1, 0, {}, "input", "output"), "cuda")
+    Y = torch.zeros(M, 1, device="cuda")
+    K_.mlp_head(hs, (X.to(torch.bfloat16) if xbf else X).cuda(), Y, M)
+    f = {"relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh, "none": lambda t: t}
+    h = f[act1](X.to(torch.bfloat16).float() @ W1.to(torch.bfloat16).float().T + b1)
+    ref = f[act2](h @ w2 + 0.3)
+    torch.testing.assert_close(Y[:, 0].cpu(), ref, rtol=3e-3, atol=3e-3)
