@@ -149,7 +149,7 @@ static_assert(sizeof(ReqRec) == 48, "ReqRec must be 48 bytes");
 // kernel of the captured graph): the number of live rows and the scoring clock.
 struct BatchHdr {
   int32_t n;
-  int32_t pad;
+  int32_t seq;    // batch sequence number (dedup-table ping-pong parity)
   int64_t now;
 };
 

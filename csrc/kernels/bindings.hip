@@ -28,6 +28,32 @@ int32_t geti(const py::dict& d, const char* k, int32_t def = 0) {
 
 hipStream_t stream_of(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+UpdateArgs update_args(const py::dict& d) {
+  UpdateArgs a{};
+  a.cfg = ptr<const ScoreCfg*>(d, "cfg");
+  a.hdr = ptr<const BatchHdr*>(d, "hdr");
+  a.n = geti(d, "n");
+  a.n_max = geti(d, "n_max");
+  a.req = ptr<const ReqRec*>(d, "req");
+  a.ring_ts = ptr<uint32_t*>(d, "ring_ts");
+  a.ring_amt = ptr<int64_t*>(d, "ring_amt");
+  a.hll = ptr<uint8_t*>(d, "hll");
+  a.rt = ptr<AcctRT*>(d, "rt");
+  a.ev = ptr<uint16_t*>(d, "ev");
+  a.ring_size = geti(d, "ring_size");
+  a.ev_ring = geti(d, "ev_ring");
+  a.ev_dim = geti(d, "ev_dim");
+  a.dbuf = ptr<int32_t*>(d, "dbuf");
+  a.dcap = geti(d, "dcap");
+  a.dmax = geti(d, "dmax");
+  a.region = geti(d, "region", 2);
+  if (!a.dbuf || !a.cfg || !a.req || !a.rt) throw std::runtime_error("update args: missing pointers");
+  if (a.n_max > a.dmax || a.dcap < 2 * a.dmax) throw std::runtime_error("update args: dedup scratch too small");
+  if (a.ev && a.ev_dim != 16) throw std::runtime_error("update args: event dim must be 16");
+  if (a.region < 0 && !a.hdr) throw std::runtime_error("update args: ping-pong region needs hdr");
+  return a;
+}
+
 void check(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
@@ -61,6 +87,9 @@ PYBIND11_MODULE(_hipk, m) {
     a.ip_flags = ptr<const uint32_t*>(d, "ip_flags");
     a.X = ptr<float*>(d, "X");
     a.feat = ptr<FeatRec*>(d, "feat");
+    a.dbuf = ptr<int32_t*>(d, "dbuf");
+    a.dcap = geti(d, "dcap");
+    a.dmax = geti(d, "dmax");
     a.x_stride = geti(d, "x_stride");
     a.ring_size = geti(d, "ring_size");
     a.n_rows = geti(d, "n_rows");
@@ -69,32 +98,9 @@ PYBIND11_MODULE(_hipk, m) {
   });
 
   m.def("feature_update", [](py::dict d, uintptr_t s) {
-    UpdateArgs a{};
-    a.cfg = ptr<const ScoreCfg*>(d, "cfg");
-    a.n_ptr = ptr<const int32_t*>(d, "n_ptr");
-    a.n = geti(d, "n");
-    a.n_max = geti(d, "n_max");
-    a.req = ptr<const ReqRec*>(d, "req");
-    a.ring_ts = ptr<uint32_t*>(d, "ring_ts");
-    a.ring_amt = ptr<int64_t*>(d, "ring_amt");
-    a.hll = ptr<uint8_t*>(d, "hll");
-    a.rt = ptr<AcctRT*>(d, "rt");
-    a.ev = ptr<uint16_t*>(d, "ev");
-    a.ring_size = geti(d, "ring_size");
-    a.ev_ring = geti(d, "ev_ring");
-    a.ev_dim = geti(d, "ev_dim");
-    a.dcap = geti(d, "dcap");
-    a.dkeys = ptr<int32_t*>(d, "dkeys");
-    a.dfirst = ptr<int32_t*>(d, "dfirst");
-    a.dcount = ptr<int32_t*>(d, "dcount");
-    a.dfill = ptr<int32_t*>(d, "dfill");
-    a.doff = ptr<int32_t*>(d, "doff");
-    a.dlist = ptr<int32_t*>(d, "dlist");
-    a.dtotal = ptr<int32_t*>(d, "dtotal");
-    if (!a.dkeys || !a.dfirst || !a.dcount || !a.dfill || !a.doff || !a.dlist || !a.dtotal)
-      throw std::runtime_error("feature_update: dedup scratch missing");
-    if (a.ev && a.ev_dim != 16) throw std::runtime_error("feature_update: event dim must be 16");
-    launch_feature_update(a, stream_of(s));
+    UpdateArgs a = update_args(d);
+    if (geti(d, "segments_only")) launch_update_segments(a, stream_of(s));
+    else launch_feature_update(a, stream_of(s));
     check("feature_update");
   });
 
@@ -116,6 +122,7 @@ PYBIND11_MODULE(_hipk, m) {
     a.average = geti(d, "average");
     a.binary_class = geti(d, "binary_class", -1);
     a.all_positive = geti(d, "all_positive", 1);
+    a.no_finish = geti(d, "no_finish", 0);
     const int groups = geti(d, "groups", 1);
     launch_tree_ensemble_grouped(a, groups, ptr<float*>(d, "partial"), stream_of(s));
     check("tree_ensemble");
@@ -166,6 +173,11 @@ PYBIND11_MODULE(_hipk, m) {
     a.x_bf16 = geti(d, "x_bf16");
     a.act1 = geti(d, "act1");
     a.act2 = geti(d, "act2");
+    a.partial = ptr<const float*>(d, "partial");
+    a.pbase = ptr<const float*>(d, "pbase");
+    a.groups = geti(d, "groups", 1);
+    a.p_average = geti(d, "p_average", 0);
+    a.p_ntrees = geti(d, "p_ntrees", 1);
     if (a.k_pad % 32 || a.k_pad < a.K) throw std::runtime_error("mlp_head: k_pad must be a multiple of 32 >= K");
     launch_mlp_head(a, stream_of(s));
     check("mlp_head");
@@ -182,6 +194,8 @@ PYBIND11_MODULE(_hipk, m) {
     a.out = ptr<ResultRec*>(d, "out");
     a.metrics = ptr<unsigned long long*>(d, "metrics");
     a.n_rows = geti(d, "n_rows");
+    a.do_update = geti(d, "do_update");
+    if (a.do_update) a.upd = update_args(d["upd"].cast<py::dict>());
     launch_ensemble(a, stream_of(s));
     check("ensemble");
   });

@@ -1,26 +1,37 @@
-// K1 feature_assemble (+K7 blacklist probe, +K8 HLL count, + rule pass) and
-// K6 feature_update (+HLL add, +event-ring encode) for gfx950.
+// K1 feature_assemble (+K7 blacklist probe, +K8 HLL count, + rule pass, + dedup insert) and
+// K6 feature_update (ordered per-account event application) for gfx950.
 //
 // Reference semantics (golden spec: igaming_platform_amd/golden/features.py):
 //   read path   services/risk/internal/features/redis_store.go:60-116, scoring/engine.go:326-417
 //   write path  redis_store.go:119-168
 //   rules       scoring/engine.go:420-483
 //   blacklist   redis_store.go:267-293
-#include "common.h"
-#include "launch.h"
+#include "update.h"
 
 namespace igp {
 
 // ---------------------------------------------------------------------------------- K1
-// One wave64 per request. The 256-entry tx ring is scanned coalesced (lane l reads entries
-// l, l+64, ...); HLL registers are 4 per lane; the account rows are broadcast loads.
+// One wave64 per request. Every independent load is issued before the first use: the
+// 256-entry ts ring as one uint4 per lane (1 KiB/wave, coalesced), HLL registers (4 per
+// lane), the account rows (broadcast), the ext row, and the blacklist/ip-intel probes;
+// the 1h amounts are then fetched only for in-window entries (predicated, issued together).
+// Lane 0 also registers the request in the batch dedup table (score-then-update) and each
+// wave clears a slice of the other parity's table for the next batch.
 __global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs a) {
   const int lane = threadIdx.x & 63;
   const int row = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (row >= a.n_rows) return;
   const ScoreCfg& cfg = *a.cfg;
   const int n_live = a.hdr->n;
+  const int seq = a.hdr->seq;
   const int64_t now = a.hdr->now;
+  if (a.dbuf) {  // clear this wave's slice of the next batch's dedup region
+    const DedupTab nt = dedup_region(a.dbuf, a.dcap, a.dmax, (seq + 1) & 1);
+    const int chunk = (a.dcap + a.n_rows - 1) / a.n_rows;
+    const int e0 = row * chunk;
+    dedup_clear_range(nt, e0, min(a.dcap, e0 + chunk), lane);
+    if (row == 0 && lane < 2) nt.ctr[lane] = 0;
+  }
   float* xr = a.X + (size_t)row * a.x_stride;
   const int ext_w = cfg.ext_width;
   if (row >= n_live) {  // padded row of a graph bucket: deterministic zeros
@@ -28,17 +39,40 @@ __global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs a) {
     if (lane < 32) reinterpret_cast<int32_t*>(a.feat + row)[lane] = (lane == 27) ? -1 : 0;
     return;
   }
-  const ReqRec& rq = a.req[row];
+  const ReqRec rq = a.req[row];
   const int s = rq.slot;
   const int64_t amount = rq.amount;
   const int tx_type = rq.tx_type;
 
+  // ---- issue the account loads
+  const int rs = a.ring_size;  // multiple of 64; 256 = one uint4 per lane
+  uint4 tsv = make_uint4(0, 0, 0, 0);
+  uint32_t tsx[12];           // entries beyond 256 (ring sizes up to 1024), rarely used
+  uint32_t wd = 0, wi = 0;
+  AcctRT rt{};
+  AcctBatch bt{};
+  if (s >= 0) {
+    const uint32_t* ts = a.ring_ts + (size_t)s * rs;
+    if (lane * 4 < rs) tsv = reinterpret_cast<const uint4*>(ts)[lane];
+#pragma unroll
+    for (int q = 0; q < 12; ++q) tsx[q] = (256 + q * 64 + lane < rs) ? ts[256 + q * 64 + lane] : 0u;
+    const uint32_t* h = reinterpret_cast<const uint32_t*>(a.hll + (size_t)s * 512);
+    wd = h[lane];
+    wi = h[64 + lane];
+    rt = a.rt[s];
+    bt = a.batch[s];
+  } else {
+#pragma unroll
+    for (int q = 0; q < 12; ++q) tsx[q] = 0u;
+  }
   // ---- K7: blacklist (lanes 0..2) and IP intelligence (lane 3) probes
   uint64_t key = 0;
   if (lane == 0) key = rq.dev_hash;
   else if (lane == 1) key = rq.fp_hash;
   else if (lane == 2) key = rq.ip_hash;
+  else if (lane == 3) key = rq.ip_hash;
   bool hit = false;
+  int ipf = 0;
   if (lane < 3 && key != 0 && a.bl_keys) {
     uint32_t i = (uint32_t)key & (uint32_t)cfg.bl_mask;
     for (int p = 0; p < cfg.bl_max_probe; ++p) {
@@ -51,20 +85,23 @@ __global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs a) {
       }
       i = (i + 1) & (uint32_t)cfg.bl_mask;
     }
-  }
-  int ipf = 0;
-  if (lane == 3 && a.ip_keys) {
-    const uint64_t ik = rq.ip_hash;
-    if (ik) {
-      uint32_t i = (uint32_t)ik & (uint32_t)cfg.ip_mask;
-      for (int p = 0; p < cfg.ip_max_probe; ++p) {
-        const uint64_t k = a.ip_keys[i];
-        if (k == 0) break;
-        if (k == ik) { ipf = (int)a.ip_flags[i]; break; }
-        i = (i + 1) & (uint32_t)cfg.ip_mask;
-      }
+  } else if (lane == 3 && key != 0 && a.ip_keys) {
+    uint32_t i = (uint32_t)key & (uint32_t)cfg.ip_mask;
+    for (int p = 0; p < cfg.ip_max_probe; ++p) {
+      const uint64_t k = a.ip_keys[i];
+      if (k == 0) break;
+      if (k == key) { ipf = (int)a.ip_flags[i]; break; }
+      i = (i + 1) & (uint32_t)cfg.ip_mask;
     }
   }
+  // ext row copy (independent of everything else)
+  if (ext_w > 0) {
+    const float* e = s >= 0 ? a.ext + (size_t)s * ext_w : nullptr;
+    for (int j = lane; j < ext_w; j += 64) xr[30 + j] = e ? e[j] : 0.f;
+  }
+  // dedup insert for score-then-update
+  if (a.dbuf && lane == 0 && s >= 0) dedup_insert(dedup_region(a.dbuf, a.dcap, a.dmax, seq & 1), s, row);
+
   const bool blacklisted = __ballot(hit) != 0ull;
   ipf = __shfl(ipf, 3, 64);
 
@@ -72,27 +109,37 @@ __global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs a) {
   int c1 = 0, c5 = 0, c60 = 0;
   long long s60 = 0;
   int hll_dev = 0, hll_ip = 0;
-  AcctRT rt{};
-  AcctBatch bt{};
   if (s >= 0) {
-    const uint32_t* ts = a.ring_ts + (size_t)s * a.ring_size;
-    const int64_t* am = a.ring_amt + (size_t)s * a.ring_size;
-    for (int j = lane; j < a.ring_size; j += 64) {
-      const int64_t t = (int64_t)ts[j];
-      if (t == 0) continue;
-      c1 += t >= now - 60;
-      c5 += t >= now - 300;
-      if (t >= now - 3600) { ++c60; s60 += am[j]; }
+    const int64_t* am = a.ring_amt + (size_t)s * rs;
+    const uint32_t tv[4] = {tsv.x, tsv.y, tsv.z, tsv.w};
+    bool in1h[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t t = (int64_t)tv[q];
+      const bool v = t != 0;
+      c1 += v && t >= now - 60;
+      c5 += v && t >= now - 300;
+      in1h[q] = v && t >= now - 3600;
+      c60 += in1h[q];
     }
+    long long amv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) amv[q] = in1h[q] ? am[lane * 4 + q] : 0;
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {
+      const int64_t t = (int64_t)tsx[q];
+      if (t != 0) {
+        c1 += t >= now - 60;
+        c5 += t >= now - 300;
+        if (t >= now - 3600) { ++c60; s60 += am[256 + q * 64 + lane]; }
+      }
+    }
+    s60 += amv[0] + amv[1] + amv[2] + amv[3];
     c1 = wave_sum(c1);
     c5 = wave_sum(c5);
     c60 = wave_sum(c60);
     s60 = wave_sum(s60);
-    rt = a.rt[s];
-    bt = a.batch[s];
     // ---- K8: HyperLogLog counts (p = 8; 4 registers per lane)
-    const uint32_t* h = reinterpret_cast<const uint32_t*>(a.hll + (size_t)s * 512);
-    const uint32_t wd = h[lane], wi = h[64 + lane];
     double zd = 0, zi = 0;
     int vd = 0, vi = 0;
 #pragma unroll
@@ -170,221 +217,213 @@ __global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs a) {
   f.reserved0 = (int32_t)reasons;
   f.reserved1 = score > 100 ? 100 : score;
 
-  // ---- writes: lane 0 the record and the 30 normalised model inputs; all lanes the ext row
-  if (lane == 0) {
-    a.feat[row] = f;
-    const int id = cfg.log_identity;
-    xr[0] = minmax_scale((float)f.tx_count_1m, 0.f, 20.f);
-    xr[1] = minmax_scale((float)f.tx_count_5m, 0.f, 50.f);
-    xr[2] = minmax_scale((float)f.tx_count_1h, 0.f, 200.f);
-    xr[3] = log_transform((float)f.tx_sum_1h, id);
-    xr[4] = f.tx_avg_1h;
-    xr[5] = minmax_scale((float)f.unique_devices_24h, 0.f, 10.f);
-    xr[6] = minmax_scale((float)f.unique_ips_24h, 0.f, 20.f);
-    xr[7] = (float)f.ip_country_changes_7d;
-    xr[8] = (float)f.device_age_days;
-    xr[9] = minmax_scale((float)f.account_age_days, 0.f, 365.f);
-    xr[10] = log_transform((float)f.total_deposits, id);
-    xr[11] = log_transform((float)f.total_withdrawals, id);
-    xr[12] = (float)f.net_deposit;
-    xr[13] = (float)f.deposit_count;
-    xr[14] = (float)f.withdraw_count;
-    xr[15] = minmax_scale((float)f.time_since_last_tx, 0.f, 86400.f);
-    xr[16] = (float)f.session_duration;
-    xr[17] = f.avg_bet_size;
-    xr[18] = f.win_rate;
-    xr[19] = (flags & FR_VPN) ? 1.f : 0.f;
-    xr[20] = (flags & FR_PROXY) ? 1.f : 0.f;
-    xr[21] = (flags & FR_TOR) ? 1.f : 0.f;
-    xr[22] = (flags & FR_DISPOSABLE) ? 1.f : 0.f;
-    xr[23] = (float)f.bonus_claim_count;
-    xr[24] = f.bonus_wager_rate;
-    xr[25] = (flags & FR_BONUS_ONLY) ? 1.f : 0.f;
-    xr[26] = log_transform((float)amount, id);
-    xr[27] = tx_type == TX_DEPOSIT ? 1.f : 0.f;
-    xr[28] = tx_type == TX_WITHDRAW ? 1.f : 0.f;
-    xr[29] = tx_type == TX_BET ? 1.f : 0.f;
+  // ---- writes: the 30 normalised inputs spread over lanes 0..29, the record by lane 0
+  const int id = cfg.log_identity;
+  float xv = 0.f;
+  switch (lane) {
+    case 0: xv = minmax_scale((float)f.tx_count_1m, 0.f, 20.f); break;
+    case 1: xv = minmax_scale((float)f.tx_count_5m, 0.f, 50.f); break;
+    case 2: xv = minmax_scale((float)f.tx_count_1h, 0.f, 200.f); break;
+    case 3: xv = log_transform((float)f.tx_sum_1h, id); break;
+    case 4: xv = f.tx_avg_1h; break;
+    case 5: xv = minmax_scale((float)f.unique_devices_24h, 0.f, 10.f); break;
+    case 6: xv = minmax_scale((float)f.unique_ips_24h, 0.f, 20.f); break;
+    case 7: xv = (float)f.ip_country_changes_7d; break;
+    case 8: xv = (float)f.device_age_days; break;
+    case 9: xv = minmax_scale((float)f.account_age_days, 0.f, 365.f); break;
+    case 10: xv = log_transform((float)f.total_deposits, id); break;
+    case 11: xv = log_transform((float)f.total_withdrawals, id); break;
+    case 12: xv = (float)f.net_deposit; break;
+    case 13: xv = (float)f.deposit_count; break;
+    case 14: xv = (float)f.withdraw_count; break;
+    case 15: xv = minmax_scale((float)f.time_since_last_tx, 0.f, 86400.f); break;
+    case 16: xv = (float)f.session_duration; break;
+    case 17: xv = f.avg_bet_size; break;
+    case 18: xv = f.win_rate; break;
+    case 19: xv = (flags & FR_VPN) ? 1.f : 0.f; break;
+    case 20: xv = (flags & FR_PROXY) ? 1.f : 0.f; break;
+    case 21: xv = (flags & FR_TOR) ? 1.f : 0.f; break;
+    case 22: xv = (flags & FR_DISPOSABLE) ? 1.f : 0.f; break;
+    case 23: xv = (float)f.bonus_claim_count; break;
+    case 24: xv = f.bonus_wager_rate; break;
+    case 25: xv = (flags & FR_BONUS_ONLY) ? 1.f : 0.f; break;
+    case 26: xv = log_transform((float)amount, id); break;
+    case 27: xv = tx_type == TX_DEPOSIT ? 1.f : 0.f; break;
+    case 28: xv = tx_type == TX_WITHDRAW ? 1.f : 0.f; break;
+    case 29: xv = tx_type == TX_BET ? 1.f : 0.f; break;
+    default: break;
   }
-  if (ext_w > 0) {
-    const float* e = s >= 0 ? a.ext + (size_t)s * ext_w : nullptr;
-    for (int j = lane; j < ext_w; j += 64) xr[30 + j] = e ? e[j] : 0.f;
-  }
+  if (lane < 30) xr[lane] = xv;
+  if (lane == 0) a.feat[row] = f;
 }
 
 // ---------------------------------------------------------------------------------- K6
-// Ordered per-account event application without serial scans:
-//   reset   scratch table (keys, first, count, fill, off) + segment allocator
-//   insert  each event registers its slot: first index (atomicMin) and count (atomicAdd)
-//   single  accounts with one event in the batch apply it directly (the common case); the
-//           first event of a multi-event account reserves a segment of `count` list entries
-//   fill    every event of a multi-event account writes its index into that segment
-//   multi   the owner sorts its segment (batch order) and applies the events sequentially
-//           with the account's AcctRT held in registers (one load, one store).
-// The state of an account is only ever written by its single owner thread, so no atomics
-// touch the feature store itself.
+__device__ __forceinline__ int upd_n(const UpdateArgs& a) {
+  const int n = a.hdr ? a.hdr->n : a.n;
+  return n < a.n_max ? n : a.n_max;
+}
+
+__device__ __forceinline__ DedupTab upd_region(const UpdateArgs& a) {
+  const int r = a.region >= 0 ? a.region : (a.hdr->seq & 1);
+  return dedup_region(a.dbuf, a.dcap, a.dmax, r);
+}
 
 __global__ void dedup_reset_kernel(UpdateArgs a) {
+  const DedupTab t = upd_region(a);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < a.dcap) { a.dkeys[i] = -1; a.dfirst[i] = 0x7fffffff; a.dcount[i] = 0; a.dfill[i] = 0; }
-  if (i == 0) *a.dtotal = 0;
-}
-
-__device__ __forceinline__ uint32_t mix32(uint32_t x) {
-  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
-  return x;
-}
-
-__device__ __forceinline__ int n_events(const UpdateArgs& a) {
-  const int n = a.n_ptr ? *a.n_ptr : a.n;
-  return n < a.n_max ? n : a.n_max;
+  if (i < t.cap) { t.keys[i] = -1; t.first[i] = 0x7fffffff; t.count[i] = 0; t.fill[i] = 0; }
+  if (i < 2) t.ctr[i] = 0;
 }
 
 __global__ void dedup_insert_kernel(UpdateArgs a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_events(a)) return;
+  if (i >= upd_n(a)) return;
   const int s = a.req[i].slot;
-  if (s < 0) return;
-  uint32_t h = mix32((uint32_t)s) & (uint32_t)(a.dcap - 1);
-  for (int p = 0; p < a.dcap; ++p) {
-    const int prev = atomicCAS(&a.dkeys[h], -1, s);
-    if (prev == -1 || prev == s) {
-      atomicMin(&a.dfirst[h], i);
-      atomicAdd(&a.dcount[h], 1);
-      return;
-    }
-    h = (h + 1) & (uint32_t)(a.dcap - 1);
-  }
-}
-
-__device__ __forceinline__ int dedup_find(const UpdateArgs& a, int s) {
-  uint32_t h = mix32((uint32_t)s) & (uint32_t)(a.dcap - 1);
-  for (int p = 0; p < a.dcap; ++p) {
-    const int k = a.dkeys[h];
-    if (k == s) return (int)h;
-    if (k == -1) return -1;
-    h = (h + 1) & (uint32_t)(a.dcap - 1);
-  }
-  return -1;
-}
-
-__device__ __forceinline__ void hll_add(uint8_t* rg, uint32_t& exp, uint64_t h, int64_t now, int ttl,
-                                        bool& changed) {
-  if (now >= (int64_t)exp) {
-    uint4* w = reinterpret_cast<uint4*>(rg);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) w[k] = make_uint4(0, 0, 0, 0);
-  }
-  const int idx = (int)(h & 255u);
-  const uint64_t wv = h >> 8;
-  const int rank = wv ? (__clzll((long long)wv) - 8 + 1) : 57;
-  if (rank > rg[idx]) {
-    rg[idx] = (uint8_t)rank;
-    changed = true;
-  }
-  exp = (uint32_t)(now + ttl);
-}
-
-// apply one event to an account whose AcctRT `r` the caller holds in registers
-__device__ void apply_event(const UpdateArgs& a, int j, AcctRT& r) {
-  const ReqRec ev = a.req[j];
-  const int s = ev.slot;
-  const int64_t now = ev.ts;
-  const ScoreCfg& cfg = *a.cfg;
-  const int64_t amt = ev.amount;
-  // tx ring (ZADD + trim; here: overwrite the oldest entry)
-  const int hd = r.ring_head;
-  a.ring_ts[(size_t)s * a.ring_size + hd] = (uint32_t)now;
-  a.ring_amt[(size_t)s * a.ring_size + hd] = amt;
-  r.ring_head = hd + 1 == a.ring_size ? 0 : hd + 1;
-  // INCRBY + EXPIRE 1h (compat sum)
-  if (now >= (int64_t)r.sum_exp) r.sum_compat = 0;
-  r.sum_compat += amt;
-  r.sum_exp = (uint32_t)(now + cfg.sum_ttl);
-  // PFADD + EXPIRE 24h
-  bool new_dev = false, new_ip = false;
-  uint8_t* regs = a.hll + (size_t)s * 512;
-  if (ev.dev_hash) hll_add(regs, r.hll_dev_exp, ev.dev_hash, now, cfg.hll_ttl, new_dev);
-  if (ev.ip_hash) hll_add(regs + 256, r.hll_ip_exp, ev.ip_hash, now, cfg.hll_ttl, new_ip);
-  // SET last_tx EX 7d; SETNX session_start + EXPIRE 30 min
-  r.last_tx = (uint32_t)now;
-  r.last_tx_exp = (uint32_t)(now + cfg.last_tx_ttl);
-  if (now >= (int64_t)r.session_exp || r.session_start == 0) r.session_start = (uint32_t)now;
-  r.session_exp = (uint32_t)(now + cfg.session_ttl);
-  // event ring for the bonus-abuse GRU (golden.features.encode_event)
-  if (a.ev) {
-    uint16_t* e = a.ev + ((size_t)s * a.ev_ring + r.ev_head) * a.ev_dim;
-    const int tt = ev.tx_type;
-    const int64_t prev = (int64_t)r.last_event_ts;
-    const int64_t dt = (prev > 0 && now >= prev) ? now - prev : 0;
-    const double hour = (double)(now % 86400) / 3600.0;
-    uint32_t w[8];
-    w[0] = (uint32_t)f32_to_bf16((float)(log1p((double)(amt > 0 ? amt : 0)) / 16.0)) |
-           ((uint32_t)f32_to_bf16(tt == 0 ? 1.f : 0.f) << 16);
-    w[1] = (uint32_t)f32_to_bf16(tt == 1 ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(tt == 2 ? 1.f : 0.f) << 16);
-    w[2] = (uint32_t)f32_to_bf16(tt == 3 ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(tt == 4 ? 1.f : 0.f) << 16);
-    w[3] = (uint32_t)f32_to_bf16(tt == 5 ? 1.f : 0.f) |
-           ((uint32_t)f32_to_bf16((float)(log1p((double)dt) / 12.0)) << 16);
-    w[4] = (uint32_t)f32_to_bf16((float)sin(2.0 * M_PI * hour / 24.0)) |
-           ((uint32_t)f32_to_bf16((float)cos(2.0 * M_PI * hour / 24.0)) << 16);
-    w[5] = (uint32_t)f32_to_bf16(new_dev ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(new_ip ? 1.f : 0.f) << 16);
-    w[6] = (uint32_t)f32_to_bf16(amt >= 100000 ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(1.f) << 16);
-    w[7] = 0u;
-    uint4* e4 = reinterpret_cast<uint4*>(e);  // ev_dim == 16 (32 B, 16-B aligned)
-    e4[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    e4[1] = make_uint4(w[4], w[5], w[6], w[7]);
-    r.ev_head = r.ev_head + 1 == a.ev_ring ? 0 : r.ev_head + 1;
-    r.ev_count = r.ev_count + 1 > a.ev_ring ? a.ev_ring : r.ev_count + 1;
-  }
-  r.last_event_ts = (uint32_t)now;
+  if (s >= 0) dedup_insert(upd_region(a), s, i);
 }
 
 __global__ void update_single_kernel(UpdateArgs a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_events(a)) return;
+  if (i >= upd_n(a)) return;
   const int s = a.req[i].slot;
-  if (s < 0) return;
-  const int h = dedup_find(a, s);
-  if (h < 0 || a.dfirst[h] != i) return;
-  const int c = a.dcount[h];
-  if (c == 1) {
-    AcctRT r = a.rt[s];
-    apply_event(a, i, r);
-    a.rt[s] = r;
-  } else {
-    a.doff[h] = atomicAdd(a.dtotal, c);
-  }
+  if (s >= 0) update_first_event(a, upd_region(a), i, s);
 }
 
 __global__ void update_fill_kernel(UpdateArgs a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_events(a)) return;
+  if (i >= upd_n(a)) return;
   const int s = a.req[i].slot;
   if (s < 0) return;
-  const int h = dedup_find(a, s);
-  if (h < 0 || a.dcount[h] < 2) return;
-  const int pos = atomicAdd(&a.dfill[h], 1);
-  a.dlist[a.doff[h] + pos] = i;
+  const DedupTab t = upd_region(a);
+  const int h = dedup_find(t, s);
+  if (h < 0 || t.count[h] < 2) return;
+  t.list[t.off[h] + atomicAdd(&t.fill[h], 1)] = i;
 }
 
-__global__ void update_multi_kernel(UpdateArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_events(a)) return;
-  const int s = a.req[i].slot;
-  if (s < 0) return;
-  const int h = dedup_find(a, s);
-  if (h < 0 || a.dfirst[h] != i) return;
-  const int c = a.dcount[h];
-  if (c < 2) return;
-  int* lst = a.dlist + a.doff[h];
-  for (int x = 1; x < c; ++x) {  // insertion sort: batch order (segments are short)
+// sequential fallback: insertion-sort the segment in memory, apply with AcctRT in registers
+__device__ void apply_segment_serial(const UpdateArgs& a, const DedupTab& t, int h) {
+  const int c = t.count[h];
+  int* lst = t.list + t.off[h];
+  for (int x = 1; x < c; ++x) {
     const int v = lst[x];
     int y = x - 1;
     while (y >= 0 && lst[y] > v) { lst[y + 1] = lst[y]; --y; }
     lst[y + 1] = v;
   }
+  const int s = a.req[lst[0]].slot;
   AcctRT r = a.rt[s];
   for (int x = 0; x < c; ++x) apply_event(a, lst[x], r);
   a.rt[s] = r;
+}
+
+// PFADD of up to 64 same-account events at once: the per-register winner writes the max,
+// each event learns whether it raised its register (the GRU's new-device/new-ip feature)
+// exactly as the sequential order would have.
+__device__ __forceinline__ uint32_t hll_segment(const UpdateArgs& a, uint8_t* rg, uint32_t exp, uint64_t hq,
+                                                int64_t ts, int lane, bool& changed) {
+  const bool has = hq != 0;
+  const uint64_t any = __ballot(has);
+  if (!any) return exp;
+  const int fl = __ffsll((long long)any) - 1;
+  const int ll = 63 - __clzll((long long)any);
+  const int64_t tfirst = __shfl(ts, fl, 64), tlast = __shfl(ts, ll, 64);
+  const bool reset = tfirst >= (int64_t)exp;
+  const int idx = has ? (int)(hq & 255u) : -1;
+  const int rank = has ? hll_rank(hq) : 0;
+  const int before = (has && !reset) ? (int)rg[idx] : 0;
+  if (reset) {
+    reinterpret_cast<uint32_t*>(rg)[lane] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  }
+  int pm = before;
+  bool win = has;
+  for (int y = 0; y < 64; ++y) {
+    const int iy = __shfl(idx, y, 64), ry = __shfl(rank, y, 64);
+    if (has && iy == idx && y != lane) {
+      if (y < lane) pm = max(pm, ry);
+      if (ry > rank || (ry == rank && y < lane)) win = false;
+    }
+  }
+  changed = has && rank > pm;
+  if (win && rank > before) rg[idx] = (uint8_t)rank;
+  return (uint32_t)(tlast + a.cfg->hll_ttl);
+}
+
+// one wave per multi-event account: events sorted in registers, applied in parallel. Valid
+// when the segment spans less than the shortest TTL (then no key can expire mid-segment);
+// otherwise (or above 64 events) lane 0 applies the segment sequentially.
+__global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const DedupTab t = upd_region(a);
+  if (w >= t.ctr[1]) return;
+  const int h = t.mlist[w];
+  const int c = t.count[h];
+  const int* lst = t.list + t.off[h];
+  const ScoreCfg& cfg = *a.cfg;
+  const int min_ttl = min(min(cfg.session_ttl, cfg.sum_ttl), min(cfg.hll_ttl, cfg.last_tx_ttl));
+  int span_ok = 0;
+  int key = 0x7fffffc0 | lane;
+  int64_t ts = 0;
+  if (c <= 64) {
+    if (lane < c) key = lst[lane];
+    if (lane < c) ts = a.req[key].ts;
+    const int64_t big = 0x3fffffffffffffffLL;
+    const int64_t tmx = wave_max(lane < c ? ts : -big);
+    const int64_t tmn = -wave_max(lane < c ? -ts : -big);
+    span_ok = (tmx - tmn) < (int64_t)min_ttl;
+  }
+  if (!span_ok) {
+    if (lane == 0) apply_segment_serial(a, t, h);
+    return;
+  }
+  // sort (distinct keys): rank = #smaller, then push each key to lane `rank`
+  int rank = 0;
+  for (int y = 0; y < 64; ++y) rank += __shfl(key, y, 64) < key;
+  const int j = __builtin_amdgcn_ds_permute(rank * 4, key);
+  const bool act = lane < c;
+  ReqRec ev{};
+  if (act) ev = a.req[j];
+  ts = act ? ev.ts : 0;
+  const int s = __shfl(act ? ev.slot : 0, 0, 64);
+  AcctRT r = a.rt[s];
+  const int64_t ts0 = __shfl(ts, 0, 64);
+  const int64_t tsl = __shfl(ts, c - 1, 64);
+  const int64_t amt = act ? ev.amount : 0;
+  // tx ring: consecutive positions from the head
+  if (act) {
+    const int pos = (r.ring_head + lane) % a.ring_size;
+    a.ring_ts[(size_t)s * a.ring_size + pos] = (uint32_t)ts;
+    a.ring_amt[(size_t)s * a.ring_size + pos] = amt;
+  }
+  // compat sum: only the first event can find the key expired (span < TTL)
+  const long long tot = wave_sum((long long)amt);
+  r.sum_compat = (ts0 >= (int64_t)r.sum_exp ? 0 : r.sum_compat) + tot;
+  r.sum_exp = (uint32_t)(tsl + cfg.sum_ttl);
+  // HyperLogLogs
+  uint8_t* regs = a.hll + (size_t)s * 512;
+  bool new_dev = false, new_ip = false;
+  r.hll_dev_exp = hll_segment(a, regs, r.hll_dev_exp, act ? ev.dev_hash : 0, ts, lane, new_dev);
+  r.hll_ip_exp = hll_segment(a, regs + 256, r.hll_ip_exp, act ? ev.ip_hash : 0, ts, lane, new_ip);
+  // last tx / session
+  if (ts0 >= (int64_t)r.session_exp || r.session_start == 0) r.session_start = (uint32_t)ts0;
+  r.session_exp = (uint32_t)(tsl + cfg.session_ttl);
+  r.last_tx = (uint32_t)tsl;
+  r.last_tx_exp = (uint32_t)(tsl + cfg.last_tx_ttl);
+  // event ring: event x's predecessor is event x-1 (event 0's is the stored last event)
+  const int64_t up = __shfl(ts, lane > 0 ? lane - 1 : 0, 64);
+  const int64_t prev = lane == 0 ? (int64_t)r.last_event_ts : up;
+  if (a.ev && act) {
+    const int pos = (r.ev_head + lane) % a.ev_ring;
+    write_event_row(a.ev + ((size_t)s * a.ev_ring + pos) * a.ev_dim, amt, ev.tx_type, ts, prev, new_dev, new_ip);
+  }
+  if (a.ev) {
+    r.ev_head = (r.ev_head + c) % a.ev_ring;
+    r.ev_count = r.ev_count + c > a.ev_ring ? a.ev_ring : r.ev_count + c;
+  }
+  r.ring_head = (r.ring_head + c) % a.ring_size;
+  r.last_event_ts = (uint32_t)tsl;
+  if (lane == 0) a.rt[s] = r;
 }
 
 // ---------------------------------------------------------------------------------- launch
@@ -393,14 +432,21 @@ void launch_feature_assemble(const AssembleArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(feature_assemble_kernel, dim3((a.n_rows + 3) / 4), dim3(256), 0, st, a);
 }
 
+void launch_update_segments(const UpdateArgs& a, hipStream_t st) {
+  if (a.n_max <= 0) return;
+  const int g = (a.n_max + 255) / 256;
+  hipLaunchKernelGGL(update_fill_kernel, dim3(g), dim3(256), 0, st, a);
+  // at most n/2 accounts can have >= 2 events: one wave each
+  hipLaunchKernelGGL(update_multi_kernel, dim3((a.n_max / 2 + 3) / 4 + 1), dim3(256), 0, st, a);
+}
+
 void launch_feature_update(const UpdateArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
   hipLaunchKernelGGL(dedup_reset_kernel, dim3((a.dcap + 255) / 256), dim3(256), 0, st, a);
   const int g = (a.n_max + 255) / 256;
   hipLaunchKernelGGL(dedup_insert_kernel, dim3(g), dim3(256), 0, st, a);
   hipLaunchKernelGGL(update_single_kernel, dim3(g), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(update_fill_kernel, dim3(g), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(update_multi_kernel, dim3(g), dim3(256), 0, st, a);
+  launch_update_segments(a, st);
 }
 
 }  // namespace igp

@@ -212,7 +212,23 @@ __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a) {
     const int r = ch / (kp / 8), kc = (ch % (kp / 8)) * 8;
     const int row = row0 + r;
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (row < M) {
+    if (row < M && a.partial) {
+      // reduce the tree ensemble's group partials: sum_g P[g][row][k] (+ base, / T)
+      float f[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = kc + j;
+        float s = 0.f;
+        if (k < a.K) {
+          for (int g = 0; g < a.groups; ++g) s += a.partial[((size_t)g * a.M + row) * a.K + k];
+          if (a.p_average) s /= (float)a.p_ntrees;
+          if (a.pbase) s += a.pbase[k];
+        }
+        f[j] = s;
+      }
+      v = make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
+                     pack_bf16x2(f[6], f[7]));
+    } else if (row < M) {
       if (a.x_bf16) {
         const uint16_t* src = reinterpret_cast<const uint16_t*>(a.X) + (size_t)row * a.ldx + kc;
         uint16_t t[8];

@@ -9,10 +9,12 @@
 
 namespace igp {
 
+// Dedup scratch: 3 regions (0/1 = scorer ping-pong by BatchHdr::seq parity, 2 = standalone
+// event ingestion), each = keys/first/count/fill/off [cap] + list/mlist [dmax] + 2 counters.
 struct AssembleArgs {
   const BatchHdr* hdr;
   const ScoreCfg* cfg;
-  const ReqRec* req;         // [n_rows]
+  const ReqRec* req;        // [n_rows]
   const uint32_t* ring_ts;
   const int64_t* ring_amt;
   const uint8_t* hll;       // [C][2][256]
@@ -25,6 +27,9 @@ struct AssembleArgs {
   const uint32_t* ip_flags;
   float* X;                 // [n_rows][x_stride]
   FeatRec* feat;            // [n_rows]
+  int32_t* dbuf;            // dedup regions (nullable: no score-then-update)
+  int32_t dcap;
+  int32_t dmax;
   int32_t x_stride;
   int32_t ring_size;
   int32_t n_rows;           // rows covered by the launch (graph bucket)
@@ -32,7 +37,7 @@ struct AssembleArgs {
 
 struct UpdateArgs {
   const ScoreCfg* cfg;
-  const int32_t* n_ptr;     // live event count in device memory (nullable -> n)
+  const BatchHdr* hdr;      // scorer path: live count + seq parity (nullable -> n, region)
   int32_t n;
   int32_t n_max;            // grid coverage
   const ReqRec* req;        // events (ReqRec.ts = event time)
@@ -40,22 +45,21 @@ struct UpdateArgs {
   int64_t* ring_amt;
   uint8_t* hll;
   AcctRT* rt;
-  uint16_t* ev;             // event ring bf16 [C][ev_ring][ev_dim] (nullable)
+  uint16_t* ev;             // event ring bf16 [C][ev_ring][16] (nullable)
   int32_t ring_size;
   int32_t ev_ring;
   int32_t ev_dim;
-  int32_t dcap;             // dedup scratch capacity (power of two >= 2 * n_max)
-  int32_t* dkeys;
-  int32_t* dfirst;
-  int32_t* dcount;
-  int32_t* dfill;
-  int32_t* doff;
-  int32_t* dlist;           // [n_max] segment lists of multi-event accounts
-  int32_t* dtotal;          // segment allocator
+  int32_t* dbuf;
+  int32_t dcap;             // power of two >= 2 * dmax
+  int32_t dmax;
+  int32_t region;           // -1: hdr->seq & 1; else fixed region (2 = standalone)
 };
 
 void launch_feature_assemble(const AssembleArgs& a, hipStream_t st);
+// standalone event ingestion (event bus / history replay): reset + insert + single + segments
 void launch_feature_update(const UpdateArgs& a, hipStream_t st);
+// scorer path tail: segment fill + per-account wave apply (insert ran in K1, singles in K5)
+void launch_update_segments(const UpdateArgs& a, hipStream_t st);
 
 // ---- K2 tree ensemble (complete layout)
 struct TreeArgs {
@@ -75,6 +79,7 @@ struct TreeArgs {
   int32_t average;          // 1 = AVERAGE aggregate
   int32_t binary_class;     // -1 unless classifier binary case
   int32_t all_positive;
+  int32_t no_finish;        // grouped launch: leave partials for the consumer (mlp_head)
 };
 void launch_tree_ensemble(const TreeArgs& a, hipStream_t st);
 void launch_tree_ensemble_grouped(const TreeArgs& a, int groups, float* partial, hipStream_t st);
@@ -107,6 +112,12 @@ struct HeadArgs {
   int32_t ldx, ldy;
   int32_t x_bf16;
   int32_t act1, act2;
+  // optional: X is a tree partial slab [groups][M][K] to be reduced (+base, /T) while staging
+  const float* partial;
+  const float* pbase;
+  int32_t groups;
+  int32_t p_average;
+  int32_t p_ntrees;
 };
 void launch_mlp_head(const HeadArgs& a, hipStream_t st);
 
@@ -121,6 +132,8 @@ struct EnsembleArgs {
   ResultRec* out;
   unsigned long long* metrics;  // [128] score histogram(101) | actions(4) | ml_high | rows (nullable)
   int32_t n_rows;
+  int32_t do_update;        // apply single-event accounts / open segments (score-then-update)
+  UpdateArgs upd;
 };
 void launch_ensemble(const EnsembleArgs& a, hipStream_t st);
 

@@ -1,13 +1,16 @@
 // K2 tree_ensemble: ONNX-ML TreeEnsemble{Classifier,Regressor} on the complete-tree layout
 // (csrc/runtime/trees.h). Semantics: CPU executor (csrc/runtime/trees.cpp).
 //
-// Block = 256 threads = 4 waves, 64 samples (lane = sample). The block's 64-row X tile
-// ([64][F+1] f32, +1 pad -> conflict-free column reads) and its tree group's node table
-// (8 B/node) are staged in LDS; the four waves split the group's trees and each lane keeps
-// 4 traversals in flight (independent LDS chains hide the ds_read latency). Leaf vectors
-// are read from L2. Wave partials are reduced through LDS; with several tree groups per
-// sample tile (small batches) partial sums go to a scratch slab and a finisher kernel adds
-// base values and applies the post transform.
+// Block = 256 threads = 4 waves, 64 samples. The block's X tile ([64][F+1] f32; the +1 pad
+// makes the per-lane column reads conflict-free at the root) and its tree group's node table
+// (8 B/node) are staged in LDS. Traversal: lane = sample, the four waves split the group's
+// trees, each lane keeps 4 traversals in flight (independent LDS chains hide ds_read latency).
+//  * K < 16: each lane accumulates its leaf values directly (4-32 B per visit).
+//  * K >= 16 (leaf vectors, e.g. stacked GBDT->MLP embeddings): traversal only records leaf
+//    indices in LDS; a second phase puts lanes on the K targets so that each wave-load reads
+//    whole contiguous leaf rows (coalesced) instead of 64 scattered 16-B pieces.
+// Several tree groups per sample tile (small batches) write partial sums to a slab; a
+// finisher (or the consuming mlp_head kernel) adds base values and the post transform.
 #include "common.h"
 #include "launch.h"
 
@@ -26,41 +29,75 @@ __device__ __forceinline__ int tree_step(int i, float x, float2 nd) {
   return 2 * i + (c ? 1 : 2);
 }
 
+__device__ __forceinline__ void post_row(const TreeArgs& a, const float* s, float* o, int K) {
+  if (a.binary_class >= 0) {
+    float v = s[0];
+    if (a.average) v /= (float)a.n_trees;
+    if (a.base) v += a.base[0];
+    const int c = a.binary_class;
+    if (a.post == 1) {
+      o[c] = 1.f / (1.f + expf(-v));
+      o[1 - c] = 1.f / (1.f + expf(v));
+    } else {
+      o[c] = v;
+      o[1 - c] = a.all_positive ? 1.f - v : -v;
+    }
+    return;
+  }
+  float mx = -INFINITY;
+  for (int k = 0; k < K; ++k) {
+    float v = s[k];
+    if (a.average) v /= (float)a.n_trees;
+    if (a.base) v += a.base[k];
+    if (a.post == 1) v = 1.f / (1.f + expf(-v));
+    o[k] = v;
+    mx = fmaxf(mx, v);
+  }
+  if (a.post == 2) {
+    float sum = 0.f;
+    for (int k = 0; k < K; ++k) { o[k] = expf(o[k] - mx); sum += o[k]; }
+    for (int k = 0; k < K; ++k) o[k] /= sum;
+  }
+}
+
 template <int K>
 __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_group, int feat_w,
                                                    int nodes_in_lds, float* partial) {
+  constexpr bool TWO_PHASE = K >= 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int xs = feat_w + 1;
   float* sx = reinterpret_cast<float*>(smem);                       // [64][feat_w+1]
-  float2* sn = reinterpret_cast<float2*>(smem + ((TR_ROWS * xs * 4 + 15) & ~15));
+  const size_t x_bytes = ((size_t)TR_ROWS * xs * 4 + 15) & ~size_t(15);
+  const size_t red_b = TWO_PHASE ? (size_t)TR_ROWS * K * 4 : (size_t)5 * TR_ROWS * K * 4;
+  const size_t base_b = x_bytes > red_b ? x_bytes : red_b;
+  float2* sn = reinterpret_cast<float2*>(smem + base_b);             // group node table
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row0 = blockIdx.x * TR_ROWS;
   const int g = blockIdx.y;
   const int t0 = g * trees_per_group;
   const int t1 = min(a.n_trees, t0 + trees_per_group);
+  const int nt = t1 - t0;
   const int n_int = (1 << a.depth) - 1;
   const int n_leaf = 1 << a.depth;
+  const size_t node_b = ((size_t)trees_per_group * n_int * 8 + 15) & ~size_t(15);
+  uint16_t* sleaf = reinterpret_cast<uint16_t*>(smem + base_b + (nodes_in_lds ? node_b : 0));
 
-  // stage X tile
   for (int e = tid; e < TR_ROWS * feat_w; e += 256) {
     const int r = e / feat_w, c = e - r * feat_w;
     const int row = row0 + r;
     sx[r * xs + c] = row < a.n_rows ? a.X[(size_t)row * a.x_stride + c] : 0.f;
   }
-  // stage this group's nodes
   const float2* gn = a.nodes + (size_t)t0 * n_int;
-  const int nn = (t1 - t0) * n_int;
   if (nodes_in_lds)
-    for (int e = tid; e < nn; e += 256) sn[e] = gn[e];
+    for (int e = tid; e < nt * n_int; e += 256) sn[e] = gn[e];
   __syncthreads();
   const float2* nodes = nodes_in_lds ? sn : gn;
-
-  float acc[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) acc[k] = 0.f;
   const float* xrow = sx + lane * xs;
 
-  // trees of this wave: t0 + wave + 4j
+  float acc[TWO_PHASE ? 1 : K];
+#pragma unroll
+  for (int k = 0; k < (TWO_PHASE ? 1 : K); ++k) acc[k] = 0.f;
+
   for (int tb = t0 + wave; tb < t1; tb += 4 * TR_ILP) {
     int idx[TR_ILP];
     int tt[TR_ILP];
@@ -81,7 +118,10 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
     }
 #pragma unroll
     for (int q = 0; q < TR_ILP; ++q) {
-      if (tt[q] < t1) {
+      if (tt[q] >= t1) continue;
+      if constexpr (TWO_PHASE) {
+        sleaf[lane * nt + (tt[q] - t0)] = (uint16_t)(idx[q] - n_int);
+      } else {
         const float* lf = a.leaves + ((size_t)tt[q] * n_leaf + (idx[q] - n_int)) * K;
         if constexpr (K % 4 == 0) {
 #pragma unroll
@@ -96,59 +136,55 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
       }
     }
   }
-  // reduce the 4 waves through LDS (reuse the X tile region)
   __syncthreads();
-  float* red = sx;  // [4][64][K]
-#pragma unroll
-  for (int k = 0; k < K; ++k) red[(wave * TR_ROWS + lane) * K + k] = acc[k];
-  __syncthreads();
-  for (int e = tid; e < TR_ROWS * K; e += 256) {
-    const int r = e / K, k = e - r * K;
-    const int row = row0 + r;
-    float v = red[(0 * TR_ROWS + r) * K + k] + red[(1 * TR_ROWS + r) * K + k] +
-              red[(2 * TR_ROWS + r) * K + k] + red[(3 * TR_ROWS + r) * K + k];
-    if (row >= a.n_rows) continue;
-    if (partial) {
-      partial[((size_t)g * a.n_rows + row) * K + k] = v;
-    } else {
-      red[(4 * TR_ROWS + r) * K + k] = v;  // final sums, post-transform below
-    }
-  }
-  if (partial) return;
-  __syncthreads();
-  // post transform, one thread per row
-  for (int r = tid; r < TR_ROWS; r += 256) {
-    const int row = row0 + r;
-    if (row >= a.n_rows) continue;
-    float* o = a.out + (size_t)row * a.n_out;
-    const float* s = red + (4 * TR_ROWS + r) * K;
-    if (a.binary_class >= 0) {
-      float v = s[0];
-      if (a.average) v /= (float)a.n_trees;
-      if (a.base) v += a.base[0];
-      const int c = a.binary_class;
-      if (a.post == 1) {
-        o[c] = 1.f / (1.f + expf(-v));
-        o[1 - c] = 1.f / (1.f + expf(v));
+  float* red = sx;  // reuse the X tile region: [5][64][K] (K < 16) or [64][K] (two-phase)
+  if constexpr (TWO_PHASE) {
+    // phase 2: lanes over targets, coalesced leaf rows
+    constexpr int SPP = 256 / K;  // samples per pass
+    const int k = tid % K, sp = tid / K;
+    const bool rowwise = !partial && (a.post == 2 || a.binary_class >= 0);
+    for (int r = sp; r < TR_ROWS; r += SPP) {
+      const uint16_t* li = sleaf + r * nt;
+      float v = 0.f;
+      for (int t = 0; t < nt; ++t) v += a.leaves[((size_t)(t0 + t) * n_leaf + li[t]) * K + k];
+      const int row = row0 + r;
+      if (row >= a.n_rows) continue;
+      if (partial) {
+        partial[((size_t)g * a.n_rows + row) * K + k] = v;
+      } else if (rowwise) {
+        red[r * K + k] = v;
       } else {
-        o[c] = v;
-        o[1 - c] = a.all_positive ? 1.f - v : -v;
+        if (a.average) v /= (float)a.n_trees;
+        if (a.base) v += a.base[k];
+        if (a.post == 1) v = 1.f / (1.f + expf(-v));
+        a.out[(size_t)row * a.n_out + k] = v;
       }
-      continue;
     }
-    float mx = -INFINITY;
-    for (int k = 0; k < K; ++k) {
-      float v = s[k];
-      if (a.average) v /= (float)a.n_trees;
-      if (a.base) v += a.base[k];
-      if (a.post == 1) v = 1.f / (1.f + expf(-v));
-      o[k] = v;
-      mx = fmaxf(mx, v);
+    if (!rowwise) return;
+    __syncthreads();
+    for (int r = tid; r < TR_ROWS; r += 256) {
+      const int row = row0 + r;
+      if (row < a.n_rows) post_row(a, red + r * K, a.out + (size_t)row * a.n_out, K);
     }
-    if (a.post == 2) {
-      float sum = 0.f;
-      for (int k = 0; k < K; ++k) { o[k] = expf(o[k] - mx); sum += o[k]; }
-      for (int k = 0; k < K; ++k) o[k] /= sum;
+    return;
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; ++k) red[(wave * TR_ROWS + lane) * K + k] = acc[k];
+    __syncthreads();
+    for (int e = tid; e < TR_ROWS * K; e += 256) {
+      const int r = e / K, k = e - r * K;
+      const int row = row0 + r;
+      const float v = red[(0 * TR_ROWS + r) * K + k] + red[(1 * TR_ROWS + r) * K + k] +
+                      red[(2 * TR_ROWS + r) * K + k] + red[(3 * TR_ROWS + r) * K + k];
+      if (row >= a.n_rows) continue;
+      if (partial) partial[((size_t)g * a.n_rows + row) * K + k] = v;
+      else red[(4 * TR_ROWS + r) * K + k] = v;
+    }
+    if (partial) return;
+    __syncthreads();
+    for (int r = tid; r < TR_ROWS; r += 256) {
+      const int row = row0 + r;
+      if (row < a.n_rows) post_row(a, red + (4 * TR_ROWS + r) * K, a.out + (size_t)row * a.n_out, K);
     }
   }
 }
@@ -157,37 +193,13 @@ __global__ void tree_finish_kernel(TreeArgs a, const float* partial, int groups)
   const int row = blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= a.n_rows) return;
   const int K = a.k;
-  float* o = a.out + (size_t)row * a.n_out;
-  if (a.binary_class >= 0) {
-    float v = 0.f;
-    for (int g = 0; g < groups; ++g) v += partial[((size_t)g * a.n_rows + row) * K];
-    if (a.average) v /= (float)a.n_trees;
-    if (a.base) v += a.base[0];
-    const int c = a.binary_class;
-    if (a.post == 1) {
-      o[c] = 1.f / (1.f + expf(-v));
-      o[1 - c] = 1.f / (1.f + expf(v));
-    } else {
-      o[c] = v;
-      o[1 - c] = a.all_positive ? 1.f - v : -v;
-    }
-    return;
-  }
-  float mx = -INFINITY;
+  float s[64];
   for (int k = 0; k < K; ++k) {
     float v = 0.f;
     for (int g = 0; g < groups; ++g) v += partial[((size_t)g * a.n_rows + row) * K + k];
-    if (a.average) v /= (float)a.n_trees;
-    if (a.base) v += a.base[k];
-    if (a.post == 1) v = 1.f / (1.f + expf(-v));
-    o[k] = v;
-    mx = fmaxf(mx, v);
+    s[k] = v;
   }
-  if (a.post == 2) {
-    float sum = 0.f;
-    for (int k = 0; k < K; ++k) { o[k] = expf(o[k] - mx); sum += o[k]; }
-    for (int k = 0; k < K; ++k) o[k] /= sum;
-  }
+  post_row(a, s, a.out + (size_t)row * a.n_out, K);
 }
 
 // regressor / multi-output without a row-wise post transform: one thread per (row, target)
@@ -205,20 +217,21 @@ __global__ void tree_finish_elem_kernel(TreeArgs a, const float* partial, int gr
 }
 
 template <int K>
-static void launch_k(const TreeArgs& a, int groups, float* partial, hipStream_t st) {
+static void launch_k(const TreeArgs& a, int groups, float* partial, int no_finish, hipStream_t st) {
   const int tpg = (a.n_trees + groups - 1) / groups;
   const int feat_w = a.x_stride;
   const int n_int = (1 << a.depth) - 1;
   const size_t x_bytes = ((size_t)TR_ROWS * (feat_w + 1) * 4 + 15) & ~size_t(15);
-  const size_t red_bytes = (size_t)5 * TR_ROWS * K * 4;
-  const size_t node_bytes = (size_t)tpg * n_int * 8;
-  size_t lds = x_bytes > red_bytes ? x_bytes : red_bytes;
-  int in_lds = (lds + node_bytes) <= 96 * 1024;  // keep >= 1 block/CU with headroom
-  if (in_lds) lds = x_bytes + node_bytes > red_bytes ? x_bytes + node_bytes : red_bytes;
+  const size_t red_bytes = K >= 16 ? (size_t)TR_ROWS * K * 4 : (size_t)5 * TR_ROWS * K * 4;
+  const size_t node_bytes = ((size_t)tpg * n_int * 8 + 15) & ~size_t(15);
+  const size_t leaf_bytes = K >= 16 ? (size_t)TR_ROWS * tpg * 2 : 0;
+  const size_t base = x_bytes > red_bytes ? x_bytes : red_bytes;
+  int in_lds = (base + node_bytes + leaf_bytes) <= 96 * 1024;  // keep >= 1 block/CU with headroom
+  const size_t lds = base + (in_lds ? node_bytes : 0) + leaf_bytes;
   dim3 grid((a.n_rows + TR_ROWS - 1) / TR_ROWS, groups);
   hipLaunchKernelGGL((tree_kernel<K>), grid, dim3(256), lds, st, a, tpg, feat_w, in_lds,
                      groups > 1 ? partial : nullptr);
-  if (groups > 1) {
+  if (groups > 1 && !no_finish) {
     if (a.binary_class < 0 && a.post != 2 && a.n_out == K)
       hipLaunchKernelGGL(tree_finish_elem_kernel, dim3((a.n_rows * K + 255) / 256), dim3(256), 0, st, a,
                          partial, groups);
@@ -227,16 +240,18 @@ static void launch_k(const TreeArgs& a, int groups, float* partial, hipStream_t 
   }
 }
 
-// partial scratch: [groups][n_rows][K] f32, provided by the caller when groups > 1
+// partial scratch: [groups][n_rows][K] f32, provided by the caller when groups > 1.
+// no_finish: leave the partial slab for a consumer that reduces it (mlp_head).
 void launch_tree_ensemble_grouped(const TreeArgs& a, int groups, float* partial, hipStream_t st) {
+  const int nf = a.no_finish;
   switch (a.k) {
-    case 1: launch_k<1>(a, groups, partial, st); break;
-    case 2: launch_k<2>(a, groups, partial, st); break;
-    case 4: launch_k<4>(a, groups, partial, st); break;
-    case 8: launch_k<8>(a, groups, partial, st); break;
-    case 16: launch_k<16>(a, groups, partial, st); break;
-    case 32: launch_k<32>(a, groups, partial, st); break;
-    case 64: launch_k<64>(a, groups, partial, st); break;
+    case 1: launch_k<1>(a, groups, partial, nf, st); break;
+    case 2: launch_k<2>(a, groups, partial, nf, st); break;
+    case 4: launch_k<4>(a, groups, partial, nf, st); break;
+    case 8: launch_k<8>(a, groups, partial, nf, st); break;
+    case 16: launch_k<16>(a, groups, partial, nf, st); break;
+    case 32: launch_k<32>(a, groups, partial, nf, st); break;
+    case 64: launch_k<64>(a, groups, partial, nf, st); break;
     default: break;  // host validates K before launch
   }
 }

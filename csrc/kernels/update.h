@@ -1,0 +1,168 @@
+// Feature-store write path shared by feature_assemble (dedup insert), ensemble (single-event
+// apply) and the segment kernels. Golden: igaming_platform_amd/golden/features.py
+// GoldenFeatureStore.apply == redis_store.go:119-168 on the ring representation.
+#pragma once
+#include "common.h"
+#include "launch.h"
+
+namespace igp {
+
+// One dedup region: per-batch hash table slot -> (first event, count) plus segment lists of
+// accounts that have several events in the batch.
+struct DedupTab {
+  int32_t* keys;
+  int32_t* first;
+  int32_t* count;
+  int32_t* fill;
+  int32_t* off;
+  int32_t* list;    // [n_max]
+  int32_t* mlist;   // [n_max] hash slots of multi-event accounts
+  int32_t* ctr;     // [0] segment allocator, [1] multi-account count
+  int32_t cap;
+};
+
+__device__ __forceinline__ DedupTab dedup_region(int32_t* buf, int cap, int n_max, int region) {
+  const size_t rs = ((size_t)5 * cap + 2 * (size_t)n_max + 2 + 15) & ~size_t(15);
+  int32_t* b = buf + rs * region;
+  DedupTab t;
+  t.keys = b;
+  t.first = b + cap;
+  t.count = b + 2 * cap;
+  t.fill = b + 3 * cap;
+  t.off = b + 4 * cap;
+  t.list = b + 5 * cap;
+  t.mlist = t.list + n_max;
+  t.ctr = t.mlist + n_max;
+  t.cap = cap;
+  return t;
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ void dedup_insert(const DedupTab& t, int s, int i) {
+  uint32_t h = mix32((uint32_t)s) & (uint32_t)(t.cap - 1);
+  for (int p = 0; p < t.cap; ++p) {
+    const int prev = atomicCAS(&t.keys[h], -1, s);
+    if (prev == -1 || prev == s) {
+      atomicMin(&t.first[h], i);
+      atomicAdd(&t.count[h], 1);
+      return;
+    }
+    h = (h + 1) & (uint32_t)(t.cap - 1);
+  }
+}
+
+__device__ __forceinline__ int dedup_find(const DedupTab& t, int s) {
+  uint32_t h = mix32((uint32_t)s) & (uint32_t)(t.cap - 1);
+  for (int p = 0; p < t.cap; ++p) {
+    const int k = t.keys[h];
+    if (k == s) return (int)h;
+    if (k == -1) return -1;
+    h = (h + 1) & (uint32_t)(t.cap - 1);
+  }
+  return -1;
+}
+
+// clear entries [e0, e1) of a region (keys, first, count, fill)
+__device__ __forceinline__ void dedup_clear_range(const DedupTab& t, int e0, int e1, int lane) {
+  for (int e = e0 + lane; e < e1; e += 64) {
+    t.keys[e] = -1;
+    t.first[e] = 0x7fffffff;
+    t.count[e] = 0;
+    t.fill[e] = 0;
+  }
+}
+
+__device__ __forceinline__ int hll_rank(uint64_t h) {
+  const uint64_t wv = h >> 8;
+  return wv ? (__clzll((long long)wv) - 8 + 1) : 57;
+}
+
+__device__ __forceinline__ void hll_add(uint8_t* rg, uint32_t& exp, uint64_t h, int64_t now, int ttl,
+                                        bool& changed) {
+  if (now >= (int64_t)exp) {
+    uint4* w = reinterpret_cast<uint4*>(rg);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = make_uint4(0, 0, 0, 0);
+  }
+  const int idx = (int)(h & 255u);
+  const int rank = hll_rank(h);
+  if (rank > rg[idx]) {
+    rg[idx] = (uint8_t)rank;
+    changed = true;
+  }
+  exp = (uint32_t)(now + ttl);
+}
+
+// encode + store one GRU event row (golden.features.encode_event), dim 16 bf16 = 32 B
+__device__ __forceinline__ void write_event_row(uint16_t* e, int64_t amt, int tt, int64_t now, int64_t prev,
+                                                bool new_dev, bool new_ip) {
+  const int64_t dt = (prev > 0 && now >= prev) ? now - prev : 0;
+  const double hour = (double)(now % 86400) / 3600.0;
+  uint32_t w[8];
+  w[0] = (uint32_t)f32_to_bf16((float)(log1p((double)(amt > 0 ? amt : 0)) / 16.0)) |
+         ((uint32_t)f32_to_bf16(tt == 0 ? 1.f : 0.f) << 16);
+  w[1] = (uint32_t)f32_to_bf16(tt == 1 ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(tt == 2 ? 1.f : 0.f) << 16);
+  w[2] = (uint32_t)f32_to_bf16(tt == 3 ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(tt == 4 ? 1.f : 0.f) << 16);
+  w[3] = (uint32_t)f32_to_bf16(tt == 5 ? 1.f : 0.f) |
+         ((uint32_t)f32_to_bf16((float)(log1p((double)dt) / 12.0)) << 16);
+  w[4] = (uint32_t)f32_to_bf16((float)sin(2.0 * M_PI * hour / 24.0)) |
+         ((uint32_t)f32_to_bf16((float)cos(2.0 * M_PI * hour / 24.0)) << 16);
+  w[5] = (uint32_t)f32_to_bf16(new_dev ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(new_ip ? 1.f : 0.f) << 16);
+  w[6] = (uint32_t)f32_to_bf16(amt >= 100000 ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(1.f) << 16);
+  w[7] = 0u;
+  uint4* e4 = reinterpret_cast<uint4*>(e);
+  e4[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  e4[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+// apply one event to an account whose AcctRT `r` the caller holds in registers
+__device__ __forceinline__ void apply_event(const UpdateArgs& a, int j, AcctRT& r) {
+  const ReqRec ev = a.req[j];
+  const int s = ev.slot;
+  const int64_t now = ev.ts;
+  const ScoreCfg& cfg = *a.cfg;
+  const int64_t amt = ev.amount;
+  const int hd = r.ring_head;
+  a.ring_ts[(size_t)s * a.ring_size + hd] = (uint32_t)now;
+  a.ring_amt[(size_t)s * a.ring_size + hd] = amt;
+  r.ring_head = hd + 1 == a.ring_size ? 0 : hd + 1;
+  if (now >= (int64_t)r.sum_exp) r.sum_compat = 0;
+  r.sum_compat += amt;
+  r.sum_exp = (uint32_t)(now + cfg.sum_ttl);
+  bool new_dev = false, new_ip = false;
+  uint8_t* regs = a.hll + (size_t)s * 512;
+  if (ev.dev_hash) hll_add(regs, r.hll_dev_exp, ev.dev_hash, now, cfg.hll_ttl, new_dev);
+  if (ev.ip_hash) hll_add(regs + 256, r.hll_ip_exp, ev.ip_hash, now, cfg.hll_ttl, new_ip);
+  r.last_tx = (uint32_t)now;
+  r.last_tx_exp = (uint32_t)(now + cfg.last_tx_ttl);
+  if (now >= (int64_t)r.session_exp || r.session_start == 0) r.session_start = (uint32_t)now;
+  r.session_exp = (uint32_t)(now + cfg.session_ttl);
+  if (a.ev) {
+    write_event_row(a.ev + ((size_t)s * a.ev_ring + r.ev_head) * a.ev_dim, amt, ev.tx_type, now,
+                    (int64_t)r.last_event_ts, new_dev, new_ip);
+    r.ev_head = r.ev_head + 1 == a.ev_ring ? 0 : r.ev_head + 1;
+    r.ev_count = r.ev_count + 1 > a.ev_ring ? a.ev_ring : r.ev_count + 1;
+  }
+  r.last_event_ts = (uint32_t)now;
+}
+
+// the batch's first event of account s: apply it (single) or open its segment (multi)
+__device__ __forceinline__ void update_first_event(const UpdateArgs& a, const DedupTab& t, int i, int s) {
+  const int h = dedup_find(t, s);
+  if (h < 0 || t.first[h] != i) return;
+  const int c = t.count[h];
+  if (c == 1) {
+    AcctRT r = a.rt[s];
+    apply_event(a, i, r);
+    a.rt[s] = r;
+  } else {
+    t.off[h] = atomicAdd(&t.ctr[0], c);
+    t.mlist[atomicAdd(&t.ctr[1], 1)] = h;
+  }
+}
+
+}  // namespace igp

@@ -60,7 +60,7 @@ class GpuScorer:
         self.use_graphs = cfg.gpu.use_graphs if use_graphs is None else use_graphs
         self.buckets = sorted(set(int(b) for b in cfg.gpu.buckets))
         self.bmax = self.buckets[-1]
-        if store.max_events < self.bmax:
+        if store.dmax < self.bmax:
             raise ValueError("store.max_events must cover the largest bucket (score-then-update)")
         self.width = cfg.features.width
         if plan is not None and plan.in_width > 0 and plan.in_width != self.width:
@@ -86,6 +86,7 @@ class GpuScorer:
         self.refresh_config()
         self.graphs: Dict[tuple, "torch.cuda.CUDAGraph"] = {}
         self._slot = 0
+        self._seq = 0
         self._lock = threading.Lock()
         self.stream = torch.cuda.Stream(device=dev)
         self.batches = 0
@@ -134,21 +135,30 @@ class GpuScorer:
 
     # ------------------------------------------------------------------ the step
     def _kernels(self, bucket: int) -> None:
-        K.feature_assemble(self.store, self.hdr, self.cfg_dev, self.req, self.X, self.feat, bucket)
+        upd = self.update_features
+        K.feature_assemble(self.store, self.hdr, self.cfg_dev, self.req, self.X, self.feat, bucket, dedup=upd)
         cur = self.X
         if self.plan is not None:
-            for s, out in zip(self.plan.steps, self.step_out):
+            steps = self.plan.steps
+            skip_next_input = None
+            for i, (s, out) in enumerate(zip(steps, self.step_out)):
                 if s.kind == "tree":
                     g = self.tree_groups.get(bucket, 1)
-                    K.tree_ensemble(s, cur, out, bucket, partial=self.tree_partial, groups=g)
+                    fuse = (g > 1 and i + 1 < len(steps) and steps[i + 1].kind == "head" and s.post == 0
+                            and s.binary_class < 0 and steps[i + 1].k == s.k)
+                    K.tree_ensemble(s, cur, None if fuse else out, bucket, partial=self.tree_partial,
+                                    groups=g, no_finish=fuse)
+                    skip_next_input = (self.tree_partial, g, s) if fuse else None
                 elif s.kind == "dense":
                     K.dense(cur, s.w, s.b, out, bucket, s.n, s.k, act=s.act, m_ptr=self.n_ptr)
                 elif s.kind == "head":
-                    K.mlp_head(s, cur, out, bucket, m_ptr=self.n_ptr)
+                    K.mlp_head(s, cur, out, bucket, m_ptr=self.n_ptr, tree_partial=skip_next_input)
+                    skip_next_input = None
                 cur = out
-        K.ensemble(self.hdr, self.cfg_dev, self.feat, self.X, self.ml, self.res, bucket, self.metrics)
-        if self.update_features:
-            K.feature_update(self.store, self.cfg_dev, self.req, bucket, n_ptr=self.n_ptr)
+        ud = K.update_args(self.store, self.cfg_dev, self.req, bucket, hdr=self.hdr, region=-1) if upd else None
+        K.ensemble(self.hdr, self.cfg_dev, self.feat, self.X, self.ml, self.res, bucket, self.metrics, upd=ud)
+        if upd:
+            K.update_segments(self.store, self.cfg_dev, self.req, bucket, self.hdr)
 
     def _body(self, slot: int, bucket: int, with_features: bool = False) -> None:
         nbytes = HDR_BYTES + REQ_BYTES * bucket
@@ -186,6 +196,7 @@ class GpuScorer:
     def _write_hdr(self, slot: int, n: int, now: int) -> None:
         h = self.host_slab_np[slot][:HDR_BYTES].view(BATCHHDR)
         h["n"] = n
+        h["seq"] = self._seq
         h["now"] = now
 
     def slab_view(self, slot: int, n: int) -> np.ndarray:
@@ -200,6 +211,7 @@ class GpuScorer:
     def submit_packed(self, slot: int, n: int, now: int, want_features: bool = False) -> Pending:
         """Launch a batch whose ReqRec rows are already in ``slab_view(slot, n)``."""
         b = self.bucket_for(max(n, 1))
+        self._seq += 1
         self._write_hdr(slot, n, now)
         t0 = time.perf_counter()
         with torch.cuda.stream(self.stream):

@@ -71,14 +71,19 @@ class DeviceFeatureStore:
         self._bl_version = -1
         self._ip_version = -1
         self.max_events = int(max_events)
+        # dedup scratch for ordered score-then-update: 3 regions (scorer ping-pong + standalone)
+        self.dmax = self.max_events
         self.dcap = _pow2_at_least(2 * self.max_events)
-        self.dkeys = torch.empty(self.dcap, dtype=torch.int32, **z)
-        self.dfirst = torch.empty(self.dcap, dtype=torch.int32, **z)
-        self.dcount = torch.empty(self.dcap, dtype=torch.int32, **z)
-        self.dfill = torch.empty(self.dcap, dtype=torch.int32, **z)
-        self.doff = torch.empty(self.dcap, dtype=torch.int32, **z)
-        self.dlist = torch.empty(self.max_events, dtype=torch.int32, **z)
-        self.dtotal = torch.zeros(1, dtype=torch.int32, **z)
+        self.dregion = (5 * self.dcap + 2 * self.dmax + 2 + 15) & ~15
+        self.dbuf = torch.empty(3 * self.dregion, dtype=torch.int32, **z)
+        self.reset_dedup()
+
+    def reset_dedup(self) -> None:
+        r = self.dbuf.view(3, self.dregion)
+        r[:, : self.dcap].fill_(-1)                            # keys
+        r[:, self.dcap: 2 * self.dcap].fill_(0x7FFFFFFF)        # first
+        r[:, 2 * self.dcap: 4 * self.dcap].zero_()              # count, fill
+        r[:, 5 * self.dcap + 2 * self.dmax:].zero_()            # counters
 
     # ------------------------------------------------------------------ sizing
     def bytes_per_account(self) -> int:

@@ -56,7 +56,7 @@ REQREC = np.dtype([
     ("fp_hash", "<u8"), ("ip_hash", "<u8"), ("ts", "<i8"),
 ])
 
-BATCHHDR = np.dtype([("n", "<i4"), ("pad", "<i4"), ("now", "<i8")])
+BATCHHDR = np.dtype([("n", "<i4"), ("seq", "<i4"), ("now", "<i8")])
 
 MODEL_NONE, MODEL_HEURISTIC, MODEL_OUTPUT = 0, 1, 2
 

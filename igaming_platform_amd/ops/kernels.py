@@ -53,10 +53,13 @@ def _opt(t: Optional[torch.Tensor], name: str, **kw):
 
 # --------------------------------------------------------------------------- K1
 def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch.Tensor,
-                     X: torch.Tensor, feat: torch.Tensor, n_rows: int) -> None:
+                     X: torch.Tensor, feat: torch.Tensor, n_rows: int, dedup: bool = False) -> None:
+    """K1. ``dedup=True`` also registers each request for score-then-update (ping-pong region)."""
     dev = store.device
     if X.dim() != 2 or X.shape[1] < 30 + store.ext_width:
         raise ValueError("X must be [rows, >= 30 + ext_width]")
+    if dedup and n_rows > store.dmax:
+        raise ValueError("score-then-update batch larger than the store's dedup capacity")
     d = dict(
         hdr=_need(hdr, "hdr", torch.int64, 2, dev), cfg=_need(cfg_dev, "cfg", torch.uint8, 176, dev),
         req=_need(req, "req", torch.uint8, 48 * n_rows, dev),
@@ -67,19 +70,24 @@ def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch
         ip_keys=_need(store.ip_keys, "ip_keys", torch.int64), ip_flags=_need(store.ip_flags, "ip_flags", torch.int32),
         X=_need(X, "X", torch.float32, X.shape[1] * n_rows, dev),
         feat=_need(feat, "feat", torch.int32, 32 * n_rows, dev),
+        dbuf=_need(store.dbuf, "dbuf", torch.int32) if dedup else None, dcap=int(store.dcap), dmax=int(store.dmax),
         x_stride=int(X.shape[1]), ring_size=int(store.ring_ts.shape[1]), n_rows=int(n_rows),
     )
     _mod().feature_assemble(d, _stream())
 
 
 # --------------------------------------------------------------------------- K6
-def feature_update(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int,
-                   n_ptr: Optional[torch.Tensor] = None, n: int = 0) -> None:
+def update_args(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, n: int = 0,
+                hdr: Optional[torch.Tensor] = None, region: int = 2) -> dict:
     dev = store.device
-    if n_max > store.max_events:
-        raise ValueError(f"feature_update: {n_max} events > store.max_events {store.max_events}")
-    d = dict(
-        cfg=_need(cfg_dev, "cfg", torch.uint8, 176, dev), n_ptr=_opt(n_ptr, "n_ptr", dtype=torch.int32),
+    if n_max > store.dmax:
+        raise ValueError(f"feature_update: {n_max} events > store dedup capacity {store.dmax}")
+    if region < 0 and hdr is None:
+        raise ValueError("ping-pong dedup region needs the batch header")
+    if store.ev is not None and store.ev.shape[2] != 16:
+        raise ValueError("event ring dim must be 16")
+    return dict(
+        cfg=_need(cfg_dev, "cfg", torch.uint8, 176, dev), hdr=_opt(hdr, "hdr", dtype=torch.int64, min_numel=2),
         n=int(n), n_max=int(n_max), req=_need(req, "req", torch.uint8, 48 * n_max, dev),
         ring_ts=_need(store.ring_ts, "ring_ts", torch.int32), ring_amt=_need(store.ring_amt, "ring_amt", torch.int64),
         hll=_need(store.hll, "hll", torch.uint8), rt=_need(store.rt, "rt", torch.int32),
@@ -87,21 +95,28 @@ def feature_update(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int,
         ring_size=int(store.ring_ts.shape[1]),
         ev_ring=int(store.ev.shape[1]) if store.ev is not None else 0,
         ev_dim=int(store.ev.shape[2]) if store.ev is not None else 0,
-        dcap=int(store.dcap), dkeys=_need(store.dkeys, "dkeys", torch.int32),
-        dfirst=_need(store.dfirst, "dfirst", torch.int32), dcount=_need(store.dcount, "dcount", torch.int32),
-        dfill=_need(store.dfill, "dfill", torch.int32), doff=_need(store.doff, "doff", torch.int32),
-        dlist=_need(store.dlist, "dlist", torch.int32, n_max), dtotal=_need(store.dtotal, "dtotal", torch.int32),
+        dbuf=_need(store.dbuf, "dbuf", torch.int32), dcap=int(store.dcap), dmax=int(store.dmax), region=int(region),
     )
-    if store.ev is not None and store.ev.shape[2] != 16:
-        raise ValueError("event ring dim must be 16")
-    if n_ptr is None and n > n_max:
+
+
+def feature_update(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, n: int = 0) -> None:
+    """Standalone ordered event ingestion (event bus / history replay): ``n`` events."""
+    if n > n_max:
         raise ValueError("n > n_max")
+    d = update_args(store, cfg_dev, req, n_max, n=n, region=2)
+    _mod().feature_update(d, _stream())
+
+
+def update_segments(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, hdr: torch.Tensor) -> None:
+    """Scorer tail: ordered apply of multi-event accounts (insert ran in K1, singles in K5)."""
+    d = update_args(store, cfg_dev, req, n_max, hdr=hdr, region=-1)
+    d["segments_only"] = 1
     _mod().feature_update(d, _stream())
 
 
 # --------------------------------------------------------------------------- K2
-def tree_ensemble(tp, X: torch.Tensor, out: torch.Tensor, n_rows: int,
-                  partial: Optional[torch.Tensor] = None, groups: int = 1) -> None:
+def tree_ensemble(tp, X: torch.Tensor, out: Optional[torch.Tensor], n_rows: int,
+                  partial: Optional[torch.Tensor] = None, groups: int = 1, no_finish: bool = False) -> None:
     """``tp``: models.plan.TreeStep with device tensors."""
     dev = X.device
     if tp.k not in (1, 2, 4, 8, 16, 32, 64):
@@ -110,13 +125,17 @@ def tree_ensemble(tp, X: torch.Tensor, out: torch.Tensor, n_rows: int,
         raise ValueError("X narrower than the ensemble's largest feature id")
     if groups > 1 and (partial is None or partial.numel() < groups * n_rows * tp.k):
         raise ValueError("grouped tree launch needs a [groups, rows, K] partial buffer")
+    if no_finish and groups <= 1:
+        raise ValueError("no_finish needs a grouped launch")
+    if out is None and not no_finish:
+        raise ValueError("tree_ensemble: out required")
     d = dict(
         X=_need(X, "X", torch.float32, X.shape[1] * n_rows), nodes=_need(tp.nodes, "nodes", torch.float32, device=dev),
         leaves=_need(tp.leaves, "leaves", torch.float32, device=dev), base=_opt(tp.base, "base", dtype=torch.float32),
-        out=_need(out, "out", torch.float32, tp.n_out * n_rows, dev), x_stride=int(X.shape[1]),
+        out=_opt(out, "out", dtype=torch.float32, min_numel=tp.n_out * n_rows), x_stride=int(X.shape[1]),
         n_rows=int(n_rows), n_trees=tp.n_trees, depth=tp.depth, k=tp.k, n_out=tp.n_out, post=tp.post,
         average=tp.average, binary_class=tp.binary_class, all_positive=tp.all_positive,
-        groups=int(groups), partial=_opt(partial, "partial", dtype=torch.float32),
+        groups=int(groups), partial=_opt(partial, "partial", dtype=torch.float32), no_finish=int(no_finish),
     )
     if tp.nodes.numel() < tp.n_trees * ((1 << tp.depth) - 1) * 2:
         raise ValueError("node table smaller than n_trees * (2^depth - 1)")
@@ -153,33 +172,51 @@ def dense(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], Y: tor
         _mod().gemm(d, _stream())
 
 
-def mlp_head(hs, X: torch.Tensor, Y: torch.Tensor, M: int, m_ptr: Optional[torch.Tensor] = None) -> None:
-    """``hs``: models.plan.HeadStep. Y[:M, 0] = act2(act1(X W1^T + b1) . w2 + b2)."""
+def mlp_head(hs, X: Optional[torch.Tensor], Y: torch.Tensor, M: int, m_ptr: Optional[torch.Tensor] = None,
+             tree_partial=None) -> None:
+    """``hs``: models.plan.HeadStep. Y[:M, 0] = act2(act1(X W1^T + b1) . w2 + b2).
+    ``tree_partial=(slab, groups, tree_step)``: X is the preceding tree ensemble's unreduced
+    group partials [groups, M, K]; the head reduces them while staging (no finisher launch)."""
+    if tree_partial is not None:
+        slab, groups, ts = tree_partial
+        if ts.k != hs.k or slab.numel() < groups * M * hs.k or ts.post != 0 or ts.binary_class >= 0:
+            raise ValueError("mlp_head: tree partial slab does not match the head")
+        X = slab
     dev = X.device
     if X.dtype not in (torch.float32, torch.bfloat16):
         raise ValueError("mlp_head: X must be float32 or bfloat16")
-    if X.shape[1] < hs.k or X.shape[0] < M or Y.shape[0] < M or Y.dtype != torch.float32:
-        raise ValueError("mlp_head: operand shapes/dtypes")
+    if tree_partial is None and (X.shape[1] < hs.k or X.shape[0] < M):
+        raise ValueError("mlp_head: operand shapes")
+    if Y.shape[0] < M or Y.dtype != torch.float32:
+        raise ValueError("mlp_head: output shape/dtype")
     if hs.w1.shape[0] < -(-hs.n1 // 64) * 64 or hs.w1.shape[1] % 32 or hs.w1.shape[1] < hs.k:
         raise ValueError("mlp_head: W1 padding")
     d = dict(X=_need(X, "X", device=dev), W1=_need(hs.w1, "W1", torch.bfloat16, device=dev),
              b1=_opt(hs.b1, "b1", dtype=torch.float32, min_numel=hs.n1),
              w2=_need(hs.w2, "w2", torch.float32, hs.n1, dev), b2=float(hs.b2),
              Y=_need(Y, "Y", torch.float32, M, dev), m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32),
-             M=int(M), K=int(hs.k), N1=int(hs.n1), k_pad=int(hs.w1.shape[1]), ldx=int(X.shape[1]),
+             M=int(M), K=int(hs.k), N1=int(hs.n1), k_pad=int(hs.w1.shape[1]), ldx=int(X.shape[1]) if X.dim() == 2 else hs.k,
              ldy=int(Y.shape[1]), x_bf16=int(X.dtype == torch.bfloat16), act1=ACT[hs.act1], act2=ACT[hs.act2])
+    if tree_partial is not None:
+        slab, groups, ts = tree_partial
+        d.update(partial=_need(slab, "partial", torch.float32, groups * M * hs.k, dev), ldx=hs.k,
+                 pbase=_opt(ts.base, "pbase", dtype=torch.float32, min_numel=hs.k), groups=int(groups),
+                 p_average=int(ts.average), p_ntrees=int(ts.n_trees))
     _mod().mlp_head(d, _stream())
 
 
 # --------------------------------------------------------------------------- K5 / K10
 def ensemble(hdr, cfg_dev, feat, X, ml: Optional[torch.Tensor], out, n_rows: int,
-             metrics: Optional[torch.Tensor] = None) -> None:
+             metrics: Optional[torch.Tensor] = None, upd: Optional[dict] = None) -> None:
     dev = feat.device
     d = dict(hdr=_need(hdr, "hdr", torch.int64, 2, dev), cfg=_need(cfg_dev, "cfg", torch.uint8, 176, dev),
              feat=_need(feat, "feat", torch.int32, 32 * n_rows, dev),
              X=_need(X, "X", torch.float32, X.shape[1] * n_rows, dev), x_stride=int(X.shape[1]),
              ml=_opt(ml, "ml", dtype=torch.float32), out=_need(out, "out", torch.int32, 2 * n_rows, dev),
-             metrics=_opt(metrics, "metrics", dtype=torch.int64, min_numel=128), n_rows=int(n_rows))
+             metrics=_opt(metrics, "metrics", dtype=torch.int64, min_numel=128), n_rows=int(n_rows),
+             do_update=int(upd is not None), upd=upd)
+    if ml is not None and ml.numel() < n_rows:
+        raise ValueError("ensemble: model output shorter than the batch")
     _mod().ensemble(d, _stream())
 
 
