@@ -30,14 +30,7 @@ import numpy as np
 
 BASELINE_P99_MS = 50.0  # README.md:58 "< 50ms latency" (the only published number)
 
-CONFIGS = {
-    "cfg3": dict(model="stacked", width=128, batch=8192,
-                 desc="cfg3 GBDT(100 trees,d7,128 feat)+MLP(32-256-1) stacked, TreeEnsembleRegressor->Gemm"),
-    "cfg2": dict(model="gbdt", width=128, batch=1024,
-                 desc="cfg2 GBDT fraud ensemble, 100 trees d7, 128 features, TreeEnsembleClassifier"),
-    "cfg1": dict(model="logistic", width=32, batch=8192, desc="cfg1 32-feature logistic (GPU path)"),
-    "heuristic": dict(model="heuristic", width=30, batch=8192, desc="reference rules + mockPredict heuristic"),
-}
+CONFIGS = ("cfg3", "cfg2", "cfg1", "heuristic")  # igaming_platform_amd/utils/benchkit.py
 
 
 def parse():
@@ -78,50 +71,14 @@ def main():
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         dist.init_process_group("nccl", device_id=dev)
 
-    from igaming_platform_amd.config import Config
-    from igaming_platform_amd.engine.scorer import GpuScorer
-    from igaming_platform_amd.features.device_store import DeviceFeatureStore
-    from igaming_platform_amd.layouts import REQREC
-    from igaming_platform_amd.models.plan import compile_onnx, to_device
-    from igaming_platform_amd.native import native
-    from igaming_platform_amd.onnx import builders
-    from igaming_platform_amd.ops import kernels as K
-    from igaming_platform_amd.utils.synth import NOW0, make_population, make_requests
+    from igaming_platform_amd.utils import benchkit
+    from igaming_platform_amd.utils.synth import NOW0
 
-    c = CONFIGS[a.config]
-    B = a.batch or c["batch"]
-    cfg = Config()
-    cfg.features.width = c["width"]
-    cfg.gpu.buckets = [B]
-    cfg.gpu.max_batch = B
+    S = benchkit.build(a.config, a.batch, a.accounts, dev, rank=rank, depth=a.depth,
+                       use_graphs=not a.no_graphs)
+    sc, pool, B = S.scorer, S.pool, S.batch
+    c = dict(desc=S.desc)
     n_acc = a.accounts
-
-    # ---- per-rank shard: population, HBM store, model replica
-    pop = make_population(n_acc, c["width"] - 30, seed=1000 + rank, fast_hash=True)
-    store = DeviceFeatureStore(n_acc, cfg.features, dev, events=True, max_events=B)
-    store.set_batch_features(np.arange(n_acc), pop.batch)
-    if c["width"] > 30:
-        store.set_ext(np.arange(n_acc), pop.ext)
-    for i in range(0, 200):
-        store.blacklist.add("device", f"bad-device-{rank}-{i}")
-    store.sync_tables()
-    plan = None
-    model = "heuristic"
-    if c["model"] != "heuristic":
-        m = native().OnnxModel.from_bytes(builders.build(c["model"]).SerializeToString())
-        plan = to_device(compile_onnx(m), dev)
-        model = "plan"
-    sc = GpuScorer(cfg, store, plan=plan, model=model, device=dev, pipeline_depth=a.depth,
-                   use_graphs=not a.no_graphs)
-    rng = np.random.default_rng(7 + rank)
-    # warm the feature store with ~an hour of history (velocity windows, HLLs, sessions)
-    for h in range(24):
-        r = make_requests(pop, B, rng, NOW0 - 3600 + 150 * h, spread_s=150, hot_frac=0.01)
-        t = torch.from_numpy(r.view(np.uint8).copy()).to(dev)
-        K.feature_update(store, sc.cfg_dev, t, B, n=B)
-    torch.cuda.synchronize(dev)
-    sc.capture()
-    pool = [make_requests(pop, B, rng, NOW0, hot_frac=0.02, unknown_frac=0.001) for _ in range(8)]
 
     gathered = torch.zeros(world * B * 2, dtype=torch.int32, device=dev) if world > 1 else None
     met_sum = torch.zeros(128, dtype=torch.int64, device=dev)

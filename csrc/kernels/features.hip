@@ -94,10 +94,15 @@ __global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs a) {
       i = (i + 1) & (uint32_t)cfg.ip_mask;
     }
   }
-  // ext row copy (independent of everything else)
-  if (ext_w > 0) {
-    const float* e = s >= 0 ? a.ext + (size_t)s * ext_w : nullptr;
-    for (int j = lane; j < ext_w; j += 64) xr[30 + j] = e ? e[j] : 0.f;
+  // ext row: loaded now (with the other account loads), stored at the end
+  float extv[4];
+  {
+    const float* e = a.ext + (size_t)(s >= 0 ? s : 0) * ext_w;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = lane + 64 * u;
+      extv[u] = (s >= 0 && j < ext_w) ? e[j] : 0.f;
+    }
   }
   // dedup insert for score-then-update
   if (a.dbuf && lane == 0 && s >= 0) dedup_insert(dedup_region(a.dbuf, a.dcap, a.dmax, seq & 1), s, row);
@@ -254,6 +259,12 @@ __global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs a) {
     default: break;
   }
   if (lane < 30) xr[lane] = xv;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int j = lane + 64 * u;
+    if (j < ext_w) xr[30 + j] = extv[u];
+  }
+  for (int j = lane + 256; j < ext_w; j += 64) xr[30 + j] = s >= 0 ? a.ext[(size_t)s * ext_w + j] : 0.f;
   if (lane == 0) a.feat[row] = f;
 }
 
@@ -297,7 +308,9 @@ __global__ void update_fill_kernel(UpdateArgs a) {
   const DedupTab t = upd_region(a);
   const int h = dedup_find(t, s);
   if (h < 0 || t.count[h] < 2) return;
-  t.list[t.off[h] + atomicAdd(&t.fill[h], 1)] = i;
+  const int off = t.off[h];
+  const int pos = atomicAdd(&t.fill[h], 1);
+  if (off >= 0 && pos < t.count[h] && off + pos < t.nmax) t.list[off + pos] = i;
 }
 
 // sequential fallback: insertion-sort the segment in memory, apply with AcctRT in registers
@@ -356,9 +369,10 @@ __global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const DedupTab t = upd_region(a);
-  if (w >= t.ctr[1]) return;
+  if (w >= min(t.ctr[1], t.nmax)) return;
   const int h = t.mlist[w];
   const int c = t.count[h];
+  if (h < 0 || h >= t.cap || t.off[h] < 0 || t.off[h] + c > t.nmax || c < 2) return;
   const int* lst = t.list + t.off[h];
   const ScoreCfg& cfg = *a.cfg;
   const int min_ttl = min(min(cfg.session_ttl, cfg.sum_ttl), min(cfg.hll_ttl, cfg.last_tx_ttl));

@@ -82,14 +82,46 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
   const size_t node_b = ((size_t)trees_per_group * n_int * 8 + 15) & ~size_t(15);
   uint16_t* sleaf = reinterpret_cast<uint16_t*>(smem + base_b + (nodes_in_lds ? node_b : 0));
 
-  for (int e = tid; e < TR_ROWS * feat_w; e += 256) {
-    const int r = e / feat_w, c = e - r * feat_w;
-    const int row = row0 + r;
-    sx[r * xs + c] = row < a.n_rows ? a.X[(size_t)row * a.x_stride + c] : 0.f;
+  // stage the X tile: all global loads of a thread are issued before its LDS stores
+  // (8 independent loads in flight instead of a load->store round trip per element)
+  {
+    constexpr int UN = 8;
+    const int total = TR_ROWS * feat_w;
+    for (int base = 0; base < total; base += 256 * UN) {
+      float v[UN];
+#pragma unroll
+      for (int u = 0; u < UN; ++u) {
+        const int e = base + u * 256 + tid;
+        const int r = e / feat_w, c = e - r * feat_w;
+        const int row = row0 + r;
+        v[u] = (e < total && row < a.n_rows) ? a.X[(size_t)row * a.x_stride + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < UN; ++u) {
+        const int e = base + u * 256 + tid;
+        const int r = e / feat_w, c = e - r * feat_w;
+        if (e < total) sx[r * xs + c] = v[u];
+      }
+    }
   }
   const float2* gn = a.nodes + (size_t)t0 * n_int;
-  if (nodes_in_lds)
-    for (int e = tid; e < nt * n_int; e += 256) sn[e] = gn[e];
+  if (nodes_in_lds) {
+    constexpr int UN = 8;
+    const int total = nt * n_int;
+    for (int base = 0; base < total; base += 256 * UN) {
+      float2 v[UN];
+#pragma unroll
+      for (int u = 0; u < UN; ++u) {
+        const int e = base + u * 256 + tid;
+        v[u] = e < total ? gn[e] : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < UN; ++u) {
+        const int e = base + u * 256 + tid;
+        if (e < total) sn[e] = v[u];
+      }
+    }
+  }
   __syncthreads();
   const float2* nodes = nodes_in_lds ? sn : gn;
   const float* xrow = sx + lane * xs;
@@ -146,7 +178,15 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
     for (int r = sp; r < TR_ROWS; r += SPP) {
       const uint16_t* li = sleaf + r * nt;
       float v = 0.f;
-      for (int t = 0; t < nt; ++t) v += a.leaves[((size_t)(t0 + t) * n_leaf + li[t]) * K + k];
+      int t = 0;
+      for (; t + 8 <= nt; t += 8) {  // 8 leaf-row loads in flight per lane
+        float p[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) p[u] = a.leaves[((size_t)(t0 + t + u) * n_leaf + li[t + u]) * K + k];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v += p[u];
+      }
+      for (; t < nt; ++t) v += a.leaves[((size_t)(t0 + t) * n_leaf + li[t]) * K + k];
       const int row = row0 + r;
       if (row >= a.n_rows) continue;
       if (partial) {

@@ -19,6 +19,7 @@ struct DedupTab {
   int32_t* mlist;   // [n_max] hash slots of multi-event accounts
   int32_t* ctr;     // [0] segment allocator, [1] multi-account count
   int32_t cap;
+  int32_t nmax;     // capacity of list / mlist
 };
 
 __device__ __forceinline__ DedupTab dedup_region(int32_t* buf, int cap, int n_max, int region) {
@@ -34,6 +35,7 @@ __device__ __forceinline__ DedupTab dedup_region(int32_t* buf, int cap, int n_ma
   t.mlist = t.list + n_max;
   t.ctr = t.mlist + n_max;
   t.cap = cap;
+  t.nmax = n_max;
   return t;
 }
 
@@ -160,8 +162,14 @@ __device__ __forceinline__ void update_first_event(const UpdateArgs& a, const De
     apply_event(a, i, r);
     a.rt[s] = r;
   } else {
-    t.off[h] = atomicAdd(&t.ctr[0], c);
-    t.mlist[atomicAdd(&t.ctr[1], 1)] = h;
+    // capacity guards: a batch has at most nmax events, so these only trip on misuse
+    // (e.g. a re-played batch header); the segment is then skipped, never written out of bounds
+    const int off = atomicAdd(&t.ctr[0], c);
+    t.off[h] = off + c <= t.nmax ? off : -1;
+    if (off + c <= t.nmax) {
+      const int m = atomicAdd(&t.ctr[1], 1);
+      if (m < t.nmax) t.mlist[m] = h;
+    }
   }
 }
 

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Per-kernel device time of one scoring step (events around each launch, interleaved rounds
+in one process). Usage: python tools/kbench.py [--config cfg3] [--rounds 50]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg3")
+    ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--accounts", type=int, default=1 << 20)
+    ap.add_argument("--rounds", type=int, default=50)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    import torch
+    from igaming_platform_amd.ops import kernels as K
+    from igaming_platform_amd.utils import benchkit
+    from igaming_platform_amd.utils.synth import NOW0
+    dev = torch.device("cuda", 0)
+    S = benchkit.build(a.config, a.batch, a.accounts, dev)
+    sc, B = S.scorer, S.batch
+    # load a request batch into the device slab once
+    slot = 0
+    v = sc.slab_view(slot, B)
+    v[:] = S.pool[0]
+    v["ts"] = NOW0
+    sc._seq += 1
+    sc._write_hdr(slot, B, NOW0)
+    nb = 16 + 48 * B
+    sc.dev_slab[:nb].copy_(sc.host_slab[slot][:nb])
+    torch.cuda.synchronize()
+
+    steps = sc.plan.steps if sc.plan else []
+    tree = next((s for s in steps if s.kind == "tree"), None)
+    head = next((s for s in steps if s.kind == "head"), None)
+    g = sc.tree_groups.get(B, 1)
+    ud = K.update_args(sc.store, sc.cfg_dev, sc.req, B, hdr=sc.hdr, region=-1)
+    ops = {
+        "h2d_slab": lambda: sc.dev_slab[:nb].copy_(sc.host_slab[slot][:nb], non_blocking=True),
+        "feature_assemble": lambda: K.feature_assemble(sc.store, sc.hdr, sc.cfg_dev, sc.req, sc.X, sc.feat, B, dedup=True),
+        "ensemble+single_update": lambda: K.ensemble(sc.hdr, sc.cfg_dev, sc.feat, sc.X, sc.ml, sc.res, B, sc.metrics, upd=ud),
+        "update_segments": lambda: K.update_segments(sc.store, sc.cfg_dev, sc.req, B, sc.hdr),
+        "d2h_results": lambda: sc.host_res[slot][:B].copy_(sc.res[:B], non_blocking=True),
+    }
+    if tree is not None:
+        ops["tree_ensemble"] = lambda: K.tree_ensemble(tree, sc.X, None if head else sc.step_out[0], B,
+                                                        partial=sc.tree_partial, groups=g, no_finish=head is not None)
+    if head is not None:
+        out = sc.step_out[-1]
+        ops["mlp_head"] = lambda: K.mlp_head(head, sc.X, out, B, m_ptr=sc.n_ptr,
+                                             tree_partial=(sc.tree_partial, g, tree) if tree else None)
+    if sc.graphs:
+        gr = sc.graphs[(B, slot)]
+        ops["full_step_graph"] = gr.replay
+    times = {k: [] for k in ops}
+    for r in range(a.rounds):
+        # a fresh batch sequence number per round, as the scorer does per micro-batch
+        sc._seq += 1
+        sc._write_hdr(slot, B, NOW0)
+        for k, f in ops.items():
+            if k == "full_step_graph":  # the graph re-copies the slab: give it its own batch seq
+                sc._seq += 1
+                sc._write_hdr(slot, B, NOW0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            f()
+            e1.record()
+            e1.synchronize()
+            times[k].append(e0.elapsed_time(e1) * 1e3)
+    res = {k: dict(median_us=float(np.median(v[5:])), min_us=float(np.min(v[5:]))) for k, v in times.items()}
+    for k, v in res.items():
+        print(f"{k:28s} median {v['median_us']:8.1f} us   min {v['min_us']:8.1f} us")
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(dict(config=a.config, batch=B, kernels=res), f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
