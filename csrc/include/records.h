@@ -10,7 +10,7 @@ enum TxType : uint8_t { TX_DEPOSIT = 0, TX_WITHDRAW = 1, TX_BET = 2, TX_WIN = 3,
 
 // FeatRec flag bits
 enum : int32_t { FR_VPN = 1, FR_PROXY = 2, FR_TOR = 4, FR_DISPOSABLE = 8, FR_BONUS_ONLY = 16,
-                 FR_BLACKLISTED = 32, FR_PARTIAL = 64 };
+                 FR_BLACKLISTED = 32, FR_PARTIAL = 64, FR_NOT_OWNED = 128 };
 
 // 128-byte per-request raw feature record, written by feature_assemble. Field order follows
 // proto FeatureVector (risk.proto:197-235); int64 members are 8-byte aligned.
@@ -128,7 +128,9 @@ struct ScoreCfg {
   int32_t ip_mask;          // ip-intel table capacity - 1
   int32_t ip_max_probe;
   int32_t ext_width;        // feature-vector columns beyond the 30 reference ones
-  int32_t pad[5];
+  int32_t owner_filter;     // 1: rows whose owner (ReqRec.tx_type bits 8..15) != my_rank are skipped
+  int32_t my_rank;
+  int32_t pad[3];
 };
 static_assert(sizeof(ScoreCfg) == 176, "ScoreCfg must be 176 bytes");
 
@@ -136,7 +138,7 @@ static_assert(sizeof(ScoreCfg) == 176, "ScoreCfg must be 176 bytes");
 // contiguous slab [BatchHdr | ReqRec x n]: one H2D copy per micro-batch.
 struct ReqRec {
   int32_t slot;       // feature-store slot on this GPU (-1 = unknown account)
-  int32_t tx_type;    // TxType
+  int32_t tx_type;    // TxType in bits 0..7, owner rank in bits 8..15 (broadcast serving mode)
   int64_t amount;     // cents
   uint64_t dev_hash;  // XXH64 digests, 0 = absent
   uint64_t fp_hash;

@@ -209,4 +209,44 @@ PYBIND11_MODULE(_hipk, m) {
     launch_ltv(a, stream_of(s));
     check("ltv");
   });
+  m.def("gru", [](py::dict d, uintptr_t s) {
+    GruArgs a{};
+    a.n_layers = geti(d, "n_layers");
+    if (a.n_layers < 1 || a.n_layers > 2) throw std::runtime_error("gru: 1 or 2 layers");
+    for (int l = 0; l < a.n_layers; ++l) {
+      const std::string p = "l" + std::to_string(l) + "_";
+      a.layer[l].W = ptr<const uint16_t*>(d, (p + "W").c_str());
+      a.layer[l].R = ptr<const uint16_t*>(d, (p + "R").c_str());
+      a.layer[l].bias = ptr<const float*>(d, (p + "bias").c_str());
+      a.layer[l].kx_pad = geti(d, (p + "kx_pad").c_str());
+      a.layer[l].lbr = geti(d, (p + "lbr").c_str());
+      if (!a.layer[l].W || !a.layer[l].R || !a.layer[l].bias) throw std::runtime_error("gru: missing layer weights");
+    }
+    a.H = geti(d, "H");
+    a.T = geti(d, "T");
+    a.I = geti(d, "I");
+    a.mode = geti(d, "mode");
+    a.X = ptr<const float*>(d, "X");
+    a.x_rows = geti(d, "x_rows");
+    a.ev = ptr<const uint16_t*>(d, "ev");
+    a.rt = ptr<const AcctRT*>(d, "rt");
+    a.slots = ptr<const int32_t*>(d, "slots");
+    a.ev_ring = geti(d, "ev_ring");
+    a.m_ptr = ptr<const int32_t*>(d, "m_ptr");
+    a.n_rows = geti(d, "n_rows");
+    a.yh = ptr<float*>(d, "yh");
+    a.head_w = ptr<const float*>(d, "head_w");
+    a.head_b = d.contains("head_b") ? d["head_b"].cast<float>() : 0.f;
+    a.head_act = geti(d, "head_act");
+    a.out = ptr<float*>(d, "out");
+    if (a.H != 64 && a.H != 128 && a.H != 256) throw std::runtime_error("gru: H must be 64, 128 or 256");
+    if (a.layer[0].kx_pad != 32 && a.layer[0].kx_pad != 64) throw std::runtime_error("gru: input dim must pad to 32 or 64");
+    if (a.n_layers == 2 && a.layer[1].kx_pad != a.H) throw std::runtime_error("gru: layer 2 input must be H");
+    if (a.I % 8 != 0 || a.I > a.layer[0].kx_pad) throw std::runtime_error("gru: I must be a multiple of 8 <= kx_pad");
+    if (a.mode == 1 && (!a.ev || !a.rt || !a.slots || a.ev_ring < a.T)) throw std::runtime_error("gru: event-ring input");
+    if (a.mode == 0 && (!a.X || a.x_rows < a.n_rows)) throw std::runtime_error("gru: dense input");
+    if (a.head_w && !a.out) throw std::runtime_error("gru: head needs out");
+    launch_gru(a, stream_of(s));
+    check("gru");
+  });
 }

@@ -60,4 +60,9 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf
 // precise variant (matches the CPU executor to ~1 ulp)
 __device__ __forceinline__ float sigmoid_precise(float x) { return 1.f / (1.f + expf(-x)); }
 
+// request ownership (multi-GPU broadcast serving): the row belongs to this rank's shard
+__device__ __forceinline__ bool row_owned(const ReqRec& r, const ScoreCfg& c) {
+  return !c.owner_filter || ((r.tx_type >> 8) & 0xff) == c.my_rank;
+}
+
 }  // namespace igp

@@ -41,8 +41,8 @@ __global__ void __launch_bounds__(256) ensemble_kernel(EnsembleArgs a) {
   const int row = blockIdx.x * 256 + tid;
   const int n_live = a.hdr->n;
   if (row < a.n_rows) {
-    if (row >= n_live) {
-      a.out[row] = ResultRec{0u, 0.f};
+    if (row >= n_live || (a.feat[row].flags & FR_NOT_OWNED)) {
+      a.out[row] = ResultRec{0u, 0.f};  // padding / another rank's request: zero (merge by sum)
     } else {
       const ScoreCfg& cfg = *a.cfg;
       const FeatRec& f = a.feat[row];

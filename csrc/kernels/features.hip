@@ -40,9 +40,14 @@ __global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs a) {
     return;
   }
   const ReqRec rq = a.req[row];
+  if (!row_owned(rq, cfg)) {  // another rank's request: inert row, no dedup entry
+    for (int j = lane; j < 30 + ext_w; j += 64) xr[j] = 0.f;
+    if (lane < 32) reinterpret_cast<int32_t*>(a.feat + row)[lane] = (lane == 27) ? -1 : (lane == 3 ? FR_NOT_OWNED : 0);
+    return;
+  }
   const int s = rq.slot;
   const int64_t amount = rq.amount;
-  const int tx_type = rq.tx_type;
+  const int tx_type = rq.tx_type & 0xff;
 
   // ---- issue the account loads
   const int rs = a.ring_size;  // multiple of 64; 256 = one uint4 per lane
@@ -289,22 +294,22 @@ __global__ void dedup_reset_kernel(UpdateArgs a) {
 __global__ void dedup_insert_kernel(UpdateArgs a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= upd_n(a)) return;
-  const int s = a.req[i].slot;
-  if (s >= 0) dedup_insert(upd_region(a), s, i);
+  const ReqRec& r = a.req[i];
+  if (r.slot >= 0 && row_owned(r, *a.cfg)) dedup_insert(upd_region(a), r.slot, i);
 }
 
 __global__ void update_single_kernel(UpdateArgs a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= upd_n(a)) return;
-  const int s = a.req[i].slot;
-  if (s >= 0) update_first_event(a, upd_region(a), i, s);
+  const ReqRec& r = a.req[i];
+  if (r.slot >= 0 && row_owned(r, *a.cfg)) update_first_event(a, upd_region(a), i, r.slot);
 }
 
 __global__ void update_fill_kernel(UpdateArgs a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= upd_n(a)) return;
   const int s = a.req[i].slot;
-  if (s < 0) return;
+  if (s < 0 || !row_owned(a.req[i], *a.cfg)) return;
   const DedupTab t = upd_region(a);
   const int h = dedup_find(t, s);
   if (h < 0 || t.count[h] < 2) return;
@@ -429,7 +434,8 @@ __global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
   const int64_t prev = lane == 0 ? (int64_t)r.last_event_ts : up;
   if (a.ev && act) {
     const int pos = (r.ev_head + lane) % a.ev_ring;
-    write_event_row(a.ev + ((size_t)s * a.ev_ring + pos) * a.ev_dim, amt, ev.tx_type, ts, prev, new_dev, new_ip);
+    write_event_row(a.ev + ((size_t)s * a.ev_ring + pos) * a.ev_dim, amt, ev.tx_type & 0xff, ts, prev, new_dev,
+                    new_ip);
   }
   if (a.ev) {
     r.ev_head = (r.ev_head + c) % a.ev_ring;

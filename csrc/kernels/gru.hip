@@ -1,0 +1,376 @@
+// K4: stacked ONNX GRU (1-2 layers, forward, layout 0) over a per-account event history,
+// with the N=1 head (Gemm + Sigmoid) fused — the CheckBonusAbuse model of config 5.
+//
+// Batch-parallel recurrence: a workgroup owns M = 16*RT sequences and runs ALL T steps of
+// BOTH layers for them, so no grid-wide synchronisation is ever needed (every wave's exit is
+// unconditional). Per step and layer:
+//   gates[M, 3H] = x_t[M, K] . W^T  +  h_{t-1}[M, H] . R^T        (MFMA 16x16x32 bf16)
+// Weights stream from L2 as fragment-packed 1 KiB wave loads (shared by the RT row tiles);
+// x_t / h_{t-1} A-fragments come from LDS (bf16, ping-pong buffers per layer); the f32
+// hidden state never leaves registers: lane (l&15, l>>4) of the wave that owns hidden tile
+// ht computes the same (row, unit) every step, so z/r/h~ combine lane-locally.
+// Layer 2 consumes layer 1's h_t straight from LDS (Y never touches HBM). The layer-1 input
+// of step t+1 is prefetched into registers during step t (from the HBM event ring, mode 1,
+// or a dense [T][B][I] tensor, mode 0).
+#include "common.h"
+#include "launch.h"
+
+namespace igp {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+namespace {
+
+constexpr int GRU_PAD = 8;  // bf16 row padding in LDS (16 B)
+
+__device__ __forceinline__ float sig_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_(float x) { return 1.f - 2.f / (__expf(2.f * x) + 1.f); }
+
+__device__ __forceinline__ bf16x8 ld_frag(const uint16_t* P, int nt, int KS, int ks, int lane) {
+  const uint4 v = *reinterpret_cast<const uint4*>(P + ((((size_t)nt * KS + ks) * 64 + lane) << 3));
+  return *reinterpret_cast<const bf16x8*>(&v);
+}
+
+__device__ __forceinline__ bf16x8 lds_frag(const uint16_t* base, int stride, int row, int k) {
+  const uint4 v = *reinterpret_cast<const uint4*>(base + row * stride + k);
+  return *reinterpret_cast<const bf16x8*>(&v);
+}
+
+
+// One GRU layer step for this wave's hidden tiles. KSX/KSH: K/32 of the input / hidden parts.
+template <int RT, int KSX, int KSH, int LBR>
+__device__ __forceinline__ void layer_step(const GruLayerArgs& g, const float* bias, const uint16_t* in,
+                                           int in_stride, const uint16_t* hprev, uint16_t* hnext,
+                                           uint16_t* rb, float (&hs)[KSH / 2][RT][4], int lane, int wave) {
+  constexpr int HT = KSH * 2;      // hidden tiles of 16 units
+  constexpr int HTW = KSH / 2;     // per wave (4 waves)
+  constexpr int H = KSH * 32;
+  constexpr int HS = H + GRU_PAD;
+  const int arow = lane & 15, akof = 8 * (lane >> 4);
+  const int crow = (lane >> 4) * 4, ccol = lane & 15;
+  if constexpr (LBR != 0) {
+#pragma unroll
+    for (int i = 0; i < HTW; ++i) {
+      const int ht = wave + 4 * i;
+      f32x4 az[RT], ar[RT], ax[RT], ah[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) az[rt] = ar[rt] = ax[rt] = ah[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+      for (int ks = 0; ks < KSX; ++ks) {
+        const bf16x8 bz = ld_frag(g.W, ht, KSX, ks, lane);
+        const bf16x8 br = ld_frag(g.W, HT + ht, KSX, ks, lane);
+        const bf16x8 bh = ld_frag(g.W, 2 * HT + ht, KSX, ks, lane);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const bf16x8 a = lds_frag(in, in_stride, rt * 16 + arow, ks * 32 + akof);
+          az[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bz, az[rt], 0, 0, 0);
+          ar[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, br, ar[rt], 0, 0, 0);
+          ax[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, ax[rt], 0, 0, 0);
+        }
+      }
+#pragma unroll 2
+      for (int ks = 0; ks < KSH; ++ks) {
+        const bf16x8 bz = ld_frag(g.R, ht, KSH, ks, lane);
+        const bf16x8 br = ld_frag(g.R, HT + ht, KSH, ks, lane);
+        const bf16x8 bh = ld_frag(g.R, 2 * HT + ht, KSH, ks, lane);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const bf16x8 a = lds_frag(hprev, HS, rt * 16 + arow, ks * 32 + akof);
+          az[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bz, az[rt], 0, 0, 0);
+          ar[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, br, ar[rt], 0, 0, 0);
+          ah[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, ah[rt], 0, 0, 0);
+        }
+      }
+      const int j = ht * 16 + ccol;
+      const float bz_ = bias[j] + bias[3 * H + j];
+      const float br_ = bias[H + j] + bias[4 * H + j];
+      const float bxh = bias[2 * H + j], bhh = bias[5 * H + j];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float z = sig_(az[rt][r] + bz_);
+          const float rr = sig_(ar[rt][r] + br_);
+          const float hh = tanh_(ax[rt][r] + bxh + rr * (ah[rt][r] + bhh));
+          const float h = (1.f - z) * hh + z * hs[i][rt][r];
+          hs[i][rt][r] = h;
+          hnext[(rt * 16 + crow + r) * HS + j] = f32_to_bf16(h);
+        }
+    }
+  } else {
+    // linear_before_reset = 0: h~ = tanh(x Wh + (r * h_{t-1}) Rh + b) needs r for every unit
+    // of the row first -> phase A (z, r; r*h to LDS), block barrier, phase B (h gate).
+    float zk[HTW][RT][4];
+    f32x4 axk[HTW][RT];
+#pragma unroll
+    for (int i = 0; i < HTW; ++i) {
+      const int ht = wave + 4 * i;
+      f32x4 az[RT], ar[RT], ax[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) az[rt] = ar[rt] = ax[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+      for (int ks = 0; ks < KSX; ++ks) {
+        const bf16x8 bz = ld_frag(g.W, ht, KSX, ks, lane);
+        const bf16x8 br = ld_frag(g.W, HT + ht, KSX, ks, lane);
+        const bf16x8 bh = ld_frag(g.W, 2 * HT + ht, KSX, ks, lane);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const bf16x8 a = lds_frag(in, in_stride, rt * 16 + arow, ks * 32 + akof);
+          az[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bz, az[rt], 0, 0, 0);
+          ar[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, br, ar[rt], 0, 0, 0);
+          ax[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, ax[rt], 0, 0, 0);
+        }
+      }
+#pragma unroll 2
+      for (int ks = 0; ks < KSH; ++ks) {
+        const bf16x8 bz = ld_frag(g.R, ht, KSH, ks, lane);
+        const bf16x8 br = ld_frag(g.R, HT + ht, KSH, ks, lane);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const bf16x8 a = lds_frag(hprev, HS, rt * 16 + arow, ks * 32 + akof);
+          az[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bz, az[rt], 0, 0, 0);
+          ar[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, br, ar[rt], 0, 0, 0);
+        }
+      }
+      const int j = ht * 16 + ccol;
+      const float bz_ = bias[j] + bias[3 * H + j];
+      const float br_ = bias[H + j] + bias[4 * H + j];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        axk[i][rt] = ax[rt];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          zk[i][rt][r] = sig_(az[rt][r] + bz_);
+          const float rr = sig_(ar[rt][r] + br_);
+          rb[(rt * 16 + crow + r) * HS + j] = f32_to_bf16(rr * hs[i][rt][r]);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < HTW; ++i) {
+      const int ht = wave + 4 * i;
+      f32x4 ah[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) ah[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+      for (int ks = 0; ks < KSH; ++ks) {
+        const bf16x8 bh = ld_frag(g.R, 2 * HT + ht, KSH, ks, lane);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const bf16x8 a = lds_frag(rb, HS, rt * 16 + arow, ks * 32 + akof);
+          ah[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, ah[rt], 0, 0, 0);
+        }
+      }
+      const int j = ht * 16 + ccol;
+      const float bxh = bias[2 * H + j], bhh = bias[5 * H + j];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float hh = tanh_(axk[i][rt][r] + bxh + ah[rt][r] + bhh);
+          const float z = zk[i][rt][r];
+          const float h = (1.f - z) * hh + z * hs[i][rt][r];
+          hs[i][rt][r] = h;
+          hnext[(rt * 16 + crow + r) * HS + j] = f32_to_bf16(h);
+        }
+    }
+  }
+}
+
+}  // namespace
+
+template <int RT, int KSH>
+__device__ __forceinline__ void emit_outputs(const GruArgs& a, float (&hs)[KSH / 2][RT][4], float* red, int row0,
+                                             int n_live, int lane, int wave, int tid) {
+  constexpr int M = RT * 16, H = KSH * 32, HTW = KSH / 2;
+  const int crow = (lane >> 4) * 4, ccol = lane & 15;
+  if (a.yh) {
+#pragma unroll
+    for (int i = 0; i < HTW; ++i)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = row0 + rt * 16 + crow + r;
+          if (row < n_live) a.yh[(size_t)row * H + (wave + 4 * i) * 16 + ccol] = hs[i][rt][r];
+        }
+  }
+  if (a.head_w) {
+    float part[RT][4];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[rt][r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < HTW; ++i) {
+      const float w = a.head_w[(wave + 4 * i) * 16 + ccol];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part[rt][r] += hs[i][rt][r] * w;
+    }
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = part[rt][r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+        if (ccol == 0) red[wave * M + rt * 16 + crow + r] = v;
+      }
+    __syncthreads();
+    if (tid < M && row0 + tid < n_live) {
+      float v = red[tid] + red[M + tid] + red[2 * M + tid] + red[3 * M + tid] + a.head_b;
+      if (a.head_act == 2) v = 1.f / (1.f + expf(-v));
+      a.out[row0 + tid] = v;
+    }
+  }
+}
+
+template <int RT, int KSX, int KSH, int LBR>
+__global__ void __launch_bounds__(256) gru_kernel(GruArgs a) {
+  constexpr int M = RT * 16;
+  constexpr int H = KSH * 32;
+  constexpr int HS = H + GRU_PAD;
+  constexpr int XS = KSX * 32 + GRU_PAD;
+  constexpr int HTW = KSH / 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n_live = a.m_ptr ? min(*a.m_ptr, a.n_rows) : a.n_rows;
+  const int row0 = blockIdx.x * M;
+  if (row0 >= n_live) return;
+
+  // ---- LDS carve-up: hb[layer][pingpong][M][HS] | xb[pingpong][M][XS] | rb[M][HS] | bias[2][6H] | red[4][M]
+  uint16_t* const hb = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* const xb = hb + 4 * M * HS;
+  uint16_t* const rb = xb + 2 * M * XS;
+  float* const bias = reinterpret_cast<float*>(rb + M * HS);
+  float* const red = bias + 12 * H;
+#define HB(l, b) (hb + ((l) * 2 + (b)) * (M * HS))
+#define XB(b) (xb + (b) * (M * XS))
+
+  // zero h_0 (both layers, both buffers) and the x buffers (their K padding stays zero)
+  {
+    uint32_t* z = reinterpret_cast<uint32_t*>(smem);
+    const int words = (4 * M * HS + 2 * M * XS) / 2;
+    for (int i = tid; i < words; i += 256) z[i] = 0u;
+  }
+  for (int i = tid; i < 6 * H; i += 256) bias[i] = a.layer[0].bias[i];
+  if (a.n_layers == 2)
+    for (int i = tid; i < 6 * H; i += 256) bias[6 * H + i] = a.layer[1].bias[i];
+
+  // ---- layer-1 input staging: thread -> (row rr, 8-element chunk c), fixed for all t
+  const int I = a.I;
+  const int chunks = I >> 3;
+  const int my_rr = tid / max(chunks, 1), my_c = tid - my_rr * max(chunks, 1);
+  const bool stager = chunks > 0 && my_rr < M;
+  const int grow = row0 + my_rr;
+  int slot = -1, head = 0, valid_from = a.T;
+  if (stager && grow < n_live) {
+    if (a.mode == 1) {
+      slot = a.slots[grow];
+      if (slot >= 0) {
+        const AcctRT r = a.rt[slot];
+        const int cnt = min(r.ev_count, a.T);
+        head = r.ev_head;
+        valid_from = a.T - cnt;
+      }
+    } else {
+      valid_from = 0;
+    }
+  }
+  auto load_x = [&](int t) -> uint4 {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (!stager || t < valid_from) return v;
+    if (a.mode == 1) {
+      int idx = (head - a.T + t) % a.ev_ring;
+      if (idx < 0) idx += a.ev_ring;
+      v = *reinterpret_cast<const uint4*>(a.ev + (((size_t)slot * a.ev_ring + idx) * I + my_c * 8));
+    } else {
+      const float* src = a.X + (((size_t)t * a.x_rows + grow) * I + my_c * 8);
+      const float4 f0 = *reinterpret_cast<const float4*>(src);
+      const float4 f1 = *reinterpret_cast<const float4*>(src + 4);
+      v.x = (uint32_t)f32_to_bf16(f0.x) | ((uint32_t)f32_to_bf16(f0.y) << 16);
+      v.y = (uint32_t)f32_to_bf16(f0.z) | ((uint32_t)f32_to_bf16(f0.w) << 16);
+      v.z = (uint32_t)f32_to_bf16(f1.x) | ((uint32_t)f32_to_bf16(f1.y) << 16);
+      v.w = (uint32_t)f32_to_bf16(f1.z) | ((uint32_t)f32_to_bf16(f1.w) << 16);
+    }
+    return v;
+  };
+  __syncthreads();  // zeroing done before the first staged row lands
+  if (stager) *reinterpret_cast<uint4*>(XB(0) + my_rr * XS + my_c * 8) = load_x(0);
+
+  float hs0[HTW][RT][4], hs1[HTW][RT][4];
+#pragma unroll
+  for (int i = 0; i < HTW; ++i)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hs0[i][rt][r] = hs1[i][rt][r] = 0.f;
+  __syncthreads();
+
+  for (int t = 0; t < a.T; ++t) {
+    const int pb = t & 1, nb = pb ^ 1;
+    const uint4 xn = (t + 1 < a.T) ? load_x(t + 1) : make_uint4(0, 0, 0, 0);
+    layer_step<RT, KSX, KSH, LBR>(a.layer[0], bias, XB(pb), XS, HB(0, pb), HB(0, nb), rb, hs0, lane, wave);
+    __syncthreads();
+    if (a.n_layers == 2) {
+      layer_step<RT, KSH, KSH, LBR>(a.layer[1], bias + 6 * H, HB(0, nb), HS, HB(1, pb), HB(1, nb), rb, hs1, lane,
+                                    wave);
+    }
+    if (stager && t + 1 < a.T) *reinterpret_cast<uint4*>(XB(nb) + my_rr * XS + my_c * 8) = xn;
+    __syncthreads();
+  }
+
+  // ---- outputs from the last layer's registers (static register indexing in both branches)
+  if (a.n_layers == 2)
+    emit_outputs<RT, KSH>(a, hs1, red, row0, n_live, lane, wave, tid);
+  else
+    emit_outputs<RT, KSH>(a, hs0, red, row0, n_live, lane, wave, tid);
+#undef HB
+#undef XB
+}
+
+static size_t gru_lds_bytes(int RT, int KSX, int KSH) {
+  const int M = RT * 16, H = KSH * 32, HS = H + GRU_PAD, XS = KSX * 32 + GRU_PAD;
+  return (size_t)4 * M * HS * 2 + (size_t)2 * M * XS * 2 + (size_t)M * HS * 2 + (size_t)2 * 6 * H * 4 +
+         (size_t)4 * M * 4;
+}
+
+template <int RT, int KSX, int KSH>
+static void launch_gru_t(const GruArgs& a, hipStream_t st) {
+  const int M = RT * 16;
+  if (a.layer[0].lbr)
+    hipLaunchKernelGGL((gru_kernel<RT, KSX, KSH, 1>), dim3((a.n_rows + M - 1) / M), dim3(256),
+                       gru_lds_bytes(RT, KSX, KSH), st, a);
+  else
+    hipLaunchKernelGGL((gru_kernel<RT, KSX, KSH, 0>), dim3((a.n_rows + M - 1) / M), dim3(256),
+                       gru_lds_bytes(RT, KSX, KSH), st, a);
+}
+
+template <int RT, int KSX>
+static void launch_gru_h(const GruArgs& a, hipStream_t st) {
+  switch (a.H) {
+    case 64: launch_gru_t<RT, KSX, 2>(a, st); break;
+    case 128: launch_gru_t<RT, KSX, 4>(a, st); break;
+    case 256: launch_gru_t<RT, KSX, 8>(a, st); break;
+    default: break;
+  }
+}
+
+void launch_gru(const GruArgs& a, hipStream_t st) {
+  if (a.n_rows <= 0) return;
+  // rows per workgroup: 32 amortises each streamed weight fragment over two MFMA row tiles;
+  // drop to 16 when that would leave most of the 256 CUs idle.
+  const bool rt2 = a.n_rows >= 32 * 192;
+  const int ksx = a.layer[0].kx_pad / 32;
+  if (rt2) {
+    if (ksx == 1) launch_gru_h<2, 1>(a, st); else launch_gru_h<2, 2>(a, st);
+  } else {
+    if (ksx == 1) launch_gru_h<1, 1>(a, st); else launch_gru_h<1, 2>(a, st);
+  }
+}
+
+}  // namespace igp

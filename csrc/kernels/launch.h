@@ -138,28 +138,36 @@ struct EnsembleArgs {
 void launch_ensemble(const EnsembleArgs& a, hipStream_t st);
 
 // ---- K4 GRU sequence (recurrent weights resident in VGPRs)
+// ---- K4 GRU (1-2 stacked ONNX GRU layers, forward, layout 0) + optional N=1 head
+// Weights are fragment-packed on the host: P[nt][ks][lane][8] = W[nt*16 + (lane&15)]
+// [ks*32 + 8*(lane>>4) + j], so one wave load of a B fragment is 1 KiB contiguous.
+struct GruLayerArgs {
+  const uint16_t* W;        // packed bf16, N = 3H rows, K = kx_pad (input dim padded to 32)
+  const uint16_t* R;        // packed bf16, N = 3H rows, K = H
+  const float* bias;        // [6H]: Wb z,r,h | Rb z,r,h
+  int32_t kx_pad;
+  int32_t lbr;              // linear_before_reset
+};
 struct GruArgs {
-  const uint16_t* X;        // bf16 [T][B][I] (I <= 32) when G == nullptr
-  const float* G;           // precomputed input projection f32 [T][B][3H] (nullable)
-  const uint16_t* Wf;       // bf16 input weights fragments [3H][32] (used when G == nullptr)
-  const uint16_t* R;        // bf16 [3H][H]
-  const float* bias;        // [6H] (Wb z,r,h | Rb z,r,h)
-  uint16_t* Y;              // bf16 [T][B][H] (nullable)
-  float* Yh;                // f32 [B][H] (nullable)
-  int32_t T, B, I, H;
-  int32_t linear_before_reset;
+  GruLayerArgs layer[2];
+  int32_t n_layers, H, T, I;
+  // input: mode 0 dense X f32 [T][x_rows][I]; mode 1 per-account event ring (bf16 [C][ring][I])
+  int32_t mode;
+  const float* X;
+  int32_t x_rows;
+  const uint16_t* ev;
+  const AcctRT* rt;
+  const int32_t* slots;     // [rows] (-1 -> empty history)
+  int32_t ev_ring;
+  const int32_t* m_ptr;     // live row count on device (nullable)
+  int32_t n_rows;
+  float* yh;                // [rows][H] last layer's final hidden state (nullable)
+  const float* head_w;      // [H] (nullable): out[r] = act(h . w + b)
+  float head_b;
+  int32_t head_act;         // 0 none, 2 sigmoid
+  float* out;               // [rows]
 };
 void launch_gru(const GruArgs& a, hipStream_t st);
-
-// ---- event history gather for the GRU: ring -> [T][B][dim] bf16, oldest first
-struct EventGatherArgs {
-  const uint16_t* ev;       // [C][ring][dim]
-  const AcctRT* rt;
-  const int32_t* slot;      // [B]
-  uint16_t* out;            // [T][B][dim_pad]
-  int32_t B, ring, dim, dim_pad;
-};
-void launch_event_gather(const EventGatherArgs& a, hipStream_t st);
 
 // ---- K9 LTV / churn / segment
 struct LtvArgs {

@@ -144,7 +144,7 @@ __device__ __forceinline__ void apply_event(const UpdateArgs& a, int j, AcctRT& 
   if (now >= (int64_t)r.session_exp || r.session_start == 0) r.session_start = (uint32_t)now;
   r.session_exp = (uint32_t)(now + cfg.session_ttl);
   if (a.ev) {
-    write_event_row(a.ev + ((size_t)s * a.ev_ring + r.ev_head) * a.ev_dim, amt, ev.tx_type, now,
+    write_event_row(a.ev + ((size_t)s * a.ev_ring + r.ev_head) * a.ev_dim, amt, ev.tx_type & 0xff, now,
                     (int64_t)r.last_event_ts, new_dev, new_ip);
     r.ev_head = r.ev_head + 1 == a.ev_ring ? 0 : r.ev_head + 1;
     r.ev_count = r.ev_count + 1 > a.ev_ring ? a.ev_ring : r.ev_count + 1;

@@ -177,6 +177,46 @@ PYBIND11_MODULE(_native, m) {
         PYBIND11_BYTES_AS_STRING_AND_SIZE(data.ptr(), &p, &n);
         wire::parse_tx(p, size_t(n), b);
       })
+      .def("parse_tx_list", [](wire::RequestBatch& b, py::list items) {
+        // micro-batcher path: many unary ScoreTransactionRequest payloads -> one columnar batch
+        std::vector<std::pair<const char*, size_t>> bufs;
+        bufs.reserve(items.size());
+        for (auto it : items) {
+          char* p; py::ssize_t n;
+          if (PYBIND11_BYTES_AS_STRING_AND_SIZE(it.ptr(), &p, &n) != 0) throw std::runtime_error("parse_tx_list: bytes expected");
+          bufs.emplace_back(p, size_t(n));
+        }
+        py::gil_scoped_release rel;
+        b.reserve(b.size() + bufs.size());
+        for (auto& x : bufs) wire::parse_tx(x.first, x.second, b);
+      })
+      .def("pack_reqrec", [](const wire::RequestBatch& b, py::array_t<int32_t, py::array::c_style> slots,
+                             py::array out, int64_t ts, py::object owners) {
+        // fill REQREC rows (48 B: slot, tx_type | owner<<8, amount, dev, fp, ip, ts) in place
+        const size_t n = b.size();
+        if (size_t(slots.size()) != n) throw std::runtime_error("pack_reqrec: slots length");
+        if (size_t(out.nbytes()) < n * sizeof(ReqRec)) throw std::runtime_error("pack_reqrec: output too small");
+        if (!(out.flags() & py::array::c_style)) throw std::runtime_error("pack_reqrec: output must be contiguous");
+        const int32_t* own = nullptr;
+        py::array_t<int32_t, py::array::c_style | py::array::forcecast> own_arr;
+        if (!owners.is_none()) {
+          own_arr = owners;
+          if (size_t(own_arr.size()) != n) throw std::runtime_error("pack_reqrec: owners length");
+          own = own_arr.data();
+        }
+        ReqRec* o = reinterpret_cast<ReqRec*>(out.mutable_data());
+        const int32_t* sl = slots.data();
+        py::gil_scoped_release rel;
+        for (size_t k = 0; k < n; ++k) {
+          o[k].slot = sl[k];
+          o[k].tx_type = int32_t(b.tx_type[k]) | (own ? (own[k] << 8) : 0);
+          o[k].amount = b.amount[k];
+          o[k].dev_hash = b.device_hash[k];
+          o[k].fp_hash = b.fp_hash[k];
+          o[k].ip_hash = b.ip_hash[k];
+          o[k].ts = ts;
+        }
+      }, py::arg("slots"), py::arg("out"), py::arg("ts"), py::arg("owners") = py::none())
       .def("clear", &wire::RequestBatch::clear)
       .def("__len__", &wire::RequestBatch::size)
       .def_readonly("account_id", &wire::RequestBatch::account_id)
@@ -253,6 +293,19 @@ PYBIND11_MODULE(_native, m) {
     if (i >= v.n) throw std::runtime_error("index out of range");
     return py::bytes(wire::serialize_tx_response(v, i));
   }, py::arg("results"), py::arg("features") = py::none(), py::arg("response_ms") = py::none(), py::arg("index") = 0);
+  m.def("serialize_tx_responses", [view](py::array res, py::object feat, py::object ms) {
+    wire::ResultView v;
+    py::array kr; py::object kf, km;
+    view(res, feat, ms, v, kr, kf, km);
+    std::vector<std::string> outs(v.n);
+    {
+      py::gil_scoped_release rel;
+      for (size_t i = 0; i < v.n; ++i) outs[i] = wire::serialize_tx_response(v, i);
+    }
+    py::list l;
+    for (auto& o : outs) l.append(py::bytes(o));
+    return l;
+  }, py::arg("results"), py::arg("features") = py::none(), py::arg("response_ms") = py::none());
   m.def("serialize_feature_vector", [](py::array feat) {
     auto f = py::array_t<int32_t, py::array::c_style | py::array::forcecast>(feat);
     if (f.size() != 32) throw std::runtime_error("FeatRec must have 32 int32 words");

@@ -1,0 +1,300 @@
+"""Scoring backends behind the RiskEngine facade.
+
+Both take REQREC rows (slot already resolved by the registry) and return the same thing —
+``(res, feats)``: ResultRec ``uint32[n,2]`` (what the C++ wire serializer consumes) and
+optionally FeatRec rows — so the API layer, clients and tests are backend-agnostic:
+
+* :class:`CpuBackend` — the golden semantics (``golden/``) with ONNX models run by the C++
+  CPU executor (``csrc/runtime/executor.cpp``). This is config 1 (BASELINE.json: unary
+  ScoreTransaction on CPU, heuristic model, batch 1) and the fallback when no GPU is present.
+* :class:`GpuBackend` — one MI355X shard: HBM feature store + captured-graph scorer.
+
+Reference: services/risk/internal/scoring/engine.go:152-303 (Score), 486-488 (score-then-update).
+"""
+from __future__ import annotations
+
+import threading
+import time
+from typing import Optional, Tuple
+
+import numpy as np
+
+from ..config import Config, REASON_BIT
+from ..golden import scoring as GS
+from ..golden.features import BatchFeatures, GoldenFeatureStore, TxEvent, model_input
+from ..layouts import (ACCTBATCH, FEATREC, FR_BLACKLISTED, FR_BONUS_ONLY, FR_PARTIAL, FR_PROXY, FR_TOR,
+                       FR_VPN, REQREC, pack_results)
+from ..features.tables import Blacklist, IPIntel
+
+Result = Tuple[np.ndarray, Optional[np.ndarray]]
+
+
+def _featrec_from_golden(f, row, bl: bool, rule: int, reasons) -> np.ndarray:
+    r = np.zeros(1, FEATREC)[0]
+    for k in FEATREC.names:
+        if k in f and not isinstance(f[k], bool):
+            r[k] = f[k]
+    flags = (FR_VPN if f["is_vpn"] else 0) | (FR_PROXY if f["is_proxy"] else 0) | (FR_TOR if f["is_tor"] else 0)
+    flags |= (FR_BONUS_ONLY if f["bonus_only_player"] else 0) | (FR_BLACKLISTED if bl else 0)
+    flags |= FR_PARTIAL if f.get("_partial") else 0
+    r["flags"] = flags
+    r["tx_type"] = int(row["tx_type"]) & 0xFF
+    r["slot"] = int(row["slot"])
+    r["amount"] = int(row["amount"])
+    r["rule_score"] = rule
+    r["rule_reasons"] = sum(1 << REASON_BIT[x] for x in reasons)
+    return r
+
+
+class CpuBackend:
+    """Golden-semantics scorer on the host; the feature store is keyed by slot."""
+
+    kind = "cpu"
+
+    def __init__(self, cfg: Config, model: str = "heuristic", executor=None, input_name: str = "input",
+                 output_name: str = "output", ml_col: int = 0,
+                 blacklist: Optional[Blacklist] = None, ipintel: Optional[IPIntel] = None):
+        if model == "plan" and executor is None:
+            model = "none"
+        self.cfg = cfg
+        self.model = model
+        self.executor, self.input_name, self.output_name, self.ml_col = executor, input_name, output_name, ml_col
+        self.store = GoldenFeatureStore(cfg.features)
+        self.blacklist = blacklist or Blacklist()
+        self.ipintel = ipintel or IPIntel()
+        self.scoring = cfg.scoring
+        self._lock = threading.RLock()
+        self._tables_version = None
+        self.refresh_config()
+
+    # ------------------------------------------------------------------ state
+    def _sync_tables(self) -> None:
+        v = (self.blacklist.table.version, self.ipintel.table.version)
+        if v == self._tables_version:
+            return
+        self.store.blacklist = dict(self.blacklist.active_keys(0))
+        t = self.ipintel.table
+        self.store.ip_intel = {int(k): int(x) for k, x in zip(t.keys.view(np.uint64), t.vals) if int(k) != 0}
+        self._tables_version = v
+
+    def refresh_config(self, scoring=None) -> None:
+        with self._lock:
+            if scoring is not None:
+                self.scoring = scoring
+            self._sync_tables()
+
+    def set_batch_rows(self, slots, rows) -> None:
+        with self._lock:
+            for s, b in zip(slots, np.asarray(rows, ACCTBATCH)):
+                if not b["present"]:
+                    self.store.set_batch(str(int(s)), None)
+                    continue
+                self.store.set_batch(str(int(s)), BatchFeatures(
+                    total_deposits=int(b["total_deposits"]), total_withdrawals=int(b["total_withdrawals"]),
+                    deposit_count=int(b["deposit_count"]), withdraw_count=int(b["withdraw_count"]),
+                    total_bets=int(b["total_bets"]), total_wins=int(b["total_wins"]),
+                    bet_count=int(b["bet_count"]), win_count=int(b["win_count"]),
+                    avg_bet_size=float(b["avg_bet_size"]), account_created_at=int(b["account_created_at"]),
+                    bonus_claim_count=int(b["bonus_claim_count"]),
+                    bonus_wager_complete=float(b["bonus_wager_complete"])))
+
+    def set_ext(self, slots, ext) -> None:
+        with self._lock:
+            for s, e in zip(slots, ext):
+                self.store.set_ext(str(int(s)), e)
+
+    def reset_accounts(self, slots) -> None:
+        with self._lock:
+            for s in slots:
+                self.store.accounts.pop(str(int(s)), None)
+
+    def ingest(self, events: np.ndarray) -> None:
+        with self._lock:
+            for row in events:
+                s = int(row["slot"])
+                if s >= 0:
+                    self.store.apply(TxEvent(str(s), int(row["amount"]), int(row["tx_type"]) & 0xFF,
+                                             int(row["dev_hash"]), int(row["ip_hash"]), int(row["ts"])))
+
+    # ------------------------------------------------------------------ scoring
+    def _features(self, row, now: int):
+        s = int(row["slot"])
+        key = str(s) if s >= 0 else "__unknown__"
+        f = self.store.raw_features(key, now, ip_hash=int(row["ip_hash"]))
+        if s < 0:
+            f["_partial"] = True
+        bl = self.store.blacklisted([int(row["dev_hash"]), int(row["fp_hash"]), int(row["ip_hash"])], now)
+        amount, tx = int(row["amount"]), int(row["tx_type"]) & 0xFF
+        rule, reasons = GS.apply_rules(self.scoring, f, amount, tx, bl)
+        st = self.store.accounts.get(key) if s >= 0 else None
+        x = model_input(f, amount, tx, self.cfg.features.log_transform, self.cfg.features.width,
+                        st.ext if st is not None else None)
+        return f, bl, rule, reasons, x
+
+    def _ml(self, X: np.ndarray):
+        n = len(X)
+        if self.model == "none" or n == 0:
+            return [None] * n
+        if self.model == "heuristic":
+            return [GS.heuristic_predict(x) for x in X]
+        try:
+            y = self.executor.run({self.input_name: np.ascontiguousarray(X, np.float32)})
+            yv = y[self.output_name] if self.output_name in y else list(y.values())[-1]
+            yv = np.asarray(yv, np.float32).reshape(n, -1)[:, self.ml_col]
+        except Exception:  # model error -> neutral score (engine.go:279-282)
+            return [self.scoring.ml_error_score] * n
+        return [self.scoring.ml_error_score if not np.isfinite(v) else GS.clamp01_f32(v) for v in yv]
+
+    def score(self, req: np.ndarray, now: Optional[int] = None, want_features: bool = True,
+              update: bool = True) -> Result:
+        now = int(time.time()) if now is None else int(now)
+        n = len(req)
+        sc = np.zeros(n, np.int32); rs = np.zeros(n, np.int32); act = np.zeros(n, np.int32)
+        rmask = np.zeros(n, np.int32); mlv = np.zeros(n, np.float32)
+        feats = np.zeros(n, FEATREC)
+        with self._lock:
+            self._sync_tables()
+            rows = [self._features(r, now) for r in req]
+            ml = self._ml(np.stack([r[4] for r in rows]) if n else np.zeros((0, self.cfg.features.width)))
+            for i, (f, bl, rule, reasons, _) in enumerate(rows):
+                score, action, rr, m = GS.ensemble(self.scoring, rule, reasons, ml[i])
+                sc[i], act[i], rs[i], mlv[i] = score, action, rule, m
+                rmask[i] = sum(1 << REASON_BIT[r] for r in rr)
+                if want_features:
+                    feats[i] = _featrec_from_golden(f, req[i], bl, rule, reasons)
+            if update:  # score-then-update, in request order (engine.go:486-488)
+                for row in req:
+                    s = int(row["slot"])
+                    if s >= 0:
+                        self.store.apply(TxEvent(str(s), int(row["amount"]), int(row["tx_type"]) & 0xFF,
+                                                 int(row["dev_hash"]), int(row["ip_hash"]), now))
+        res = pack_results(sc, rs, act, rmask, mlv, np.full(n, self.model != "none"))
+        return res, (feats if want_features else None)
+
+    def features(self, slot: int, now: int) -> np.ndarray:
+        r = np.zeros(1, REQREC)
+        r["slot"], r["tx_type"] = slot, 255
+        with self._lock:
+            self._sync_tables()
+            f, bl, rule, reasons, _ = self._features(r[0], now)
+        return _featrec_from_golden(f, r[0], bl, rule, reasons)
+
+    def event_history(self, slot: int) -> np.ndarray:
+        with self._lock:
+            return self.store.event_history(str(slot))
+
+    def metrics(self) -> Optional[np.ndarray]:
+        return None
+
+
+class GpuBackend:
+    """One GPU shard: HBM feature store + captured-graph scorer."""
+
+    kind = "gpu"
+
+    def __init__(self, cfg: Config, capacity: int, device, plan=None, model: str = "plan",
+                 blacklist: Optional[Blacklist] = None, ipintel: Optional[IPIntel] = None,
+                 capture: bool = True, owner_filter: bool = False, rank: int = 0):
+        import torch
+        from .scorer import GpuScorer
+        from ..features.device_store import DeviceFeatureStore
+        self.torch = torch
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.store = DeviceFeatureStore(capacity, cfg.features, self.device, events=True,
+                                        blacklist=blacklist, ipintel=ipintel, max_events=max(cfg.gpu.buckets))
+        self.blacklist, self.ipintel = self.store.blacklist, self.store.ipintel
+        self.scorer = GpuScorer(cfg, self.store, plan=plan, model=model, device=self.device,
+                                owner_filter=owner_filter, rank=rank)
+        if capture and self.scorer.use_graphs:
+            self.scorer.capture()
+        self._lock = threading.RLock()
+        self._fx = None
+
+    def refresh_config(self, scoring=None) -> None:
+        with self._lock:
+            with self.torch.cuda.stream(self.scorer.stream):
+                self.scorer.refresh_config(scoring)
+            self.scorer.stream.synchronize()
+
+    def set_batch_rows(self, slots, rows) -> None:
+        with self._lock:
+            self.store.set_batch_features(np.asarray(slots), rows)
+            self.torch.cuda.synchronize(self.device)
+
+    def set_ext(self, slots, ext) -> None:
+        with self._lock:
+            self.store.set_ext(np.asarray(slots), ext)
+            self.torch.cuda.synchronize(self.device)
+
+    def reset_accounts(self, slots) -> None:
+        with self._lock:
+            self.store.reset_accounts(slots)
+            self.torch.cuda.synchronize(self.device)
+
+    def ingest(self, events: np.ndarray) -> None:
+        """IngestEvents: ordered feature update without scoring (standalone dedup region)."""
+        from ..ops import kernels as K
+        torch = self.torch
+        with self._lock:
+            for i in range(0, len(events), self.store.dmax):
+                chunk = np.ascontiguousarray(events[i:i + self.store.dmax], REQREC)
+                t = torch.from_numpy(chunk.view(np.uint8).copy()).to(self.device)
+                with torch.cuda.stream(self.scorer.stream):
+                    K.feature_update(self.store, self.scorer.cfg_dev, t, len(chunk), n=len(chunk))
+                self.scorer.stream.synchronize()
+
+    def score(self, req: np.ndarray, now: Optional[int] = None, want_features: bool = True,
+              update: bool = True) -> Result:
+        if not update:
+            raise ValueError("the GPU scorer always applies score-then-update")
+        res, feats = [], []
+        n = len(req)
+        for i in range(0, max(n, 1), self.scorer.bmax):
+            chunk = req[i:i + self.scorer.bmax]
+            with self._lock:
+                p = self.scorer.submit(chunk, now=now, want_features=want_features)
+            r, f = self.scorer.wait(p, unpack=False)
+            res.append(r.view(np.uint32).reshape(-1, 2))
+            if f is not None:
+                feats.append(f.view(FEATREC).reshape(-1))
+        return np.concatenate(res), (np.concatenate(feats) if want_features else None)
+
+    def features(self, slot: int, now: int) -> np.ndarray:
+        """GetFeatures: K1 on a synthetic request for ``slot`` (no update)."""
+        from ..ops import kernels as K
+        torch = self.torch
+        with self._lock:
+            if self._fx is None:
+                self._fx = dict(slab=torch.zeros(16 + 48 * 64, dtype=torch.uint8, device=self.device),
+                                X=torch.zeros((64, self.cfg.features.width), dtype=torch.float32, device=self.device),
+                                feat=torch.zeros((64, 32), dtype=torch.int32, device=self.device))
+            h = np.zeros(1, [("n", "<i4"), ("seq", "<i4"), ("now", "<i8")])
+            h["n"], h["now"] = 1, now
+            r = np.zeros(1, REQREC)
+            r["slot"], r["tx_type"], r["ts"] = slot, 255 | (self.scorer.rank << 8), now
+            buf = np.concatenate([h.view(np.uint8), r.view(np.uint8)])
+            fx = self._fx
+            with torch.cuda.stream(self.scorer.stream):
+                fx["slab"][:len(buf)].copy_(torch.from_numpy(buf))
+                K.feature_assemble(self.store, fx["slab"][:16].view(torch.int64), self.scorer.cfg_dev,
+                                   fx["slab"][16:16 + 48], fx["X"], fx["feat"], 1)
+            self.scorer.stream.synchronize()
+            return fx["feat"][0].cpu().numpy().view(FEATREC)[0]
+
+    def event_history(self, slot: int) -> np.ndarray:
+        """[event_ring, event_dim] f32, oldest first, right-aligned (GRU input)."""
+        with self._lock:
+            raw = self.store.ev[slot].cpu().numpy()
+            rt = self.store.read_rt(slot)
+        ev = (raw.view(np.uint16).astype(np.uint32) << 16).view(np.float32)
+        R = ev.shape[0]
+        head, cnt = int(rt["ev_head"]), min(int(rt["ev_count"]), R)
+        out = np.zeros_like(ev)
+        if cnt:
+            idx = [(head - cnt + i) % R for i in range(cnt)]
+            out[R - cnt:] = ev[idx]
+        return out
+
+    def metrics(self) -> np.ndarray:
+        return self.scorer.read_metrics()

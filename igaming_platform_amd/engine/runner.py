@@ -1,0 +1,92 @@
+"""Device execution of a compiled :class:`Plan` (tree / dense / fused head / GRU steps).
+
+Owns the per-step activation buffers (sized for the largest bucket), the tree-partial slab
+used by the tree->head fusion and the per-bucket tree group counts. Launches are eager on the
+current stream; callers (the fraud scorer, the LTV and abuse services) capture them in
+their own hipGraphs together with their copies, so a model step never re-captures.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from ..models.plan import Plan
+from ..ops import kernels as K
+
+
+def tree_groups(step, bucket: int) -> int:
+    """Split the trees of one ensemble into ``g`` groups so a small batch still fills the
+    256 CUs (>= ~512 workgroups), without shrinking a group below 8 trees."""
+    tiles = -(-bucket // 64)
+    return max(1, min(max(1, step.n_trees // 8), -(-512 // tiles)))
+
+
+class DeviceModel:
+    def __init__(self, plan: Plan, device, buckets: Sequence[int]):
+        self.plan = plan
+        self.device = torch.device(device)
+        self.buckets = sorted(set(int(b) for b in buckets))
+        B = self.buckets[-1]
+        self.step_out: List[torch.Tensor] = []
+        self.tree_partial: Optional[torch.Tensor] = None
+        self.tree_groups: Dict[int, int] = {}
+        steps = plan.steps
+        for i, s in enumerate(steps):
+            last = i == len(steps) - 1
+            feeds_mma = (not last) and steps[i + 1].kind in ("dense", "head")
+            dt = torch.bfloat16 if (s.kind in ("dense", "gru") and feeds_mma) else torch.float32
+            self.step_out.append(torch.zeros((B, s.out_width), dtype=dt, device=self.device))
+            if s.kind == "tree":
+                need = 0
+                for b in self.buckets:
+                    g = tree_groups(s, b)
+                    self.tree_groups[b] = g
+                    need = max(need, g * b * s.k)
+                self.tree_partial = torch.zeros(max(need, 1), dtype=torch.float32, device=self.device)
+        # sequence models: the GRU layers (+ an N=1 head) run as ONE fused K4 launch
+        self.gru: Optional[K.GruPack] = None
+        self.gru_steps = 0
+        if any(s.kind == "gru" for s in steps):
+            n = 0
+            while n < len(steps) and steps[n].kind == "gru":
+                n += 1
+            head = steps[n] if n < len(steps) and steps[n].kind == "dense" and steps[n].n == 1 else None
+            if n == 0 or n + (head is not None) != len(steps):
+                raise ValueError("sequence model must be GRU layers followed by at most an N=1 head")
+            self.gru = K.GruPack(steps[:n], head, self.device)
+            self.gru_steps = len(steps)
+            self.seq_len = steps[0].seq
+        self.out = self.step_out[-1] if self.step_out else None
+
+    @property
+    def out_width(self) -> int:
+        return self.plan.out_width
+
+    def run(self, X: torch.Tensor, bucket: int, m_ptr: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """X: [rows, in] f32 (or [T, rows, I] for a GRU model); returns the last step's buffer."""
+        steps = self.plan.steps
+        if self.gru is not None:
+            T = X.shape[0]
+            if self.gru.head_w is not None:
+                K.gru(self.gru, bucket, T, out=self.out, X=X, m_ptr=m_ptr)
+            else:
+                K.gru(self.gru, bucket, T, yh=self.out, X=X, m_ptr=m_ptr)
+            return self.out
+        cur = X
+        fused_partial = None
+        for i, (s, out) in enumerate(zip(steps, self.step_out)):
+            if s.kind == "tree":
+                g = self.tree_groups.get(bucket, 1)
+                fuse = (g > 1 and i + 1 < len(steps) and steps[i + 1].kind == "head" and s.post == 0
+                        and s.binary_class < 0 and steps[i + 1].k == s.k)
+                K.tree_ensemble(s, cur, None if fuse else out, bucket, partial=self.tree_partial,
+                                groups=g, no_finish=fuse)
+                fused_partial = (self.tree_partial, g, s) if fuse else None
+            elif s.kind == "dense":
+                K.dense(cur, s.w, s.b, out, bucket, s.n, s.k, act=s.act, m_ptr=m_ptr)
+            elif s.kind == "head":
+                K.mlp_head(s, cur, out, bucket, m_ptr=m_ptr, tree_partial=fused_partial)
+                fused_partial = None
+            cur = out
+        return cur

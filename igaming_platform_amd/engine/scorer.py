@@ -30,6 +30,7 @@ from ..layouts import (BATCHHDR, FEATREC, MODEL_HEURISTIC, MODEL_NONE, MODEL_OUT
                        unpack_results)
 from ..models.plan import Plan
 from ..ops import kernels as K
+from .runner import DeviceModel
 
 HDR_BYTES = 16
 REQ_BYTES = REQREC.itemsize
@@ -48,8 +49,12 @@ class Pending:
 class GpuScorer:
     def __init__(self, cfg: Config, store, plan: Optional[Plan] = None, model: str = "plan",
                  device=None, pipeline_depth: int = 2, update_features: bool = True,
-                 use_graphs: Optional[bool] = None):
+                 use_graphs: Optional[bool] = None, owner_filter: bool = False, rank: int = 0):
         self.cfg = cfg
+        # broadcast serving (multi-GPU): every rank sees the whole batch, scores only the rows
+        # whose owner byte (ReqRec.tx_type bits 8-15) is its rank, zeroes the rest
+        self.owner_filter = bool(owner_filter)
+        self.rank = int(rank)
         self.store = store
         self.device = torch.device(device) if device is not None else store.device
         self.plan = plan
@@ -93,43 +98,32 @@ class GpuScorer:
 
     # ------------------------------------------------------------------ buffers / config
     def _alloc_model_buffers(self):
-        dev, B = self.device, self.bmax
+        self.model_dev = None
         self.step_out: List[torch.Tensor] = []
         self.tree_partial = None
         self.tree_groups: Dict[int, int] = {}
+        self.ml = None
         if self.plan is None:
-            self.ml = None
             return
-        steps = self.plan.steps
-        for i, s in enumerate(steps):
-            last = i == len(steps) - 1
-            feeds_mma = (not last) and steps[i + 1].kind in ("dense", "head")
-            dt = torch.bfloat16 if (s.kind == "dense" and feeds_mma) else torch.float32
-            self.step_out.append(torch.zeros((B, s.out_width), dtype=dt, device=dev))
-            if s.kind == "tree":
-                need = 0
-                for b in self.buckets:
-                    g = self._tree_groups(s, b)
-                    self.tree_groups[b] = g
-                    need = max(need, g * b * s.k)
-                if need:
-                    self.tree_partial = torch.zeros(need, dtype=torch.float32, device=dev)
-            if s.kind == "gru":
-                raise ValueError("fraud scoring models take a feature vector; GRU models run in the abuse scorer")
-        self.ml = self.step_out[-1]
-
-    @staticmethod
-    def _tree_groups(s, bucket: int) -> int:
-        tiles = -(-bucket // 64)
-        g = max(1, min(max(1, s.n_trees // 8), -(-512 // tiles)))
-        return g if g > 1 else 1
+        if any(s.kind == "gru" for s in self.plan.steps):
+            raise ValueError("fraud scoring models take a feature vector; GRU models run in the abuse scorer")
+        self.model_dev = DeviceModel(self.plan, self.device, self.buckets)
+        self.step_out = self.model_dev.step_out
+        self.tree_partial = self.model_dev.tree_partial
+        self.tree_groups = self.model_dev.tree_groups
+        self.ml = self.model_dev.out
 
     def refresh_config(self, scoring=None) -> None:
-        """Write the device config block (thresholds, weights, table sizes)."""
+        """Write the device config block (thresholds, weights, table sizes). The last
+        ``scoring`` given stays in force for later refreshes (e.g. a blacklist sync)."""
+        if scoring is not None:
+            self.scoring = scoring
+        scoring = getattr(self, "scoring", None) or self.cfg.scoring
         kind = {"none": MODEL_NONE, "heuristic": MODEL_HEURISTIC, "plan": MODEL_OUTPUT}[self.model]
         ml_col = self.plan.ml_col if self.plan is not None else 0
         ml_stride = self.plan.out_width if self.plan is not None else 1
-        c = score_cfg(self.cfg, kind, ml_col=ml_col, ml_stride=ml_stride, sc=scoring, **self.store.table_params())
+        c = score_cfg(self.cfg, kind, ml_col=ml_col, ml_stride=ml_stride, sc=scoring,
+                      owner_filter=self.owner_filter, my_rank=self.rank, **self.store.table_params())
         self.store.sync_tables()
         self.cfg_dev.copy_(torch.from_numpy(c.view(np.uint8).copy()))
 
@@ -137,24 +131,8 @@ class GpuScorer:
     def _kernels(self, bucket: int) -> None:
         upd = self.update_features
         K.feature_assemble(self.store, self.hdr, self.cfg_dev, self.req, self.X, self.feat, bucket, dedup=upd)
-        cur = self.X
-        if self.plan is not None:
-            steps = self.plan.steps
-            skip_next_input = None
-            for i, (s, out) in enumerate(zip(steps, self.step_out)):
-                if s.kind == "tree":
-                    g = self.tree_groups.get(bucket, 1)
-                    fuse = (g > 1 and i + 1 < len(steps) and steps[i + 1].kind == "head" and s.post == 0
-                            and s.binary_class < 0 and steps[i + 1].k == s.k)
-                    K.tree_ensemble(s, cur, None if fuse else out, bucket, partial=self.tree_partial,
-                                    groups=g, no_finish=fuse)
-                    skip_next_input = (self.tree_partial, g, s) if fuse else None
-                elif s.kind == "dense":
-                    K.dense(cur, s.w, s.b, out, bucket, s.n, s.k, act=s.act, m_ptr=self.n_ptr)
-                elif s.kind == "head":
-                    K.mlp_head(s, cur, out, bucket, m_ptr=self.n_ptr, tree_partial=skip_next_input)
-                    skip_next_input = None
-                cur = out
+        if self.model_dev is not None:
+            self.model_dev.run(self.X, bucket, m_ptr=self.n_ptr)
         ud = K.update_args(self.store, self.cfg_dev, self.req, bucket, hdr=self.hdr, region=-1) if upd else None
         K.ensemble(self.hdr, self.cfg_dev, self.feat, self.X, self.ml, self.res, bucket, self.metrics, upd=ud)
         if upd:

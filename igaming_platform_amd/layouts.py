@@ -21,6 +21,7 @@ FEATREC = np.dtype([
     ("rule_score", "<i4"),
 ])
 FR_VPN, FR_PROXY, FR_TOR, FR_DISPOSABLE, FR_BONUS_ONLY, FR_BLACKLISTED, FR_PARTIAL = 1, 2, 4, 8, 16, 32, 64
+FR_NOT_OWNED = 128
 
 ACCTRT = np.dtype([
     ("hll_dev_exp", "<u4"), ("hll_ip_exp", "<u4"), ("last_tx", "<u4"), ("last_tx_exp", "<u4"),
@@ -48,7 +49,8 @@ SCORECFG = np.dtype([
     ("model_kind", "<i4"), ("ml_col", "<i4"), ("ml_stride", "<i4"), ("log_identity", "<i4"),
     ("sum_compat", "<i4"), ("session_ttl", "<i4"), ("last_tx_ttl", "<i4"), ("hll_ttl", "<i4"),
     ("sum_ttl", "<i4"), ("bl_mask", "<i4"), ("bl_max_probe", "<i4"), ("ip_mask", "<i4"),
-    ("ip_max_probe", "<i4"), ("ext_width", "<i4"), ("pad", "<i4", (6,)),
+    ("ip_max_probe", "<i4"), ("ext_width", "<i4"), ("owner_filter", "<i4"), ("my_rank", "<i4"),
+    ("pad", "<i4", (4,)),
 ])
 
 REQREC = np.dtype([
@@ -71,7 +73,7 @@ def check_layouts(mod) -> None:
 
 def score_cfg(cfg: Config, model_kind: int, ml_col: int = 0, ml_stride: int = 1,
               bl_mask: int = 0, bl_max_probe: int = 0, ip_mask: int = 0, ip_max_probe: int = 0,
-              sc: ScoringConfig = None) -> np.ndarray:
+              sc: ScoringConfig = None, owner_filter: bool = False, my_rank: int = 0) -> np.ndarray:
     sc = sc or cfg.scoring
     f = cfg.features
     w = sc.weights
@@ -109,6 +111,8 @@ def score_cfg(cfg: Config, model_kind: int, ml_col: int = 0, ml_stride: int = 1,
     c["ip_mask"] = ip_mask
     c["ip_max_probe"] = ip_max_probe
     c["ext_width"] = f.width - 30
+    c["owner_filter"] = 1 if owner_filter else 0
+    c["my_rank"] = my_rank
     return c
 
 
@@ -124,3 +128,14 @@ def unpack_results(res: np.ndarray):
         "reasons": (p >> 20).astype(np.int32),
         "ml": res[:, 1].view(np.float32).copy(),
     }
+
+
+def pack_results(score, rule_score, action, reasons, ml, ml_present) -> np.ndarray:
+    """Columns -> ResultRec[n] (uint32 [n,2]); inverse of :func:`unpack_results`."""
+    n = len(score)
+    out = np.zeros((n, 2), np.uint32)
+    out[:, 0] = ((np.asarray(score, np.uint32) & 0xFF) | ((np.asarray(rule_score, np.uint32) & 0xFF) << 8)
+                 | ((np.asarray(action, np.uint32) & 0x3) << 16)
+                 | (np.asarray(ml_present, np.uint32) << 18) | (np.asarray(reasons, np.uint32) << 20))
+    out[:, 1] = np.asarray(ml, np.float32).view(np.uint32)
+    return out

@@ -344,8 +344,6 @@ def to_device(plan: Plan, device) -> Plan:
             s.w1 = _bf16_padded(s.w1_np).to(device)
             s.b1 = None if s.b1_np is None else torch.from_numpy(np.ascontiguousarray(s.b1_np)).to(device)
             s.w2 = torch.from_numpy(s.w2_np).to(device)
-        elif s.kind == "gru":
-            s.dev = gru_device_weights(s, device)
     return plan
 
 

@@ -228,3 +228,92 @@ def ltv(pf: torch.Tensor, out: torch.Tensor, model_ltv: Optional[torch.Tensor] =
     d = dict(pf=_need(pf, "pf", torch.float32), out=_need(out, "out", torch.float32, 6 * B),
              ltv_model=_opt(model_ltv, "ltv_model", dtype=torch.float32, min_numel=B), B=int(B))
     _mod().ltv(d, _stream())
+
+
+# --------------------------------------------------------------------------- K4
+def pack_fragments(w, k_pad: int) -> torch.Tensor:
+    """[N, K] float -> bf16 MFMA B-fragment order P[N/16][k_pad/32][64 lanes][8]
+    (lane l of tile (nt, ks) holds W[nt*16 + (l&15)][ks*32 + 8*(l>>4) .. +8])."""
+    import numpy as np
+    w = np.asarray(w, np.float32)
+    n, k = w.shape
+    if n % 16 or k > k_pad or k_pad % 32:
+        raise ValueError("pack_fragments: N must be a multiple of 16 and K <= k_pad (multiple of 32)")
+    buf = np.zeros((n, k_pad), np.float32)
+    buf[:, :k] = w
+    # [nt, 16 rows, ks, 4 kgroups, 8] -> [nt, ks, kgroup, row, 8] (lane = kgroup*16 + row)
+    t = buf.reshape(n // 16, 16, k_pad // 32, 4, 8).transpose(0, 2, 3, 1, 4)
+    return torch.from_numpy(np.ascontiguousarray(t).reshape(-1)).to(torch.bfloat16)
+
+
+class GruPack:
+    """Device weights of a 1-2 layer GRU chain (+ optional N=1 head) for the K4 kernel."""
+
+    def __init__(self, layers, head=None, device="cuda"):
+        import numpy as np
+        if not 1 <= len(layers) <= 2:
+            raise ValueError("gru: 1 or 2 stacked layers are lowered")
+        H = layers[0].hidden
+        if H not in (64, 128, 256):
+            raise ValueError("gru: hidden size must be 64, 128 or 256")
+        if layers[0].in_dim % 8 or layers[0].in_dim > 64:
+            raise ValueError("gru: input dim must be a multiple of 8, <= 64")
+        if len(layers) == 2 and (layers[1].hidden != H or layers[1].in_dim != H):
+            raise ValueError("gru: layer 2 must be H -> H")
+        if len({int(l.linear_before_reset) for l in layers}) != 1:
+            raise ValueError("gru: layers must share linear_before_reset")
+        self.H, self.I, self.n_layers = H, layers[0].in_dim, len(layers)
+        self.lbr = int(layers[0].linear_before_reset)
+        dev = torch.device(device)
+        self.layers = []
+        for i, l in enumerate(layers):
+            kx = H if i == 1 else (32 if l.in_dim <= 32 else 64)
+            self.layers.append(dict(W=pack_fragments(l.w_np, kx).to(dev), R=pack_fragments(l.r_np, H).to(dev),
+                                    bias=torch.from_numpy(np.ascontiguousarray(l.b_np, np.float32)).to(dev),
+                                    kx_pad=kx, lbr=self.lbr))
+        self.head_w = self.head_b = None
+        self.head_act = 0
+        if head is not None:
+            if head.n != 1 or head.k != H or head.act not in ("none", "sigmoid"):
+                raise ValueError("gru: head must be dense H -> 1 with none/sigmoid")
+            self.head_w = torch.from_numpy(np.ascontiguousarray(head.w_np[0], np.float32)).to(dev)
+            self.head_b = float(head.b_np[0]) if head.b_np is not None else 0.0
+            self.head_act = ACT[head.act]
+        self.device = dev
+
+
+def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh: Optional[torch.Tensor] = None,
+        X: Optional[torch.Tensor] = None, store=None, slots: Optional[torch.Tensor] = None,
+        m_ptr: Optional[torch.Tensor] = None) -> None:
+    """K4. Input either dense ``X`` f32 [T, rows, I] or the store's event rings for ``slots``."""
+    dev = gp.device
+    d = dict(n_layers=gp.n_layers, H=gp.H, T=int(T), I=gp.I, n_rows=int(n_rows),
+             m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32, device=dev))
+    for i, l in enumerate(gp.layers):
+        d[f"l{i}_W"] = _need(l["W"], "W", torch.bfloat16, device=dev)
+        d[f"l{i}_R"] = _need(l["R"], "R", torch.bfloat16, device=dev)
+        d[f"l{i}_bias"] = _need(l["bias"], "bias", torch.float32, 6 * gp.H, dev)
+        d[f"l{i}_kx_pad"] = l["kx_pad"]
+        d[f"l{i}_lbr"] = l["lbr"]
+    if X is not None:
+        if X.dim() != 3 or X.shape[0] < T or X.shape[1] < n_rows or X.shape[2] != gp.I:
+            raise ValueError(f"gru: X must be [T>={T}, rows>={n_rows}, {gp.I}]")
+        d.update(mode=0, X=_need(X, "X", torch.float32, device=dev), x_rows=int(X.shape[1]))
+    else:
+        if store is None or slots is None or store.ev is None:
+            raise ValueError("gru: need X or (store with event rings, slots)")
+        if store.ev.shape[2] != gp.I or store.ev.shape[1] < T:
+            raise ValueError("gru: event ring width / length does not match the model")
+        d.update(mode=1, ev=_need(store.ev, "ev", torch.int16, device=dev),
+                 rt=_need(store.rt, "rt", torch.int32, device=dev),
+                 slots=_need(slots, "slots", torch.int32, n_rows, dev), ev_ring=int(store.ev.shape[1]))
+    if yh is not None:
+        d["yh"] = _need(yh, "yh", torch.float32, n_rows * gp.H, dev)
+    if gp.head_w is not None:
+        if out is None:
+            raise ValueError("gru: a model with a head needs out")
+        d.update(head_w=_need(gp.head_w, "head_w", torch.float32, gp.H, dev), head_b=gp.head_b,
+                 head_act=gp.head_act, out=_need(out, "out", torch.float32, n_rows, dev))
+    elif yh is None:
+        raise ValueError("gru: nothing to write (no head, no yh)")
+    _mod().gru(d, _stream())
