@@ -8,6 +8,7 @@
 #include <memory>
 
 #include "account_index.h"
+#include "link_index.h"
 #include "executor.h"
 #include "onnx_model.h"
 #include "trees.h"
@@ -252,6 +253,21 @@ PYBIND11_MODULE(_native, m) {
       .def("__len__", &AccountIndex::size)
       .def_property_readonly("capacity", &AccountIndex::capacity)
       .def("id_of", &AccountIndex::id_of);
+
+  py::class_<LinkIndex, std::shared_ptr<LinkIndex>>(m, "LinkIndex")
+      .def(py::init<int>(), py::arg("per_key") = 32)
+      .def("add", [](LinkIndex& ix, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> dev,
+                     py::array_t<int64_t, py::array::c_style | py::array::forcecast> acct) {
+        if (dev.size() != acct.size()) throw std::runtime_error("LinkIndex.add: length mismatch");
+        const uint64_t* d = dev.data();
+        const int64_t* a = acct.data();
+        const size_t n = size_t(dev.size());
+        py::gil_scoped_release rel;
+        ix.add(d, a, n);
+      })
+      .def("linked", &LinkIndex::linked, py::arg("acct"), py::arg("limit") = 16)
+      .def("devices_of", &LinkIndex::devices_of)
+      .def("n_devices", &LinkIndex::n_devices);
 
   // results: uint32[n,2] (ResultRec), feats: int32[n,32] (FeatRec) or None, ms: int64[n] or None
   auto view = [](py::array res, py::object feat, py::object ms, wire::ResultView& v,

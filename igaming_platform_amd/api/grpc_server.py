@@ -1,0 +1,371 @@
+"""risk.v1 gRPC server: raw-bytes generic handlers, interceptors, health, reflection.
+
+Same service/method names and wire contract as the reference
+(proto/risk/v1/risk.proto:10-32). Unlike the reference binary — which registers the
+service only in a commented block (services/risk/cmd/main.go:98-142) — every RPC is served.
+
+The two scoring RPCs never materialise per-field Python objects: the handlers receive the
+request bytes (no deserializer), the C++ wire codec parses them, and the response bytes
+come back from the C++ serializer. Unary ScoreTransaction goes through the micro-batcher.
+Interceptors mirror the reference chain (main.go:303-353): logging (OK at debug, errors at
+info), recovery (exceptions -> INTERNAL "internal server error"), metrics (the counters the
+reference's no-op interceptor lists).
+"""
+from __future__ import annotations
+
+import threading
+import time
+from concurrent import futures
+from typing import Callable, Dict, Optional
+
+import grpc
+
+from ..golden import ltv as GL
+from ..obs.logging import get_logger
+from ..proto import health_v1 as HV
+from ..proto import reflection_v1 as RV
+from ..proto import risk_v1 as P
+from ..proto.builder import file_containing_symbol, file_descriptor_proto_bytes
+from .batcher import MicroBatcher
+
+log = get_logger("grpc")
+
+
+def _ts(seconds: float):
+    t = P.Timestamp()
+    t.seconds = int(seconds)
+    t.nanos = int((seconds - int(seconds)) * 1e9)
+    return t
+
+
+class InvalidArgument(ValueError):
+    pass
+
+
+# ============================================================================ interceptors
+def _wrap_unary(h, fn_wrap):
+    if h is None or h.unary_unary is None:
+        return h
+    return grpc.unary_unary_rpc_method_handler(fn_wrap(h.unary_unary), request_deserializer=h.request_deserializer,
+                                               response_serializer=h.response_serializer)
+
+
+class LoggingInterceptor(grpc.ServerInterceptor):
+    """main.go:305-323: duration per call; OK at debug, errors at info."""
+
+    def intercept_service(self, continuation, details):
+        method = details.method
+
+        def wrap(fn):
+            def call(req, ctx):
+                t0 = time.perf_counter()
+                try:
+                    return fn(req, ctx)
+                finally:
+                    code = ctx.code() if hasattr(ctx, "code") else None
+                    fields = dict(method=method, duration_ms=round((time.perf_counter() - t0) * 1e3, 3))
+                    if code not in (None, grpc.StatusCode.OK):
+                        fields["code"] = str(code)
+                        log.info("grpc request failed", extra={"fields": fields})
+                    else:
+                        log.debug("grpc request", extra={"fields": fields})
+            return call
+        return _wrap_unary(continuation(details), wrap)
+
+
+class RecoveryInterceptor(grpc.ServerInterceptor):
+    """main.go:329-342: a panic becomes codes.Internal "internal server error"."""
+
+    def intercept_service(self, continuation, details):
+        method = details.method
+
+        def wrap(fn):
+            def call(req, ctx):
+                try:
+                    return fn(req, ctx)
+                except InvalidArgument as e:
+                    ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+                except grpc.RpcError:
+                    raise
+                except Exception:
+                    c = ctx.code() if hasattr(ctx, "code") else None
+                    if c not in (None, grpc.StatusCode.OK):  # the handler already aborted with a status
+                        raise
+                    log.error("panic recovered", exc_info=True, extra={"fields": dict(method=method)})
+                    ctx.abort(grpc.StatusCode.INTERNAL, "internal server error")
+            return call
+        return _wrap_unary(continuation(details), wrap)
+
+
+class MetricsInterceptor(grpc.ServerInterceptor):
+    """main.go:344-353 lists request count / latency / errors; they are recorded here."""
+
+    def __init__(self, metrics):
+        self.m = metrics
+
+    def intercept_service(self, continuation, details):
+        method = details.method.rsplit("/", 1)[-1]
+
+        def wrap(fn):
+            def call(req, ctx):
+                t0 = time.perf_counter()
+                code = "OK"
+                try:
+                    return fn(req, ctx)
+                except BaseException:
+                    code = "ERROR"
+                    raise
+                finally:
+                    c = ctx.code() if hasattr(ctx, "code") else None
+                    if c not in (None, grpc.StatusCode.OK):
+                        code = c.name
+                    self.m.requests.labels(method=method, code=code).inc()
+                    self.m.latency.labels(method=method).observe(time.perf_counter() - t0)
+            return call
+        return _wrap_unary(continuation(details), wrap)
+
+
+# ============================================================================ risk.v1
+class RiskServicer:
+    def __init__(self, engine, batcher: Optional[MicroBatcher] = None):
+        self.e = engine
+        self.batcher = batcher
+
+    # ---- scoring (raw bytes in / out)
+    def ScoreTransaction(self, data: bytes, ctx) -> bytes:
+        t0 = time.perf_counter()
+        if self.batcher is not None:
+            return self.batcher.submit(data, t0).result()
+        return self.e.score_tx_bytes(data, t0)
+
+    def ScoreBatch(self, data: bytes, ctx) -> bytes:
+        return self.e.score_batch_bytes(data, time.perf_counter())
+
+    # ---- LTV / segment
+    def PredictLTV(self, req, ctx):
+        if not req.account_id:
+            raise InvalidArgument("account_id is required")
+        r = self.e.predict_ltv(req.account_id)
+        return P.PredictLTVResponse(account_id=req.account_id, predicted_ltv=r.predicted_ltv, segment=r.segment,
+                                    churn_risk=r.churn_risk, predicted_active_days=r.survival_days,
+                                    confidence=r.confidence, next_best_action=r.next_best_action,
+                                    predicted_at=_ts(time.time()))
+
+    def GetPlayerSegment(self, req, ctx):
+        if not req.account_id:
+            raise InvalidArgument("account_id is required")
+        r = self.e.predict_ltv(req.account_id)
+        return P.GetPlayerSegmentResponse(account_id=req.account_id, segment=r.segment, ltv=r.predicted_ltv,
+                                          churn_risk=r.churn_risk, recommended_actions=r.recommended_actions())
+
+    def CheckBonusAbuse(self, req, ctx):
+        if not req.account_id:
+            raise InvalidArgument("account_id is required")
+        r = self.e.check_bonus_abuse(req.account_id, req.bonus_id)
+        return P.CheckBonusAbuseResponse(is_abuser=r.is_abuser, abuse_score=r.abuse_score, signals=r.signals,
+                                         linked_accounts=r.linked_accounts)
+
+    # ---- blacklist
+    def AddToBlacklist(self, req, ctx):
+        exp = req.expires_at.seconds if req.HasField("expires_at") else 0
+        try:
+            e = self.e.add_to_blacklist(req.type, req.value, req.reason, req.created_by, expires_at=exp)
+        except ValueError as err:
+            raise InvalidArgument(str(err))
+        return P.AddToBlacklistResponse(success=True, id=e.id)
+
+    def CheckBlacklist(self, req, ctx):
+        ms = self.e.check_blacklist(req.device_id, req.fingerprint, req.ip_address, req.email)
+        return P.CheckBlacklistResponse(
+            is_blacklisted=bool(ms),
+            matches=[P.BlacklistMatch(type=m.type, value=m.value, reason=m.reason, created_at=_ts(m.created_at))
+                     for m in ms])
+
+    # ---- features
+    def GetFeatures(self, req, ctx):
+        if not req.account_id:
+            raise InvalidArgument("account_id is required")
+        fv = P.FeatureVector()
+        fv.ParseFromString(self.e.get_features_bytes(req.account_id))
+        return P.GetFeaturesResponse(account_id=req.account_id, features=fv, computed_at=_ts(time.time()))
+
+    # ---- thresholds (engine.go:491-504)
+    def UpdateThresholds(self, req, ctx):
+        try:
+            b, r = self.e.update_thresholds(req.block_threshold, req.review_threshold)
+        except ValueError as err:
+            raise InvalidArgument(str(err))
+        return P.UpdateThresholdsResponse(success=True, block_threshold=b, review_threshold=r)
+
+    def GetThresholds(self, req, ctx):
+        b, r = self.e.get_thresholds()
+        return P.GetThresholdsResponse(block_threshold=b, review_threshold=r)
+
+
+RAW = {"ScoreTransaction", "ScoreBatch"}
+
+
+def risk_handler(servicer: RiskServicer) -> grpc.GenericRpcHandler:
+    handlers = {}
+    for rpc, req_name, resp_name in P.METHODS:
+        fn = getattr(servicer, rpc)
+        if rpc in RAW:
+            handlers[rpc] = grpc.unary_unary_rpc_method_handler(fn)  # bytes in, bytes out
+        else:
+            handlers[rpc] = grpc.unary_unary_rpc_method_handler(
+                fn, request_deserializer=P.M[req_name].FromString,
+                response_serializer=lambda m: m.SerializeToString())
+    return grpc.method_handlers_generic_handler(P.SERVICE, handlers)
+
+
+# ============================================================================ grpc.health.v1
+class HealthServicer:
+    """Check + Watch; NOT_SERVING on shutdown (main.go:145-147, 249)."""
+
+    def __init__(self):
+        self._status: Dict[str, int] = {"": HV.STATUS["SERVING"]}
+        self._cv = threading.Condition()
+
+    def set(self, service: str, status: str) -> None:
+        with self._cv:
+            self._status[service] = HV.STATUS[status]
+            self._cv.notify_all()
+
+    def Check(self, req, ctx):
+        with self._cv:
+            st = self._status.get(req.service)
+        if st is None:
+            ctx.abort(grpc.StatusCode.NOT_FOUND, "unknown service")
+        return HV.HealthCheckResponse(status=st)
+
+    def Watch(self, req, ctx):
+        last = None
+        while ctx.is_active():
+            with self._cv:
+                st = self._status.get(req.service, HV.STATUS["SERVICE_UNKNOWN"])
+                if st == last:
+                    self._cv.wait(timeout=1.0)
+                    continue
+            last = st
+            yield HV.HealthCheckResponse(status=st)
+
+
+def health_handler(h: HealthServicer) -> grpc.GenericRpcHandler:
+    ser = lambda m: m.SerializeToString()  # noqa: E731
+    return grpc.method_handlers_generic_handler(HV.SERVICE, {
+        "Check": grpc.unary_unary_rpc_method_handler(h.Check, request_deserializer=HV.HealthCheckRequest.FromString,
+                                                     response_serializer=ser),
+        "Watch": grpc.unary_stream_rpc_method_handler(h.Watch, request_deserializer=HV.HealthCheckRequest.FromString,
+                                                      response_serializer=ser),
+    })
+
+
+# ============================================================================ reflection
+SERVICES = [P.SERVICE, HV.SERVICE, "grpc.reflection.v1alpha.ServerReflection", "grpc.reflection.v1.ServerReflection"]
+
+
+def _request_kind(data: bytes):
+    """Which oneof member the reflection request carries (proto3 oneof presence on the wire)."""
+    i, out = 0, {}
+    while i < len(data):
+        key, shift = 0, 0
+        while True:
+            b = data[i]; i += 1
+            key |= (b & 0x7F) << shift; shift += 7
+            if b < 0x80:
+                break
+        fno, wt = key >> 3, key & 7
+        if wt == 2:
+            ln, shift = 0, 0
+            while True:
+                b = data[i]; i += 1
+                ln |= (b & 0x7F) << shift; shift += 7
+                if b < 0x80:
+                    break
+            out[fno] = data[i:i + ln]
+            i += ln
+        elif wt == 0:
+            while data[i] & 0x80:
+                i += 1
+            i += 1
+        else:
+            break
+    return out
+
+
+def reflection_handler(pkg: str) -> grpc.GenericRpcHandler:
+    M = RV.M[pkg]
+
+    def info(req_iter, ctx):
+        for raw in req_iter:
+            f = _request_kind(raw)
+            orig = M["ServerReflectionRequest"].FromString(raw)
+            resp = M["ServerReflectionResponse"](valid_host=orig.host, original_request=orig)
+            try:
+                if 7 in f:
+                    resp.list_services_response.service.extend([M["ServiceResponse"](name=s) for s in SERVICES])
+                elif 4 in f:
+                    fname = file_containing_symbol(f[4].decode())
+                    resp.file_descriptor_response.file_descriptor_proto.extend(_with_deps(fname))
+                elif 3 in f:
+                    resp.file_descriptor_response.file_descriptor_proto.extend(_with_deps(f[3].decode()))
+                else:
+                    resp.error_response.error_code = grpc.StatusCode.UNIMPLEMENTED.value[0]
+                    resp.error_response.error_message = "not supported"
+            except KeyError as e:
+                resp.error_response.error_code = grpc.StatusCode.NOT_FOUND.value[0]
+                resp.error_response.error_message = f"not found: {e}"
+            yield resp.SerializeToString()
+
+    return grpc.method_handlers_generic_handler(f"{pkg}.ServerReflection", {
+        "ServerReflectionInfo": grpc.stream_stream_rpc_method_handler(info)})
+
+
+def _with_deps(fname: str):
+    from google.protobuf import descriptor_pb2
+    out, seen, todo = [], set(), [fname]
+    while todo:
+        n = todo.pop()
+        if n in seen:
+            continue
+        seen.add(n)
+        b = file_descriptor_proto_bytes(n)
+        out.append(b)
+        todo.extend(descriptor_pb2.FileDescriptorProto.FromString(b).dependency)
+    return out
+
+
+# ============================================================================ server
+class RiskServer:
+    def __init__(self, engine, port: int = 0, host: str = "127.0.0.1", workers: int = 64,
+                 batching: bool = True, max_batch: Optional[int] = None, wait_us: Optional[int] = None):
+        self.engine = engine
+        cfg = engine.cfg
+        self.batcher = None
+        if batching:
+            self.batcher = MicroBatcher(engine.score_tx_many_bytes, max_batch or cfg.gpu.max_batch,
+                                        cfg.gpu.wait_us if wait_us is None else wait_us, workers=2,
+                                        on_batch=lambda n: engine.metrics.batch_size.observe(n))
+        self.health = HealthServicer()
+        self.health.set(P.SERVICE, "SERVING")
+        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers),
+                                  interceptors=[LoggingInterceptor(), RecoveryInterceptor(),
+                                                MetricsInterceptor(engine.metrics)],
+                                  options=[("grpc.max_receive_message_length", 64 << 20),
+                                           ("grpc.max_send_message_length", 64 << 20)])
+        self.server.add_generic_rpc_handlers([risk_handler(RiskServicer(engine, self.batcher)),
+                                              health_handler(self.health)] +
+                                             [reflection_handler(p) for p in RV.PKGS])
+        self.port = self.server.add_insecure_port(f"{host}:{port}")
+
+    def start(self) -> "RiskServer":
+        self.server.start()
+        log.info("grpc server listening", extra={"fields": dict(port=self.port)})
+        return self
+
+    def stop(self, grace: float = 5.0) -> None:
+        self.health.set("", "NOT_SERVING")
+        self.health.set(P.SERVICE, "NOT_SERVING")
+        self.server.stop(grace).wait()
+        if self.batcher is not None:
+            self.batcher.close()

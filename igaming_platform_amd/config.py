@@ -131,6 +131,7 @@ class GPUConfig:
     blacklist_capacity: int = 1 << 16
     use_graphs: bool = True
     fallback: str = "cpu"        # on GPU fault: cpu | fail
+    batch_timeout_ms: int = 2000  # watchdog: a device batch slower than this marks the shard unhealthy
 
 
 @dataclass
@@ -143,6 +144,12 @@ class ServerConfig:
 
 
 @dataclass
+class AbuseConfig:
+    """CheckBonusAbuse decision threshold (engine/abuse.py documents the signal weights)."""
+    threshold: float = 0.7
+
+
+@dataclass
 class Config:
     server: ServerConfig = field(default_factory=ServerConfig)
     scoring: ScoringConfig = field(default_factory=ScoringConfig)
@@ -151,6 +158,7 @@ class Config:
     ltv_model: ModelConfig = field(default_factory=ModelConfig)
     abuse_model: ModelConfig = field(default_factory=ModelConfig)
     gpu: GPUConfig = field(default_factory=GPUConfig)
+    abuse: AbuseConfig = field(default_factory=AbuseConfig)
 
     # ------------------------------------------------------------------ loading
     @classmethod

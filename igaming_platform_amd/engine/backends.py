@@ -171,6 +171,12 @@ class CpuBackend:
         res = pack_results(sc, rs, act, rmask, mlv, np.full(n, self.model != "none"))
         return res, (feats if want_features else None)
 
+    def submit(self, req: np.ndarray, now: Optional[int] = None, want_features: bool = True):
+        return self.score(req, now, want_features)
+
+    def collect(self, pending) -> Result:
+        return pending
+
     def features(self, slot: int, now: int) -> np.ndarray:
         r = np.zeros(1, REQREC)
         r["slot"], r["tx_type"] = slot, 255
@@ -186,6 +192,46 @@ class CpuBackend:
     def metrics(self) -> Optional[np.ndarray]:
         return None
 
+    # ------------------------------------------------------------------ durability
+    def snapshot(self, path: str) -> None:
+        """JSON snapshot of the host feature state (our own file format; no pickle)."""
+        import base64
+        import dataclasses
+        import json
+        import os
+        out = {}
+        with self._lock:
+            for k, st in self.store.accounts.items():
+                d = {f.name: getattr(st, f.name) for f in dataclasses.fields(st)}
+                d["hll_dev"] = base64.b64encode(bytes(st.hll_dev)).decode()
+                d["hll_ip"] = base64.b64encode(bytes(st.hll_ip)).decode()
+                d["batch"] = dataclasses.asdict(st.batch) if st.batch is not None else None
+                d["ext"] = None if st.ext is None else np.asarray(st.ext, np.float32).tolist()
+                d["events"] = [np.asarray(e, np.float32).tolist() for e in st.events]
+                out[k] = d
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(dict(version=1, ring_size=self.cfg.features.ring_size, accounts=out), f)
+        os.replace(tmp, path)
+
+    def restore(self, path: str) -> int:
+        import base64
+        import json
+        from ..golden.features import AccountState
+        with open(path) as f:
+            data = json.load(f)
+        if data["ring_size"] != self.cfg.features.ring_size:
+            raise ValueError("snapshot ring size differs from the configured ring size")
+        with self._lock:
+            for k, d in data["accounts"].items():
+                d["hll_dev"] = bytearray(base64.b64decode(d["hll_dev"]))
+                d["hll_ip"] = bytearray(base64.b64decode(d["hll_ip"]))
+                d["batch"] = BatchFeatures(**d["batch"]) if d["batch"] is not None else None
+                d["ext"] = None if d["ext"] is None else np.asarray(d["ext"], np.float32)
+                d["events"] = [np.asarray(e, np.float32) for e in d["events"]]
+                self.store.accounts[k] = AccountState(**d)
+        return len(data["accounts"])
+
 
 class GpuBackend:
     """One GPU shard: HBM feature store + captured-graph scorer."""
@@ -200,7 +246,8 @@ class GpuBackend:
         from ..features.device_store import DeviceFeatureStore
         self.torch = torch
         self.cfg = cfg
-        self.device = torch.device(device)
+        from ..ops.kernels import as_device
+        self.device = as_device(device)
         self.store = DeviceFeatureStore(capacity, cfg.features, self.device, events=True,
                                         blacklist=blacklist, ipintel=ipintel, max_events=max(cfg.gpu.buckets))
         self.blacklist, self.ipintel = self.store.blacklist, self.store.ipintel
@@ -209,6 +256,7 @@ class GpuBackend:
         if capture and self.scorer.use_graphs:
             self.scorer.capture()
         self._lock = threading.RLock()
+        self._slot_locks = [threading.Lock() for _ in range(self.scorer.depth)]
         self._fx = None
 
     def refresh_config(self, scoring=None) -> None:
@@ -244,21 +292,50 @@ class GpuBackend:
                     K.feature_update(self.store, self.scorer.cfg_dev, t, len(chunk), n=len(chunk))
                 self.scorer.stream.synchronize()
 
+    def submit(self, req: np.ndarray, now: Optional[int] = None, want_features: bool = True):
+        """Launch the batch (chunks of the largest bucket); returns a handle for :meth:`collect`.
+        A pipeline slot's pinned buffers are reused only after its results were collected."""
+        sc = self.scorer
+        pend = []
+        n = len(req)
+        for i in range(0, max(n, 1), sc.bmax):
+            chunk = req[i:i + sc.bmax]
+            with self._lock:
+                slot = sc.next_slot()
+            self._slot_locks[slot].acquire()
+            try:
+                with self._lock:
+                    pend.append(sc.submit_into(slot, chunk, now, want_features))
+            except BaseException:
+                self._slot_locks[slot].release()
+                raise
+        return pend
+
+    def collect(self, pend, timeout_s: Optional[float] = None) -> Result:
+        res, feats = [], []
+        try:
+            for p in pend:
+                if timeout_s is not None:
+                    t_end = time.perf_counter() + timeout_s
+                    while not p.event.query():
+                        if time.perf_counter() > t_end:
+                            raise TimeoutError(f"GPU batch exceeded {timeout_s * 1e3:.0f} ms on {self.device}")
+                        time.sleep(20e-6)
+                r, f = self.scorer.wait(p, unpack=False)
+                res.append(r.view(np.uint32).reshape(-1, 2))
+                if f is not None:
+                    feats.append(f.view(FEATREC).reshape(-1))
+        finally:
+            for p in pend:
+                self._slot_locks[p.slot].release()
+        want = bool(pend) and pend[0].want_features
+        return np.concatenate(res), (np.concatenate(feats) if want else None)
+
     def score(self, req: np.ndarray, now: Optional[int] = None, want_features: bool = True,
               update: bool = True) -> Result:
         if not update:
             raise ValueError("the GPU scorer always applies score-then-update")
-        res, feats = [], []
-        n = len(req)
-        for i in range(0, max(n, 1), self.scorer.bmax):
-            chunk = req[i:i + self.scorer.bmax]
-            with self._lock:
-                p = self.scorer.submit(chunk, now=now, want_features=want_features)
-            r, f = self.scorer.wait(p, unpack=False)
-            res.append(r.view(np.uint32).reshape(-1, 2))
-            if f is not None:
-                feats.append(f.view(FEATREC).reshape(-1))
-        return np.concatenate(res), (np.concatenate(feats) if want_features else None)
+        return self.collect(self.submit(req, now, want_features))
 
     def features(self, slot: int, now: int) -> np.ndarray:
         """GetFeatures: K1 on a synthetic request for ``slot`` (no update)."""

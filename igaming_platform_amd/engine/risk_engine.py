@@ -1,0 +1,472 @@
+"""RiskEngine: the risk.v1 service logic behind the gRPC layer.
+
+Reference: ``ScoringEngine`` (services/risk/internal/scoring/engine.go:179-543) wired as the
+commented block of services/risk/cmd/main.go:98-142, plus the RPCs the reference declares
+but never serves (PredictLTV, GetPlayerSegment, CheckBonusAbuse, blacklist, GetFeatures).
+
+Hot path (ScoreBatch / micro-batched ScoreTransaction), all columnar:
+  request bytes -> C++ wire codec (RequestBatch) -> C++ AccountIndex (owner, slot)
+  -> REQREC rows per owner shard -> backend (GPU graph or CPU golden) -> ResultRec
+  -> C++ serializer -> response bytes.
+Thresholds are an immutable ``ScoringConfig`` snapshot swapped under a lock and pushed to
+every shard's device config block (fixes the unguarded read of quirk Q6).
+"""
+from __future__ import annotations
+
+import base64
+import collections
+import dataclasses
+import json
+import os
+import threading
+import time
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from ..config import ACTION_NAMES, Config, REASON_CODES, TX_TYPE_ID, TX_UNKNOWN
+from ..features.tables import Blacklist, IPIntel
+from ..golden import scoring as GS
+from ..layouts import ACCTBATCH, FEATREC, REQREC, unpack_results
+from ..native import native
+from ..obs.logging import get_logger
+from ..obs.metrics import Metrics
+from ..utils.faults import Faults, InjectedFault
+from ..utils.hashing import SEED_DEVICE, SEED_FINGERPRINT, SEED_IP, id_hash
+from .backends import CpuBackend, GpuBackend
+from .registry import AccountRegistry
+
+log = get_logger("engine")
+
+
+def _load_onnx(src):
+    """bytes | path | _native.OnnxModel -> _native.OnnxModel (None if src is falsy)."""
+    if not src:
+        return None
+    N = native()
+    if isinstance(src, (bytes, bytearray)):
+        return N.OnnxModel.from_bytes(bytes(src))
+    if isinstance(src, str):
+        with open(src, "rb") as f:
+            return N.OnnxModel.from_bytes(f.read())
+    return src
+
+
+class RiskEngine:
+    def __init__(self, cfg: Optional[Config] = None, backend: str = "auto", devices: Optional[Sequence[int]] = None,
+                 capacity: Optional[int] = None, fraud_model=None, ltv_model=None, abuse_model=None,
+                 shards: int = 1, capture: bool = True, faults: Optional[Faults] = None):
+        import copy
+        self.cfg = copy.deepcopy(cfg) if cfg is not None else Config()
+        cfg = self.cfg
+        self.faults = faults or Faults()
+        self.metrics = Metrics()
+        N = native()
+        self.N = N
+        if backend == "auto":
+            backend = "cpu"
+            try:
+                import torch
+                if torch.cuda.is_available():
+                    backend = "gpu"
+            except Exception:
+                pass
+        self.kind = backend
+        if backend == "gpu":
+            import torch
+            if devices is None:
+                devices = list(range(min(max(cfg.gpu.devices, 1), torch.cuda.device_count())))
+            self.devices = list(devices)
+            world = len(self.devices)
+        else:
+            self.devices = []
+            world = max(int(shards), 1)
+        self.world = world
+        self.capacity = int(capacity or cfg.gpu.accounts_per_gpu)
+        self.registry = AccountRegistry(self.capacity, world)
+        self.blacklist = Blacklist(cfg.gpu.blacklist_capacity)
+        self.ipintel = IPIntel(cfg.gpu.blacklist_capacity)
+        self.links = N.LinkIndex(32)
+        self._lock = threading.RLock()
+        self.scoring = cfg.scoring
+        self.audit: collections.deque = collections.deque(maxlen=100_000)
+
+        # ---- models
+        fm = _load_onnx(fraud_model if fraud_model is not None else cfg.fraud_model.path)
+        mkind = cfg.fraud_model.kind
+        if mkind == "auto":
+            mkind = "onnx" if fm is not None else "heuristic"  # missing model -> mockPredict (onnx_model.go:51-60)
+        if mkind == "onnx" and fm is None:
+            raise ValueError("fraud_model.kind=onnx but no model given")
+        self.model_kind = mkind
+        self.fraud_onnx = fm
+        self.backends: List = []
+        self.healthy = [True] * world
+        if backend == "gpu":
+            from ..models.plan import compile_onnx, to_device
+            for r, d in enumerate(self.devices):
+                plan = to_device(compile_onnx(fm), f"cuda:{d}") if mkind == "onnx" else None
+                model = {"onnx": "plan", "heuristic": "heuristic", "none": "none"}[mkind]
+                self.backends.append(GpuBackend(cfg, self.capacity, f"cuda:{d}", plan=plan, model=model,
+                                                blacklist=self.blacklist, ipintel=self.ipintel, capture=capture))
+                self.metrics.gpu_healthy.labels(gpu=str(d)).set(1)
+        else:
+            for _ in range(world):
+                self.backends.append(self._cpu_backend(mkind, fm))
+        self.fallback: Optional[CpuBackend] = None
+        if cfg.gpu.fallback == "cpu":  # degraded tier: golden scorer without the shard's feature state
+            self.fallback = self._cpu_backend(mkind, fm)
+
+        # ---- LTV / abuse services
+        from .abuse import AbuseGpu, AbuseService
+        from .ltv import LtvGpu, LtvService
+        lm = _load_onnx(ltv_model if ltv_model is not None else cfg.ltv_model.path)
+        am = _load_onnx(abuse_model if abuse_model is not None else cfg.abuse_model.path)
+        ltv_width = int(lm.inputs()[0][2][-1]) if lm is not None else 0
+        if backend == "gpu":
+            from ..models.plan import compile_onnx, to_device
+            lg = []
+            for d in self.devices:
+                lp = to_device(compile_onnx(lm), f"cuda:{d}") if lm is not None else None
+                g = LtvGpu(f"cuda:{d}", lp, buckets=cfg.gpu.buckets, in_width=ltv_width, use_graphs=capture)
+                g.capture()
+                lg.append(g)
+            self.ltv = LtvService(self.registry, world, gpu=lg, model_width=ltv_width)
+            ag = None
+            if am is not None:
+                ag = []
+                for r, d in enumerate(self.devices):
+                    ap = to_device(compile_onnx(am), f"cuda:{d}")
+                    ag.append(AbuseGpu(self.backends[r].store, ap, bmax=max(cfg.gpu.buckets)))
+            self.abuse = AbuseService(self, threshold=cfg.abuse.threshold, gpu=ag)
+        else:
+            self.ltv = LtvService(self.registry, world, executor=N.Executor(lm) if lm is not None else None,
+                                  model_width=ltv_width)
+            self.abuse = AbuseService(self, threshold=cfg.abuse.threshold,
+                                      executor=N.Executor(am) if am is not None else None)
+        self.started_at = time.time()
+        log.info("risk engine ready", extra={"fields": dict(backend=backend, shards=world, capacity=self.capacity,
+                                                              model=mkind)})
+
+    def _cpu_backend(self, mkind, fm) -> CpuBackend:
+        if mkind == "onnx":
+            ml_col, out_name = 0, self.cfg.fraud_model.output_name
+            try:
+                from ..models.plan import compile_onnx
+                p = compile_onnx(fm)
+                ml_col, out_name = p.ml_col, p.output_name
+            except Exception:
+                pass
+            in_name = fm.inputs()[0][0]
+            return CpuBackend(self.cfg, model="plan", executor=self.N.Executor(fm), input_name=in_name,
+                              output_name=out_name, ml_col=ml_col, blacklist=self.blacklist, ipintel=self.ipintel)
+        return CpuBackend(self.cfg, model=mkind, blacklist=self.blacklist, ipintel=self.ipintel)
+
+    # ================================================================== scoring (columnar)
+    def _score_parsed(self, rb, now: int, want_features: bool = True):
+        """RequestBatch -> (ResultRec [n,2] uint32, FeatRec [n] or None)."""
+        n = len(rb)
+        slots, owners, _ = self.registry.resolve_batch(rb, insert=True)
+        req = np.empty(n, REQREC)
+        rb.pack_reqrec(slots, req.view(np.uint8), now, None)
+        res = np.zeros((n, 2), np.uint32)
+        feats = np.zeros(n, FEATREC) if want_features else None
+        groups = [(0, None)] if self.world == 1 else [(o, np.nonzero(owners == o)[0]) for o in range(self.world)]
+        pend = []
+        for o, sel in groups:
+            sub = req if sel is None else req[sel]
+            if len(sub) == 0:
+                continue
+            pend.append((o, sel, sub, self._submit(o, sub, now, want_features)))
+        for o, sel, sub, p in pend:
+            r, f = self._collect(o, sub, now, want_features, p)
+            if sel is None:
+                res[:], feats = r, f
+            else:
+                res[sel] = r
+                if want_features:
+                    feats[sel] = f
+        cols = rb.columns()
+        self.links.add(cols["device_hash"], (owners.astype(np.int64) << 32) | np.where(slots >= 0, slots, -1))
+        self.metrics.observe_results(res)
+        self.metrics.batch_size.observe(n)
+        return res, feats, slots, owners
+
+    def _submit(self, o: int, sub: np.ndarray, now: int, want_features: bool):
+        be = self.backends[o]
+        if not self.healthy[o] and self.fallback is not None:
+            return ("fallback", None)
+        try:
+            if self.faults.active("backend_error", shard=o):
+                raise InjectedFault(f"injected backend error on shard {o}")
+            return ("ok", be.submit(sub, now, want_features))
+        except Exception as e:  # shard failure -> degrade to the CPU fallback
+            self._mark_unhealthy(o, e)
+            return ("fallback", None)
+
+    def _collect(self, o: int, sub: np.ndarray, now: int, want_features: bool, p):
+        state, h = p
+        if state == "ok":
+            try:
+                be = self.backends[o]
+                if be.kind == "gpu":
+                    return be.collect(h, timeout_s=self.cfg.gpu.batch_timeout_ms / 1e3)
+                return be.collect(h)
+            except Exception as e:
+                self._mark_unhealthy(o, e)
+        if self.fallback is None:
+            raise RuntimeError(f"shard {o} failed and no fallback is configured")
+        self.metrics.fallbacks.labels(reason="shard_unhealthy").inc(len(sub))
+        # the fallback has no feature state for this shard: partial features (engine.go:267-270)
+        fb = sub.copy()
+        fb["slot"] = -1
+        return self.fallback.score(fb, now, want_features, update=False)
+
+    def _mark_unhealthy(self, o: int, err: Exception) -> None:
+        if self.healthy[o]:
+            log.error("shard unhealthy", extra={"fields": dict(shard=o, error=str(err))})
+        self.healthy[o] = False
+        if self.devices:
+            self.metrics.gpu_healthy.labels(gpu=str(self.devices[o])).set(0)
+
+    def recover(self, shard: Optional[int] = None) -> None:
+        """Mark shard(s) healthy again (after an operator or watchdog check)."""
+        for o in ([shard] if shard is not None else range(self.world)):
+            self.healthy[o] = True
+            if self.devices:
+                self.metrics.gpu_healthy.labels(gpu=str(self.devices[o])).set(1)
+
+    # ---- wire-level entry points (gRPC handlers call these with raw bytes)
+    def score_batch_bytes(self, data: bytes, t0: Optional[float] = None) -> bytes:
+        t0 = time.perf_counter() if t0 is None else t0
+        rb = self.N.RequestBatch()
+        rb.parse_batch(data)
+        res, feats, slots, owners = self._score_parsed(rb, int(time.time()))
+        ms = np.full(len(rb), int((time.perf_counter() - t0) * 1e3), np.int64)
+        self._audit(rb, res)
+        return self.N.serialize_batch_response(res, feats.view(np.int32).reshape(-1, 32) if feats is not None else None, ms)
+
+    def score_tx_bytes(self, data: bytes, t0: Optional[float] = None) -> bytes:
+        return self.score_tx_many_bytes([data], [t0 if t0 is not None else time.perf_counter()])[0]
+
+    def score_tx_many_bytes(self, items: List[bytes], t0s: Sequence[float]) -> List[bytes]:
+        """Micro-batcher path: many unary requests, one device batch, one response each."""
+        rb = self.N.RequestBatch()
+        rb.parse_tx_list(items)
+        res, feats, _, _ = self._score_parsed(rb, int(time.time()))
+        now = time.perf_counter()
+        ms = np.array([int((now - t) * 1e3) for t in t0s], np.int64)
+        self._audit(rb, res)
+        return self.N.serialize_tx_responses(res, feats.view(np.int32).reshape(-1, 32) if feats is not None else None, ms)
+
+    def _audit(self, rb, res: np.ndarray) -> None:
+        """risk_scores audit log (init-db.sql:122-138) as an in-memory ring; ids resolved lazily."""
+        ts = time.time()
+        ids = rb.account_id
+        self.audit.extend(zip([ts] * len(ids), ids, res[:, 0].tolist(), res[:, 1].tolist()))
+
+    # ================================================================== python-level API
+    def _tx_bytes(self, tx: Dict) -> bytes:
+        from ..proto import risk_v1 as P
+        m = P.ScoreTransactionRequest()
+        for k, v in tx.items():
+            if k == "metadata":
+                m.metadata.update(v)
+            else:
+                setattr(m, k, v)
+        return m.SerializeToString()
+
+    def score(self, txs: Sequence[Dict], now: Optional[int] = None) -> List[Dict]:
+        """Score dict transactions (ScoreTransactionRequest field names). Returns dicts."""
+        rb = self.N.RequestBatch()
+        rb.parse_tx_list([self._tx_bytes(t) for t in txs])
+        res, feats, slots, _ = self._score_parsed(rb, int(time.time()) if now is None else int(now))
+        cols = unpack_results(res)
+        out = []
+        for i in range(len(txs)):
+            mask = int(cols["reasons"][i])
+            out.append(dict(score=int(cols["score"][i]), action=int(cols["action"][i]),
+                            action_name=ACTION_NAMES.get(int(cols["action"][i]), "?"),
+                            reason_codes=[REASON_CODES[b] for b in range(len(REASON_CODES)) if mask >> b & 1],
+                            rule_score=int(cols["rule_score"][i]), ml_score=float(cols["ml"][i]),
+                            features=feats[i] if feats is not None else None))
+        return out
+
+    def explain(self, tx: Dict, now: Optional[int] = None) -> str:
+        """``ScoreWithExplanation`` (engine.go:507-543)."""
+        t0 = time.perf_counter()
+        r = self.score([tx], now)[0]
+        f = r["features"]
+        fd = {k: (f[k].item() if hasattr(f[k], "item") else f[k]) for k in FEATREC.names} if f is not None else {}
+        fl = int(fd.get("flags", 0))
+        fd.update(is_vpn=bool(fl & 1), is_proxy=bool(fl & 2), bonus_only_player=bool(fl & 16))
+        sr = GS.ScoreResult(r["score"], r["action"], r["reason_codes"], r["rule_score"], r["ml_score"], fd,
+                            int((time.perf_counter() - t0) * 1e3))
+        return GS.explain(self.scoring, sr)
+
+    def get_features(self, account_id: str, now: Optional[int] = None) -> np.ndarray:
+        now = int(time.time()) if now is None else int(now)
+        slot, owner = self.registry.resolve(account_id, insert=False)
+        if slot < 0 or self.faults.active("feature_store_down"):
+            r = np.zeros(1, FEATREC)[0]
+            r["flags"] = 64  # partial
+            r["slot"] = -1
+            return r
+        return self.backends[owner].features(slot, now)
+
+    def get_features_bytes(self, account_id: str, now: Optional[int] = None) -> bytes:
+        rec = np.array([self.get_features(account_id, now)], FEATREC)
+        return self.N.serialize_feature_vector(rec.view(np.int32))
+
+    # ---- thresholds (engine.go:491-504)
+    def get_thresholds(self):
+        s = self.scoring
+        return s.block_threshold, s.review_threshold
+
+    def update_thresholds(self, block: int, review: int):
+        if not (0 <= review <= 100 and 0 <= block <= 100):
+            raise ValueError("thresholds must be in [0, 100]")
+        with self._lock:
+            self.scoring = dataclasses.replace(self.scoring, block_threshold=int(block), review_threshold=int(review))
+            self._push_config()
+        log.info("thresholds updated", extra={"fields": dict(block=block, review=review)})
+        return self.get_thresholds()
+
+    def set_scoring(self, **kw) -> None:
+        """Replace any ScoringConfig fields (rule limits, weights) atomically."""
+        with self._lock:
+            self.scoring = dataclasses.replace(self.scoring, **kw)
+            self._push_config()
+
+    def _push_config(self) -> None:
+        for be in self.backends:
+            be.refresh_config(self.scoring)
+        if self.fallback is not None:
+            self.fallback.refresh_config(self.scoring)
+
+    # ---- blacklist (risk.proto:151-181; redis_store.go:251-293)
+    def add_to_blacklist(self, type_: str, value: str, reason: str = "", created_by: str = "",
+                         expires_at: int = 0):
+        with self._lock:
+            e = self.blacklist.add(type_, value, reason, created_by, expires_at=expires_at, now=int(time.time()))
+            self._push_config()
+        return e
+
+    def check_blacklist(self, device_id: str = "", fingerprint: str = "", ip: str = "", email: str = "",
+                        now: Optional[int] = None):
+        now = int(time.time()) if now is None else int(now)
+        return self.blacklist.check(now, device_id=device_id, fingerprint=fingerprint, ip=ip, email=email)
+
+    def set_ip_intel(self, ip: str, vpn: bool = False, proxy: bool = False, tor: bool = False) -> None:
+        with self._lock:
+            self.ipintel.set(ip, vpn, proxy, tor)
+            self._push_config()
+
+    # ---- feature ingestion (event path)
+    def ingest_events(self, events: Sequence[Dict]) -> int:
+        """TransactionEvents -> ordered feature update on the owner shard (no scoring).
+        Each event: account_id, amount, transaction_type, ts (unix s), device_id, ip_address."""
+        if not events:
+            return 0
+        rb = self.N.RequestBatch()
+        rb.parse_tx_list([self._tx_bytes({k: v for k, v in e.items() if k != "ts"}) for e in events])
+        slots, owners, _ = self.registry.resolve_batch(rb, insert=True)
+        req = np.empty(len(events), REQREC)
+        rb.pack_reqrec(slots, req.view(np.uint8), 0, None)
+        req["ts"] = [int(e.get("ts") or time.time()) for e in events]
+        for o in range(self.world):
+            sel = owners == o
+            if np.any(sel):
+                self.backends[o].ingest(req[sel])
+        cols = rb.columns()
+        self.links.add(cols["device_hash"], (owners.astype(np.int64) << 32) | np.where(slots >= 0, slots, -1))
+        return len(events)
+
+    # ---- warehouse batch features (engine.go:127-140 / the hourly job, main.go:227-236)
+    def load_batch_features(self, account_ids: Sequence[str], rows: np.ndarray) -> None:
+        rows = np.asarray(rows, ACCTBATCH)
+        slots, owners = self.registry.resolve_ids(list(account_ids), insert=True)
+        for o in range(self.world):
+            sel = np.nonzero((owners == o) & (slots >= 0))[0]
+            if len(sel):
+                self.backends[o].set_batch_rows(slots[sel], rows[sel])
+
+    def load_ext_features(self, account_ids: Sequence[str], ext: np.ndarray) -> None:
+        slots, owners = self.registry.resolve_ids(list(account_ids), insert=True)
+        ext = np.asarray(ext, np.float32)
+        for o in range(self.world):
+            sel = np.nonzero((owners == o) & (slots >= 0))[0]
+            if len(sel):
+                self.backends[o].set_ext(slots[sel], ext[sel])
+
+    def delete_account_features(self, account_ids: Sequence[str]) -> None:
+        """``DeleteAccountFeatures`` (redis_store.go:230-240)."""
+        slots, owners = self.registry.resolve_ids(list(account_ids), insert=False)
+        for o in range(self.world):
+            sel = np.nonzero((owners == o) & (slots >= 0))[0]
+            if len(sel):
+                self.backends[o].reset_accounts(slots[sel])
+
+    # ---- LTV / segment / abuse
+    def set_players(self, account_ids, features, ext=None) -> None:
+        self.ltv.set_players(account_ids, features, ext)
+
+    def predict_ltv(self, account_id: str):
+        return self.ltv.predict([account_id])[0]
+
+    def predict_ltv_batch(self, account_ids: Sequence[str]):
+        return self.ltv.predict(account_ids)
+
+    def check_bonus_abuse(self, account_id: str, bonus_id: str = "", now: Optional[int] = None):
+        now = int(time.time()) if now is None else int(now)
+        return self.abuse.check([account_id], now)[0]
+
+    def linked_accounts(self, owner: int, slot: int, limit: int = 16) -> List[str]:
+        keys = self.links.linked((int(owner) << 32) | int(slot), limit)
+        return [self.registry.id_of(int(k) >> 32, int(k) & 0xFFFFFFFF) for k in keys]
+
+    # ---- health / durability
+    def health(self) -> Dict:
+        return dict(backend=self.kind, shards=self.world, healthy=list(self.healthy),
+                    accounts=[self.registry.size(o) for o in range(self.world)],
+                    uptime_s=round(time.time() - self.started_at, 1))
+
+    def ready(self) -> bool:
+        return all(self.healthy) or self.fallback is not None
+
+    def snapshot(self, directory: str) -> None:
+        """Feature shards + account registry -> ``directory`` (restart keeps velocity windows)."""
+        os.makedirs(directory, exist_ok=True)
+        meta = dict(version=1, world=self.world, kind=self.kind, ids=[])
+        for o in range(self.world):
+            n = self.registry.size(o)
+            meta["ids"].append([self.registry.id_of(o, s) for s in range(n)])
+            be = self.backends[o]
+            if be.kind == "gpu":
+                be.store.snapshot(os.path.join(directory, f"shard{o}.npz"), n_used=max(n, 1))
+            else:
+                be.snapshot(os.path.join(directory, f"shard{o}.json"))
+        tmp = os.path.join(directory, "registry.json.tmp")
+        with open(tmp, "w") as f:
+            json.dump(meta, f)
+        os.replace(tmp, os.path.join(directory, "registry.json"))
+
+    def restore(self, directory: str) -> int:
+        with open(os.path.join(directory, "registry.json")) as f:
+            meta = json.load(f)
+        if meta["world"] != self.world:
+            raise ValueError(f"snapshot has {meta['world']} shards, engine has {self.world}")
+        total = 0
+        for o in range(self.world):
+            ids = meta["ids"][o]
+            if ids:
+                got, _ = self.registry.index[o].lookup(ids, True)
+                if list(got) != list(range(len(ids))):
+                    raise ValueError("registry must be empty before restore")
+            be = self.backends[o]
+            if be.kind == "gpu":
+                be.store.restore(os.path.join(directory, f"shard{o}.npz"))
+            else:
+                be.restore(os.path.join(directory, f"shard{o}.json"))
+            total += len(ids)
+        return total

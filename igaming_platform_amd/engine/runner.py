@@ -25,7 +25,7 @@ def tree_groups(step, bucket: int) -> int:
 class DeviceModel:
     def __init__(self, plan: Plan, device, buckets: Sequence[int]):
         self.plan = plan
-        self.device = torch.device(device)
+        self.device = K.as_device(device)
         self.buckets = sorted(set(int(b) for b in buckets))
         B = self.buckets[-1]
         self.step_out: List[torch.Tensor] = []

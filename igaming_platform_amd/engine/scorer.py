@@ -56,7 +56,7 @@ class GpuScorer:
         self.owner_filter = bool(owner_filter)
         self.rank = int(rank)
         self.store = store
-        self.device = torch.device(device) if device is not None else store.device
+        self.device = K.as_device(device) if device is not None else store.device
         self.plan = plan
         if plan is None and model == "plan":
             model = "none"
@@ -202,6 +202,15 @@ class GpuScorer:
             ev.record(self.stream)
         self.batches += 1
         return Pending(slot, n, b, ev, t0, want_features)
+
+    def submit_into(self, slot: int, req: np.ndarray, now: Optional[int] = None,
+                    want_features: bool = False) -> Pending:
+        n = len(req)
+        now = int(time.time()) if now is None else int(now)
+        v = self.slab_view(slot, n)
+        v[:] = req
+        v["ts"] = now
+        return self.submit_packed(slot, n, now, want_features)
 
     def submit(self, req: np.ndarray, now: Optional[int] = None, want_features: bool = False) -> Pending:
         """``req``: REQREC structured array (rows; ts is overwritten with ``now``)."""

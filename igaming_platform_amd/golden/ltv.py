@@ -233,17 +233,19 @@ def predict(f: PlayerFeatures, ltv_override: float = None) -> LTVPrediction:
     )
 
 
+SEGMENT_PLAYBOOK = {
+    SEG_VIP: ["EXCLUSIVE_EVENT_INVITE", "VIP_MANAGER_CALL"],
+    SEG_HIGH: ["LOYALTY_REWARD", "RETENTION_BONUS"],
+    SEG_MEDIUM: ["STANDARD_PROMOTION", "SUGGEST_BONUS"],
+    SEG_LOW: ["SMALL_DEPOSIT_BONUS", "ONBOARDING_GUIDE"],
+    SEG_CHURNING: ["SEND_WINBACK_BONUS", "SEND_ENGAGEMENT_EMAIL"],
+}
+
+
 def recommended_actions(seg: int, f: PlayerFeatures, churn: float) -> List[str]:
     """GetPlayerSegment.recommended_actions: the NBA first, then segment-generic actions."""
     acts = [next_best_action(seg, f, churn)]
-    extra = {
-        SEG_VIP: ["EXCLUSIVE_EVENT_INVITE", "VIP_MANAGER_CALL"],
-        SEG_HIGH: ["LOYALTY_REWARD", "RETENTION_BONUS"],
-        SEG_MEDIUM: ["STANDARD_PROMOTION", "SUGGEST_BONUS"],
-        SEG_LOW: ["SMALL_DEPOSIT_BONUS", "ONBOARDING_GUIDE"],
-        SEG_CHURNING: ["SEND_WINBACK_BONUS", "SEND_ENGAGEMENT_EMAIL"],
-    }.get(seg, [])
-    for a in extra:
+    for a in SEGMENT_PLAYBOOK.get(seg, []):
         if a not in acts:
             acts.append(a)
     return acts

@@ -129,28 +129,33 @@ def _gru_weights(rng, in_dim: int, hidden: int):
     return w, r, b
 
 
-def gru(seq: int = 100, in_dim: int = 16, hidden: int = 256, seed: int = 5):
+def gru(seq: int = 100, in_dim: int = 16, hidden: int = 256, seed: int = 5, layers: int = 2,
+        linear_before_reset: int = 1, head: bool = True):
     rng = np.random.default_rng(seed)
     w1, r1, b1 = _gru_weights(rng, in_dim, hidden)
-    w2, r2, b2 = _gru_weights(rng, hidden, hidden)
     wh = (rng.standard_normal((hidden, 1)) * np.sqrt(1.0 / hidden)).astype(np.float32)
     bh = np.array([0.0], np.float32)
-    nodes = [
-        node("GRU", ["input", "W1", "R1", "B1"], ["Y1", "Yh1"], hidden_size=hidden,
-             linear_before_reset=1),
-        node("Squeeze", ["Y1", "ax1"], ["X2"]),
-        node("GRU", ["X2", "W2", "R2", "B2"], ["Y2", "Yh2"], hidden_size=hidden,
-             linear_before_reset=1),
-        node("Reshape", ["Yh2", "shp"], ["h"]),
-        node("Gemm", ["h", "Wh", "Bh"], ["logit"]),
-        node("Sigmoid", ["logit"], ["output"]),
-    ]
-    inits = [tensor("W1", w1), tensor("R1", r1), tensor("B1", b1), tensor("W2", w2),
-             tensor("R2", r2), tensor("B2", b2), tensor("Wh", wh), tensor("Bh", bh),
+    lbr = int(linear_before_reset)
+    nodes = [node("GRU", ["input", "W1", "R1", "B1"], ["Y1", "Yh1"], hidden_size=hidden, linear_before_reset=lbr)]
+    inits = [tensor("W1", w1), tensor("R1", r1), tensor("B1", b1),
              tensor("ax1", np.array([1], np.int64)), tensor("shp", np.array([-1, hidden], np.int64))]
-    return model(nodes, [value_info("input", S.FLOAT, [seq, "N", in_dim])],
-                 [value_info("output", S.FLOAT, ["N", 1])], inits, name="abuse_gru",
-                 metadata={"family": "gru", "layers": "2", "hidden": str(hidden), "seq": str(seq)})
+    last_h = "Yh1"
+    if layers == 2:
+        w2, r2, b2 = _gru_weights(rng, hidden, hidden)
+        nodes += [node("Squeeze", ["Y1", "ax1"], ["X2"]),
+                  node("GRU", ["X2", "W2", "R2", "B2"], ["Y2", "Yh2"], hidden_size=hidden, linear_before_reset=lbr)]
+        inits += [tensor("W2", w2), tensor("R2", r2), tensor("B2", b2)]
+        last_h = "Yh2"
+    if head:
+        nodes += [node("Reshape", [last_h, "shp"], ["h"]), node("Gemm", ["h", "Wh", "Bh"], ["logit"]),
+                  node("Sigmoid", ["logit"], ["output"])]
+        inits += [tensor("Wh", wh), tensor("Bh", bh)]
+        out_vi = value_info("output", S.FLOAT, ["N", 1])
+    else:
+        nodes.append(node("Reshape", [last_h, "shp"], ["output"]))
+        out_vi = value_info("output", S.FLOAT, ["N", hidden])
+    return model(nodes, [value_info("input", S.FLOAT, [seq, "N", in_dim])], [out_vi], inits, name="abuse_gru",
+                 metadata={"family": "gru", "layers": str(layers), "hidden": str(hidden), "seq": str(seq)})
 
 
 BUILDERS = {"logistic": logistic, "gbdt": gbdt, "stacked": stacked, "ltv_mlp": ltv_mlp, "gru": gru}

@@ -27,6 +27,14 @@ def _mod():
     return m
 
 
+def as_device(device) -> torch.device:
+    """torch.device with an explicit index ("cuda" -> "cuda:<current>")."""
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
 def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
@@ -264,7 +272,7 @@ class GruPack:
             raise ValueError("gru: layers must share linear_before_reset")
         self.H, self.I, self.n_layers = H, layers[0].in_dim, len(layers)
         self.lbr = int(layers[0].linear_before_reset)
-        dev = torch.device(device)
+        dev = as_device(device)
         self.layers = []
         for i, l in enumerate(layers):
             kx = H if i == 1 else (32 if l.in_dim <= 32 else 64)

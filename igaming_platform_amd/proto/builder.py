@@ -97,8 +97,12 @@ def build_file(file_name: str, package: str, messages: Dict[str, Sequence[Tuple]
             _add_field(m, fd, name, number, ftype, label, package)
     for sname, methods in (services or {}).items():
         s = fd.service.add(name=sname)
-        for mname, itype, otype in methods:
-            s.method.add(name=mname, input_type=f".{package}.{itype}", output_type=f".{package}.{otype}")
+        for spec in methods:
+            mname, itype, otype = spec[:3]
+            mode = spec[3] if len(spec) > 3 else ""
+            s.method.add(name=mname, input_type=f".{package}.{itype}", output_type=f".{package}.{otype}",
+                         client_streaming=mode in ("client_stream", "bidi"),
+                         server_streaming=mode in ("server_stream", "bidi"))
     _POOL.Add(fd)
     out = {}
     for mname in messages:
@@ -115,6 +119,16 @@ def enum_values(full_name: str) -> Dict[str, int]:
 
 def file_descriptor(file_name: str):
     return _POOL.FindFileByName(file_name)
+
+
+def file_descriptor_proto_bytes(file_name: str) -> bytes:
+    p = descriptor_pb2.FileDescriptorProto()
+    _POOL.FindFileByName(file_name).CopyToProto(p)
+    return p.SerializeToString()
+
+
+def file_containing_symbol(symbol: str) -> str:
+    return _POOL.FindFileContainingSymbol(symbol).name
 
 
 def timestamp_class():

@@ -19,7 +19,7 @@ M = build_file(
     enums={"ServingStatus": [("UNKNOWN", 0), ("SERVING", 1), ("NOT_SERVING", 2),
                              ("SERVICE_UNKNOWN", 3)]},
     services={"Health": [("Check", "HealthCheckRequest", "HealthCheckResponse"),
-                         ("Watch", "HealthCheckRequest", "HealthCheckResponse")]},
+                         ("Watch", "HealthCheckRequest", "HealthCheckResponse", "server_stream")]},
 )
 STATUS = enum_values("grpc.health.v1.ServingStatus")
 HealthCheckRequest = M["HealthCheckRequest"]

@@ -1,0 +1,82 @@
+"""Risk service binary: ``python -m igaming_platform_amd.serve [--config cfg.yaml] [--backend auto]``.
+
+Mirrors services/risk/cmd/main.go:72-258: env config (same names), JSON logging, engine
+construction, gRPC server (risk.v1 + health + reflection, interceptors), HTTP endpoints,
+the hourly batch-feature refresh ticker (a stub in the reference; here it reloads a
+warehouse snapshot file when one is configured), periodic feature-store snapshots, and a
+graceful shutdown on SIGINT/SIGTERM (health -> NOT_SERVING, 30 s grace).
+
+``--synthetic-model gbdt|stacked|logistic`` generates a random-init ONNX fraud model (no
+network / no checkpoints in this environment).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+import threading
+import time
+
+from .config import Config
+from .obs.logging import get_logger, setup_logger
+
+
+def build_engine(a, cfg: Config):
+    from .engine.risk_engine import RiskEngine
+    fraud = None
+    if a.synthetic_model:
+        from .onnx import builders
+        kw = {"n_features": cfg.features.width} if a.synthetic_model == "logistic" else {}
+        fraud = builders.build(a.synthetic_model, **kw).SerializeToString()
+    return RiskEngine(cfg, backend=a.backend, fraud_model=fraud, capacity=a.accounts or None,
+                      shards=a.shards)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="MI355X risk scoring service (risk.v1)")
+    ap.add_argument("--config", default=os.environ.get("CONFIG_PATH", ""))
+    ap.add_argument("--backend", default="auto", choices=["auto", "gpu", "cpu"])
+    ap.add_argument("--gpus", type=int, default=0, help="GPU shards (default: config / RISK_GPUS)")
+    ap.add_argument("--shards", type=int, default=1, help="CPU shards (backend=cpu)")
+    ap.add_argument("--accounts", type=int, default=0, help="feature-store accounts per shard")
+    ap.add_argument("--synthetic-model", default="", choices=["", "gbdt", "stacked", "logistic"])
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--snapshot-dir", default=os.environ.get("RISK_SNAPSHOT_DIR", ""))
+    ap.add_argument("--snapshot-every-s", type=float, default=300.0)
+    ap.add_argument("--no-batching", action="store_true")
+    a = ap.parse_args(argv)
+    cfg = Config.load(a.config or None)
+    if a.gpus:
+        cfg.gpu.devices = a.gpus
+    log = setup_logger(cfg.server.log_level)
+    from .api.grpc_server import RiskServer
+    from .api.http_server import HttpServer
+    eng = build_engine(a, cfg)
+    if a.snapshot_dir and os.path.exists(os.path.join(a.snapshot_dir, "registry.json")):
+        n = eng.restore(a.snapshot_dir)
+        log.info("feature store restored", extra={"fields": dict(accounts=n, dir=a.snapshot_dir)})
+    gs = RiskServer(eng, port=cfg.server.grpc_port, host=a.host, batching=not a.no_batching).start()
+    hs = HttpServer(eng, port=cfg.server.http_port, host=a.host, timeout_s=cfg.server.http_timeout_s).start()
+    stop = threading.Event()
+
+    def _sig(signum, frame):
+        log.info("shutdown signal", extra={"fields": dict(signal=signum)})
+        stop.set()
+
+    signal.signal(signal.SIGINT, _sig)
+    signal.signal(signal.SIGTERM, _sig)
+    last_snap = time.time()
+    while not stop.wait(1.0):
+        if a.snapshot_dir and time.time() - last_snap >= a.snapshot_every_s:
+            eng.snapshot(a.snapshot_dir)
+            last_snap = time.time()
+    gs.stop(cfg.server.shutdown_grace_s)
+    hs.stop()
+    if a.snapshot_dir:
+        eng.snapshot(a.snapshot_dir)
+    log.info("server stopped")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,231 @@
+"""Engine (CPU backend) against the golden model, plus thresholds, blacklist, sharding,
+snapshots, degradation and the LTV / abuse services."""
+import numpy as np
+import pytest
+
+from igaming_platform_amd.config import Config, REASON_CODES, TX_TYPE_ID
+from igaming_platform_amd.engine.risk_engine import RiskEngine
+from igaming_platform_amd.golden import ltv as GL, scoring as GS
+from igaming_platform_amd.golden.features import BatchFeatures, GoldenFeatureStore, TxEvent, model_input
+from igaming_platform_amd.layouts import ACCTBATCH
+from igaming_platform_amd.utils.faults import Faults
+from igaming_platform_amd.utils.hashing import SEED_DEVICE, SEED_FINGERPRINT, SEED_IP, id_hash
+
+NOW = 1_760_000_000
+
+
+def _txs(n, rng, n_acc=30):
+    types = ["deposit", "withdraw", "bet", "win"]
+    out = []
+    for i in range(n):
+        a = int(rng.integers(0, n_acc))
+        out.append(dict(account_id=f"acc-{a}", amount=int(rng.choice([500, 5000, 150000, 2_000_000])),
+                        transaction_type=types[int(rng.integers(0, 4))],
+                        device_id=f"dev-{a}-{int(rng.integers(0, 5))}", ip_address=f"10.1.{a}.{int(rng.integers(0, 7))}",
+                        fingerprint=f"fp-{a}"))
+    return out
+
+
+def _batch_rows(n_acc, rng):
+    rows = np.zeros(n_acc, ACCTBATCH)
+    rows["present"] = 1
+    rows["total_deposits"] = rng.integers(0, 10**6, n_acc)
+    rows["total_withdrawals"] = rng.integers(0, 10**6, n_acc)
+    rows["deposit_count"] = rng.integers(0, 5, n_acc)
+    rows["bet_count"] = rng.integers(0, 50, n_acc)
+    rows["win_count"] = rows["bet_count"] // 3
+    rows["bonus_claim_count"] = rng.integers(0, 6, n_acc)
+    rows["account_created_at"] = NOW - rng.integers(0, 60, n_acc) * 86400
+    rows["avg_bet_size"] = 12.5
+    return rows
+
+
+class Golden:
+    """Sequential golden re-implementation of the batch semantics (score all, then update)."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.st = GoldenFeatureStore(cfg.features)
+
+    def load(self, ids, rows):
+        for i, r in zip(ids, rows):
+            self.st.set_batch(i, BatchFeatures(
+                total_deposits=int(r["total_deposits"]), total_withdrawals=int(r["total_withdrawals"]),
+                deposit_count=int(r["deposit_count"]), withdraw_count=0, bet_count=int(r["bet_count"]),
+                win_count=int(r["win_count"]), avg_bet_size=float(r["avg_bet_size"]),
+                account_created_at=int(r["account_created_at"]), bonus_claim_count=int(r["bonus_claim_count"])))
+
+    def score(self, txs, now, blacklist=()):
+        self.st.blacklist = {h: 0 for h in blacklist}
+        out = []
+        for t in txs:
+            ip = id_hash(t.get("ip_address", ""), SEED_IP)
+            f = self.st.raw_features(t["account_id"], now, ip_hash=ip)
+            bl = self.st.blacklisted([id_hash(t.get("device_id", ""), SEED_DEVICE),
+                                      id_hash(t.get("fingerprint", ""), SEED_FINGERPRINT), ip], now)
+            tx = TX_TYPE_ID.get(t["transaction_type"], 255)
+            rule, reasons = GS.apply_rules(self.cfg.scoring, f, t["amount"], tx, bl)
+            x = model_input(f, t["amount"], tx, self.cfg.features.log_transform, self.cfg.features.width)
+            out.append(GS.ensemble(self.cfg.scoring, rule, reasons, GS.heuristic_predict(x)))
+        for t in txs:
+            self.st.apply(TxEvent(t["account_id"], t["amount"], TX_TYPE_ID.get(t["transaction_type"], 255),
+                                  id_hash(t.get("device_id", ""), SEED_DEVICE), id_hash(t.get("ip_address", ""), SEED_IP),
+                                  now))
+        return out
+
+
+@pytest.mark.parametrize("shards", [1, 3])
+def test_engine_matches_golden_over_batches(shards):
+    cfg = Config()
+    rng = np.random.default_rng(7)
+    eng = RiskEngine(cfg, backend="cpu", capacity=200, shards=shards)
+    gold = Golden(cfg)
+    ids = [f"acc-{i}" for i in range(30)]
+    rows = _batch_rows(30, rng)
+    eng.load_batch_features(ids, rows)
+    gold.load(ids, rows)
+    eng.add_to_blacklist("device", "dev-3-1", "chargeback", "test")
+    bl = [id_hash("dev-3-1", SEED_DEVICE)]
+    for step in range(6):
+        txs = _txs(40, rng)
+        now = NOW + step * 20
+        got = eng.score(txs, now=now)
+        exp = gold.score(txs, now, bl)
+        for g, (s, a, reasons, ml) in zip(got, exp):
+            assert (g["score"], g["action"], g["reason_codes"]) == (s, a, reasons)
+            assert g["ml_score"] == pytest.approx(ml, abs=1e-6)
+
+
+def test_thresholds_update_changes_actions():
+    eng = RiskEngine(Config(), backend="cpu", capacity=50)
+    tx = dict(account_id="x", amount=2_000_000, transaction_type="deposit")
+    assert eng.score([tx], now=NOW)[0]["score"] == 24
+    assert eng.get_thresholds() == (80, 50)
+    eng.update_thresholds(20, 10)
+    r = eng.score([tx], now=NOW)[0]
+    assert r["action"] == 3 and eng.get_thresholds() == (20, 10)
+    with pytest.raises(ValueError):
+        eng.update_thresholds(101, 10)
+
+
+def test_blacklist_types_and_expiry():
+    eng = RiskEngine(Config(), backend="cpu", capacity=50)
+    eng.add_to_blacklist("ip", "6.6.6.6", "botnet", "ops", expires_at=NOW + 100)
+    eng.add_to_blacklist("email", "x@evil.test", "fraud", "ops")
+    assert [m.type for m in eng.check_blacklist(ip="6.6.6.6", now=NOW)] == ["ip"]
+    assert eng.check_blacklist(ip="6.6.6.6", now=NOW + 101) == []
+    assert eng.check_blacklist(email="x@evil.test", now=NOW)[0].reason == "fraud"
+    r = eng.score([dict(account_id="a", amount=1, transaction_type="bet", ip_address="6.6.6.6")], now=NOW)[0]
+    assert "KNOWN_FRAUDSTER" in r["reason_codes"]
+    r = eng.score([dict(account_id="a", amount=1, transaction_type="bet", ip_address="6.6.6.6")], now=NOW + 200)[0]
+    assert "KNOWN_FRAUDSTER" not in r["reason_codes"]
+    with pytest.raises(ValueError):
+        eng.add_to_blacklist("phone", "1", "", "")
+
+
+def test_ingest_then_features_and_velocity_rule():
+    eng = RiskEngine(Config(), backend="cpu", capacity=50)
+    eng.ingest_events([dict(account_id="v", amount=100, transaction_type="bet", ts=NOW - i) for i in range(12)])
+    f = eng.get_features("v", now=NOW)
+    assert f["tx_count_1m"] == 12 and f["tx_sum_1h"] == 1200
+    r = eng.score([dict(account_id="v", amount=100, transaction_type="bet")], now=NOW)[0]
+    assert r["reason_codes"][0] == "HIGH_VELOCITY"
+    assert eng.get_features("nobody", now=NOW)["flags"] & 64
+
+
+def test_snapshot_restore_round_trip(tmp_path):
+    cfg = Config()
+    a = RiskEngine(cfg, backend="cpu", capacity=50, shards=2)
+    txs = _txs(30, np.random.default_rng(2), n_acc=10)
+    a.score(txs, now=NOW)
+    a.snapshot(str(tmp_path))
+    b = RiskEngine(cfg, backend="cpu", capacity=50, shards=2)
+    assert b.restore(str(tmp_path)) == sum(a.registry.size(o) for o in range(2))
+    for i in range(10):
+        fa, fb = a.get_features(f"acc-{i}", now=NOW + 5), b.get_features(f"acc-{i}", now=NOW + 5)
+        assert fa.tobytes() == fb.tobytes()
+
+
+def test_shard_failure_degrades_to_fallback():
+    faults = Faults("")
+    eng = RiskEngine(Config(), backend="cpu", capacity=50, shards=2, faults=faults)
+    txs = [dict(account_id=f"acc-{i}", amount=100, transaction_type="bet") for i in range(20)]
+    eng.score(txs, now=NOW)
+    faults.set("backend_error", shard=1)
+    r = eng.score(txs, now=NOW)
+    assert len(r) == 20 and eng.healthy == [True, False] and eng.ready()
+    _, owners = eng.registry.resolve_ids([t["account_id"] for t in txs])
+    for x, o in zip(r, owners):
+        if o == 1:  # degraded rows: partial features (engine.go:267-270)
+            assert x["features"]["flags"] & 64
+    faults.clear()
+    eng.recover()
+    assert eng.healthy == [True, True]
+
+
+def test_ltv_and_segment_cpu():
+    eng = RiskEngine(Config(), backend="cpu", capacity=50)
+    vip = GL.PlayerFeatures(days_since_registration=400, days_since_last_bet=1, days_since_last_deposit=2,
+                            sessions_per_week=6, deposit_frequency=5, net_revenue=20000, bet_count=500)
+    eng.set_players(["vip"], [vip])
+    r = eng.predict_ltv("vip")
+    p = GL.predict(GL.PlayerFeatures.from_row(np.float32(vip.row())))
+    assert r.segment == GL.SEG_VIP == p.segment and r.found
+    assert r.predicted_ltv == pytest.approx(p.predicted_ltv, rel=1e-6)
+    assert r.recommended_actions()[0] == p.next_best_action
+    assert not eng.predict_ltv("unknown").found
+
+
+def test_ltv_model_cpu_matches_executor():
+    from igaming_platform_amd.engine.ltv import ltv_model_input
+    from igaming_platform_amd.native import native
+    from igaming_platform_amd.onnx import builders
+    m = builders.build("ltv_mlp", n_features=64, width=64, layers=2).SerializeToString()
+    eng = RiskEngine(Config(), backend="cpu", capacity=50, ltv_model=m)
+    f = GL.PlayerFeatures(days_since_registration=200, net_revenue=300, days_since_last_bet=10)
+    eng.set_players(["p"], [f])
+    X = ltv_model_input(np.float32([f.row()]), None, 64)
+    ml = native().Executor(native().OnnxModel.from_bytes(m)).run({"input": X})["output"][0, 0]
+    r = eng.predict_ltv("p")
+    assert r.predicted_ltv == pytest.approx(GL.predict(f, float(ml)).predicted_ltv, rel=1e-5)
+
+
+def test_bonus_abuse_signals_and_links():
+    eng = RiskEngine(Config(), backend="cpu", capacity=50)
+    rows = np.zeros(1, ACCTBATCH)
+    rows["present"], rows["bonus_claim_count"], rows["total_deposits"] = 1, 5, 100
+    eng.load_batch_features(["abuser"], rows)
+    eng.score([dict(account_id="abuser", amount=1, transaction_type="bet", device_id="shared"),
+               dict(account_id="alt1", amount=1, transaction_type="bet", device_id="shared")], now=NOW)
+    r = eng.check_bonus_abuse("abuser", "welcome", now=NOW)
+    assert "BONUS_ONLY_PLAYER" in r.signals and "LOW_WAGER_COMPLETION" in r.signals
+    assert "SHARED_DEVICE" in r.signals and r.linked_accounts == ["alt1"]
+    assert r.is_abuser and r.abuse_score == pytest.approx(0.8)
+    clean = eng.check_bonus_abuse("nobody", now=NOW)
+    assert not clean.is_abuser and clean.signals == []
+
+
+def test_bonus_abuse_gru_model_cpu():
+    from igaming_platform_amd.onnx import builders
+    m = builders.build("gru", seq=100, hidden=64, layers=2).SerializeToString()
+    eng = RiskEngine(Config(), backend="cpu", capacity=50, abuse_model=m)
+    eng.ingest_events([dict(account_id="g", amount=100 * i, transaction_type="deposit", ts=NOW - 100 + i)
+                       for i in range(30)])
+    r = eng.check_bonus_abuse("g", now=NOW)
+    assert r.model_score is not None and 0.0 < r.model_score < 1.0
+
+
+def test_explain_text():
+    eng = RiskEngine(Config(), backend="cpu", capacity=50)
+    txt = eng.explain(dict(account_id="e", amount=500000, transaction_type="deposit"), now=NOW)
+    assert "Fraud Score Analysis" in txt and "NEW_ACCOUNT_LARGE_TX (+30)" in txt
+
+
+def test_onnx_fraud_model_cpu():
+    from igaming_platform_amd.onnx import builders
+    cfg = Config()
+    cfg.features.width = 32
+    m = builders.build("logistic", n_features=32).SerializeToString()
+    eng = RiskEngine(cfg, backend="cpu", capacity=50, fraud_model=m)
+    r = eng.score([dict(account_id="m", amount=1000, transaction_type="deposit")], now=NOW)[0]
+    assert 0.0 < r["ml_score"] < 1.0 and eng.model_kind == "onnx"
