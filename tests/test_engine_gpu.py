@@ -1,0 +1,128 @@
+"""GPU engine end-to-end: the same request stream through a GPU engine and a CPU (golden)
+engine must give the same decisions; LTV / abuse / features / snapshots on the device."""
+import numpy as np
+import pytest
+
+from igaming_platform_amd.config import Config
+from igaming_platform_amd.golden import ltv as GL
+from igaming_platform_amd.layouts import ACCTBATCH
+
+pytestmark = pytest.mark.gpu
+NOW = 1_760_000_000
+
+
+def _txs(n, rng, n_acc=40):
+    types = ["deposit", "withdraw", "bet", "win", "bonus"]
+    return [dict(account_id=f"acc-{int(a)}", amount=int(rng.choice([500, 5000, 150000, 2_000_000])),
+                 transaction_type=types[int(rng.integers(0, 5))], device_id=f"dev-{int(a)}-{int(rng.integers(0, 5))}",
+                 ip_address=f"10.1.{int(a)}.{int(rng.integers(0, 7))}", fingerprint=f"fp-{int(a)}")
+            for a in rng.integers(0, n_acc, n)]
+
+
+def _engines(**kw):
+    from igaming_platform_amd.engine.risk_engine import RiskEngine
+    cfg = Config()
+    cfg.gpu.buckets = [64, 256, 1024]
+    cfg.gpu.max_batch = 1024
+    g = RiskEngine(cfg, backend="gpu", capacity=4096, **kw)
+    c = RiskEngine(cfg, backend="cpu", capacity=4096, **kw)
+    rng = np.random.default_rng(0)
+    ids = [f"acc-{i}" for i in range(40)]
+    rows = np.zeros(40, ACCTBATCH)
+    rows["present"] = 1
+    rows["total_deposits"] = rng.integers(0, 10**6, 40)
+    rows["total_withdrawals"] = rng.integers(0, 10**6, 40)
+    rows["deposit_count"] = rng.integers(0, 5, 40)
+    rows["bonus_claim_count"] = rng.integers(0, 6, 40)
+    rows["account_created_at"] = NOW - rng.integers(0, 30, 40) * 86400
+    for e in (g, c):
+        e.load_batch_features(ids, rows)
+        e.add_to_blacklist("device", "dev-3-1", "x", "t")
+        e.set_ip_intel("10.1.5.2", vpn=True)
+    return g, c
+
+
+def test_gpu_engine_matches_cpu_engine_heuristic():
+    g, c = _engines()
+    rng = np.random.default_rng(1)
+    for step in range(5):
+        txs = _txs(300, rng)
+        a = g.score(txs, now=NOW + step * 30)
+        b = c.score(txs, now=NOW + step * 30)
+        for x, y in zip(a, b):
+            assert (x["score"], x["action"], x["reason_codes"], x["rule_score"]) == \
+                   (y["score"], y["action"], y["reason_codes"], y["rule_score"])
+            assert x["ml_score"] == pytest.approx(y["ml_score"], abs=1e-6)
+    for i in range(40):
+        fg, fc = g.get_features(f"acc-{i}", now=NOW + 200), c.get_features(f"acc-{i}", now=NOW + 200)
+        for k in ("tx_count_1h", "tx_sum_1h", "unique_devices_24h", "unique_ips_24h", "time_since_last_tx_sec"):
+            assert fg[k] == fc[k], (i, k)
+
+
+def test_gpu_engine_with_stacked_model_close_to_cpu():
+    from igaming_platform_amd.onnx import builders
+    cfg_w = 128
+    m = builders.build("stacked", n_trees=20, depth=5).SerializeToString()
+    from igaming_platform_amd.engine.risk_engine import RiskEngine
+    cfg = Config()
+    cfg.features.width = cfg_w
+    cfg.gpu.buckets = [64, 256]
+    cfg.gpu.max_batch = 256
+    g = RiskEngine(cfg, backend="gpu", capacity=1024, fraud_model=m)
+    c = RiskEngine(cfg, backend="cpu", capacity=1024, fraud_model=m)
+    txs = _txs(200, np.random.default_rng(3))
+    a, b = g.score(txs, now=NOW), c.score(txs, now=NOW)
+    ml_a = np.array([x["ml_score"] for x in a])
+    ml_b = np.array([x["ml_score"] for x in b])
+    np.testing.assert_allclose(ml_a, ml_b, atol=2e-2)   # bf16 MFMA head vs fp32 executor
+    assert np.mean([x["rule_score"] == y["rule_score"] for x, y in zip(a, b)]) == 1.0
+
+
+def test_gpu_ltv_matches_cpu():
+    from igaming_platform_amd.onnx import builders
+    m = builders.build("ltv_mlp", n_features=256, width=512, layers=4).SerializeToString()
+    g, c = _engines(ltv_model=m)
+    rng = np.random.default_rng(4)
+    players = [GL.PlayerFeatures(days_since_registration=int(rng.integers(1, 900)),
+                                 days_since_last_bet=int(rng.integers(0, 60)),
+                                 days_since_last_deposit=int(rng.integers(0, 90)),
+                                 sessions_per_week=float(rng.uniform(0, 8)), net_revenue=float(rng.uniform(-500, 30000)),
+                                 deposit_frequency=float(rng.uniform(0, 6)), bet_count=int(rng.integers(0, 400)),
+                                 support_tickets=int(rng.integers(0, 6))) for _ in range(100)]
+    ids = [f"p{i}" for i in range(100)]
+    for e in (g, c):
+        e.set_players(ids, players)
+    rg, rc = g.predict_ltv_batch(ids), c.predict_ltv_batch(ids)
+    for x, y in zip(rg, rc):
+        assert x.churn_risk == pytest.approx(y.churn_risk) and x.survival_days == y.survival_days
+        assert x.predicted_ltv == pytest.approx(y.predicted_ltv, rel=3e-2, abs=1.0)
+        assert x.confidence == pytest.approx(y.confidence)
+
+
+def test_gpu_abuse_gru_matches_cpu():
+    from igaming_platform_amd.onnx import builders
+    m = builders.build("gru", seq=100, hidden=256, layers=2).SerializeToString()
+    g, c = _engines(abuse_model=m)
+    ev = [dict(account_id=f"acc-{i % 10}", amount=100 * (i % 13) + 1, transaction_type=["deposit", "bet"][i % 2],
+               device_id=f"d{i % 3}", ts=NOW - 500 + i) for i in range(150)]
+    g.ingest_events(ev)
+    c.ingest_events(ev)
+    for i in range(10):
+        a = g.check_bonus_abuse(f"acc-{i}", now=NOW)
+        b = c.check_bonus_abuse(f"acc-{i}", now=NOW)
+        assert a.model_score == pytest.approx(b.model_score, abs=1e-2)
+        assert a.signals[:1] == b.signals[:1]
+
+
+def test_gpu_snapshot_restore(tmp_path):
+    g, _ = _engines()
+    g.score(_txs(100, np.random.default_rng(5)), now=NOW)
+    g.snapshot(str(tmp_path))
+    from igaming_platform_amd.engine.risk_engine import RiskEngine
+    cfg = Config()
+    cfg.gpu.buckets = [64, 256, 1024]
+    cfg.gpu.max_batch = 1024
+    h = RiskEngine(cfg, backend="gpu", capacity=4096)
+    h.restore(str(tmp_path))
+    for i in range(40):
+        assert g.get_features(f"acc-{i}", now=NOW + 3).tobytes() == h.get_features(f"acc-{i}", now=NOW + 3).tobytes()
