@@ -72,7 +72,9 @@ class CpuBackend:
         v = (self.blacklist.table.version, self.ipintel.table.version)
         if v == self._tables_version:
             return
-        self.store.blacklist = dict(self.blacklist.active_keys(0))
+        # from the hash tables (what every rank holds), exactly like the device probe (K7)
+        b = self.blacklist.table
+        self.store.blacklist = {int(k): int(x) for k, x in zip(b.keys, b.vals) if int(k) != 0}
         t = self.ipintel.table
         self.store.ip_intel = {int(k): int(x) for k, x in zip(t.keys.view(np.uint64), t.vals) if int(k) != 0}
         self._tables_version = v

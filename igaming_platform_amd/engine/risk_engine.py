@@ -55,7 +55,9 @@ def _load_onnx(src):
 class RiskEngine:
     def __init__(self, cfg: Optional[Config] = None, backend: str = "auto", devices: Optional[Sequence[int]] = None,
                  capacity: Optional[int] = None, fraud_model=None, ltv_model=None, abuse_model=None,
-                 shards: int = 1, capture: bool = True, faults: Optional[Faults] = None):
+                 shards: int = 1, capture: bool = True, faults: Optional[Faults] = None, spmd=None):
+        """``spmd``: a comm (parallel.comm.TorchComm) when this is rank 0 of a one-process-per-GPU
+        group; every other rank runs :func:`serve_shard`. Accounts are then owned by ranks."""
         import copy
         self.cfg = copy.deepcopy(cfg) if cfg is not None else Config()
         cfg = self.cfg
@@ -72,7 +74,12 @@ class RiskEngine:
             except Exception:
                 pass
         self.kind = backend
-        if backend == "gpu":
+        self.group = None
+        if spmd is not None:
+            import torch
+            self.devices = [torch.cuda.current_device()] if backend == "gpu" else []
+            world = spmd.world
+        elif backend == "gpu":
             import torch
             if devices is None:
                 devices = list(range(min(max(cfg.gpu.devices, 1), torch.cuda.device_count())))
@@ -102,7 +109,16 @@ class RiskEngine:
         self.fraud_onnx = fm
         self.backends: List = []
         self.healthy = [True] * world
-        if backend == "gpu":
+        if spmd is not None:
+            from ..parallel.spmd import ShardProxy, ShardRunner, SpmdGroup
+            local = make_local_backend(cfg, backend, self.capacity, fm, mkind, self.blacklist, self.ipintel,
+                                       owner_filter=True, rank=0, capture=capture)
+            self.local = local
+            self._abuse_am = abuse_model if abuse_model is not None else cfg.abuse_model.path
+            abuse_gpu = make_abuse_gpu(cfg, local, self._abuse_am)
+            self.group = SpmdGroup(spmd, ShardRunner(spmd, local, abuse_gpu))
+            self.backends = [ShardProxy(self.group, o, local) for o in range(world)]
+        elif backend == "gpu":
             from ..models.plan import compile_onnx, to_device
             for r, d in enumerate(self.devices):
                 plan = to_device(compile_onnx(fm), f"cuda:{d}") if mkind == "onnx" else None
@@ -123,7 +139,21 @@ class RiskEngine:
         lm = _load_onnx(ltv_model if ltv_model is not None else cfg.ltv_model.path)
         am = _load_onnx(abuse_model if abuse_model is not None else cfg.abuse_model.path)
         ltv_width = int(lm.inputs()[0][2][-1]) if lm is not None else 0
-        if backend == "gpu":
+        if spmd is not None:
+            lg = None
+            if backend == "gpu":
+                from ..models.plan import compile_onnx, to_device
+                dev = f"cuda:{self.devices[0]}"
+                g = LtvGpu(dev, to_device(compile_onnx(lm), dev) if lm is not None else None, buckets=cfg.gpu.buckets,
+                           in_width=ltv_width, use_graphs=capture)
+                g.capture()
+                lg = [g]
+            self.ltv = LtvService(self.registry, world, gpu=lg, model_width=ltv_width,
+                                  executor=N.Executor(lm) if (lm is not None and lg is None) else None)
+            self.abuse = AbuseService(self, threshold=cfg.abuse.threshold, group=self.group,
+                                      executor=N.Executor(am) if (am is not None and backend != "gpu") else None,
+                                      group_model=am is not None and backend == "gpu")
+        elif backend == "gpu":
             from ..models.plan import compile_onnx, to_device
             lg = []
             for d in self.devices:
@@ -169,6 +199,14 @@ class RiskEngine:
         slots, owners, _ = self.registry.resolve_batch(rb, insert=True)
         req = np.empty(n, REQREC)
         rb.pack_reqrec(slots, req.view(np.uint8), now, None)
+        if self.group is not None:
+            req["tx_type"] |= owners.astype(np.int32) << 8
+            res, feats = self.group.score(req, now, want_features)
+            cols = rb.columns()
+            self.links.add(cols["device_hash"], (owners.astype(np.int64) << 32) | np.where(slots >= 0, slots, -1))
+            self.metrics.observe_results(res)
+            self.metrics.batch_size.observe(n)
+            return res, feats, slots, owners
         res = np.zeros((n, 2), np.uint32)
         feats = np.zeros(n, FEATREC) if want_features else None
         groups = [(0, None)] if self.world == 1 else [(o, np.nonzero(owners == o)[0]) for o in range(self.world)]
@@ -339,6 +377,9 @@ class RiskEngine:
             self._push_config()
 
     def _push_config(self) -> None:
+        if self.group is not None:
+            self.backends[0].refresh_config(self.scoring)
+            return
         for be in self.backends:
             be.refresh_config(self.scoring)
         if self.fallback is not None:
@@ -426,6 +467,12 @@ class RiskEngine:
         return [self.registry.id_of(int(k) >> 32, int(k) & 0xFFFFFFFF) for k in keys]
 
     # ---- health / durability
+    def close(self) -> None:
+        """Release the SPMD workers (rank 0 only)."""
+        if self.group is not None:
+            self.group.stop()
+            self.group = None
+
     def health(self) -> Dict:
         return dict(backend=self.kind, shards=self.world, healthy=list(self.healthy),
                     accounts=[self.registry.size(o) for o in range(self.world)],
@@ -441,11 +488,15 @@ class RiskEngine:
         for o in range(self.world):
             n = self.registry.size(o)
             meta["ids"].append([self.registry.id_of(o, s) for s in range(n)])
+            if self.group is not None:
+                continue
             be = self.backends[o]
             if be.kind == "gpu":
                 be.store.snapshot(os.path.join(directory, f"shard{o}.npz"), n_used=max(n, 1))
             else:
                 be.snapshot(os.path.join(directory, f"shard{o}.json"))
+        if self.group is not None:
+            self.group.snapshot(directory, [self.registry.size(o) for o in range(self.world)])
         tmp = os.path.join(directory, "registry.json.tmp")
         with open(tmp, "w") as f:
             json.dump(meta, f)
@@ -463,10 +514,65 @@ class RiskEngine:
                 got, _ = self.registry.index[o].lookup(ids, True)
                 if list(got) != list(range(len(ids))):
                     raise ValueError("registry must be empty before restore")
+            total += len(ids)
+            if self.group is not None:
+                continue
             be = self.backends[o]
             if be.kind == "gpu":
                 be.store.restore(os.path.join(directory, f"shard{o}.npz"))
             else:
                 be.restore(os.path.join(directory, f"shard{o}.json"))
-            total += len(ids)
+        if self.group is not None:
+            self.group.restore(directory)
         return total
+
+
+# ============================================================================ shard construction
+def make_local_backend(cfg: Config, kind: str, capacity: int, fm, mkind: str, blacklist, ipintel,
+                       owner_filter: bool = False, rank: int = 0, capture: bool = True):
+    """The backend of THIS process's shard (used by SPMD rank 0 and by every worker rank)."""
+    if kind == "gpu":
+        import torch
+        from ..models.plan import compile_onnx, to_device
+        dev = f"cuda:{torch.cuda.current_device()}"
+        plan = to_device(compile_onnx(fm), dev) if mkind == "onnx" else None
+        model = {"onnx": "plan", "heuristic": "heuristic", "none": "none"}[mkind]
+        return GpuBackend(cfg, capacity, dev, plan=plan, model=model, blacklist=blacklist, ipintel=ipintel,
+                          capture=capture, owner_filter=owner_filter, rank=rank)
+    N = native()
+    if mkind == "onnx":
+        from ..models.plan import compile_onnx
+        ml_col, out_name = 0, cfg.fraud_model.output_name
+        try:
+            p = compile_onnx(fm)
+            ml_col, out_name = p.ml_col, p.output_name
+        except Exception:
+            pass
+        return CpuBackend(cfg, model="plan", executor=N.Executor(fm), input_name=fm.inputs()[0][0],
+                          output_name=out_name, ml_col=ml_col, blacklist=blacklist, ipintel=ipintel)
+    return CpuBackend(cfg, model=mkind, blacklist=blacklist, ipintel=ipintel)
+
+
+def make_abuse_gpu(cfg: Config, local, abuse_model):
+    am = _load_onnx(abuse_model)
+    if am is None or local.kind != "gpu":
+        return None
+    from ..models.plan import compile_onnx, to_device
+    from .abuse import AbuseGpu
+    return AbuseGpu(local.store, to_device(compile_onnx(am), str(local.device)), bmax=max(cfg.gpu.buckets))
+
+
+def serve_shard(cfg: Config, comm, backend: str = "gpu", capacity: Optional[int] = None, fraud_model=None,
+                abuse_model=None, capture: bool = True) -> int:
+    """Worker rank (>= 1) of an SPMD group: build the same local shard as rank 0 and serve
+    its ops until rank 0 stops the group."""
+    from ..parallel.spmd import run_worker
+    fm = _load_onnx(fraud_model if fraud_model is not None else cfg.fraud_model.path)
+    mkind = cfg.fraud_model.kind
+    if mkind == "auto":
+        mkind = "onnx" if fm is not None else "heuristic"
+    local = make_local_backend(cfg, backend, int(capacity or cfg.gpu.accounts_per_gpu), fm, mkind,
+                               Blacklist(cfg.gpu.blacklist_capacity), IPIntel(cfg.gpu.blacklist_capacity),
+                               owner_filter=True, rank=comm.rank, capture=capture)
+    abuse_gpu = make_abuse_gpu(cfg, local, abuse_model if abuse_model is not None else cfg.abuse_model.path)
+    return run_worker(comm, local, abuse_gpu)

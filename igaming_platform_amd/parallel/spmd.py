@@ -1,0 +1,292 @@
+"""SPMD multi-GPU serving: one process per GPU, rank 0 runs the API.
+
+Data parallelism by account owner (``owner = XXH64(account_id) % world``):
+every account's feature state lives on exactly one rank. Per ScoreBatch / micro-batch:
+
+  rank 0: registry resolves (owner, slot) for every request -> REQREC rows with the owner
+          in bits 8-15 of ``tx_type``  --broadcast-->  all ranks
+  rank r: scores the whole slab with ``owner_filter`` on (rows it does not own come out as
+          all-zero records, never touching its shard) and score-then-updates its own rows
+  all:    one all_reduce(SUM) of [ResultRec | FeatRec] — exactly one rank contributes each
+          row, so the sum IS the merged result, bit for bit.
+
+Cold-path ops (thresholds, blacklist/ip tables, warehouse rows, GetFeatures, event
+histories, GRU abuse scores) use the same broadcast-then-reduce protocol. Collectives go
+through :mod:`.comm` (RCCL over xGMI for GPUs, gloo on CPU).
+"""
+from __future__ import annotations
+
+import dataclasses
+import io
+import json
+from typing import Optional
+
+import numpy as np
+
+from ..config import RuleWeights, ScoringConfig
+from ..layouts import ACCTBATCH, FEATREC, REQREC
+
+OP_SCORE, OP_INGEST, OP_CONFIG, OP_TABLES, OP_BATCH, OP_EXT, OP_FEATURES, OP_RESET, OP_STOP, OP_EVHIST, \
+    OP_ABUSE, OP_SNAPSHOT, OP_RESTORE = range(1, 14)
+
+
+def owners_of(req: np.ndarray) -> np.ndarray:
+    return (req["tx_type"] >> 8) & 0xFF
+
+
+def _tables_bytes(blacklist, ipintel) -> bytes:
+    buf = io.BytesIO()
+    bt, it = blacklist.table, ipintel.table
+    np.savez(buf, bl_keys=bt.keys, bl_vals=bt.vals, bl_meta=np.array([bt.max_probe, bt.n], np.int64),
+             ip_keys=it.keys, ip_vals=it.vals, ip_meta=np.array([it.max_probe, it.n], np.int64))
+    return buf.getvalue()
+
+
+def _load_tables(data: bytes, blacklist, ipintel) -> None:
+    with np.load(io.BytesIO(data), allow_pickle=False) as z:
+        for tab, p in ((blacklist.table, "bl"), (ipintel.table, "ip")):
+            if len(z[f"{p}_keys"]) != tab.cap:
+                raise ValueError("table capacity differs across ranks")
+            with tab._lock:
+                tab.keys[:] = z[f"{p}_keys"]
+                tab.vals[:] = z[f"{p}_vals"]
+                tab.max_probe, tab.n = int(z[f"{p}_meta"][0]), int(z[f"{p}_meta"][1])
+                tab.version += 1
+
+
+def scoring_to_json(s: ScoringConfig) -> bytes:
+    return json.dumps(dataclasses.asdict(s)).encode()
+
+
+def scoring_from_json(b: bytes) -> ScoringConfig:
+    d = json.loads(b.decode())
+    d["weights"] = RuleWeights(**d["weights"])
+    return ScoringConfig(**d)
+
+
+class ShardRunner:
+    """What every rank (0 included) executes for one op on its local backend."""
+
+    def __init__(self, comm, backend, abuse_gpu=None):
+        self.comm = comm
+        self.be = backend
+        self.rank = comm.rank
+        self.abuse_gpu = abuse_gpu
+
+    def _mine(self, owners: np.ndarray) -> np.ndarray:
+        return owners == self.rank
+
+    def score(self, req: np.ndarray, now: int, want_features: bool) -> np.ndarray:
+        n = len(req)
+        mine = self._mine(owners_of(req))
+        res = np.zeros((n, 2), np.uint32)
+        feats = np.zeros(n, FEATREC)
+        if self.be.kind == "gpu":
+            r, f = self.be.score(req, now, want_features)  # owner_filter: foreign rows are inert zeros
+            res[:] = r
+            if want_features:
+                feats[mine] = f[mine]
+        elif np.any(mine):
+            r, f = self.be.score(req[mine], now, want_features)
+            res[mine] = r
+            if want_features:
+                feats[mine] = f
+        words = [res.astype(np.int64).reshape(-1)]
+        if want_features:
+            words.append(feats.view(np.int64).reshape(-1))
+        return self.comm.sum_i64(np.concatenate(words))
+
+    def handle(self, op: int, hdr: np.ndarray, payload: bytes):
+        n, now, aux, aux2 = int(hdr[1]), int(hdr[2]), int(hdr[3]), int(hdr[4])
+        if op == OP_SCORE:
+            return self.score(np.frombuffer(payload, REQREC).copy(), now, bool(aux))
+        if op == OP_INGEST:
+            ev = np.frombuffer(payload, REQREC).copy()
+            mine = self._mine(owners_of(ev))
+            if np.any(mine):
+                self.be.ingest(ev[mine])
+            return None
+        if op == OP_CONFIG:
+            self.be.refresh_config(scoring_from_json(payload))
+            return None
+        if op == OP_TABLES:
+            _load_tables(payload, self.be.blacklist, self.be.ipintel)
+            self.be.refresh_config(None)
+            return None
+        if op in (OP_BATCH, OP_EXT, OP_RESET):
+            slots = np.frombuffer(payload[:4 * n], np.int32)
+            owners = np.frombuffer(payload[4 * n:8 * n], np.int32)
+            mine = self._mine(owners)
+            body = payload[8 * n:]
+            if np.any(mine):
+                if op == OP_BATCH:
+                    self.be.set_batch_rows(slots[mine], np.frombuffer(body, ACCTBATCH)[mine])
+                elif op == OP_EXT:
+                    self.be.set_ext(slots[mine], np.frombuffer(body, np.float32).reshape(n, -1)[mine])
+                else:
+                    self.be.reset_accounts(slots[mine])
+            return None
+        if op == OP_FEATURES:  # aux = owner, aux2 = slot
+            rec = np.zeros(1, FEATREC)
+            if aux == self.rank:
+                rec[0] = self.be.features(aux2, now)
+            return self.comm.sum_i64(rec.view(np.int64).reshape(-1))
+        if op == OP_EVHIST:
+            h = None
+            if aux == self.rank:
+                h = np.ascontiguousarray(self.be.event_history(aux2), np.float32)
+            shape = np.asarray(hdr[5:7], np.int64)
+            buf = np.zeros(int(shape[0]) * int(shape[1]), np.float32) if h is None else h.reshape(-1)
+            return self.comm.sum_i64(np.pad(buf, (0, len(buf) % 2)).view(np.int64))
+        if op == OP_ABUSE:
+            slots = np.frombuffer(payload[:4 * n], np.int32)
+            owners = np.frombuffer(payload[4 * n:8 * n], np.int32)
+            out = np.zeros(n, np.float32)
+            mine = self._mine(owners)
+            if np.any(mine) and self.abuse_gpu is not None:
+                out[mine] = self.abuse_gpu.score_slots(slots[mine])
+            return self.comm.sum_i64(np.pad(out, (0, n % 2)).view(np.int64))
+        if op in (OP_SNAPSHOT, OP_RESTORE):  # payload: {"dir": ..., "used": [slots in use per rank]}
+            import os
+            meta = json.loads(payload.decode())
+            path = os.path.join(meta["dir"], f"shard{self.rank}." + ("npz" if self.be.kind == "gpu" else "json"))
+            if op == OP_SNAPSHOT:
+                if self.be.kind == "gpu":
+                    self.be.store.snapshot(path, n_used=max(int(meta["used"][self.rank]), 1))
+                else:
+                    self.be.snapshot(path)
+            elif self.be.kind == "gpu":
+                self.be.store.restore(path)
+            else:
+                self.be.restore(path)
+            self.comm.barrier()
+            return None
+        raise ValueError(f"unknown op {op}")
+
+
+class SpmdGroup:
+    """Rank 0's handle on the group: issues an op to every rank and runs its own share."""
+
+    def __init__(self, comm, runner: ShardRunner):
+        if comm.rank != 0:
+            raise ValueError("SpmdGroup lives on rank 0; other ranks call run_worker()")
+        self.comm = comm
+        self.runner = runner
+        self.world = comm.world
+
+    def _issue(self, op: int, payload: bytes = b"", n: int = 0, now: int = 0, aux: int = 0, aux2: int = 0,
+               extra=(0, 0)):
+        hdr = np.array([op, n, now, aux, aux2, extra[0], extra[1], 0], np.int64)
+        self.comm.bcast_i64(hdr, 0)
+        self.comm.bcast_bytes(payload, 0)
+        return self.runner.handle(op, hdr, payload)
+
+    # ---- hot path
+    def score(self, req: np.ndarray, now: int, want_features: bool = True):
+        n = len(req)
+        out = self._issue(OP_SCORE, np.ascontiguousarray(req).tobytes(), n=n, now=now, aux=int(want_features))
+        res = out[:2 * n].astype(np.uint32).reshape(n, 2)
+        feats = out[2 * n:].view(FEATREC).copy() if want_features else None
+        return res, feats
+
+    # ---- cold path
+    def ingest(self, ev: np.ndarray) -> None:
+        self._issue(OP_INGEST, np.ascontiguousarray(ev).tobytes(), n=len(ev))
+
+    def refresh_config(self, scoring: ScoringConfig) -> None:
+        self._issue(OP_CONFIG, scoring_to_json(scoring))
+
+    def sync_tables(self, blacklist, ipintel) -> None:
+        self._issue(OP_TABLES, _tables_bytes(blacklist, ipintel))
+
+    def _rows(self, op, slots, owners, body: bytes = b"") -> None:
+        n = len(slots)
+        self._issue(op, np.asarray(slots, np.int32).tobytes() + np.asarray(owners, np.int32).tobytes() + body, n=n)
+
+    def set_batch_rows(self, slots, owners, rows) -> None:
+        self._rows(OP_BATCH, slots, owners, np.ascontiguousarray(rows, ACCTBATCH).tobytes())
+
+    def set_ext(self, slots, owners, ext) -> None:
+        self._rows(OP_EXT, slots, owners, np.ascontiguousarray(ext, np.float32).tobytes())
+
+    def reset_accounts(self, slots, owners) -> None:
+        self._rows(OP_RESET, slots, owners)
+
+    def features(self, owner: int, slot: int, now: int) -> np.ndarray:
+        return self._issue(OP_FEATURES, now=now, aux=owner, aux2=slot).view(FEATREC)[0].copy()
+
+    def event_history(self, owner: int, slot: int, shape) -> np.ndarray:
+        out = self._issue(OP_EVHIST, aux=owner, aux2=slot, extra=shape)
+        return out.view(np.float32)[: shape[0] * shape[1]].reshape(shape).copy()
+
+    def abuse_scores(self, slots, owners) -> np.ndarray:
+        n = len(slots)
+        out = self._issue(OP_ABUSE, np.asarray(slots, np.int32).tobytes() + np.asarray(owners, np.int32).tobytes(),
+                          n=n)
+        return out.view(np.float32)[:n].copy()
+
+    def snapshot(self, directory: str, used) -> None:
+        self._issue(OP_SNAPSHOT, json.dumps({"dir": directory, "used": [int(u) for u in used]}).encode())
+
+    def restore(self, directory: str) -> None:
+        self._issue(OP_RESTORE, json.dumps({"dir": directory, "used": []}).encode())
+
+    def stop(self) -> None:
+        hdr = np.array([OP_STOP, 0, 0, 0, 0, 0, 0, 0], np.int64)
+        self.comm.bcast_i64(hdr, 0)
+        self.comm.bcast_bytes(b"", 0)
+
+
+def run_worker(comm, backend, abuse_gpu=None) -> int:
+    """Loop of ranks >= 1 until rank 0 sends STOP. Returns the number of ops served."""
+    runner = ShardRunner(comm, backend, abuse_gpu)
+    served = 0
+    while True:
+        hdr = comm.bcast_i64(np.zeros(8, np.int64), 0)
+        payload = comm.bcast_bytes(None, 0)
+        op = int(hdr[0])
+        if op == OP_STOP:
+            return served
+        runner.handle(op, hdr, payload)
+        served += 1
+
+
+class ShardProxy:
+    """Backend-shaped handle for owner ``o`` of an SPMD group (cold-path ops only; the
+    engine sends scoring batches to the whole group at once)."""
+
+    kind = "spmd"
+
+    def __init__(self, group: SpmdGroup, owner: int, local):
+        self.g, self.o, self.local = group, owner, local
+        self.blacklist, self.ipintel = local.blacklist, local.ipintel
+
+    def refresh_config(self, scoring=None) -> None:
+        if self.o == 0:  # one broadcast for the whole group
+            self.g.sync_tables(self.blacklist, self.ipintel)
+            if scoring is not None:
+                self.g.refresh_config(scoring)
+
+    def ingest(self, ev: np.ndarray) -> None:
+        ev = ev.copy()
+        ev["tx_type"] = (ev["tx_type"] & 0xFF) | (self.o << 8)
+        self.g.ingest(ev)
+
+    def set_batch_rows(self, slots, rows) -> None:
+        self.g.set_batch_rows(slots, np.full(len(slots), self.o, np.int32), rows)
+
+    def set_ext(self, slots, ext) -> None:
+        self.g.set_ext(slots, np.full(len(slots), self.o, np.int32), ext)
+
+    def reset_accounts(self, slots) -> None:
+        self.g.reset_accounts(slots, np.full(len(slots), self.o, np.int32))
+
+    def features(self, slot: int, now: int) -> np.ndarray:
+        return self.g.features(self.o, int(slot), now)
+
+    def event_history(self, slot: int) -> np.ndarray:
+        shape = self.local.event_history(0).shape
+        return self.g.event_history(self.o, int(slot), shape)
+
+    def metrics(self):
+        return None

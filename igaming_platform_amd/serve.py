@@ -21,15 +21,18 @@ from .config import Config
 from .obs.logging import get_logger, setup_logger
 
 
-def build_engine(a, cfg: Config):
+def _fraud_model(a, cfg: Config):
+    if not a.synthetic_model:
+        return None
+    from .onnx import builders
+    kw = {"n_features": cfg.features.width} if a.synthetic_model == "logistic" else {}
+    return builders.build(a.synthetic_model, **kw).SerializeToString()
+
+
+def build_engine(a, cfg: Config, comm=None):
     from .engine.risk_engine import RiskEngine
-    fraud = None
-    if a.synthetic_model:
-        from .onnx import builders
-        kw = {"n_features": cfg.features.width} if a.synthetic_model == "logistic" else {}
-        fraud = builders.build(a.synthetic_model, **kw).SerializeToString()
-    return RiskEngine(cfg, backend=a.backend, fraud_model=fraud, capacity=a.accounts or None,
-                      shards=a.shards)
+    return RiskEngine(cfg, backend=a.backend, fraud_model=_fraud_model(a, cfg), capacity=a.accounts or None,
+                      shards=a.shards, spmd=comm)
 
 
 def main(argv=None) -> int:
@@ -49,9 +52,25 @@ def main(argv=None) -> int:
     if a.gpus:
         cfg.gpu.devices = a.gpus
     log = setup_logger(cfg.server.log_level)
+    comm = None
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        # one process per GPU (torchrun): rank 0 serves the API, the others own their shards
+        import torch
+        from .parallel.comm import init_from_env
+        backend = a.backend if a.backend != "auto" else ("gpu" if torch.cuda.is_available() else "cpu")
+        a.backend = backend
+        if backend == "gpu":
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        comm = init_from_env("nccl" if backend == "gpu" else "gloo",
+                             device=f"cuda:{torch.cuda.current_device()}" if backend == "gpu" else None)
+        if comm.rank != 0:
+            from .engine.risk_engine import serve_shard
+            n = serve_shard(cfg, comm, backend=backend, capacity=a.accounts or None, fraud_model=_fraud_model(a, cfg))
+            log.info("shard worker stopped", extra={"fields": dict(rank=comm.rank, ops=n)})
+            return 0
     from .api.grpc_server import RiskServer
     from .api.http_server import HttpServer
-    eng = build_engine(a, cfg)
+    eng = build_engine(a, cfg, comm)
     if a.snapshot_dir and os.path.exists(os.path.join(a.snapshot_dir, "registry.json")):
         n = eng.restore(a.snapshot_dir)
         log.info("feature store restored", extra={"fields": dict(accounts=n, dir=a.snapshot_dir)})
@@ -74,6 +93,7 @@ def main(argv=None) -> int:
     hs.stop()
     if a.snapshot_dir:
         eng.snapshot(a.snapshot_dir)
+    eng.close()
     log.info("server stopped")
     return 0
 
