@@ -204,10 +204,25 @@ PYBIND11_MODULE(_hipk, m) {
     LtvArgs a{};
     a.pf = ptr<const float*>(d, "pf");
     a.ltv_model = ptr<const float*>(d, "ltv_model");
+    a.slots = ptr<const int32_t*>(d, "slots");
     a.out = ptr<float*>(d, "out");
     a.B = geti(d, "B");
     launch_ltv(a, stream_of(s));
     check("ltv");
+  });
+  m.def("ltv_assemble", [](py::dict d, uintptr_t s) {
+    LtvAssembleArgs a{};
+    a.slots = ptr<const int32_t*>(d, "slots");
+    a.pf_tab = ptr<const float*>(d, "pf_tab");
+    a.ext_tab = ptr<const float*>(d, "ext_tab");
+    a.ext_w = geti(d, "ext_w");
+    a.X = ptr<float*>(d, "X");
+    a.x_w = geti(d, "x_w");
+    a.m_ptr = ptr<const int32_t*>(d, "m_ptr");
+    a.n_rows = geti(d, "n_rows");
+    if (!a.slots || !a.pf_tab || !a.X || a.x_w < 25) throw std::runtime_error("ltv_assemble: bad args");
+    launch_ltv_assemble(a, stream_of(s));
+    check("ltv_assemble");
   });
   m.def("gru", [](py::dict d, uintptr_t s) {
     GruArgs a{};

@@ -171,11 +171,25 @@ void launch_gru(const GruArgs& a, hipStream_t st);
 
 // ---- K9 LTV / churn / segment
 struct LtvArgs {
-  const float* pf;          // [B][25] player features (golden.ltv.PLAYER_COLUMNS)
+  const float* pf;          // [B][25] player features (golden.ltv.PLAYER_COLUMNS), or the table when slots != null
+  const int32_t* slots;     // [B] rows of the device-resident player table (nullable; -1 -> empty profile)
   const float* ltv_model;   // [B] learned LTV (nullable -> formula)
   float* out;               // [B][6]: ltv, churn, survival, confidence, segment, nba
   int32_t B;
 };
 void launch_ltv(const LtvArgs& a, hipStream_t st);
+
+// LTV model input from the device-resident tables: X[r] = [sign*log1p|pf[slot]| (25) | ext[slot] (ext_w)]
+struct LtvAssembleArgs {
+  const int32_t* slots;
+  const float* pf_tab;      // [C][25]
+  const float* ext_tab;     // [C][ext_w] (nullable)
+  int32_t ext_w;
+  float* X;                 // [rows][x_w], x_w = 25 + ext_w
+  int32_t x_w;
+  const int32_t* m_ptr;     // live rows (nullable)
+  int32_t n_rows;
+};
+void launch_ltv_assemble(const LtvAssembleArgs& a, hipStream_t st);
 
 }  // namespace igp

@@ -26,9 +26,18 @@ __device__ double engagement(const float* p) {
 }
 
 __global__ void ltv_kernel(LtvArgs a) {
+  __shared__ float zero_row[P_NCOLS];
+  if (threadIdx.x < P_NCOLS) zero_row[threadIdx.x] = 0.f;
+  __syncthreads();  // before any early exit: every thread of the block reaches it
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.B) return;
-  const float* p = a.pf + (size_t)i * P_NCOLS;
+  const float* p;
+  if (a.slots) {
+    const int s = a.slots[i];
+    p = s >= 0 ? a.pf + (size_t)s * P_NCOLS : zero_row;
+  } else {
+    p = a.pf + (size_t)i * P_NCOLS;
+  }
   const int dsr = (int)p[P_DSR], dsld = (int)p[P_DSLD], dslb = (int)p[P_DSLB];
   const double spw = p[P_SPW], net = p[P_NET], df = p[P_DFREQ];
   // churn (ltv.go:228-262)
@@ -82,6 +91,31 @@ __global__ void ltv_kernel(LtvArgs a) {
   o[3] = (float)c;
   o[4] = (float)seg;
   o[5] = (float)nba;
+}
+
+// element-parallel gather: consecutive threads write consecutive columns of a row
+__global__ void __launch_bounds__(256) ltv_assemble_kernel(LtvAssembleArgs a) {
+  const int n_live = a.m_ptr ? min(*a.m_ptr, a.n_rows) : a.n_rows;
+  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const int r = (int)(idx / a.x_w), c = (int)(idx % a.x_w);
+  if (r >= a.n_rows) return;
+  float v = 0.f;
+  const int s = r < n_live ? a.slots[r] : -1;
+  if (s >= 0) {
+    if (c < P_NCOLS) {
+      const float x = a.pf_tab[(size_t)s * P_NCOLS + c];
+      v = copysignf(log1pf(fabsf(x)), x);
+    } else if (a.ext_tab && c - P_NCOLS < a.ext_w) {
+      v = a.ext_tab[(size_t)s * a.ext_w + (c - P_NCOLS)];
+    }
+  }
+  a.X[(size_t)r * a.x_w + c] = v;
+}
+
+void launch_ltv_assemble(const LtvAssembleArgs& a, hipStream_t st) {
+  if (a.n_rows <= 0) return;
+  const size_t total = (size_t)a.n_rows * a.x_w;
+  hipLaunchKernelGGL(ltv_assemble_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
 }
 
 void launch_ltv(const LtvArgs& a, hipStream_t st) {

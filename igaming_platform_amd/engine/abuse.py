@@ -66,9 +66,11 @@ def rule_signals(feat, scoring, n_linked: int) -> List[str]:
 
 
 class AbuseGpu:
-    """K4 over the event rings of one GPU shard, one launch per batch of slots."""
+    """K4 over the HBM event rings of one GPU shard. Requests carry only slots; one captured
+    hipGraph per bucket: H2D [n | slots] -> fused 2-layer GRU + head (reads the rings) -> D2H."""
 
-    def __init__(self, store, plan, bmax: int = 8192):
+    def __init__(self, store, plan, bmax: int = 8192, buckets: Sequence[int] = (), use_graphs: bool = True,
+                 depth: int = 2):
         import torch
         from ..ops import kernels as K
         self.torch, self.K = torch, K
@@ -83,27 +85,98 @@ class AbuseGpu:
         self.T = steps[0].seq or store.ev.shape[1]
         if self.T > store.ev.shape[1]:
             raise ValueError(f"abuse model sequence length {self.T} exceeds the event ring {store.ev.shape[1]}")
-        self.bmax = bmax
-        self.slots = torch.zeros(bmax, dtype=torch.int32, device=self.device)
-        self.out = torch.zeros(bmax, dtype=torch.float32, device=self.device)
-        self.stream = torch.cuda.Stream(device=self.device)
+        self.buckets = sorted(set(int(b) for b in (buckets or [bmax])))
+        B = self.bmax = self.buckets[-1]
+        dev = self.device
+        self.dev_slab = torch.zeros(16 + 4 * B, dtype=torch.uint8, device=dev)
+        self.n_ptr = self.dev_slab[:4].view(torch.int32)
+        self.slots = self.dev_slab[16:].view(torch.int32)
+        self.out = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.depth = depth
+        self.host = [torch.zeros(16 + 4 * B, dtype=torch.uint8).pin_memory() for _ in range(depth)]
+        self.host_out = [torch.zeros(B, dtype=torch.float32).pin_memory() for _ in range(depth)]
+        self.stream = torch.cuda.Stream(device=dev)
+        self.graphs: Dict[tuple, object] = {}
+        self.use_graphs = use_graphs
+        self._slot = 0
         self._lock = threading.Lock()
+        self._slot_locks = [threading.Lock() for _ in range(depth)]
 
-    def launch(self, n: int) -> None:
-        self.K.gru(self.gp, n, self.T, out=self.out, store=self.store, slots=self.slots)
+    def _body(self, slot: int, b: int) -> None:
+        self.dev_slab[:16 + 4 * b].copy_(self.host[slot][:16 + 4 * b], non_blocking=True)
+        self.K.gru(self.gp, b, self.T, out=self.out, store=self.store, slots=self.slots, m_ptr=self.n_ptr)
+        self.host_out[slot][:b].copy_(self.out[:b], non_blocking=True)
+
+    def _pack(self, slot: int, slots: np.ndarray, b: int) -> None:
+        h = self.host[slot].numpy()
+        h[:4].view(np.int32)[0] = len(slots)
+        v = h[16:16 + 4 * b].view(np.int32)
+        v[:len(slots)] = slots
+        v[len(slots):] = -1
+
+    def capture(self) -> None:
+        torch = self.torch
+        if not self.use_graphs:
+            return
+        with torch.cuda.device(self.device):
+            for b in self.buckets:
+                for slot in range(self.depth):
+                    self._pack(slot, np.zeros(0, np.int32), b)
+                    s = torch.cuda.Stream(device=self.device)
+                    s.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(s):
+                        self._body(slot, b)
+                    torch.cuda.current_stream().wait_stream(s)
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=s):
+                        self._body(slot, b)
+                    self.graphs[(b, slot)] = g
+            torch.cuda.synchronize(self.device)
+
+    def bucket_for(self, n: int) -> int:
+        for b in self.buckets:
+            if n <= b:
+                return b
+        raise ValueError(f"abuse batch of {n} exceeds {self.bmax}")
+
+    def next_slot(self) -> int:
+        with self._lock:
+            s = self._slot
+            self._slot = (self._slot + 1) % self.depth
+        return s
+
+    def submit_packed(self, slot: int, n: int):
+        torch = self.torch
+        b = self.bucket_for(max(n, 1))
+        with torch.cuda.stream(self.stream):
+            g = self.graphs.get((b, slot))
+            if g is not None:
+                g.replay()
+            else:
+                self._body(slot, b)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        return slot, n, ev
+
+    def submit(self, slots: np.ndarray):
+        slot = self.next_slot()
+        self._slot_locks[slot].acquire()
+        self._pack(slot, np.asarray(slots, np.int32), self.bucket_for(max(len(slots), 1)))
+        with self._lock:
+            return self.submit_packed(slot, len(slots))
+
+    def wait(self, p, release: bool = True) -> np.ndarray:
+        slot, n, ev = p
+        try:
+            ev.synchronize()
+            return self.host_out[slot][:n].numpy().copy()
+        finally:
+            if release:
+                self._slot_locks[slot].release()
 
     def score_slots(self, slots: np.ndarray) -> np.ndarray:
-        torch = self.torch
-        res = []
-        with self._lock:
-            for i in range(0, len(slots), self.bmax):
-                chunk = np.ascontiguousarray(slots[i:i + self.bmax], np.int32)
-                with torch.cuda.stream(self.stream):
-                    self.slots[:len(chunk)].copy_(torch.from_numpy(chunk), non_blocking=False)
-                    self.launch(len(chunk))
-                    r = self.out[:len(chunk)].cpu()
-                res.append(r.numpy())
-        return np.concatenate(res) if res else np.zeros(0, np.float32)
+        out = [self.wait(self.submit(slots[i:i + self.bmax])) for i in range(0, len(slots), self.bmax)]
+        return np.concatenate(out) if out else np.zeros(0, np.float32)
 
 
 class AbuseService:

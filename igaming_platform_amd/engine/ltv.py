@@ -2,13 +2,15 @@
 
 Reference: ``LTVPredictor`` (services/risk/internal/prediction/ltv.go:113-151) reads a
 ``PlayerDataSource`` that has no implementation anywhere in the reference. Here the player
-profile is a host-resident table (one row of ``golden.ltv.PLAYER_COLUMNS`` per account,
-loaded by the warehouse job / ``set_players``), and prediction runs:
+profile is a table with one row of ``golden.ltv.PLAYER_COLUMNS`` per account (loaded by
+the warehouse job / ``set_players``; a host mirror plus, on GPUs, an HBM-resident copy in
+the same slot space as the fraud feature store), and prediction runs:
 
-* GPU (:class:`LtvGpu`): one captured hipGraph per batch bucket —
-  H2D [model input | player rows] -> optional learned LTV model (config 4: MLP 4x512 on
-  MFMA, ``DeviceModel``) -> K9 ``ltv_segment`` (churn, segment, survival, confidence, NBA,
-  with the model output replacing the formula LTV before the churn adjustment) -> D2H.
+* GPU (:class:`LtvGpu`): requests carry only slots; one captured hipGraph per bucket —
+  H2D [n | slots] -> ``ltv_assemble`` (model input gathered from the HBM tables) -> learned
+  LTV model (config 4: MLP 4x512 on MFMA, ``DeviceModel``) -> K9 ``ltv_segment`` (churn,
+  segment, survival, confidence, NBA; the model output replaces the formula LTV before the
+  churn adjustment) -> D2H [n, 6].
 * CPU: the golden float64 formula (+ the model through the C++ executor).
 
 The learned model's input row is :func:`ltv_model_input`: signed log1p of the 25 profile
@@ -91,9 +93,11 @@ class PlayerTable:
 
 
 class LtvGpu:
-    """Graph-captured K3 (optional model) + K9 pipeline on one GPU."""
+    """Player profiles resident in HBM; one captured hipGraph per batch bucket:
+    H2D [n | slots] -> ltv_assemble (model input gathered from the tables) -> MLP (MFMA)
+    -> K9 (reads the profile rows by slot) -> D2H [n, 6]."""
 
-    def __init__(self, device, plan=None, buckets: Sequence[int] = (64, 256, 1024, 4096, 8192),
+    def __init__(self, device, capacity: int, plan=None, buckets: Sequence[int] = (64, 256, 1024, 4096, 8192),
                  in_width: int = 0, use_graphs: bool = True, depth: int = 2):
         import torch
         from ..ops import kernels as K
@@ -101,21 +105,23 @@ class LtvGpu:
         self.torch, self.K = torch, K
         self.device = K.as_device(device)
         self.buckets = sorted(set(int(b) for b in buckets))
-        B = self.buckets[-1]
-        self.bmax = B
+        B = self.bmax = self.buckets[-1]
         self.plan = plan
-        self.in_width = (plan.in_width if plan is not None else 0) or in_width
+        self.w = (plan.in_width if plan is not None else 0) or in_width
+        if plan is not None and self.w < N_COLS:
+            raise ValueError(f"LTV model input ({self.w}) must hold the {N_COLS} profile columns")
         self.model = DeviceModel(plan, self.device, self.buckets) if plan is not None else None
-        if self.model is not None and plan.out_width < 1:
-            raise ValueError("LTV model must produce at least one output column")
         dev = self.device
-        self.w = self.in_width
-        row_bytes = 4 * (self.w + N_COLS)
-        self.slab_bytes = 16 + row_bytes * B
-        self.dev_slab = torch.zeros(self.slab_bytes, dtype=torch.uint8, device=dev)
+        self.capacity = int(capacity)
+        self.pf_tab = torch.zeros((self.capacity, N_COLS), dtype=torch.float32, device=dev)
+        self.ext_w = max(self.w - N_COLS, 0) if plan is not None else 0
+        self.ext_tab = torch.zeros((self.capacity, self.ext_w), dtype=torch.float32, device=dev) if self.ext_w else None
+        self.X = torch.zeros((B, self.w), dtype=torch.float32, device=dev) if plan is not None else None
+        self.dev_slab = torch.zeros(16 + 4 * B, dtype=torch.uint8, device=dev)
         self.n_ptr = self.dev_slab[:4].view(torch.int32)
+        self.slots = self.dev_slab[16:].view(torch.int32)
         self.depth = depth
-        self.host = [torch.zeros(self.slab_bytes, dtype=torch.uint8).pin_memory() for _ in range(depth)]
+        self.host = [torch.zeros(16 + 4 * B, dtype=torch.uint8).pin_memory() for _ in range(depth)]
         self.host_out = [torch.zeros((B, 6), dtype=torch.float32).pin_memory() for _ in range(depth)]
         self.out = torch.zeros((B, 6), dtype=torch.float32, device=dev)
         self.stream = torch.cuda.Stream(device=dev)
@@ -123,23 +129,30 @@ class LtvGpu:
         self._slot = 0
         self.use_graphs = use_graphs
         self._lock = threading.Lock()
+        self._slot_locks = [threading.Lock() for _ in range(depth)]
 
-    def _views(self, b: int):
-        t = self.torch
-        X = self.dev_slab[16:16 + 4 * self.w * b].view(t.float32).view(b, self.w) if self.w else None
-        off = 16 + 4 * self.w * b
-        pf = self.dev_slab[off: off + 4 * N_COLS * b].view(t.float32).view(b, N_COLS)
-        return X, pf
+    # ---- tables
+    def set_rows(self, slots: np.ndarray, rows: np.ndarray, ext: Optional[np.ndarray] = None) -> None:
+        torch = self.torch
+        idx = torch.as_tensor(np.asarray(slots, np.int64), device=self.device)
+        with torch.cuda.stream(self.stream):
+            self.pf_tab.index_copy_(0, idx, torch.as_tensor(np.asarray(rows, np.float32), device=self.device))
+            if ext is not None and self.ext_tab is not None:
+                e = np.zeros((len(slots), self.ext_w), np.float32)
+                w = min(self.ext_w, np.asarray(ext).shape[1])
+                e[:, :w] = np.asarray(ext, np.float32)[:, :w]
+                self.ext_tab.index_copy_(0, idx, torch.as_tensor(e, device=self.device))
+        self.stream.synchronize()
 
+    # ---- the step
     def _body(self, slot: int, b: int) -> None:
-        nbytes = 16 + 4 * (self.w + N_COLS) * b
-        self.dev_slab[:nbytes].copy_(self.host[slot][:nbytes], non_blocking=True)
-        X, pf = self._views(b)
+        self.dev_slab[:16 + 4 * b].copy_(self.host[slot][:16 + 4 * b], non_blocking=True)
         ml = None
         if self.model is not None:
-            y = self.model.run(X, b, m_ptr=self.n_ptr)
-            ml = y[:b, 0] if y.shape[1] == 1 else y[:b, 0].contiguous()
-        self.K.ltv(pf, self.out[:b], model_ltv=ml)
+            self.K.ltv_assemble(self.slots, self.pf_tab, self.ext_tab, self.X, b, m_ptr=self.n_ptr)
+            y = self.model.run(self.X, b, m_ptr=self.n_ptr)
+            ml = y[:b, 0]
+        self.K.ltv(self.pf_tab, self.out, model_ltv=ml, slots=self.slots, rows=b)
         self.host_out[slot][:b].copy_(self.out[:b], non_blocking=True)
 
     def capture(self) -> None:
@@ -149,6 +162,7 @@ class LtvGpu:
         with torch.cuda.device(self.device):
             for b in self.buckets:
                 for slot in range(self.depth):
+                    self._pack(slot, np.zeros(0, np.int32), b)
                     s = torch.cuda.Stream(device=self.device)
                     s.wait_stream(torch.cuda.current_stream())
                     with torch.cuda.stream(s):
@@ -166,17 +180,22 @@ class LtvGpu:
                 return b
         raise ValueError(f"LTV batch of {n} exceeds {self.bmax}")
 
-    def host_views(self, slot: int, b: int):
+    def _pack(self, slot: int, slots: np.ndarray, b: int) -> None:
         h = self.host[slot].numpy()
-        X = h[16:16 + 4 * self.w * b].view(np.float32).reshape(b, self.w) if self.w else None
-        off = 16 + 4 * self.w * b
-        pf = h[off: off + 4 * N_COLS * b].view(np.float32).reshape(b, N_COLS)
-        return X, pf
+        h[:4].view(np.int32)[0] = len(slots)
+        v = h[16:16 + 4 * b].view(np.int32)
+        v[:len(slots)] = slots
+        v[len(slots):] = -1
+
+    def next_slot(self) -> int:
+        with self._lock:
+            s = self._slot
+            self._slot = (self._slot + 1) % self.depth
+        return s
 
     def submit_packed(self, slot: int, n: int):
         torch = self.torch
         b = self.bucket_for(max(n, 1))
-        self.host[slot].numpy()[:4].view(np.int32)[0] = n
         with torch.cuda.stream(self.stream):
             g = self.graphs.get((b, slot))
             if g is not None:
@@ -187,33 +206,25 @@ class LtvGpu:
             ev.record(self.stream)
         return slot, n, ev
 
-    def next_slot(self) -> int:
-        s = self._slot
-        self._slot = (self._slot + 1) % self.depth
-        return s
+    def submit(self, slots: np.ndarray):
+        slot = self.next_slot()
+        self._slot_locks[slot].acquire()
+        self._pack(slot, np.asarray(slots, np.int32), self.bucket_for(max(len(slots), 1)))
+        with self._lock:
+            return self.submit_packed(slot, len(slots))
 
-    def wait(self, p) -> np.ndarray:
+    def wait(self, p, release: bool = True) -> np.ndarray:
         slot, n, ev = p
-        ev.synchronize()
-        return self.host_out[slot][:n].numpy().copy()
+        try:
+            ev.synchronize()
+            return self.host_out[slot][:n].numpy().copy()
+        finally:
+            if release:
+                self._slot_locks[slot].release()
 
-    def predict_rows(self, pf: np.ndarray, X: Optional[np.ndarray]) -> np.ndarray:
-        """[n, 25] profile rows (+ model input) -> [n, 6] (ltv, churn, survival, conf, seg, nba)."""
-        out = []
-        for i in range(0, max(len(pf), 1), self.bmax):
-            chunk = pf[i:i + self.bmax]
-            n = len(chunk)
-            with self._lock:
-                slot = self.next_slot()
-                b = self.bucket_for(max(n, 1))
-                hx, hp = self.host_views(slot, b)
-                hp[:n] = chunk
-                hp[n:] = 0
-                if hx is not None:
-                    hx[:n] = X[i:i + n] if X is not None else 0
-                    hx[n:] = 0
-                p = self.submit_packed(slot, n)
-            out.append(self.wait(p))
+    def predict_slots(self, slots: np.ndarray) -> np.ndarray:
+        """slots -> [n, 6] (ltv, churn, survival, confidence, segment, nba)."""
+        out = [self.wait(self.submit(slots[i:i + self.bmax])) for i in range(0, max(len(slots), 1), self.bmax)]
         return np.concatenate(out) if out else np.zeros((0, 6), np.float32)
 
 
@@ -231,9 +242,15 @@ class LtvService:
                     ext: Optional[np.ndarray] = None) -> None:
         slots, owners = self.registry.resolve_ids(list(account_ids), insert=True)
         rows = np.array([f.row() for f in features], np.float32).reshape(-1, N_COLS)
+        self.set_rows(slots, owners, rows, ext)
+
+    def set_rows(self, slots: np.ndarray, owners: np.ndarray, rows: np.ndarray, ext=None) -> None:
         for o in np.unique(owners):
             sel = np.nonzero((owners == o) & (slots >= 0))[0]
-            self.table.set(int(o), slots[sel], rows[sel], None if ext is None else np.asarray(ext)[sel])
+            e = None if ext is None else np.asarray(ext)[sel]
+            self.table.set(int(o), slots[sel], rows[sel], e)
+            if self.gpu is not None:
+                self.gpu[int(o) % len(self.gpu)].set_rows(slots[sel], rows[sel], e)
 
     def predict(self, account_ids: Sequence[str]) -> List[LtvResult]:
         slots, owners = self.registry.resolve_ids(list(account_ids), insert=False)
@@ -241,10 +258,10 @@ class LtvService:
         for o in np.unique(owners):
             sel = np.nonzero(owners == o)[0]
             rows, present, ext = self.table.get(int(o), slots[sel])
-            X = ltv_model_input(rows, ext, self.model_width) if self.model_width else None
             if self.gpu is not None:
-                res = self.gpu[int(o) % len(self.gpu)].predict_rows(rows, X)
+                res = self.gpu[int(o) % len(self.gpu)].predict_slots(np.where(present, slots[sel], -1))
             else:
+                X = ltv_model_input(rows, ext, self.model_width) if self.model_width else None
                 res = self._cpu(rows, X)
             for k, i in enumerate(sel):
                 r = res[k]

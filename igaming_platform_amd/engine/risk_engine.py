@@ -144,8 +144,8 @@ class RiskEngine:
             if backend == "gpu":
                 from ..models.plan import compile_onnx, to_device
                 dev = f"cuda:{self.devices[0]}"
-                g = LtvGpu(dev, to_device(compile_onnx(lm), dev) if lm is not None else None, buckets=cfg.gpu.buckets,
-                           in_width=ltv_width, use_graphs=capture)
+                g = LtvGpu(dev, self.capacity, to_device(compile_onnx(lm), dev) if lm is not None else None,
+                           buckets=cfg.gpu.buckets, in_width=ltv_width, use_graphs=capture)
                 g.capture()
                 lg = [g]
             self.ltv = LtvService(self.registry, world, gpu=lg, model_width=ltv_width,
@@ -158,7 +158,8 @@ class RiskEngine:
             lg = []
             for d in self.devices:
                 lp = to_device(compile_onnx(lm), f"cuda:{d}") if lm is not None else None
-                g = LtvGpu(f"cuda:{d}", lp, buckets=cfg.gpu.buckets, in_width=ltv_width, use_graphs=capture)
+                g = LtvGpu(f"cuda:{d}", self.capacity, lp, buckets=cfg.gpu.buckets, in_width=ltv_width,
+                           use_graphs=capture)
                 g.capture()
                 lg.append(g)
             self.ltv = LtvService(self.registry, world, gpu=lg, model_width=ltv_width)
@@ -167,7 +168,9 @@ class RiskEngine:
                 ag = []
                 for r, d in enumerate(self.devices):
                     ap = to_device(compile_onnx(am), f"cuda:{d}")
-                    ag.append(AbuseGpu(self.backends[r].store, ap, bmax=max(cfg.gpu.buckets)))
+                    g = AbuseGpu(self.backends[r].store, ap, buckets=cfg.gpu.buckets, use_graphs=capture)
+                    g.capture()
+                    ag.append(g)
             self.abuse = AbuseService(self, threshold=cfg.abuse.threshold, gpu=ag)
         else:
             self.ltv = LtvService(self.registry, world, executor=N.Executor(lm) if lm is not None else None,
@@ -559,7 +562,9 @@ def make_abuse_gpu(cfg: Config, local, abuse_model):
         return None
     from ..models.plan import compile_onnx, to_device
     from .abuse import AbuseGpu
-    return AbuseGpu(local.store, to_device(compile_onnx(am), str(local.device)), bmax=max(cfg.gpu.buckets))
+    g = AbuseGpu(local.store, to_device(compile_onnx(am), str(local.device)), buckets=cfg.gpu.buckets)
+    g.capture()
+    return g
 
 
 def serve_shard(cfg: Config, comm, backend: str = "gpu", capacity: Optional[int] = None, fraud_model=None,

@@ -229,13 +229,36 @@ def ensemble(hdr, cfg_dev, feat, X, ml: Optional[torch.Tensor], out, n_rows: int
 
 
 # --------------------------------------------------------------------------- K9
-def ltv(pf: torch.Tensor, out: torch.Tensor, model_ltv: Optional[torch.Tensor] = None) -> None:
-    B = pf.shape[0]
+def ltv(pf: torch.Tensor, out: torch.Tensor, model_ltv: Optional[torch.Tensor] = None,
+        slots: Optional[torch.Tensor] = None, rows: Optional[int] = None) -> None:
+    """K9. ``pf`` is [B, 25] rows, or (with ``slots``) the [C, 25] device player table."""
     if pf.dim() != 2 or pf.shape[1] != 25:
         raise ValueError("ltv: player features must be [B, 25]")
+    B = pf.shape[0] if slots is None else int(rows)
+    if slots is not None:
+        _need(slots, "slots", torch.int32, B)
     d = dict(pf=_need(pf, "pf", torch.float32), out=_need(out, "out", torch.float32, 6 * B),
-             ltv_model=_opt(model_ltv, "ltv_model", dtype=torch.float32, min_numel=B), B=int(B))
+             ltv_model=_opt(model_ltv, "ltv_model", dtype=torch.float32, min_numel=B), B=int(B),
+             slots=None if slots is None else slots.data_ptr())
     _mod().ltv(d, _stream())
+
+
+def ltv_assemble(slots: torch.Tensor, pf_tab: torch.Tensor, ext_tab: Optional[torch.Tensor], X: torch.Tensor,
+                 n_rows: int, m_ptr: Optional[torch.Tensor] = None) -> None:
+    """LTV model input rows gathered from the device-resident player tables."""
+    dev = X.device
+    if X.dim() != 2 or pf_tab.dim() != 2 or pf_tab.shape[1] != 25 or X.shape[0] < n_rows:
+        raise ValueError("ltv_assemble: shapes")
+    ext_w = 0 if ext_tab is None else int(ext_tab.shape[1])
+    if ext_tab is not None and ext_tab.shape[0] != pf_tab.shape[0]:
+        raise ValueError("ltv_assemble: table row counts differ")
+    if X.shape[1] < 25:
+        raise ValueError("ltv_assemble: model input narrower than the profile")
+    d = dict(slots=_need(slots, "slots", torch.int32, n_rows, dev), pf_tab=_need(pf_tab, "pf_tab", torch.float32, device=dev),
+             ext_tab=_opt(ext_tab, "ext_tab", dtype=torch.float32, device=dev), ext_w=ext_w,
+             X=_need(X, "X", torch.float32, X.shape[1] * n_rows, dev), x_w=int(X.shape[1]),
+             m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32, device=dev), n_rows=int(n_rows))
+    _mod().ltv_assemble(d, _stream())
 
 
 # --------------------------------------------------------------------------- K4

@@ -70,3 +70,77 @@ def build(config: str, batch: int, accounts: int, dev, rank: int = 0, depth: int
     sc.capture()
     pool = [make_requests(pop, B, rng, NOW0, hot_frac=hot_frac, unknown_frac=0.001) for _ in range(n_pool)]
     return Setup(cfg, store, sc, pop, pool, B, c["desc"])
+
+
+# ----------------------------------------------------------------------------- model-service configs
+MODEL_CONFIGS = {
+    "cfg4": dict(kind="ltv", batch=8192, metric="LTV predictions/sec (whole node)", unit="predictions/s",
+                 desc="cfg4 LTV regression MLP 4x512 (256 features = 25 profile + 231 ext, HBM-resident tables) "
+                      "+ K9 churn/segment/NBA, streaming micro-batches (hipGraph)"),
+    "cfg5": dict(kind="abuse", batch=4096, metric="bonus-abuse checks/sec (whole node)", unit="checks/s",
+                 desc="cfg5 bonus-abuse GRU 2x256 over the last 100 player events (HBM event rings, I=16) "
+                      "+ Gemm/Sigmoid head, fused K4"),
+}
+
+
+@dataclass
+class ModelSetup:
+    runner: Any          # LtvGpu | AbuseGpu (submit(slots) / wait(p) / out)
+    pool: List[np.ndarray]
+    batch: int
+    desc: str
+    metric: str
+    unit: str
+    store: Any = None
+
+
+def build_model(config: str, batch: int, accounts: int, dev, rank: int = 0, depth: int = 2,
+                use_graphs: bool = True, n_pool: int = 8) -> ModelSetup:
+    import torch
+
+    from ..config import FeatureConfig
+    from ..models.plan import compile_onnx, to_device
+    from ..native import native
+    from ..onnx import builders
+
+    c = MODEL_CONFIGS[config]
+    B = batch or c["batch"]
+    rng = np.random.default_rng(11 + rank)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    N = native()
+    if c["kind"] == "ltv":
+        from ..engine.ltv import LtvGpu
+        m = N.OnnxModel.from_bytes(builders.build("ltv_mlp", n_features=256, width=512, layers=4).SerializeToString())
+        runner = LtvGpu(dev, accounts, to_device(compile_onnx(m), dev), buckets=[B], use_graphs=use_graphs,
+                        depth=depth)
+        # synthetic player profiles (same column semantics as golden.ltv.PLAYER_COLUMNS)
+        for s in range(0, accounts, 1 << 18):
+            n = min(1 << 18, accounts - s)
+            pf = torch.rand((n, 25), generator=g, device=dev) * torch.tensor(
+                [900, 90, 60, 500, 10, 120, 1e5, 8e4, 3e4, 500, 8, 5e3, 2e5, 1.8e5, 3000, 1, 80, 60, 20, 15, 1,
+                 1, 1, 1, 8], device=dev)
+            runner.pf_tab[s:s + n].copy_(pf.floor_())
+            runner.ext_tab[s:s + n].normal_(generator=g)
+        store = None
+    else:
+        from ..engine.abuse import AbuseGpu
+        from ..features.device_store import DeviceFeatureStore
+        fc = FeatureConfig()
+        store = DeviceFeatureStore(accounts, fc, dev, events=True, max_events=64)
+        for s in range(0, accounts, 1 << 16):  # full 100-event histories, ~N(0,1) encoded events
+            n = min(1 << 16, accounts - s)
+            ev = torch.randn((n, fc.event_ring, fc.event_dim), generator=g, device=dev).to(torch.bfloat16)
+            store.ev[s:s + n].copy_(ev.view(torch.int16))
+        rt = store.rt.view(-1, store.rt.shape[1])
+        from ..layouts import ACCTRT
+        head_col = ACCTRT.fields["ev_head"][1] // 4
+        cnt_col = ACCTRT.fields["ev_count"][1] // 4
+        rt[:, head_col] = torch.randint(0, fc.event_ring, (accounts,), generator=g, device=dev, dtype=torch.int32)
+        rt[:, cnt_col] = fc.event_ring
+        m = N.OnnxModel.from_bytes(builders.build("gru", seq=100, in_dim=16, hidden=256).SerializeToString())
+        runner = AbuseGpu(store, to_device(compile_onnx(m), dev), buckets=[B], use_graphs=use_graphs, depth=depth)
+    torch.cuda.synchronize(dev)
+    runner.capture()
+    pool = [rng.integers(0, accounts, B).astype(np.int32) for _ in range(n_pool)]
+    return ModelSetup(runner, pool, B, c["desc"], c["metric"], c["unit"], store)
