@@ -1,0 +1,258 @@
+"""T4: the wallet and bonus services as thin clients of an in-process risk.v1 server —
+including the reference's fail-open (deposit/bet) / fail-closed (withdraw) semantics."""
+import datetime as dt
+import os
+
+import grpc
+import numpy as np
+import pytest
+
+from igaming_platform_amd.api.grpc_server import RiskServer
+from igaming_platform_amd.bonus.engine import (BonusEngine, BonusError, GrpcAbuseChecker, PlayerInfo, load_rules,
+                                               load_rules_file)
+from igaming_platform_amd.clients.risk_client import RiskClient
+from igaming_platform_amd.config import Config
+from igaming_platform_amd.engine.risk_engine import RiskEngine
+from igaming_platform_amd.events import bus as EB
+from igaming_platform_amd.layouts import ACCTBATCH
+from igaming_platform_amd.wallet.domain import CLEARING_ACCOUNT, WalletError
+from igaming_platform_amd.wallet.grpc_api import WalletClient, WalletServer
+from igaming_platform_amd.wallet.repository import BonusRepository, Database
+from igaming_platform_amd.wallet.service import GrpcRisk, WalletService
+
+RULES = os.path.join(os.path.dirname(__file__), "..", "igaming_platform_amd", "bonus", "configs", "bonus_rules.yaml")
+
+
+@pytest.fixture(scope="module")
+def risk():
+    eng = RiskEngine(Config(), backend="cpu", capacity=5000)
+    srv = RiskServer(eng, port=0, batching=False).start()
+    cli = RiskClient(f"127.0.0.1:{srv.port}")
+    yield eng, srv, cli
+    cli.close()
+    srv.stop(0.2)
+
+
+def _wallet(cli, bus=None, **kw):
+    return WalletService(Database(), risk=GrpcRisk(cli), bus=bus, **kw)
+
+
+def test_wallet_flow_and_double_entry_ledger(risk):
+    eng, srv, cli = risk
+    bus = EB.EventBus()
+    bus.declare_queue("audit")
+    bus.bind("audit", EB.EXCHANGE_WALLET, "#")
+    w = _wallet(cli, bus)
+    a = w.create_account("player-1", "eur")
+    assert w.create_account("player-1").id == a.id and a.currency == "EUR"      # idempotent by player
+    t, nb, score = w.deposit(a.id, 10_000, "dep-1", "card", ip="1.2.3.4", device_id="dev-a")
+    assert nb == 10_000 and score is not None and t.status == "completed"
+    assert w.deposit(a.id, 10_000, "dep-1")[0].id == t.id                       # idempotent replay
+    w.grant_bonus(a.id, 2_000, "bonus-1")
+    bt, nb, _, real, bonus = w.bet(a.id, 3_000, "bet-1", "g1", "r1", "slots")
+    assert (real, bonus, nb) == (1_000, 2_000, 9_000)                           # bonus money first
+    wt, nb = w.win(a.id, 500, "win-1", "g1", "r1", bet_transaction_id=bt.id)
+    assert nb == 9_500
+    rt, nb = w.refund(a.id, bt.id, "ref-1", "game void")
+    assert nb == 12_500 and w.get_transaction(bt.id).status == "reversed"
+    with pytest.raises(WalletError) as e:
+        w.refund(a.id, bt.id, "ref-2")
+    assert e.value.code == "INVALID_OPERATION"
+    acct = w.get_balance(a.id)
+    assert (acct.balance, acct.bonus) == (12_500, 0)
+    assert w.ledger.verify_balance(acct)
+    assert w.ledger.balance(a.id) + w.ledger.clearing_balance() == 0            # entries net to zero
+    txs, total, more = w.history(a.id, limit=2)
+    assert total == 5 and len(txs) == 2 and more
+    assert [x.type for x in w.history(a.id, types=["bet"])[0]] == ["bet"]
+    assert len(bus.queues["audit"]) >= 6                                       # outbox relayed to the bus
+
+
+def test_wallet_validation_errors(risk):
+    eng, srv, cli = risk
+    w = _wallet(cli)
+    a = w.create_account("player-2")
+    for fn, code in ((lambda: w.deposit(a.id, 0, "k"), "INVALID_AMOUNT"),
+                     (lambda: w.bet(a.id, 10, "k2"), "INSUFFICIENT_BALANCE"),
+                     (lambda: w.deposit("nope", 10, "k3"), "ACCOUNT_NOT_FOUND")):
+        with pytest.raises(WalletError) as e:
+            fn()
+        assert e.value.code == code
+    w.deposit(a.id, 1000, "d")
+    w.set_status(a.id, "suspended")
+    with pytest.raises(WalletError) as e:
+        w.bet(a.id, 10, "b")
+    assert e.value.code == "ACCOUNT_SUSPENDED"
+    rows = w.db.query("SELECT action, old_value, new_value FROM audit_log WHERE entity_id = ?", (a.id,))
+    assert [tuple(r) for r in rows] == [("status", "active", "suspended")]
+
+
+def test_optimistic_lock_conflict_is_retried(risk):
+    eng, srv, cli = risk
+    w = _wallet(cli)
+    a = w.create_account("player-lock")
+    w.deposit(a.id, 1000, "d1")
+    stale = w.accounts.get_by_id(a.id)
+    w.deposit(a.id, 1000, "d2")
+    from igaming_platform_amd.wallet.domain import ConcurrentUpdate
+    with pytest.raises(ConcurrentUpdate):
+        w.accounts.update_balance(a.id, 5, 0, stale.version)
+    assert w.get_balance(a.id).balance == 2000
+
+
+def test_risk_block_and_review_thresholds(risk):
+    eng, srv, cli = risk
+    eng.add_to_blacklist("device", "stolen-phone", "chargeback", "t")
+    w = _wallet(cli, block_threshold=40, review_threshold=30)
+    a = w.create_account("player-3")
+    with pytest.raises(WalletError) as e:   # blacklist +50 rule points, new account large deposit +30
+        w.deposit(a.id, 500_000, "big", device_id="stolen-phone")
+    assert e.value.code == "RISK_BLOCKED"
+    w.deposit(a.id, 5_000, "small")
+    with pytest.raises(WalletError) as e:
+        w.withdraw(a.id, 4_000, "wd", device_id="stolen-phone")
+    assert e.value.code == "RISK_REVIEW"
+
+
+def test_fail_open_deposit_fail_closed_withdraw():
+    dead = RiskClient("127.0.0.1:1", timeout_s=0.3)       # nothing listens: risk unavailable
+    w = WalletService(Database(), risk=GrpcRisk(dead, timeout_s=0.3))
+    a = w.create_account("player-4")
+    t, nb, score = w.deposit(a.id, 5_000, "d")                # fail-open (wallet_service.go:270-272)
+    assert nb == 5_000 and score is None
+    w.bet(a.id, 100, "b")                                     # fail-open (:388-389)
+    with pytest.raises(WalletError) as e:                    # fail-closed (:605-608)
+        w.withdraw(a.id, 1_000, "w")
+    assert e.value.code == "RISK_REVIEW" and w.get_balance(a.id).balance == 4_900
+    dead.close()
+
+
+def test_wallet_grpc_api(risk):
+    eng, srv, cli = risk
+    w = _wallet(cli)
+    ws = WalletServer(w, port=0).start()
+    wc = WalletClient(f"127.0.0.1:{ws.port}")
+    try:
+        acc = wc.call("CreateAccount", player_id="grpc-player", currency="USD").account
+        assert wc.call("GetAccount", player_id="grpc-player").account.id == acc.id
+        d = wc.call("Deposit", account_id=acc.id, amount=7_000, idempotency_key="k1", payment_method="card")
+        assert d.new_balance == 7_000 and d.transaction.type == "deposit"
+        b = wc.call("Bet", account_id=acc.id, amount=1_000, idempotency_key="k2", game_id="g", round_id="r",
+                    game_category="slots")
+        assert b.real_deducted == 1_000 and b.new_balance == 6_000
+        bal = wc.call("GetBalance", account_id=acc.id)
+        assert (bal.balance, bal.total, bal.withdrawable) == (6_000, 6_000, 6_000)
+        h = wc.call("GetTransactionHistory", account_id=acc.id, limit=10)
+        assert h.total == 2 and [t.type for t in h.transactions] == ["bet", "deposit"]
+        assert wc.call("GetTransaction", transaction_id=b.transaction.id).transaction.amount == 1_000
+        with pytest.raises(grpc.RpcError) as e:
+            wc.call("Bet", account_id=acc.id, amount=10**9, idempotency_key="k3")
+        assert e.value.code() == grpc.StatusCode.FAILED_PRECONDITION and "INSUFFICIENT_BALANCE" in e.value.details()
+        with pytest.raises(grpc.RpcError) as e:
+            wc.call("GetBalance", account_id="missing")
+        assert e.value.code() == grpc.StatusCode.NOT_FOUND
+    finally:
+        wc.close()
+        ws.stop(0.2)
+
+
+# ------------------------------------------------------------------ bonus engine
+def _bonus(risk_checker=None, wallet=None, players=None, when="2025-06-03T12:00:00"):
+    t = dt.datetime.fromisoformat(when).replace(tzinfo=dt.timezone.utc).timestamp()
+    db = wallet.db if wallet is not None else Database()
+    return BonusEngine(load_rules_file(RULES), BonusRepository(db), risk=risk_checker, wallet=wallet,
+                       players=players or (lambda a: PlayerInfo(a, account_age_days=2, total_deposits=0)),
+                       clock=lambda: t)
+
+
+def test_rules_dsl_loads_and_validates():
+    rules = load_rules_file(RULES)
+    assert len(rules) == 10 and {r.type for r in rules} >= {"deposit_match", "free_spins", "cashback", "freebet",
+                                                           "no_deposit", "reload"}
+    with pytest.raises(ValueError):
+        load_rules("bonus_rules:\n  - {id: x, name: y, type: deposit_match, bogus_key: 1}\n")
+    with pytest.raises(ValueError):
+        load_rules("bonus_rules:\n  - {id: x, name: y, type: lottery}\n")
+
+
+def test_eligibility_conditions_and_schedule():
+    tue = _bonus(when="2025-06-03T12:00:00")       # a Tuesday
+    ids = {r.id for r in tue.eligible("acc-1")}
+    assert "first_deposit_match" in ids and "tuesday_reload" not in ids          # reload needs 2 deposits
+    assert "vip_monthly_match" not in ids and "promo_spring_reload" not in ids   # segment / promo code
+    assert "promo_spring_reload" in {r.id for r in tue.eligible("acc-1", promo_code="SPRING75")}
+    regular = _bonus(when="2025-06-03T12:00:00",
+                     players=lambda a: PlayerInfo(a, account_age_days=60, total_deposits=3, segment="medium"))
+    ids = {r.id for r in regular.eligible("acc-2")}
+    assert "tuesday_reload" in ids and "first_deposit_match" not in ids and "high_stake_match" in ids
+    wed = _bonus(when="2025-06-04T12:00:00",
+                 players=lambda a: PlayerInfo(a, account_age_days=60, total_deposits=3, segment="medium"))
+    assert "tuesday_reload" not in {r.id for r in wed.eligible("acc-2")}
+
+
+def test_award_wager_maxbet_expire(risk):
+    eng, srv, cli = risk
+    w = _wallet(cli)
+    be = _bonus(wallet=w)
+    w.bonus = be
+    a = w.create_account("bonus-player")
+    w.deposit(a.id, 20_000, "d1")
+    b = be.award(a.id, "first_deposit_match", deposit_amount=20_000)
+    assert b.bonus_amount == 20_000 and b.wagering_required == 20_000 * 30
+    assert w.get_balance(a.id).bonus == 20_000
+    with pytest.raises(BonusError) as e:
+        be.award(a.id, "first_deposit_match", deposit_amount=20_000)
+    assert e.value.code == "ALREADY_CLAIMED"
+    with pytest.raises(BonusError) as e:
+        be.award(a.id, "second_deposit_match", deposit_amount=100)
+    assert e.value.code in ("NOT_ELIGIBLE", "MIN_DEPOSIT")
+    with pytest.raises(WalletError) as e:             # 10% of the bonus = 2,000; absolute cap 800
+        w.bet(a.id, 900, "big-bet", game_category="slots")
+    assert e.value.code == "BONUS_RESTRICTION"
+    w.bet(a.id, 800, "b1", game_category="slots")
+    w.bet(a.id, 800, "b2", game_category="video_poker")   # 40% weight
+    w.bet(a.id, 800, "b3", game_category="live_dealer")   # excluded
+    cur = be.repo.get(b.id)
+    assert cur.wagering_progress == 800 + 320
+    assert be.expire(now=b.expires_at + 1) == 1 and be.repo.get(b.id).status == "expired"
+
+
+def test_withdrawal_forfeits_active_bonus(risk):
+    eng, srv, cli = risk
+    w = _wallet(cli)
+    be = _bonus(wallet=w)
+    w.bonus = be
+    a = w.create_account("forfeit-player")
+    w.deposit(a.id, 3_000, "d1")
+    b = be.award(a.id, "verification_reward")
+    assert b.bonus_amount == 1_000
+    w.withdraw(a.id, 1_000, "w1")
+    assert be.repo.get(b.id).status == "forfeited"
+
+
+def test_abuse_check_blocks_and_fails_open(risk):
+    eng, srv, cli = risk
+    rows = np.zeros(1, ACCTBATCH)
+    rows["present"], rows["bonus_claim_count"], rows["total_deposits"] = 1, 6, 100
+    eng.load_batch_features(["abuser-1"], rows)
+    eng.score([dict(account_id="abuser-1", amount=10, transaction_type="bet", device_id="farm"),
+               dict(account_id="abuser-2", amount=10, transaction_type="bet", device_id="farm")])
+    be = _bonus(risk_checker=GrpcAbuseChecker(cli))
+    with pytest.raises(BonusError) as e:
+        be.award("abuser-1", "verification_reward")
+    assert e.value.code == "ABUSE_SUSPECTED" and "SHARED_DEVICE" in e.value.message
+
+    class Down:
+        def check_bonus_abuse(self, *a):
+            raise ConnectionError("risk down")
+
+    assert _bonus(risk_checker=Down()).award("abuser-1", "verification_reward").bonus_amount == 1_000
+
+
+def test_cashback_and_amount_rules():
+    be = _bonus()
+    r = be.get_rule("weekly_cashback")
+    assert BonusEngine.bonus_amount(r, 0, net_loss=100_000) == 8_000
+    assert BonusEngine.bonus_amount(r, 0, net_loss=10**8) == 30_000
+    assert BonusEngine.bonus_amount(be.get_rule("high_stake_match"), 10**7) == 150_000
+    assert BonusEngine.wager_contribution(be.get_rule("first_deposit_match"), "sports", 100) == 0
