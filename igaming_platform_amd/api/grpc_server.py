@@ -16,11 +16,10 @@ from __future__ import annotations
 import threading
 import time
 from concurrent import futures
-from typing import Callable, Dict, Optional
+from typing import Dict, Optional
 
 import grpc
 
-from ..golden import ltv as GL
 from ..obs.logging import get_logger
 from ..proto import health_v1 as HV
 from ..proto import reflection_v1 as RV

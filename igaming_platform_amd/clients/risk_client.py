@@ -2,7 +2,7 @@
 wallet_service.go:40-42, 123-138; bonus_engine.go:139-141)."""
 from __future__ import annotations
 
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, Optional, Sequence
 
 import grpc
 

@@ -19,7 +19,6 @@ columns followed by the account's extra LTV features (zeros when none are loaded
 from __future__ import annotations
 
 import threading
-import time
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
 

@@ -7,7 +7,7 @@ Each owner has its own C++ :class:`AccountIndex` (open addressing, full-id verif
 from __future__ import annotations
 
 import threading
-from typing import List, Optional, Sequence, Tuple
+from typing import Sequence, Tuple
 
 import numpy as np
 

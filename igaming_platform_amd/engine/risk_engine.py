@@ -13,7 +13,6 @@ every shard's device config block (fixes the unguarded read of quirk Q6).
 """
 from __future__ import annotations
 
-import base64
 import collections
 import dataclasses
 import json
@@ -24,7 +23,7 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-from ..config import ACTION_NAMES, Config, REASON_CODES, TX_TYPE_ID, TX_UNKNOWN
+from ..config import ACTION_NAMES, Config, REASON_CODES
 from ..features.tables import Blacklist, IPIntel
 from ..golden import scoring as GS
 from ..layouts import ACCTBATCH, FEATREC, REQREC, unpack_results
@@ -32,7 +31,6 @@ from ..native import native
 from ..obs.logging import get_logger
 from ..obs.metrics import Metrics
 from ..utils.faults import Faults, InjectedFault
-from ..utils.hashing import SEED_DEVICE, SEED_FINGERPRINT, SEED_IP, id_hash
 from .backends import CpuBackend, GpuBackend
 from .registry import AccountRegistry
 
@@ -105,6 +103,14 @@ class RiskEngine:
             mkind = "onnx" if fm is not None else "heuristic"  # missing model -> mockPredict (onnx_model.go:51-60)
         if mkind == "onnx" and fm is None:
             raise ValueError("fraud_model.kind=onnx but no model given")
+        if mkind == "onnx":
+            dims = fm.inputs()[0][2]
+            w = int(dims[-1]) if dims and int(dims[-1]) > 0 else cfg.features.width
+            if w != cfg.features.width:
+                if cfg.features.width != 30:
+                    raise ValueError(f"model input width {w} != features.width {cfg.features.width}")
+                # columns >= 30 are the account's extra features (warehouse ext table)
+                cfg.features.width = w
         self.model_kind = mkind
         self.fraud_onnx = fm
         self.backends: List = []

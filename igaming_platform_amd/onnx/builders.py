@@ -15,7 +15,7 @@ names. Input name ``input`` / primary output ``output`` follow ``onnx_model.go:3
 """
 from __future__ import annotations
 
-from typing import Dict, List
+from typing import Dict
 
 import numpy as np
 

@@ -12,7 +12,7 @@ from typing import List
 import numpy as np
 
 from . import schema as S
-from .writer import attr, model, node, tensor, tree_attrs, value_info
+from .writer import model, node, tree_attrs, value_info
 
 
 def _tree_dict(tree, scale: float, k_index: int = 0, n_targets: int = 1):

@@ -19,7 +19,6 @@ from __future__ import annotations
 import dataclasses
 import io
 import json
-from typing import Optional
 
 import numpy as np
 

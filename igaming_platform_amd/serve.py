@@ -18,7 +18,7 @@ import threading
 import time
 
 from .config import Config
-from .obs.logging import get_logger, setup_logger
+from .obs.logging import setup_logger
 
 
 def _fraud_model(a, cfg: Config):

@@ -70,7 +70,8 @@ def make_population(n: int, ext_width: int, seed: int = 0, now: int = NOW0, pool
         fp = rng.integers(1, 2 ** 63, (n, pool), dtype=np.int64).astype(np.uint64)
     else:
         dev = np.stack([_digests(f"dev-{i}-", pool, SEED_DEVICE) for i in range(n)]) if n else np.zeros((0, pool), np.uint64)
-        ip = np.stack([_digests(f"10.{i % 250}.{i // 250 % 250}.", pool, SEED_IP) for i in range(n)]) if n else np.zeros((0, pool), np.uint64)
+        ip = (np.stack([_digests(f"10.{i % 250}.{i // 250 % 250}.", pool, SEED_IP) for i in range(n)]) if n
+              else np.zeros((0, pool), np.uint64))
         fp = np.stack([_digests(f"fp-{i}-", pool, SEED_FINGERPRINT) for i in range(n)]) if n else np.zeros((0, pool), np.uint64)
     return Population(ids, b, ext, dev, ip, fp)
 

@@ -18,8 +18,7 @@ import time
 from contextlib import contextmanager
 from typing import Iterator, List, Optional, Sequence
 
-from .domain import (ACTIVE, CLEARING_ACCOUNT, Account, ConcurrentUpdate, LedgerEntry, Transaction, WalletError,
-                     not_found)
+from .domain import CLEARING_ACCOUNT, Account, ConcurrentUpdate, LedgerEntry, Transaction, WalletError, not_found
 
 SCHEMA = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
                       "deploy", "schema.sql")

@@ -14,9 +14,7 @@ Risk semantics (wallet_service.go:263-272, 380-389, 598-608
 """
 from __future__ import annotations
 
-import json
 import time
-from dataclasses import asdict
 from typing import List, Optional, Protocol, Sequence, Tuple
 
 from ..events import bus as EB

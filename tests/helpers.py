@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from igaming_platform_amd.config import Config, TX_TYPE_ID
+from igaming_platform_amd.config import Config
 from igaming_platform_amd.golden import scoring as GS
 from igaming_platform_amd.golden.features import GoldenFeatureStore, model_input
 from igaming_platform_amd.layouts import FR_BLACKLISTED

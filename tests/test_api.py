@@ -5,7 +5,6 @@ import threading
 import urllib.request
 
 import grpc
-import numpy as np
 import pytest
 
 from igaming_platform_amd.api.grpc_server import RiskServer

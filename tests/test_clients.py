@@ -15,7 +15,7 @@ from igaming_platform_amd.config import Config
 from igaming_platform_amd.engine.risk_engine import RiskEngine
 from igaming_platform_amd.events import bus as EB
 from igaming_platform_amd.layouts import ACCTBATCH
-from igaming_platform_amd.wallet.domain import CLEARING_ACCOUNT, WalletError
+from igaming_platform_amd.wallet.domain import WalletError
 from igaming_platform_amd.wallet.grpc_api import WalletClient, WalletServer
 from igaming_platform_amd.wallet.repository import BonusRepository, Database
 from igaming_platform_amd.wallet.service import GrpcRisk, WalletService

@@ -3,7 +3,6 @@
 answers and snapshots must equal a single-process engine with the same owner routing."""
 import os
 import socket
-import tempfile
 
 import numpy as np
 import pytest

@@ -3,7 +3,7 @@ snapshots, degradation and the LTV / abuse services."""
 import numpy as np
 import pytest
 
-from igaming_platform_amd.config import Config, REASON_CODES, TX_TYPE_ID
+from igaming_platform_amd.config import Config, TX_TYPE_ID
 from igaming_platform_amd.engine.risk_engine import RiskEngine
 from igaming_platform_amd.golden import ltv as GL, scoring as GS
 from igaming_platform_amd.golden.features import BatchFeatures, GoldenFeatureStore, TxEvent, model_input

@@ -4,7 +4,6 @@ import pytest
 
 from igaming_platform_amd.config import Config, REASON_BIT
 from igaming_platform_amd.golden import ltv as GL
-from igaming_platform_amd.layouts import FEATREC, REQREC
 from igaming_platform_amd.utils.hashing import SEED_IP, id_hash
 
 from .helpers import build_world, compare_featrec, golden_score

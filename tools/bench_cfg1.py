@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Config 1: risk.v1.ScoreTransaction end to end over gRPC on the CPU path (C++ executor,
+32-feature logistic model, batch = 1 — no micro-batching), N concurrent unary clients.
+Prints one JSON line: scores/s + p50/p99 latency (client-measured, includes gRPC)."""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clients", type=int, default=8)
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--accounts", type=int, default=10000)
+    a = ap.parse_args()
+    from igaming_platform_amd.api.grpc_server import RiskServer
+    from igaming_platform_amd.clients.risk_client import RiskClient
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.engine.risk_engine import RiskEngine
+    from igaming_platform_amd.onnx import builders
+    from igaming_platform_amd.proto import risk_v1 as P
+    cfg = Config()
+    cfg.features.width = 32
+    eng = RiskEngine(cfg, backend="cpu", capacity=a.accounts * 2,
+                     fraud_model=builders.build("logistic", n_features=32).SerializeToString())
+    srv = RiskServer(eng, port=0, batching=False).start()
+    lat, stop, errs = [], threading.Event(), []
+    lock = threading.Lock()
+
+    def client(i):
+        c = RiskClient(f"127.0.0.1:{srv.port}")
+        rng = np.random.default_rng(i)
+        mine = []
+        types = ["deposit", "withdraw", "bet", "win"]
+        while not stop.is_set():
+            req = P.ScoreTransactionRequest(account_id=f"acc-{int(rng.integers(0, a.accounts))}",
+                                            amount=int(rng.integers(100, 500000)),
+                                            transaction_type=types[int(rng.integers(0, 4))],
+                                            device_id=f"dev-{int(rng.integers(0, 50000))}", ip_address="10.0.0.1")
+            t0 = time.perf_counter()
+            try:
+                c.call("ScoreTransaction", req)
+            except Exception as e:  # pragma: no cover
+                errs.append(e)
+                continue
+            mine.append((time.perf_counter() - t0) * 1e3)
+        with lock:
+            lat.extend(mine)
+        c.close()
+
+    th = [threading.Thread(target=client, args=(i,)) for i in range(a.clients)]
+    t0 = time.perf_counter()
+    [t.start() for t in th]
+    time.sleep(a.seconds)
+    stop.set()
+    [t.join() for t in th]
+    el = time.perf_counter() - t0
+    srv.stop(0.5)
+    out = dict(metric="fraud scores/sec (risk.v1.ScoreTransaction over gRPC, CPU executor)", value=len(lat) / el,
+               unit="scores/s", n_gpus=0, higher_is_better=True, dtype="fp32", data="synthetic",
+               config=dict(model="cfg1 32-feature logistic (Gemm+Sigmoid), C++ CPU executor", batch=1,
+                           clients=a.clients, seconds=a.seconds),
+               p50_latency_ms=float(np.percentile(lat, 50)), p99_latency_ms=float(np.percentile(lat, 99)),
+               latency_baseline_ms=50.0, errors=len(errs))
+    print(json.dumps(out))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
