@@ -8,6 +8,7 @@
 #include <memory>
 
 #include "account_index.h"
+#include "cpu_scorer.h"
 #include "link_index.h"
 #include "executor.h"
 #include "onnx_model.h"
@@ -268,6 +269,104 @@ PYBIND11_MODULE(_native, m) {
       .def("linked", &LinkIndex::linked, py::arg("acct"), py::arg("limit") = 16)
       .def("devices_of", &LinkIndex::devices_of)
       .def("n_devices", &LinkIndex::n_devices);
+
+  py::class_<CpuScorer, std::shared_ptr<CpuScorer>>(m, "CpuScorer")
+      .def(py::init<int64_t, int, int, int, int>(), py::arg("capacity"), py::arg("ring_size") = 256,
+           py::arg("event_ring") = 100, py::arg("event_dim") = 16, py::arg("ext_width") = 0)
+      .def("set_cfg", [](CpuScorer& c, py::array_t<uint8_t, py::array::c_style | py::array::forcecast> b) {
+        if (b.size() != (py::ssize_t)sizeof(ScoreCfg)) throw std::runtime_error("ScoreCfg must be 176 bytes");
+        ScoreCfg cfg;
+        std::memcpy(&cfg, b.data(), sizeof cfg);
+        c.set_cfg(cfg);
+      })
+      .def("set_tables", [](CpuScorer& c, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> bk,
+                            py::array_t<uint32_t, py::array::c_style | py::array::forcecast> be,
+                            py::array_t<uint64_t, py::array::c_style | py::array::forcecast> ik,
+                            py::array_t<uint32_t, py::array::c_style | py::array::forcecast> iv) {
+        if (bk.size() != be.size() || ik.size() != iv.size()) throw std::runtime_error("table sizes");
+        c.set_tables(bk.data(), be.data(), bk.size(), ik.data(), iv.data(), ik.size());
+      })
+      .def("set_model", [](CpuScorer& c, py::object ex, std::string in, std::string out, int col) {
+        if (ex.is_none()) { c.set_model(nullptr, "", "", 0); return; }
+        c.set_model(ex.cast<std::shared_ptr<exec::Executor>>(), in, out, col);
+      })
+      .def("set_batch", [](CpuScorer& c, py::array_t<int32_t, py::array::c_style | py::array::forcecast> slots,
+                           py::array rows) {
+        if ((size_t)rows.nbytes() != (size_t)slots.size() * sizeof(AcctBatch)) throw std::runtime_error("rows");
+        c.set_batch(slots.data(), reinterpret_cast<const AcctBatch*>(rows.data()), slots.size());
+      })
+      .def("set_ext", [](CpuScorer& c, py::array_t<int32_t, py::array::c_style | py::array::forcecast> slots,
+                         py::array_t<float, py::array::c_style | py::array::forcecast> e) {
+        if (e.ndim() != 2 || e.shape(0) != slots.size()) throw std::runtime_error("ext must be [n, w]");
+        c.set_ext(slots.data(), e.data(), slots.size(), (int)e.shape(1));
+      })
+      .def("reset", [](CpuScorer& c, py::array_t<int32_t, py::array::c_style | py::array::forcecast> slots) {
+        c.reset(slots.data(), slots.size());
+      })
+      .def("ingest", [](CpuScorer& c, py::array req) {
+        if (req.nbytes() % sizeof(ReqRec)) throw std::runtime_error("ReqRec rows expected");
+        const ReqRec* r = reinterpret_cast<const ReqRec*>(req.data());
+        const size_t n = req.nbytes() / sizeof(ReqRec);
+        py::gil_scoped_release rel;
+        c.ingest(r, n);
+      })
+      .def("score", [](CpuScorer& c, py::array req, int64_t now, bool update, bool want_features) {
+        if (req.nbytes() % sizeof(ReqRec)) throw std::runtime_error("ReqRec rows expected");
+        const size_t n = req.nbytes() / sizeof(ReqRec);
+        py::array_t<uint32_t> res({(py::ssize_t)n, (py::ssize_t)2});
+        py::object feat = py::none();
+        FeatRec* fp = nullptr;
+        if (want_features) {
+          py::array_t<int32_t> f({(py::ssize_t)n, (py::ssize_t)32});
+          fp = reinterpret_cast<FeatRec*>(f.mutable_data());
+          feat = f;
+        }
+        const ReqRec* r = reinterpret_cast<const ReqRec*>(req.data());
+        ResultRec* rp = reinterpret_cast<ResultRec*>(res.mutable_data());
+        {
+          py::gil_scoped_release rel;
+          c.score(r, n, now, update, rp, fp);
+        }
+        return py::make_tuple(res, feat);
+      }, py::arg("req"), py::arg("now"), py::arg("update") = true, py::arg("want_features") = true)
+      .def("features", [](CpuScorer& c, int32_t slot, int64_t now) {
+        FeatRec f = c.features(slot, now);
+        py::array_t<int32_t> out(32);
+        std::memcpy(out.mutable_data(), &f, sizeof f);
+        return out;
+      })
+      .def("event_history", [](CpuScorer& c, int32_t slot) {
+        py::array_t<float> out({(py::ssize_t)c.event_ring(), (py::ssize_t)c.event_dim()});
+        c.event_history(slot, out.mutable_data());
+        return out;
+      })
+      .def("state", [](CpuScorer& c) {
+        py::dict d;
+        d["ring_ts"] = vec_np(c.ring_ts);
+        d["ring_amt"] = vec_np(c.ring_amt);
+        d["hll"] = vec_np(c.hll);
+        d["rt"] = py::array_t<uint8_t>(c.rt.size() * sizeof(AcctRT), reinterpret_cast<const uint8_t*>(c.rt.data()));
+        d["batch"] = py::array_t<uint8_t>(c.batch.size() * sizeof(AcctBatch),
+                                          reinterpret_cast<const uint8_t*>(c.batch.data()));
+        d["ext"] = vec_np(c.ext);
+        d["ev"] = vec_np(c.ev);
+        return d;
+      })
+      .def("load_state", [](CpuScorer& c, py::dict d) {
+        auto load = [&](const char* k, void* dst, size_t nbytes) {
+          py::array a = d[k].cast<py::array>();
+          if ((size_t)a.nbytes() != nbytes) throw std::runtime_error(std::string("state size mismatch: ") + k);
+          std::memcpy(dst, py::array::ensure(a, py::array::c_style).data(), nbytes);
+        };
+        load("ring_ts", c.ring_ts.data(), c.ring_ts.size() * 4);
+        load("ring_amt", c.ring_amt.data(), c.ring_amt.size() * 8);
+        load("hll", c.hll.data(), c.hll.size());
+        load("rt", c.rt.data(), c.rt.size() * sizeof(AcctRT));
+        load("batch", c.batch.data(), c.batch.size() * sizeof(AcctBatch));
+        load("ext", c.ext.data(), c.ext.size() * 4);
+        load("ev", c.ev.data(), c.ev.size() * 2);
+      })
+      .def_property_readonly("capacity", &CpuScorer::capacity);
 
   // results: uint32[n,2] (ResultRec), feats: int32[n,32] (FeatRec) or None, ms: int64[n] or None
   auto view = [](py::array res, py::object feat, py::object ms, wire::ResultView& v,

@@ -13,6 +13,7 @@ reference's no-op interceptor lists).
 """
 from __future__ import annotations
 
+import asyncio
 import threading
 import time
 from concurrent import futures
@@ -334,9 +335,124 @@ def _with_deps(fname: str):
     return out
 
 
-# ============================================================================ server
+# ============================================================================ asyncio server
+class AioInterceptor(grpc.aio.ServerInterceptor):
+    """The reference's interceptor chain (main.go:303-353) as one async wrapper: recovery
+    (exceptions -> INTERNAL "internal server error"), metrics, logging (OK at debug, errors
+    at info)."""
+
+    def __init__(self, metrics):
+        self.m = metrics
+
+    async def intercept_service(self, continuation, details):
+        h = await continuation(details)
+        if h is None or h.unary_unary is None:
+            return h
+        inner, method = h.unary_unary, details.method
+        short = method.rsplit("/", 1)[-1]
+        m = self.m
+
+        async def call(req, ctx):
+            t0 = time.perf_counter()
+            code = "OK"
+            try:
+                return await inner(req, ctx)
+            except InvalidArgument as e:
+                code = "INVALID_ARGUMENT"
+                await ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+            except grpc.aio.AbortError:
+                c = ctx.code() if hasattr(ctx, "code") else None
+                code = c.name if c is not None else "ABORTED"
+                raise
+            except Exception:
+                code = "INTERNAL"
+                log.error("panic recovered", exc_info=True, extra={"fields": dict(method=method)})
+                await ctx.abort(grpc.StatusCode.INTERNAL, "internal server error")
+            finally:
+                dt = time.perf_counter() - t0
+                m.requests.labels(method=short, code=code).inc()
+                m.latency.labels(method=short).observe(dt)
+                if code != "OK":
+                    log.info("grpc request failed", extra={"fields": dict(method=method, code=code,
+                                                                          duration_ms=round(dt * 1e3, 3))})
+                elif log.isEnabledFor(10):
+                    log.debug("grpc request", extra={"fields": dict(method=method, duration_ms=round(dt * 1e3, 3))})
+
+        return grpc.unary_unary_rpc_method_handler(call, request_deserializer=h.request_deserializer,
+                                                   response_serializer=h.response_serializer)
+
+
+INLINE = {"CheckBlacklist", "GetThresholds"}   # pure host work: never leaves the event loop
+
+
+def aio_risk_handler(servicer: RiskServicer, pool, inline_all: bool) -> grpc.GenericRpcHandler:
+    """Async adapters over RiskServicer. Work that may wait on a GPU runs in ``pool`` so the
+    event loop keeps accepting calls; on the CPU backend everything runs inline (cheapest)."""
+    handlers = {}
+    for rpc, req_name, resp_name in P.METHODS:
+        fn = getattr(servicer, rpc)
+        if rpc == "ScoreTransaction" and servicer.batcher is not None:
+            async def h(data, ctx, _b=servicer.batcher):
+                return await asyncio.wrap_future(_b.submit(data, time.perf_counter()))
+        elif inline_all or rpc in INLINE:
+            async def h(req, ctx, _f=fn):
+                return _f(req, ctx)
+        else:
+            async def h(req, ctx, _f=fn):
+                return await asyncio.get_running_loop().run_in_executor(pool, _f, req, ctx)
+        if rpc in RAW:
+            handlers[rpc] = grpc.unary_unary_rpc_method_handler(h)
+        else:
+            handlers[rpc] = grpc.unary_unary_rpc_method_handler(
+                h, request_deserializer=P.M[req_name].FromString, response_serializer=lambda m: m.SerializeToString())
+    return grpc.method_handlers_generic_handler(P.SERVICE, handlers)
+
+
+def aio_health_handler(h: HealthServicer) -> grpc.GenericRpcHandler:
+    ser = lambda m: m.SerializeToString()  # noqa: E731
+
+    async def check(req, ctx):
+        with h._cv:
+            st = h._status.get(req.service)
+        if st is None:
+            await ctx.abort(grpc.StatusCode.NOT_FOUND, "unknown service")
+        return HV.HealthCheckResponse(status=st)
+
+    async def watch(req, ctx):
+        last = None
+        while True:
+            with h._cv:
+                st = h._status.get(req.service, HV.STATUS["SERVICE_UNKNOWN"])
+            if st != last:
+                last = st
+                yield HV.HealthCheckResponse(status=st)
+            await asyncio.sleep(0.2)
+
+    return grpc.method_handlers_generic_handler(HV.SERVICE, {
+        "Check": grpc.unary_unary_rpc_method_handler(check, request_deserializer=HV.HealthCheckRequest.FromString,
+                                                     response_serializer=ser),
+        "Watch": grpc.unary_stream_rpc_method_handler(watch, request_deserializer=HV.HealthCheckRequest.FromString,
+                                                      response_serializer=ser),
+    })
+
+
+def aio_reflection_handler(pkg: str) -> grpc.GenericRpcHandler:
+    sync = reflection_handler(pkg)
+    info = sync.service(type("D", (), {"method": f"/{pkg}.ServerReflection/ServerReflectionInfo"})()).stream_stream
+
+    async def ainfo(req_iter, ctx):
+        async for raw in req_iter:
+            for out in info(iter([raw]), ctx):
+                yield out
+
+    return grpc.method_handlers_generic_handler(f"{pkg}.ServerReflection", {
+        "ServerReflectionInfo": grpc.stream_stream_rpc_method_handler(ainfo)})
+
+
 class RiskServer:
-    def __init__(self, engine, port: int = 0, host: str = "127.0.0.1", workers: int = 64,
+    """risk.v1 on a ``grpc.aio`` server whose event loop runs on a dedicated thread."""
+
+    def __init__(self, engine, port: int = 0, host: str = "127.0.0.1", workers: int = 16,
                  batching: bool = True, max_batch: Optional[int] = None, wait_us: Optional[int] = None):
         self.engine = engine
         cfg = engine.cfg
@@ -347,24 +463,37 @@ class RiskServer:
                                         on_batch=lambda n: engine.metrics.batch_size.observe(n))
         self.health = HealthServicer()
         self.health.set(P.SERVICE, "SERVING")
-        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers),
-                                  interceptors=[LoggingInterceptor(), RecoveryInterceptor(),
-                                                MetricsInterceptor(engine.metrics)],
-                                  options=[("grpc.max_receive_message_length", 64 << 20),
-                                           ("grpc.max_send_message_length", 64 << 20)])
-        self.server.add_generic_rpc_handlers([risk_handler(RiskServicer(engine, self.batcher)),
-                                              health_handler(self.health)] +
-                                             [reflection_handler(p) for p in RV.PKGS])
-        self.port = self.server.add_insecure_port(f"{host}:{port}")
+        self.pool = futures.ThreadPoolExecutor(max_workers=workers, thread_name_prefix="risk-rpc")
+        self._servicer = RiskServicer(engine, self.batcher)
+        self._host, self._port_req = host, port
+        self.loop = asyncio.new_event_loop()
+        self._thread = threading.Thread(target=self.loop.run_forever, name="risk-grpc-loop", daemon=True)
+        self._thread.start()
+        self.server = None
+        self.port = asyncio.run_coroutine_threadsafe(self._build(), self.loop).result(30)
+
+    async def _build(self) -> int:
+        self.server = grpc.aio.server(interceptors=[AioInterceptor(self.engine.metrics)],
+                                      options=[("grpc.max_receive_message_length", 64 << 20),
+                                               ("grpc.max_send_message_length", 64 << 20),
+                                               ("grpc.so_reuseport", 0)])
+        inline = self.engine.kind != "gpu" and self.engine.group is None
+        self.server.add_generic_rpc_handlers([aio_risk_handler(self._servicer, self.pool, inline),
+                                              aio_health_handler(self.health)] +
+                                             [aio_reflection_handler(p) for p in RV.PKGS])
+        return self.server.add_insecure_port(f"{self._host}:{self._port_req}")
 
     def start(self) -> "RiskServer":
-        self.server.start()
+        asyncio.run_coroutine_threadsafe(self.server.start(), self.loop).result(30)
         log.info("grpc server listening", extra={"fields": dict(port=self.port)})
         return self
 
     def stop(self, grace: float = 5.0) -> None:
         self.health.set("", "NOT_SERVING")
         self.health.set(P.SERVICE, "NOT_SERVING")
-        self.server.stop(grace).wait()
+        asyncio.run_coroutine_threadsafe(self.server.stop(grace), self.loop).result(grace + 30)
+        self.loop.call_soon_threadsafe(self.loop.stop)
+        self._thread.join(timeout=5)
+        self.pool.shutdown(wait=False)
         if self.batcher is not None:
             self.batcher.close()

@@ -47,9 +47,10 @@ def _featrec_from_golden(f, row, bl: bool, rule: int, reasons) -> np.ndarray:
 
 
 class CpuBackend:
-    """Golden-semantics scorer on the host; the feature store is keyed by slot."""
+    """Golden-semantics scorer on the host (the pure-Python spec; ``backend="golden"``)."""
 
     kind = "cpu"
+    snapshot_ext = "json"
 
     def __init__(self, cfg: Config, model: str = "heuristic", executor=None, input_name: str = "input",
                  output_name: str = "output", ml_col: int = 0,
@@ -239,6 +240,7 @@ class GpuBackend:
     """One GPU shard: HBM feature store + captured-graph scorer."""
 
     kind = "gpu"
+    snapshot_ext = "npz"
 
     def __init__(self, cfg: Config, capacity: int, device, plan=None, model: str = "plan",
                  blacklist: Optional[Blacklist] = None, ipintel: Optional[IPIntel] = None,
@@ -377,3 +379,98 @@ class GpuBackend:
 
     def metrics(self) -> np.ndarray:
         return self.scorer.read_metrics()
+
+
+class NativeCpuBackend:
+    """CPU shard on the C++ ``CpuScorer`` (csrc/runtime/cpu_scorer.cpp): the same SoA state and
+    record formats as the GPU store, GIL released while scoring. The default CPU backend."""
+
+    kind = "cpu"
+    snapshot_ext = "npz"
+
+    def __init__(self, cfg: Config, capacity: int, model: str = "heuristic", executor=None,
+                 input_name: str = "input", output_name: str = "output", ml_col: int = 0,
+                 blacklist: Optional[Blacklist] = None, ipintel: Optional[IPIntel] = None):
+        from ..native import native
+        if model == "plan" and executor is None:
+            model = "none"
+        self.cfg = cfg
+        self.model = model
+        f = cfg.features
+        self.sc = native().CpuScorer(int(capacity), f.ring_size, f.event_ring, f.event_dim, f.width - 30)
+        self.sc.set_model(executor if model == "plan" else None, input_name, output_name, ml_col)
+        self.blacklist = blacklist or Blacklist()
+        self.ipintel = ipintel or IPIntel()
+        self.scoring = cfg.scoring
+        self._tables_version = None
+        self._lock = threading.RLock()
+        self.refresh_config()
+
+    def refresh_config(self, scoring=None) -> None:
+        from ..layouts import MODEL_HEURISTIC, MODEL_NONE, MODEL_OUTPUT, score_cfg
+        with self._lock:
+            if scoring is not None:
+                self.scoring = scoring
+            b, t = self.blacklist.table, self.ipintel.table
+            kind = {"none": MODEL_NONE, "heuristic": MODEL_HEURISTIC, "plan": MODEL_OUTPUT}[self.model]
+            c = score_cfg(self.cfg, kind, sc=self.scoring, bl_mask=b.mask, bl_max_probe=max(b.max_probe, 1),
+                          ip_mask=t.mask, ip_max_probe=max(t.max_probe, 1))
+            self.sc.set_cfg(c.view(np.uint8))
+            v = (b.version, t.version)
+            if v != self._tables_version:
+                self.sc.set_tables(b.keys, b.vals, t.keys, t.vals)
+                self._tables_version = v
+
+    def _sync(self) -> None:
+        if (self.blacklist.table.version, self.ipintel.table.version) != self._tables_version:
+            self.refresh_config()
+
+    def set_batch_rows(self, slots, rows) -> None:
+        self.sc.set_batch(np.asarray(slots, np.int32), np.ascontiguousarray(rows, ACCTBATCH).view(np.uint8))
+
+    def set_ext(self, slots, ext) -> None:
+        if self.cfg.features.width > 30:
+            self.sc.set_ext(np.asarray(slots, np.int32), np.asarray(ext, np.float32).reshape(len(slots), -1))
+
+    def reset_accounts(self, slots) -> None:
+        self.sc.reset(np.asarray(slots, np.int32))
+
+    def ingest(self, events: np.ndarray) -> None:
+        self.sc.ingest(np.ascontiguousarray(events, REQREC).view(np.uint8))
+
+    def score(self, req: np.ndarray, now: Optional[int] = None, want_features: bool = True,
+              update: bool = True) -> Result:
+        now = int(time.time()) if now is None else int(now)
+        self._sync()
+        res, feat = self.sc.score(np.ascontiguousarray(req, REQREC).view(np.uint8), now, update, want_features)
+        return res, (feat.view(FEATREC).reshape(-1) if feat is not None else None)
+
+    def submit(self, req: np.ndarray, now: Optional[int] = None, want_features: bool = True):
+        return self.score(req, now, want_features)
+
+    def collect(self, pending) -> Result:
+        return pending
+
+    def features(self, slot: int, now: int) -> np.ndarray:
+        self._sync()
+        return self.sc.features(int(slot), int(now)).view(FEATREC)[0]
+
+    def event_history(self, slot: int) -> np.ndarray:
+        return self.sc.event_history(int(slot))
+
+    def metrics(self):
+        return None
+
+    def snapshot(self, path: str) -> None:
+        import os
+        st = self.sc.state()
+        tmp = path + ".tmp.npz"
+        np.savez(tmp, version=np.array([1]), ring_size=np.array([self.cfg.features.ring_size]), **st)
+        os.replace(tmp, path)
+
+    def restore(self, path: str) -> int:
+        with np.load(path, allow_pickle=False) as z:
+            if int(z["ring_size"][0]) != self.cfg.features.ring_size:
+                raise ValueError("snapshot ring size differs from the configured ring size")
+            self.sc.load_state({k: z[k] for k in ("ring_ts", "ring_amt", "hll", "rt", "batch", "ext", "ev")})
+        return self.sc.capacity

@@ -31,7 +31,7 @@ from ..native import native
 from ..obs.logging import get_logger
 from ..obs.metrics import Metrics
 from ..utils.faults import Faults, InjectedFault
-from .backends import CpuBackend, GpuBackend
+from .backends import CpuBackend, GpuBackend, NativeCpuBackend
 from .registry import AccountRegistry
 
 log = get_logger("engine")
@@ -84,6 +84,8 @@ class RiskEngine:
             self.devices = list(devices)
             world = len(self.devices)
         else:
+            if backend not in ("cpu", "golden"):
+                raise ValueError(f"backend must be auto|gpu|cpu|golden, got {backend!r}")
             self.devices = []
             world = max(int(shards), 1)
         self.world = world
@@ -134,10 +136,10 @@ class RiskEngine:
                 self.metrics.gpu_healthy.labels(gpu=str(d)).set(1)
         else:
             for _ in range(world):
-                self.backends.append(self._cpu_backend(mkind, fm))
-        self.fallback: Optional[CpuBackend] = None
-        if cfg.gpu.fallback == "cpu":  # degraded tier: golden scorer without the shard's feature state
-            self.fallback = self._cpu_backend(mkind, fm)
+                self.backends.append(self._cpu_backend(mkind, fm, backend, self.capacity))
+        self.fallback = None
+        if cfg.gpu.fallback == "cpu":  # degraded tier: CPU scorer without the shard's feature state
+            self.fallback = self._cpu_backend(mkind, fm, "golden" if backend == "golden" else "cpu", 1)
 
         # ---- LTV / abuse services
         from .abuse import AbuseGpu, AbuseService
@@ -187,7 +189,9 @@ class RiskEngine:
         log.info("risk engine ready", extra={"fields": dict(backend=backend, shards=world, capacity=self.capacity,
                                                               model=mkind)})
 
-    def _cpu_backend(self, mkind, fm) -> CpuBackend:
+    def _cpu_backend(self, mkind, fm, kind: str = "cpu", capacity: int = 1):
+        if kind == "cpu":
+            return make_local_backend(self.cfg, "cpu", capacity, fm, mkind, self.blacklist, self.ipintel)
         if mkind == "onnx":
             ml_col, out_name = 0, self.cfg.fraud_model.output_name
             try:
@@ -500,10 +504,11 @@ class RiskEngine:
             if self.group is not None:
                 continue
             be = self.backends[o]
+            path = os.path.join(directory, f"shard{o}.{be.snapshot_ext}")
             if be.kind == "gpu":
-                be.store.snapshot(os.path.join(directory, f"shard{o}.npz"), n_used=max(n, 1))
+                be.store.snapshot(path, n_used=max(n, 1))
             else:
-                be.snapshot(os.path.join(directory, f"shard{o}.json"))
+                be.snapshot(path)
         if self.group is not None:
             self.group.snapshot(directory, [self.registry.size(o) for o in range(self.world)])
         tmp = os.path.join(directory, "registry.json.tmp")
@@ -527,10 +532,11 @@ class RiskEngine:
             if self.group is not None:
                 continue
             be = self.backends[o]
+            path = os.path.join(directory, f"shard{o}.{be.snapshot_ext}")
             if be.kind == "gpu":
-                be.store.restore(os.path.join(directory, f"shard{o}.npz"))
+                be.store.restore(path)
             else:
-                be.restore(os.path.join(directory, f"shard{o}.json"))
+                be.restore(path)
         if self.group is not None:
             self.group.restore(directory)
         return total
@@ -549,6 +555,8 @@ def make_local_backend(cfg: Config, kind: str, capacity: int, fm, mkind: str, bl
         return GpuBackend(cfg, capacity, dev, plan=plan, model=model, blacklist=blacklist, ipintel=ipintel,
                           capture=capture, owner_filter=owner_filter, rank=rank)
     N = native()
+    cls = CpuBackend if kind == "golden" else NativeCpuBackend
+    kw = {} if kind == "golden" else {"capacity": capacity}
     if mkind == "onnx":
         from ..models.plan import compile_onnx
         ml_col, out_name = 0, cfg.fraud_model.output_name
@@ -557,9 +565,9 @@ def make_local_backend(cfg: Config, kind: str, capacity: int, fm, mkind: str, bl
             ml_col, out_name = p.ml_col, p.output_name
         except Exception:
             pass
-        return CpuBackend(cfg, model="plan", executor=N.Executor(fm), input_name=fm.inputs()[0][0],
-                          output_name=out_name, ml_col=ml_col, blacklist=blacklist, ipintel=ipintel)
-    return CpuBackend(cfg, model=mkind, blacklist=blacklist, ipintel=ipintel)
+        return cls(cfg, model="plan", executor=N.Executor(fm), input_name=fm.inputs()[0][0],
+                   output_name=out_name, ml_col=ml_col, blacklist=blacklist, ipintel=ipintel, **kw)
+    return cls(cfg, model=mkind, blacklist=blacklist, ipintel=ipintel, **kw)
 
 
 def make_abuse_gpu(cfg: Config, local, abuse_model):

@@ -7,8 +7,11 @@ engines (tests, multi-tenant) never collide.
 """
 from __future__ import annotations
 
+import threading
+
 import numpy as np
 from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, generate_latest
+from prometheus_client.core import CounterMetricFamily
 
 LAT_BUCKETS = (0.0001, 0.00025, 0.0005, 0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1.0, 2.5)
 ACTIONS = {1: "approve", 2: "review", 3: "block"}
@@ -19,11 +22,12 @@ class Metrics:
         r = self.registry = CollectorRegistry()
         self.requests = Counter("risk_requests_total", "RPCs by method and status code", ["method", "code"], registry=r)
         self.latency = Histogram("risk_latency_seconds", "RPC latency", ["method"], buckets=LAT_BUCKETS, registry=r)
-        self.scores = Counter("risk_scores_total", "transactions scored", registry=r)
-        self.score_bucket = Counter("risk_score_bucket_total", "final scores by decile", ["decile"], registry=r)
-        self.actions = Counter("risk_action_total", "decisions by action", ["action"], registry=r)
-        self.ml_high = Counter("risk_ml_high_risk_total", "ML score above the high-risk threshold", registry=r)
-        self.blacklist_hits = Counter("risk_blacklist_hits_total", "requests matching the blacklist", registry=r)
+        # decision counters: plain accumulators on the hot path, exported at scrape time
+        self._lock = threading.Lock()
+        self._dec = [0] * 11
+        self._act = [0] * 4
+        self._n = self._ml_high = self._bl = 0
+        r.register(_DecisionCollector(self))
         self.batch_size = Histogram("gpu_batch_size", "rows per device micro-batch",
                                     buckets=(1, 8, 64, 256, 1024, 4096, 8192), registry=r)
         self.step = Histogram("gpu_step_seconds", "device step time by phase", ["phase"], buckets=LAT_BUCKETS,
@@ -35,29 +39,59 @@ class Metrics:
         self.accounts = Gauge("risk_accounts", "accounts resident in the feature store", ["gpu"], registry=r)
 
     def observe_results(self, res: np.ndarray, feats=None) -> None:
-        """Vectorised decision accounting from ResultRec rows (uint32 [n,2])."""
+        """Decision accounting from ResultRec rows (uint32 [n,2])."""
         n = len(res)
         if n == 0:
             return
+        if n <= 8:  # unary path: plain ints, no numpy temporaries
+            with self._lock:
+                for p in res[:, 0].tolist():
+                    self._dec[min((p & 0xFF) // 10, 10)] += 1
+                    self._act[(p >> 16) & 3] += 1
+                    self._ml_high += (p >> 28) & 1
+                    self._bl += (p >> 27) & 1
+                self._n += n
+            return
         p = res[:, 0].astype(np.uint32)
-        score = (p & 0xFF).astype(np.int64)
-        action = ((p >> 16) & 3).astype(np.int64)
-        reasons = p >> 20
-        self.scores.inc(n)
-        dec = np.bincount(np.minimum(score // 10, 10), minlength=11)
-        for d, c in enumerate(dec):
-            if c:
-                self.score_bucket.labels(decile=str(d * 10)).inc(int(c))
-        act = np.bincount(action, minlength=4)
-        for a, name in ACTIONS.items():
-            if act[a]:
-                self.actions.labels(action=name).inc(int(act[a]))
-        hi = int(np.count_nonzero(reasons & (1 << 8)))
-        if hi:
-            self.ml_high.inc(hi)
-        bl = int(np.count_nonzero(reasons & (1 << 7)))
-        if bl:
-            self.blacklist_hits.inc(bl)
+        dec = np.bincount(np.minimum((p & 0xFF) // 10, 10), minlength=11)
+        act = np.bincount((p >> 16) & 3, minlength=4)
+        hi = int(np.count_nonzero(p & (1 << 28)))
+        bl = int(np.count_nonzero(p & (1 << 27)))
+        with self._lock:
+            for i in range(11):
+                self._dec[i] += int(dec[i])
+            for i in range(4):
+                self._act[i] += int(act[i])
+            self._ml_high += hi
+            self._bl += bl
+            self._n += n
 
     def render(self) -> bytes:
         return generate_latest(self.registry)
+
+
+class _DecisionCollector:
+    def __init__(self, m: Metrics):
+        self.m = m
+
+    def collect(self):
+        m = self.m
+        with m._lock:
+            dec, act, n, hi, bl = list(m._dec), list(m._act), m._n, m._ml_high, m._bl
+        c = CounterMetricFamily("risk_scores", "transactions scored")
+        c.add_metric([], n)
+        yield c
+        c = CounterMetricFamily("risk_score_bucket", "final scores by decile", labels=["decile"])
+        for d, v in enumerate(dec):
+            c.add_metric([str(d * 10)], v)
+        yield c
+        c = CounterMetricFamily("risk_action", "decisions by action", labels=["action"])
+        for a, name in ACTIONS.items():
+            c.add_metric([name], act[a])
+        yield c
+        c = CounterMetricFamily("risk_ml_high_risk", "ML score above the high-risk threshold")
+        c.add_metric([], hi)
+        yield c
+        c = CounterMetricFamily("risk_blacklist_hits", "requests matching the blacklist")
+        c.add_metric([], bl)
+        yield c

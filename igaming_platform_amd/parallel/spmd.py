@@ -148,7 +148,7 @@ class ShardRunner:
         if op in (OP_SNAPSHOT, OP_RESTORE):  # payload: {"dir": ..., "used": [slots in use per rank]}
             import os
             meta = json.loads(payload.decode())
-            path = os.path.join(meta["dir"], f"shard{self.rank}." + ("npz" if self.be.kind == "gpu" else "json"))
+            path = os.path.join(meta["dir"], f"shard{self.rank}.{self.be.snapshot_ext}")
             if op == OP_SNAPSHOT:
                 if self.be.kind == "gpu":
                     self.be.store.snapshot(path, n_used=max(int(meta["used"][self.rank]), 1))

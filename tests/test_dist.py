@@ -105,4 +105,4 @@ def test_spmd_serving_matches_single_process(world, tmp_path):
     assert len(served) == world - 1 and all(n > 10 for n in served)
     # every rank wrote its own shard file; rank 0 the registry
     names = sorted(os.listdir(tmp_path / "spmd"))
-    assert names == ["registry.json"] + [f"shard{r}.json" for r in range(world)]
+    assert names == ["registry.json"] + [f"shard{r}.npz" for r in range(world)]

@@ -229,3 +229,35 @@ def test_onnx_fraud_model_cpu():
     eng = RiskEngine(cfg, backend="cpu", capacity=50, fraud_model=m)
     r = eng.score([dict(account_id="m", amount=1000, transaction_type="deposit")], now=NOW)[0]
     assert 0.0 < r["ml_score"] < 1.0 and eng.model_kind == "onnx"
+
+
+@pytest.mark.parametrize("log_mode,sum_mode,width", [("log1p", "sliding", 30), ("identity", "compat", 30),
+                                                     ("log1p", "sliding", 48)])
+def test_native_cpu_backend_equals_golden_backend(log_mode, sum_mode, width):
+    """The C++ CpuScorer (serving path) against the pure-Python golden backend (the spec)."""
+    cfg = Config()
+    cfg.features.log_transform, cfg.features.sum_mode, cfg.features.width = log_mode, sum_mode, width
+    rng = np.random.default_rng(11)
+    engines = [RiskEngine(cfg, backend=b, capacity=200) for b in ("cpu", "golden")]
+    ids = [f"acc-{i}" for i in range(30)]
+    rows = _batch_rows(30, rng)
+    ext = rng.standard_normal((30, width - 30)).astype(np.float32)
+    for e in engines:
+        e.load_batch_features(ids, rows)
+        if width > 30:
+            e.load_ext_features(ids, ext)
+        e.add_to_blacklist("fingerprint", "fp-7", "x", "t", expires_at=NOW + 30)
+        e.set_ip_intel("10.1.4.3", proxy=True)
+        e.ingest_events([dict(account_id=f"acc-{i % 30}", amount=100 + i, transaction_type="deposit",
+                              device_id=f"d{i % 4}", ts=NOW - 4000 + 37 * i) for i in range(120)])
+    for step in range(5):
+        txs = _txs(50, rng)
+        a, b = (e.score(txs, now=NOW + 17 * step) for e in engines)
+        for x, y in zip(a, b):
+            assert (x["score"], x["action"], x["reason_codes"], x["rule_score"]) == \
+                   (y["score"], y["action"], y["reason_codes"], y["rule_score"])
+            assert x["ml_score"] == pytest.approx(y["ml_score"], abs=1e-7)
+            assert x["features"].tobytes() == y["features"].tobytes()
+    for i in range(30):
+        assert engines[0].get_features(f"acc-{i}", NOW + 99).tobytes() == \
+               engines[1].get_features(f"acc-{i}", NOW + 99).tobytes()
