@@ -254,6 +254,10 @@ PYBIND11_MODULE(_hipk, m) {
     a.head_b = d.contains("head_b") ? d["head_b"].cast<float>() : 0.f;
     a.head_act = geti(d, "head_act");
     a.out = ptr<float*>(d, "out");
+    a.tile_rows = geti(d, "tile_rows");
+    a.waves = geti(d, "waves");
+    a.pipeline = geti(d, "pipeline", 1);
+    if (a.tile_rows != 0 && a.tile_rows != 16 && a.tile_rows != 32) throw std::runtime_error("gru: tile_rows 16|32");
     if (a.H != 64 && a.H != 128 && a.H != 256) throw std::runtime_error("gru: H must be 64, 128 or 256");
     if (a.layer[0].kx_pad != 32 && a.layer[0].kx_pad != 64) throw std::runtime_error("gru: input dim must pad to 32 or 64");
     if (a.n_layers == 2 && a.layer[1].kx_pad != a.H) throw std::runtime_error("gru: layer 2 input must be H");

@@ -27,9 +27,27 @@ constexpr int GRU_PAD = 8;  // bf16 row padding in LDS (16 B)
 __device__ __forceinline__ float sig_(float x) { return 1.f / (1.f + __expf(-x)); }
 __device__ __forceinline__ float tanh_(float x) { return 1.f - 2.f / (__expf(2.f * x) + 1.f); }
 
-__device__ __forceinline__ bf16x8 ld_frag(const uint16_t* P, int nt, int KS, int ks, int lane) {
-  const uint4 v = *reinterpret_cast<const uint4*>(P + ((((size_t)nt * KS + ks) * 64 + lane) << 3));
-  return *reinterpret_cast<const bf16x8*>(&v);
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+// Weight fragments come through a buffer resource: the per-lane part is ONE VGPR (lane*16)
+// shared by every fragment load and the fragment index goes into the scalar offset, so no
+// 64-bit per-load addresses are materialised (they were hoisted out of the time loop and spilled).
+struct WFrag {
+  __amdgpu_buffer_rsrc_t rsrc;
+  int voff;
+};
+
+__device__ __forceinline__ WFrag wfrag(const uint16_t* base, size_t elems, int lane) {
+  WFrag w;
+  w.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), 0, (int)(elems * 2), 0x00020000);
+  w.voff = lane * 16;
+  return w;
+}
+
+__device__ __forceinline__ bf16x8 ld_frag(const WFrag& w, int nt, int KS, int ks) {
+  const int soff = __builtin_amdgcn_readfirstlane((nt * KS + ks) * 1024);
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(w.rsrc, w.voff, soff, 0);
+  return __builtin_bit_cast(bf16x8, v);
 }
 
 __device__ __forceinline__ bf16x8 lds_frag(const uint16_t* base, int stride, int row, int k) {
@@ -39,152 +57,145 @@ __device__ __forceinline__ bf16x8 lds_frag(const uint16_t* base, int stride, int
 
 
 // One GRU layer step for this wave's hidden tiles. KSX/KSH: K/32 of the input / hidden parts.
-template <int RT, int KSX, int KSH, int LBR>
-__device__ __forceinline__ void layer_step(const GruLayerArgs& g, const float* bias, const uint16_t* in,
+// The recurrence is latency-bound on the streamed weight fragments: tiles are processed in
+// groups of G (G*RT <= 2, so accumulators stay at 32 floats) and every k-step issues the
+// 3*G fragments of the group at once; with the k loop unrolled by 2 ~12 loads are in flight.
+template <int RT, int KSX, int KSH, int LBR, int NW>
+__device__ __forceinline__ void layer_step(const WFrag& gW, const WFrag& gR, const float* bias, const uint16_t* in,
                                            int in_stride, const uint16_t* hprev, uint16_t* hnext,
-                                           uint16_t* rb, float (&hs)[KSH / 2][RT][4], int lane, int wave) {
+                                           uint16_t* rb, float (&hs)[KSH * 2 / NW][RT][4], int lane, int wave) {
   constexpr int HT = KSH * 2;      // hidden tiles of 16 units
-  constexpr int HTW = KSH / 2;     // per wave (4 waves)
+  constexpr int HTW = HT / NW;     // per wave
+  constexpr int G = (RT == 1 && HTW >= 2) ? 2 : 1;
   constexpr int H = KSH * 32;
   constexpr int HS = H + GRU_PAD;
   const int arow = lane & 15, akof = 8 * (lane >> 4);
   const int crow = (lane >> 4) * 4, ccol = lane & 15;
-  if constexpr (LBR != 0) {
+  float zk[LBR ? 1 : HTW][RT][4];  // linear_before_reset = 0: z and the x-part of h~ wait for r*h
+  float xk[LBR ? 1 : HTW][RT][4];
 #pragma unroll
-    for (int i = 0; i < HTW; ++i) {
-      const int ht = wave + 4 * i;
-      f32x4 az[RT], ar[RT], ax[RT], ah[RT];
+  for (int g0 = 0; g0 < HTW; g0 += G) {
+    f32x4 az[G][RT], ar[G][RT], ax[G][RT], ah[G][RT];
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) az[rt] = ar[rt] = ax[rt] = ah[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-      for (int ks = 0; ks < KSX; ++ks) {
-        const bf16x8 bz = ld_frag(g.W, ht, KSX, ks, lane);
-        const bf16x8 br = ld_frag(g.W, HT + ht, KSX, ks, lane);
-        const bf16x8 bh = ld_frag(g.W, 2 * HT + ht, KSX, ks, lane);
+    for (int u = 0; u < G; ++u)
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-          const bf16x8 a = lds_frag(in, in_stride, rt * 16 + arow, ks * 32 + akof);
-          az[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bz, az[rt], 0, 0, 0);
-          ar[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, br, ar[rt], 0, 0, 0);
-          ax[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, ax[rt], 0, 0, 0);
+      for (int rt = 0; rt < RT; ++rt) az[u][rt] = ar[u][rt] = ax[u][rt] = ah[u][rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KSX; ++ks) {  // input projection x_t . W^T
+      bf16x8 bz[G], br[G], bh[G];
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        const int ht = wave + NW * (g0 + u);
+        bz[u] = ld_frag(gW, ht, KSX, ks);
+        br[u] = ld_frag(gW, HT + ht, KSX, ks);
+        bh[u] = ld_frag(gW, 2 * HT + ht, KSX, ks);
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const bf16x8 a = lds_frag(in, in_stride, rt * 16 + arow, ks * 32 + akof);
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+          az[u][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bz[u], az[u][rt], 0, 0, 0);
+          ar[u][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, br[u], ar[u][rt], 0, 0, 0);
+          ax[u][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh[u], ax[u][rt], 0, 0, 0);
         }
       }
+    }
 #pragma unroll 2
-      for (int ks = 0; ks < KSH; ++ks) {
-        const bf16x8 bz = ld_frag(g.R, ht, KSH, ks, lane);
-        const bf16x8 br = ld_frag(g.R, HT + ht, KSH, ks, lane);
-        const bf16x8 bh = ld_frag(g.R, 2 * HT + ht, KSH, ks, lane);
+    for (int ks = 0; ks < KSH; ++ks) {  // recurrent projection h_{t-1} . R^T
+      bf16x8 bz[G], br[G], bh[G];
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-          const bf16x8 a = lds_frag(hprev, HS, rt * 16 + arow, ks * 32 + akof);
-          az[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bz, az[rt], 0, 0, 0);
-          ar[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, br, ar[rt], 0, 0, 0);
-          ah[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, ah[rt], 0, 0, 0);
+      for (int u = 0; u < G; ++u) {
+        const int ht = wave + NW * (g0 + u);
+        bz[u] = ld_frag(gR, ht, KSH, ks);
+        br[u] = ld_frag(gR, HT + ht, KSH, ks);
+        if constexpr (LBR != 0) bh[u] = ld_frag(gR, 2 * HT + ht, KSH, ks);
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const bf16x8 a = lds_frag(hprev, HS, rt * 16 + arow, ks * 32 + akof);
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+          az[u][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bz[u], az[u][rt], 0, 0, 0);
+          ar[u][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, br[u], ar[u][rt], 0, 0, 0);
+          if constexpr (LBR != 0) ah[u][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh[u], ah[u][rt], 0, 0, 0);
         }
       }
-      const int j = ht * 16 + ccol;
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const int i = g0 + u;
+      const int j = (wave + NW * i) * 16 + ccol;
       const float bz_ = bias[j] + bias[3 * H + j];
       const float br_ = bias[H + j] + bias[4 * H + j];
-      const float bxh = bias[2 * H + j], bhh = bias[5 * H + j];
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float z = sig_(az[rt][r] + bz_);
-          const float rr = sig_(ar[rt][r] + br_);
-          const float hh = tanh_(ax[rt][r] + bxh + rr * (ah[rt][r] + bhh));
-          const float h = (1.f - z) * hh + z * hs[i][rt][r];
-          hs[i][rt][r] = h;
-          hnext[(rt * 16 + crow + r) * HS + j] = f32_to_bf16(h);
+          const float z = sig_(az[u][rt][r] + bz_);
+          const float rr = sig_(ar[u][rt][r] + br_);
+          if constexpr (LBR != 0) {
+            const float hh = tanh_(ax[u][rt][r] + bias[2 * H + j] + rr * (ah[u][rt][r] + bias[5 * H + j]));
+            const float h = (1.f - z) * hh + z * hs[i][rt][r];
+            hs[i][rt][r] = h;
+            hnext[(rt * 16 + crow + r) * HS + j] = f32_to_bf16(h);
+          } else {
+            zk[i][rt][r] = z;
+            xk[i][rt][r] = ax[u][rt][r];
+            rb[(rt * 16 + crow + r) * HS + j] = f32_to_bf16(rr * hs[i][rt][r]);
+          }
         }
     }
-  } else {
-    // linear_before_reset = 0: h~ = tanh(x Wh + (r * h_{t-1}) Rh + b) needs r for every unit
-    // of the row first -> phase A (z, r; r*h to LDS), block barrier, phase B (h gate).
-    float zk[HTW][RT][4];
-    f32x4 axk[HTW][RT];
-#pragma unroll
-    for (int i = 0; i < HTW; ++i) {
-      const int ht = wave + 4 * i;
-      f32x4 az[RT], ar[RT], ax[RT];
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) az[rt] = ar[rt] = ax[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-      for (int ks = 0; ks < KSX; ++ks) {
-        const bf16x8 bz = ld_frag(g.W, ht, KSX, ks, lane);
-        const bf16x8 br = ld_frag(g.W, HT + ht, KSX, ks, lane);
-        const bf16x8 bh = ld_frag(g.W, 2 * HT + ht, KSX, ks, lane);
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-          const bf16x8 a = lds_frag(in, in_stride, rt * 16 + arow, ks * 32 + akof);
-          az[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bz, az[rt], 0, 0, 0);
-          ar[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, br, ar[rt], 0, 0, 0);
-          ax[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, ax[rt], 0, 0, 0);
-        }
-      }
-#pragma unroll 2
-      for (int ks = 0; ks < KSH; ++ks) {
-        const bf16x8 bz = ld_frag(g.R, ht, KSH, ks, lane);
-        const bf16x8 br = ld_frag(g.R, HT + ht, KSH, ks, lane);
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-          const bf16x8 a = lds_frag(hprev, HS, rt * 16 + arow, ks * 32 + akof);
-          az[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bz, az[rt], 0, 0, 0);
-          ar[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, br, ar[rt], 0, 0, 0);
-        }
-      }
-      const int j = ht * 16 + ccol;
-      const float bz_ = bias[j] + bias[3 * H + j];
-      const float br_ = bias[H + j] + bias[4 * H + j];
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        axk[i][rt] = ax[rt];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          zk[i][rt][r] = sig_(az[rt][r] + bz_);
-          const float rr = sig_(ar[rt][r] + br_);
-          rb[(rt * 16 + crow + r) * HS + j] = f32_to_bf16(rr * hs[i][rt][r]);
-        }
-      }
-    }
+  }
+  if constexpr (LBR == 0) {
+    // h~ = tanh(x Wh + (r * h_{t-1}) Rh + b): needs r for every unit of the row -> barrier
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < HTW; ++i) {
-      const int ht = wave + 4 * i;
-      f32x4 ah[RT];
+    for (int g0 = 0; g0 < HTW; g0 += G) {
+      f32x4 ah[G][RT];
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) ah[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int u = 0; u < G; ++u)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) ah[u][rt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
       for (int ks = 0; ks < KSH; ++ks) {
-        const bf16x8 bh = ld_frag(g.R, 2 * HT + ht, KSH, ks, lane);
+        bf16x8 bh[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u) bh[u] = ld_frag(gR, 2 * HT + wave + NW * (g0 + u), KSH, ks);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
           const bf16x8 a = lds_frag(rb, HS, rt * 16 + arow, ks * 32 + akof);
-          ah[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, ah[rt], 0, 0, 0);
+#pragma unroll
+          for (int u = 0; u < G; ++u)
+            ah[u][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh[u], ah[u][rt], 0, 0, 0);
         }
       }
-      const int j = ht * 16 + ccol;
-      const float bxh = bias[2 * H + j], bhh = bias[5 * H + j];
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt)
+      for (int u = 0; u < G; ++u) {
+        const int i = g0 + u;
+        const int j = (wave + NW * i) * 16 + ccol;
+        const float bxh = bias[2 * H + j], bhh = bias[5 * H + j];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float hh = tanh_(axk[i][rt][r] + bxh + ah[rt][r] + bhh);
-          const float z = zk[i][rt][r];
-          const float h = (1.f - z) * hh + z * hs[i][rt][r];
-          hs[i][rt][r] = h;
-          hnext[(rt * 16 + crow + r) * HS + j] = f32_to_bf16(h);
-        }
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float hh = tanh_(xk[i][rt][r] + bxh + ah[u][rt][r] + bhh);
+            const float z = zk[i][rt][r];
+            const float h = (1.f - z) * hh + z * hs[i][rt][r];
+            hs[i][rt][r] = h;
+            hnext[(rt * 16 + crow + r) * HS + j] = f32_to_bf16(h);
+          }
+      }
     }
   }
 }
 
 }  // namespace
 
-template <int RT, int KSH>
-__device__ __forceinline__ void emit_outputs(const GruArgs& a, float (&hs)[KSH / 2][RT][4], float* red, int row0,
+template <int RT, int KSH, int NW>
+__device__ __forceinline__ void emit_outputs(const GruArgs& a, float (&hs)[KSH * 2 / NW][RT][4], float* red, int row0,
                                              int n_live, int lane, int wave, int tid) {
-  constexpr int M = RT * 16, H = KSH * 32, HTW = KSH / 2;
+  constexpr int M = RT * 16, H = KSH * 32, HTW = KSH * 2 / NW;
   const int crow = (lane >> 4) * 4, ccol = lane & 15;
   if (a.yh) {
 #pragma unroll
@@ -194,7 +205,7 @@ __device__ __forceinline__ void emit_outputs(const GruArgs& a, float (&hs)[KSH /
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = row0 + rt * 16 + crow + r;
-          if (row < n_live) a.yh[(size_t)row * H + (wave + 4 * i) * 16 + ccol] = hs[i][rt][r];
+          if (row < n_live) a.yh[(size_t)row * H + (wave + NW * i) * 16 + ccol] = hs[i][rt][r];
         }
   }
   if (a.head_w) {
@@ -205,7 +216,7 @@ __device__ __forceinline__ void emit_outputs(const GruArgs& a, float (&hs)[KSH /
       for (int r = 0; r < 4; ++r) part[rt][r] = 0.f;
 #pragma unroll
     for (int i = 0; i < HTW; ++i) {
-      const float w = a.head_w[(wave + 4 * i) * 16 + ccol];
+      const float w = a.head_w[(wave + NW * i) * 16 + ccol];
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -222,25 +233,31 @@ __device__ __forceinline__ void emit_outputs(const GruArgs& a, float (&hs)[KSH /
       }
     __syncthreads();
     if (tid < M && row0 + tid < n_live) {
-      float v = red[tid] + red[M + tid] + red[2 * M + tid] + red[3 * M + tid] + a.head_b;
+      float v = a.head_b;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v += red[w * M + tid];
       if (a.head_act == 2) v = 1.f / (1.f + expf(-v));
       a.out[row0 + tid] = v;
     }
   }
 }
 
-template <int RT, int KSX, int KSH, int LBR>
-__global__ void __launch_bounds__(256) gru_kernel(GruArgs a) {
+template <int RT, int KSX, int KSH, int LBR, int NW>
+__global__ void __launch_bounds__(NW * 64) gru_kernel(GruArgs a) {
   constexpr int M = RT * 16;
   constexpr int H = KSH * 32;
   constexpr int HS = H + GRU_PAD;
   constexpr int XS = KSX * 32 + GRU_PAD;
-  constexpr int HTW = KSH / 2;
+  constexpr int HTW = KSH * 2 / NW;
+  constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n_live = a.m_ptr ? min(*a.m_ptr, a.n_rows) : a.n_rows;
   const int row0 = blockIdx.x * M;
   if (row0 >= n_live) return;
+  const WFrag w0 = wfrag(a.layer[0].W, (size_t)3 * H * KSX * 32, lane), r0 = wfrag(a.layer[0].R, (size_t)3 * H * H, lane);
+  const WFrag w1 = wfrag(a.layer[1].W, (size_t)3 * H * H, lane), r1 = wfrag(a.layer[1].R, (size_t)3 * H * H, lane);
 
   // ---- LDS carve-up: hb[layer][pingpong][M][HS] | xb[pingpong][M][XS] | rb[M][HS] | bias[2][6H] | red[4][M]
   uint16_t* const hb = reinterpret_cast<uint16_t*>(smem);
@@ -255,11 +272,11 @@ __global__ void __launch_bounds__(256) gru_kernel(GruArgs a) {
   {
     uint32_t* z = reinterpret_cast<uint32_t*>(smem);
     const int words = (4 * M * HS + 2 * M * XS) / 2;
-    for (int i = tid; i < words; i += 256) z[i] = 0u;
+    for (int i = tid; i < words; i += NT) z[i] = 0u;
   }
-  for (int i = tid; i < 6 * H; i += 256) bias[i] = a.layer[0].bias[i];
+  for (int i = tid; i < 6 * H; i += NT) bias[i] = a.layer[0].bias[i];
   if (a.n_layers == 2)
-    for (int i = tid; i < 6 * H; i += 256) bias[6 * H + i] = a.layer[1].bias[i];
+    for (int i = tid; i < 6 * H; i += NT) bias[6 * H + i] = a.layer[1].bias[i];
 
   // ---- layer-1 input staging: thread -> (row rr, 8-element chunk c), fixed for all t
   const int I = a.I;
@@ -314,11 +331,11 @@ __global__ void __launch_bounds__(256) gru_kernel(GruArgs a) {
   for (int t = 0; t < a.T; ++t) {
     const int pb = t & 1, nb = pb ^ 1;
     const uint4 xn = (t + 1 < a.T) ? load_x(t + 1) : make_uint4(0, 0, 0, 0);
-    layer_step<RT, KSX, KSH, LBR>(a.layer[0], bias, XB(pb), XS, HB(0, pb), HB(0, nb), rb, hs0, lane, wave);
+    layer_step<RT, KSX, KSH, LBR, NW>(w0, r0, bias, XB(pb), XS, HB(0, pb), HB(0, nb), rb, hs0, lane, wave);
     __syncthreads();
     if (a.n_layers == 2) {
-      layer_step<RT, KSH, KSH, LBR>(a.layer[1], bias + 6 * H, HB(0, nb), HS, HB(1, pb), HB(1, nb), rb, hs1, lane,
-                                    wave);
+      layer_step<RT, KSH, KSH, LBR, NW>(w1, r1, bias + 6 * H, HB(0, nb), HS, HB(1, pb), HB(1, nb), rb, hs1, lane,
+                                        wave);
     }
     if (stager && t + 1 < a.T) *reinterpret_cast<uint4*>(XB(nb) + my_rr * XS + my_c * 8) = xn;
     __syncthreads();
@@ -326,28 +343,220 @@ __global__ void __launch_bounds__(256) gru_kernel(GruArgs a) {
 
   // ---- outputs from the last layer's registers (static register indexing in both branches)
   if (a.n_layers == 2)
-    emit_outputs<RT, KSH>(a, hs1, red, row0, n_live, lane, wave, tid);
+    emit_outputs<RT, KSH, NW>(a, hs1, red, row0, n_live, lane, wave, tid);
   else
-    emit_outputs<RT, KSH>(a, hs0, red, row0, n_live, lane, wave, tid);
+    emit_outputs<RT, KSH, NW>(a, hs0, red, row0, n_live, lane, wave, tid);
 #undef HB
 #undef XB
 }
 
-static size_t gru_lds_bytes(int RT, int KSX, int KSH) {
+// Two stacked layers, layer-pipelined: waves [0, NW/2) run layer 1 at step t while waves
+// [NW/2, NW) run layer 2 at step t-1 (it needs h1_{t-1} and h2_{t-2}, both complete after the
+// previous barrier). The two layers' weight-fragment load chains overlap and each step costs
+// one block barrier. Buffers: H1[s] lives in hb1[(s+1)&1], H2[s] in hb2[(s+1)&1], H[-1] = 0.
+template <int RT, int KSX, int KSH, int LBR, int NW>
+__global__ void __launch_bounds__(NW * 64) gru2_pipe_kernel(GruArgs a) {
+  constexpr int M = RT * 16;
+  constexpr int H = KSH * 32;
+  constexpr int HS = H + GRU_PAD;
+  constexpr int XS = KSX * 32 + GRU_PAD;
+  constexpr int NWL = NW / 2;               // waves per layer
+  constexpr int HTW = KSH * 2 / NWL;
+  constexpr int NT = NW * 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int layer = wave / NWL, lw = wave - layer * NWL;   // wave-uniform
+  const int n_live = a.m_ptr ? min(*a.m_ptr, a.n_rows) : a.n_rows;
+  const int row0 = blockIdx.x * M;
+  if (row0 >= n_live) return;
+  const WFrag w0 = wfrag(a.layer[0].W, (size_t)3 * H * KSX * 32, lane), r0 = wfrag(a.layer[0].R, (size_t)3 * H * H, lane);
+  const WFrag w1 = wfrag(a.layer[1].W, (size_t)3 * H * H, lane), r1 = wfrag(a.layer[1].R, (size_t)3 * H * H, lane);
+
+  // LDS: hb[layer][pingpong][M][HS] | xb[2][M][XS] | rb[layer][M][HS] | bias[2][6H] | red[NWL][M]
+  uint16_t* const hb = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* const xb = hb + 4 * M * HS;
+  uint16_t* const rb = xb + 2 * M * XS;
+  float* const bias = reinterpret_cast<float*>(rb + 2 * M * HS);
+  float* const red = bias + 12 * H;
+#define HB(l, b) (hb + ((l) * 2 + (b)) * (M * HS))
+#define XB(b) (xb + (b) * (M * XS))
+  {
+    uint32_t* z = reinterpret_cast<uint32_t*>(smem);
+    const int words = (4 * M * HS + 2 * M * XS) / 2;
+    for (int i = tid; i < words; i += NT) z[i] = 0u;
+  }
+  for (int i = tid; i < 6 * H; i += NT) {
+    bias[i] = a.layer[0].bias[i];
+    bias[6 * H + i] = a.layer[1].bias[i];
+  }
+  const int I = a.I;
+  const int chunks = I >> 3;
+  const int my_rr = tid / max(chunks, 1), my_c = tid - my_rr * max(chunks, 1);
+  const bool stager = chunks > 0 && my_rr < M;
+  const int grow = row0 + my_rr;
+  int slot = -1, head = 0, valid_from = a.T;
+  if (stager && grow < n_live) {
+    if (a.mode == 1) {
+      slot = a.slots[grow];
+      if (slot >= 0) {
+        const AcctRT r = a.rt[slot];
+        head = r.ev_head;
+        valid_from = a.T - min(r.ev_count, a.T);
+      }
+    } else {
+      valid_from = 0;
+    }
+  }
+  auto load_x = [&](int t) -> uint4 {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (!stager || t < valid_from || t >= a.T) return v;
+    if (a.mode == 1) {
+      int idx = (head - a.T + t) % a.ev_ring;
+      if (idx < 0) idx += a.ev_ring;
+      v = *reinterpret_cast<const uint4*>(a.ev + (((size_t)slot * a.ev_ring + idx) * I + my_c * 8));
+    } else {
+      const float* src = a.X + (((size_t)t * a.x_rows + grow) * I + my_c * 8);
+      const float4 f0 = *reinterpret_cast<const float4*>(src);
+      const float4 f1 = *reinterpret_cast<const float4*>(src + 4);
+      v.x = (uint32_t)f32_to_bf16(f0.x) | ((uint32_t)f32_to_bf16(f0.y) << 16);
+      v.y = (uint32_t)f32_to_bf16(f0.z) | ((uint32_t)f32_to_bf16(f0.w) << 16);
+      v.z = (uint32_t)f32_to_bf16(f1.x) | ((uint32_t)f32_to_bf16(f1.y) << 16);
+      v.w = (uint32_t)f32_to_bf16(f1.z) | ((uint32_t)f32_to_bf16(f1.w) << 16);
+    }
+    return v;
+  };
+  __syncthreads();
+  if (stager) *reinterpret_cast<uint4*>(XB(0) + my_rr * XS + my_c * 8) = load_x(0);
+  float hs[HTW][RT][4];
+#pragma unroll
+  for (int i = 0; i < HTW; ++i)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hs[i][rt][r] = 0.f;
+  __syncthreads();
+
+  for (int t = 0; t <= a.T; ++t) {
+    const uint4 xn = load_x(t + 1);
+    if (layer == 0) {
+      if (t < a.T)  // H1[t] from x_t and H1[t-1]
+        layer_step<RT, KSX, KSH, LBR, NWL>(w0, r0, bias, XB(t & 1), XS, HB(0, t & 1), HB(0, (t + 1) & 1),
+                                           rb, hs, lane, lw);
+      else if (LBR == 0)
+        __syncthreads();  // match the other half's internal barrier
+    } else {
+      if (t >= 1)   // H2[t-1] from H1[t-1] and H2[t-2]
+        layer_step<RT, KSH, KSH, LBR, NWL>(w1, r1, bias + 6 * H, HB(0, t & 1), HS, HB(1, (t - 1) & 1),
+                                           HB(1, t & 1), rb + M * HS, hs, lane, lw);
+      else if (LBR == 0)
+        __syncthreads();
+    }
+    if (stager && t + 1 < a.T) *reinterpret_cast<uint4*>(XB((t + 1) & 1) + my_rr * XS + my_c * 8) = xn;
+    __syncthreads();
+  }
+
+  // ---- outputs: H2[T-1] in the layer-2 waves' registers
+  const int crow = (lane >> 4) * 4, ccol = lane & 15;
+  if (layer == 1 && a.yh) {
+#pragma unroll
+    for (int i = 0; i < HTW; ++i)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = row0 + rt * 16 + crow + r;
+          if (row < n_live) a.yh[(size_t)row * H + (lw + NWL * i) * 16 + ccol] = hs[i][rt][r];
+        }
+  }
+  if (a.head_w) {
+    if (layer == 1) {
+      float part[RT][4];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part[rt][r] = 0.f;
+#pragma unroll
+      for (int i = 0; i < HTW; ++i) {
+        const float w = a.head_w[(lw + NWL * i) * 16 + ccol];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) part[rt][r] += hs[i][rt][r] * w;
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = part[rt][r];
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+          if (ccol == 0) red[lw * M + rt * 16 + crow + r] = v;
+        }
+    }
+    __syncthreads();
+    if (tid < M && row0 + tid < n_live) {
+      float v = a.head_b;
+#pragma unroll
+      for (int w = 0; w < NWL; ++w) v += red[w * M + tid];
+      if (a.head_act == 2) v = 1.f / (1.f + expf(-v));
+      a.out[row0 + tid] = v;
+    }
+  }
+#undef HB
+#undef XB
+}
+
+static size_t gru_pipe_lds_bytes(int RT, int KSX, int KSH, int NW) {
+  const int M = RT * 16, H = KSH * 32, HS = H + GRU_PAD, XS = KSX * 32 + GRU_PAD;
+  return (size_t)4 * M * HS * 2 + (size_t)2 * M * XS * 2 + (size_t)2 * M * HS * 2 + (size_t)2 * 6 * H * 4 +
+         (size_t)NW * M * 4;
+}
+
+static size_t gru_lds_bytes(int RT, int KSX, int KSH, int NW) {
   const int M = RT * 16, H = KSH * 32, HS = H + GRU_PAD, XS = KSX * 32 + GRU_PAD;
   return (size_t)4 * M * HS * 2 + (size_t)2 * M * XS * 2 + (size_t)M * HS * 2 + (size_t)2 * 6 * H * 4 +
-         (size_t)4 * M * 4;
+         (size_t)NW * M * 4;
+}
+
+template <int RT, int KSX, int KSH, int NW>
+static void launch_gru_w(const GruArgs& a, hipStream_t st) {
+  const int M = RT * 16;
+  const dim3 grid((a.n_rows + M - 1) / M), block(NW * 64);
+  const size_t lds = gru_lds_bytes(RT, KSX, KSH, NW);
+  if (a.layer[0].lbr)
+    hipLaunchKernelGGL((gru_kernel<RT, KSX, KSH, 1, NW>), grid, block, lds, st, a);
+  else
+    hipLaunchKernelGGL((gru_kernel<RT, KSX, KSH, 0, NW>), grid, block, lds, st, a);
+}
+
+template <int RT, int KSX, int KSH, int NW>
+static void launch_gru_pipe(const GruArgs& a, hipStream_t st) {
+  const int M = RT * 16;
+  const dim3 grid((a.n_rows + M - 1) / M), block(NW * 64);
+  const size_t lds = gru_pipe_lds_bytes(RT, KSX, KSH, NW);
+  if (a.layer[0].lbr)
+    hipLaunchKernelGGL((gru2_pipe_kernel<RT, KSX, KSH, 1, NW>), grid, block, lds, st, a);
+  else
+    hipLaunchKernelGGL((gru2_pipe_kernel<RT, KSX, KSH, 0, NW>), grid, block, lds, st, a);
 }
 
 template <int RT, int KSX, int KSH>
 static void launch_gru_t(const GruArgs& a, hipStream_t st) {
-  const int M = RT * 16;
-  if (a.layer[0].lbr)
-    hipLaunchKernelGGL((gru_kernel<RT, KSX, KSH, 1>), dim3((a.n_rows + M - 1) / M), dim3(256),
-                       gru_lds_bytes(RT, KSX, KSH), st, a);
-  else
-    hipLaunchKernelGGL((gru_kernel<RT, KSX, KSH, 0>), dim3((a.n_rows + M - 1) / M), dim3(256),
-                       gru_lds_bytes(RT, KSX, KSH), st, a);
+  if (a.n_layers == 2 && a.pipeline) {
+    // 2 hidden tiles per wave: H/32 waves per layer (H=256: 16 waves = 1024 threads)
+    if constexpr (KSH == 8) {
+      return launch_gru_pipe<RT, KSX, KSH, 16>(a, st);
+    } else if constexpr (KSH == 4) {
+      return launch_gru_pipe<RT, KSX, KSH, 8>(a, st);
+    } else {
+      return launch_gru_pipe<RT, KSX, KSH, 4>(a, st);
+    }
+  }
+  if constexpr (KSH >= 4) {  // 8 waves: 2 hidden tiles per wave (measured faster than 4 for H >= 128)
+    if (a.waves != 4) return launch_gru_w<RT, KSX, KSH, 8>(a, st);
+  }
+  launch_gru_w<RT, KSX, KSH, 4>(a, st);
 }
 
 template <int RT, int KSX>
@@ -362,11 +571,12 @@ static void launch_gru_h(const GruArgs& a, hipStream_t st) {
 
 void launch_gru(const GruArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
-  // rows per workgroup: 32 amortises each streamed weight fragment over two MFMA row tiles;
-  // drop to 16 when that would leave most of the 256 CUs idle.
-  const bool rt2 = a.n_rows >= 32 * 192;
+  // rows per workgroup: every CU streams the full weight set each step (a per-CU L2 bandwidth
+  // bound, tools/gru_bench.py), so 32 rows amortise each fragment over two MFMA row tiles once
+  // the batch fills the 256 CUs at 32 rows; below that 16 keeps more CUs streaming.
+  const int tr = a.tile_rows ? a.tile_rows : (a.n_rows >= 32 * 256 ? 32 : 16);
   const int ksx = a.layer[0].kx_pad / 32;
-  if (rt2) {
+  if (tr == 32) {
     if (ksx == 1) launch_gru_h<2, 1>(a, st); else launch_gru_h<2, 2>(a, st);
   } else {
     if (ksx == 1) launch_gru_h<1, 1>(a, st); else launch_gru_h<1, 2>(a, st);

@@ -166,6 +166,9 @@ struct GruArgs {
   float head_b;
   int32_t head_act;         // 0 none, 2 sigmoid
   float* out;               // [rows]
+  int32_t tile_rows;        // 0 auto | 16 | 32 rows per workgroup
+  int32_t waves;            // 0 auto (4) | 8 waves per workgroup (H >= 128)
+  int32_t pipeline;         // 2 layers: layer-pipelined kernel (layer 1 @ t || layer 2 @ t-1)
 };
 void launch_gru(const GruArgs& a, hipStream_t st);
 

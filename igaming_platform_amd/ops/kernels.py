@@ -294,6 +294,7 @@ class GruPack:
         if len({int(l.linear_before_reset) for l in layers}) != 1:
             raise ValueError("gru: layers must share linear_before_reset")
         self.H, self.I, self.n_layers = H, layers[0].in_dim, len(layers)
+        self.waves = 0
         self.lbr = int(layers[0].linear_before_reset)
         dev = as_device(device)
         self.layers = []
@@ -315,11 +316,12 @@ class GruPack:
 
 def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh: Optional[torch.Tensor] = None,
         X: Optional[torch.Tensor] = None, store=None, slots: Optional[torch.Tensor] = None,
-        m_ptr: Optional[torch.Tensor] = None) -> None:
+        m_ptr: Optional[torch.Tensor] = None, tile_rows: int = 0, waves: int = 0, pipeline: int = 1) -> None:
     """K4. Input either dense ``X`` f32 [T, rows, I] or the store's event rings for ``slots``."""
     dev = gp.device
     d = dict(n_layers=gp.n_layers, H=gp.H, T=int(T), I=gp.I, n_rows=int(n_rows),
-             m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32, device=dev))
+             m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32, device=dev), tile_rows=int(tile_rows),
+             waves=int(waves or gp.waves), pipeline=int(pipeline))
     for i, l in enumerate(gp.layers):
         d[f"l{i}_W"] = _need(l["W"], "W", torch.bfloat16, device=dev)
         d[f"l{i}_R"] = _need(l["R"], "R", torch.bfloat16, device=dev)
