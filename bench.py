@@ -8,9 +8,12 @@ default config = cfg 3, the data-parallel headline: GBDT+MLP stacked ensemble
 
 One timed step per GPU = one full scoring micro-batch, nothing skipped:
   host: pack 8192 requests (48 B ReqRec) into a pinned slab
-  GPU (one captured hipGraph): H2D slab -> feature_assemble (ring windows, HLL, blacklist,
-      ip-intel, rules) -> tree ensemble -> MFMA dense -> GEMV+sigmoid -> ensemble/action
-      (+metrics) -> feature_update (score-then-update) -> D2H results
+  GPU, two captured hipGraphs on two streams (engine/scorer.py):
+      state: H2D slab -> dedup insert -> feature_assemble (ring windows, HLL, blacklist,
+             ip-intel, rules, single-event score-then-update) -> multi-event update segments
+      model: tree ensemble -> fused MFMA dense+GEMV+sigmoid -> ensemble/action (+metrics)
+             -> D2H results
+      batch i+1's state graph overlaps batch i's model graph
   RCCL: all_gather of the packed results across ranks (+ metrics all_reduce every 16 steps)
 Per-GPU work is fixed as N grows (weak scaling): global batch = 8192 x N per step.
 
@@ -41,7 +44,7 @@ def parse():
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="per-GPU micro-batch (default: the config's)")
     ap.add_argument("--accounts", type=int, default=1 << 20, help="feature-store accounts per GPU")
-    ap.add_argument("--depth", type=int, default=2, help="pipeline depth (batches in flight)")
+    ap.add_argument("--depth", type=int, default=3, help="pipeline depth (batches in flight)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the per-step RCCL all_gather")
     ap.add_argument("--json-out", default="")
@@ -88,17 +91,15 @@ def main():
 
     def step(i: int, now: int):
         slot = sc.next_slot()
-        v = sc.slab_view(slot, B)
-        v[:] = pool[i % len(pool)]
-        v["ts"] = now
+        sc.pack(slot, pool[i % len(pool)])  # the wire decoder's output: raw REQREC rows
         p = sc.submit_packed(slot, B, now)
         if world > 1 and not a.no_gather:
-            with torch.cuda.stream(sc.stream):
-                dist.all_gather_into_tensor(gathered, sc.res[:B].reshape(-1))
+            with torch.cuda.stream(sc.mstream):  # results / metrics live on the model stream
+                dist.all_gather_into_tensor(gathered, sc.slots[slot].res[:B].reshape(-1))
                 if i % 16 == 15:
                     met_sum.copy_(sc.metrics)
                     dist.all_reduce(met_sum)
-                p.event.record(sc.stream)
+                p.event.record(sc.mstream)
         return p
 
     inflight = []

@@ -1,5 +1,6 @@
 // Fixed-layout records shared by the HIP kernels (device) and the C++ runtime (host).
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 namespace igp {
@@ -133,6 +134,10 @@ struct ScoreCfg {
   int32_t pad[3];
 };
 static_assert(sizeof(ScoreCfg) == 176, "ScoreCfg must be 176 bytes");
+// feature_assemble reads ScoreCfg bytes 128..159 as two int4 (csrc/kernels/features.hip)
+static_assert(offsetof(ScoreCfg, bl_mask) == 132 && offsetof(ScoreCfg, ip_max_probe) == 144 &&
+                  offsetof(ScoreCfg, ext_width) == 148 && offsetof(ScoreCfg, my_rank) == 156,
+              "ScoreCfg K1 block moved");
 
 // One scoring request / transaction event as shipped host->device (48 bytes). A batch is a
 // contiguous slab [BatchHdr | ReqRec x n]: one H2D copy per micro-batch.

@@ -46,11 +46,12 @@ UpdateArgs update_args(const py::dict& d) {
   a.dbuf = ptr<int32_t*>(d, "dbuf");
   a.dcap = geti(d, "dcap");
   a.dmax = geti(d, "dmax");
-  a.region = geti(d, "region", 2);
+  a.region = geti(d, "region", DEDUP_STANDALONE);
   if (!a.dbuf || !a.cfg || !a.req || !a.rt) throw std::runtime_error("update args: missing pointers");
   if (a.n_max > a.dmax || a.dcap < 2 * a.dmax) throw std::runtime_error("update args: dedup scratch too small");
   if (a.ev && a.ev_dim != 16) throw std::runtime_error("update args: event dim must be 16");
-  if (a.region < 0 && !a.hdr) throw std::runtime_error("update args: ping-pong region needs hdr");
+  if (a.region < 0 && !a.hdr) throw std::runtime_error("update args: ring region needs hdr");
+  if (a.region > DEDUP_STANDALONE) throw std::runtime_error("update args: bad dedup region");
   return a;
 }
 
@@ -69,6 +70,8 @@ PYBIND11_MODULE(_hipk, m) {
   m.attr("SIZEOF_ACCTRT") = (int)sizeof(AcctRT);
   m.attr("SIZEOF_ACCTBATCH") = (int)sizeof(AcctBatch);
   m.attr("SIZEOF_REQREC") = (int)sizeof(ReqRec);
+  m.attr("DEDUP_LIST") = DEDUP_LIST;
+  m.attr("DEDUP_REGIONS") = DEDUP_RING + 1;
 
   m.def("feature_assemble", [](py::dict d, uintptr_t s) {
     AssembleArgs a{};
@@ -93,6 +96,11 @@ PYBIND11_MODULE(_hipk, m) {
     a.x_stride = geti(d, "x_stride");
     a.ring_size = geti(d, "ring_size");
     a.n_rows = geti(d, "n_rows");
+    if (a.dbuf) {
+      if (!d.contains("upd")) throw std::runtime_error("feature_assemble: score-then-update needs upd args");
+      a.upd = update_args(d["upd"].cast<py::dict>());
+      if (a.upd.region >= 0 || a.upd.dbuf != a.dbuf) throw std::runtime_error("feature_assemble: upd region");
+    }
     launch_feature_assemble(a, stream_of(s));
     check("feature_assemble");
   });
@@ -100,6 +108,7 @@ PYBIND11_MODULE(_hipk, m) {
   m.def("feature_update", [](py::dict d, uintptr_t s) {
     UpdateArgs a = update_args(d);
     if (geti(d, "segments_only")) launch_update_segments(a, stream_of(s));
+    else if (geti(d, "insert_only")) launch_dedup_insert(a, stream_of(s));
     else launch_feature_update(a, stream_of(s));
     check("feature_update");
   });
@@ -194,8 +203,6 @@ PYBIND11_MODULE(_hipk, m) {
     a.out = ptr<ResultRec*>(d, "out");
     a.metrics = ptr<unsigned long long*>(d, "metrics");
     a.n_rows = geti(d, "n_rows");
-    a.do_update = geti(d, "do_update");
-    if (a.do_update) a.upd = update_args(d["upd"].cast<py::dict>());
     launch_ensemble(a, stream_of(s));
     check("ensemble");
   });

@@ -9,6 +9,18 @@
 
 namespace igp {
 
+// Hide a wave-uniform value's uniformity from the compiler, so loads addressed by it are
+// issued as vector memory ops: random per-wave gathers (account rows) miss the small scalar
+// cache and serialise on it, while a vector load of a broadcast address is one request.
+__device__ __forceinline__ int as_vgpr(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// Mark a loaded value as used here: keeps the compiler from sinking its load below a branch
+// (the load then issues together with the other first-level loads).
+__device__ __forceinline__ void keep_issued(int x) { asm volatile("" ::"v"(x)); }
+
 template <class T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

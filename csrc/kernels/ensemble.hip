@@ -8,7 +8,8 @@
 // with the reference's addition order, so scores match the Go arithmetic bit-for-bit.
 // Metrics (score histogram, action counts) are aggregated per block in LDS, then one
 // global atomic per bucket per block.
-#include "update.h"
+#include "common.h"
+#include "launch.h"
 
 namespace igp {
 
@@ -69,10 +70,6 @@ __global__ void __launch_bounds__(256) ensemble_kernel(EnsembleArgs a) {
                               ((uint32_t)action << 16) | ((cfg.model_kind != 0 ? 1u : 0u) << 18) |
                               (reasons << 20);
       a.out[row] = ResultRec{packed, (float)ml};
-      // score-then-update (engine.go:486-488): accounts with one event in this batch apply it
-      // here; multi-event accounts get a segment for the ordered wave apply that follows.
-      if (a.do_update && f.slot >= 0)
-        update_first_event(a.upd, dedup_region(a.upd.dbuf, a.upd.dcap, a.upd.dmax, a.hdr->seq & 1), row, f.slot);
       if (a.metrics) {
         atomicAdd(&cnt[MET_HIST + (fin < 0 ? 0 : fin)], 1u);
         atomicAdd(&cnt[MET_ACTION + action], 1u);

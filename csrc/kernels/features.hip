@@ -11,107 +11,198 @@
 namespace igp {
 
 // ---------------------------------------------------------------------------------- K1
-// One wave64 per request. Every independent load is issued before the first use: the
-// 256-entry ts ring as one uint4 per lane (1 KiB/wave, coalesced), HLL registers (4 per
-// lane), the account rows (broadcast), the ext row, and the blacklist/ip-intel probes;
-// the 1h amounts are then fetched only for in-window entries (predicated, issued together).
-// Lane 0 also registers the request in the batch dedup table (score-then-update) and each
-// wave clears a slice of the other parity's table for the next batch.
-__global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int row = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (row >= a.n_rows) return;
+__device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h, int c, int s, AcctRT r,
+                                   int lane);
+
+// PFADD on a register file held one uint32 (4 registers) per lane: the owner lane of the
+// register updates and stores its word; an expired key (TTL) is rewritten as zeros first.
+__device__ __forceinline__ bool hll_add_wave(uint32_t* words, uint32_t w, uint32_t& exp, uint64_t h, int64_t now,
+                                             int ttl, int lane) {
+  const bool reset = now >= (int64_t)exp;
+  if (reset) w = 0u;
+  const int idx = (int)(h & 255u);
+  const int rank = hll_rank(h);
+  const int sh = 8 * (idx & 3);
+  const bool mine = lane == (idx >> 2) && rank > (int)((w >> sh) & 0xffu);
+  if (mine) w = (w & ~(0xffu << sh)) | ((uint32_t)rank << sh);
+  if (reset || mine) words[lane] = w;
+  exp = (uint32_t)(now + ttl);
+  return __ballot(mine) != 0ull;
+}
+
+// apply_event (update.h) spread over a wave that already holds the account's AcctRT (uniform)
+// and HLL registers (wd / wi: 4 per lane); same arithmetic, same stored bytes.
+__device__ __forceinline__ void apply_event_wave(const UpdateArgs& a, const ReqRec& ev, AcctRT r, uint32_t wd,
+                                                 uint32_t wi, int lane) {
+  const int s = ev.slot;
+  const int64_t now = event_ts(a, ev);
   const ScoreCfg& cfg = *a.cfg;
-  const int n_live = a.hdr->n;
-  const int seq = a.hdr->seq;
-  const int64_t now = a.hdr->now;
-  if (a.dbuf) {  // clear this wave's slice of the next batch's dedup region
-    const DedupTab nt = dedup_region(a.dbuf, a.dcap, a.dmax, (seq + 1) & 1);
+  const int64_t amt = ev.amount;
+  const int hd = r.ring_head;
+  if (lane == 0) {
+    a.ring_ts[(size_t)s * a.ring_size + hd] = (uint32_t)now;
+    a.ring_amt[(size_t)s * a.ring_size + hd] = amt;
+  }
+  r.ring_head = hd + 1 == a.ring_size ? 0 : hd + 1;
+  if (now >= (int64_t)r.sum_exp) r.sum_compat = 0;
+  r.sum_compat += amt;
+  r.sum_exp = (uint32_t)(now + cfg.sum_ttl);
+  uint32_t* regs = reinterpret_cast<uint32_t*>(a.hll + (size_t)s * 512);
+  bool new_dev = false, new_ip = false;
+  if (ev.dev_hash) new_dev = hll_add_wave(regs, wd, r.hll_dev_exp, ev.dev_hash, now, cfg.hll_ttl, lane);
+  if (ev.ip_hash) new_ip = hll_add_wave(regs + 64, wi, r.hll_ip_exp, ev.ip_hash, now, cfg.hll_ttl, lane);
+  r.last_tx = (uint32_t)now;
+  r.last_tx_exp = (uint32_t)(now + cfg.last_tx_ttl);
+  if (now >= (int64_t)r.session_exp || r.session_start == 0) r.session_start = (uint32_t)now;
+  r.session_exp = (uint32_t)(now + cfg.session_ttl);
+  if (a.ev) {
+    uint32_t* e = reinterpret_cast<uint32_t*>(a.ev + ((size_t)s * a.ev_ring + r.ev_head) * a.ev_dim);
+    if (lane < 8) e[lane] = event_word(lane, amt, ev.tx_type & 0xff, now, (int64_t)r.last_event_ts, new_dev, new_ip);
+    r.ev_head = r.ev_head + 1 == a.ev_ring ? 0 : r.ev_head + 1;
+    r.ev_count = r.ev_count + 1 > a.ev_ring ? a.ev_ring : r.ev_count + 1;
+  }
+  r.last_event_ts = (uint32_t)now;
+  if (lane == 0) a.rt[s] = r;
+}
+
+__device__ __forceinline__ void clear_next_dedup(const AssembleArgs& a, int row, int seq, int lane) {
+  if (a.dbuf) {  // clear this wave's slice of batch seq+2's dedup region (after every load:
+                 // no store precedes the account loads, so uniform ones can go scalar)
+    const DedupTab nt = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq + 2));
     const int chunk = (a.dcap + a.n_rows - 1) / a.n_rows;
     const int e0 = row * chunk;
     dedup_clear_range(nt, e0, min(a.dcap, e0 + chunk), lane);
     if (row == 0 && lane < 2) nt.ctr[lane] = 0;
   }
+}
+
+// One wave64 per request. Every independent load is issued before the first use: the
+// 256-entry ts ring as one uint4 per lane (1 KiB/wave, coalesced), HLL registers (4 per
+// lane), the account rows (broadcast), the ext row, and the blacklist/ip-intel probes;
+// the 1h amounts are then fetched only for in-window entries (predicated, issued together).
+// Score-then-update: dedup_insert_kernel registered the batch first; a wave whose account has
+// no other event in the batch applies the event itself once its reads are done (AcctRT and
+// the HLL registers are already in registers), and every wave clears a slice of the other
+// parity's dedup table for the next batch after its loads.
+__device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
+  const int lane = threadIdx.x & 63;
+  const int row = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (row >= a.n_rows) return;
+  const ScoreCfg& cfg = *a.cfg;
+  // ---- dependency level 1: the request row and the batch header (independent loads). Under a
+  // full grid every dependent global-load level costs several microseconds, so the kernel is
+  // organised as two load levels: the row, then everything the row addresses.
+  const uint4* rp = reinterpret_cast<const uint4*>(a.req + as_vgpr(row));
+  const uint4 q0 = rp[0], q1 = rp[1], q2 = rp[2];
+  ReqRec rq;
+  rq.slot = (int32_t)q0.x;
+  rq.tx_type = (int32_t)q0.y;
+  rq.amount = (int64_t)(((uint64_t)q0.w << 32) | q0.z);
+  rq.dev_hash = ((uint64_t)q1.y << 32) | q1.x;
+  rq.fp_hash = ((uint64_t)q1.w << 32) | q1.z;
+  rq.ip_hash = ((uint64_t)q2.y << 32) | q2.x;
+  rq.ts = (int64_t)(((uint64_t)q2.w << 32) | q2.z);
+  const int4 hv = *reinterpret_cast<const int4*>(a.hdr);  // BatchHdr {n, seq, now}
+  // ScoreCfg bytes 128..159 in two 16-byte loads: {., bl_mask, bl_max_probe, ip_mask} and
+  // {ip_max_probe, ext_width, owner_filter, my_rank} (records.h; static_asserts there)
+  const int4 c8 = reinterpret_cast<const int4*>(a.cfg)[8];
+  const int4 c9 = reinterpret_cast<const int4*>(a.cfg)[9];
+  const int2 own = make_int2(c9.z, c9.w);
+  const int ext_w = c9.y;
+  const int n_live = hv.x;
+  const int seq = hv.y;
+  const int64_t now = (int64_t)(((uint64_t)(uint32_t)hv.w << 32) | (uint32_t)hv.z);
   float* xr = a.X + (size_t)row * a.x_stride;
-  const int ext_w = cfg.ext_width;
   if (row >= n_live) {  // padded row of a graph bucket: deterministic zeros
+    keep_issued((int)(q0.x ^ q0.z ^ q1.x ^ q1.z ^ q2.x ^ q2.z) ^ own.x);
+    clear_next_dedup(a, row, seq, lane);
     for (int j = lane; j < 30 + ext_w; j += 64) xr[j] = 0.f;
     if (lane < 32) reinterpret_cast<int32_t*>(a.feat + row)[lane] = (lane == 27) ? -1 : 0;
     return;
   }
-  const ReqRec rq = a.req[row];
-  if (!row_owned(rq, cfg)) {  // another rank's request: inert row, no dedup entry
+  if (own.x && ((rq.tx_type >> 8) & 0xff) != own.y) {  // another rank's request: inert row
+    clear_next_dedup(a, row, seq, lane);
     for (int j = lane; j < 30 + ext_w; j += 64) xr[j] = 0.f;
     if (lane < 32) reinterpret_cast<int32_t*>(a.feat + row)[lane] = (lane == 27) ? -1 : (lane == 3 ? FR_NOT_OWNED : 0);
     return;
   }
-  const int s = rq.slot;
+  const int s = __builtin_amdgcn_readfirstlane(rq.slot);  // account rows go through SGPRs
   const int64_t amount = rq.amount;
   const int tx_type = rq.tx_type & 0xff;
 
-  // ---- issue the account loads
-  const int rs = a.ring_size;  // multiple of 64; 256 = one uint4 per lane
-  uint4 tsv = make_uint4(0, 0, 0, 0);
-  uint32_t tsx[12];           // entries beyond 256 (ring sizes up to 1024), rarely used
-  uint32_t wd = 0, wi = 0;
-  AcctRT rt{};
-  AcctBatch bt{};
-  if (s >= 0) {
-    const uint32_t* ts = a.ring_ts + (size_t)s * rs;
-    if (lane * 4 < rs) tsv = reinterpret_cast<const uint4*>(ts)[lane];
+  // ---- dependency level 2: every load addressed by the row, branch-free (clamped addresses,
+  // results masked afterwards) so the compiler issues them back to back before the first use
+  const bool has = s >= 0;
+  const int sc = has ? s : 0;
+  const int rs = a.ring_size;  // multiple of 64; 256 = one uint4 of ts + 4 amounts per lane
+  const int rl = min(lane, rs / 4 - 1);
+  uint4 tsv = reinterpret_cast<const uint4*>(a.ring_ts + (size_t)sc * rs)[rl];
+  const longlong2* am2 = reinterpret_cast<const longlong2*>(a.ring_amt + (size_t)sc * rs);
+  const longlong2 am01 = am2[2 * rl], am23 = am2[2 * rl + 1];
+  const uint32_t* hreg = reinterpret_cast<const uint32_t*>(a.hll + (size_t)sc * 512);
+  uint32_t wd = hreg[lane], wi = hreg[64 + lane];
+  AcctRT rt = a.rt[sc];
+  AcctBatch bt = a.batch[sc];
+  const float* e = a.ext + (size_t)sc * ext_w;
+  float extv[2];  // ext widths up to 128 preloaded; wider rows finish in a loop at the end
 #pragma unroll
-    for (int q = 0; q < 12; ++q) tsx[q] = (256 + q * 64 + lane < rs) ? ts[256 + q * 64 + lane] : 0u;
-    const uint32_t* h = reinterpret_cast<const uint32_t*>(a.hll + (size_t)s * 512);
-    wd = h[lane];
-    wi = h[64 + lane];
-    rt = a.rt[s];
-    bt = a.batch[s];
-  } else {
-#pragma unroll
-    for (int q = 0; q < 12; ++q) tsx[q] = 0u;
+  for (int u = 0; u < 2; ++u) extv[u] = e[max(0, min(lane + 64 * u, ext_w - 1))];
+  // score-then-update: first probe of the batch's dedup entry
+  uint32_t dh = 0;
+  int dkey = -1, dfirst = -1, dcount = 0;
+  if (a.dbuf) {  // kernel-uniform
+    const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
+    dh = mix32((uint32_t)sc) & (uint32_t)(t.cap - 1);
+    dkey = t.keys[dh];
+    dfirst = t.first[dh];
+    dcount = t.count[dh];
   }
-  // ---- K7: blacklist (lanes 0..2) and IP intelligence (lane 3) probes
+  // K7: blacklist (lanes 0..2: device, fingerprint, ip) and IP intelligence (lane 3): the first
+  // probe slot's key and value are loaded with the rest, collisions walk on (rare)
   uint64_t key = 0;
   if (lane == 0) key = rq.dev_hash;
   else if (lane == 1) key = rq.fp_hash;
-  else if (lane == 2) key = rq.ip_hash;
-  else if (lane == 3) key = rq.ip_hash;
+  else if (lane == 2 || lane == 3) key = rq.ip_hash;
+  const bool tabs = a.bl_keys && a.ip_keys;  // kernel-uniform
+  const bool bl_lane = tabs && lane < 3 && key != 0;
+  const bool ip_lane = tabs && lane == 3 && key != 0;
+  const uint64_t* pkeys = lane < 3 ? a.bl_keys : a.ip_keys;
+  const uint32_t* pvals = lane < 3 ? a.bl_exp : a.ip_flags;
+  const uint32_t pmask = (uint32_t)(lane < 3 ? c8.y : c8.w);
+  uint32_t pi = (bl_lane || ip_lane) ? ((uint32_t)key & pmask) : 0u;
+  uint64_t pk = 0;
+  uint32_t pv = 0;
+  if (tabs) {
+    pk = pkeys[pi];
+    pv = pvals[pi];
+  }
+  // ---- mask what a missing account / short ring must not see
+  if (!has) {
+    tsv = make_uint4(0, 0, 0, 0);
+    wd = wi = 0u;
+    rt = AcctRT{};
+    bt = AcctBatch{};
+    extv[0] = extv[1] = 0.f;
+    dkey = -1;
+  }
+  if (lane * 4 >= rs) tsv = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    if (lane + 64 * u >= ext_w) extv[u] = 0.f;
   bool hit = false;
   int ipf = 0;
-  if (lane < 3 && key != 0 && a.bl_keys) {
-    uint32_t i = (uint32_t)key & (uint32_t)cfg.bl_mask;
-    for (int p = 0; p < cfg.bl_max_probe; ++p) {
-      const uint64_t k = a.bl_keys[i];
-      if (k == 0) break;
-      if (k == key) {
-        const uint32_t e = a.bl_exp[i];
-        hit = (e == 0u) || (now < (int64_t)e);
-        break;
-      }
-      i = (i + 1) & (uint32_t)cfg.bl_mask;
+  if (bl_lane || ip_lane) {
+    const int max_probe = lane < 3 ? c8.z : c9.x;
+    for (int p = 1; p < max_probe && pk != 0 && pk != key; ++p) {
+      pi = (pi + 1) & pmask;
+      pk = pkeys[pi];
+      pv = pvals[pi];
     }
-  } else if (lane == 3 && key != 0 && a.ip_keys) {
-    uint32_t i = (uint32_t)key & (uint32_t)cfg.ip_mask;
-    for (int p = 0; p < cfg.ip_max_probe; ++p) {
-      const uint64_t k = a.ip_keys[i];
-      if (k == 0) break;
-      if (k == key) { ipf = (int)a.ip_flags[i]; break; }
-      i = (i + 1) & (uint32_t)cfg.ip_mask;
+    if (pk == key && max_probe > 0) {
+      if (bl_lane) hit = (pv == 0u) || (now < (int64_t)pv);
+      else ipf = (int)pv;
     }
   }
-  // ext row: loaded now (with the other account loads), stored at the end
-  float extv[4];
-  {
-    const float* e = a.ext + (size_t)(s >= 0 ? s : 0) * ext_w;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int j = lane + 64 * u;
-      extv[u] = (s >= 0 && j < ext_w) ? e[j] : 0.f;
-    }
-  }
-  // dedup insert for score-then-update
-  if (a.dbuf && lane == 0 && s >= 0) dedup_insert(dedup_region(a.dbuf, a.dcap, a.dmax, seq & 1), s, row);
-
   const bool blacklisted = __ballot(hit) != 0ull;
   ipf = __shfl(ipf, 3, 64);
 
@@ -132,16 +223,14 @@ __global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs a) {
       in1h[q] = v && t >= now - 3600;
       c60 += in1h[q];
     }
-    long long amv[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) amv[q] = in1h[q] ? am[lane * 4 + q] : 0;
-#pragma unroll
-    for (int q = 0; q < 12; ++q) {
-      const int64_t t = (int64_t)tsx[q];
+    const long long amv[4] = {in1h[0] ? am01.x : 0, in1h[1] ? am01.y : 0, in1h[2] ? am23.x : 0,
+                              in1h[3] ? am23.y : 0};
+    for (int q = 256 + lane; q < rs; q += 64) {  // rings longer than 256 entries (rare)
+      const int64_t t = (int64_t)a.ring_ts[(size_t)s * rs + q];
       if (t != 0) {
         c1 += t >= now - 60;
         c5 += t >= now - 300;
-        if (t >= now - 3600) { ++c60; s60 += am[256 + q * 64 + lane]; }
+        if (t >= now - 3600) { ++c60; s60 += am[q]; }
       }
     }
     s60 += amv[0] + amv[1] + amv[2] + amv[3];
@@ -265,13 +354,48 @@ __global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs a) {
   }
   if (lane < 30) xr[lane] = xv;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < 2; ++u) {
     const int j = lane + 64 * u;
     if (j < ext_w) xr[30 + j] = extv[u];
   }
-  for (int j = lane + 256; j < ext_w; j += 64) xr[30 + j] = s >= 0 ? a.ext[(size_t)s * ext_w + j] : 0.f;
+  for (int j = lane + 128; j < ext_w; j += 64) xr[30 + j] = s >= 0 ? a.ext[(size_t)s * ext_w + j] : 0.f;
   if (lane == 0) a.feat[row] = f;
+  clear_next_dedup(a, row, seq, lane);
+
+  // ---- score-then-update (engine.go:486-488). An account whose only event in the batch is
+  // this request has had all its reads done (by this wave), so the event is applied here by
+  // the whole wave; a multi-event account's batch is applied by its last-finishing wave.
+  if (a.dbuf && s >= 0) {
+    const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
+    int h = (int)dh;
+    if (dkey != s) {  // probe collision: walk the chain
+      h = dedup_find(t, s);
+      if (h >= 0) { dfirst = t.first[h]; dcount = t.count[h]; }
+    }
+    if (h >= 0) {
+      if (dcount == 1) {
+        apply_event_wave(a.upd, rq, rt, wd, wi, lane);
+      } else {
+        // multi-event account: queue this row, then count it as read (its loads were all
+        // consumed above); the wave that completes the count applies the account's whole
+        // batch in row order (no other row of it can still be reading)
+        int last = 0;
+        if (lane == 0) {
+          const int pos = atomicAdd(&t.fill[h], 1);
+          if (pos < DEDUP_LIST) t.list[(size_t)h * DEDUP_LIST + pos] = row;
+          __threadfence();
+          last = atomicAdd(&t.done[h], 1) == dcount - 1;
+        }
+        if (__shfl(last, 0, 64)) {
+          __threadfence();
+          apply_segment_wave(a.upd, t, h, dcount, s, rt, lane);
+        }
+      }
+    }
+  }
 }
+
+__global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs a) { feature_assemble_body(a); }
 
 // ---------------------------------------------------------------------------------- K6
 __device__ __forceinline__ int upd_n(const UpdateArgs& a) {
@@ -280,14 +404,14 @@ __device__ __forceinline__ int upd_n(const UpdateArgs& a) {
 }
 
 __device__ __forceinline__ DedupTab upd_region(const UpdateArgs& a) {
-  const int r = a.region >= 0 ? a.region : (a.hdr->seq & 1);
+  const int r = a.region >= 0 ? a.region : dedup_ring_region(a.hdr->seq);
   return dedup_region(a.dbuf, a.dcap, a.dmax, r);
 }
 
 __global__ void dedup_reset_kernel(UpdateArgs a) {
   const DedupTab t = upd_region(a);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < t.cap) { t.keys[i] = -1; t.first[i] = 0x7fffffff; t.count[i] = 0; t.fill[i] = 0; }
+  if (i < t.cap) { t.keys[i] = -1; t.first[i] = 0x7fffffff; t.count[i] = 0; t.fill[i] = 0; t.done[i] = 0; }
   if (i < 2) t.ctr[i] = 0;
 }
 
@@ -302,36 +426,25 @@ __global__ void update_single_kernel(UpdateArgs a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= upd_n(a)) return;
   const ReqRec& r = a.req[i];
-  if (r.slot >= 0 && row_owned(r, *a.cfg)) update_first_event(a, upd_region(a), i, r.slot);
+  if (r.slot >= 0 && row_owned(r, *a.cfg)) update_event(a, upd_region(a), i, r.slot);
 }
 
-__global__ void update_fill_kernel(UpdateArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= upd_n(a)) return;
-  const int s = a.req[i].slot;
-  if (s < 0 || !row_owned(a.req[i], *a.cfg)) return;
-  const DedupTab t = upd_region(a);
-  const int h = dedup_find(t, s);
-  if (h < 0 || t.count[h] < 2) return;
-  const int off = t.off[h];
-  const int pos = atomicAdd(&t.fill[h], 1);
-  if (off >= 0 && pos < t.count[h] && off + pos < t.nmax) t.list[off + pos] = i;
-}
-
-// sequential fallback: insertion-sort the segment in memory, apply with AcctRT in registers
-__device__ void apply_segment_serial(const UpdateArgs& a, const DedupTab& t, int h) {
-  const int c = t.count[h];
-  int* lst = t.list + t.off[h];
-  for (int x = 1; x < c; ++x) {
-    const int v = lst[x];
-    int y = x - 1;
-    while (y >= 0 && lst[y] > v) { lst[y + 1] = lst[y]; --y; }
-    lst[y + 1] = v;
-  }
-  const int s = a.req[lst[0]].slot;
+// account s has more events in the batch than its dedup list holds: find them in row order
+// (64 rows per ballot) and apply them one by one on lane 0 (degenerate traffic only)
+__device__ void apply_scan_serial(const UpdateArgs& a, int s, int lane) {
+  const int n = upd_n(a);
   AcctRT r = a.rt[s];
-  for (int x = 0; x < c; ++x) apply_event(a, lst[x], r);
-  a.rt[s] = r;
+  for (int base = 0; base < n; base += 64) {
+    const int i = base + lane;
+    const bool m = i < n && a.req[i].slot == s && row_owned(a.req[i], *a.cfg);
+    uint64_t b = __ballot(m);
+    while (b) {
+      const int l = __ffsll((long long)b) - 1;
+      b &= b - 1;
+      if (lane == 0) apply_event(a, base + l, r);
+    }
+  }
+  if (lane == 0) a.rt[s] = r;
 }
 
 // PFADD of up to 64 same-account events at once: the per-register winner writes the max,
@@ -367,47 +480,42 @@ __device__ __forceinline__ uint32_t hll_segment(const UpdateArgs& a, uint8_t* rg
   return (uint32_t)(tlast + a.cfg->hll_ttl);
 }
 
-// one wave per multi-event account: events sorted in registers, applied in parallel. Valid
-// when the segment spans less than the shortest TTL (then no key can expire mid-segment);
-// otherwise (or above 64 events) lane 0 applies the segment sequentially.
-__global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  const DedupTab t = upd_region(a);
-  if (w >= min(t.ctr[1], t.nmax)) return;
-  const int h = t.mlist[w];
-  const int c = t.count[h];
-  if (h < 0 || h >= t.cap || t.off[h] < 0 || t.off[h] + c > t.nmax || c < 2) return;
-  const int* lst = t.list + t.off[h];
-  const ScoreCfg& cfg = *a.cfg;
-  const int min_ttl = min(min(cfg.session_ttl, cfg.sum_ttl), min(cfg.hll_ttl, cfg.last_tx_ttl));
-  int span_ok = 0;
-  int key = 0x7fffffc0 | lane;
-  int64_t ts = 0;
-  if (c <= 64) {
-    if (lane < c) key = lst[lane];
-    if (lane < c) ts = a.req[key].ts;
-    const int64_t big = 0x3fffffffffffffffLL;
-    const int64_t tmx = wave_max(lane < c ? ts : -big);
-    const int64_t tmn = -wave_max(lane < c ? -ts : -big);
-    span_ok = (tmx - tmn) < (int64_t)min_ttl;
-  }
-  if (!span_ok) {
-    if (lane == 0) apply_segment_serial(a, t, h);
+// the c (>= 2) events of account s (dedup hash slot h) in row order, by one wave holding the
+// account's pre-batch AcctRT `r`: events sorted in registers and applied in parallel when
+// the segment spans less than the shortest TTL (then no key can expire mid-segment);
+// otherwise lane 0 applies them one by one; more than DEDUP_LIST events: ordered batch scan.
+__device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h, int c, int s, AcctRT r,
+                                   int lane) {
+  if (c > DEDUP_LIST) {
+    apply_scan_serial(a, s, lane);
     return;
   }
-  // sort (distinct keys): rank = #smaller, then push each key to lane `rank`
+  // sort the (distinct) row indices: rank = #smaller, then push each to lane `rank`
+  const int key = lane < c ? t.list[(size_t)h * DEDUP_LIST + lane] : (0x7fffffc0 | lane);
   int rank = 0;
   for (int y = 0; y < 64; ++y) rank += __shfl(key, y, 64) < key;
   const int j = __builtin_amdgcn_ds_permute(rank * 4, key);
   const bool act = lane < c;
   ReqRec ev{};
   if (act) ev = a.req[j];
-  ts = act ? ev.ts : 0;
-  const int s = __shfl(act ? ev.slot : 0, 0, 64);
-  AcctRT r = a.rt[s];
+  const int64_t ts = act ? event_ts(a, ev) : 0;
+  const ScoreCfg& cfg = *a.cfg;
+  const int min_ttl = min(min(cfg.session_ttl, cfg.sum_ttl), min(cfg.hll_ttl, cfg.last_tx_ttl));
   const int64_t ts0 = __shfl(ts, 0, 64);
   const int64_t tsl = __shfl(ts, c - 1, 64);
+  const int64_t big = 0x3fffffffffffffffLL;
+  const int64_t tmx = wave_max(act ? ts : -big);
+  const int64_t tmn = -wave_max(act ? -ts : -big);
+  // parallel apply is exact when the segment spans less than the shortest TTL (no key can
+  // expire mid-segment); otherwise lane 0 applies the sorted events one by one
+  if (tmx - tmn >= (int64_t)min_ttl) {
+    for (int x = 0; x < c; ++x) {
+      const int jx = __shfl(j, x, 64);
+      if (lane == 0) apply_event(a, jx, r);
+    }
+    if (lane == 0) a.rt[s] = r;
+    return;
+  }
   const int64_t amt = act ? ev.amount : 0;
   // tx ring: consecutive positions from the head
   if (act) {
@@ -446,16 +554,33 @@ __global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
   if (lane == 0) a.rt[s] = r;
 }
 
+// standalone ingestion: one wave per multi-event account listed by update_single
+__global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const DedupTab t = upd_region(a);
+  if (w >= min(t.ctr[0], t.nmax)) return;
+  const int h = t.mlist[w];
+  if (h < 0 || h >= t.cap) return;
+  const int c = t.count[h];
+  const int s = t.keys[h];
+  if (c < 2 || s < 0) return;
+  apply_segment_wave(a, t, h, c, s, a.rt[s], lane);
+}
+
 // ---------------------------------------------------------------------------------- launch
 void launch_feature_assemble(const AssembleArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
   hipLaunchKernelGGL(feature_assemble_kernel, dim3((a.n_rows + 3) / 4), dim3(256), 0, st, a);
 }
 
+void launch_dedup_insert(const UpdateArgs& a, hipStream_t st) {
+  if (a.n_max <= 0) return;
+  hipLaunchKernelGGL(dedup_insert_kernel, dim3((a.n_max + 255) / 256), dim3(256), 0, st, a);
+}
+
 void launch_update_segments(const UpdateArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
-  const int g = (a.n_max + 255) / 256;
-  hipLaunchKernelGGL(update_fill_kernel, dim3(g), dim3(256), 0, st, a);
   // at most n/2 accounts can have >= 2 events: one wave each
   hipLaunchKernelGGL(update_multi_kernel, dim3((a.n_max / 2 + 3) / 4 + 1), dim3(256), 0, st, a);
 }

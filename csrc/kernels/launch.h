@@ -9,8 +9,38 @@
 
 namespace igp {
 
-// Dedup scratch: 3 regions (0/1 = scorer ping-pong by BatchHdr::seq parity, 2 = standalone
-// event ingestion), each = keys/first/count/fill/off [cap] + list/mlist [dmax] + 2 counters.
+// events of one account per batch held in its dedup list (more: ordered scan of the batch)
+constexpr int DEDUP_LIST = 64;
+
+// scorer batches rotate over DEDUP_RING dedup regions by BatchHdr::seq: batch q's K1 clears
+// the region of batch q+2, so batch q+1's dedup insert (copy stream) can run while batch q is
+// still in K1 / update_segments on the state stream. Region DEDUP_STANDALONE: event ingestion.
+constexpr int DEDUP_RING = 3;
+constexpr int DEDUP_STANDALONE = 3;
+__host__ __device__ inline int dedup_ring_region(int seq) { return (int)((unsigned)seq % DEDUP_RING); }
+
+// Dedup scratch: DEDUP_RING + 1 regions, each = keys/first/count/fill [cap] + list [cap][DEDUP_LIST] + mlist [dmax]
+// + 2 counters (update.h dedup_region).
+struct UpdateArgs {
+  const ScoreCfg* cfg;
+  const BatchHdr* hdr;      // scorer path: live count + seq parity (nullable -> n, region)
+  int32_t n;
+  int32_t n_max;            // grid coverage
+  const ReqRec* req;        // events (ReqRec.ts = event time)
+  uint32_t* ring_ts;
+  int64_t* ring_amt;
+  uint8_t* hll;
+  AcctRT* rt;
+  uint16_t* ev;             // event ring bf16 [C][ev_ring][16] (nullable)
+  int32_t ring_size;
+  int32_t ev_ring;
+  int32_t ev_dim;
+  int32_t* dbuf;
+  int32_t dcap;             // power of two >= 2 * dmax
+  int32_t dmax;
+  int32_t region;           // -1: hdr->seq & 1; else fixed region (2 = standalone)
+};
+
 struct AssembleArgs {
   const BatchHdr* hdr;
   const ScoreCfg* cfg;
@@ -33,32 +63,19 @@ struct AssembleArgs {
   int32_t x_stride;
   int32_t ring_size;
   int32_t n_rows;           // rows covered by the launch (graph bucket)
+  // score-then-update (dbuf != null): the batch's dedup insert ran before K1 (dedup_insert);
+  // each wave applies its request's event when it is the account's only one in the batch
+  // and opens the segment of a multi-event account (applied by update_segments after K1)
+  UpdateArgs upd;
 };
 
-struct UpdateArgs {
-  const ScoreCfg* cfg;
-  const BatchHdr* hdr;      // scorer path: live count + seq parity (nullable -> n, region)
-  int32_t n;
-  int32_t n_max;            // grid coverage
-  const ReqRec* req;        // events (ReqRec.ts = event time)
-  uint32_t* ring_ts;
-  int64_t* ring_amt;
-  uint8_t* hll;
-  AcctRT* rt;
-  uint16_t* ev;             // event ring bf16 [C][ev_ring][16] (nullable)
-  int32_t ring_size;
-  int32_t ev_ring;
-  int32_t ev_dim;
-  int32_t* dbuf;
-  int32_t dcap;             // power of two >= 2 * dmax
-  int32_t dmax;
-  int32_t region;           // -1: hdr->seq & 1; else fixed region (2 = standalone)
-};
 
 void launch_feature_assemble(const AssembleArgs& a, hipStream_t st);
 // standalone event ingestion (event bus / history replay): reset + insert + single + segments
 void launch_feature_update(const UpdateArgs& a, hipStream_t st);
-// scorer path tail: segment fill + per-account wave apply (insert ran in K1, singles in K5)
+// scorer path: dedup insert of the batch (before K1; K1 applies single-event accounts) ...
+void launch_dedup_insert(const UpdateArgs& a, hipStream_t st);
+// ... and the tail after K1: segment fill + per-account wave apply of multi-event accounts
 void launch_update_segments(const UpdateArgs& a, hipStream_t st);
 
 // ---- K2 tree ensemble (complete layout)
@@ -132,8 +149,6 @@ struct EnsembleArgs {
   ResultRec* out;
   unsigned long long* metrics;  // [128] score histogram(101) | actions(4) | ml_high | rows (nullable)
   int32_t n_rows;
-  int32_t do_update;        // apply single-event accounts / open segments (score-then-update)
-  UpdateArgs upd;
 };
 void launch_ensemble(const EnsembleArgs& a, hipStream_t st);
 

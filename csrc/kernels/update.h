@@ -1,4 +1,4 @@
-// Feature-store write path shared by feature_assemble (dedup insert), ensemble (single-event
+// Feature-store write path shared by the dedup/update kernels, feature_assemble (single-event
 // apply) and the segment kernels. Golden: igaming_platform_amd/golden/features.py
 // GoldenFeatureStore.apply == redis_store.go:119-168 on the ring representation.
 #pragma once
@@ -7,32 +7,36 @@
 
 namespace igp {
 
-// One dedup region: per-batch hash table slot -> (first event, count) plus segment lists of
-// accounts that have several events in the batch.
+// One dedup region: per-batch hash table slot -> (account, first event, event count), the
+// events of multi-event accounts (up to DEDUP_LIST per account, by arrival; the apply sorts
+// them) and the list of multi-event hash slots.
 struct DedupTab {
   int32_t* keys;
   int32_t* first;
   int32_t* count;
   int32_t* fill;
-  int32_t* off;
-  int32_t* list;    // [n_max]
+  int32_t* done;    // scorer path: rows of the account whose reads are complete
+  int32_t* list;    // [cap][DEDUP_LIST]
   int32_t* mlist;   // [n_max] hash slots of multi-event accounts
-  int32_t* ctr;     // [0] segment allocator, [1] multi-account count
+  int32_t* ctr;     // [0] multi-account count, [1] spare
   int32_t cap;
-  int32_t nmax;     // capacity of list / mlist
+  int32_t nmax;     // capacity of mlist
 };
 
+__host__ __device__ inline size_t dedup_region_size(int cap, int n_max) {
+  return ((size_t)5 * cap + (size_t)cap * DEDUP_LIST + (size_t)n_max + 2 + 15) & ~size_t(15);
+}
+
 __device__ __forceinline__ DedupTab dedup_region(int32_t* buf, int cap, int n_max, int region) {
-  const size_t rs = ((size_t)5 * cap + 2 * (size_t)n_max + 2 + 15) & ~size_t(15);
-  int32_t* b = buf + rs * region;
+  int32_t* b = buf + dedup_region_size(cap, n_max) * region;
   DedupTab t;
   t.keys = b;
   t.first = b + cap;
   t.count = b + 2 * cap;
   t.fill = b + 3 * cap;
-  t.off = b + 4 * cap;
+  t.done = b + 4 * cap;
   t.list = b + 5 * cap;
-  t.mlist = t.list + n_max;
+  t.mlist = t.list + (size_t)cap * DEDUP_LIST;
   t.ctr = t.mlist + n_max;
   t.cap = cap;
   t.nmax = n_max;
@@ -68,13 +72,14 @@ __device__ __forceinline__ int dedup_find(const DedupTab& t, int s) {
   return -1;
 }
 
-// clear entries [e0, e1) of a region (keys, first, count, fill)
+// clear entries [e0, e1) of a region (keys, first, count, fill, done)
 __device__ __forceinline__ void dedup_clear_range(const DedupTab& t, int e0, int e1, int lane) {
   for (int e = e0 + lane; e < e1; e += 64) {
     t.keys[e] = -1;
     t.first[e] = 0x7fffffff;
     t.count[e] = 0;
     t.fill[e] = 0;
+    t.done[e] = 0;
   }
 }
 
@@ -99,33 +104,53 @@ __device__ __forceinline__ void hll_add(uint8_t* rg, uint32_t& exp, uint64_t h, 
   exp = (uint32_t)(now + ttl);
 }
 
-// encode + store one GRU event row (golden.features.encode_event), dim 16 bf16 = 32 B
+// word k (bf16 pair) of one encoded GRU event row (golden.features.encode_event), dim 16
+__device__ __forceinline__ uint32_t event_word(int k, int64_t amt, int tt, int64_t now, int64_t prev, bool new_dev,
+                                               bool new_ip) {
+  switch (k) {
+    case 0:
+      return (uint32_t)f32_to_bf16((float)(log1p((double)(amt > 0 ? amt : 0)) / 16.0)) |
+             ((uint32_t)f32_to_bf16(tt == 0 ? 1.f : 0.f) << 16);
+    case 1: return (uint32_t)f32_to_bf16(tt == 1 ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(tt == 2 ? 1.f : 0.f) << 16);
+    case 2: return (uint32_t)f32_to_bf16(tt == 3 ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(tt == 4 ? 1.f : 0.f) << 16);
+    case 3: {
+      const int64_t dt = (prev > 0 && now >= prev) ? now - prev : 0;
+      return (uint32_t)f32_to_bf16(tt == 5 ? 1.f : 0.f) |
+             ((uint32_t)f32_to_bf16((float)(log1p((double)dt) / 12.0)) << 16);
+    }
+    case 4: {
+      const double hour = (double)(now % 86400) / 3600.0;
+      return (uint32_t)f32_to_bf16((float)sin(2.0 * M_PI * hour / 24.0)) |
+             ((uint32_t)f32_to_bf16((float)cos(2.0 * M_PI * hour / 24.0)) << 16);
+    }
+    case 5: return (uint32_t)f32_to_bf16(new_dev ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(new_ip ? 1.f : 0.f) << 16);
+    case 6: return (uint32_t)f32_to_bf16(amt >= 100000 ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(1.f) << 16);
+    default: return 0u;
+  }
+}
+
+// encode + store one GRU event row (one thread), dim 16 bf16 = 32 B
 __device__ __forceinline__ void write_event_row(uint16_t* e, int64_t amt, int tt, int64_t now, int64_t prev,
                                                 bool new_dev, bool new_ip) {
-  const int64_t dt = (prev > 0 && now >= prev) ? now - prev : 0;
-  const double hour = (double)(now % 86400) / 3600.0;
   uint32_t w[8];
-  w[0] = (uint32_t)f32_to_bf16((float)(log1p((double)(amt > 0 ? amt : 0)) / 16.0)) |
-         ((uint32_t)f32_to_bf16(tt == 0 ? 1.f : 0.f) << 16);
-  w[1] = (uint32_t)f32_to_bf16(tt == 1 ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(tt == 2 ? 1.f : 0.f) << 16);
-  w[2] = (uint32_t)f32_to_bf16(tt == 3 ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(tt == 4 ? 1.f : 0.f) << 16);
-  w[3] = (uint32_t)f32_to_bf16(tt == 5 ? 1.f : 0.f) |
-         ((uint32_t)f32_to_bf16((float)(log1p((double)dt) / 12.0)) << 16);
-  w[4] = (uint32_t)f32_to_bf16((float)sin(2.0 * M_PI * hour / 24.0)) |
-         ((uint32_t)f32_to_bf16((float)cos(2.0 * M_PI * hour / 24.0)) << 16);
-  w[5] = (uint32_t)f32_to_bf16(new_dev ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(new_ip ? 1.f : 0.f) << 16);
-  w[6] = (uint32_t)f32_to_bf16(amt >= 100000 ? 1.f : 0.f) | ((uint32_t)f32_to_bf16(1.f) << 16);
-  w[7] = 0u;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) w[k] = event_word(k, amt, tt, now, prev, new_dev, new_ip);
   uint4* e4 = reinterpret_cast<uint4*>(e);
   e4[0] = make_uint4(w[0], w[1], w[2], w[3]);
   e4[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+// event time: the batch clock on the scorer path (hdr set: every request of a scoring batch
+// happens "now"), the event's own ts for standalone ingestion (event bus, history replay)
+__device__ __forceinline__ int64_t event_ts(const UpdateArgs& a, const ReqRec& ev) {
+  return a.hdr ? a.hdr->now : ev.ts;
 }
 
 // apply one event to an account whose AcctRT `r` the caller holds in registers
 __device__ __forceinline__ void apply_event(const UpdateArgs& a, int j, AcctRT& r) {
   const ReqRec ev = a.req[j];
   const int s = ev.slot;
-  const int64_t now = ev.ts;
+  const int64_t now = event_ts(a, ev);
   const ScoreCfg& cfg = *a.cfg;
   const int64_t amt = ev.amount;
   const int hd = r.ring_head;
@@ -152,24 +177,28 @@ __device__ __forceinline__ void apply_event(const UpdateArgs& a, int j, AcctRT& 
   r.last_event_ts = (uint32_t)now;
 }
 
-// the batch's first event of account s: apply it (single) or open its segment (multi)
-__device__ __forceinline__ void update_first_event(const UpdateArgs& a, const DedupTab& t, int i, int s) {
+// event i of a multi-event account (hash slot h): append it to the account's list; the
+// account's first event also enters the multi-account list (applied by update_multi)
+__device__ __forceinline__ void note_multi_event(const DedupTab& t, int h, int i, bool first) {
+  const int pos = atomicAdd(&t.fill[h], 1);
+  if (pos < DEDUP_LIST) t.list[(size_t)h * DEDUP_LIST + pos] = i;
+  if (first) {
+    const int m = atomicAdd(&t.ctr[0], 1);
+    if (m < t.nmax) t.mlist[m] = h;
+  }
+}
+
+// event i of account s: apply it (the account's only event) or queue it (multi)
+__device__ __forceinline__ void update_event(const UpdateArgs& a, const DedupTab& t, int i, int s) {
   const int h = dedup_find(t, s);
-  if (h < 0 || t.first[h] != i) return;
+  if (h < 0) return;
   const int c = t.count[h];
   if (c == 1) {
     AcctRT r = a.rt[s];
     apply_event(a, i, r);
     a.rt[s] = r;
   } else {
-    // capacity guards: a batch has at most nmax events, so these only trip on misuse
-    // (e.g. a re-played batch header); the segment is then skipped, never written out of bounds
-    const int off = atomicAdd(&t.ctr[0], c);
-    t.off[h] = off + c <= t.nmax ? off : -1;
-    if (off + c <= t.nmax) {
-      const int m = atomicAdd(&t.ctr[1], 1);
-      if (m < t.nmax) t.mlist[m] = h;
-    }
+    note_multi_event(t, h, i, t.first[h] == i);
   }
 }
 

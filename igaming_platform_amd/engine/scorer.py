@@ -1,26 +1,42 @@
 """GPU scoring pipeline for one MI355X (one feature shard, one model replica).
 
-One micro-batch = one captured hipGraph replay:
+One micro-batch = three captured hipGraphs on three HIP streams:
 
-  H2D  pinned slab [BatchHdr | ReqRec x n] -> device slab            (one copy)
-  K1   feature_assemble (+blacklist, +ip-intel, +HLL counts, +rules) -> X, FeatRec
-  K2/K3/K4  model steps of the compiled ONNX plan                      -> ml
-  K5   ensemble + action (+K10 metrics histogram)                      -> ResultRec
-  K6   feature_update: the batch's own transactions (score-then-update, engine.go:486-488)
-  D2H  ResultRec [n] -> pinned result buffer                           (one copy)
+  copy stream
+    H2D  pinned slab [BatchHdr | ReqRec x n] -> the slot's device slab      (one copy)
+    K6a  dedup insert: the batch's accounts -> its dedup ring region
+  state stream (owns the HBM feature store; batches run strictly in submit order)
+    K1   feature_assemble (+blacklist, +ip-intel, +HLL counts, +rules) -> X, FeatRec, then
+         score-then-update: a wave applies its event when its account has no other event in
+         the batch; for a multi-event account the last wave to finish its reads applies the
+         account's events in row order
+  model stream (reads only the slot's X / FeatRec; never touches the store)
+    K2/K3 model steps of the compiled ONNX plan                            -> ml
+    K5   ensemble + action (+K10 metrics histogram)                        -> ResultRec
+    D2H  ResultRec [n] -> pinned result buffer                             (one copy)
+
+Score-then-update (engine.go:486-488) needs only the batch's own requests and the state K1
+read, so the whole store read-modify-write finishes inside K1, and the next batch's K1 starts
+while this batch's trees / MLP / ensemble still run on the model stream; its copy
+and dedup insert run even earlier, under this batch's K1 (dedup regions rotate over three by
+batch seq; K1 of batch q clears the region of batch q+2, so the copy of batch q waits for the
+state graph of batch q-2). Each pipeline slot has its own device slab, X, FeatRec, result and
+model activation buffers; a slot is reused only after the model graph that last read it.
 
 Graphs are captured per (batch bucket, pipeline slot); a batch is padded to the smallest
-bucket >= n and kernels read the live count from the device header, so padded rows are
-inert. Thresholds/weights live in a device config block (``cfg_dev``): UpdateThresholds
-is a 176-byte copy, never a re-capture. Pipeline slots double-buffer the pinned host
-memory so the host packs batch i+1 while the GPU runs batch i.
+bucket >= n and kernels read the live count and the clock from the device header, so padded
+rows are inert and ReqRec.ts is ignored (every request of a batch happens at its ``now``).
+Thresholds/weights live in a device config block (``cfg_dev``): UpdateThresholds is a
+176-byte copy, never a re-capture. Pipeline slots multi-buffer the pinned host memory so the
+host packs batch i+1 while the GPU runs batch i.
 """
 from __future__ import annotations
 
+import collections
 import threading
 import time
 from dataclasses import dataclass
-from typing import Dict, List, Optional
+from typing import Dict, Optional
 
 import numpy as np
 import torch
@@ -34,6 +50,10 @@ from .runner import DeviceModel
 
 HDR_BYTES = 16
 REQ_BYTES = REQREC.itemsize
+
+
+class _Slot:
+    """Device buffers of one pipeline slot (slab, model input/output, results)."""
 
 
 @dataclass
@@ -73,45 +93,62 @@ class GpuScorer:
         dev = self.device
         B = self.bmax
         self.slab_bytes = HDR_BYTES + REQ_BYTES * B
-        self.dev_slab = torch.zeros(self.slab_bytes, dtype=torch.uint8, device=dev)
-        self.hdr = self.dev_slab[:HDR_BYTES].view(torch.int64)
-        self.n_ptr = self.dev_slab[:4].view(torch.int32)
-        self.req = self.dev_slab[HDR_BYTES:]
         self.depth = int(pipeline_depth)
         self.host_slab = [torch.zeros(self.slab_bytes, dtype=torch.uint8).pin_memory() for _ in range(self.depth)]
         self.host_slab_np = [t.numpy() for t in self.host_slab]
-        self.X = torch.zeros((B, self.width), dtype=torch.float32, device=dev)
-        self.feat = torch.zeros((B, 32), dtype=torch.int32, device=dev)
-        self.res = torch.zeros((B, 2), dtype=torch.int32, device=dev)
         self.host_res = [torch.zeros((B, 2), dtype=torch.int32).pin_memory() for _ in range(self.depth)]
         self.host_feat = [torch.zeros((B, 32), dtype=torch.int32).pin_memory() for _ in range(self.depth)]
+        self.slots = [self._alloc_slot() for _ in range(self.depth)]
+        self._cur = 0  # slot of the last submitted batch (the un-indexed buffer properties)
         self.metrics = torch.zeros(128, dtype=torch.int64, device=dev)
-        self._alloc_model_buffers()
+        self.cstream = torch.cuda.Stream(device=dev)   # H2D + dedup insert
+        self.stream = torch.cuda.Stream(device=dev)    # state stream (feature store owner)
+        self.mstream = torch.cuda.Stream(device=dev)   # model / result stream
+        self._copy_ev = [torch.cuda.Event() for _ in range(self.depth)]
+        self._state_ev = [torch.cuda.Event() for _ in range(self.depth)]
+        self._model_ev = [torch.cuda.Event() for _ in range(self.depth)]
+        self._state_hist: collections.deque = collections.deque(maxlen=2)  # state events, batch order
         self.cfg_dev = torch.zeros(176, dtype=torch.uint8, device=dev)
         self.refresh_config()
-        self.graphs: Dict[tuple, "torch.cuda.CUDAGraph"] = {}
+        self.graphs: Dict[tuple, tuple] = {}
         self._slot = 0
         self._seq = 0
         self._lock = threading.Lock()
-        self.stream = torch.cuda.Stream(device=dev)
         self.batches = 0
 
     # ------------------------------------------------------------------ buffers / config
-    def _alloc_model_buffers(self):
-        self.model_dev = None
-        self.step_out: List[torch.Tensor] = []
-        self.tree_partial = None
-        self.tree_groups: Dict[int, int] = {}
-        self.ml = None
-        if self.plan is None:
-            return
-        if any(s.kind == "gru" for s in self.plan.steps):
-            raise ValueError("fraud scoring models take a feature vector; GRU models run in the abuse scorer")
-        self.model_dev = DeviceModel(self.plan, self.device, self.buckets)
-        self.step_out = self.model_dev.step_out
-        self.tree_partial = self.model_dev.tree_partial
-        self.tree_groups = self.model_dev.tree_groups
-        self.ml = self.model_dev.out
+    def _alloc_slot(self) -> "_Slot":
+        dev, B = self.device, self.bmax
+        sb = _Slot()
+        sb.dev_slab = torch.zeros(self.slab_bytes, dtype=torch.uint8, device=dev)
+        sb.hdr = sb.dev_slab[:HDR_BYTES].view(torch.int64)
+        sb.n_ptr = sb.dev_slab[:4].view(torch.int32)
+        sb.req = sb.dev_slab[HDR_BYTES:]
+        sb.X = torch.zeros((B, self.width), dtype=torch.float32, device=dev)
+        sb.feat = torch.zeros((B, 32), dtype=torch.int32, device=dev)
+        sb.res = torch.zeros((B, 2), dtype=torch.int32, device=dev)
+        sb.model = None
+        if self.plan is not None:
+            if any(s.kind == "gru" for s in self.plan.steps):
+                raise ValueError("fraud scoring models take a feature vector; GRU models run in the abuse scorer")
+            sb.model = DeviceModel(self.plan, dev, self.buckets)
+        return sb
+
+    # buffers of the last submitted batch (tests / tools)
+    X = property(lambda self: self.slots[self._cur].X)
+    feat = property(lambda self: self.slots[self._cur].feat)
+    res = property(lambda self: self.slots[self._cur].res)
+    hdr = property(lambda self: self.slots[self._cur].hdr)
+    req = property(lambda self: self.slots[self._cur].req)
+    n_ptr = property(lambda self: self.slots[self._cur].n_ptr)
+    dev_slab = property(lambda self: self.slots[self._cur].dev_slab)
+    model_dev = property(lambda self: self.slots[self._cur].model)
+    ml = property(lambda self: self.slots[self._cur].model.out if self.slots[self._cur].model else None)
+    step_out = property(lambda self: self.slots[self._cur].model.step_out if self.slots[self._cur].model else [])
+    tree_partial = property(lambda self: self.slots[self._cur].model.tree_partial
+                            if self.slots[self._cur].model else None)
+    tree_groups = property(lambda self: self.slots[self._cur].model.tree_groups
+                           if self.slots[self._cur].model else {})
 
     def refresh_config(self, scoring=None) -> None:
         """Write the device config block (thresholds, weights, table sizes). The last
@@ -125,44 +162,54 @@ class GpuScorer:
         c = score_cfg(self.cfg, kind, ml_col=ml_col, ml_stride=ml_stride, sc=scoring,
                       owner_filter=self.owner_filter, my_rank=self.rank, **self.store.table_params())
         self.store.sync_tables()
+        # batches already on the model stream finish under the config they were submitted with
+        torch.cuda.current_stream(self.device).wait_stream(self.mstream)
         self.cfg_dev.copy_(torch.from_numpy(c.view(np.uint8).copy()))
 
     # ------------------------------------------------------------------ the step
-    def _kernels(self, bucket: int) -> None:
-        upd = self.update_features
-        K.feature_assemble(self.store, self.hdr, self.cfg_dev, self.req, self.X, self.feat, bucket, dedup=upd)
-        if self.model_dev is not None:
-            self.model_dev.run(self.X, bucket, m_ptr=self.n_ptr)
-        ud = K.update_args(self.store, self.cfg_dev, self.req, bucket, hdr=self.hdr, region=-1) if upd else None
-        K.ensemble(self.hdr, self.cfg_dev, self.feat, self.X, self.ml, self.res, bucket, self.metrics, upd=ud)
-        if upd:
-            K.update_segments(self.store, self.cfg_dev, self.req, bucket, self.hdr)
-
-    def _body(self, slot: int, bucket: int, with_features: bool = False) -> None:
+    def _copy_body(self, slot: int, bucket: int) -> None:
+        sb = self.slots[slot]
         nbytes = HDR_BYTES + REQ_BYTES * bucket
-        self.dev_slab[:nbytes].copy_(self.host_slab[slot][:nbytes], non_blocking=True)
-        self._kernels(bucket)
-        self.host_res[slot][:bucket].copy_(self.res[:bucket], non_blocking=True)
+        sb.dev_slab[:nbytes].copy_(self.host_slab[slot][:nbytes], non_blocking=True)
+        if self.update_features:
+            K.dedup_insert(self.store, self.cfg_dev, sb.req, bucket, sb.hdr)
+
+    def _state_body(self, slot: int, bucket: int) -> None:
+        sb, upd = self.slots[slot], self.update_features
+        K.feature_assemble(self.store, sb.hdr, self.cfg_dev, sb.req, sb.X, sb.feat, bucket, dedup=upd)
+
+    def _model_body(self, slot: int, bucket: int, with_features: bool = False) -> None:
+        sb = self.slots[slot]
+        ml = None
+        if sb.model is not None:
+            ml = sb.model.run(sb.X, bucket, m_ptr=sb.n_ptr)
+        K.ensemble(sb.hdr, self.cfg_dev, sb.feat, sb.X, ml, sb.res, bucket, self.metrics)
+        self.host_res[slot][:bucket].copy_(sb.res[:bucket], non_blocking=True)
         if with_features:
-            self.host_feat[slot][:bucket].copy_(self.feat[:bucket], non_blocking=True)
+            self.host_feat[slot][:bucket].copy_(sb.feat[:bucket], non_blocking=True)
 
     def capture(self) -> None:
-        """Capture one graph per (bucket, pipeline slot); run each once eagerly first."""
+        """Capture the copy, state and model graphs per (bucket, pipeline slot); each body runs
+        once eagerly first (n = 0)."""
         if not self.use_graphs:
             return
         with torch.cuda.device(self.device):
             for b in self.buckets:
                 for slot in range(self.depth):
                     self._write_hdr(slot, 0, 0)
-                    s = torch.cuda.Stream(device=self.device)
-                    s.wait_stream(torch.cuda.current_stream())
-                    with torch.cuda.stream(s):
-                        self._body(slot, b)
-                    torch.cuda.current_stream().wait_stream(s)
-                    g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, stream=s):
-                        self._body(slot, b)
-                    self.graphs[(b, slot)] = g
+                    pair = []
+                    for body in (lambda: self._copy_body(slot, b), lambda: self._state_body(slot, b),
+                                 lambda: self._model_body(slot, b)):
+                        s = torch.cuda.Stream(device=self.device)
+                        s.wait_stream(torch.cuda.current_stream())
+                        with torch.cuda.stream(s):
+                            body()
+                        torch.cuda.current_stream().wait_stream(s)
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g, stream=s):
+                            body()
+                        pair.append(g)
+                    self.graphs[(b, slot)] = tuple(pair)
             torch.cuda.synchronize(self.device)
 
     def bucket_for(self, n: int) -> int:
@@ -192,35 +239,59 @@ class GpuScorer:
         self._seq += 1
         self._write_hdr(slot, n, now)
         t0 = time.perf_counter()
-        with torch.cuda.stream(self.stream):
-            g = self.graphs.get((b, slot))
-            if g is not None and not want_features:
-                g.replay()
+        g = self.graphs.get((b, slot))
+        with torch.cuda.stream(self.cstream):
+            self.cstream.wait_event(self._model_ev[slot])  # the slot's device buffers are free
+            if len(self._state_hist) == 2:  # K1 of batch seq-2 has cleared this batch's dedup region
+                self.cstream.wait_event(self._state_hist[0])
+            if g is not None:
+                g[0].replay()
             else:
-                self._body(slot, b, with_features=want_features)
+                self._copy_body(slot, b)
+            self._copy_ev[slot].record(self.cstream)
+        with torch.cuda.stream(self.stream):
+            self.stream.wait_event(self._copy_ev[slot])
+            if g is not None:
+                g[1].replay()
+            else:
+                self._state_body(slot, b)
+            sev = torch.cuda.Event()
+            sev.record(self.stream)
+        self._state_ev[slot] = sev
+        self._state_hist.append(sev)
+        with torch.cuda.stream(self.mstream):
+            self.mstream.wait_event(sev)
+            if g is not None and not want_features:
+                g[2].replay()
+            else:
+                self._model_body(slot, b, with_features=want_features)
             ev = torch.cuda.Event()
-            ev.record(self.stream)
+            ev.record(self.mstream)
+        self._model_ev[slot] = ev
+        self._cur = slot
         self.batches += 1
         return Pending(slot, n, b, ev, t0, want_features)
 
+    def pack(self, slot: int, req: np.ndarray) -> int:
+        """Copy REQREC rows into the slot's pinned slab as raw bytes (a field-wise structured
+        copy costs ~20x more). Row ``ts`` is ignored on this path: kernels use the batch clock."""
+        n = len(req)
+        if req.dtype != REQREC:
+            req = np.asarray(req, REQREC)
+        src = np.ascontiguousarray(req).view(np.uint8).reshape(-1)
+        np.copyto(self.host_slab_np[slot][HDR_BYTES:HDR_BYTES + REQ_BYTES * n], src)
+        return n
+
     def submit_into(self, slot: int, req: np.ndarray, now: Optional[int] = None,
                     want_features: bool = False) -> Pending:
-        n = len(req)
         now = int(time.time()) if now is None else int(now)
-        v = self.slab_view(slot, n)
-        v[:] = req
-        v["ts"] = now
-        return self.submit_packed(slot, n, now, want_features)
+        return self.submit_packed(slot, self.pack(slot, req), now, want_features)
 
     def submit(self, req: np.ndarray, now: Optional[int] = None, want_features: bool = False) -> Pending:
-        """``req``: REQREC structured array (rows; ts is overwritten with ``now``)."""
-        n = len(req)
+        """``req``: REQREC structured array (every row is scored and applied at ``now``)."""
         now = int(time.time()) if now is None else int(now)
         slot = self.next_slot()
-        v = self.slab_view(slot, n)
-        v[:] = req
-        v["ts"] = now
-        return self.submit_packed(slot, n, now, want_features)
+        return self.submit_packed(slot, self.pack(slot, req), now, want_features)
 
     def wait(self, p: Pending, unpack: bool = True):
         p.event.synchronize()
@@ -238,6 +309,7 @@ class GpuScorer:
         return self.wait(self.submit(req, now, want_features))
 
     def read_metrics(self, reset: bool = False) -> np.ndarray:
+        self.mstream.synchronize()
         m = self.metrics.cpu().numpy().copy()
         if reset:
             self.metrics.zero_()

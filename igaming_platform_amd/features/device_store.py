@@ -30,6 +30,10 @@ from ..config import FeatureConfig
 from ..layouts import ACCTBATCH, ACCTRT
 from .tables import Blacklist, IPIntel
 
+DEDUP_LIST = 64  # events per account per batch kept in a dedup list (launch.h DEDUP_LIST)
+DEDUP_REGIONS = 4  # 3 scorer ring regions (by batch seq) + 1 standalone ingestion region
+DEDUP_STANDALONE = 3
+
 
 def _pow2_at_least(n: int) -> int:
     c = 1
@@ -71,19 +75,21 @@ class DeviceFeatureStore:
         self._bl_version = -1
         self._ip_version = -1
         self.max_events = int(max_events)
-        # dedup scratch for ordered score-then-update: 3 regions (scorer ping-pong + standalone)
+        # dedup scratch for ordered score-then-update: scorer ring regions + standalone
         self.dmax = self.max_events
         self.dcap = _pow2_at_least(2 * self.max_events)
-        self.dregion = (5 * self.dcap + 2 * self.dmax + 2 + 15) & ~15
-        self.dbuf = torch.empty(3 * self.dregion, dtype=torch.int32, **z)
+        # per region (csrc/kernels/update.h dedup_region): keys/first/count/fill/done [cap],
+        # per-account event lists [cap][DEDUP_LIST], multi-account list [dmax], 2 counters
+        self.dregion = (5 * self.dcap + self.dcap * DEDUP_LIST + self.dmax + 2 + 15) & ~15
+        self.dbuf = torch.empty(DEDUP_REGIONS * self.dregion, dtype=torch.int32, **z)
         self.reset_dedup()
 
     def reset_dedup(self) -> None:
-        r = self.dbuf.view(3, self.dregion)
+        r = self.dbuf.view(DEDUP_REGIONS, self.dregion)
         r[:, : self.dcap].fill_(-1)                            # keys
         r[:, self.dcap: 2 * self.dcap].fill_(0x7FFFFFFF)        # first
-        r[:, 2 * self.dcap: 4 * self.dcap].zero_()              # count, fill
-        r[:, 5 * self.dcap + 2 * self.dmax:].zero_()            # counters
+        r[:, 2 * self.dcap: 5 * self.dcap].zero_()              # count, fill, done
+        r[:, (5 + DEDUP_LIST) * self.dcap + self.dmax:].zero_()  # counters
 
     # ------------------------------------------------------------------ sizing
     def bytes_per_account(self) -> int:

@@ -69,6 +69,10 @@ def check_layouts(mod) -> None:
         want = getattr(mod, "SIZEOF_" + name)
         if dt.itemsize != want:
             raise RuntimeError(f"layout drift: {name} is {dt.itemsize} B in Python, {want} B in C")
+    from .features.device_store import DEDUP_LIST, DEDUP_REGIONS
+    if (getattr(mod, "DEDUP_LIST", DEDUP_LIST), getattr(mod, "DEDUP_REGIONS", DEDUP_REGIONS)) != (DEDUP_LIST,
+                                                                                                 DEDUP_REGIONS):
+        raise RuntimeError("layout drift: dedup scratch layout differs between Python and C")
 
 
 def score_cfg(cfg: Config, model_kind: int, ml_col: int = 0, ml_stride: int = 1,

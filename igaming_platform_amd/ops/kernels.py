@@ -11,8 +11,9 @@ from typing import Optional
 
 import torch
 
-from ..native import hipk
+from ..features.device_store import DEDUP_STANDALONE
 from ..layouts import check_layouts
+from ..native import hipk
 
 ACT = {"none": 0, "relu": 1, "sigmoid": 2, "tanh": 3}
 _checked = False
@@ -62,7 +63,9 @@ def _opt(t: Optional[torch.Tensor], name: str, **kw):
 # --------------------------------------------------------------------------- K1
 def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch.Tensor,
                      X: torch.Tensor, feat: torch.Tensor, n_rows: int, dedup: bool = False) -> None:
-    """K1. ``dedup=True`` also registers each request for score-then-update (ping-pong region)."""
+    """K1. ``dedup=True``: score-then-update. :func:`dedup_insert` must have registered the
+    batch first; K1 then applies each single-event account's event and opens the segments
+    that :func:`update_segments` applies afterwards (dedup ring region by batch seq)."""
     dev = store.device
     if X.dim() != 2 or X.shape[1] < 30 + store.ext_width:
         raise ValueError("X must be [rows, >= 30 + ext_width]")
@@ -81,17 +84,19 @@ def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch
         dbuf=_need(store.dbuf, "dbuf", torch.int32) if dedup else None, dcap=int(store.dcap), dmax=int(store.dmax),
         x_stride=int(X.shape[1]), ring_size=int(store.ring_ts.shape[1]), n_rows=int(n_rows),
     )
+    if dedup:
+        d["upd"] = update_args(store, cfg_dev, req, n_rows, hdr=hdr, region=-1)
     _mod().feature_assemble(d, _stream())
 
 
 # --------------------------------------------------------------------------- K6
 def update_args(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, n: int = 0,
-                hdr: Optional[torch.Tensor] = None, region: int = 2) -> dict:
+                hdr: Optional[torch.Tensor] = None, region: int = DEDUP_STANDALONE) -> dict:
     dev = store.device
     if n_max > store.dmax:
         raise ValueError(f"feature_update: {n_max} events > store dedup capacity {store.dmax}")
     if region < 0 and hdr is None:
-        raise ValueError("ping-pong dedup region needs the batch header")
+        raise ValueError("ring dedup region needs the batch header")
     if store.ev is not None and store.ev.shape[2] != 16:
         raise ValueError("event ring dim must be 16")
     return dict(
@@ -111,12 +116,19 @@ def feature_update(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, 
     """Standalone ordered event ingestion (event bus / history replay): ``n`` events."""
     if n > n_max:
         raise ValueError("n > n_max")
-    d = update_args(store, cfg_dev, req, n_max, n=n, region=2)
+    d = update_args(store, cfg_dev, req, n_max, n=n, region=DEDUP_STANDALONE)
+    _mod().feature_update(d, _stream())
+
+
+def dedup_insert(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, hdr: torch.Tensor) -> None:
+    """Scorer head: register the batch's accounts in its dedup region (before K1)."""
+    d = update_args(store, cfg_dev, req, n_max, hdr=hdr, region=-1)
+    d["insert_only"] = 1
     _mod().feature_update(d, _stream())
 
 
 def update_segments(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, hdr: torch.Tensor) -> None:
-    """Scorer tail: ordered apply of multi-event accounts (insert ran in K1, singles in K5)."""
+    """Scorer tail: ordered apply of multi-event accounts (insert before K1, singles in K1)."""
     d = update_args(store, cfg_dev, req, n_max, hdr=hdr, region=-1)
     d["segments_only"] = 1
     _mod().feature_update(d, _stream())
@@ -215,14 +227,13 @@ def mlp_head(hs, X: Optional[torch.Tensor], Y: torch.Tensor, M: int, m_ptr: Opti
 
 # --------------------------------------------------------------------------- K5 / K10
 def ensemble(hdr, cfg_dev, feat, X, ml: Optional[torch.Tensor], out, n_rows: int,
-             metrics: Optional[torch.Tensor] = None, upd: Optional[dict] = None) -> None:
+             metrics: Optional[torch.Tensor] = None) -> None:
     dev = feat.device
     d = dict(hdr=_need(hdr, "hdr", torch.int64, 2, dev), cfg=_need(cfg_dev, "cfg", torch.uint8, 176, dev),
              feat=_need(feat, "feat", torch.int32, 32 * n_rows, dev),
              X=_need(X, "X", torch.float32, X.shape[1] * n_rows, dev), x_stride=int(X.shape[1]),
              ml=_opt(ml, "ml", dtype=torch.float32), out=_need(out, "out", torch.int32, 2 * n_rows, dev),
-             metrics=_opt(metrics, "metrics", dtype=torch.int64, min_numel=128), n_rows=int(n_rows),
-             do_update=int(upd is not None), upd=upd)
+             metrics=_opt(metrics, "metrics", dtype=torch.int64, min_numel=128), n_rows=int(n_rows))
     if ml is not None and ml.numel() < n_rows:
         raise ValueError("ensemble: model output shorter than the batch")
     _mod().ensemble(d, _stream())

@@ -41,11 +41,12 @@ def main():
     tree = next((s for s in steps if s.kind == "tree"), None)
     head = next((s for s in steps if s.kind == "head"), None)
     g = sc.tree_groups.get(B, 1)
-    ud = K.update_args(sc.store, sc.cfg_dev, sc.req, B, hdr=sc.hdr, region=-1)
     ops = {
         "h2d_slab": lambda: sc.dev_slab[:nb].copy_(sc.host_slab[slot][:nb], non_blocking=True),
-        "feature_assemble": lambda: K.feature_assemble(sc.store, sc.hdr, sc.cfg_dev, sc.req, sc.X, sc.feat, B, dedup=True),
-        "ensemble+single_update": lambda: K.ensemble(sc.hdr, sc.cfg_dev, sc.feat, sc.X, sc.ml, sc.res, B, sc.metrics, upd=ud),
+        "dedup_insert": lambda: K.dedup_insert(sc.store, sc.cfg_dev, sc.req, B, sc.hdr),
+        "feature_assemble+single_update": lambda: K.feature_assemble(sc.store, sc.hdr, sc.cfg_dev, sc.req, sc.X,
+                                                                     sc.feat, B, dedup=True),
+        "ensemble": lambda: K.ensemble(sc.hdr, sc.cfg_dev, sc.feat, sc.X, sc.ml, sc.res, B, sc.metrics),
         "update_segments": lambda: K.update_segments(sc.store, sc.cfg_dev, sc.req, B, sc.hdr),
         "d2h_results": lambda: sc.host_res[slot][:B].copy_(sc.res[:B], non_blocking=True),
     }
@@ -57,8 +58,8 @@ def main():
         ops["mlp_head"] = lambda: K.mlp_head(head, sc.X, out, B, m_ptr=sc.n_ptr,
                                              tree_partial=(sc.tree_partial, g, tree) if tree else None)
     if sc.graphs:
-        gr = sc.graphs[(B, slot)]
-        ops["full_step_graph"] = gr.replay
+        gc, gs, gm = sc.graphs[(B, slot)]
+        ops["full_step_graph"] = lambda: (gc.replay(), gs.replay(), gm.replay())
     times = {k: [] for k in ops}
     for r in range(a.rounds):
         # a fresh batch sequence number per round, as the scorer does per micro-batch
