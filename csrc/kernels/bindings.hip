@@ -88,6 +88,8 @@ PYBIND11_MODULE(_hipk, m) {
     a.bl_exp = ptr<const uint32_t*>(d, "bl_exp");
     a.ip_keys = ptr<const uint64_t*>(d, "ip_keys");
     a.ip_flags = ptr<const uint32_t*>(d, "ip_flags");
+    a.hll_lc = ptr<const int32_t*>(d, "hll_lc");
+    if (!a.hll_lc) throw std::runtime_error("feature_assemble: hll_lc table required");
     a.X = ptr<float*>(d, "X");
     a.feat = ptr<FeatRec*>(d, "feat");
     a.dbuf = ptr<int32_t*>(d, "dbuf");

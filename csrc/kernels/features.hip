@@ -11,6 +11,13 @@
 namespace igp {
 
 // ---------------------------------------------------------------------------------- K1
+// model input l (onnx_model.go:133-184): 1 = minMaxScale(x, 0, k1_hi[l]), 2 = logTransform
+__constant__ int k1_kind[32] = {1, 1, 1, 2, 0, 1, 1, 0, 0, 1, 2, 2, 0, 0, 0, 1,
+                                0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 0, 0, 0, 0, 0};
+__constant__ float k1_hi[32] = {20.f, 50.f, 200.f, 1.f, 1.f, 10.f, 20.f, 1.f, 1.f, 365.f, 1.f, 1.f, 1.f, 1.f, 1.f,
+                                86400.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f,
+                                1.f, 1.f};
+
 __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h, int c, int s, AcctRT r,
                                    int lane);
 
@@ -31,9 +38,11 @@ __device__ __forceinline__ bool hll_add_wave(uint32_t* words, uint32_t w, uint32
 }
 
 // apply_event (update.h) spread over a wave that already holds the account's AcctRT (uniform)
-// and HLL registers (wd / wi: 4 per lane); same arithmetic, same stored bytes.
+// and HLL registers (wd / wi: 4 per lane); same arithmetic, same stored bytes. The event row
+// is built by lanes 0..7 (one word each) with a single double log1p pass (lane 0: amount,
+// lane 3: dt) and the batch's precomputed hour-of-day word `hour_word`.
 __device__ __forceinline__ void apply_event_wave(const UpdateArgs& a, const ReqRec& ev, AcctRT r, uint32_t wd,
-                                                 uint32_t wi, int lane) {
+                                                 uint32_t wi, int lane, uint32_t hour_word) {
   const int s = ev.slot;
   const int64_t now = event_ts(a, ev);
   const ScoreCfg& cfg = *a.cfg;
@@ -57,7 +66,22 @@ __device__ __forceinline__ void apply_event_wave(const UpdateArgs& a, const ReqR
   r.session_exp = (uint32_t)(now + cfg.session_ttl);
   if (a.ev) {
     uint32_t* e = reinterpret_cast<uint32_t*>(a.ev + ((size_t)s * a.ev_ring + r.ev_head) * a.ev_dim);
-    if (lane < 8) e[lane] = event_word(lane, amt, ev.tx_type & 0xff, now, (int64_t)r.last_event_ts, new_dev, new_ip);
+    const int tt = ev.tx_type & 0xff;
+    const int64_t prev = (int64_t)r.last_event_ts;
+    const int64_t dt = (prev > 0 && now >= prev) ? now - prev : 0;
+    const double l = log1p(lane == 0 ? (double)(amt > 0 ? amt : 0) : (double)dt);
+    float lo = 0.f, hi = 0.f;
+    switch (lane) {  // bf16 pairs of golden.features.encode_event (update.h event_word)
+      case 0: lo = (float)(l / 16.0); hi = tt == 0; break;
+      case 1: lo = tt == 1; hi = tt == 2; break;
+      case 2: lo = tt == 3; hi = tt == 4; break;
+      case 3: lo = tt == 5; hi = (float)(l / 12.0); break;
+      case 5: lo = new_dev; hi = new_ip; break;
+      case 6: lo = amt >= 100000; hi = 1.f; break;
+      default: break;
+    }
+    const uint32_t w = lane == 4 ? hour_word : ((uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16));
+    if (lane < 8) e[lane] = w;
     r.ev_head = r.ev_head + 1 == a.ev_ring ? 0 : r.ev_head + 1;
     r.ev_count = r.ev_count + 1 > a.ev_ring ? a.ev_ring : r.ev_count + 1;
   }
@@ -148,7 +172,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) extv[u] = e[max(0, min(lane + 64 * u, ext_w - 1))];
   // score-then-update: first probe of the batch's dedup entry
-  uint32_t dh = 0;
+  uint32_t dh = 0, hour_word = 0;
   int dkey = -1, dfirst = -1, dcount = 0;
   if (a.dbuf) {  // kernel-uniform
     const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
@@ -156,6 +180,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     dkey = t.keys[dh];
     dfirst = t.first[dh];
     dcount = t.count[dh];
+    hour_word = (uint32_t)t.ctr[1];
   }
   // K7: blacklist (lanes 0..2: device, fingerprint, ip) and IP intelligence (lane 3): the first
   // probe slot's key and value are loaded with the rest, collisions walk on (rare)
@@ -249,12 +274,15 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     }
     zd = wave_sum(zd); zi = wave_sum(zi);
     vd = wave_sum(vd); vi = wave_sum(vi);
+    // linear counting (E <= 2.5 m, V > 0): floor(m ln(m / V) + 0.5) from the host-computed
+    // table (libm log, as the golden model); otherwise the harmonic estimate
     const double m = 256.0, alpha = 0.7213 / (1.0 + 1.079 / 256.0);
-    double ed = alpha * m * m / zd, ei = alpha * m * m / zi;
-    if (ed <= 2.5 * m && vd > 0) ed = m * log(m / (double)vd);
-    if (ei <= 2.5 * m && vi > 0) ei = m * log(m / (double)vi);
-    hll_dev = now < (int64_t)rt.hll_dev_exp ? (int)floor(ed + 0.5) : 0;
-    hll_ip = now < (int64_t)rt.hll_ip_exp ? (int)floor(ei + 0.5) : 0;
+    const double ed = alpha * m * m / zd, ei = alpha * m * m / zi;
+    const int ld = a.hll_lc[vd], li = a.hll_lc[vi];
+    const int cd = (ed <= 2.5 * m && vd > 0) ? ld : (int)floor(ed + 0.5);
+    const int ci = (ei <= 2.5 * m && vi > 0) ? li : (int)floor(ei + 0.5);
+    hll_dev = now < (int64_t)rt.hll_dev_exp ? cd : 0;
+    hll_ip = now < (int64_t)rt.hll_ip_exp ? ci : 0;
   }
 
   // ---- assemble raw features (wave-uniform values)
@@ -317,41 +345,28 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
   f.reserved1 = score > 100 ? 100 : score;
 
   // ---- writes: the 30 normalised inputs spread over lanes 0..29, the record by lane 0
+  // each lane l < 30 produces model input l: its raw value is selected into the lane from the
+  // (wave-uniform) features, then one pass of the lane's transform (min-max / log / identity)
+  // runs for the whole wave instead of 30 divergent cases
   const int id = cfg.log_identity;
-  float xv = 0.f;
-  switch (lane) {
-    case 0: xv = minmax_scale((float)f.tx_count_1m, 0.f, 20.f); break;
-    case 1: xv = minmax_scale((float)f.tx_count_5m, 0.f, 50.f); break;
-    case 2: xv = minmax_scale((float)f.tx_count_1h, 0.f, 200.f); break;
-    case 3: xv = log_transform((float)f.tx_sum_1h, id); break;
-    case 4: xv = f.tx_avg_1h; break;
-    case 5: xv = minmax_scale((float)f.unique_devices_24h, 0.f, 10.f); break;
-    case 6: xv = minmax_scale((float)f.unique_ips_24h, 0.f, 20.f); break;
-    case 7: xv = (float)f.ip_country_changes_7d; break;
-    case 8: xv = (float)f.device_age_days; break;
-    case 9: xv = minmax_scale((float)f.account_age_days, 0.f, 365.f); break;
-    case 10: xv = log_transform((float)f.total_deposits, id); break;
-    case 11: xv = log_transform((float)f.total_withdrawals, id); break;
-    case 12: xv = (float)f.net_deposit; break;
-    case 13: xv = (float)f.deposit_count; break;
-    case 14: xv = (float)f.withdraw_count; break;
-    case 15: xv = minmax_scale((float)f.time_since_last_tx, 0.f, 86400.f); break;
-    case 16: xv = (float)f.session_duration; break;
-    case 17: xv = f.avg_bet_size; break;
-    case 18: xv = f.win_rate; break;
-    case 19: xv = (flags & FR_VPN) ? 1.f : 0.f; break;
-    case 20: xv = (flags & FR_PROXY) ? 1.f : 0.f; break;
-    case 21: xv = (flags & FR_TOR) ? 1.f : 0.f; break;
-    case 22: xv = (flags & FR_DISPOSABLE) ? 1.f : 0.f; break;
-    case 23: xv = (float)f.bonus_claim_count; break;
-    case 24: xv = f.bonus_wager_rate; break;
-    case 25: xv = (flags & FR_BONUS_ONLY) ? 1.f : 0.f; break;
-    case 26: xv = log_transform((float)amount, id); break;
-    case 27: xv = tx_type == TX_DEPOSIT ? 1.f : 0.f; break;
-    case 28: xv = tx_type == TX_WITHDRAW ? 1.f : 0.f; break;
-    case 29: xv = tx_type == TX_BET ? 1.f : 0.f; break;
-    default: break;
-  }
+  float raw = 0.f;
+#define IGP_PUT(l, v) raw = lane == (l) ? (float)(v) : raw
+  IGP_PUT(0, f.tx_count_1m); IGP_PUT(1, f.tx_count_5m); IGP_PUT(2, f.tx_count_1h); IGP_PUT(3, f.tx_sum_1h);
+  IGP_PUT(4, f.tx_avg_1h); IGP_PUT(5, f.unique_devices_24h); IGP_PUT(6, f.unique_ips_24h);
+  IGP_PUT(7, f.ip_country_changes_7d); IGP_PUT(8, f.device_age_days); IGP_PUT(9, f.account_age_days);
+  IGP_PUT(10, f.total_deposits); IGP_PUT(11, f.total_withdrawals); IGP_PUT(12, f.net_deposit);
+  IGP_PUT(13, f.deposit_count); IGP_PUT(14, f.withdraw_count); IGP_PUT(15, f.time_since_last_tx);
+  IGP_PUT(16, f.session_duration); IGP_PUT(17, f.avg_bet_size); IGP_PUT(18, f.win_rate);
+  IGP_PUT(19, (flags & FR_VPN) ? 1.f : 0.f); IGP_PUT(20, (flags & FR_PROXY) ? 1.f : 0.f);
+  IGP_PUT(21, (flags & FR_TOR) ? 1.f : 0.f); IGP_PUT(22, (flags & FR_DISPOSABLE) ? 1.f : 0.f);
+  IGP_PUT(23, f.bonus_claim_count); IGP_PUT(24, f.bonus_wager_rate); IGP_PUT(25, (flags & FR_BONUS_ONLY) ? 1.f : 0.f);
+  IGP_PUT(26, amount); IGP_PUT(27, tx_type == TX_DEPOSIT ? 1.f : 0.f); IGP_PUT(28, tx_type == TX_WITHDRAW ? 1.f : 0.f);
+  IGP_PUT(29, tx_type == TX_BET ? 1.f : 0.f);
+#undef IGP_PUT
+  const int kind = k1_kind[lane & 31];
+  float xv = raw;
+  if (kind == 1) xv = minmax_scale(raw, 0.f, k1_hi[lane & 31]);
+  else if (kind == 2) xv = log_transform(raw, id);
   if (lane < 30) xr[lane] = xv;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -374,7 +389,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     }
     if (h >= 0) {
       if (dcount == 1) {
-        apply_event_wave(a.upd, rq, rt, wd, wi, lane);
+        apply_event_wave(a.upd, rq, rt, wd, wi, lane, hour_word);
       } else {
         // multi-event account: queue this row, then count it as read (its loads were all
         // consumed above); the wave that completes the count applies the account's whole
@@ -417,6 +432,8 @@ __global__ void dedup_reset_kernel(UpdateArgs a) {
 
 __global__ void dedup_insert_kernel(UpdateArgs a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  // the batch clock's hour-of-day event-row word (sin/cos in double), once per batch for K1
+  if (i == 0 && a.hdr) upd_region(a).ctr[1] = (int32_t)event_word(4, 0, 0, a.hdr->now, 0, false, false);
   if (i >= upd_n(a)) return;
   const ReqRec& r = a.req[i];
   if (r.slot >= 0 && row_owned(r, *a.cfg)) dedup_insert(upd_region(a), r.slot, i);

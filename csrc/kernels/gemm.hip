@@ -192,59 +192,97 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs a) {
 }
 
 // Fused dense + N==1 head: y[r] = act2( sum_n act1(x[r] . W1[n] + b1[n]) * w2[n] + b2 ).
-// 64 rows per block; the block's A tile (64 x K_pad bf16) is staged in LDS once, W1 fragments
-// stream from L2 (W1 is tiny and shared by every block); the 64 x N1 hidden tile lives only
-// in accumulators: bias + act1 + w2-weighting happen in registers, rows are reduced across
-// lanes (xor shuffles) and across the two column-waves through LDS.
-__global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a) {
+// 32 rows per block (8192 rows -> 256 blocks, one per CU); the A tile (32 x K_pad bf16) and,
+// when it fits, all of W1 (N1_pad x K_pad bf16) are staged in LDS once, so the MFMA loop reads
+// only LDS. The four waves split each 64-column chunk of the hidden layer (16 columns each);
+// the 32 x N1 hidden tile lives only in accumulators: bias + act1 + w2-weighting happen in
+// registers, rows are reduced across lanes (xor shuffles) and across the waves through LDS.
+constexpr int HD_ROWS = 32;
+constexpr int HD_W_LDS_MAX = 64 * 1024;  // W1 staged in LDS up to this many bytes
+
+__device__ __forceinline__ uint4 head_a_chunk(const HeadArgs& a, int row, int kc, int M) {
+  if (row >= M) return make_uint4(0, 0, 0, 0);
+  float f[8];
+  if (a.partial) {
+    // reduce the tree ensemble's group partials: sum_g P[g][row][k] (+ base, / T)
+    if (kc + 8 <= a.K && (a.K & 3) == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = 0.f;
+      for (int g = 0; g < a.groups; ++g) {
+        const float4* src = reinterpret_cast<const float4*>(a.partial + ((size_t)g * a.M + row) * a.K + kc);
+        const float4 p = src[0], q = src[1];
+        f[0] += p.x; f[1] += p.y; f[2] += p.z; f[3] += p.w; f[4] += q.x; f[5] += q.y; f[6] += q.z; f[7] += q.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = 0.f;
+        if (kc + j < a.K)
+          for (int g = 0; g < a.groups; ++g) v += a.partial[((size_t)g * a.M + row) * a.K + kc + j];
+        f[j] = v;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = kc + j;
+      if (k < a.K) {
+        if (a.p_average) f[j] /= (float)a.p_ntrees;
+        if (a.pbase) f[j] += a.pbase[k];
+      } else {
+        f[j] = 0.f;
+      }
+    }
+  } else if (a.x_bf16) {
+    const uint16_t* src = reinterpret_cast<const uint16_t*>(a.X) + (size_t)row * a.ldx + kc;
+    uint16_t t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = (kc + j < a.K) ? src[j] : 0;
+    return make_uint4(t[0] | (t[1] << 16), t[2] | (t[3] << 16), t[4] | (t[5] << 16), t[6] | (t[7] << 16));
+  } else {
+    const float* src = reinterpret_cast<const float*>(a.X) + (size_t)row * a.ldx + kc;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (kc + j < a.K) ? src[j] : 0.f;
+  }
+  return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
+                    pack_bf16x2(f[6], f[7]));
+}
+
+__global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a, int w_lds) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int kp = a.k_pad;
   const int lds_row = kp + G_PAD;
+  const int n1p = (a.N1 + 63) & ~63;
   uint16_t* sA = reinterpret_cast<uint16_t*>(smem);
-  float* sred = reinterpret_cast<float*>(smem + (((size_t)64 * lds_row * 2 + 15) & ~size_t(15)));
+  uint16_t* sW = sA + HD_ROWS * lds_row;
+  float* sred = reinterpret_cast<float*>(smem + (((size_t)(HD_ROWS + (w_lds ? n1p : 0)) * lds_row * 2 + 15) &
+                                                 ~size_t(15)));
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
   const int M = a.m_ptr ? min(*a.m_ptr, a.M) : a.M;
-  const int row0 = blockIdx.x * 64;
+  const int row0 = blockIdx.x * HD_ROWS;
   if (row0 >= M) return;
-  // stage A: 64 rows x kp (f32 or bf16 -> bf16), zero-padded past K and M
-  for (int ch = tid; ch < 64 * (kp / 8); ch += 256) {
-    const int r = ch / (kp / 8), kc = (ch % (kp / 8)) * 8;
-    const int row = row0 + r;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (row < M && a.partial) {
-      // reduce the tree ensemble's group partials: sum_g P[g][row][k] (+ base, / T)
-      float f[8];
+  const int kch = kp / 8;  // 16-byte chunks per row
+  // stage W1 (all loads of a thread in flight before its stores) and the A tile
+  if (w_lds) {
+    constexpr int UN = 4;
+    const int total = n1p * kch;
+    for (int base = 0; base < total; base += 256 * UN) {
+      uint4 v[UN];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = kc + j;
-        float s = 0.f;
-        if (k < a.K) {
-          for (int g = 0; g < a.groups; ++g) s += a.partial[((size_t)g * a.M + row) * a.K + k];
-          if (a.p_average) s /= (float)a.p_ntrees;
-          if (a.pbase) s += a.pbase[k];
-        }
-        f[j] = s;
+      for (int u = 0; u < UN; ++u) {
+        const int ch = base + u * 256 + tid;
+        v[u] = ch < total ? *reinterpret_cast<const uint4*>(a.W1 + (size_t)(ch / kch) * kp + (ch % kch) * 8)
+                          : make_uint4(0, 0, 0, 0);
       }
-      v = make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
-                     pack_bf16x2(f[6], f[7]));
-    } else if (row < M) {
-      if (a.x_bf16) {
-        const uint16_t* src = reinterpret_cast<const uint16_t*>(a.X) + (size_t)row * a.ldx + kc;
-        uint16_t t[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) t[j] = (kc + j < a.K) ? src[j] : 0;
-        v = make_uint4(t[0] | (t[1] << 16), t[2] | (t[3] << 16), t[4] | (t[5] << 16), t[6] | (t[7] << 16));
-      } else {
-        const float* src = reinterpret_cast<const float*>(a.X) + (size_t)row * a.ldx + kc;
-        float f[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = (kc + j < a.K) ? src[j] : 0.f;
-        v = make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
-                       pack_bf16x2(f[6], f[7]));
+      for (int u = 0; u < UN; ++u) {
+        const int ch = base + u * 256 + tid;
+        if (ch < total) *reinterpret_cast<uint4*>(&sW[(ch / kch) * lds_row + (ch % kch) * 8]) = v[u];
       }
     }
-    *reinterpret_cast<uint4*>(&sA[r * lds_row + kc]) = v;
+  }
+  for (int ch = tid; ch < HD_ROWS * kch; ch += 256) {
+    const int r = ch / kch, kc = (ch % kch) * 8;
+    *reinterpret_cast<uint4*>(&sA[r * lds_row + kc]) = head_a_chunk(a, row0 + r, kc, M);
   }
   __syncthreads();
   float part[2][4];
@@ -253,41 +291,27 @@ __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) part[i][q] = 0.f;
   for (int c0 = 0; c0 < a.N1; c0 += 64) {
-    f32x4 acc[2][2];
+    const int n = c0 + wave * 16 + (lane & 15);  // this lane's B-fragment column
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    for (int k0 = 0; k0 < kp; k0 += 32) {
+      const int kof = k0 + 8 * (lane >> 4);
+      const bf16x8 fb = w_lds ? *reinterpret_cast<const bf16x8*>(&sW[n * lds_row + kof])
+                              : *reinterpret_cast<const bf16x8*>(a.W1 + (size_t)n * kp + kof);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bf16x8 fa = *reinterpret_cast<const bf16x8*>(&sA[(i * 16 + (lane & 15)) * lds_row + kof]);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[i], 0, 0, 0);
+      }
+    }
+    const bool ok = n < a.N1;
+    const float b1 = ok && a.b1 ? a.b1[n] : 0.f;
+    const float w2 = ok ? a.w2[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < kp; k0 += 32) {
-      const int kof = k0 + 8 * (lane >> 4);
-      bf16x8 fa[2], fb[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        fa[i] = *reinterpret_cast<const bf16x8*>(&sA[(wm * 32 + i * 16 + (lane & 15)) * lds_row + kof]);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = c0 + wn * 32 + j * 16 + (lane & 15);
-        fb[j] = *reinterpret_cast<const bf16x8*>(a.W1 + (size_t)n * kp + kof);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = c0 + wn * 32 + j * 16 + (lane & 15);
-      const bool ok = col < a.N1;
-      const float b1 = ok && a.b1 ? a.b1[col] : 0.f;
-      const float w2 = ok ? a.w2[col] : 0.f;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) part[i][q] += act_fn(acc[i][j][q] + b1, a.act1) * w2;
-    }
+      for (int q = 0; q < 4; ++q) part[i][q] += act_fn(acc[i][q] + b1, a.act1) * w2;
   }
-  // reduce over the 16 lanes that share rows (lane & 15 differs)
+  // reduce over the 16 lanes that share rows (lane & 15 = column), then over the 4 waves
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -303,22 +327,26 @@ __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) sred[wn * 64 + wm * 32 + i * 16 + (lane >> 4) * 4 + q] = part[i][q];
+      for (int q = 0; q < 4; ++q) sred[wave * HD_ROWS + i * 16 + (lane >> 4) * 4 + q] = part[i][q];
   }
   __syncthreads();
-  if (tid < 64) {
+  if (tid < HD_ROWS) {
     const int row = row0 + tid;
     if (row < M) {
-      const float v = act_fn(sred[tid] + sred[64 + tid] + a.b2, a.act2);
-      a.Y[(size_t)row * a.ldy] = v;
+      const float v = sred[tid] + sred[HD_ROWS + tid] + sred[2 * HD_ROWS + tid] + sred[3 * HD_ROWS + tid];
+      a.Y[(size_t)row * a.ldy] = act_fn(v + a.b2, a.act2);
     }
   }
 }
 
 void launch_mlp_head(const HeadArgs& a, hipStream_t st) {
   if (a.M <= 0) return;
-  const size_t lds = (((size_t)64 * (a.k_pad + G_PAD) * 2 + 15) & ~size_t(15)) + 128 * sizeof(float);
-  hipLaunchKernelGGL(mlp_head_kernel, dim3((a.M + 63) / 64), dim3(256), lds, st, a);
+  const size_t lds_row = (size_t)a.k_pad + G_PAD;
+  const size_t n1p = (size_t)((a.N1 + 63) & ~63);
+  const int w_lds = n1p * lds_row * 2 <= (size_t)HD_W_LDS_MAX;
+  const size_t lds = ((((size_t)HD_ROWS + (w_lds ? n1p : 0)) * lds_row * 2 + 15) & ~size_t(15)) +
+                     4 * HD_ROWS * sizeof(float);
+  hipLaunchKernelGGL(mlp_head_kernel, dim3((a.M + HD_ROWS - 1) / HD_ROWS), dim3(256), lds, st, a, w_lds);
 }
 
 void launch_gemm(const GemmArgs& a, hipStream_t st) {

@@ -55,6 +55,7 @@ struct AssembleArgs {
   const uint32_t* bl_exp;
   const uint64_t* ip_keys;  // ip-intel table (nullable)
   const uint32_t* ip_flags;
+  const int32_t* hll_lc;    // [257]: floor(256 ln(256 / v) + 0.5), HLL linear counting by zero count v
   float* X;                 // [n_rows][x_stride]
   FeatRec* feat;            // [n_rows]
   int32_t* dbuf;            // dedup regions (nullable: no score-then-update)

@@ -82,43 +82,48 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
   const size_t node_b = ((size_t)trees_per_group * n_int * 8 + 15) & ~size_t(15);
   uint16_t* sleaf = reinterpret_cast<uint16_t*>(smem + base_b + (nodes_in_lds ? node_b : 0));
 
-  // stage the X tile: all global loads of a thread are issued before its LDS stores
-  // (8 independent loads in flight instead of a load->store round trip per element)
-  {
-    constexpr int UN = 8;
-    const int total = TR_ROWS * feat_w;
-    for (int base = 0; base < total; base += 256 * UN) {
-      float v[UN];
-#pragma unroll
-      for (int u = 0; u < UN; ++u) {
-        const int e = base + u * 256 + tid;
-        const int r = e / feat_w, c = e - r * feat_w;
-        const int row = row0 + r;
-        v[u] = (e < total && row < a.n_rows) ? a.X[(size_t)row * a.x_stride + c] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < UN; ++u) {
-        const int e = base + u * 256 + tid;
-        const int r = e / feat_w, c = e - r * feat_w;
-        if (e < total) sx[r * xs + c] = v[u];
-      }
-    }
-  }
+  // stage the X tile and the group's node table: the first chunk of both is loaded with every
+  // load of a thread in flight (one memory round trip instead of one per chunk), then stored
   const float2* gn = a.nodes + (size_t)t0 * n_int;
-  if (nodes_in_lds) {
-    constexpr int UN = 8;
-    const int total = nt * n_int;
-    for (int base = 0; base < total; base += 256 * UN) {
-      float2 v[UN];
+  {
+    constexpr int UX = 32, UN = 16;
+    const int xt = TR_ROWS * feat_w;
+    const int ntot = nodes_in_lds ? nt * n_int : 0;
+    // element e = xb + u*256 + tid of the row-major [64][feat_w] tile: (r, c) advanced
+    // incrementally (no per-element integer division)
+    const int dr = 256 / feat_w, dc = 256 % feat_w;
+    for (int xb = 0, nb = 0; xb < xt || nb < ntot; xb += 256 * UX, nb += 256 * UN) {
+      float v[UX];
+      float2 w[UN];
+      int rr[UX], cc[UX];
+      {
+        int r = (xb + tid) / feat_w, c = (xb + tid) - r * feat_w;
 #pragma unroll
-      for (int u = 0; u < UN; ++u) {
-        const int e = base + u * 256 + tid;
-        v[u] = e < total ? gn[e] : make_float2(0.f, 0.f);
+        for (int u = 0; u < UX; ++u) {
+          rr[u] = r;
+          cc[u] = c;
+          r += dr;
+          c += dc;
+          if (c >= feat_w) { c -= feat_w; ++r; }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UX; ++u) {
+        const int row = row0 + rr[u];
+        v[u] = (rr[u] < TR_ROWS && row < a.n_rows) ? a.X[(size_t)row * a.x_stride + cc[u]] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < UN; ++u) {
-        const int e = base + u * 256 + tid;
-        if (e < total) sn[e] = v[u];
+        const int e = nb + u * 256 + tid;
+        w[u] = e < ntot ? gn[e] : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < UX; ++u)
+        if (rr[u] < TR_ROWS) sx[rr[u] * xs + cc[u]] = v[u];
+#pragma unroll
+      for (int u = 0; u < UN; ++u) {
+        const int e = nb + u * 256 + tid;
+        if (e < ntot) sn[e] = w[u];
       }
     }
   }
@@ -175,29 +180,46 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
     constexpr int SPP = 256 / K;  // samples per pass
     const int k = tid % K, sp = tid / K;
     const bool rowwise = !partial && (a.post == 2 || a.binary_class >= 0);
-    for (int r = sp; r < TR_ROWS; r += SPP) {
-      const uint16_t* li = sleaf + r * nt;
-      float v = 0.f;
-      int t = 0;
-      for (; t + 8 <= nt; t += 8) {  // 8 leaf-row loads in flight per lane
-        float p[8];
+    // each thread owns target k of rows sp, sp + SPP, ...: all its rows advance through the
+    // trees together, so every step has RPT x 4 independent leaf loads in flight (the loads are
+    // L2 hits; the step count, not bandwidth, sets the time). Per row the trees are still
+    // summed in order t0, t0+1, ...
+    constexpr int RPT = TR_ROWS / SPP;  // rows per thread
+    float v[RPT];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) p[u] = a.leaves[((size_t)(t0 + t + u) * n_leaf + li[t + u]) * K + k];
+    for (int j = 0; j < RPT; ++j) v[j] = 0.f;
+    const float* lk = a.leaves + (size_t)t0 * n_leaf * K + k;  // 32-bit offsets below (SGPR base)
+    constexpr int TU = RPT >= 8 ? 4 : 8;  // trees per step: RPT x TU loads in flight
+    for (int t = 0; t < nt; t += TU) {
+      float p[RPT][TU];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v += p[u];
+      for (int j = 0; j < RPT; ++j) {
+        const uint16_t* li = sleaf + (sp + j * SPP) * nt;
+#pragma unroll
+        for (int u = 0; u < TU; ++u)
+          p[j][u] = (t + u < nt) ? lk[((t + u) * n_leaf + (int)li[t + u]) * K] : 0.f;
       }
-      for (; t < nt; ++t) v += a.leaves[((size_t)(t0 + t) * n_leaf + li[t]) * K + k];
+#pragma unroll
+      for (int j = 0; j < RPT; ++j)
+#pragma unroll
+        for (int u = 0; u < TU; ++u)
+          if (t + u < nt) v[j] += p[j][u];
+    }
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      const int r = sp + j * SPP;
       const int row = row0 + r;
+      float vv = v[j];
       if (row >= a.n_rows) continue;
       if (partial) {
-        partial[((size_t)g * a.n_rows + row) * K + k] = v;
+        partial[((size_t)g * a.n_rows + row) * K + k] = vv;
       } else if (rowwise) {
-        red[r * K + k] = v;
+        red[r * K + k] = vv;
       } else {
-        if (a.average) v /= (float)a.n_trees;
-        if (a.base) v += a.base[k];
-        if (a.post == 1) v = 1.f / (1.f + expf(-v));
-        a.out[(size_t)row * a.n_out + k] = v;
+        if (a.average) vv /= (float)a.n_trees;
+        if (a.base) vv += a.base[k];
+        if (a.post == 1) vv = 1.f / (1.f + expf(-vv));
+        a.out[(size_t)row * a.n_out + k] = vv;
       }
     }
     if (!rowwise) return;

@@ -27,6 +27,7 @@ from typing import Dict, Optional
 import numpy as np
 
 from ..config import FeatureConfig
+from ..golden.hll import linear_count as hll_linear_count
 from ..layouts import ACCTBATCH, ACCTRT
 from .tables import Blacklist, IPIntel
 
@@ -74,6 +75,9 @@ class DeviceFeatureStore:
         self.ip_flags = torch.zeros(self.ipintel.table.cap, dtype=torch.int32, **z)
         self._bl_version = -1
         self._ip_version = -1
+        # HLL linear-counting table floor(m ln(m / V) + 0.5), V = zero registers (golden/hll.py)
+        self.hll_lc = torch.tensor([0] + [hll_linear_count(v) for v in range(1, 257)], dtype=torch.int32,
+                                   device=self.device)
         self.max_events = int(max_events)
         # dedup scratch for ordered score-then-update: scorer ring regions + standalone
         self.dmax = self.max_events

@@ -36,6 +36,11 @@ def add(regs: bytearray, h: int) -> None:
         regs[idx] = r
 
 
+def linear_count(v: int) -> int:
+    """Linear-counting estimate for ``v`` zero registers (the device reads a table of these)."""
+    return int(math.floor(M * math.log(M / v) + 0.5))
+
+
 def count(regs) -> int:
     z = 0.0
     v = 0

@@ -79,6 +79,7 @@ def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch
         batch=_need(store.batch, "batch", torch.int32), ext=_need(store.ext, "ext", torch.float32),
         bl_keys=_need(store.bl_keys, "bl_keys", torch.int64), bl_exp=_need(store.bl_exp, "bl_exp", torch.int32),
         ip_keys=_need(store.ip_keys, "ip_keys", torch.int64), ip_flags=_need(store.ip_flags, "ip_flags", torch.int32),
+        hll_lc=_need(store.hll_lc, "hll_lc", torch.int32, 257),
         X=_need(X, "X", torch.float32, X.shape[1] * n_rows, dev),
         feat=_need(feat, "feat", torch.int32, 32 * n_rows, dev),
         dbuf=_need(store.dbuf, "dbuf", torch.int32) if dedup else None, dcap=int(store.dcap), dmax=int(store.dmax),
@@ -161,6 +162,8 @@ def tree_ensemble(tp, X: torch.Tensor, out: Optional[torch.Tensor], n_rows: int,
         raise ValueError("node table smaller than n_trees * (2^depth - 1)")
     if tp.leaves.numel() < tp.n_trees * (1 << tp.depth) * tp.k:
         raise ValueError("leaf table smaller than n_trees * 2^depth * K")
+    if tp.n_trees * (1 << tp.depth) * tp.k >= 2 ** 31:
+        raise ValueError("leaf table too large for the kernel's 32-bit offsets")
     _mod().tree_ensemble(d, _stream())
 
 
