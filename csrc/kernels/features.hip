@@ -21,34 +21,62 @@ __constant__ float k1_hi[32] = {20.f, 50.f, 200.f, 1.f, 1.f, 10.f, 20.f, 1.f, 1.
 __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h, int c, int s, AcctRT r,
                                    int lane);
 
-// PFADD on a register file held one uint32 (4 registers) per lane: the owner lane of the
-// register updates and stores its word; an expired key (TTL) is rewritten as zeros first.
-__device__ __forceinline__ bool hll_add_wave(uint32_t* words, uint32_t w, uint32_t& exp, uint64_t h, int64_t now,
-                                             int ttl, int lane) {
-  const bool reset = now >= (int64_t)exp;
-  if (reset) w = 0u;
-  const int idx = (int)(h & 255u);
-  const int rank = hll_rank(h);
-  const int sh = 8 * (idx & 3);
-  const bool mine = lane == (idx >> 2) && rank > (int)((w >> sh) & 0xffu);
-  if (mine) w = (w & ~(0xffu << sh)) | ((uint32_t)rank << sh);
-  if (reset || mine) words[lane] = w;
-  exp = (uint32_t)(now + ttl);
-  return __ballot(mine) != 0ull;
+// K1 runs one request per 16-lane quarter of a wave (4 requests per wave, 16 per block): the
+// per-request work is either 16-wide (tx ring, HLL registers, model inputs, ext row) or scalar
+// (features, rules, update bookkeeping), and scalar work computed on a quarter instead of a
+// whole wave takes a quarter of the VALU issue slots. Reductions / ballots stay inside the
+// quarter (xor shuffles 1..8, ballot bits of the quarter).
+constexpr int K1_QL = 16;  // lanes per request
+
+__device__ __forceinline__ uint32_t qballot(bool p, int qb) { return (uint32_t)(__ballot(p) >> qb) & 0xffffu; }
+
+template <class T>
+__device__ __forceinline__ T qsum(T v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  return v;
 }
 
-// apply_event (update.h) spread over a wave that already holds the account's AcctRT (uniform)
-// and HLL registers (wd / wi: 4 per lane); same arithmetic, same stored bytes. The event row
-// is built by lanes 0..7 (one word each) with a single double log1p pass (lane 0: amount,
-// lane 3: dt) and the batch's precomputed hour-of-day word `hour_word`.
-__device__ __forceinline__ void apply_event_wave(const UpdateArgs& a, const ReqRec& ev, AcctRT r, uint32_t wd,
-                                                 uint32_t wi, int lane, uint32_t hour_word) {
+__device__ __forceinline__ uint32_t pick4(const uint32_t (&w)[4], int i) {
+  return i == 0 ? w[0] : i == 1 ? w[1] : i == 2 ? w[2] : w[3];
+}
+
+// PFADD on a register file held as 4 words (16 registers) per lane of a quarter: lane ql holds
+// words ql + 16 i. The owner lane of the register updates and stores its word; an expired key
+// (TTL) is rewritten as zeros first. Returns whether the register rose (golden new_device).
+__device__ __forceinline__ bool hll_add_q(uint32_t* words, const uint32_t (&w)[4], uint32_t& exp, uint64_t h,
+                                          int64_t now, int ttl, int ql, int qb) {
+  const bool reset = now >= (int64_t)exp;
+  const int idx = (int)(h & 255u);
+  const int rank = hll_rank(h);
+  const int wix = idx >> 2, sh = 8 * (idx & 3);
+  const bool own = ql == (wix & 15);
+  uint32_t cur = reset ? 0u : pick4(w, wix >> 4);
+  const bool mine = own && rank > (int)((cur >> sh) & 0xffu);
+  if (reset) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) words[ql + 16 * i] = 0u;
+  }
+  if (mine) words[wix] = (cur & ~(0xffu << sh)) | ((uint32_t)rank << sh);
+  exp = (uint32_t)(now + ttl);
+  return qballot(mine, qb) != 0u;
+}
+
+// apply_event (update.h) by the 16 lanes of a quarter that already hold the account's AcctRT
+// and HLL registers; same arithmetic, same stored bytes. The event row is built by lanes 0..7
+// (one word each) with a single double log1p pass (lane 0: amount, lane 3: dt) and the
+// batch's precomputed hour-of-day word `hour_word` (dedup_insert_kernel).
+__device__ __forceinline__ void apply_event_q(const UpdateArgs& a, const ReqRec& ev, AcctRT r,
+                                              const uint32_t (&wd)[4], const uint32_t (&wi)[4], int ql, int qb,
+                                              uint32_t hour_word) {
   const int s = ev.slot;
   const int64_t now = event_ts(a, ev);
   const ScoreCfg& cfg = *a.cfg;
   const int64_t amt = ev.amount;
   const int hd = r.ring_head;
-  if (lane == 0) {
+  if (ql == 0) {
     a.ring_ts[(size_t)s * a.ring_size + hd] = (uint32_t)now;
     a.ring_amt[(size_t)s * a.ring_size + hd] = amt;
   }
@@ -58,8 +86,8 @@ __device__ __forceinline__ void apply_event_wave(const UpdateArgs& a, const ReqR
   r.sum_exp = (uint32_t)(now + cfg.sum_ttl);
   uint32_t* regs = reinterpret_cast<uint32_t*>(a.hll + (size_t)s * 512);
   bool new_dev = false, new_ip = false;
-  if (ev.dev_hash) new_dev = hll_add_wave(regs, wd, r.hll_dev_exp, ev.dev_hash, now, cfg.hll_ttl, lane);
-  if (ev.ip_hash) new_ip = hll_add_wave(regs + 64, wi, r.hll_ip_exp, ev.ip_hash, now, cfg.hll_ttl, lane);
+  if (ev.dev_hash) new_dev = hll_add_q(regs, wd, r.hll_dev_exp, ev.dev_hash, now, cfg.hll_ttl, ql, qb);
+  if (ev.ip_hash) new_ip = hll_add_q(regs + 64, wi, r.hll_ip_exp, ev.ip_hash, now, cfg.hll_ttl, ql, qb);
   r.last_tx = (uint32_t)now;
   r.last_tx_exp = (uint32_t)(now + cfg.last_tx_ttl);
   if (now >= (int64_t)r.session_exp || r.session_start == 0) r.session_start = (uint32_t)now;
@@ -69,9 +97,9 @@ __device__ __forceinline__ void apply_event_wave(const UpdateArgs& a, const ReqR
     const int tt = ev.tx_type & 0xff;
     const int64_t prev = (int64_t)r.last_event_ts;
     const int64_t dt = (prev > 0 && now >= prev) ? now - prev : 0;
-    const double l = log1p(lane == 0 ? (double)(amt > 0 ? amt : 0) : (double)dt);
+    const double l = log1p(ql == 0 ? (double)(amt > 0 ? amt : 0) : (double)dt);
     float lo = 0.f, hi = 0.f;
-    switch (lane) {  // bf16 pairs of golden.features.encode_event (update.h event_word)
+    switch (ql) {  // bf16 pairs of golden.features.encode_event (update.h event_word)
       case 0: lo = (float)(l / 16.0); hi = tt == 0; break;
       case 1: lo = tt == 1; hi = tt == 2; break;
       case 2: lo = tt == 3; hi = tt == 4; break;
@@ -80,43 +108,56 @@ __device__ __forceinline__ void apply_event_wave(const UpdateArgs& a, const ReqR
       case 6: lo = amt >= 100000; hi = 1.f; break;
       default: break;
     }
-    const uint32_t w = lane == 4 ? hour_word : ((uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16));
-    if (lane < 8) e[lane] = w;
+    const uint32_t w = ql == 4 ? hour_word : ((uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16));
+    if (ql < 8) e[ql] = w;
     r.ev_head = r.ev_head + 1 == a.ev_ring ? 0 : r.ev_head + 1;
     r.ev_count = r.ev_count + 1 > a.ev_ring ? a.ev_ring : r.ev_count + 1;
   }
   r.last_event_ts = (uint32_t)now;
-  if (lane == 0) a.rt[s] = r;
+  if (ql == 0) a.rt[s] = r;
 }
 
-__device__ __forceinline__ void clear_next_dedup(const AssembleArgs& a, int row, int seq, int lane) {
-  if (a.dbuf) {  // clear this wave's slice of batch seq+2's dedup region (after every load:
-                 // no store precedes the account loads, so uniform ones can go scalar)
+// clear this request's slice of batch seq+2's dedup region (after the request's loads)
+__device__ __forceinline__ void clear_next_dedup(const AssembleArgs& a, int row, int seq, int ql) {
+  if (a.dbuf) {
     const DedupTab nt = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq + 2));
     const int chunk = (a.dcap + a.n_rows - 1) / a.n_rows;
-    const int e0 = row * chunk;
-    dedup_clear_range(nt, e0, min(a.dcap, e0 + chunk), lane);
-    if (row == 0 && lane < 2) nt.ctr[lane] = 0;
+    const int e0 = row * chunk, e1 = min(a.dcap, e0 + chunk);
+    for (int e = e0 + ql; e < e1; e += K1_QL) {
+      nt.keys[e] = -1;
+      nt.first[e] = 0x7fffffff;
+      nt.count[e] = 0;
+      nt.fill[e] = 0;
+      nt.done[e] = 0;
+    }
+    if (row == 0 && ql < 2) nt.ctr[ql] = 0;
   }
 }
 
-// One wave64 per request. Every independent load is issued before the first use: the
-// 256-entry ts ring as one uint4 per lane (1 KiB/wave, coalesced), HLL registers (4 per
-// lane), the account rows (broadcast), the ext row, and the blacklist/ip-intel probes;
-// the 1h amounts are then fetched only for in-window entries (predicated, issued together).
-// Score-then-update: dedup_insert_kernel registered the batch first; a wave whose account has
-// no other event in the batch applies the event itself once its reads are done (AcctRT and
-// the HLL registers are already in registers), and every wave clears a slice of the other
-// parity's dedup table for the next batch after its loads.
+// inert row (graph padding / another rank's request): zero inputs, FeatRec with slot -1
+__device__ __forceinline__ void inert_row(const AssembleArgs& a, float* xr, int row, int ql, int ext_w, int flag) {
+  for (int j = ql; j < 30 + ext_w; j += K1_QL) xr[j] = 0.f;
+  int32_t* fr = reinterpret_cast<int32_t*>(a.feat + row);
+  fr[ql] = ql == 3 ? flag : 0;
+  fr[ql + 16] = ql + 16 == 27 ? -1 : 0;
+}
+
+// Loads are organised in two dependency levels (under a full grid each dependent global-load
+// level costs microseconds): level 1 = the request row + batch header + config words; level 2
+// = everything the row addresses (ts ring, amounts, HLL registers, account rows, ext row, dedup
+// probe, blacklist / ip-intel first probe slot), issued branch-free before the first use.
+// Score-then-update: dedup_insert_kernel registered the batch first; a request whose account
+// has no other event in the batch applies its event right after its own reads; for a
+// multi-event account the last request to finish its reads applies the account's events in
+// row order, with the whole wave, after every quarter of the wave is done.
 __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
   const int lane = threadIdx.x & 63;
-  const int row = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (row >= a.n_rows) return;
+  const int ql = lane & 15, qb = lane & 48;
+  const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
+  const bool in_grid = row < a.n_rows;
   const ScoreCfg& cfg = *a.cfg;
-  // ---- dependency level 1: the request row and the batch header (independent loads). Under a
-  // full grid every dependent global-load level costs several microseconds, so the kernel is
-  // organised as two load levels: the row, then everything the row addresses.
-  const uint4* rp = reinterpret_cast<const uint4*>(a.req + as_vgpr(row));
+  // ---- level 1
+  const uint4* rp = reinterpret_cast<const uint4*>(a.req + as_vgpr(in_grid ? row : 0));
   const uint4 q0 = rp[0], q1 = rp[1], q2 = rp[2];
   ReqRec rq;
   rq.slot = (int32_t)q0.x;
@@ -131,281 +172,294 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
   // {ip_max_probe, ext_width, owner_filter, my_rank} (records.h; static_asserts there)
   const int4 c8 = reinterpret_cast<const int4*>(a.cfg)[8];
   const int4 c9 = reinterpret_cast<const int4*>(a.cfg)[9];
-  const int2 own = make_int2(c9.z, c9.w);
   const int ext_w = c9.y;
   const int n_live = hv.x;
   const int seq = hv.y;
   const int64_t now = (int64_t)(((uint64_t)(uint32_t)hv.w << 32) | (uint32_t)hv.z);
   float* xr = a.X + (size_t)row * a.x_stride;
-  if (row >= n_live) {  // padded row of a graph bucket: deterministic zeros
-    keep_issued((int)(q0.x ^ q0.z ^ q1.x ^ q1.z ^ q2.x ^ q2.z) ^ own.x);
-    clear_next_dedup(a, row, seq, lane);
-    for (int j = lane; j < 30 + ext_w; j += 64) xr[j] = 0.f;
-    if (lane < 32) reinterpret_cast<int32_t*>(a.feat + row)[lane] = (lane == 27) ? -1 : 0;
-    return;
+  const bool padded = in_grid && row >= n_live;
+  const bool foreign = in_grid && !padded && c9.z && ((rq.tx_type >> 8) & 0xff) != c9.w;
+  const bool live = in_grid && !padded && !foreign;
+  if (padded || foreign) {
+    inert_row(a, xr, row, ql, ext_w, foreign ? FR_NOT_OWNED : 0);
+    clear_next_dedup(a, row, seq, ql);
   }
-  if (own.x && ((rq.tx_type >> 8) & 0xff) != own.y) {  // another rank's request: inert row
-    clear_next_dedup(a, row, seq, lane);
-    for (int j = lane; j < 30 + ext_w; j += 64) xr[j] = 0.f;
-    if (lane < 32) reinterpret_cast<int32_t*>(a.feat + row)[lane] = (lane == 27) ? -1 : (lane == 3 ? FR_NOT_OWNED : 0);
-    return;
-  }
-  const int s = __builtin_amdgcn_readfirstlane(rq.slot);  // account rows go through SGPRs
-  const int64_t amount = rq.amount;
-  const int tx_type = rq.tx_type & 0xff;
-
-  // ---- dependency level 2: every load addressed by the row, branch-free (clamped addresses,
-  // results masked afterwards) so the compiler issues them back to back before the first use
-  const bool has = s >= 0;
-  const int sc = has ? s : 0;
-  const int rs = a.ring_size;  // multiple of 64; 256 = one uint4 of ts + 4 amounts per lane
-  const int rl = min(lane, rs / 4 - 1);
-  uint4 tsv = reinterpret_cast<const uint4*>(a.ring_ts + (size_t)sc * rs)[rl];
-  const longlong2* am2 = reinterpret_cast<const longlong2*>(a.ring_amt + (size_t)sc * rs);
-  const longlong2 am01 = am2[2 * rl], am23 = am2[2 * rl + 1];
-  const uint32_t* hreg = reinterpret_cast<const uint32_t*>(a.hll + (size_t)sc * 512);
-  uint32_t wd = hreg[lane], wi = hreg[64 + lane];
-  AcctRT rt = a.rt[sc];
-  AcctBatch bt = a.batch[sc];
-  const float* e = a.ext + (size_t)sc * ext_w;
-  float extv[2];  // ext widths up to 128 preloaded; wider rows finish in a loop at the end
+  int last = 0, h = -1, s = -1, dcount = 0;
+  if (live) {
+    s = rq.slot;
+    const int64_t amount = rq.amount;
+    const int tx_type = rq.tx_type & 0xff;
+    // ---- level 2 (clamped addresses, masked afterwards)
+    const bool has = s >= 0;
+    const int sc = has ? s : 0;
+    const int rs = a.ring_size;  // multiple of 64: lane ql holds entries 4 (ql + 16 i) .. +3
+    const int n4 = rs / 4;
+    const uint4* ts4 = reinterpret_cast<const uint4*>(a.ring_ts + (size_t)sc * rs);
+    const longlong2* am2 = reinterpret_cast<const longlong2*>(a.ring_amt + (size_t)sc * rs);
+    uint4 tsv[4];
+    longlong2 am[8];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) extv[u] = e[max(0, min(lane + 64 * u, ext_w - 1))];
-  // score-then-update: first probe of the batch's dedup entry
-  uint32_t dh = 0, hour_word = 0;
-  int dkey = -1, dfirst = -1, dcount = 0;
-  if (a.dbuf) {  // kernel-uniform
-    const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
-    dh = mix32((uint32_t)sc) & (uint32_t)(t.cap - 1);
-    dkey = t.keys[dh];
-    dfirst = t.first[dh];
-    dcount = t.count[dh];
-    hour_word = (uint32_t)t.ctr[1];
-  }
-  // K7: blacklist (lanes 0..2: device, fingerprint, ip) and IP intelligence (lane 3): the first
-  // probe slot's key and value are loaded with the rest, collisions walk on (rare)
-  uint64_t key = 0;
-  if (lane == 0) key = rq.dev_hash;
-  else if (lane == 1) key = rq.fp_hash;
-  else if (lane == 2 || lane == 3) key = rq.ip_hash;
-  const bool tabs = a.bl_keys && a.ip_keys;  // kernel-uniform
-  const bool bl_lane = tabs && lane < 3 && key != 0;
-  const bool ip_lane = tabs && lane == 3 && key != 0;
-  const uint64_t* pkeys = lane < 3 ? a.bl_keys : a.ip_keys;
-  const uint32_t* pvals = lane < 3 ? a.bl_exp : a.ip_flags;
-  const uint32_t pmask = (uint32_t)(lane < 3 ? c8.y : c8.w);
-  uint32_t pi = (bl_lane || ip_lane) ? ((uint32_t)key & pmask) : 0u;
-  uint64_t pk = 0;
-  uint32_t pv = 0;
-  if (tabs) {
-    pk = pkeys[pi];
-    pv = pvals[pi];
-  }
-  // ---- mask what a missing account / short ring must not see
-  if (!has) {
-    tsv = make_uint4(0, 0, 0, 0);
-    wd = wi = 0u;
-    rt = AcctRT{};
-    bt = AcctBatch{};
-    extv[0] = extv[1] = 0.f;
-    dkey = -1;
-  }
-  if (lane * 4 >= rs) tsv = make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < 4; ++i) {
+      const int e = min(ql + 16 * i, n4 - 1);
+      tsv[i] = ts4[e];
+      am[2 * i] = am2[2 * e];
+      am[2 * i + 1] = am2[2 * e + 1];
+    }
+    const uint32_t* hreg = reinterpret_cast<const uint32_t*>(a.hll + (size_t)sc * 512);
+    uint32_t wd[4], wi[4];
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
-    if (lane + 64 * u >= ext_w) extv[u] = 0.f;
-  bool hit = false;
-  int ipf = 0;
-  if (bl_lane || ip_lane) {
-    const int max_probe = lane < 3 ? c8.z : c9.x;
-    for (int p = 1; p < max_probe && pk != 0 && pk != key; ++p) {
-      pi = (pi + 1) & pmask;
+    for (int i = 0; i < 4; ++i) {
+      wd[i] = hreg[ql + 16 * i];
+      wi[i] = hreg[64 + ql + 16 * i];
+    }
+    AcctRT rt = a.rt[sc];
+    AcctBatch bt = a.batch[sc];
+    const float* e = a.ext + (size_t)sc * ext_w;
+    float extv[7];  // ext widths up to 112 preloaded; wider rows finish in a loop at the end
+#pragma unroll
+    for (int u = 0; u < 7; ++u) extv[u] = e[max(0, min(ql + 16 * u, ext_w - 1))];
+    uint32_t dh = 0, hour_word = 0;
+    int dkey = -1, dfirst = -1;
+    if (a.dbuf) {  // kernel-uniform
+      const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
+      dh = mix32((uint32_t)sc) & (uint32_t)(t.cap - 1);
+      dkey = t.keys[dh];
+      dfirst = t.first[dh];
+      dcount = t.count[dh];
+      hour_word = (uint32_t)t.ctr[1];
+    }
+    // K7: blacklist (lanes 0..2: device, fingerprint, ip) and IP intelligence (lane 3)
+    uint64_t key = 0;
+    if (ql == 0) key = rq.dev_hash;
+    else if (ql == 1) key = rq.fp_hash;
+    else if (ql == 2 || ql == 3) key = rq.ip_hash;
+    const bool tabs = a.bl_keys && a.ip_keys;  // kernel-uniform
+    const bool bl_lane = tabs && ql < 3 && key != 0;
+    const bool ip_lane = tabs && ql == 3 && key != 0;
+    const uint64_t* pkeys = ql < 3 ? a.bl_keys : a.ip_keys;
+    const uint32_t* pvals = ql < 3 ? a.bl_exp : a.ip_flags;
+    const uint32_t pmask = (uint32_t)(ql < 3 ? c8.y : c8.w);
+    uint32_t pi = (bl_lane || ip_lane) ? ((uint32_t)key & pmask) : 0u;
+    uint64_t pk = 0;
+    uint32_t pv = 0;
+    if (tabs) {
       pk = pkeys[pi];
       pv = pvals[pi];
     }
-    if (pk == key && max_probe > 0) {
-      if (bl_lane) hit = (pv == 0u) || (now < (int64_t)pv);
-      else ipf = (int)pv;
-    }
-  }
-  const bool blacklisted = __ballot(hit) != 0ull;
-  ipf = __shfl(ipf, 3, 64);
-
-  // ---- window counts / sums from the tx ring
-  int c1 = 0, c5 = 0, c60 = 0;
-  long long s60 = 0;
-  int hll_dev = 0, hll_ip = 0;
-  if (s >= 0) {
-    const int64_t* am = a.ring_amt + (size_t)s * rs;
-    const uint32_t tv[4] = {tsv.x, tsv.y, tsv.z, tsv.w};
-    bool in1h[4];
+    // ---- mask what a missing account / short ring must not see
+    if (!has) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t t = (int64_t)tv[q];
-      const bool v = t != 0;
-      c1 += v && t >= now - 60;
-      c5 += v && t >= now - 300;
-      in1h[q] = v && t >= now - 3600;
-      c60 += in1h[q];
+      for (int i = 0; i < 4; ++i) { tsv[i] = make_uint4(0, 0, 0, 0); wd[i] = wi[i] = 0u; }
+      rt = AcctRT{};
+      bt = AcctBatch{};
+#pragma unroll
+      for (int u = 0; u < 7; ++u) extv[u] = 0.f;
+      dkey = -1;
     }
-    const long long amv[4] = {in1h[0] ? am01.x : 0, in1h[1] ? am01.y : 0, in1h[2] ? am23.x : 0,
-                              in1h[3] ? am23.y : 0};
-    for (int q = 256 + lane; q < rs; q += 64) {  // rings longer than 256 entries (rare)
-      const int64_t t = (int64_t)a.ring_ts[(size_t)s * rs + q];
-      if (t != 0) {
-        c1 += t >= now - 60;
-        c5 += t >= now - 300;
-        if (t >= now - 3600) { ++c60; s60 += am[q]; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (ql + 16 * i >= n4) tsv[i] = make_uint4(0, 0, 0, 0);
+    bool hit = false;
+    int ipf = 0;
+    if (bl_lane || ip_lane) {
+      const int max_probe = ql < 3 ? c8.z : c9.x;
+      for (int p = 1; p < max_probe && pk != 0 && pk != key; ++p) {
+        pi = (pi + 1) & pmask;
+        pk = pkeys[pi];
+        pv = pvals[pi];
+      }
+      if (pk == key && max_probe > 0) {
+        if (bl_lane) hit = (pv == 0u) || (now < (int64_t)pv);
+        else ipf = (int)pv;
       }
     }
-    s60 += amv[0] + amv[1] + amv[2] + amv[3];
-    c1 = wave_sum(c1);
-    c5 = wave_sum(c5);
-    c60 = wave_sum(c60);
-    s60 = wave_sum(s60);
-    // ---- K8: HyperLogLog counts (p = 8; 4 registers per lane)
-    double zd = 0, zi = 0;
-    int vd = 0, vi = 0;
+    const bool blacklisted = qballot(hit, qb) != 0u;
+    ipf = __shfl(ipf, qb + 3, 64);
+
+    // ---- window counts / sums from the tx ring
+    int c1 = 0, c5 = 0, c60 = 0;
+    long long s60 = 0;
+    int hll_dev = 0, hll_ip = 0;
+    if (has) {
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int rd = (wd >> (8 * b)) & 0xff, ri = (wi >> (8 * b)) & 0xff;
-      zd += exp2_neg(rd); vd += rd == 0;
-      zi += exp2_neg(ri); vi += ri == 0;
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t tv[4] = {tsv[i].x, tsv[i].y, tsv[i].z, tsv[i].w};
+        const long long av[4] = {am[2 * i].x, am[2 * i].y, am[2 * i + 1].x, am[2 * i + 1].y};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t t = (int64_t)tv[j];
+          const bool v = t != 0;
+          c1 += v && t >= now - 60;
+          c5 += v && t >= now - 300;
+          const bool in1h = v && t >= now - 3600;
+          c60 += in1h;
+          s60 += in1h ? av[j] : 0;
+        }
+      }
+      const int64_t* amp = a.ring_amt + (size_t)s * rs;
+      for (int q = 256 + ql; q < rs; q += K1_QL) {  // rings longer than 256 entries (rare)
+        const int64_t t = (int64_t)a.ring_ts[(size_t)s * rs + q];
+        if (t != 0) {
+          c1 += t >= now - 60;
+          c5 += t >= now - 300;
+          if (t >= now - 3600) { ++c60; s60 += amp[q]; }
+        }
+      }
+      c1 = qsum(c1);
+      c5 = qsum(c5);
+      c60 = qsum(c60);
+      s60 = qsum(s60);
+      // ---- K8: HyperLogLog counts (p = 8; 16 registers per lane)
+      double zd = 0, zi = 0;
+      int vd = 0, vi = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int rd = (wd[i] >> (8 * b)) & 0xff, ri = (wi[i] >> (8 * b)) & 0xff;
+          zd += exp2_neg(rd); vd += rd == 0;
+          zi += exp2_neg(ri); vi += ri == 0;
+        }
+      zd = qsum(zd); zi = qsum(zi);
+      vd = qsum(vd); vi = qsum(vi);
+      // linear counting (E <= 2.5 m, V > 0): floor(m ln(m / V) + 0.5) from the host-computed
+      // table (libm log, as the golden model); otherwise the harmonic estimate
+      const double m = 256.0, alpha = 0.7213 / (1.0 + 1.079 / 256.0);
+      const double ed = alpha * m * m / zd, ei = alpha * m * m / zi;
+      const int ld = a.hll_lc[vd], li = a.hll_lc[vi];
+      const int cd = (ed <= 2.5 * m && vd > 0) ? ld : (int)floor(ed + 0.5);
+      const int ci = (ei <= 2.5 * m && vi > 0) ? li : (int)floor(ei + 0.5);
+      hll_dev = now < (int64_t)rt.hll_dev_exp ? cd : 0;
+      hll_ip = now < (int64_t)rt.hll_ip_exp ? ci : 0;
     }
-    zd = wave_sum(zd); zi = wave_sum(zi);
-    vd = wave_sum(vd); vi = wave_sum(vi);
-    // linear counting (E <= 2.5 m, V > 0): floor(m ln(m / V) + 0.5) from the host-computed
-    // table (libm log, as the golden model); otherwise the harmonic estimate
-    const double m = 256.0, alpha = 0.7213 / (1.0 + 1.079 / 256.0);
-    const double ed = alpha * m * m / zd, ei = alpha * m * m / zi;
-    const int ld = a.hll_lc[vd], li = a.hll_lc[vi];
-    const int cd = (ed <= 2.5 * m && vd > 0) ? ld : (int)floor(ed + 0.5);
-    const int ci = (ei <= 2.5 * m && vi > 0) ? li : (int)floor(ei + 0.5);
-    hll_dev = now < (int64_t)rt.hll_dev_exp ? cd : 0;
-    hll_ip = now < (int64_t)rt.hll_ip_exp ? ci : 0;
-  }
 
-  // ---- assemble raw features (wave-uniform values)
-  FeatRec f{};
-  f.tx_count_1m = c1;
-  f.tx_count_5m = c5;
-  f.tx_count_1h = c60;
-  f.tx_sum_1h = cfg.sum_compat ? ((s >= 0 && now < (int64_t)rt.sum_exp) ? rt.sum_compat : 0) : s60;
-  f.tx_avg_1h = c60 > 0 ? (float)((double)f.tx_sum_1h / (double)c60) : 0.f;
-  f.unique_devices_24h = hll_dev;
-  f.unique_ips_24h = hll_ip;
-  if (s >= 0) {
-    if (rt.last_tx > 0 && now < (int64_t)rt.last_tx_exp) f.time_since_last_tx = (int32_t)(now - (int64_t)rt.last_tx);
-    if (rt.session_start > 0 && now < (int64_t)rt.session_exp)
-      f.session_duration = (int32_t)(now - (int64_t)rt.session_start);
-  }
-  int flags = 0;
-  if (s >= 0 && bt.present) {
-    f.total_deposits = bt.total_deposits;
-    f.total_withdrawals = bt.total_withdrawals;
-    f.net_deposit = bt.total_deposits - bt.total_withdrawals;
-    f.deposit_count = bt.deposit_count;
-    f.withdraw_count = bt.withdraw_count;
-    f.avg_bet_size = bt.avg_bet_size;
-    f.account_age_days = (int32_t)((now - bt.account_created_at) / 86400);
-    f.bonus_claim_count = bt.bonus_claim_count;
-    f.bonus_wager_rate = bt.bonus_wager_complete;
-    if (bt.bet_count > 0) f.win_rate = (float)((double)bt.win_count / (double)bt.bet_count);
-    if (bt.bonus_claim_count > 3 && bt.total_deposits < 5000) flags |= FR_BONUS_ONLY;
-  } else {
-    flags |= FR_PARTIAL;
-  }
-  if (ipf & 1) flags |= FR_VPN;
-  if (ipf & 2) flags |= FR_PROXY;
-  if (ipf & 4) flags |= FR_TOR;
-  if (blacklisted) flags |= FR_BLACKLISTED;
-  f.flags = flags;
-  f.tx_type = tx_type;
-  f.slot = s;
-  f.amount = amount;
-
-  // ---- rule pass (engine.go:420-483), raw features
-  int score = 0;
-  uint32_t reasons = 0;
-  if (f.tx_count_1m > cfg.max_tx_per_minute) { score += cfg.w_high_velocity; reasons |= 1u << 0; }
-  if (f.account_age_days < cfg.new_account_days && amount > cfg.large_deposit_amount) {
-    score += cfg.w_new_account_large_tx; reasons |= 1u << 1;
-  }
-  if (f.unique_devices_24h > cfg.max_devices_per_day) { score += cfg.w_multiple_devices; reasons |= 1u << 2; }
-  if (f.unique_ips_24h > cfg.max_ips_per_day) { score += cfg.w_ip_country_mismatch; reasons |= 1u << 3; }
-  if (flags & (FR_VPN | FR_PROXY | FR_TOR)) { score += cfg.w_vpn; reasons |= 1u << 4; }
-  if (f.time_since_last_tx < 300 && tx_type == TX_WITHDRAW) {
-    if (f.deposit_count > 0 && f.total_withdrawals > f.total_deposits * 80 / 100) {
-      score += cfg.w_rapid_deposit_withdraw; reasons |= 1u << 5;
+    // ---- assemble raw features (quarter-uniform values)
+    FeatRec f{};
+    f.tx_count_1m = c1;
+    f.tx_count_5m = c5;
+    f.tx_count_1h = c60;
+    f.tx_sum_1h = cfg.sum_compat ? ((has && now < (int64_t)rt.sum_exp) ? rt.sum_compat : 0) : s60;
+    f.tx_avg_1h = c60 > 0 ? (float)((double)f.tx_sum_1h / (double)c60) : 0.f;
+    f.unique_devices_24h = hll_dev;
+    f.unique_ips_24h = hll_ip;
+    if (has) {
+      if (rt.last_tx > 0 && now < (int64_t)rt.last_tx_exp) f.time_since_last_tx = (int32_t)(now - (int64_t)rt.last_tx);
+      if (rt.session_start > 0 && now < (int64_t)rt.session_exp)
+        f.session_duration = (int32_t)(now - (int64_t)rt.session_start);
     }
-  }
-  if (flags & FR_BONUS_ONLY) { score += cfg.w_bonus_abuse; reasons |= 1u << 6; }
-  if (blacklisted) { score += cfg.w_known_fraudster; reasons |= 1u << 7; }
-  f.reserved0 = (int32_t)reasons;
-  f.reserved1 = score > 100 ? 100 : score;
+    int flags = 0;
+    if (has && bt.present) {
+      f.total_deposits = bt.total_deposits;
+      f.total_withdrawals = bt.total_withdrawals;
+      f.net_deposit = bt.total_deposits - bt.total_withdrawals;
+      f.deposit_count = bt.deposit_count;
+      f.withdraw_count = bt.withdraw_count;
+      f.avg_bet_size = bt.avg_bet_size;
+      f.account_age_days = (int32_t)((now - bt.account_created_at) / 86400);
+      f.bonus_claim_count = bt.bonus_claim_count;
+      f.bonus_wager_rate = bt.bonus_wager_complete;
+      if (bt.bet_count > 0) f.win_rate = (float)((double)bt.win_count / (double)bt.bet_count);
+      if (bt.bonus_claim_count > 3 && bt.total_deposits < 5000) flags |= FR_BONUS_ONLY;
+    } else {
+      flags |= FR_PARTIAL;
+    }
+    if (ipf & 1) flags |= FR_VPN;
+    if (ipf & 2) flags |= FR_PROXY;
+    if (ipf & 4) flags |= FR_TOR;
+    if (blacklisted) flags |= FR_BLACKLISTED;
+    f.flags = flags;
+    f.tx_type = tx_type;
+    f.slot = s;
+    f.amount = amount;
 
-  // ---- writes: the 30 normalised inputs spread over lanes 0..29, the record by lane 0
-  // each lane l < 30 produces model input l: its raw value is selected into the lane from the
-  // (wave-uniform) features, then one pass of the lane's transform (min-max / log / identity)
-  // runs for the whole wave instead of 30 divergent cases
-  const int id = cfg.log_identity;
-  float raw = 0.f;
-#define IGP_PUT(l, v) raw = lane == (l) ? (float)(v) : raw
-  IGP_PUT(0, f.tx_count_1m); IGP_PUT(1, f.tx_count_5m); IGP_PUT(2, f.tx_count_1h); IGP_PUT(3, f.tx_sum_1h);
-  IGP_PUT(4, f.tx_avg_1h); IGP_PUT(5, f.unique_devices_24h); IGP_PUT(6, f.unique_ips_24h);
-  IGP_PUT(7, f.ip_country_changes_7d); IGP_PUT(8, f.device_age_days); IGP_PUT(9, f.account_age_days);
-  IGP_PUT(10, f.total_deposits); IGP_PUT(11, f.total_withdrawals); IGP_PUT(12, f.net_deposit);
-  IGP_PUT(13, f.deposit_count); IGP_PUT(14, f.withdraw_count); IGP_PUT(15, f.time_since_last_tx);
-  IGP_PUT(16, f.session_duration); IGP_PUT(17, f.avg_bet_size); IGP_PUT(18, f.win_rate);
-  IGP_PUT(19, (flags & FR_VPN) ? 1.f : 0.f); IGP_PUT(20, (flags & FR_PROXY) ? 1.f : 0.f);
-  IGP_PUT(21, (flags & FR_TOR) ? 1.f : 0.f); IGP_PUT(22, (flags & FR_DISPOSABLE) ? 1.f : 0.f);
-  IGP_PUT(23, f.bonus_claim_count); IGP_PUT(24, f.bonus_wager_rate); IGP_PUT(25, (flags & FR_BONUS_ONLY) ? 1.f : 0.f);
-  IGP_PUT(26, amount); IGP_PUT(27, tx_type == TX_DEPOSIT ? 1.f : 0.f); IGP_PUT(28, tx_type == TX_WITHDRAW ? 1.f : 0.f);
-  IGP_PUT(29, tx_type == TX_BET ? 1.f : 0.f);
+    // ---- rule pass (engine.go:420-483), raw features
+    int score = 0;
+    uint32_t reasons = 0;
+    if (f.tx_count_1m > cfg.max_tx_per_minute) { score += cfg.w_high_velocity; reasons |= 1u << 0; }
+    if (f.account_age_days < cfg.new_account_days && amount > cfg.large_deposit_amount) {
+      score += cfg.w_new_account_large_tx; reasons |= 1u << 1;
+    }
+    if (f.unique_devices_24h > cfg.max_devices_per_day) { score += cfg.w_multiple_devices; reasons |= 1u << 2; }
+    if (f.unique_ips_24h > cfg.max_ips_per_day) { score += cfg.w_ip_country_mismatch; reasons |= 1u << 3; }
+    if (flags & (FR_VPN | FR_PROXY | FR_TOR)) { score += cfg.w_vpn; reasons |= 1u << 4; }
+    if (f.time_since_last_tx < 300 && tx_type == TX_WITHDRAW) {
+      if (f.deposit_count > 0 && f.total_withdrawals > f.total_deposits * 80 / 100) {
+        score += cfg.w_rapid_deposit_withdraw; reasons |= 1u << 5;
+      }
+    }
+    if (flags & FR_BONUS_ONLY) { score += cfg.w_bonus_abuse; reasons |= 1u << 6; }
+    if (blacklisted) { score += cfg.w_known_fraudster; reasons |= 1u << 7; }
+    f.reserved0 = (int32_t)reasons;
+    f.reserved1 = score > 100 ? 100 : score;
+
+    // ---- the 30 model inputs: lane ql produces inputs ql and ql + 16 (raw value selected
+    // from the quarter-uniform features, then one pass of each transform for the quarter)
+    const int id = cfg.log_identity;
+    float r0 = 0.f, r1 = 0.f;
+#define IGP_PUT(l, v) \
+  if ((l) < 16) r0 = ql == (l) ? (float)(v) : r0; else r1 = ql == (l) - 16 ? (float)(v) : r1
+    IGP_PUT(0, f.tx_count_1m); IGP_PUT(1, f.tx_count_5m); IGP_PUT(2, f.tx_count_1h); IGP_PUT(3, f.tx_sum_1h);
+    IGP_PUT(4, f.tx_avg_1h); IGP_PUT(5, f.unique_devices_24h); IGP_PUT(6, f.unique_ips_24h);
+    IGP_PUT(7, f.ip_country_changes_7d); IGP_PUT(8, f.device_age_days); IGP_PUT(9, f.account_age_days);
+    IGP_PUT(10, f.total_deposits); IGP_PUT(11, f.total_withdrawals); IGP_PUT(12, f.net_deposit);
+    IGP_PUT(13, f.deposit_count); IGP_PUT(14, f.withdraw_count); IGP_PUT(15, f.time_since_last_tx);
+    IGP_PUT(16, f.session_duration); IGP_PUT(17, f.avg_bet_size); IGP_PUT(18, f.win_rate);
+    IGP_PUT(19, (flags & FR_VPN) ? 1.f : 0.f); IGP_PUT(20, (flags & FR_PROXY) ? 1.f : 0.f);
+    IGP_PUT(21, (flags & FR_TOR) ? 1.f : 0.f); IGP_PUT(22, (flags & FR_DISPOSABLE) ? 1.f : 0.f);
+    IGP_PUT(23, f.bonus_claim_count); IGP_PUT(24, f.bonus_wager_rate);
+    IGP_PUT(25, (flags & FR_BONUS_ONLY) ? 1.f : 0.f); IGP_PUT(26, amount);
+    IGP_PUT(27, tx_type == TX_DEPOSIT ? 1.f : 0.f); IGP_PUT(28, tx_type == TX_WITHDRAW ? 1.f : 0.f);
+    IGP_PUT(29, tx_type == TX_BET ? 1.f : 0.f);
 #undef IGP_PUT
-  const int kind = k1_kind[lane & 31];
-  float xv = raw;
-  if (kind == 1) xv = minmax_scale(raw, 0.f, k1_hi[lane & 31]);
-  else if (kind == 2) xv = log_transform(raw, id);
-  if (lane < 30) xr[lane] = xv;
+    float x0 = r0, x1 = r1;
+    const int k0 = k1_kind[ql], k1 = k1_kind[ql + 16];
+    if (k0 == 1) x0 = minmax_scale(r0, 0.f, k1_hi[ql]);
+    if (k1 == 1) x1 = minmax_scale(r1, 0.f, k1_hi[ql + 16]);
+    if (k0 == 2) x0 = log_transform(r0, id);
+    if (k1 == 2) x1 = log_transform(r1, id);
+    xr[ql] = x0;
+    if (ql + 16 < 30) xr[ql + 16] = x1;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int j = lane + 64 * u;
-    if (j < ext_w) xr[30 + j] = extv[u];
-  }
-  for (int j = lane + 128; j < ext_w; j += 64) xr[30 + j] = s >= 0 ? a.ext[(size_t)s * ext_w + j] : 0.f;
-  if (lane == 0) a.feat[row] = f;
-  clear_next_dedup(a, row, seq, lane);
-
-  // ---- score-then-update (engine.go:486-488). An account whose only event in the batch is
-  // this request has had all its reads done (by this wave), so the event is applied here by
-  // the whole wave; a multi-event account's batch is applied by its last-finishing wave.
-  if (a.dbuf && s >= 0) {
-    const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
-    int h = (int)dh;
-    if (dkey != s) {  // probe collision: walk the chain
-      h = dedup_find(t, s);
-      if (h >= 0) { dfirst = t.first[h]; dcount = t.count[h]; }
+    for (int u = 0; u < 7; ++u) {
+      const int j = ql + 16 * u;
+      if (j < ext_w) xr[30 + j] = extv[u];
     }
-    if (h >= 0) {
-      if (dcount == 1) {
-        apply_event_wave(a.upd, rq, rt, wd, wi, lane, hour_word);
-      } else {
-        // multi-event account: queue this row, then count it as read (its loads were all
-        // consumed above); the wave that completes the count applies the account's whole
-        // batch in row order (no other row of it can still be reading)
-        int last = 0;
-        if (lane == 0) {
+    for (int j = ql + 112; j < ext_w; j += K1_QL) xr[30 + j] = has ? a.ext[(size_t)s * ext_w + j] : 0.f;
+    if (ql == 0) a.feat[row] = f;
+    clear_next_dedup(a, row, seq, ql);
+
+    // ---- score-then-update (engine.go:486-488)
+    if (a.dbuf && has) {
+      const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
+      h = (int)dh;
+      if (dkey != s) {  // probe collision: walk the chain
+        h = dedup_find(t, s);
+        if (h >= 0) { dfirst = t.first[h]; dcount = t.count[h]; }
+      }
+      if (h >= 0) {
+        if (dcount == 1) {
+          apply_event_q(a.upd, rq, rt, wd, wi, ql, qb, hour_word);
+        } else if (ql == 0) {
+          // multi-event account: queue this row, then count it as read (its loads were all
+          // consumed above); the request that completes the count applies the account's batch
           const int pos = atomicAdd(&t.fill[h], 1);
           if (pos < DEDUP_LIST) t.list[(size_t)h * DEDUP_LIST + pos] = row;
           __threadfence();
           last = atomicAdd(&t.done[h], 1) == dcount - 1;
         }
-        if (__shfl(last, 0, 64)) {
-          __threadfence();
-          apply_segment_wave(a.upd, t, h, dcount, s, rt, lane);
-        }
       }
+    }
+  }
+  // multi-event accounts completed by a quarter of this wave: applied with the whole wave
+  uint64_t lm = __ballot(ql == 0 && last);
+  if (lm) {
+    const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
+    __threadfence();
+    while (lm) {
+      const int src = __ffsll((long long)lm) - 1;
+      lm &= lm - 1;
+      const int hb = __shfl(h, src, 64), cb = __shfl(dcount, src, 64), sb = __shfl(s, src, 64);
+      apply_segment_wave(a.upd, t, hb, cb, sb, a.rt[sb], lane);
     }
   }
 }
@@ -588,7 +642,7 @@ __global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
 // ---------------------------------------------------------------------------------- launch
 void launch_feature_assemble(const AssembleArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
-  hipLaunchKernelGGL(feature_assemble_kernel, dim3((a.n_rows + 3) / 4), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(feature_assemble_kernel, dim3((a.n_rows + 15) / 16), dim3(256), 0, st, a);
 }
 
 void launch_dedup_insert(const UpdateArgs& a, hipStream_t st) {
