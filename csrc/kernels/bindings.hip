@@ -134,6 +134,7 @@ PYBIND11_MODULE(_hipk, m) {
     a.binary_class = geti(d, "binary_class", -1);
     a.all_positive = geti(d, "all_positive", 1);
     a.no_finish = geti(d, "no_finish", 0);
+    a.all_leq = geti(d, "all_leq", 0);
     const int groups = geti(d, "groups", 1);
     launch_tree_ensemble_grouped(a, groups, ptr<float*>(d, "partial"), stream_of(s));
     check("tree_ensemble");

@@ -539,7 +539,7 @@ __device__ __forceinline__ uint32_t hll_segment(const UpdateArgs& a, uint8_t* rg
   }
   int pm = before;
   bool win = has;
-  for (int y = 0; y < 64; ++y) {
+  for (int y = 0; y <= ll; ++y) {  // events occupy lanes 0..ll
     const int iy = __shfl(idx, y, 64), ry = __shfl(rank, y, 64);
     if (has && iy == idx && y != lane) {
       if (y < lane) pm = max(pm, ry);
@@ -564,7 +564,7 @@ __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h
   // sort the (distinct) row indices: rank = #smaller, then push each to lane `rank`
   const int key = lane < c ? t.list[(size_t)h * DEDUP_LIST + lane] : (0x7fffffc0 | lane);
   int rank = 0;
-  for (int y = 0; y < 64; ++y) rank += __shfl(key, y, 64) < key;
+  for (int y = 0; y < c; ++y) rank += __shfl(key, y, 64) < key;  // lanes >= c hold sentinels
   const int j = __builtin_amdgcn_ds_permute(rank * 4, key);
   const bool act = lane < c;
   ReqRec ev{};

@@ -98,6 +98,7 @@ struct TreeArgs {
   int32_t binary_class;     // -1 unless classifier binary case
   int32_t all_positive;
   int32_t no_finish;        // grouped launch: leave partials for the consumer (mlp_head)
+  int32_t all_leq;          // every node BRANCH_LEQ (fast decision path; missing tracks allowed)
 };
 void launch_tree_ensemble(const TreeArgs& a, hipStream_t st);
 void launch_tree_ensemble_grouped(const TreeArgs& a, int groups, float* partial, hipStream_t st);

@@ -60,7 +60,16 @@ __device__ __forceinline__ void post_row(const TreeArgs& a, const float* s, floa
   }
 }
 
-template <int K>
+template <bool LEQ>
+__device__ __forceinline__ int tree_next(int i, float x, float2 nd) {
+  if constexpr (LEQ) {
+    const bool c = x <= nd.x || (((__float_as_uint(nd.y) >> 19) & 1u) && isnan(x));
+    return 2 * i + (c ? 1 : 2);
+  }
+  else return tree_step(i, x, nd);
+}
+
+template <int K, bool LEQ>
 __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_group, int feat_w,
                                                    int nodes_in_lds, float* partial) {
   constexpr bool TWO_PHASE = K >= 16;
@@ -89,14 +98,28 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
     constexpr int UX = 32, UN = 16;
     const int xt = TR_ROWS * feat_w;
     const int ntot = nodes_in_lds ? nt * n_int : 0;
-    // element e = xb + u*256 + tid of the row-major [64][feat_w] tile: (r, c) advanced
-    // incrementally (no per-element integer division)
+    // X: 16-byte loads when rows are float4-aligned (the usual case), else element loads with
+    // (r, c) advanced incrementally; the tile is stored with a +1 column pad (conflict-free
+    // per-lane column reads at the root)
+    const bool vec = (feat_w & 3) == 0 && (a.x_stride & 3) == 0;
+    const int f4 = feat_w >> 2;
     const int dr = 256 / feat_w, dc = 256 % feat_w;
     for (int xb = 0, nb = 0; xb < xt || nb < ntot; xb += 256 * UX, nb += 256 * UN) {
       float v[UX];
       float2 w[UN];
       int rr[UX], cc[UX];
-      {
+      if (vec) {
+#pragma unroll
+        for (int u = 0; u < UX / 4; ++u) {
+          const int e4 = (xb >> 2) + u * 256 + tid;  // float4 index in the tile
+          const int r = e4 / f4, c = (e4 - r * f4) * 4;
+          const int row = row0 + r;
+          float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (r < TR_ROWS && row < a.n_rows) q = *reinterpret_cast<const float4*>(a.X + (size_t)row * a.x_stride + c);
+          v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
+          rr[4 * u] = r; cc[4 * u] = c;
+        }
+      } else {
         int r = (xb + tid) / feat_w, c = (xb + tid) - r * feat_w;
 #pragma unroll
         for (int u = 0; u < UX; ++u) {
@@ -106,20 +129,29 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
           c += dc;
           if (c >= feat_w) { c -= feat_w; ++r; }
         }
-      }
 #pragma unroll
-      for (int u = 0; u < UX; ++u) {
-        const int row = row0 + rr[u];
-        v[u] = (rr[u] < TR_ROWS && row < a.n_rows) ? a.X[(size_t)row * a.x_stride + cc[u]] : 0.f;
+        for (int u = 0; u < UX; ++u) {
+          const int row = row0 + rr[u];
+          v[u] = (rr[u] < TR_ROWS && row < a.n_rows) ? a.X[(size_t)row * a.x_stride + cc[u]] : 0.f;
+        }
       }
 #pragma unroll
       for (int u = 0; u < UN; ++u) {
         const int e = nb + u * 256 + tid;
         w[u] = e < ntot ? gn[e] : make_float2(0.f, 0.f);
       }
+      if (vec) {
 #pragma unroll
-      for (int u = 0; u < UX; ++u)
-        if (rr[u] < TR_ROWS) sx[rr[u] * xs + cc[u]] = v[u];
+        for (int u = 0; u < UX / 4; ++u)
+          if (rr[4 * u] < TR_ROWS) {
+            float* d = sx + rr[4 * u] * xs + cc[4 * u];
+            d[0] = v[4 * u]; d[1] = v[4 * u + 1]; d[2] = v[4 * u + 2]; d[3] = v[4 * u + 3];
+          }
+      } else {
+#pragma unroll
+        for (int u = 0; u < UX; ++u)
+          if (rr[u] < TR_ROWS) sx[rr[u] * xs + cc[u]] = v[u];
+      }
 #pragma unroll
       for (int u = 0; u < UN; ++u) {
         const int e = nb + u * 256 + tid;
@@ -149,7 +181,7 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
         if (tt[q] < t1) {
           const float2 nd = nodes[(tt[q] - t0) * n_int + idx[q]];
           const int f = __float_as_uint(nd.y) & 0xffff;
-          idx[q] = tree_step(idx[q], xrow[f], nd);
+          idx[q] = tree_next<LEQ>(idx[q], xrow[f], nd);
         }
       }
     }
@@ -188,22 +220,35 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
     float v[RPT];
 #pragma unroll
     for (int j = 0; j < RPT; ++j) v[j] = 0.f;
-    const float* lk = a.leaves + (size_t)t0 * n_leaf * K + k;  // 32-bit offsets below (SGPR base)
+    // leaf loads through a buffer resource: per-lane offset (leaf, k) in a VGPR, the tree's
+    // base (uniform) in an SGPR offset
+    const float* lbase = a.leaves + (size_t)t0 * n_leaf * K;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(lbase), 0, nt * n_leaf * K * 4, 0x00020000);
+    const int tstride = n_leaf * K * 4;  // bytes per tree
     constexpr int TU = RPT >= 8 ? 4 : 8;  // trees per step: RPT x TU loads in flight
-    for (int t = 0; t < nt; t += TU) {
+    int t = 0;
+    for (; t + TU <= nt; t += TU) {
       float p[RPT][TU];
 #pragma unroll
       for (int j = 0; j < RPT; ++j) {
-        const uint16_t* li = sleaf + (sp + j * SPP) * nt;
+        const uint16_t* li = sleaf + (sp + j * SPP) * nt + t;
 #pragma unroll
         for (int u = 0; u < TU; ++u)
-          p[j][u] = (t + u < nt) ? lk[((t + u) * n_leaf + (int)li[t + u]) * K] : 0.f;
+          p[j][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                        rsrc, ((int)li[u] * K + k) * 4, (t + u) * tstride, 0));
       }
 #pragma unroll
       for (int j = 0; j < RPT; ++j)
 #pragma unroll
-        for (int u = 0; u < TU; ++u)
-          if (t + u < nt) v[j] += p[j][u];
+        for (int u = 0; u < TU; ++u) v[j] += p[j][u];
+    }
+    for (; t < nt; ++t) {
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        const int l = sleaf[(sp + j * SPP) * nt + t];
+        v[j] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (l * K + k) * 4, t * tstride, 0));
+      }
     }
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
@@ -278,8 +323,8 @@ __global__ void tree_finish_elem_kernel(TreeArgs a, const float* partial, int gr
   a.out[e] = v;  // n_out == K
 }
 
-template <int K>
-static void launch_k(const TreeArgs& a, int groups, float* partial, int no_finish, hipStream_t st) {
+template <int K, bool LEQ>
+static void launch_kl(const TreeArgs& a, int groups, float* partial, int no_finish, hipStream_t st) {
   const int tpg = (a.n_trees + groups - 1) / groups;
   const int feat_w = a.x_stride;
   const int n_int = (1 << a.depth) - 1;
@@ -291,7 +336,7 @@ static void launch_k(const TreeArgs& a, int groups, float* partial, int no_finis
   int in_lds = (base + node_bytes + leaf_bytes) <= 96 * 1024;  // keep >= 1 block/CU with headroom
   const size_t lds = base + (in_lds ? node_bytes : 0) + leaf_bytes;
   dim3 grid((a.n_rows + TR_ROWS - 1) / TR_ROWS, groups);
-  hipLaunchKernelGGL((tree_kernel<K>), grid, dim3(256), lds, st, a, tpg, feat_w, in_lds,
+  hipLaunchKernelGGL((tree_kernel<K, LEQ>), grid, dim3(256), lds, st, a, tpg, feat_w, in_lds,
                      groups > 1 ? partial : nullptr);
   if (groups > 1 && !no_finish) {
     if (a.binary_class < 0 && a.post != 2 && a.n_out == K)
@@ -302,6 +347,11 @@ static void launch_k(const TreeArgs& a, int groups, float* partial, int no_finis
   }
 }
 
+template <int K>
+static void launch_k(const TreeArgs& a, int groups, float* partial, int no_finish, hipStream_t st) {
+  if (a.all_leq) launch_kl<K, true>(a, groups, partial, no_finish, st);
+  else launch_kl<K, false>(a, groups, partial, no_finish, st);
+}
 // partial scratch: [groups][n_rows][K] f32, provided by the caller when groups > 1.
 // no_finish: leave the partial slab for a consumer that reduces it (mlp_head).
 void launch_tree_ensemble_grouped(const TreeArgs& a, int groups, float* partial, hipStream_t st) {

@@ -54,6 +54,13 @@ class TreeStep:
     def out_width(self) -> int:
         return self.n_out
 
+    @property
+    def all_leq(self) -> bool:
+        """Every node is BRANCH_LEQ (sklearn-style ensembles; missing-value tracks allowed): the
+        kernel then skips decoding the comparison mode per node."""
+        meta = self.nodes_np.reshape(-1, 2)[:, 1].view(np.uint32)
+        return bool(np.all(((meta >> 16) & 0x7) == 0))
+
 
 @dataclass
 class DenseStep:

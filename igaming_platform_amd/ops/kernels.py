@@ -157,6 +157,7 @@ def tree_ensemble(tp, X: torch.Tensor, out: Optional[torch.Tensor], n_rows: int,
         n_rows=int(n_rows), n_trees=tp.n_trees, depth=tp.depth, k=tp.k, n_out=tp.n_out, post=tp.post,
         average=tp.average, binary_class=tp.binary_class, all_positive=tp.all_positive,
         groups=int(groups), partial=_opt(partial, "partial", dtype=torch.float32), no_finish=int(no_finish),
+        all_leq=int(tp.all_leq),
     )
     if tp.nodes.numel() < tp.n_trees * ((1 << tp.depth) - 1) * 2:
         raise ValueError("node table smaller than n_trees * (2^depth - 1)")
