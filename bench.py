@@ -68,11 +68,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one rank per GPU; IGP_DIST_BACKEND=gloo lets several ranks share one GPU to rehearse the
+    # multi-rank path on a 1-GPU box (RCCL refuses two ranks on one device)
+    backend = os.environ.get("IGP_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local_dev = local % ndev if backend != "nccl" else local
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from igaming_platform_amd.utils import benchkit
     from igaming_platform_amd.utils.synth import NOW0
