@@ -267,6 +267,13 @@ PYBIND11_MODULE(_hipk, m) {
     a.tile_rows = geti(d, "tile_rows");
     a.waves = geti(d, "waves");
     a.pipeline = geti(d, "pipeline", 1);
+    a.ws = geti(d, "ws");
+    a.ws_clusters = geti(d, "ws_clusters");
+    a.ws_sync = ptr<int32_t*>(d, "ws_sync");
+    a.ws_x = ptr<uint16_t*>(d, "ws_x");
+    a.ws_part = ptr<float*>(d, "ws_part");
+    a.ws_err = ptr<int32_t*>(d, "ws_err");
+    a.ws_trace = ptr<int64_t*>(d, "ws_trace");
     if (a.tile_rows != 0 && a.tile_rows != 16 && a.tile_rows != 32) throw std::runtime_error("gru: tile_rows 16|32");
     if (a.H != 64 && a.H != 128 && a.H != 256) throw std::runtime_error("gru: H must be 64, 128 or 256");
     if (a.layer[0].kx_pad != 32 && a.layer[0].kx_pad != 64) throw std::runtime_error("gru: input dim must pad to 32 or 64");
@@ -278,4 +285,5 @@ PYBIND11_MODULE(_hipk, m) {
     launch_gru(a, stream_of(s));
     check("gru");
   });
+  m.def("gru_ws_clusters", [](int n_rows) { return gru_ws_clusters(n_rows); });
 }

@@ -571,6 +571,16 @@ static void launch_gru_h(const GruArgs& a, hipStream_t st) {
 
 void launch_gru(const GruArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
+  // weight-stationary clusters while all of them fit one wave of the chip (1 workgroup per CU);
+  // beyond that the batch-parallel kernel at 32 rows per workgroup streams weights at a better
+  // rate than two waves of clusters (tools/gru_bench.py: 8192 rows 5.6 M vs 4.5 M seq/s)
+  static int n_cu = [] {
+    int dev = 0, v = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    return v > 0 ? v : 256;
+  }();
+  if (a.ws && gru_ws_eligible(a) && gru_ws_clusters(a.n_rows) * 8 <= n_cu) return launch_gru_ws(a, st);
   // rows per workgroup: every CU streams the full weight set each step (a per-CU L2 bandwidth
   // bound, tools/gru_bench.py), so 32 rows amortise each fragment over two MFMA row tiles once
   // the batch fills the 256 CUs at 32 rows; below that 16 keeps more CUs streaming.

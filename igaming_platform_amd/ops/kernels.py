@@ -327,16 +327,47 @@ class GruPack:
             self.head_b = float(head.b_np[0]) if head.b_np is not None else 0.0
             self.head_act = ACT[head.act]
         self.device = dev
+        # weight-stationary cluster kernel (csrc/kernels/gru_ws.hip) for 2 x 256, lbr = 1, I <= 32
+        self.ws_ok = self.n_layers == 2 and H == 256 and self.lbr == 1 and self.I <= 32
+        self._ws = None
+        self._ws_old = []  # superseded workspaces stay alive: captured graphs keep their pointers
+        self.ws_err = torch.zeros(1, dtype=torch.int32, device=dev) if self.ws_ok else None
+
+    def workspace(self, n_rows: int):
+        """Hand-off slabs / counters / head partials for ``n_rows`` (grow-only)."""
+        if not self.ws_ok:
+            return None
+        ncl = -(-int(n_rows) // 128)
+        if self._ws is None or self._ws["clusters"] < ncl:
+            if self._ws is not None:
+                self._ws_old.append(self._ws)
+            dev = self.device
+            self._ws = dict(clusters=ncl,
+                            sync=torch.zeros(ncl * 16, dtype=torch.int32, device=dev),
+                            x=torch.zeros(ncl * 2 * 8 * 2 * 128 * 32, dtype=torch.int16, device=dev),
+                            part=torch.zeros(ncl * 8 * 128, dtype=torch.float32, device=dev))
+        return self._ws
+
+    def ws_failed(self) -> bool:
+        """True if a cluster launch ever timed out waiting for a non-resident member."""
+        return bool(self.ws_err is not None and int(self.ws_err.item()) != 0)
 
 
 def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh: Optional[torch.Tensor] = None,
         X: Optional[torch.Tensor] = None, store=None, slots: Optional[torch.Tensor] = None,
-        m_ptr: Optional[torch.Tensor] = None, tile_rows: int = 0, waves: int = 0, pipeline: int = 1) -> None:
-    """K4. Input either dense ``X`` f32 [T, rows, I] or the store's event rings for ``slots``."""
+        m_ptr: Optional[torch.Tensor] = None, tile_rows: int = 0, waves: int = 0, pipeline: int = 1,
+        ws: int = 1, ws_trace: Optional[torch.Tensor] = None) -> None:
+    """K4. Input either dense ``X`` f32 [T, rows, I] or the store's event rings for ``slots``.
+    ``ws=1`` runs the weight-stationary cluster kernel when the model shape allows it."""
     dev = gp.device
     d = dict(n_layers=gp.n_layers, H=gp.H, T=int(T), I=gp.I, n_rows=int(n_rows),
              m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32, device=dev), tile_rows=int(tile_rows),
              waves=int(waves or gp.waves), pipeline=int(pipeline))
+    w = gp.workspace(n_rows) if ws else None
+    if w is not None:
+        d.update(ws=1, ws_clusters=w["clusters"], ws_sync=w["sync"].data_ptr(), ws_x=w["x"].data_ptr(),
+                 ws_part=w["part"].data_ptr(), ws_err=gp.ws_err.data_ptr(),
+                 ws_trace=_opt(ws_trace, "ws_trace", dtype=torch.int64, min_numel=64 * 8 + 4, device=dev))
     for i, l in enumerate(gp.layers):
         d[f"l{i}_W"] = _need(l["W"], "W", torch.bfloat16, device=dev)
         d[f"l{i}_R"] = _need(l["R"], "R", torch.bfloat16, device=dev)

@@ -86,3 +86,68 @@ def test_gru_respects_live_rows():
     dm.run(X, 256, m_ptr=n)
     o = dm.out.cpu().numpy().reshape(-1)
     assert np.all(o[100:] == -7.0) and np.all(o[:100] != -7.0)
+
+
+def _ws_pack(seq=24):
+    from igaming_platform_amd.ops import kernels as K
+    N, m, plan = _model(seq=seq, hidden=256, layers=2, linear_before_reset=1, head=True)
+    gp = K.GruPack([s for s in plan.steps if s.kind == "gru"], plan.steps[-1], "cuda")
+    assert gp.ws_ok
+    return N, m, gp
+
+
+@pytest.mark.parametrize("rows", [1, 130, 4096, 4500])
+def test_gru_weight_stationary_matches_batch_parallel(rows):
+    """gru_ws.hip (8-workgroup clusters, weights in VGPRs, sc1 hand-offs) == gru.hip and the
+    fp32 executor, at 1 cluster, a partial cluster, a full chip (32 clusters) and > 1 wave of
+    clusters (the grid is larger than the CU count)."""
+    import torch
+    from igaming_platform_amd.ops import kernels as K
+    T = 24
+    N, m, gp = _ws_pack(T)
+    rng = np.random.default_rng(rows)
+    X = rng.standard_normal((T, rows, 16)).astype(np.float32)
+    Xd = torch.from_numpy(X).cuda()
+    o_ws = torch.full((rows,), -9.0, device="cuda")
+    o_bp = torch.full((rows,), -9.0, device="cuda")
+    K.gru(gp, rows, T, out=o_ws, X=Xd, ws=1)
+    K.gru(gp, rows, T, out=o_bp, X=Xd, ws=0)
+    torch.cuda.synchronize()
+    assert not gp.ws_failed()
+    a, b = o_ws.cpu().numpy(), o_bp.cpu().numpy()
+    assert np.all(a != -9.0)
+    np.testing.assert_allclose(a, b, rtol=0, atol=2e-3)
+    if rows <= 130:
+        ref = N.Executor(m).run({"input": X})["output"].reshape(-1)
+        np.testing.assert_allclose(a, ref, rtol=0, atol=1e-2)
+
+
+def test_gru_weight_stationary_yh_and_live_rows():
+    """Y_h (no head) from the cluster kernel; rows past the device live count stay untouched;
+    repeated launches (fresh counters each time) agree bit for bit."""
+    import torch
+    from igaming_platform_amd.ops import kernels as K
+    from igaming_platform_amd.native import native
+    from igaming_platform_amd.onnx import builders
+    from igaming_platform_amd.models.plan import compile_onnx, to_device
+    N = native()
+    m = N.OnnxModel.from_bytes(builders.build("gru", seq=10, hidden=256, layers=2, linear_before_reset=1,
+                                              head=False).SerializeToString())
+    plan = to_device(compile_onnx(m), "cuda")
+    gp = K.GruPack([s for s in plan.steps if s.kind == "gru"], None, "cuda")
+    rows, live = 512, 300
+    X = torch.randn(10, rows, 16, device="cuda")
+    yh = torch.full((rows, 256), 5.0, device="cuda")
+    n = torch.tensor([live], dtype=torch.int32, device="cuda")
+    K.gru(gp, rows, 10, yh=yh, X=X, m_ptr=n, ws=1)
+    y1 = yh.clone()
+    K.gru(gp, rows, 10, yh=yh, X=X, m_ptr=n, ws=1)
+    torch.cuda.synchronize()
+    assert not gp.ws_failed()
+    assert torch.equal(y1, yh)
+    assert torch.all(yh[live:] == 5.0)
+    ref = N.Executor(m).run({"input": np.ascontiguousarray(X[:, :live].cpu().numpy())})
+    yref = [v for k, v in ref.items()][0].reshape(live, -1)
+    got = yh[:live].cpu().numpy()
+    if yref.shape[1] == 256:
+        np.testing.assert_allclose(got, yref, rtol=0, atol=2e-2)

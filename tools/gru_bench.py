@@ -21,11 +21,11 @@ def main() -> int:
     ref = {}
     for B in (512, 4096, 8192):
         slots = torch.from_numpy(np.random.default_rng(B).integers(0, 1 << 18, B).astype(np.int32)).to(dev)
-        for tr, w, pipe in ((16, 4, 0), (16, 8, 0), (32, 4, 0), (16, 0, 1), (32, 0, 1)):
+        for tr, w, pipe, ws in ((16, 0, 1, 1), (16, 4, 0, 0), (16, 8, 0, 0), (32, 4, 0, 0), (16, 0, 1, 0), (32, 0, 1, 0)):
             if True:
                 out = torch.zeros(B, device=dev)
                 run = lambda: K.gru(R.gp, B, R.T, out=out, store=R.store, slots=slots, tile_rows=tr, waves=w,  # noqa
-                                    pipeline=pipe)
+                                    pipeline=pipe, ws=ws)
                 run()
                 torch.cuda.synchronize()
                 if B not in ref:
@@ -40,8 +40,8 @@ def main() -> int:
                     e1.synchronize()
                     ts.append(e0.elapsed_time(e1))
                 ms = float(np.median(ts[2:]))
-                r = dict(batch=B, tile_rows=tr, waves=w, pipeline=pipe, ms=ms, seq_per_s=B / ms * 1e3, us_per_step=ms * 10,
-                         max_diff_vs_first=diff)
+                r = dict(batch=B, ws=ws, tile_rows=tr, waves=w, pipeline=pipe, ms=ms, seq_per_s=B / ms * 1e3, us_per_step=ms * 10,
+                         max_diff_vs_first=diff, ws_failed=R.gp.ws_failed())
                 res.append(r)
                 print(json.dumps(r), flush=True)
     with open(os.environ.get("OUT", "gpurun_out/gru_sweep.json"), "w") as f:
