@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--depth", type=int, default=3, help="pipeline depth (batches in flight)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the per-step RCCL all_gather")
+    ap.add_argument("--stream", action="store_true",
+                    help="scorer configs: streaming mode, one launch per batch running copy(i) || state(i-1) "
+                         "|| model(i-2) (measured slower on ROCm 7.2 than the default three-stream pipeline: "
+                         "~35 us between consecutive multi-branch graph launches)")
     ap.add_argument("--json-out", default="")
     return ap.parse_args()
 
@@ -88,6 +92,8 @@ def main():
     if a.config in benchkit.MODEL_CONFIGS:
         return model_bench(a, world, rank, dev)
 
+    if a.stream and not a.no_graphs:
+        return stream_bench(a, world, rank, dev)
     S = benchkit.build(a.config, a.batch, a.accounts, dev, rank=rank, depth=a.depth,
                        use_graphs=not a.no_graphs)
     sc, pool, B = S.scorer, S.pool, S.batch
@@ -99,15 +105,17 @@ def main():
 
     def step(i: int, now: int):
         slot = sc.next_slot()
-        sc.pack(slot, pool[i % len(pool)])  # the wire decoder's output: raw REQREC rows
-        p = sc.submit_packed(slot, B, now)
+        # the wire decoder's output (raw REQREC rows) -> pinned slab -> three graphs; with the
+        # native driver (default) the row copy and every launch are issued from C++
+        p = sc.submit_rows(slot, pool[i % len(pool)], now)
         if world > 1 and not a.no_gather:
             with torch.cuda.stream(sc.mstream):  # results / metrics live on the model stream
                 dist.all_gather_into_tensor(gathered, sc.slots[slot].res[:B].reshape(-1))
                 if i % 16 == 15:
                     met_sum.copy_(sc.metrics)
                     dist.all_reduce(met_sum)
-                p.event.record(sc.mstream)
+                if p.event is not None:
+                    p.event.record(sc.mstream)
         return p
 
     inflight = []
@@ -166,6 +174,7 @@ def main():
             "accounts_per_gpu": n_acc,
             "pipeline_depth": a.depth,
             "graphs": not a.no_graphs,
+            "driver": "native" if sc.driver is not None else "python",
             "numerics": "fp32 features+trees, bf16 MFMA MLP (fp32 accumulate), fp64 ensemble",
         },
         "p99_latency_ms": p99,
@@ -181,6 +190,88 @@ def main():
                 f.write(line + "\n")
     if world > 1:
         dist.destroy_process_group()
+
+
+def _emit(a, world: int, rank: int, out: dict) -> None:
+    import torch.distributed as dist
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def stream_bench(a, world: int, rank: int, dev) -> None:
+    """Scorer configs in streaming mode (engine/scorer.py capture_pipelined): launch p runs
+    copy + dedup insert of batch p || feature assembly + store update of batch p-1 || model +
+    ensemble + D2H of batch p-2, one hipGraphLaunch per micro-batch. The timed region starts
+    with an empty pipeline and ends after the two drain launches: every timed batch is fully
+    scored and its results are on the host."""
+    import torch
+    import torch.distributed as dist
+    from igaming_platform_amd.utils import benchkit
+    from igaming_platform_amd.utils.synth import NOW0
+    S = benchkit.build(a.config, a.batch, a.accounts, dev, rank=rank, depth=3, use_graphs=True)
+    sc, pool, B = S.scorer, S.pool, S.batch
+    sc.capture_pipelined()
+    gathered = torch.zeros(world * B * 2, dtype=torch.int32, device=dev) if world > 1 else None
+    met_sum = torch.zeros(128, dtype=torch.int64, device=dev)
+    lat: list = []
+    scored = [0]
+
+    def step(i: int, now: int):
+        slot, done = sc.pipe_reserve()
+        sc.pack(slot, pool[i % len(pool)])  # the wire decoder's output: raw REQREC rows
+        sc.pipe_launch(B, now)
+        if world > 1 and not a.no_gather:
+            with torch.cuda.stream(sc.pstream):  # results of the batch this launch finished
+                dist.all_gather_into_tensor(gathered, sc.slots[(slot + 1) % 3].res[:B].reshape(-1))
+                if i % 16 == 15:
+                    met_sum.copy_(sc.metrics)
+                    dist.all_reduce(met_sum)
+        return done
+
+    def account(done):
+        for n, _, ms in done:
+            scored[0] += n
+            lat.append(ms)
+
+    for i in range(a.warmup):
+        step(i, NOW0 + i // 50)
+    sc.pipe_drain()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        account(step(a.warmup + i, NOW0 + (a.warmup + i) // 50))
+    account(sc.pipe_drain())
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    assert scored[0] == B * a.steps, (scored[0], B * a.steps)
+    stats = torch.tensor([elapsed, float(np.percentile(lat, 99)), float(np.percentile(lat, 50))],
+                         dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+    elapsed, p99, p50 = (float(x) for x in stats.cpu())
+    out = {
+        "metric": "fraud scores/sec (whole node) + p99 score latency",
+        "value": world * B * a.steps / elapsed, "unit": "scores/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "config": {"model": S.desc, "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
+                   "per_gpu_batch": B, "accounts_per_gpu": a.accounts, "pipeline": "streaming (1 launch/batch)",
+                   "graphs": True,
+                   "numerics": "fp32 features+trees, bf16 MFMA MLP (fp32 accumulate), fp64 ensemble"},
+        "p99_latency_ms": p99, "p50_latency_ms": p50, "latency_baseline_ms": BASELINE_P99_MS,
+        "latency_vs_baseline": BASELINE_P99_MS / p99 if p99 > 0 else None,
+    }
+    _emit(a, world, rank, out)
 
 
 def model_bench(a, world: int, rank: int, dev) -> None:

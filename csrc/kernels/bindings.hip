@@ -62,6 +62,10 @@ void check(const char* what) {
 
 }  // namespace
 
+namespace igp {
+void register_driver(py::module_& m);
+}
+
 PYBIND11_MODULE(_hipk, m) {
   m.doc() = "igaming_platform_amd gfx950 HIP kernels";
   m.attr("ARCH") = "gfx950";
@@ -72,6 +76,7 @@ PYBIND11_MODULE(_hipk, m) {
   m.attr("SIZEOF_REQREC") = (int)sizeof(ReqRec);
   m.attr("DEDUP_LIST") = DEDUP_LIST;
   m.attr("DEDUP_REGIONS") = DEDUP_RING + 1;
+  igp::register_driver(m);
 
   m.def("feature_assemble", [](py::dict d, uintptr_t s) {
     AssembleArgs a{};

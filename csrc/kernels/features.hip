@@ -441,10 +441,16 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
           apply_event_q(a.upd, rq, rt, wd, wi, ql, qb, hour_word);
         } else if (ql == 0) {
           // multi-event account: queue this row, then count it as read (its loads were all
-          // consumed above); the request that completes the count applies the account's batch
+          // consumed above); the request that completes the count applies the account's batch.
+          // Hand-off without an L2 writeback fence (MI355X_MICROARCH.md, sc1 table, first row):
+          // the list entry is an sc1 store drained by vmcnt(0) before the agent-scope add, and
+          // the wave whose add returns the last count reads the list with sc1 loads. (A
+          // __threadfence here wrote back the XCD's dirty L2 - every X / FeatRec row of the
+          // batch - once per multi-event row.)
           const int pos = atomicAdd(&t.fill[h], 1);
-          if (pos < DEDUP_LIST) t.list[(size_t)h * DEDUP_LIST + pos] = row;
-          __threadfence();
+          if (pos < DEDUP_LIST)
+            __hip_atomic_store(&t.list[(size_t)h * DEDUP_LIST + pos], row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           last = atomicAdd(&t.done[h], 1) == dcount - 1;
         }
       }
@@ -454,7 +460,6 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
   uint64_t lm = __ballot(ql == 0 && last);
   if (lm) {
     const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
-    __threadfence();
     while (lm) {
       const int src = __ffsll((long long)lm) - 1;
       lm &= lm - 1;
@@ -562,7 +567,10 @@ __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h
     return;
   }
   // sort the (distinct) row indices: rank = #smaller, then push each to lane `rank`
-  const int key = lane < c ? t.list[(size_t)h * DEDUP_LIST + lane] : (0x7fffffc0 | lane);
+  // sc1 load: the entries come from other waves of the same launch (feature_assemble hand-off)
+  const int key = lane < c ? __hip_atomic_load(&t.list[(size_t)h * DEDUP_LIST + lane], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                           : (0x7fffffc0 | lane);
   int rank = 0;
   for (int y = 0; y < c; ++y) rank += __shfl(key, y, 64) < key;  // lanes >= c hold sentinels
   const int j = __builtin_amdgcn_ds_permute(rank * 4, key);

@@ -19,9 +19,10 @@
 // inter-workgroup visibility, first row of the sc1 table): every byte stored with 16-B `sc1`
 // buffer stores, every storing wave `s_waitcnt vmcnt(0)`, a workgroup barrier, then ONE lane
 // adds to the cluster's monotonic counter (agent-scope atomic); consumers poll it with `sc1`
-// loads, barrier, and read every handed-off byte with 16-B `sc1` buffer loads. Counters are
-// zeroed by the launch (a memset node when captured). Every poll is bounded: a cluster that is
-// not co-resident (another persistent kernel holding CUs) sets *ws_err and every wave exits.
+// loads, barrier, and read every handed-off byte with 16-B `sc1` buffer loads. A counter starts
+// at 0 (allocation) and member 0 returns it to 0 with an atomic after the cluster's final
+// arrival. Every poll is bounded: a cluster that is not co-resident (another persistent kernel
+// holding CUs) sets *ws_err and every wave exits; the host then resets and falls back.
 //
 // The f32 hidden state never leaves registers (lane-local z/r/h~ combine, as in gru.hip); the
 // head is a fixed-order sum of per-member f32 partials (deterministic).
@@ -45,7 +46,7 @@ constexpr int WS_XS = 32 + 8;
 constexpr int WS_UW = WS_H / WS_CL;   // hidden units per member (32)
 constexpr int WS_SLICE = 2 * WS_M * WS_UW;  // bf16 per member slice (both layers)
 constexpr int WS_CH = WS_SLICE / 8;   // 16-B chunks per slice (1024)
-constexpr int WS_SPIN = 1 << 21;      // bounded polls (~seconds): never hang the GPU
+constexpr uint64_t WS_WAIT_TICKS = 20000000;  // 200 ms of wall_clock64 (100 MHz): never hang the GPU
 constexpr int SC1 = 16;               // buffer aux bit: sc1 (L2-coherent, bypasses L1)
 
 // v_exp_f32 + v_rcp_f32 (1 ulp): the IEEE divide sequence would cost ~10 VALU per gate
@@ -125,11 +126,14 @@ __device__ __forceinline__ void ws_layer(const bf16x8 (&wz)[16], const bf16x8 (&
 
 // bounded poll of the cluster counter by one lane; returns false on timeout
 __device__ __forceinline__ bool ws_wait(int32_t* cnt, int target) {
-  for (int n = 0; n < WS_SPIN; ++n) {
-    if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
-    __builtin_amdgcn_s_sleep(1);
+  const uint64_t t0 = wall_clock64();
+  for (;;) {
+    for (int n = 0; n < 64; ++n) {
+      if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (wall_clock64() - t0 > WS_WAIT_TICKS) return false;
   }
-  return false;
 }
 
 __global__ void __launch_bounds__(256, 1) gru_ws_kernel(GruArgs a) {
@@ -156,6 +160,14 @@ __global__ void __launch_bounds__(256, 1) gru_ws_kernel(GruArgs a) {
   const int j = ht * 16 + ccol;            // this lane's hidden unit
   const int T = a.T;
   int32_t* const cnt = a.ws_sync + cl * 16;
+  // outputs start as NaN: a cluster that gives up (bounded wait) leaves them so, and the host
+  // detects it (AbuseGpu.wait) instead of reading the previous batch's values
+  if (a.head_w && mem == 0 && tid < WS_M && row0 + tid < n_live) a.out[row0 + tid] = __builtin_nanf("");
+  if (a.yh)
+    for (int e = tid; e < WS_M * WS_UW; e += 256) {
+      const int row = row0 + e / WS_UW;
+      if (row < n_live) a.yh[(size_t)row * WS_H + mem * WS_UW + e % WS_UW] = __builtin_nanf("");
+    }
 
   // ---- weights -> registers (stationary for the whole launch)
   bf16x8 wz[16], wr[16], wh[16];
@@ -367,27 +379,32 @@ __global__ void __launch_bounds__(256, 1) gru_ws_kernel(GruArgs a) {
         if (row < n_live) a.yh[(size_t)row * WS_H + j] = hs[rt][r];
       }
   }
-  if (!a.head_w) return;
-  if (layer == 1) {
-    const float w = a.head_w[j];
-#pragma unroll
-    for (int rt = 0; rt < WS_RT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = hs[rt][r] * w;
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-        if (ccol == 0) red[(wave & 1) * WS_M + rt * 16 + crow + r] = v;
-      }
-  }
-  __syncthreads();
   float* const part = a.ws_part + (size_t)cl * WS_CL * WS_M;
-  if (tid < WS_M) {
-    const float v = red[tid] + red[WS_M + tid];
-    __hip_atomic_store(part + mem * WS_M + tid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.head_w) {
+    if (layer == 1) {
+      const float w = a.head_w[j];
+#pragma unroll
+      for (int rt = 0; rt < WS_RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = hs[rt][r] * w;
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+          if (ccol == 0) red[(wave & 1) * WS_M + rt * 16 + crow + r] = v;
+        }
+    }
+    __syncthreads();
+    if (tid < WS_M) {
+      const float v = red[tid] + red[WS_M + tid];
+      __hip_atomic_store(part + mem * WS_M + tid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  // final arrival: member 0 waits for all eight, combines the head partials, then returns the
+  // counter to 0 with an atomic (no member touches it again in this launch). The reset must
+  // take the atomic path: a memset node between graph replays left a stale counter line
+  // visible to the next replay's sc1 polls.
   if (tid == 0) {
     __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bool ok = true;
@@ -399,7 +416,7 @@ __global__ void __launch_bounds__(256, 1) gru_ws_kernel(GruArgs a) {
   }
   __syncthreads();
   if (mem != 0 || !*sflag) return;
-  if (tid < WS_M && row0 + tid < n_live) {
+  if (a.head_w && tid < WS_M && row0 + tid < n_live) {
     float v = a.head_b;
 #pragma unroll
     for (int m2 = 0; m2 < WS_CL; ++m2)
@@ -407,6 +424,7 @@ __global__ void __launch_bounds__(256, 1) gru_ws_kernel(GruArgs a) {
     if (a.head_act == 2) v = 1.f / (1.f + expf(-v));
     a.out[row0 + tid] = v;
   }
+  if (tid == 0) __hip_atomic_exchange(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace
@@ -428,7 +446,6 @@ bool gru_ws_eligible(const GruArgs& a) {
 void launch_gru_ws(const GruArgs& a, hipStream_t st) {
   const int ncl = gru_ws_clusters(a.n_rows);
   const int grid = ((ncl + 7) / 8) * 64;
-  hipMemsetAsync(a.ws_sync, 0, (size_t)ncl * 16 * sizeof(int32_t), st);
   hipLaunchKernelGGL(gru_ws_kernel, dim3(grid), dim3(256), gru_ws_lds_bytes(), st, a);
 }
 

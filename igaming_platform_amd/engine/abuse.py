@@ -23,6 +23,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from ..layouts import FR_BONUS_ONLY, FR_PROXY, FR_TOR, FR_VPN
+from ..obs.logging import get_logger
 
 SIGNAL_WEIGHTS: Dict[str, float] = {
     "BONUS_ONLY_PLAYER": 0.35,
@@ -63,6 +64,9 @@ def rule_signals(feat, scoring, n_linked: int) -> List[str]:
     if n_linked > 0:
         s.append("SHARED_DEVICE")
     return s
+
+
+log = get_logger("abuse")
 
 
 class AbuseGpu:
@@ -122,7 +126,7 @@ class AbuseGpu:
             for b in self.buckets:
                 for slot in range(self.depth):
                     self._pack(slot, np.zeros(0, np.int32), b)
-                    s = torch.cuda.Stream(device=self.device)
+                    s = self.stream  # capture on the replay stream: no extra streams / hardware queues
                     s.wait_stream(torch.cuda.current_stream())
                     with torch.cuda.stream(s):
                         self._body(slot, b)
@@ -169,10 +173,30 @@ class AbuseGpu:
         slot, n, ev = p
         try:
             ev.synchronize()
-            return self.host_out[slot][:n].numpy().copy()
+            out = self.host_out[slot][:n].numpy().copy()
+            if self.gp.ws_ok and n and np.isnan(out).any():
+                out = self._ws_fallback(slot, n)
+            return out
         finally:
             if release:
                 self._slot_locks[slot].release()
+
+    def _ws_fallback(self, slot: int, n: int) -> np.ndarray:
+        """A weight-stationary cluster launch gave up (its workgroups were not co-resident):
+        switch this model to the batch-parallel K4, re-capture, and recompute the batch."""
+        torch = self.torch
+        log.error("abuse GRU: cluster kernel timed out; falling back to the batch-parallel kernel")
+        with self._lock:
+            torch.cuda.synchronize(self.device)
+            self.gp.disable_ws()
+            b = self.bucket_for(max(n, 1))
+            with torch.cuda.stream(self.stream):
+                self._body(slot, b)
+            self.stream.synchronize()
+            out = self.host_out[slot][:n].numpy().copy()
+            self.graphs.clear()
+            self.capture()
+        return out
 
     def score_slots(self, slots: np.ndarray) -> np.ndarray:
         out = [self.wait(self.submit(slots[i:i + self.bmax])) for i in range(0, len(slots), self.bmax)]

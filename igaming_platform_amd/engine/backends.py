@@ -321,7 +321,7 @@ class GpuBackend:
             for p in pend:
                 if timeout_s is not None:
                     t_end = time.perf_counter() + timeout_s
-                    while not p.event.query():
+                    while not self.scorer.done(p):
                         if time.perf_counter() > t_end:
                             raise TimeoutError(f"GPU batch exceeded {timeout_s * 1e3:.0f} ms on {self.device}")
                         time.sleep(20e-6)

@@ -162,7 +162,7 @@ class LtvGpu:
             for b in self.buckets:
                 for slot in range(self.depth):
                     self._pack(slot, np.zeros(0, np.int32), b)
-                    s = torch.cuda.Stream(device=self.device)
+                    s = self.stream  # capture on the replay stream: no extra streams / hardware queues
                     s.wait_stream(torch.cuda.current_stream())
                     with torch.cuda.stream(s):
                         self._body(slot, b)

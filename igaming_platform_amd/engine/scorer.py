@@ -33,6 +33,7 @@ host packs batch i+1 while the GPU runs batch i.
 from __future__ import annotations
 
 import collections
+import os
 import threading
 import time
 from dataclasses import dataclass
@@ -111,6 +112,7 @@ class GpuScorer:
         self.cfg_dev = torch.zeros(176, dtype=torch.uint8, device=dev)
         self.refresh_config()
         self.graphs: Dict[tuple, tuple] = {}
+        self.driver = None
         self._slot = 0
         self._seq = 0
         self._lock = threading.Lock()
@@ -189,18 +191,24 @@ class GpuScorer:
             self.host_feat[slot][:bucket].copy_(sb.feat[:bucket], non_blocking=True)
 
     def capture(self) -> None:
-        """Capture the copy, state and model graphs per (bucket, pipeline slot); each body runs
-        once eagerly first (n = 0)."""
+        """Capture the copy, state, model and model+features graphs per (bucket, pipeline
+        slot); each body runs once eagerly first (n = 0). With the native driver
+        (csrc/kernels/driver.hip, default) every later submit is issued from C++."""
         if not self.use_graphs:
             return
+        # Each body is captured on the stream it replays on: HIP multiplexes streams onto
+        # GPU_MAX_HW_QUEUES (4) hardware queues, and throwaway capture streams shifted the copy
+        # and model streams onto ONE queue, which serialised the pipeline (rocprofv3 queue ids).
+        # With the default stream plus these three, every stream owns a queue.
         with torch.cuda.device(self.device):
             for b in self.buckets:
                 for slot in range(self.depth):
                     self._write_hdr(slot, 0, 0)
                     pair = []
-                    for body in (lambda: self._copy_body(slot, b), lambda: self._state_body(slot, b),
-                                 lambda: self._model_body(slot, b)):
-                        s = torch.cuda.Stream(device=self.device)
+                    for body, s in ((lambda: self._copy_body(slot, b), self.cstream),
+                                    (lambda: self._state_body(slot, b), self.stream),
+                                    (lambda: self._model_body(slot, b), self.mstream),
+                                    (lambda: self._model_body(slot, b, with_features=True), self.mstream)):
                         s.wait_stream(torch.cuda.current_stream())
                         with torch.cuda.stream(s):
                             body()
@@ -211,6 +219,107 @@ class GpuScorer:
                         pair.append(g)
                     self.graphs[(b, slot)] = tuple(pair)
             torch.cuda.synchronize(self.device)
+        self.driver = None
+        if os.environ.get("IGP_NATIVE_DRIVER", "1") != "0":
+            d = K._mod().PipeDriver(self.cstream.cuda_stream, self.stream.cuda_stream, self.mstream.cuda_stream,
+                                    self.depth, [t.data_ptr() for t in self.host_slab])
+            for (b, slot), g in self.graphs.items():
+                d.set_graphs(b, slot, g[0].raw_cuda_graph_exec(), g[1].raw_cuda_graph_exec(),
+                             g[2].raw_cuda_graph_exec(), g[3].raw_cuda_graph_exec())
+            self.driver = d
+
+    # ------------------------------------------------------------------ streaming (one launch per batch)
+    def capture_pipelined(self) -> None:
+        """Streaming mode: per bucket, three graphs; graph p runs copy(slot p) || state(slot
+        p-1) || model(slot p-2) on three forked capture streams, so a saturated stream costs
+        ONE hipGraphLaunch per micro-batch instead of three launches plus six event operations
+        (the host, not the GPU, bounded the three-graph pipeline: tools/host_probe.py).
+        Ordering is the graph sequence itself: launch p+1 starts after every branch of
+        launch p, which gives copy(q) -> state(q) -> model(q) and store updates in batch
+        order; dedup regions rotate as in the three-stream mode (K1 of batch q clears the
+        region of q+2, which no branch of its launch touches)."""
+        if self.depth != 3:
+            raise ValueError("streaming mode needs pipeline_depth=3")
+        if not self.graphs:
+            self.capture()  # eager warm-up of every body
+        dev = self.device
+        s0, s1, s2 = self.cstream, self.stream, self.mstream  # no extra streams (hardware queues)
+        self.pstream = s0
+        self.pgraphs: Dict[tuple, object] = {}
+        with torch.cuda.device(dev):
+            for b in self.buckets:
+                for p in range(3):
+                    g = torch.cuda.CUDAGraph()
+                    s0.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.graph(g, stream=s0):
+                        s1.wait_stream(s0)
+                        s2.wait_stream(s0)
+                        self._copy_body(p, b)
+                        with torch.cuda.stream(s1):
+                            self._state_body((p + 2) % 3, b)
+                        with torch.cuda.stream(s2):
+                            self._model_body((p + 1) % 3, b)
+                        s0.wait_stream(s1)
+                        s0.wait_stream(s2)
+                    self.pgraphs[(b, p)] = g
+            torch.cuda.synchronize(dev)
+        self._pstep = 0
+        self._pev: collections.deque = collections.deque()   # (step, event) of launches in flight
+        self._pbatch: Dict[int, tuple] = {}                   # step -> (n, bucket, t_submit)
+
+    def pipe_reserve(self, max_inflight: int = 2):
+        """Wait until at most ``max_inflight - 1`` launches are in flight, so the next step's
+        slot (its pinned slab last read by launch p-3) may be packed. Returns (slot, the
+        completions that wait produced: (n, result rows, latency_ms) per finished batch)."""
+        p = self._pstep
+        done = []
+        while self._pev and self._pev[0][0] <= p - max_inflight:
+            done += self.pipe_launch_wait()
+        return p % 3, done
+
+    def pipe_launch(self, n: int, now: int) -> None:
+        """Launch streaming step p: batch p's rows are packed in ``slab_view(p % 3, n)`` after
+        :meth:`pipe_reserve`; n = 0 launches an empty batch (drain)."""
+        p = self._pstep
+        slot = p % 3
+        b = self.bucket_for(max(n, 1))
+        # one launch runs three batches' stages: the largest of their buckets (padded rows are inert)
+        for q in (p - 1, p - 2):
+            if q in self._pbatch:
+                b = max(b, self._pbatch[q][1])
+        self._seq += 1
+        self._write_hdr(slot, n, now)
+        with torch.cuda.stream(self.pstream):
+            self.pgraphs[(b, slot)].replay()
+            ev = torch.cuda.Event()
+            ev.record(self.pstream)
+        self._pev.append((p, ev))
+        if n > 0:
+            self._pbatch[p] = (n, b, time.perf_counter())
+        self._pstep = p + 1
+        self.batches += 1
+
+    def pipe_drain(self):
+        """Two empty launches finish the batches in flight; returns their completions."""
+        done = []
+        for _ in range(2):
+            done += self.pipe_reserve()[1]
+            self.pipe_launch(0, 0)
+        while self._pev:
+            done += self.pipe_launch_wait()
+        return done
+
+    def pipe_launch_wait(self):
+        q, ev = self._pev.popleft()
+        ev.synchronize()
+        t = time.perf_counter()
+        out = []
+        bq = q - 2  # launch q finished batch q-2
+        if bq in self._pbatch:
+            nb, _, ts = self._pbatch.pop(bq)
+            # a copy: the pinned rows are overwritten by batch bq+3's D2H
+            out.append((nb, self.host_res[bq % 3][:nb].numpy().copy(), (t - ts) * 1e3))
+        return out
 
     def bucket_for(self, n: int) -> int:
         for b in self.buckets:
@@ -233,12 +342,24 @@ class GpuScorer:
             self._slot = (self._slot + 1) % self.depth
         return s
 
-    def submit_packed(self, slot: int, n: int, now: int, want_features: bool = False) -> Pending:
-        """Launch a batch whose ReqRec rows are already in ``slab_view(slot, n)``."""
+    def submit_packed(self, slot: int, n: int, now: int, want_features: bool = False,
+                      rows: Optional[np.ndarray] = None) -> Pending:
+        """Launch a batch whose ReqRec rows are already in ``slab_view(slot, n)`` (or, with the
+        native driver, are copied from ``rows`` by it)."""
         b = self.bucket_for(max(n, 1))
         self._seq += 1
-        self._write_hdr(slot, n, now)
         t0 = time.perf_counter()
+        if self.driver is not None:
+            if rows is not None:
+                rows = np.ascontiguousarray(rows)
+            self.driver.submit(slot, b, n, self._seq, int(now), 0 if rows is None else rows.ctypes.data,
+                               bool(want_features))
+            self._cur = slot
+            self.batches += 1
+            return Pending(slot, n, b, None, t0, want_features)
+        if rows is not None:
+            self.pack(slot, rows)
+        self._write_hdr(slot, n, now)
         g = self.graphs.get((b, slot))
         with torch.cuda.stream(self.cstream):
             self.cstream.wait_event(self._model_ev[slot])  # the slot's device buffers are free
@@ -293,8 +414,22 @@ class GpuScorer:
         slot = self.next_slot()
         return self.submit_packed(slot, self.pack(slot, req), now, want_features)
 
+    def submit_rows(self, slot: int, rows: np.ndarray, now: int) -> Pending:
+        """Copy REQREC ``rows`` into the slot's pinned slab and launch (the copy runs in the
+        native driver without the GIL when it is active)."""
+        if rows.dtype != REQREC:
+            rows = np.asarray(rows, REQREC)
+        return self.submit_packed(slot, len(rows), now, rows=rows)
+
+    def done(self, p: Pending) -> bool:
+        """Non-blocking completion check (the backend watchdog polls it)."""
+        return self.driver.query(p.slot) if p.event is None else p.event.query()
+
     def wait(self, p: Pending, unpack: bool = True):
-        p.event.synchronize()
+        if p.event is None:
+            self.driver.wait(p.slot)
+        else:
+            p.event.synchronize()
         res = self.host_res[p.slot][:p.n].numpy().copy()
         feats = self.host_feat[p.slot][:p.n].numpy().copy() if p.want_features else None
         if not unpack:

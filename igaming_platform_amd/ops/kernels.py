@@ -7,6 +7,8 @@ All launches go to the caller's current torch stream and are hipGraph-capturable
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional
 
 import torch
@@ -352,6 +354,19 @@ class GruPack:
         """True if a cluster launch ever timed out waiting for a non-resident member."""
         return bool(self.ws_err is not None and int(self.ws_err.item()) != 0)
 
+    def disable_ws(self) -> None:
+        """After a failed cluster launch (NaN outputs / ws_err): counters back to 0 and every
+        later launch on the batch-parallel kernel (callers re-capture their graphs)."""
+        self.ws_ok = False
+        for w in [self._ws] + self._ws_old:
+            if w is not None:
+                w["sync"].zero_()
+        if self.ws_err is not None:
+            self.ws_err.zero_()
+
+
+_GRU_WS = os.environ.get("IGP_GRU_WS", "1") != "0"  # 0: always the batch-parallel K4 (A/B runs)
+
 
 def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh: Optional[torch.Tensor] = None,
         X: Optional[torch.Tensor] = None, store=None, slots: Optional[torch.Tensor] = None,
@@ -363,7 +378,7 @@ def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh
     d = dict(n_layers=gp.n_layers, H=gp.H, T=int(T), I=gp.I, n_rows=int(n_rows),
              m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32, device=dev), tile_rows=int(tile_rows),
              waves=int(waves or gp.waves), pipeline=int(pipeline))
-    w = gp.workspace(n_rows) if ws else None
+    w = gp.workspace(n_rows) if ws and _GRU_WS else None
     if w is not None:
         d.update(ws=1, ws_clusters=w["clusters"], ws_sync=w["sync"].data_ptr(), ws_x=w["x"].data_ptr(),
                  ws_part=w["part"].data_ptr(), ws_err=gp.ws_err.data_ptr(),
