@@ -108,6 +108,7 @@ PYBIND11_MODULE(_hipk, m) {
       a.upd = update_args(d["upd"].cast<py::dict>());
       if (a.upd.region >= 0 || a.upd.dbuf != a.dbuf) throw std::runtime_error("feature_assemble: upd region");
     }
+    a.trace = ptr<int64_t*>(d, "trace");
     launch_feature_assemble(a, stream_of(s));
     check("feature_assemble");
   });

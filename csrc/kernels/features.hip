@@ -11,12 +11,15 @@
 namespace igp {
 
 // ---------------------------------------------------------------------------------- K1
-// model input l (onnx_model.go:133-184): 1 = minMaxScale(x, 0, k1_hi[l]), 2 = logTransform
-__constant__ int k1_kind[32] = {1, 1, 1, 2, 0, 1, 1, 0, 0, 1, 2, 2, 0, 0, 0, 1,
-                                0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 0, 0, 0, 0, 0};
-__constant__ float k1_hi[32] = {20.f, 50.f, 200.f, 1.f, 1.f, 10.f, 20.f, 1.f, 1.f, 365.f, 1.f, 1.f, 1.f, 1.f, 1.f,
-                                86400.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f,
-                                1.f, 1.f};
+// model input l (onnx_model.go:133-184): minMaxScale(x, 0, hi(l)) or logTransform. Selected in
+// registers: per-lane __constant__ tables were vector loads issued after the account loads, a
+// dependent memory round trip in the middle of the compute phase (tools/kbench.py trace).
+constexpr uint32_t K1_MINMAX = (1u << 0) | (1u << 1) | (1u << 2) | (1u << 5) | (1u << 6) | (1u << 9) | (1u << 15);
+constexpr uint32_t K1_LOG = (1u << 3) | (1u << 10) | (1u << 11) | (1u << 26);
+__device__ __forceinline__ float k1_hi(int l) {
+  return l == 0 ? 20.f : l == 1 ? 50.f : l == 2 ? 200.f : l == 5 ? 10.f : l == 6 ? 20.f : l == 9 ? 365.f
+       : l == 15 ? 86400.f : 1.f;
+}
 
 __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h, int c, int s, AcctRT r,
                                    int lane);
@@ -68,12 +71,11 @@ __device__ __forceinline__ bool hll_add_q(uint32_t* words, const uint32_t (&w)[4
 // and HLL registers; same arithmetic, same stored bytes. The event row is built by lanes 0..7
 // (one word each) with a single double log1p pass (lane 0: amount, lane 3: dt) and the
 // batch's precomputed hour-of-day word `hour_word` (dedup_insert_kernel).
-__device__ __forceinline__ void apply_event_q(const UpdateArgs& a, const ReqRec& ev, AcctRT r,
+__device__ __forceinline__ void apply_event_q(const UpdateArgs& a, const ScoreCfg& cfg, const ReqRec& ev, AcctRT r,
                                               const uint32_t (&wd)[4], const uint32_t (&wi)[4], int ql, int qb,
                                               uint32_t hour_word) {
   const int s = ev.slot;
   const int64_t now = event_ts(a, ev);
-  const ScoreCfg& cfg = *a.cfg;
   const int64_t amt = ev.amount;
   const int hd = r.ring_head;
   if (ql == 0) {
@@ -151,11 +153,25 @@ __device__ __forceinline__ void inert_row(const AssembleArgs& a, float* xr, int 
 // multi-event account the last request to finish its reads applies the account's events in
 // row order, with the whole wave, after every quarter of the wave is done.
 __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
+  // phase trace of 8 sample waves (wave ids 0, 293, ...): [wave][phase] wall_clock64
+  const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  int64_t* const trow = (a.trace && (threadIdx.x & 63) == 0 && gw % 293 == 0 && gw / 293 < 8) ? a.trace + (gw / 293) * 8 : nullptr;
+#define K1_MARK(k) \
+  if (trow) trow[k] = (int64_t)wall_clock64()
+  K1_MARK(0);
   const int lane = threadIdx.x & 63;
   const int ql = lane & 15, qb = lane & 48;
   const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
   const bool in_grid = row < a.n_rows;
-  const ScoreCfg& cfg = *a.cfg;
+  // the config block by value, loaded once at the top: through a reference, every field read
+  // after a store (X, FeatRec, rings) is a fresh scalar load the compiler must re-issue (it
+  // cannot prove the stores do not alias the block)
+  const ScoreCfg cfg = *a.cfg;
+  // HLL linear-counting table -> LDS, loaded beside the level-1 loads (a global lookup after
+  // the HLL sums was a dependent round trip)
+  __shared__ int s_lc[257];
+  const int lc0 = a.hll_lc[threadIdx.x];
+  const int lc1 = threadIdx.x == 0 ? a.hll_lc[256] : 0;
   // ---- level 1
   const uint4* rp = reinterpret_cast<const uint4*>(a.req + as_vgpr(in_grid ? row : 0));
   const uint4 q0 = rp[0], q1 = rp[1], q2 = rp[2];
@@ -177,6 +193,11 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
   const int seq = hv.y;
   const int64_t now = (int64_t)(((uint64_t)(uint32_t)hv.w << 32) | (uint32_t)hv.z);
   float* xr = a.X + (size_t)row * a.x_stride;
+  s_lc[threadIdx.x] = lc0;
+  if (threadIdx.x == 0) s_lc[256] = lc1;
+  __syncthreads();
+  if (trow) keep_issued(hv.x + (int)rq.slot);
+  K1_MARK(1);
   const bool padded = in_grid && row >= n_live;
   const bool foreign = in_grid && !padded && c9.z && ((rq.tx_type >> 8) & 0xff) != c9.w;
   const bool live = in_grid && !padded && !foreign;
@@ -274,6 +295,8 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       }
     }
     const bool blacklisted = qballot(hit, qb) != 0u;
+    if (trow) keep_issued((int)rt.ring_head + (int)tsv[0].x + (int)wd[0] + (int)bt.present + (int)extv[0]);
+    K1_MARK(2);
     ipf = __shfl(ipf, qb + 3, 64);
 
     // ---- window counts / sums from the tx ring
@@ -326,7 +349,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       // table (libm log, as the golden model); otherwise the harmonic estimate
       const double m = 256.0, alpha = 0.7213 / (1.0 + 1.079 / 256.0);
       const double ed = alpha * m * m / zd, ei = alpha * m * m / zi;
-      const int ld = a.hll_lc[vd], li = a.hll_lc[vi];
+      const int ld = s_lc[vd], li = s_lc[vi];
       const int cd = (ed <= 2.5 * m && vd > 0) ? ld : (int)floor(ed + 0.5);
       const int ci = (ei <= 2.5 * m && vi > 0) ? li : (int)floor(ei + 0.5);
       hll_dev = now < (int64_t)rt.hll_dev_exp ? cd : 0;
@@ -412,11 +435,10 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     IGP_PUT(29, tx_type == TX_BET ? 1.f : 0.f);
 #undef IGP_PUT
     float x0 = r0, x1 = r1;
-    const int k0 = k1_kind[ql], k1 = k1_kind[ql + 16];
-    if (k0 == 1) x0 = minmax_scale(r0, 0.f, k1_hi[ql]);
-    if (k1 == 1) x1 = minmax_scale(r1, 0.f, k1_hi[ql + 16]);
-    if (k0 == 2) x0 = log_transform(r0, id);
-    if (k1 == 2) x1 = log_transform(r1, id);
+    if ((K1_MINMAX >> ql) & 1u) x0 = minmax_scale(r0, 0.f, k1_hi(ql));
+    if ((K1_MINMAX >> (ql + 16)) & 1u) x1 = minmax_scale(r1, 0.f, k1_hi(ql + 16));
+    if ((K1_LOG >> ql) & 1u) x0 = log_transform(r0, id);
+    if ((K1_LOG >> (ql + 16)) & 1u) x1 = log_transform(r1, id);
     xr[ql] = x0;
     if (ql + 16 < 30) xr[ql + 16] = x1;
 #pragma unroll
@@ -425,6 +447,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       if (j < ext_w) xr[30 + j] = extv[u];
     }
     for (int j = ql + 112; j < ext_w; j += K1_QL) xr[30 + j] = has ? a.ext[(size_t)s * ext_w + j] : 0.f;
+    K1_MARK(3);
     if (ql == 0) a.feat[row] = f;
     clear_next_dedup(a, row, seq, ql);
 
@@ -438,7 +461,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       }
       if (h >= 0) {
         if (dcount == 1) {
-          apply_event_q(a.upd, rq, rt, wd, wi, ql, qb, hour_word);
+          apply_event_q(a.upd, cfg, rq, rt, wd, wi, ql, qb, hour_word);
         } else if (ql == 0) {
           // multi-event account: queue this row, then count it as read (its loads were all
           // consumed above); the request that completes the count applies the account's batch.
@@ -457,6 +480,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     }
   }
   // multi-event accounts completed by a quarter of this wave: applied with the whole wave
+  K1_MARK(4);
   uint64_t lm = __ballot(ql == 0 && last);
   if (lm) {
     const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
@@ -467,6 +491,11 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       apply_segment_wave(a.upd, t, hb, cb, sb, a.rt[sb], lane);
     }
   }
+  if (trow) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    K1_MARK(5);
+  }
+#undef K1_MARK
 }
 
 __global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs a) { feature_assemble_body(a); }

@@ -1,9 +1,7 @@
 #!/bin/bash
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_gpu_all.log 2>&1 || exit 1
-timeout -k 10 300 python bench.py > gpurun_out/bench_k1.log 2>&1 || exit 2
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-rm -rf $R/gpurun_out/prof_k1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_k1 -o run -- python $R/bench.py --steps 100 --warmup 10 > $R/gpurun_out/prof_k1.log 2>&1 || exit 3
+rm -rf $R/gpurun_out/prof_sweep
+timeout -k 10 300 rocprofv3 --kernel-trace -d $R/gpurun_out/prof_sweep -o run -- python $R/tools/kbench.py --rounds 3 --only h2d_slab > $R/gpurun_out/kb_sweep.log 2>&1 || exit 3

@@ -64,7 +64,8 @@ def _opt(t: Optional[torch.Tensor], name: str, **kw):
 
 # --------------------------------------------------------------------------- K1
 def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch.Tensor,
-                     X: torch.Tensor, feat: torch.Tensor, n_rows: int, dedup: bool = False) -> None:
+                     X: torch.Tensor, feat: torch.Tensor, n_rows: int, dedup: bool = False,
+                     trace: Optional[torch.Tensor] = None) -> None:
     """K1. ``dedup=True``: score-then-update. :func:`dedup_insert` must have registered the
     batch first; K1 then applies each single-event account's event and opens the segments
     that :func:`update_segments` applies afterwards (dedup ring region by batch seq)."""
@@ -86,6 +87,7 @@ def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch
         feat=_need(feat, "feat", torch.int32, 32 * n_rows, dev),
         dbuf=_need(store.dbuf, "dbuf", torch.int32) if dedup else None, dcap=int(store.dcap), dmax=int(store.dmax),
         x_stride=int(X.shape[1]), ring_size=int(store.ring_ts.shape[1]), n_rows=int(n_rows),
+        trace=_opt(trace, "trace", dtype=torch.int64, min_numel=64, device=dev),
     )
     if dedup:
         d["upd"] = update_args(store, cfg_dev, req, n_rows, hdr=hdr, region=-1)

@@ -18,13 +18,15 @@ def main():
     ap.add_argument("--accounts", type=int, default=1 << 20)
     ap.add_argument("--rounds", type=int, default=50)
     ap.add_argument("--out", default="")
+    ap.add_argument("--hot", type=float, default=0.02, help="fraction of requests on 16 hot accounts")
+    ap.add_argument("--only", default="", help="comma-separated op names to run")
     a = ap.parse_args()
     import torch
     from igaming_platform_amd.ops import kernels as K
     from igaming_platform_amd.utils import benchkit
     from igaming_platform_amd.utils.synth import NOW0
     dev = torch.device("cuda", 0)
-    S = benchkit.build(a.config, a.batch, a.accounts, dev)
+    S = benchkit.build(a.config, a.batch, a.accounts, dev, hot_frac=a.hot)
     sc, B = S.scorer, S.batch
     # load a request batch into the device slab once
     slot = 0
@@ -46,6 +48,8 @@ def main():
         "dedup_insert": lambda: K.dedup_insert(sc.store, sc.cfg_dev, sc.req, B, sc.hdr),
         "feature_assemble+single_update": lambda: K.feature_assemble(sc.store, sc.hdr, sc.cfg_dev, sc.req, sc.X,
                                                                      sc.feat, B, dedup=True),
+        "feature_assemble_no_update": lambda: K.feature_assemble(sc.store, sc.hdr, sc.cfg_dev, sc.req, sc.X,
+                                                                 sc.feat, B, dedup=False),
         "ensemble": lambda: K.ensemble(sc.hdr, sc.cfg_dev, sc.feat, sc.X, sc.ml, sc.res, B, sc.metrics),
         "update_segments": lambda: K.update_segments(sc.store, sc.cfg_dev, sc.req, B, sc.hdr),
         "d2h_results": lambda: sc.host_res[slot][:B].copy_(sc.res[:B], non_blocking=True),
@@ -58,8 +62,12 @@ def main():
         ops["mlp_head"] = lambda: K.mlp_head(head, sc.X, out, B, m_ptr=sc.n_ptr,
                                              tree_partial=(sc.tree_partial, g, tree) if tree else None)
     if sc.graphs:
-        gc, gs, gm = sc.graphs[(B, slot)]
+        gc, gs, gm = sc.graphs[(B, slot)][:3]
         ops["full_step_graph"] = lambda: (gc.replay(), gs.replay(), gm.replay())
+    ops_all = dict(ops)
+    if a.only:
+        keep = set(a.only.split(","))
+        ops = {k: v for k, v in ops.items() if k in keep}
     times = {k: [] for k in ops}
     for r in range(a.rounds):
         # a fresh batch sequence number per round, as the scorer does per micro-batch
@@ -75,6 +83,23 @@ def main():
             e1.record()
             e1.synchronize()
             times[k].append(e0.elapsed_time(e1) * 1e3)
+    # K1 phase trace of 8 sample waves (wall_clock64, 100 MHz -> us from the earliest start)
+    tr = torch.zeros(64, dtype=torch.int64, device=dev)
+    for dd in (True, False):
+        for _ in range(3):
+            sc._seq += 1
+            sc._write_hdr(slot, B, NOW0)
+            sc.dev_slab[:nb].copy_(sc.host_slab[slot][:nb])
+            if dd:
+                K.dedup_insert(sc.store, sc.cfg_dev, sc.req, B, sc.hdr)
+            tr.zero_()
+            K.feature_assemble(sc.store, sc.hdr, sc.cfg_dev, sc.req, sc.X, sc.feat, B, dedup=dd, trace=tr)
+            torch.cuda.synchronize()
+        t = tr.cpu().numpy().reshape(8, 8)[:, :6].astype(np.float64)
+        t0 = t[t > 0].min()
+        print(f"K1 trace (update={dd}) us: start / level1 / level2 / compute / stores / end")
+        for w in range(8):
+            print("   wave", w * 293, [round((x - t0) / 100.0, 2) if x > 0 else None for x in t[w]])
     res = {k: dict(median_us=float(np.median(v[5:])), min_us=float(np.min(v[5:]))) for k, v in times.items()}
     for k, v in res.items():
         print(f"{k:28s} median {v['median_us']:8.1f} us   min {v['min_us']:8.1f} us")
