@@ -66,6 +66,10 @@ def maybe_launch_torchrun(a) -> None:
 def main():
     a = parse()
     maybe_launch_torchrun(a)
+    # HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues (default 4): the scorer's
+    # copy / state / model streams, the default stream and RCCL's communication stream (N > 1)
+    # each get a queue of their own when 8 are allowed. Set before the HIP runtime initialises.
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     import torch
     import torch.distributed as dist
 
@@ -146,6 +150,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    host = sc.driver.stats() if sc.driver is not None else {}
     stats = torch.tensor([elapsed, float(np.percentile(lat, 99)), float(np.percentile(lat, 50))],
                          dtype=torch.float64, device=dev)
     if world > 1:
@@ -181,6 +186,7 @@ def main():
         "p50_latency_ms": p50,
         "latency_baseline_ms": BASELINE_P99_MS,
         "latency_vs_baseline": BASELINE_P99_MS / p99 if p99 > 0 else None,
+        "host_us_per_batch": {k: round(float(v), 2) for k, v in host.items()},
     }
     if rank == 0:
         line = json.dumps(out)

@@ -13,6 +13,9 @@
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 
+#include <dlfcn.h>
+
+#include <chrono>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -25,6 +28,35 @@ namespace py = pybind11;
 
 namespace igp {
 namespace {
+
+// roctx ranges (batch phases visible to `rocprofv3 --marker-trace`), resolved
+// lazily with dlopen so the extension has no link-time dependency on the profiler SDK
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  Roctx() {
+    void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_LOCAL);
+    if (h) {
+      push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+      pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+      if (!push || !pop) push = nullptr;
+    }
+  }
+};
+const Roctx& roctx() {
+  static Roctx r;
+  return r;
+}
+struct Range {
+  explicit Range(const char* name) : on(roctx().push != nullptr) {
+    if (on) roctx().push(name);
+  }
+  ~Range() {
+    if (on) roctx().pop();
+  }
+  bool on;
+};
 
 void hip_ok(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("PipeDriver ") + what + ": " + hipGetErrorString(e));
@@ -62,8 +94,11 @@ class PipeDriver {
     if (it == graphs_.end()) throw std::runtime_error("PipeDriver: no graphs for this bucket/slot");
     const Graphs g = it->second;
     py::gil_scoped_release nogil;
+    Range range("igp.submit");
+    const auto t0 = clk::now();
     char* slab = slabs_[slot];
     if (rows) std::memcpy(slab + sizeof(BatchHdr), reinterpret_cast<const void*>(rows), (size_t)n * sizeof(ReqRec));
+    const auto t1 = clk::now();
     BatchHdr* h = reinterpret_cast<BatchHdr*>(slab);
     h->n = n;
     h->seq = seq;
@@ -71,14 +106,28 @@ class PipeDriver {
     hipEvent_t ce = ev_[3 * slot], se = ev_[3 * slot + 1], me = ev_[3 * slot + 2];
     if (recorded_[3 * slot + 2]) hip_ok(hipStreamWaitEvent(cs_, me, 0), "wait model");
     if (hist_.size() == 2) hip_ok(hipStreamWaitEvent(cs_, ev_[3 * hist_.front() + 1], 0), "wait state-2");
+    const auto t2 = clk::now();
     hip_ok(hipGraphLaunch(g.c, cs_), "copy graph");
+    const auto t3 = clk::now();
     hip_ok(hipEventRecord(ce, cs_), "record copy");
     hip_ok(hipStreamWaitEvent(ss_, ce, 0), "wait copy");
+    const auto t4 = clk::now();
     hip_ok(hipGraphLaunch(g.s, ss_), "state graph");
+    const auto t5 = clk::now();
     hip_ok(hipEventRecord(se, ss_), "record state");
     hip_ok(hipStreamWaitEvent(ms_, se, 0), "wait state");
+    const auto t6 = clk::now();
     hip_ok(hipGraphLaunch(with_features ? g.mf : g.m, ms_), "model graph");
+    const auto t7 = clk::now();
     hip_ok(hipEventRecord(me, ms_), "record model");
+    const auto t8 = clk::now();
+    auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    st_[0] += us(t0, t1);                          // row copy
+    st_[1] += us(t1, t2) + us(t3, t4) + us(t5, t6) + us(t7, t8);  // event waits / records
+    st_[2] += us(t2, t3);                          // copy graph launch
+    st_[3] += us(t4, t5);                          // state graph launch
+    st_[4] += us(t6, t7);                          // model graph launch
+    st_[5] += 1;
     recorded_[3 * slot] = recorded_[3 * slot + 1] = recorded_[3 * slot + 2] = true;
     hist_.push_back(slot);
     if (hist_.size() > 2) hist_.erase(hist_.begin());
@@ -86,7 +135,26 @@ class PipeDriver {
 
   void wait(int slot) {
     py::gil_scoped_release nogil;
+    Range range("igp.wait");
+    const auto t0 = clk::now();
     hip_ok(hipEventSynchronize(ev_[3 * slot + 2]), "sync model");
+    st_[6] += std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+  }
+
+  // host time per submit (us): rows copy, event ops, copy / state / model graph launch, and
+  // the total blocked in wait(); reset after reading
+  py::dict stats() {
+    py::dict d;
+    const double n = st_[5] > 0 ? st_[5] : 1;
+    d["submits"] = st_[5];
+    d["rows_copy_us"] = st_[0] / n;
+    d["event_ops_us"] = st_[1] / n;
+    d["copy_launch_us"] = st_[2] / n;
+    d["state_launch_us"] = st_[3] / n;
+    d["model_launch_us"] = st_[4] / n;
+    d["wait_us"] = st_[6] / n;
+    for (double& v : st_) v = 0;
+    return d;
   }
 
   bool query(int slot) { return hipEventQuery(ev_[3 * slot + 2]) == hipSuccess; }
@@ -96,6 +164,8 @@ class PipeDriver {
   uintptr_t model_event(int slot) const { return reinterpret_cast<uintptr_t>(ev_[3 * slot + 2]); }
 
  private:
+  using clk = std::chrono::steady_clock;
+  double st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   struct Graphs {
     hipGraphExec_t c, s, m, mf;  // mf: model graph that also copies the FeatRec rows to the host
   };
@@ -118,7 +188,8 @@ void register_driver(py::module_& m) {
       .def("submit", &PipeDriver::submit)
       .def("wait", &PipeDriver::wait)
       .def("query", &PipeDriver::query)
-      .def("model_event", &PipeDriver::model_event);
+      .def("model_event", &PipeDriver::model_event)
+      .def("stats", &PipeDriver::stats);
 }
 
 }  // namespace igp
