@@ -107,14 +107,23 @@ def main():
     gathered = torch.zeros(world * B * 2, dtype=torch.int32, device=dev) if world > 1 else None
     met_sum = torch.zeros(128, dtype=torch.int64, device=dev)
 
+    gather_work = {}  # slot -> async all_gather still reading that slot's result rows
+
     def step(i: int, now: int):
         slot = sc.next_slot()
+        if slot in gather_work:
+            # the slot's result rows are rewritten by this batch's model graph: the model stream
+            # waits for the gather that read them (issued `depth` batches ago, long finished),
+            # so the collective never sits on the model stream's critical path
+            with torch.cuda.stream(sc.mstream):
+                gather_work.pop(slot).wait()
         # the wire decoder's output (raw REQREC rows) -> pinned slab -> three graphs; with the
         # native driver (default) the row copy and every launch are issued from C++
         p = sc.submit_rows(slot, pool[i % len(pool)], now)
         if world > 1 and not a.no_gather:
             with torch.cuda.stream(sc.mstream):  # results / metrics live on the model stream
-                dist.all_gather_into_tensor(gathered, sc.slots[slot].res[:B].reshape(-1))
+                gather_work[slot] = dist.all_gather_into_tensor(gathered, sc.slots[slot].res[:B].reshape(-1),
+                                                                async_op=True)
                 if i % 16 == 15:
                     met_sum.copy_(sc.metrics)
                     dist.all_reduce(met_sum)
@@ -146,6 +155,9 @@ def main():
     for q in inflight:
         sc.wait(q, unpack=False)
         lat.append((time.perf_counter() - q.t_submit) * 1e3)
+    for w in gather_work.values():
+        w.wait()
+    gather_work.clear()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
