@@ -70,12 +70,15 @@ __device__ __forceinline__ bf16x8 wfrag(const uint16_t* p, int nt, int KS, int k
 // L = 0: A = [x_t | h1_{t-1}] (1 + 8 k-steps); L = 1: A = [h1_{t-1} | h2_{t-2}] (8 + 8).
 // x-part -> ax (the input half of h~), h-part -> ah (recurrent half, scaled by r): LBR = 1.
 // The A fragments of k-step ks+1 are read from LDS before the MFMAs of ks are issued (the
-// weights hold ~200 VGPRs, so without an explicit prefetch one A buffer serialises LDS latency
-// against every three MFMAs).
+// weights hold ~200 registers, so without an explicit prefetch one A buffer serialises LDS
+// latency against every three MFMAs). Software-pipelined over row-tile pairs: the gate
+// epilogue (exp / rcp / fma, ~20 VALU per element) of pair p-1 is placed beside the MFMAs of
+// pair p, so it issues in the MFMA pipe's free VALU slots instead of after them (the
+// accumulators are double-buffered in AGPRs).
 template <int L>
-__device__ __forceinline__ void ws_layer(const bf16x8 (&wz)[16], const bf16x8 (&wr)[16], const bf16x8 (&wh)[16],
-                                         const uint16_t* X, const uint16_t* H1, const uint16_t* H2,
-                                         float (&hs)[WS_RT][4], const float (&bv)[4], int lane) {
+__device__ __forceinline__ void ws_mfma_pair(const bf16x8 (&wz)[16], const bf16x8 (&wr)[16], const bf16x8 (&wh)[16],
+                                             const uint16_t* X, const uint16_t* H1, const uint16_t* H2, int rt0,
+                                             int lane, f32x4 (&acc)[4][2]) {
   constexpr int NK = L == 0 ? 9 : 16;  // k-steps
   constexpr int NX = L == 0 ? 1 : 8;   // k-steps of the input part
   const int arow = lane & 15, akof = 8 * (lane >> 4);
@@ -89,38 +92,54 @@ __device__ __forceinline__ void ws_layer(const bf16x8 (&wz)[16], const bf16x8 (&
     }
   };
 #pragma unroll
-  for (int rt0 = 0; rt0 < WS_RT; rt0 += 2) {
-    f32x4 az[2], ar[2], ax[2], ah[2];
+  for (int g = 0; g < 4; ++g)
 #pragma unroll
-    for (int u = 0; u < 2; ++u) az[u] = ar[u] = ax[u] = ah[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 cur[2] = {afrag(0, rt0), afrag(0, rt0 + 1)};
+    for (int u = 0; u < 2; ++u) acc[g][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 cur[2] = {afrag(0, rt0), afrag(0, rt0 + 1)};
 #pragma unroll
-    for (int ks = 0; ks < NK; ++ks) {
-      bf16x8 nxt[2] = {cur[0], cur[1]};
-      if (ks + 1 < NK) {
-        nxt[0] = afrag(ks + 1, rt0);
-        nxt[1] = afrag(ks + 1, rt0 + 1);
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        az[u] = MFMA(cur[u], wz[ks], az[u]);
-        ar[u] = MFMA(cur[u], wr[ks], ar[u]);
-        if (ks < NX) ax[u] = MFMA(cur[u], wh[ks], ax[u]);
-        else ah[u] = MFMA(cur[u], wh[ks], ah[u]);
-      }
-      cur[0] = nxt[0];
-      cur[1] = nxt[1];
+  for (int ks = 0; ks < NK; ++ks) {
+    bf16x8 nxt[2] = {cur[0], cur[1]};
+    if (ks + 1 < NK) {
+      nxt[0] = afrag(ks + 1, rt0);
+      nxt[1] = afrag(ks + 1, rt0 + 1);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float z = sig_(az[u][r] + bv[0]);
-        const float rr = sig_(ar[u][r] + bv[1]);
-        const float hh = tanh_(ax[u][r] + bv[2] + rr * (ah[u][r] + bv[3]));
-        hs[rt0 + u][r] = (1.f - z) * hh + z * hs[rt0 + u][r];
-      }
+    for (int u = 0; u < 2; ++u) {
+      acc[0][u] = MFMA(cur[u], wz[ks], acc[0][u]);
+      acc[1][u] = MFMA(cur[u], wr[ks], acc[1][u]);
+      if (ks < NX) acc[2][u] = MFMA(cur[u], wh[ks], acc[2][u]);
+      else acc[3][u] = MFMA(cur[u], wh[ks], acc[3][u]);
+    }
+    cur[0] = nxt[0];
+    cur[1] = nxt[1];
   }
+}
+
+__device__ __forceinline__ void ws_epilogue(const f32x4 (&acc)[4][2], float (&hs)[WS_RT][4], const float (&bv)[4],
+                                            int rt0) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float z = sig_(acc[0][u][r] + bv[0]);
+      const float rr = sig_(acc[1][u][r] + bv[1]);
+      const float hh = tanh_(acc[2][u][r] + bv[2] + rr * (acc[3][u][r] + bv[3]));
+      hs[rt0 + u][r] = (1.f - z) * hh + z * hs[rt0 + u][r];
+    }
+}
+
+template <int L>
+__device__ __forceinline__ void ws_layer(const bf16x8 (&wz)[16], const bf16x8 (&wr)[16], const bf16x8 (&wh)[16],
+                                         const uint16_t* X, const uint16_t* H1, const uint16_t* H2,
+                                         float (&hs)[WS_RT][4], const float (&bv)[4], int lane) {
+  f32x4 acc[2][4][2];
+  ws_mfma_pair<L>(wz, wr, wh, X, H1, H2, 0, lane, acc[0]);
+#pragma unroll
+  for (int p = 1; p < WS_RT / 2; ++p) {
+    ws_mfma_pair<L>(wz, wr, wh, X, H1, H2, 2 * p, lane, acc[p & 1]);
+    ws_epilogue(acc[(p - 1) & 1], hs, bv, 2 * (p - 1));
+  }
+  ws_epilogue(acc[(WS_RT / 2 - 1) & 1], hs, bv, WS_RT - 2);
 }
 #undef MFMA
 
