@@ -33,12 +33,39 @@ constexpr int K1_QL = 16;  // lanes per request
 
 __device__ __forceinline__ uint32_t qballot(bool p, int qb) { return (uint32_t)(__ballot(p) >> qb) & 0xffffu; }
 
+// DPP lane moves inside a 16-lane row (= one request's quarter): no LDS round trip, unlike
+// __shfl_xor (ds_bpermute, ~100 cycles per dependent step; K1 had ~100 of them).
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL, class T>
+__device__ __forceinline__ T dpp_t(T v) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "dpp_t: 4- or 8-byte values");
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, dpp_i<CTRL>(__builtin_bit_cast(int, v)));
+  } else {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = dpp_i<CTRL>((int)b), hi = dpp_i<CTRL>((int)(b >> 32));
+    return __builtin_bit_cast(T, (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+  }
+}
+constexpr int DPP_QUAD_X1 = 0xB1;     // quad_perm [1,0,3,2]: partner lane ^ 1
+constexpr int DPP_QUAD_X2 = 0x4E;     // quad_perm [2,3,0,1]: partner lane ^ 2
+constexpr int DPP_HALF_MIRROR = 0x141;  // lane i <-> 7 - i within 8: the other quad
+constexpr int DPP_MIRROR = 0x140;       // lane i <-> 15 - i within 16: the other half
+constexpr int DPP_SHR2 = 0x112;         // lane i <- lane i - 2 (row_shr:2)
+constexpr int DPP_SHL2 = 0x102;         // lane i <- lane i + 2 (row_shl:2)
+
+// sum over the 16 lanes of a quarter; every lane gets the sum. After the two quad steps all
+// lanes of a quad hold the same value, so the mirror partners add the same pairs as the xor
+// butterfly (1, 2, 4, 8) did: results are bit-identical, floating point included.
 template <class T>
 __device__ __forceinline__ T qsum(T v) {
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
+  v += dpp_t<DPP_QUAD_X1>(v);
+  v += dpp_t<DPP_QUAD_X2>(v);
+  v += dpp_t<DPP_HALF_MIRROR>(v);
+  v += dpp_t<DPP_MIRROR>(v);
   return v;
 }
 
@@ -437,8 +464,16 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     float x0 = r0, x1 = r1;
     if ((K1_MINMAX >> ql) & 1u) x0 = minmax_scale(r0, 0.f, k1_hi(ql));
     if ((K1_MINMAX >> (ql + 16)) & 1u) x1 = minmax_scale(r1, 0.f, k1_hi(ql + 16));
-    if ((K1_LOG >> ql) & 1u) x0 = log_transform(r0, id);
-    if ((K1_LOG >> (ql + 16)) & 1u) x1 = log_transform(r1, id);
+    // one divergent log1p pass for the quarter instead of two: lanes 3, 10, 11 transform their
+    // x0; input 26 (x1 of lane 10) is moved to lane 12, transformed there and moved back
+    static_assert(K1_LOG == ((1u << 3) | (1u << 10) | (1u << 11) | (1u << 26)), "log lanes moved");
+    const bool lg0 = (K1_LOG >> ql) & 1u;
+    const float in26 = dpp_t<DPP_SHR2>(r1);  // lane 12 <- lane 10's x1 input
+    const float lin = lg0 ? r0 : in26;
+    const float lout = (lg0 || ql == 12) ? log_transform(lin, id) : 0.f;
+    const float lout26 = dpp_t<DPP_SHL2>(lout);  // lane 10 <- lane 12
+    if (lg0) x0 = lout;
+    if (ql == 10) x1 = lout26;
     xr[ql] = x0;
     if (ql + 16 < 30) xr[ql + 16] = x1;
 #pragma unroll

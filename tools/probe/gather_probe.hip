@@ -28,6 +28,8 @@ struct Tabs {
   const int* slots;   // [B]
   float* out;         // [B]
   int B;
+  float* X;           // [B][128] model-input rows (K1 output shape)
+  uint4* feat;        // [B][8] 128-B FeatRec rows
 };
 
 template <int V>
@@ -38,7 +40,7 @@ __global__ void __launch_bounds__(256) gather(Tabs t) {
   const int s = t.slots[row];
   uint32_t acc = 0;
   float facc = 0.f;
-  if (V == 0 || V == 2 || V == 4) {  // ring
+  if (V == 0 || V == 2 || V == 4 || V == 6) {  // ring
     uint4 a[4], b[8];
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i] = t.ts[(size_t)s * 64 + ql + 16 * i];
@@ -49,7 +51,7 @@ __global__ void __launch_bounds__(256) gather(Tabs t) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc += b[i].y;
   }
-  if (V == 0 || V == 3) {  // HLL 8 x 4 B, ext 7 x 4 B (K1's shapes)
+  if (V == 0 || V == 3 || V == 6) {  // HLL 8 x 4 B, ext 7 x 4 B (K1's shapes)
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc += t.hll[(size_t)s * 128 + ql + 16 * i];
 #pragma unroll
@@ -63,7 +65,7 @@ __global__ void __launch_bounds__(256) gather(Tabs t) {
     const float4 e0 = e4[ql], e1 = e4[min(16 + ql, 24)];
     facc += e0.x + e1.y;
   }
-  if (V == 0 || V == 1 || V == 4) {  // account rows (every lane of the quarter loads them)
+  if (V == 0 || V == 1 || V == 4 || V == 6) {  // account rows (every lane of the quarter loads them)
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc += t.rt[(size_t)s * 4 + i].x;
 #pragma unroll
@@ -72,6 +74,18 @@ __global__ void __launch_bounds__(256) gather(Tabs t) {
   facc += (float)acc;
 #pragma unroll
   for (int o = 1; o < 16; o <<= 1) facc += __shfl_xor(facc, o, 64);
+  if (V >= 5) {  // K1's output stores: X row (30 + 98 floats, 4 B lanes) + FeatRec by one lane
+    float* xr = t.X + (size_t)row * 128;
+    xr[ql] = facc;
+    if (ql + 16 < 30) xr[ql + 16] = facc;
+#pragma unroll
+    for (int u = 0; u < 7; ++u)
+      if (ql + 16 * u < 98) xr[30 + ql + 16 * u] = facc + u;
+    if (ql == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t.feat[(size_t)row * 8 + k] = make_uint4(acc, k, 0, 0);
+    }
+  }
   if (ql == 0) t.out[row] = facc;
 }
 
@@ -103,7 +117,7 @@ float time_variant(Tabs t, hipStream_t st, int reps) {
 int main(int argc, char** argv) {
   const size_t C = argc > 1 ? std::atol(argv[1]) : (1 << 20);
   const int B = 8192, reps = 50;
-  void *ts, *amt, *hll, *ext, *rt, *bat, *slots, *out;
+  void *ts, *amt, *hll, *ext, *rt, *bat, *slots, *out, *X, *feat;
   CK(hipMalloc(&ts, C * 1024));
   CK(hipMalloc(&amt, C * 2048));
   CK(hipMalloc(&hll, C * 512));
@@ -112,6 +126,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&bat, C * 80));
   CK(hipMalloc(&slots, (size_t)(reps + 5) * B * 4));
   CK(hipMalloc(&out, B * 4));
+  CK(hipMalloc(&X, (size_t)B * 512));
+  CK(hipMalloc(&feat, (size_t)B * 128));
   CK(hipMemset(ts, 1, C * 1024));
   CK(hipMemset(amt, 2, C * 2048));
   CK(hipMemset(hll, 3, C * 512));
@@ -121,7 +137,7 @@ int main(int argc, char** argv) {
   hipStream_t st;
   CK(hipStreamCreate(&st));
   Tabs t{(const uint4*)ts, (const uint4*)amt, (const uint32_t*)hll, (const float*)ext, (const uint4*)rt,
-         (const uint4*)bat, (const int*)slots, (float*)out, B};
+         (const uint4*)bat, (const int*)slots, (float*)out, B, (float*)X, (uint4*)feat};
   std::mt19937_64 g(1);
   std::vector<int> hs((size_t)(reps + 5) * B);
   for (int round = 0; round < 2; ++round) {
@@ -133,6 +149,8 @@ int main(int argc, char** argv) {
     std::printf("  ring only (3 KiB)                 %7.2f\n", time_variant<2>(t, st, reps));
     std::printf("  hll+ext only (4-B lanes)          %7.2f\n", time_variant<3>(t, st, reps));
     std::printf("  full, hll/ext as 16-B loads       %7.2f\n", time_variant<4>(t, st, reps));
+    std::printf("  stores only (X row + FeatRec)     %7.2f\n", time_variant<5>(t, st, reps));
+    std::printf("  full loads + K1 stores            %7.2f\n", time_variant<6>(t, st, reps));
   }
   return 0;
 }
