@@ -197,6 +197,9 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
   // HLL linear-counting table -> LDS, loaded beside the level-1 loads (a global lookup after
   // the HLL sums was a dependent round trip)
   __shared__ int s_lc[257];
+  // per-request staging of the X row (30 + up to 112 ext floats) and the FeatRec
+  __shared__ __attribute__((aligned(16))) float s_xst[16][144];
+  __shared__ __attribute__((aligned(16))) uint2 s_fst[16][16];
   const int lc0 = a.hll_lc[threadIdx.x];
   const int lc1 = threadIdx.x == 0 ? a.hll_lc[256] : 0;
   // ---- level 1
@@ -474,16 +477,32 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     const float lout26 = dpp_t<DPP_SHL2>(lout);  // lane 10 <- lane 12
     if (lg0) x0 = lout;
     if (ql == 10) x1 = lout26;
-    xr[ql] = x0;
-    if (ql + 16 < 30) xr[ql + 16] = x1;
+    // X row and FeatRec go out through LDS as whole words: written directly, the ext part (offset
+    // 30 floats) straddled cache lines in 9 partial 4-B store instructions per wave and the
+    // FeatRec left as 8 single-lane 16-B stores; staged, a wave writes its 4 rows in 2 x 16-B and
+    // 1 x 8-B store instructions over contiguous memory
+    float* const sx = s_xst[threadIdx.x >> 4];
+    sx[ql] = x0;
+    if (ql + 16 < 30) sx[ql + 16] = x1;
 #pragma unroll
     for (int u = 0; u < 7; ++u) {
       const int j = ql + 16 * u;
-      if (j < ext_w) xr[30 + j] = extv[u];
+      if (j < ext_w) sx[30 + j] = extv[u];
+    }
+    if (ql == 0) *reinterpret_cast<FeatRec*>(s_fst[threadIdx.x >> 4]) = f;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int wst = 30 + min(ext_w, 112);
+    if (((wst | (int)a.x_stride) & 3) == 0) {
+      for (int c = ql; c < (wst >> 2); c += K1_QL)
+        reinterpret_cast<float4*>(xr)[c] = reinterpret_cast<const float4*>(sx)[c];
+    } else {
+      for (int c = ql; c < wst; c += K1_QL) xr[c] = sx[c];
     }
     for (int j = ql + 112; j < ext_w; j += K1_QL) xr[30 + j] = has ? a.ext[(size_t)s * ext_w + j] : 0.f;
     K1_MARK(3);
-    if (ql == 0) a.feat[row] = f;
+    reinterpret_cast<uint2*>(a.feat + row)[ql] = s_fst[threadIdx.x >> 4][ql];
     clear_next_dedup(a, row, seq, ql);
 
     // ---- score-then-update (engine.go:486-488)

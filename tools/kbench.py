@@ -100,7 +100,7 @@ def main():
         print(f"K1 trace (update={dd}) us: start / level1 / level2 / compute / stores / end")
         for w in range(8):
             print("   wave", w * 293, [round((x - t0) / 100.0, 2) if x > 0 else None for x in t[w]])
-    res = {k: dict(median_us=float(np.median(v[5:])), min_us=float(np.min(v[5:]))) for k, v in times.items()}
+    res = {k: dict(median_us=float(np.median(v[min(5, len(v) - 1):])), min_us=float(np.min(v[min(5, len(v) - 1):]))) for k, v in times.items()}
     for k, v in res.items():
         print(f"{k:28s} median {v['median_us']:8.1f} us   min {v['min_us']:8.1f} us")
     if a.out:
