@@ -109,6 +109,10 @@ PYBIND11_MODULE(_hipk, m) {
       if (a.upd.region >= 0 || a.upd.dbuf != a.dbuf) throw std::runtime_error("feature_assemble: upd region");
     }
     a.trace = ptr<int64_t*>(d, "trace");
+    {
+      const char* xe = getenv("IGP_K1_EXP");
+      a.exp_flags = xe ? atoi(xe) : 0;
+    }
     launch_feature_assemble(a, stream_of(s));
     check("feature_assemble");
   });
@@ -141,6 +145,7 @@ PYBIND11_MODULE(_hipk, m) {
     a.all_positive = geti(d, "all_positive", 1);
     a.no_finish = geti(d, "no_finish", 0);
     a.all_leq = geti(d, "all_leq", 0);
+    a.trace = ptr<int64_t*>(d, "trace");
     const int groups = geti(d, "groups", 1);
     launch_tree_ensemble_grouped(a, groups, ptr<float*>(d, "partial"), stream_of(s));
     check("tree_ensemble");
@@ -196,6 +201,7 @@ PYBIND11_MODULE(_hipk, m) {
     a.groups = geti(d, "groups", 1);
     a.p_average = geti(d, "p_average", 0);
     a.p_ntrees = geti(d, "p_ntrees", 1);
+    a.trace = ptr<int64_t*>(d, "trace");
     if (a.k_pad % 32 || a.k_pad < a.K) throw std::runtime_error("mlp_head: k_pad must be a multiple of 32 >= K");
     launch_mlp_head(a, stream_of(s));
     check("mlp_head");

@@ -6,6 +6,8 @@
 //   write path  redis_store.go:119-168
 //   rules       scoring/engine.go:420-483
 //   blacklist   redis_store.go:267-293
+#include <stdexcept>
+
 #include "update.h"
 
 namespace igp {
@@ -146,23 +148,6 @@ __device__ __forceinline__ void apply_event_q(const UpdateArgs& a, const ScoreCf
   if (ql == 0) a.rt[s] = r;
 }
 
-// clear this request's slice of batch seq+2's dedup region (after the request's loads)
-__device__ __forceinline__ void clear_next_dedup(const AssembleArgs& a, int row, int seq, int ql) {
-  if (a.dbuf) {
-    const DedupTab nt = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq + 2));
-    const int chunk = (a.dcap + a.n_rows - 1) / a.n_rows;
-    const int e0 = row * chunk, e1 = min(a.dcap, e0 + chunk);
-    for (int e = e0 + ql; e < e1; e += K1_QL) {
-      nt.keys[e] = -1;
-      nt.first[e] = 0x7fffffff;
-      nt.count[e] = 0;
-      nt.fill[e] = 0;
-      nt.done[e] = 0;
-    }
-    if (row == 0 && ql < 2) nt.ctr[ql] = 0;
-  }
-}
-
 // inert row (graph padding / another rank's request): zero inputs, FeatRec with slot -1
 __device__ __forceinline__ void inert_row(const AssembleArgs& a, float* xr, int row, int ql, int ext_w, int flag) {
   for (int j = ql; j < 30 + ext_w; j += K1_QL) xr[j] = 0.f;
@@ -175,10 +160,12 @@ __device__ __forceinline__ void inert_row(const AssembleArgs& a, float* xr, int 
 // level costs microseconds): level 1 = the request row + batch header + config words; level 2
 // = everything the row addresses (ts ring, amounts, HLL registers, account rows, ext row, dedup
 // probe, blacklist / ip-intel first probe slot), issued branch-free before the first use.
-// Score-then-update: dedup_insert_kernel registered the batch first; a request whose account
-// has no other event in the batch applies its event right after its own reads; for a
-// multi-event account the last request to finish its reads applies the account's events in
-// row order, with the whole wave, after every quarter of the wave is done.
+// Score-then-update: dedup_insert_list_kernel registered the batch first; a request whose
+// account has no other event in the batch applies its event right after its own reads; the
+// accounts with several events are applied after K1 by update_multi_kernel, in row order. (An
+// in-kernel hand-off - the last request of an account to finish its reads applies the
+// account's events - put chains of device-scope atomics and dependent loads at the end of
+// K1: a 20 us tail behind 14 us of work at B=8192.)
 __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
   // phase trace of 8 sample waves (wave ids 0, 293, ...): [wave][phase] wall_clock64
   const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -233,9 +220,8 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
   const bool live = in_grid && !padded && !foreign;
   if (padded || foreign) {
     inert_row(a, xr, row, ql, ext_w, foreign ? FR_NOT_OWNED : 0);
-    clear_next_dedup(a, row, seq, ql);
   }
-  int last = 0, h = -1, s = -1, dcount = 0;
+  int h = -1, s = -1, dcount = 0;
   if (live) {
     s = rq.slot;
     const int64_t amount = rq.amount;
@@ -246,16 +232,9 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     const int rs = a.ring_size;  // multiple of 64: lane ql holds entries 4 (ql + 16 i) .. +3
     const int n4 = rs / 4;
     const uint4* ts4 = reinterpret_cast<const uint4*>(a.ring_ts + (size_t)sc * rs);
-    const longlong2* am2 = reinterpret_cast<const longlong2*>(a.ring_amt + (size_t)sc * rs);
     uint4 tsv[4];
-    longlong2 am[8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = min(ql + 16 * i, n4 - 1);
-      tsv[i] = ts4[e];
-      am[2 * i] = am2[2 * e];
-      am[2 * i + 1] = am2[2 * e + 1];
-    }
+    for (int i = 0; i < 4; ++i) tsv[i] = ts4[min(ql + 16 * i, n4 - 1)];
     const uint32_t* hreg = reinterpret_cast<const uint32_t*>(a.hll + (size_t)sc * 512);
     uint32_t wd[4], wi[4];
 #pragma unroll
@@ -334,22 +313,30 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     long long s60 = 0;
     int hll_dev = 0, hll_ip = 0;
     if (has) {
+      // the amount ring (2 KB per account, half the bytes K1 gathers) is read only where the ts
+      // ring shows an entry inside the hour, and not at all for the compat (INCRBY) sum: a
+      // third dependent level in exchange for ~half the HBM traffic of the gather (same-box
+      // A/B, cfg3 bench: 109.6 vs 106.1 M scores/s for the full-ring load)
+      const int64_t* amp = a.ring_amt + (size_t)s * rs;
+      const bool want_amt = !cfg.sum_compat;
+      long long av[16];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t tv[4] = {tsv[i].x, tsv[i].y, tsv[i].z, tsv[i].w};
-        const long long av[4] = {am[2 * i].x, am[2 * i].y, am[2 * i + 1].x, am[2 * i + 1].y};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int64_t t = (int64_t)tv[j];
-          const bool v = t != 0;
+          const bool v = t != 0 && ql + 16 * i < n4;  // rings < 256 entries: clamped lanes are copies
           c1 += v && t >= now - 60;
           c5 += v && t >= now - 300;
           const bool in1h = v && t >= now - 3600;
           c60 += in1h;
-          s60 += in1h ? av[j] : 0;
+          av[4 * i + j] = 0;
+          if (in1h && want_amt) av[4 * i + j] = amp[4 * (ql + 16 * i) + j];
         }
       }
-      const int64_t* amp = a.ring_amt + (size_t)s * rs;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s60 += av[k];
       for (int q = 256 + ql; q < rs; q += K1_QL) {  // rings longer than 256 entries (rare)
         const int64_t t = (int64_t)a.ring_ts[(size_t)s * rs + q];
         if (t != 0) {
@@ -503,7 +490,6 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     for (int j = ql + 112; j < ext_w; j += K1_QL) xr[30 + j] = has ? a.ext[(size_t)s * ext_w + j] : 0.f;
     K1_MARK(3);
     reinterpret_cast<uint2*>(a.feat + row)[ql] = s_fst[threadIdx.x >> 4][ql];
-    clear_next_dedup(a, row, seq, ql);
 
     // ---- score-then-update (engine.go:486-488)
     if (a.dbuf && has) {
@@ -516,35 +502,11 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       if (h >= 0) {
         if (dcount == 1) {
           apply_event_q(a.upd, cfg, rq, rt, wd, wi, ql, qb, hour_word);
-        } else if (ql == 0) {
-          // multi-event account: queue this row, then count it as read (its loads were all
-          // consumed above); the request that completes the count applies the account's batch.
-          // Hand-off without an L2 writeback fence (MI355X_MICROARCH.md, sc1 table, first row):
-          // the list entry is an sc1 store drained by vmcnt(0) before the agent-scope add, and
-          // the wave whose add returns the last count reads the list with sc1 loads. (A
-          // __threadfence here wrote back the XCD's dirty L2 - every X / FeatRec row of the
-          // batch - once per multi-event row.)
-          const int pos = atomicAdd(&t.fill[h], 1);
-          if (pos < DEDUP_LIST)
-            __hip_atomic_store(&t.list[(size_t)h * DEDUP_LIST + pos], row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          last = atomicAdd(&t.done[h], 1) == dcount - 1;
         }
       }
     }
   }
-  // multi-event accounts completed by a quarter of this wave: applied with the whole wave
   K1_MARK(4);
-  uint64_t lm = __ballot(ql == 0 && last);
-  if (lm) {
-    const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
-    while (lm) {
-      const int src = __ffsll((long long)lm) - 1;
-      lm &= lm - 1;
-      const int hb = __shfl(h, src, 64), cb = __shfl(dcount, src, 64), sb = __shfl(s, src, 64);
-      apply_segment_wave(a.upd, t, hb, cb, sb, a.rt[sb], lane);
-    }
-  }
   if (trow) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     K1_MARK(5);
@@ -579,6 +541,37 @@ __global__ void dedup_insert_kernel(UpdateArgs a) {
   if (i >= upd_n(a)) return;
   const ReqRec& r = a.req[i];
   if (r.slot >= 0 && row_owned(r, *a.cfg)) dedup_insert(upd_region(a), r.slot, i);
+}
+
+// Scorer head: register the batch's events in its dedup region (cleared two batches ahead by
+// update_multi_kernel) and build, for every account, its row list (position = the count its
+// row's add returned) and the list of multi-event accounts (added by the account's second
+// row). One thread per row, 64-thread workgroups spread over the chip: the kernel is a chain
+// of memory-side atomics (CAS, add, add), not work.
+__global__ void __launch_bounds__(64) dedup_insert_list_kernel(UpdateArgs a) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  const DedupTab t = upd_region(a);
+  // the batch clock's hour-of-day event-row word (sin/cos in double), once per batch for K1
+  if (i == 0) t.ctr[1] = (int32_t)event_word(4, 0, 0, a.hdr->now, 0, false, false);
+  if (i >= upd_n(a)) return;
+  const int2 r = *reinterpret_cast<const int2*>(a.req + i);  // {slot, tx_type}
+  const ScoreCfg& cfg = *a.cfg;
+  if (r.x < 0 || (cfg.owner_filter && ((r.y >> 8) & 0xff) != cfg.my_rank)) return;
+  uint32_t h = mix32((uint32_t)r.x) & (uint32_t)(t.cap - 1);
+  for (int p = 0; p < t.cap; ++p) {
+    const int prev = atomicCAS(&t.keys[h], -1, r.x);
+    if (prev == -1 || prev == r.x) {
+      atomicMin(&t.first[h], i);
+      const int pos = atomicAdd(&t.count[h], 1);
+      if (pos < DEDUP_LIST) t.list[(size_t)h * DEDUP_LIST + pos] = i;
+      if (pos == 1) {
+        const int m = atomicAdd(&t.ctr[0], 1);
+        if (m < t.nmax) t.mlist[m] = (int)h;
+      }
+      return;
+    }
+    h = (h + 1) & (uint32_t)(t.cap - 1);
+  }
 }
 
 __global__ void update_single_kernel(UpdateArgs a) {
@@ -717,17 +710,33 @@ __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h
 }
 
 // standalone ingestion: one wave per multi-event account listed by update_single
+constexpr int UPD_MULTI_BLOCKS = 64;  // 256 waves loop over the list (any count, no big grid)
 __global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
   const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const DedupTab t = upd_region(a);
-  if (w >= min(t.ctr[0], t.nmax)) return;
-  const int h = t.mlist[w];
-  if (h < 0 || h >= t.cap) return;
-  const int c = t.count[h];
-  const int s = t.keys[h];
-  if (c < 2 || s < 0) return;
-  apply_segment_wave(a, t, h, c, s, a.rt[s], lane);
+  const int nm = min(t.ctr[0], t.nmax);
+  for (int w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); w < nm;
+       w += UPD_MULTI_BLOCKS * 4) {
+    const int h = t.mlist[w];
+    if (h < 0 || h >= t.cap) continue;
+    const int c = t.count[h];
+    const int s = t.keys[h];
+    if (c < 2 || s < 0) continue;
+    apply_segment_wave(a, t, h, c, s, a.rt[s], lane);
+  }
+  // scorer ring: clear the region of batch seq+2 (= seq-1's, consumed by now) for its insert;
+  // the copy of batch seq+2 waits for this batch's state graph
+  if (a.region < 0) {
+    const DedupTab nt = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(a.hdr->seq + 2));
+    const int4 m1 = make_int4(-1, -1, -1, -1), big = make_int4(0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff);
+    const int4 z = make_int4(0, 0, 0, 0);
+    for (int e4 = blockIdx.x * 256 + threadIdx.x; e4 < (nt.cap >> 2); e4 += UPD_MULTI_BLOCKS * 256) {
+      reinterpret_cast<int4*>(nt.keys)[e4] = m1;
+      reinterpret_cast<int4*>(nt.first)[e4] = big;
+      reinterpret_cast<int4*>(nt.count)[e4] = z;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) nt.ctr[0] = 0;
+  }
 }
 
 // ---------------------------------------------------------------------------------- launch
@@ -738,13 +747,14 @@ void launch_feature_assemble(const AssembleArgs& a, hipStream_t st) {
 
 void launch_dedup_insert(const UpdateArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
-  hipLaunchKernelGGL(dedup_insert_kernel, dim3((a.n_max + 255) / 256), dim3(256), 0, st, a);
+  if (!a.hdr || a.region >= 0 || (a.dcap & 3)) throw std::runtime_error("dedup_insert: scorer ring regions only");
+  hipLaunchKernelGGL(dedup_insert_list_kernel, dim3((a.n_max + 63) / 64), dim3(64), 0, st, a);
 }
 
 void launch_update_segments(const UpdateArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
-  // at most n/2 accounts can have >= 2 events: one wave each
-  hipLaunchKernelGGL(update_multi_kernel, dim3((a.n_max / 2 + 3) / 4 + 1), dim3(256), 0, st, a);
+  // one wave per multi-event account, 256 waves looping over the region's list
+  hipLaunchKernelGGL(update_multi_kernel, dim3(UPD_MULTI_BLOCKS), dim3(256), 0, st, a);
 }
 
 void launch_feature_update(const UpdateArgs& a, hipStream_t st) {

@@ -205,7 +205,40 @@ __device__ __forceinline__ uint4 head_a_chunk(const HeadArgs& a, int row, int kc
   float f[8];
   if (a.partial) {
     // reduce the tree ensemble's group partials: sum_g P[g][row][k] (+ base, / T)
-    if (kc + 8 <= a.K && (a.K & 3) == 0) {
+    if (kc + 8 <= a.K && (a.K & 3) == 0 && a.groups <= 8) {
+      // straight-line: every group's pair of 16-B loads (clamped group index) and the base
+      // values in flight at once (a loop waited per group), summed in group order as before
+      const int gl = a.groups - 1;
+      float4 p[8], q[8];
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const float4* src = reinterpret_cast<const float4*>(a.partial + ((size_t)min(g, gl) * a.M + row) * a.K + kc);
+        p[g] = src[0];
+        q[g] = src[1];
+      }
+      float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
+      if (a.pbase) {
+        b0 = reinterpret_cast<const float4*>(a.pbase + kc)[0];
+        b1 = reinterpret_cast<const float4*>(a.pbase + kc)[1];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        if (g <= gl) {
+          f[0] += p[g].x; f[1] += p[g].y; f[2] += p[g].z; f[3] += p[g].w;
+          f[4] += q[g].x; f[5] += q[g].y; f[6] += q[g].z; f[7] += q[g].w;
+        }
+      }
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (a.p_average) f[j] /= (float)a.p_ntrees;
+        f[j] += bb[j];  // 0 without a base: x + 0 == x
+      }
+      return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
+                        pack_bf16x2(f[6], f[7]));
+    } else if (kc + 8 <= a.K && (a.K & 3) == 0) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = 0.f;
       for (int g = 0; g < a.groups; ++g) {
@@ -256,16 +289,51 @@ __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a, int w_lds) {
   uint16_t* sW = sA + HD_ROWS * lds_row;
   float* sred = reinterpret_cast<float*>(smem + (((size_t)(HD_ROWS + (w_lds ? n1p : 0)) * lds_row * 2 + 15) &
                                                  ~size_t(15)));
+  float* sb1 = sred + 4 * HD_ROWS;  // [n1p] b1, then [n1p] w2 (zero past N1)
+  float* sw2 = sb1 + n1p;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int M = a.m_ptr ? min(*a.m_ptr, a.M) : a.M;
   const int row0 = blockIdx.x * HD_ROWS;
   if (row0 >= M) return;
+  int64_t* const trow = (a.trace && tid == 0 && (blockIdx.x & 31) == 0 && blockIdx.x < 256) ? a.trace + (blockIdx.x >> 5) * 8 : nullptr;
+#define HD_MARK(k) \
+  if (trow) trow[k] = (int64_t)wall_clock64()
+  HD_MARK(0);
   const int kch = kp / 8;  // 16-byte chunks per row
-  // stage W1 (all loads of a thread in flight before its stores) and the A tile
-  if (w_lds) {
-    constexpr int UN = 4;
-    const int total = n1p * kch;
-    for (int base = 0; base < total; base += 256 * UN) {
+  // stage W1, b1 / w2 and the A tile with one memory round trip in the common case: the first
+  // W1 pass, the head vectors and the first A chunk are all issued before anything is stored
+  // (b1 / w2 used to be global loads inside the column loop: one dependent round trip per
+  // 64-column chunk)
+  constexpr int UN = 4;
+  const int wtotal = w_lds ? n1p * kch : 0;
+  uint4 wv[UN];
+#pragma unroll
+  for (int u = 0; u < UN; ++u) {
+    const int ch = u * 256 + tid;
+    wv[u] = ch < wtotal ? *reinterpret_cast<const uint4*>(a.W1 + (size_t)(ch / kch) * kp + (ch % kch) * 8)
+                        : make_uint4(0, 0, 0, 0);
+  }
+  const float b1v = (tid < a.N1 && a.b1) ? a.b1[tid] : 0.f;
+  const float w2v = tid < a.N1 ? a.w2[tid] : 0.f;
+  const int ach = HD_ROWS * kch;
+  const uint4 av = tid < ach ? head_a_chunk(a, row0 + tid / kch, (tid % kch) * 8, M) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int u = 0; u < UN; ++u) {
+    const int ch = u * 256 + tid;
+    if (ch < wtotal) *reinterpret_cast<uint4*>(&sW[(ch / kch) * lds_row + (ch % kch) * 8]) = wv[u];
+  }
+  if (tid < n1p) {
+    sb1[tid] = b1v;
+    sw2[tid] = w2v;
+  }
+  for (int n = tid + 256; n < n1p; n += 256) {
+    sb1[n] = (n < a.N1 && a.b1) ? a.b1[n] : 0.f;
+    sw2[n] = n < a.N1 ? a.w2[n] : 0.f;
+  }
+  if (tid < ach) *reinterpret_cast<uint4*>(&sA[(tid / kch) * lds_row + (tid % kch) * 8]) = av;
+  if (wtotal > 256 * UN) {
+    const int total = wtotal;
+    for (int base = 256 * UN; base < total; base += 256 * UN) {
       uint4 v[UN];
 #pragma unroll
       for (int u = 0; u < UN; ++u) {
@@ -280,11 +348,12 @@ __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a, int w_lds) {
       }
     }
   }
-  for (int ch = tid; ch < HD_ROWS * kch; ch += 256) {
+  for (int ch = tid + 256; ch < ach; ch += 256) {
     const int r = ch / kch, kc = (ch % kch) * 8;
     *reinterpret_cast<uint4*>(&sA[r * lds_row + kc]) = head_a_chunk(a, row0 + r, kc, M);
   }
   __syncthreads();
+  HD_MARK(1);
   float part[2][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -303,9 +372,8 @@ __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a, int w_lds) {
         acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[i], 0, 0, 0);
       }
     }
-    const bool ok = n < a.N1;
-    const float b1 = ok && a.b1 ? a.b1[n] : 0.f;
-    const float w2 = ok ? a.w2[n] : 0.f;
+    const float b1 = sb1[n];
+    const float w2 = sw2[n];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -329,7 +397,9 @@ __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a, int w_lds) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) sred[wave * HD_ROWS + i * 16 + (lane >> 4) * 4 + q] = part[i][q];
   }
+  HD_MARK(2);
   __syncthreads();
+  HD_MARK(3);
   if (tid < HD_ROWS) {
     const int row = row0 + tid;
     if (row < M) {
@@ -337,6 +407,11 @@ __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a, int w_lds) {
       a.Y[(size_t)row * a.ldy] = act_fn(v + a.b2, a.act2);
     }
   }
+  if (trow) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    HD_MARK(4);
+  }
+#undef HD_MARK
 }
 
 void launch_mlp_head(const HeadArgs& a, hipStream_t st) {
@@ -345,7 +420,7 @@ void launch_mlp_head(const HeadArgs& a, hipStream_t st) {
   const size_t n1p = (size_t)((a.N1 + 63) & ~63);
   const int w_lds = n1p * lds_row * 2 <= (size_t)HD_W_LDS_MAX;
   const size_t lds = ((((size_t)HD_ROWS + (w_lds ? n1p : 0)) * lds_row * 2 + 15) & ~size_t(15)) +
-                     4 * HD_ROWS * sizeof(float);
+                     4 * HD_ROWS * sizeof(float) + 2 * n1p * sizeof(float);
   hipLaunchKernelGGL(mlp_head_kernel, dim3((a.M + HD_ROWS - 1) / HD_ROWS), dim3(256), lds, st, a, w_lds);
 }
 

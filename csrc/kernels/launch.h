@@ -69,6 +69,7 @@ struct AssembleArgs {
   // each wave applies its request's event when it is the account's only one in the batch
   // and opens the segment of a multi-event account (applied by update_segments after K1)
   UpdateArgs upd;
+  int32_t exp_flags;        // A/B experiment bits for same-box comparisons (env IGP_K1_EXP); none defined
 };
 
 
@@ -100,6 +101,7 @@ struct TreeArgs {
   int32_t all_positive;
   int32_t no_finish;        // grouped launch: leave partials for the consumer (mlp_head)
   int32_t all_leq;          // every node BRANCH_LEQ (fast decision path; missing tracks allowed)
+  int64_t* trace;           // nullable: phase trace of sample blocks (tools/tree_bench.py)
 };
 void launch_tree_ensemble(const TreeArgs& a, hipStream_t st);
 void launch_tree_ensemble_grouped(const TreeArgs& a, int groups, float* partial, hipStream_t st);
@@ -138,6 +140,7 @@ struct HeadArgs {
   int32_t groups;
   int32_t p_average;
   int32_t p_ntrees;
+  int64_t* trace;           // nullable: phase trace of 8 sample blocks (tools/kbench.py)
 };
 void launch_mlp_head(const HeadArgs& a, hipStream_t st);
 

@@ -90,6 +90,12 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
   const int n_leaf = 1 << a.depth;
   const size_t node_b = ((size_t)trees_per_group * n_int * 8 + 15) & ~size_t(15);
   uint16_t* sleaf = reinterpret_cast<uint16_t*>(smem + base_b + (nodes_in_lds ? node_b : 0));
+  // phase trace: wave 0 of blocks x = 0, 64 of groups 0..3: [sample][phase] wall_clock64
+  const int tsmp = g * 2 + (blockIdx.x >> 6);
+  int64_t* const trow = (a.trace && tid == 0 && (blockIdx.x & 63) == 0 && tsmp < 8) ? a.trace + tsmp * 8 : nullptr;
+#define TR_MARK(k) \
+  if (trow) trow[k] = (int64_t)wall_clock64()
+  TR_MARK(0);
 
   // stage the X tile and the group's node table: the first chunk of both is loaded with every
   // load of a thread in flight (one memory round trip instead of one per chunk), then stored
@@ -160,6 +166,7 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
     }
   }
   __syncthreads();
+  TR_MARK(1);
   const float2* nodes = nodes_in_lds ? sn : gn;
   const float* xrow = sx + lane * xs;
 
@@ -205,68 +212,82 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
       }
     }
   }
+  TR_MARK(2);
   __syncthreads();
+  TR_MARK(3);
   float* red = sx;  // reuse the X tile region: [5][64][K] (K < 16) or [64][K] (two-phase)
   if constexpr (TWO_PHASE) {
-    // phase 2: lanes over targets, coalesced leaf rows
-    constexpr int SPP = 256 / K;  // samples per pass
-    const int k = tid % K, sp = tid / K;
+    // phase 2: lanes over 16-B column chunks of the targets, K/4 lanes read one whole leaf row
+    // (coalesced). 16-B loads: a quarter of the load instructions of one-target-per-lane, so
+    // the same bytes need a quarter of the dependent L2 round trips (the step count, not
+    // bandwidth, sets the time: the leaves are L2 hits)
+    constexpr int LPR = K / 4;          // lanes per row
+    constexpr int SPP = 256 / LPR;      // samples per pass
+    const int k4 = tid % LPR, sp = tid / LPR;
     const bool rowwise = !partial && (a.post == 2 || a.binary_class >= 0);
-    // each thread owns target k of rows sp, sp + SPP, ...: all its rows advance through the
-    // trees together, so every step has RPT x 4 independent leaf loads in flight (the loads are
-    // L2 hits; the step count, not bandwidth, sets the time). Per row the trees are still
-    // summed in order t0, t0+1, ...
+    // each thread owns columns 4 k4 .. 4 k4 + 3 of rows sp, sp + SPP, ...: its rows advance
+    // through the trees together, RPT x TU independent loads in flight per step. Per row the
+    // trees are still summed in order t0, t0+1, ... (same sums as a scalar loop)
     constexpr int RPT = TR_ROWS / SPP;  // rows per thread
-    float v[RPT];
+    float4 v[RPT];
 #pragma unroll
-    for (int j = 0; j < RPT; ++j) v[j] = 0.f;
-    // leaf loads through a buffer resource: per-lane offset (leaf, k) in a VGPR, the tree's
+    for (int j = 0; j < RPT; ++j) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // leaf loads through a buffer resource: per-lane offset (leaf, k4) in a VGPR, the tree's
     // base (uniform) in an SGPR offset
     const float* lbase = a.leaves + (size_t)t0 * n_leaf * K;
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(lbase), 0, nt * n_leaf * K * 4, 0x00020000);
     const int tstride = n_leaf * K * 4;  // bytes per tree
-    constexpr int TU = RPT >= 8 ? 4 : 8;  // trees per step: RPT x TU loads in flight
+    constexpr int TU = RPT >= 4 ? 4 : 8;  // trees per step
+    auto ld = [&](int l, int t) {
+      return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, (l * K + 4 * k4) * 4, t * tstride, 0));
+    };
     int t = 0;
     for (; t + TU <= nt; t += TU) {
-      float p[RPT][TU];
+      float4 p[RPT][TU];
 #pragma unroll
       for (int j = 0; j < RPT; ++j) {
         const uint16_t* li = sleaf + (sp + j * SPP) * nt + t;
 #pragma unroll
-        for (int u = 0; u < TU; ++u)
-          p[j][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                        rsrc, ((int)li[u] * K + k) * 4, (t + u) * tstride, 0));
+        for (int u = 0; u < TU; ++u) p[j][u] = ld((int)li[u], t + u);
       }
 #pragma unroll
       for (int j = 0; j < RPT; ++j)
 #pragma unroll
-        for (int u = 0; u < TU; ++u) v[j] += p[j][u];
+        for (int u = 0; u < TU; ++u) {
+          v[j].x += p[j][u].x; v[j].y += p[j][u].y; v[j].z += p[j][u].z; v[j].w += p[j][u].w;
+        }
     }
     for (; t < nt; ++t) {
 #pragma unroll
       for (int j = 0; j < RPT; ++j) {
-        const int l = sleaf[(sp + j * SPP) * nt + t];
-        v[j] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (l * K + k) * 4, t * tstride, 0));
+        const float4 q = ld((int)sleaf[(sp + j * SPP) * nt + t], t);
+        v[j].x += q.x; v[j].y += q.y; v[j].z += q.z; v[j].w += q.w;
       }
     }
+    TR_MARK(4);
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
       const int r = sp + j * SPP;
       const int row = row0 + r;
-      float vv = v[j];
       if (row >= a.n_rows) continue;
       if (partial) {
-        partial[((size_t)g * a.n_rows + row) * K + k] = vv;
+        *reinterpret_cast<float4*>(partial + ((size_t)g * a.n_rows + row) * K + 4 * k4) = v[j];
       } else if (rowwise) {
-        red[r * K + k] = vv;
+        *reinterpret_cast<float4*>(red + r * K + 4 * k4) = v[j];
       } else {
-        if (a.average) vv /= (float)a.n_trees;
-        if (a.base) vv += a.base[k];
-        if (a.post == 1) vv = 1.f / (1.f + expf(-vv));
-        a.out[(size_t)row * a.n_out + k] = vv;
+        float vv[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int k = 4 * k4 + c;
+          if (a.average) vv[c] /= (float)a.n_trees;
+          if (a.base) vv[c] += a.base[k];
+          if (a.post == 1) vv[c] = 1.f / (1.f + expf(-vv[c]));
+          a.out[(size_t)row * a.n_out + k] = vv[c];
+        }
       }
     }
+    TR_MARK(5);
     if (!rowwise) return;
     __syncthreads();
     for (int r = tid; r < TR_ROWS; r += 256) {
@@ -295,6 +316,8 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
     }
   }
 }
+
+#undef TR_MARK
 
 __global__ void tree_finish_kernel(TreeArgs a, const float* partial, int groups) {
   const int row = blockIdx.x * blockDim.x + threadIdx.x;

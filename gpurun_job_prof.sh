@@ -1,4 +1,7 @@
 #!/bin/bash
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python bench.py > gpurun_out/bench_host.log 2>&1 || exit 1
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+rm -rf $R/gpurun_out/prof_b
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $R/gpurun_out/prof_b -o run -- python $R/bench.py --steps 300 --warmup 50 > $R/gpurun_out/prof_b.log 2>&1 || exit 3

@@ -4,24 +4,26 @@ One micro-batch = three captured hipGraphs on three HIP streams:
 
   copy stream
     H2D  pinned slab [BatchHdr | ReqRec x n] -> the slot's device slab      (one copy)
-    K6a  dedup insert: the batch's accounts -> its dedup ring region
+    K6a  dedup insert: the batch's accounts -> its dedup ring region, with per-account row
+         lists and the list of accounts with several events in the batch
   state stream (owns the HBM feature store; batches run strictly in submit order)
     K1   feature_assemble (+blacklist, +ip-intel, +HLL counts, +rules) -> X, FeatRec, then
-         score-then-update: a wave applies its event when its account has no other event in
-         the batch; for a multi-event account the last wave to finish its reads applies the
-         account's events in row order
+         score-then-update of every account with one event in the batch
+    K6b  update_multi: the multi-event accounts' events in row order (one wave each), then
+         clear the dedup region of batch seq+2
   model stream (reads only the slot's X / FeatRec; never touches the store)
     K2/K3 model steps of the compiled ONNX plan                            -> ml
     K5   ensemble + action (+K10 metrics histogram)                        -> ResultRec
     D2H  ResultRec [n] -> pinned result buffer                             (one copy)
 
 Score-then-update (engine.go:486-488) needs only the batch's own requests and the state K1
-read, so the whole store read-modify-write finishes inside K1, and the next batch's K1 starts
-while this batch's trees / MLP / ensemble still run on the model stream; its copy
+read, so the whole store read-modify-write finishes in the state graph, and the next batch's
+K1 starts while this batch's trees / MLP / ensemble still run on the model stream; its copy
 and dedup insert run even earlier, under this batch's K1 (dedup regions rotate over three by
-batch seq; K1 of batch q clears the region of batch q+2, so the copy of batch q waits for the
-state graph of batch q-2). Each pipeline slot has its own device slab, X, FeatRec, result and
-model activation buffers; a slot is reused only after the model graph that last read it.
+batch seq; the state graph of batch q clears the region of batch q+2, so the copy of batch q
+waits for the state graph of batch q-2). Each pipeline slot has its own device slab, X,
+FeatRec, result and model activation buffers; a slot is reused only after the model graph
+that last read it.
 
 Graphs are captured per (batch bucket, pipeline slot); a batch is padded to the smallest
 bucket >= n and kernels read the live count and the clock from the device header, so padded
@@ -179,6 +181,8 @@ class GpuScorer:
     def _state_body(self, slot: int, bucket: int) -> None:
         sb, upd = self.slots[slot], self.update_features
         K.feature_assemble(self.store, sb.hdr, self.cfg_dev, sb.req, sb.X, sb.feat, bucket, dedup=upd)
+        if upd:
+            K.update_segments(self.store, self.cfg_dev, sb.req, bucket, sb.hdr)
 
     def _model_body(self, slot: int, bucket: int, with_features: bool = False) -> None:
         sb = self.slots[slot]

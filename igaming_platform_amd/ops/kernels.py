@@ -126,14 +126,16 @@ def feature_update(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, 
 
 
 def dedup_insert(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, hdr: torch.Tensor) -> None:
-    """Scorer head: register the batch's accounts in its dedup region (before K1)."""
+    """Scorer head: register the batch's accounts in its dedup region (before K1), with the
+    per-account row lists and the multi-event account list :func:`update_segments` reads."""
     d = update_args(store, cfg_dev, req, n_max, hdr=hdr, region=-1)
     d["insert_only"] = 1
     _mod().feature_update(d, _stream())
 
 
 def update_segments(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, hdr: torch.Tensor) -> None:
-    """Scorer tail: ordered apply of multi-event accounts (insert before K1, singles in K1)."""
+    """Scorer tail (after K1): ordered apply of the multi-event accounts (insert before K1,
+    single-event accounts in K1), then clear the dedup region of batch seq+2."""
     d = update_args(store, cfg_dev, req, n_max, hdr=hdr, region=-1)
     d["segments_only"] = 1
     _mod().feature_update(d, _stream())
@@ -141,8 +143,10 @@ def update_segments(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int,
 
 # --------------------------------------------------------------------------- K2
 def tree_ensemble(tp, X: torch.Tensor, out: Optional[torch.Tensor], n_rows: int,
-                  partial: Optional[torch.Tensor] = None, groups: int = 1, no_finish: bool = False) -> None:
-    """``tp``: models.plan.TreeStep with device tensors."""
+                  partial: Optional[torch.Tensor] = None, groups: int = 1, no_finish: bool = False,
+                  trace: Optional[torch.Tensor] = None) -> None:
+    """``tp``: models.plan.TreeStep with device tensors. ``trace``: int64 [64] phase timestamps
+    (wall_clock64) of 8 sample workgroups, for tools/tree_bench.py."""
     dev = X.device
     if tp.k not in (1, 2, 4, 8, 16, 32, 64):
         raise ValueError(f"tree kernel built for K in 1,2,4,8,16,32,64; got {tp.k}")
@@ -161,7 +165,7 @@ def tree_ensemble(tp, X: torch.Tensor, out: Optional[torch.Tensor], n_rows: int,
         n_rows=int(n_rows), n_trees=tp.n_trees, depth=tp.depth, k=tp.k, n_out=tp.n_out, post=tp.post,
         average=tp.average, binary_class=tp.binary_class, all_positive=tp.all_positive,
         groups=int(groups), partial=_opt(partial, "partial", dtype=torch.float32), no_finish=int(no_finish),
-        all_leq=int(tp.all_leq),
+        all_leq=int(tp.all_leq), trace=_opt(trace, "trace", dtype=torch.int64, min_numel=64),
     )
     if tp.nodes.numel() < tp.n_trees * ((1 << tp.depth) - 1) * 2:
         raise ValueError("node table smaller than n_trees * (2^depth - 1)")
@@ -201,7 +205,7 @@ def dense(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], Y: tor
 
 
 def mlp_head(hs, X: Optional[torch.Tensor], Y: torch.Tensor, M: int, m_ptr: Optional[torch.Tensor] = None,
-             tree_partial=None) -> None:
+             tree_partial=None, trace: Optional[torch.Tensor] = None) -> None:
     """``hs``: models.plan.HeadStep. Y[:M, 0] = act2(act1(X W1^T + b1) . w2 + b2).
     ``tree_partial=(slab, groups, tree_step)``: X is the preceding tree ensemble's unreduced
     group partials [groups, M, K]; the head reduces them while staging (no finisher launch)."""
@@ -230,6 +234,8 @@ def mlp_head(hs, X: Optional[torch.Tensor], Y: torch.Tensor, M: int, m_ptr: Opti
         d.update(partial=_need(slab, "partial", torch.float32, groups * M * hs.k, dev), ldx=hs.k,
                  pbase=_opt(ts.base, "pbase", dtype=torch.float32, min_numel=hs.k), groups=int(groups),
                  p_average=int(ts.average), p_ntrees=int(ts.n_trees))
+    if trace is not None:
+        d["trace"] = _need(trace, "trace", torch.int64, 64, dev)
     _mod().mlp_head(d, _stream())
 
 

@@ -19,9 +19,10 @@ def _txs(n, rng, n_acc=40):
             for a in rng.integers(0, n_acc, n)]
 
 
-def _engines(**kw):
+def _engines(ring_size=256, **kw):
     from igaming_platform_amd.engine.risk_engine import RiskEngine
     cfg = Config()
+    cfg.features.ring_size = ring_size
     cfg.gpu.buckets = [64, 256, 1024]
     cfg.gpu.max_batch = 1024
     g = RiskEngine(cfg, backend="gpu", capacity=4096, **kw)
@@ -42,10 +43,11 @@ def _engines(**kw):
     return g, c
 
 
-def test_gpu_engine_matches_cpu_engine_heuristic():
-    g, c = _engines()
+@pytest.mark.parametrize("ring_size", [256, 64])
+def test_gpu_engine_matches_cpu_engine_heuristic(ring_size):
+    g, c = _engines(ring_size)
     rng = np.random.default_rng(1)
-    for step in range(5):
+    for step in range(5 if ring_size == 256 else 10):  # 64: ~75 events per account, the ring wraps
         txs = _txs(300, rng)
         a = g.score(txs, now=NOW + step * 30)
         b = c.score(txs, now=NOW + step * 30)

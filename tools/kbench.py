@@ -100,6 +100,48 @@ def main():
         print(f"K1 trace (update={dd}) us: start / level1 / level2 / compute / stores / end")
         for w in range(8):
             print("   wave", w * 293, [round((x - t0) / 100.0, 2) if x > 0 else None for x in t[w]])
+    # K1 with the update on rotating pool batches (the bench's access pattern): event timing
+    # of the kernel alone + phase trace of the last one
+    for var in os.environ.get("KB_K1_MODES", "full").split(","):  # full | nodedup | noseg
+      ts_k1 = []
+      for i in range(24):
+          vv = sc.slab_view(slot, B)
+          vv[:] = S.pool[i % len(S.pool)]
+          vv["ts"] = NOW0 + 1 + i
+          sc._seq += 1
+          sc._write_hdr(slot, B, NOW0 + 1 + i)
+          sc.dev_slab[:nb].copy_(sc.host_slab[slot][:nb])
+          if var != "nodedup":
+              K.dedup_insert(sc.store, sc.cfg_dev, sc.req, B, sc.hdr)
+          tr.zero_()
+          e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+          e0.record()
+          K.feature_assemble(sc.store, sc.hdr, sc.cfg_dev, sc.req, sc.X, sc.feat, B, dedup=var != "nodedup", trace=tr)
+          e1.record()
+          e1.synchronize()
+          ts_k1.append(e0.elapsed_time(e1) * 1e3)
+          if var not in ("nodedup", "noseg"):
+              K.update_segments(sc.store, sc.cfg_dev, sc.req, B, sc.hdr)
+      print(f"[{var}] K1+update on rotating pool batches: median {np.median(ts_k1[8:]):.1f} us (first pass {np.median(ts_k1[:8]):.1f})")
+      t = tr.cpu().numpy().reshape(8, 8)[:, :6].astype(np.float64)
+      t0 = t[t > 0].min()
+      print("K1 trace (update, rotating batches) us: start / level1 / level2 / compute / stores / end")
+      for w in range(8):
+          print("   wave", w * 293, [round((x - t0) / 100.0, 2) if x > 0 else None for x in t[w]])
+    # mlp_head (8 sample blocks) phase trace
+    tr = torch.zeros(64, dtype=torch.int64, device=dev)
+    if head is not None:
+        for _ in range(3):
+            tr.zero_()
+            ops["mlp_head"]() if "mlp_head" in ops else None
+            K.mlp_head(head, sc.X, sc.step_out[-1], B, m_ptr=sc.n_ptr,
+                       tree_partial=(sc.tree_partial, g, tree) if tree else None, trace=tr)
+            torch.cuda.synchronize()
+        t = tr.cpu().numpy().reshape(8, 8)[:, :5].astype(np.float64)
+        t0 = t[t > 0].min()
+        print("mlp_head trace us: start / staged / mfma done / synced / stored")
+        for b in range(8):
+            print("   block", b * 32, [round((x - t0) / 100.0, 2) if x > 0 else None for x in t[b]])
     res = {k: dict(median_us=float(np.median(v[min(5, len(v) - 1):])), min_us=float(np.min(v[min(5, len(v) - 1):]))) for k, v in times.items()}
     for k, v in res.items():
         print(f"{k:28s} median {v['median_us']:8.1f} us   min {v['min_us']:8.1f} us")
