@@ -28,6 +28,20 @@ int32_t geti(const py::dict& d, const char* k, int32_t def = 0) {
 
 hipStream_t stream_of(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+EnsembleArgs ensemble_args(const py::dict& d) {
+  EnsembleArgs a{};
+  a.hdr = ptr<const BatchHdr*>(d, "hdr");
+  a.cfg = ptr<const ScoreCfg*>(d, "cfg");
+  a.feat = ptr<const FeatRec*>(d, "feat");
+  a.X = ptr<const float*>(d, "X");
+  a.x_stride = geti(d, "x_stride");
+  a.ml = ptr<const float*>(d, "ml");
+  a.out = ptr<ResultRec*>(d, "out");
+  a.metrics = ptr<unsigned long long*>(d, "metrics");
+  a.n_rows = geti(d, "n_rows");
+  return a;
+}
+
 UpdateArgs update_args(const py::dict& d) {
   UpdateArgs a{};
   a.cfg = ptr<const ScoreCfg*>(d, "cfg");
@@ -202,22 +216,18 @@ PYBIND11_MODULE(_hipk, m) {
     a.p_average = geti(d, "p_average", 0);
     a.p_ntrees = geti(d, "p_ntrees", 1);
     a.trace = ptr<int64_t*>(d, "trace");
+    if (d.contains("ens") && !d["ens"].is_none()) {
+      a.fuse_ens = 1;
+      a.ens = ensemble_args(d["ens"].cast<py::dict>());
+      if (!a.ens.hdr || !a.ens.cfg || !a.ens.feat || !a.ens.out) throw std::runtime_error("mlp_head: ensemble args");
+    }
     if (a.k_pad % 32 || a.k_pad < a.K) throw std::runtime_error("mlp_head: k_pad must be a multiple of 32 >= K");
     launch_mlp_head(a, stream_of(s));
     check("mlp_head");
   });
 
   m.def("ensemble", [](py::dict d, uintptr_t s) {
-    EnsembleArgs a{};
-    a.hdr = ptr<const BatchHdr*>(d, "hdr");
-    a.cfg = ptr<const ScoreCfg*>(d, "cfg");
-    a.feat = ptr<const FeatRec*>(d, "feat");
-    a.X = ptr<const float*>(d, "X");
-    a.x_stride = geti(d, "x_stride");
-    a.ml = ptr<const float*>(d, "ml");
-    a.out = ptr<ResultRec*>(d, "out");
-    a.metrics = ptr<unsigned long long*>(d, "metrics");
-    a.n_rows = geti(d, "n_rows");
+    const EnsembleArgs a = ensemble_args(d);
     launch_ensemble(a, stream_of(s));
     check("ensemble");
   });

@@ -7,6 +7,7 @@
 // bias + activation are fused into the epilogue. 4 waves in a 2x2 arrangement, BK = 64,
 // two LDS buffers: tile k+1 is loaded to registers while tile k's MFMAs run.
 #include "common.h"
+#include "ensemble.h"
 #include "launch.h"
 
 namespace igp {
@@ -294,7 +295,16 @@ __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a, int w_lds) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int M = a.m_ptr ? min(*a.m_ptr, a.M) : a.M;
   const int row0 = blockIdx.x * HD_ROWS;
-  if (row0 >= M) return;
+  __shared__ unsigned int ecnt[MET_N];  // fused K5 metrics
+  const bool fm = a.fuse_ens && a.ens.metrics;
+  if (row0 >= M) {
+    // past the live rows: the fused ensemble still writes the inert rows' (zero) results
+    if (a.fuse_ens)
+      for (int r = row0 + tid; r < min(row0 + HD_ROWS, a.ens.n_rows); r += 256) ensemble_row(a.ens, r, true, 0.f, nullptr);
+    return;
+  }
+  if (fm)
+    for (int i = tid; i < MET_N; i += 256) ecnt[i] = 0;
   int64_t* const trow = (a.trace && tid == 0 && (blockIdx.x & 31) == 0 && blockIdx.x < 256) ? a.trace + (blockIdx.x >> 5) * 8 : nullptr;
 #define HD_MARK(k) \
   if (trow) trow[k] = (int64_t)wall_clock64()
@@ -402,10 +412,17 @@ __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a, int w_lds) {
   HD_MARK(3);
   if (tid < HD_ROWS) {
     const int row = row0 + tid;
+    float y = 0.f;
     if (row < M) {
       const float v = sred[tid] + sred[HD_ROWS + tid] + sred[2 * HD_ROWS + tid] + sred[3 * HD_ROWS + tid];
-      a.Y[(size_t)row * a.ldy] = act_fn(v + a.b2, a.act2);
+      y = act_fn(v + a.b2, a.act2);
+      a.Y[(size_t)row * a.ldy] = y;
     }
+    if (a.fuse_ens && row < a.ens.n_rows) ensemble_row(a.ens, row, true, y, fm ? ecnt : nullptr);
+  }
+  if (fm) {
+    __syncthreads();
+    ensemble_metrics_flush(a.ens, ecnt, tid, 256);
   }
   if (trow) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

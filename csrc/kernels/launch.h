@@ -122,6 +122,18 @@ void launch_gemm(const GemmArgs& a, hipStream_t st);
 void launch_gemv(const GemmArgs& a, hipStream_t st);  // N == 1 heads
 
 // dense(N1) + act1 + dense(N1 -> 1) + act2 fused; W1 bf16 [N1_pad(64)][k_pad(32)]
+// ---- K5 ensemble + action + metrics
+struct EnsembleArgs {
+  const BatchHdr* hdr;
+  const ScoreCfg* cfg;
+  const FeatRec* feat;
+  const float* X;           // for the heuristic model
+  int32_t x_stride;
+  const float* ml;          // model output (nullable)
+  ResultRec* out;
+  unsigned long long* metrics;  // [128] score histogram(101) | actions(4) | ml_high | rows (nullable)
+  int32_t n_rows;
+};
 struct HeadArgs {
   const void* X;
   const uint16_t* W1;
@@ -141,21 +153,13 @@ struct HeadArgs {
   int32_t p_average;
   int32_t p_ntrees;
   int64_t* trace;           // nullable: phase trace of 8 sample blocks (tools/kbench.py)
+  // optional fused K5: each block runs the ensemble of its rows on the Y values it computed
+  // (ml = Y[row], the plan's ml_col 0); the standalone ensemble launch is then skipped
+  int32_t fuse_ens;
+  EnsembleArgs ens;
 };
 void launch_mlp_head(const HeadArgs& a, hipStream_t st);
 
-// ---- K5 ensemble + action + metrics
-struct EnsembleArgs {
-  const BatchHdr* hdr;
-  const ScoreCfg* cfg;
-  const FeatRec* feat;
-  const float* X;           // for the heuristic model
-  int32_t x_stride;
-  const float* ml;          // model output (nullable)
-  ResultRec* out;
-  unsigned long long* metrics;  // [128] score histogram(101) | actions(4) | ml_high | rows (nullable)
-  int32_t n_rows;
-};
 void launch_ensemble(const EnsembleArgs& a, hipStream_t st);
 
 // ---- K4 GRU sequence (recurrent weights resident in VGPRs)

@@ -63,9 +63,19 @@ class DeviceModel:
     def out_width(self) -> int:
         return self.plan.out_width
 
-    def run(self, X: torch.Tensor, bucket: int, m_ptr: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """X: [rows, in] f32 (or [T, rows, I] for a GRU model); returns the last step's buffer."""
+    def fuses_ensemble(self) -> bool:
+        """Whether :meth:`run` can run the scorer's K5 ensemble in the epilogue of its last step
+        (an N=1 MLP head whose output column is the model score)."""
         steps = self.plan.steps
+        return (self.gru is None and bool(steps) and steps[-1].kind == "head" and self.plan.ml_col == 0)
+
+    def run(self, X: torch.Tensor, bucket: int, m_ptr: Optional[torch.Tensor] = None,
+            ens: Optional[dict] = None) -> torch.Tensor:
+        """X: [rows, in] f32 (or [T, rows, I] for a GRU model); returns the last step's buffer.
+        ``ens`` (only when :meth:`fuses_ensemble`): K5 arguments for the fused head epilogue."""
+        steps = self.plan.steps
+        if ens is not None and not self.fuses_ensemble():
+            raise ValueError("this plan cannot fuse the ensemble")
         if self.gru is not None:
             T = X.shape[0]
             if self.gru.head_w is not None:
@@ -86,7 +96,8 @@ class DeviceModel:
             elif s.kind == "dense":
                 K.dense(cur, s.w, s.b, out, bucket, s.n, s.k, act=s.act, m_ptr=m_ptr)
             elif s.kind == "head":
-                K.mlp_head(s, cur, out, bucket, m_ptr=m_ptr, tree_partial=fused_partial)
+                K.mlp_head(s, cur, out, bucket, m_ptr=m_ptr, tree_partial=fused_partial,
+                           ens=ens if i == len(steps) - 1 else None)
                 fused_partial = None
             cur = out
         return cur

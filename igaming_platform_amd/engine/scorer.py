@@ -104,8 +104,10 @@ class GpuScorer:
         self.slots = [self._alloc_slot() for _ in range(self.depth)]
         self._cur = 0  # slot of the last submitted batch (the un-indexed buffer properties)
         self.metrics = torch.zeros(128, dtype=torch.int64, device=dev)
-        self.cstream = torch.cuda.Stream(device=dev)   # H2D + dedup insert
         self.stream = torch.cuda.Stream(device=dev)    # state stream (feature store owner)
+        # H2D + dedup insert; IGP_STREAMS=2 runs them in order on the state stream (one
+        # cross-queue wait per batch fewer, copy no longer beside K1)
+        self.cstream = self.stream if os.environ.get("IGP_STREAMS", "3") == "2" else torch.cuda.Stream(device=dev)
         self.mstream = torch.cuda.Stream(device=dev)   # model / result stream
         self._copy_ev = [torch.cuda.Event() for _ in range(self.depth)]
         self._state_ev = [torch.cuda.Event() for _ in range(self.depth)]
@@ -186,10 +188,14 @@ class GpuScorer:
 
     def _model_body(self, slot: int, bucket: int, with_features: bool = False) -> None:
         sb = self.slots[slot]
-        ml = None
-        if sb.model is not None:
-            ml = sb.model.run(sb.X, bucket, m_ptr=sb.n_ptr)
-        K.ensemble(sb.hdr, self.cfg_dev, sb.feat, sb.X, ml, sb.res, bucket, self.metrics)
+        if sb.model is not None and sb.model.fuses_ensemble() and os.environ.get("IGP_FUSE_ENS", "1") != "0":
+            # K5 in the MLP head's epilogue: one launch fewer, ml never re-read
+            ens = K.ensemble_args(sb.hdr, self.cfg_dev, sb.feat, sb.X, sb.model.step_out[-1], sb.res, bucket,
+                                  self.metrics)
+            sb.model.run(sb.X, bucket, m_ptr=sb.n_ptr, ens=ens)
+        else:
+            ml = sb.model.run(sb.X, bucket, m_ptr=sb.n_ptr) if sb.model is not None else None
+            K.ensemble(sb.hdr, self.cfg_dev, sb.feat, sb.X, ml, sb.res, bucket, self.metrics)
         self.host_res[slot][:bucket].copy_(sb.res[:bucket], non_blocking=True)
         if with_features:
             self.host_feat[slot][:bucket].copy_(sb.feat[:bucket], non_blocking=True)

@@ -205,10 +205,12 @@ def dense(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], Y: tor
 
 
 def mlp_head(hs, X: Optional[torch.Tensor], Y: torch.Tensor, M: int, m_ptr: Optional[torch.Tensor] = None,
-             tree_partial=None, trace: Optional[torch.Tensor] = None) -> None:
+             tree_partial=None, trace: Optional[torch.Tensor] = None, ens: Optional[dict] = None) -> None:
     """``hs``: models.plan.HeadStep. Y[:M, 0] = act2(act1(X W1^T + b1) . w2 + b2).
     ``tree_partial=(slab, groups, tree_step)``: X is the preceding tree ensemble's unreduced
-    group partials [groups, M, K]; the head reduces them while staging (no finisher launch)."""
+    group partials [groups, M, K]; the head reduces them while staging (no finisher launch).
+    ``ens``: :func:`ensemble_args` of the scorer's K5 on this Y (model column 0): the head's
+    epilogue runs the ensemble of its rows, replacing the standalone ensemble launch."""
     if tree_partial is not None:
         slab, groups, ts = tree_partial
         if ts.k != hs.k or slab.numel() < groups * M * hs.k or ts.post != 0 or ts.binary_class >= 0:
@@ -236,12 +238,16 @@ def mlp_head(hs, X: Optional[torch.Tensor], Y: torch.Tensor, M: int, m_ptr: Opti
                  p_average=int(ts.average), p_ntrees=int(ts.n_trees))
     if trace is not None:
         d["trace"] = _need(trace, "trace", torch.int64, 64, dev)
+    if ens is not None:
+        if ens["n_rows"] > M:
+            raise ValueError("mlp_head: fused ensemble covers more rows than the head")
+        d["ens"] = ens
     _mod().mlp_head(d, _stream())
 
 
 # --------------------------------------------------------------------------- K5 / K10
-def ensemble(hdr, cfg_dev, feat, X, ml: Optional[torch.Tensor], out, n_rows: int,
-             metrics: Optional[torch.Tensor] = None) -> None:
+def ensemble_args(hdr, cfg_dev, feat, X, ml: Optional[torch.Tensor], out, n_rows: int,
+                  metrics: Optional[torch.Tensor] = None) -> dict:
     dev = feat.device
     d = dict(hdr=_need(hdr, "hdr", torch.int64, 2, dev), cfg=_need(cfg_dev, "cfg", torch.uint8, 176, dev),
              feat=_need(feat, "feat", torch.int32, 32 * n_rows, dev),
@@ -250,7 +256,12 @@ def ensemble(hdr, cfg_dev, feat, X, ml: Optional[torch.Tensor], out, n_rows: int
              metrics=_opt(metrics, "metrics", dtype=torch.int64, min_numel=128), n_rows=int(n_rows))
     if ml is not None and ml.numel() < n_rows:
         raise ValueError("ensemble: model output shorter than the batch")
-    _mod().ensemble(d, _stream())
+    return d
+
+
+def ensemble(hdr, cfg_dev, feat, X, ml: Optional[torch.Tensor], out, n_rows: int,
+             metrics: Optional[torch.Tensor] = None) -> None:
+    _mod().ensemble(ensemble_args(hdr, cfg_dev, feat, X, ml, out, n_rows, metrics), _stream())
 
 
 # --------------------------------------------------------------------------- K9

@@ -161,3 +161,29 @@ def test_streaming_mode_matches_three_stream_mode():
     torch.cuda.synchronize()
     for name in ("rt", "ring_ts", "ring_amt", "hll"):
         assert torch.equal(getattr(A.store, name), getattr(B.store, name)), name
+
+
+def test_fused_head_ensemble_matches_standalone():
+    """cfg3 (trees -> MLP head): the ensemble run in the head's epilogue writes the same result
+    records and metrics as the standalone K5 kernel over the head's output, including padded
+    rows of a partial batch."""
+    import torch
+    from igaming_platform_amd.ops import kernels as K
+    from igaming_platform_amd.utils import benchkit
+    from igaming_platform_amd.utils.synth import NOW0, make_requests
+    dev = torch.device("cuda", 0)
+    S = benchkit.build("cfg3", 512, 4096, dev, depth=2, history_batches=2, hot_frac=0.1)
+    sc = S.scorer
+    assert sc.slots[0].model.fuses_ensemble()
+    rng = np.random.default_rng(11)
+    for n in (512, 301):
+        res, _ = sc.wait(sc.submit(make_requests(S.pop, n, rng, NOW0), now=NOW0), unpack=False)
+        torch.cuda.synchronize()
+        sb = sc.slots[sc._cur]
+        fused = sb.res.clone()
+        m0 = sc.metrics.clone()
+        K.ensemble(sb.hdr, sc.cfg_dev, sb.feat, sb.X, sb.model.step_out[-1], sb.res, 512, sc.metrics)
+        torch.cuda.synchronize()
+        assert torch.equal(fused, sb.res)
+        assert int((sc.metrics - m0)[106]) == n  # rows counted once more by the standalone pass
+        np.testing.assert_array_equal(res, fused[:n].cpu().numpy())
