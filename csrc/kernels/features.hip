@@ -566,7 +566,7 @@ __global__ void __launch_bounds__(64) dedup_insert_list_kernel(UpdateArgs a) {
       if (pos < DEDUP_LIST) t.list[(size_t)h * DEDUP_LIST + pos] = i;
       if (pos == 1) {
         const int m = atomicAdd(&t.ctr[0], 1);
-        if (m < t.nmax) t.mlist[m] = (int)h;
+        if (2 * m + 1 < t.nmax) *reinterpret_cast<int2*>(t.mlist + 2 * m) = make_int2((int)h, r.x);
       }
       return;
     }
@@ -602,8 +602,9 @@ __device__ void apply_scan_serial(const UpdateArgs& a, int s, int lane) {
 // PFADD of up to 64 same-account events at once: the per-register winner writes the max,
 // each event learns whether it raised its register (the GRU's new-device/new-ip feature)
 // exactly as the sequential order would have.
+// pre: the lane's register byte rg[hq & 255], loaded by the caller beside the other HLL's
 __device__ __forceinline__ uint32_t hll_segment(const UpdateArgs& a, uint8_t* rg, uint32_t exp, uint64_t hq,
-                                                int64_t ts, int lane, bool& changed) {
+                                                int64_t ts, int lane, bool& changed, int pre) {
   const bool has = hq != 0;
   const uint64_t any = __ballot(has);
   if (!any) return exp;
@@ -613,7 +614,7 @@ __device__ __forceinline__ uint32_t hll_segment(const UpdateArgs& a, uint8_t* rg
   const bool reset = tfirst >= (int64_t)exp;
   const int idx = has ? (int)(hq & 255u) : -1;
   const int rank = has ? hll_rank(hq) : 0;
-  const int before = (has && !reset) ? (int)rg[idx] : 0;
+  const int before = (has && !reset) ? pre : 0;
   if (reset) {
     reinterpret_cast<uint32_t*>(rg)[lane] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -644,9 +645,9 @@ __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h
   }
   // sort the (distinct) row indices: rank = #smaller, then push each to lane `rank`
   // sc1 load: the entries come from other waves of the same launch (feature_assemble hand-off)
-  const int key = lane < c ? __hip_atomic_load(&t.list[(size_t)h * DEDUP_LIST + lane], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT)
-                           : (0x7fffffc0 | lane);
+  const int raw = __hip_atomic_load(&t.list[(size_t)h * DEDUP_LIST + lane], __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);  // all 64 lanes: no wait on c first
+  const int key = lane < c ? raw : (0x7fffffc0 | lane);
   int rank = 0;
   for (int y = 0; y < c; ++y) rank += __shfl(key, y, 64) < key;  // lanes >= c hold sentinels
   const int j = __builtin_amdgcn_ds_permute(rank * 4, key);
@@ -685,8 +686,11 @@ __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h
   // HyperLogLogs
   uint8_t* regs = a.hll + (size_t)s * 512;
   bool new_dev = false, new_ip = false;
-  r.hll_dev_exp = hll_segment(a, regs, r.hll_dev_exp, act ? ev.dev_hash : 0, ts, lane, new_dev);
-  r.hll_ip_exp = hll_segment(a, regs + 256, r.hll_ip_exp, act ? ev.ip_hash : 0, ts, lane, new_ip);
+  const uint64_t dq = act ? ev.dev_hash : 0, iq = act ? ev.ip_hash : 0;
+  const int pd = dq ? (int)regs[dq & 255u] : 0;  // both registers in one memory round trip
+  const int pi = iq ? (int)regs[256 + (iq & 255u)] : 0;
+  r.hll_dev_exp = hll_segment(a, regs, r.hll_dev_exp, dq, ts, lane, new_dev, pd);
+  r.hll_ip_exp = hll_segment(a, regs + 256, r.hll_ip_exp, iq, ts, lane, new_ip, pi);
   // last tx / session
   if (ts0 >= (int64_t)r.session_exp || r.session_start == 0) r.session_start = (uint32_t)ts0;
   r.session_exp = (uint32_t)(tsl + cfg.session_ttl);
@@ -711,18 +715,24 @@ __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h
 
 // standalone ingestion: one wave per multi-event account listed by update_single
 constexpr int UPD_MULTI_BLOCKS = 64;  // 256 waves loop over the list (any count, no big grid)
+// dependent memory round trips per account: {list count, first pair} -> {count, AcctRT, row
+// list} -> request rows -> both HLL registers -> stores (the pair carries the account slot, so
+// count, AcctRT and the row list are loaded together)
 __global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
   const int lane = threadIdx.x & 63;
   const DedupTab t = upd_region(a);
-  const int nm = min(t.ctr[0], t.nmax);
-  for (int w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); w < nm;
-       w += UPD_MULTI_BLOCKS * 4) {
-    const int h = t.mlist[w];
-    if (h < 0 || h >= t.cap) continue;
+  const int npair = t.nmax >> 1;
+  const int w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  int2 hs = w0 < npair ? *reinterpret_cast<const int2*>(t.mlist + 2 * w0) : make_int2(-1, -1);  // speculative
+  const int nm = min(t.ctr[0], npair);
+  for (int w = w0; w < nm; w += UPD_MULTI_BLOCKS * 4) {
+    if (w != w0) hs = *reinterpret_cast<const int2*>(t.mlist + 2 * w);
+    const int h = hs.x, s = hs.y;
+    if (h < 0 || h >= t.cap || s < 0) continue;
     const int c = t.count[h];
-    const int s = t.keys[h];
-    if (c < 2 || s < 0) continue;
-    apply_segment_wave(a, t, h, c, s, a.rt[s], lane);
+    const AcctRT r = a.rt[s];
+    if (c < 2) continue;
+    apply_segment_wave(a, t, h, c, s, r, lane);
   }
   // scorer ring: clear the region of batch seq+2 (= seq-1's, consumed by now) for its insert;
   // the copy of batch seq+2 waits for this batch's state graph

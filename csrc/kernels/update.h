@@ -17,10 +17,10 @@ struct DedupTab {
   int32_t* fill;
   int32_t* done;    // scorer path: rows of the account whose reads are complete
   int32_t* list;    // [cap][DEDUP_LIST]
-  int32_t* mlist;   // [n_max] hash slots of multi-event accounts
+  int32_t* mlist;   // [n_max / 2] pairs {hash slot, account slot} of multi-event accounts
   int32_t* ctr;     // [0] multi-account count, [1] spare
   int32_t cap;
-  int32_t nmax;     // capacity of mlist
+  int32_t nmax;     // ints in mlist (n_max / 2 pairs: each listed account has >= 2 events)
 };
 
 __host__ __device__ inline size_t dedup_region_size(int cap, int n_max) {
@@ -179,12 +179,12 @@ __device__ __forceinline__ void apply_event(const UpdateArgs& a, int j, AcctRT& 
 
 // event i of a multi-event account (hash slot h): append it to the account's list; the
 // account's first event also enters the multi-account list (applied by update_multi)
-__device__ __forceinline__ void note_multi_event(const DedupTab& t, int h, int i, bool first) {
+__device__ __forceinline__ void note_multi_event(const DedupTab& t, int h, int s, int i, bool first) {
   const int pos = atomicAdd(&t.fill[h], 1);
   if (pos < DEDUP_LIST) t.list[(size_t)h * DEDUP_LIST + pos] = i;
   if (first) {
     const int m = atomicAdd(&t.ctr[0], 1);
-    if (m < t.nmax) t.mlist[m] = h;
+    if (2 * m + 1 < t.nmax) *reinterpret_cast<int2*>(t.mlist + 2 * m) = make_int2(h, s);
   }
 }
 
@@ -198,7 +198,7 @@ __device__ __forceinline__ void update_event(const UpdateArgs& a, const DedupTab
     apply_event(a, i, r);
     a.rt[s] = r;
   } else {
-    note_multi_event(t, h, i, t.first[h] == i);
+    note_multi_event(t, h, s, i, t.first[h] == i);
   }
 }
 

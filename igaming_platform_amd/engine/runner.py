@@ -7,6 +7,8 @@ their own hipGraphs together with their copies, so a model step never re-capture
 """
 from __future__ import annotations
 
+import os
+
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -18,6 +20,9 @@ from ..ops import kernels as K
 def tree_groups(step, bucket: int) -> int:
     """Split the trees of one ensemble into ``g`` groups so a small batch still fills the
     256 CUs (>= ~512 workgroups), without shrinking a group below 8 trees."""
+    forced = int(os.environ.get("IGP_TREE_GROUPS", "0"))  # same-box A/B override
+    if forced > 0:
+        return max(1, min(forced, step.n_trees))
     tiles = -(-bucket // 64)
     return max(1, min(max(1, step.n_trees // 8), -(-512 // tiles)))
 

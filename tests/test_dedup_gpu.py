@@ -68,5 +68,7 @@ def test_dedup_region_after_insert(hot):
             if c <= DEDUP_LIST:  # the account's rows, in any order
                 assert sorted(lists[h, :c].tolist()) == rows_of[s], s
         multi = {int(h) for h in np.nonzero(count >= 2)[0]}
-        assert ctr[0] == len(multi) and set(mlist[:ctr[0]].tolist()) == multi
+        pairs = mlist[:2 * ctr[0]].reshape(-1, 2)  # {hash slot, account slot}
+        assert ctr[0] == len(multi) and set(pairs[:, 0].tolist()) == multi
+        assert (keys[pairs[:, 0]] == pairs[:, 1]).all()
         assert ctr[1] != 0
