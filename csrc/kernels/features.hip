@@ -724,7 +724,10 @@ __global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
   const int npair = t.nmax >> 1;
   const int w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   int2 hs = w0 < npair ? *reinterpret_cast<const int2*>(t.mlist + 2 * w0) : make_int2(-1, -1);  // speculative
-  const int nm = min(t.ctr[0], npair);
+  // a batch with no live rows (graph warm-up, an empty padded launch) applies nothing: the
+  // region's list may still hold the previous user of the region (a scorer that took over
+  // the store carries the batch sequence over)
+  const int nm = upd_n(a) > 0 ? min(t.ctr[0], npair) : 0;
   for (int w = w0; w < nm; w += UPD_MULTI_BLOCKS * 4) {
     if (w != w0) hs = *reinterpret_cast<const int2*>(t.mlist + 2 * w);
     const int h = hs.x, s = hs.y;

@@ -1,7 +1,8 @@
 """HTTP side endpoints of the risk service (services/risk/cmd/main.go:165-214):
 ``/metrics`` (Prometheus), ``/health`` (always 200), ``/ready`` (engine health),
 ``/debug/thresholds`` (the LIVE thresholds — the reference reports the static env config,
-quirk Q7), ``/debug/score`` (``ScoreWithExplanation``; a stub in the reference), plus
+quirk Q7), ``/debug/score`` (``ScoreWithExplanation``; a stub in the reference),
+``POST /admin/reload_model`` (model hot-reload), plus
 ``/debug/features`` and ``/debug/engine``."""
 from __future__ import annotations
 
@@ -87,6 +88,25 @@ def make_handler(engine):
                 else:
                     self._send(404, "not found")
             except Exception as e:  # never take the side server down
+                log.error("http handler error", exc_info=True)
+                self._send(500, f"error: {e}")
+
+        def do_POST(self):
+            u = urlparse(self.path)
+            try:
+                if u.path == "/admin/reload_model":  # body: ONNX model bytes (empty: heuristic)
+                    n = int(self.headers.get("Content-Length", "0"))
+                    if n > 1 << 30:
+                        return self._send(413, "model too large")
+                    body = self.rfile.read(n) if n else b""
+                    v = engine.reload_model(body)
+                    self._send(200, json.dumps({"model_version": v, "model_kind": engine.model_kind}),
+                               "application/json")
+                else:
+                    self._send(404, "not found")
+            except ValueError as e:
+                self._send(400, f"error: {e}")
+            except Exception as e:
                 log.error("http handler error", exc_info=True)
                 self._send(500, f"error: {e}")
 

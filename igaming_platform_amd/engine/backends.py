@@ -46,6 +46,23 @@ def _featrec_from_golden(f, row, bl: bool, rule: int, reasons) -> np.ndarray:
     return r
 
 
+def cpu_model_spec(cfg: Config, fm, mkind: str) -> dict:
+    """Model arguments of a CPU backend for an ONNX model ``fm`` (``mkind`` "onnx") or a
+    built-in model kind ("heuristic" / "none")."""
+    if mkind != "onnx":
+        return dict(model=mkind, executor=None, input_name="input", output_name=cfg.fraud_model.output_name, ml_col=0)
+    from ..models.plan import compile_onnx
+    ml_col, out_name = 0, cfg.fraud_model.output_name
+    try:
+        p = compile_onnx(fm)
+        ml_col, out_name = p.ml_col, p.output_name
+    except Exception:
+        pass
+    from ..native import native
+    return dict(model="plan", executor=native().Executor(fm), input_name=fm.inputs()[0][0], output_name=out_name,
+                ml_col=ml_col)
+
+
 class CpuBackend:
     """Golden-semantics scorer on the host (the pure-Python spec; ``backend="golden"``)."""
 
@@ -79,6 +96,14 @@ class CpuBackend:
         t = self.ipintel.table
         self.store.ip_intel = {int(k): int(x) for k, x in zip(t.keys.view(np.uint64), t.vals) if int(k) != 0}
         self._tables_version = v
+
+    def swap_model(self, fm, mkind: str) -> None:
+        """Model hot-reload: the next batch scores with the new model (feature state kept)."""
+        spec = cpu_model_spec(self.cfg, fm, mkind)
+        with self._lock:
+            self.model = spec["model"]
+            self.executor, self.input_name = spec["executor"], spec["input_name"]
+            self.output_name, self.ml_col = spec["output_name"], spec["ml_col"]
 
     def refresh_config(self, scoring=None) -> None:
         with self._lock:
@@ -263,6 +288,35 @@ class GpuBackend:
         self._slot_locks = [threading.Lock() for _ in range(self.scorer.depth)]
         self._fx = None
 
+    def swap_model(self, fm, mkind: str) -> None:
+        """Model hot-reload: drain the shard, build a scorer for the new plan on the same HBM
+        feature store (new graphs, same store, batch sequence and metrics carried over so the
+        dedup region ring stays consistent), swap it in. Scoring resumes with the new model."""
+        from ..models.plan import compile_onnx, to_device
+        from .scorer import GpuScorer
+        torch = self.torch
+        plan = to_device(compile_onnx(fm), self.device) if mkind == "onnx" else None
+        model = {"onnx": "plan", "heuristic": "heuristic", "none": "none"}[mkind]
+        with self._lock:
+            for lk in self._slot_locks:
+                lk.acquire()
+            try:
+                old = self.scorer
+                torch.cuda.synchronize(self.device)
+                sc = GpuScorer(self.cfg, self.store, plan=plan, model=model, device=self.device,
+                               pipeline_depth=old.depth, owner_filter=old.owner_filter, rank=old.rank,
+                               use_graphs=old.use_graphs)
+                sc._seq = old._seq  # dedup regions rotate by batch seq (one is still dirty)
+                sc.metrics = old.metrics
+                sc.refresh_config(getattr(old, "scoring", None))
+                if old.graphs and sc.use_graphs:
+                    sc.capture()
+                torch.cuda.synchronize(self.device)
+                self.scorer = sc
+            finally:
+                for lk in self._slot_locks:
+                    lk.release()
+
     def refresh_config(self, scoring=None) -> None:
         with self._lock:
             with self.torch.cuda.stream(self.scorer.stream):
@@ -405,6 +459,15 @@ class NativeCpuBackend:
         self._tables_version = None
         self._lock = threading.RLock()
         self.refresh_config()
+
+    def swap_model(self, fm, mkind: str) -> None:
+        """Model hot-reload: the C++ scorer's executor is replaced between batches."""
+        spec = cpu_model_spec(self.cfg, fm, mkind)
+        with self._lock:
+            self.model = spec["model"]
+            self.sc.set_model(spec["executor"] if self.model == "plan" else None, spec["input_name"],
+                              spec["output_name"], spec["ml_col"])
+            self.refresh_config()
 
     def refresh_config(self, scoring=None) -> None:
         from ..layouts import MODEL_HEURISTIC, MODEL_NONE, MODEL_OUTPUT, score_cfg

@@ -115,6 +115,7 @@ class RiskEngine:
                 cfg.features.width = w
         self.model_kind = mkind
         self.fraud_onnx = fm
+        self.model_version = 1
         self.backends: List = []
         self.healthy = [True] * world
         if spmd is not None:
@@ -382,6 +383,36 @@ class RiskEngine:
             self._push_config()
         log.info("thresholds updated", extra={"fields": dict(block=block, review=review)})
         return self.get_thresholds()
+
+    # ---- model hot-reload: versioned, broadcast to every shard
+    def reload_model(self, fraud_model) -> int:
+        """Swap the fraud model (ONNX bytes or path; None/b"" = the built-in heuristic) on every
+        shard between batches; feature state, thresholds and metrics are kept. The input width
+        must match the running feature layout. Returns the new model version."""
+        raw = fraud_model
+        if isinstance(raw, str):
+            with open(raw, "rb") as f:
+                raw = f.read()
+        raw = bytes(raw or b"")
+        fm = _load_onnx(raw)
+        mkind = "onnx" if fm is not None else "heuristic"
+        if fm is not None:
+            dims = fm.inputs()[0][2]
+            w = int(dims[-1]) if dims and int(dims[-1]) > 0 else self.cfg.features.width
+            if w != self.cfg.features.width:
+                raise ValueError(f"model input width {w} != running features.width {self.cfg.features.width}")
+        with self._lock:
+            if self.group is not None:
+                self.group.reload_model(raw)
+            else:
+                for be in self.backends:
+                    be.swap_model(fm, mkind)
+            if self.fallback is not None:
+                self.fallback.swap_model(fm, mkind)
+            self.fraud_onnx, self.model_kind = fm, mkind
+            self.model_version += 1
+        log.info("fraud model reloaded", extra={"fields": dict(version=self.model_version, kind=mkind)})
+        return self.model_version
 
     def set_scoring(self, **kw) -> None:
         """Replace any ScoringConfig fields (rule limits, weights) atomically."""

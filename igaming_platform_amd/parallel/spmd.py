@@ -26,7 +26,7 @@ from ..config import RuleWeights, ScoringConfig
 from ..layouts import ACCTBATCH, FEATREC, REQREC
 
 OP_SCORE, OP_INGEST, OP_CONFIG, OP_TABLES, OP_BATCH, OP_EXT, OP_FEATURES, OP_RESET, OP_STOP, OP_EVHIST, \
-    OP_ABUSE, OP_SNAPSHOT, OP_RESTORE = range(1, 14)
+    OP_ABUSE, OP_SNAPSHOT, OP_RESTORE, OP_RELOAD = range(1, 15)
 
 
 def owners_of(req: np.ndarray) -> np.ndarray:
@@ -107,6 +107,11 @@ class ShardRunner:
             return None
         if op == OP_CONFIG:
             self.be.refresh_config(scoring_from_json(payload))
+            return None
+        if op == OP_RELOAD:  # payload: ONNX bytes (empty: built-in heuristic)
+            from ..native import native
+            fm = native().OnnxModel.from_bytes(payload) if payload else None
+            self.be.swap_model(fm, "onnx" if fm is not None else "heuristic")
             return None
         if op == OP_TABLES:
             _load_tables(payload, self.be.blacklist, self.be.ipintel)
@@ -197,6 +202,9 @@ class SpmdGroup:
 
     def sync_tables(self, blacklist, ipintel) -> None:
         self._issue(OP_TABLES, _tables_bytes(blacklist, ipintel))
+
+    def reload_model(self, onnx_bytes: bytes) -> None:
+        self._issue(OP_RELOAD, onnx_bytes)
 
     def _rows(self, op, slots, owners, body: bytes = b"") -> None:
         n = len(slots)

@@ -22,7 +22,7 @@ def stack():
     eng = RiskEngine(Config(), backend="cpu", capacity=1000)
     gs = RiskServer(eng, port=0, max_batch=64, wait_us=500).start()
     hs = HttpServer(eng, port=0).start()
-    cli = RiskClient(f"127.0.0.1:{gs.port}")
+    cli = RiskClient(f"127.0.0.1:{gs.port}", timeout_s=30.0)  # first calls pay lazy init on a loaded box
     yield eng, gs, hs, cli
     cli.close()
     gs.stop(0.5)

@@ -261,3 +261,41 @@ def test_native_cpu_backend_equals_golden_backend(log_mode, sum_mode, width):
     for i in range(30):
         assert engines[0].get_features(f"acc-{i}", NOW + 99).tobytes() == \
                engines[1].get_features(f"acc-{i}", NOW + 99).tobytes()
+
+
+@pytest.mark.parametrize("backend", ["cpu", "golden"])
+def test_model_hot_reload_keeps_state(backend):
+    """reload_model swaps the fraud model between batches: the scores after the swap equal an
+    engine that ran the new model from the start (feature updates do not depend on the model);
+    the version counts up; a width mismatch is refused."""
+    from igaming_platform_amd.onnx import builders
+    m = builders.build("logistic", n_features=30).SerializeToString()
+    a = RiskEngine(Config(), backend=backend, capacity=80)
+    b = RiskEngine(Config(), backend=backend, capacity=80, fraud_model=m)
+    rng = np.random.default_rng(5)
+    t1, t2 = _txs(120, rng), _txs(120, rng)
+    a.score(t1, now=NOW)
+    b.score(t1, now=NOW)
+    assert a.model_kind == "heuristic" and a.model_version == 1
+    assert a.reload_model(m) == 2 and a.model_kind == "onnx"
+    ra, rb = a.score(t2, now=NOW + 30), b.score(t2, now=NOW + 30)
+    assert [(x["score"], x["action"], x["ml_score"]) for x in ra] == [(x["score"], x["action"], x["ml_score"]) for x in rb]
+    with pytest.raises(ValueError):
+        a.reload_model(builders.build("logistic", n_features=32).SerializeToString())
+    assert a.reload_model(None) == 3 and a.model_kind == "heuristic"
+
+
+def test_http_reload_model_endpoint():
+    import json
+    import urllib.request
+    from igaming_platform_amd.api.http_server import HttpServer
+    from igaming_platform_amd.onnx import builders
+    eng = RiskEngine(Config(), backend="cpu", capacity=20)
+    srv = HttpServer(eng).start()
+    try:
+        body = builders.build("logistic", n_features=30).SerializeToString()
+        req = urllib.request.Request(f"http://127.0.0.1:{srv.port}/admin/reload_model", data=body, method="POST")
+        with urllib.request.urlopen(req, timeout=30) as r:
+            assert json.loads(r.read()) == {"model_version": 2, "model_kind": "onnx"}
+    finally:
+        srv.stop()

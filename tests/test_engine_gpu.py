@@ -187,3 +187,28 @@ def test_fused_head_ensemble_matches_standalone():
         assert torch.equal(fused, sb.res)
         assert int((sc.metrics - m0)[106]) == n  # rows counted once more by the standalone pass
         np.testing.assert_array_equal(res, fused[:n].cpu().numpy())
+
+
+def test_gpu_model_hot_reload():
+    """GpuBackend.swap_model: a new scorer (new graphs) on the same HBM feature store; scores
+    after the swap equal a GPU engine that ran the new model from the start."""
+    from igaming_platform_amd.onnx import builders
+    m = builders.build("logistic", n_features=30).SerializeToString()
+    a, _ = _engines()
+    from igaming_platform_amd.engine.risk_engine import RiskEngine
+    b, _ = _engines(fraud_model=m)
+    rng = np.random.default_rng(8)
+    t1, t2 = _txs(300, rng), _txs(300, rng)
+    a.score(t1, now=NOW)
+    b.score(t1, now=NOW)
+    for i in range(40):
+        fa, fb = a.get_features(f"acc-{i}", now=NOW + 5), b.get_features(f"acc-{i}", now=NOW + 5)
+        diff = [k for k in fa.dtype.names if fa[k] != fb[k]]
+        assert not diff, ("before reload", i, [(k, fa[k], fb[k]) for k in diff])
+    assert a.reload_model(m) == 2
+    ra, rb = a.score(t2, now=NOW + 20), b.score(t2, now=NOW + 20)
+    assert [(x["score"], x["action"], x["ml_score"]) for x in ra] == [(x["score"], x["action"], x["ml_score"]) for x in rb]
+    for i in range(40):
+        fa, fb = a.get_features(f"acc-{i}", now=NOW + 30), b.get_features(f"acc-{i}", now=NOW + 30)
+        diff = [k for k in fa.dtype.names if fa[k] != fb[k]]
+        assert not diff, (i, [(k, fa[k], fb[k]) for k in diff])
