@@ -37,6 +37,7 @@ EnsembleArgs ensemble_args(const py::dict& d) {
   a.x_stride = geti(d, "x_stride");
   a.ml = ptr<const float*>(d, "ml");
   a.out = ptr<ResultRec*>(d, "out");
+  a.host_out = ptr<ResultRec*>(d, "host_out");
   a.metrics = ptr<unsigned long long*>(d, "metrics");
   a.n_rows = geti(d, "n_rows");
   return a;

@@ -34,6 +34,7 @@ __device__ __forceinline__ void ensemble_row(const EnsembleArgs& a, int row, boo
   const int n_live = a.hdr->n;
   if (row >= n_live || (a.feat[row].flags & FR_NOT_OWNED)) {
     a.out[row] = ResultRec{0u, 0.f};  // padding / another rank's request: zero (merge by sum)
+    if (a.host_out) a.host_out[row] = ResultRec{0u, 0.f};
     return;
   }
   const ScoreCfg& cfg = *a.cfg;
@@ -60,6 +61,9 @@ __device__ __forceinline__ void ensemble_row(const EnsembleArgs& a, int row, boo
   const uint32_t packed = (uint32_t)(fin & 0xff) | ((uint32_t)(rule & 0xff) << 8) | ((uint32_t)action << 16) |
                           ((cfg.model_kind != 0 ? 1u : 0u) << 18) | (reasons << 20);
   a.out[row] = ResultRec{packed, (float)ml};
+  // host copy: 8-B stores over the bus, visible to the host once the kernel's completion
+  // signal (system-scope release) is
+  if (a.host_out) a.host_out[row] = ResultRec{packed, (float)ml};
   if (cnt) {
     atomicAdd(&cnt[MET_HIST + (fin < 0 ? 0 : fin)], 1u);
     atomicAdd(&cnt[MET_ACTION + action], 1u);

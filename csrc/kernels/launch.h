@@ -131,6 +131,7 @@ struct EnsembleArgs {
   int32_t x_stride;
   const float* ml;          // model output (nullable)
   ResultRec* out;
+  ResultRec* host_out;      // nullable: pinned host rows written directly (no D2H copy node)
   unsigned long long* metrics;  // [128] score histogram(101) | actions(4) | ml_high | rows (nullable)
   int32_t n_rows;
 };

@@ -116,6 +116,7 @@ class GpuScorer:
         self.cfg_dev = torch.zeros(176, dtype=torch.uint8, device=dev)
         self.refresh_config()
         self.graphs: Dict[tuple, tuple] = {}
+        self._host_results = os.environ.get("IGP_HOST_RESULTS", "1") != "0"
         self.driver = None
         self._slot = 0
         self._seq = 0
@@ -188,15 +189,19 @@ class GpuScorer:
 
     def _model_body(self, slot: int, bucket: int, with_features: bool = False) -> None:
         sb = self.slots[slot]
+        # K5 writes the result rows straight into the slot's pinned host buffer as well (no
+        # D2H copy node on the model stream); IGP_HOST_RESULTS=0 restores the copy
+        host = self.host_res[slot] if self._host_results else None
         if sb.model is not None and sb.model.fuses_ensemble() and os.environ.get("IGP_FUSE_ENS", "1") != "0":
             # K5 in the MLP head's epilogue: one launch fewer, ml never re-read
             ens = K.ensemble_args(sb.hdr, self.cfg_dev, sb.feat, sb.X, sb.model.step_out[-1], sb.res, bucket,
-                                  self.metrics)
+                                  self.metrics, host_out=host)
             sb.model.run(sb.X, bucket, m_ptr=sb.n_ptr, ens=ens)
         else:
             ml = sb.model.run(sb.X, bucket, m_ptr=sb.n_ptr) if sb.model is not None else None
-            K.ensemble(sb.hdr, self.cfg_dev, sb.feat, sb.X, ml, sb.res, bucket, self.metrics)
-        self.host_res[slot][:bucket].copy_(sb.res[:bucket], non_blocking=True)
+            K.ensemble(sb.hdr, self.cfg_dev, sb.feat, sb.X, ml, sb.res, bucket, self.metrics, host_out=host)
+        if host is None:
+            self.host_res[slot][:bucket].copy_(sb.res[:bucket], non_blocking=True)
         if with_features:
             self.host_feat[slot][:bucket].copy_(sb.feat[:bucket], non_blocking=True)
 

@@ -247,7 +247,9 @@ def mlp_head(hs, X: Optional[torch.Tensor], Y: torch.Tensor, M: int, m_ptr: Opti
 
 # --------------------------------------------------------------------------- K5 / K10
 def ensemble_args(hdr, cfg_dev, feat, X, ml: Optional[torch.Tensor], out, n_rows: int,
-                  metrics: Optional[torch.Tensor] = None) -> dict:
+                  metrics: Optional[torch.Tensor] = None, host_out: Optional[torch.Tensor] = None) -> dict:
+    """``host_out``: pinned host int32 [>= n_rows, 2] rows the kernel also writes (the D2H
+    copy of the results is then not needed)."""
     dev = feat.device
     d = dict(hdr=_need(hdr, "hdr", torch.int64, 2, dev), cfg=_need(cfg_dev, "cfg", torch.uint8, 176, dev),
              feat=_need(feat, "feat", torch.int32, 32 * n_rows, dev),
@@ -256,12 +258,17 @@ def ensemble_args(hdr, cfg_dev, feat, X, ml: Optional[torch.Tensor], out, n_rows
              metrics=_opt(metrics, "metrics", dtype=torch.int64, min_numel=128), n_rows=int(n_rows))
     if ml is not None and ml.numel() < n_rows:
         raise ValueError("ensemble: model output shorter than the batch")
+    if host_out is not None:
+        if host_out.is_cuda or not host_out.is_pinned() or host_out.dtype != torch.int32 or \
+                not host_out.is_contiguous() or host_out.numel() < 2 * n_rows:
+            raise ValueError("ensemble: host_out must be pinned contiguous int32 [>= n_rows, 2]")
+        d["host_out"] = host_out.data_ptr()
     return d
 
 
 def ensemble(hdr, cfg_dev, feat, X, ml: Optional[torch.Tensor], out, n_rows: int,
-             metrics: Optional[torch.Tensor] = None) -> None:
-    _mod().ensemble(ensemble_args(hdr, cfg_dev, feat, X, ml, out, n_rows, metrics), _stream())
+             metrics: Optional[torch.Tensor] = None, host_out: Optional[torch.Tensor] = None) -> None:
+    _mod().ensemble(ensemble_args(hdr, cfg_dev, feat, X, ml, out, n_rows, metrics, host_out), _stream())
 
 
 # --------------------------------------------------------------------------- K9
