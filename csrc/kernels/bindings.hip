@@ -5,6 +5,7 @@
 #include <pybind11/stl.h>
 
 #include <string>
+#include <vector>
 
 #include "launch.h"
 
@@ -130,6 +131,15 @@ PYBIND11_MODULE(_hipk, m) {
     }
     launch_feature_assemble(a, stream_of(s));
     check("feature_assemble");
+  });
+
+  // a stream whose kernels run only on the CUs set in `mask` (32 CUs per word): lets the
+  // scorer keep its state and model streams on disjoint CUs (tools: IGP_CU_SPLIT)
+  m.def("cu_stream", [](std::vector<uint32_t> mask) {
+    hipStream_t st = nullptr;
+    const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data());
+    if (e != hipSuccess) throw std::runtime_error(std::string("hipExtStreamCreateWithCUMask: ") + hipGetErrorString(e));
+    return reinterpret_cast<uintptr_t>(st);
   });
 
   m.def("feature_update", [](py::dict d, uintptr_t s) {

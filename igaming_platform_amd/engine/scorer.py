@@ -53,6 +53,7 @@ from .runner import DeviceModel
 
 HDR_BYTES = 16
 REQ_BYTES = REQREC.itemsize
+_CU_STREAMS: Dict[tuple, tuple] = {}  # (device, split) -> CU-masked (state, copy, model) streams
 
 
 class _Slot:
@@ -109,6 +110,15 @@ class GpuScorer:
         # cross-queue wait per batch fewer, copy no longer beside K1)
         self.cstream = self.stream if os.environ.get("IGP_STREAMS", "3") == "2" else torch.cuda.Stream(device=dev)
         self.mstream = torch.cuda.Stream(device=dev)   # model / result stream
+        # state/copy streams and the model stream on disjoint CU halves (CU-masked HIP streams):
+        # K1 and the tree/MLP kernels slowed each other 2-7x when sharing CUs (rocprofv3
+        # timeline); same-box A/B cfg3 109.1 vs 97.5 M scores/s (3 runs each, profiles/NOTES.md).
+        # Only with a model plan: the heuristic model stream is just the ensemble.
+        split = os.environ.get("IGP_CU_SPLIT", "auto")
+        if split == "auto":
+            split = "half" if plan is not None else "none"
+        if split != "none":
+            self._cu_split(split)
         self._copy_ev = [torch.cuda.Event() for _ in range(self.depth)]
         self._state_ev = [torch.cuda.Event() for _ in range(self.depth)]
         self._model_ev = [torch.cuda.Event() for _ in range(self.depth)]
@@ -122,6 +132,33 @@ class GpuScorer:
         self._seq = 0
         self._lock = threading.Lock()
         self.batches = 0
+
+    def _cu_split(self, spec: str) -> None:
+        """``half`` = ``lo:n_cu/2``; ``lo:N``: CUs [0, N) run the copy + state streams, the
+        rest the model stream; ``mod:A/B``: CU i goes to the state side when i % B < A."""
+        n_cu = torch.cuda.get_device_properties(self.device).multi_processor_count
+        if spec == "half":
+            spec = f"lo:{n_cu // 2}"
+        kind, arg = spec.split(":")
+        if kind == "lo":
+            st = [i < int(arg) for i in range(n_cu)]
+        else:
+            a, b = (int(x) for x in arg.split("/"))
+            st = [i % b < a for i in range(n_cu)]
+
+        def words(sel):
+            w = [0] * ((n_cu + 31) // 32)
+            for i, on in enumerate(sel):
+                if on:
+                    w[i // 32] |= 1 << (i % 32)
+            return w
+
+        key = (self.device.index, kind, arg)
+        if key not in _CU_STREAMS:  # HIP streams live for the process: reused by later scorers
+            with torch.cuda.device(self.device):
+                _CU_STREAMS[key] = tuple(torch.cuda.ExternalStream(K._mod().cu_stream(words(m)), device=self.device)
+                                         for m in (st, st, [not x for x in st]))
+        self.stream, self.cstream, self.mstream = _CU_STREAMS[key]
 
     # ------------------------------------------------------------------ buffers / config
     def _alloc_slot(self) -> "_Slot":
