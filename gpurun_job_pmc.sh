@@ -1,8 +1,8 @@
+#!/bin/bash
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -q -m gpu -x > gpurun_out/t_gpu_all.log 2>&1 || exit 1
-for i in 1 2 3; do timeout -k 10 300 python bench.py > gpurun_out/bench_cfg3_$i.log 2>&1 || exit 3; done
-timeout -k 10 300 python tools/overlap_probe.py > gpurun_out/overlap.log 2>&1 || exit 4
 cd /tmp && export TMPDIR=/tmp
-rm -rf $GRAFT_REPO_ROOT/gpurun_out/pmc1
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_INSTS_VALU --kernel-include-regex "tree_kernel|mlp_head|feature_assemble" --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc1 -o run -- python $GRAFT_REPO_ROOT/tools/kbench.py --rounds 5 > $GRAFT_REPO_ROOT/gpurun_out/pmc1.log 2>&1 || exit 5
+R=$GRAFT_REPO_ROOT
+rm -rf $R/gpurun_out/pmc_r1 $R/gpurun_out/pmc_r2
+timeout -k 10 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU SQ_WAVES --kernel-include-regex "feature_assemble|tree_kernel" --output-format csv -d $R/gpurun_out/pmc_r1 -o run -- python $R/tools/kbench.py --rounds 1 --only h2d_slab > $R/gpurun_out/pmc_r1.log 2>&1 || exit 5
+timeout -k 10 200 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_CYCLES_VMEM_RD --kernel-include-regex "feature_assemble|tree_kernel" --output-format csv -d $R/gpurun_out/pmc_r2 -o run -- python $R/tools/kbench.py --rounds 1 --only h2d_slab > $R/gpurun_out/pmc_r2.log 2>&1 || exit 6
