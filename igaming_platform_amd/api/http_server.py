@@ -2,7 +2,8 @@
 ``/metrics`` (Prometheus), ``/health`` (always 200), ``/ready`` (engine health),
 ``/debug/thresholds`` (the LIVE thresholds — the reference reports the static env config,
 quirk Q7), ``/debug/score`` (``ScoreWithExplanation``; a stub in the reference),
-``POST /admin/reload_model`` (model hot-reload), plus
+``POST /admin/reload_model`` (model hot-reload), ``POST /admin/flush_audit``
+(drain the risk_scores audit ring into ``server.audit_db``), plus
 ``/debug/features`` and ``/debug/engine``."""
 from __future__ import annotations
 
@@ -102,6 +103,11 @@ def make_handler(engine):
                     v = engine.reload_model(body)
                     self._send(200, json.dumps({"model_version": v, "model_kind": engine.model_kind}),
                                "application/json")
+                elif u.path == "/admin/flush_audit":
+                    path = engine.cfg.server.audit_db
+                    if not path:
+                        return self._send(409, "server.audit_db (AUDIT_DB) is not set")
+                    self._send(200, json.dumps({"rows": engine.flush_audit(path)}), "application/json")
                 else:
                     self._send(404, "not found")
             except ValueError as e:

@@ -141,6 +141,7 @@ class ServerConfig:
     log_level: str = "info"
     shutdown_grace_s: float = 30.0
     http_timeout_s: float = 10.0
+    audit_db: str = ""           # SQLite file the risk_scores audit ring drains into ("" = in-memory only)
 
 
 @dataclass
@@ -195,6 +196,7 @@ class Config:
         s.grpc_port = geti("GRPC_PORT", s.grpc_port)
         s.http_port = geti("HTTP_PORT", s.http_port)
         s.log_level = env.get("LOG_LEVEL", s.log_level) or s.log_level
+        s.audit_db = env.get("AUDIT_DB", s.audit_db)
         sc = self.scoring
         sc.block_threshold = geti("BLOCK_THRESHOLD", sc.block_threshold)
         sc.review_threshold = geti("REVIEW_THRESHOLD", sc.review_threshold)

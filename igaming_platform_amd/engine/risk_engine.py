@@ -317,6 +317,35 @@ class RiskEngine:
         ids = rb.account_id
         self.audit.extend(zip([ts] * len(ids), ids, res[:, 0].tolist(), res[:, 1].tolist()))
 
+    def flush_audit(self, path: str) -> int:
+        """Drain the audit ring into the ``risk_scores`` table of the SQLite database at ``path``
+        (created from ``deploy/schema.sql`` if absent). The reference declares the table
+        (init-db.sql:122-138) and never writes it. Returns the number of rows written."""
+        import sqlite3
+
+        with self._lock:
+            rows = list(self.audit)
+            self.audit.clear()
+        db = sqlite3.connect(path)
+        try:
+            has = db.execute("SELECT name FROM sqlite_master WHERE type='table' AND name='risk_scores'").fetchone()
+            if not has:
+                schema = os.path.join(os.path.dirname(__file__), "..", "..", "deploy", "schema.sql")
+                db.executescript(open(schema).read())
+            recs = np.array([(p, m) for _, _, p, m in rows], np.uint32).reshape(-1, 2)
+            ml = recs[:, 1].view(np.float32)
+            out = []
+            for (ts, aid, p, _), m in zip(rows, ml.tolist()):
+                reasons = [REASON_CODES[b] for b in range(len(REASON_CODES)) if (p >> 20) >> b & 1]
+                out.append((aid, p & 0xFF, (p >> 8) & 0xFF, m, ACTION_NAMES.get((p >> 16) & 3, "unspecified"),
+                            json.dumps(reasons), str(self.model_version), ts))
+            db.executemany("INSERT INTO risk_scores(account_id, score, rule_score, ml_score, action, reason_codes,"
+                           " model_version, created_at) VALUES (?,?,?,?,?,?,?,?)", out)
+            db.commit()
+        finally:
+            db.close()
+        return len(rows)
+
     # ================================================================== python-level API
     def _tx_bytes(self, tx: Dict) -> bytes:
         from ..proto import risk_v1 as P

@@ -299,3 +299,36 @@ def test_http_reload_model_endpoint():
             assert json.loads(r.read()) == {"model_version": 2, "model_kind": "onnx"}
     finally:
         srv.stop()
+
+
+def test_audit_ring_drains_into_risk_scores(tmp_path):
+    """Every scored request lands in the risk_scores audit table (init-db.sql:122-138, declared and
+    never written by the reference): same score / rule score / action / reasons as the response,
+    via the engine call and via POST /admin/flush_audit."""
+    import json
+    import sqlite3
+    import urllib.request
+    from igaming_platform_amd.api.http_server import HttpServer
+    from igaming_platform_amd.proto import risk_v1 as P
+    cfg = Config()
+    cfg.server.audit_db = str(tmp_path / "audit.db")
+    eng = RiskEngine(cfg, backend="cpu", capacity=60)
+    txs = _txs(50, np.random.default_rng(9))
+    out = eng.score_tx_many_bytes([eng._tx_bytes(t) for t in txs], [0.0] * len(txs))
+    resp = [P.ScoreTransactionResponse.FromString(b) for b in out]
+    assert eng.flush_audit(cfg.server.audit_db) == 50 and len(eng.audit) == 0
+    db = sqlite3.connect(cfg.server.audit_db)
+    rows = db.execute("SELECT account_id, score, rule_score, action, reason_codes FROM risk_scores ORDER BY id").fetchall()
+    names = {v: k.lower() for k, v in P.ACTION.items()}
+    for t, r, (aid, sc, rs, act, reasons) in zip(txs, resp, rows):
+        assert (aid, sc, rs) == (t["account_id"], r.score, r.rule_score)
+        assert names[r.action].endswith(act) and json.loads(reasons) == list(r.reason_codes)
+    eng.score_tx_many_bytes([eng._tx_bytes(t) for t in txs[:7]], [0.0] * 7)
+    srv = HttpServer(eng).start()
+    try:
+        req = urllib.request.Request(f"http://127.0.0.1:{srv.port}/admin/flush_audit", data=b"", method="POST")
+        with urllib.request.urlopen(req, timeout=30) as r:
+            assert json.loads(r.read()) == {"rows": 7}
+    finally:
+        srv.stop()
+    assert db.execute("SELECT COUNT(*) FROM risk_scores").fetchone()[0] == 57
