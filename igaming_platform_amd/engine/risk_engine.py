@@ -97,6 +97,7 @@ class RiskEngine:
         self._lock = threading.RLock()
         self.scoring = cfg.scoring
         self.audit: collections.deque = collections.deque(maxlen=100_000)
+        self.ltv_audit: collections.deque = collections.deque(maxlen=100_000)
 
         # ---- models
         fm = _load_onnx(fraud_model if fraud_model is not None else cfg.fraud_model.path)
@@ -319,13 +320,16 @@ class RiskEngine:
 
     def flush_audit(self, path: str) -> int:
         """Drain the audit ring into the ``risk_scores`` table of the SQLite database at ``path``
-        (created from ``deploy/schema.sql`` if absent). The reference declares the table
-        (init-db.sql:122-138) and never writes it. Returns the number of rows written."""
+        (created from ``deploy/schema.sql`` if absent), and the LTV ring (PredictLTV /
+        GetPlayerSegment answers) into ``ltv_predictions``. The reference declares both tables
+        (init-db.sql:122-155) and never writes them. Returns the number of rows written."""
         import sqlite3
 
         with self._lock:
             rows = list(self.audit)
             self.audit.clear()
+            ltv_rows = list(self.ltv_audit)
+            self.ltv_audit.clear()
         db = sqlite3.connect(path)
         try:
             has = db.execute("SELECT name FROM sqlite_master WHERE type='table' AND name='risk_scores'").fetchone()
@@ -341,10 +345,16 @@ class RiskEngine:
                             json.dumps(reasons), str(self.model_version), ts))
             db.executemany("INSERT INTO risk_scores(account_id, score, rule_score, ml_score, action, reason_codes,"
                            " model_version, created_at) VALUES (?,?,?,?,?,?,?,?)", out)
+            from ..golden.ltv import SEGMENTS
+            db.executemany("INSERT INTO ltv_predictions(account_id, predicted_ltv, segment, churn_risk, survival_days,"
+                           " confidence, next_best_action, model_version, created_at) VALUES (?,?,?,?,?,?,?,?,?)",
+                           [(r.account_id, float(r.predicted_ltv), SEGMENTS[int(r.segment)], float(r.churn_risk),
+                             int(r.survival_days), float(r.confidence), r.next_best_action, str(self.model_version), ts)
+                            for ts, r in ltv_rows])
             db.commit()
         finally:
             db.close()
-        return len(rows)
+        return len(rows) + len(ltv_rows)
 
     # ================================================================== python-level API
     def _tx_bytes(self, tx: Dict) -> bytes:
@@ -526,10 +536,13 @@ class RiskEngine:
         self.ltv.set_players(account_ids, features, ext)
 
     def predict_ltv(self, account_id: str):
-        return self.ltv.predict([account_id])[0]
+        return self.predict_ltv_batch([account_id])[0]
 
     def predict_ltv_batch(self, account_ids: Sequence[str]):
-        return self.ltv.predict(account_ids)
+        out = self.ltv.predict(account_ids)
+        ts = time.time()
+        self.ltv_audit.extend((ts, r) for r in out if r.found)
+        return out
 
     def check_bonus_abuse(self, account_id: str, bonus_id: str = "", now: Optional[int] = None):
         now = int(time.time()) if now is None else int(now)

@@ -176,6 +176,28 @@ def test_ltv_and_segment_cpu():
     assert not eng.predict_ltv("unknown").found
 
 
+def test_ltv_predictions_audit(tmp_path):
+    """Answered PredictLTV calls land in ltv_predictions (init-db.sql:141-155, declared and never
+    written by the reference) with the values returned; unknown players are not logged."""
+    import sqlite3
+    eng = RiskEngine(Config(), backend="cpu", capacity=50)
+    vip = GL.PlayerFeatures(days_since_registration=400, days_since_last_bet=1, days_since_last_deposit=2,
+                            sessions_per_week=6, deposit_frequency=5, net_revenue=20000, bet_count=500)
+    low = GL.PlayerFeatures(days_since_registration=30, days_since_last_bet=40, days_since_last_deposit=50,
+                            sessions_per_week=0.2, deposit_frequency=0.1, net_revenue=15, bet_count=3)
+    eng.set_players(["vip", "low"], [vip, low])
+    got = eng.predict_ltv_batch(["vip", "low", "nobody"])
+    path = str(tmp_path / "audit.db")
+    assert eng.flush_audit(path) == 2 and len(eng.ltv_audit) == 0
+    rows = sqlite3.connect(path).execute(
+        "SELECT account_id, predicted_ltv, segment, churn_risk, survival_days, next_best_action "
+        "FROM ltv_predictions ORDER BY id").fetchall()
+    assert [r[0] for r in rows] == ["vip", "low"]
+    for r, g in zip(rows, got):
+        assert r[1] == pytest.approx(g.predicted_ltv, rel=1e-6) and r[2] == GL.SEGMENTS[g.segment]
+        assert r[3] == pytest.approx(g.churn_risk, rel=1e-6) and r[4] == g.survival_days and r[5] == g.next_best_action
+
+
 def test_ltv_model_cpu_matches_executor():
     from igaming_platform_amd.engine.ltv import ltv_model_input
     from igaming_platform_amd.native import native
