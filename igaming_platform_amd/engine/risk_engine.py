@@ -13,7 +13,6 @@ every shard's device config block (fixes the unguarded read of quirk Q6).
 """
 from __future__ import annotations
 
-import collections
 import dataclasses
 import json
 import os
@@ -31,6 +30,7 @@ from ..native import native
 from ..obs.logging import get_logger
 from ..obs.metrics import Metrics
 from ..utils.faults import Faults, InjectedFault
+from .audit import AuditLog
 from .backends import CpuBackend, GpuBackend, NativeCpuBackend
 from .registry import AccountRegistry
 
@@ -96,8 +96,8 @@ class RiskEngine:
         self.links = N.LinkIndex(32)
         self._lock = threading.RLock()
         self.scoring = cfg.scoring
-        self.audit: collections.deque = collections.deque(maxlen=100_000)
-        self.ltv_audit: collections.deque = collections.deque(maxlen=100_000)
+        # risk_scores / ltv_predictions audit (engine/audit.py): on when AUDIT_DB is configured
+        self.auditlog = AuditLog(enabled=bool(cfg.server.audit_db))
 
         # ---- models
         fm = _load_onnx(fraud_model if fraud_model is not None else cfg.fraud_model.path)
@@ -149,6 +149,7 @@ class RiskEngine:
         lm = _load_onnx(ltv_model if ltv_model is not None else cfg.ltv_model.path)
         am = _load_onnx(abuse_model if abuse_model is not None else cfg.abuse_model.path)
         ltv_width = int(lm.inputs()[0][2][-1]) if lm is not None else 0
+        self.ltv_model_version = "onnx-1" if lm is not None else "rules"  # ltv.go:113-151 formula
         if spmd is not None:
             lg = None
             if backend == "gpu":
@@ -211,6 +212,7 @@ class RiskEngine:
     def _score_parsed(self, rb, now: int, want_features: bool = True):
         """RequestBatch -> (ResultRec [n,2] uint32, FeatRec [n] or None)."""
         n = len(rb)
+        version = self.model_version  # read before scoring: a concurrent reload bumps it after its swap
         slots, owners, _ = self.registry.resolve_batch(rb, insert=True)
         req = np.empty(n, REQREC)
         rb.pack_reqrec(slots, req.view(np.uint8), now, None)
@@ -219,8 +221,7 @@ class RiskEngine:
             res, feats = self.group.score(req, now, want_features)
             cols = rb.columns()
             self.links.add(cols["device_hash"], (owners.astype(np.int64) << 32) | np.where(slots >= 0, slots, -1))
-            self.metrics.observe_results(res)
-            self.metrics.batch_size.observe(n)
+            self._observe(rb, res, version)
             return res, feats, slots, owners
         res = np.zeros((n, 2), np.uint32)
         feats = np.zeros(n, FEATREC) if want_features else None
@@ -241,9 +242,20 @@ class RiskEngine:
                     feats[sel] = f
         cols = rb.columns()
         self.links.add(cols["device_hash"], (owners.astype(np.int64) << 32) | np.where(slots >= 0, slots, -1))
-        self.metrics.observe_results(res)
-        self.metrics.batch_size.observe(n)
+        self._observe(rb, res, version)
         return res, feats, slots, owners
+
+    def _observe(self, rb, res: np.ndarray, version: int) -> None:
+        """Metrics + the risk_scores audit entry of one scored batch (every scoring entry point
+        goes through :meth:`_score_parsed`, so ScoreWithExplanation and /debug/score are logged
+        too). ``version`` is the model version the batch was scored with."""
+        self.metrics.observe_results(res)
+        self.metrics.batch_size.observe(len(res))
+        if self.auditlog.enabled:
+            before = self.auditlog.evicted_rows
+            self.auditlog.record_scores(rb.account_id, res, version)
+            if self.auditlog.evicted_rows != before:
+                self.metrics.audit_evicted.inc(self.auditlog.evicted_rows - before)
 
     def _submit(self, o: int, sub: np.ndarray, now: int, want_features: bool):
         be = self.backends[o]
@@ -296,7 +308,6 @@ class RiskEngine:
         rb.parse_batch(data)
         res, feats, slots, owners = self._score_parsed(rb, int(time.time()))
         ms = np.full(len(rb), int((time.perf_counter() - t0) * 1e3), np.int64)
-        self._audit(rb, res)
         return self.N.serialize_batch_response(res, feats.view(np.int32).reshape(-1, 32) if feats is not None else None, ms)
 
     def score_tx_bytes(self, data: bytes, t0: Optional[float] = None) -> bytes:
@@ -309,52 +320,15 @@ class RiskEngine:
         res, feats, _, _ = self._score_parsed(rb, int(time.time()))
         now = time.perf_counter()
         ms = np.array([int((now - t) * 1e3) for t in t0s], np.int64)
-        self._audit(rb, res)
         return self.N.serialize_tx_responses(res, feats.view(np.int32).reshape(-1, 32) if feats is not None else None, ms)
 
-    def _audit(self, rb, res: np.ndarray) -> None:
-        """risk_scores audit log (init-db.sql:122-138) as an in-memory ring; ids resolved lazily."""
-        ts = time.time()
-        ids = rb.account_id
-        self.audit.extend(zip([ts] * len(ids), ids, res[:, 0].tolist(), res[:, 1].tolist()))
-
     def flush_audit(self, path: str) -> int:
-        """Drain the audit ring into the ``risk_scores`` table of the SQLite database at ``path``
-        (created from ``deploy/schema.sql`` if absent), and the LTV ring (PredictLTV /
-        GetPlayerSegment answers) into ``ltv_predictions``. The reference declares both tables
-        (init-db.sql:122-155) and never writes them. Returns the number of rows written."""
-        import sqlite3
-
-        with self._lock:
-            rows = list(self.audit)
-            self.audit.clear()
-            ltv_rows = list(self.ltv_audit)
-            self.ltv_audit.clear()
-        db = sqlite3.connect(path)
-        try:
-            has = db.execute("SELECT name FROM sqlite_master WHERE type='table' AND name='risk_scores'").fetchone()
-            if not has:
-                schema = os.path.join(os.path.dirname(__file__), "..", "..", "deploy", "schema.sql")
-                db.executescript(open(schema).read())
-            recs = np.array([(p, m) for _, _, p, m in rows], np.uint32).reshape(-1, 2)
-            ml = recs[:, 1].view(np.float32)
-            out = []
-            for (ts, aid, p, _), m in zip(rows, ml.tolist()):
-                reasons = [REASON_CODES[b] for b in range(len(REASON_CODES)) if (p >> 20) >> b & 1]
-                out.append((aid, p & 0xFF, (p >> 8) & 0xFF, m, ACTION_NAMES.get((p >> 16) & 3, "unspecified"),
-                            json.dumps(reasons), str(self.model_version), ts))
-            db.executemany("INSERT INTO risk_scores(account_id, score, rule_score, ml_score, action, reason_codes,"
-                           " model_version, created_at) VALUES (?,?,?,?,?,?,?,?)", out)
-            from ..golden.ltv import SEGMENTS
-            db.executemany("INSERT INTO ltv_predictions(account_id, predicted_ltv, segment, churn_risk, survival_days,"
-                           " confidence, next_best_action, model_version, created_at) VALUES (?,?,?,?,?,?,?,?,?)",
-                           [(r.account_id, float(r.predicted_ltv), SEGMENTS[int(r.segment)], float(r.churn_risk),
-                             int(r.survival_days), float(r.confidence), r.next_best_action, str(self.model_version), ts)
-                            for ts, r in ltv_rows])
-            db.commit()
-        finally:
-            db.close()
-        return len(rows) + len(ltv_rows)
+        """Drain the score audit ring into the ``risk_scores`` table of the SQLite database at
+        ``path`` and the LTV ring (PredictLTV / GetPlayerSegment answers) into
+        ``ltv_predictions`` (deploy/schema.sql; the reference declares both tables,
+        init-db.sql:122-155, and never writes them). Rows survive a failed write. Returns the
+        number of rows written."""
+        return self.auditlog.flush(path)
 
     # ================================================================== python-level API
     def _tx_bytes(self, tx: Dict) -> bytes:
@@ -540,8 +514,7 @@ class RiskEngine:
 
     def predict_ltv_batch(self, account_ids: Sequence[str]):
         out = self.ltv.predict(account_ids)
-        ts = time.time()
-        self.ltv_audit.extend((ts, r) for r in out if r.found)
+        self.auditlog.record_ltv(out, self.ltv_model_version)
         return out
 
     def check_bonus_abuse(self, account_id: str, bonus_id: str = "", now: Optional[int] = None):

@@ -35,6 +35,8 @@ class Metrics:
         self.queue_depth = Gauge("gpu_queue_depth", "requests waiting in the micro-batcher", ["gpu"], registry=r)
         self.gpu_healthy = Gauge("gpu_healthy", "1 if the shard is serving from its GPU", ["gpu"], registry=r)
         self.collective = Histogram("rccl_seconds", "collective time by op", ["op"], buckets=LAT_BUCKETS, registry=r)
+        self.audit_evicted = Counter("risk_audit_evicted_rows_total",
+                                     "audit rows dropped from the ring before a flush", registry=r)
         self.fallbacks = Counter("risk_fallback_total", "rows scored by the CPU fallback", ["reason"], registry=r)
         self.accounts = Gauge("risk_accounts", "accounts resident in the feature store", ["gpu"], registry=r)
 

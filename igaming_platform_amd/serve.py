@@ -47,6 +47,8 @@ def main(argv=None) -> int:
     ap.add_argument("--snapshot-dir", default=os.environ.get("RISK_SNAPSHOT_DIR", ""))
     ap.add_argument("--snapshot-every-s", type=float, default=300.0)
     ap.add_argument("--no-batching", action="store_true")
+    ap.add_argument("--audit-flush-every-s", type=float, default=2.0,
+                    help="drain the risk_scores / ltv_predictions rings into AUDIT_DB this often")
     a = ap.parse_args(argv)
     cfg = Config.load(a.config or None)
     if a.gpus:
@@ -84,13 +86,18 @@ def main(argv=None) -> int:
 
     signal.signal(signal.SIGINT, _sig)
     signal.signal(signal.SIGTERM, _sig)
-    last_snap = time.time()
+    from .engine.audit import flush_if_configured
+    last_snap = last_flush = time.time()
     while not stop.wait(1.0):
         if a.snapshot_dir and time.time() - last_snap >= a.snapshot_every_s:
             eng.snapshot(a.snapshot_dir)
             last_snap = time.time()
+        if time.time() - last_flush >= a.audit_flush_every_s:  # AUDIT_DB set: drain the audit rings
+            flush_if_configured(eng, log)
+            last_flush = time.time()
     gs.stop(cfg.server.shutdown_grace_s)
     hs.stop()
+    flush_if_configured(eng, log)  # rows scored during the grace period
     if a.snapshot_dir:
         eng.snapshot(a.snapshot_dir)
     eng.close()

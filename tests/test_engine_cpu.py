@@ -180,7 +180,9 @@ def test_ltv_predictions_audit(tmp_path):
     """Answered PredictLTV calls land in ltv_predictions (init-db.sql:141-155, declared and never
     written by the reference) with the values returned; unknown players are not logged."""
     import sqlite3
-    eng = RiskEngine(Config(), backend="cpu", capacity=50)
+    cfg = Config()
+    cfg.server.audit_db = str(tmp_path / "audit.db")
+    eng = RiskEngine(cfg, backend="cpu", capacity=50)
     vip = GL.PlayerFeatures(days_since_registration=400, days_since_last_bet=1, days_since_last_deposit=2,
                             sessions_per_week=6, deposit_frequency=5, net_revenue=20000, bet_count=500)
     low = GL.PlayerFeatures(days_since_registration=30, days_since_last_bet=40, days_since_last_deposit=50,
@@ -188,14 +190,15 @@ def test_ltv_predictions_audit(tmp_path):
     eng.set_players(["vip", "low"], [vip, low])
     got = eng.predict_ltv_batch(["vip", "low", "nobody"])
     path = str(tmp_path / "audit.db")
-    assert eng.flush_audit(path) == 2 and len(eng.ltv_audit) == 0
+    assert eng.flush_audit(path) == 2 and eng.auditlog.pending() == 0
     rows = sqlite3.connect(path).execute(
-        "SELECT account_id, predicted_ltv, segment, churn_risk, survival_days, next_best_action "
+        "SELECT account_id, predicted_ltv, segment, churn_risk, survival_days, next_best_action, model_version "
         "FROM ltv_predictions ORDER BY id").fetchall()
     assert [r[0] for r in rows] == ["vip", "low"]
     for r, g in zip(rows, got):
         assert r[1] == pytest.approx(g.predicted_ltv, rel=1e-6) and r[2] == GL.SEGMENTS[g.segment]
         assert r[3] == pytest.approx(g.churn_risk, rel=1e-6) and r[4] == g.survival_days and r[5] == g.next_best_action
+        assert r[6] == "rules"  # the LTV model's own version, not the fraud model's
 
 
 def test_ltv_model_cpu_matches_executor():
@@ -338,7 +341,7 @@ def test_audit_ring_drains_into_risk_scores(tmp_path):
     txs = _txs(50, np.random.default_rng(9))
     out = eng.score_tx_many_bytes([eng._tx_bytes(t) for t in txs], [0.0] * len(txs))
     resp = [P.ScoreTransactionResponse.FromString(b) for b in out]
-    assert eng.flush_audit(cfg.server.audit_db) == 50 and len(eng.audit) == 0
+    assert eng.flush_audit(cfg.server.audit_db) == 50 and eng.auditlog.pending() == 0
     db = sqlite3.connect(cfg.server.audit_db)
     rows = db.execute("SELECT account_id, score, rule_score, action, reason_codes FROM risk_scores ORDER BY id").fetchall()
     names = {v: k.lower() for k, v in P.ACTION.items()}
@@ -354,3 +357,56 @@ def test_audit_ring_drains_into_risk_scores(tmp_path):
     finally:
         srv.stop()
     assert db.execute("SELECT COUNT(*) FROM risk_scores").fetchone()[0] == 57
+
+
+def test_audit_version_stamped_at_score_time_and_explain_logged(tmp_path):
+    """rows scored before a model reload keep the old model version; explain()
+    (ScoreWithExplanation, /debug/score) and score() are audited like the wire paths."""
+    import sqlite3
+    from igaming_platform_amd.onnx import builders
+    cfg = Config()
+    cfg.server.audit_db = str(tmp_path / "audit.db")
+    eng = RiskEngine(cfg, backend="cpu", capacity=60)
+    txs = _txs(6, np.random.default_rng(3))
+    eng.score(txs[:3])
+    eng.explain(txs[3])
+    eng.reload_model(builders.build("logistic", n_features=30).SerializeToString())
+    eng.score(txs[4:6])
+    assert eng.flush_audit(cfg.server.audit_db) == 6
+    vers = [r[0] for r in sqlite3.connect(cfg.server.audit_db).execute(
+        "SELECT model_version FROM risk_scores ORDER BY id")]
+    assert vers == ["1"] * 4 + ["2"] * 2
+
+
+def test_audit_flush_into_db_without_ltv_table_and_failure_keeps_rows(tmp_path):
+    """The schema script runs on every flush (an existing DB with only risk_scores gains
+    ltv_predictions), and a failed write puts the drained rows back."""
+    import sqlite3
+    cfg = Config()
+    path = str(tmp_path / "old.db")
+    db = sqlite3.connect(path)
+    db.execute("CREATE TABLE risk_scores (id INTEGER PRIMARY KEY AUTOINCREMENT, account_id TEXT, score INT,"
+               " rule_score INT, ml_score REAL, action TEXT, reason_codes TEXT, model_version TEXT, created_at REAL)")
+    db.commit()
+    db.close()
+    cfg.server.audit_db = path
+    eng = RiskEngine(cfg, backend="cpu", capacity=60)
+    vip = GL.PlayerFeatures(days_since_registration=400, days_since_last_bet=1, days_since_last_deposit=2,
+                            sessions_per_week=6, deposit_frequency=5, net_revenue=20000, bet_count=500)
+    eng.set_players(["vip"], [vip])
+    eng.predict_ltv("vip")
+    eng.score(_txs(4, np.random.default_rng(1)))
+    assert eng.flush_audit(path) == 5
+    eng.score(_txs(3, np.random.default_rng(2)))
+    bad = str(tmp_path / "no_such_dir" / "x.db")
+    with pytest.raises(sqlite3.OperationalError):
+        eng.flush_audit(bad)
+    assert eng.auditlog.pending() == 3
+    assert eng.flush_audit(path) == 3
+    assert sqlite3.connect(path).execute("SELECT COUNT(*) FROM risk_scores").fetchone()[0] == 7
+
+
+def test_audit_disabled_without_audit_db():
+    eng = RiskEngine(Config(), backend="cpu", capacity=20)
+    eng.score(_txs(3, np.random.default_rng(1)))
+    assert eng.auditlog.pending() == 0
