@@ -51,8 +51,27 @@ def parse():
                     help="scorer configs: streaming mode, one launch per batch running copy(i) || state(i-1) "
                          "|| model(i-2) (measured slower on ROCm 7.2 than the default three-stream pipeline: "
                          "~35 us between consecutive multi-branch graph launches)")
+    ap.add_argument("--numerics", default="auto", choices=["auto", "fp32", "bf16"],
+                    help="dense-layer numerics: fp32 = the ONNX model's f32 contract (default for the fraud "
+                         "scorers), bf16 = bf16 MFMA with f32 accumulate (default for cfg4 / cfg5)")
     ap.add_argument("--json-out", default="")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.numerics == "auto":
+        a.numerics = "bf16" if a.config in ("cfg4", "cfg5") else "fp32"
+    if a.config == "cfg5" and a.numerics != "bf16":
+        ap.error("cfg5's GRU kernel runs bf16 weights (f32 state / accumulate) only")
+    return a
+
+
+def numerics_desc(a) -> str:
+    if a.config == "cfg5":
+        return "bf16 MFMA weights/activations, fp32 accumulate and state"
+    if a.config == "cfg4":
+        return ("bf16 MFMA weights/activations, fp32 accumulate" if a.numerics == "bf16"
+                else "fp32 MFMA (v_mfma_f32_16x16x4_f32) end to end")
+    dense = ("fp32 MFMA (v_mfma_f32_16x16x4_f32) MLP" if a.numerics == "fp32"
+             else "bf16 MFMA MLP (fp32 accumulate)")
+    return f"fp32 features+trees, {dense}, fp64 ensemble"
 
 
 def maybe_launch_torchrun(a) -> None:
@@ -99,7 +118,7 @@ def main():
     if a.stream and not a.no_graphs:
         return stream_bench(a, world, rank, dev)
     S = benchkit.build(a.config, a.batch, a.accounts, dev, rank=rank, depth=a.depth,
-                       use_graphs=not a.no_graphs)
+                       use_graphs=not a.no_graphs, precision=a.numerics)
     sc, pool, B = S.scorer, S.pool, S.batch
     c = dict(desc=S.desc)
     n_acc = a.accounts
@@ -180,7 +199,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": a.numerics,
         "data": "synthetic",
         "config": {
             "model": c["desc"],
@@ -192,7 +211,7 @@ def main():
             "pipeline_depth": a.depth,
             "graphs": not a.no_graphs,
             "driver": "native" if sc.driver is not None else "python",
-            "numerics": "fp32 features+trees, bf16 MFMA MLP (fp32 accumulate), fp64 ensemble",
+            "numerics": numerics_desc(a),
         },
         "p99_latency_ms": p99,
         "p50_latency_ms": p50,
@@ -232,7 +251,8 @@ def stream_bench(a, world: int, rank: int, dev) -> None:
     import torch.distributed as dist
     from igaming_platform_amd.utils import benchkit
     from igaming_platform_amd.utils.synth import NOW0
-    S = benchkit.build(a.config, a.batch, a.accounts, dev, rank=rank, depth=3, use_graphs=True)
+    S = benchkit.build(a.config, a.batch, a.accounts, dev, rank=rank, depth=3, use_graphs=True,
+                       precision=a.numerics)
     sc, pool, B = S.scorer, S.pool, S.batch
     sc.capture_pipelined()
     gathered = torch.zeros(world * B * 2, dtype=torch.int32, device=dev) if world > 1 else None
@@ -281,11 +301,11 @@ def stream_bench(a, world: int, rank: int, dev) -> None:
         "metric": "fraud scores/sec (whole node) + p99 score latency",
         "value": world * B * a.steps / elapsed, "unit": "scores/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "scaling": "weak", "vs_baseline": None, "dtype": a.numerics, "data": "synthetic",
         "config": {"model": S.desc, "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
                    "per_gpu_batch": B, "accounts_per_gpu": a.accounts, "pipeline": "streaming (1 launch/batch)",
                    "graphs": True,
-                   "numerics": "fp32 features+trees, bf16 MFMA MLP (fp32 accumulate), fp64 ensemble"},
+                   "numerics": numerics_desc(a)},
         "p99_latency_ms": p99, "p50_latency_ms": p50, "latency_baseline_ms": BASELINE_P99_MS,
         "latency_vs_baseline": BASELINE_P99_MS / p99 if p99 > 0 else None,
     }
@@ -298,7 +318,7 @@ def model_bench(a, world: int, rank: int, dev) -> None:
     import torch.distributed as dist
     from igaming_platform_amd.utils import benchkit
     S = benchkit.build_model(a.config, a.batch, a.accounts, dev, rank=rank, depth=a.depth,
-                             use_graphs=not a.no_graphs)
+                             use_graphs=not a.no_graphs, precision=a.numerics)
     R, B = S.runner, S.batch
     out_w = R.out[:B].numel()
     gathered = torch.zeros(world * out_w, dtype=torch.float32, device=dev) if world > 1 else None
@@ -344,11 +364,11 @@ def model_bench(a, world: int, rank: int, dev) -> None:
     out = {
         "metric": S.metric, "value": world * B * a.steps / elapsed, "unit": S.unit, "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "scaling": "weak", "vs_baseline": None, "dtype": a.numerics, "data": "synthetic",
         "config": {"model": S.desc, "global_batch": B * world, "seq_len": 100 if a.config == "cfg5" else 1,
                    "parallelism": f"dp{world}", "per_gpu_batch": B, "accounts_per_gpu": a.accounts,
                    "pipeline_depth": a.depth, "graphs": not a.no_graphs,
-                   "numerics": "bf16 MFMA weights/activations, fp32 accumulate and state"},
+                   "numerics": numerics_desc(a)},
         "p99_latency_ms": p99, "p50_latency_ms": p50,
     }
     if rank == 0:

@@ -179,7 +179,7 @@ PYBIND11_MODULE(_hipk, m) {
   auto gemm_args = [](const py::dict& d) {
     GemmArgs a{};
     a.X = ptr<const void*>(d, "X");
-    a.W = ptr<const uint16_t*>(d, "W");
+    a.W = ptr<const void*>(d, "W");
     a.bias = ptr<const float*>(d, "bias");
     a.Y = ptr<void*>(d, "Y");
     a.m_ptr = ptr<const int32_t*>(d, "m_ptr");
@@ -192,6 +192,7 @@ PYBIND11_MODULE(_hipk, m) {
     a.x_bf16 = geti(d, "x_bf16");
     a.y_bf16 = geti(d, "y_bf16");
     a.act = geti(d, "act");
+    a.w_f32 = geti(d, "w_f32", 0);
     return a;
   };
   m.def("gemm", [gemm_args](py::dict d, uintptr_t s) {
@@ -206,7 +207,8 @@ PYBIND11_MODULE(_hipk, m) {
   m.def("mlp_head", [](py::dict d, uintptr_t s) {
     HeadArgs a{};
     a.X = ptr<const void*>(d, "X");
-    a.W1 = ptr<const uint16_t*>(d, "W1");
+    a.W1 = ptr<const void*>(d, "W1");
+    a.w1_f32 = geti(d, "w1_f32", 0);
     a.b1 = ptr<const float*>(d, "b1");
     a.w2 = ptr<const float*>(d, "w2");
     a.b2 = d.contains("b2") ? d["b2"].cast<float>() : 0.f;

@@ -42,12 +42,10 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int M = a.m_ptr ? min(*a.m_ptr, a.M) : a.M;
-  // XCD-aware remap (blocks sharing an X row panel land on one XCD's L2)
-  const int nbx = (a.N + BN - 1) / BN;
   const int row0 = blockIdx.y * BM;
   const int col0 = blockIdx.x * BN;
   if (row0 >= M) return;
-  (void)nbx;
+  const uint16_t* const W = reinterpret_cast<const uint16_t*>(a.W);
   const int K = a.K;
   const int k_pad = a.ldw;
   const int n_kt = (K + G_BK - 1) / G_BK;
@@ -99,7 +97,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
       const int r = ch >> 3, kc = (ch & 7) * 8;
       const int n = col0 + r, k = k0 + kc;
       // W is zero padded to [N_pad][K_pad] with N_pad a multiple of 128, K_pad of 64
-      rb[c] = (k < k_pad) ? *reinterpret_cast<const uint4*>(a.W + (size_t)n * k_pad + k) : make_uint4(0, 0, 0, 0);
+      rb[c] = (k < k_pad) ? *reinterpret_cast<const uint4*>(W + (size_t)n * k_pad + k) : make_uint4(0, 0, 0, 0);
     }
   };
   auto store_tile = [&](int buf) {
@@ -182,7 +180,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs a) {
   for (int k = lane; k < a.K; k += 64) {
     const float x = a.x_bf16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(a.X)[(size_t)row * a.ldx + k])
                              : reinterpret_cast<const float*>(a.X)[(size_t)row * a.ldx + k];
-    s += x * bf16_to_f32(a.W[k]);
+    s += x * (a.w_f32 ? reinterpret_cast<const float*>(a.W)[k] : bf16_to_f32(reinterpret_cast<const uint16_t*>(a.W)[k]));
   }
   s = wave_sum(s);
   if (lane == 0) {
@@ -201,9 +199,14 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs a) {
 constexpr int HD_ROWS = 32;
 constexpr int HD_W_LDS_MAX = 64 * 1024;  // W1 staged in LDS up to this many bytes
 
-__device__ __forceinline__ uint4 head_a_chunk(const HeadArgs& a, int row, int kc, int M) {
-  if (row >= M) return make_uint4(0, 0, 0, 0);
-  float f[8];
+// the 8 f32 inputs of row `row`, columns kc..kc+7 (zero past K / M); returns false when the
+// chunk is already bf16 (x_bf16 input, packed into *raw)
+__device__ __forceinline__ bool head_a_f32(const HeadArgs& a, int row, int kc, int M, float f[8], uint4* raw) {
+  if (row >= M) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = 0.f;
+    return true;
+  }
   if (a.partial) {
     // reduce the tree ensemble's group partials: sum_g P[g][row][k] (+ base, / T)
     if (kc + 8 <= a.K && (a.K & 3) == 0 && a.groups <= 8) {
@@ -237,8 +240,7 @@ __device__ __forceinline__ uint4 head_a_chunk(const HeadArgs& a, int row, int kc
         if (a.p_average) f[j] /= (float)a.p_ntrees;
         f[j] += bb[j];  // 0 without a base: x + 0 == x
       }
-      return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
-                        pack_bf16x2(f[6], f[7]));
+      return true;
     } else if (kc + 8 <= a.K && (a.K & 3) == 0) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = 0.f;
@@ -271,18 +273,29 @@ __device__ __forceinline__ uint4 head_a_chunk(const HeadArgs& a, int row, int kc
     uint16_t t[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) t[j] = (kc + j < a.K) ? src[j] : 0;
-    return make_uint4(t[0] | (t[1] << 16), t[2] | (t[3] << 16), t[4] | (t[5] << 16), t[6] | (t[7] << 16));
+    *raw = make_uint4(t[0] | (t[1] << 16), t[2] | (t[3] << 16), t[4] | (t[5] << 16), t[6] | (t[7] << 16));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = bf16_to_f32(t[j]);
+    return false;
   } else {
     const float* src = reinterpret_cast<const float*>(a.X) + (size_t)row * a.ldx + kc;
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = (kc + j < a.K) ? src[j] : 0.f;
   }
+  return true;
+}
+
+__device__ __forceinline__ uint4 head_a_chunk(const HeadArgs& a, int row, int kc, int M) {
+  float f[8];
+  uint4 raw;
+  if (!head_a_f32(a, row, kc, M, f, &raw)) return raw;
   return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
                     pack_bf16x2(f[6], f[7]));
 }
 
 __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a, int w_lds) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint16_t* const W1 = reinterpret_cast<const uint16_t*>(a.W1);
   const int kp = a.k_pad;
   const int lds_row = kp + G_PAD;
   const int n1p = (a.N1 + 63) & ~63;
@@ -320,7 +333,7 @@ __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a, int w_lds) {
 #pragma unroll
   for (int u = 0; u < UN; ++u) {
     const int ch = u * 256 + tid;
-    wv[u] = ch < wtotal ? *reinterpret_cast<const uint4*>(a.W1 + (size_t)(ch / kch) * kp + (ch % kch) * 8)
+    wv[u] = ch < wtotal ? *reinterpret_cast<const uint4*>(W1 + (size_t)(ch / kch) * kp + (ch % kch) * 8)
                         : make_uint4(0, 0, 0, 0);
   }
   const float b1v = (tid < a.N1 && a.b1) ? a.b1[tid] : 0.f;
@@ -348,7 +361,7 @@ __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a, int w_lds) {
 #pragma unroll
       for (int u = 0; u < UN; ++u) {
         const int ch = base + u * 256 + tid;
-        v[u] = ch < total ? *reinterpret_cast<const uint4*>(a.W1 + (size_t)(ch / kch) * kp + (ch % kch) * 8)
+        v[u] = ch < total ? *reinterpret_cast<const uint4*>(W1 + (size_t)(ch / kch) * kp + (ch % kch) * 8)
                           : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
@@ -375,7 +388,7 @@ __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a, int w_lds) {
     for (int k0 = 0; k0 < kp; k0 += 32) {
       const int kof = k0 + 8 * (lane >> 4);
       const bf16x8 fb = w_lds ? *reinterpret_cast<const bf16x8*>(&sW[n * lds_row + kof])
-                              : *reinterpret_cast<const bf16x8*>(a.W1 + (size_t)n * kp + kof);
+                              : *reinterpret_cast<const bf16x8*>(W1 + (size_t)n * kp + kof);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const bf16x8 fa = *reinterpret_cast<const bf16x8*>(&sA[(i * 16 + (lane & 15)) * lds_row + kof]);
@@ -431,8 +444,251 @@ __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a, int w_lds) {
 #undef HD_MARK
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Reference-precision (fp32) variants: the ONNX fraud model contract is f32
+// (onnx_model.go:221-238), and final = int(0.4 rule + 0.6 ml 100) truncates, so a bf16 head
+// (~1e-2 ml error) moves decisions across thresholds. These keep every operand in f32 and run
+// on v_mfma_f32_16x16x4_f32: lane l supplies A[l & 15][k] and B[k][l & 15] with
+// k = 4 (l >> 4) + j for the j-th of four consecutive MFMAs, so one 16-B LDS read per operand
+// feeds four MFMAs and four MFMAs cover 16 k (the sum over k is order-free up to rounding).
+typedef __attribute__((ext_vector_type(4))) float f32v4;
+
+__device__ __forceinline__ f32x4 mfma4_f32(const float4& av, const float4& bv, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc, 0, 0, 0);
+  return acc;
+}
+
+// mlp_head in f32: same blocking as the bf16 kernel (32 rows per block, 4 waves x 16 hidden
+// columns per 64-column chunk), A tile and W1 (f32 [n1p][k_pad]) staged in LDS with rows
+// padded by 4 floats.
+__global__ void __launch_bounds__(256) mlp_head_f32_kernel(HeadArgs a, int w_lds) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  const float* const W1 = reinterpret_cast<const float*>(a.W1);
+  const int kp = a.k_pad;
+  const int lds_row = kp + 4;
+  const int n1p = (a.N1 + 63) & ~63;
+  float* sA = smf;
+  float* sW = sA + HD_ROWS * lds_row;
+  float* sred = sW + (w_lds ? n1p * lds_row : 0);
+  float* sb1 = sred + 4 * HD_ROWS;
+  float* sw2 = sb1 + n1p;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = a.m_ptr ? min(*a.m_ptr, a.M) : a.M;
+  const int row0 = blockIdx.x * HD_ROWS;
+  __shared__ unsigned int ecnt[MET_N];
+  const bool fm = a.fuse_ens && a.ens.metrics;
+  if (row0 >= M) {
+    if (a.fuse_ens)
+      for (int r = row0 + tid; r < min(row0 + HD_ROWS, a.ens.n_rows); r += 256) ensemble_row(a.ens, r, true, 0.f, nullptr);
+    return;
+  }
+  if (fm)
+    for (int i = tid; i < MET_N; i += 256) ecnt[i] = 0;
+  const int kq = kp / 4;  // float4 chunks per row
+  if (w_lds) {
+    const int total = n1p * kq;
+    for (int base = 0; base < total; base += 256 * 4) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int ch = base + u * 256 + tid;
+        v[u] = ch < total ? *reinterpret_cast<const float4*>(W1 + (size_t)(ch / kq) * kp + (ch % kq) * 4)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int ch = base + u * 256 + tid;
+        if (ch < total) *reinterpret_cast<float4*>(&sW[(ch / kq) * lds_row + (ch % kq) * 4]) = v[u];
+      }
+    }
+  }
+  for (int n = tid; n < n1p; n += 256) {
+    sb1[n] = (n < a.N1 && a.b1) ? a.b1[n] : 0.f;
+    sw2[n] = n < a.N1 ? a.w2[n] : 0.f;
+  }
+  const int k8 = kp / 8;
+  for (int ch = tid; ch < HD_ROWS * k8; ch += 256) {
+    const int r = ch / k8, kc = (ch % k8) * 8;
+    float f[8];
+    uint4 raw;
+    head_a_f32(a, row0 + r, kc, M, f, &raw);
+    *reinterpret_cast<float4*>(&sA[r * lds_row + kc]) = make_float4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<float4*>(&sA[r * lds_row + kc + 4]) = make_float4(f[4], f[5], f[6], f[7]);
+  }
+  __syncthreads();
+  float part[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) part[i][q] = 0.f;
+  for (int c0 = 0; c0 < a.N1; c0 += 64) {
+    const int n = c0 + wave * 16 + (lane & 15);
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    for (int k0 = 0; k0 < kp; k0 += 16) {
+      const int kk = k0 + 4 * (lane >> 4);
+      const float4 bv = w_lds ? *reinterpret_cast<const float4*>(&sW[n * lds_row + kk])
+                              : *reinterpret_cast<const float4*>(W1 + (size_t)n * kp + kk);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float4 av = *reinterpret_cast<const float4*>(&sA[(i * 16 + (lane & 15)) * lds_row + kk]);
+        acc[i] = mfma4_f32(av, bv, acc[i]);
+      }
+    }
+    const float b1 = sb1[n];
+    const float w2 = sw2[n];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) part[i][q] += act_fn(acc[i][q] + b1, a.act1) * w2;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v = part[i][q];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      part[i][q] = v;
+    }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sred[wave * HD_ROWS + i * 16 + (lane >> 4) * 4 + q] = part[i][q];
+  }
+  __syncthreads();
+  if (tid < HD_ROWS) {
+    const int row = row0 + tid;
+    float y = 0.f;
+    if (row < M) {
+      const float v = sred[tid] + sred[HD_ROWS + tid] + sred[2 * HD_ROWS + tid] + sred[3 * HD_ROWS + tid];
+      y = act_fn(v + a.b2, a.act2);
+      a.Y[(size_t)row * a.ldy] = y;
+    }
+    if (a.fuse_ens && row < a.ens.n_rows) ensemble_row(a.ens, row, true, y, fm ? ecnt : nullptr);
+  }
+  if (fm) {
+    __syncthreads();
+    ensemble_metrics_flush(a.ens, ecnt, tid, 256);
+  }
+}
+
+// f32 dense layer: 64 x 64 output tile per block, 4 waves in 2 x 2 (32 x 32 each = 2 x 2
+// fragments), BK = 32 floats staged in two LDS buffers (next tile's global loads in flight
+// under the current tile's MFMAs).
+constexpr int GF_BK = 32;
+constexpr int GF_ROW = GF_BK + 4;
+__global__ void __launch_bounds__(256) gemm_f32_kernel(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) float sA[2][64 * GF_ROW];
+  __shared__ __attribute__((aligned(16))) float sB[2][64 * GF_ROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int M = a.m_ptr ? min(*a.m_ptr, a.M) : a.M;
+  const int row0 = blockIdx.y * 64, col0 = blockIdx.x * 64;
+  if (row0 >= M) return;
+  const float* const W = reinterpret_cast<const float*>(a.W);
+  const int K = a.K, k_pad = a.ldw;
+  const int n_kt = (K + GF_BK - 1) / GF_BK;
+  float4 ra[2], rb[2];
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * GF_BK;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int ch = tid + c * 256;          // 512 chunks = 64 rows x 8 float4
+      const int r = ch >> 3, kc = (ch & 7) * 4;
+      const int row = row0 + r, k = k0 + kc;
+      float f[4] = {0.f, 0.f, 0.f, 0.f};
+      if (row < M) {
+        if (a.x_bf16) {
+          const uint16_t* src = reinterpret_cast<const uint16_t*>(a.X) + (size_t)row * a.ldx + k;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) f[j] = (k + j < K) ? bf16_to_f32(src[j]) : 0.f;
+        } else {
+          const float* src = reinterpret_cast<const float*>(a.X) + (size_t)row * a.ldx + k;
+          if (k + 4 <= K && (a.ldx & 3) == 0) {
+            const float4 p = *reinterpret_cast<const float4*>(src);
+            f[0] = p.x; f[1] = p.y; f[2] = p.z; f[3] = p.w;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) f[j] = (k + j < K) ? src[j] : 0.f;
+          }
+        }
+      }
+      ra[c] = make_float4(f[0], f[1], f[2], f[3]);
+      const int n = col0 + r;
+      rb[c] = (k < k_pad) ? *reinterpret_cast<const float4*>(W + (size_t)n * k_pad + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int ch = tid + c * 256;
+      *reinterpret_cast<float4*>(&sA[buf][(ch >> 3) * GF_ROW + (ch & 7) * 4]) = ra[c];
+      *reinterpret_cast<float4*>(&sB[buf][(ch >> 3) * GF_ROW + (ch & 7) * 4]) = rb[c];
+    }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < n_kt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < n_kt) load_tile(kt + 1);
+#pragma unroll
+    for (int kk = 0; kk < GF_BK; kk += 16) {
+      const int kof = kk + 4 * (lane >> 4);
+      float4 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const float4*>(&sA[cur][(wm * 32 + i * 16 + (lane & 15)) * GF_ROW + kof]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = *reinterpret_cast<const float4*>(&sB[cur][(wn * 32 + j * 16 + (lane & 15)) * GF_ROW + kof]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma4_f32(fa[i], fb[j], acc[i][j]);
+    }
+    if (kt + 1 < n_kt) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = col0 + wn * 32 + j * 16 + (lane & 15);
+      if (col >= a.N) continue;
+      const float b = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = row0 + wm * 32 + i * 16 + (lane >> 4) * 4 + q;
+        if (row >= M) continue;
+        const float v = act_fn(acc[i][j][q] + b, a.act);
+        if (a.y_bf16) reinterpret_cast<uint16_t*>(a.Y)[(size_t)row * a.ldy + col] = f32_to_bf16(v);
+        else reinterpret_cast<float*>(a.Y)[(size_t)row * a.ldy + col] = v;
+      }
+    }
+}
+
 void launch_mlp_head(const HeadArgs& a, hipStream_t st) {
   if (a.M <= 0) return;
+  if (a.w1_f32) {
+    const size_t lds_row = (size_t)a.k_pad + 4;
+    const size_t n1p = (size_t)((a.N1 + 63) & ~63);
+    const int w_lds = n1p * lds_row * 4 <= (size_t)(96 * 1024);
+    const size_t lds = ((size_t)HD_ROWS + (w_lds ? n1p : 0)) * lds_row * 4 + 4 * HD_ROWS * sizeof(float) +
+                       2 * n1p * sizeof(float);
+    hipLaunchKernelGGL(mlp_head_f32_kernel, dim3((a.M + HD_ROWS - 1) / HD_ROWS), dim3(256), lds, st, a, w_lds);
+    return;
+  }
   const size_t lds_row = (size_t)a.k_pad + G_PAD;
   const size_t n1p = (size_t)((a.N1 + 63) & ~63);
   const int w_lds = n1p * lds_row * 2 <= (size_t)HD_W_LDS_MAX;
@@ -443,6 +699,10 @@ void launch_mlp_head(const HeadArgs& a, hipStream_t st) {
 
 void launch_gemm(const GemmArgs& a, hipStream_t st) {
   if (a.M <= 0) return;
+  if (a.w_f32) {
+    hipLaunchKernelGGL(gemm_f32_kernel, dim3((a.N + 63) / 64, (a.M + 63) / 64), dim3(256), 0, st, a);
+    return;
+  }
   const bool big = a.M >= 4096 && a.N >= 128;
   if (big) {
     dim3 grid((a.N + 127) / 128, (a.M + 127) / 128);

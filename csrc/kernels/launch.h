@@ -109,7 +109,7 @@ void launch_tree_ensemble_grouped(const TreeArgs& a, int groups, float* partial,
 // ---- K3 dense layers: Y = act(X W^T + b)
 struct GemmArgs {
   const void* X;            // [M][ldx] f32 or bf16
-  const uint16_t* W;        // bf16 [N_pad][K_pad] (row n = output column n)
+  const void* W;            // bf16 or f32 (w_f32) [N_pad][K_pad] (row n = output column n)
   const float* bias;        // [N] nullable
   void* Y;                  // [M][ldy] f32 or bf16
   const int32_t* m_ptr;     // live rows in device memory (nullable -> M)
@@ -117,6 +117,7 @@ struct GemmArgs {
   int32_t ldx, ldy, ldw;
   int32_t x_bf16, y_bf16;
   int32_t act;              // 0 none, 1 relu, 2 sigmoid, 3 tanh
+  int32_t w_f32;            // 1: f32 weights, f32 MFMA (v_mfma_f32_16x16x4_f32), reference precision
 };
 void launch_gemm(const GemmArgs& a, hipStream_t st);
 void launch_gemv(const GemmArgs& a, hipStream_t st);  // N == 1 heads
@@ -137,7 +138,7 @@ struct EnsembleArgs {
 };
 struct HeadArgs {
   const void* X;
-  const uint16_t* W1;
+  const void* W1;           // bf16, or f32 when w1_f32 (reference-precision head)
   const float* b1;          // [N1] nullable
   const float* w2;          // [N1] f32
   float b2;
@@ -158,6 +159,7 @@ struct HeadArgs {
   // (ml = Y[row], the plan's ml_col 0); the standalone ensemble launch is then skipped
   int32_t fuse_ens;
   EnsembleArgs ens;
+  int32_t w1_f32;           // 1: f32 W1 / activations, v_mfma_f32_16x16x4_f32 (no bf16 rounding anywhere)
 };
 void launch_mlp_head(const HeadArgs& a, hipStream_t st);
 

@@ -119,6 +119,7 @@ class ModelConfig:
     kind: str = "auto"           # auto | onnx | heuristic | none
     input_name: str = "input"    # onnx_model.go:37
     output_name: str = "output"  # onnx_model.go:38
+    precision: str = "fp32"      # dense-layer numerics on the GPU: fp32 (reference) | bf16
 
 
 @dataclass

@@ -295,7 +295,7 @@ class GpuBackend:
         from ..models.plan import compile_onnx, to_device
         from .scorer import GpuScorer
         torch = self.torch
-        plan = to_device(compile_onnx(fm), self.device) if mkind == "onnx" else None
+        plan = to_device(compile_onnx(fm), self.device, self.cfg.fraud_model.precision) if mkind == "onnx" else None
         model = {"onnx": "plan", "heuristic": "heuristic", "none": "none"}[mkind]
         with self._lock:
             for lk in self._slot_locks:

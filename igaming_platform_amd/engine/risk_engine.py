@@ -131,7 +131,8 @@ class RiskEngine:
         elif backend == "gpu":
             from ..models.plan import compile_onnx, to_device
             for r, d in enumerate(self.devices):
-                plan = to_device(compile_onnx(fm), f"cuda:{d}") if mkind == "onnx" else None
+                plan = (to_device(compile_onnx(fm), f"cuda:{d}", cfg.fraud_model.precision)
+                        if mkind == "onnx" else None)
                 model = {"onnx": "plan", "heuristic": "heuristic", "none": "none"}[mkind]
                 self.backends.append(GpuBackend(cfg, self.capacity, f"cuda:{d}", plan=plan, model=model,
                                                 blacklist=self.blacklist, ipintel=self.ipintel, capture=capture))
@@ -155,7 +156,7 @@ class RiskEngine:
             if backend == "gpu":
                 from ..models.plan import compile_onnx, to_device
                 dev = f"cuda:{self.devices[0]}"
-                g = LtvGpu(dev, self.capacity, to_device(compile_onnx(lm), dev) if lm is not None else None,
+                g = LtvGpu(dev, self.capacity, to_device(compile_onnx(lm), dev, cfg.ltv_model.precision) if lm is not None else None,
                            buckets=cfg.gpu.buckets, in_width=ltv_width, use_graphs=capture)
                 g.capture()
                 lg = [g]
@@ -168,7 +169,7 @@ class RiskEngine:
             from ..models.plan import compile_onnx, to_device
             lg = []
             for d in self.devices:
-                lp = to_device(compile_onnx(lm), f"cuda:{d}") if lm is not None else None
+                lp = to_device(compile_onnx(lm), f"cuda:{d}", cfg.ltv_model.precision) if lm is not None else None
                 g = LtvGpu(f"cuda:{d}", self.capacity, lp, buckets=cfg.gpu.buckets, in_width=ltv_width,
                            use_graphs=capture)
                 g.capture()
@@ -596,7 +597,7 @@ def make_local_backend(cfg: Config, kind: str, capacity: int, fm, mkind: str, bl
         import torch
         from ..models.plan import compile_onnx, to_device
         dev = f"cuda:{torch.cuda.current_device()}"
-        plan = to_device(compile_onnx(fm), dev) if mkind == "onnx" else None
+        plan = to_device(compile_onnx(fm), dev, cfg.fraud_model.precision) if mkind == "onnx" else None
         model = {"onnx": "plan", "heuristic": "heuristic", "none": "none"}[mkind]
         return GpuBackend(cfg, capacity, dev, plan=plan, model=model, blacklist=blacklist, ipintel=ipintel,
                           capture=capture, owner_filter=owner_filter, rank=rank)

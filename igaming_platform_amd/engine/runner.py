@@ -40,7 +40,9 @@ class DeviceModel:
         for i, s in enumerate(steps):
             last = i == len(steps) - 1
             feeds_mma = (not last) and steps[i + 1].kind in ("dense", "head")
-            dt = torch.bfloat16 if (s.kind in ("dense", "gru") and feeds_mma) else torch.float32
+            # bf16 plans hand bf16 activations to the next MFMA layer; fp32 plans stay f32
+            dt = (torch.bfloat16 if (s.kind in ("dense", "gru") and feeds_mma and plan.precision == "bf16")
+                  else torch.float32)
             self.step_out.append(torch.zeros((B, s.out_width), dtype=dt, device=self.device))
             if s.kind == "tree":
                 need = 0

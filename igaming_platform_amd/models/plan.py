@@ -127,6 +127,7 @@ class Plan:
     input_name: str
     output_name: str
     seq_input: bool = False
+    precision: str = "fp32"   # dense / head weights on device: fp32 (reference, f32 MFMA) | bf16
 
     def describe(self) -> str:
         parts = []
@@ -337,18 +338,37 @@ def _bf16_padded(w: np.ndarray, n_mult: int = 128, k_mult: int = 64):
     return torch.from_numpy(buf).to(torch.bfloat16)
 
 
-def to_device(plan: Plan, device) -> Plan:
+def _f32_padded(w: np.ndarray, n_mult: int = 128, k_mult: int = 64):
     import torch
+    n, k = w.shape
+    buf = np.zeros((-(-n // n_mult) * n_mult, -(-k // k_mult) * k_mult), np.float32)
+    buf[:n, :k] = w
+    return torch.from_numpy(buf)
+
+
+PRECISIONS = ("fp32", "bf16")
+
+
+def to_device(plan: Plan, device, precision: str = "fp32") -> Plan:
+    """Upload the plan's tensors. ``precision`` selects the dense / head weight format:
+    ``fp32`` (default) keeps the ONNX model's f32 numerics end to end (f32 MFMA,
+    onnx_model.go:221-238 contract); ``bf16`` runs the dense layers on the bf16 MFMA path
+    (f32 accumulate). Trees are always f32; GRU weights are always bf16 (K4)."""
+    import torch
+    if precision not in PRECISIONS:
+        raise ValueError(f"precision must be one of {PRECISIONS}, got {precision!r}")
+    plan.precision = precision
+    pad = _f32_padded if precision == "fp32" else _bf16_padded
     for s in plan.steps:
         if s.kind == "tree":
             s.nodes = torch.from_numpy(s.nodes_np).to(device)
             s.leaves = torch.from_numpy(s.leaves_np).to(device)
             s.base = None if s.base_np is None else torch.from_numpy(s.base_np).to(device)
         elif s.kind == "dense":
-            s.w = _bf16_padded(s.w_np).to(device)
+            s.w = pad(s.w_np).to(device)
             s.b = None if s.b_np is None else torch.from_numpy(np.ascontiguousarray(s.b_np)).to(device)
         elif s.kind == "head":
-            s.w1 = _bf16_padded(s.w1_np).to(device)
+            s.w1 = pad(s.w1_np).to(device)
             s.b1 = None if s.b1_np is None else torch.from_numpy(np.ascontiguousarray(s.b1_np)).to(device)
             s.w2 = torch.from_numpy(s.w2_np).to(device)
     return plan

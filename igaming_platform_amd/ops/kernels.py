@@ -183,8 +183,8 @@ def dense(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], Y: tor
     dev = X.device
     if X.dtype not in (torch.float32, torch.bfloat16) or Y.dtype not in (torch.float32, torch.bfloat16):
         raise ValueError("dense: X and Y must be float32 or bfloat16")
-    if W.dtype != torch.bfloat16 or W.dim() != 2:
-        raise ValueError("dense: W must be 2-D bfloat16")
+    if W.dtype not in (torch.bfloat16, torch.float32) or W.dim() != 2:
+        raise ValueError("dense: W must be 2-D bfloat16 or float32")
     if N == 1:
         if W.shape[1] < K:
             raise ValueError("dense: W narrower than K")
@@ -197,7 +197,8 @@ def dense(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], Y: tor
     d = dict(X=_need(X, "X", device=dev), W=_need(W, "W", device=dev), bias=_opt(bias, "bias", dtype=torch.float32),
              Y=_need(Y, "Y", device=dev), m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32), M=int(M), N=int(N),
              K=int(K), ldx=int(X.shape[1]), ldy=int(Y.shape[1]), ldw=int(W.shape[1]),
-             x_bf16=int(X.dtype == torch.bfloat16), y_bf16=int(Y.dtype == torch.bfloat16), act=ACT[act])
+             x_bf16=int(X.dtype == torch.bfloat16), y_bf16=int(Y.dtype == torch.bfloat16), act=ACT[act],
+             w_f32=int(W.dtype == torch.float32))
     if N == 1:
         _mod().gemv(d, _stream())
     else:
@@ -225,7 +226,11 @@ def mlp_head(hs, X: Optional[torch.Tensor], Y: torch.Tensor, M: int, m_ptr: Opti
         raise ValueError("mlp_head: output shape/dtype")
     if hs.w1.shape[0] < -(-hs.n1 // 64) * 64 or hs.w1.shape[1] % 32 or hs.w1.shape[1] < hs.k:
         raise ValueError("mlp_head: W1 padding")
-    d = dict(X=_need(X, "X", device=dev), W1=_need(hs.w1, "W1", torch.bfloat16, device=dev),
+    w1_f32 = hs.w1.dtype == torch.float32
+    if w1_f32 and hs.w1.shape[1] * 4 * -(-hs.n1 // 64) * 64 > (1 << 30):
+        raise ValueError("mlp_head: f32 W1 too large")
+    d = dict(X=_need(X, "X", device=dev), W1=_need(hs.w1, "W1", (torch.bfloat16, torch.float32), device=dev),
+             w1_f32=int(w1_f32),
              b1=_opt(hs.b1, "b1", dtype=torch.float32, min_numel=hs.n1),
              w2=_need(hs.w2, "w2", torch.float32, hs.n1, dev), b2=float(hs.b2),
              Y=_need(Y, "Y", torch.float32, M, dev), m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32),

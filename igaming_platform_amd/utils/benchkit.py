@@ -29,7 +29,7 @@ class Setup:
 
 def build(config: str, batch: int, accounts: int, dev, rank: int = 0, depth: int = 2,
           use_graphs: bool = True, history_batches: int = 24, n_pool: int = 8,
-          hot_frac: float = 0.02) -> Setup:
+          hot_frac: float = 0.02, precision: str = "fp32") -> Setup:
     import torch
 
     from ..config import Config
@@ -58,7 +58,7 @@ def build(config: str, batch: int, accounts: int, dev, rank: int = 0, depth: int
     plan, model = None, "heuristic"
     if c["model"] != "heuristic":
         m = native().OnnxModel.from_bytes(builders.build(c["model"]).SerializeToString())
-        plan = to_device(compile_onnx(m), dev)
+        plan = to_device(compile_onnx(m), dev, precision)
         model = "plan"
     sc = GpuScorer(cfg, store, plan=plan, model=model, device=dev, pipeline_depth=depth, use_graphs=use_graphs)
     rng = np.random.default_rng(7 + rank)
@@ -95,7 +95,7 @@ class ModelSetup:
 
 
 def build_model(config: str, batch: int, accounts: int, dev, rank: int = 0, depth: int = 2,
-                use_graphs: bool = True, n_pool: int = 8) -> ModelSetup:
+                use_graphs: bool = True, n_pool: int = 8, precision: str = "bf16") -> ModelSetup:
     import torch
 
     from ..config import FeatureConfig
@@ -112,7 +112,7 @@ def build_model(config: str, batch: int, accounts: int, dev, rank: int = 0, dept
     if c["kind"] == "ltv":
         from ..engine.ltv import LtvGpu
         m = N.OnnxModel.from_bytes(builders.build("ltv_mlp", n_features=256, width=512, layers=4).SerializeToString())
-        runner = LtvGpu(dev, accounts, to_device(compile_onnx(m), dev), buckets=[B], use_graphs=use_graphs,
+        runner = LtvGpu(dev, accounts, to_device(compile_onnx(m), dev, precision), buckets=[B], use_graphs=use_graphs,
                         depth=depth)
         # synthetic player profiles (same column semantics as golden.ltv.PLAYER_COLUMNS)
         for s in range(0, accounts, 1 << 18):

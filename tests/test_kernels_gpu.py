@@ -231,26 +231,36 @@ def test_stacked_tree_embedding_matches_cpu():
 
 
 # ----------------------------------------------------------------------------- dense / MFMA
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("M,N,Kd,act,xbf", [
     (1, 32, 32, "relu", False), (37, 256, 32, "relu", False), (4096, 512, 256, "relu", True),
     (8192, 256, 32, "none", False), (1000, 768, 16, "none", True), (333, 1, 256, "sigmoid", False),
     (5000, 512, 512, "tanh", True),
 ])
-def test_dense_mfma_matches_torch_fp32(M, N, Kd, act, xbf):
+def test_dense_mfma_matches_torch_fp32(M, N, Kd, act, xbf, precision):
+    """fp32 weights (f32 MFMA) vs a true fp32 torch reference; bf16 weights vs the same
+    reference with the error bf16 operands imply (and tightly vs bf16-rounded operands)."""
     import torch
-    from igaming_platform_amd.models.plan import _bf16_padded
+    from igaming_platform_amd.models.plan import _bf16_padded, _f32_padded
     from igaming_platform_amd.ops import kernels as K
     g = torch.Generator().manual_seed(M + N + Kd)
     X = torch.randn(M, Kd, generator=g)
+    if xbf:
+        X = X.to(torch.bfloat16).float()  # the producer hands bf16 activations: exact in both
     W = torch.randn(N, Kd, generator=g) / Kd ** 0.5     # [N, K] = output rows
     b = torch.randn(N, generator=g) * 0.1
     Xd = (X.to(torch.bfloat16) if xbf else X).cuda()
-    Wd = _bf16_padded(W.numpy()).cuda()
+    Wd = (_f32_padded if precision == "fp32" else _bf16_padded)(W.numpy()).cuda()
     Y = torch.zeros(M, N, dtype=torch.float32, device="cuda")
     K.dense(Xd, Wd, b.cuda(), Y, M, N, Kd, act=act)
-    ref = X.to(torch.bfloat16).float() @ W.to(torch.bfloat16).float().T + b
-    ref = {"relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh, "none": lambda t: t}[act](ref)
-    torch.testing.assert_close(Y.cpu(), ref, rtol=2e-3, atol=2e-3)
+    f = {"relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh, "none": lambda t: t}[act]
+    ref32 = f(X.double() @ W.double().T + b.double()).float()
+    if precision == "fp32":
+        torch.testing.assert_close(Y.cpu(), ref32, rtol=1e-5, atol=2e-5)
+    else:
+        refb = f(X.to(torch.bfloat16).float() @ W.to(torch.bfloat16).float().T + b)
+        torch.testing.assert_close(Y.cpu(), refb, rtol=2e-3, atol=2e-3)
+        torch.testing.assert_close(Y.cpu(), ref32, rtol=3e-2, atol=3e-2)
 
 
 def test_dense_respects_live_rows():
@@ -267,37 +277,49 @@ def test_dense_respects_live_rows():
 
 
 # ----------------------------------------------------------------------------- full model plans
-@pytest.mark.parametrize("kind,width", [("logistic", 32), ("gbdt", 128), ("stacked", 128)])
-def test_scorer_with_model_matches_executor_and_golden(kind, width):
-    import torch
+@pytest.mark.parametrize("kind,width,precision", [("logistic", 32, "fp32"), ("gbdt", 128, "fp32"),
+                                                ("stacked", 128, "fp32"), ("stacked", 128, "bf16")])
+def test_scorer_with_model_matches_executor_and_golden(kind, width, precision):
+    """fp32 (the default, the ONNX model's f32 contract): on 10240 requests the device's score,
+    action and reason mask are EXACTLY the golden rules + ensemble fed by the C++ fp32
+    executor run on the golden feature vectors (no device value reused), and ml agrees to
+    1e-5. bf16 (opt-in): ml within 2e-2 and the ensemble exact given the device's own ml."""
     from igaming_platform_amd.engine.scorer import GpuScorer
+    from igaming_platform_amd.golden import scoring as GS
     from igaming_platform_amd.models.plan import compile_onnx, to_device
     from igaming_platform_amd.native import native
     from igaming_platform_amd.onnx import builders
     cfg = Config()
     cfg.features.width = width
     cfg.gpu.buckets = [256, 1024]
-    pop, gold, store = _store_and_world(cfg, n_acc=300, seed=2)
+    pop, gold, store = _store_and_world(cfg, n_acc=3000, seed=2)
     N = native()
     m = N.OnnxModel.from_bytes(builders.build(kind).SerializeToString())
-    plan = to_device(compile_onnx(m), "cuda")
+    plan = to_device(compile_onnx(m), "cuda", precision)
     sc = GpuScorer(cfg, store, plan=plan, model="plan", update_features=False)
     sc.capture()
     rng = np.random.default_rng(4)
     from igaming_platform_amd.utils.synth import make_requests
-    req = make_requests(pop, 1000, rng, NOW, hot_frac=0.1)
-    out = sc.score(req, now=NOW)
-    X = sc.X[:1000].cpu().numpy()
-    ref = N.Executor(m).run({"input": X})["output"]
-    col = plan.ml_col
-    ml_ref = np.clip(ref[:, col], 0, 1)
-    tol = 2e-2 if kind != "gbdt" else 1e-5   # bf16 MFMA head vs fp32 executor
-    np.testing.assert_allclose(out["ml"], ml_ref, atol=tol)
-    # rules/ensemble exact given the device's own ml value
-    for i, row in enumerate(req):
-        g = golden_score(cfg, gold, pop, row, NOW, model="plan", ml_override=float(out["ml"][i]))
-        assert out["score"][i] == g["score"] and out["action"][i] == g["action"], i
-        assert out["reasons"][i] == sum(1 << REASON_BIT[r] for r in g["reasons"]), i
+    n_rows = 10240 if precision == "fp32" else 1024
+    req = make_requests(pop, n_rows, rng, NOW, hot_frac=0.1)
+    outs = [sc.score(req[i:i + 1024], now=NOW) for i in range(0, n_rows, 1024)]
+    out = {k: np.concatenate([o[k] for o in outs]) for k in ("ml", "score", "action", "reasons")}
+    gs = [golden_score(cfg, gold, pop, row, NOW, model="none") for row in req]
+    Xg = np.stack([g["x"] for g in gs]).astype(np.float32)
+    ref = N.Executor(m).run({"input": Xg})["output"]
+    ml_ref = np.array([GS.clamp01_f32(v) for v in ref[:, plan.ml_col]], np.float32)
+    if precision == "fp32":
+        np.testing.assert_allclose(out["ml"], ml_ref, atol=1e-5, rtol=0)
+    else:
+        np.testing.assert_allclose(out["ml"], ml_ref, atol=2e-2)
+    bad = []
+    for i, g in enumerate(gs):
+        ml = float(ml_ref[i]) if precision == "fp32" else float(out["ml"][i])
+        score, action, reasons, _ = GS.ensemble(cfg.scoring, g["rule"], g["reasons"], ml)
+        mask = sum(1 << REASON_BIT[r] for r in reasons)
+        if (out["score"][i], out["action"][i], out["reasons"][i]) != (score, action, mask):
+            bad.append((i, out["score"][i], score, out["action"][i], action))
+    assert not bad, f"{len(bad)} of {n_rows} decisions differ: {bad[:5]}"
 
 
 # ----------------------------------------------------------------------------- LTV
@@ -331,24 +353,32 @@ def test_ltv_kernel_matches_golden():
         assert GL.NBA_CODES[int(o[i, 5])] == p.next_best_action, i
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("M,K,N1,act1,act2,xbf", [
     (8192, 32, 256, "relu", "sigmoid", False), (100, 512, 512, "relu", "none", True),
     (1, 64, 64, "tanh", "sigmoid", False), (4097, 256, 130, "relu", "sigmoid", True),
 ])
-def test_mlp_head_matches_torch_fp32(M, K, N1, act1, act2, xbf):
+def test_mlp_head_matches_torch_fp32(M, K, N1, act1, act2, xbf, precision):
     import torch
     from igaming_platform_amd.models.plan import HeadStep, to_device, Plan
     from igaming_platform_amd.ops import kernels as K_
     g = torch.Generator().manual_seed(M + K + N1)
     X = torch.randn(M, K, generator=g)
+    if xbf:
+        X = X.to(torch.bfloat16).float()
     W1 = torch.randn(N1, K, generator=g) / K ** 0.5
     b1 = torch.randn(N1, generator=g) * 0.1
     w2 = torch.randn(N1, generator=g) / N1 ** 0.5
     hs = HeadStep(n1=N1, k=K, act1=act1, act2=act2, w1_np=W1.numpy(), b1_np=b1.numpy(), w2_np=w2.numpy(), b2=0.3)
-    to_device(Plan("t", K, [hs], 1, 0, {}, "input", "output"), "cuda")
+    to_device(Plan("t", K, [hs], 1, 0, {}, "input", "output"), "cuda", precision)
     Y = torch.zeros(M, 1, device="cuda")
     K_.mlp_head(hs, (X.to(torch.bfloat16) if xbf else X).cuda(), Y, M)
     f = {"relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh, "none": lambda t: t}
-    h = f[act1](X.to(torch.bfloat16).float() @ W1.to(torch.bfloat16).float().T + b1)
-    ref = f[act2](h @ w2 + 0.3)
-    torch.testing.assert_close(Y[:, 0].cpu(), ref, rtol=3e-3, atol=3e-3)
+    h32 = f[act1](X.double() @ W1.double().T + b1.double())
+    ref32 = f[act2](h32 @ w2.double() + 0.3).float()
+    if precision == "fp32":
+        torch.testing.assert_close(Y[:, 0].cpu(), ref32, rtol=1e-5, atol=1e-5)
+    else:
+        h = f[act1](X.to(torch.bfloat16).float() @ W1.to(torch.bfloat16).float().T + b1)
+        ref = f[act2](h @ w2 + 0.3)
+        torch.testing.assert_close(Y[:, 0].cpu(), ref, rtol=3e-3, atol=3e-3)
