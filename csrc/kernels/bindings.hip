@@ -80,6 +80,7 @@ void check(const char* what) {
 
 namespace igp {
 void register_driver(py::module_& m);
+void register_exchange(py::module_& m);
 }
 
 PYBIND11_MODULE(_hipk, m) {
@@ -93,6 +94,7 @@ PYBIND11_MODULE(_hipk, m) {
   m.attr("DEDUP_LIST") = DEDUP_LIST;
   m.attr("DEDUP_REGIONS") = DEDUP_RING + 1;
   igp::register_driver(m);
+  igp::register_exchange(m);
 
   m.def("feature_assemble", [](py::dict d, uintptr_t s) {
     AssembleArgs a{};

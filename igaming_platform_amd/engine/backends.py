@@ -269,19 +269,24 @@ class GpuBackend:
 
     def __init__(self, cfg: Config, capacity: int, device, plan=None, model: str = "plan",
                  blacklist: Optional[Blacklist] = None, ipintel: Optional[IPIntel] = None,
-                 capture: bool = True, owner_filter: bool = False, rank: int = 0):
+                 capture: bool = True, owner_filter: bool = False, rank: int = 0, exchange: Optional[dict] = None):
+        """``exchange``: dict(comms, world, senders, cbuckets) -> the shard is one rank of an
+        owner-routed data-parallel group (engine/dp.py): batches arrive through the RCCL
+        exchange and only this GPU's own rows are scored."""
         import torch
-        from .scorer import GpuScorer
         from ..features.device_store import DeviceFeatureStore
         self.torch = torch
         self.cfg = cfg
         from ..ops.kernels import as_device
         self.device = as_device(device)
+        self.exchange = exchange
+        self.rank = rank
+        self.owner_filter = owner_filter
+        dmax = max(cfg.gpu.buckets) * (exchange["senders"] if exchange else 1)
         self.store = DeviceFeatureStore(capacity, cfg.features, self.device, events=True,
-                                        blacklist=blacklist, ipintel=ipintel, max_events=max(cfg.gpu.buckets))
+                                        blacklist=blacklist, ipintel=ipintel, max_events=dmax)
         self.blacklist, self.ipintel = self.store.blacklist, self.store.ipintel
-        self.scorer = GpuScorer(cfg, self.store, plan=plan, model=model, device=self.device,
-                                owner_filter=owner_filter, rank=rank)
+        self.scorer = self._make_scorer(plan, model, 2 if exchange is None else 3)
         if capture and self.scorer.use_graphs:
             self.scorer.capture()
         self._lock = threading.RLock()
@@ -293,7 +298,6 @@ class GpuBackend:
         feature store (new graphs, same store, batch sequence and metrics carried over so the
         dedup region ring stays consistent), swap it in. Scoring resumes with the new model."""
         from ..models.plan import compile_onnx, to_device
-        from .scorer import GpuScorer
         torch = self.torch
         plan = to_device(compile_onnx(fm), self.device, self.cfg.fraud_model.precision) if mkind == "onnx" else None
         model = {"onnx": "plan", "heuristic": "heuristic", "none": "none"}[mkind]
@@ -303,9 +307,7 @@ class GpuBackend:
             try:
                 old = self.scorer
                 torch.cuda.synchronize(self.device)
-                sc = GpuScorer(self.cfg, self.store, plan=plan, model=model, device=self.device,
-                               pipeline_depth=old.depth, owner_filter=old.owner_filter, rank=old.rank,
-                               use_graphs=old.use_graphs)
+                sc = self._make_scorer(plan, model, old.depth, use_graphs=old.use_graphs)
                 sc._seq = old._seq  # dedup regions rotate by batch seq (one is still dirty)
                 sc.metrics = old.metrics
                 sc.refresh_config(getattr(old, "scoring", None))
@@ -316,6 +318,38 @@ class GpuBackend:
             finally:
                 for lk in self._slot_locks:
                     lk.release()
+
+    def _make_scorer(self, plan, model: str, depth: int, use_graphs=None):
+        if self.exchange is not None:
+            from .dp import DpGpuScorer
+            x = self.exchange
+            return DpGpuScorer(self.cfg, self.store, x["comms"], x["world"], self.rank, x["senders"], x["cbuckets"],
+                               plan=plan, model=model, device=self.device, pipeline_depth=depth)
+        from .scorer import GpuScorer
+        return GpuScorer(self.cfg, self.store, plan=plan, model=model, device=self.device, pipeline_depth=depth,
+                         owner_filter=self.owner_filter, rank=self.rank, use_graphs=use_graphs)
+
+    def exchange_score(self, req: Optional[np.ndarray], owners: Optional[np.ndarray], C: int, now: int,
+                       want_features: bool) -> Result:
+        """One owner-routed exchange step (collective over the group): this rank's ingress
+        rows (None on a non-ingress rank) go to their owners; this GPU scores the rows it
+        owns; returns the ingress rows' (res, feats) in request order."""
+        sc = self.scorer
+        with self._lock:
+            slot = sc.next_slot()
+        self._slot_locks[slot].acquire()
+        try:
+            with self._lock:
+                if req is None:
+                    p = sc.submit_chunks(slot, C, now, None, want_features)
+                else:
+                    p = sc.submit_rows(slot, req, owners, now, want_features, C=C)
+            res, feats = sc.wait_x(p)
+        finally:
+            self._slot_locks[slot].release()
+        if req is None:
+            return res, feats
+        return res, (feats.copy() if feats is not None else None)
 
     def refresh_config(self, scoring=None) -> None:
         with self._lock:

@@ -1,0 +1,266 @@
+"""Data-parallel GPU scorer: the three-stream scoring pipeline of :mod:`.scorer` behind the
+owner-routed RCCL exchange of :mod:`..parallel.exchange` (one process per GPU).
+
+Per micro-batch on every rank (``csrc/kernels/exchange.hip`` XchgDriver; no host sync, no
+row-count read-back):
+
+  xs stream    H2D  the ingress rank's chunks [world][1 + C] ReqRec + the batch header, then
+               the RCCL all-to-all of the chunks (each owner gets its rows from every sender)
+  copy stream  exchange_compact -> contiguous owned rows + BatchHdr.n; K6a dedup insert
+  state stream K1 feature_assemble + score-then-update (unchanged graphs)
+  model stream trees / MLP head / K5 ensemble -> exchange_scatter into result chunks
+  ys stream    RCCL all-to-all of the results back to the senders; D2H to pinned memory
+
+Each GPU scores only its own accounts' rows (``senders * C`` rows at most per batch: one
+sender for the serving front end on rank 0, every rank in ``bench.py --gpus N``). With a
+world of 1 the same code runs through RCCL's single-rank path (tests on a 1-GPU box).
+"""
+from __future__ import annotations
+
+import copy
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..layouts import REQREC
+from ..native import hipk
+from ..ops import kernels as K
+from ..parallel.exchange import FEAT_BYTES, RES_BYTES, build_chunks, gather_results, result_width
+from .scorer import HDR_BYTES, GpuScorer
+
+REQ = REQREC.itemsize
+
+
+@dataclass
+class XPending:
+    slot: int
+    C: int
+    n: int
+    gather: Optional[np.ndarray]
+    want_features: bool
+    t_submit: float
+
+
+class DpGpuScorer(GpuScorer):
+    """GpuScorer whose batches arrive through the exchange. ``cbuckets``: chunk capacities
+    (rows per owner per sender); the scorer graphs run ``senders * C`` rows."""
+
+    def __init__(self, cfg, store, comms: Sequence, world: int, rank: int, senders: int,
+                 cbuckets: Sequence[int], plan=None, model: str = "plan", device=None, pipeline_depth: int = 3,
+                 update_features: bool = True):
+        self.world, self.senders = int(world), int(senders)
+        if not 1 <= self.senders <= self.world:
+            raise ValueError("senders must be in [1, world]")
+        if self.world > hipk().XCHG_MAX_WORLD:
+            raise ValueError("world too large for the exchange kernels")
+        self.cbuckets = sorted(set(int(c) for c in cbuckets))
+        cfg = copy.deepcopy(cfg)
+        cfg.gpu.buckets = [self.senders * c for c in self.cbuckets]
+        # CUs reserved for the RCCL streams (collective kernels poll: sharing CUs with K1 slowed
+        # both ~2x in the rocprofv3 timeline)
+        self._comm_cus = (int(os.environ.get("IGP_XCHG_COMM_CUS", "8"))
+                          if os.environ.get("IGP_XCHG_STREAMS", "3") == "5" else 0)
+        super().__init__(cfg, store, plan=plan, model=model, device=device, pipeline_depth=pipeline_depth,
+                         update_features=update_features, use_graphs=True, owner_filter=False, rank=rank)
+        self.comms = list(comms)
+        if len(self.comms) != 2:
+            raise ValueError("the exchange needs two RCCL communicators (rows, results)")
+        cmax, dev = self.cbuckets[-1], self.device
+        self.xbytes_max = self.world * (cmax + 1) * REQ
+        self.rbytes_max = self.world * cmax * (RES_BYTES + FEAT_BYTES)
+        for sb in self.slots:
+            sb.xsend = torch.zeros(self.xbytes_max, dtype=torch.uint8, device=dev)
+            sb.xrecv = torch.zeros(self.xbytes_max, dtype=torch.uint8, device=dev)
+            sb.route = torch.zeros(self.bmax + 1, dtype=torch.int32, device=dev)
+            sb.rsend = torch.zeros(self.rbytes_max, dtype=torch.uint8, device=dev)
+            sb.rrecv = torch.zeros(self.rbytes_max, dtype=torch.uint8, device=dev)
+        self.host_x = [torch.zeros(self.xbytes_max, dtype=torch.uint8).pin_memory() for _ in range(self.depth)]
+        self.host_x_np = [t.numpy() for t in self.host_x]
+        self.host_rr = [torch.zeros(self.rbytes_max, dtype=torch.uint8).pin_memory() for _ in range(self.depth)]
+        cs = getattr(self, "comm_streams", ())
+        if os.environ.get("IGP_XCHG_STREAMS", "3") == "3":
+            # the row all-to-all on the copy stream, the result all-to-all + D2H on the model
+            # stream: two cross-stream hops per batch, as in the single-GPU pipeline
+            self.xstream, self.ystream = self.cstream, self.mstream
+        elif len(cs) == 2:
+            self.xstream, self.ystream = cs
+        else:  # no CU split (IGP_CU_SPLIT=none / heuristic model)
+            self.xstream, self.ystream = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+        self.xgraphs = {}
+        self.xdriver = None
+
+    # ------------------------------------------------------------------ graph bodies
+    def cap(self, C: int) -> int:
+        return self.senders * C
+
+    def _send_body(self, slot: int, C: int) -> None:
+        sb, nb = self.slots[slot], self.world * (C + 1) * REQ
+        sb.xsend[:nb].copy_(self.host_x[slot][:nb], non_blocking=True)
+        sb.dev_slab[:HDR_BYTES].copy_(self.host_slab[slot][:HDR_BYTES], non_blocking=True)
+
+    def _post_body(self, slot: int, C: int) -> None:
+        sb, b = self.slots[slot], self.cap(C)
+        hipk().exchange_compact(sb.xrecv.data_ptr(), sb.req.data_ptr(), sb.dev_slab.data_ptr(), sb.route.data_ptr(),
+                                self.world, C, b, torch.cuda.current_stream().cuda_stream)
+        if self.update_features:
+            K.dedup_insert(self.store, self.cfg_dev, sb.req, b, sb.hdr)
+
+    def _xmodel_body(self, slot: int, C: int, with_features: bool) -> None:
+        sb, b = self.slots[slot], self.cap(C)
+        if sb.model is not None and sb.model.fuses_ensemble():
+            ens = K.ensemble_args(sb.hdr, self.cfg_dev, sb.feat, sb.X, sb.model.step_out[-1], sb.res, b, self.metrics)
+            sb.model.run(sb.X, b, m_ptr=sb.n_ptr, ens=ens)
+        else:
+            ml = sb.model.run(sb.X, b, m_ptr=sb.n_ptr) if sb.model is not None else None
+            K.ensemble(sb.hdr, self.cfg_dev, sb.feat, sb.X, ml, sb.res, b, self.metrics)
+        hipk().exchange_scatter(sb.dev_slab.data_ptr(), sb.route.data_ptr(), sb.res.data_ptr(),
+                                sb.feat.data_ptr() if with_features else 0, sb.rsend.data_ptr(), C, b,
+                                torch.cuda.current_stream().cuda_stream)
+
+    # ---- collectives captured into the graphs (RCCL stream capture, IGP_XCHG_CAPTURE=1)
+    def _a2a_rows(self, slot: int, C: int) -> None:
+        sb = self.slots[slot]
+        self.comms[0].all_to_all(sb.xsend.data_ptr(), sb.xrecv.data_ptr(), (C + 1) * REQ,
+                                 torch.cuda.current_stream().cuda_stream)
+
+    def _a2a_results(self, slot: int, C: int, with_features: bool) -> None:
+        sb, W = self.slots[slot], result_width(with_features)
+        self.comms[1].all_to_all(sb.rsend.data_ptr(), sb.rrecv.data_ptr(), C * W,
+                                 torch.cuda.current_stream().cuda_stream)
+        nb = self.world * C * W
+        self.host_rr[slot][:nb].copy_(sb.rrecv[:nb], non_blocking=True)
+
+    def _sendpost_body(self, slot: int, C: int) -> None:
+        self._send_body(slot, C)
+        self._a2a_rows(slot, C)
+        self._post_body(slot, C)
+
+    def _model_results_body(self, slot: int, C: int, with_features: bool) -> None:
+        self._xmodel_body(slot, C, with_features)
+        self._a2a_results(slot, C, with_features)
+
+    def capture(self) -> None:
+        """Capture send / post / state / model / model+features graphs per (C, slot), each on
+        the stream it replays on, and hand them to the native exchange driver. With
+        IGP_XCHG_CAPTURE=1 (default) the two all-to-alls and the D2H copy are captured into the
+        send and model graphs too (three graph launches per batch)."""
+        dev = self.device
+        self.captured = os.environ.get("IGP_XCHG_CAPTURE", "1") == "1" and self.xstream is self.cstream \
+            and self.ystream is self.mstream
+        with torch.cuda.device(dev):
+            for C in self.cbuckets:
+                for slot in range(self.depth):
+                    self._write_hdr(slot, 0, 0)
+                    gs = []
+                    if self.captured:
+                        bodies = ((lambda: self._sendpost_body(slot, C), self.cstream),
+                                  None,
+                                  (lambda: self._state_body(slot, self.cap(C)), self.stream),
+                                  (lambda: self._model_results_body(slot, C, False), self.mstream),
+                                  (lambda: self._model_results_body(slot, C, True), self.mstream))
+                    else:
+                        bodies = ((lambda: self._send_body(slot, C), self.xstream),
+                                  (lambda: self._post_body(slot, C), self.cstream),
+                                  (lambda: self._state_body(slot, self.cap(C)), self.stream),
+                                  (lambda: self._xmodel_body(slot, C, False), self.mstream),
+                                  (lambda: self._xmodel_body(slot, C, True), self.mstream))
+                    for item in bodies:
+                        if item is None:
+                            gs.append(None)
+                            continue
+                        body, s = item
+                        s.wait_stream(torch.cuda.current_stream())
+                        with torch.cuda.stream(s):
+                            body()
+                        torch.cuda.current_stream().wait_stream(s)
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g, stream=s):
+                            body()
+                        gs.append(g)
+                    self.xgraphs[(C, slot)] = tuple(gs)
+            torch.cuda.synchronize(dev)
+        m = hipk()
+        d = m.XchgDriver(self.cstream.cuda_stream, self.stream.cuda_stream, self.mstream.cuda_stream,
+                         self.xstream.cuda_stream, self.ystream.cuda_stream, self.depth, self.world,
+                         self.comms[0], self.comms[1])
+        for slot, sb in enumerate(self.slots):
+            d.set_slot(slot, self.host_slab[slot].data_ptr(), self.host_x[slot].data_ptr(),
+                       self.host_rr[slot].data_ptr(), sb.xsend.data_ptr(), sb.xrecv.data_ptr(), sb.rsend.data_ptr(),
+                       sb.rrecv.data_ptr(), self.xbytes_max, self.rbytes_max)
+        for (C, slot), g in self.xgraphs.items():
+            d.set_graphs(C, slot, *[0 if x is None else x.raw_cuda_graph_exec() for x in g])
+        d.set_captured(self.captured)
+        self.xdriver = d
+        self.driver = None  # the three-graph driver of the single-GPU path is not used here
+
+    # ------------------------------------------------------------------ batches
+    def cbucket_for(self, c: int) -> int:
+        for b in self.cbuckets:
+            if c <= b:
+                return b
+        raise ValueError(f"{c} rows for one owner exceed the largest chunk capacity {self.cbuckets[-1]}")
+
+    def submit_chunks(self, slot: int, C: int, now: int, chunks: Optional[np.ndarray] = None,
+                      want_features: bool = False, n: int = 0, gather: Optional[np.ndarray] = None,
+                      prefilled: bool = False) -> XPending:
+        """Launch one exchange step with prebuilt ``chunks`` (REQREC [world * (C + 1)], from
+        :func:`build_chunks`; None: this rank ingests nothing this step, unless ``prefilled``:
+        the chunks were built in the slot's pinned buffer already)."""
+        import time
+        if self.xdriver is None:
+            raise RuntimeError("DpGpuScorer.capture() has not run")
+        self._seq += 1
+        t0 = time.perf_counter()
+        nb = self.world * (C + 1) * REQ
+        if prefilled:
+            src = 0
+        elif chunks is None:
+            hx = self.host_x_np[slot][:nb].view(REQREC)
+            hx["slot"][np.arange(self.world) * (C + 1)] = 0
+            src = 0
+        else:
+            if chunks.dtype != REQREC or len(chunks) != self.world * (C + 1):
+                raise ValueError("chunks must be REQREC [world * (C + 1)]")
+            src = chunks.ctypes.data
+        self.xdriver.submit(slot, C, self._seq, int(now), src, nb if src else 0, bool(want_features))
+        self._cur = slot
+        self.batches += 1
+        return XPending(slot, C, n, gather, want_features, t0)
+
+    def submit_rows(self, slot: int, req: np.ndarray, owners: np.ndarray, now: int,
+                    want_features: bool = False, C: Optional[int] = None) -> XPending:
+        """Ingress: route REQREC ``req`` by ``owners`` and launch."""
+        from ..parallel.exchange import max_owner_count
+        C = C or self.cbucket_for(max(max_owner_count(owners, self.world), 1))
+        buf = self.host_x_np[slot][:self.world * (C + 1) * REQ].view(REQREC)
+        _, gather, _ = build_chunks(np.asarray(req, REQREC), owners, self.world, C, out=buf)
+        return self.submit_chunks(slot, C, now, None, want_features, n=len(req), gather=gather, prefilled=True)
+
+    def wait_x(self, p: XPending, gather: bool = True):
+        """Block until the step's results are on the host. ``gather``: return (res, feats) of
+        the ingress rows in request order; else the raw result chunks."""
+        self.xdriver.wait(p.slot)
+        W = result_width(p.want_features)
+        raw = self.host_rr[p.slot][:self.world * p.C * W].numpy()
+        if not gather:
+            return raw
+        if p.gather is None or p.n == 0:
+            return np.zeros((0, 2), np.uint32), None
+        return gather_results(raw, p.gather, self.world, p.C, p.want_features)
+
+    def route_overflow(self, slot: int, C: int) -> int:
+        """Rows dropped by the compact kernel because they exceeded ``senders * C`` (always 0
+        when every sender respects the chunk capacity; a test hook)."""
+        return int(self.slots[slot].route[self.cap(C)].item())
+
+    def done(self, p) -> bool:
+        return self.xdriver.query(p.slot)
+
+
+def exchange_buckets(batch_buckets: Sequence[int]) -> List[int]:
+    """Chunk capacities for the rank-0 serving front end: any micro-batch of up to the largest
+    bucket fits (one sender), routed per owner into the smallest fitting chunk."""
+    return sorted(set(int(b) for b in batch_buckets))

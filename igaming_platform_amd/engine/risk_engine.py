@@ -122,11 +122,12 @@ class RiskEngine:
         if spmd is not None:
             from ..parallel.spmd import ShardProxy, ShardRunner, SpmdGroup
             local = make_local_backend(cfg, backend, self.capacity, fm, mkind, self.blacklist, self.ipintel,
-                                       owner_filter=True, rank=0, capture=capture)
+                                       rank=0, capture=capture, comm=spmd)
             self.local = local
             self._abuse_am = abuse_model if abuse_model is not None else cfg.abuse_model.path
             abuse_gpu = make_abuse_gpu(cfg, local, self._abuse_am)
-            self.group = SpmdGroup(spmd, ShardRunner(spmd, local, abuse_gpu))
+            self.group = SpmdGroup(spmd, ShardRunner(spmd, local, abuse_gpu), max_rows=max(cfg.gpu.buckets),
+                                   chunk_buckets=local.scorer.cbuckets if local.kind == "gpu" else None)
             self.backends = [ShardProxy(self.group, o, local) for o in range(world)]
         elif backend == "gpu":
             from ..models.plan import compile_onnx, to_device
@@ -217,9 +218,8 @@ class RiskEngine:
         slots, owners, _ = self.registry.resolve_batch(rb, insert=True)
         req = np.empty(n, REQREC)
         rb.pack_reqrec(slots, req.view(np.uint8), now, None)
-        if self.group is not None:
-            req["tx_type"] |= owners.astype(np.int32) << 8
-            res, feats = self.group.score(req, now, want_features)
+        if self.group is not None:  # owner-routed exchange: each rank scores its own rows
+            res, feats = self.group.score(req, owners, now, want_features)
             cols = rb.columns()
             self.links.add(cols["device_hash"], (owners.astype(np.int64) << 32) | np.where(slots >= 0, slots, -1))
             self._observe(rb, res, version)
@@ -591,16 +591,24 @@ class RiskEngine:
 
 # ============================================================================ shard construction
 def make_local_backend(cfg: Config, kind: str, capacity: int, fm, mkind: str, blacklist, ipintel,
-                       owner_filter: bool = False, rank: int = 0, capture: bool = True):
-    """The backend of THIS process's shard (used by SPMD rank 0 and by every worker rank)."""
+                       owner_filter: bool = False, rank: int = 0, capture: bool = True, comm=None):
+    """The backend of THIS process's shard (used by SPMD rank 0 and by every worker rank).
+    ``comm``: the SPMD group; a GPU shard then joins the owner-routed RCCL exchange (two
+    communicators of its own, created collectively here) and scores only its own rows."""
     if kind == "gpu":
         import torch
         from ..models.plan import compile_onnx, to_device
         dev = f"cuda:{torch.cuda.current_device()}"
         plan = to_device(compile_onnx(fm), dev, cfg.fraud_model.precision) if mkind == "onnx" else None
         model = {"onnx": "plan", "heuristic": "heuristic", "none": "none"}[mkind]
+        exchange = None
+        if comm is not None:
+            from ..parallel.exchange import rccl_comms
+            from .dp import exchange_buckets
+            exchange = dict(comms=rccl_comms(comm.rank, comm.world), world=comm.world, senders=1,
+                            cbuckets=exchange_buckets(cfg.gpu.buckets))
         return GpuBackend(cfg, capacity, dev, plan=plan, model=model, blacklist=blacklist, ipintel=ipintel,
-                          capture=capture, owner_filter=owner_filter, rank=rank)
+                          capture=capture, owner_filter=owner_filter, rank=rank, exchange=exchange)
     N = native()
     cls = CpuBackend if kind == "golden" else NativeCpuBackend
     kw = {} if kind == "golden" else {"capacity": capacity}
@@ -629,9 +637,9 @@ def make_abuse_gpu(cfg: Config, local, abuse_model):
 
 
 def serve_shard(cfg: Config, comm, backend: str = "gpu", capacity: Optional[int] = None, fraud_model=None,
-                abuse_model=None, capture: bool = True) -> int:
+                abuse_model=None, capture: bool = True):
     """Worker rank (>= 1) of an SPMD group: build the same local shard as rank 0 and serve
-    its ops until rank 0 stops the group."""
+    its ops until rank 0 stops the group. Returns (ops served, rows this shard scored)."""
     from ..parallel.spmd import run_worker
     fm = _load_onnx(fraud_model if fraud_model is not None else cfg.fraud_model.path)
     mkind = cfg.fraud_model.kind
@@ -639,6 +647,6 @@ def serve_shard(cfg: Config, comm, backend: str = "gpu", capacity: Optional[int]
         mkind = "onnx" if fm is not None else "heuristic"
     local = make_local_backend(cfg, backend, int(capacity or cfg.gpu.accounts_per_gpu), fm, mkind,
                                Blacklist(cfg.gpu.blacklist_capacity), IPIntel(cfg.gpu.blacklist_capacity),
-                               owner_filter=True, rank=comm.rank, capture=capture)
+                               rank=comm.rank, capture=capture, comm=comm)
     abuse_gpu = make_abuse_gpu(cfg, local, abuse_model if abuse_model is not None else cfg.abuse_model.path)
     return run_worker(comm, local, abuse_gpu)

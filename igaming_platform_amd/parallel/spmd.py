@@ -3,22 +3,23 @@
 Data parallelism by account owner (``owner = XXH64(account_id) % world``):
 every account's feature state lives on exactly one rank. Per ScoreBatch / micro-batch:
 
-  rank 0: registry resolves (owner, slot) for every request -> REQREC rows with the owner
-          in bits 8-15 of ``tx_type``  --broadcast-->  all ranks
-  rank r: scores the whole slab with ``owner_filter`` on (rows it does not own come out as
-          all-zero records, never touching its shard) and score-then-updates its own rows
-  all:    one all_reduce(SUM) of [ResultRec | FeatRec] — exactly one rank contributes each
-          row, so the sum IS the merged result, bit for bit.
+  rank 0: C++ parse + registry resolve (owner, slot) for every request; one 64-byte header
+          broadcast (op, n, now, want_features, chunk capacity C)
+  all:    the owner-routed exchange (:mod:`.exchange`): rank 0's rows travel to their owners
+          in per-owner chunks (RCCL all-to-all over xGMI between GPUs, device-resident; gloo
+          between CPU shards), every rank scores ONLY the rows it owns (score-then-update of
+          its own shard), and the packed 8-byte results (+ 128-byte FeatRec when features are
+          wanted) come back to rank 0 with a second all-to-all and one D2H copy.
 
 Cold-path ops (thresholds, blacklist/ip tables, warehouse rows, GetFeatures, event
-histories, GRU abuse scores) use the same broadcast-then-reduce protocol. Collectives go
-through :mod:`.comm` (RCCL over xGMI for GPUs, gloo on CPU).
+histories, GRU abuse scores) use a broadcast-then-reduce protocol over :mod:`.comm`.
 """
 from __future__ import annotations
 
 import dataclasses
 import io
 import json
+import threading
 
 import numpy as np
 
@@ -71,34 +72,37 @@ class ShardRunner:
         self.be = backend
         self.rank = comm.rank
         self.abuse_gpu = abuse_gpu
+        self.hx = None
+        if backend.kind != "gpu":
+            from .exchange import HostExchange
+            self.hx = HostExchange(comm.rank, comm.world)
+
+    @property
+    def rows_scored(self) -> int:
+        """Rows this rank scored through the exchange (its own accounts only): the device
+        metrics row counter on a GPU shard (K10, reads the device), the host count otherwise."""
+        if self.hx is not None:
+            return self.hx.rows_scored
+        return int(self.be.scorer.read_metrics()[106])
 
     def _mine(self, owners: np.ndarray) -> np.ndarray:
         return owners == self.rank
 
-    def score(self, req: np.ndarray, now: int, want_features: bool) -> np.ndarray:
-        n = len(req)
-        mine = self._mine(owners_of(req))
-        res = np.zeros((n, 2), np.uint32)
-        feats = np.zeros(n, FEATREC)
+    def score(self, req, owners, C: int, now: int, want_features: bool):
+        """One owner-routed exchange step (collective). ``req``/``owners``: the ingress rows
+        (rank 0) or None. Returns (res, feats) of the ingress rows in request order."""
         if self.be.kind == "gpu":
-            r, f = self.be.score(req, now, want_features)  # owner_filter: foreign rows are inert zeros
-            res[:] = r
-            if want_features:
-                feats[mine] = f[mine]
-        elif np.any(mine):
-            r, f = self.be.score(req[mine], now, want_features)
-            res[mine] = r
-            if want_features:
-                feats[mine] = f
-        words = [res.astype(np.int64).reshape(-1)]
-        if want_features:
-            words.append(feats.view(np.int64).reshape(-1))
-        return self.comm.sum_i64(np.concatenate(words))
+            return self.be.exchange_score(req, owners, C, now, want_features)
+
+        def score_fn(rows, wf):
+            return self.be.score(rows, now, wf)
+
+        return self.hx.step(req, owners, C, want_features, score_fn)
 
     def handle(self, op: int, hdr: np.ndarray, payload: bytes):
         n, now, aux, aux2 = int(hdr[1]), int(hdr[2]), int(hdr[3]), int(hdr[4])
-        if op == OP_SCORE:
-            return self.score(np.frombuffer(payload, REQREC).copy(), now, bool(aux))
+        if op == OP_SCORE:  # a worker's share of a step rank 0 started (no payload: the exchange)
+            return self.score(None, None, aux2, now, bool(aux))
         if op == OP_INGEST:
             ev = np.frombuffer(payload, REQREC).copy()
             mine = self._mine(owners_of(ev))
@@ -169,28 +173,54 @@ class ShardRunner:
 
 
 class SpmdGroup:
-    """Rank 0's handle on the group: issues an op to every rank and runs its own share."""
+    """Rank 0's handle on the group: issues an op to every rank and runs its own share.
+    Ops are serialised (one collective sequence at a time) by a lock."""
 
-    def __init__(self, comm, runner: ShardRunner):
+    def __init__(self, comm, runner: ShardRunner, max_rows: int = 8192, chunk_buckets=None):
         if comm.rank != 0:
             raise ValueError("SpmdGroup lives on rank 0; other ranks call run_worker()")
         self.comm = comm
         self.runner = runner
         self.world = comm.world
+        self.max_rows = int(max_rows)
+        self.chunk_buckets = sorted(chunk_buckets) if chunk_buckets else None
+        self._lock = threading.Lock()
 
     def _issue(self, op: int, payload: bytes = b"", n: int = 0, now: int = 0, aux: int = 0, aux2: int = 0,
                extra=(0, 0)):
         hdr = np.array([op, n, now, aux, aux2, extra[0], extra[1], 0], np.int64)
-        self.comm.bcast_i64(hdr, 0)
-        self.comm.bcast_bytes(payload, 0)
-        return self.runner.handle(op, hdr, payload)
+        with self._lock:
+            self.comm.bcast_i64(hdr, 0)
+            self.comm.bcast_bytes(payload, 0)
+            return self.runner.handle(op, hdr, payload)
+
+    def _chunk_capacity(self, owners: np.ndarray) -> int:
+        from .exchange import max_owner_count
+        c = max(max_owner_count(owners, self.world), 1)
+        if self.chunk_buckets is not None:  # GPU shards: the captured chunk capacities
+            for b in self.chunk_buckets:
+                if c <= b:
+                    return b
+            raise ValueError(f"{c} rows for one owner exceed the largest chunk bucket")
+        return 1 << (c - 1).bit_length()
 
     # ---- hot path
-    def score(self, req: np.ndarray, now: int, want_features: bool = True):
+    def score(self, req: np.ndarray, owners: np.ndarray, now: int, want_features: bool = True):
+        """Owner-routed scoring of ``req`` (REQREC) whose accounts live on ``owners``: one
+        header broadcast + one exchange step per ``max_rows`` rows."""
         n = len(req)
-        out = self._issue(OP_SCORE, np.ascontiguousarray(req).tobytes(), n=n, now=now, aux=int(want_features))
-        res = out[:2 * n].astype(np.uint32).reshape(n, 2)
-        feats = out[2 * n:].view(FEATREC).copy() if want_features else None
+        res = np.zeros((n, 2), np.uint32)
+        feats = np.zeros(n, FEATREC) if want_features else None
+        for i in range(0, n, self.max_rows):
+            sub, own = req[i:i + self.max_rows], np.asarray(owners[i:i + self.max_rows], np.int64)
+            C = self._chunk_capacity(own)
+            hdr = np.array([OP_SCORE, len(sub), now, int(want_features), C, 0, 0, 0], np.int64)
+            with self._lock:
+                self.comm.bcast_i64(hdr, 0)
+                r, f = self.runner.score(sub, own, C, now, want_features)
+            res[i:i + len(sub)] = r
+            if want_features:
+                feats[i:i + len(sub)] = f
         return res, feats
 
     # ---- cold path
@@ -240,20 +270,20 @@ class SpmdGroup:
 
     def stop(self) -> None:
         hdr = np.array([OP_STOP, 0, 0, 0, 0, 0, 0, 0], np.int64)
-        self.comm.bcast_i64(hdr, 0)
-        self.comm.bcast_bytes(b"", 0)
+        with self._lock:
+            self.comm.bcast_i64(hdr, 0)
 
 
-def run_worker(comm, backend, abuse_gpu=None) -> int:
-    """Loop of ranks >= 1 until rank 0 sends STOP. Returns the number of ops served."""
+def run_worker(comm, backend, abuse_gpu=None):
+    """Loop of ranks >= 1 until rank 0 sends STOP. Returns (ops served, rows scored)."""
     runner = ShardRunner(comm, backend, abuse_gpu)
     served = 0
     while True:
         hdr = comm.bcast_i64(np.zeros(8, np.int64), 0)
-        payload = comm.bcast_bytes(None, 0)
         op = int(hdr[0])
         if op == OP_STOP:
-            return served
+            return served, runner.rows_scored
+        payload = b"" if op == OP_SCORE else comm.bcast_bytes(None, 0)
         runner.handle(op, hdr, payload)
         served += 1
 

@@ -50,6 +50,10 @@ def main(argv=None) -> int:
     ap.add_argument("--audit-flush-every-s", type=float, default=2.0,
                     help="drain the risk_scores / ltv_predictions rings into AUDIT_DB this often")
     a = ap.parse_args(argv)
+    # HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues (default 4): the scorer's
+    # copy / state / model streams, the exchange's two RCCL streams and the default stream each
+    # get a queue of their own with 8 (must be set before the HIP runtime initialises)
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     cfg = Config.load(a.config or None)
     if a.gpus:
         cfg.gpu.devices = a.gpus
@@ -67,8 +71,9 @@ def main(argv=None) -> int:
                              device=f"cuda:{torch.cuda.current_device()}" if backend == "gpu" else None)
         if comm.rank != 0:
             from .engine.risk_engine import serve_shard
-            n = serve_shard(cfg, comm, backend=backend, capacity=a.accounts or None, fraud_model=_fraud_model(a, cfg))
-            log.info("shard worker stopped", extra={"fields": dict(rank=comm.rank, ops=n)})
+            n, rows = serve_shard(cfg, comm, backend=backend, capacity=a.accounts or None,
+                                  fraud_model=_fraud_model(a, cfg))
+            log.info("shard worker stopped", extra={"fields": dict(rank=comm.rank, ops=n, rows_scored=rows)})
             return 0
     from .api.grpc_server import RiskServer
     from .api.http_server import HttpServer

@@ -22,14 +22,18 @@ class Setup:
     store: Any
     scorer: Any
     pop: Any
-    pool: List[np.ndarray]
+    pool: List[Any]
     batch: int
     desc: str
+    chunk: int = 0       # data-parallel exchange: chunk capacity C (rows per owner per sender)
 
 
 def build(config: str, batch: int, accounts: int, dev, rank: int = 0, depth: int = 2,
           use_graphs: bool = True, history_batches: int = 24, n_pool: int = 8,
-          hot_frac: float = 0.02, precision: str = "fp32") -> Setup:
+          hot_frac: float = 0.02, precision: str = "fp32", dp: dict = None) -> Setup:
+    """``dp=dict(world=N, comms=[2 RcclComm])``: this rank is one of N ingress ranks of the
+    owner-routed exchange (engine/dp.py): its pool entries are (chunks, rows) whose rows are
+    spread over every owner uniformly at random, as hash routing spreads real accounts."""
     import torch
 
     from ..config import Config
@@ -47,8 +51,14 @@ def build(config: str, batch: int, accounts: int, dev, rank: int = 0, depth: int
     cfg.features.width = c["width"]
     cfg.gpu.buckets = [B]
     cfg.gpu.max_batch = B
-    pop = make_population(accounts, c["width"] - 30, seed=1000 + rank, fast_hash=True)
-    store = DeviceFeatureStore(accounts, cfg.features, dev, events=True, max_events=B)
+    world = dp["world"] if dp else 1
+    C = 0
+    if dp:
+        from ..parallel.exchange import chunk_capacity
+        C = chunk_capacity(B, world)
+    # one population layout on every owner in DP mode (rows from any ingress rank match it)
+    pop = make_population(accounts, c["width"] - 30, seed=1000 + (0 if dp else rank), fast_hash=True)
+    store = DeviceFeatureStore(accounts, cfg.features, dev, events=True, max_events=world * C if dp else B)
     store.set_batch_features(np.arange(accounts), pop.batch)
     if c["width"] > 30:
         store.set_ext(np.arange(accounts), pop.ext)
@@ -60,7 +70,12 @@ def build(config: str, batch: int, accounts: int, dev, rank: int = 0, depth: int
         m = native().OnnxModel.from_bytes(builders.build(c["model"]).SerializeToString())
         plan = to_device(compile_onnx(m), dev, precision)
         model = "plan"
-    sc = GpuScorer(cfg, store, plan=plan, model=model, device=dev, pipeline_depth=depth, use_graphs=use_graphs)
+    if dp:
+        from ..engine.dp import DpGpuScorer
+        sc = DpGpuScorer(cfg, store, dp["comms"], world, rank, senders=world, cbuckets=[C], plan=plan, model=model,
+                         device=dev, pipeline_depth=depth)
+    else:
+        sc = GpuScorer(cfg, store, plan=plan, model=model, device=dev, pipeline_depth=depth, use_graphs=use_graphs)
     rng = np.random.default_rng(7 + rank)
     for h in range(history_batches):  # ~an hour of history: windows, HLLs, sessions
         r = make_requests(pop, B, rng, NOW0 - 3600 + 150 * h, spread_s=150, hot_frac=0.01)
@@ -69,7 +84,21 @@ def build(config: str, batch: int, accounts: int, dev, rank: int = 0, depth: int
     torch.cuda.synchronize(dev)
     sc.capture()
     pool = [make_requests(pop, B, rng, NOW0, hot_frac=hot_frac, unknown_frac=0.001) for _ in range(n_pool)]
-    return Setup(cfg, store, sc, pop, pool, B, c["desc"])
+    if dp:
+        from ..parallel.exchange import build_chunks
+        chunks = []
+        for rows in pool:
+            owners = rng.integers(0, world, len(rows))
+            # a row whose owner's chunk is full waits for the next step in a server; the bench
+            # drops it from this step and counts only the rows actually sent (P ~ 1e-5 per step)
+            keep = np.ones(len(rows), bool)
+            for o in range(world):
+                idx = np.nonzero(owners == o)[0]
+                keep[idx[C:]] = False
+            buf = build_chunks(rows[keep], owners[keep], world, C)[0]
+            chunks.append((buf, int(keep.sum())))
+        pool = chunks
+    return Setup(cfg, store, sc, pop, pool, B, c["desc"], C)
 
 
 # ----------------------------------------------------------------------------- model-service configs
