@@ -122,7 +122,8 @@ def main():
     if a.stream and not a.no_graphs:
         return stream_bench(a, world, rank, dev)
     if (world > 1 and a.dp_mode == "exchange") or os.environ.get("IGP_FORCE_EXCHANGE") == "1":
-        return dp_bench(a, world, rank, dev)  # (forced at N = 1: RCCL's single-rank path, for tests)
+        if dp_bench(a, world, rank, dev) is not None:  # (forced at N = 1: RCCL's single-rank path, for tests)
+            return
     S = benchkit.build(a.config, a.batch, a.accounts, dev, rank=rank, depth=a.depth,
                        use_graphs=not a.no_graphs, precision=a.numerics)
     sc, pool, B = S.scorer, S.pool, S.batch
@@ -217,6 +218,7 @@ def main():
             "pipeline_depth": a.depth,
             "graphs": not a.no_graphs,
             "driver": "native" if sc.driver is not None else "python",
+            "dp_mode": a.dp_mode if world > 1 else "none",
             "numerics": numerics_desc(a),
         },
         "scope": "engine_only",
@@ -250,8 +252,23 @@ def dp_bench(a, world: int, rank: int, dev) -> None:
     from igaming_platform_amd.utils.synth import NOW0
     if a.depth < 2:
         raise SystemExit("the exchange pipeline needs --depth >= 2")
+    err = ""
+    try:
+        comms = rccl_comms(rank, world)
+    except Exception as e:  # RCCL refused (e.g. ranks sharing a GPU): every rank falls back together
+        comms, err = None, f"{type(e).__name__}: {e}"
+    if world > 1:
+        bad = torch.tensor([0 if comms is not None else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        if int(bad.item()):
+            print(json.dumps({"warning": "exchange communicators failed; replicas fallback", "rank": rank,
+                              "error": err}), file=sys.stderr, flush=True)
+            a.dp_mode = "replicas (exchange init failed)"
+            return None
+    elif comms is None:
+        raise RuntimeError(err)
     S = benchkit.build(a.config, a.batch, a.accounts, dev, rank=rank, depth=a.depth, precision=a.numerics,
-                       dp=dict(world=world, comms=rccl_comms(rank, world)))
+                       dp=dict(world=world, comms=comms))
     sc, pool, B, C = S.scorer, S.pool, S.batch, S.chunk
     met_sum = torch.zeros(128, dtype=torch.int64, device=dev)
 
@@ -311,7 +328,8 @@ def dp_bench(a, world: int, rank: int, dev) -> None:
         "vs_baseline": None, "dtype": a.numerics, "data": "synthetic",
         "config": {"model": S.desc, "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
                    "per_gpu_batch": B, "accounts_per_gpu": a.accounts, "pipeline_depth": a.depth, "graphs": True,
-                   "driver": "native exchange (XchgDriver, RCCL all-to-all x2 per step)",
+                   "driver": "native exchange (XchgDriver; two RCCL all-to-alls per step"
+                             + (", captured in the hipGraphs)" if sc.captured else ", issued by the driver)"),
                    "dp_mode": "exchange", "chunk_capacity": C, "rows_scored": total,
                    "rows_dropped_by_route": int(over.sum().item()),
                    "numerics": numerics_desc(a)},
@@ -321,6 +339,7 @@ def dp_bench(a, world: int, rank: int, dev) -> None:
         "host_us_per_batch": {k: round(float(v), 2) for k, v in host.items()},
     }
     _emit(a, world, rank, out)
+    return out
 
 
 def _emit(a, world: int, rank: int, out: dict) -> None:

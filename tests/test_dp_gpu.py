@@ -112,3 +112,50 @@ def test_spmd_engine_world1_matches_plain_gpu_engine():
         spmd.close()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,C", [(2, 64), (3, 40), (8, 16)])
+def test_exchange_kernels_multi_sender_layout(world, C):
+    """exchange_compact / exchange_scatter on a receive buffer holding several senders' chunks
+    (the N > 1 layout RCCL delivers) against their host twins (parallel/exchange.py)."""
+    import torch
+    from igaming_platform_amd.layouts import FEATREC, REQREC
+    from igaming_platform_amd.native import hipk
+    from igaming_platform_amd.parallel.exchange import build_chunks, compact, scatter_results
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(world)
+    recv = np.zeros(world * (C + 1), REQREC)
+    for p in range(world):  # chunk p = what sender p routed to this rank
+        n = int(rng.integers(0, C + 1))
+        rows = np.zeros(n, REQREC)
+        rows["slot"] = rng.integers(0, 1000, n)
+        rows["tx_type"] = rng.integers(0, 4, n) | (p << 8)
+        rows["amount"] = rng.integers(1, 10**6, n)
+        rows["dev_hash"] = rng.integers(1, 2**62, n)
+        recv[p * (C + 1):(p + 1) * (C + 1)] = build_chunks(rows, np.zeros(n, np.int64), 1, C)[0]
+    cap = world * C
+    d_recv = torch.from_numpy(recv.view(np.uint8).copy()).to(dev)
+    slab = torch.zeros(16 + 48 * cap, dtype=torch.uint8, device=dev)
+    route = torch.full((cap + 1,), -7, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    hipk().exchange_compact(d_recv.data_ptr(), slab.data_ptr() + 16, slab.data_ptr(), route.data_ptr(), world, C, cap, s)
+    torch.cuda.synchronize()
+    rows_ref, route_ref = compact(recv, world, C)
+    n = int(slab[:4].view(torch.int32).item())
+    assert n == len(rows_ref)
+    got = slab[16:16 + 48 * n].cpu().numpy().view(REQREC)
+    np.testing.assert_array_equal(got.view(np.uint8), rows_ref.view(np.uint8))
+    np.testing.assert_array_equal(route[:n].cpu().numpy(), route_ref)
+    assert int(route[cap].item()) == 0
+    # scatter: result + feature rows of the compact rows back into per-sender chunks
+    res = rng.integers(0, 2**31, (cap, 2)).astype(np.int32)
+    feats = rng.integers(0, 2**31, (cap, 32)).astype(np.int32)
+    send = torch.zeros(world * C * 136, dtype=torch.uint8, device=dev)
+    d_res, d_feat = torch.from_numpy(res).to(dev), torch.from_numpy(feats).to(dev)
+    hipk().exchange_scatter(slab.data_ptr(), route.data_ptr(), d_res.data_ptr(), d_feat.data_ptr(), send.data_ptr(),
+                            C, cap, s)
+    torch.cuda.synchronize()
+    want = scatter_results(res[:n].view(np.uint32), feats[:n].copy().view(FEATREC).reshape(-1), route_ref, world, C)
+    got = send.cpu().numpy().reshape(world, C * 136)
+    mask = scatter_results(np.ones((n, 2), np.uint32), np.ones(n, FEATREC), route_ref, world, C) != 0
+    np.testing.assert_array_equal(got[mask], want[mask])
