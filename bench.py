@@ -58,6 +58,12 @@ def parse():
                     help="N > 1: exchange = every rank ingests 8192 rows/step spread over all owners and "
                          "the owner-routed RCCL exchange (the serving path, engine/dp.py) moves each row to "
                          "its owner and the results back; replicas = N independent single-GPU pipelines")
+    ap.add_argument("--scope", default="engine_only", choices=["engine_only", "e2e", "grpc"],
+                    help="engine_only: pre-resolved ReqRec rows (the headline); e2e: ScoreBatch request bytes "
+                         "-> parse -> UUID AccountIndex -> GPU -> serialized response bytes, in-process; grpc: the "
+                         "same over grpc.aio with client processes (tools/bench_e2e.py)")
+    ap.add_argument("--rpc", default="batch", choices=["batch", "tx"], help="--scope grpc: ScoreBatch or unary "
+                    "ScoreTransaction through the micro-batcher")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
     if a.numerics == "auto":
@@ -88,6 +94,12 @@ def maybe_launch_torchrun(a) -> None:
 
 def main():
     a = parse()
+    if a.scope != "engine_only":  # 1 GPU, the request path end to end (tools/bench_e2e.py)
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+        import bench_e2e
+        argv = ["--scope", a.scope, "--rpc", a.rpc, "--accounts", str(a.accounts), "--steps", str(a.steps),
+                "--warmup", str(a.warmup)] + (["--json-out", a.json_out] if a.json_out else [])
+        return bench_e2e.main(argv)
     maybe_launch_torchrun(a)
     # HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues (default 4): the scorer's
     # copy / state / model streams, the default stream and RCCL's communication stream (N > 1)

@@ -177,7 +177,8 @@ PYBIND11_MODULE(_native, m) {
       .def("parse_tx", [](wire::RequestBatch& b, py::bytes data) {
         char* p; py::ssize_t n;
         PYBIND11_BYTES_AS_STRING_AND_SIZE(data.ptr(), &p, &n);
-        wire::parse_tx(p, size_t(n), b);
+        const std::string& own = b.own(p, size_t(n));
+        wire::parse_tx(own.data(), own.size(), b);
       })
       .def("parse_tx_list", [](wire::RequestBatch& b, py::list items) {
         // micro-batcher path: many unary ScoreTransactionRequest payloads -> one columnar batch
@@ -190,7 +191,17 @@ PYBIND11_MODULE(_native, m) {
         }
         py::gil_scoped_release rel;
         b.reserve(b.size() + bufs.size());
-        for (auto& x : bufs) wire::parse_tx(x.first, x.second, b);
+        size_t total = 0;
+        for (auto& x : bufs) total += x.second;
+        std::string all;  // one arena copy for the whole micro-batch
+        all.reserve(total);
+        for (auto& x : bufs) all.append(x.first, x.second);
+        const std::string& own = b.own(all.data(), all.size());
+        size_t off = 0;
+        for (auto& x : bufs) {
+          wire::parse_tx(own.data() + off, x.second, b);
+          off += x.second;
+        }
       })
       .def("pack_reqrec", [](const wire::RequestBatch& b, py::array_t<int32_t, py::array::c_style> slots,
                              py::array out, int64_t ts, py::object owners) {
@@ -221,7 +232,12 @@ PYBIND11_MODULE(_native, m) {
       }, py::arg("slots"), py::arg("out"), py::arg("ts"), py::arg("owners") = py::none())
       .def("clear", &wire::RequestBatch::clear)
       .def("__len__", &wire::RequestBatch::size)
-      .def_readonly("account_id", &wire::RequestBatch::account_id)
+      .def_property_readonly("account_id", [](const wire::RequestBatch& b) {
+        py::list l(b.account_id.size());
+        for (size_t k = 0; k < b.account_id.size(); ++k)
+          l[k] = py::str(b.account_id[k].data(), b.account_id[k].size());
+        return l;
+      })
       .def("columns", [](const wire::RequestBatch& b) {
         py::dict d;
         d["account_hash"] = vec_np(b.account_hash);
@@ -237,12 +253,25 @@ PYBIND11_MODULE(_native, m) {
 
   py::class_<AccountIndex, std::shared_ptr<AccountIndex>>(m, "AccountIndex")
       .def(py::init<int64_t>())
-      .def("lookup_batch", [](AccountIndex& ix, const wire::RequestBatch& b, bool insert) {
+      .def("lookup_batch", [](AccountIndex& ix, const wire::RequestBatch& b, bool insert, py::object sel) {
+        // sel: optional bool/uint8 mask (rows of other owners are skipped, slot -1)
         py::array_t<int32_t> slots(b.size());
         py::array_t<uint8_t> fresh(b.size());
-        ix.lookup(b.account_id, b.account_hash, insert, slots.mutable_data(), fresh.mutable_data());
+        py::array_t<uint8_t, py::array::c_style | py::array::forcecast> m;
+        const uint8_t* mp = nullptr;
+        if (!sel.is_none()) {
+          m = sel;
+          if (size_t(m.size()) != b.size()) throw std::runtime_error("lookup_batch: mask length");
+          mp = m.data();
+        }
+        int32_t* sp = slots.mutable_data();
+        uint8_t* fp = fresh.mutable_data();
+        {
+          py::gil_scoped_release rel;
+          ix.lookup_views(b.account_id.data(), b.account_hash.data(), b.account_check.data(), b.size(), insert, sp, fp, mp);
+        }
         return py::make_tuple(slots, fresh);
-      })
+      }, py::arg("batch"), py::arg("insert") = true, py::arg("sel") = py::none())
       .def("lookup", [](AccountIndex& ix, const std::vector<std::string>& ids, bool insert) {
         std::vector<uint64_t> h(ids.size());
         for (size_t k = 0; k < ids.size(); ++k) h[k] = id_hash(ids[k], SEED_ACCOUNT);
@@ -256,7 +285,7 @@ PYBIND11_MODULE(_native, m) {
       .def("id_of", &AccountIndex::id_of);
 
   py::class_<LinkIndex, std::shared_ptr<LinkIndex>>(m, "LinkIndex")
-      .def(py::init<int>(), py::arg("per_key") = 32)
+      .def(py::init<int, int64_t>(), py::arg("per_key") = 8, py::arg("buckets") = int64_t(1) << 18)
       .def("add", [](LinkIndex& ix, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> dev,
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> acct) {
         if (dev.size() != acct.size()) throw std::runtime_error("LinkIndex.add: length mismatch");

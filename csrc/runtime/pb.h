@@ -110,7 +110,29 @@ struct Writer {
   void msg(uint32_t field, const std::string& body) {
     tag(field, LEN); varint(body.size()); buf.append(body);
   }
+  // header of a sub-message whose body (of `size` bytes) the caller writes next
+  void msg_header(uint32_t field, size_t size) { tag(field, LEN); varint(size); }
   static size_t varint_size(uint64_t v) { size_t n = 1; while (v >= 0x80) { v >>= 7; ++n; } return n; }
+};
+
+// Same field API as Writer, counting bytes only (sizes nested messages before writing them).
+struct Sizer {
+  size_t n = 0;
+  void varint(uint64_t v) { n += Writer::varint_size(v); }
+  void tag(uint32_t field, uint32_t wire) { varint((uint64_t(field) << 3) | wire); }
+  void u64(uint32_t field, uint64_t v) { if (v) { tag(field, VARINT); varint(v); } }
+  void i64(uint32_t field, int64_t v) { if (v) { tag(field, VARINT); varint(uint64_t(v)); } }
+  void i32(uint32_t field, int32_t v) { if (v) { tag(field, VARINT); varint(uint64_t(int64_t(v))); } }
+  void boolean(uint32_t field, bool v) { if (v) { tag(field, VARINT); varint(1); } }
+  void f32(uint32_t field, float v) {
+    uint32_t u; std::memcpy(&u, &v, 4);
+    if (u == 0) return;
+    tag(field, I32);
+    n += 4;
+  }
+  void str(uint32_t field, std::string_view s) { if (!s.empty()) str_always(field, s); }
+  void str_always(uint32_t field, std::string_view s) { tag(field, LEN); varint(s.size()); n += s.size(); }
+  void msg_header(uint32_t field, size_t size) { tag(field, LEN); varint(size); }
 };
 
 }  // namespace igp::pb

@@ -2,6 +2,7 @@
 
 #include <cstring>
 
+#include "account_index.h"
 #include "pb.h"
 #include "xxh64.h"
 
@@ -13,13 +14,18 @@ const char* const kReasonCodes[12] = {
     "ML_HIGH_RISK", "SUSPICIOUS_PATTERN", "MULTI_ACCOUNT", "DEVICE_FINGERPRINT_MISMATCH"};
 
 void RequestBatch::clear() {
-  account_id.clear(); account_hash.clear(); amount.clear(); tx_type.clear();
-  device_hash.clear(); fp_hash.clear(); ip_hash.clear();
+  account_id.clear(); account_hash.clear(); account_check.clear(); amount.clear(); tx_type.clear();
+  device_hash.clear(); fp_hash.clear(); ip_hash.clear(); arena.clear();
 }
 
 void RequestBatch::reserve(size_t n) {
-  account_id.reserve(n); account_hash.reserve(n); amount.reserve(n); tx_type.reserve(n);
+  account_id.reserve(n); account_hash.reserve(n); account_check.reserve(n); amount.reserve(n); tx_type.reserve(n);
   device_hash.reserve(n); fp_hash.reserve(n); ip_hash.reserve(n);
+}
+
+const std::string& RequestBatch::own(const char* data, size_t n) {
+  arena.emplace_back(std::make_unique<std::string>(data, n));
+  return *arena.back();
 }
 
 uint8_t tx_type_id(const char* s, size_t n) {
@@ -49,8 +55,9 @@ void parse_tx(const char* data, size_t n, RequestBatch& out) {
       default: r.skip(w);  // player_id, currency, game/round, user_agent, session, metadata
     }
   }
-  out.account_id.emplace_back(acct);
+  out.account_id.push_back(acct);  // a view into the batch's arena copy of the payload
   out.account_hash.push_back(id_hash(acct, SEED_ACCOUNT));
+  out.account_check.push_back(id_check(acct));
   out.amount.push_back(amount);
   out.tx_type.push_back(tx_type_id(type.data(), type.size()));
   out.device_hash.push_back(id_hash(dev, SEED_DEVICE));
@@ -59,7 +66,8 @@ void parse_tx(const char* data, size_t n, RequestBatch& out) {
 }
 
 void parse_batch(const char* data, size_t n, RequestBatch& out) {
-  pb::Reader r(data, n);
+  const std::string& own = out.own(data, n);
+  pb::Reader r(own.data(), own.size());
   uint32_t f, w;
   while (r.tag(f, w)) {
     if (f == 1 && w == pb::LEN) {
@@ -71,8 +79,11 @@ void parse_batch(const char* data, size_t n, RequestBatch& out) {
   }
 }
 
-std::string serialize_feature_vector(const FeatRec& x) {
-  pb::Writer o;
+// Field emitters templated on the sink: pb::Writer appends bytes, pb::Sizer only counts them,
+// so a nested message is sized first and then written straight into the one output buffer
+// (no per-row temporary strings).
+template <class W>
+void emit_feature_vector(W& o, const FeatRec& x) {
   o.i32(1, x.tx_count_1m);
   o.i32(2, x.tx_count_5m);
   o.i32(3, x.tx_count_1h);
@@ -99,11 +110,10 @@ std::string serialize_feature_vector(const FeatRec& x) {
   o.i32(24, x.bonus_claim_count);
   o.f32(25, x.bonus_wager_rate);
   o.boolean(26, x.flags & FR_BONUS_ONLY);
-  return o.buf;
 }
 
-std::string serialize_tx_response(const ResultView& v, size_t i) {
-  pb::Writer o;
+template <class W>
+void emit_tx_response(W& o, const ResultView& v, size_t i) {
   const uint32_t p = v.res[i].packed;
   o.i32(1, int32_t(IGP_RES_SCORE(p)));
   o.i32(2, int32_t(IGP_RES_ACTION(p)));
@@ -114,14 +124,35 @@ std::string serialize_tx_response(const ResultView& v, size_t i) {
   o.i32(4, int32_t(IGP_RES_RULE(p)));
   o.f32(5, v.res[i].ml);
   if (v.response_ms) o.i64(6, v.response_ms[i]);
-  if (v.feat) o.msg(7, serialize_feature_vector(v.feat[i]));
+  if (v.feat) {
+    pb::Sizer fs;
+    emit_feature_vector(fs, v.feat[i]);
+    o.msg_header(7, fs.n);
+    emit_feature_vector(o, v.feat[i]);
+  }
+}
+
+std::string serialize_feature_vector(const FeatRec& x) {
+  pb::Writer o;
+  emit_feature_vector(o, x);
+  return o.buf;
+}
+
+std::string serialize_tx_response(const ResultView& v, size_t i) {
+  pb::Writer o;
+  emit_tx_response(o, v, i);
   return o.buf;
 }
 
 std::string serialize_batch_response(const ResultView& v) {
   pb::Writer o;
-  o.buf.reserve(v.n * (v.feat ? 96 : 24));
-  for (size_t i = 0; i < v.n; ++i) o.msg(1, serialize_tx_response(v, i));
+  o.buf.reserve(v.n * (v.feat ? 112 : 28));
+  for (size_t i = 0; i < v.n; ++i) {
+    pb::Sizer s;
+    emit_tx_response(s, v, i);
+    o.msg_header(1, s.n);
+    emit_tx_response(o, v, i);
+  }
   return o.buf;
 }
 

@@ -37,14 +37,13 @@ class AccountRegistry:
             return np.asarray(slots, np.int32), owners, np.asarray(fresh, bool)
         slots = np.full(n, -1, np.int32)
         fresh = np.zeros(n, bool)
-        ids = batch.account_id
         for o in range(self.world):
-            sel = np.nonzero(owners == o)[0]
-            if len(sel) == 0:
+            mine = owners == o
+            if not mine.any():
                 continue
-            s, f = self.index[o].lookup([ids[i] for i in sel], insert)
-            slots[sel] = s
-            fresh[sel] = np.asarray(f, bool)
+            s, f = self.index[o].lookup_batch(batch, insert, mine)  # C++, GIL released
+            slots[mine] = s[mine]
+            fresh[mine] = np.asarray(f, bool)[mine]
         return slots, owners, fresh
 
     def resolve_ids(self, ids: Sequence[str], insert: bool = False) -> Tuple[np.ndarray, np.ndarray]:

@@ -93,7 +93,12 @@ class RiskEngine:
         self.registry = AccountRegistry(self.capacity, world)
         self.blacklist = Blacklist(cfg.gpu.blacklist_capacity)
         self.ipintel = IPIntel(cfg.gpu.blacklist_capacity)
-        self.links = N.LinkIndex(32)
+        self.links = N.LinkIndex(8)  # 8 most recent accounts per device / devices per account
+        # link inserts run off the scoring path on one background thread (C++, GIL released);
+        # linked_accounts() waits for the inserts already queued
+        import concurrent.futures as _cf
+        self._link_pool = _cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="risk-links")
+        self._link_pending: List = []
         self._lock = threading.RLock()
         self.scoring = cfg.scoring
         # risk_scores / ltv_predictions audit (engine/audit.py): on when AUDIT_DB is configured
@@ -220,8 +225,7 @@ class RiskEngine:
         rb.pack_reqrec(slots, req.view(np.uint8), now, None)
         if self.group is not None:  # owner-routed exchange: each rank scores its own rows
             res, feats = self.group.score(req, owners, now, want_features)
-            cols = rb.columns()
-            self.links.add(cols["device_hash"], (owners.astype(np.int64) << 32) | np.where(slots >= 0, slots, -1))
+            self._add_links(rb, slots, owners)
             self._observe(rb, res, version)
             return res, feats, slots, owners
         res = np.zeros((n, 2), np.uint32)
@@ -241,10 +245,26 @@ class RiskEngine:
                 res[sel] = r
                 if want_features:
                     feats[sel] = f
-        cols = rb.columns()
-        self.links.add(cols["device_hash"], (owners.astype(np.int64) << 32) | np.where(slots >= 0, slots, -1))
+        self._add_links(rb, slots, owners)
         self._observe(rb, res, version)
         return res, feats, slots, owners
+
+    def _add_links(self, rb, slots: np.ndarray, owners: np.ndarray) -> None:
+        """(device, account) co-occurrences of a batch -> the link index, asynchronously."""
+        dev = rb.columns()["device_hash"]
+        keys = (owners.astype(np.int64) << 32) | np.where(slots >= 0, slots, -1)
+        with self._lock:
+            self._link_pending = [f for f in self._link_pending if not f.done()]
+            if len(self._link_pending) >= 8:  # the worker fell behind: insert inline (bounded queue)
+                self.links.add(dev, keys)
+                return
+            self._link_pending.append(self._link_pool.submit(self.links.add, dev, keys))
+
+    def _flush_links(self) -> None:
+        with self._lock:
+            pend, self._link_pending = self._link_pending, []
+        for f in pend:
+            f.result()
 
     def _observe(self, rb, res: np.ndarray, version: int) -> None:
         """Metrics + the risk_scores audit entry of one scored batch (every scoring entry point
@@ -477,8 +497,7 @@ class RiskEngine:
             sel = owners == o
             if np.any(sel):
                 self.backends[o].ingest(req[sel])
-        cols = rb.columns()
-        self.links.add(cols["device_hash"], (owners.astype(np.int64) << 32) | np.where(slots >= 0, slots, -1))
+        self._add_links(rb, slots, owners)
         return len(events)
 
     # ---- warehouse batch features (engine.go:127-140 / the hourly job, main.go:227-236)
@@ -523,6 +542,7 @@ class RiskEngine:
         return self.abuse.check([account_id], now)[0]
 
     def linked_accounts(self, owner: int, slot: int, limit: int = 16) -> List[str]:
+        self._flush_links()
         keys = self.links.linked((int(owner) << 32) | int(slot), limit)
         return [self.registry.id_of(int(k) >> 32, int(k) & 0xFFFFFFFF) for k in keys]
 

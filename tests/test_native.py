@@ -232,3 +232,23 @@ def test_link_index_bounds_and_links():
     L.add(np.array([7, 7, 7], np.uint64), np.array([1, 2, 3], np.int64))
     assert L.linked(3, 10) == [2]          # per-device list keeps the 2 most recent accounts
     assert L.devices_of(1) == [7]
+
+
+def test_link_index_account_zero_and_bounded_buckets():
+    L = N.LinkIndex(4, 4)   # 4 buckets x 4 ways: at most 16 devices / 16 accounts are tracked
+    L.add(np.array([5, 5], np.uint64), np.array([0, 9], np.int64))   # account key 0 is a real slot
+    assert L.devices_of(0) == [5] and L.linked(0, 4) == [9]
+    L.add(np.arange(100, 300, dtype=np.uint64), np.arange(1000, 1200, dtype=np.int64))
+    assert L.n_devices() <= 16   # fixed memory: old keys were evicted
+    assert L.linked(1199, 4) == [] and L.devices_of(1199) == [299]
+
+
+def test_account_index_batch_lookup_with_owner_mask():
+    rb = N.RequestBatch()
+    rb.parse_tx_list([P.ScoreTransactionRequest(account_id=a, amount=1).SerializeToString()
+                      for a in ["x", "y", "x", "z"]])
+    ix = N.AccountIndex(8)
+    s, f = ix.lookup_batch(rb, True, np.array([1, 0, 1, 1], bool))
+    assert list(s) == [0, -1, 0, 1] and list(f) == [1, 0, 0, 1]
+    s, _ = ix.lookup_batch(rb, False)
+    assert list(s) == [0, -1, 0, 1] and ix.id_of(1) == "z" and list(rb.account_id) == ["x", "y", "x", "z"]

@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""End-to-end scoring benches (VERDICT r1 "put the real request path in the timed region"):
+
+``--scope e2e``  raw ``ScoreBatchRequest`` bytes -> C++ wire parse -> AccountIndex lookup of the
+                 UUID account-id strings -> ReqRec pack -> GPU pipeline -> C++ response
+                 serialisation (FeatureVector per row included), in-process, T caller threads
+                 (``RiskEngine.score_batch_bytes``: what the ScoreBatch handler runs).
+``--scope grpc`` the same server behind ``grpc.aio`` on 127.0.0.1: client processes send raw
+                 ``ScoreBatch`` payloads, or unary ``ScoreTransaction`` calls that the
+                 micro-batcher merges into device batches (``--rpc tx``).
+
+Synthetic data: UUID account ids with warehouse batch features and 98 extended features loaded
+through the engine's own loaders; random-init cfg3 weights (GBDT 100 x d7 -> MLP 32-256-1).
+Prints one JSON line with "scope", throughput and p50/p99 latency (client-measured for grpc)."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+import uuid
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+BASELINE_P99_MS = 50.0  # README.md:58
+TYPES = ["deposit", "withdraw", "bet", "win"]
+
+
+def account_id(i: int) -> str:
+    return str(uuid.UUID(int=(i * 0x9E3779B97F4A7C15 + 0x632BE59BD9B4E019) & ((1 << 128) - 1), version=4))
+
+
+def make_payloads(n_accounts: int, n_payloads: int, batch: int, seed: int):
+    """Serialized ScoreBatchRequest messages of ``batch`` transactions each."""
+    from igaming_platform_amd.proto import risk_v1 as P
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n_payloads):
+        acc = rng.integers(0, n_accounts, batch)
+        amt = np.maximum(1, rng.lognormal(7.5, 1.6, batch)).astype(np.int64)
+        typ = rng.choice(4, batch, p=[0.25, 0.1, 0.55, 0.1])
+        dev = rng.integers(0, 6, batch)
+        req = P.ScoreBatchRequest(transactions=[
+            P.ScoreTransactionRequest(account_id=account_id(int(a)), amount=int(m), transaction_type=TYPES[int(t)],
+                                      currency="EUR", device_id=f"dev-{int(a)}-{int(d)}",
+                                      ip_address=f"10.{int(a) % 250}.{int(a) // 250 % 250}.{int(d)}",
+                                      fingerprint=f"fp-{int(a)}-{int(d)}", session_id=f"s-{int(a)}")
+            for a, m, t, d in zip(acc, amt, typ, dev)])
+        out.append(req.SerializeToString())
+    return out
+
+
+def tx_payloads(n_accounts: int, n: int, seed: int):
+    from igaming_platform_amd.proto import risk_v1 as P
+    rng = np.random.default_rng(seed)
+    return [P.ScoreTransactionRequest(account_id=account_id(int(a)), amount=int(rng.integers(100, 500000)),
+                                      transaction_type=TYPES[int(rng.integers(0, 4))], device_id=f"dev-{int(a)}-0",
+                                      ip_address="10.0.0.1").SerializeToString()
+            for a in rng.integers(0, n_accounts, n)]
+
+
+def build_engine(accounts: int, batch: int, backend: str):
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.engine.risk_engine import RiskEngine
+    from igaming_platform_amd.layouts import ACCTBATCH
+    from igaming_platform_amd.onnx import builders
+    from igaming_platform_amd.utils.synth import make_population
+    cfg = Config()
+    cfg.features.width = 128
+    cfg.gpu.buckets = sorted({64, 512, 2048, batch})
+    cfg.gpu.max_batch = batch
+    eng = RiskEngine(cfg, backend=backend, capacity=accounts + 1024,
+                     fraud_model=builders.build("stacked").SerializeToString())
+    pop = make_population(accounts, 98, seed=3, fast_hash=True)
+    ids = [account_id(i) for i in range(accounts)]
+    step = 1 << 18
+    for s in range(0, accounts, step):
+        eng.load_batch_features(ids[s:s + step], np.asarray(pop.batch[s:s + step], ACCTBATCH))
+        eng.load_ext_features(ids[s:s + step], pop.ext[s:s + step])
+    return eng
+
+
+def run_e2e(a) -> dict:
+    eng = build_engine(a.accounts, a.batch, a.backend)
+    payloads = make_payloads(a.accounts, a.payloads, a.batch, seed=11)
+    n_req = a.batch
+    for i in range(a.warmup):  # windows / HLLs fill, graphs warm
+        eng.score_batch_bytes(payloads[i % len(payloads)])
+    lat, lock = [], threading.Lock()
+    counter = {"i": 0}
+
+    def worker():
+        while True:
+            with lock:
+                i = counter["i"]
+                if i >= a.steps:
+                    return
+                counter["i"] = i + 1
+            t0 = time.perf_counter()
+            out = eng.score_batch_bytes(payloads[i % len(payloads)], t0)
+            dt = (time.perf_counter() - t0) * 1e3
+            assert len(out) > n_req  # every response carries n_req ScoreTransactionResponse messages
+            with lock:
+                lat.append(dt)
+
+    th = [threading.Thread(target=worker) for _ in range(a.threads)]
+    t0 = time.perf_counter()
+    [t.start() for t in th]
+    [t.join() for t in th]
+    el = time.perf_counter() - t0
+    eng.close()
+    return dict(metric="fraud scores/sec (risk.v1.ScoreBatch bytes in -> bytes out, in-process)",
+                value=a.steps * n_req / el, unit="scores/s", scope="e2e", n_gpus=1 if a.backend == "gpu" else 0,
+                steps=a.steps, warmup=a.warmup, ms_per_step=el / a.steps * 1e3, higher_is_better=True,
+                scaling="weak", vs_baseline=None, dtype="fp32", data="synthetic (UUID ids, random-init cfg3 weights)",
+                config=dict(model="cfg3 GBDT(100,d7,128f)+MLP(32-256-1)", batch_per_request=n_req,
+                            caller_threads=a.threads, accounts=a.accounts,
+                            path="C++ parse -> AccountIndex(UUID) -> pack -> GPU graphs -> C++ serialize"),
+                p50_latency_ms=float(np.percentile(lat, 50)), p99_latency_ms=float(np.percentile(lat, 99)),
+                latency_baseline_ms=BASELINE_P99_MS,
+                latency_vs_baseline=BASELINE_P99_MS / float(np.percentile(lat, 99)))
+
+
+def _client(i, port, kind, accounts, batch, n_payloads, t_start, t_end, q):
+    import grpc
+    from igaming_platform_amd.proto import risk_v1 as P
+    ch = grpc.insecure_channel(f"127.0.0.1:{port}", options=[("grpc.max_receive_message_length", 256 << 20),
+                                                             ("grpc.max_send_message_length", 256 << 20)])
+    if kind == "batch":
+        call = ch.unary_unary(P.method_path("ScoreBatch"))
+        payloads = make_payloads(accounts, n_payloads, batch, seed=100 + i)
+        per = batch
+    else:
+        call = ch.unary_unary(P.method_path("ScoreTransaction"))
+        payloads = tx_payloads(accounts, 4096, seed=100 + i)
+        per = 1
+    lat, errs, k = [], 0, 0
+    while time.time() < t_start - 1.0:  # connect / warm before the window
+        call(payloads[k % len(payloads)], timeout=30)
+        k += 1
+    while time.time() < t_end:
+        t0 = time.perf_counter()
+        try:
+            call(payloads[k % len(payloads)], timeout=30)
+        except Exception:
+            errs += 1
+            continue
+        finally:
+            k += 1
+        if time.time() >= t_start:
+            lat.append((time.perf_counter() - t0) * 1e3)
+    ch.close()
+    q.put((lat, errs, per))
+
+
+def run_grpc(a) -> dict:
+    import multiprocessing as mp
+    from igaming_platform_amd.api.grpc_server import RiskServer
+    eng = build_engine(a.accounts, a.batch, a.backend)
+    srv = RiskServer(eng, port=0, batching=a.rpc == "tx", workers=16).start()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    lead = 25.0  # client start-up (import + payload generation) happens before the window
+    t_end = time.time() + lead + a.seconds
+    procs = [ctx.Process(target=_client, args=(i, srv.port, "batch" if a.rpc == "batch" else "tx", a.accounts,
+                                               a.batch, 4, t_end - a.seconds, t_end, q))
+             for i in range(a.clients)]
+    [p.start() for p in procs]
+    res = [q.get(timeout=a.seconds + lead + 300) for _ in procs]
+    [p.join() for p in procs]
+    srv.stop(0.5)
+    eng.close()
+    lat = [x for r in res for x in r[0]]
+    per = res[0][2]
+    calls = len(lat)
+    return dict(metric=("fraud scores/sec (risk.v1.ScoreBatch over gRPC)" if a.rpc == "batch" else
+                        "fraud scores/sec (unary risk.v1.ScoreTransaction over gRPC, micro-batched)"),
+                value=calls * per / a.seconds, unit="scores/s", scope="grpc", n_gpus=1 if a.backend == "gpu" else 0,
+                higher_is_better=True, dtype="fp32", data="synthetic (UUID ids, random-init cfg3 weights)",
+                config=dict(model="cfg3 GBDT(100,d7,128f)+MLP(32-256-1)", rpc=a.rpc, clients=a.clients,
+                            seconds=a.seconds, transactions_per_call=per, accounts=a.accounts,
+                            server="grpc.aio, raw-bytes handlers, C++ codec"
+                                   + (", MicroBatcher" if a.rpc == "tx" else "")),
+                calls=calls, errors=sum(r[1] for r in res),
+                p50_latency_ms=float(np.percentile(lat, 50)), p99_latency_ms=float(np.percentile(lat, 99)),
+                latency_baseline_ms=BASELINE_P99_MS,
+                latency_vs_baseline=BASELINE_P99_MS / float(np.percentile(lat, 99)))
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scope", default="e2e", choices=["e2e", "grpc"])
+    ap.add_argument("--rpc", default="batch", choices=["batch", "tx"])
+    ap.add_argument("--backend", default="gpu", choices=["gpu", "cpu"])
+    ap.add_argument("--accounts", type=int, default=1 << 20)
+    ap.add_argument("--batch", type=int, default=8192)
+    ap.add_argument("--payloads", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--threads", type=int, default=3)
+    ap.add_argument("--clients", type=int, default=8)
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--json-out", default="")
+    a = ap.parse_args(argv)
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    out = run_e2e(a) if a.scope == "e2e" else run_grpc(a)
+    line = json.dumps(out)
+    print(line, flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            f.write(line + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
