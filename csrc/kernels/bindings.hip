@@ -323,4 +323,44 @@ PYBIND11_MODULE(_hipk, m) {
     check("gru");
   });
   m.def("gru_ws_clusters", [](int n_rows) { return gru_ws_clusters(n_rows); });
+
+  m.def("mlp_chain", [](py::dict d, uintptr_t s) {
+    MlpChainArgs a{};
+    a.X = ptr<const float*>(d, "X");
+    a.ldx = geti(d, "ldx");
+    a.slots = ptr<const int32_t*>(d, "slots");
+    a.pf_tab = ptr<const float*>(d, "pf_tab");
+    a.ext_tab = ptr<const float*>(d, "ext_tab");
+    a.ext_w = geti(d, "ext_w");
+    a.in_w = geti(d, "in_w");
+    a.in_live = geti(d, "in_live");
+    a.m_ptr = ptr<const int32_t*>(d, "m_ptr");
+    a.n_rows = geti(d, "n_rows");
+    a.n_layers = geti(d, "n_layers");
+    if (a.n_layers < 1 || a.n_layers > MC_MAX_LAYERS) throw std::runtime_error("mlp_chain: 1..8 layers");
+    for (int l = 0; l < a.n_layers; ++l) {
+      const std::string p = "l" + std::to_string(l) + "_";
+      a.W[l] = ptr<const uint16_t*>(d, (p + "W").c_str());
+      a.bias[l] = ptr<const float*>(d, (p + "b").c_str());
+      a.N[l] = geti(d, (p + "N").c_str());
+      a.K[l] = geti(d, (p + "K").c_str());
+      a.act[l] = geti(d, (p + "act").c_str());
+      if (!a.W[l]) throw std::runtime_error("mlp_chain: missing weights");
+      if (a.N[l] < 64 || a.N[l] > 512 || a.N[l] % 64) throw std::runtime_error("mlp_chain: N must be 64..512, % 64");
+      if (a.K[l] < 64 || a.K[l] > 512 || a.K[l] % 64) throw std::runtime_error("mlp_chain: K must be 64..512, % 64");
+      if (l > 0 && a.K[l] != a.N[l - 1]) throw std::runtime_error("mlp_chain: K[l] != N[l-1]");
+    }
+    if (a.in_w != a.K[0] || a.in_live > a.in_w || a.in_live < 1) throw std::runtime_error("mlp_chain: input width");
+    a.w2 = ptr<const float*>(d, "w2");
+    a.b2 = d.contains("b2") ? d["b2"].cast<float>() : 0.f;
+    a.act2 = geti(d, "act2");
+    a.ml = ptr<float*>(d, "ml");
+    a.ltv_out = ptr<float*>(d, "ltv_out");
+    if (!a.w2) throw std::runtime_error("mlp_chain: head weights required");
+    if (!a.slots && !a.X) throw std::runtime_error("mlp_chain: input");
+    if (a.slots && !a.pf_tab) throw std::runtime_error("mlp_chain: LTV gather needs the profile table");
+    if (a.ltv_out && !a.slots) throw std::runtime_error("mlp_chain: the K9 epilogue needs slots");
+    launch_mlp_chain(a, stream_of(s));
+    check("mlp_chain");
+  });
 }

@@ -235,4 +235,32 @@ struct LtvAssembleArgs {
 };
 void launch_ltv_assemble(const LtvAssembleArgs& a, hipStream_t st);
 
+// ---- K3 fused MLP chain (mlp_fused.hip): up to 8 dense layers with the activation tile in LDS,
+// the last one followed by an N -> 1 head; optional LTV input gather and K9 epilogue
+constexpr int MC_MAX_LAYERS = 8;
+struct MlpChainArgs {
+  const float* X;           // dense input [rows][ldx] f32 (when slots == null)
+  int32_t ldx;
+  const int32_t* slots;     // LTV gather: player slots [rows] (-1: empty profile)
+  const float* pf_tab;      // [C][25]
+  const float* ext_tab;     // [C][ext_w] (nullable)
+  int32_t ext_w;
+  int32_t in_w;             // staged input width = K[0] (multiple of 64)
+  int32_t in_live;          // real input columns (<= in_w; the rest are zero)
+  const int32_t* m_ptr;     // live rows in device memory (nullable)
+  int32_t n_rows;
+  int32_t n_layers;
+  const uint16_t* W[MC_MAX_LAYERS];  // bf16 [N][K] row-major
+  const float* bias[MC_MAX_LAYERS];  // [N] (nullable)
+  int32_t N[MC_MAX_LAYERS];          // multiple of 64, <= 512
+  int32_t K[MC_MAX_LAYERS];          // multiple of 64, <= 512; K[l] == N[l-1]
+  int32_t act[MC_MAX_LAYERS];
+  const float* w2;          // head [N_last] f32
+  float b2;
+  int32_t act2;
+  float* ml;                // [rows] head output (nullable)
+  float* ltv_out;           // [rows][6] K9 output (nullable; needs slots + pf_tab)
+};
+void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st);
+
 }  // namespace igp

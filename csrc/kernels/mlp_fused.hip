@@ -1,0 +1,200 @@
+// K3 MLP chain fused into one kernel (VERDICT r1 "fused 4-layer MLP ... activation tile in
+// LDS, weights streamed from L2"): cfg 4's LTV model, input [rows, 256] -> 4 x (Gemm 512 + Relu)
+// -> Gemm 512 -> 1, plus (optionally) the model input gather from the HBM player tables and the
+// K9 churn / segment / next-best-action epilogue.
+//
+// One workgroup = 32 rows, 4 waves (8192 rows -> 256 workgroups, one per CU). The 32-row
+// activation tile lives in LDS for the whole chain (bf16, two 32 x 520 buffers ping-ponged
+// between layers: 66.5 KB), so hidden activations never touch HBM and the chain is one launch
+// instead of five. Each wave owns a quarter of a layer's output columns (N/4 <= 128: eight
+// 16-column MFMA tiles x two 16-row tiles, v_mfma_f32_16x16x32_bf16, f32 accumulators). A
+// fragments come from LDS (ds_read_b128; the 1040-byte row pitch spreads a 16-row read over all
+// 64 banks); B fragments are 16-byte loads straight from the weights [N][K] (L2-resident: the
+// whole 4 x 512 chain is 1.8 MB bf16, every workgroup reads it), prefetched two K-steps ahead
+// into a 3-deep register ring. Bias + activation + bf16 rounding of a hidden layer happen in
+// the epilogue that writes the next layer's LDS tile; the last hidden layer's epilogue instead
+// applies the N -> 1 head (per-lane partial dots, xor-shuffle row sums, a 4-wave LDS reduce).
+//
+// Numerics = the unfused bf16 path (gemm.hip / mlp_head): bf16 weights and activations, f32
+// accumulation, bf16 rounding of each hidden activation.
+#include "common.h"
+#include "launch.h"
+#include "ltv.h"
+
+namespace igp {
+
+typedef __attribute__((ext_vector_type(8))) short mc_bf16x8;
+typedef __attribute__((ext_vector_type(4))) float mc_f32x4;
+
+constexpr int MC_ROWS = 32;
+constexpr int MC_LDA = 512 + 8;  // bf16 elements per LDS row (1040 B)
+
+__device__ __forceinline__ float mc_act(float v, int act) {
+  switch (act) {
+    case 1: return v > 0.f ? v : 0.f;
+    case 2: return 1.f / (1.f + expf(-v));
+    case 3: return tanhf(v);
+    default: return v;
+  }
+}
+
+// one layer's MFMA loop: acc[m][j] += Hin[m-th 16 rows][:K] . W[col tile j][:K]^T
+template <int NKS>
+__device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, const uint16_t* __restrict__ W, int K,
+                                             int colw, int NT, int lane, mc_f32x4 (&acc)[2][8]) {
+  mc_bf16x8 fb[3][8];
+  const int kq = 8 * (lane >> 4);
+  const uint16_t* wrow = W + (size_t)(colw + (lane & 15)) * K + kq;
+  auto load = [&](int ks, mc_bf16x8 (&dst)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < NT) dst[j] = *reinterpret_cast<const mc_bf16x8*>(wrow + (size_t)j * 16 * K + ks * 32);
+  };
+  load(0, fb[0]);
+  if (NKS > 1) load(1, fb[1]);
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    if (ks + 2 < NKS) load(ks + 2, fb[(ks + 2) % 3]);
+    const mc_bf16x8 fa0 = *reinterpret_cast<const mc_bf16x8*>(&Hin[(lane & 15) * MC_LDA + ks * 32 + kq]);
+    const mc_bf16x8 fa1 = *reinterpret_cast<const mc_bf16x8*>(&Hin[(16 + (lane & 15)) * MC_LDA + ks * 32 + kq]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < NT) {
+        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, fb[ks % 3][j], acc[0][j], 0, 0, 0);
+        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1, fb[ks % 3][j], acc[1][j], 0, 0, 0);
+      }
+  }
+}
+
+__global__ void __launch_bounds__(256) mlp_chain_kernel(MlpChainArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t H[2][MC_ROWS * MC_LDA];
+  __shared__ float part[4][MC_ROWS];
+  __shared__ float mlv[MC_ROWS];
+  __shared__ float pfl[MC_ROWS][P_NCOLS];  // raw profile rows for the K9 epilogue
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row0 = blockIdx.x * MC_ROWS;
+  const int n_live = a.m_ptr ? min(*a.m_ptr, a.n_rows) : a.n_rows;
+  if (row0 >= n_live) return;  // uniform per block, before any barrier
+
+  // ---- stage the 32-row input tile (bf16) into H[0]: thread t stages row t/8, columns
+  // [32 (t%8), +32), all 32 loads issued before the first use (one memory round trip, not 32);
+  // LTV: the raw 25 profile values of each row are kept in LDS for the K9 epilogue
+  const int K0 = a.in_w;  // padded to the first layer's K (a multiple of 64); columns >= in_live are 0
+  {
+    const int r = tid >> 3, row = row0 + r;
+    const bool live = row < n_live;
+    const int s = (live && a.slots) ? a.slots[row] : -1;
+    for (int c0 = (tid & 7) * 32; c0 < K0; c0 += 256) {
+      float v[32];
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        const int c = c0 + i;
+        float x = 0.f;
+        if (live && c < a.in_live) {
+          if (a.slots) {
+            if (s >= 0) {
+              if (c < P_NCOLS) x = a.pf_tab[(size_t)s * P_NCOLS + c];
+              else if (a.ext_tab && c - P_NCOLS < a.ext_w) x = a.ext_tab[(size_t)s * a.ext_w + (c - P_NCOLS)];
+            }
+          } else {
+            x = a.X[(size_t)row * a.ldx + c];
+          }
+        }
+        v[i] = x;
+      }
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        const int c = c0 + i;
+        float x = v[i];
+        if (a.slots && c < P_NCOLS) {
+          if (a.ltv_out) pfl[r][c] = x;
+          x = copysignf(log1pf(fabsf(x)), x);  // [sign*log1p|profile| (25) | extended features]
+        }
+        H[0][r * MC_LDA + c] = f32_to_bf16(x);
+      }
+    }
+  }
+  __syncthreads();
+
+  int cur = 0;
+  for (int l = 0; l < a.n_layers; ++l) {
+    const int K = a.K[l], N = a.N[l], NT = N >> 6;
+    const int colw = wave * (N >> 2);
+    mc_f32x4 acc[2][8];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[m][j] = mc_f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint16_t* Hin = H[cur];
+    switch (K >> 5) {  // K-steps of 32 (the host allows 2..16)
+      case 2: mc_layer_mma<2>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      case 4: mc_layer_mma<4>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      case 6: mc_layer_mma<6>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      case 8: mc_layer_mma<8>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      case 10: mc_layer_mma<10>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      case 12: mc_layer_mma<12>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      case 14: mc_layer_mma<14>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      default: mc_layer_mma<16>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+    }
+    const float* bias = a.bias[l];
+    const int act = a.act[l];
+    if (l + 1 < a.n_layers) {
+      // hidden layer: bias + act -> bf16 -> the next layer's LDS tile
+      uint16_t* Hout = H[cur ^ 1];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (j >= NT) continue;
+          const int col = colw + j * 16 + (lane & 15);
+          const float b = bias ? bias[col] : 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            Hout[(m * 16 + 4 * (lane >> 4) + q) * MC_LDA + col] = f32_to_bf16(mc_act(acc[m][j][q] + b, act));
+        }
+      __syncthreads();
+      cur ^= 1;
+      continue;
+    }
+    // last hidden layer: y[r] = act2(sum_n act(h[r][n] + b[n]) * w2[n] + b2)
+    float rs[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (j >= NT) continue;
+      const int col = colw + j * 16 + (lane & 15);
+      const float b = bias ? bias[col] : 0.f, w = a.w2[col];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rs[m][q] += mc_act(acc[m][j][q] + b, act) * w;
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float v = rs[m][q];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        if ((lane & 15) == 0) part[wave][m * 16 + 4 * (lane >> 4) + q] = v;
+      }
+  }
+  __syncthreads();
+  if (tid < MC_ROWS) {
+    const float y = mc_act(part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid] + a.b2, a.act2);
+    mlv[tid] = y;
+    const int row = row0 + tid;
+    if (row < a.n_rows) {
+      if (a.ml) a.ml[row] = y;
+      if (a.ltv_out) ltv_row(pfl[tid], &mlv[tid], a.ltv_out + (size_t)row * 6);  // K9, learned LTV
+    }
+  }
+}
+
+void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st) {
+  if (a.n_rows <= 0) return;
+  hipLaunchKernelGGL(mlp_chain_kernel, dim3((a.n_rows + MC_ROWS - 1) / MC_ROWS), dim3(256), 0, st, a);
+}
+
+}  // namespace igp

@@ -18,6 +18,7 @@ columns followed by the account's extra LTV features (zeros when none are loaded
 """
 from __future__ import annotations
 
+import os
 import threading
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
@@ -110,6 +111,12 @@ class LtvGpu:
         if plan is not None and self.w < N_COLS:
             raise ValueError(f"LTV model input ({self.w}) must hold the {N_COLS} profile columns")
         self.model = DeviceModel(plan, self.device, self.buckets) if plan is not None else None
+        # a dense chain (cfg 4: 256 -> 4 x 512 -> 1, bf16) runs as ONE fused kernel with the
+        # table gather and K9 in it (csrc/kernels/mlp_fused.hip); IGP_MLP_FUSED=0: layer kernels
+        self.chain = None
+        if (plan is not None and plan.precision == "bf16" and os.environ.get("IGP_MLP_FUSED", "1") != "0"
+                and K.MlpChainPack.eligible(plan.steps)):
+            self.chain = K.MlpChainPack(plan.steps, self.device)
         dev = self.device
         self.capacity = int(capacity)
         self.pf_tab = torch.zeros((self.capacity, N_COLS), dtype=torch.float32, device=dev)
@@ -146,6 +153,11 @@ class LtvGpu:
     # ---- the step
     def _body(self, slot: int, b: int) -> None:
         self.dev_slab[:16 + 4 * b].copy_(self.host[slot][:16 + 4 * b], non_blocking=True)
+        if self.chain is not None:
+            self.K.mlp_chain(self.chain, b, slots=self.slots, pf_tab=self.pf_tab, ext_tab=self.ext_tab,
+                             ltv_out=self.out, m_ptr=self.n_ptr)
+            self.host_out[slot][:b].copy_(self.out[:b], non_blocking=True)
+            return
         ml = None
         if self.model is not None:
             self.K.ltv_assemble(self.slots, self.pf_tab, self.ext_tab, self.X, b, m_ptr=self.n_ptr)

@@ -442,3 +442,83 @@ def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh
     elif yh is None:
         raise ValueError("gru: nothing to write (no head, no yh)")
     _mod().gru(d, _stream())
+
+
+# --------------------------------------------------------------------------- K3 fused MLP chain
+class MlpChainPack:
+    """Device weights of a dense chain for the fused kernel (csrc/kernels/mlp_fused.hip):
+    ``steps`` = DenseStep* + HeadStep (models/plan.py). Each layer's bf16 W [N][K_pad] (K padded
+    with zeros to a multiple of 64), f32 bias; the head's N -> 1 vector in f32."""
+
+    MAX_LAYERS = 8
+
+    @staticmethod
+    def eligible(steps) -> bool:
+        if not steps or steps[-1].kind != "head" or any(s.kind != "dense" for s in steps[:-1]):
+            return False
+        if len(steps) > MlpChainPack.MAX_LAYERS:
+            return False
+        widths = [s.n for s in steps[:-1]] + [steps[-1].n1]
+        ks = [s.k for s in steps[:-1]] + [steps[-1].k]
+        if any(n % 64 or n < 64 or n > 512 for n in widths) or any(k < 1 or k > 512 for k in ks):
+            return False
+        return all(ks[i] == widths[i - 1] for i in range(1, len(ks)))
+
+    def __init__(self, steps, device):
+        import numpy as np
+        if not self.eligible(steps):
+            raise ValueError("mlp_chain: the plan is not a dense chain the fused kernel covers")
+        dev = as_device(device)
+        self.layers = []
+        for s in steps:
+            w = s.w1_np if s.kind == "head" else s.w_np
+            b = s.b1_np if s.kind == "head" else s.b_np
+            n, k = w.shape
+            kp = -(-k // 64) * 64
+            buf = np.zeros((n, kp), np.float32)
+            buf[:, :k] = w
+            self.layers.append(dict(W=torch.from_numpy(buf).to(torch.bfloat16).to(dev),
+                                    b=None if b is None else torch.from_numpy(np.ascontiguousarray(b, np.float32)).to(dev),
+                                    N=n, K=kp, act=ACT[s.act1 if s.kind == "head" else s.act]))
+        head = steps[-1]
+        self.w2 = torch.from_numpy(np.ascontiguousarray(head.w2_np, np.float32)).to(dev)
+        self.b2, self.act2 = float(head.b2), ACT[head.act2]
+        self.in_live = steps[0].k
+        self.in_w = self.layers[0]["K"]
+        self.device = dev
+
+
+def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, slots: Optional[torch.Tensor] = None,
+              pf_tab: Optional[torch.Tensor] = None, ext_tab: Optional[torch.Tensor] = None,
+              ml: Optional[torch.Tensor] = None, ltv_out: Optional[torch.Tensor] = None,
+              m_ptr: Optional[torch.Tensor] = None) -> None:
+    """Fused dense chain + N=1 head over ``n_rows`` rows. Input: dense ``X`` [rows, >= in] f32, or
+    the LTV gather (``slots`` into ``pf_tab`` [C, 25] / ``ext_tab`` [C, ext_w]); outputs ``ml``
+    [rows] and/or the K9 rows ``ltv_out`` [rows, 6]."""
+    dev = pk.device
+    d = dict(n_rows=int(n_rows), n_layers=len(pk.layers), in_w=pk.in_w, in_live=pk.in_live,
+             m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32, device=dev), w2=_need(pk.w2, "w2", torch.float32, device=dev),
+             b2=pk.b2, act2=pk.act2,
+             ml=_opt(ml, "ml", dtype=torch.float32, min_numel=n_rows, device=dev),
+             ltv_out=_opt(ltv_out, "ltv_out", dtype=torch.float32, min_numel=6 * n_rows, device=dev))
+    if slots is not None:
+        if pf_tab is None or pf_tab.dim() != 2 or pf_tab.shape[1] != 25:
+            raise ValueError("mlp_chain: LTV gather needs the [C, 25] profile table")
+        ext_w = 0 if ext_tab is None else int(ext_tab.shape[1])
+        if 25 + ext_w < pk.in_live:
+            raise ValueError("mlp_chain: tables narrower than the model input")
+        d.update(slots=_need(slots, "slots", torch.int32, n_rows, dev), pf_tab=_need(pf_tab, "pf_tab", torch.float32, device=dev),
+                 ext_tab=_opt(ext_tab, "ext_tab", dtype=torch.float32, device=dev), ext_w=ext_w)
+    else:
+        if X is None or X.dim() != 2 or X.shape[1] < pk.in_live or X.shape[0] < n_rows:
+            raise ValueError("mlp_chain: X must be [>= rows, >= model input]")
+        if ltv_out is not None:
+            raise ValueError("mlp_chain: the K9 epilogue needs slots")
+        d.update(X=_need(X, "X", torch.float32, device=dev), ldx=int(X.shape[1]))
+    if ml is None and ltv_out is None:
+        raise ValueError("mlp_chain: nothing to write")
+    for i, l in enumerate(pk.layers):
+        d[f"l{i}_W"] = _need(l["W"], "W", torch.bfloat16, l["N"] * l["K"], dev)
+        d[f"l{i}_b"] = _opt(l["b"], "b", dtype=torch.float32, min_numel=l["N"], device=dev)
+        d[f"l{i}_N"], d[f"l{i}_K"], d[f"l{i}_act"] = l["N"], l["K"], l["act"]
+    _mod().mlp_chain(d, _stream())
