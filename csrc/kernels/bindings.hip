@@ -356,6 +356,13 @@ PYBIND11_MODULE(_hipk, m) {
     a.act2 = geti(d, "act2");
     a.ml = ptr<float*>(d, "ml");
     a.ltv_out = ptr<float*>(d, "ltv_out");
+    a.rows_per_block = geti(d, "rows_per_block", 32);
+    a.waves = geti(d, "waves", 4);
+    if (a.rows_per_block != 16 && a.rows_per_block != 32 && a.rows_per_block != 64)
+      throw std::runtime_error("mlp_chain: 16, 32 or 64 rows per block");
+    if (a.waves != 4 && a.waves != 8) throw std::runtime_error("mlp_chain: 4 or 8 waves");
+    for (int l = 0; l < a.n_layers; ++l)
+      if (a.N[l] % (16 * a.waves)) throw std::runtime_error("mlp_chain: N must be a multiple of 16 x waves");
     if (!a.w2) throw std::runtime_error("mlp_chain: head weights required");
     if (!a.slots && !a.X) throw std::runtime_error("mlp_chain: input");
     if (a.slots && !a.pf_tab) throw std::runtime_error("mlp_chain: LTV gather needs the profile table");

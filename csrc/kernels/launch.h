@@ -260,6 +260,8 @@ struct MlpChainArgs {
   int32_t act2;
   float* ml;                // [rows] head output (nullable)
   float* ltv_out;           // [rows][6] K9 output (nullable; needs slots + pf_tab)
+  int32_t rows_per_block;   // 16, 32 (default) or 64 rows per workgroup
+  int32_t waves;            // 4 (default) or 8 (32 rows; each wave owns N/8 columns)
 };
 void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st);
 

@@ -26,7 +26,6 @@ namespace igp {
 typedef __attribute__((ext_vector_type(8))) short mc_bf16x8;
 typedef __attribute__((ext_vector_type(4))) float mc_f32x4;
 
-constexpr int MC_ROWS = 32;
 constexpr int MC_LDA = 512 + 8;  // bf16 elements per LDS row (1040 B)
 
 __device__ __forceinline__ float mc_act(float v, int act) {
@@ -38,37 +37,54 @@ __device__ __forceinline__ float mc_act(float v, int act) {
   }
 }
 
-// one layer's MFMA loop: acc[m][j] += Hin[m-th 16 rows][:K] . W[col tile j][:K]^T
-template <int NKS>
+// one layer's MFMA loop: acc[m][j] += Hin[m-th 16 rows][:K] . W[col tile j][:K]^T.
+// W arrives fragment-packed (MlpChainPack): tile (nt, ks) = 64 lanes x 8 bf16 contiguous, lane l
+// holding W[16 nt + (l & 15)][32 ks + 8 (l >> 4) .. +8], so each B-fragment load is one fully
+// coalesced 1 KB wave read (row-major W made it 16 half-used 128-B lines per instruction and
+// the texture path, not the MFMA, set the pace: 92 -> see profiles/NOTES.md).
+template <int NKS, int MT, int JT>
 __device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, const uint16_t* __restrict__ W, int K,
-                                             int colw, int NT, int lane, mc_f32x4 (&acc)[2][8]) {
-  mc_bf16x8 fb[3][8];
+                                             int colw, int NT, int lane, mc_f32x4 (&acc)[MT][JT]) {
+  mc_bf16x8 fb[3][JT];
   const int kq = 8 * (lane >> 4);
-  const uint16_t* wrow = W + (size_t)(colw + (lane & 15)) * K + kq;
-  auto load = [&](int ks, mc_bf16x8 (&dst)[8]) {
+  const uint16_t* wt = W + ((size_t)(colw >> 4) * NKS) * 512 + lane * 8;  // this wave's first n-tile
+  // branch-free: tiles j >= NT (layers narrower than 512) re-load tile NT-1 and their
+  // accumulators are never read; a guarded load made hipcc branch and wait vmcnt(0) per load
+  int jt[JT];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (j < NT) dst[j] = *reinterpret_cast<const mc_bf16x8*>(wrow + (size_t)j * 16 * K + ks * 32);
+  for (int j = 0; j < JT; ++j) jt[j] = (j < NT ? j : NT - 1) * NKS;
+  auto load = [&](int ks, mc_bf16x8 (&dst)[JT]) {
+#pragma unroll
+    for (int j = 0; j < JT; ++j) dst[j] = *reinterpret_cast<const mc_bf16x8*>(wt + ((size_t)jt[j] + ks) * 512);
   };
   load(0, fb[0]);
   if (NKS > 1) load(1, fb[1]);
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
     if (ks + 2 < NKS) load(ks + 2, fb[(ks + 2) % 3]);
-    const mc_bf16x8 fa0 = *reinterpret_cast<const mc_bf16x8*>(&Hin[(lane & 15) * MC_LDA + ks * 32 + kq]);
-    const mc_bf16x8 fa1 = *reinterpret_cast<const mc_bf16x8*>(&Hin[(16 + (lane & 15)) * MC_LDA + ks * 32 + kq]);
+    // keep the prefetch at the top of the step: without this fence the scheduler sank each
+    // load next to its MFMAs and the loop ran at vmcnt(1) (one load in flight per wave)
+    __builtin_amdgcn_sched_barrier(0);
+    mc_bf16x8 fa[MT];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (j < NT) {
-        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, fb[ks % 3][j], acc[0][j], 0, 0, 0);
-        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1, fb[ks % 3][j], acc[1][j], 0, 0, 0);
-      }
+    for (int m = 0; m < MT; ++m)
+      fa[m] = *reinterpret_cast<const mc_bf16x8*>(&Hin[(16 * m + (lane & 15)) * MC_LDA + ks * 32 + kq]);
+#pragma unroll
+    for (int j = 0; j < JT; ++j)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[ks % 3][j], acc[m][j], 0, 0, 0);
   }
 }
 
-__global__ void __launch_bounds__(256) mlp_chain_kernel(MlpChainArgs a) {
+template <int MC_ROWS, int WAVES>
+__global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
+  constexpr int MT = MC_ROWS / 16;            // 16-row MFMA tiles per wave
+  constexpr int THREADS = 64 * WAVES;
+  constexpr int PARTS = THREADS / MC_ROWS;    // staging threads per row
+  constexpr int JT = 32 / WAVES;              // 16-column tiles per wave at N = 512
   __shared__ __attribute__((aligned(16))) uint16_t H[2][MC_ROWS * MC_LDA];
-  __shared__ float part[4][MC_ROWS];
+  __shared__ float part[WAVES][MC_ROWS];
   __shared__ float mlv[MC_ROWS];
   __shared__ float pfl[MC_ROWS][P_NCOLS];  // raw profile rows for the K9 epilogue
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -81,10 +97,10 @@ __global__ void __launch_bounds__(256) mlp_chain_kernel(MlpChainArgs a) {
   // LTV: the raw 25 profile values of each row are kept in LDS for the K9 epilogue
   const int K0 = a.in_w;  // padded to the first layer's K (a multiple of 64); columns >= in_live are 0
   {
-    const int r = tid >> 3, row = row0 + r;
+    const int r = tid / PARTS, row = row0 + r;
     const bool live = row < n_live;
     const int s = (live && a.slots) ? a.slots[row] : -1;
-    for (int c0 = (tid & 7) * 32; c0 < K0; c0 += 256) {
+    for (int c0 = (tid % PARTS) * 32; c0 < K0; c0 += PARTS * 32) {
       float v[32];
 #pragma unroll
       for (int i = 0; i < 32; ++i) {
@@ -118,23 +134,23 @@ __global__ void __launch_bounds__(256) mlp_chain_kernel(MlpChainArgs a) {
 
   int cur = 0;
   for (int l = 0; l < a.n_layers; ++l) {
-    const int K = a.K[l], N = a.N[l], NT = N >> 6;
-    const int colw = wave * (N >> 2);
-    mc_f32x4 acc[2][8];
+    const int K = a.K[l], N = a.N[l], NT = N / (16 * WAVES);
+    const int colw = wave * (N / WAVES);
+    mc_f32x4 acc[MT][JT];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[m][j] = mc_f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < JT; ++j) acc[m][j] = mc_f32x4{0.f, 0.f, 0.f, 0.f};
     const uint16_t* Hin = H[cur];
     switch (K >> 5) {  // K-steps of 32 (the host allows 2..16)
-      case 2: mc_layer_mma<2>(Hin, a.W[l], K, colw, NT, lane, acc); break;
-      case 4: mc_layer_mma<4>(Hin, a.W[l], K, colw, NT, lane, acc); break;
-      case 6: mc_layer_mma<6>(Hin, a.W[l], K, colw, NT, lane, acc); break;
-      case 8: mc_layer_mma<8>(Hin, a.W[l], K, colw, NT, lane, acc); break;
-      case 10: mc_layer_mma<10>(Hin, a.W[l], K, colw, NT, lane, acc); break;
-      case 12: mc_layer_mma<12>(Hin, a.W[l], K, colw, NT, lane, acc); break;
-      case 14: mc_layer_mma<14>(Hin, a.W[l], K, colw, NT, lane, acc); break;
-      default: mc_layer_mma<16>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      case 2: mc_layer_mma<2, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      case 4: mc_layer_mma<4, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      case 6: mc_layer_mma<6, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      case 8: mc_layer_mma<8, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      case 10: mc_layer_mma<10, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      case 12: mc_layer_mma<12, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      case 14: mc_layer_mma<14, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      default: mc_layer_mma<16, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
     }
     const float* bias = a.bias[l];
     const int act = a.act[l];
@@ -142,9 +158,9 @@ __global__ void __launch_bounds__(256) mlp_chain_kernel(MlpChainArgs a) {
       // hidden layer: bias + act -> bf16 -> the next layer's LDS tile
       uint16_t* Hout = H[cur ^ 1];
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+      for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < JT; ++j) {
           if (j >= NT) continue;
           const int col = colw + j * 16 + (lane & 15);
           const float b = bias ? bias[col] : 0.f;
@@ -157,19 +173,21 @@ __global__ void __launch_bounds__(256) mlp_chain_kernel(MlpChainArgs a) {
       continue;
     }
     // last hidden layer: y[r] = act2(sum_n act(h[r][n] + b[n]) * w2[n] + b2)
-    float rs[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    float rs[MT][4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int m = 0; m < MT; ++m) rs[m][0] = rs[m][1] = rs[m][2] = rs[m][3] = 0.f;
+#pragma unroll
+    for (int j = 0; j < JT; ++j) {
       if (j >= NT) continue;
       const int col = colw + j * 16 + (lane & 15);
       const float b = bias ? bias[col] : 0.f, w = a.w2[col];
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+      for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int q = 0; q < 4; ++q) rs[m][q] += mc_act(acc[m][j][q] + b, act) * w;
     }
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         float v = rs[m][q];
@@ -182,7 +200,10 @@ __global__ void __launch_bounds__(256) mlp_chain_kernel(MlpChainArgs a) {
   }
   __syncthreads();
   if (tid < MC_ROWS) {
-    const float y = mc_act(part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid] + a.b2, a.act2);
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) sum += part[w][tid];
+    const float y = mc_act(sum + a.b2, a.act2);
     mlv[tid] = y;
     const int row = row0 + tid;
     if (row < a.n_rows) {
@@ -194,7 +215,15 @@ __global__ void __launch_bounds__(256) mlp_chain_kernel(MlpChainArgs a) {
 
 void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
-  hipLaunchKernelGGL(mlp_chain_kernel, dim3((a.n_rows + MC_ROWS - 1) / MC_ROWS), dim3(256), 0, st, a);
+  const int r = a.rows_per_block;
+  if (a.waves == 8)
+    hipLaunchKernelGGL((mlp_chain_kernel<32, 8>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
+  else if (r == 64)
+    hipLaunchKernelGGL((mlp_chain_kernel<64, 4>), dim3((a.n_rows + 63) / 64), dim3(256), 0, st, a);
+  else if (r == 16)
+    hipLaunchKernelGGL((mlp_chain_kernel<16, 4>), dim3((a.n_rows + 15) / 16), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((mlp_chain_kernel<32, 4>), dim3((a.n_rows + 31) / 32), dim3(256), 0, st, a);
 }
 
 }  // namespace igp

@@ -250,6 +250,29 @@ PYBIND11_MODULE(_native, m) {
       });
 
   m.def("tx_type_id", [](const std::string& s) { return int(wire::tx_type_id(s.data(), s.size())); });
+  // batch identifier digests (utils/hashing.id_hash semantics: "" -> 0, a real 0 -> 1)
+  m.def("id_hashes", [](py::list values, uint64_t seed) {
+    std::vector<std::string_view> v;
+    v.reserve(values.size());
+    for (auto it : values) {
+      char* p; py::ssize_t n;
+      if (PyUnicode_Check(it.ptr())) {
+        const char* u = PyUnicode_AsUTF8AndSize(it.ptr(), &n);
+        if (!u) throw py::error_already_set();
+        p = const_cast<char*>(u);
+      } else if (PYBIND11_BYTES_AS_STRING_AND_SIZE(it.ptr(), &p, &n) != 0) {
+        throw std::runtime_error("id_hashes: str or bytes expected");
+      }
+      v.emplace_back(p, size_t(n));
+    }
+    py::array_t<uint64_t> out(v.size());
+    uint64_t* o = out.mutable_data();
+    {
+      py::gil_scoped_release rel;
+      for (size_t k = 0; k < v.size(); ++k) o[k] = id_hash(v[k], seed);
+    }
+    return out;
+  });
 
   py::class_<AccountIndex, std::shared_ptr<AccountIndex>>(m, "AccountIndex")
       .def(py::init<int64_t>())

@@ -127,9 +127,41 @@ class MetricsInterceptor(grpc.ServerInterceptor):
 
 # ============================================================================ risk.v1
 class RiskServicer:
-    def __init__(self, engine, batcher: Optional[MicroBatcher] = None):
+    def __init__(self, engine, batcher: Optional[MicroBatcher] = None, ltv_batcher: Optional[MicroBatcher] = None,
+                 abuse_batcher: Optional[MicroBatcher] = None):
         self.e = engine
         self.batcher = batcher
+        # cold RPCs: concurrent unary calls merge into one batched engine call (one LTV graph /
+        # one K1 feature read + one GRU launch per shard) instead of a device batch of one each
+        self.ltv_batcher = ltv_batcher
+        self.abuse_batcher = abuse_batcher
+
+    def _ltv(self, account_id: str):
+        if self.ltv_batcher is not None:
+            return self.ltv_batcher.submit(account_id).result()
+        return self.e.predict_ltv(account_id)
+
+    def _abuse(self, account_id: str, bonus_id: str):
+        if self.abuse_batcher is not None:
+            return self.abuse_batcher.submit(account_id).result()
+        return self.e.check_bonus_abuse(account_id, bonus_id)
+
+    @staticmethod
+    def ltv_response(req, r):
+        return P.PredictLTVResponse(account_id=req.account_id, predicted_ltv=r.predicted_ltv, segment=r.segment,
+                                    churn_risk=r.churn_risk, predicted_active_days=r.survival_days,
+                                    confidence=r.confidence, next_best_action=r.next_best_action,
+                                    predicted_at=_ts(time.time()))
+
+    @staticmethod
+    def segment_response(req, r):
+        return P.GetPlayerSegmentResponse(account_id=req.account_id, segment=r.segment, ltv=r.predicted_ltv,
+                                          churn_risk=r.churn_risk, recommended_actions=r.recommended_actions())
+
+    @staticmethod
+    def abuse_response(r):
+        return P.CheckBonusAbuseResponse(is_abuser=r.is_abuser, abuse_score=r.abuse_score, signals=r.signals,
+                                         linked_accounts=r.linked_accounts)
 
     # ---- scoring (raw bytes in / out)
     def ScoreTransaction(self, data: bytes, ctx) -> bytes:
@@ -145,25 +177,17 @@ class RiskServicer:
     def PredictLTV(self, req, ctx):
         if not req.account_id:
             raise InvalidArgument("account_id is required")
-        r = self.e.predict_ltv(req.account_id)
-        return P.PredictLTVResponse(account_id=req.account_id, predicted_ltv=r.predicted_ltv, segment=r.segment,
-                                    churn_risk=r.churn_risk, predicted_active_days=r.survival_days,
-                                    confidence=r.confidence, next_best_action=r.next_best_action,
-                                    predicted_at=_ts(time.time()))
+        return self.ltv_response(req, self._ltv(req.account_id))
 
     def GetPlayerSegment(self, req, ctx):
         if not req.account_id:
             raise InvalidArgument("account_id is required")
-        r = self.e.predict_ltv(req.account_id)
-        return P.GetPlayerSegmentResponse(account_id=req.account_id, segment=r.segment, ltv=r.predicted_ltv,
-                                          churn_risk=r.churn_risk, recommended_actions=r.recommended_actions())
+        return self.segment_response(req, self._ltv(req.account_id))
 
     def CheckBonusAbuse(self, req, ctx):
         if not req.account_id:
             raise InvalidArgument("account_id is required")
-        r = self.e.check_bonus_abuse(req.account_id, req.bonus_id)
-        return P.CheckBonusAbuseResponse(is_abuser=r.is_abuser, abuse_score=r.abuse_score, signals=r.signals,
-                                         linked_accounts=r.linked_accounts)
+        return self.abuse_response(self._abuse(req.account_id, req.bonus_id))
 
     # ---- blacklist
     def AddToBlacklist(self, req, ctx):
@@ -394,6 +418,18 @@ def aio_risk_handler(servicer: RiskServicer, pool, inline_all: bool) -> grpc.Gen
         if rpc == "ScoreTransaction" and servicer.batcher is not None:
             async def h(data, ctx, _b=servicer.batcher):
                 return await asyncio.wrap_future(_b.submit(data, time.perf_counter()))
+        elif rpc in ("PredictLTV", "GetPlayerSegment") and servicer.ltv_batcher is not None:
+            build = servicer.ltv_response if rpc == "PredictLTV" else servicer.segment_response
+
+            async def h(req, ctx, _b=servicer.ltv_batcher, _build=build):
+                if not req.account_id:
+                    raise InvalidArgument("account_id is required")
+                return _build(req, await asyncio.wrap_future(_b.submit(req.account_id)))
+        elif rpc == "CheckBonusAbuse" and servicer.abuse_batcher is not None:
+            async def h(req, ctx, _b=servicer.abuse_batcher):
+                if not req.account_id:
+                    raise InvalidArgument("account_id is required")
+                return servicer.abuse_response(await asyncio.wrap_future(_b.submit(req.account_id)))
         elif inline_all or rpc in INLINE:
             async def h(req, ctx, _f=fn):
                 return _f(req, ctx)
@@ -461,10 +497,16 @@ class RiskServer:
             self.batcher = MicroBatcher(engine.score_tx_many_bytes, max_batch or cfg.gpu.max_batch,
                                         cfg.gpu.wait_us if wait_us is None else wait_us, workers=2,
                                         on_batch=lambda n: engine.metrics.batch_size.observe(n))
+        self.ltv_batcher = self.abuse_batcher = None
+        if batching:
+            wait = cfg.gpu.wait_us if wait_us is None else wait_us
+            self.ltv_batcher = MicroBatcher(lambda ids, _t: engine.predict_ltv_batch(ids), 4096, wait, workers=1)
+            self.abuse_batcher = MicroBatcher(lambda ids, _t: engine.check_bonus_abuse_batch(ids), 4096, wait,
+                                              workers=1)
         self.health = HealthServicer()
         self.health.set(P.SERVICE, "SERVING")
         self.pool = futures.ThreadPoolExecutor(max_workers=workers, thread_name_prefix="risk-rpc")
-        self._servicer = RiskServicer(engine, self.batcher)
+        self._servicer = RiskServicer(engine, self.batcher, self.ltv_batcher, self.abuse_batcher)
         self._host, self._port_req = host, port
         self.loop = asyncio.new_event_loop()
         self._thread = threading.Thread(target=self.loop.run_forever, name="risk-grpc-loop", daemon=True)
@@ -495,5 +537,6 @@ class RiskServer:
         self.loop.call_soon_threadsafe(self.loop.stop)
         self._thread.join(timeout=5)
         self.pool.shutdown(wait=False)
-        if self.batcher is not None:
-            self.batcher.close()
+        for b in (self.batcher, self.ltv_batcher, self.abuse_batcher):
+            if b is not None:
+                b.close()

@@ -213,6 +213,9 @@ class CpuBackend:
             f, bl, rule, reasons, _ = self._features(r[0], now)
         return _featrec_from_golden(f, r[0], bl, rule, reasons)
 
+    def features_many(self, slots, now: int) -> np.ndarray:
+        return np.array([self.features(int(s), now) for s in slots], FEATREC).reshape(-1)
+
     def event_history(self, slot: int) -> np.ndarray:
         with self._lock:
             return self.store.event_history(str(slot))
@@ -429,27 +432,42 @@ class GpuBackend:
             raise ValueError("the GPU scorer always applies score-then-update")
         return self.collect(self.submit(req, now, want_features))
 
+    FX_ROWS = 1024  # rows per K1 launch of the feature read path
+
     def features(self, slot: int, now: int) -> np.ndarray:
         """GetFeatures: K1 on a synthetic request for ``slot`` (no update)."""
+        return self.features_many(np.array([slot], np.int32), now)[0]
+
+    def features_many(self, slots, now: int) -> np.ndarray:
+        """Feature rows of many accounts in one K1 launch per 1024 (no update): batched
+        GetFeatures / the CheckBonusAbuse rule signals. Returns FEATREC [n]."""
         from ..ops import kernels as K
         torch = self.torch
+        slots = np.asarray(slots, np.int32)
+        out = np.zeros(len(slots), FEATREC)
+        R = self.FX_ROWS
         with self._lock:
             if self._fx is None:
-                self._fx = dict(slab=torch.zeros(16 + 48 * 64, dtype=torch.uint8, device=self.device),
-                                X=torch.zeros((64, self.cfg.features.width), dtype=torch.float32, device=self.device),
-                                feat=torch.zeros((64, 32), dtype=torch.int32, device=self.device))
-            h = np.zeros(1, [("n", "<i4"), ("seq", "<i4"), ("now", "<i8")])
-            h["n"], h["now"] = 1, now
-            r = np.zeros(1, REQREC)
-            r["slot"], r["tx_type"], r["ts"] = slot, 255 | (self.scorer.rank << 8), now
-            buf = np.concatenate([h.view(np.uint8), r.view(np.uint8)])
+                self._fx = dict(slab=torch.zeros(16 + 48 * R, dtype=torch.uint8, device=self.device),
+                                X=torch.zeros((R, self.cfg.features.width), dtype=torch.float32, device=self.device),
+                                feat=torch.zeros((R, 32), dtype=torch.int32, device=self.device))
             fx = self._fx
-            with torch.cuda.stream(self.scorer.stream):
-                fx["slab"][:len(buf)].copy_(torch.from_numpy(buf))
-                K.feature_assemble(self.store, fx["slab"][:16].view(torch.int64), self.scorer.cfg_dev,
-                                   fx["slab"][16:16 + 48], fx["X"], fx["feat"], 1)
-            self.scorer.stream.synchronize()
-            return fx["feat"][0].cpu().numpy().view(FEATREC)[0]
+            for i in range(0, len(slots), R):
+                sl = slots[i:i + R]
+                n = len(sl)
+                h = np.zeros(1, [("n", "<i4"), ("seq", "<i4"), ("now", "<i8")])
+                h["n"], h["now"] = n, now
+                r = np.zeros(n, REQREC)
+                r["slot"], r["tx_type"], r["ts"] = sl, 255 | (self.scorer.rank << 8), now
+                buf = np.concatenate([h.view(np.uint8), r.view(np.uint8)])
+                bucket = 64 if n <= 64 else R
+                with torch.cuda.stream(self.scorer.stream):
+                    fx["slab"][:len(buf)].copy_(torch.from_numpy(buf))
+                    K.feature_assemble(self.store, fx["slab"][:16].view(torch.int64), self.scorer.cfg_dev,
+                                       fx["slab"][16:16 + 48 * bucket], fx["X"], fx["feat"], bucket)
+                    host = fx["feat"][:n].cpu()
+                out[i:i + n] = host.numpy().view(FEATREC).reshape(-1)
+        return out
 
     def event_history(self, slot: int) -> np.ndarray:
         """[event_ring, event_dim] f32, oldest first, right-aligned (GRU input)."""
@@ -551,6 +569,10 @@ class NativeCpuBackend:
     def features(self, slot: int, now: int) -> np.ndarray:
         self._sync()
         return self.sc.features(int(slot), int(now)).view(FEATREC)[0]
+
+    def features_many(self, slots, now: int) -> np.ndarray:
+        self._sync()
+        return np.array([self.sc.features(int(s), int(now)).view(FEATREC)[0] for s in slots], FEATREC).reshape(-1)
 
     def event_history(self, slot: int) -> np.ndarray:
         return self.sc.event_history(int(slot))

@@ -81,12 +81,16 @@ class PlayerTable:
             if ext is not None and self.ext[owner] is not None:
                 self.ext[owner][slots] = ext[:, : self.ext[owner].shape[1]]
 
-    def get(self, owner: int, slots: np.ndarray):
+    def get(self, owner: int, slots: np.ndarray, with_rows: bool = True):
+        """(rows, present, ext) of ``slots``; ``with_rows=False`` (GPU path: the device holds the
+        tables) returns only the presence mask."""
         with self.lock:
             ok = (slots >= 0)
             s = np.where(ok, slots, 0)
-            rows = self.rows[owner][s].copy()
             present = self.present[owner][s] & ok
+            if not with_rows:
+                return None, present, None
+            rows = self.rows[owner][s].copy()
             ext = self.ext[owner][s].copy() if self.ext[owner] is not None else None
         rows[~present] = 0
         return rows, present, ext
@@ -123,19 +127,29 @@ class LtvGpu:
         self.ext_w = max(self.w - N_COLS, 0) if plan is not None else 0
         self.ext_tab = torch.zeros((self.capacity, self.ext_w), dtype=torch.float32, device=dev) if self.ext_w else None
         self.X = torch.zeros((B, self.w), dtype=torch.float32, device=dev) if plan is not None else None
-        self.dev_slab = torch.zeros(16 + 4 * B, dtype=torch.uint8, device=dev)
-        self.n_ptr = self.dev_slab[:4].view(torch.int32)
-        self.slots = self.dev_slab[16:].view(torch.int32)
         self.depth = depth
         self.host = [torch.zeros(16 + 4 * B, dtype=torch.uint8).pin_memory() for _ in range(depth)]
         self.host_out = [torch.zeros((B, 6), dtype=torch.float32).pin_memory() for _ in range(depth)]
-        self.out = torch.zeros((B, 6), dtype=torch.float32, device=dev)
-        self.stream = torch.cuda.Stream(device=dev)
+        # the fused chain keeps no state between launches: each pipeline slot gets its own device
+        # buffers and stream, so batch i+1's H2D / kernel overlap batch i's kernel / D2H (the
+        # layer-kernel path shares the DeviceModel activations and stays on one stream)
+        n_bufs = depth if self.chain is not None else 1
+        self._slabs = [torch.zeros(16 + 4 * B, dtype=torch.uint8, device=dev) for _ in range(n_bufs)]
+        self._outs = [torch.zeros((B, 6), dtype=torch.float32, device=dev) for _ in range(n_bufs)]
+        self._streams = [torch.cuda.Stream(device=dev) for _ in range(n_bufs)]
+        self._use(0)
         self.graphs: Dict[tuple, object] = {}
         self._slot = 0
         self.use_graphs = use_graphs
         self._lock = threading.Lock()
         self._slot_locks = [threading.Lock() for _ in range(depth)]
+
+    def _use(self, slot: int) -> None:
+        """Point the step buffers at pipeline slot ``slot``'s (a no-op with one buffer set)."""
+        i = slot % len(self._slabs)
+        self.dev_slab, self.out, self.stream = self._slabs[i], self._outs[i], self._streams[i]
+        self.n_ptr = self.dev_slab[:4].view(self.torch.int32)
+        self.slots = self.dev_slab[16:].view(self.torch.int32)
 
     # ---- tables
     def set_rows(self, slots: np.ndarray, rows: np.ndarray, ext: Optional[np.ndarray] = None) -> None:
@@ -173,6 +187,7 @@ class LtvGpu:
         with torch.cuda.device(self.device):
             for b in self.buckets:
                 for slot in range(self.depth):
+                    self._use(slot)
                     self._pack(slot, np.zeros(0, np.int32), b)
                     s = self.stream  # capture on the replay stream: no extra streams / hardware queues
                     s.wait_stream(torch.cuda.current_stream())
@@ -207,6 +222,7 @@ class LtvGpu:
     def submit_packed(self, slot: int, n: int):
         torch = self.torch
         b = self.bucket_for(max(n, 1))
+        self._use(slot)
         with torch.cuda.stream(self.stream):
             g = self.graphs.get((b, slot))
             if g is not None:
@@ -266,18 +282,22 @@ class LtvService:
     def predict(self, account_ids: Sequence[str]) -> List[LtvResult]:
         slots, owners = self.registry.resolve_ids(list(account_ids), insert=False)
         out: List[Optional[LtvResult]] = [None] * len(account_ids)
+        nba = GL.NBA_CODES
         for o in np.unique(owners):
             sel = np.nonzero(owners == o)[0]
-            rows, present, ext = self.table.get(int(o), slots[sel])
+            rows, present, ext = self.table.get(int(o), slots[sel], with_rows=self.gpu is None)
             if self.gpu is not None:
                 res = self.gpu[int(o) % len(self.gpu)].predict_slots(np.where(present, slots[sel], -1))
             else:
                 X = ltv_model_input(rows, ext, self.model_width) if self.model_width else None
                 res = self._cpu(rows, X)
-            for k, i in enumerate(sel):
-                r = res[k]
-                out[i] = LtvResult(account_ids[i], float(r[0]), int(r[4]), float(r[1]), int(r[2]), float(r[3]),
-                                   GL.NBA_CODES[int(r[5])], found=bool(present[k]))
+            # columns -> Python scalars in bulk (tolist) before building the per-account results
+            ltv, churn, surv, conf = (res[:, c].astype(np.float64).tolist() for c in (0, 1, 2, 3))
+            seg, act = res[:, 4].astype(np.int64).tolist(), res[:, 5].astype(np.int64).tolist()
+            pres = present.tolist()
+            for k, i in enumerate(sel.tolist()):
+                out[i] = LtvResult(account_ids[i], ltv[k], seg[k], churn[k], int(surv[k]), conf[k], nba[act[k]],
+                                   found=pres[k])
         return out  # type: ignore[return-value]
 
     def _cpu(self, rows: np.ndarray, X: Optional[np.ndarray]) -> np.ndarray:

@@ -12,7 +12,7 @@ from typing import Sequence, Tuple
 import numpy as np
 
 from ..native import native
-from ..utils.hashing import SEED_ACCOUNT, id_hash
+from ..utils.hashing import SEED_ACCOUNT
 
 
 class AccountRegistry:
@@ -47,7 +47,11 @@ class AccountRegistry:
         return slots, owners, fresh
 
     def resolve_ids(self, ids: Sequence[str], insert: bool = False) -> Tuple[np.ndarray, np.ndarray]:
-        h = np.array([id_hash(i, SEED_ACCOUNT) for i in ids], np.uint64)
+        ids = list(ids)
+        if self.world == 1:  # digests and lookups in C++ (GIL released)
+            s, _ = self.index[0].lookup(ids, insert)
+            return np.asarray(s, np.int32), np.zeros(len(ids), np.int32)
+        h = native().id_hashes(ids, SEED_ACCOUNT)
         owners = self.owner_of_hash(h)
         slots = np.full(len(ids), -1, np.int32)
         for o in range(self.world):

@@ -538,11 +538,17 @@ class RiskEngine:
         return out
 
     def check_bonus_abuse(self, account_id: str, bonus_id: str = "", now: Optional[int] = None):
-        now = int(time.time()) if now is None else int(now)
-        return self.abuse.check([account_id], now)[0]
+        return self.check_bonus_abuse_batch([account_id], now)[0]
 
-    def linked_accounts(self, owner: int, slot: int, limit: int = 16) -> List[str]:
-        self._flush_links()
+    def check_bonus_abuse_batch(self, account_ids: Sequence[str], now: Optional[int] = None):
+        """CheckBonusAbuse for many accounts: one K1 feature read and one GRU launch per shard
+        (the gRPC layer's micro-batcher merges concurrent unary calls into one of these)."""
+        now = int(time.time()) if now is None else int(now)
+        return self.abuse.check(list(account_ids), now)
+
+    def linked_accounts(self, owner: int, slot: int, limit: int = 16, flush: bool = True) -> List[str]:
+        if flush:  # the inserts of batches scored so far
+            self._flush_links()
         keys = self.links.linked((int(owner) << 32) | int(slot), limit)
         return [self.registry.id_of(int(k) >> 32, int(k) & 0xFFFFFFFF) for k in keys]
 

@@ -475,9 +475,8 @@ class MlpChainPack:
             b = s.b1_np if s.kind == "head" else s.b_np
             n, k = w.shape
             kp = -(-k // 64) * 64
-            buf = np.zeros((n, kp), np.float32)
-            buf[:, :k] = w
-            self.layers.append(dict(W=torch.from_numpy(buf).to(torch.bfloat16).to(dev),
+            # MFMA B-fragment order (pack_fragments): one 1 KB contiguous wave load per 16x32 tile
+            self.layers.append(dict(W=pack_fragments(w, kp).to(dev),
                                     b=None if b is None else torch.from_numpy(np.ascontiguousarray(b, np.float32)).to(dev),
                                     N=n, K=kp, act=ACT[s.act1 if s.kind == "head" else s.act]))
         head = steps[-1]
@@ -486,6 +485,11 @@ class MlpChainPack:
         self.in_live = steps[0].k
         self.in_w = self.layers[0]["K"]
         self.device = dev
+
+    def waves(self) -> int:
+        """Waves per workgroup: 8 needs every layer width to be a multiple of 128."""
+        w = int(os.environ.get("IGP_MLP_WAVES", "8"))  # 8: +11 % cfg4 over 4 (same-box A/B, NOTES.md)
+        return w if all(l["N"] % (16 * w) == 0 for l in self.layers) else 4
 
 
 def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, slots: Optional[torch.Tensor] = None,
@@ -497,6 +501,7 @@ def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, s
     [rows] and/or the K9 rows ``ltv_out`` [rows, 6]."""
     dev = pk.device
     d = dict(n_rows=int(n_rows), n_layers=len(pk.layers), in_w=pk.in_w, in_live=pk.in_live,
+             rows_per_block=int(os.environ.get("IGP_MLP_ROWS", "32")), waves=pk.waves(),
              m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32, device=dev), w2=_need(pk.w2, "w2", torch.float32, device=dev),
              b2=pk.b2, act2=pk.act2,
              ml=_opt(ml, "ml", dtype=torch.float32, min_numel=n_rows, device=dev),

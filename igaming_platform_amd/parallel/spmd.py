@@ -27,7 +27,7 @@ from ..config import RuleWeights, ScoringConfig
 from ..layouts import ACCTBATCH, FEATREC, REQREC
 
 OP_SCORE, OP_INGEST, OP_CONFIG, OP_TABLES, OP_BATCH, OP_EXT, OP_FEATURES, OP_RESET, OP_STOP, OP_EVHIST, \
-    OP_ABUSE, OP_SNAPSHOT, OP_RESTORE, OP_RELOAD = range(1, 15)
+    OP_ABUSE, OP_SNAPSHOT, OP_RESTORE, OP_RELOAD, OP_FEATMANY = range(1, 16)
 
 
 def owners_of(req: np.ndarray) -> np.ndarray:
@@ -139,6 +139,14 @@ class ShardRunner:
             if aux == self.rank:
                 rec[0] = self.be.features(aux2, now)
             return self.comm.sum_i64(rec.view(np.int64).reshape(-1))
+        if op == OP_FEATMANY:  # payload: slots | owners; each rank fills the rows it owns
+            slots = np.frombuffer(payload[:4 * n], np.int32)
+            owners = np.frombuffer(payload[4 * n:8 * n], np.int32)
+            recs = np.zeros(n, FEATREC)
+            mine = self._mine(owners)
+            if np.any(mine):
+                recs[mine] = self.be.features_many(slots[mine], now)
+            return self.comm.sum_i64(recs.view(np.int64).reshape(-1))
         if op == OP_EVHIST:
             h = None
             if aux == self.rank:
@@ -252,6 +260,12 @@ class SpmdGroup:
     def features(self, owner: int, slot: int, now: int) -> np.ndarray:
         return self._issue(OP_FEATURES, now=now, aux=owner, aux2=slot).view(FEATREC)[0].copy()
 
+    def features_many(self, slots, owners, now: int) -> np.ndarray:
+        n = len(slots)
+        out = self._issue(OP_FEATMANY, np.asarray(slots, np.int32).tobytes() + np.asarray(owners, np.int32).tobytes(),
+                          n=n, now=now)
+        return out.view(FEATREC).reshape(-1)[:n].copy()
+
     def event_history(self, owner: int, slot: int, shape) -> np.ndarray:
         out = self._issue(OP_EVHIST, aux=owner, aux2=slot, extra=shape)
         return out.view(np.float32)[: shape[0] * shape[1]].reshape(shape).copy()
@@ -320,6 +334,9 @@ class ShardProxy:
 
     def features(self, slot: int, now: int) -> np.ndarray:
         return self.g.features(self.o, int(slot), now)
+
+    def features_many(self, slots, now: int) -> np.ndarray:
+        return self.g.features_many(slots, np.full(len(slots), self.o, np.int32), now)
 
     def event_history(self, slot: int) -> np.ndarray:
         shape = self.local.event_history(0).shape

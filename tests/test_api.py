@@ -90,6 +90,27 @@ def test_ltv_segment_abuse(stack):
     assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
 
 
+def test_concurrent_cold_rpcs_are_micro_batched(stack):
+    """PredictLTV / GetPlayerSegment / CheckBonusAbuse calls in flight together merge into one
+    batched engine call (one LTV launch / one feature read + GRU launch per shard), and each
+    caller still gets its own account's answer."""
+    from concurrent.futures import ThreadPoolExecutor
+    eng, gs, _, cli = stack
+    ids = [f"cold-{i}" for i in range(48)]
+    eng.set_players(ids, [GL.PlayerFeatures(days_since_registration=10 + i, net_revenue=50 * i) for i in range(48)])
+    want_ltv = {i: eng.predict_ltv(i).predicted_ltv for i in ids}
+    lb, ab = gs.ltv_batcher.batches, gs.abuse_batcher.batches
+    with ThreadPoolExecutor(48) as ex:
+        ltv = list(ex.map(lambda i: cli.predict_ltv(i), ids))
+        seg = list(ex.map(lambda i: cli.player_segment(i), ids))
+        abu = list(ex.map(lambda i: cli.check_bonus_abuse(i), ids))
+    assert [r.account_id for r in ltv] == ids and [r.account_id for r in seg] == ids
+    assert all(r.predicted_ltv == pytest.approx(want_ltv[i], rel=1e-6) for r, i in zip(ltv, ids))
+    assert all(not r.is_abuser for r in abu)
+    assert gs.ltv_batcher.items >= 96 and gs.abuse_batcher.items >= 48
+    assert gs.ltv_batcher.batches - lb < 96 and gs.abuse_batcher.batches - ab < 48
+
+
 def test_blacklist_rpcs(stack):
     eng, gs, hs, cli = stack
     r = cli.add_to_blacklist("device", "bad-dev", "chargeback", "analyst")

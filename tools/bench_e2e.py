@@ -63,6 +63,50 @@ def tx_payloads(n_accounts: int, n: int, seed: int):
             for a in rng.integers(0, n_accounts, n)]
 
 
+def build_cold_engine(accounts: int, backend: str):
+    """Engine with the cfg 4 LTV MLP and the cfg 5 abuse GRU loaded, player profiles for every
+    account (PredictLTV / GetPlayerSegment / CheckBonusAbuse benches)."""
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.engine.risk_engine import RiskEngine
+    from igaming_platform_amd.onnx import builders
+    cfg = Config()
+    cfg.gpu.buckets = [64, 512, 4096]
+    cfg.gpu.max_batch = 4096
+    eng = RiskEngine(cfg, backend=backend, capacity=accounts + 1024,
+                     ltv_model=builders.build("ltv_mlp", n_features=256, width=512, layers=4).SerializeToString(),
+                     abuse_model=builders.build("gru", seq=100, in_dim=16, hidden=256).SerializeToString())
+    rng = np.random.default_rng(5)
+    ids = [account_id(i) for i in range(accounts)]
+    slots, owners = eng.registry.resolve_ids(ids, insert=True)
+    rows = np.floor(rng.uniform(0, 1, (accounts, 25)) * np.array(
+        [900, 90, 60, 500, 10, 120, 1e5, 8e4, 3e4, 500, 8, 5e3, 2e5, 1.8e5, 3000, 1, 80, 60, 20, 15, 1, 1, 1, 1, 8]))
+    eng.ltv.set_rows(slots, owners, rows.astype(np.float32), rng.normal(0, 1, (accounts, 231)).astype(np.float32))
+    return eng
+
+
+def run_cold_engine(a) -> dict:
+    """The batched engine calls behind the micro-batched cold RPCs, in-process (4096 accounts each)."""
+    eng = build_cold_engine(a.accounts, a.backend)
+    rng = np.random.default_rng(9)
+    fn = eng.predict_ltv_batch if a.rpc == "ltv" else eng.check_bonus_abuse_batch
+    batches = [[account_id(int(i)) for i in rng.integers(0, a.accounts, 4096)] for _ in range(4)]
+    for i in range(3):
+        fn(batches[i % 4])
+    lat = []
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        t = time.perf_counter()
+        fn(batches[i % 4])
+        lat.append((time.perf_counter() - t) * 1e3)
+    el = time.perf_counter() - t0
+    eng.close()
+    return dict(metric=f"{'PredictLTV' if a.rpc == 'ltv' else 'CheckBonusAbuse'} answers/sec (batched engine call, "
+                       f"4096 accounts, in-process)", value=a.steps * 4096 / el, unit="answers/s",
+                scope="engine_batched", n_gpus=1 if a.backend == "gpu" else 0, steps=a.steps,
+                data="synthetic (UUID ids, random-init cfg4 / cfg5 weights)",
+                p50_latency_ms=float(np.percentile(lat, 50)), p99_latency_ms=float(np.percentile(lat, 99)))
+
+
 def build_engine(accounts: int, batch: int, backend: str):
     from igaming_platform_amd.config import Config
     from igaming_platform_amd.engine.risk_engine import RiskEngine
@@ -134,6 +178,12 @@ def _client(i, port, kind, accounts, batch, n_payloads, t_start, t_end, q):
         call = ch.unary_unary(P.method_path("ScoreBatch"))
         payloads = make_payloads(accounts, n_payloads, batch, seed=100 + i)
         per = batch
+    elif kind in ("ltv", "abuse"):
+        rpc, req = (("PredictLTV", P.PredictLTVRequest) if kind == "ltv" else ("CheckBonusAbuse", P.CheckBonusAbuseRequest))
+        call = ch.unary_unary(P.method_path(rpc))
+        rng = np.random.default_rng(100 + i)
+        payloads = [req(account_id=account_id(int(x))).SerializeToString() for x in rng.integers(0, accounts, 4096)]
+        per = 1
     else:
         call = ch.unary_unary(P.method_path("ScoreTransaction"))
         payloads = tx_payloads(accounts, 4096, seed=100 + i)
@@ -160,13 +210,14 @@ def _client(i, port, kind, accounts, batch, n_payloads, t_start, t_end, q):
 def run_grpc(a) -> dict:
     import multiprocessing as mp
     from igaming_platform_amd.api.grpc_server import RiskServer
-    eng = build_engine(a.accounts, a.batch, a.backend)
-    srv = RiskServer(eng, port=0, batching=a.rpc == "tx", workers=16).start()
+    cold = a.rpc in ("ltv", "abuse")
+    eng = build_cold_engine(a.accounts, a.backend) if cold else build_engine(a.accounts, a.batch, a.backend)
+    srv = RiskServer(eng, port=0, batching=a.rpc != "batch", workers=16).start()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     lead = 25.0  # client start-up (import + payload generation) happens before the window
     t_end = time.time() + lead + a.seconds
-    procs = [ctx.Process(target=_client, args=(i, srv.port, "batch" if a.rpc == "batch" else "tx", a.accounts,
+    procs = [ctx.Process(target=_client, args=(i, srv.port, a.rpc, a.accounts,
                                                a.batch, 4, t_end - a.seconds, t_end, q))
              for i in range(a.clients)]
     [p.start() for p in procs]
@@ -177,11 +228,18 @@ def run_grpc(a) -> dict:
     lat = [x for r in res for x in r[0]]
     per = res[0][2]
     calls = len(lat)
-    return dict(metric=("fraud scores/sec (risk.v1.ScoreBatch over gRPC)" if a.rpc == "batch" else
-                        "fraud scores/sec (unary risk.v1.ScoreTransaction over gRPC, micro-batched)"),
+    names = {"batch": "fraud scores/sec (risk.v1.ScoreBatch over gRPC)",
+             "tx": "fraud scores/sec (unary risk.v1.ScoreTransaction over gRPC, micro-batched)",
+             "ltv": "PredictLTV answers/sec (unary over gRPC, micro-batched)",
+             "abuse": "CheckBonusAbuse answers/sec (unary over gRPC, micro-batched)"}
+    batcher = {"tx": srv.batcher, "ltv": srv.ltv_batcher, "abuse": srv.abuse_batcher}.get(a.rpc)
+    mean_batch = (batcher.items / max(batcher.batches, 1)) if batcher is not None else None
+    return dict(metric=names[a.rpc], mean_device_batch=mean_batch,
                 value=calls * per / a.seconds, unit="scores/s", scope="grpc", n_gpus=1 if a.backend == "gpu" else 0,
-                higher_is_better=True, dtype="fp32", data="synthetic (UUID ids, random-init cfg3 weights)",
-                config=dict(model="cfg3 GBDT(100,d7,128f)+MLP(32-256-1)", rpc=a.rpc, clients=a.clients,
+                higher_is_better=True, dtype="fp32", data="synthetic (UUID ids, random-init weights)",
+                config=dict(model={"ltv": "cfg4 LTV MLP 4x512 (bf16) + K9", "abuse": "cfg5 GRU 2x256 over 100 events"
+                                   " + rule signals"}.get(a.rpc, "cfg3 GBDT(100,d7,128f)+MLP(32-256-1)"),
+                            rpc=a.rpc, clients=a.clients,
                             seconds=a.seconds, transactions_per_call=per, accounts=a.accounts,
                             server="grpc.aio, raw-bytes handlers, C++ codec"
                                    + (", MicroBatcher" if a.rpc == "tx" else "")),
@@ -193,8 +251,8 @@ def run_grpc(a) -> dict:
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--scope", default="e2e", choices=["e2e", "grpc"])
-    ap.add_argument("--rpc", default="batch", choices=["batch", "tx"])
+    ap.add_argument("--scope", default="e2e", choices=["e2e", "grpc", "engine_batched"])
+    ap.add_argument("--rpc", default="batch", choices=["batch", "tx", "ltv", "abuse"])
     ap.add_argument("--backend", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--accounts", type=int, default=1 << 20)
     ap.add_argument("--batch", type=int, default=8192)
@@ -207,7 +265,7 @@ def main(argv=None) -> int:
     ap.add_argument("--json-out", default="")
     a = ap.parse_args(argv)
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-    out = run_e2e(a) if a.scope == "e2e" else run_grpc(a)
+    out = {"e2e": run_e2e, "grpc": run_grpc, "engine_batched": run_cold_engine}[a.scope](a)
     line = json.dumps(out)
     print(line, flush=True)
     if a.json_out:
