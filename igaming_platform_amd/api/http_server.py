@@ -3,8 +3,9 @@
 ``/debug/thresholds`` (the LIVE thresholds — the reference reports the static env config,
 quirk Q7), ``/debug/score`` (``ScoreWithExplanation``; a stub in the reference),
 ``POST /admin/reload_model`` (model hot-reload), ``POST /admin/flush_audit``
-(drain the risk_scores audit ring into ``server.audit_db``), plus
-``/debug/features`` and ``/debug/engine``."""
+(drain the risk_scores audit ring into ``server.audit_db``), plus ``/debug/features``,
+``/debug/velocity`` (GetVelocity + CheckRateLimit), ``/debug/feature_importance`` and
+``/debug/engine``."""
 from __future__ import annotations
 
 import json
@@ -84,6 +85,15 @@ def make_handler(engine):
                         return self._send(400, "account_id is required")
                     f = engine.get_features(q["account_id"])
                     self._send(200, json.dumps({k: f[k].item() for k in FEATREC.names}), "application/json")
+                elif u.path == "/debug/velocity":  # GetVelocity + CheckRateLimit (redis_store.go:171-203)
+                    if not q.get("account_id"):
+                        return self._send(400, "account_id is required")
+                    c1, c5, ch = engine.get_velocity(q["account_id"])
+                    lim = engine.check_rate_limit(q["account_id"], q.get("max_per_min"), q.get("max_per_hour"))
+                    self._send(200, json.dumps({"count_1m": c1, "count_5m": c5, "count_1h": ch, "rate_limited": lim}),
+                               "application/json")
+                elif u.path == "/debug/feature_importance":
+                    self._send(200, json.dumps(engine.get_feature_importance()), "application/json")
                 elif u.path == "/debug/engine":
                     self._send(200, json.dumps(engine.health()), "application/json")
                 else:

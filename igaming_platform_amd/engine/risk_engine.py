@@ -18,7 +18,7 @@ import json
 import os
 import threading
 import time
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -103,6 +103,8 @@ class RiskEngine:
         self.scoring = cfg.scoring
         # risk_scores / ltv_predictions audit (engine/audit.py): on when AUDIT_DB is configured
         self.auditlog = AuditLog(enabled=bool(cfg.server.audit_db))
+        from ..features.store_ops import KVStore
+        self.kv = KVStore()  # IncrementCounter / SetFeature / GetFeature keys (redis_store.go:206-227)
 
         # ---- models
         fm = _load_onnx(fraud_model if fraud_model is not None else cfg.fraud_model.path)
@@ -518,12 +520,71 @@ class RiskEngine:
                 self.backends[o].set_ext(slots[sel], ext[sel])
 
     def delete_account_features(self, account_ids: Sequence[str]) -> None:
-        """``DeleteAccountFeatures`` (redis_store.go:230-240)."""
+        """``DeleteAccountFeatures`` (redis_store.go:230-240): the shard state and the account's
+        named features."""
+        from ..features.store_ops import feature_key
+        for a in account_ids:
+            self.kv.delete_prefix(feature_key(a, ""))
         slots, owners = self.registry.resolve_ids(list(account_ids), insert=False)
         for o in range(self.world):
             sel = np.nonzero((owners == o) & (slots >= 0))[0]
             if len(sel):
                 self.backends[o].reset_accounts(slots[sel])
+
+    # ---- feature-store auxiliary operations (redis_store.go:171-240) and feature importance
+    def get_velocity_batch(self, account_ids: Sequence[str], now: Optional[int] = None) -> np.ndarray:
+        """``GetVelocity`` for many accounts: int32 [n, 3] = (count_1m, count_5m, count_1h), one
+        feature read (K1 launch on a GPU shard) per shard; unknown accounts count 0."""
+        now = int(time.time()) if now is None else int(now)
+        slots, owners = self.registry.resolve_ids(list(account_ids), insert=False)
+        out = np.zeros((len(slots), 3), np.int32)
+        for o in np.unique(owners):
+            sel = np.nonzero((owners == o) & (slots >= 0))[0]
+            if len(sel):
+                f = self.backends[int(o)].features_many(slots[sel], now)
+                out[sel] = np.stack([f["tx_count_1m"], f["tx_count_5m"], f["tx_count_1h"]], 1)
+        return out
+
+    def get_velocity(self, account_id: str, now: Optional[int] = None) -> Tuple[int, int, int]:
+        c = self.get_velocity_batch([account_id], now)[0]
+        return int(c[0]), int(c[1]), int(c[2])
+
+    def check_rate_limit_batch(self, account_ids: Sequence[str], max_per_min: Optional[int] = None,
+                               max_per_hour: Optional[int] = None, now: Optional[int] = None) -> np.ndarray:
+        """``CheckRateLimit``: count_1m >= max_per_min or count_1h >= max_per_hour (defaults: the
+        live MaxTxPerMinute / MaxTxPerHour)."""
+        s = self.scoring
+        mpm = s.max_tx_per_minute if max_per_min is None else int(max_per_min)
+        mph = s.max_tx_per_hour if max_per_hour is None else int(max_per_hour)
+        v = self.get_velocity_batch(account_ids, now)
+        return (v[:, 0] >= mpm) | (v[:, 2] >= mph)
+
+    def check_rate_limit(self, account_id: str, max_per_min: Optional[int] = None,
+                         max_per_hour: Optional[int] = None, now: Optional[int] = None) -> bool:
+        return bool(self.check_rate_limit_batch([account_id], max_per_min, max_per_hour, now)[0])
+
+    def increment_counter(self, key: str, ttl_s: float, now: Optional[float] = None) -> int:
+        """``IncrementCounter``: INCR + EXPIRE of a named counter."""
+        return self.kv.incr(key, ttl_s, now)
+
+    def set_feature(self, account_id: str, feature: str, value, ttl_s: float = 0.0,
+                    now: Optional[float] = None) -> None:
+        """``SetFeature``: an account-scoped named value with a TTL."""
+        from ..features.store_ops import feature_key
+        self.kv.set(feature_key(account_id, feature), value, ttl_s, now)
+
+    def get_feature(self, account_id: str, feature: str, now: Optional[float] = None) -> Optional[str]:
+        """``GetFeature``: the value or None (Redis nil) when absent / expired."""
+        from ..features.store_ops import feature_key
+        return self.kv.get(feature_key(account_id, feature), now)
+
+    def get_feature_importance(self) -> Dict[str, float]:
+        """``GetFeatureImportance`` (onnx_model.go:329-345) of the loaded fraud model."""
+        from ..features.store_ops import STATIC_IMPORTANCE, plan_importance
+        if self.model_kind != "onnx" or self.fraud_onnx is None:
+            return dict(STATIC_IMPORTANCE)
+        from ..models.plan import compile_onnx
+        return plan_importance(compile_onnx(self.fraud_onnx), self.cfg.features.width)
 
     # ---- LTV / segment / abuse
     def set_players(self, account_ids, features, ext=None) -> None:

@@ -410,3 +410,44 @@ def test_audit_disabled_without_audit_db():
     eng = RiskEngine(Config(), backend="cpu", capacity=20)
     eng.score(_txs(3, np.random.default_rng(1)))
     assert eng.auditlog.pending() == 0
+
+
+def test_velocity_rate_limit_counters_and_features():
+    """GetVelocity / CheckRateLimit / IncrementCounter / Set+GetFeature / DeleteAccountFeatures
+    (redis_store.go:171-240)."""
+    eng = RiskEngine(Config(), backend="cpu", capacity=50)
+    evs = [dict(account_id="v1", amount=100, transaction_type="bet", ts=NOW - d) for d in (30, 100, 1000, 4000, 59)]
+    eng.ingest_events(evs)
+    assert eng.get_velocity("v1", now=NOW) == (2, 3, 4)          # 30 s, 59 s | +100 s | +1000 s (4000 s: out)
+    assert eng.get_velocity("nobody", now=NOW) == (0, 0, 0)
+    assert eng.check_rate_limit("v1", max_per_min=2, max_per_hour=100, now=NOW)
+    assert not eng.check_rate_limit("v1", max_per_min=3, max_per_hour=5, now=NOW)
+    assert eng.check_rate_limit("v1", max_per_min=3, max_per_hour=4, now=NOW)
+    eng.set_scoring(max_tx_per_minute=10, max_tx_per_hour=4)   # defaults: the live config
+    assert list(eng.check_rate_limit_batch(["v1", "nobody"], now=NOW)) == [True, False]
+    assert eng.increment_counter("bonus:claims:v1", 60, now=NOW) == 1
+    assert eng.increment_counter("bonus:claims:v1", 60, now=NOW + 10) == 2
+    assert eng.increment_counter("bonus:claims:v1", 60, now=NOW + 71) == 1  # expired 60 s after the last INCR
+    eng.set_feature("v1", "kyc_level", 3, ttl_s=100, now=NOW)
+    assert eng.get_feature("v1", "kyc_level", now=NOW + 50) == "3"
+    assert eng.get_feature("v1", "kyc_level", now=NOW + 101) is None
+    eng.set_feature("v1", "vip", "gold", now=NOW)
+    eng.delete_account_features(["v1"])
+    assert eng.get_feature("v1", "vip", now=NOW) is None
+    assert eng.get_velocity("v1", now=NOW) == (0, 0, 0)
+
+
+def test_feature_importance_from_the_loaded_model():
+    from igaming_platform_amd.features.store_ops import STATIC_IMPORTANCE
+    from igaming_platform_amd.onnx import builders
+    assert RiskEngine(Config(), backend="cpu", capacity=10).get_feature_importance() == STATIC_IMPORTANCE
+    cfg = Config()
+    cfg.features.width = 128
+    imp = RiskEngine(cfg, backend="cpu", capacity=10,
+                     fraud_model=builders.build("stacked", n_trees=20, depth=4).SerializeToString()).get_feature_importance()
+    assert imp and abs(sum(imp.values()) - 1) < 1e-9 and all(v > 0 for v in imp.values())
+    assert list(imp.values()) == sorted(imp.values(), reverse=True)
+    assert set(imp) <= set(__import__("igaming_platform_amd.features.store_ops", fromlist=["x"]).input_names(128))
+    lg = RiskEngine(Config(), backend="cpu", capacity=10,
+                    fraud_model=builders.build("logistic", n_features=30).SerializeToString()).get_feature_importance()
+    assert len(lg) == 30 and "tx_count_1m" in lg

@@ -214,3 +214,22 @@ def test_gpu_model_hot_reload():
         fa, fb = a.get_features(f"acc-{i}", now=NOW + 30), b.get_features(f"acc-{i}", now=NOW + 30)
         diff = [k for k in fa.dtype.names if fa[k] != fb[k]]
         assert not diff, (i, [(k, fa[k], fb[k]) for k in diff])
+
+
+def test_gpu_velocity_rate_limit_and_batched_features_match_cpu():
+    """GetVelocity / CheckRateLimit / batched feature reads: one K1 launch over many accounts on
+    the GPU shard, equal to the CPU engine's per-account values."""
+    g, c = _engines()
+    rng = np.random.default_rng(4)
+    for step in range(3):
+        txs = _txs(300, rng)
+        g.score(txs, now=NOW + step * 40)
+        c.score(txs, now=NOW + step * 40)
+    ids = [f"acc-{i}" for i in range(40)] + ["nobody"]
+    np.testing.assert_array_equal(g.get_velocity_batch(ids, now=NOW + 130), c.get_velocity_batch(ids, now=NOW + 130))
+    assert list(g.check_rate_limit_batch(ids, 5, 20, now=NOW + 130)) == list(c.check_rate_limit_batch(ids, 5, 20, now=NOW + 130))
+    slots, _ = g.registry.resolve_ids(ids[:40])
+    fg = g.backends[0].features_many(slots, NOW + 130)
+    for i, s in enumerate(slots):
+        one = g.backends[0].features(int(s), NOW + 130)
+        assert fg[i].tobytes() == one.tobytes()
