@@ -81,6 +81,7 @@ void check(const char* what) {
 namespace igp {
 void register_driver(py::module_& m);
 void register_exchange(py::module_& m);
+void register_watch(py::module_& m);
 }
 
 PYBIND11_MODULE(_hipk, m) {
@@ -95,6 +96,7 @@ PYBIND11_MODULE(_hipk, m) {
   m.attr("DEDUP_REGIONS") = DEDUP_RING + 1;
   igp::register_driver(m);
   igp::register_exchange(m);
+  igp::register_watch(m);
 
   m.def("feature_assemble", [](py::dict d, uintptr_t s) {
     AssembleArgs a{};

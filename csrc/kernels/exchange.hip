@@ -194,6 +194,7 @@ class RcclComm {
   // 0 = healthy; otherwise the ncclResult_t of an asynchronous failure (a peer died)
   int async_error() const {
     int e = 0;
+    if (!comm_) return 0;
     (void)r_.async_error(comm_, &e);
     return e;
   }
@@ -357,6 +358,8 @@ class XchgDriver {
   }
   // last submitted batch's state-stream event (snapshot ordering)
   uintptr_t state_event(int slot) const { return reinterpret_cast<uintptr_t>(ev_[6 * slot + 3]); }
+  // the slot's completion event (the watchdog's deadline wait, watch.hip)
+  uintptr_t done_event(int slot) const { return reinterpret_cast<uintptr_t>(E(slot, 5)); }
 
   py::dict stats() {
     py::dict d;
@@ -440,6 +443,7 @@ void register_exchange(py::module_& m) {
       .def("wait", &XchgDriver::wait)
       .def("query", &XchgDriver::query)
       .def("state_event", &XchgDriver::state_event)
+      .def("done_event", &XchgDriver::done_event)
       .def("stats", &XchgDriver::stats);
   // kernel launches (captured into the exchange graphs from Python)
   m.def("exchange_compact", [](uintptr_t recv, uintptr_t rows, uintptr_t hdr, uintptr_t route, int N, int C, int cap,

@@ -133,6 +133,14 @@ class GPUConfig:
     use_graphs: bool = True
     fallback: str = "cpu"        # on GPU fault: cpu | fail
     batch_timeout_ms: int = 2000  # watchdog: a device batch slower than this marks the shard unhealthy
+    # failure handling (engine/risk_engine.py): a quarantined shard whose late batches drained
+    # returns to service; one still unhealthy after rehome_after_s (or any remote shard of a
+    # failed SPMD group) is rebuilt on a surviving device from snapshot_dir
+    auto_recover: bool = True
+    rehome_after_s: float = 30.0
+    rehome_grace_s: float = 5.0   # SPMD: wait this long for survivors' final snapshots
+    snapshot_dir: str = ""        # where snapshots are written / re-homed shards restore from
+    spmd_heartbeat_s: float = 2.0  # SPMD liveness op period (0: off)
 
 
 @dataclass
@@ -213,6 +221,8 @@ class Config:
         self.gpu.devices = geti("RISK_GPUS", self.gpu.devices)
         self.gpu.max_batch = geti("RISK_MAX_BATCH", self.gpu.max_batch)
         self.gpu.wait_us = geti("RISK_BATCH_WAIT_US", self.gpu.wait_us)
+        self.gpu.batch_timeout_ms = geti("RISK_BATCH_TIMEOUT_MS", self.gpu.batch_timeout_ms)
+        self.gpu.snapshot_dir = env.get("RISK_SNAPSHOT_DIR", self.gpu.snapshot_dir) or self.gpu.snapshot_dir
         lt = env.get("RISK_LOG_TRANSFORM")
         if lt:
             self.features.log_transform = lt

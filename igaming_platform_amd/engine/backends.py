@@ -264,6 +264,10 @@ class CpuBackend:
         return len(data["accounts"])
 
 
+class BatchTimeout(TimeoutError):
+    """A device batch overran the watchdog deadline (its slot is quarantined until it drains)."""
+
+
 class GpuBackend:
     """One GPU shard: HBM feature store + captured-graph scorer."""
 
@@ -295,6 +299,10 @@ class GpuBackend:
         self._lock = threading.RLock()
         self._slot_locks = [threading.Lock() for _ in range(self.scorer.depth)]
         self._fx = None
+        self._watch = None               # EventWatch (csrc/kernels/watch.hip), made on first use
+        self.quarantined: set = set()    # slots whose batch overran its deadline, not yet drained
+        self.on_drained = None           # callback(backend) once every quarantined slot drained
+        self.timeouts = 0
 
     def swap_model(self, fm, mkind: str) -> None:
         """Model hot-reload: drain the shard, build a scorer for the new plan on the same HBM
@@ -333,10 +341,11 @@ class GpuBackend:
                          owner_filter=self.owner_filter, rank=self.rank, use_graphs=use_graphs)
 
     def exchange_score(self, req: Optional[np.ndarray], owners: Optional[np.ndarray], C: int, now: int,
-                       want_features: bool) -> Result:
+                       want_features: bool, timeout_s: Optional[float] = None) -> Result:
         """One owner-routed exchange step (collective over the group): this rank's ingress
         rows (None on a non-ingress rank) go to their owners; this GPU scores the rows it
-        owns; returns the ingress rows' (res, feats) in request order."""
+        owns; returns the ingress rows' (res, feats) in request order. ``timeout_s``: the
+        step's deadline (past it the RCCL communicators are aborted, TimeoutError)."""
         sc = self.scorer
         with self._lock:
             slot = sc.next_slot()
@@ -347,7 +356,7 @@ class GpuBackend:
                     p = sc.submit_chunks(slot, C, now, None, want_features)
                 else:
                     p = sc.submit_rows(slot, req, owners, now, want_features, C=C)
-            res, feats = sc.wait_x(p)
+            res, feats = sc.wait_x(p, timeout_s=timeout_s)
         finally:
             self._slot_locks[slot].release()
         if req is None:
@@ -407,24 +416,87 @@ class GpuBackend:
         return pend
 
     def collect(self, pend, timeout_s: Optional[float] = None) -> Result:
+        """Results of :meth:`submit`'s batches. ``timeout_s``: the watchdog deadline per batch,
+        an event wait (no polling). A batch that overruns it is quarantined with every batch
+        behind it: their slots stay locked (never reused) until a drain thread has seen them
+        complete, then ``on_drained`` fires; the caller gets :class:`BatchTimeout`."""
         res, feats = [], []
+        release = list(pend)
         try:
-            for p in pend:
-                if timeout_s is not None:
-                    t_end = time.perf_counter() + timeout_s
-                    while not self.scorer.done(p):
-                        if time.perf_counter() > t_end:
-                            raise TimeoutError(f"GPU batch exceeded {timeout_s * 1e3:.0f} ms on {self.device}")
-                        time.sleep(20e-6)
+            for i, p in enumerate(pend):
+                if timeout_s is not None and not self.scorer.done(p):
+                    if self._watch is None:
+                        from ..native import hipk
+                        self._watch = hipk().EventWatch()
+                    if not self._watch.wait_for(self.scorer.done_event(p), timeout_s * 1e3):
+                        release = list(pend[:i])
+                        self._quarantine(list(pend[i:]))
+                        raise BatchTimeout(f"GPU batch exceeded {timeout_s * 1e3:.0f} ms on {self.device}")
                 r, f = self.scorer.wait(p, unpack=False)
                 res.append(r.view(np.uint32).reshape(-1, 2))
                 if f is not None:
                     feats.append(f.view(FEATREC).reshape(-1))
         finally:
-            for p in pend:
+            for p in release:
                 self._slot_locks[p.slot].release()
         want = bool(pend) and pend[0].want_features
         return np.concatenate(res), (np.concatenate(feats) if want else None)
+
+    def stall(self, ms: float) -> None:
+        """Fault injection: queue a ``ms`` device stall on the copy stream (ahead of the next
+        batch's graphs)."""
+        from ..native import hipk
+        hipk().stall(self.scorer.cstream.cuda_stream, float(ms) * 1e3)
+
+    def _quarantine(self, pend) -> None:
+        """Keep the overrunning batches' slots out of service and drain them on a thread that
+        blocks (GIL released) until the device finishes them; a batch that never finishes
+        keeps its slot quarantined (the engine re-homes the shard after ``rehome_after_s``)."""
+        with self._lock:
+            self.timeouts += 1
+            self.quarantined.update(p.slot for p in pend)
+        sc = self.scorer
+
+        def drain():
+            for p in pend:
+                try:
+                    sc.wait(p, unpack=False)
+                except Exception:  # device error: the slot stays quarantined
+                    return
+                with self._lock:
+                    self.quarantined.discard(p.slot)
+                self._slot_locks[p.slot].release()
+            cb = self.on_drained
+            if cb is not None and not self.quarantined:
+                cb(self)
+        threading.Thread(target=drain, daemon=True, name=f"gpu-drain-{self.device}").start()
+
+    def leave_exchange(self, timeout_s: float = 5.0) -> None:
+        """Failover (rank 0 of a failed SPMD group): abort the RCCL exchange and serve this
+        shard through the plain single-GPU pipeline on the same HBM store (new scorer and
+        graphs; batch sequence and metrics carried over)."""
+        if self.exchange is None:
+            return
+        torch = self.torch
+        old = self.scorer
+        with self._lock:
+            old.abort_exchange()
+            ev = torch.cuda.Event()
+            ev.record(old.mstream)
+            from ..native import hipk
+            if not hipk().EventWatch().wait_for(int(ev.cuda_event), timeout_s * 1e3):
+                raise TimeoutError("the exchange streams did not drain after the abort")
+            torch.cuda.synchronize(self.device)
+            self.exchange = None
+            sc = self._make_scorer(old.plan, old.model, 2, use_graphs=old.use_graphs)
+            sc._seq = old._seq
+            sc.metrics = old.metrics
+            sc.refresh_config(getattr(old, "scoring", None))
+            if sc.use_graphs:
+                sc.capture()
+            torch.cuda.synchronize(self.device)
+            self._slot_locks = [threading.Lock() for _ in range(sc.depth)]
+            self.scorer = sc
 
     def score(self, req: np.ndarray, now: Optional[int] = None, want_features: bool = True,
               update: bool = True) -> Result:

@@ -91,6 +91,7 @@ class DpGpuScorer(GpuScorer):
             self.xstream, self.ystream = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
         self.xgraphs = {}
         self.xdriver = None
+        self._watch = None
 
     # ------------------------------------------------------------------ graph bodies
     def cap(self, C: int) -> int:
@@ -239,9 +240,17 @@ class DpGpuScorer(GpuScorer):
         _, gather, _ = build_chunks(np.asarray(req, REQREC), owners, self.world, C, out=buf)
         return self.submit_chunks(slot, C, now, None, want_features, n=len(req), gather=gather, prefilled=True)
 
-    def wait_x(self, p: XPending, gather: bool = True):
+    def wait_x(self, p: XPending, gather: bool = True, timeout_s: Optional[float] = None):
         """Block until the step's results are on the host. ``gather``: return (res, feats) of
-        the ingress rows in request order; else the raw result chunks."""
+        the ingress rows in request order; else the raw result chunks. ``timeout_s``: the
+        step's deadline (event wait, csrc/kernels/watch.hip); past it the RCCL communicators
+        are aborted (a peer died inside the all-to-all) and TimeoutError is raised."""
+        if timeout_s is not None:
+            if self._watch is None:
+                self._watch = hipk().EventWatch()
+            if not self._watch.wait_for(self.xdriver.done_event(p.slot), timeout_s * 1e3):
+                codes = self.abort_exchange()
+                raise TimeoutError(f"exchange step exceeded {timeout_s:.1f} s (RCCL async errors {codes})")
         self.xdriver.wait(p.slot)
         W = result_width(p.want_features)
         raw = self.host_rr[p.slot][:self.world * p.C * W].numpy()
@@ -258,6 +267,18 @@ class DpGpuScorer(GpuScorer):
 
     def done(self, p) -> bool:
         return self.xdriver.query(p.slot)
+
+    def abort_exchange(self) -> List[int]:
+        """Failover: abort both communicators (cancels collectives still waiting on a dead peer
+        so the streams drain). Returns their async error codes read before the abort."""
+        codes = []
+        for c in self.comms:
+            try:
+                codes.append(int(c.async_error()))
+                c.abort()
+            except Exception:  # already torn down
+                codes.append(-1)
+        return codes
 
 
 def exchange_buckets(batch_buckets: Sequence[int]) -> List[int]:

@@ -14,6 +14,7 @@ every shard's device config block (fixes the unguarded read of quirk Q6).
 from __future__ import annotations
 
 import dataclasses
+import functools
 import json
 import os
 import threading
@@ -33,6 +34,7 @@ from ..utils.faults import Faults, InjectedFault
 from .audit import AuditLog
 from .backends import CpuBackend, GpuBackend, NativeCpuBackend
 from .registry import AccountRegistry
+from ..parallel.spmd import GroupFailure
 
 log = get_logger("engine")
 
@@ -123,6 +125,13 @@ class RiskEngine:
                 cfg.features.width = w
         self.model_kind = mkind
         self.fraud_onnx = fm
+        self._capture = capture
+        self._abuse_am = abuse_model if abuse_model is not None else cfg.abuse_model.path
+        # failure handling state (see _group_failed / rehome)
+        self._snapshot_dir = cfg.gpu.snapshot_dir or None
+        self.failover = dict(group_failed=False, error=None, rehomed=[], rehome_errors={})
+        self.rehome_done = threading.Event()
+        self._rehome_threads: List[threading.Thread] = []
         self.model_version = 1
         self.backends: List = []
         self.healthy = [True] * world
@@ -131,10 +140,13 @@ class RiskEngine:
             local = make_local_backend(cfg, backend, self.capacity, fm, mkind, self.blacklist, self.ipintel,
                                        rank=0, capture=capture, comm=spmd)
             self.local = local
-            self._abuse_am = abuse_model if abuse_model is not None else cfg.abuse_model.path
             abuse_gpu = make_abuse_gpu(cfg, local, self._abuse_am)
             self.group = SpmdGroup(spmd, ShardRunner(spmd, local, abuse_gpu), max_rows=max(cfg.gpu.buckets),
-                                   chunk_buckets=local.scorer.cbuckets if local.kind == "gpu" else None)
+                                   chunk_buckets=local.scorer.cbuckets if local.kind == "gpu" else None,
+                                   heartbeat_s=cfg.gpu.spmd_heartbeat_s,
+                                   used_fn=lambda: [self.registry.size(o) for o in range(self.world)],
+                                   on_failure=self._group_failed)
+            self._spmd_abuse_gpu = abuse_gpu
             self.backends = [ShardProxy(self.group, o, local) for o in range(world)]
         elif backend == "gpu":
             from ..models.plan import compile_onnx, to_device
@@ -142,8 +154,10 @@ class RiskEngine:
                 plan = (to_device(compile_onnx(fm), f"cuda:{d}", cfg.fraud_model.precision)
                         if mkind == "onnx" else None)
                 model = {"onnx": "plan", "heuristic": "heuristic", "none": "none"}[mkind]
-                self.backends.append(GpuBackend(cfg, self.capacity, f"cuda:{d}", plan=plan, model=model,
-                                                blacklist=self.blacklist, ipintel=self.ipintel, capture=capture))
+                be = GpuBackend(cfg, self.capacity, f"cuda:{d}", plan=plan, model=model,
+                                blacklist=self.blacklist, ipintel=self.ipintel, capture=capture)
+                be.on_drained = functools.partial(self._on_drained, r)
+                self.backends.append(be)
                 self.metrics.gpu_healthy.labels(gpu=str(d)).set(1)
         else:
             for _ in range(world):
@@ -225,8 +239,15 @@ class RiskEngine:
         slots, owners, _ = self.registry.resolve_batch(rb, insert=True)
         req = np.empty(n, REQREC)
         rb.pack_reqrec(slots, req.view(np.uint8), now, None)
-        if self.group is not None:  # owner-routed exchange: each rank scores its own rows
-            res, feats = self.group.score(req, owners, now, want_features)
+        g = self.group
+        if g is not None:  # owner-routed exchange: each rank scores its own rows
+            try:
+                res, feats = g.score(req, owners, now, want_features)
+            except GroupFailure:
+                # the batch died with the group (some rows may have been applied on their
+                # shards): answer all of it from the stateless fallback; later batches go to
+                # the local and re-homed shards (_group_failed)
+                res, feats = self._fallback_score(req, now, want_features, "group_failed")
             self._add_links(rb, slots, owners)
             self._observe(rb, res, version)
             return res, feats, slots, owners
@@ -287,7 +308,11 @@ class RiskEngine:
         try:
             if self.faults.active("backend_error", shard=o):
                 raise InjectedFault(f"injected backend error on shard {o}")
-            return ("ok", be.submit(sub, now, want_features))
+            if be.kind == "gpu" and self.faults.active("gpu_timeout", shard=o):
+                # a real device stall ahead of the batch: the watchdog deadline has to catch it
+                ms = float(self.faults.params("gpu_timeout").get("ms", 3 * self.cfg.gpu.batch_timeout_ms))
+                be.stall(ms)
+            return ("ok", (be, be.submit(sub, now, want_features)))
         except Exception as e:  # shard failure -> degrade to the CPU fallback
             self._mark_unhealthy(o, e)
             return ("fallback", None)
@@ -295,34 +320,157 @@ class RiskEngine:
     def _collect(self, o: int, sub: np.ndarray, now: int, want_features: bool, p):
         state, h = p
         if state == "ok":
+            be, h = h
             try:
-                be = self.backends[o]
                 if be.kind == "gpu":
                     return be.collect(h, timeout_s=self.cfg.gpu.batch_timeout_ms / 1e3)
                 return be.collect(h)
             except Exception as e:
                 self._mark_unhealthy(o, e)
+        return self._fallback_score(sub, now, want_features, "shard_unhealthy", shard=o)
+
+    def _fallback_score(self, sub: np.ndarray, now: int, want_features: bool, reason: str, shard=None):
         if self.fallback is None:
-            raise RuntimeError(f"shard {o} failed and no fallback is configured")
-        self.metrics.fallbacks.labels(reason="shard_unhealthy").inc(len(sub))
+            raise RuntimeError(f"shard {shard if shard is not None else '*'} failed and no fallback is configured")
+        self.metrics.fallbacks.labels(reason=reason).inc(len(sub))
         # the fallback has no feature state for this shard: partial features (engine.go:267-270)
         fb = sub.copy()
         fb["slot"] = -1
         return self.fallback.score(fb, now, want_features, update=False)
 
     def _mark_unhealthy(self, o: int, err: Exception) -> None:
-        if self.healthy[o]:
+        first = self.healthy[o]
+        if first:
             log.error("shard unhealthy", extra={"fields": dict(shard=o, error=str(err))})
         self.healthy[o] = False
-        if self.devices:
+        if self.devices and o < len(self.devices):
             self.metrics.gpu_healthy.labels(gpu=str(self.devices[o])).set(0)
+        if (first and self.group is None and self.kind == "gpu" and self.cfg.gpu.auto_recover
+                and len(self.devices) > 1 and not self.failover["group_failed"]):
+            # a shard that neither drains nor recovers is rebuilt on a surviving GPU
+            t = threading.Timer(self.cfg.gpu.rehome_after_s, self._rehome_if_still_unhealthy, args=(o,))
+            t.daemon = True
+            t.start()
 
     def recover(self, shard: Optional[int] = None) -> None:
         """Mark shard(s) healthy again (after an operator or watchdog check)."""
         for o in ([shard] if shard is not None else range(self.world)):
             self.healthy[o] = True
-            if self.devices:
+            if self.devices and o < len(self.devices):
                 self.metrics.gpu_healthy.labels(gpu=str(self.devices[o])).set(1)
+
+    # ---- failure handling: drain, failover, re-home (SURVEY §5.3)
+    def _on_drained(self, o: int, be) -> None:
+        """A quarantined GPU shard's late batches all completed: its state is consistent (each
+        late batch applied its events once), so it returns to service (``auto_recover``)."""
+        if self.cfg.gpu.auto_recover and self.backends[o] is be and not self.healthy[o]:
+            log.info("shard drained, back in service", extra={"fields": dict(shard=o)})
+            self.recover(o)
+
+    def _rehome_if_still_unhealthy(self, o: int) -> None:
+        if self.healthy[o] or self._snapshot_dir is None:
+            return
+        alive = [d for k, d in enumerate(self.devices) if self.healthy[k] and k != o]
+        if not alive:
+            return
+        try:
+            self.rehome(o, device=alive[0])
+        except Exception as e:
+            log.error("re-home failed", extra={"fields": dict(shard=o, error=str(e))})
+
+    def _group_failed(self, err: BaseException) -> None:
+        """SPMD group failure (called once, by the thread whose collective failed): rank 0
+        leaves the group and serves alone. Its own shard keeps its state (a GPU shard drops
+        the RCCL exchange and runs the single-GPU pipeline on the same HBM store); every
+        remote shard is unhealthy (rows -> stateless fallback) until :meth:`rehome` rebuilds
+        it here from the snapshot directory, on a background thread."""
+        with self._lock:
+            g = self.group
+            if g is None:
+                return
+            self.group = None
+        self.failover.update(group_failed=True, error=str(err), t_failed=time.time())
+        log.error("spmd group failed: failing over to rank 0", extra={"fields": dict(error=str(err))})
+        g.abandon()
+        local = self.local
+        try:
+            if local.kind == "gpu":
+                local.leave_exchange()
+        except Exception as e:  # rank 0's own device is stuck too: everything falls back
+            log.error("local shard unusable after the group failure", extra={"fields": dict(error=str(e))})
+            self._mark_unhealthy(0, e)
+        self.backends = [local] + [DeadShard(o) for o in range(1, self.world)]
+        for o in range(1, self.world):
+            self.healthy[o] = False
+        ag = getattr(self, "_spmd_abuse_gpu", None)
+        self.abuse.group, self.abuse.group_model = None, False
+        if ag is not None:
+            self.abuse.gpu = [ag] + [None] * (self.world - 1)
+        if self.cfg.gpu.auto_recover and self._snapshot_dir is not None:
+            t = threading.Thread(target=self._rehome_all, args=(list(range(1, self.world)), True), daemon=True,
+                                 name="spmd-rehome")
+            self._rehome_threads.append(t)
+            t.start()
+        else:
+            self.rehome_done.set()
+
+    def _rehome_all(self, owners, wait_final: bool) -> None:
+        try:
+            for o in owners:
+                try:
+                    self.rehome(o, wait_final=wait_final)
+                except Exception as e:
+                    self.failover["rehome_errors"][o] = str(e)
+                    log.error("re-home failed", extra={"fields": dict(shard=o, error=str(e))})
+        finally:
+            self.rehome_done.set()
+
+    def rehome(self, o: int, directory: Optional[str] = None, device=None, wait_final: bool = False) -> int:
+        """Rebuild shard ``o`` in this process from its snapshot in ``directory`` (default: the
+        last snapshot directory) and put it back in service; returns the accounts restored.
+        ``device``: GPU ordinal for a GPU shard (default: this process's device).
+        ``wait_final``: first wait up to ``rehome_grace_s`` for the shard's final snapshot
+        (written by a surviving SPMD worker when the group failed). The engine's account
+        registry is live on rank 0, so every account keeps its slot."""
+        directory = directory or self._snapshot_dir
+        if directory is None:
+            raise ValueError("no snapshot directory to re-home from")
+        if wait_final:
+            marker = os.path.join(directory, f"shard{o}.final")
+            t_end = time.time() + self.cfg.gpu.rehome_grace_s
+            t_fail = self.failover.get("t_failed", 0) - 60
+            while time.time() < t_end and not (os.path.exists(marker) and os.path.getmtime(marker) >= t_fail):
+                time.sleep(0.05)
+        kind = self.kind if self.kind in ("gpu", "golden") else "cpu"
+        if kind == "gpu":
+            import torch
+            dev = int(device) if device is not None else torch.cuda.current_device()
+            with torch.cuda.device(dev):
+                be = make_local_backend(self.cfg, "gpu", self.capacity, self.fraud_onnx, self.model_kind,
+                                        self.blacklist, self.ipintel, rank=o, capture=self._capture)
+        else:
+            be = make_local_backend(self.cfg, kind, self.capacity, self.fraud_onnx, self.model_kind,
+                                    self.blacklist, self.ipintel, rank=o)
+        path = os.path.join(directory, f"shard{o}.{be.snapshot_ext}")
+        n = 0
+        if os.path.exists(path):
+            if be.kind == "gpu":
+                n = be.store.restore(path)
+            else:
+                be.restore(path)
+                n = self.registry.size(o)
+        else:
+            log.error("no snapshot for shard: it restarts empty", extra={"fields": dict(shard=o, path=path)})
+        be.refresh_config(self.scoring)
+        if be.kind == "gpu":
+            be.on_drained = functools.partial(self._on_drained, o)
+            if self.abuse.gpu is not None and self._abuse_am is not None:
+                self.abuse.gpu[o] = make_abuse_gpu(self.cfg, be, self._abuse_am)
+        self.backends[o] = be
+        self.failover["rehomed"].append(dict(shard=o, path=path, accounts=int(n), t=time.time()))
+        self.recover(o)
+        log.info("shard re-homed", extra={"fields": dict(shard=o, path=path, accounts=int(n))})
+        return int(n)
 
     # ---- wire-level entry points (gRPC handlers call these with raw bytes)
     def score_batch_bytes(self, data: bytes, t0: Optional[float] = None) -> bytes:
@@ -621,16 +769,21 @@ class RiskEngine:
             self.group = None
 
     def health(self) -> Dict:
+        fo = self.failover
         return dict(backend=self.kind, shards=self.world, healthy=list(self.healthy),
                     accounts=[self.registry.size(o) for o in range(self.world)],
-                    uptime_s=round(time.time() - self.started_at, 1))
+                    uptime_s=round(time.time() - self.started_at, 1),
+                    failover=dict(group_failed=fo["group_failed"], error=fo["error"],
+                                  rehomed=[r["shard"] for r in fo["rehomed"]]))
 
     def ready(self) -> bool:
         return all(self.healthy) or self.fallback is not None
 
     def snapshot(self, directory: str) -> None:
-        """Feature shards + account registry -> ``directory`` (restart keeps velocity windows)."""
+        """Feature shards + account registry -> ``directory`` (restart keeps velocity windows;
+        a failed shard is re-homed from here)."""
         os.makedirs(directory, exist_ok=True)
+        self._snapshot_dir = directory
         meta = dict(version=1, world=self.world, kind=self.kind, ids=[])
         for o in range(self.world):
             n = self.registry.size(o)
@@ -674,6 +827,38 @@ class RiskEngine:
         if self.group is not None:
             self.group.restore(directory)
         return total
+
+
+class ShardUnavailable(RuntimeError):
+    """The shard's process died with the SPMD group and is being re-homed."""
+
+
+class DeadShard:
+    """Stand-in for a shard lost with its SPMD worker until :meth:`RiskEngine.rehome` rebuilds
+    it: scoring skips it (its rows go to the fallback), state ops fail fast, config pushes and
+    model swaps are no-ops (the rebuilt shard takes the engine's current config and model)."""
+
+    kind = "dead"
+
+    def __init__(self, owner: int):
+        self.o = owner
+
+    def refresh_config(self, scoring=None) -> None:
+        pass
+
+    def swap_model(self, fm, mkind: str) -> None:
+        pass
+
+    def metrics(self):
+        return None
+
+    def __getattr__(self, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+
+        def unavailable(*a, **k):
+            raise ShardUnavailable(f"shard {self.o} is being re-homed after its worker failed")
+        return unavailable
 
 
 # ============================================================================ shard construction

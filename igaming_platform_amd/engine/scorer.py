@@ -482,8 +482,12 @@ class GpuScorer:
         return self.submit_packed(slot, len(rows), now, rows=rows)
 
     def done(self, p: Pending) -> bool:
-        """Non-blocking completion check (the backend watchdog polls it)."""
+        """Non-blocking completion check."""
         return self.driver.query(p.slot) if p.event is None else p.event.query()
+
+    def done_event(self, p: Pending) -> int:
+        """Raw hipEvent_t that completes with the batch (the watchdog's deadline wait)."""
+        return self.driver.model_event(p.slot) if p.event is None else int(p.event.cuda_event)
 
     def wait(self, p: Pending, unpack: bool = True):
         if p.event is None:

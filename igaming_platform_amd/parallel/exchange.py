@@ -119,14 +119,19 @@ class HostExchange:
     the multi-process CPU tests. ``score_fn(rows, want_features) -> (res, feats)`` scores
     this rank's owned rows; ``rows_scored`` counts them (tests assert owned-rows-only)."""
 
-    def __init__(self, rank: int, world: int):
+    def __init__(self, rank: int, world: int, comm=None):
+        """``comm``: a :class:`~.comm.TorchComm` (its per-op deadline bounds both all-to-alls);
+        None: plain torch.distributed calls on the default group."""
         self.rank, self.world = rank, world
+        self.comm = comm
         self.rows_scored = 0
         self.batches = 0
 
     def _a2a(self, send: np.ndarray, per_peer: int) -> np.ndarray:
         if self.world == 1:
             return send.copy()
+        if self.comm is not None and hasattr(self.comm, "all_to_all_bytes"):
+            return self.comm.all_to_all_bytes(send, per_peer)
         import torch
         import torch.distributed as dist
         s = torch.from_numpy(np.ascontiguousarray(send).view(np.uint8).reshape(-1))

@@ -13,13 +13,27 @@ every account's feature state lives on exactly one rank. Per ScoreBatch / micro-
 
 Cold-path ops (thresholds, blacklist/ip tables, warehouse rows, GetFeatures, event
 histories, GRU abuse scores) use a broadcast-then-reduce protocol over :mod:`.comm`.
+
+Failure handling (reference: engine.go:279-282 degrades a failed model call,
+cmd/main.go:329-342 recovers a failed handler): every collective rank 0 issues carries a
+deadline (:mod:`.comm`), and a heartbeat op (OP_PING, an all-reduce of ones) runs every
+``heartbeat_s`` so a dead worker is noticed while the API is idle too. The first failed
+collective marks the group failed (:class:`GroupFailure`) and calls ``on_failure``: the
+engine then scores that batch on its stateless fallback, leaves the group and re-homes every
+remote shard onto rank 0 from its snapshot (engine/risk_engine.py ``_group_failed``). A
+surviving worker whose collective fails writes a final snapshot of its shard next to the
+periodic ones (``shard<r>.<ext>`` + ``shard<r>.final``) before it exits, so its state is
+re-homed without loss; a dead worker's shard comes back from its last periodic snapshot.
 """
 from __future__ import annotations
 
 import dataclasses
 import io
 import json
+import logging
+import os
 import threading
+import time
 
 import numpy as np
 
@@ -27,7 +41,17 @@ from ..config import RuleWeights, ScoringConfig
 from ..layouts import ACCTBATCH, FEATREC, REQREC
 
 OP_SCORE, OP_INGEST, OP_CONFIG, OP_TABLES, OP_BATCH, OP_EXT, OP_FEATURES, OP_RESET, OP_STOP, OP_EVHIST, \
-    OP_ABUSE, OP_SNAPSHOT, OP_RESTORE, OP_RELOAD, OP_FEATMANY = range(1, 16)
+    OP_ABUSE, OP_SNAPSHOT, OP_RESTORE, OP_RELOAD, OP_FEATMANY, OP_PING = range(1, 17)
+
+log = logging.getLogger("igaming_platform_amd.spmd")
+
+# slots beyond the last count rank 0 announced that a survivor's final snapshot also covers
+# (accounts created since the previous heartbeat)
+FINAL_SNAPSHOT_MARGIN = 65536
+
+
+class GroupFailure(RuntimeError):
+    """A collective of the SPMD group failed or missed its deadline (a rank died or hung)."""
 
 
 def owners_of(req: np.ndarray) -> np.ndarray:
@@ -75,7 +99,9 @@ class ShardRunner:
         self.hx = None
         if backend.kind != "gpu":
             from .exchange import HostExchange
-            self.hx = HostExchange(comm.rank, comm.world)
+            self.hx = HostExchange(comm.rank, comm.world, comm)
+        self.snapshot_dir = None  # the directory of the last OP_SNAPSHOT (final snapshot on failure)
+        self.used = [0] * comm.world  # slots in use per rank (rank 0's registry, via OP_PING)
 
     @property
     def rows_scored(self) -> int:
@@ -92,7 +118,9 @@ class ShardRunner:
         """One owner-routed exchange step (collective). ``req``/``owners``: the ingress rows
         (rank 0) or None. Returns (res, feats) of the ingress rows in request order."""
         if self.be.kind == "gpu":
-            return self.be.exchange_score(req, owners, C, now, want_features)
+            t = getattr(self.comm, "op_timeout", None)
+            return self.be.exchange_score(req, owners, C, now, want_features,
+                                          timeout_s=t.total_seconds() if t is not None else None)
 
         def score_fn(rows, wf):
             return self.be.score(rows, now, wf)
@@ -103,6 +131,10 @@ class ShardRunner:
         n, now, aux, aux2 = int(hdr[1]), int(hdr[2]), int(hdr[3]), int(hdr[4])
         if op == OP_SCORE:  # a worker's share of a step rank 0 started (no payload: the exchange)
             return self.score(None, None, aux2, now, bool(aux))
+        if op == OP_PING:  # heartbeat: payload = slots in use per rank; all-reduce proves liveness
+            if payload:
+                self.used = np.frombuffer(payload, np.int64).tolist()
+            return self.comm.sum_i64(np.ones(1, np.int64))
         if op == OP_INGEST:
             ev = np.frombuffer(payload, REQREC).copy()
             mine = self._mine(owners_of(ev))
@@ -167,6 +199,8 @@ class ShardRunner:
             meta = json.loads(payload.decode())
             path = os.path.join(meta["dir"], f"shard{self.rank}.{self.be.snapshot_ext}")
             if op == OP_SNAPSHOT:
+                self.snapshot_dir = meta["dir"]
+                self.used = [int(u) for u in meta["used"]] or self.used
                 if self.be.kind == "gpu":
                     self.be.store.snapshot(path, n_used=max(int(meta["used"][self.rank]), 1))
                 else:
@@ -179,12 +213,38 @@ class ShardRunner:
             return None
         raise ValueError(f"unknown op {op}")
 
+    def final_snapshot(self) -> str:
+        """After the group failed: this shard's current state -> the snapshot directory of the
+        last OP_SNAPSHOT (+ a ``.final`` marker rank 0's re-home waits for). Returns the path
+        ('' when no snapshot directory is known)."""
+        if not self.snapshot_dir or self.rank == 0:
+            return ""
+        path = os.path.join(self.snapshot_dir, f"shard{self.rank}.{self.be.snapshot_ext}")
+        if self.be.kind == "gpu":
+            xd = getattr(self.be.scorer, "abort_exchange", None)
+            if xd is not None:
+                xd()  # unblock the RCCL exchange kernels still waiting on the dead peer
+            cap = self.be.store.capacity
+            self.be.store.snapshot(path, n_used=min(cap, max(int(self.used[self.rank]), 1) + FINAL_SNAPSHOT_MARGIN))
+        else:
+            self.be.snapshot(path)
+        tmp = os.path.join(self.snapshot_dir, f"shard{self.rank}.final.tmp")
+        with open(tmp, "w") as f:
+            json.dump(dict(rank=self.rank, time=time.time()), f)
+        os.replace(tmp, os.path.join(self.snapshot_dir, f"shard{self.rank}.final"))
+        return path
+
 
 class SpmdGroup:
     """Rank 0's handle on the group: issues an op to every rank and runs its own share.
     Ops are serialised (one collective sequence at a time) by a lock."""
 
-    def __init__(self, comm, runner: ShardRunner, max_rows: int = 8192, chunk_buckets=None):
+    def __init__(self, comm, runner: ShardRunner, max_rows: int = 8192, chunk_buckets=None,
+                 heartbeat_s: float = 0.0, used_fn=None, on_failure=None):
+        """``heartbeat_s`` > 0: an OP_PING every that many seconds (liveness while idle; its
+        payload tells the workers how many slots rank 0's registry gives each shard, from
+        ``used_fn()``). ``on_failure(exc)``: called once, from the thread whose collective
+        failed, when the group fails."""
         if comm.rank != 0:
             raise ValueError("SpmdGroup lives on rank 0; other ranks call run_worker()")
         self.comm = comm
@@ -193,14 +253,65 @@ class SpmdGroup:
         self.max_rows = int(max_rows)
         self.chunk_buckets = sorted(chunk_buckets) if chunk_buckets else None
         self._lock = threading.Lock()
+        self.failed: BaseException = None
+        self.on_failure = on_failure
+        self.used_fn = used_fn
+        self.heartbeats = 0
+        self._stop = threading.Event()
+        self._hb = None
+        if heartbeat_s > 0 and self.world > 1:
+            self._hb = threading.Thread(target=self._heartbeat, args=(float(heartbeat_s),), daemon=True,
+                                        name="spmd-heartbeat")
+            self._hb.start()
+
+    def _fail(self, e: BaseException) -> "GroupFailure":
+        first = self.failed is None
+        if first:
+            self.failed = e
+            log.error("spmd group failed: %s", e)
+            self._stop.set()
+        if first and self.on_failure is not None:
+            self.on_failure(e)
+        return e if isinstance(e, GroupFailure) else GroupFailure(str(e))
+
+    def _collective(self, fn):
+        """Run ``fn`` (one op's collectives) under the group lock; a failure or missed deadline
+        marks the group failed and raises :class:`GroupFailure` (now and on every later op)."""
+        with self._lock:
+            if self.failed is not None:
+                raise GroupFailure(f"spmd group failed earlier: {self.failed}")
+            try:
+                return fn()
+            except GroupFailure:
+                raise
+            except Exception as e:  # gloo: timeout / connection reset by a dead peer
+                err = e
+        raise self._fail(err) from err
 
     def _issue(self, op: int, payload: bytes = b"", n: int = 0, now: int = 0, aux: int = 0, aux2: int = 0,
                extra=(0, 0)):
         hdr = np.array([op, n, now, aux, aux2, extra[0], extra[1], 0], np.int64)
-        with self._lock:
+
+        def run():
             self.comm.bcast_i64(hdr, 0)
             self.comm.bcast_bytes(payload, 0)
             return self.runner.handle(op, hdr, payload)
+        return self._collective(run)
+
+    def ping(self) -> int:
+        """One heartbeat: every rank answers (returns the number of live ranks)."""
+        used = self.used_fn() if self.used_fn is not None else [0] * self.world
+        payload = np.asarray(used, np.int64).tobytes()
+        out = self._issue(OP_PING, payload)
+        self.heartbeats += 1
+        return int(out[0])
+
+    def _heartbeat(self, every: float) -> None:
+        while not self._stop.wait(every):
+            try:
+                self.ping()
+            except GroupFailure:
+                return
 
     def _chunk_capacity(self, owners: np.ndarray) -> int:
         from .exchange import max_owner_count
@@ -223,9 +334,11 @@ class SpmdGroup:
             sub, own = req[i:i + self.max_rows], np.asarray(owners[i:i + self.max_rows], np.int64)
             C = self._chunk_capacity(own)
             hdr = np.array([OP_SCORE, len(sub), now, int(want_features), C, 0, 0, 0], np.int64)
-            with self._lock:
+
+            def step():
                 self.comm.bcast_i64(hdr, 0)
-                r, f = self.runner.score(sub, own, C, now, want_features)
+                return self.runner.score(sub, own, C, now, want_features)
+            r, f = self._collective(step)
             res[i:i + len(sub)] = r
             if want_features:
                 feats[i:i + len(sub)] = f
@@ -283,22 +396,54 @@ class SpmdGroup:
         self._issue(OP_RESTORE, json.dumps({"dir": directory, "used": []}).encode())
 
     def stop(self) -> None:
+        """Release the workers (no-op once the group failed: they leave on their own)."""
+        self._stop.set()
+        if self.failed is not None:
+            return
         hdr = np.array([OP_STOP, 0, 0, 0, 0, 0, 0, 0], np.int64)
-        with self._lock:
-            self.comm.bcast_i64(hdr, 0)
+        try:
+            self._collective(lambda: self.comm.bcast_i64(hdr, 0))
+        except GroupFailure:
+            pass
+
+    def abandon(self) -> None:
+        """After a failure: stop the heartbeat and tear the process group down, which makes the
+        surviving workers' pending collectives fail at once (they then write their final
+        snapshots and exit) instead of waiting for the group timeout."""
+        self._stop.set()
+        try:
+            import torch.distributed as dist
+            if dist.is_initialized():
+                dist.destroy_process_group()
+        except Exception as e:  # already broken: nothing left to release
+            log.warning("destroy_process_group after failure: %s", e)
 
 
 def run_worker(comm, backend, abuse_gpu=None):
-    """Loop of ranks >= 1 until rank 0 sends STOP. Returns (ops served, rows scored)."""
+    """Loop of ranks >= 1 until rank 0 sends STOP. Returns (ops served, rows scored). When a
+    collective fails (rank 0 or a peer died / the group was torn down), the shard writes its
+    final snapshot (if rank 0 ever sent a snapshot directory) and the loop returns."""
     runner = ShardRunner(comm, backend, abuse_gpu)
     served = 0
     while True:
-        hdr = comm.bcast_i64(np.zeros(8, np.int64), 0)
-        op = int(hdr[0])
-        if op == OP_STOP:
-            return served, runner.rows_scored
-        payload = b"" if op == OP_SCORE else comm.bcast_bytes(None, 0)
-        runner.handle(op, hdr, payload)
+        try:
+            # idle wait for rank 0's next op: no per-op deadline (rank 0's heartbeats keep the
+            # group timeout from firing while the API is idle)
+            hdr = comm.bcast_i64(np.zeros(8, np.int64), 0, deadline=False)
+            op = int(hdr[0])
+            if op == OP_STOP:
+                return served, runner.rows_scored
+            payload = b"" if op == OP_SCORE else comm.bcast_bytes(None, 0)
+            runner.handle(op, hdr, payload)
+        except Exception as e:
+            log.error("spmd worker %d: group failed (%s); writing the final snapshot", comm.rank, e)
+            try:
+                path = runner.final_snapshot()
+                if path:
+                    log.info("spmd worker %d: final snapshot %s", comm.rank, path)
+            except Exception as e2:  # the shard itself is broken: rank 0 falls back to the periodic snapshot
+                log.error("spmd worker %d: final snapshot failed: %s", comm.rank, e2)
+            return served, -1
         served += 1
 
 

@@ -55,6 +55,8 @@ def main(argv=None) -> int:
     # get a queue of their own with 8 (must be set before the HIP runtime initialises)
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     cfg = Config.load(a.config or None)
+    if a.snapshot_dir:
+        cfg.gpu.snapshot_dir = a.snapshot_dir  # failed shards are re-homed from here
     if a.gpus:
         cfg.gpu.devices = a.gpus
     log = setup_logger(cfg.server.log_level)
@@ -67,8 +69,9 @@ def main(argv=None) -> int:
         a.backend = backend
         if backend == "gpu":
             torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-        comm = init_from_env("nccl" if backend == "gpu" else "gloo",
-                             device=f"cuda:{torch.cuda.current_device()}" if backend == "gpu" else None)
+        # control plane over gloo (deadlines / heartbeats that fail without taking rank 0
+        # down); GPU shards move their rows over RCCL communicators of their own
+        comm = init_from_env("gloo")
         if comm.rank != 0:
             from .engine.risk_engine import serve_shard
             n, rows = serve_shard(cfg, comm, backend=backend, capacity=a.accounts or None,

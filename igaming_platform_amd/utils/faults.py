@@ -1,8 +1,8 @@
 """Fault injection hooks: ``FAULT_INJECT="backend_error:shard=0,model_error"``.
 
 Names used by the engine: ``backend_error`` (a shard's scoring step raises -> the shard is
-marked unhealthy and its rows go to the CPU fallback), ``gpu_timeout`` (same, via the
-batch deadline), ``model_error`` (ML fails -> ml_error_score, engine.go:279-282),
+marked unhealthy and its rows go to the CPU fallback), ``gpu_timeout:ms=N`` (a real N ms
+device stall is queued ahead of the shard's batch, so the watchdog deadline fires), ``model_error`` (ML fails -> ml_error_score, engine.go:279-282),
 ``feature_store_down`` (features unavailable -> partial features, engine.go:267-270).
 """
 from __future__ import annotations
@@ -39,6 +39,10 @@ class Faults:
                 self._active.clear()
             else:
                 self._active.pop(name, None)
+
+    def params(self, name: str) -> Dict[str, str]:
+        with self._lock:
+            return dict(self._active.get(name, {}))
 
     def active(self, name: str, **match) -> bool:
         with self._lock:

@@ -157,6 +157,7 @@ def test_health_and_reflection(stack):
 
 def test_http_endpoints_and_metrics(stack):
     eng, gs, hs, cli = stack
+    cli.score("feat-http", 777, "deposit")  # this test's own RPC (xdist may run it before the others)
     assert _http(hs, "/health") == (200, "OK")
     assert _http(hs, "/ready") == (200, "Ready")
     code, body = _http(hs, "/debug/score?account_id=http-1&amount=500000&type=deposit")
@@ -164,7 +165,7 @@ def test_http_endpoints_and_metrics(stack):
     code, body = _http(hs, "/metrics")
     assert 'risk_requests_total{code="OK",method="ScoreTransaction"}' in body
     assert "risk_action_total" in body and "risk_latency_seconds_bucket" in body
-    code, body = _http(hs, "/debug/features?account_id=feat-1")
+    code, body = _http(hs, "/debug/features?account_id=feat-http")
     assert json.loads(body)["tx_sum_1h"] == 777
 
 

@@ -138,10 +138,11 @@ def main():
                        tree_partial=(sc.tree_partial, g, tree) if tree else None, trace=tr)
             torch.cuda.synchronize()
         t = tr.cpu().numpy().reshape(8, 8)[:, :5].astype(np.float64)
-        t0 = t[t > 0].min()
-        print("mlp_head trace us: start / staged / mfma done / synced / stored")
-        for b in range(8):
-            print("   block", b * 32, [round((x - t0) / 100.0, 2) if x > 0 else None for x in t[b]])
+        if (t > 0).any():
+            t0 = t[t > 0].min()
+            print("mlp_head trace us: start / staged / mfma done / synced / stored")
+            for b in range(8):
+                print("   block", b * 32, [round((x - t0) / 100.0, 2) if x > 0 else None for x in t[b]])
     res = {k: dict(median_us=float(np.median(v[min(5, len(v) - 1):])), min_us=float(np.min(v[min(5, len(v) - 1):]))) for k, v in times.items()}
     for k, v in res.items():
         print(f"{k:28s} median {v['median_us']:8.1f} us   min {v['min_us']:8.1f} us")
