@@ -180,6 +180,39 @@ PYBIND11_MODULE(_hipk, m) {
     check("tree_ensemble");
   });
 
+  m.def("tree_sparse", [](py::dict d, uintptr_t s) {
+    TreeSparseArgs a{};
+    a.X = ptr<const float*>(d, "X");
+    a.nodes = ptr<const int32_t*>(d, "nodes");
+    a.roots = ptr<const int32_t*>(d, "roots");
+    a.leaf_w = ptr<const float*>(d, "leaf_w");
+    a.leaf_has = ptr<const uint8_t*>(d, "leaf_has");
+    a.base = ptr<const float*>(d, "base");
+    a.out = ptr<float*>(d, "out");
+    a.x_stride = geti(d, "x_stride");
+    a.n_rows = geti(d, "n_rows");
+    a.n_trees = geti(d, "n_trees");
+    a.depth = geti(d, "depth");
+    a.k = geti(d, "k");
+    a.n_out = geti(d, "n_out");
+    a.post = geti(d, "post");
+    a.aggregate = geti(d, "aggregate");
+    a.binary_class = geti(d, "binary_class", -1);
+    a.all_positive = geti(d, "all_positive", 1);
+    a.feat_w = geti(d, "feat_w");
+    const int groups = geti(d, "groups", 1);
+    float* partial = ptr<float*>(d, "partial");
+    if (!a.X || !a.nodes || !a.roots || !a.leaf_w || !a.leaf_has || !a.out) throw std::runtime_error("tree_sparse: args");
+    if (a.k < 1 || a.k > 64) throw std::runtime_error("tree_sparse: 1..64 targets");
+    if (a.post < 0 || a.post > 4 || a.aggregate < 0 || a.aggregate > 3) throw std::runtime_error("tree_sparse: post/aggregate");
+    if (a.feat_w < 1 || a.feat_w > a.x_stride) throw std::runtime_error("tree_sparse: feature width");
+    if (a.depth < 0 || a.depth > 4096) throw std::runtime_error("tree_sparse: depth");
+    if (groups < 1 || (groups > 1 && !partial)) throw std::runtime_error("tree_sparse: grouped launch needs partial");
+    if (a.binary_class >= 0 ? a.n_out != 2 : a.n_out != a.k) throw std::runtime_error("tree_sparse: n_out");
+    launch_tree_sparse(a, groups, partial, stream_of(s));
+    check("tree_sparse");
+  });
+
   auto gemm_args = [](const py::dict& d) {
     GemmArgs a{};
     a.X = ptr<const void*>(d, "X");

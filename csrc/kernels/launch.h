@@ -106,6 +106,29 @@ struct TreeArgs {
 void launch_tree_ensemble(const TreeArgs& a, hipStream_t st);
 void launch_tree_ensemble_grouped(const TreeArgs& a, int groups, float* partial, hipStream_t st);
 
+// ---- K2b general trees on the pointer layout (csrc/runtime/trees.h Sparse)
+struct TreeSparseArgs {
+  const float* X;           // [n][x_stride]
+  const int32_t* nodes;     // [N][4] {meta, threshold bits, true child, false child | leaf row}
+  const int32_t* roots;     // [T] root node of each tree
+  const float* leaf_w;      // [L][K]
+  const uint8_t* leaf_has;  // [L][K] target written by the leaf (MIN / MAX)
+  const float* base;        // [K] (nullable)
+  float* out;               // [n][n_out]
+  int32_t x_stride;
+  int32_t n_rows;
+  int32_t n_trees;
+  int32_t depth;            // longest root-to-leaf path (bounds the traversal loop)
+  int32_t k;                // targets (<= 64)
+  int32_t n_out;
+  int32_t post;             // tree_post.h TreePostKind
+  int32_t aggregate;        // 0 sum, 1 average, 2 min, 3 max
+  int32_t binary_class;     // -1 unless classifier binary case
+  int32_t all_positive;
+  int32_t feat_w;           // largest feature id + 1 (the staged X tile width)
+};
+void launch_tree_sparse(const TreeSparseArgs& a, int groups, float* partial, hipStream_t st);
+
 // ---- K3 dense layers: Y = act(X W^T + b)
 struct GemmArgs {
   const void* X;            // [M][ldx] f32 or bf16

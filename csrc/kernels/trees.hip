@@ -13,6 +13,7 @@
 // finisher (or the consuming mlp_head kernel) adds base values and the post transform.
 #include "common.h"
 #include "launch.h"
+#include "tree_post.h"
 
 namespace igp {
 
@@ -34,30 +35,26 @@ __device__ __forceinline__ void post_row(const TreeArgs& a, const float* s, floa
     float v = s[0];
     if (a.average) v /= (float)a.n_trees;
     if (a.base) v += a.base[0];
-    const int c = a.binary_class;
-    if (a.post == 1) {
-      o[c] = 1.f / (1.f + expf(-v));
-      o[1 - c] = 1.f / (1.f + expf(v));
-    } else {
-      o[c] = v;
-      o[1 - c] = a.all_positive ? 1.f - v : -v;
-    }
+    tree_post_binary(a.post, a.binary_class, a.all_positive, v, o);
     return;
   }
-  float mx = -INFINITY;
   for (int k = 0; k < K; ++k) {
     float v = s[k];
     if (a.average) v /= (float)a.n_trees;
     if (a.base) v += a.base[k];
-    if (a.post == 1) v = 1.f / (1.f + expf(-v));
     o[k] = v;
-    mx = fmaxf(mx, v);
   }
-  if (a.post == 2) {
-    float sum = 0.f;
-    for (int k = 0; k < K; ++k) { o[k] = expf(o[k] - mx); sum += o[k]; }
-    for (int k = 0; k < K; ++k) o[k] /= sum;
-  }
+  tree_post_inplace(a.post, K, o);
+}
+
+// element-wise post transforms (NONE / LOGISTIC / PROBIT); the softmax family is row-wise
+__device__ __forceinline__ float post_elem(int post, float v) {
+  if (post == TP_LOGISTIC) return 1.f / (1.f + expf(-v));
+  if (post == TP_PROBIT) return 1.41421356f * tp_erfinv(2 * v - 1);
+  return v;
+}
+__host__ __device__ __forceinline__ bool post_rowwise(const TreeArgs& a) {
+  return a.post == TP_SOFTMAX || a.post == TP_SOFTMAX_ZERO || a.binary_class >= 0;
 }
 
 template <bool LEQ>
@@ -224,7 +221,7 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
     constexpr int LPR = K / 4;          // lanes per row
     constexpr int SPP = 256 / LPR;      // samples per pass
     const int k4 = tid % LPR, sp = tid / LPR;
-    const bool rowwise = !partial && (a.post == 2 || a.binary_class >= 0);
+    const bool rowwise = !partial && post_rowwise(a);
     // each thread owns columns 4 k4 .. 4 k4 + 3 of rows sp, sp + SPP, ...: its rows advance
     // through the trees together, RPT x TU independent loads in flight per step. Per row the
     // trees are still summed in order t0, t0+1, ... (same sums as a scalar loop)
@@ -282,8 +279,7 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
           const int k = 4 * k4 + c;
           if (a.average) vv[c] /= (float)a.n_trees;
           if (a.base) vv[c] += a.base[k];
-          if (a.post == 1) vv[c] = 1.f / (1.f + expf(-vv[c]));
-          a.out[(size_t)row * a.n_out + k] = vv[c];
+          a.out[(size_t)row * a.n_out + k] = post_elem(a.post, vv[c]);
         }
       }
     }
@@ -342,8 +338,7 @@ __global__ void tree_finish_elem_kernel(TreeArgs a, const float* partial, int gr
   for (int g = 0; g < groups; ++g) v += partial[(size_t)g * a.n_rows * K + e];
   if (a.average) v /= (float)a.n_trees;
   if (a.base) v += a.base[k];
-  if (a.post == 1) v = 1.f / (1.f + expf(-v));
-  a.out[e] = v;  // n_out == K
+  a.out[e] = post_elem(a.post, v);  // n_out == K
 }
 
 template <int K, bool LEQ>
@@ -362,7 +357,7 @@ static void launch_kl(const TreeArgs& a, int groups, float* partial, int no_fini
   hipLaunchKernelGGL((tree_kernel<K, LEQ>), grid, dim3(256), lds, st, a, tpg, feat_w, in_lds,
                      groups > 1 ? partial : nullptr);
   if (groups > 1 && !no_finish) {
-    if (a.binary_class < 0 && a.post != 2 && a.n_out == K)
+    if (!post_rowwise(a) && a.n_out == K)
       hipLaunchKernelGGL(tree_finish_elem_kernel, dim3((a.n_rows * K + 255) / 256), dim3(256), 0, st, a,
                          partial, groups);
     else

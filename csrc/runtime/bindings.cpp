@@ -142,6 +142,45 @@ PYBIND11_MODULE(_native, m) {
         for (auto& kv : out) res[py::str(kv.first)] = tensor_to_np(kv.second);
         return res;
       })
+      .def("tree_info", [](const exec::Executor& ex, size_t node_index) {
+        const trees::Ensemble* e = ex.ensemble(node_index);
+        if (!e) throw std::runtime_error("node is not a TreeEnsemble");
+        size_t n_nodes = 0;
+        for (auto& tr : e->trees) n_nodes += tr.size();
+        py::dict d;
+        d["depth"] = e->max_depth;
+        d["n_trees"] = e->n_trees();
+        d["n_nodes"] = n_nodes;
+        d["k"] = e->n_targets;
+        d["aggregate"] = e->aggregate;
+        d["post"] = e->post;
+        return d;
+      }, py::arg("node_index"))
+      .def("tree_sparse", [](const exec::Executor& ex, size_t node_index) {
+        const trees::Ensemble* e = ex.ensemble(node_index);
+        if (!e) throw std::runtime_error("node is not a TreeEnsemble");
+        trees::Sparse sp = trees::to_sparse(*e);
+        const int64_t N = int64_t(sp.nodes.size() / 4), L = int64_t(sp.leaf_w.size() / std::max(sp.k, 1));
+        py::dict d;
+        d["depth"] = sp.depth;
+        d["n_trees"] = sp.n_trees;
+        d["k"] = sp.k;
+        d["nodes"] = py::array_t<int32_t>({N, int64_t(4)}, sp.nodes.data());
+        d["roots"] = vec_np(sp.roots);
+        d["leaf_w"] = py::array_t<float>({L, int64_t(sp.k)}, sp.leaf_w.data());
+        d["leaf_has"] = py::array_t<uint8_t>({L, int64_t(sp.k)}, sp.leaf_has.data());
+        d["base_values"] = vec_np(e->base_values);
+        d["post"] = e->post;
+        d["aggregate"] = e->aggregate;
+        d["classifier"] = e->classifier;
+        d["binary_case"] = e->binary_case;
+        d["binary_class"] = e->binary_class & 1;
+        d["weights_all_positive"] = !(e->binary_class & 0x100);
+        d["n_outputs"] = e->n_outputs;
+        d["max_feature"] = e->max_feature;
+        d["classlabels"] = vec_np(e->classlabels);
+        return d;
+      }, py::arg("node_index"))
       .def("tree_complete", [](const exec::Executor& ex, size_t node_index, int32_t limit) {
         const trees::Ensemble* e = ex.ensemble(node_index);
         if (!e) throw std::runtime_error("node is not a TreeEnsemble");

@@ -306,6 +306,45 @@ void post_transform(const Ensemble& e, const float* scores, int64_t n, float* ou
   }
 }
 
+uint32_t node_meta(uint32_t feat, uint32_t mode, uint32_t miss) {
+  return (feat & 0xffff) | (mode << 16) | (miss << 19);
+}
+
+Sparse to_sparse(const Ensemble& e) {
+  Sparse sp;
+  sp.depth = std::max<int32_t>(e.max_depth, 0);
+  sp.n_trees = e.n_trees();
+  sp.k = e.n_targets;
+  size_t total = 0;
+  for (auto& tr : e.trees) total += tr.size();
+  if (total >= (size_t(1) << 31)) throw std::runtime_error("TreeEnsemble: too many nodes for 32-bit indices");
+  sp.nodes.assign(total * 4, 0);
+  sp.roots.resize(e.trees.size());
+  int32_t off = 0;
+  for (size_t t = 0; t < e.trees.size(); ++t) {
+    const auto& tr = e.trees[t];
+    sp.roots[t] = off;  // compile() puts each root at index 0
+    for (size_t i = 0; i < tr.size(); ++i) {
+      const GNode& g = tr[i];
+      int32_t* o = &sp.nodes[(size_t(off) + i) * 4];
+      if (g.mode == LEAF) {
+        o[0] = int32_t(node_meta(0, LEAF, 0));
+        o[2] = g.leaf;
+        continue;
+      }
+      if (g.feat < 0 || g.feat > 0xffff) throw std::runtime_error("TreeEnsemble: feature id out of the device range");
+      o[0] = int32_t(node_meta(uint32_t(g.feat), g.mode, g.miss));
+      std::memcpy(&o[1], &g.thr, 4);
+      o[2] = off + g.t;
+      o[3] = off + g.f;
+    }
+    off += int32_t(tr.size());
+  }
+  sp.leaf_w = e.leaf_w;
+  sp.leaf_has = e.leaf_has;
+  return sp;
+}
+
 Complete to_complete(const Ensemble& e, int32_t max_depth_limit) {
   if (e.max_depth > max_depth_limit)
     throw std::runtime_error("TreeEnsemble: depth " + std::to_string(e.max_depth) +
@@ -320,7 +359,7 @@ Complete to_complete(const Ensemble& e, int32_t max_depth_limit) {
   c.nodes.assign(size_t(c.n_trees) * n_int * 2, 0.f);
   c.leaves.assign(size_t(c.n_trees) * n_leaf * c.k, 0.f);
   auto meta_bits = [](uint32_t feat, uint32_t mode, uint32_t miss) {
-    uint32_t m = (feat & 0xffff) | (mode << 16) | (miss << 19);
+    uint32_t m = node_meta(feat, mode, miss);
     float f;
     std::memcpy(&f, &m, 4);
     return f;

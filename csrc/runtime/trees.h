@@ -62,4 +62,19 @@ struct Complete {
 };
 Complete to_complete(const Ensemble& e, int32_t max_depth_limit = 12);
 
+// Pointer layout for the device's general tree kernel (any depth, any shape): all trees'
+// nodes in one array, 16 B each {meta, threshold bits, true child, false child}; a leaf has
+// mode LEAF and its leaf row in the "true child" slot. Children / leaf rows are global indices.
+struct Sparse {
+  int32_t depth = 0;   // longest root-to-leaf path (edges)
+  int32_t n_trees = 0;
+  int32_t k = 1;
+  std::vector<int32_t> nodes;    // [N][4]
+  std::vector<int32_t> roots;    // [T]
+  std::vector<float> leaf_w;     // [L][K]
+  std::vector<uint8_t> leaf_has; // [L][K]
+};
+Sparse to_sparse(const Ensemble& e);
+uint32_t node_meta(uint32_t feat, uint32_t mode, uint32_t miss);
+
 }  // namespace igp::trees

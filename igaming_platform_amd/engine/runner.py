@@ -93,7 +93,10 @@ class DeviceModel:
         cur = X
         fused_partial = None
         for i, (s, out) in enumerate(zip(steps, self.step_out)):
-            if s.kind == "tree":
+            if s.kind == "tree" and s.layout == "sparse":
+                K.tree_sparse(s, cur, out, bucket, partial=self.tree_partial, groups=self.tree_groups.get(bucket, 1))
+                fused_partial = None
+            elif s.kind == "tree":
                 g = self.tree_groups.get(bucket, 1)
                 fuse = (g > 1 and i + 1 < len(steps) and steps[i + 1].kind == "head" and s.post == 0
                         and s.binary_class < 0 and steps[i + 1].k == s.k)

@@ -4,7 +4,11 @@ The C++ reader parses the file; this module walks the (single-input) chain from 
 input to the primary output and lowers it to fused device steps:
 
 * ``TreeStep``   TreeEnsemble{Classifier,Regressor} (+ a following Sigmoid folded into the
-                 post transform) -> K2 ``tree_ensemble`` on the complete-tree layout.
+                 post transform) -> K2 ``tree_ensemble`` on the complete-tree layout, or K2b
+                 ``tree_sparse`` on the pointer layout for deep (> 12) or very unbalanced trees,
+                 MIN / MAX aggregates and target counts the complete kernel is not built for.
+                 Every post transform (NONE, LOGISTIC, SOFTMAX, SOFTMAX_ZERO, PROBIT) runs on
+                 the device.
 * ``DenseStep``  Gemm / MatMul(+Add) with a following Relu/Sigmoid/Tanh fused into the
                  epilogue -> K3 ``gemm`` (MFMA) or ``gemv`` (N == 1).
 * ``GRUStep``    ONNX GRU (forward, layout 0) -> K4 (cfg 5).
@@ -36,18 +40,26 @@ class TreeStep:
     depth: int
     k: int
     n_out: int
-    post: int            # kernel post code: 0 none, 1 logistic, 2 softmax
+    post: int            # kernel post code (POST): 0 none, 1 logistic, 2 softmax, 3 softmax_zero, 4 probit
     average: int
     binary_class: int    # -1 unless the classifier binary case
     all_positive: int
     max_feature: int
-    nodes_np: np.ndarray
-    leaves_np: np.ndarray
+    nodes_np: np.ndarray  # complete: [T][2^D-1][2] f32; sparse: [N][4] int32
+    leaves_np: Optional[np.ndarray]  # complete: [T][2^D][K]; sparse: None
     base_np: Optional[np.ndarray]
     classifier: bool = False
+    layout: str = "complete"   # complete (K2) | sparse (K2b pointer layout)
+    aggregate: int = 0         # 0 sum, 1 average, 2 min, 3 max
+    roots_np: Optional[np.ndarray] = None     # sparse: [T] root node index
+    leaf_w_np: Optional[np.ndarray] = None    # sparse: [L][K]
+    leaf_has_np: Optional[np.ndarray] = None  # sparse: [L][K] uint8
     nodes: Any = None
     leaves: Any = None
     base: Any = None
+    roots: Any = None
+    leaf_w: Any = None
+    leaf_has: Any = None
     kind: str = "tree"
 
     @property
@@ -58,8 +70,31 @@ class TreeStep:
     def all_leq(self) -> bool:
         """Every node is BRANCH_LEQ (sklearn-style ensembles; missing-value tracks allowed): the
         kernel then skips decoding the comparison mode per node."""
+        if self.layout != "complete":
+            return False
         meta = self.nodes_np.reshape(-1, 2)[:, 1].view(np.uint32)
         return bool(np.all(((meta >> 16) & 0x7) == 0))
+
+
+COMPLETE_K = (1, 2, 4, 8, 16, 32, 64)   # target counts the complete-tree kernel is built for
+SPARSE_MAX_K = 64
+
+
+def choose_tree_layout(info: Dict[str, Any], depth_limit: int = 12) -> str:
+    """complete (K2) when the ensemble fits it without much padding, else sparse (K2b).
+    ``IGP_TREE_LAYOUT=complete|sparse`` forces one (the complete layout still needs SUM /
+    AVERAGE, depth <= ``depth_limit`` and a supported K)."""
+    import os
+    D, T, N, K = int(info["depth"]), int(info["n_trees"]), int(info["n_nodes"]), int(info["k"])
+    fits = int(info["aggregate"]) in (0, 1) and D <= depth_limit and K in COMPLETE_K
+    forced = os.environ.get("IGP_TREE_LAYOUT", "auto")
+    if forced == "sparse" or not fits:
+        return "sparse"
+    if forced == "complete":
+        return "complete"
+    # the complete layout stores 2^(D+1) - 1 slots per tree: keep it when that is within 8x
+    # of the real node count (balanced GBDTs are ~1x; a few deep paths blow it up)
+    return "complete" if T * ((1 << (D + 1)) - 1) <= 8 * max(N, 1) + 64 * T else "sparse"
 
 
 @dataclass
@@ -133,7 +168,7 @@ class Plan:
         parts = []
         for s in self.steps:
             if s.kind == "tree":
-                parts.append(f"tree(T={s.n_trees},D={s.depth},K={s.k},post={s.post})")
+                parts.append(f"tree(T={s.n_trees},D={s.depth},K={s.k},post={s.post},{s.layout})")
             elif s.kind == "dense":
                 parts.append(f"dense({s.k}->{s.n},{s.act})")
             elif s.kind == "head":
@@ -185,27 +220,33 @@ def compile_onnx(model, input_name: str = "input", output_name: str = "output",
         visited.add(id(n))
         op, a = n["op_type"], n["attrs"]
         if op in ("TreeEnsembleClassifier", "TreeEnsembleRegressor"):
-            c = ex.tree_complete(index[id(n)], depth_limit)
-            if c["aggregate"] not in (0, 1):
-                raise PlanError("TreeEnsemble aggregate MIN/MAX is CPU-only")
-            post = {0: 0, 1: 1, 2: 2}.get(int(c["post"]))
-            if post is None:
-                raise PlanError(f"TreeEnsemble post_transform {POST[int(c['post'])]} is CPU-only")
+            info = ex.tree_info(index[id(n)])
+            if int(info["k"]) > SPARSE_MAX_K:
+                raise PlanError(f"TreeEnsemble with {info['k']} targets (> {SPARSE_MAX_K}) is CPU-only")
+            layout = choose_tree_layout(info, depth_limit)
+            c = (ex.tree_complete(index[id(n)], depth_limit) if layout == "complete"
+                 else ex.tree_sparse(index[id(n)]))
+            post = int(c["post"])
             binary = bool(c["binary_case"])
             k = int(c["k"])
             n_out = int(c["n_outputs"]) if c["classifier"] else k
-            base = c["base_values"]
+            base = np.asarray(c["base_values"], np.float32)
             if binary:
-                bv = base[:1] if len(base) == 1 else (base[c["binary_class"]:c["binary_class"] + 1]
-                                                      if len(base) == 2 else None)
-                base = bv
+                base = base[:1] if len(base) == 1 else (base[c["binary_class"]:c["binary_class"] + 1]
+                                                        if len(base) == 2 else None)
+            elif len(base):  # targets past the given base values get 0 (executor semantics)
+                base = np.pad(base[:k], (0, max(0, k - len(base))))
+            sparse = layout == "sparse"
             ts = TreeStep(n_trees=int(c["n_trees"]), depth=int(c["depth"]), k=k, n_out=n_out, post=post,
                           average=int(c["aggregate"] == 1), binary_class=int(c["binary_class"]) if binary else -1,
                           all_positive=int(bool(c["weights_all_positive"])), max_feature=int(c["max_feature"]),
-                          nodes_np=np.ascontiguousarray(c["nodes"], np.float32),
-                          leaves_np=np.ascontiguousarray(c["leaves"], np.float32),
+                          nodes_np=np.ascontiguousarray(c["nodes"], np.int32 if sparse else np.float32),
+                          leaves_np=None if sparse else np.ascontiguousarray(c["leaves"], np.float32),
                           base_np=None if base is None or len(base) == 0 else np.asarray(base, np.float32),
-                          classifier=bool(c["classifier"]))
+                          classifier=bool(c["classifier"]), layout=layout, aggregate=int(c["aggregate"]),
+                          roots_np=np.ascontiguousarray(c["roots"], np.int32) if sparse else None,
+                          leaf_w_np=np.ascontiguousarray(c["leaf_w"], np.float32) if sparse else None,
+                          leaf_has_np=np.ascontiguousarray(c["leaf_has"], np.uint8) if sparse else None)
             steps.append(ts)
             width = n_out
             if c["classifier"]:
@@ -349,6 +390,35 @@ def _f32_padded(w: np.ndarray, n_mult: int = 128, k_mult: int = 64):
 PRECISIONS = ("fp32", "bf16")
 
 
+def validate_sparse(s: TreeStep) -> None:
+    """Host check of a pointer-layout ensemble before it reaches the device: every child / root
+    index is a node, every leaf row exists, and no root-to-leaf path is longer than ``depth``
+    (the kernel's traversal bound), so K2b can only read inside its arrays."""
+    nodes = s.nodes_np.reshape(-1, 4)
+    N, L = nodes.shape[0], s.leaf_w_np.shape[0]
+    if s.leaf_w_np.shape != (L, s.k) or s.leaf_has_np.shape != (L, s.k):
+        raise PlanError("sparse trees: leaf tables must be [L, K]")
+    if s.roots_np.shape != (s.n_trees,) or (s.roots_np < 0).any() or (s.roots_np >= N).any():
+        raise PlanError("sparse trees: root index out of range")
+    mode = (nodes[:, 0].view(np.uint32) >> 16) & 7
+    leaf = mode == 7
+    if ((nodes[leaf, 2] < 0) | (nodes[leaf, 2] >= L)).any():
+        raise PlanError("sparse trees: leaf row out of range")
+    ch = nodes[~leaf][:, 2:4]
+    if ((ch < 0) | (ch >= N)).any():
+        raise PlanError("sparse trees: child index out of range")
+    if (nodes[~leaf, 0].view(np.uint32) & 0xFFFF).max(initial=0) > s.max_feature:
+        raise PlanError("sparse trees: feature id above max_feature")
+    # longest path by level expansion from the roots (bounded by depth + 1 levels)
+    frontier = s.roots_np.astype(np.int64)
+    for _ in range(s.depth + 1):
+        inner = frontier[~leaf[frontier]]
+        if inner.size == 0:
+            return
+        frontier = np.unique(np.concatenate([nodes[inner, 2], nodes[inner, 3]]).astype(np.int64))
+    raise PlanError("sparse trees: a path is longer than the declared depth (cycle?)")
+
+
 def to_device(plan: Plan, device, precision: str = "fp32") -> Plan:
     """Upload the plan's tensors. ``precision`` selects the dense / head weight format:
     ``fp32`` (default) keeps the ONNX model's f32 numerics end to end (f32 MFMA,
@@ -362,8 +432,14 @@ def to_device(plan: Plan, device, precision: str = "fp32") -> Plan:
     for s in plan.steps:
         if s.kind == "tree":
             s.nodes = torch.from_numpy(s.nodes_np).to(device)
-            s.leaves = torch.from_numpy(s.leaves_np).to(device)
             s.base = None if s.base_np is None else torch.from_numpy(s.base_np).to(device)
+            if s.layout == "sparse":
+                validate_sparse(s)
+                s.roots = torch.from_numpy(s.roots_np).to(device)
+                s.leaf_w = torch.from_numpy(s.leaf_w_np).to(device)
+                s.leaf_has = torch.from_numpy(s.leaf_has_np).to(device)
+            else:
+                s.leaves = torch.from_numpy(s.leaves_np).to(device)
         elif s.kind == "dense":
             s.w = pad(s.w_np).to(device)
             s.b = None if s.b_np is None else torch.from_numpy(np.ascontiguousarray(s.b_np)).to(device)

@@ -49,11 +49,14 @@ def gradient_boosting(est, n_features: int, input_name: str = "input", output_na
                  metadata={"family": "gbdt", "source": "sklearn"})
 
 
-def random_forest(est, n_features: int, input_name: str = "input", output_name: str = "output"):
-    """RandomForestRegressor -> TreeEnsembleRegressor with AVERAGE aggregation."""
+def random_forest(est, n_features: int, input_name: str = "input", output_name: str = "output",
+                  aggregate: str = "AVERAGE", post_transform: str = "NONE"):
+    """RandomForestRegressor -> TreeEnsembleRegressor with AVERAGE aggregation (``aggregate``
+    MIN / MAX / SUM and a ``post_transform`` give the other TreeEnsemble variants over the same
+    fitted trees: the device parity tests use them)."""
     trees = [_tree_dict(t, 1.0) for t in est.estimators_]
     a = tree_attrs(trees, "target")
-    a.update(n_targets=1, aggregate_function="AVERAGE", post_transform="NONE")
+    a.update(n_targets=1, aggregate_function=aggregate, post_transform=post_transform)
     return model([node("TreeEnsembleRegressor", [input_name], [output_name], domain="ai.onnx.ml", **a)],
                  [value_info(input_name, S.FLOAT, ["N", n_features])],
                  [value_info(output_name, S.FLOAT, ["N", 1])], name="sklearn_rf", metadata={"family": "gbdt"})

@@ -176,6 +176,34 @@ def tree_ensemble(tp, X: torch.Tensor, out: Optional[torch.Tensor], n_rows: int,
     _mod().tree_ensemble(d, _stream())
 
 
+def tree_sparse(tp, X: torch.Tensor, out: torch.Tensor, n_rows: int, partial: Optional[torch.Tensor] = None,
+                groups: int = 1) -> None:
+    """K2b: ``tp`` a sparse-layout TreeStep with device tensors (pointer layout validated by
+    :func:`models.plan.validate_sparse` at upload). ``partial``: [groups, rows, K] scratch."""
+    dev = X.device
+    if tp.layout != "sparse":
+        raise ValueError("tree_sparse needs a sparse-layout TreeStep")
+    if X.shape[1] <= tp.max_feature:
+        raise ValueError("X narrower than the ensemble's largest feature id")
+    if groups > 1 and (partial is None or partial.numel() < groups * n_rows * tp.k):
+        raise ValueError("grouped tree launch needs a [groups, rows, K] partial buffer")
+    n_nodes = tp.nodes.shape[0]
+    d = dict(X=_need(X, "X", torch.float32, X.shape[1] * n_rows, device=dev),
+             nodes=_need(tp.nodes, "nodes", torch.int32, 4 * n_nodes, device=dev),
+             roots=_need(tp.roots, "roots", torch.int32, tp.n_trees, device=dev),
+             leaf_w=_need(tp.leaf_w, "leaf_w", torch.float32, device=dev),
+             leaf_has=_need(tp.leaf_has, "leaf_has", torch.uint8, tp.leaf_w.numel(), device=dev),
+             base=_opt(tp.base, "base", dtype=torch.float32, min_numel=1 if tp.binary_class >= 0 else tp.k),
+             out=_need(out, "out", torch.float32, tp.n_out * n_rows, device=dev), x_stride=int(X.shape[1]),
+             n_rows=int(n_rows), n_trees=tp.n_trees, depth=tp.depth, k=tp.k, n_out=tp.n_out, post=tp.post,
+             aggregate=tp.aggregate, binary_class=tp.binary_class, all_positive=tp.all_positive,
+             feat_w=int(max(tp.max_feature, 0) + 1), groups=int(groups),
+             partial=_opt(partial, "partial", dtype=torch.float32))
+    if out.dim() == 2 and out.shape[1] != tp.n_out:
+        raise ValueError("out must have n_out columns")
+    _mod().tree_sparse(d, _stream())
+
+
 # --------------------------------------------------------------------------- K3
 def dense(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], Y: torch.Tensor,
           M: int, N: int, K: int, act: str = "none", m_ptr: Optional[torch.Tensor] = None) -> None:
