@@ -294,6 +294,24 @@ def dp_bench(a, world: int, rank: int, dev) -> None:
                 dist.all_reduce(met_sum)
         return p
 
+    # probe: two steps under a deadline (event wait; past it the communicators are aborted), so a
+    # broken or hung exchange on a new node falls back to replicas instead of hanging the bench
+    ok, err = 1, ""
+    try:
+        for i in range(2):
+            sc.wait_x(step(i, NOW0), gather=False, timeout_s=float(os.environ.get("IGP_XCHG_PROBE_S", "60")))
+    except Exception as e:
+        ok, err = 0, f"{type(e).__name__}: {e}"
+        sc.abort_exchange()
+    if world > 1:
+        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        ok = int(flag.item())
+    if not ok:
+        print(json.dumps({"warning": "exchange probe failed; replicas fallback", "rank": rank, "error": err}),
+              file=sys.stderr, flush=True)
+        a.dp_mode = "replicas (exchange probe failed)"
+        return None
     inflight, lat, rows = [], [], 0
     for i in range(a.warmup):
         inflight.append(step(i, NOW0 + i // 50))

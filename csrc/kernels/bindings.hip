@@ -146,6 +146,11 @@ PYBIND11_MODULE(_hipk, m) {
     return reinterpret_cast<uintptr_t>(st);
   });
 
+  m.def("cu_stream_destroy", [](uintptr_t st) {
+    const hipError_t e = hipStreamDestroy(reinterpret_cast<hipStream_t>(st));
+    if (e != hipSuccess) throw std::runtime_error(std::string("hipStreamDestroy: ") + hipGetErrorString(e));
+  });
+
   m.def("feature_update", [](py::dict d, uintptr_t s) {
     UpdateArgs a = update_args(d);
     if (geti(d, "segments_only")) launch_update_segments(a, stream_of(s));

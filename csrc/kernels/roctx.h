@@ -3,12 +3,16 @@
 #pragma once
 #include <dlfcn.h>
 
+#include <cstdlib>
+
 namespace igp {
 
 struct Roctx {
   int (*push)(const char*) = nullptr;
   int (*pop)() = nullptr;
   Roctx() {
+    const char* env = std::getenv("IGP_ROCTX");  // IGP_ROCTX=0: no ranges, no profiler library load
+    if (env && env[0] == '0') return;
     void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
     if (!h) h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_LOCAL);
     if (h) {

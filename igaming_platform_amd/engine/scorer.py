@@ -56,6 +56,20 @@ REQ_BYTES = REQREC.itemsize
 _CU_STREAMS: Dict[tuple, tuple] = {}  # (device, split) -> CU-masked (state, copy, model) streams
 
 
+def _destroy_cu_streams() -> None:
+    """Interpreter exit: drain and destroy the CU-masked streams while the HIP runtime (and a
+    profiler attached to it) is still up, instead of leaving them to runtime teardown."""
+    import torch
+    for key, streams in list(_CU_STREAMS.items()):
+        try:
+            for st in streams:
+                st.synchronize()
+                K._mod().cu_stream_destroy(st.cuda_stream)
+        except Exception:  # best effort at exit
+            pass
+    _CU_STREAMS.clear()
+
+
 class _Slot:
     """Device buffers of one pipeline slot (slab, model input/output, results)."""
 
@@ -165,6 +179,9 @@ class GpuScorer:
             with torch.cuda.device(self.device):
                 _CU_STREAMS[key] = tuple(torch.cuda.ExternalStream(K._mod().cu_stream(words(m)), device=self.device)
                                          for m in masks)
+            if len(_CU_STREAMS) == 1:
+                import atexit
+                atexit.register(_destroy_cu_streams)
         self.stream, self.cstream, self.mstream = _CU_STREAMS[key][:3]
         self.comm_streams = _CU_STREAMS[key][3:]
 
