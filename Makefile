@@ -8,7 +8,7 @@ STEPS     ?= 300
 WARMUP    ?= 30
 CONFIG    ?= cfg3
 
-.PHONY: all build build-sanitize test test-gpu test-dist lint bench bench-all profile serve serve-spmd \
+.PHONY: all build build-sanitize test-sanitize test test-gpu test-dist lint bench bench-all profile serve serve-spmd \
         wallet bonus-validate models api-test health clean help
 
 all: build
@@ -18,6 +18,9 @@ build: ## compile the C++ runtime (_native) and the gfx950 HIP kernels (_hipk) i
 
 build-sanitize: ## host runtime with ASan/UBSan (GPU sanitizers are not available on the pool)
 	$(PY) -m igaming_platform_amd._build --sanitize
+
+test-sanitize: build ## native / engine / API tests against the ASan+UBSan host runtime (child interpreter)
+	$(PY) -m pytest tests/test_sanitize.py -q
 
 test: build ## CPU suite (golden, native runtime, engine, API, clients, gloo multi-process)
 	$(PY) -m pytest tests -q -m "not gpu"

@@ -447,7 +447,7 @@ PYBIND11_MODULE(_native, m) {
         auto load = [&](const char* k, void* dst, size_t nbytes) {
           py::array a = d[k].cast<py::array>();
           if ((size_t)a.nbytes() != nbytes) throw std::runtime_error(std::string("state size mismatch: ") + k);
-          std::memcpy(dst, py::array::ensure(a, py::array::c_style).data(), nbytes);
+          if (nbytes) std::memcpy(dst, py::array::ensure(a, py::array::c_style).data(), nbytes);  // empty: dst may be null
         };
         load("ring_ts", c.ring_ts.data(), c.ring_ts.size() * 4);
         load("ring_amt", c.ring_amt.data(), c.ring_amt.size() * 8);

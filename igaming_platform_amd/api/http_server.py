@@ -13,8 +13,6 @@ import threading
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from urllib.parse import parse_qs, urlparse
 
-import numpy as np
-
 from ..layouts import FEATREC
 from ..obs.logging import get_logger
 
@@ -22,17 +20,19 @@ log = get_logger("http")
 
 
 def _device_metrics(engine) -> bytes:
-    """K10 device histograms (per shard, summed) in Prometheus text format."""
-    tot = None
-    for be in engine.backends:
-        m = be.metrics() if hasattr(be, "metrics") else None
-        if m is not None:
-            tot = m.astype(np.int64) if tot is None else tot + m
-    if tot is None:
+    """K10 device counters in Prometheus text format: whole-group totals, plus the rows each
+    shard scored (SPMD: one all-reduce of every rank's counter block, OP_METRICS) so owner skew
+    across GPUs is visible."""
+    per = engine.shard_metrics() if hasattr(engine, "shard_metrics") else None
+    if per is None:
         return b""
+    tot = per.sum(0)
     lines = ["# HELP risk_device_rows_total rows scored on the GPUs (K10 counters)",
              "# TYPE risk_device_rows_total counter", f"risk_device_rows_total {int(tot[106])}",
-             "# HELP risk_device_action_total decisions counted on the GPUs", "# TYPE risk_device_action_total counter"]
+             "# HELP risk_shard_rows_total rows scored by each shard (owner-routed DP)",
+             "# TYPE risk_shard_rows_total counter"]
+    lines += [f'risk_shard_rows_total{{shard="{o}"}} {int(per[o, 106])}' for o in range(per.shape[0])]
+    lines += ["# HELP risk_device_action_total decisions counted on the GPUs", "# TYPE risk_device_action_total counter"]
     for a, name in ((1, "approve"), (2, "review"), (3, "block")):
         lines.append(f'risk_device_action_total{{action="{name}"}} {int(tot[101 + a])}')
     lines += ["# HELP risk_device_score_total final-score histogram counted on the GPUs",

@@ -178,7 +178,8 @@ class RiskEngine:
             if backend == "gpu":
                 from ..models.plan import compile_onnx, to_device
                 dev = f"cuda:{self.devices[0]}"
-                g = LtvGpu(dev, self.capacity, to_device(compile_onnx(lm), dev, cfg.ltv_model.precision) if lm is not None else None,
+                lplan = to_device(compile_onnx(lm), dev, cfg.ltv_model.precision) if lm is not None else None
+                g = LtvGpu(dev, self.capacity, lplan,
                            buckets=cfg.gpu.buckets, in_width=ltv_width, use_graphs=capture)
                 g.capture()
                 lg = [g]
@@ -760,6 +761,21 @@ class RiskEngine:
             self._flush_links()
         keys = self.links.linked((int(owner) << 32) | int(slot), limit)
         return [self.registry.id_of(int(k) >> 32, int(k) & 0xFFFFFFFF) for k in keys]
+
+    def shard_metrics(self) -> Optional[np.ndarray]:
+        """[shards, 128] K10 device counters per shard (SPMD: one all-reduce over the group;
+        CPU shards report only their row count), or None when no shard keeps device counters."""
+        g = self.group
+        if g is not None:
+            try:
+                return g.shard_metrics()
+            except GroupFailure:
+                return None
+        rows = []
+        for be in self.backends:
+            m = be.metrics() if hasattr(be, "metrics") and be.kind == "gpu" else None
+            rows.append(np.zeros(128, np.int64) if m is None else np.asarray(m, np.int64)[:128])
+        return np.stack(rows) if any(r.any() for r in rows) else None
 
     # ---- health / durability
     def close(self) -> None:

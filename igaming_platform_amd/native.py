@@ -20,11 +20,26 @@ def _autobuild_enabled() -> bool:
     return os.environ.get("IGP_AUTOBUILD", "1") != "0"
 
 
+def _load_so(name: str, path: str):
+    """Import extension ``name`` from an explicit file (IGP_NATIVE_SO: the ASan/UBSan build)."""
+    import importlib.util
+    import sys
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    sys.modules[name] = mod
+    return mod
+
+
 def native():
     global _native
     if _native is None:
         with _lock:
             if _native is None:
+                so = os.environ.get("IGP_NATIVE_SO")
+                if so:
+                    _native = _load_so("igaming_platform_amd._native", so)
+                    return _native
                 try:
                     _native = importlib.import_module("igaming_platform_amd._native")
                 except ImportError:

@@ -2,7 +2,8 @@
 
 Names used by the engine: ``backend_error`` (a shard's scoring step raises -> the shard is
 marked unhealthy and its rows go to the CPU fallback), ``gpu_timeout:ms=N`` (a real N ms
-device stall is queued ahead of the shard's batch, so the watchdog deadline fires), ``model_error`` (ML fails -> ml_error_score, engine.go:279-282),
+device stall is queued ahead of the shard's batch, so the watchdog deadline fires),
+``model_error`` (ML fails -> ml_error_score, engine.go:279-282),
 ``feature_store_down`` (features unavailable -> partial features, engine.go:267-270).
 """
 from __future__ import annotations

@@ -78,8 +78,9 @@ def _worker(rank, world, port, snap_dir, q):
             eng = RiskEngine(cfg, backend="cpu", capacity=200, spmd=comm)
             res = _script(eng, snap_dir)
             rows0 = eng.group.runner.rows_scored
+            shard_rows = eng.shard_metrics()[:, 106].tolist()  # OP_METRICS all-reduce (/metrics)
             eng.close()
-            q.put(("ok", res, rows0))
+            q.put(("ok", res, rows0, shard_rows))
         else:
             n, rows = serve_shard(cfg, comm, backend="cpu", capacity=200)
             q.put(("served", n, rows, rank))
@@ -118,6 +119,7 @@ def test_spmd_serving_matches_single_process(world, tmp_path):
     rows = {0: next(m[2] for m in msgs if m[0] == "ok")}
     rows.update({m[3]: m[2] for m in served})
     assert [rows[r] for r in range(world)] == want.tolist()
+    assert next(m[3] for m in msgs if m[0] == "ok") == want.tolist()   # the same counts through /metrics
     # every rank wrote its own shard file; rank 0 the registry
     names = sorted(os.listdir(tmp_path / "spmd"))
     assert names == ["registry.json"] + [f"shard{r}.npz" for r in range(world)]

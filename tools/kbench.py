@@ -122,7 +122,8 @@ def main():
           ts_k1.append(e0.elapsed_time(e1) * 1e3)
           if var not in ("nodedup", "noseg"):
               K.update_segments(sc.store, sc.cfg_dev, sc.req, B, sc.hdr)
-      print(f"[{var}] K1+update on rotating pool batches: median {np.median(ts_k1[8:]):.1f} us (first pass {np.median(ts_k1[:8]):.1f})")
+      print(f"[{var}] K1+update on rotating pool batches: median {np.median(ts_k1[8:]):.1f} us "
+            f"(first pass {np.median(ts_k1[:8]):.1f})")
       t = tr.cpu().numpy().reshape(8, 8)[:, :6].astype(np.float64)
       t0 = t[t > 0].min()
       print("K1 trace (update, rotating batches) us: start / level1 / level2 / compute / stores / end")
@@ -143,7 +144,8 @@ def main():
             print("mlp_head trace us: start / staged / mfma done / synced / stored")
             for b in range(8):
                 print("   block", b * 32, [round((x - t0) / 100.0, 2) if x > 0 else None for x in t[b]])
-    res = {k: dict(median_us=float(np.median(v[min(5, len(v) - 1):])), min_us=float(np.min(v[min(5, len(v) - 1):]))) for k, v in times.items()}
+    res = {k: dict(median_us=float(np.median(v[min(5, len(v) - 1):])), min_us=float(np.min(v[min(5, len(v) - 1):])))
+           for k, v in times.items()}
     for k, v in res.items():
         print(f"{k:28s} median {v['median_us']:8.1f} us   min {v['min_us']:8.1f} us")
     if a.out:
