@@ -10,15 +10,26 @@
 // (rocprofv3 timeline: GPU 58 % busy). The driver issues the same sequence with raw HIP calls
 // on the graphs' exec handles, writes the batch header and copies the packed request rows
 // into the pinned slab itself, all with the GIL released.
+//
+// Asynchronous issue (set_async(true)): submit() only queues the batch; a driver thread of its
+// own does the row copy, the header and the launches, so the caller's per-batch Python work
+// (pool selection, bookkeeping, the wait for an older batch) overlaps the ~40 us of HIP calls
+// instead of adding to them. wait(slot) / query(slot) / model_event(slot) first wait for the
+// slot's queued batch to be issued; issue errors resurface on the next call.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 
 #include <dlfcn.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <exception>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -46,9 +57,22 @@ class PipeDriver {
     ev_.resize(3 * depth);
     for (auto& e : ev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event create");
     recorded_.assign(3 * depth, false);
+    host_done_.assign(depth, 0);
   }
   ~PipeDriver() {
+    stop_worker();
     for (auto& e : ev_) (void)hipEventDestroy(e);
+  }
+
+  void set_async(bool on) {
+    if (on && !worker_.joinable()) {
+      pending_.assign(depth_, 0);
+      stop_ = false;
+      worker_ = std::thread([this] { loop(); });
+    } else if (!on) {
+      stop_worker();
+    }
+    async_ = on;
   }
 
   void set_graphs(int bucket, int slot, uintptr_t gc, uintptr_t gs, uintptr_t gm, uintptr_t gmf) {
@@ -62,10 +86,86 @@ class PipeDriver {
   // model graph); the caller must not repack a slot's pinned slab before wait(slot) of its
   // previous batch returned.
   void submit(int slot, int bucket, int n, int seq, int64_t now, uintptr_t rows, bool with_features) {
+    if (slot < 0 || slot >= depth_) throw std::runtime_error("PipeDriver: bad slot");
     auto it = graphs_.find(key(bucket, slot));
     if (it == graphs_.end()) throw std::runtime_error("PipeDriver: no graphs for this bucket/slot");
-    const Graphs g = it->second;
+    const Cmd c{slot, n, seq, now, rows, with_features, it->second};
+    if (async_) {
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        rethrow_locked();
+        q_.push_back(c);
+        ++pending_[slot];
+      }
+      cv_.notify_one();
+      return;
+    }
     py::gil_scoped_release nogil;
+    issue(c);
+  }
+
+ private:
+  struct Graphs {
+    hipGraphExec_t c, s, m, mf;  // mf: model graph that also copies the FeatRec rows to the host
+  };
+  struct Cmd {
+    int slot, n, seq;
+    int64_t now;
+    uintptr_t rows;
+    bool with_features;
+    Graphs g;
+  };
+
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;
+      const Cmd c = q_.front();
+      q_.pop_front();
+      lk.unlock();
+      std::exception_ptr err;
+      try {
+        issue(c);
+      } catch (...) {
+        err = std::current_exception();
+      }
+      lk.lock();
+      if (err && !err_) err_ = err;
+      --pending_[c.slot];
+      done_cv_.notify_all();
+    }
+  }
+  void stop_worker() {
+    if (!worker_.joinable()) return;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    worker_.join();
+  }
+  void rethrow_locked() {
+    if (err_) {
+      std::exception_ptr e = err_;
+      err_ = nullptr;
+      std::rethrow_exception(e);
+    }
+  }
+  // async mode: block until the slot's queued batches are issued
+  void drain_slot(int slot) {
+    if (!async_) return;
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return pending_[slot] == 0; });
+    rethrow_locked();
+  }
+
+  void issue(const Cmd& cmd) {
+    const int slot = cmd.slot, n = cmd.n, seq = cmd.seq;
+    const int64_t now = cmd.now;
+    const uintptr_t rows = cmd.rows;
+    const bool with_features = cmd.with_features;
+    const Graphs g = cmd.g;
     Range range("igp.submit");
     const auto t0 = clk::now();
     char* slab = slabs_[slot];
@@ -76,7 +176,9 @@ class PipeDriver {
     h->seq = seq;
     h->now = now;
     hipEvent_t ce = ev_[3 * slot], se = ev_[3 * slot + 1], me = ev_[3 * slot + 2];
-    if (recorded_[3 * slot + 2]) hip_ok(hipStreamWaitEvent(cs_, me, 0), "wait model");
+    // the slot's previous batch: skipped when the host already saw it complete (wait(slot))
+    if (recorded_[3 * slot + 2] && !host_done_[slot]) hip_ok(hipStreamWaitEvent(cs_, me, 0), "wait model");
+    host_done_[slot] = 0;
     if (hist_.size() == 2) hip_ok(hipStreamWaitEvent(cs_, ev_[3 * hist_.front() + 1], 0), "wait state-2");
     const auto t2 = clk::now();
     hip_ok(hipGraphLaunch(g.c, cs_), "copy graph");
@@ -105,11 +207,15 @@ class PipeDriver {
     if (hist_.size() > 2) hist_.erase(hist_.begin());
   }
 
+ public:
   void wait(int slot) {
+    if (slot < 0 || slot >= depth_) throw std::runtime_error("PipeDriver: bad slot");
     py::gil_scoped_release nogil;
+    drain_slot(slot);
     Range range("igp.wait");
     const auto t0 = clk::now();
     hip_ok(hipEventSynchronize(ev_[3 * slot + 2]), "sync model");
+    host_done_[slot] = 1;
     st_[6] += std::chrono::duration<double, std::micro>(clk::now() - t0).count();
   }
 
@@ -129,26 +235,44 @@ class PipeDriver {
     return d;
   }
 
-  bool query(int slot) { return hipEventQuery(ev_[3 * slot + 2]) == hipSuccess; }
+  bool query(int slot) {
+    if (async_) {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (pending_[slot] > 0) return false;
+    }
+    return hipEventQuery(ev_[3 * slot + 2]) == hipSuccess;
+  }
 
-  // the state-stream event of the last submitted batch (callers that must order host work after
-  // the store update, e.g. snapshots, sync the whole device instead)
-  uintptr_t model_event(int slot) const { return reinterpret_cast<uintptr_t>(ev_[3 * slot + 2]); }
+  // the slot's model-stream event (completes with its batch; async mode: after it is issued)
+  uintptr_t model_event(int slot) {
+    {
+      py::gil_scoped_release nogil;
+      drain_slot(slot);
+    }
+    return reinterpret_cast<uintptr_t>(ev_[3 * slot + 2]);
+  }
 
  private:
   using clk = std::chrono::steady_clock;
   double st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  struct Graphs {
-    hipGraphExec_t c, s, m, mf;  // mf: model graph that also copies the FeatRec rows to the host
-  };
   static int64_t key(int bucket, int slot) { return ((int64_t)bucket << 8) | slot; }
   hipStream_t cs_, ss_, ms_;
   int depth_;
   std::vector<char*> slabs_;
   std::vector<hipEvent_t> ev_;
   std::vector<bool> recorded_;
+  std::vector<uint8_t> host_done_;  // wait(slot) returned since the slot's last submit (bytes: set by waiter threads)
   std::vector<int> hist_;  // slots of the last two submitted batches, oldest first
   std::unordered_map<int64_t, Graphs> graphs_;
+  // async issue
+  bool async_ = false;
+  bool stop_ = false;
+  std::thread worker_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::deque<Cmd> q_;
+  std::vector<int> pending_;
+  std::exception_ptr err_;
 };
 
 }  // namespace
@@ -161,6 +285,7 @@ void register_driver(py::module_& m) {
       .def("wait", &PipeDriver::wait)
       .def("query", &PipeDriver::query)
       .def("model_event", &PipeDriver::model_event)
+      .def("set_async", &PipeDriver::set_async)
       .def("stats", &PipeDriver::stats);
 }
 

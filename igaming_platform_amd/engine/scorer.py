@@ -39,7 +39,7 @@ import os
 import threading
 import time
 from dataclasses import dataclass
-from typing import Dict, Optional
+from typing import Any, Dict, Optional
 
 import numpy as np
 import torch
@@ -82,6 +82,7 @@ class Pending:
     event: "torch.cuda.Event"
     t_submit: float
     want_features: bool
+    keep: Any = None   # request rows the native driver still reads (asynchronous issue)
 
 
 class GpuScorer:
@@ -303,6 +304,9 @@ class GpuScorer:
             for (b, slot), g in self.graphs.items():
                 d.set_graphs(b, slot, g[0].raw_cuda_graph_exec(), g[1].raw_cuda_graph_exec(),
                              g[2].raw_cuda_graph_exec(), g[3].raw_cuda_graph_exec())
+            # IGP_ASYNC_SUBMIT=1: the driver's own thread issues each batch (csrc/kernels/driver.hip)
+            if os.environ.get("IGP_ASYNC_SUBMIT", "0") == "1":
+                d.set_async(True)
             self.driver = d
 
     # ------------------------------------------------------------------ streaming (one launch per batch)
@@ -433,7 +437,7 @@ class GpuScorer:
                                bool(want_features))
             self._cur = slot
             self.batches += 1
-            return Pending(slot, n, b, None, t0, want_features)
+            return Pending(slot, n, b, None, t0, want_features, keep=rows)
         if rows is not None:
             self.pack(slot, rows)
         self._write_hdr(slot, n, now)
