@@ -4,10 +4,12 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "launch.h"
+#include "oplist.h"
 
 namespace py = pybind11;
 using namespace igp;
@@ -76,7 +78,25 @@ void check(const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// launch now on stream s, or (record mode, oplist.h) append the launch to the list being built
+template <class F>
+void launch_or_record(F f, uintptr_t s, const char* what) {
+  if (OpList* r = recording()) {
+    r->ops.emplace_back(std::move(f));
+    return;
+  }
+  f(stream_of(s));
+  check(what);
+}
+
 }  // namespace
+
+namespace igp {
+OpList*& recording() {
+  thread_local OpList* cur = nullptr;
+  return cur;
+}
+}  // namespace igp
 
 namespace igp {
 void register_driver(py::module_& m);
@@ -133,8 +153,30 @@ PYBIND11_MODULE(_hipk, m) {
       const char* xe = getenv("IGP_K1_EXP");
       a.exp_flags = xe ? atoi(xe) : 0;
     }
-    launch_feature_assemble(a, stream_of(s));
-    check("feature_assemble");
+    launch_or_record([a](hipStream_t st) { launch_feature_assemble(a, st); }, s, "feature_assemble");
+  });
+
+  // record mode (oplist.h): launches between record_begin() and record_end() are stored, not run
+  py::class_<OpList, std::shared_ptr<OpList>>(m, "OpList").def_property_readonly(
+      "size", [](const OpList& o) { return o.ops.size(); });
+  m.def("record_begin", []() {
+    if (recording()) throw std::runtime_error("record_begin: already recording on this thread");
+    recording() = new OpList();
+  });
+  m.def("record_end", []() {
+    OpList* r = recording();
+    if (!r) throw std::runtime_error("record_end: not recording");
+    recording() = nullptr;
+    return std::shared_ptr<OpList>(r);
+  });
+  // stream-ordered copy between pinned host and device memory (recordable)
+  m.def("memcpy_async", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t s) {
+    if (!dst || !src) throw std::runtime_error("memcpy_async: null pointer");
+    launch_or_record([dst, src, n](hipStream_t st) {
+      const hipError_t e = hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n,
+                                          hipMemcpyDefault, st);
+      if (e != hipSuccess) throw std::runtime_error(std::string("memcpy_async: ") + hipGetErrorString(e));
+    }, s, "memcpy_async");
   });
 
   // a stream whose kernels run only on the CUs set in `mask` (32 CUs per word): lets the
@@ -153,10 +195,12 @@ PYBIND11_MODULE(_hipk, m) {
 
   m.def("feature_update", [](py::dict d, uintptr_t s) {
     UpdateArgs a = update_args(d);
-    if (geti(d, "segments_only")) launch_update_segments(a, stream_of(s));
-    else if (geti(d, "insert_only")) launch_dedup_insert(a, stream_of(s));
-    else launch_feature_update(a, stream_of(s));
-    check("feature_update");
+    const int mode = geti(d, "segments_only") ? 1 : geti(d, "insert_only") ? 2 : 0;
+    launch_or_record([a, mode](hipStream_t st) {
+      if (mode == 1) launch_update_segments(a, st);
+      else if (mode == 2) launch_dedup_insert(a, st);
+      else launch_feature_update(a, st);
+    }, s, "feature_update");
   });
 
   m.def("tree_ensemble", [](py::dict d, uintptr_t s) {
@@ -181,8 +225,9 @@ PYBIND11_MODULE(_hipk, m) {
     a.all_leq = geti(d, "all_leq", 0);
     a.trace = ptr<int64_t*>(d, "trace");
     const int groups = geti(d, "groups", 1);
-    launch_tree_ensemble_grouped(a, groups, ptr<float*>(d, "partial"), stream_of(s));
-    check("tree_ensemble");
+    float* partial = ptr<float*>(d, "partial");
+    launch_or_record([a, groups, partial](hipStream_t st) { launch_tree_ensemble_grouped(a, groups, partial, st); },
+                     s, "tree_ensemble");
   });
 
   m.def("tree_sparse", [](py::dict d, uintptr_t s) {
@@ -214,8 +259,8 @@ PYBIND11_MODULE(_hipk, m) {
     if (a.depth < 0 || a.depth > 4096) throw std::runtime_error("tree_sparse: depth");
     if (groups < 1 || (groups > 1 && !partial)) throw std::runtime_error("tree_sparse: grouped launch needs partial");
     if (a.binary_class >= 0 ? a.n_out != 2 : a.n_out != a.k) throw std::runtime_error("tree_sparse: n_out");
-    launch_tree_sparse(a, groups, partial, stream_of(s));
-    check("tree_sparse");
+    launch_or_record([a, groups, partial](hipStream_t st) { launch_tree_sparse(a, groups, partial, st); }, s,
+                     "tree_sparse");
   });
 
   auto gemm_args = [](const py::dict& d) {
@@ -238,12 +283,12 @@ PYBIND11_MODULE(_hipk, m) {
     return a;
   };
   m.def("gemm", [gemm_args](py::dict d, uintptr_t s) {
-    launch_gemm(gemm_args(d), stream_of(s));
-    check("gemm");
+    const GemmArgs a = gemm_args(d);
+    launch_or_record([a](hipStream_t st) { launch_gemm(a, st); }, s, "gemm");
   });
   m.def("gemv", [gemm_args](py::dict d, uintptr_t s) {
-    launch_gemv(gemm_args(d), stream_of(s));
-    check("gemv");
+    const GemmArgs a = gemm_args(d);
+    launch_or_record([a](hipStream_t st) { launch_gemv(a, st); }, s, "gemv");
   });
 
   m.def("mlp_head", [](py::dict d, uintptr_t s) {
@@ -277,14 +322,12 @@ PYBIND11_MODULE(_hipk, m) {
       if (!a.ens.hdr || !a.ens.cfg || !a.ens.feat || !a.ens.out) throw std::runtime_error("mlp_head: ensemble args");
     }
     if (a.k_pad % 32 || a.k_pad < a.K) throw std::runtime_error("mlp_head: k_pad must be a multiple of 32 >= K");
-    launch_mlp_head(a, stream_of(s));
-    check("mlp_head");
+    launch_or_record([a](hipStream_t st) { launch_mlp_head(a, st); }, s, "mlp_head");
   });
 
   m.def("ensemble", [](py::dict d, uintptr_t s) {
     const EnsembleArgs a = ensemble_args(d);
-    launch_ensemble(a, stream_of(s));
-    check("ensemble");
+    launch_or_record([a](hipStream_t st) { launch_ensemble(a, st); }, s, "ensemble");
   });
 
   m.def("ltv", [](py::dict d, uintptr_t s) {
@@ -294,8 +337,7 @@ PYBIND11_MODULE(_hipk, m) {
     a.slots = ptr<const int32_t*>(d, "slots");
     a.out = ptr<float*>(d, "out");
     a.B = geti(d, "B");
-    launch_ltv(a, stream_of(s));
-    check("ltv");
+    launch_or_record([a](hipStream_t st) { launch_ltv(a, st); }, s, "ltv");
   });
   m.def("ltv_assemble", [](py::dict d, uintptr_t s) {
     LtvAssembleArgs a{};
@@ -308,8 +350,7 @@ PYBIND11_MODULE(_hipk, m) {
     a.m_ptr = ptr<const int32_t*>(d, "m_ptr");
     a.n_rows = geti(d, "n_rows");
     if (!a.slots || !a.pf_tab || !a.X || a.x_w < 25) throw std::runtime_error("ltv_assemble: bad args");
-    launch_ltv_assemble(a, stream_of(s));
-    check("ltv_assemble");
+    launch_or_record([a](hipStream_t st) { launch_ltv_assemble(a, st); }, s, "ltv_assemble");
   });
   m.def("gru", [](py::dict d, uintptr_t s) {
     GruArgs a{};
@@ -359,6 +400,7 @@ PYBIND11_MODULE(_hipk, m) {
     if (a.mode == 1 && (!a.ev || !a.rt || !a.slots || a.ev_ring < a.T)) throw std::runtime_error("gru: event-ring input");
     if (a.mode == 0 && (!a.X || a.x_rows < a.n_rows)) throw std::runtime_error("gru: dense input");
     if (a.head_w && !a.out) throw std::runtime_error("gru: head needs out");
+    if (recording()) throw std::runtime_error("gru: not recordable (host-side scratch resets); use graphs");
     launch_gru(a, stream_of(s));
     check("gru");
   });
@@ -407,7 +449,6 @@ PYBIND11_MODULE(_hipk, m) {
     if (!a.slots && !a.X) throw std::runtime_error("mlp_chain: input");
     if (a.slots && !a.pf_tab) throw std::runtime_error("mlp_chain: LTV gather needs the profile table");
     if (a.ltv_out && !a.slots) throw std::runtime_error("mlp_chain: the K9 epilogue needs slots");
-    launch_mlp_chain(a, stream_of(s));
-    check("mlp_chain");
+    launch_or_record([a](hipStream_t st) { launch_mlp_chain(a, st); }, s, "mlp_chain");
   });
 }

@@ -26,6 +26,7 @@
 #include <cstring>
 #include <deque>
 #include <exception>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -34,6 +35,7 @@
 #include <vector>
 
 #include "../include/records.h"
+#include "oplist.h"
 #include "roctx.h"
 
 namespace py = pybind11;
@@ -77,8 +79,22 @@ class PipeDriver {
 
   void set_graphs(int bucket, int slot, uintptr_t gc, uintptr_t gs, uintptr_t gm, uintptr_t gmf) {
     if (slot < 0 || slot >= depth_) throw std::runtime_error("PipeDriver: bad slot");
-    graphs_[key(bucket, slot)] = {reinterpret_cast<hipGraphExec_t>(gc), reinterpret_cast<hipGraphExec_t>(gs),
-                                  reinterpret_cast<hipGraphExec_t>(gm), reinterpret_cast<hipGraphExec_t>(gmf)};
+    Graphs& g = graphs_[key(bucket, slot)];
+    g.c = reinterpret_cast<hipGraphExec_t>(gc);
+    g.s = reinterpret_cast<hipGraphExec_t>(gs);
+    g.m = reinterpret_cast<hipGraphExec_t>(gm);
+    g.mf = reinterpret_cast<hipGraphExec_t>(gmf);
+  }
+  // direct-launch mode: the stages' recorded launches (oplist.h) replace the graph replays
+  void set_ops(int bucket, int slot, std::shared_ptr<OpList> c, std::shared_ptr<OpList> s,
+               std::shared_ptr<OpList> m, std::shared_ptr<OpList> mf) {
+    if (slot < 0 || slot >= depth_) throw std::runtime_error("PipeDriver: bad slot");
+    if (!c || !s || !m || !mf) throw std::runtime_error("PipeDriver: set_ops needs four op lists");
+    Graphs& g = graphs_[key(bucket, slot)];
+    g.oc = std::move(c);
+    g.os = std::move(s);
+    g.om = std::move(m);
+    g.omf = std::move(mf);
   }
 
   // rows: pointer to n packed ReqRec (0: already in the slab); the batch is tracked by its slot
@@ -106,8 +122,13 @@ class PipeDriver {
 
  private:
   struct Graphs {
-    hipGraphExec_t c, s, m, mf;  // mf: model graph that also copies the FeatRec rows to the host
+    hipGraphExec_t c = nullptr, s = nullptr, m = nullptr, mf = nullptr;  // mf: + FeatRec rows to the host
+    std::shared_ptr<OpList> oc, os, om, omf;  // direct-launch mode (set_ops)
   };
+  static void stage(hipGraphExec_t g, const std::shared_ptr<OpList>& ops, hipStream_t st, const char* what) {
+    if (ops) ops->run(st);
+    else hip_ok(hipGraphLaunch(g, st), what);
+  }
   struct Cmd {
     int slot, n, seq;
     int64_t now;
@@ -181,17 +202,17 @@ class PipeDriver {
     host_done_[slot] = 0;
     if (hist_.size() == 2) hip_ok(hipStreamWaitEvent(cs_, ev_[3 * hist_.front() + 1], 0), "wait state-2");
     const auto t2 = clk::now();
-    hip_ok(hipGraphLaunch(g.c, cs_), "copy graph");
+    stage(g.c, g.oc, cs_, "copy graph");
     const auto t3 = clk::now();
     hip_ok(hipEventRecord(ce, cs_), "record copy");
     hip_ok(hipStreamWaitEvent(ss_, ce, 0), "wait copy");
     const auto t4 = clk::now();
-    hip_ok(hipGraphLaunch(g.s, ss_), "state graph");
+    stage(g.s, g.os, ss_, "state graph");
     const auto t5 = clk::now();
     hip_ok(hipEventRecord(se, ss_), "record state");
     hip_ok(hipStreamWaitEvent(ms_, se, 0), "wait state");
     const auto t6 = clk::now();
-    hip_ok(hipGraphLaunch(with_features ? g.mf : g.m, ms_), "model graph");
+    stage(with_features ? g.mf : g.m, with_features ? g.omf : g.om, ms_, "model graph");
     const auto t7 = clk::now();
     hip_ok(hipEventRecord(me, ms_), "record model");
     const auto t8 = clk::now();
@@ -281,6 +302,7 @@ void register_driver(py::module_& m) {
   py::class_<PipeDriver>(m, "PipeDriver")
       .def(py::init<uintptr_t, uintptr_t, uintptr_t, int, py::list>())
       .def("set_graphs", &PipeDriver::set_graphs)
+      .def("set_ops", &PipeDriver::set_ops)
       .def("submit", &PipeDriver::submit)
       .def("wait", &PipeDriver::wait)
       .def("query", &PipeDriver::query)

@@ -240,7 +240,7 @@ class GpuScorer:
     def _copy_body(self, slot: int, bucket: int) -> None:
         sb = self.slots[slot]
         nbytes = HDR_BYTES + REQ_BYTES * bucket
-        sb.dev_slab[:nbytes].copy_(self.host_slab[slot][:nbytes], non_blocking=True)
+        K.memcpy_async(sb.dev_slab, self.host_slab[slot], nbytes)
         if self.update_features:
             K.dedup_insert(self.store, self.cfg_dev, sb.req, bucket, sb.hdr)
 
@@ -264,9 +264,9 @@ class GpuScorer:
             ml = sb.model.run(sb.X, bucket, m_ptr=sb.n_ptr) if sb.model is not None else None
             K.ensemble(sb.hdr, self.cfg_dev, sb.feat, sb.X, ml, sb.res, bucket, self.metrics, host_out=host)
         if host is None:
-            self.host_res[slot][:bucket].copy_(sb.res[:bucket], non_blocking=True)
+            K.memcpy_async(self.host_res[slot], sb.res, bucket * sb.res[0].numel() * sb.res.element_size())
         if with_features:
-            self.host_feat[slot][:bucket].copy_(sb.feat[:bucket], non_blocking=True)
+            K.memcpy_async(self.host_feat[slot], sb.feat, bucket * sb.feat[0].numel() * sb.feat.element_size())
 
     def capture(self) -> None:
         """Capture the copy, state, model and model+features graphs per (bucket, pipeline
@@ -304,6 +304,22 @@ class GpuScorer:
             for (b, slot), g in self.graphs.items():
                 d.set_graphs(b, slot, g[0].raw_cuda_graph_exec(), g[1].raw_cuda_graph_exec(),
                              g[2].raw_cuda_graph_exec(), g[3].raw_cuda_graph_exec())
+            # direct launch (csrc/kernels/oplist.h): the stages' kernels issued as plain launches
+            # instead of graph replays (a graph launch costs ~7 us of queue time on MI355X)
+            self.direct = (os.environ.get("IGP_DIRECT_LAUNCH", "1") == "1"
+                           and not any(s.kind == "gru" for s in (self.plan.steps if self.plan else [])))
+            if self.direct:
+                with torch.cuda.device(self.device):
+                    for b in self.buckets:
+                        for slot in range(self.depth):
+                            lists = []
+                            for body in (lambda: self._copy_body(slot, b), lambda: self._state_body(slot, b),
+                                         lambda: self._model_body(slot, b),
+                                         lambda: self._model_body(slot, b, with_features=True)):
+                                with K.Recorder() as r:
+                                    body()
+                                lists.append(r.ops)
+                            d.set_ops(b, slot, *lists)
             # IGP_ASYNC_SUBMIT=1: the driver's own thread issues each batch (csrc/kernels/driver.hip)
             if os.environ.get("IGP_ASYNC_SUBMIT", "0") == "1":
                 d.set_async(True)

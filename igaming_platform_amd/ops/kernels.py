@@ -42,6 +42,30 @@ def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+def memcpy_async(dst: torch.Tensor, src: torch.Tensor, nbytes: int) -> None:
+    """Stream-ordered copy of ``nbytes`` between contiguous tensors (pinned host <-> device),
+    recordable by the native driver's direct-launch mode (csrc/kernels/oplist.h)."""
+    if nbytes > dst.numel() * dst.element_size() or nbytes > src.numel() * src.element_size():
+        raise ValueError("memcpy_async: nbytes exceeds a tensor")
+    if not (dst.is_contiguous() and src.is_contiguous()):
+        raise ValueError("memcpy_async: tensors must be contiguous")
+    _mod().memcpy_async(dst.data_ptr(), src.data_ptr(), int(nbytes), _stream())
+
+
+class Recorder:
+    """``with Recorder() as r: body()`` -> ``r.ops``: the body's launches as a native op list
+    (nothing runs on the device while recording)."""
+
+    def __enter__(self):
+        _mod().record_begin()
+        self.ops = None
+        return self
+
+    def __exit__(self, *exc):
+        self.ops = _mod().record_end()
+        return False
+
+
 def _need(t: Optional[torch.Tensor], name: str, dtype=None, min_numel: int = 0, device=None):
     if t is None:
         raise ValueError(f"{name}: tensor required")

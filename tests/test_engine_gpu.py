@@ -165,6 +165,36 @@ def test_streaming_mode_matches_three_stream_mode():
         assert torch.equal(getattr(A.store, name), getattr(B.store, name)), name
 
 
+@pytest.mark.parametrize("env", ["IGP_DIRECT_LAUNCH", "IGP_ASYNC_SUBMIT"])
+def test_direct_launch_and_async_issue_match_graph_replay(env, monkeypatch):
+    """The native driver's direct-launch mode (recorded kernel launches instead of graph
+    replays, csrc/kernels/oplist.h) and its asynchronous issue thread give bit-identical results,
+    features and feature-store state to the graph-replay pipeline (mixed batch sizes, hot
+    accounts with several events per batch)."""
+    import torch
+    from igaming_platform_amd.utils import benchkit
+    from igaming_platform_amd.utils.synth import NOW0, make_requests
+    dev = torch.device("cuda", 0)
+    A = benchkit.build("cfg3", 512, 4096, dev, depth=3, history_batches=4, hot_frac=0.2)
+    monkeypatch.setenv(env, "1")
+    B = benchkit.build("cfg3", 512, 4096, dev, depth=3, history_batches=4, hot_frac=0.2)
+    if env == "IGP_DIRECT_LAUNCH":
+        assert B.scorer.direct
+    rng = np.random.default_rng(5)
+    batches = [make_requests(A.pop, n, rng, NOW0, hot_frac=0.2) for n in (512, 300, 512, 17, 512, 64, 200)]
+    for i, r in enumerate(batches):
+        pa = A.scorer.submit(r, now=NOW0 + i, want_features=bool(i % 2))
+        pb = B.scorer.submit(r, now=NOW0 + i, want_features=bool(i % 2))
+        ra, fa = A.scorer.wait(pa, unpack=False)
+        rb, fb = B.scorer.wait(pb, unpack=False)
+        np.testing.assert_array_equal(ra, rb)
+        if fa is not None:
+            np.testing.assert_array_equal(fa, fb)
+    torch.cuda.synchronize()
+    for name in ("rt", "ring_ts", "ring_amt", "hll"):
+        assert torch.equal(getattr(A.store, name), getattr(B.store, name)), name
+
+
 def test_fused_head_ensemble_matches_standalone():
     """cfg3 (trees -> MLP head): the ensemble run in the head's epilogue writes the same result
     records and metrics as the standalone K5 kernel over the head's output, including padded
