@@ -229,6 +229,7 @@ def main():
             "accounts_per_gpu": n_acc,
             "pipeline_depth": a.depth,
             "graphs": not a.no_graphs,
+            "launch": "direct (recorded op lists)" if getattr(sc, "direct", False) else "hipGraph replay",
             "driver": "native" if sc.driver is not None else "python",
             "dp_mode": a.dp_mode if world > 1 else "none",
             "numerics": numerics_desc(a),
@@ -358,6 +359,7 @@ def dp_bench(a, world: int, rank: int, dev) -> None:
         "vs_baseline": None, "dtype": a.numerics, "data": "synthetic",
         "config": {"model": S.desc, "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
                    "per_gpu_batch": B, "accounts_per_gpu": a.accounts, "pipeline_depth": a.depth, "graphs": True,
+                   "launch": "direct (recorded op lists)" if getattr(sc, "direct", False) else "hipGraph replay",
                    "driver": "native exchange (XchgDriver; two RCCL all-to-alls per step"
                              + (", captured in the hipGraphs)" if sc.captured else ", issued by the driver)"),
                    "dp_mode": "exchange", "chunk_capacity": C, "rows_scored": total,

@@ -157,8 +157,13 @@ PYBIND11_MODULE(_hipk, m) {
   });
 
   // record mode (oplist.h): launches between record_begin() and record_end() are stored, not run
-  py::class_<OpList, std::shared_ptr<OpList>>(m, "OpList").def_property_readonly(
-      "size", [](const OpList& o) { return o.ops.size(); });
+  py::class_<OpList, std::shared_ptr<OpList>>(m, "OpList")
+      .def_property_readonly("size", [](const OpList& o) { return o.ops.size(); })
+      .def("run", [](const OpList& o, uintptr_t s) {  // issue the recorded launches on stream s
+        py::gil_scoped_release nogil;
+        o.run(stream_of(s));
+        check("OpList.run");
+      });
   m.def("record_begin", []() {
     if (recording()) throw std::runtime_error("record_begin: already recording on this thread");
     recording() = new OpList();

@@ -26,12 +26,14 @@
 
 #include <chrono>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
 #include <vector>
 
 #include "../include/records.h"
+#include "oplist.h"
 #include "roctx.h"
 
 namespace py = pybind11;
@@ -255,7 +257,25 @@ class XchgDriver {
   void set_captured(bool c) { captured_ = c; }
   void set_graphs(int C, int slot, uintptr_t send, uintptr_t post, uintptr_t state, uintptr_t model, uintptr_t model_f) {
     check_slot(slot);
-    graphs_[key(C, slot)] = {G(send), G(post), G(state), G(model), G(model_f)};
+    Graphs& g = graphs_[key(C, slot)];
+    g.send = G(send);
+    g.post = G(post);
+    g.state = G(state);
+    g.model = G(model);
+    g.model_f = G(model_f);
+  }
+  // direct launch: the five stage bodies as recorded op lists; the driver issues the two
+  // all-to-alls and the D2H itself (the uncaptured path)
+  void set_ops(int C, int slot, std::shared_ptr<OpList> send, std::shared_ptr<OpList> post,
+               std::shared_ptr<OpList> state, std::shared_ptr<OpList> model, std::shared_ptr<OpList> model_f) {
+    check_slot(slot);
+    if (!send || !post || !state || !model || !model_f) throw std::runtime_error("XchgDriver: set_ops needs five lists");
+    Graphs& g = graphs_[key(C, slot)];
+    g.osend = std::move(send);
+    g.opost = std::move(post);
+    g.ostate = std::move(state);
+    g.omodel = std::move(model);
+    g.omodel_f = std::move(model_f);
   }
 
   // src: nbytes of prebuilt chunks ([N][C+1] ReqRec) copied into the slot's pinned buffer
@@ -270,7 +290,9 @@ class XchgDriver {
     const size_t rbytes = (size_t)C * W;
     if (nbytes > sl.host_x_bytes || (size_t)world_ * xbytes > sl.host_x_bytes) throw std::runtime_error("XchgDriver: chunks exceed the slot buffer");
     if ((size_t)world_ * rbytes > sl.host_rr_bytes) throw std::runtime_error("XchgDriver: results exceed the slot buffer");
-    if (with_features && !g.model_f) throw std::runtime_error("XchgDriver: no feature graph");
+    const bool direct = g.osend != nullptr;
+    if (with_features && !g.model_f && !direct) throw std::runtime_error("XchgDriver: no feature graph");
+    if (captured_ && direct) throw std::runtime_error("XchgDriver: direct launch needs set_captured(False)");
     py::gil_scoped_release nogil;
     Range range("igp.xsubmit");
     const auto t0 = clk::now();
@@ -312,20 +334,20 @@ class XchgDriver {
       return;
     }
     if (done_recorded_[slot]) hip_ok(hipStreamWaitEvent(xs_, e_done, 0), "wait done");
-    hip_ok(hipGraphLaunch(g.send, xs_), "send graph");
+    stage(g.send, g.osend, xs_, "send graph");
     const auto t2 = clk::now();
     if (copy_only_) hip_ok(hipMemcpyAsync(sl.xrecv, sl.xsend, xbytes, hipMemcpyDeviceToDevice, xs_), "rows D2D");
     else nccl_ok(r_, r_.all_to_all(sl.xsend, sl.xrecv, xbytes, kUint8, reinterpret_cast<void*>(cx_), xs_), "all_to_all rows");
     const auto t3 = clk::now();
     hop(xs_, cs_, e_x, "x -> copy");
     if (hist_.size() == 2) hip_ok(hipStreamWaitEvent(cs_, E(hist_.front(), 3), 0), "wait state-2");
-    hip_ok(hipGraphLaunch(g.post, cs_), "post graph");
+    stage(g.post, g.opost, cs_, "post graph");
     hip_ok(hipEventRecord(e_post, cs_), "record post");
     hip_ok(hipStreamWaitEvent(ss_, e_post, 0), "wait post");
-    hip_ok(hipGraphLaunch(g.state, ss_), "state graph");
+    stage(g.state, g.ostate, ss_, "state graph");
     hip_ok(hipEventRecord(e_state, ss_), "record state");
     hip_ok(hipStreamWaitEvent(ms_, e_state, 0), "wait state");
-    hip_ok(hipGraphLaunch(with_features ? g.model_f : g.model, ms_), "model graph");
+    stage(with_features ? g.model_f : g.model, with_features ? g.omodel_f : g.omodel, ms_, "model graph");
     hop(ms_, ys_, e_model, "model -> y");
     const auto t4 = clk::now();
     if (copy_only_) hip_ok(hipMemcpyAsync(sl.rrecv, sl.rsend, rbytes, hipMemcpyDeviceToDevice, ys_), "results D2D");
@@ -376,8 +398,14 @@ class XchgDriver {
  private:
   using clk = std::chrono::steady_clock;
   struct Graphs {
-    hipGraphExec_t send, post, state, model, model_f;
+    hipGraphExec_t send = nullptr, post = nullptr, state = nullptr, model = nullptr, model_f = nullptr;
+    // direct-launch mode (oplist.h): recorded stage launches instead of graph replays
+    std::shared_ptr<OpList> osend, opost, ostate, omodel, omodel_f;
   };
+  static void stage(hipGraphExec_t g, const std::shared_ptr<OpList>& ops, hipStream_t st, const char* what) {
+    if (ops) ops->run(st);
+    else hip_ok(hipGraphLaunch(g, st), what);
+  }
   struct Slot {
     char* host_hdr;
     char* host_x;
@@ -438,6 +466,7 @@ void register_exchange(py::module_& m) {
            py::keep_alive<1, 9>(), py::keep_alive<1, 10>())
       .def("set_slot", &XchgDriver::set_slot)
       .def("set_graphs", &XchgDriver::set_graphs)
+      .def("set_ops", &XchgDriver::set_ops)
       .def("set_captured", &XchgDriver::set_captured)
       .def("submit", &XchgDriver::submit)
       .def("wait", &XchgDriver::wait)
@@ -451,7 +480,14 @@ void register_exchange(py::module_& m) {
     if (N < 1 || N > XCHG_MAX_WORLD || C < 1 || cap < 1) throw std::runtime_error("exchange_compact: bad sizes");
     XchgCompactArgs a{P<const ReqRec*>(recv), P<ReqRec*>(rows), P<BatchHdr*>(hdr), P<int32_t*>(route), N, C, cap};
     const int threads = N * C;
-    hipLaunchKernelGGL(exchange_compact_kernel, dim3((threads + 255) / 256), dim3(256), 0, P<hipStream_t>(stream), a);
+    auto f = [a, threads](hipStream_t st) {
+      hipLaunchKernelGGL(exchange_compact_kernel, dim3((threads + 255) / 256), dim3(256), 0, st, a);
+    };
+    if (OpList* r = recording()) {
+      r->ops.emplace_back(f);
+      return;
+    }
+    f(P<hipStream_t>(stream));
     hip_ok(hipGetLastError(), "exchange_compact");
   });
   m.def("exchange_scatter", [](uintptr_t hdr, uintptr_t route, uintptr_t res, uintptr_t feat, uintptr_t send, int C,
@@ -459,7 +495,14 @@ void register_exchange(py::module_& m) {
     if (C < 1 || cap < 1) throw std::runtime_error("exchange_scatter: bad sizes");
     XchgScatterArgs a{P<const BatchHdr*>(hdr), P<const int32_t*>(route), P<const ResultRec*>(res),
                       P<const FeatRec*>(feat), P<uint8_t*>(send), C, cap};
-    hipLaunchKernelGGL(exchange_scatter_kernel, dim3((cap + 255) / 256), dim3(256), 0, P<hipStream_t>(stream), a);
+    auto f = [a, cap](hipStream_t st) {
+      hipLaunchKernelGGL(exchange_scatter_kernel, dim3((cap + 255) / 256), dim3(256), 0, st, a);
+    };
+    if (OpList* r = recording()) {
+      r->ops.emplace_back(f);
+      return;
+    }
+    f(P<hipStream_t>(stream));
     hip_ok(hipGetLastError(), "exchange_scatter");
   });
 }

@@ -145,7 +145,7 @@ class AbuseGpu:
                         self._body(slot, b)
                     torch.cuda.current_stream().wait_stream(s)
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, stream=s):
+                    with self.K.graph_capture(g, s):
                         self._body(slot, b)
                     self.graphs[(b, slot)] = g
             torch.cuda.synchronize(self.device)

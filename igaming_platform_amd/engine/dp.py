@@ -99,8 +99,8 @@ class DpGpuScorer(GpuScorer):
 
     def _send_body(self, slot: int, C: int) -> None:
         sb, nb = self.slots[slot], self.world * (C + 1) * REQ
-        sb.xsend[:nb].copy_(self.host_x[slot][:nb], non_blocking=True)
-        sb.dev_slab[:HDR_BYTES].copy_(self.host_slab[slot][:HDR_BYTES], non_blocking=True)
+        K.memcpy_async(sb.xsend, self.host_x[slot], nb)
+        K.memcpy_async(sb.dev_slab, self.host_slab[slot], HDR_BYTES)
 
     def _post_body(self, slot: int, C: int) -> None:
         sb, b = self.slots[slot], self.cap(C)
@@ -149,8 +149,13 @@ class DpGpuScorer(GpuScorer):
         IGP_XCHG_CAPTURE=1 (default) the two all-to-alls and the D2H copy are captured into the
         send and model graphs too (three graph launches per batch)."""
         dev = self.device
-        self.captured = os.environ.get("IGP_XCHG_CAPTURE", "1") == "1" and self.xstream is self.cstream \
-            and self.ystream is self.mstream
+        # IGP_XCHG_DIRECT=1: the stage bodies as recorded launch lists (csrc/kernels/oplist.h)
+        # with the collectives issued by the driver. Off by default: same-box world-1 A/B 67.4 vs
+        # 100.9 M scores/s for the captured graphs (RCCL inside the graphs beats driver-issued
+        # collectives, profiles/r2/direct3)
+        self.direct = os.environ.get("IGP_XCHG_DIRECT", "0") == "1"
+        self.captured = (not self.direct and os.environ.get("IGP_XCHG_CAPTURE", "1") == "1"
+                         and self.xstream is self.cstream and self.ystream is self.mstream)
         with torch.cuda.device(dev):
             for C in self.cbuckets:
                 for slot in range(self.depth):
@@ -177,8 +182,13 @@ class DpGpuScorer(GpuScorer):
                         with torch.cuda.stream(s):
                             body()
                         torch.cuda.current_stream().wait_stream(s)
+                        if self.direct:
+                            with K.Recorder() as r:
+                                body()
+                            gs.append(r.ops)
+                            continue
                         g = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(g, stream=s):
+                        with K.graph_capture(g, s):
                             body()
                         gs.append(g)
                     self.xgraphs[(C, slot)] = tuple(gs)
@@ -192,7 +202,10 @@ class DpGpuScorer(GpuScorer):
                        self.host_rr[slot].data_ptr(), sb.xsend.data_ptr(), sb.xrecv.data_ptr(), sb.rsend.data_ptr(),
                        sb.rrecv.data_ptr(), self.xbytes_max, self.rbytes_max)
         for (C, slot), g in self.xgraphs.items():
-            d.set_graphs(C, slot, *[0 if x is None else x.raw_cuda_graph_exec() for x in g])
+            if self.direct:
+                d.set_ops(C, slot, *g)
+            else:
+                d.set_graphs(C, slot, *[0 if x is None else x.raw_cuda_graph_exec() for x in g])
         d.set_captured(self.captured)
         self.xdriver = d
         self.driver = None  # the three-graph driver of the single-GPU path is not used here

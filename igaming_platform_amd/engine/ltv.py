@@ -117,6 +117,12 @@ class LtvGpu:
         self.model = DeviceModel(plan, self.device, self.buckets) if plan is not None else None
         # a dense chain (cfg 4: 256 -> 4 x 512 -> 1, bf16) runs as ONE fused kernel with the
         # table gather and K9 in it (csrc/kernels/mlp_fused.hip); IGP_MLP_FUSED=0: layer kernels
+        # IGP_LTV_DIRECT=1: the step's recorded launches (csrc/kernels/oplist.h) instead of a graph
+        # replay. Off by default: cfg4 same box 96.4 vs 172.7 M/s for graphs (the step is one
+        # fused kernel between two small copies; as stream copies they cost more than as graph
+        # nodes, profiles/r2/direct3)
+        self.direct = os.environ.get("IGP_LTV_DIRECT", "0") == "1" and not (
+            plan is not None and any(st.kind == "gru" for st in plan.steps))
         self.chain = None
         if (plan is not None and plan.precision == "bf16" and os.environ.get("IGP_MLP_FUSED", "1") != "0"
                 and K.MlpChainPack.eligible(plan.steps)):
@@ -166,19 +172,21 @@ class LtvGpu:
 
     # ---- the step
     def _body(self, slot: int, b: int) -> None:
-        self.dev_slab[:16 + 4 * b].copy_(self.host[slot][:16 + 4 * b], non_blocking=True)
+        K = self.K
+        K.memcpy_async(self.dev_slab, self.host[slot], 16 + 4 * b)
+        nout = b * self.out.shape[1] * self.out.element_size()
         if self.chain is not None:
-            self.K.mlp_chain(self.chain, b, slots=self.slots, pf_tab=self.pf_tab, ext_tab=self.ext_tab,
-                             ltv_out=self.out, m_ptr=self.n_ptr)
-            self.host_out[slot][:b].copy_(self.out[:b], non_blocking=True)
+            K.mlp_chain(self.chain, b, slots=self.slots, pf_tab=self.pf_tab, ext_tab=self.ext_tab,
+                        ltv_out=self.out, m_ptr=self.n_ptr)
+            K.memcpy_async(self.host_out[slot], self.out, nout)
             return
         ml = None
         if self.model is not None:
-            self.K.ltv_assemble(self.slots, self.pf_tab, self.ext_tab, self.X, b, m_ptr=self.n_ptr)
+            K.ltv_assemble(self.slots, self.pf_tab, self.ext_tab, self.X, b, m_ptr=self.n_ptr)
             y = self.model.run(self.X, b, m_ptr=self.n_ptr)
             ml = y[:b, 0]
-        self.K.ltv(self.pf_tab, self.out, model_ltv=ml, slots=self.slots, rows=b)
-        self.host_out[slot][:b].copy_(self.out[:b], non_blocking=True)
+        K.ltv(self.pf_tab, self.out, model_ltv=ml, slots=self.slots, rows=b)
+        K.memcpy_async(self.host_out[slot], self.out, nout)
 
     def capture(self) -> None:
         torch = self.torch
@@ -194,8 +202,13 @@ class LtvGpu:
                     with torch.cuda.stream(s):
                         self._body(slot, b)
                     torch.cuda.current_stream().wait_stream(s)
+                    if self.direct:  # recorded launches (csrc/kernels/oplist.h), no graph replay
+                        with self.K.Recorder() as r:
+                            self._body(slot, b)
+                        self.graphs[(b, slot)] = r.ops
+                        continue
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, stream=s):
+                    with self.K.graph_capture(g, s):
                         self._body(slot, b)
                     self.graphs[(b, slot)] = g
             torch.cuda.synchronize(self.device)
@@ -225,10 +238,12 @@ class LtvGpu:
         self._use(slot)
         with torch.cuda.stream(self.stream):
             g = self.graphs.get((b, slot))
-            if g is not None:
-                g.replay()
-            else:
+            if g is None:
                 self._body(slot, b)
+            elif self.direct:
+                g.run(self.stream.cuda_stream)
+            else:
+                g.replay()
             ev = torch.cuda.Event()
             ev.record(self.stream)
         return slot, n, ev

@@ -292,7 +292,7 @@ class GpuScorer:
                             body()
                         torch.cuda.current_stream().wait_stream(s)
                         g = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(g, stream=s):
+                        with K.graph_capture(g, s):
                             body()
                         pair.append(g)
                     self.graphs[(b, slot)] = tuple(pair)
@@ -348,7 +348,7 @@ class GpuScorer:
                 for p in range(3):
                     g = torch.cuda.CUDAGraph()
                     s0.wait_stream(torch.cuda.current_stream())
-                    with torch.cuda.graph(g, stream=s0):
+                    with K.graph_capture(g, s0):
                         s1.wait_stream(s0)
                         s2.wait_stream(s0)
                         self._copy_body(p, b)

@@ -7,6 +7,8 @@ All launches go to the caller's current torch stream and are hipGraph-capturable
 """
 from __future__ import annotations
 
+import contextlib
+
 import os
 
 from typing import Optional
@@ -50,6 +52,22 @@ def memcpy_async(dst: torch.Tensor, src: torch.Tensor, nbytes: int) -> None:
     if not (dst.is_contiguous() and src.is_contiguous()):
         raise ValueError("memcpy_async: tensors must be contiguous")
     _mod().memcpy_async(dst.data_ptr(), src.data_ptr(), int(nbytes), _stream())
+
+
+@contextlib.contextmanager
+def graph_capture(g, stream):
+    """``torch.cuda.graph(g, stream=stream)`` with the garbage collector paused for the capture:
+    a collection inside it can destroy native objects of an earlier pipeline (HIP events,
+    drivers) whose HIP calls are illegal while a stream captures and abort the process."""
+    import gc
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(g, stream=stream):
+            yield
+    finally:
+        if was:
+            gc.enable()
 
 
 class Recorder:
