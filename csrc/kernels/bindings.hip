@@ -102,6 +102,7 @@ namespace igp {
 void register_driver(py::module_& m);
 void register_exchange(py::module_& m);
 void register_watch(py::module_& m);
+void register_copy(py::module_& m);
 }
 
 PYBIND11_MODULE(_hipk, m) {
@@ -117,6 +118,7 @@ PYBIND11_MODULE(_hipk, m) {
   igp::register_driver(m);
   igp::register_exchange(m);
   igp::register_watch(m);
+  igp::register_copy(m);
 
   m.def("feature_assemble", [](py::dict d, uintptr_t s) {
     AssembleArgs a{};

@@ -58,12 +58,15 @@ class PipeDriver {
     for (auto h : host_slabs) slabs_.push_back(reinterpret_cast<char*>(h.cast<uintptr_t>()));
     ev_.resize(3 * depth);
     for (auto& e : ev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event create");
+    pe_.resize(depth);
+    for (auto& e : pe_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event create");
     recorded_.assign(3 * depth, false);
     host_done_.assign(depth, 0);
   }
   ~PipeDriver() {
     stop_worker();
     for (auto& e : ev_) (void)hipEventDestroy(e);
+    for (auto& e : pe_) (void)hipEventDestroy(e);
   }
 
   void set_async(bool on) {
@@ -96,6 +99,11 @@ class PipeDriver {
     g.om = std::move(m);
     g.omf = std::move(mf);
   }
+  // direct launch with a split state stage: `s` of set_ops holds K1 only, `su` the update
+  void set_state_update(int bucket, int slot, std::shared_ptr<OpList> su) {
+    if (slot < 0 || slot >= depth_) throw std::runtime_error("PipeDriver: bad slot");
+    graphs_[key(bucket, slot)].osu = std::move(su);
+  }
 
   // rows: pointer to n packed ReqRec (0: already in the slab); the batch is tracked by its slot
   // (wait(slot)). Slot reuse is ordered on the device (the copy waits for the slot's previous
@@ -124,6 +132,7 @@ class PipeDriver {
   struct Graphs {
     hipGraphExec_t c = nullptr, s = nullptr, m = nullptr, mf = nullptr;  // mf: + FeatRec rows to the host
     std::shared_ptr<OpList> oc, os, om, omf;  // direct-launch mode (set_ops)
+    std::shared_ptr<OpList> osu;              // split state stage: the update after K1
   };
   static void stage(hipGraphExec_t g, const std::shared_ptr<OpList>& ops, hipStream_t st, const char* what) {
     if (ops) ops->run(st);
@@ -200,7 +209,7 @@ class PipeDriver {
     // the slot's previous batch: skipped when the host already saw it complete (wait(slot))
     if (recorded_[3 * slot + 2] && !host_done_[slot]) hip_ok(hipStreamWaitEvent(cs_, me, 0), "wait model");
     host_done_[slot] = 0;
-    if (hist_.size() == 2) hip_ok(hipStreamWaitEvent(cs_, ev_[3 * hist_.front() + 1], 0), "wait state-2");
+    if (hist_.size() == 2) hip_ok(hipStreamWaitEvent(cs_, pe_[hist_.front()], 0), "wait state-2");
     const auto t2 = clk::now();
     stage(g.c, g.oc, cs_, "copy graph");
     const auto t3 = clk::now();
@@ -211,6 +220,11 @@ class PipeDriver {
     const auto t5 = clk::now();
     hip_ok(hipEventRecord(se, ss_), "record state");
     hip_ok(hipStreamWaitEvent(ms_, se, 0), "wait state");
+    // split state stage (direct launch): the model waited for K1 only; the multi-event update
+    // (which also clears the dedup region of batch seq+2) follows on the state stream and its
+    // own event gates that region's reuse
+    if (g.osu) g.osu->run(ss_);
+    hip_ok(hipEventRecord(pe_[slot], ss_), "record post");
     const auto t6 = clk::now();
     stage(with_features ? g.mf : g.m, with_features ? g.omf : g.om, ms_, "model graph");
     const auto t7 = clk::now();
@@ -281,6 +295,7 @@ class PipeDriver {
   int depth_;
   std::vector<char*> slabs_;
   std::vector<hipEvent_t> ev_;
+  std::vector<hipEvent_t> pe_;  // per slot: the state stream's work of the batch is complete
   std::vector<bool> recorded_;
   std::vector<uint8_t> host_done_;  // wait(slot) returned since the slot's last submit (bytes: set by waiter threads)
   std::vector<int> hist_;  // slots of the last two submitted batches, oldest first
@@ -303,6 +318,7 @@ void register_driver(py::module_& m) {
       .def(py::init<uintptr_t, uintptr_t, uintptr_t, int, py::list>())
       .def("set_graphs", &PipeDriver::set_graphs)
       .def("set_ops", &PipeDriver::set_ops)
+      .def("set_state_update", &PipeDriver::set_state_update)
       .def("submit", &PipeDriver::submit)
       .def("wait", &PipeDriver::wait)
       .def("query", &PipeDriver::query)

@@ -123,6 +123,7 @@ class LtvGpu:
         # nodes, profiles/r2/direct3)
         self.direct = os.environ.get("IGP_LTV_DIRECT", "0") == "1" and not (
             plan is not None and any(st.kind == "gru" for st in plan.steps))
+        self._pull_copy = os.environ.get("IGP_PULL_COPY", "0") == "1"
         self.chain = None
         if (plan is not None and plan.precision == "bf16" and os.environ.get("IGP_MLP_FUSED", "1") != "0"
                 and K.MlpChainPack.eligible(plan.steps)):
@@ -173,12 +174,13 @@ class LtvGpu:
     # ---- the step
     def _body(self, slot: int, b: int) -> None:
         K = self.K
-        K.memcpy_async(self.dev_slab, self.host[slot], 16 + 4 * b)
+        cp = K.pull_copy if self._pull_copy else K.memcpy_async
+        cp(self.dev_slab, self.host[slot], 16 + 4 * b)
         nout = b * self.out.shape[1] * self.out.element_size()
         if self.chain is not None:
             K.mlp_chain(self.chain, b, slots=self.slots, pf_tab=self.pf_tab, ext_tab=self.ext_tab,
                         ltv_out=self.out, m_ptr=self.n_ptr)
-            K.memcpy_async(self.host_out[slot], self.out, nout)
+            cp(self.host_out[slot], self.out, nout)
             return
         ml = None
         if self.model is not None:
@@ -186,7 +188,7 @@ class LtvGpu:
             y = self.model.run(self.X, b, m_ptr=self.n_ptr)
             ml = y[:b, 0]
         K.ltv(self.pf_tab, self.out, model_ltv=ml, slots=self.slots, rows=b)
-        K.memcpy_async(self.host_out[slot], self.out, nout)
+        cp(self.host_out[slot], self.out, nout)
 
     def capture(self) -> None:
         torch = self.torch

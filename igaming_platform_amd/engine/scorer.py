@@ -101,6 +101,8 @@ class GpuScorer:
             model = "none"
         self.model = model
         self.update_features = update_features
+        self._pull_copy = os.environ.get("IGP_PULL_COPY", "0") == "1"
+        self.direct = False
         self.use_graphs = cfg.gpu.use_graphs if use_graphs is None else use_graphs
         self.buckets = sorted(set(int(b) for b in cfg.gpu.buckets))
         self.bmax = self.buckets[-1]
@@ -240,14 +242,18 @@ class GpuScorer:
     def _copy_body(self, slot: int, bucket: int) -> None:
         sb = self.slots[slot]
         nbytes = HDR_BYTES + REQ_BYTES * bucket
-        K.memcpy_async(sb.dev_slab, self.host_slab[slot], nbytes)
+        # IGP_PULL_COPY=1: a kernel on the copy stream pulls the slab from pinned memory
+        (K.pull_copy if self._pull_copy else K.memcpy_async)(sb.dev_slab, self.host_slab[slot], nbytes)
         if self.update_features:
             K.dedup_insert(self.store, self.cfg_dev, sb.req, bucket, sb.hdr)
 
-    def _state_body(self, slot: int, bucket: int) -> None:
+    def _state_body(self, slot: int, bucket: int, part: str = "all") -> None:
+        """K1 (part "k1"), then the multi-event update that also clears the dedup region of
+        batch seq+2 (part "update")."""
         sb, upd = self.slots[slot], self.update_features
-        K.feature_assemble(self.store, sb.hdr, self.cfg_dev, sb.req, sb.X, sb.feat, bucket, dedup=upd)
-        if upd:
+        if part in ("all", "k1"):
+            K.feature_assemble(self.store, sb.hdr, self.cfg_dev, sb.req, sb.X, sb.feat, bucket, dedup=upd)
+        if upd and part in ("all", "update"):
             K.update_segments(self.store, self.cfg_dev, sb.req, bucket, sb.hdr)
 
     def _model_body(self, slot: int, bucket: int, with_features: bool = False) -> None:
@@ -312,14 +318,21 @@ class GpuScorer:
                 with torch.cuda.device(self.device):
                     for b in self.buckets:
                         for slot in range(self.depth):
+                            # the state stage split in two (IGP_SPLIT_STATE, default on): the
+                            # model waits for K1 only, the multi-event update runs beside it
+                            split = os.environ.get("IGP_SPLIT_STATE", "1") == "1"
                             lists = []
-                            for body in (lambda: self._copy_body(slot, b), lambda: self._state_body(slot, b),
+                            for body in (lambda: self._copy_body(slot, b),
+                                         lambda: self._state_body(slot, b, "k1" if split else "all"),
                                          lambda: self._model_body(slot, b),
-                                         lambda: self._model_body(slot, b, with_features=True)):
+                                         lambda: self._model_body(slot, b, with_features=True),
+                                         lambda: self._state_body(slot, b, "update")):
                                 with K.Recorder() as r:
                                     body()
                                 lists.append(r.ops)
-                            d.set_ops(b, slot, *lists)
+                            d.set_ops(b, slot, *lists[:4])
+                            if split:
+                                d.set_state_update(b, slot, lists[4])
             # IGP_ASYNC_SUBMIT=1: the driver's own thread issues each batch (csrc/kernels/driver.hip)
             if os.environ.get("IGP_ASYNC_SUBMIT", "0") == "1":
                 d.set_async(True)

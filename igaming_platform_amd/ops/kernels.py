@@ -70,6 +70,16 @@ def graph_capture(g, stream):
             gc.enable()
 
 
+def pull_copy(dst: torch.Tensor, src: torch.Tensor, nbytes: int) -> None:
+    """Copy ``nbytes`` with a kernel on the current stream that reads / writes the pinned host
+    side directly (csrc/kernels/copy.hip): no DMA-engine hand-off; recordable."""
+    if nbytes > dst.numel() * dst.element_size() or nbytes > src.numel() * src.element_size():
+        raise ValueError("pull_copy: nbytes exceeds a tensor")
+    if not (dst.is_contiguous() and src.is_contiguous()):
+        raise ValueError("pull_copy: tensors must be contiguous")
+    _mod().pull_copy(dst.data_ptr(), src.data_ptr(), int(nbytes), _stream())
+
+
 class Recorder:
     """``with Recorder() as r: body()`` -> ``r.ops``: the body's launches as a native op list
     (nothing runs on the device while recording)."""
