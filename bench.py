@@ -266,10 +266,22 @@ def dp_bench(a, world: int, rank: int, dev) -> None:
     if a.depth < 2:
         raise SystemExit("the exchange pipeline needs --depth >= 2")
     err = ""
-    try:
-        comms = rccl_comms(rank, world)
-    except Exception as e:  # RCCL refused (e.g. ranks sharing a GPU): every rank falls back together
-        comms, err = None, f"{type(e).__name__}: {e}"
+    # communicator set-up under a deadline (a daemon thread: ncclCommInitRank blocks), so a
+    # node where it cannot complete falls back to replicas instead of hanging the sweep
+    import threading
+    box = {}
+
+    def _init():
+        try:
+            box["comms"] = rccl_comms(rank, world)
+        except Exception as e:  # RCCL refused (e.g. ranks sharing a GPU): every rank falls back together
+            box["err"] = f"{type(e).__name__}: {e}"
+    th = threading.Thread(target=_init, daemon=True, name="rccl-init")
+    th.start()
+    th.join(float(os.environ.get("IGP_XCHG_INIT_S", "120")))
+    comms = box.get("comms")
+    if comms is None:
+        err = box.get("err", "communicator set-up timed out")
     if world > 1:
         bad = torch.tensor([0 if comms is not None else 1], dtype=torch.int32, device=dev)
         dist.all_reduce(bad, op=dist.ReduceOp.MAX)

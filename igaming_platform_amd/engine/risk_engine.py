@@ -445,7 +445,15 @@ class RiskEngine:
         kind = self.kind if self.kind in ("gpu", "golden") else "cpu"
         if kind == "gpu":
             import torch
+            from ..features.device_store import DeviceFeatureStore
             dev = int(device) if device is not None else torch.cuda.current_device()
+            # a re-homed shard needs a whole store on this device: refuse (the shard stays on the
+            # fallback) instead of running the survivor out of HBM
+            need = DeviceFeatureStore.estimate_bytes(self.cfg.features, self.capacity)
+            free, _ = torch.cuda.mem_get_info(dev)
+            if need > 0.9 * free:
+                raise MemoryError(f"re-homing shard {o} needs ~{need / 2**30:.1f} GiB, "
+                                  f"{free / 2**30:.1f} GiB free on cuda:{dev}")
             with torch.cuda.device(dev):
                 be = make_local_backend(self.cfg, "gpu", self.capacity, self.fraud_onnx, self.model_kind,
                                         self.blacklist, self.ipintel, rank=o, capture=self._capture)

@@ -107,11 +107,21 @@ class DeviceFeatureStore:
         return self.bytes_per_account() * self.capacity
 
     @staticmethod
-    def capacity_for(fcfg: FeatureConfig, hbm_bytes: int, fraction: float = 0.6, events: bool = True) -> int:
+    def _per_account(fcfg: FeatureConfig, events: bool = True) -> int:
         per = fcfg.ring_size * 12 + 512 + ACCTRT.itemsize + ACCTBATCH.itemsize + max(fcfg.width - 30, 1) * 4
         if events:
             per += fcfg.event_ring * fcfg.event_dim * 2
-        return int(hbm_bytes * fraction // per)
+        return per
+
+    @staticmethod
+    def capacity_for(fcfg: FeatureConfig, hbm_bytes: int, fraction: float = 0.6, events: bool = True) -> int:
+        return int(hbm_bytes * fraction // DeviceFeatureStore._per_account(fcfg, events))
+
+    @staticmethod
+    def estimate_bytes(fcfg: FeatureConfig, capacity: int, events: bool = True) -> int:
+        """HBM a store of ``capacity`` accounts takes (per-account arrays; tables and dedup
+        scratch are small)."""
+        return DeviceFeatureStore._per_account(fcfg, events) * int(capacity)
 
     # ------------------------------------------------------------------ writes
     def set_batch_features(self, slots: np.ndarray, rows: np.ndarray) -> None:
