@@ -213,6 +213,8 @@ class RiskEngine:
             self.abuse = AbuseService(self, threshold=cfg.abuse.threshold,
                                       executor=N.Executor(am) if am is not None else None)
         self.started_at = time.time()
+        if self.group is not None:
+            self.group.start_heartbeat()
         log.info("risk engine ready", extra={"fields": dict(backend=backend, shards=world, capacity=self.capacity,
                                                               model=mkind)})
 

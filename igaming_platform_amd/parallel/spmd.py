@@ -274,8 +274,12 @@ class SpmdGroup:
         self.heartbeats = 0
         self._stop = threading.Event()
         self._hb = None
-        if heartbeat_s > 0 and self.world > 1:
-            self._hb = threading.Thread(target=self._heartbeat, args=(float(heartbeat_s),), daemon=True,
+        self.heartbeat_s = float(heartbeat_s)
+
+    def start_heartbeat(self) -> None:
+        """Start the liveness op (call once the owner of ``on_failure`` is fully built)."""
+        if self._hb is None and self.heartbeat_s > 0 and self.world > 1:
+            self._hb = threading.Thread(target=self._heartbeat, args=(self.heartbeat_s,), daemon=True,
                                         name="spmd-heartbeat")
             self._hb.start()
 
