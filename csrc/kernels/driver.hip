@@ -69,6 +69,10 @@ class PipeDriver {
     for (auto& e : pe_) (void)hipEventDestroy(e);
   }
 
+  // serial mode: batches of up to `max_bucket` rows run all stages on one stream (direct launch
+  // only); larger ones keep the three-stream pipeline
+  void set_serial(int max_bucket) { serial_max_ = max_bucket; }
+
   void set_async(bool on) {
     if (on && !worker_.joinable()) {
       pending_.assign(depth_, 0);
@@ -113,7 +117,7 @@ class PipeDriver {
     if (slot < 0 || slot >= depth_) throw std::runtime_error("PipeDriver: bad slot");
     auto it = graphs_.find(key(bucket, slot));
     if (it == graphs_.end()) throw std::runtime_error("PipeDriver: no graphs for this bucket/slot");
-    const Cmd c{slot, n, seq, now, rows, with_features, it->second};
+    const Cmd c{slot, bucket, n, seq, now, rows, with_features, it->second};
     if (async_) {
       {
         std::lock_guard<std::mutex> lk(mu_);
@@ -139,7 +143,7 @@ class PipeDriver {
     else hip_ok(hipGraphLaunch(g, st), what);
   }
   struct Cmd {
-    int slot, n, seq;
+    int slot, bucket, n, seq;
     int64_t now;
     uintptr_t rows;
     bool with_features;
@@ -206,6 +210,32 @@ class PipeDriver {
     h->seq = seq;
     h->now = now;
     hipEvent_t ce = ev_[3 * slot], se = ev_[3 * slot + 1], me = ev_[3 * slot + 2];
+    const bool serial = cmd.bucket <= serial_max_ && g.oc && g.os && g.om && g.omf;
+    if (serial && !hist_.empty() && !serial_hist_) {
+      // the previous batch ran as three stages: its state work (store updates) comes first
+      hip_ok(hipStreamWaitEvent(cs_, pe_[hist_.back()], 0), "wait previous state");
+    }
+    serial_hist_ = serial;
+    if (serial) {
+      // serial mode (small micro-batches): every stage on the copy stream in order - no
+      // cross-queue waits (~12 us each when unsatisfied) and no event calls but the completion
+      // record; stream order gives the slot / dedup-region / store ordering
+      const auto ts = clk::now();
+      g.oc->run(cs_);
+      g.os->run(cs_);
+      if (g.osu) g.osu->run(cs_);
+      (with_features ? g.omf : g.om)->run(cs_);
+      hip_ok(hipEventRecord(pe_[slot], cs_), "record post");
+      hip_ok(hipEventRecord(me, cs_), "record model");
+      st_[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
+      st_[2] += std::chrono::duration<double, std::micro>(clk::now() - ts).count();
+      st_[5] += 1;
+      host_done_[slot] = 0;
+      recorded_[3 * slot] = recorded_[3 * slot + 1] = recorded_[3 * slot + 2] = true;
+      hist_.push_back(slot);
+      if (hist_.size() > 2) hist_.erase(hist_.begin());
+      return;
+    }
     // the slot's previous batch: skipped when the host already saw it complete (wait(slot))
     if (recorded_[3 * slot + 2] && !host_done_[slot]) hip_ok(hipStreamWaitEvent(cs_, me, 0), "wait model");
     host_done_[slot] = 0;
@@ -300,6 +330,8 @@ class PipeDriver {
   std::vector<uint8_t> host_done_;  // wait(slot) returned since the slot's last submit (bytes: set by waiter threads)
   std::vector<int> hist_;  // slots of the last two submitted batches, oldest first
   std::unordered_map<int64_t, Graphs> graphs_;
+  int serial_max_ = 0;
+  bool serial_hist_ = false;  // the last issued batch ran in serial mode
   // async issue
   bool async_ = false;
   bool stop_ = false;
@@ -319,6 +351,7 @@ void register_driver(py::module_& m) {
       .def("set_graphs", &PipeDriver::set_graphs)
       .def("set_ops", &PipeDriver::set_ops)
       .def("set_state_update", &PipeDriver::set_state_update)
+      .def("set_serial", &PipeDriver::set_serial)
       .def("submit", &PipeDriver::submit)
       .def("wait", &PipeDriver::wait)
       .def("query", &PipeDriver::query)

@@ -103,6 +103,7 @@ class GpuScorer:
         self.update_features = update_features
         self._pull_copy = os.environ.get("IGP_PULL_COPY", "0") == "1"
         self.direct = False
+        self.serial = False
         self.use_graphs = cfg.gpu.use_graphs if use_graphs is None else use_graphs
         self.buckets = sorted(set(int(b) for b in cfg.gpu.buckets))
         self.bmax = self.buckets[-1]
@@ -133,7 +134,12 @@ class GpuScorer:
         # Only with a model plan: the heuristic model stream is just the ensemble.
         split = os.environ.get("IGP_CU_SPLIT", "auto")
         if split == "auto":
-            split = "half" if plan is not None else "none"
+            # serial mode (small micro-batches, see capture) runs every stage on one stream: give
+            # that stream the whole GPU
+            serial = (self.use_graphs and os.environ.get("IGP_NATIVE_DRIVER", "1") != "0"
+                      and os.environ.get("IGP_DIRECT_LAUNCH", "1") == "1"
+                      and self.bmax <= int(os.environ.get("IGP_SERIAL_MAX_BUCKET", "0")))
+            split = "half" if plan is not None and not serial else "none"
         if split != "none":
             self._cu_split(split)
         self._copy_ev = [torch.cuda.Event() for _ in range(self.depth)]
@@ -333,6 +339,14 @@ class GpuScorer:
                             d.set_ops(b, slot, *lists[:4])
                             if split:
                                 d.set_state_update(b, slot, lists[4])
+            # serial mode (IGP_SERIAL_MAX_BUCKET > 0): batches up to that many rows run the three
+            # stages back to back on one stream. Off: the overlap of batch i+1's K1 with batch i's
+            # model is worth more than the hand-offs it costs even at 1024 rows (same box: cfg2
+            # 22.6 vs 11.0 M scores/s, cfg3 107 vs 57 M; profiles/r2/serial)
+            smax = int(os.environ.get("IGP_SERIAL_MAX_BUCKET", "0")) if self.direct else 0
+            self.serial = self.direct and self.bmax <= smax   # every bucket of this scorer runs serially
+            if self.direct and smax > 0:
+                d.set_serial(smax)  # buckets <= smax serial, larger ones three-stream
             # IGP_ASYNC_SUBMIT=1: the driver's own thread issues each batch (csrc/kernels/driver.hip)
             if os.environ.get("IGP_ASYNC_SUBMIT", "0") == "1":
                 d.set_async(True)

@@ -165,9 +165,11 @@ def test_streaming_mode_matches_three_stream_mode():
         assert torch.equal(getattr(A.store, name), getattr(B.store, name)), name
 
 
-@pytest.mark.parametrize("env", [dict(IGP_DIRECT_LAUNCH="1", IGP_SPLIT_STATE="1"),
-                                 dict(IGP_DIRECT_LAUNCH="1", IGP_SPLIT_STATE="0"),
-                                 dict(IGP_DIRECT_LAUNCH="1", IGP_ASYNC_SUBMIT="1")])
+@pytest.mark.parametrize("env", [dict(IGP_DIRECT_LAUNCH="1", IGP_SPLIT_STATE="1", IGP_SERIAL_MAX_BUCKET="0"),
+                                 dict(IGP_DIRECT_LAUNCH="1", IGP_SPLIT_STATE="0", IGP_SERIAL_MAX_BUCKET="0"),
+                                 dict(IGP_DIRECT_LAUNCH="1", IGP_SERIAL_MAX_BUCKET="4096"),
+                                 dict(IGP_DIRECT_LAUNCH="1", IGP_SERIAL_MAX_BUCKET="64"),  # mixed
+                                 dict(IGP_DIRECT_LAUNCH="1", IGP_ASYNC_SUBMIT="1", IGP_SERIAL_MAX_BUCKET="0")])
 def test_direct_launch_and_async_issue_match_graph_replay(env, monkeypatch):
     """The native driver's direct-launch mode (recorded kernel launches instead of graph
     replays, csrc/kernels/oplist.h) and its asynchronous issue thread give bit-identical results,
@@ -178,12 +180,14 @@ def test_direct_launch_and_async_issue_match_graph_replay(env, monkeypatch):
     from igaming_platform_amd.utils.synth import NOW0, make_requests
     dev = torch.device("cuda", 0)
     monkeypatch.setenv("IGP_DIRECT_LAUNCH", "0")       # the reference: graph replay
-    A = benchkit.build("cfg3", 512, 4096, dev, depth=3, history_batches=4, hot_frac=0.2)
+    bk = [64, 512]  # with IGP_SERIAL_MAX_BUCKET=64 small batches run serially, large ones on 3 streams
+    A = benchkit.build("cfg3", 512, 4096, dev, depth=3, history_batches=4, hot_frac=0.2, buckets=bk)
     assert not A.scorer.direct
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    B = benchkit.build("cfg3", 512, 4096, dev, depth=3, history_batches=4, hot_frac=0.2)
+    B = benchkit.build("cfg3", 512, 4096, dev, depth=3, history_batches=4, hot_frac=0.2, buckets=bk)
     assert B.scorer.direct
+    assert B.scorer.serial == (int(env["IGP_SERIAL_MAX_BUCKET"]) >= 512)
     rng = np.random.default_rng(5)
     batches = [make_requests(A.pop, n, rng, NOW0, hot_frac=0.2) for n in (512, 300, 512, 17, 512, 64, 200)]
     for i, r in enumerate(batches):
