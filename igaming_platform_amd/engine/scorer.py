@@ -136,10 +136,12 @@ class GpuScorer:
         if split == "auto":
             # serial mode (small micro-batches, see capture) runs every stage on one stream: give
             # that stream the whole GPU
-            serial = (self.use_graphs and os.environ.get("IGP_NATIVE_DRIVER", "1") != "0"
-                      and os.environ.get("IGP_DIRECT_LAUNCH", "1") == "1"
-                      and self.bmax <= int(os.environ.get("IGP_SERIAL_MAX_BUCKET", "0")))
-            split = "half" if plan is not None and not serial else "none"
+            # With direct launch the masks no longer pay (same-box A/Bs, 3000-step runs: no split
+            # 107.6 vs half 101.8 M scores/s, 5 x 600 steps on another box: median 130.5 vs 127.5;
+            # profiles/r2/cu, cu3): they were a win for the graph-replay pipeline only
+            direct = (self.use_graphs and os.environ.get("IGP_NATIVE_DRIVER", "1") != "0"
+                      and os.environ.get("IGP_DIRECT_LAUNCH", "1") == "1")
+            split = "half" if plan is not None and not direct else "none"
         if split != "none":
             self._cu_split(split)
         self._copy_ev = [torch.cuda.Event() for _ in range(self.depth)]
