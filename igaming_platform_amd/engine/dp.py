@@ -94,6 +94,10 @@ class DpGpuScorer(GpuScorer):
         self._watch = None
 
     # ------------------------------------------------------------------ graph bodies
+    @staticmethod
+    def _direct_default() -> bool:
+        return os.environ.get("IGP_XCHG_DIRECT", "0") == "1"
+
     def cap(self, C: int) -> int:
         return self.senders * C
 

@@ -139,8 +139,7 @@ class GpuScorer:
             # With direct launch the masks no longer pay (same-box A/Bs, 3000-step runs: no split
             # 107.6 vs half 101.8 M scores/s, 5 x 600 steps on another box: median 130.5 vs 127.5;
             # profiles/r2/cu, cu3): they were a win for the graph-replay pipeline only
-            direct = (self.use_graphs and os.environ.get("IGP_NATIVE_DRIVER", "1") != "0"
-                      and os.environ.get("IGP_DIRECT_LAUNCH", "1") == "1")
+            direct = self.use_graphs and os.environ.get("IGP_NATIVE_DRIVER", "1") != "0" and self._direct_default()
             split = "half" if plan is not None and not direct else "none"
         if split != "none":
             self._cu_split(split)
@@ -157,6 +156,12 @@ class GpuScorer:
         self._seq = 0
         self._lock = threading.Lock()
         self.batches = 0
+
+    @staticmethod
+    def _direct_default() -> bool:
+        """Whether this pipeline issues its stages by direct launch (the exchange scorer keeps
+        graph replay by default and overrides this)."""
+        return os.environ.get("IGP_DIRECT_LAUNCH", "1") == "1"
 
     def _cu_split(self, spec: str) -> None:
         """``half`` = ``lo:n_cu/2``; ``lo:N``: CUs [0, N) run the copy + state streams, the
