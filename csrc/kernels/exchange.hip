@@ -264,6 +264,11 @@ class XchgDriver {
     g.model = G(model);
     g.model_f = G(model_f);
   }
+  // captured mode with the state stage (K1 + update, no collectives) as recorded launches
+  void set_state_ops(int C, int slot, std::shared_ptr<OpList> state) {
+    check_slot(slot);
+    graphs_[key(C, slot)].ostate = std::move(state);
+  }
   // direct launch: the five stage bodies as recorded op lists; the driver issues the two
   // all-to-alls and the D2H itself (the uncaptured path)
   void set_ops(int C, int slot, std::shared_ptr<OpList> send, std::shared_ptr<OpList> post,
@@ -320,7 +325,7 @@ class XchgDriver {
       hip_ok(hipGraphLaunch(g.send, cs_), "send+post graph");
       hip_ok(hipEventRecord(e_post, cs_), "record post");
       hip_ok(hipStreamWaitEvent(ss_, e_post, 0), "wait post");
-      hip_ok(hipGraphLaunch(g.state, ss_), "state graph");
+      stage(g.state, g.ostate, ss_, "state graph");  // recorded launches when set (set_state_ops)
       hip_ok(hipEventRecord(e_state, ss_), "record state");
       hip_ok(hipStreamWaitEvent(ms_, e_state, 0), "wait state");
       hip_ok(hipGraphLaunch(with_features ? g.model_f : g.model, ms_), "model+results graph");
@@ -467,6 +472,7 @@ void register_exchange(py::module_& m) {
       .def("set_slot", &XchgDriver::set_slot)
       .def("set_graphs", &XchgDriver::set_graphs)
       .def("set_ops", &XchgDriver::set_ops)
+      .def("set_state_ops", &XchgDriver::set_state_ops)
       .def("set_captured", &XchgDriver::set_captured)
       .def("submit", &XchgDriver::submit)
       .def("wait", &XchgDriver::wait)

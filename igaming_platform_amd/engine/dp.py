@@ -210,6 +210,14 @@ class DpGpuScorer(GpuScorer):
                 d.set_ops(C, slot, *g)
             else:
                 d.set_graphs(C, slot, *[0 if x is None else x.raw_cuda_graph_exec() for x in g])
+        # IGP_XCHG_STATE_DIRECT=1 (captured mode): the collective-free state stage as recorded
+        # launches, the two stages with RCCL inside stay graphs
+        if self.captured and os.environ.get("IGP_XCHG_STATE_DIRECT", "0") == "1":
+            with torch.cuda.device(dev):
+                for (C, slot) in self.xgraphs:
+                    with K.Recorder() as r:
+                        self._state_body(slot, self.cap(C))
+                    d.set_state_ops(C, slot, r.ops)
         d.set_captured(self.captured)
         self.xdriver = d
         self.driver = None  # the three-graph driver of the single-GPU path is not used here
