@@ -96,6 +96,10 @@ OpList*& recording() {
   thread_local OpList* cur = nullptr;
   return cur;
 }
+StopEvent& stop_event() {
+  thread_local StopEvent se;
+  return se;
+}
 }  // namespace igp
 
 namespace igp {
@@ -183,6 +187,7 @@ PYBIND11_MODULE(_hipk, m) {
       const hipError_t e = hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n,
                                           hipMemcpyDefault, st);
       if (e != hipSuccess) throw std::runtime_error(std::string("memcpy_async: ") + hipGetErrorString(e));
+      stop_event().bound = false;  // a copy after the stage's last kernel: the driver records the event
     }, s, "memcpy_async");
   });
 

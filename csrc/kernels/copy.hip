@@ -28,7 +28,7 @@ void launch_pull_copy(void* dst, const void* src, size_t n, hipStream_t st) {
   const size_t n16 = n / 16;
   const int ntail = (int)(n - n16 * 16);
   const int blocks = (int)std::min<size_t>(std::max<size_t>((n16 + 255) / 256, 1), 1024);
-  hipLaunchKernelGGL(pull_copy_kernel, dim3(blocks), dim3(256), 0, st, reinterpret_cast<uint4*>(dst),
+  IGP_LAUNCH(pull_copy_kernel, dim3(blocks), dim3(256), 0, st, reinterpret_cast<uint4*>(dst),
                      reinterpret_cast<const uint4*>(src), n16, reinterpret_cast<uint8_t*>(dst) + n16 * 16,
                      reinterpret_cast<const uint8_t*>(src) + n16 * 16, ntail);
 }

@@ -62,6 +62,8 @@ class PipeDriver {
     for (auto& e : pe_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event create");
     recorded_.assign(3 * depth, false);
     host_done_.assign(depth, 0);
+    const char* xe = getenv("IGP_EXT_EVENTS");
+    ext_events_ = !(xe && atoi(xe) == 0);
   }
   ~PipeDriver() {
     stop_worker();
@@ -72,6 +74,10 @@ class PipeDriver {
   // serial mode: batches of up to `max_bucket` rows run all stages on one stream (direct launch
   // only); larger ones keep the three-stream pipeline
   void set_serial(int max_bucket) { serial_max_ = max_bucket; }
+
+  // stage-end events bound to the stages' last kernels (oplist.h) instead of recorded markers
+  void set_ext_events(bool on) { ext_events_ = on; }
+  bool ext_events() const { return ext_events_; }
 
   void set_async(bool on) {
     if (on && !worker_.joinable()) {
@@ -141,6 +147,14 @@ class PipeDriver {
   static void stage(hipGraphExec_t g, const std::shared_ptr<OpList>& ops, hipStream_t st, const char* what) {
     if (ops) ops->run(st);
     else hip_ok(hipGraphLaunch(g, st), what);
+  }
+  // stage with its end event bound to its last kernel (oplist.h run_recording); false: the
+  // caller records ev (graph replay, IGP_EXT_EVENTS=0, or a stage ending in a copy)
+  bool stage_rec(hipGraphExec_t g, const std::shared_ptr<OpList>& ops, hipStream_t st, hipEvent_t ev,
+                 const char* what) const {
+    if (ops && ext_events_) return ops->run_recording(st, ev);
+    stage(g, ops, st, what);
+    return false;
   }
   struct Cmd {
     int slot, bucket, n, seq;
@@ -241,24 +255,25 @@ class PipeDriver {
     host_done_[slot] = 0;
     if (hist_.size() == 2) hip_ok(hipStreamWaitEvent(cs_, pe_[hist_.front()], 0), "wait state-2");
     const auto t2 = clk::now();
-    stage(g.c, g.oc, cs_, "copy graph");
+    const bool cb = stage_rec(g.c, g.oc, cs_, ce, "copy graph");
     const auto t3 = clk::now();
-    hip_ok(hipEventRecord(ce, cs_), "record copy");
+    if (!cb) hip_ok(hipEventRecord(ce, cs_), "record copy");
     hip_ok(hipStreamWaitEvent(ss_, ce, 0), "wait copy");
     const auto t4 = clk::now();
-    stage(g.s, g.os, ss_, "state graph");
+    const bool sb = stage_rec(g.s, g.os, ss_, se, "state graph");
     const auto t5 = clk::now();
-    hip_ok(hipEventRecord(se, ss_), "record state");
+    if (!sb) hip_ok(hipEventRecord(se, ss_), "record state");
     hip_ok(hipStreamWaitEvent(ms_, se, 0), "wait state");
     // split state stage (direct launch): the model waited for K1 only; the multi-event update
     // (which also clears the dedup region of batch seq+2) follows on the state stream and its
     // own event gates that region's reuse
-    if (g.osu) g.osu->run(ss_);
-    hip_ok(hipEventRecord(pe_[slot], ss_), "record post");
+    const bool pb = g.osu && ext_events_ && g.osu->run_recording(ss_, pe_[slot]);
+    if (g.osu && !ext_events_) g.osu->run(ss_);
+    if (!pb) hip_ok(hipEventRecord(pe_[slot], ss_), "record post");
     const auto t6 = clk::now();
-    stage(with_features ? g.mf : g.m, with_features ? g.omf : g.om, ms_, "model graph");
+    const bool mb = stage_rec(with_features ? g.mf : g.m, with_features ? g.omf : g.om, ms_, me, "model graph");
     const auto t7 = clk::now();
-    hip_ok(hipEventRecord(me, ms_), "record model");
+    if (!mb) hip_ok(hipEventRecord(me, ms_), "record model");
     const auto t8 = clk::now();
     auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
     st_[0] += us(t0, t1);                          // row copy
@@ -334,6 +349,7 @@ class PipeDriver {
   bool serial_hist_ = false;  // the last issued batch ran in serial mode
   // async issue
   bool async_ = false;
+  bool ext_events_ = true;
   bool stop_ = false;
   std::thread worker_;
   std::mutex mu_;
@@ -352,6 +368,8 @@ void register_driver(py::module_& m) {
       .def("set_ops", &PipeDriver::set_ops)
       .def("set_state_update", &PipeDriver::set_state_update)
       .def("set_serial", &PipeDriver::set_serial)
+      .def("set_ext_events", &PipeDriver::set_ext_events)
+      .def_property_readonly("ext_events", &PipeDriver::ext_events)
       .def("submit", &PipeDriver::submit)
       .def("wait", &PipeDriver::wait)
       .def("query", &PipeDriver::query)

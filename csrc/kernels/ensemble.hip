@@ -29,7 +29,7 @@ __global__ void __launch_bounds__(256) ensemble_kernel(EnsembleArgs a) {
 
 void launch_ensemble(const EnsembleArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
-  hipLaunchKernelGGL(ensemble_kernel, dim3((a.n_rows + 255) / 256), dim3(256), 0, st, a);
+  IGP_LAUNCH(ensemble_kernel, dim3((a.n_rows + 255) / 256), dim3(256), 0, st, a);
 }
 
 }  // namespace igp

@@ -487,7 +487,7 @@ void register_exchange(py::module_& m) {
     XchgCompactArgs a{P<const ReqRec*>(recv), P<ReqRec*>(rows), P<BatchHdr*>(hdr), P<int32_t*>(route), N, C, cap};
     const int threads = N * C;
     auto f = [a, threads](hipStream_t st) {
-      hipLaunchKernelGGL(exchange_compact_kernel, dim3((threads + 255) / 256), dim3(256), 0, st, a);
+      IGP_LAUNCH(exchange_compact_kernel, dim3((threads + 255) / 256), dim3(256), 0, st, a);
     };
     if (OpList* r = recording()) {
       r->ops.emplace_back(f);
@@ -502,7 +502,7 @@ void register_exchange(py::module_& m) {
     XchgScatterArgs a{P<const BatchHdr*>(hdr), P<const int32_t*>(route), P<const ResultRec*>(res),
                       P<const FeatRec*>(feat), P<uint8_t*>(send), C, cap};
     auto f = [a, cap](hipStream_t st) {
-      hipLaunchKernelGGL(exchange_scatter_kernel, dim3((cap + 255) / 256), dim3(256), 0, st, a);
+      IGP_LAUNCH(exchange_scatter_kernel, dim3((cap + 255) / 256), dim3(256), 0, st, a);
     };
     if (OpList* r = recording()) {
       r->ops.emplace_back(f);

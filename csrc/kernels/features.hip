@@ -758,27 +758,27 @@ __global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
 // ---------------------------------------------------------------------------------- launch
 void launch_feature_assemble(const AssembleArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
-  hipLaunchKernelGGL(feature_assemble_kernel, dim3((a.n_rows + 15) / 16), dim3(256), 0, st, a);
+  IGP_LAUNCH(feature_assemble_kernel, dim3((a.n_rows + 15) / 16), dim3(256), 0, st, a);
 }
 
 void launch_dedup_insert(const UpdateArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
   if (!a.hdr || a.region >= 0 || (a.dcap & 3)) throw std::runtime_error("dedup_insert: scorer ring regions only");
-  hipLaunchKernelGGL(dedup_insert_list_kernel, dim3((a.n_max + 63) / 64), dim3(64), 0, st, a);
+  IGP_LAUNCH(dedup_insert_list_kernel, dim3((a.n_max + 63) / 64), dim3(64), 0, st, a);
 }
 
 void launch_update_segments(const UpdateArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
   // one wave per multi-event account, 256 waves looping over the region's list
-  hipLaunchKernelGGL(update_multi_kernel, dim3(UPD_MULTI_BLOCKS), dim3(256), 0, st, a);
+  IGP_LAUNCH(update_multi_kernel, dim3(UPD_MULTI_BLOCKS), dim3(256), 0, st, a);
 }
 
 void launch_feature_update(const UpdateArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
-  hipLaunchKernelGGL(dedup_reset_kernel, dim3((a.dcap + 255) / 256), dim3(256), 0, st, a);
+  IGP_LAUNCH(dedup_reset_kernel, dim3((a.dcap + 255) / 256), dim3(256), 0, st, a);
   const int g = (a.n_max + 255) / 256;
-  hipLaunchKernelGGL(dedup_insert_kernel, dim3(g), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(update_single_kernel, dim3(g), dim3(256), 0, st, a);
+  IGP_LAUNCH(dedup_insert_kernel, dim3(g), dim3(256), 0, st, a);
+  IGP_LAUNCH(update_single_kernel, dim3(g), dim3(256), 0, st, a);
   launch_update_segments(a, st);
 }
 

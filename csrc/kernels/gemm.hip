@@ -686,7 +686,7 @@ void launch_mlp_head(const HeadArgs& a, hipStream_t st) {
     const int w_lds = n1p * lds_row * 4 <= (size_t)(96 * 1024);
     const size_t lds = ((size_t)HD_ROWS + (w_lds ? n1p : 0)) * lds_row * 4 + 4 * HD_ROWS * sizeof(float) +
                        2 * n1p * sizeof(float);
-    hipLaunchKernelGGL(mlp_head_f32_kernel, dim3((a.M + HD_ROWS - 1) / HD_ROWS), dim3(256), lds, st, a, w_lds);
+    IGP_LAUNCH(mlp_head_f32_kernel, dim3((a.M + HD_ROWS - 1) / HD_ROWS), dim3(256), lds, st, a, w_lds);
     return;
   }
   const size_t lds_row = (size_t)a.k_pad + G_PAD;
@@ -694,28 +694,28 @@ void launch_mlp_head(const HeadArgs& a, hipStream_t st) {
   const int w_lds = n1p * lds_row * 2 <= (size_t)HD_W_LDS_MAX;
   const size_t lds = ((((size_t)HD_ROWS + (w_lds ? n1p : 0)) * lds_row * 2 + 15) & ~size_t(15)) +
                      4 * HD_ROWS * sizeof(float) + 2 * n1p * sizeof(float);
-  hipLaunchKernelGGL(mlp_head_kernel, dim3((a.M + HD_ROWS - 1) / HD_ROWS), dim3(256), lds, st, a, w_lds);
+  IGP_LAUNCH(mlp_head_kernel, dim3((a.M + HD_ROWS - 1) / HD_ROWS), dim3(256), lds, st, a, w_lds);
 }
 
 void launch_gemm(const GemmArgs& a, hipStream_t st) {
   if (a.M <= 0) return;
   if (a.w_f32) {
-    hipLaunchKernelGGL(gemm_f32_kernel, dim3((a.N + 63) / 64, (a.M + 63) / 64), dim3(256), 0, st, a);
+    IGP_LAUNCH(gemm_f32_kernel, dim3((a.N + 63) / 64, (a.M + 63) / 64), dim3(256), 0, st, a);
     return;
   }
   const bool big = a.M >= 4096 && a.N >= 128;
   if (big) {
     dim3 grid((a.N + 127) / 128, (a.M + 127) / 128);
-    hipLaunchKernelGGL((gemm_kernel<128, 128>), grid, dim3(256), 0, st, a);
+    IGP_LAUNCH((gemm_kernel<128, 128>), grid, dim3(256), 0, st, a);
   } else {
     dim3 grid((a.N + 63) / 64, (a.M + 63) / 64);
-    hipLaunchKernelGGL((gemm_kernel<64, 64>), grid, dim3(256), 0, st, a);
+    IGP_LAUNCH((gemm_kernel<64, 64>), grid, dim3(256), 0, st, a);
   }
 }
 
 void launch_gemv(const GemmArgs& a, hipStream_t st) {
   if (a.M <= 0) return;
-  hipLaunchKernelGGL(gemv_kernel, dim3((a.M + 3) / 4), dim3(256), 0, st, a);
+  IGP_LAUNCH(gemv_kernel, dim3((a.M + 3) / 4), dim3(256), 0, st, a);
 }
 
 }  // namespace igp

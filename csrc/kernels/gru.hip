@@ -525,9 +525,9 @@ static void launch_gru_w(const GruArgs& a, hipStream_t st) {
   const dim3 grid((a.n_rows + M - 1) / M), block(NW * 64);
   const size_t lds = gru_lds_bytes(RT, KSX, KSH, NW);
   if (a.layer[0].lbr)
-    hipLaunchKernelGGL((gru_kernel<RT, KSX, KSH, 1, NW>), grid, block, lds, st, a);
+    IGP_LAUNCH((gru_kernel<RT, KSX, KSH, 1, NW>), grid, block, lds, st, a);
   else
-    hipLaunchKernelGGL((gru_kernel<RT, KSX, KSH, 0, NW>), grid, block, lds, st, a);
+    IGP_LAUNCH((gru_kernel<RT, KSX, KSH, 0, NW>), grid, block, lds, st, a);
 }
 
 template <int RT, int KSX, int KSH, int NW>
@@ -536,9 +536,9 @@ static void launch_gru_pipe(const GruArgs& a, hipStream_t st) {
   const dim3 grid((a.n_rows + M - 1) / M), block(NW * 64);
   const size_t lds = gru_pipe_lds_bytes(RT, KSX, KSH, NW);
   if (a.layer[0].lbr)
-    hipLaunchKernelGGL((gru2_pipe_kernel<RT, KSX, KSH, 1, NW>), grid, block, lds, st, a);
+    IGP_LAUNCH((gru2_pipe_kernel<RT, KSX, KSH, 1, NW>), grid, block, lds, st, a);
   else
-    hipLaunchKernelGGL((gru2_pipe_kernel<RT, KSX, KSH, 0, NW>), grid, block, lds, st, a);
+    IGP_LAUNCH((gru2_pipe_kernel<RT, KSX, KSH, 0, NW>), grid, block, lds, st, a);
 }
 
 template <int RT, int KSX, int KSH>

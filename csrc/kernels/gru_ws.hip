@@ -465,7 +465,7 @@ bool gru_ws_eligible(const GruArgs& a) {
 void launch_gru_ws(const GruArgs& a, hipStream_t st) {
   const int ncl = gru_ws_clusters(a.n_rows);
   const int grid = ((ncl + 7) / 8) * 64;
-  hipLaunchKernelGGL(gru_ws_kernel, dim3(grid), dim3(256), gru_ws_lds_bytes(), st, a);
+  IGP_LAUNCH(gru_ws_kernel, dim3(grid), dim3(256), gru_ws_lds_bytes(), st, a);
 }
 
 }  // namespace igp

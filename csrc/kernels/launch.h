@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "../include/records.h"
+#include "oplist.h"
 
 namespace igp {
 

@@ -44,12 +44,12 @@ __global__ void __launch_bounds__(256) ltv_assemble_kernel(LtvAssembleArgs a) {
 void launch_ltv_assemble(const LtvAssembleArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
   const size_t total = (size_t)a.n_rows * a.x_w;
-  hipLaunchKernelGGL(ltv_assemble_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
+  IGP_LAUNCH(ltv_assemble_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
 }
 
 void launch_ltv(const LtvArgs& a, hipStream_t st) {
   if (a.B <= 0) return;
-  hipLaunchKernelGGL(ltv_kernel, dim3((a.B + 255) / 256), dim3(256), 0, st, a);
+  IGP_LAUNCH(ltv_kernel, dim3((a.B + 255) / 256), dim3(256), 0, st, a);
 }
 
 }  // namespace igp

@@ -217,13 +217,13 @@ void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
   const int r = a.rows_per_block;
   if (a.waves == 8)
-    hipLaunchKernelGGL((mlp_chain_kernel<32, 8>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
+    IGP_LAUNCH((mlp_chain_kernel<32, 8>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
   else if (r == 64)
-    hipLaunchKernelGGL((mlp_chain_kernel<64, 4>), dim3((a.n_rows + 63) / 64), dim3(256), 0, st, a);
+    IGP_LAUNCH((mlp_chain_kernel<64, 4>), dim3((a.n_rows + 63) / 64), dim3(256), 0, st, a);
   else if (r == 16)
-    hipLaunchKernelGGL((mlp_chain_kernel<16, 4>), dim3((a.n_rows + 15) / 16), dim3(256), 0, st, a);
+    IGP_LAUNCH((mlp_chain_kernel<16, 4>), dim3((a.n_rows + 15) / 16), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((mlp_chain_kernel<32, 4>), dim3((a.n_rows + 31) / 32), dim3(256), 0, st, a);
+    IGP_LAUNCH((mlp_chain_kernel<32, 4>), dim3((a.n_rows + 31) / 32), dim3(256), 0, st, a);
 }
 
 }  // namespace igp

@@ -354,14 +354,14 @@ static void launch_kl(const TreeArgs& a, int groups, float* partial, int no_fini
   int in_lds = (base + node_bytes + leaf_bytes) <= 96 * 1024;  // keep >= 1 block/CU with headroom
   const size_t lds = base + (in_lds ? node_bytes : 0) + leaf_bytes;
   dim3 grid((a.n_rows + TR_ROWS - 1) / TR_ROWS, groups);
-  hipLaunchKernelGGL((tree_kernel<K, LEQ>), grid, dim3(256), lds, st, a, tpg, feat_w, in_lds,
+  IGP_LAUNCH((tree_kernel<K, LEQ>), grid, dim3(256), lds, st, a, tpg, feat_w, in_lds,
                      groups > 1 ? partial : nullptr);
   if (groups > 1 && !no_finish) {
     if (!post_rowwise(a) && a.n_out == K)
-      hipLaunchKernelGGL(tree_finish_elem_kernel, dim3((a.n_rows * K + 255) / 256), dim3(256), 0, st, a,
+      IGP_LAUNCH(tree_finish_elem_kernel, dim3((a.n_rows * K + 255) / 256), dim3(256), 0, st, a,
                          partial, groups);
     else
-      hipLaunchKernelGGL(tree_finish_kernel, dim3((a.n_rows + 255) / 256), dim3(256), 0, st, a, partial, groups);
+      IGP_LAUNCH(tree_finish_kernel, dim3((a.n_rows + 255) / 256), dim3(256), 0, st, a, partial, groups);
   }
 }
 

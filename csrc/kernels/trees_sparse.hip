@@ -177,11 +177,11 @@ static void launch_sparse_k(const TreeSparseArgs& a, int groups, float* partial,
   dim3 grid((a.n_rows + TS_ROWS - 1) / TS_ROWS, groups);
   float* p = groups > 1 ? partial : nullptr;
   if (staged)
-    hipLaunchKernelGGL((tree_sparse_kernel<KT, true>), grid, dim3(256), x_bytes + red_bytes, st, a, tpg, feat_w, p);
+    IGP_LAUNCH((tree_sparse_kernel<KT, true>), grid, dim3(256), x_bytes + red_bytes, st, a, tpg, feat_w, p);
   else
-    hipLaunchKernelGGL((tree_sparse_kernel<KT, false>), grid, dim3(256), red_bytes, st, a, tpg, feat_w, p);
+    IGP_LAUNCH((tree_sparse_kernel<KT, false>), grid, dim3(256), red_bytes, st, a, tpg, feat_w, p);
   if (groups > 1)
-    hipLaunchKernelGGL(tree_sparse_finish_kernel<KT>, dim3((a.n_rows + 255) / 256), dim3(256), 0, st, a, partial,
+    IGP_LAUNCH(tree_sparse_finish_kernel<KT>, dim3((a.n_rows + 255) / 256), dim3(256), 0, st, a, partial,
                        groups);
 }
 

@@ -169,7 +169,8 @@ def test_streaming_mode_matches_three_stream_mode():
                                  dict(IGP_DIRECT_LAUNCH="1", IGP_SPLIT_STATE="0", IGP_SERIAL_MAX_BUCKET="0"),
                                  dict(IGP_DIRECT_LAUNCH="1", IGP_SERIAL_MAX_BUCKET="4096"),
                                  dict(IGP_DIRECT_LAUNCH="1", IGP_SERIAL_MAX_BUCKET="64"),  # mixed
-                                 dict(IGP_DIRECT_LAUNCH="1", IGP_ASYNC_SUBMIT="1", IGP_SERIAL_MAX_BUCKET="0")])
+                                 dict(IGP_DIRECT_LAUNCH="1", IGP_ASYNC_SUBMIT="1", IGP_SERIAL_MAX_BUCKET="0"),
+                                 dict(IGP_DIRECT_LAUNCH="1", IGP_EXT_EVENTS="0", IGP_SERIAL_MAX_BUCKET="0")])
 def test_direct_launch_and_async_issue_match_graph_replay(env, monkeypatch):
     """The native driver's direct-launch mode (recorded kernel launches instead of graph
     replays, csrc/kernels/oplist.h) and its asynchronous issue thread give bit-identical results,
@@ -188,6 +189,7 @@ def test_direct_launch_and_async_issue_match_graph_replay(env, monkeypatch):
     B = benchkit.build("cfg3", 512, 4096, dev, depth=3, history_batches=4, hot_frac=0.2, buckets=bk)
     assert B.scorer.direct
     assert B.scorer.serial == (int(env["IGP_SERIAL_MAX_BUCKET"]) >= 512)
+    assert B.scorer.driver.ext_events == (env.get("IGP_EXT_EVENTS", "1") != "0")
     rng = np.random.default_rng(5)
     batches = [make_requests(A.pop, n, rng, NOW0, hot_frac=0.2) for n in (512, 300, 512, 17, 512, 64, 200)]
     for i, r in enumerate(batches):
@@ -198,6 +200,42 @@ def test_direct_launch_and_async_issue_match_graph_replay(env, monkeypatch):
         np.testing.assert_array_equal(ra, rb)
         if fa is not None:
             np.testing.assert_array_equal(fa, fb)
+    torch.cuda.synchronize()
+    for name in ("rt", "ring_ts", "ring_amt", "hll"):
+        assert torch.equal(getattr(A.store, name), getattr(B.store, name)), name
+
+
+@pytest.mark.parametrize("ext", ["1", "0"])
+def test_pipelined_direct_launch_matches_graph_replay(ext, monkeypatch):
+    """Three batches in flight (submit ahead, wait oldest): the direct-launch driver with the
+    stage-end events bound to the stages' last kernels (IGP_EXT_EVENTS=1, oplist.h
+    run_recording) or recorded as markers (0) orders the copy / state / model hand-offs, the
+    dedup-region reuse and the slot reuse exactly as graph replay does: identical results and
+    feature-store state."""
+    import torch
+    from igaming_platform_amd.utils import benchkit
+    from igaming_platform_amd.utils.synth import NOW0, make_requests
+    dev = torch.device("cuda", 0)
+    monkeypatch.setenv("IGP_DIRECT_LAUNCH", "0")
+    monkeypatch.setenv("IGP_SERIAL_MAX_BUCKET", "0")
+    A = benchkit.build("cfg3", 2048, 4096, dev, depth=3, history_batches=4, hot_frac=0.3, buckets=[2048])
+    monkeypatch.setenv("IGP_DIRECT_LAUNCH", "1")
+    monkeypatch.setenv("IGP_EXT_EVENTS", ext)
+    B = benchkit.build("cfg3", 2048, 4096, dev, depth=3, history_batches=4, hot_frac=0.3, buckets=[2048])
+    assert B.scorer.direct and B.scorer.driver.ext_events == (ext == "1")
+    rng = np.random.default_rng(17)
+    batches = [make_requests(A.pop, 2048, rng, NOW0, hot_frac=0.3) for _ in range(12)]
+    outs = []
+    for S in (A, B):
+        got, inflight = [], []
+        for i, r in enumerate(batches):
+            inflight.append(S.scorer.submit(r, now=NOW0 + i))
+            if len(inflight) == 3:
+                got.append(S.scorer.wait(inflight.pop(0), unpack=False)[0].copy())
+        got += [S.scorer.wait(p, unpack=False)[0].copy() for p in inflight]
+        outs.append(got)
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
     torch.cuda.synchronize()
     for name in ("rt", "ring_ts", "ring_amt", "hll"):
         assert torch.equal(getattr(A.store, name), getattr(B.store, name)), name
