@@ -56,10 +56,17 @@ class PipeDriver {
         depth_(depth) {
     if (depth < 1 || (int)host_slabs.size() != depth) throw std::runtime_error("PipeDriver: one host slab per slot");
     for (auto h : host_slabs) slabs_.push_back(reinterpret_cast<char*>(h.cast<uintptr_t>()));
+    // the copy / state / post-state events only order work between this device's queues: no
+    // system-scope fence (cache writeback + invalidate at the stage's end, which also slows the
+    // kernels running beside it); the model event keeps it (the host reads results from pinned
+    // memory after it). IGP_EVENT_DEVSCOPE=0 restores system scope everywhere.
+    const char* ds = getenv("IGP_EVENT_DEVSCOPE");
+    const unsigned dev_flags = hipEventDisableTiming | ((ds && atoi(ds) == 0) ? 0u : (unsigned)hipEventDisableSystemFence);
     ev_.resize(3 * depth);
-    for (auto& e : ev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event create");
+    for (size_t i = 0; i < ev_.size(); ++i)
+      hip_ok(hipEventCreateWithFlags(&ev_[i], i % 3 == 2 ? hipEventDisableTiming : dev_flags), "event create");
     pe_.resize(depth);
-    for (auto& e : pe_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event create");
+    for (auto& e : pe_) hip_ok(hipEventCreateWithFlags(&e, dev_flags), "event create");
     recorded_.assign(3 * depth, false);
     host_done_.assign(depth, 0);
     const char* xe = getenv("IGP_EXT_EVENTS");

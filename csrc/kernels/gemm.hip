@@ -488,6 +488,11 @@ __global__ void __launch_bounds__(256) mlp_head_f32_kernel(HeadArgs a, int w_lds
   }
   if (fm)
     for (int i = tid; i < MET_N; i += 256) ecnt[i] = 0;
+  // phase trace of 8 sample blocks (tools/kbench.py): start / staged / mfma done / synced / stored
+  int64_t* const trow = (a.trace && tid == 0 && (blockIdx.x & 31) == 0 && blockIdx.x < 256) ? a.trace + (blockIdx.x >> 5) * 8 : nullptr;
+#define HF_MARK(k) \
+  if (trow) trow[k] = (int64_t)wall_clock64()
+  HF_MARK(0);
   const int kq = kp / 4;  // float4 chunks per row
   if (w_lds) {
     const int total = n1p * kq;
@@ -520,6 +525,7 @@ __global__ void __launch_bounds__(256) mlp_head_f32_kernel(HeadArgs a, int w_lds
     *reinterpret_cast<float4*>(&sA[r * lds_row + kc + 4]) = make_float4(f[4], f[5], f[6], f[7]);
   }
   __syncthreads();
+  HF_MARK(1);
   float part[2][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -562,7 +568,9 @@ __global__ void __launch_bounds__(256) mlp_head_f32_kernel(HeadArgs a, int w_lds
 #pragma unroll
       for (int q = 0; q < 4; ++q) sred[wave * HD_ROWS + i * 16 + (lane >> 4) * 4 + q] = part[i][q];
   }
+  HF_MARK(2);
   __syncthreads();
+  HF_MARK(3);
   if (tid < HD_ROWS) {
     const int row = row0 + tid;
     float y = 0.f;
@@ -577,6 +585,164 @@ __global__ void __launch_bounds__(256) mlp_head_f32_kernel(HeadArgs a, int w_lds
     __syncthreads();
     ensemble_metrics_flush(a.ens, ecnt, tid, 256);
   }
+  if (trow) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    HF_MARK(4);
+  }
+#undef HF_MARK
+}
+
+// mlp_head f32, specialised on k_pad (KP = 32 / 64) and the hidden activation (ACT), W1 staged
+// in LDS: what the generic kernel above lost to its runtime shape (compiler output of the generic
+// k loop: a flat load selecting LDS or global W1 per k-step behind a full vmcnt/lgkmcnt wait, the
+// two accumulators shuffled through AGPR moves every iteration, and a four-way activation switch
+// per element; phase trace 5 us staging + 5 us for 64 MFMAs per wave). Here every staging load
+// (the first 8 W1 chunks per thread, b1 / w2, the A chunk with all tree-group partials) is in
+// flight before anything is stored (one memory round trip), the A fragments of both row tiles
+// stay in registers across the column chunks, and the k loop is unrolled. Same MFMA sequence
+// and summation order as the generic kernel: bit-identical results.
+template <int KP, int ACT>
+__global__ void __launch_bounds__(256) mlp_head_f32_fast_kernel(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  constexpr int LR = KP + 4;  // LDS row stride (floats)
+  constexpr int KQ = KP / 4;  // float4 chunks per W1 row
+  constexpr int K8 = KP / 8;  // 8-float A chunks per row
+  constexpr int KS = KP / 16;  // k-steps of four 16x16x4 MFMAs
+  const float* const W1 = reinterpret_cast<const float*>(a.W1);
+  const int n1p = (a.N1 + 63) & ~63;
+  float* sA = smf;
+  float* sW = sA + HD_ROWS * LR;
+  float* sred = sW + n1p * LR;
+  float* sb1 = sred + 4 * HD_ROWS;
+  float* sw2 = sb1 + n1p;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = a.m_ptr ? min(*a.m_ptr, a.M) : a.M;
+  const int row0 = blockIdx.x * HD_ROWS;
+  __shared__ unsigned int ecnt[MET_N];
+  const bool fm = a.fuse_ens && a.ens.metrics;
+  if (row0 >= M) {
+    if (a.fuse_ens)
+      for (int r = row0 + tid; r < min(row0 + HD_ROWS, a.ens.n_rows); r += 256) ensemble_row(a.ens, r, true, 0.f, nullptr);
+    return;
+  }
+  if (fm)
+    for (int i = tid; i < MET_N; i += 256) ecnt[i] = 0;
+  int64_t* const trow = (a.trace && tid == 0 && (blockIdx.x & 31) == 0 && blockIdx.x < 256) ? a.trace + (blockIdx.x >> 5) * 8 : nullptr;
+#define HQ_MARK(k) \
+  if (trow) trow[k] = (int64_t)wall_clock64()
+  HQ_MARK(0);
+  const int total = n1p * KQ;
+  float4 wv[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int ch = u * 256 + tid;
+    wv[u] = ch < total ? *reinterpret_cast<const float4*>(W1 + (size_t)(ch / KQ) * KP + (ch % KQ) * 4)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const float b1v = (tid < a.N1 && a.b1) ? a.b1[tid] : 0.f;
+  const float w2v = tid < a.N1 ? a.w2[tid] : 0.f;
+  const bool has_a = tid < HD_ROWS * K8;
+  float f[8];
+  uint4 raw;
+  if (has_a) head_a_f32(a, row0 + tid / K8, (tid % K8) * 8, M, f, &raw);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int ch = u * 256 + tid;
+    if (ch < total) *reinterpret_cast<float4*>(&sW[(ch / KQ) * LR + (ch % KQ) * 4]) = wv[u];
+  }
+  for (int ch = 8 * 256 + tid; ch < total; ch += 256)  // W1 wider than 8 chunks per thread
+    *reinterpret_cast<float4*>(&sW[(ch / KQ) * LR + (ch % KQ) * 4]) =
+        *reinterpret_cast<const float4*>(W1 + (size_t)(ch / KQ) * KP + (ch % KQ) * 4);
+  if (tid < n1p) {
+    sb1[tid] = b1v;
+    sw2[tid] = w2v;
+  }
+  for (int n = tid + 256; n < n1p; n += 256) {
+    sb1[n] = (n < a.N1 && a.b1) ? a.b1[n] : 0.f;
+    sw2[n] = n < a.N1 ? a.w2[n] : 0.f;
+  }
+  if (has_a) {
+    const int r = tid / K8, kc = (tid % K8) * 8;
+    *reinterpret_cast<float4*>(&sA[r * LR + kc]) = make_float4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<float4*>(&sA[r * LR + kc + 4]) = make_float4(f[4], f[5], f[6], f[7]);
+  }
+  for (int ch = tid + 256; ch < HD_ROWS * K8; ch += 256) {
+    const int r = ch / K8, kc = (ch % K8) * 8;
+    head_a_f32(a, row0 + r, kc, M, f, &raw);
+    *reinterpret_cast<float4*>(&sA[r * LR + kc]) = make_float4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<float4*>(&sA[r * LR + kc + 4]) = make_float4(f[4], f[5], f[6], f[7]);
+  }
+  __syncthreads();
+  HQ_MARK(1);
+  float4 av[2][KS];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      av[i][s] = *reinterpret_cast<const float4*>(&sA[(i * 16 + (lane & 15)) * LR + s * 16 + 4 * (lane >> 4)]);
+  float part[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) part[i][q] = 0.f;
+  for (int c0 = 0; c0 < a.N1; c0 += 64) {
+    const int n = c0 + wave * 16 + (lane & 15);
+    float4 bv[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) bv[s] = *reinterpret_cast<const float4*>(&sW[n * LR + s * 16 + 4 * (lane >> 4)]);
+    const float b1 = sb1[n];
+    const float w2 = sw2[n];
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      acc0 = mfma4_f32(av[0][s], bv[s], acc0);
+      acc1 = mfma4_f32(av[1][s], bv[s], acc1);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      part[0][q] += act_fn(acc0[q] + b1, ACT) * w2;
+      part[1][q] += act_fn(acc1[q] + b1, ACT) * w2;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v = part[i][q];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      part[i][q] = v;
+    }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sred[wave * HD_ROWS + i * 16 + (lane >> 4) * 4 + q] = part[i][q];
+  }
+  HQ_MARK(2);
+  __syncthreads();
+  HQ_MARK(3);
+  if (tid < HD_ROWS) {
+    const int row = row0 + tid;
+    float y = 0.f;
+    if (row < M) {
+      const float v = sred[tid] + sred[HD_ROWS + tid] + sred[2 * HD_ROWS + tid] + sred[3 * HD_ROWS + tid];
+      y = act_fn(v + a.b2, a.act2);
+      a.Y[(size_t)row * a.ldy] = y;
+    }
+    if (a.fuse_ens && row < a.ens.n_rows) ensemble_row(a.ens, row, true, y, fm ? ecnt : nullptr);
+  }
+  if (fm) {
+    __syncthreads();
+    ensemble_metrics_flush(a.ens, ecnt, tid, 256);
+  }
+  if (trow) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    HQ_MARK(4);
+  }
+#undef HQ_MARK
 }
 
 // f32 dense layer: 64 x 64 output tile per block, 4 waves in 2 x 2 (32 x 32 each = 2 x 2
@@ -686,7 +852,19 @@ void launch_mlp_head(const HeadArgs& a, hipStream_t st) {
     const int w_lds = n1p * lds_row * 4 <= (size_t)(96 * 1024);
     const size_t lds = ((size_t)HD_ROWS + (w_lds ? n1p : 0)) * lds_row * 4 + 4 * HD_ROWS * sizeof(float) +
                        2 * n1p * sizeof(float);
-    IGP_LAUNCH(mlp_head_f32_kernel, dim3((a.M + HD_ROWS - 1) / HD_ROWS), dim3(256), lds, st, a, w_lds);
+    const dim3 grid((a.M + HD_ROWS - 1) / HD_ROWS);
+    static const bool generic = [] {  // A/B switch: IGP_HEAD_GENERIC=1 runs the generic kernel
+      const char* e = getenv("IGP_HEAD_GENERIC");
+      return e && atoi(e) != 0;
+    }();
+    if (w_lds && (a.k_pad == 32 || a.k_pad == 64) && a.act1 >= 0 && a.act1 <= 3 && !generic) {
+#define HQ_CASE(KP, ACT) \
+  if (a.k_pad == KP && a.act1 == ACT) { IGP_LAUNCH((mlp_head_f32_fast_kernel<KP, ACT>), grid, dim3(256), lds, st, a); return; }
+      HQ_CASE(32, 0) HQ_CASE(32, 1) HQ_CASE(32, 2) HQ_CASE(32, 3)
+      HQ_CASE(64, 0) HQ_CASE(64, 1) HQ_CASE(64, 2) HQ_CASE(64, 3)
+#undef HQ_CASE
+    }
+    IGP_LAUNCH(mlp_head_f32_kernel, grid, dim3(256), lds, st, a, w_lds);
     return;
   }
   const size_t lds_row = (size_t)a.k_pad + G_PAD;
