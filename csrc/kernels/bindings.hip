@@ -238,6 +238,14 @@ PYBIND11_MODULE(_hipk, m) {
     a.trace = ptr<int64_t*>(d, "trace");
     const int groups = geti(d, "groups", 1);
     float* partial = ptr<float*>(d, "partial");
+    if (d.contains("ens") && !d["ens"].is_none()) {
+      // K5 fused into the finish kernel: only a grouped launch has one
+      if (groups <= 1 || !partial || a.no_finish) throw std::runtime_error("tree_ensemble: ensemble fusion needs a grouped launch");
+      a.fuse_ens = 1;
+      a.ens = ensemble_args(d["ens"].cast<py::dict>());
+      if (!a.ens.hdr || !a.ens.cfg || !a.ens.feat || !a.ens.out || a.ens.ml != a.out)
+        throw std::runtime_error("tree_ensemble: ensemble args (ml must be the tree output)");
+    }
     launch_or_record([a, groups, partial](hipStream_t st) { launch_tree_ensemble_grouped(a, groups, partial, st); },
                      s, "tree_ensemble");
   });

@@ -83,6 +83,18 @@ void launch_dedup_insert(const UpdateArgs& a, hipStream_t st);
 void launch_update_segments(const UpdateArgs& a, hipStream_t st);
 
 // ---- K2 tree ensemble (complete layout)
+struct EnsembleArgs {
+  const BatchHdr* hdr;
+  const ScoreCfg* cfg;
+  const FeatRec* feat;
+  const float* X;           // for the heuristic model
+  int32_t x_stride;
+  const float* ml;          // model output (nullable)
+  ResultRec* out;
+  ResultRec* host_out;      // nullable: pinned host rows written directly (no D2H copy node)
+  unsigned long long* metrics;  // [128] score histogram(101) | actions(4) | ml_high | rows (nullable)
+  int32_t n_rows;
+};
 struct TreeArgs {
   const BatchHdr* hdr;      // nullable: all n_rows live
   const float* X;           // [n][x_stride]
@@ -103,6 +115,8 @@ struct TreeArgs {
   int32_t no_finish;        // grouped launch: leave partials for the consumer (mlp_head)
   int32_t all_leq;          // every node BRANCH_LEQ (fast decision path; missing tracks allowed)
   int64_t* trace;           // nullable: phase trace of sample blocks (tools/tree_bench.py)
+  int32_t fuse_ens;         // grouped launch: K5 in the finish kernel's epilogue (ml = out)
+  EnsembleArgs ens;
 };
 void launch_tree_ensemble(const TreeArgs& a, hipStream_t st);
 void launch_tree_ensemble_grouped(const TreeArgs& a, int groups, float* partial, hipStream_t st);
@@ -148,18 +162,6 @@ void launch_gemv(const GemmArgs& a, hipStream_t st);  // N == 1 heads
 
 // dense(N1) + act1 + dense(N1 -> 1) + act2 fused; W1 bf16 [N1_pad(64)][k_pad(32)]
 // ---- K5 ensemble + action + metrics
-struct EnsembleArgs {
-  const BatchHdr* hdr;
-  const ScoreCfg* cfg;
-  const FeatRec* feat;
-  const float* X;           // for the heuristic model
-  int32_t x_stride;
-  const float* ml;          // model output (nullable)
-  ResultRec* out;
-  ResultRec* host_out;      // nullable: pinned host rows written directly (no D2H copy node)
-  unsigned long long* metrics;  // [128] score histogram(101) | actions(4) | ml_high | rows (nullable)
-  int32_t n_rows;
-};
 struct HeadArgs {
   const void* X;
   const void* W1;           // bf16, or f32 when w1_f32 (reference-precision head)

@@ -12,6 +12,7 @@
 // Several tree groups per sample tile (small batches) write partial sums to a slab; a
 // finisher (or the consuming mlp_head kernel) adds base values and the post transform.
 #include "common.h"
+#include "ensemble.h"
 #include "launch.h"
 #include "tree_post.h"
 
@@ -328,6 +329,36 @@ __global__ void tree_finish_kernel(TreeArgs a, const float* partial, int groups)
   post_row(a, s, a.out + (size_t)row * a.n_out, K);
 }
 
+// the finish kernel with the scorer's K5 ensemble in its epilogue (cfg 2: a grouped tree
+// classifier is the whole model): the row's ensemble reads the model column this thread just
+// wrote, so the standalone ensemble launch (and its queue slot) goes away. Rows past n_rows up to
+// ens.n_rows get their (zero) results as in ensemble_kernel.
+__global__ void __launch_bounds__(256) tree_finish_ens_kernel(TreeArgs a, const float* partial, int groups) {
+  __shared__ unsigned int cnt[MET_N];
+  const int tid = threadIdx.x;
+  const bool fm = a.ens.metrics != nullptr;
+  if (fm) {
+    for (int i = tid; i < MET_N; i += 256) cnt[i] = 0;
+    __syncthreads();
+  }
+  const int row = blockIdx.x * 256 + tid;
+  if (row < a.n_rows) {
+    const int K = a.k;
+    float s[64];
+    for (int k = 0; k < K; ++k) {
+      float v = 0.f;
+      for (int g = 0; g < groups; ++g) v += partial[((size_t)g * a.n_rows + row) * K + k];
+      s[k] = v;
+    }
+    post_row(a, s, a.out + (size_t)row * a.n_out, K);
+  }
+  if (row < a.ens.n_rows) ensemble_row(a.ens, row, false, 0.f, fm ? cnt : nullptr);
+  if (fm) {
+    __syncthreads();
+    ensemble_metrics_flush(a.ens, cnt, tid, 256);
+  }
+}
+
 // regressor / multi-output without a row-wise post transform: one thread per (row, target)
 __global__ void tree_finish_elem_kernel(TreeArgs a, const float* partial, int groups) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -357,7 +388,10 @@ static void launch_kl(const TreeArgs& a, int groups, float* partial, int no_fini
   IGP_LAUNCH((tree_kernel<K, LEQ>), grid, dim3(256), lds, st, a, tpg, feat_w, in_lds,
                      groups > 1 ? partial : nullptr);
   if (groups > 1 && !no_finish) {
-    if (!post_rowwise(a) && a.n_out == K)
+    if (a.fuse_ens) {
+      const int rows = a.n_rows > a.ens.n_rows ? a.n_rows : a.ens.n_rows;
+      IGP_LAUNCH(tree_finish_ens_kernel, dim3((rows + 255) / 256), dim3(256), 0, st, a, partial, groups);
+    } else if (!post_rowwise(a) && a.n_out == K)
       IGP_LAUNCH(tree_finish_elem_kernel, dim3((a.n_rows * K + 255) / 256), dim3(256), 0, st, a,
                          partial, groups);
     else

@@ -115,7 +115,7 @@ class DpGpuScorer(GpuScorer):
 
     def _xmodel_body(self, slot: int, C: int, with_features: bool) -> None:
         sb, b = self.slots[slot], self.cap(C)
-        if sb.model is not None and sb.model.fuses_ensemble():
+        if sb.model is not None and sb.model.fuses_ensemble(b):
             ens = K.ensemble_args(sb.hdr, self.cfg_dev, sb.feat, sb.X, sb.model.step_out[-1], sb.res, b, self.metrics)
             sb.model.run(sb.X, b, m_ptr=sb.n_ptr, ens=ens)
         else:

@@ -70,18 +70,26 @@ class DeviceModel:
     def out_width(self) -> int:
         return self.plan.out_width
 
-    def fuses_ensemble(self) -> bool:
-        """Whether :meth:`run` can run the scorer's K5 ensemble in the epilogue of its last step
-        (an N=1 MLP head whose output column is the model score)."""
+    def fuses_ensemble(self, bucket: Optional[int] = None) -> bool:
+        """Whether :meth:`run` can run the scorer's K5 ensemble in the epilogue of its last step:
+        an N=1 MLP head whose output column is the model score, or (for ``bucket``) a
+        complete-layout tree ensemble as the only step, launched in groups, whose finish kernel
+        then runs K5 (IGP_FUSE_TREE_ENS=0 keeps the standalone ensemble there)."""
         steps = self.plan.steps
-        return (self.gru is None and bool(steps) and steps[-1].kind == "head" and self.plan.ml_col == 0)
+        if self.gru is not None or not steps:
+            return False
+        if steps[-1].kind == "head":
+            return self.plan.ml_col == 0
+        return (bucket is not None and len(steps) == 1 and steps[0].kind == "tree"
+                and steps[0].layout != "sparse" and self.tree_groups.get(bucket, 1) > 1
+                and os.environ.get("IGP_FUSE_TREE_ENS", "1") != "0")
 
     def run(self, X: torch.Tensor, bucket: int, m_ptr: Optional[torch.Tensor] = None,
             ens: Optional[dict] = None) -> torch.Tensor:
         """X: [rows, in] f32 (or [T, rows, I] for a GRU model); returns the last step's buffer.
         ``ens`` (only when :meth:`fuses_ensemble`): K5 arguments for the fused head epilogue."""
         steps = self.plan.steps
-        if ens is not None and not self.fuses_ensemble():
+        if ens is not None and not self.fuses_ensemble(bucket):
             raise ValueError("this plan cannot fuse the ensemble")
         if self.gru is not None:
             T = X.shape[0]
@@ -101,7 +109,7 @@ class DeviceModel:
                 fuse = (g > 1 and i + 1 < len(steps) and steps[i + 1].kind == "head" and s.post == 0
                         and s.binary_class < 0 and steps[i + 1].k == s.k)
                 K.tree_ensemble(s, cur, None if fuse else out, bucket, partial=self.tree_partial,
-                                groups=g, no_finish=fuse)
+                                groups=g, no_finish=fuse, ens=ens if i == len(steps) - 1 else None)
                 fused_partial = (self.tree_partial, g, s) if fuse else None
             elif s.kind == "dense":
                 K.dense(cur, s.w, s.b, out, bucket, s.n, s.k, act=s.act, m_ptr=m_ptr)

@@ -274,8 +274,8 @@ class GpuScorer:
         # K5 writes the result rows straight into the slot's pinned host buffer as well (no
         # D2H copy node on the model stream); IGP_HOST_RESULTS=0 restores the copy
         host = self.host_res[slot] if self._host_results else None
-        if sb.model is not None and sb.model.fuses_ensemble() and os.environ.get("IGP_FUSE_ENS", "1") != "0":
-            # K5 in the MLP head's epilogue: one launch fewer, ml never re-read
+        if sb.model is not None and sb.model.fuses_ensemble(bucket) and os.environ.get("IGP_FUSE_ENS", "1") != "0":
+            # K5 in the MLP head's (or the grouped trees' finish kernel's) epilogue: one launch fewer
             ens = K.ensemble_args(sb.hdr, self.cfg_dev, sb.feat, sb.X, sb.model.step_out[-1], sb.res, bucket,
                                   self.metrics, host_out=host)
             sb.model.run(sb.X, bucket, m_ptr=sb.n_ptr, ens=ens)

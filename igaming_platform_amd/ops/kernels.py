@@ -196,9 +196,11 @@ def update_segments(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int,
 # --------------------------------------------------------------------------- K2
 def tree_ensemble(tp, X: torch.Tensor, out: Optional[torch.Tensor], n_rows: int,
                   partial: Optional[torch.Tensor] = None, groups: int = 1, no_finish: bool = False,
-                  trace: Optional[torch.Tensor] = None) -> None:
+                  trace: Optional[torch.Tensor] = None, ens: Optional[dict] = None) -> None:
     """``tp``: models.plan.TreeStep with device tensors. ``trace``: int64 [64] phase timestamps
-    (wall_clock64) of 8 sample workgroups, for tools/tree_bench.py."""
+    (wall_clock64) of 8 sample workgroups, for tools/tree_bench.py. ``ens``
+    (:func:`ensemble_args` with ``ml`` = ``out``, grouped launches only): the scorer's K5
+    ensemble runs in the finish kernel's epilogue."""
     dev = X.device
     if tp.k not in (1, 2, 4, 8, 16, 32, 64):
         raise ValueError(f"tree kernel built for K in 1,2,4,8,16,32,64; got {tp.k}")
@@ -210,6 +212,8 @@ def tree_ensemble(tp, X: torch.Tensor, out: Optional[torch.Tensor], n_rows: int,
         raise ValueError("no_finish needs a grouped launch")
     if out is None and not no_finish:
         raise ValueError("tree_ensemble: out required")
+    if ens is not None and (groups <= 1 or no_finish or ens.get("ml") != out.data_ptr()):
+        raise ValueError("tree_ensemble: ensemble fusion needs a grouped launch whose output is the ml input")
     d = dict(
         X=_need(X, "X", torch.float32, X.shape[1] * n_rows), nodes=_need(tp.nodes, "nodes", torch.float32, device=dev),
         leaves=_need(tp.leaves, "leaves", torch.float32, device=dev), base=_opt(tp.base, "base", dtype=torch.float32),
@@ -217,7 +221,7 @@ def tree_ensemble(tp, X: torch.Tensor, out: Optional[torch.Tensor], n_rows: int,
         n_rows=int(n_rows), n_trees=tp.n_trees, depth=tp.depth, k=tp.k, n_out=tp.n_out, post=tp.post,
         average=tp.average, binary_class=tp.binary_class, all_positive=tp.all_positive,
         groups=int(groups), partial=_opt(partial, "partial", dtype=torch.float32), no_finish=int(no_finish),
-        all_leq=int(tp.all_leq), trace=_opt(trace, "trace", dtype=torch.int64, min_numel=64),
+        all_leq=int(tp.all_leq), trace=_opt(trace, "trace", dtype=torch.int64, min_numel=64), ens=ens,
     )
     if tp.nodes.numel() < tp.n_trees * ((1 << tp.depth) - 1) * 2:
         raise ValueError("node table smaller than n_trees * (2^depth - 1)")

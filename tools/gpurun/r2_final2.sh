@@ -11,6 +11,11 @@ for c in cfg3 cfg2 cfg4 cfg5 heuristic; do
   timeout -k 10 300 python bench.py --config $c --steps 2000 --warmup 100 --json-out $O/bench_$c.json >> $O/bench.log 2>&1 || exit 3
 done
 timeout -k 10 200 python bench.py --json-out $O/bench_default.json >> $O/bench.log 2>&1 || exit 4
+for i in 1 2; do  # cfg2: K5 fused into the tree finish kernel vs the standalone ensemble
+  for f in 0 1; do
+    IGP_FUSE_TREE_ENS=$f timeout -k 10 200 python bench.py --config cfg2 --steps 2000 --warmup 100 --json-out $O/cfg2_fuse${f}_$i.json >> $O/bench.log 2>&1 || exit 4
+  done
+done
 timeout -k 10 300 python bench.py --scope e2e --steps 200 --warmup 20 --json-out $O/scope_e2e.json > $O/scope_e2e.log 2>&1 || exit 5
 timeout -k 10 300 python bench.py --scope grpc --rpc batch --json-out $O/scope_grpc_batch.json > $O/scope_grpc_batch.log 2>&1 || exit 6
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/f3 -o run -- python bench.py --steps 300 --warmup 30 > $O/prof3.log 2>&1 || exit 7
