@@ -444,7 +444,9 @@ def to_device(plan: Plan, device, precision: str = "fp32") -> Plan:
             s.w = pad(s.w_np).to(device)
             s.b = None if s.b_np is None else torch.from_numpy(np.ascontiguousarray(s.b_np)).to(device)
         elif s.kind == "head":
-            s.w1 = pad(s.w1_np).to(device)
+            # f32 head: K padded to 32 only (the f32 MFMA k-step is 16; the specialised kernel is
+            # built for k_pad 32 / 64), so a 32-wide tree embedding runs no all-zero k-steps
+            s.w1 = (_f32_padded(s.w1_np, k_mult=32) if precision == "fp32" else pad(s.w1_np)).to(device)
             s.b1 = None if s.b1_np is None else torch.from_numpy(np.ascontiguousarray(s.b1_np)).to(device)
             s.w2 = torch.from_numpy(s.w2_np).to(device)
     return plan
