@@ -105,6 +105,9 @@ def main():
     # copy / state / model streams, the default stream and RCCL's communication stream (N > 1)
     # each get a queue of their own when 8 are allowed. Set before the HIP runtime initialises.
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    # dmabuf IPC for RCCL / cross-process tensors: read when the HIP runtime initialises
+    # (torch.cuda.set_device below), so it must be in the environment before that
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     import torch
     import torch.distributed as dist
 
@@ -119,7 +122,6 @@ def main():
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
     if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:

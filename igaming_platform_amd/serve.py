@@ -54,6 +54,7 @@ def main(argv=None) -> int:
     # copy / state / model streams, the exchange's two RCCL streams and the default stream each
     # get a queue of their own with 8 (must be set before the HIP runtime initialises)
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL across processes)
     cfg = Config.load(a.config or None)
     if a.snapshot_dir:
         cfg.gpu.snapshot_dir = a.snapshot_dir  # failed shards are re-homed from here
