@@ -128,18 +128,19 @@ __device__ __forceinline__ void ws_epilogue(const f32x4 (&acc)[4][2], float (&hs
     }
 }
 
-template <int L>
+// row tiles [RT0, RT0 + NRT) of one layer's step (NRT even)
+template <int L, int RT0 = 0, int NRT = WS_RT>
 __device__ __forceinline__ void ws_layer(const bf16x8 (&wz)[16], const bf16x8 (&wr)[16], const bf16x8 (&wh)[16],
                                          const uint16_t* X, const uint16_t* H1, const uint16_t* H2,
                                          float (&hs)[WS_RT][4], const float (&bv)[4], int lane) {
   f32x4 acc[2][4][2];
-  ws_mfma_pair<L>(wz, wr, wh, X, H1, H2, 0, lane, acc[0]);
+  ws_mfma_pair<L>(wz, wr, wh, X, H1, H2, RT0, lane, acc[0]);
 #pragma unroll
-  for (int p = 1; p < WS_RT / 2; ++p) {
-    ws_mfma_pair<L>(wz, wr, wh, X, H1, H2, 2 * p, lane, acc[p & 1]);
-    ws_epilogue(acc[(p - 1) & 1], hs, bv, 2 * (p - 1));
+  for (int p = 1; p < NRT / 2; ++p) {
+    ws_mfma_pair<L>(wz, wr, wh, X, H1, H2, RT0 + 2 * p, lane, acc[p & 1]);
+    ws_epilogue(acc[(p - 1) & 1], hs, bv, RT0 + 2 * (p - 1));
   }
-  ws_epilogue(acc[(WS_RT / 2 - 1) & 1], hs, bv, WS_RT - 2);
+  ws_epilogue(acc[(NRT / 2 - 1) & 1], hs, bv, RT0 + NRT - 2);
 }
 #undef MFMA
 
@@ -155,6 +156,10 @@ __device__ __forceinline__ bool ws_wait(int32_t* cnt, int target) {
   }
 }
 
+// SPLIT: the cluster's 128 sequences as two independent 64-row halves in a software pipeline
+// (IGP_GRU_SPLIT): the hand-off of one half (sc1 stores draining, counter, gather) runs beside
+// the other half's MFMAs; counters cnt[0] (half A) and cnt[8] (half B).
+template <bool SPLIT>
 __global__ void __launch_bounds__(256, 1) gru_ws_kernel(GruArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // LDS: H1[M][HS] | H2[M][HS] | X[2][M][XS] (bf16) | red[2][M] f32 | xmeta[4M] | flag
@@ -298,6 +303,120 @@ __global__ void __launch_bounds__(256, 1) gru_ws_kernel(GruArgs a) {
   int64_t* const trace = (a.ws_trace && b == 0 && tid == 0) ? a.ws_trace : nullptr;
 #define WS_MARK(t, k) \
   if (trace && (t) < 64) trace[(t) * 6 + (k)] = (int64_t)wall_clock64()
+  if constexpr (SPLIT) {
+    int32_t* const cntB = cnt + 8;
+    // own columns of half h (rows 64h .. 64h + 63) of this wave's layer -> LDS
+    auto own_cols = [&](int h) {
+#pragma unroll
+      for (int rt = 0; rt < WS_RT / 2; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Hl[((4 * h + rt) * 16 + crow + r) * WS_HS + j] = f32_to_bf16(hs[4 * h + rt][r]);
+    };
+    // this member's slice of half h (both layers, 512 16-B chunks, 2 per thread) -> slab, no wait
+    auto publish = [&](int h, int par) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = i * 512 + 256 * h + tid;
+        const int row = (c >> 2) & (WS_M - 1), q = c & 3;
+        const uint16_t* src = (i ? H2 : H1) + row * WS_HS + mem * WS_UW + q * 8;
+        const u32x4 v = __builtin_bit_cast(u32x4, *reinterpret_cast<const uint4*>(src));
+        __builtin_amdgcn_raw_buffer_store_b128(v, xr, c * 16, ((par * WS_CL + mem) * WS_SLICE) * 2, SC1);
+      }
+    };
+    // the other seven members' slices of half h (14 chunks per thread) -> LDS
+    auto gather = [&](int h, int par) {
+      u32x4 v[14];
+#pragma unroll
+      for (int i = 0; i < 14; ++i) {
+        const int k = i * 256 + tid;
+        int m2 = k >> 9;
+        m2 += m2 >= mem;
+        const int w = k & 511;
+        const int c = (w >> 8) * 512 + 256 * h + (w & 255);
+        v[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, c * 16, ((par * WS_CL + m2) * WS_SLICE) * 2, SC1);
+      }
+#pragma unroll
+      for (int i = 0; i < 14; ++i) {
+        const int k = i * 256 + tid;
+        int m2 = k >> 9;
+        m2 += m2 >= mem;
+        const int w = k & 511;
+        const int c = (w >> 8) * 512 + 256 * h + (w & 255);
+        const int row = (c >> 2) & (WS_M - 1), q = c & 3;
+        *reinterpret_cast<uint4*>(((w >> 8) ? H2 : H1) + row * WS_HS + m2 * WS_UW + q * 8) = __builtin_bit_cast(uint4, v[i]);
+      }
+    };
+    // arrival (one lane) + bounded wait for all members; false: give up (the cluster exits)
+    auto arrive_wait = [&](int32_t* c, int target, bool arrive) -> bool {
+      if (tid == 0) {
+        if (arrive) __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool ok = true;
+        if (target > 0) {
+          ok = ws_wait(c, target);
+          if (!ok) atomicExch(a.ws_err, 1);
+        }
+        *sflag = ok;
+      }
+      __syncthreads();
+      return *sflag != 0;
+    };
+    for (int t = 0; t <= T; ++t) {
+      WS_MARK(t, 0);
+      const bool act = layer == 0 ? (t < T) : (t >= 1);
+      // ---- half A of step t (+ x_{t+1} staging for all rows)
+      if (layer == 0) {
+        uint4 xn[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int c = tid + 128 * u;
+          xn[u] = c < nchunk ? load_x(c, t + 1) : make_uint4(0, 0, 0, 0);
+        }
+        if (act) ws_layer<0, 0, WS_RT / 2>(wz, wr, wh, Xb + (t & 1) * (WS_M * WS_XS), H1, H2, hs, bv, lane);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int c = tid + 128 * u;
+          if (c < nchunk) *x_slot((t + 1) & 1, c) = xn[u];
+        }
+      } else if (act) {
+        ws_layer<1, 0, WS_RT / 2>(wz, wr, wh, Xb + (t & 1) * (WS_M * WS_XS), H1, H2, hs, bv, lane);
+      }
+      __syncthreads();  // every wave is done reading rows A
+      WS_MARK(t, 1);
+      if (t < T && act) own_cols(0);
+      // half B of step t-1: its stores drained under half A's MFMAs -> arrive
+      if (t >= 1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(cntB, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (t < T) publish(0, t & 1);  // drains under the gather and half B's MFMAs
+      if (t >= 1) {
+        if (!arrive_wait(cntB, WS_CL * t, false)) return;
+        gather(1, (t - 1) & 1);
+        __syncthreads();
+      }
+      WS_MARK(t, 2);
+      // ---- half B of step t
+      if (layer == 0) {
+        if (act) ws_layer<0, WS_RT / 2, WS_RT / 2>(wz, wr, wh, Xb + (t & 1) * (WS_M * WS_XS), H1, H2, hs, bv, lane);
+      } else if (act) {
+        ws_layer<1, WS_RT / 2, WS_RT / 2>(wz, wr, wh, Xb + (t & 1) * (WS_M * WS_XS), H1, H2, hs, bv, lane);
+      }
+      __syncthreads();  // every wave is done reading rows B
+      WS_MARK(t, 3);
+      if (t == T) break;
+      if (act) own_cols(1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // half A's stores of step t
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      publish(1, t & 1);
+      if (!arrive_wait(cnt, WS_CL * (t + 1), false)) return;
+      gather(0, t & 1);
+      __syncthreads();
+      WS_MARK(t, 4);
+    }
+  } else
   for (int t = 0; t <= T; ++t) {
     WS_MARK(t, 0);
     const bool act = layer == 0 ? (t < T) : (t >= 1);
@@ -443,7 +562,10 @@ __global__ void __launch_bounds__(256, 1) gru_ws_kernel(GruArgs a) {
     if (a.head_act == 2) v = 1.f / (1.f + expf(-v));
     a.out[row0 + tid] = v;
   }
-  if (tid == 0) __hip_atomic_exchange(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) {
+    __hip_atomic_exchange(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (SPLIT) __hip_atomic_exchange(cnt + 8, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 }  // namespace
@@ -465,7 +587,8 @@ bool gru_ws_eligible(const GruArgs& a) {
 void launch_gru_ws(const GruArgs& a, hipStream_t st) {
   const int ncl = gru_ws_clusters(a.n_rows);
   const int grid = ((ncl + 7) / 8) * 64;
-  IGP_LAUNCH(gru_ws_kernel, dim3(grid), dim3(256), gru_ws_lds_bytes(), st, a);
+  if (a.ws == 2) IGP_LAUNCH(gru_ws_kernel<true>, dim3(grid), dim3(256), gru_ws_lds_bytes(), st, a);
+  else IGP_LAUNCH(gru_ws_kernel<false>, dim3(grid), dim3(256), gru_ws_lds_bytes(), st, a);
 }
 
 }  // namespace igp

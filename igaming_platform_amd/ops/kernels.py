@@ -481,21 +481,29 @@ class GruPack:
 
 
 _GRU_WS = os.environ.get("IGP_GRU_WS", "1") != "0"  # 0: always the batch-parallel K4 (A/B runs)
+# 1: the cluster kernel runs its 128 sequences as two software-pipelined halves (gru_ws.hip SPLIT)
+_GRU_SPLIT = os.environ.get("IGP_GRU_SPLIT", "0") == "1"
 
 
 def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh: Optional[torch.Tensor] = None,
         X: Optional[torch.Tensor] = None, store=None, slots: Optional[torch.Tensor] = None,
         m_ptr: Optional[torch.Tensor] = None, tile_rows: int = 0, waves: int = 0, pipeline: int = 1,
-        ws: int = 1, ws_trace: Optional[torch.Tensor] = None) -> None:
+        ws: Optional[int] = None, ws_trace: Optional[torch.Tensor] = None) -> None:
     """K4. Input either dense ``X`` f32 [T, rows, I] or the store's event rings for ``slots``.
-    ``ws=1`` runs the weight-stationary cluster kernel when the model shape allows it."""
+    ``ws``: 0 the batch-parallel kernel; 1 the weight-stationary cluster kernel when the model
+    shape allows it; 2 the same with its two-half hand-off pipeline; None: 1, or 2 under
+    IGP_GRU_SPLIT=1."""
+    if ws is None:
+        ws = 2 if _GRU_SPLIT else 1
+    if ws not in (0, 1, 2):
+        raise ValueError("gru: ws must be 0, 1 or 2")
     dev = gp.device
     d = dict(n_layers=gp.n_layers, H=gp.H, T=int(T), I=gp.I, n_rows=int(n_rows),
              m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32, device=dev), tile_rows=int(tile_rows),
              waves=int(waves or gp.waves), pipeline=int(pipeline))
     w = gp.workspace(n_rows) if ws and _GRU_WS else None
     if w is not None:
-        d.update(ws=1, ws_clusters=w["clusters"], ws_sync=w["sync"].data_ptr(), ws_x=w["x"].data_ptr(),
+        d.update(ws=int(ws), ws_clusters=w["clusters"], ws_sync=w["sync"].data_ptr(), ws_x=w["x"].data_ptr(),
                  ws_part=w["part"].data_ptr(), ws_err=gp.ws_err.data_ptr(),
                  ws_trace=_opt(ws_trace, "ws_trace", dtype=torch.int64, min_numel=64 * 8 + 4, device=dev))
     for i, l in enumerate(gp.layers):

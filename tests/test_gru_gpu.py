@@ -122,6 +122,28 @@ def test_gru_weight_stationary_matches_batch_parallel(rows):
         np.testing.assert_allclose(a, ref, rtol=0, atol=1e-2)
 
 
+@pytest.mark.parametrize("rows", [130, 4096, 4500])
+def test_gru_weight_stationary_split_matches_unsplit(rows):
+    """The cluster kernel's two-half pipeline (ws=2: one half's hand-off beside the other
+    half's MFMAs, separate counters) gives bit-identical outputs to the one-pass kernel, and
+    repeated launches reuse the counters it resets."""
+    import torch
+    from igaming_platform_amd.ops import kernels as K
+    T = 24
+    N, m, gp = _ws_pack(T)
+    rng = np.random.default_rng(rows + 7)
+    Xd = torch.from_numpy(rng.standard_normal((T, rows, 16)).astype(np.float32)).cuda()
+    o1 = torch.full((rows,), -9.0, device="cuda")
+    o2 = torch.full((rows,), -9.0, device="cuda")
+    K.gru(gp, rows, T, out=o1, X=Xd, ws=1)
+    for _ in range(2):
+        o2.fill_(-9.0)
+        K.gru(gp, rows, T, out=o2, X=Xd, ws=2)
+        torch.cuda.synchronize()
+        assert not gp.ws_failed()
+        assert torch.equal(o1, o2)
+
+
 def test_gru_weight_stationary_yh_and_live_rows():
     """Y_h (no head) from the cluster kernel; rows past the device live count stay untouched;
     repeated launches (fresh counters each time) agree bit for bit."""
