@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "../include/records.h"
+#include "launch.h"
 #include "oplist.h"
 #include "roctx.h"
 
@@ -71,6 +72,8 @@ class PipeDriver {
     host_done_.assign(depth, 0);
     const char* xe = getenv("IGP_EXT_EVENTS");
     ext_events_ = !(xe && atoi(xe) == 0);
+    const char* qe = getenv("IGP_DEDUP_QUERY");  // 0: always queue the dedup-region wait
+    query_skip_ = !(qe && atoi(qe) == 0);
   }
   ~PipeDriver() {
     stop_worker();
@@ -254,13 +257,16 @@ class PipeDriver {
       host_done_[slot] = 0;
       recorded_[3 * slot] = recorded_[3 * slot + 1] = recorded_[3 * slot + 2] = true;
       hist_.push_back(slot);
-      if (hist_.size() > 2) hist_.erase(hist_.begin());
+      if ((int)hist_.size() > DEDUP_AHEAD) hist_.erase(hist_.begin());
       return;
     }
     // the slot's previous batch: skipped when the host already saw it complete (wait(slot))
     if (recorded_[3 * slot + 2] && !host_done_[slot]) hip_ok(hipStreamWaitEvent(cs_, me, 0), "wait model");
     host_done_[slot] = 0;
-    if (hist_.size() == 2) hip_ok(hipStreamWaitEvent(cs_, pe_[hist_.front()], 0), "wait state-2");
+    // the state stage of batch seq - DEDUP_AHEAD cleared this batch's dedup region: wait for it
+    // unless the host already sees it complete (an event query instead of a queue wait)
+    if ((int)hist_.size() == DEDUP_AHEAD && (!query_skip_ || hipEventQuery(pe_[hist_.front()]) != hipSuccess))
+      hip_ok(hipStreamWaitEvent(cs_, pe_[hist_.front()], 0), "wait state-3");
     const auto t2 = clk::now();
     const bool cb = stage_rec(g.c, g.oc, cs_, ce, "copy graph");
     const auto t3 = clk::now();
@@ -272,7 +278,7 @@ class PipeDriver {
     if (!sb) hip_ok(hipEventRecord(se, ss_), "record state");
     hip_ok(hipStreamWaitEvent(ms_, se, 0), "wait state");
     // split state stage (direct launch): the model waited for K1 only; the multi-event update
-    // (which also clears the dedup region of batch seq+2) follows on the state stream and its
+    // (which also clears the dedup region of batch seq+3) follows on the state stream and its
     // own event gates that region's reuse
     const bool pb = g.osu && ext_events_ && g.osu->run_recording(ss_, pe_[slot]);
     if (g.osu && !ext_events_) g.osu->run(ss_);
@@ -291,7 +297,7 @@ class PipeDriver {
     st_[5] += 1;
     recorded_[3 * slot] = recorded_[3 * slot + 1] = recorded_[3 * slot + 2] = true;
     hist_.push_back(slot);
-    if (hist_.size() > 2) hist_.erase(hist_.begin());
+    if ((int)hist_.size() > DEDUP_AHEAD) hist_.erase(hist_.begin());
   }
 
  public:
@@ -350,13 +356,14 @@ class PipeDriver {
   std::vector<hipEvent_t> pe_;  // per slot: the state stream's work of the batch is complete
   std::vector<bool> recorded_;
   std::vector<uint8_t> host_done_;  // wait(slot) returned since the slot's last submit (bytes: set by waiter threads)
-  std::vector<int> hist_;  // slots of the last two submitted batches, oldest first
+  std::vector<int> hist_;  // slots of the last DEDUP_AHEAD submitted batches, oldest first
   std::unordered_map<int64_t, Graphs> graphs_;
   int serial_max_ = 0;
   bool serial_hist_ = false;  // the last issued batch ran in serial mode
   // async issue
   bool async_ = false;
   bool ext_events_ = true;
+  bool query_skip_ = true;
   bool stop_ = false;
   std::thread worker_;
   std::mutex mu_;

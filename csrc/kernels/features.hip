@@ -754,10 +754,10 @@ __global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
     if (c < 2) continue;
     apply_segment_wave(a, t, h, c, s, r, lane);
   }
-  // scorer ring: clear the region of batch seq+2 (= seq-1's, consumed by now) for its insert;
-  // the copy of batch seq+2 waits for this batch's state graph
+  // scorer ring: clear the region of batch seq + DEDUP_AHEAD (= seq-1's, consumed by now) for
+  // its insert; the copy of that batch waits for this batch's state stage
   if (a.region < 0) {
-    const DedupTab nt = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(a.hdr->seq + 2));
+    const DedupTab nt = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(a.hdr->seq + DEDUP_AHEAD));
     const int4 m1 = make_int4(-1, -1, -1, -1), big = make_int4(0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff);
     const int4 z = make_int4(0, 0, 0, 0);
     for (int e4 = blockIdx.x * 256 + threadIdx.x; e4 < (nt.cap >> 2); e4 += UPD_MULTI_BLOCKS * 256) {
