@@ -378,7 +378,10 @@ def dp_bench(a, world: int, rank: int, dev) -> None:
                              + (", captured in the hipGraphs)" if sc.captured else ", issued by the driver)"),
                    "dp_mode": "exchange", "chunk_capacity": C, "rows_scored": total,
                    "rows_dropped_by_route": int(over.sum().item()),
-                   "numerics": numerics_desc(a)},
+                   "numerics": numerics_desc(a),
+                   # collective / queue knobs in effect, so a scaling curve is self-describing
+                   "comm_env": {k: v for k, v in sorted(os.environ.items())
+                                if k.startswith(("NCCL_", "RCCL_")) or k == "GPU_MAX_HW_QUEUES"}},
         "scope": "engine_only",
         "p99_latency_ms": p99, "p50_latency_ms": p50, "latency_baseline_ms": BASELINE_P99_MS,
         "latency_vs_baseline": BASELINE_P99_MS / p99 if p99 > 0 else None,
