@@ -103,7 +103,8 @@ def main():
     maybe_launch_torchrun(a)
     # HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues (default 4): the scorer's
     # copy / state / model streams, the default stream and RCCL's communication stream (N > 1)
-    # each get a queue of their own when 8 are allowed. Set before the HIP runtime initialises.
+    # each get a queue of their own when 8 are allowed. Set before the HIP runtime initialises; an
+    # exported value wins (the GPU boxes export 4: same-box A/B 4 vs 8 neutral, profiles/NOTES.md).
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     # dmabuf IPC for RCCL / cross-process tensors: read when the HIP runtime initialises
     # (torch.cuda.set_device below), so it must be in the environment before that
