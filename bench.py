@@ -8,13 +8,16 @@ default config = cfg 3, the data-parallel headline: GBDT+MLP stacked ensemble
 
 One timed step per GPU = one full scoring micro-batch, nothing skipped:
   host: pack 8192 requests (48 B ReqRec) into a pinned slab
-  GPU, two captured hipGraphs on two streams (engine/scorer.py):
-      state: H2D slab -> dedup insert -> feature_assemble (ring windows, HLL, blacklist,
-             ip-intel, rules, single-event score-then-update) -> multi-event update segments
-      model: tree ensemble -> fused MFMA dense+GEMV+sigmoid -> ensemble/action (+metrics)
-             -> D2H results
-      batch i+1's state graph overlaps batch i's model graph
-  RCCL: all_gather of the packed results across ranks (+ metrics all_reduce every 16 steps)
+  GPU, three streams driven by the native driver (engine/scorer.py, csrc/kernels/driver.hip;
+  stage kernels issued directly from recorded op lists):
+      copy:  H2D slab -> dedup insert
+      state: feature_assemble (ring windows, HLL, blacklist, ip-intel, rules, single-event
+             score-then-update) -> multi-event update segments
+      model: tree ensemble -> fused f32-MFMA dense+GEMV+sigmoid -> ensemble/action (+metrics)
+             -> results into pinned host memory
+      batches i, i+1, i+2 overlap across the three stages
+  N > 1 (default --dp-mode exchange): the owner-routed RCCL exchange (two all-to-alls per step)
+  moves every row to the rank owning its account and the results back (dp_bench below)
 Per-GPU work is fixed as N grows (weak scaling): global batch = 8192 x N per step.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|heuristic]
