@@ -21,6 +21,7 @@
 
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -34,6 +35,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "../include/device_ops.h"
 #include "../include/records.h"
 #include "launch.h"
 #include "oplist.h"
@@ -46,6 +48,25 @@ namespace {
 
 void hip_ok(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("PipeDriver ") + what + ": " + hipGetErrorString(e));
+}
+
+void copy_err(char* err, int32_t errlen, const char* msg) {
+  if (!err || errlen <= 0) return;
+  std::strncpy(err, msg, size_t(errlen) - 1);
+  err[errlen - 1] = 0;
+}
+
+// event wait with a deadline (hipEventSynchronize has none): query with a short back-off
+bool poll_event(hipEvent_t e, int64_t timeout_us) {
+  const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
+  for (int spin = 0;; ++spin) {
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipSuccess) return true;
+    if (q != hipErrorNotReady) hip_ok(q, "event query");
+    if (std::chrono::steady_clock::now() >= t_end) return false;
+    // spin first (a batch completes within a few hundred us), then back off
+    if (spin > 4096) std::this_thread::sleep_for(std::chrono::microseconds(10));
+  }
 }
 
 class PipeDriver {
@@ -98,6 +119,80 @@ class PipeDriver {
       stop_worker();
     }
     async_ = on;
+  }
+
+  // the slot's pinned result rows (ResultRec [bucket]) and FeatRec rows: what the native
+  // serving core reads after wait (device_ops)
+  void set_host_results(int slot, uintptr_t res, uintptr_t feat) {
+    if (slot < 0 || slot >= depth_) throw std::runtime_error("PipeDriver: bad slot");
+    if ((int)host_res_.size() != depth_) {
+      host_res_.assign(depth_, nullptr);
+      host_feat_.assign(depth_, nullptr);
+    }
+    host_res_[slot] = reinterpret_cast<char*>(res);
+    host_feat_[slot] = reinterpret_cast<char*>(feat);
+  }
+
+  // C function table for the native serving core (csrc/include/device_ops.h): the core issues
+  // this pipeline's batches from its own threads (no Python, no GIL)
+  uintptr_t device_ops() {
+    if ((int)host_res_.size() != depth_) throw std::runtime_error("PipeDriver: set_host_results first");
+    if (graphs_.empty()) throw std::runtime_error("PipeDriver: no graphs / op lists");
+    buckets_.clear();
+    for (auto& kv : graphs_) {
+      const int b = int(kv.first >> 8);
+      if (std::find(buckets_.begin(), buckets_.end(), b) == buckets_.end()) buckets_.push_back(b);
+    }
+    std::sort(buckets_.begin(), buckets_.end());
+    ops_.abi = IGP_DEVICE_OPS_ABI;
+    ops_.depth = depth_;
+    ops_.world = 1;
+    ops_.exchange = 0;
+    ops_.cap = buckets_.back();
+    ops_.features_always = 0;
+    ops_.ctx = this;
+    ops_.rows = [](void* ctx, int32_t slot) -> char* {
+      return static_cast<PipeDriver*>(ctx)->slabs_[slot] + sizeof(BatchHdr);
+    };
+    ops_.submit = [](void* ctx, int32_t slot, int32_t n, int32_t seq, int64_t now, int32_t wf, char* err,
+                     int32_t errlen) -> int32_t {
+      auto* d = static_cast<PipeDriver*>(ctx);
+      try {
+        int bucket = -1;
+        for (int b : d->buckets_)
+          if (b >= (n > 0 ? n : 1)) { bucket = b; break; }
+        if (bucket < 0) throw std::runtime_error("batch exceeds the largest bucket");
+        auto it = d->graphs_.find(key(bucket, slot));
+        if (it == d->graphs_.end()) throw std::runtime_error("no graphs for this bucket / slot");
+        d->issue(Cmd{slot, bucket, n, seq, now, 0, wf != 0, it->second});
+      } catch (const std::exception& e) {
+        copy_err(err, errlen, e.what());
+        return -1;
+      }
+      return 0;
+    };
+    ops_.wait = [](void* ctx, int32_t slot, int64_t timeout_us, char* err, int32_t errlen) -> int32_t {
+      auto* d = static_cast<PipeDriver*>(ctx);
+      try {
+        d->drain_slot(slot);
+        hipEvent_t e = d->ev_[3 * slot + 2];
+        if (timeout_us < 0) {
+          hip_ok(hipEventSynchronize(e), "sync model");
+        } else if (!poll_event(e, timeout_us)) {
+          return 1;
+        }
+        d->host_done_[slot] = 1;
+      } catch (const std::exception& e) {
+        copy_err(err, errlen, e.what());
+        return -1;
+      }
+      return 0;
+    };
+    ops_.results = [](void* ctx, int32_t slot) -> const void* { return static_cast<PipeDriver*>(ctx)->host_res_[slot]; };
+    ops_.features = [](void* ctx, int32_t slot) -> const void* {
+      return static_cast<PipeDriver*>(ctx)->host_feat_[slot];
+    };
+    return reinterpret_cast<uintptr_t>(&ops_);
   }
 
   void set_graphs(int bucket, int slot, uintptr_t gc, uintptr_t gs, uintptr_t gm, uintptr_t gmf) {
@@ -263,6 +358,13 @@ class PipeDriver {
     // the slot's previous batch: skipped when the host already saw it complete (wait(slot))
     if (recorded_[3 * slot + 2] && !host_done_[slot]) hip_ok(hipStreamWaitEvent(cs_, me, 0), "wait model");
     host_done_[slot] = 0;
+    // the slot's previous batch's split update stage (state stream, after K1) also reads the
+    // slot's device header and rows: the model event above does not cover it (the model only
+    // waited for K1), and the dedup-ring wait below only covers batch seq - DEDUP_AHEAD, so with
+    // fewer slots than DEDUP_AHEAD the copy must wait for that update itself (an event query
+    // first: no queue wait when it already finished)
+    if (recorded_[3 * slot + 1] && hipEventQuery(pe_[slot]) != hipSuccess)
+      hip_ok(hipStreamWaitEvent(cs_, pe_[slot], 0), "wait slot update");
     // the state stage of batch seq - DEDUP_AHEAD cleared this batch's dedup region: wait for it
     // unless the host already sees it complete (an event query instead of a queue wait)
     if ((int)hist_.size() == DEDUP_AHEAD && (!query_skip_ || hipEventQuery(pe_[hist_.front()]) != hipSuccess))
@@ -371,6 +473,10 @@ class PipeDriver {
   std::deque<Cmd> q_;
   std::vector<int> pending_;
   std::exception_ptr err_;
+  // native serving core interface
+  std::vector<char*> host_res_, host_feat_;
+  std::vector<int> buckets_;
+  IgpDeviceOps ops_{};
 };
 
 }  // namespace
@@ -379,6 +485,8 @@ void register_driver(py::module_& m) {
   py::class_<PipeDriver>(m, "PipeDriver")
       .def(py::init<uintptr_t, uintptr_t, uintptr_t, int, py::list>())
       .def("set_graphs", &PipeDriver::set_graphs)
+      .def("set_host_results", &PipeDriver::set_host_results)
+      .def("device_ops", &PipeDriver::device_ops)
       .def("set_ops", &PipeDriver::set_ops)
       .def("set_state_update", &PipeDriver::set_state_update)
       .def("set_serial", &PipeDriver::set_serial)

@@ -25,6 +25,7 @@
 #include <dlfcn.h>
 
 #include <chrono>
+#include <thread>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -32,6 +33,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "../include/device_ops.h"
 #include "../include/records.h"
 #include "oplist.h"
 #include "roctx.h"
@@ -87,6 +89,15 @@ __global__ __launch_bounds__(256) void exchange_compact_kernel(XchgCompactArgs a
   out[1] = q1;
   out[2] = q2;
   a.route[dst] = p * a.C + j;
+}
+
+// Before the row all-to-all: zero the chunk-header row counts of the receive buffer. After an
+// abort (a peer died inside the collective, ncclCommAbort) the kernels queued behind the
+// all-to-all still run; with the counts cleared they compact zero rows instead of replaying a
+// stale chunk of an older batch into the feature store.
+__global__ __launch_bounds__(64) void exchange_clear_kernel(ReqRec* recv, int32_t N, int32_t C) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < N) recv[(size_t)p * (C + 1)].slot = 0;
 }
 
 struct XchgScatterArgs {
@@ -286,6 +297,76 @@ class XchgDriver {
   // src: nbytes of prebuilt chunks ([N][C+1] ReqRec) copied into the slot's pinned buffer
   // (0: already there). The caller must not refill a slot before wait(slot) of its last batch.
   void submit(int slot, int C, int seq, int64_t now, uintptr_t src, size_t nbytes, bool with_features) {
+    check_slot(slot);
+    py::gil_scoped_release nogil;
+    submit_impl(slot, C, seq, now, src, nbytes, with_features);
+  }
+
+  // C function table for the native serving core (csrc/include/device_ops.h) with chunk
+  // capacity C: every step returns FeatRec rows too, so the result all-to-all has one size on
+  // every rank whatever the callers of each rank asked for
+  uintptr_t device_ops(int C) {
+    bool have = false;
+    for (auto& kv : graphs_) have |= int(kv.first >> 8) == C;
+    if (!have) throw std::runtime_error("XchgDriver: no graphs for this chunk capacity");
+    ops_C_ = C;
+    ops_.abi = IGP_DEVICE_OPS_ABI;
+    ops_.depth = depth_;
+    ops_.world = world_;
+    ops_.exchange = 1;
+    ops_.cap = C;
+    ops_.features_always = 1;
+    ops_.ctx = this;
+    ops_.rows = [](void* ctx, int32_t slot) -> char* { return static_cast<XchgDriver*>(ctx)->slots_[slot].host_x; };
+    ops_.submit = [](void* ctx, int32_t slot, int32_t, int32_t seq, int64_t now, int32_t, char* err,
+                     int32_t errlen) -> int32_t {
+      auto* d = static_cast<XchgDriver*>(ctx);
+      try {
+        d->submit_impl(slot, d->ops_C_, seq, now, 0, 0, true);
+      } catch (const std::exception& e) {
+        if (err && errlen > 0) {
+          std::strncpy(err, e.what(), size_t(errlen) - 1);
+          err[errlen - 1] = 0;
+        }
+        return -1;
+      }
+      return 0;
+    };
+    ops_.wait = [](void* ctx, int32_t slot, int64_t timeout_us, char* err, int32_t errlen) -> int32_t {
+      auto* d = static_cast<XchgDriver*>(ctx);
+      hipEvent_t e = d->E(slot, 5);
+      if (timeout_us < 0) {
+        const hipError_t r = hipEventSynchronize(e);
+        if (r == hipSuccess) return 0;
+        if (err && errlen > 0) {
+          std::strncpy(err, hipGetErrorString(r), size_t(errlen) - 1);
+          err[errlen - 1] = 0;
+        }
+        return -1;
+      }
+      const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
+      for (int spin = 0;; ++spin) {
+        const hipError_t q = hipEventQuery(e);
+        if (q == hipSuccess) return 0;
+        if (q != hipErrorNotReady) {
+          if (err && errlen > 0) {
+            std::strncpy(err, hipGetErrorString(q), size_t(errlen) - 1);
+            err[errlen - 1] = 0;
+          }
+          return -1;
+        }
+        if (std::chrono::steady_clock::now() >= t_end) return 1;
+        if (spin > 4096) std::this_thread::sleep_for(std::chrono::microseconds(10));
+      }
+    };
+    ops_.results = [](void* ctx, int32_t slot) -> const void* {
+      return static_cast<XchgDriver*>(ctx)->slots_[slot].host_rr;
+    };
+    ops_.features = [](void*, int32_t) -> const void* { return nullptr; };
+    return reinterpret_cast<uintptr_t>(&ops_);
+  }
+
+  void submit_impl(int slot, int C, int seq, int64_t now, uintptr_t src, size_t nbytes, bool with_features) {
     auto it = graphs_.find(key(C, slot));
     if (it == graphs_.end()) throw std::runtime_error("XchgDriver: no graphs for this chunk capacity / slot");
     const Graphs g = it->second;
@@ -298,7 +379,6 @@ class XchgDriver {
     const bool direct = g.osend != nullptr;
     if (with_features && !g.model_f && !direct) throw std::runtime_error("XchgDriver: no feature graph");
     if (captured_ && direct) throw std::runtime_error("XchgDriver: direct launch needs set_captured(False)");
-    py::gil_scoped_release nogil;
     Range range("igp.xsubmit");
     const auto t0 = clk::now();
     if (src) std::memcpy(sl.host_x, reinterpret_cast<const void*>(src), nbytes);
@@ -440,6 +520,8 @@ class XchgDriver {
   double st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   bool copy_only_ = false;
   bool captured_ = false;
+  IgpDeviceOps ops_{};
+  int ops_C_ = 0;
 };
 
 template <class T>
@@ -475,6 +557,7 @@ void register_exchange(py::module_& m) {
       .def("set_state_ops", &XchgDriver::set_state_ops)
       .def("set_captured", &XchgDriver::set_captured)
       .def("submit", &XchgDriver::submit)
+      .def("device_ops", &XchgDriver::device_ops)
       .def("wait", &XchgDriver::wait)
       .def("query", &XchgDriver::query)
       .def("state_event", &XchgDriver::state_event)
@@ -495,6 +578,17 @@ void register_exchange(py::module_& m) {
     }
     f(P<hipStream_t>(stream));
     hip_ok(hipGetLastError(), "exchange_compact");
+  });
+  m.def("exchange_clear", [](uintptr_t recv, int N, int C, uintptr_t stream) {
+    if (N < 1 || N > XCHG_MAX_WORLD || C < 1) throw std::runtime_error("exchange_clear: bad sizes");
+    ReqRec* r = P<ReqRec*>(recv);
+    auto f = [r, N, C](hipStream_t st) { IGP_LAUNCH(exchange_clear_kernel, dim3(1), dim3(64), 0, st, r, N, C); };
+    if (OpList* rec = recording()) {
+      rec->ops.emplace_back(f);
+      return;
+    }
+    f(P<hipStream_t>(stream));
+    hip_ok(hipGetLastError(), "exchange_clear");
   });
   m.def("exchange_scatter", [](uintptr_t hdr, uintptr_t route, uintptr_t res, uintptr_t feat, uintptr_t send, int C,
                                int cap, uintptr_t stream) {

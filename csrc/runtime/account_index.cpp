@@ -1,113 +1,238 @@
 #include "account_index.h"
 
-#include <mutex>
+#include <algorithm>
+#include <chrono>
+#include <cstring>
 #include <stdexcept>
+#include <thread>
 
 namespace igp {
+namespace {
+
+constexpr uint64_t kMagic = 0x3158444954434341ull;  // "ACCTIDX1"
+constexpr int64_t kArenaPerAccount = 64;            // bytes reserved per slot (4-byte length + id, 8-aligned)
+
+int64_t table_size(int64_t capacity) {
+  int64_t t = 16;
+  while (t < capacity * 2) t <<= 1;  // load factor <= 0.5
+  return t;
+}
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+}  // namespace
+
+size_t AccountIndex::region_bytes(int64_t capacity) {
+  const int64_t t = table_size(capacity);
+  return sizeof(Hdr) + size_t(t) * sizeof(Entry) + size_t(capacity) * sizeof(uint32_t) + 64 +
+         size_t(capacity) * kArenaPerAccount;
+}
+
+void AccountIndex::layout(void* base) {
+  hdr_ = reinterpret_cast<Hdr*>(base);
+  tab_ = reinterpret_cast<Entry*>(reinterpret_cast<char*>(base) + sizeof(Hdr));
+  slot_off_ = reinterpret_cast<uint32_t*>(tab_ + hdr_->tsize);
+  const uintptr_t a = reinterpret_cast<uintptr_t>(slot_off_ + hdr_->cap);
+  arena_ = reinterpret_cast<char*>((a + 63) & ~uintptr_t(63));
+  mask_ = hdr_->tsize - 1;
+}
+
+void AccountIndex::init_fresh(int64_t capacity) {
+  // the mapping is zero-filled: every entry is empty (h = 0) already
+  Hdr* h = reinterpret_cast<Hdr*>(region_.base());
+  h->magic = kMagic;
+  h->cap = capacity;
+  h->tsize = table_size(capacity);
+  h->arena_bytes = capacity * kArenaPerAccount;
+  h->n.store(0);
+  h->arena_used.store(8);  // offset 0 is never a valid id
+  h->collisions.store(0);
+  layout(h);
+  h->ready.store(1, std::memory_order_release);
+}
 
 AccountIndex::AccountIndex(int64_t capacity) {
   if (capacity <= 0) throw std::runtime_error("AccountIndex: capacity must be > 0");
-  int64_t t = 16;
-  while (t < capacity * 2) t <<= 1;  // load factor <= 0.5
-  cap_ = capacity;
-  mask_ = t - 1;
-  tab_.assign(size_t(t), Entry{0, 0, -1});
-  ids_.reserve(size_t(std::min<int64_t>(capacity, 1 << 20)));
+  region_ = Region::anon(region_bytes(capacity));
+  init_fresh(capacity);
 }
 
-int64_t AccountIndex::probe(uint64_t h, uint32_t check, bool& found) const {
-  int64_t i = int64_t(h & uint64_t(mask_));
-  for (;;) {
-    const Entry& e = tab_[size_t(i)];
-    if (e.h == 0) { found = false; return i; }
-    if (e.h == h && e.check == check) { found = true; return i; }
-    i = (i + 1) & mask_;
+AccountIndex::AccountIndex(int64_t capacity, const std::string& shm_name, bool create) {
+  if (capacity <= 0) throw std::runtime_error("AccountIndex: capacity must be > 0");
+  const size_t bytes = region_bytes(capacity);
+  region_ = Region::shared(shm_name, bytes, create);
+  if (create) {
+    init_fresh(capacity);
+    return;
   }
+  Hdr* h = reinterpret_cast<Hdr*>(region_.base());
+  for (int i = 0; h->ready.load(std::memory_order_acquire) != 1; ++i) {
+    if (i > 20000) throw std::runtime_error("AccountIndex: shared index " + shm_name + " never became ready");
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+  if (h->magic != kMagic || h->cap != capacity) throw std::runtime_error("AccountIndex: shared index layout mismatch");
+  layout(h);
 }
 
-int32_t AccountIndex::insert_at(int64_t i, std::string_view id, uint64_t h, uint32_t check) {
-  if (n_ >= cap_) return -1;
-  tab_[size_t(i)] = Entry{h, check, int32_t(n_)};
-  ids_.emplace_back(id);
-  return int32_t(n_++);
+int64_t AccountIndex::size() const { return std::min(hdr_->n.load(std::memory_order_acquire), hdr_->cap); }
+
+int32_t AccountIndex::published(const Entry& e) const {
+  int32_t st = e.state.load(std::memory_order_acquire);
+  for (int spin = 0; st == 0; ++spin) {
+    // an insert is between its claim and its publish (a few hundred ns); a process that died
+    // there leaves the entry claimed for good: give up after ~50 ms (the row scores as an
+    // unknown account, partial features)
+    if (spin > (1 << 16)) {
+      if (spin > (1 << 16) + 500) return -1;
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    } else {
+      cpu_relax();
+    }
+    st = e.state.load(std::memory_order_acquire);
+  }
+  return st > 0 ? st - 1 : -1;
+}
+
+bool AccountIndex::id_equal(uint32_t off8, std::string_view id) const {
+  const char* p = arena_ + size_t(off8) * 8;
+  uint32_t len;
+  std::memcpy(&len, p, 4);
+  return len == id.size() && std::memcmp(p + 4, id.data(), id.size()) == 0;
+}
+
+int32_t AccountIndex::find_from(int64_t i, std::string_view id, uint64_t h) const {
+  for (int64_t probes = 0; probes <= mask_; ++probes, i = (i + 1) & mask_) {
+    const Entry& e = tab_[size_t(i)];
+    const uint64_t hv = e.h.load(std::memory_order_acquire);
+    if (hv == 0) return -1;
+    if (hv != h) continue;
+    const int32_t s = published(e);
+    if (s >= 0 && id_equal(e.off8, id)) return s;
+  }
+  return -1;
 }
 
 int32_t AccountIndex::find(std::string_view id, uint64_t h) const {
   if (h == 0) return -1;
-  const uint32_t c = id_check(id);
-  std::shared_lock<std::shared_mutex> lk(mu_);
-  bool found;
-  int64_t i = probe(h, c, found);
-  return found ? tab_[size_t(i)].slot : -1;
+  return find_from(int64_t(h & uint64_t(mask_)), id, h);
+}
+
+int32_t AccountIndex::insert(std::string_view id, uint64_t h, bool* inserted) {
+  if (inserted) *inserted = false;
+  if (h == 0) return -1;
+  int64_t i = int64_t(h & uint64_t(mask_));
+  for (int64_t probes = 0; probes <= mask_; ++probes, i = (i + 1) & mask_) {
+    Entry& e = tab_[size_t(i)];
+    uint64_t hv = e.h.load(std::memory_order_acquire);
+    if (hv == 0) {
+      if (hdr_->n.load(std::memory_order_relaxed) >= hdr_->cap) return -1;  // full: claim nothing
+      if (e.h.compare_exchange_strong(hv, h, std::memory_order_acq_rel)) {
+        const int64_t s = hdr_->n.fetch_add(1, std::memory_order_acq_rel);
+        if (s >= hdr_->cap) {  // lost the race for the last slot
+          e.state.store(-1, std::memory_order_release);
+          return -1;
+        }
+        const int64_t need = (4 + int64_t(id.size()) + 7) & ~int64_t(7);
+        const int64_t off = hdr_->arena_used.fetch_add(need, std::memory_order_relaxed);
+        if (off + need > hdr_->arena_bytes) {  // ids far longer than a UUID filled the arena
+          e.state.store(-1, std::memory_order_release);
+          return -1;
+        }
+        char* p = arena_ + off;
+        const uint32_t len = uint32_t(id.size());
+        std::memcpy(p, &len, 4);
+        std::memcpy(p + 4, id.data(), id.size());
+        e.off8 = uint32_t(off / 8);
+        slot_off_[s] = uint32_t(off / 8);
+        e.state.store(int32_t(s + 1), std::memory_order_release);
+        if (inserted) *inserted = true;
+        return int32_t(s);
+      }
+      // another inserter claimed this entry first: hv now holds its digest
+    }
+    if (hv != h) continue;
+    const int32_t s = published(e);
+    if (s >= 0) {
+      if (id_equal(e.off8, id)) return s;
+      hdr_->collisions.fetch_add(1, std::memory_order_relaxed);
+    }
+  }
+  return -1;
 }
 
 int32_t AccountIndex::find_or_insert(std::string_view id, uint64_t h, bool* inserted) {
-  if (inserted) *inserted = false;
-  if (h == 0) return -1;
-  const uint32_t c = id_check(id);
-  {
-    std::shared_lock<std::shared_mutex> lk(mu_);
-    bool found;
-    int64_t i = probe(h, c, found);
-    if (found) return tab_[size_t(i)].slot;
+  const int32_t s = find(id, h);
+  if (s >= 0) {
+    if (inserted) *inserted = false;
+    return s;
   }
-  std::unique_lock<std::shared_mutex> lk(mu_);
-  bool found;
-  int64_t i = probe(h, c, found);
-  if (found) return tab_[size_t(i)].slot;
-  const int32_t s = insert_at(i, id, h, c);
-  if (inserted) *inserted = s >= 0;
-  return s;
+  return insert(id, h, inserted);
 }
 
-void AccountIndex::lookup(const std::vector<std::string>& ids, const std::vector<uint64_t>& hashes,
-                          bool insert, int32_t* slots, uint8_t* fresh) {
+void AccountIndex::lookup(const std::vector<std::string>& ids, const std::vector<uint64_t>& hashes, bool insert_,
+                          int32_t* slots, uint8_t* fresh) {
   std::vector<std::string_view> v(ids.begin(), ids.end());
-  std::vector<uint32_t> c(ids.size());
-  for (size_t k = 0; k < ids.size(); ++k) c[k] = id_check(ids[k]);
-  lookup_views(v.data(), hashes.data(), c.data(), ids.size(), insert, slots, fresh);
+  lookup_views(v.data(), hashes.data(), ids.size(), insert_, slots, fresh);
 }
 
-void AccountIndex::lookup_views(const std::string_view* ids, const uint64_t* h, const uint32_t* check, size_t n,
-                                bool insert, int32_t* slots, uint8_t* fresh, const uint8_t* sel) {
+void AccountIndex::lookup_views(const std::string_view* ids, const uint64_t* h, size_t n, bool insert_, int32_t* slots,
+                                uint8_t* fresh, const uint8_t* sel) {
   constexpr size_t kAhead = 16;  // probe lines in flight
-  std::vector<uint32_t> miss;
-  {
-    std::shared_lock<std::shared_mutex> lk(mu_);
-    const Entry* t = tab_.data();
-    for (size_t k = 0; k < std::min(n, kAhead); ++k) __builtin_prefetch(t + (h[k] & uint64_t(mask_)));
-    for (size_t k = 0; k < n; ++k) {
-      if (k + kAhead < n) __builtin_prefetch(t + (h[k + kAhead] & uint64_t(mask_)));
-      if (fresh) fresh[k] = 0;
-      if (h[k] == 0 || (sel && !sel[k])) { slots[k] = -1; continue; }
-      bool found;
-      const int64_t i = probe(h[k], check[k], found);
-      if (found) {
-        slots[k] = t[size_t(i)].slot;
-      } else {
-        slots[k] = -1;
-        if (insert) miss.push_back(uint32_t(k));
+  // pass 1: probe every row (prefetched), remember the first digest match and prefetch its id
+  std::vector<int64_t> cand(n, -1);
+  const Entry* t = tab_;
+  for (size_t k = 0; k < std::min(n, kAhead); ++k) __builtin_prefetch(t + (h[k] & uint64_t(mask_)));
+  for (size_t k = 0; k < n; ++k) {
+    if (k + kAhead < n) __builtin_prefetch(t + (h[k + kAhead] & uint64_t(mask_)));
+    if (fresh) fresh[k] = 0;
+    slots[k] = -1;
+    if (h[k] == 0 || (sel && !sel[k])) continue;
+    int64_t i = int64_t(h[k] & uint64_t(mask_));
+    for (int64_t probes = 0; probes <= mask_; ++probes, i = (i + 1) & mask_) {
+      const uint64_t hv = t[size_t(i)].h.load(std::memory_order_acquire);
+      if (hv == 0) break;
+      if (hv == h[k]) {
+        cand[k] = i;
+        const int32_t st = t[size_t(i)].state.load(std::memory_order_acquire);
+        if (st > 0) __builtin_prefetch(arena_ + size_t(t[size_t(i)].off8) * 8);
+        break;
       }
     }
   }
-  if (miss.empty()) return;
-  std::unique_lock<std::shared_mutex> lk(mu_);
-  for (uint32_t k : miss) {  // in row order: a batch's new accounts get slots in arrival order
-    bool found;
-    const int64_t i = probe(h[k], check[k], found);
-    if (found) {
-      slots[k] = tab_[size_t(i)].slot;  // inserted earlier in this batch (or by another thread)
-      continue;
+  // pass 2: confirm the candidates against the stored ids (lines already in flight)
+  std::vector<uint32_t> miss;
+  for (size_t k = 0; k < n; ++k) {
+    if (h[k] == 0 || (sel && !sel[k])) continue;
+    if (cand[k] >= 0) {
+      const Entry& e = t[size_t(cand[k])];
+      const int32_t s = published(e);
+      if (s >= 0 && id_equal(e.off8, ids[k])) {
+        slots[k] = s;
+        continue;
+      }
+      // digest collision (or a dead entry): the rest of the probe chain
+      const int32_t s2 = find_from((cand[k] + 1) & mask_, ids[k], h[k]);
+      if (s2 >= 0) {
+        slots[k] = s2;
+        continue;
+      }
     }
-    slots[k] = insert_at(i, ids[k], h[k], check[k]);
-    if (fresh) fresh[k] = slots[k] >= 0;
+    if (insert_) miss.push_back(uint32_t(k));
+  }
+  // pass 3: inserts in row order (a batch's new accounts get slots in arrival order)
+  for (uint32_t k : miss) {
+    bool ins = false;
+    slots[k] = insert(ids[k], h[k], &ins);
+    if (fresh) fresh[k] = ins;
   }
 }
 
 std::string AccountIndex::id_of(int32_t slot) const {
-  std::shared_lock<std::shared_mutex> lk(mu_);
-  if (slot < 0 || slot >= n_) throw std::runtime_error("AccountIndex: bad slot");
-  return ids_[size_t(slot)];
+  if (slot < 0 || slot >= size()) throw std::runtime_error("AccountIndex: bad slot");
+  const char* p = arena_ + size_t(slot_off_[slot]) * 8;
+  uint32_t len;
+  std::memcpy(&len, p, 4);
+  return std::string(p + 4, len);
 }
 
 }  // namespace igp

@@ -1,60 +1,89 @@
-// Account-id -> feature-store slot map (one per GPU shard).
+// Account-id -> feature-store slot map (one per owner shard).
 //
 // Replaces the per-account Redis key namespace ``features:<uuid>:*`` of
-// services/risk/internal/features/redis_store.go:25-35. Open addressing over 16-byte entries
-// {XXH64 digest, 32-bit check digest (a second, independently seeded XXH64), slot}: one
-// cache line holds four entries and a lookup touches one line, with no pointer chase to the
-// stored id string (96 bits identify an id; a false match needs ~2^48 ids). The batch path
-// prefetches every probe line of the batch before probing (memory-level parallelism over
-// ~8192 random lookups) and takes the lock once per batch. Full ids are kept by slot for the
-// reverse map (id_of: linked accounts, snapshots).
+// services/risk/internal/features/redis_store.go:25-35.
+//
+// Lock-free open addressing over 16-byte entries {XXH64 digest, state, id offset}; the id
+// bytes live in an append-only arena, so identity is the exact id string (a digest match is
+// always confirmed against the stored bytes: two ids that collide on 64 bits get two slots,
+// and the collision is counted). Inserts claim an empty entry with one 64-bit CAS, take the
+// next slot with a fetch_add, write the id, then publish the slot with a release store;
+// readers that meet a claimed-but-unpublished entry spin until it is published.
+//
+// The table can live in a node-shared /dev/shm region: every rank of a one-process-per-GPU
+// group then resolves ids through the same table, so an account gets ONE slot on its owner
+// no matter which rank's ingress saw it first (multi-ingress serving, engine/serving.py).
+// The batch path prefetches every probe line, then every candidate's id bytes, before it
+// compares (memory-level parallelism over ~8192 random lookups per batch).
 #pragma once
-#include <algorithm>
+#include <atomic>
 #include <cstdint>
-#include <shared_mutex>
 #include <string>
 #include <string_view>
 #include <vector>
 
+#include "shm.h"
 #include "xxh64.h"
 
 namespace igp {
 
-constexpr uint64_t SEED_ACCOUNT_CHECK = 0x41434b32;  // "ACK2"
-
-inline uint32_t id_check(std::string_view s) { return uint32_t(xxh64(s.data(), s.size(), SEED_ACCOUNT_CHECK) >> 32); }
-
 class AccountIndex {
  public:
+  // process-private index
   explicit AccountIndex(int64_t capacity);
+  // node-shared index in /dev/shm/<name> (create: this process sizes and initialises it)
+  AccountIndex(int64_t capacity, const std::string& shm_name, bool create);
+
   // slot of id, or -1
   int32_t find(std::string_view id, uint64_t h) const;
   // slot of id, inserting a fresh slot if absent; -1 if the index is full
   int32_t find_or_insert(std::string_view id, uint64_t h, bool* inserted = nullptr);
-  void lookup(const std::vector<std::string>& ids, const std::vector<uint64_t>& hashes,
-              bool insert, int32_t* slots, uint8_t* fresh);
+  void lookup(const std::vector<std::string>& ids, const std::vector<uint64_t>& hashes, bool insert, int32_t* slots,
+              uint8_t* fresh);
   // batch path: ids[k] with precomputed digests; rows with sel[k] == 0 are skipped (slot -1)
-  void lookup_views(const std::string_view* ids, const uint64_t* h, const uint32_t* check, size_t n, bool insert,
-                    int32_t* slots, uint8_t* fresh, const uint8_t* sel = nullptr);
-  int64_t size() const { return n_; }
-  int64_t capacity() const { return cap_; }
+  void lookup_views(const std::string_view* ids, const uint64_t* h, size_t n, bool insert, int32_t* slots,
+                    uint8_t* fresh, const uint8_t* sel = nullptr);
+  int64_t size() const;
+  int64_t capacity() const { return hdr_->cap; }
+  int64_t collisions() const { return hdr_->collisions.load(std::memory_order_relaxed); }
   std::string id_of(int32_t slot) const;
+  bool shared() const { return region_.shared_mapping(); }
+  void unlink_shared() { region_.unlink(); }
+
+  static size_t region_bytes(int64_t capacity);
 
  private:
+  struct Hdr {
+    uint64_t magic;
+    int64_t cap;
+    int64_t tsize;        // power of two, >= 2 * cap
+    int64_t arena_bytes;
+    std::atomic<int64_t> n;           // slots handed out (may pass cap by the racing inserts that lost)
+    std::atomic<int64_t> arena_used;  // bytes
+    std::atomic<int64_t> collisions;  // distinct ids sharing a 64-bit digest
+    std::atomic<int32_t> ready;
+    int32_t pad[5];
+  };
   struct Entry {
-    uint64_t h;      // 0 = empty (digest 0 is never stored: ids are non-empty)
-    uint32_t check;
-    int32_t slot;
+    std::atomic<uint64_t> h;      // 0 = empty
+    std::atomic<int32_t> state;   // 0 = claimed, not yet published; s + 1 = slot s; -1 = dead (index full)
+    uint32_t off8;                // id offset in the arena, 8-byte units
   };
   static_assert(sizeof(Entry) == 16, "AccountIndex entry must be 16 bytes");
-  int64_t probe(uint64_t h, uint32_t check, bool& found) const;
-  int32_t insert_at(int64_t i, std::string_view id, uint64_t h, uint32_t check);
-  int64_t cap_;
-  int64_t mask_;
-  int64_t n_ = 0;
-  std::vector<Entry> tab_;
-  std::vector<std::string> ids_; // by slot
-  mutable std::shared_mutex mu_;
+
+  void layout(void* base);
+  void init_fresh(int64_t capacity);
+  int32_t published(const Entry& e) const;  // spins on a claimed entry; slot or -1 (dead / stuck)
+  bool id_equal(uint32_t off8, std::string_view id) const;
+  int32_t find_from(int64_t i, std::string_view id, uint64_t h) const;
+  int32_t insert(std::string_view id, uint64_t h, bool* inserted);
+
+  Region region_;
+  Hdr* hdr_ = nullptr;
+  Entry* tab_ = nullptr;
+  uint32_t* slot_off_ = nullptr;  // slot -> id offset (8-byte units)
+  char* arena_ = nullptr;
+  int64_t mask_ = 0;
 };
 
 }  // namespace igp

@@ -8,7 +8,9 @@
 #include <memory>
 
 #include "account_index.h"
+#include "cpu_device.h"
 #include "cpu_scorer.h"
+#include "serve_core.h"
 #include "link_index.h"
 #include "executor.h"
 #include "onnx_model.h"
@@ -73,6 +75,19 @@ py::list value_infos(const std::vector<onnx::ValueInfo>& vs) {
 
 template <class T>
 py::array_t<T> vec_np(const std::vector<T>& v) { return py::array_t<T>(v.size(), v.data()); }
+
+// Python handle of a serving core: keeps the device object (whose function table the core
+// calls) alive for as long as the core may use it.
+struct PyServe {
+  std::shared_ptr<ServeCore> core;
+  py::object dev;
+};
+
+const IgpDeviceOps* device_ops_of(py::object dev) {
+  const uintptr_t p = dev.attr("device_ops")().cast<uintptr_t>();
+  if (!p) throw std::runtime_error("device_ops(): null function table");
+  return reinterpret_cast<const IgpDeviceOps*>(p);
+}
 
 }  // namespace
 
@@ -315,6 +330,8 @@ PYBIND11_MODULE(_native, m) {
 
   py::class_<AccountIndex, std::shared_ptr<AccountIndex>>(m, "AccountIndex")
       .def(py::init<int64_t>())
+      // node-shared index (/dev/shm/<shm_name>): one creator sizes it, the other ranks open it
+      .def(py::init<int64_t, const std::string&, bool>(), py::arg("capacity"), py::arg("shm_name"), py::arg("create"))
       .def("lookup_batch", [](AccountIndex& ix, const wire::RequestBatch& b, bool insert, py::object sel) {
         // sel: optional bool/uint8 mask (rows of other owners are skipped, slot -1)
         py::array_t<int32_t> slots(b.size());
@@ -330,7 +347,7 @@ PYBIND11_MODULE(_native, m) {
         uint8_t* fp = fresh.mutable_data();
         {
           py::gil_scoped_release rel;
-          ix.lookup_views(b.account_id.data(), b.account_hash.data(), b.account_check.data(), b.size(), insert, sp, fp, mp);
+          ix.lookup_views(b.account_id.data(), b.account_hash.data(), b.size(), insert, sp, fp, mp);
         }
         return py::make_tuple(slots, fresh);
       }, py::arg("batch"), py::arg("insert") = true, py::arg("sel") = py::none())
@@ -344,6 +361,9 @@ PYBIND11_MODULE(_native, m) {
       }, py::arg("ids"), py::arg("insert") = false)
       .def("__len__", &AccountIndex::size)
       .def_property_readonly("capacity", &AccountIndex::capacity)
+      .def_property_readonly("collisions", &AccountIndex::collisions)
+      .def_property_readonly("shared", &AccountIndex::shared)
+      .def("unlink_shared", &AccountIndex::unlink_shared)
       .def("id_of", &AccountIndex::id_of);
 
   py::class_<LinkIndex, std::shared_ptr<LinkIndex>>(m, "LinkIndex")
@@ -517,4 +537,151 @@ PYBIND11_MODULE(_native, m) {
     if (f.size() != 32) throw std::runtime_error("FeatRec must have 32 int32 words");
     return py::bytes(wire::serialize_feature_vector(*reinterpret_cast<const FeatRec*>(f.data())));
   });
+
+  // ---------------------------------------------------------------- native serving core
+  py::class_<StepClock, std::shared_ptr<StepClock>>(m, "StepClock")
+      .def(py::init<const std::string&, int, int, bool>(), py::arg("shm_name"), py::arg("world"), py::arg("rank"),
+           py::arg("create"))
+      .def(py::init<int>(), py::arg("world"))
+      .def("issued", &StepClock::issued)
+      .def("max_issued", &StepClock::max_issued)
+      .def("hold_of", &StepClock::hold_of)
+      .def("set_rank", &StepClock::set_rank)
+      .def("unlink_shared", &StepClock::unlink_shared)
+      .def_property_readonly("world", &StepClock::world)
+      .def_property_readonly("rank", &StepClock::rank);
+
+  py::class_<CpuDevice, std::shared_ptr<CpuDevice>>(m, "CpuDevice")
+      .def(py::init<std::shared_ptr<CpuScorer>, int, int>(), py::arg("scorer"), py::arg("depth") = 2,
+           py::arg("cap") = 8192, py::keep_alive<1, 2>())
+      .def("device_ops", [](const CpuDevice& d) { return reinterpret_cast<uintptr_t>(d.ops()); });
+
+  py::class_<ShmXchgDevice, std::shared_ptr<ShmXchgDevice>>(m, "ShmXchgDevice")
+      .def(py::init<std::shared_ptr<CpuScorer>, const std::string&, int, int, int, int, bool, double>(),
+           py::arg("scorer"), py::arg("shm_name"), py::arg("world"), py::arg("rank"), py::arg("depth"), py::arg("C"),
+           py::arg("create"), py::arg("timeout_s") = 60.0, py::keep_alive<1, 2>())
+      .def("device_ops", [](const ShmXchgDevice& d) { return reinterpret_cast<uintptr_t>(d.ops()); })
+      .def_property_readonly("rows_scored", &ShmXchgDevice::rows_scored)
+      .def("unlink_shared", &ShmXchgDevice::unlink_shared);
+
+  py::class_<PyServe, std::shared_ptr<PyServe>>(m, "ServeCore")
+      .def(py::init([](std::vector<std::shared_ptr<AccountIndex>> idx, py::object dev, int rank,
+                       std::shared_ptr<StepClock> clock, int max_wait_us, int64_t timeout_us, int finishers,
+                       bool features, int32_t seq0) {
+             ServeCore::Options o;
+             o.max_wait_us = max_wait_us;
+             o.timeout_us = timeout_us;
+             o.finishers = finishers;
+             o.features = features;
+             o.seq0 = seq0;
+             const IgpDeviceOps* ops = device_ops_of(dev);
+             auto p = std::make_shared<PyServe>();
+             p->dev = dev;
+             py::gil_scoped_release rel;
+             p->core = std::make_shared<ServeCore>(std::move(idx), ops, rank, std::move(clock), o);
+             return p;
+           }),
+           py::arg("indexes"), py::arg("device"), py::arg("rank") = 0, py::arg("clock") = nullptr,
+           py::arg("max_wait_us") = 200, py::arg("timeout_us") = -1, py::arg("finishers") = 2,
+           py::arg("features") = true, py::arg("seq0") = 0)
+      .def("score_batch", [](PyServe& s, py::bytes data, int64_t now, int64_t t0_ns) {
+        char* p; py::ssize_t n;
+        PYBIND11_BYTES_AS_STRING_AND_SIZE(data.ptr(), &p, &n);
+        std::string out;
+        {
+          py::gil_scoped_release rel;
+          out = s.core->score_batch(p, size_t(n), now, t0_ns);
+        }
+        return py::bytes(out);
+      }, py::arg("data"), py::arg("now") = -1, py::arg("t0_ns") = 0)
+      .def("score_rows", [](PyServe& s, py::array req, py::object owners, int64_t now, bool want_features) {
+        if (req.nbytes() % sizeof(ReqRec)) throw std::runtime_error("score_rows: ReqRec rows expected");
+        auto rq = py::array::ensure(req, py::array::c_style);
+        const size_t n = size_t(rq.nbytes()) / sizeof(ReqRec);
+        py::array_t<int32_t, py::array::c_style | py::array::forcecast> own;
+        const int32_t* op = nullptr;
+        if (!owners.is_none()) {
+          own = owners;
+          if (size_t(own.size()) != n) throw std::runtime_error("score_rows: owners length");
+          op = own.data();
+        }
+        py::array_t<uint32_t> res({(py::ssize_t)n, (py::ssize_t)2});
+        py::object feat = py::none();
+        FeatRec* fp = nullptr;
+        if (want_features) {
+          py::array_t<int32_t> f({(py::ssize_t)n, (py::ssize_t)32});
+          fp = reinterpret_cast<FeatRec*>(f.mutable_data());
+          feat = f;
+        }
+        const ReqRec* r = reinterpret_cast<const ReqRec*>(rq.data());
+        ResultRec* rp = reinterpret_cast<ResultRec*>(res.mutable_data());
+        {
+          py::gil_scoped_release rel;
+          s.core->score_rows(r, op, n, now, want_features, rp, fp);
+        }
+        return py::make_tuple(res, feat);
+      }, py::arg("req"), py::arg("owners") = py::none(), py::arg("now") = -1, py::arg("want_features") = true)
+      .def("submit_tx", [](PyServe& s, py::bytes data, uint64_t tag, int64_t now, int64_t t0_ns) {
+        char* p; py::ssize_t n;
+        PYBIND11_BYTES_AS_STRING_AND_SIZE(data.ptr(), &p, &n);
+        s.core->submit_tx(p, size_t(n), tag, now, t0_ns);  // parse + resolve of one row: GIL kept
+      }, py::arg("data"), py::arg("tag"), py::arg("now") = -1, py::arg("t0_ns") = 0)
+      .def("submit_tx_many", [](PyServe& s, py::list items, py::list tags, int64_t now, py::list t0s) {
+        const size_t n = items.size();
+        if (tags.size() != n || (t0s.size() && t0s.size() != n)) throw std::runtime_error("submit_tx_many: lengths");
+        std::vector<std::pair<const char*, size_t>> bufs(n);
+        std::vector<uint64_t> tg(n);
+        std::vector<int64_t> t0(n, 0);
+        for (size_t k = 0; k < n; ++k) {
+          char* p; py::ssize_t ln;
+          if (PYBIND11_BYTES_AS_STRING_AND_SIZE(items[k].ptr(), &p, &ln) != 0) throw std::runtime_error("bytes expected");
+          bufs[k] = {p, size_t(ln)};
+          tg[k] = tags[k].cast<uint64_t>();
+          if (t0s.size()) t0[k] = t0s[k].cast<int64_t>();
+        }
+        py::gil_scoped_release rel;
+        for (size_t k = 0; k < n; ++k) s.core->submit_tx(bufs[k].first, bufs[k].second, tg[k], now, t0[k]);
+      }, py::arg("items"), py::arg("tags"), py::arg("now") = -1, py::arg("t0s") = py::list())
+      .def("poll", [](PyServe& s, size_t max, int64_t timeout_us) {
+        std::vector<ServeCore::Done> out;
+        {
+          py::gil_scoped_release rel;
+          s.core->poll(out, max, timeout_us);
+        }
+        py::list l;
+        for (auto& d : out) {
+          if (d.err.empty()) l.append(py::make_tuple(d.tag, py::bytes(d.bytes), py::none()));
+          else l.append(py::make_tuple(d.tag, py::none(), py::str(d.err)));
+        }
+        return l;
+      }, py::arg("max") = 4096, py::arg("timeout_us") = 1000)
+      .def("pause", [](PyServe& s) { py::gil_scoped_release rel; s.core->pause(); })
+      .def("resume", [](PyServe& s) { s.core->resume(); })
+      .def("set_device", [](PyServe& s, py::object dev) {
+        const IgpDeviceOps* ops = device_ops_of(dev);
+        s.core->set_device(ops);
+        s.dev = dev;
+      })
+      .def("stop", [](PyServe& s) { py::gil_scoped_release rel; s.core->stop(); })
+      .def("set_links", [](PyServe& s, std::shared_ptr<LinkIndex> l) { s.core->set_links(std::move(l)); })
+      .def("pending_items", [](PyServe& s) { return s.core->pending_items(); })
+      .def_property_readonly("issued", [](const PyServe& s) { return s.core->issued(); })
+      .def_property_readonly("seq", [](const PyServe& s) { return s.core->seq(); })
+      .def_property_readonly("late_steps", [](const PyServe& s) { return s.core->late_steps(); })
+      .def_property_readonly("world", [](const PyServe& s) { return s.core->world(); })
+      .def("stats", [](PyServe& s, bool reset) {
+        ServeStats t = s.core->stats(reset);
+        py::dict d;
+        d["items"] = t.items; d["rows"] = t.rows; d["steps"] = t.steps; d["empty_steps"] = t.empty_steps;
+        d["unary"] = t.unary; d["parse_ns"] = t.parse_ns; d["resolve_ns"] = t.resolve_ns; d["pack_ns"] = t.pack_ns;
+        d["device_ns"] = t.device_ns; d["copy_ns"] = t.copy_ns; d["serialize_ns"] = t.serialize_ns;
+        d["submit_ns"] = t.submit_ns; d["wait_errors"] = t.wait_errors; d["max_step_rows"] = t.max_step_rows;
+        d["actions"] = py::make_tuple(t.actions[0], t.actions[1], t.actions[2], t.actions[3]);
+        py::list dl;
+        for (int k = 0; k < 11; ++k) dl.append(t.deciles[k]);
+        d["deciles"] = dl;
+        d["ml_high"] = t.ml_high; d["blacklisted"] = t.blacklisted; d["scored"] = t.scored;
+        return d;
+      }, py::arg("reset") = false)
+      .def_static("now_ns", &ServeCore::now_ns);
 }

@@ -2,7 +2,6 @@
 
 #include <cstring>
 
-#include "account_index.h"
 #include "pb.h"
 #include "xxh64.h"
 
@@ -14,12 +13,12 @@ const char* const kReasonCodes[12] = {
     "ML_HIGH_RISK", "SUSPICIOUS_PATTERN", "MULTI_ACCOUNT", "DEVICE_FINGERPRINT_MISMATCH"};
 
 void RequestBatch::clear() {
-  account_id.clear(); account_hash.clear(); account_check.clear(); amount.clear(); tx_type.clear();
+  account_id.clear(); account_hash.clear(); amount.clear(); tx_type.clear();
   device_hash.clear(); fp_hash.clear(); ip_hash.clear(); arena.clear();
 }
 
 void RequestBatch::reserve(size_t n) {
-  account_id.reserve(n); account_hash.reserve(n); account_check.reserve(n); amount.reserve(n); tx_type.reserve(n);
+  account_id.reserve(n); account_hash.reserve(n); amount.reserve(n); tx_type.reserve(n);
   device_hash.reserve(n); fp_hash.reserve(n); ip_hash.reserve(n);
 }
 
@@ -29,17 +28,29 @@ const std::string& RequestBatch::own(const char* data, size_t n) {
 }
 
 uint8_t tx_type_id(const char* s, size_t n) {
-  auto eq = [&](const char* lit) { return std::strlen(lit) == n && std::memcmp(s, lit, n) == 0; };
-  if (eq("deposit")) return TX_DEPOSIT;
-  if (eq("withdraw")) return TX_WITHDRAW;
-  if (eq("bet")) return TX_BET;
-  if (eq("win")) return TX_WIN;
-  if (eq("refund")) return TX_REFUND;
-  if (eq("bonus")) return TX_BONUS;
+  auto eq = [&](const char* lit, size_t ln) { return ln == n && std::memcmp(s, lit, n) == 0; };
+  switch (n) {
+    case 3:
+      if (eq("bet", 3)) return TX_BET;
+      if (eq("win", 3)) return TX_WIN;
+      break;
+    case 5:
+      if (eq("bonus", 5)) return TX_BONUS;
+      break;
+    case 6:
+      if (eq("refund", 6)) return TX_REFUND;
+      break;
+    case 7:
+      if (eq("deposit", 7)) return TX_DEPOSIT;
+      break;
+    case 8:
+      if (eq("withdraw", 8)) return TX_WITHDRAW;
+      break;
+  }
   return TX_UNKNOWN;
 }
 
-void parse_tx(const char* data, size_t n, RequestBatch& out) {
+void parse_tx_row(const char* data, size_t n, TxRow& out) {
   pb::Reader r(data, n);
   std::string_view acct, type, ip, dev, fp;
   int64_t amount = 0;
@@ -55,14 +66,42 @@ void parse_tx(const char* data, size_t n, RequestBatch& out) {
       default: r.skip(w);  // player_id, currency, game/round, user_agent, session, metadata
     }
   }
-  out.account_id.push_back(acct);  // a view into the batch's arena copy of the payload
-  out.account_hash.push_back(id_hash(acct, SEED_ACCOUNT));
-  out.account_check.push_back(id_check(acct));
-  out.amount.push_back(amount);
-  out.tx_type.push_back(tx_type_id(type.data(), type.size()));
-  out.device_hash.push_back(id_hash(dev, SEED_DEVICE));
-  out.fp_hash.push_back(id_hash(fp, SEED_FINGERPRINT));
-  out.ip_hash.push_back(id_hash(ip, SEED_IP));
+  out.account = acct;
+  out.account_hash = id_hash(acct, SEED_ACCOUNT);
+  ReqRec& q = out.rec;
+  q.slot = -1;
+  q.tx_type = tx_type_id(type.data(), type.size());
+  q.amount = amount;
+  q.dev_hash = id_hash(dev, SEED_DEVICE);
+  q.fp_hash = id_hash(fp, SEED_FINGERPRINT);
+  q.ip_hash = id_hash(ip, SEED_IP);
+  q.ts = 0;
+}
+
+void parse_batch_rows(const char* data, size_t n, std::vector<TxRow>& out) {
+  pb::Reader r(data, n);
+  uint32_t f, w;
+  while (r.tag(f, w)) {
+    if (f == 1 && w == pb::LEN) {
+      auto m = r.bytes();
+      out.emplace_back();
+      parse_tx_row(m.data(), m.size(), out.back());
+    } else {
+      r.skip(w);
+    }
+  }
+}
+
+void parse_tx(const char* data, size_t n, RequestBatch& out) {
+  TxRow row;
+  parse_tx_row(data, n, row);
+  out.account_id.push_back(row.account);  // a view into the batch's arena copy of the payload
+  out.account_hash.push_back(row.account_hash);
+  out.amount.push_back(row.rec.amount);
+  out.tx_type.push_back(uint8_t(row.rec.tx_type));
+  out.device_hash.push_back(row.rec.dev_hash);
+  out.fp_hash.push_back(row.rec.fp_hash);
+  out.ip_hash.push_back(row.rec.ip_hash);
 }
 
 void parse_batch(const char* data, size_t n, RequestBatch& out) {
@@ -79,11 +118,65 @@ void parse_batch(const char* data, size_t n, RequestBatch& out) {
   }
 }
 
-// Field emitters templated on the sink: pb::Writer appends bytes, pb::Sizer only counts them,
-// so a nested message is sized first and then written straight into the one output buffer
-// (no per-row temporary strings).
-template <class W>
-void emit_feature_vector(W& o, const FeatRec& x) {
+// ---------------------------------------------------------------------------- serializer
+// Raw-pointer writer: the caller guarantees the space (kMaxTxResponse per response body).
+// Field semantics are proto3's: zero scalars are not emitted, +0.0 floats are not emitted.
+namespace {
+
+struct Out {
+  char* p;
+  inline void varint(uint64_t v) {
+    while (v >= 0x80) {
+      *p++ = char(v | 0x80);
+      v >>= 7;
+    }
+    *p++ = char(v);
+  }
+  inline void tag(uint32_t field, uint32_t wire) { varint((uint64_t(field) << 3) | wire); }
+  inline void i32(uint32_t field, int32_t v) {
+    if (v) { tag(field, pb::VARINT); varint(uint64_t(int64_t(v))); }
+  }
+  inline void i64(uint32_t field, int64_t v) {
+    if (v) { tag(field, pb::VARINT); varint(uint64_t(v)); }
+  }
+  inline void boolean(uint32_t field, bool v) {
+    if (v) { tag(field, pb::VARINT); *p++ = 1; }
+  }
+  inline void f32(uint32_t field, float v) {
+    uint32_t u;
+    std::memcpy(&u, &v, 4);
+    if (u == 0) return;
+    tag(field, pb::I32);
+    std::memcpy(p, &u, 4);
+    p += 4;
+  }
+  inline void bytes(const char* s, size_t n) {
+    std::memcpy(p, s, n);
+    p += n;
+  }
+};
+
+// pre-encoded "field 3, LEN, length, bytes" of every reason code
+struct ReasonTable {
+  char enc[12][40];
+  uint8_t len[12];
+  ReasonTable() {
+    for (int b = 0; b < 12; ++b) {
+      Out o{enc[b]};
+      const size_t n = std::strlen(kReasonCodes[b]);
+      o.tag(3, pb::LEN);
+      o.varint(n);
+      o.bytes(kReasonCodes[b], n);
+      len[b] = uint8_t(o.p - enc[b]);
+    }
+  }
+};
+const ReasonTable& reasons_table() {
+  static const ReasonTable t;
+  return t;
+}
+
+inline void write_feature_vector(Out& o, const FeatRec& x) {
   o.i32(1, x.tx_count_1m);
   o.i32(2, x.tx_count_5m);
   o.i32(3, x.tx_count_1h);
@@ -112,48 +205,78 @@ void emit_feature_vector(W& o, const FeatRec& x) {
   o.boolean(26, x.flags & FR_BONUS_ONLY);
 }
 
-template <class W>
-void emit_tx_response(W& o, const ResultView& v, size_t i) {
-  const uint32_t p = v.res[i].packed;
+}  // namespace
+
+size_t write_tx_response(char* out, const ResultRec& r, const FeatRec* f, int64_t ms) {
+  Out o{out};
+  const uint32_t p = r.packed;
   o.i32(1, int32_t(IGP_RES_SCORE(p)));
   o.i32(2, int32_t(IGP_RES_ACTION(p)));
-  const uint32_t reasons = IGP_RES_REASONS(p);
   // response order = rule order, ML_HIGH_RISK appended after the rules (engine.go:284-287)
-  for (int b = 0; b < 12; ++b)
-    if (reasons >> b & 1u) o.str_always(3, kReasonCodes[b]);
-  o.i32(4, int32_t(IGP_RES_RULE(p)));
-  o.f32(5, v.res[i].ml);
-  if (v.response_ms) o.i64(6, v.response_ms[i]);
-  if (v.feat) {
-    pb::Sizer fs;
-    emit_feature_vector(fs, v.feat[i]);
-    o.msg_header(7, fs.n);
-    emit_feature_vector(o, v.feat[i]);
+  const uint32_t reasons = IGP_RES_REASONS(p);
+  if (reasons) {
+    const ReasonTable& t = reasons_table();
+    for (int b = 0; b < 12; ++b)
+      if (reasons >> b & 1u) o.bytes(t.enc[b], t.len[b]);
   }
+  o.i32(4, int32_t(IGP_RES_RULE(p)));
+  o.f32(5, r.ml);
+  o.i64(6, ms);
+  if (f) {
+    char body[400];
+    Out fb{body};
+    write_feature_vector(fb, *f);
+    const size_t n = size_t(fb.p - body);
+    o.tag(7, pb::LEN);
+    o.varint(n);
+    o.bytes(body, n);
+  }
+  return size_t(o.p - out);
+}
+
+void append_batch_response(std::string& out, const ResultRec* r, const FeatRec* f, const int64_t* ms, int64_t ms_all,
+                           size_t n) {
+  // worst case per row into an uninitialised per-thread scratch buffer, then one append of
+  // the bytes actually written (a zero-filled resize of the worst case costs more than the
+  // whole serialisation)
+  thread_local std::unique_ptr<char[]> scratch;
+  thread_local size_t scratch_cap = 0;
+  const size_t need = n * (kMaxTxResponse + 8);
+  if (scratch_cap < need) {
+    scratch.reset(new char[need]);
+    scratch_cap = need;
+  }
+  char* const start = scratch.get();
+  char* p = start;
+  char body[kMaxTxResponse];
+  for (size_t i = 0; i < n; ++i) {
+    const size_t len = write_tx_response(body, r[i], f ? f + i : nullptr, ms ? ms[i] : ms_all);
+    Out o{p};
+    o.tag(1, pb::LEN);
+    o.varint(len);
+    o.bytes(body, len);
+    p = o.p;
+  }
+  out.append(start, size_t(p - start));
 }
 
 std::string serialize_feature_vector(const FeatRec& x) {
-  pb::Writer o;
-  emit_feature_vector(o, x);
-  return o.buf;
+  char body[400];
+  Out o{body};
+  write_feature_vector(o, x);
+  return std::string(body, size_t(o.p - body));
 }
 
 std::string serialize_tx_response(const ResultView& v, size_t i) {
-  pb::Writer o;
-  emit_tx_response(o, v, i);
-  return o.buf;
+  char body[kMaxTxResponse];
+  const size_t n = write_tx_response(body, v.res[i], v.feat ? v.feat + i : nullptr, v.response_ms ? v.response_ms[i] : 0);
+  return std::string(body, n);
 }
 
 std::string serialize_batch_response(const ResultView& v) {
-  pb::Writer o;
-  o.buf.reserve(v.n * (v.feat ? 112 : 28));
-  for (size_t i = 0; i < v.n; ++i) {
-    pb::Sizer s;
-    emit_tx_response(s, v, i);
-    o.msg_header(1, s.n);
-    emit_tx_response(o, v, i);
-  }
-  return o.buf;
+  std::string out;
+  append_batch_response(out, v.res, v.feat, v.response_ms, 0, v.n);
+  return out;
 }
 
 }  // namespace igp::wire

@@ -141,6 +141,12 @@ class GPUConfig:
     rehome_grace_s: float = 5.0   # SPMD: wait this long for survivors' final snapshots
     snapshot_dir: str = ""        # where snapshots are written / re-homed shards restore from
     spmd_heartbeat_s: float = 2.0  # SPMD liveness op period (0: off)
+    # native serving core (csrc/runtime/serve_core.cpp, engine/serving.py): request bytes ->
+    # response bytes without Python on the hot path; the unary micro-batcher is its FIFO
+    native_serving: bool = True
+    serve_depth: int = 3          # pipeline slots (batches in flight) of a shard's device
+    serve_finishers: int = 2      # unary response threads
+    exchange_timeout_s: float = 10.0  # multi-rank step deadline: a peer that misses it failed
 
 
 @dataclass
@@ -223,6 +229,9 @@ class Config:
         self.gpu.wait_us = geti("RISK_BATCH_WAIT_US", self.gpu.wait_us)
         self.gpu.batch_timeout_ms = geti("RISK_BATCH_TIMEOUT_MS", self.gpu.batch_timeout_ms)
         self.gpu.snapshot_dir = env.get("RISK_SNAPSHOT_DIR", self.gpu.snapshot_dir) or self.gpu.snapshot_dir
+        ns = env.get("RISK_NATIVE_SERVING")
+        if ns not in (None, ""):
+            self.gpu.native_serving = ns.strip().lower() not in ("0", "false", "no", "off")
         lt = env.get("RISK_LOG_TRANSFORM")
         if lt:
             self.features.log_transform = lt

@@ -293,7 +293,8 @@ class GpuBackend:
         self.store = DeviceFeatureStore(capacity, cfg.features, self.device, events=True,
                                         blacklist=blacklist, ipintel=ipintel, max_events=dmax)
         self.blacklist, self.ipintel = self.store.blacklist, self.store.ipintel
-        self.scorer = self._make_scorer(plan, model, 2 if exchange is None else 3)
+        self.scorer = self._make_scorer(plan, model, (cfg.gpu.serve_depth if cfg.gpu.native_serving else 2)
+                                         if exchange is None else 3)
         if capture and self.scorer.use_graphs:
             self.scorer.capture()
         self._lock = threading.RLock()
@@ -303,6 +304,20 @@ class GpuBackend:
         self.quarantined: set = set()    # slots whose batch overran its deadline, not yet drained
         self.on_drained = None           # callback(backend) once every quarantined slot drained
         self.timeouts = 0
+        # native serving core (engine/serving.py): once attached, EVERY batch of this shard goes
+        # through it (its stepper owns the driver's slots and batch sequence)
+        self.core = None
+        self._core_pool = None
+
+    def native_device(self):
+        """The scorer's device object for the serving core (None: no native driver)."""
+        from .serving import gpu_device
+        return gpu_device(self.scorer)
+
+    def attach_core(self, core) -> None:
+        import concurrent.futures as cf
+        self.core = core
+        self._core_pool = cf.ThreadPoolExecutor(max_workers=8, thread_name_prefix=f"core-{self.device}")
 
     def swap_model(self, fm, mkind: str) -> None:
         """Model hot-reload: drain the shard, build a scorer for the new plan on the same HBM
@@ -312,23 +327,31 @@ class GpuBackend:
         torch = self.torch
         plan = to_device(compile_onnx(fm), self.device, self.cfg.fraud_model.precision) if mkind == "onnx" else None
         model = {"onnx": "plan", "heuristic": "heuristic", "none": "none"}[mkind]
+        core = self.core
         with self._lock:
+            if core is not None:
+                core.pause()  # every issued step completed (exchange: every rank converged)
             for lk in self._slot_locks:
                 lk.acquire()
             try:
                 old = self.scorer
                 torch.cuda.synchronize(self.device)
                 sc = self._make_scorer(plan, model, old.depth, use_graphs=old.use_graphs)
-                sc._seq = old._seq  # dedup regions rotate by batch seq (one is still dirty)
+                # dedup regions rotate by batch seq (one is still dirty)
+                sc._seq = core.seq if core is not None else old._seq
                 sc.metrics = old.metrics
                 sc.refresh_config(getattr(old, "scoring", None))
                 if old.graphs and sc.use_graphs:
                     sc.capture()
                 torch.cuda.synchronize(self.device)
                 self.scorer = sc
+                if core is not None:
+                    core.set_device(self.native_device())
             finally:
                 for lk in self._slot_locks:
                     lk.release()
+                if core is not None:
+                    core.resume()
 
     def _make_scorer(self, plan, model: str, depth: int, use_graphs=None):
         if self.exchange is not None:
@@ -399,6 +422,10 @@ class GpuBackend:
     def submit(self, req: np.ndarray, now: Optional[int] = None, want_features: bool = True):
         """Launch the batch (chunks of the largest bucket); returns a handle for :meth:`collect`.
         A pipeline slot's pinned buffers are reused only after its results were collected."""
+        if self.core is not None:
+            rows = np.ascontiguousarray(req, REQREC).view(np.uint8)
+            fut = self._core_pool.submit(self.core.score_rows, rows, None, int(now), bool(want_features))
+            return ("core", fut, bool(want_features))
         sc = self.scorer
         pend = []
         n = len(req)
@@ -420,6 +447,15 @@ class GpuBackend:
         an event wait (no polling). A batch that overruns it is quarantined with every batch
         behind it: their slots stay locked (never reused) until a drain thread has seen them
         complete, then ``on_drained`` fires; the caller gets :class:`BatchTimeout`."""
+        if isinstance(pend, tuple) and pend[0] == "core":
+            try:
+                res, feat = pend[1].result()
+            except RuntimeError as e:
+                if "deadline" in str(e):  # the core answered at the deadline; the step drains later
+                    self._quarantine_core()
+                    raise BatchTimeout(f"GPU batch exceeded its deadline on {self.device}") from e
+                raise
+            return np.asarray(res, np.uint32).reshape(-1, 2), (feat.view(FEATREC).reshape(-1) if pend[2] else None)
         res, feats = [], []
         release = list(pend)
         try:
@@ -447,6 +483,26 @@ class GpuBackend:
         batch's graphs)."""
         from ..native import hipk
         hipk().stall(self.scorer.cstream.cuda_stream, float(ms) * 1e3)
+
+    def _quarantine_core(self) -> None:
+        """The serving core keeps an overrunning step's slot until the device finished it;
+        watch for that, then report the shard drained (``on_drained``)."""
+        import time as _t
+        with self._lock:
+            self.timeouts += 1
+            self.quarantined.add("core")
+        core = self.core
+
+        def drain():
+            _t.sleep(0.01)
+            while core.late_steps() > 0:
+                _t.sleep(0.005)
+            with self._lock:
+                self.quarantined.discard("core")
+            cb = self.on_drained
+            if cb is not None and not self.quarantined:
+                cb(self)
+        threading.Thread(target=drain, daemon=True, name=f"gpu-drain-{self.device}").start()
 
     def _quarantine(self, pend) -> None:
         """Keep the overrunning batches' slots out of service and drain them on a thread that
@@ -584,6 +640,17 @@ class NativeCpuBackend:
         self._lock = threading.RLock()
         self.refresh_config()
 
+    core = None
+
+    def native_device(self, depth: int = 2, cap: int = 8192):
+        """A CpuDevice over this shard's CpuScorer for the serving core."""
+        from ..native import native
+        self._device = native().CpuDevice(self.sc, int(depth), int(cap))
+        return self._device
+
+    def attach_core(self, core) -> None:
+        self.core = core
+
     def swap_model(self, fm, mkind: str) -> None:
         """Model hot-reload: the C++ scorer's executor is replaced between batches."""
         spec = cpu_model_spec(self.cfg, fm, mkind)
@@ -629,6 +696,10 @@ class NativeCpuBackend:
               update: bool = True) -> Result:
         now = int(time.time()) if now is None else int(now)
         self._sync()
+        if self.core is not None and update:  # batches of this shard go through its serving core
+            res, feat = self.core.score_rows(np.ascontiguousarray(req, REQREC).view(np.uint8), None, now,
+                                             bool(want_features))
+            return res, (feat.view(FEATREC).reshape(-1) if feat is not None else None)
         res, feat = self.sc.score(np.ascontiguousarray(req, REQREC).view(np.uint8), now, update, want_features)
         return res, (feat.view(FEATREC).reshape(-1) if feat is not None else None)
 

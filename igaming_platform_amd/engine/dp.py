@@ -105,6 +105,9 @@ class DpGpuScorer(GpuScorer):
         sb, nb = self.slots[slot], self.world * (C + 1) * REQ
         K.memcpy_async(sb.xsend, self.host_x[slot], nb)
         K.memcpy_async(sb.dev_slab, self.host_slab[slot], HDR_BYTES)
+        # the receive buffer's chunk counts are zeroed ahead of the all-to-all: an aborted
+        # collective (failover) then leaves zero rows to compact instead of a stale chunk
+        hipk().exchange_clear(sb.xrecv.data_ptr(), self.world, C, torch.cuda.current_stream().cuda_stream)
 
     def _post_body(self, slot: int, C: int) -> None:
         sb, b = self.slots[slot], self.cap(C)

@@ -162,6 +162,12 @@ class RiskEngine:
         else:
             for _ in range(world):
                 self.backends.append(self._cpu_backend(mkind, fm, backend, self.capacity))
+        # native serving core of a single-shard engine (engine/serving.py): request bytes ->
+        # response bytes without Python on the hot path, and the only issuer of the shard's
+        # device batches
+        self.core = None
+        if spmd is None and world == 1 and cfg.gpu.native_serving:
+            self._attach_core(self.backends[0])
         self.fallback = None
         if cfg.gpu.fallback == "cpu":  # degraded tier: CPU scorer without the shard's feature state
             self.fallback = self._cpu_backend(mkind, fm, "golden" if backend == "golden" else "cpu", 1)
@@ -217,6 +223,31 @@ class RiskEngine:
             self.group.start_heartbeat()
         log.info("risk engine ready", extra={"fields": dict(backend=backend, shards=world, capacity=self.capacity,
                                                               model=mkind)})
+
+    def _attach_core(self, be, indexes=None, rank: int = 0, clock=None) -> None:
+        from . import serving
+        if be.kind == "gpu":
+            dev = be.native_device()
+            seq0 = be.scorer._seq
+        elif hasattr(be, "native_device"):
+            dev = be.native_device(self.cfg.gpu.serve_depth, self.cfg.gpu.max_batch)
+            seq0 = 0
+        else:
+            return  # golden (pure Python) shards keep the Python path
+        if dev is None:
+            return
+        core = serving.make_core(indexes if indexes is not None else [self.registry.index[0]], dev, self.cfg,
+                                 rank=rank, clock=clock, seq0=seq0)
+        core.set_links(self.links)
+        be.attach_core(core)
+        self.core = core
+        self.metrics.sources.append(lambda c=core: serving.core_metrics(c))
+
+    def _native_ok(self) -> bool:
+        """Whether a request may take the all-native path (the Python path keeps the audit
+        ring, fault injection and the degraded-shard fallback)."""
+        return (self.core is not None and all(self.healthy) and not self.auditlog.enabled
+                and not self.faults.any_active())
 
     def _cpu_backend(self, mkind, fm, kind: str = "cpu", capacity: int = 1):
         if kind == "cpu":
@@ -484,11 +515,19 @@ class RiskEngine:
         return int(n)
 
     # ---- wire-level entry points (gRPC handlers call these with raw bytes)
-    def score_batch_bytes(self, data: bytes, t0: Optional[float] = None) -> bytes:
+    def score_batch_bytes(self, data: bytes, t0: Optional[float] = None, now: Optional[int] = None) -> bytes:
         t0 = time.perf_counter() if t0 is None else t0
+        now = int(time.time()) if now is None else int(now)
+        if self._native_ok():
+            try:
+                return self.core.score_batch(data, now, int(t0 * 1e9))
+            except RuntimeError as e:  # device failure / deadline: the Python path falls back
+                if "ServeCore" not in str(e):
+                    raise
+                self._mark_unhealthy(0, e)
         rb = self.N.RequestBatch()
         rb.parse_batch(data)
-        res, feats, slots, owners = self._score_parsed(rb, int(time.time()))
+        res, feats, slots, owners = self._score_parsed(rb, now)
         ms = np.full(len(rb), int((time.perf_counter() - t0) * 1e3), np.int64)
         return self.N.serialize_batch_response(res, feats.view(np.int32).reshape(-1, 32) if feats is not None else None, ms)
 
@@ -789,10 +828,12 @@ class RiskEngine:
 
     # ---- health / durability
     def close(self) -> None:
-        """Release the SPMD workers (rank 0 only)."""
+        """Release the SPMD workers (rank 0 only) and stop the serving core."""
         if self.group is not None:
             self.group.stop()
             self.group = None
+        if self.core is not None:
+            self.core.stop()
 
     def health(self) -> Dict:
         fo = self.failover

@@ -324,6 +324,8 @@ class GpuScorer:
         if os.environ.get("IGP_NATIVE_DRIVER", "1") != "0":
             d = K._mod().PipeDriver(self.cstream.cuda_stream, self.stream.cuda_stream, self.mstream.cuda_stream,
                                     self.depth, [t.data_ptr() for t in self.host_slab])
+            for slot in range(self.depth):  # what the native serving core reads after a wait
+                d.set_host_results(slot, self.host_res[slot].data_ptr(), self.host_feat[slot].data_ptr())
             for (b, slot), g in self.graphs.items():
                 d.set_graphs(b, slot, g[0].raw_cuda_graph_exec(), g[1].raw_cuda_graph_exec(),
                              g[2].raw_cuda_graph_exec(), g[3].raw_cuda_graph_exec())

@@ -27,6 +27,8 @@ class Metrics:
         self._dec = [0] * 11
         self._act = [0] * 4
         self._n = self._ml_high = self._bl = 0
+        # native serving cores count their own decisions (engine/serving.py core_metrics)
+        self.sources = []
         r.register(_DecisionCollector(self))
         self.batch_size = Histogram("gpu_batch_size", "rows per device micro-batch",
                                     buckets=(1, 8, 64, 256, 1024, 4096, 8192), registry=r)
@@ -80,6 +82,13 @@ class _DecisionCollector:
         m = self.m
         with m._lock:
             dec, act, n, hi, bl = list(m._dec), list(m._act), m._n, m._ml_high, m._bl
+        for src in list(m.sources):
+            c = src()
+            if not c:
+                continue
+            dec = [a + b for a, b in zip(dec, c["deciles"])]
+            act = [a + b for a, b in zip(act, c["actions"])]
+            n, hi, bl = n + c["scored"], hi + c["ml_high"], bl + c["blacklisted"]
         c = CounterMetricFamily("risk_scores", "transactions scored")
         c.add_metric([], n)
         yield c

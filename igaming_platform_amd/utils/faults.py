@@ -45,6 +45,10 @@ class Faults:
         with self._lock:
             return dict(self._active.get(name, {}))
 
+    def any_active(self) -> bool:
+        with self._lock:
+            return bool(self._active)
+
     def active(self, name: str, **match) -> bool:
         with self._lock:
             kv = self._active.get(name)

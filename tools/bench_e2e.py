@@ -152,10 +152,21 @@ def run_e2e(a) -> dict:
                 lat.append(dt)
 
     th = [threading.Thread(target=worker) for _ in range(a.threads)]
+    core = getattr(eng, "core", None)
+    if core is not None:
+        core.stats(True)
     t0 = time.perf_counter()
     [t.start() for t in th]
     [t.join() for t in th]
     el = time.perf_counter() - t0
+    stages = {}
+    if core is not None:  # per-stage host cost of the native path, ns per row (summed over threads)
+        st = core.stats(True)
+        rows = max(int(st["rows"]), 1)
+        stages = {k[:-3] + "_ns_per_row": round(st[k] / rows, 1)
+                  for k in ("parse_ns", "resolve_ns", "pack_ns", "submit_ns", "copy_ns", "serialize_ns")}
+        stages.update(device_us_per_step=round(st["device_ns"] / max(int(st["steps"]), 1) / 1e3, 1),
+                      steps=int(st["steps"]), mean_rows_per_step=round(st["rows"] / max(int(st["steps"]), 1), 1))
     eng.close()
     return dict(metric="fraud scores/sec (risk.v1.ScoreBatch bytes in -> bytes out, in-process)",
                 value=a.steps * n_req / el, unit="scores/s", scope="e2e", n_gpus=1 if a.backend == "gpu" else 0,
@@ -163,7 +174,11 @@ def run_e2e(a) -> dict:
                 scaling="weak", vs_baseline=None, dtype="fp32", data="synthetic (UUID ids, random-init cfg3 weights)",
                 config=dict(model="cfg3 GBDT(100,d7,128f)+MLP(32-256-1)", batch_per_request=n_req,
                             caller_threads=a.threads, accounts=a.accounts,
-                            path="C++ parse -> AccountIndex(UUID) -> pack -> GPU graphs -> C++ serialize"),
+                            path=("native serving core (engine/serving.py): C++ parse -> AccountIndex(UUID) -> "
+                                  "FIFO -> stepper packs + launches -> completion -> C++ serialize, no Python "
+                                  "per batch" if core is not None else
+                                  "C++ parse -> AccountIndex(UUID) -> pack -> GPU graphs -> C++ serialize")),
+                host_stages=stages,
                 p50_latency_ms=float(np.percentile(lat, 50)), p99_latency_ms=float(np.percentile(lat, 99)),
                 latency_baseline_ms=BASELINE_P99_MS,
                 latency_vs_baseline=BASELINE_P99_MS / float(np.percentile(lat, 99)))
@@ -259,7 +274,7 @@ def main(argv=None) -> int:
     ap.add_argument("--payloads", type=int, default=6)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--threads", type=int, default=3)
+    ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--clients", type=int, default=8)
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--json-out", default="")
