@@ -63,13 +63,19 @@ __global__ __launch_bounds__(256) void exchange_compact_kernel(XchgCompactArgs a
   __syncthreads();
   if (threadIdx.x == 0) {
     int s = 0;
+    int64_t t = 0;
     for (int p = 0; p < a.N; ++p) {
       pre[p] = s;
       s += cnt[p];
+      // senders of the serving core stamp their step clock into the chunk header: the step is
+      // scored at the latest clock among the senders that sent rows (0: keep the batch header's)
+      const int64_t ts = a.recv[(size_t)p * (a.C + 1)].ts;
+      if (cnt[p] > 0 && ts > t) t = ts;
     }
     pre[a.N] = s;
     if (blockIdx.x == 0) {
       a.hdr->n = s < a.cap ? s : a.cap;
+      if (t > 0) a.hdr->now = t;
       a.route[a.cap] = s > a.cap ? s - a.cap : 0;
     }
   }

@@ -663,6 +663,7 @@ PYBIND11_MODULE(_native, m) {
         s.dev = dev;
       })
       .def("stop", [](PyServe& s) { py::gil_scoped_release rel; s.core->stop(); })
+      .def("abort", [](PyServe& s) { py::gil_scoped_release rel; s.core->abort(); })
       .def("set_links", [](PyServe& s, std::shared_ptr<LinkIndex> l) { s.core->set_links(std::move(l)); })
       .def("pending_items", [](PyServe& s) { return s.core->pending_items(); })
       .def_property_readonly("issued", [](const PyServe& s) { return s.core->issued(); })

@@ -139,10 +139,12 @@ void ShmXchgDevice::step(int slot, int64_t now) {
   wait_all(&Counter::posted, k_ + 1);
   // 2. compact the rows every sender routed to me (sender order, then row order)
   size_t n = 0;
+  int64_t t = 0;  // the step's clock: the latest clock of the senders that sent rows
   for (int p = 0; p < world_; ++p) {
     const ReqRec* chunk = send_area(p, q) + size_t(rank_) * stride;
     int c = chunk[0].slot;
     c = c < 0 ? 0 : (c > C_ ? C_ : c);
+    if (c > 0 && chunk[0].ts > t) t = chunk[0].ts;
     for (int j = 0; j < c; ++j) {
       compact_[n] = chunk[1 + j];
       compact_[n].tx_type &= 0xff;
@@ -151,7 +153,7 @@ void ShmXchgDevice::step(int slot, int64_t now) {
     }
   }
   // 3. score my rows (score-then-update of my shard)
-  if (n) sc_->score(compact_.data(), n, now, true, res_.data(), feat_.data());
+  if (n) sc_->score(compact_.data(), n, t > 0 ? t : now, true, res_.data(), feat_.data());
   rows_scored_.fetch_add(int64_t(n));
   // 4. results back: [destination p][C] ResultRec, then [C] FeatRec
   char* out = res_area(rank_, q);

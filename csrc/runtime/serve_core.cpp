@@ -45,6 +45,8 @@ struct ServeCore::Item {
   std::vector<int32_t> ostart;  // exchange: [world + 1] owner ranges of `rows`
   std::vector<int32_t> ocur;    // next untaken row per owner (direct: [1])
   int64_t remaining = 0;        // rows not yet in a step (q_mu_)
+  int64_t taken = 0;            // rows handed to steps (q_mu_)
+  int64_t aborted_rows = 0;     // rows that never reached a step (abort; m)
   int64_t now = 0;
   bool wf = false;
   ResultRec* res = nullptr;     // outputs in request order
@@ -188,8 +190,8 @@ void ServeCore::enqueue(Item* it) {
 void ServeCore::wait_item(Item* it) {
   size_t done = 0;
   std::unique_lock<std::mutex> l(it->m);
-  while (done < it->n) {
-    it->cv.wait(l, [&] { return !it->ready.empty(); });
+  while (done + size_t(it->aborted_rows) < it->n) {
+    it->cv.wait(l, [&] { return !it->ready.empty() || done + size_t(it->aborted_rows) >= it->n; });
     std::vector<std::pair<Step*, Seg>> batch;
     batch.swap(it->ready);
     l.unlock();
@@ -347,6 +349,7 @@ bool ServeCore::issue_step(std::unique_lock<std::mutex>& lk, bool allow_empty) {
       st->segs.push_back(Seg{it, 0, it->ocur[0], n, take});
       it->ocur[0] += take;
       it->remaining -= take;
+      it->taken += take;
       n += take;
       now = std::max(now, it->now);
       st->wf |= it->wf;
@@ -365,6 +368,7 @@ bool ServeCore::issue_step(std::unique_lock<std::mutex>& lk, bool allow_empty) {
         st->segs.push_back(Seg{it, o, it->ocur[o], fill[o], take});
         it->ocur[o] += take;
         it->remaining -= take;
+        it->taken += take;
         fill[o] += take;
         n += take;
         if (fill[o] == cap_) ++full;
@@ -402,6 +406,7 @@ bool ServeCore::issue_step(std::unique_lock<std::mutex>& lk, bool allow_empty) {
       ReqRec& h = chunks[size_t(o) * stride];
       std::memset(&h, 0, sizeof h);
       h.slot = fill[o];  // row count of owner o's chunk
+      h.ts = now;        // this sender's clock: the owner scores the step at its senders' latest
     }
     for (const Seg& s : st->segs)
       std::memcpy(chunks + size_t(s.owner) * stride + 1 + s.dev_pos, s.item->rows.data() + s.item_pos,
@@ -446,6 +451,11 @@ void ServeCore::stepper_loop() {
   const int64_t full_rows = exchange_ ? int64_t(cap_) * world_ * 7 / 8 : int64_t(cap_);
   int64_t hold_since = 0;
   for (;;) {
+    if (aborting_) {  // failover: no convergence with peers that may be dead
+      stopped_ = true;
+      idle_cv_.notify_all();
+      return;
+    }
     const bool peer_ahead = exchange_ && clock_->max_issued() > issued_.load();
     // pause / stop: converge on a generation (exchange: every rank at the same step count)
     const bool draining = stopping_ && queue_.empty();
@@ -706,6 +716,37 @@ void ServeCore::set_device(const IgpDeviceOps* dev) {
     steps_[s] = std::make_unique<Step>();
     free_slots_.push_back(depth_ - 1 - s);
   }
+}
+
+void ServeCore::abort() {
+  std::deque<Item*> dropped;
+  {
+    std::unique_lock<std::mutex> lk(q_mu_);
+    if (threads_.empty()) return;
+    aborting_ = true;
+    stopping_ = true;
+    dropped.swap(queue_);
+    queued_rows_ = 0;
+  }
+  q_cv_.notify_all();
+  // queued items never reach a step: fail them now (rows already in steps fail or finish with
+  // their steps)
+  for (Item* it : dropped) {
+    if (it->kind == 1) {
+      Done d{it->tag, std::string(), "ServeCore: aborted"};
+      delete it;
+      std::lock_guard<std::mutex> g(out_mu_);
+      outq_.push_back(std::move(d));
+      continue;
+    }
+    std::lock_guard<std::mutex> g(it->m);
+    it->failed = true;
+    it->err = "ServeCore: aborted";
+    it->aborted_rows = int64_t(it->n) - it->taken;
+    it->cv.notify_one();
+  }
+  out_cv_.notify_all();
+  stop();
 }
 
 void ServeCore::stop() {

@@ -124,6 +124,8 @@ class ServeCore {
   void set_device(const IgpDeviceOps* dev);
   // drain and stop the threads (exchange: keeps following peers until every rank stopped)
   void stop();
+  // failover: stop at once without converging with the peers; queued requests fail
+  void abort();
 
   void set_links(std::shared_ptr<LinkIndex> links) { links_ = std::move(links); }
   ServeStats stats(bool reset);
@@ -186,7 +188,7 @@ class ServeCore {
   std::vector<int> free_slots_;
   std::vector<std::unique_ptr<Step>> steps_;  // by slot
   int inflight_ = 0;
-  bool stopping_ = false, stopped_ = false, paused_ = false, pause_req_ = false;
+  bool stopping_ = false, stopped_ = false, paused_ = false, pause_req_ = false, aborting_ = false;
   int64_t hold_gen_ = 0;              // generation the stepper converges to (0: none)
   bool held_ = false;
   std::condition_variable idle_cv_;   // inflight_ reached 0 / paused

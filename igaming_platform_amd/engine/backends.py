@@ -289,7 +289,7 @@ class GpuBackend:
         self.exchange = exchange
         self.rank = rank
         self.owner_filter = owner_filter
-        dmax = max(cfg.gpu.buckets) * (exchange["senders"] if exchange else 1)
+        dmax = exchange["senders"] * max(exchange["cbuckets"]) if exchange else max(cfg.gpu.buckets)
         self.store = DeviceFeatureStore(capacity, cfg.features, self.device, events=True,
                                         blacklist=blacklist, ipintel=ipintel, max_events=dmax)
         self.blacklist, self.ipintel = self.store.blacklist, self.store.ipintel
@@ -650,6 +650,21 @@ class NativeCpuBackend:
 
     def attach_core(self, core) -> None:
         self.core = core
+
+    def exchange_device(self, shm_name: str, world: int, rank: int, depth: int, C: int, create: bool,
+                        timeout_s: float):
+        """This shard as one rank of a CPU data-parallel group: the owner-routed exchange over
+        /dev/shm (csrc/runtime/cpu_device.cpp ShmXchgDevice)."""
+        from ..native import native
+        self._device = native().ShmXchgDevice(self.sc, shm_name, int(world), int(rank), int(depth), int(C),
+                                              bool(create), float(timeout_s))
+        return self._device
+
+    @property
+    def rows_scored(self) -> int:
+        """Rows this shard scored through the exchange (its own accounts only)."""
+        d = getattr(self, "_device", None)
+        return int(d.rows_scored) if d is not None and hasattr(d, "rows_scored") else 0
 
     def swap_model(self, fm, mkind: str) -> None:
         """Model hot-reload: the C++ scorer's executor is replaced between batches."""

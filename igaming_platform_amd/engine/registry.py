@@ -2,7 +2,10 @@
 
 Routing is by account owner, ``owner = XXH64(account_id) % world`` (SURVEY §2.5 DP), so all of
 an account's state lives on one GPU and the hot path needs no cross-GPU feature traffic.
-Each owner has its own C++ :class:`AccountIndex` (open addressing, full-id verification).
+Each owner has its own C++ :class:`AccountIndex` (lock-free open addressing, exact id
+verification). In multi-rank serving every rank ingests, so the indexes live in /dev/shm and
+every rank of the node maps the same ones (``shm_prefix``): an account gets one slot on its
+owner whichever rank saw it first.
 """
 from __future__ import annotations
 
@@ -16,12 +19,21 @@ from ..utils.hashing import SEED_ACCOUNT
 
 
 class AccountRegistry:
-    def __init__(self, capacity_per_owner: int, world: int = 1):
+    def __init__(self, capacity_per_owner: int, world: int = 1, shm_prefix: str = "", create: bool = True):
         N = native()
         self.world = int(world)
         self.capacity = int(capacity_per_owner)
-        self.index = [N.AccountIndex(self.capacity) for _ in range(self.world)]
+        if shm_prefix:
+            self.index = [N.AccountIndex(self.capacity, f"{shm_prefix}-acct{o}", create) for o in range(self.world)]
+        else:
+            self.index = [N.AccountIndex(self.capacity) for _ in range(self.world)]
         self._lock = threading.Lock()
+
+    def unlink_shared(self) -> None:
+        """Drop the /dev/shm names (every rank has mapped the indexes; mappings stay valid)."""
+        for ix in self.index:
+            if ix.shared:
+                ix.unlink_shared()
 
     def owner_of_hash(self, h: np.ndarray) -> np.ndarray:
         return (np.asarray(h, np.uint64) % np.uint64(self.world)).astype(np.int32)

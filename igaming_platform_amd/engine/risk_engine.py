@@ -135,14 +135,21 @@ class RiskEngine:
         self.model_version = 1
         self.backends: List = []
         self.healthy = [True] * world
+        self.core = None
         if spmd is not None:
             from ..parallel.spmd import ShardProxy, ShardRunner, SpmdGroup
-            local = make_local_backend(cfg, backend, self.capacity, fm, mkind, self.blacklist, self.ipintel,
-                                       rank=0, capture=capture, comm=spmd)
+            node = SpmdNode(cfg, spmd, backend, self.capacity, fm, mkind, self.blacklist, self.ipintel,
+                            capture=capture)
+            self.node = node
+            self.registry = node.registry  # node-shared: every rank resolves ids to the same slots
+            local = node.local
             self.local = local
+            self.core = node.core
+            self.core.set_links(self.links)
+            from . import serving
+            self.metrics.sources.append(lambda c=node.core: serving.core_metrics(c))
             abuse_gpu = make_abuse_gpu(cfg, local, self._abuse_am)
-            self.group = SpmdGroup(spmd, ShardRunner(spmd, local, abuse_gpu), max_rows=max(cfg.gpu.buckets),
-                                   chunk_buckets=local.scorer.cbuckets if local.kind == "gpu" else None,
+            self.group = SpmdGroup(spmd, ShardRunner(spmd, local, abuse_gpu, node.core),
                                    heartbeat_s=cfg.gpu.spmd_heartbeat_s,
                                    used_fn=lambda: [self.registry.size(o) for o in range(self.world)],
                                    on_failure=self._group_failed)
@@ -164,8 +171,7 @@ class RiskEngine:
                 self.backends.append(self._cpu_backend(mkind, fm, backend, self.capacity))
         # native serving core of a single-shard engine (engine/serving.py): request bytes ->
         # response bytes without Python on the hot path, and the only issuer of the shard's
-        # device batches
-        self.core = None
+        # device batches (SPMD: the node's core, above)
         if spmd is None and world == 1 and cfg.gpu.native_serving:
             self._attach_core(self.backends[0])
         self.fallback = None
@@ -276,7 +282,11 @@ class RiskEngine:
         g = self.group
         if g is not None:  # owner-routed exchange: each rank scores its own rows
             try:
-                res, feats = g.score(req, owners, now, want_features)
+                try:
+                    res, feats = self.core.score_rows(req.view(np.uint8), owners, now, bool(want_features))
+                    feats = feats.view(FEATREC).reshape(-1) if feats is not None else None
+                except RuntimeError as e:  # a peer missed the step deadline: the group failed
+                    raise g.fail(e) from e
             except GroupFailure:
                 # the batch died with the group (some rows may have been applied on their
                 # shards): answer all of it from the stateless fallback; later batches go to
@@ -427,6 +437,13 @@ class RiskEngine:
         log.error("spmd group failed: failing over to rank 0", extra={"fields": dict(error=str(err))})
         g.abandon()
         local = self.local
+        core, self.core = self.core, None
+        if core is not None:
+            try:
+                core.abort()  # no convergence with the dead peer; later batches take the Python path
+            except Exception as e:
+                log.error("serving core abort failed", extra={"fields": dict(error=str(e))})
+            local.core = None
         try:
             if local.kind == "gpu":
                 local.leave_exchange()
@@ -524,7 +541,14 @@ class RiskEngine:
             except RuntimeError as e:  # device failure / deadline: the Python path falls back
                 if "ServeCore" not in str(e):
                     raise
-                self._mark_unhealthy(0, e)
+                g = self.group
+                if g is not None:
+                    try:
+                        g.fail(e)
+                    except Exception:  # GroupFailure: the failover below serves this batch
+                        pass
+                else:
+                    self._mark_unhealthy(0, e)
         rb = self.N.RequestBatch()
         rb.parse_batch(data)
         res, feats, slots, owners = self._score_parsed(rb, now)
@@ -830,9 +854,9 @@ class RiskEngine:
     def close(self) -> None:
         """Release the SPMD workers (rank 0 only) and stop the serving core."""
         if self.group is not None:
-            self.group.stop()
+            self.group.stop()  # also stops this rank's core (every rank converges)
             self.group = None
-        if self.core is not None:
+        elif self.core is not None:
             self.core.stop()
 
     def health(self) -> Dict:
@@ -942,10 +966,10 @@ def make_local_backend(cfg: Config, kind: str, capacity: int, fm, mkind: str, bl
         model = {"onnx": "plan", "heuristic": "heuristic", "none": "none"}[mkind]
         exchange = None
         if comm is not None:
-            from ..parallel.exchange import rccl_comms
-            from .dp import exchange_buckets
-            exchange = dict(comms=rccl_comms(comm.rank, comm.world), world=comm.world, senders=1,
-                            cbuckets=exchange_buckets(cfg.gpu.buckets))
+            from ..parallel.exchange import chunk_capacity, rccl_comms
+            # every rank ingests: each step carries up to C rows per (sender, owner) pair
+            exchange = dict(comms=rccl_comms(comm.rank, comm.world), world=comm.world, senders=comm.world,
+                            cbuckets=[chunk_capacity(max(cfg.gpu.buckets), comm.world)])
         return GpuBackend(cfg, capacity, dev, plan=plan, model=model, blacklist=blacklist, ipintel=ipintel,
                           capture=capture, owner_filter=owner_filter, rank=rank, exchange=exchange)
     N = native()
@@ -976,16 +1000,85 @@ def make_abuse_gpu(cfg: Config, local, abuse_model):
 
 
 def serve_shard(cfg: Config, comm, backend: str = "gpu", capacity: Optional[int] = None, fraud_model=None,
-                abuse_model=None, capture: bool = True):
+                abuse_model=None, capture: bool = True, ingress=None):
     """Worker rank (>= 1) of an SPMD group: build the same local shard as rank 0 and serve
-    its ops until rank 0 stops the group. Returns (ops served, rows this shard scored)."""
+    its cold ops until rank 0 stops the group; ``ingress(node)``, when given, runs this rank's
+    own traffic through its serving core on a thread meanwhile. Returns (ops served, rows
+    this shard scored)."""
     from ..parallel.spmd import run_worker
+    node = worker_node(cfg, comm, backend, capacity, fraud_model, capture)
+    if ingress is not None:  # this rank's own traffic, beside the cold-op loop
+        import threading
+        th = threading.Thread(target=ingress, args=(node,), name=f"ingress-{comm.rank}", daemon=True)
+        th.start()
+    abuse_gpu = make_abuse_gpu(cfg, node.local, abuse_model if abuse_model is not None else cfg.abuse_model.path)
+    out = run_worker(comm, node.local, abuse_gpu, node.core)
+    if ingress is not None:
+        th.join(60)
+    return out
+
+
+def worker_node(cfg: Config, comm, backend: str = "gpu", capacity: Optional[int] = None, fraud_model=None,
+                capture: bool = True) -> "SpmdNode":
+    """The serving objects of a worker rank (>= 1): local shard, node-shared registry, core."""
     fm = _load_onnx(fraud_model if fraud_model is not None else cfg.fraud_model.path)
     mkind = cfg.fraud_model.kind
     if mkind == "auto":
         mkind = "onnx" if fm is not None else "heuristic"
-    local = make_local_backend(cfg, backend, int(capacity or cfg.gpu.accounts_per_gpu), fm, mkind,
-                               Blacklist(cfg.gpu.blacklist_capacity), IPIntel(cfg.gpu.blacklist_capacity),
-                               rank=comm.rank, capture=capture, comm=comm)
-    abuse_gpu = make_abuse_gpu(cfg, local, abuse_model if abuse_model is not None else cfg.abuse_model.path)
-    return run_worker(comm, local, abuse_gpu)
+    return SpmdNode(cfg, comm, backend, int(capacity or cfg.gpu.accounts_per_gpu), fm, mkind,
+                    Blacklist(cfg.gpu.blacklist_capacity), IPIntel(cfg.gpu.blacklist_capacity), capture=capture)
+
+
+class SpmdNode:
+    """One rank's serving objects in a one-process-per-GPU (or per CPU shard) group:
+
+    * its local shard joined to the owner-routed exchange (GPU: two RCCL communicators of its
+      own and the XchgDriver; CPU: the /dev/shm exchange),
+    * the node-shared account registry (every rank resolves ids to the same owner slots),
+    * the step clock shared with the peers,
+    * the serving core that ingests this rank's traffic and issues its exchange steps.
+
+    The /dev/shm regions are created by rank 0, opened by the others after a barrier and
+    unlinked once every rank mapped them (nothing is left behind if a process dies later)."""
+
+    def __init__(self, cfg: Config, comm, backend: str, capacity: int, fm, mkind: str, blacklist, ipintel,
+                 capture: bool = True):
+        from . import serving
+        from ..parallel.exchange import chunk_capacity
+        rank, world = comm.rank, comm.world
+        self.rank, self.world = rank, world
+        prefix = comm.bcast_bytes(serving.shm_token().encode() if rank == 0 else None, 0).decode()
+        self.local = make_local_backend(cfg, backend, capacity, fm, mkind, blacklist, ipintel, rank=rank,
+                                        capture=capture, comm=comm if backend == "gpu" else None)
+        C = chunk_capacity(max(cfg.gpu.buckets), world)
+        op_t = getattr(comm, "op_timeout", None)
+        timeout_s = min(cfg.gpu.exchange_timeout_s, op_t.total_seconds()) if op_t else cfg.gpu.exchange_timeout_s
+
+        def regions(create: bool):
+            reg = AccountRegistry(capacity, world, shm_prefix=prefix, create=create)
+            clock = native().StepClock(f"{prefix}-clock", world, rank, create)
+            if self.local.kind == "gpu":
+                dev = self.local.native_device()
+            else:
+                dev = self.local.exchange_device(f"{prefix}-xchg", world, rank, cfg.gpu.serve_depth, C, create,
+                                                 timeout_s)
+            return reg, clock, dev
+        if rank == 0:
+            self.registry, self.clock, dev = regions(True)
+        comm.barrier()
+        if rank != 0:
+            self.registry, self.clock, dev = regions(False)
+        comm.barrier()
+        if rank == 0:
+            self.registry.unlink_shared()
+            self.clock.unlink_shared()
+            if hasattr(dev, "unlink_shared"):
+                dev.unlink_shared()
+        seq0 = self.local.scorer._seq if self.local.kind == "gpu" else 0
+        self.core = serving.make_core(self.registry.index, dev, cfg, rank=rank, clock=self.clock, seq0=seq0)
+        self.local.attach_core(self.core)
+
+    def score_batch_bytes(self, data: bytes, now: Optional[int] = None) -> bytes:
+        """This rank's ingress: ScoreBatch request bytes -> response bytes."""
+        import time as _t
+        return self.core.score_batch(data, int(_t.time()) if now is None else int(now), _t.perf_counter_ns())

@@ -1,29 +1,30 @@
-"""SPMD multi-GPU serving: one process per GPU, rank 0 runs the API.
+"""SPMD multi-GPU serving: one process per GPU, every rank ingests.
 
 Data parallelism by account owner (``owner = XXH64(account_id) % world``):
-every account's feature state lives on exactly one rank. Per ScoreBatch / micro-batch:
+every account's feature state lives on exactly one rank. The hot path is each rank's native
+serving core (engine/serving.py, csrc/runtime/serve_core.cpp): its own ingress (gRPC
+listener / bench threads) parses and resolves requests through the node-shared account
+registry (/dev/shm), and its stepper issues owner-routed exchange steps (RCCL all-to-all over
+xGMI between GPUs, /dev/shm between CPU shards): every rank scores ONLY the rows it owns and
+the results return to the ingress rank. Ranks keep their step sequences aligned through a
+shared step clock; no host collective, no lock and no header broadcast per step.
 
-  rank 0: C++ parse + registry resolve (owner, slot) for every request; one 64-byte header
-          broadcast (op, n, now, want_features, chunk capacity C)
-  all:    the owner-routed exchange (:mod:`.exchange`): rank 0's rows travel to their owners
-          in per-owner chunks (RCCL all-to-all over xGMI between GPUs, device-resident; gloo
-          between CPU shards), every rank scores ONLY the rows it owns (score-then-update of
-          its own shard), and the packed 8-byte results (+ 128-byte FeatRec when features are
-          wanted) come back to rank 0 with a second all-to-all and one D2H copy.
-
-Cold-path ops (thresholds, blacklist/ip tables, warehouse rows, GetFeatures, event
-histories, GRU abuse scores) use a broadcast-then-reduce protocol over :mod:`.comm`.
+This module is the control plane (cold ops) over gloo: rank 0 broadcasts an op (thresholds,
+blacklist/ip tables, warehouse rows, GetFeatures, event histories, GRU abuse scores,
+snapshots, model reloads) and every rank applies it to its local shard; state-changing ops
+end with a barrier, so a request any rank ingests after the op returned sees it everywhere.
 
 Failure handling (reference: engine.go:279-282 degrades a failed model call,
 cmd/main.go:329-342 recovers a failed handler): every collective rank 0 issues carries a
-deadline (:mod:`.comm`), and a heartbeat op (OP_PING, an all-reduce of ones) runs every
-``heartbeat_s`` so a dead worker is noticed while the API is idle too. The first failed
-collective marks the group failed (:class:`GroupFailure`) and calls ``on_failure``: the
-engine then scores that batch on its stateless fallback, leaves the group and re-homes every
-remote shard onto rank 0 from its snapshot (engine/risk_engine.py ``_group_failed``). A
-surviving worker whose collective fails writes a final snapshot of its shard next to the
-periodic ones (``shard<r>.<ext>`` + ``shard<r>.final``) before it exits, so its state is
-re-homed without loss; a dead worker's shard comes back from its last periodic snapshot.
+deadline (:mod:`.comm`), a heartbeat op (OP_PING, an all-reduce of ones) runs every
+``heartbeat_s`` so a dead worker is noticed while the API is idle too, and an exchange step a
+peer never joins fails at the step deadline. The first failure marks the group failed
+(:class:`GroupFailure`) and calls ``on_failure``: the engine then scores that batch on its
+stateless fallback, leaves the group and re-homes every remote shard onto rank 0 from its
+snapshot (engine/risk_engine.py ``_group_failed``). A surviving worker whose collective fails
+aborts its serving core and writes a final snapshot of its shard next to the periodic ones
+(``shard<r>.<ext>`` + ``shard<r>.final``) before it exits, so its state is re-homed without
+loss; a dead worker's shard comes back from its last periodic snapshot.
 """
 from __future__ import annotations
 
@@ -38,10 +39,11 @@ import time
 import numpy as np
 
 from ..config import RuleWeights, ScoringConfig
-from ..layouts import ACCTBATCH, FEATREC, REQREC
+from ..layouts import ACCTBATCH, FEATREC, REQREC  # noqa: F401  (REQREC: OP_INGEST rows)
 
-OP_SCORE, OP_INGEST, OP_CONFIG, OP_TABLES, OP_BATCH, OP_EXT, OP_FEATURES, OP_RESET, OP_STOP, OP_EVHIST, \
-    OP_ABUSE, OP_SNAPSHOT, OP_RESTORE, OP_RELOAD, OP_FEATMANY, OP_PING, OP_METRICS = range(1, 18)
+OP_INGEST, OP_CONFIG, OP_TABLES, OP_BATCH, OP_EXT, OP_FEATURES, OP_RESET, OP_STOP, OP_EVHIST, \
+    OP_ABUSE, OP_SNAPSHOT, OP_RESTORE, OP_RELOAD, OP_FEATMANY, OP_PING, OP_METRICS = range(2, 18)
+MUTATING = (OP_INGEST, OP_CONFIG, OP_TABLES, OP_BATCH, OP_EXT, OP_RESET, OP_RELOAD)
 MET_WORDS = 128   # K10 device counter block (csrc/include/records.h MET_*); [106] = rows scored
 
 log = logging.getLogger("igaming_platform_amd.spmd")
@@ -90,27 +92,24 @@ def scoring_from_json(b: bytes) -> ScoringConfig:
 
 
 class ShardRunner:
-    """What every rank (0 included) executes for one op on its local backend."""
+    """What every rank (0 included) executes for one cold op on its local backend."""
 
-    def __init__(self, comm, backend, abuse_gpu=None):
+    def __init__(self, comm, backend, abuse_gpu=None, core=None):
         self.comm = comm
         self.be = backend
         self.rank = comm.rank
         self.abuse_gpu = abuse_gpu
-        self.hx = None
-        if backend.kind != "gpu":
-            from .exchange import HostExchange
-            self.hx = HostExchange(comm.rank, comm.world, comm)
+        self.core = core  # this rank's serving core (paused around snapshots / restores)
         self.snapshot_dir = None  # the directory of the last OP_SNAPSHOT (final snapshot on failure)
-        self.used = [0] * comm.world  # slots in use per rank (rank 0's registry, via OP_PING)
+        self.used = [0] * comm.world  # slots in use per rank (the shared registry, via OP_PING)
 
     @property
     def rows_scored(self) -> int:
         """Rows this rank scored through the exchange (its own accounts only): the device
         metrics row counter on a GPU shard (K10, reads the device), the host count otherwise."""
-        if self.hx is not None:
-            return self.hx.rows_scored
-        return int(self.be.scorer.read_metrics()[106])
+        if self.be.kind == "gpu":
+            return int(self.be.scorer.read_metrics()[106])
+        return int(getattr(self.be, "rows_scored", 0))
 
     def local_metrics(self) -> np.ndarray:
         """This shard's K10 counters (GPU), or just its exchange row count (CPU shards)."""
@@ -118,30 +117,33 @@ class ShardRunner:
         if self.be.kind == "gpu":
             v = np.asarray(self.be.scorer.read_metrics(), np.int64)
             m[:min(len(v), MET_WORDS)] = v[:MET_WORDS]
-        elif self.hx is not None:
-            m[106] = self.hx.rows_scored
+        else:
+            m[106] = self.rows_scored
         return m
 
     def _mine(self, owners: np.ndarray) -> np.ndarray:
         return owners == self.rank
 
-    def score(self, req, owners, C: int, now: int, want_features: bool):
-        """One owner-routed exchange step (collective). ``req``/``owners``: the ingress rows
-        (rank 0) or None. Returns (res, feats) of the ingress rows in request order."""
-        if self.be.kind == "gpu":
-            t = getattr(self.comm, "op_timeout", None)
-            return self.be.exchange_score(req, owners, C, now, want_features,
-                                          timeout_s=t.total_seconds() if t is not None else None)
-
-        def score_fn(rows, wf):
-            return self.be.score(rows, now, wf)
-
-        return self.hx.step(req, owners, C, want_features, score_fn)
+    def _quiesced(self, fn):
+        """Run ``fn`` with this rank's serving core paused (every rank does the same for the
+        same op, so the exchange converges to one step count first)."""
+        if self.core is None:
+            return fn()
+        self.core.pause()
+        try:
+            return fn()
+        finally:
+            self.core.resume()
 
     def handle(self, op: int, hdr: np.ndarray, payload: bytes):
+        out = self._handle(op, hdr, payload)
+        if op in MUTATING:
+            # a request ingested anywhere after the op returned must see it on every shard
+            self.comm.barrier()
+        return out
+
+    def _handle(self, op: int, hdr: np.ndarray, payload: bytes):
         n, now, aux, aux2 = int(hdr[1]), int(hdr[2]), int(hdr[3]), int(hdr[4])
-        if op == OP_SCORE:  # a worker's share of a step rank 0 started (no payload: the exchange)
-            return self.score(None, None, aux2, now, bool(aux))
         if op == OP_METRICS:  # every shard's K10 counter block, one row per rank (sum-reduce)
             out = np.zeros((self.comm.world, MET_WORDS), np.int64)
             out[self.rank] = self.local_metrics()
@@ -217,13 +219,13 @@ class ShardRunner:
                 self.snapshot_dir = meta["dir"]
                 self.used = [int(u) for u in meta["used"]] or self.used
                 if self.be.kind == "gpu":
-                    self.be.store.snapshot(path, n_used=max(int(meta["used"][self.rank]), 1))
+                    self._quiesced(lambda: self.be.store.snapshot(path, n_used=max(int(meta["used"][self.rank]), 1)))
                 else:
-                    self.be.snapshot(path)
+                    self._quiesced(lambda: self.be.snapshot(path))
             elif self.be.kind == "gpu":
-                self.be.store.restore(path)
+                self._quiesced(lambda: self.be.store.restore(path))
             else:
-                self.be.restore(path)
+                self._quiesced(lambda: self.be.restore(path))
             self.comm.barrier()
             return None
         raise ValueError(f"unknown op {op}")
@@ -239,6 +241,9 @@ class ShardRunner:
             xd = getattr(self.be.scorer, "abort_exchange", None)
             if xd is not None:
                 xd()  # unblock the RCCL exchange kernels still waiting on the dead peer
+        if self.core is not None:
+            self.core.abort()  # no convergence with a dead peer; steps in flight fail at their deadline
+        if self.be.kind == "gpu":
             cap = self.be.store.capacity
             self.be.store.snapshot(path, n_used=min(cap, max(int(self.used[self.rank]), 1) + FINAL_SNAPSHOT_MARGIN))
         else:
@@ -254,8 +259,7 @@ class SpmdGroup:
     """Rank 0's handle on the group: issues an op to every rank and runs its own share.
     Ops are serialised (one collective sequence at a time) by a lock."""
 
-    def __init__(self, comm, runner: ShardRunner, max_rows: int = 8192, chunk_buckets=None,
-                 heartbeat_s: float = 0.0, used_fn=None, on_failure=None):
+    def __init__(self, comm, runner: ShardRunner, heartbeat_s: float = 0.0, used_fn=None, on_failure=None):
         """``heartbeat_s`` > 0: an OP_PING every that many seconds (liveness while idle; its
         payload tells the workers how many slots rank 0's registry gives each shard, from
         ``used_fn()``). ``on_failure(exc)``: called once, from the thread whose collective
@@ -265,8 +269,6 @@ class SpmdGroup:
         self.comm = comm
         self.runner = runner
         self.world = comm.world
-        self.max_rows = int(max_rows)
-        self.chunk_buckets = sorted(chunk_buckets) if chunk_buckets else None
         self._lock = threading.Lock()
         self.failed: BaseException = None
         self.on_failure = on_failure
@@ -282,6 +284,10 @@ class SpmdGroup:
             self._hb = threading.Thread(target=self._heartbeat, args=(self.heartbeat_s,), daemon=True,
                                         name="spmd-heartbeat")
             self._hb.start()
+
+    def fail(self, e: BaseException) -> "GroupFailure":
+        """A hot-path exchange step failed (a peer missed its deadline): the group is failed."""
+        return self._fail(e)
 
     def _fail(self, e: BaseException) -> "GroupFailure":
         first = self.failed is None
@@ -331,37 +337,6 @@ class SpmdGroup:
                 self.ping()
             except GroupFailure:
                 return
-
-    def _chunk_capacity(self, owners: np.ndarray) -> int:
-        from .exchange import max_owner_count
-        c = max(max_owner_count(owners, self.world), 1)
-        if self.chunk_buckets is not None:  # GPU shards: the captured chunk capacities
-            for b in self.chunk_buckets:
-                if c <= b:
-                    return b
-            raise ValueError(f"{c} rows for one owner exceed the largest chunk bucket")
-        return 1 << (c - 1).bit_length()
-
-    # ---- hot path
-    def score(self, req: np.ndarray, owners: np.ndarray, now: int, want_features: bool = True):
-        """Owner-routed scoring of ``req`` (REQREC) whose accounts live on ``owners``: one
-        header broadcast + one exchange step per ``max_rows`` rows."""
-        n = len(req)
-        res = np.zeros((n, 2), np.uint32)
-        feats = np.zeros(n, FEATREC) if want_features else None
-        for i in range(0, n, self.max_rows):
-            sub, own = req[i:i + self.max_rows], np.asarray(owners[i:i + self.max_rows], np.int64)
-            C = self._chunk_capacity(own)
-            hdr = np.array([OP_SCORE, len(sub), now, int(want_features), C, 0, 0, 0], np.int64)
-
-            def step():
-                self.comm.bcast_i64(hdr, 0)
-                return self.runner.score(sub, own, C, now, want_features)
-            r, f = self._collective(step)
-            res[i:i + len(sub)] = r
-            if want_features:
-                feats[i:i + len(sub)] = f
-        return res, feats
 
     # ---- cold path
     def ingest(self, ev: np.ndarray) -> None:
@@ -419,7 +394,8 @@ class SpmdGroup:
         self._issue(OP_RESTORE, json.dumps({"dir": directory, "used": []}).encode())
 
     def stop(self) -> None:
-        """Release the workers (no-op once the group failed: they leave on their own)."""
+        """Release the workers (no-op once the group failed: they leave on their own); every
+        rank then stops its serving core (the cores converge on one final step count)."""
         self._stop.set()
         if self.failed is not None:
             return
@@ -427,7 +403,9 @@ class SpmdGroup:
         try:
             self._collective(lambda: self.comm.bcast_i64(hdr, 0))
         except GroupFailure:
-            pass
+            return
+        if self.runner.core is not None:
+            self.runner.core.stop()
 
     def abandon(self) -> None:
         """After a failure: stop the heartbeat and tear the process group down, which makes the
@@ -442,11 +420,13 @@ class SpmdGroup:
             log.warning("destroy_process_group after failure: %s", e)
 
 
-def run_worker(comm, backend, abuse_gpu=None):
-    """Loop of ranks >= 1 until rank 0 sends STOP. Returns (ops served, rows scored). When a
-    collective fails (rank 0 or a peer died / the group was torn down), the shard writes its
-    final snapshot (if rank 0 ever sent a snapshot directory) and the loop returns."""
-    runner = ShardRunner(comm, backend, abuse_gpu)
+def run_worker(comm, backend, abuse_gpu=None, core=None):
+    """Cold-op loop of ranks >= 1 until rank 0 sends STOP (the rank's serving core keeps
+    ingesting and stepping on its own threads meanwhile). Returns (ops served, rows scored).
+    When a collective fails (rank 0 or a peer died / the group was torn down), the shard
+    aborts its core, writes its final snapshot (if rank 0 ever sent a snapshot directory) and
+    the loop returns."""
+    runner = ShardRunner(comm, backend, abuse_gpu, core)
     served = 0
     while True:
         try:
@@ -455,8 +435,10 @@ def run_worker(comm, backend, abuse_gpu=None):
             hdr = comm.bcast_i64(np.zeros(8, np.int64), 0, deadline=False)
             op = int(hdr[0])
             if op == OP_STOP:
+                if core is not None:
+                    core.stop()
                 return served, runner.rows_scored
-            payload = b"" if op == OP_SCORE else comm.bcast_bytes(None, 0)
+            payload = comm.bcast_bytes(None, 0)
             runner.handle(op, hdr, payload)
         except Exception as e:
             log.error("spmd worker %d: group failed (%s); writing the final snapshot", comm.rank, e)
