@@ -61,10 +61,15 @@ def parse():
                     help="N > 1: exchange = every rank ingests 8192 rows/step spread over all owners and "
                          "the owner-routed RCCL exchange (the serving path, engine/dp.py) moves each row to "
                          "its owner and the results back; replicas = N independent single-GPU pipelines")
-    ap.add_argument("--scope", default="engine_only", choices=["engine_only", "e2e", "grpc"],
-                    help="engine_only: pre-resolved ReqRec rows (the headline); e2e: ScoreBatch request bytes "
-                         "-> parse -> UUID AccountIndex -> GPU -> serialized response bytes, in-process; grpc: the "
-                         "same over grpc.aio with client processes (tools/bench_e2e.py)")
+    ap.add_argument("--scope", default="serving", choices=["serving", "engine_only", "e2e", "grpc"],
+                    help="serving (default): the serving objects of every rank - risk.v1 ScoreBatch request bytes "
+                         "(UUID account ids) -> the rank's native serving core (C++ parse, node-shared AccountIndex, "
+                         "owner-routed RCCL exchange steps for N > 1, GPU pipeline) -> response bytes with the "
+                         "FeatureVector, every rank ingesting; engine_only: pre-resolved ReqRec rows into the "
+                         "device pipeline (device-pipeline number); e2e / grpc: tools/bench_e2e.py")
+    ap.add_argument("--threads", type=int, default=8, help="serving scope: ingress threads per rank")
+    ap.add_argument("--requests", type=int, default=0, help="serving scope: transactions per ScoreBatch request "
+                    "(default: the config's micro-batch)")
     ap.add_argument("--rpc", default="batch", choices=["batch", "tx"], help="--scope grpc: ScoreBatch or unary "
                     "ScoreTransaction through the micro-batcher")
     ap.add_argument("--json-out", default="")
@@ -97,6 +102,9 @@ def maybe_launch_torchrun(a) -> None:
 
 def main():
     a = parse()
+    if a.scope == "serving":
+        maybe_launch_torchrun(a)
+        return serving_bench(a)
     if a.scope != "engine_only":  # 1 GPU, the request path end to end (tools/bench_e2e.py)
         sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
         import bench_e2e
@@ -393,6 +401,181 @@ def dp_bench(a, world: int, rank: int, dev) -> None:
     }
     _emit(a, world, rank, out)
     return out
+
+
+def serving_bench(a) -> None:
+    """The serving objects end to end, every rank ingesting (bench.py --gpus N runs
+    the serving path, not a hand-built scorer). Per rank:
+
+      * N = 1: ``RiskEngine`` (GPU backend) and its native serving core over the three-stream
+        pipeline; N > 1: ``SpmdNode`` - the rank's shard joined to the owner-routed RCCL
+        exchange (two all-to-alls per step over xGMI, every rank a sender), the node-shared
+        account registry (/dev/shm) and the step clock, driven by the rank's serving core
+      * ``--threads`` ingress threads call ``core.score_batch(request bytes)``: each request is
+        a serialized risk.v1 ScoreBatchRequest of ``--requests`` transactions on UUID account
+        ids spread over every owner; the response is the serialized ScoreBatchResponse with a
+        FeatureVector per transaction (nothing skipped: parse, resolve, routing, feature
+        assembly + store update, trees, MLP, ensemble, results back, serialization)
+
+    A step = one ScoreBatch request per rank (K per rank timed, W untimed first); the value is
+    the whole job's transactions per second, the latency the per-request bytes-in -> bytes-out
+    time (it includes the micro-batch queueing inside the core)."""
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    import threading
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+    import bench_e2e
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.layouts import ACCTBATCH
+    from igaming_platform_amd.onnx import builders
+    from igaming_platform_amd.utils import benchkit
+    from igaming_platform_amd.utils.synth import NOW0, make_population
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # IGP_BENCH_BACKEND=cpu: the same serving objects on CPU shards (protocol rehearsal without a GPU)
+    kind = os.environ.get("IGP_BENCH_BACKEND", "gpu")
+    if kind == "gpu":
+        torch.cuda.set_device(local)
+
+    def sync():
+        if kind == "gpu":
+            torch.cuda.synchronize(local)
+    comm = None
+    if world > 1:
+        # the control plane (shm names, barriers, RCCL unique ids, result reduce) runs over gloo;
+        # the hot path moves rows over the exchange's own RCCL communicators
+        dist.init_process_group("gloo")
+        from igaming_platform_amd.parallel.comm import TorchComm
+        comm = TorchComm("gloo")
+    if a.config not in benchkit.CONFIGS or benchkit.CONFIGS[a.config]["model"] == "heuristic":
+        raise SystemExit("serving scope: a fraud model config (cfg1 / cfg2 / cfg3)")
+    c = benchkit.CONFIGS[a.config]
+    B = a.requests or a.batch or c["batch"]
+    cfg = Config()
+    cfg.features.width = c["width"]
+    cfg.fraud_model.precision = a.numerics
+    cfg.gpu.buckets = sorted({64, 512, 2048, B})
+    cfg.gpu.max_batch = B
+    cfg.gpu.serve_depth = a.depth
+    cfg.gpu.spmd_heartbeat_s = 0.0
+    n_acc = a.accounts
+    fm = builders.build(c["model"]).SerializeToString()
+    if world == 1:
+        from igaming_platform_amd.engine.risk_engine import RiskEngine
+        eng = RiskEngine(cfg, backend=kind, capacity=n_acc + 4096, fraud_model=fm)
+        core, registry, backend = eng.core, eng.registry, eng.backends[0]
+        mode = "native serving core over the single-GPU three-stream pipeline"
+    else:
+        from igaming_platform_amd.engine.risk_engine import SpmdNode, _load_onnx
+        from igaming_platform_amd.features.tables import Blacklist, IPIntel
+        node = SpmdNode(cfg, comm, kind, n_acc + 4096, _load_onnx(fm), "onnx",
+                        Blacklist(cfg.gpu.blacklist_capacity), IPIntel(cfg.gpu.blacklist_capacity))
+        core, registry, backend = node.core, node.registry, node.local
+        mode = "native serving core per rank, owner-routed RCCL exchange (every rank ingests)"
+    if core is None:
+        raise RuntimeError("no native serving core (IGP native driver disabled?)")
+    # this rank's accounts: the global population is world x n_acc UUIDs; a rank loads the
+    # warehouse rows of the accounts it owns (owner = XXH64(id) % world)
+    pop = make_population(n_acc, c["width"] - 30, seed=3, fast_hash=True)
+    total = n_acc * world
+    from igaming_platform_amd.native import native
+    from igaming_platform_amd.utils.hashing import SEED_ACCOUNT
+    step = 1 << 17
+    for s0 in range(0, total, step):
+        ids = [bench_e2e.account_id(i) for i in range(s0, min(total, s0 + step))]
+        h = native().id_hashes(ids, SEED_ACCOUNT)
+        mine = np.nonzero((h % np.uint64(world)).astype(np.int64) == rank)[0]
+        if not len(mine):
+            continue
+        sel = [ids[i] for i in mine]
+        slots, _ = registry.resolve_ids(sel, insert=True)
+        rows = np.asarray(pop.batch[(s0 + mine) % n_acc], ACCTBATCH)
+        ok = slots >= 0
+        backend.set_batch_rows(slots[ok], rows[ok])
+        if c["width"] > 30:
+            backend.set_ext(slots[ok], pop.ext[(s0 + mine)[ok] % n_acc])
+    payloads = bench_e2e.make_payloads(total, 6, B, seed=11 + rank)
+    lat = []
+    lock = threading.Lock()
+
+    def run(n_req: int, t_base: int, record: bool):
+        counter = {"i": 0}
+
+        def worker():
+            while True:
+                with lock:
+                    i = counter["i"]
+                    if i >= n_req:
+                        return
+                    counter["i"] = i + 1
+                t0 = time.perf_counter_ns()
+                out = core.score_batch(payloads[i % len(payloads)], t_base + i // 50, t0)
+                dt = (time.perf_counter_ns() - t0) / 1e6
+                if len(out) < B:
+                    raise RuntimeError("short response")
+                if record:
+                    with lock:
+                        lat.append(dt)
+        th = [threading.Thread(target=worker) for _ in range(a.threads)]
+        [t.start() for t in th]
+        [t.join() for t in th]
+
+    def barrier():
+        if comm is not None:
+            comm.barrier()
+
+    run(max(a.warmup, a.threads), NOW0 - 3600, False)   # history + warm graphs / caches
+    barrier()
+    sync()
+    core.stats(True)
+    t0 = time.perf_counter()
+    run(a.steps, NOW0, True)
+    sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    st = core.stats(True)
+    rows = max(int(st["rows"]), 1)
+    stages = {k[:-3] + "_ns_per_row": round(st[k] / rows, 1)
+              for k in ("parse_ns", "resolve_ns", "pack_ns", "submit_ns", "copy_ns", "serialize_ns")}
+    stages.update(device_us_per_step=round(st["device_ns"] / max(int(st["steps"]), 1) / 1e3, 1),
+                  device_steps=int(st["steps"]), empty_steps=int(st["empty_steps"]),
+                  mean_rows_per_device_step=round(st["rows"] / max(int(st["steps"]), 1), 1))
+    p99, p50 = float(np.percentile(lat, 99)), float(np.percentile(lat, 50))
+    if comm is not None:  # the slowest rank's clock and latencies
+        mx = torch.tensor([elapsed, p99, p50], dtype=torch.float64)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        elapsed, p99, p50 = (float(x) for x in mx)
+    out = {
+        "metric": "fraud scores/sec (whole node) + p99 score latency",
+        "value": world * a.steps * B / elapsed, "unit": "scores/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": a.numerics, "data": "synthetic (UUID account ids, random-init weights)",
+        "config": {"model": c["desc"], "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
+                   "per_gpu_batch": B, "transactions_per_request": B, "accounts_per_gpu": n_acc,
+                   "ingress_threads_per_rank": a.threads, "pipeline_depth": a.depth, "serving": mode,
+                   "numerics": numerics_desc(a),
+                   "comm_env": {k: v for k, v in sorted(os.environ.items())
+                                if k.startswith(("NCCL_", "RCCL_")) or k == "GPU_MAX_HW_QUEUES"}},
+        "scope": "serving (risk.v1 ScoreBatch bytes in -> bytes out, in-process, every rank ingesting)",
+        "p99_latency_ms": p99, "p50_latency_ms": p50, "latency_what": "per ScoreBatch request, bytes in -> bytes "
+        "out, including the serving core's micro-batch queueing",
+        "latency_baseline_ms": BASELINE_P99_MS, "latency_vs_baseline": BASELINE_P99_MS / p99 if p99 > 0 else None,
+        "host_stages_rank0": stages,
+    }
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        node.core.stop()
+        dist.destroy_process_group()
+    else:
+        eng.close()
 
 
 def _emit(a, world: int, rank: int, out: dict) -> None:

@@ -56,6 +56,16 @@ void copy_err(char* err, int32_t errlen, const char* msg) {
   err[errlen - 1] = 0;
 }
 
+// the serving core calls a device's function table from threads of its own: the first call
+// on a thread makes the driver's device current there (streams / events / graphs of device d)
+void bind_device(int d) {
+  thread_local int cur = -1;
+  if (cur != d) {
+    hip_ok(hipSetDevice(d), "set device");
+    cur = d;
+  }
+}
+
 // event wait with a deadline (hipEventSynchronize has none): query with a short back-off
 bool poll_event(hipEvent_t e, int64_t timeout_us) {
   const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
@@ -84,6 +94,7 @@ class PipeDriver {
     // memory after it). IGP_EVENT_DEVSCOPE=0 restores system scope everywhere.
     const char* ds = getenv("IGP_EVENT_DEVSCOPE");
     const unsigned dev_flags = hipEventDisableTiming | ((ds && atoi(ds) == 0) ? 0u : (unsigned)hipEventDisableSystemFence);
+    hip_ok(hipGetDevice(&device_), "get device");  // the serving core's threads bind to it
     ev_.resize(3 * depth);
     for (size_t i = 0; i < ev_.size(); ++i)
       hip_ok(hipEventCreateWithFlags(&ev_[i], i % 3 == 2 ? hipEventDisableTiming : dev_flags), "event create");
@@ -158,6 +169,7 @@ class PipeDriver {
                      int32_t errlen) -> int32_t {
       auto* d = static_cast<PipeDriver*>(ctx);
       try {
+        bind_device(d->device_);
         int bucket = -1;
         for (int b : d->buckets_)
           if (b >= (n > 0 ? n : 1)) { bucket = b; break; }
@@ -174,6 +186,7 @@ class PipeDriver {
     ops_.wait = [](void* ctx, int32_t slot, int64_t timeout_us, char* err, int32_t errlen) -> int32_t {
       auto* d = static_cast<PipeDriver*>(ctx);
       try {
+        bind_device(d->device_);
         d->drain_slot(slot);
         hipEvent_t e = d->ev_[3 * slot + 2];
         if (timeout_us < 0) {
@@ -477,6 +490,7 @@ class PipeDriver {
   std::vector<char*> host_res_, host_feat_;
   std::vector<int> buckets_;
   IgpDeviceOps ops_{};
+  int device_ = 0;
 };
 
 }  // namespace

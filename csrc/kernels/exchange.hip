@@ -137,6 +137,16 @@ void hip_ok(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("exchange ") + what + ": " + hipGetErrorString(e));
 }
 
+// the serving core calls the driver's function table from threads of its own: the first call
+// on a thread makes the driver's device current there
+void bind_device(int d) {
+  thread_local int cur = -1;
+  if (cur != d) {
+    hip_ok(hipSetDevice(d), "set device");
+    cur = d;
+  }
+}
+
 // ------------------------------------------------------------------------------- RCCL (dlopen)
 struct Uid {
   char b[128];
@@ -249,6 +259,7 @@ class XchgDriver {
       : cs_(S(cs)), ss_(S(ss)), ms_(S(ms)), xs_(S(xs)), ys_(S(ys)), depth_(depth), world_(world),
         cx_(cx.ptr()), cy_(cy.ptr()), r_(rccl("")) {
     if (cx.world() != world || cy.world() != world) throw std::runtime_error("XchgDriver: communicator world");
+    hip_ok(hipGetDevice(&device_), "get device");  // the serving core's threads bind to it
     ev_.resize(6 * depth);
     for (auto& e : ev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event create");
     done_recorded_.assign(depth, false);
@@ -328,6 +339,7 @@ class XchgDriver {
                      int32_t errlen) -> int32_t {
       auto* d = static_cast<XchgDriver*>(ctx);
       try {
+        bind_device(d->device_);
         d->submit_impl(slot, d->ops_C_, seq, now, 0, 0, true);
       } catch (const std::exception& e) {
         if (err && errlen > 0) {
@@ -340,6 +352,15 @@ class XchgDriver {
     };
     ops_.wait = [](void* ctx, int32_t slot, int64_t timeout_us, char* err, int32_t errlen) -> int32_t {
       auto* d = static_cast<XchgDriver*>(ctx);
+      try {
+        bind_device(d->device_);
+      } catch (const std::exception& ex) {
+        if (err && errlen > 0) {
+          std::strncpy(err, ex.what(), size_t(errlen) - 1);
+          err[errlen - 1] = 0;
+        }
+        return -1;
+      }
       hipEvent_t e = d->E(slot, 5);
       if (timeout_us < 0) {
         const hipError_t r = hipEventSynchronize(e);
@@ -528,6 +549,7 @@ class XchgDriver {
   bool captured_ = false;
   IgpDeviceOps ops_{};
   int ops_C_ = 0;
+  int device_ = 0;
 };
 
 template <class T>

@@ -131,6 +131,7 @@ void ServeCore::resolve_rows(std::vector<wire::TxRow>& rows, Item* it) {
       it->rows[k].slot = slots[k];
     }
     it->ocur.assign(1, 0);
+    it->ostart = {0, int32_t(n)};  // one owner (a world-1 exchange reads the owner ranges too)
   } else {
     // counting sort by owner (owner = digest % world, the registry's routing)
     it->ostart.assign(world_ + 1, 0);
@@ -259,6 +260,7 @@ void ServeCore::score_rows(const ReqRec* rows, const int32_t* owners, size_t n, 
   if (world_ == 1) {
     it.rows.assign(rows, rows + n);
     it.ocur.assign(1, 0);
+    it.ostart = {0, int32_t(n)};
   } else {
     if (!owners) throw std::runtime_error("ServeCore.score_rows: owners required when world > 1");
     it.ostart.assign(world_ + 1, 0);

@@ -195,7 +195,7 @@ def _ingress_worker(rank, world, port, q, barrier):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3])
 def test_multi_ingress_every_rank_ingests_and_matches_single_process(world):
     """Every rank ingests ScoreBatch traffic through its own native serving core; rows travel
     to their owners over the exchange and back. Every rank's responses (and the features
