@@ -409,13 +409,71 @@ class AioInterceptor(grpc.aio.ServerInterceptor):
 INLINE = {"CheckBlacklist", "GetThresholds"}   # pure host work: never leaves the event loop
 
 
-def aio_risk_handler(servicer: RiskServicer, pool, inline_all: bool) -> grpc.GenericRpcHandler:
+class NativeUnary:
+    """Unary ScoreTransaction through a native serving core (engine/serving.py): the handler
+    enqueues the request bytes (``core.submit_tx``: C++ parse + resolve, one row into the
+    core's FIFO, where concurrent calls share device micro-batches) and awaits a future; one
+    poller thread drains the core's completion queue and resolves a whole batch of futures
+    with one ``call_soon_threadsafe``. No Python per-request thread, queue or lock on the hot
+    path (the Python MicroBatcher is gone from ScoreTransaction)."""
+
+    def __init__(self, core, loop, now_fn=None, ok_fn=None, fallback=None, pool=None):
+        """``ok_fn() -> bool``: whether the native path may serve now (else ``fallback(bytes)``
+        runs in ``pool``: the engine's Python path with its audit ring / fault injection /
+        degraded-shard fallback)."""
+        import itertools
+        self.core, self.loop = core, loop
+        self.ok_fn, self.fallback, self.pool = ok_fn, fallback, pool
+        self._tags = itertools.count(1)
+        self._pending: Dict[int, "asyncio.Future"] = {}
+        self._stop = threading.Event()
+        self.calls = 0
+        self.now_fn = now_fn or (lambda: int(time.time()))
+        self._th = threading.Thread(target=self._poll, name="native-unary-poll", daemon=True)
+        self._th.start()
+
+    async def call(self, data: bytes) -> bytes:
+        if self.ok_fn is not None and not self.ok_fn():
+            return await self.loop.run_in_executor(self.pool, self.fallback, data)
+        fut = self.loop.create_future()
+        tag = next(self._tags)
+        self._pending[tag] = fut
+        self.core.submit_tx(data, tag, self.now_fn(), time.perf_counter_ns())
+        self.calls += 1
+        return await fut
+
+    def _resolve(self, items) -> None:
+        for tag, body, err in items:
+            fut = self._pending.pop(tag, None)
+            if fut is None or fut.done():
+                continue
+            if err is not None:
+                fut.set_exception(InvalidArgument(err) if "pb:" in err else RuntimeError(err))
+            else:
+                fut.set_result(body)
+
+    def _poll(self) -> None:
+        while not self._stop.is_set():
+            items = self.core.poll(8192, 20000)
+            if items:
+                self.loop.call_soon_threadsafe(self._resolve, items)
+
+    def close(self) -> None:
+        self._stop.set()
+        self._th.join(timeout=2)
+
+
+def aio_risk_handler(servicer: RiskServicer, pool, inline_all: bool, native_tx: "NativeUnary" = None
+                     ) -> grpc.GenericRpcHandler:
     """Async adapters over RiskServicer. Work that may wait on a GPU runs in ``pool`` so the
     event loop keeps accepting calls; on the CPU backend everything runs inline (cheapest)."""
     handlers = {}
     for rpc, req_name, resp_name in P.METHODS:
         fn = getattr(servicer, rpc)
-        if rpc == "ScoreTransaction" and servicer.batcher is not None:
+        if rpc == "ScoreTransaction" and native_tx is not None:
+            async def h(data, ctx, _n=native_tx):
+                return await _n.call(data)
+        elif rpc == "ScoreTransaction" and servicer.batcher is not None:
             async def h(data, ctx, _b=servicer.batcher):
                 return await asyncio.wrap_future(_b.submit(data, time.perf_counter()))
         elif rpc in ("PredictLTV", "GetPlayerSegment") and servicer.ltv_batcher is not None:
@@ -489,11 +547,21 @@ class RiskServer:
     """risk.v1 on a ``grpc.aio`` server whose event loop runs on a dedicated thread."""
 
     def __init__(self, engine, port: int = 0, host: str = "127.0.0.1", workers: int = 16,
-                 batching: bool = True, max_batch: Optional[int] = None, wait_us: Optional[int] = None):
+                 batching: bool = True, max_batch: Optional[int] = None, wait_us: Optional[int] = None,
+                 reuseport: bool = False, extra_ports=()):
+        """``reuseport``: bind with SO_REUSEPORT so every rank of a multi-GPU group listens on
+        the same port (the kernel spreads connections over the ranks); ``extra_ports``: more
+        listening ports (rank 0's internal port for cold RPCs forwarded by the other ranks)."""
         self.engine = engine
         cfg = engine.cfg
         self.batcher = None
-        if batching:
+        self.native_tx = None
+        self._reuseport = bool(reuseport)
+        self._extra_ports = list(extra_ports)
+        # unary ScoreTransaction: the serving core's own FIFO when the engine has one (the
+        # Python MicroBatcher stays for engines without a core: golden / multi-shard CPU)
+        use_native = batching and getattr(engine, "core", None) is not None
+        if batching and not use_native:
             self.batcher = MicroBatcher(engine.score_tx_many_bytes, max_batch or cfg.gpu.max_batch,
                                         cfg.gpu.wait_us if wait_us is None else wait_us, workers=2,
                                         on_batch=lambda n: engine.metrics.batch_size.observe(n))
@@ -511,6 +579,9 @@ class RiskServer:
         self.loop = asyncio.new_event_loop()
         self._thread = threading.Thread(target=self.loop.run_forever, name="risk-grpc-loop", daemon=True)
         self._thread.start()
+        if use_native:
+            self.native_tx = NativeUnary(engine.core, self.loop, ok_fn=engine._native_ok, fallback=engine.score_tx_bytes,
+                                         pool=self.pool)
         self.server = None
         self.port = asyncio.run_coroutine_threadsafe(self._build(), self.loop).result(30)
 
@@ -518,11 +589,13 @@ class RiskServer:
         self.server = grpc.aio.server(interceptors=[AioInterceptor(self.engine.metrics)],
                                       options=[("grpc.max_receive_message_length", 64 << 20),
                                                ("grpc.max_send_message_length", 64 << 20),
-                                               ("grpc.so_reuseport", 0)])
+                                               ("grpc.so_reuseport", 1 if self._reuseport else 0)])
         inline = self.engine.kind != "gpu" and self.engine.group is None
-        self.server.add_generic_rpc_handlers([aio_risk_handler(self._servicer, self.pool, inline),
+        self.server.add_generic_rpc_handlers([aio_risk_handler(self._servicer, self.pool, inline, self.native_tx),
                                               aio_health_handler(self.health)] +
                                              [aio_reflection_handler(p) for p in RV.PKGS])
+        for p in self._extra_ports:
+            self.server.add_insecure_port(f"{self._host}:{p}")
         return self.server.add_insecure_port(f"{self._host}:{self._port_req}")
 
     def start(self) -> "RiskServer":
@@ -537,6 +610,68 @@ class RiskServer:
         self.loop.call_soon_threadsafe(self.loop.stop)
         self._thread.join(timeout=5)
         self.pool.shutdown(wait=False)
-        for b in (self.batcher, self.ltv_batcher, self.abuse_batcher):
+        for b in (self.batcher, self.ltv_batcher, self.abuse_batcher, self.native_tx):
             if b is not None:
                 b.close()
+
+
+class IngressServer:
+    """risk.v1 on a worker rank (>= 1) of a multi-GPU group: ScoreBatch and ScoreTransaction go
+    through THIS rank's serving core (its own parse / resolve / exchange steps: every rank
+    ingests), every other RPC is forwarded byte-for-byte to rank 0's internal port (the cold
+    ops are rank 0's control plane). Same port as rank 0 with SO_REUSEPORT by default, so one
+    address spreads connections over every rank of the node."""
+
+    def __init__(self, node, upstream: str, port: int, host: str = "0.0.0.0", reuseport: bool = True, metrics=None):
+        from ..obs.metrics import Metrics
+        self.node, self.upstream = node, upstream
+        self.metrics = metrics or Metrics()
+        self.health = HealthServicer()
+        self.health.set(P.SERVICE, "SERVING")
+        self._host, self._port_req, self._reuseport = host, port, reuseport
+        self.loop = asyncio.new_event_loop()
+        self._thread = threading.Thread(target=self.loop.run_forever, name="ingress-grpc-loop", daemon=True)
+        self._thread.start()
+        self.native_tx = NativeUnary(node.core, self.loop)
+        self.port = asyncio.run_coroutine_threadsafe(self._build(), self.loop).result(30)
+
+    async def _build(self) -> int:
+        opts = [("grpc.max_receive_message_length", 64 << 20), ("grpc.max_send_message_length", 64 << 20)]
+        self._up = grpc.aio.insecure_channel(self.upstream, options=opts)
+        self.server = grpc.aio.server(interceptors=[AioInterceptor(self.metrics)],
+                                      options=opts + [("grpc.so_reuseport", 1 if self._reuseport else 0)])
+        core, ntx = self.node.core, self.native_tx
+        pool = futures.ThreadPoolExecutor(max_workers=16, thread_name_prefix="ingress-rpc")
+        self._pool = pool
+        handlers = {}
+        for rpc, _, _ in P.METHODS:
+            if rpc == "ScoreBatch":
+                async def h(data, ctx, _c=core):
+                    loop = asyncio.get_running_loop()
+                    return await loop.run_in_executor(pool, _c.score_batch, data, int(time.time()),
+                                                      time.perf_counter_ns())
+            elif rpc == "ScoreTransaction":
+                async def h(data, ctx, _n=ntx):
+                    return await _n.call(data)
+            else:
+                fwd = self._up.unary_unary(P.method_path(rpc))
+
+                async def h(data, ctx, _f=fwd):  # cold RPC: rank 0 answers it
+                    return await _f(data, timeout=30)
+            handlers[rpc] = grpc.unary_unary_rpc_method_handler(h)
+        self.server.add_generic_rpc_handlers([grpc.method_handlers_generic_handler(P.SERVICE, handlers),
+                                              aio_health_handler(self.health)])
+        return self.server.add_insecure_port(f"{self._host}:{self._port_req}")
+
+    def start(self) -> "IngressServer":
+        asyncio.run_coroutine_threadsafe(self.server.start(), self.loop).result(30)
+        log.info("ingress grpc server listening", extra={"fields": dict(port=self.port, upstream=self.upstream)})
+        return self
+
+    def stop(self, grace: float = 5.0) -> None:
+        self.health.set(P.SERVICE, "NOT_SERVING")
+        asyncio.run_coroutine_threadsafe(self.server.stop(grace), self.loop).result(grace + 30)
+        self.loop.call_soon_threadsafe(self.loop.stop)
+        self._thread.join(timeout=5)
+        self.native_tx.close()
+        self._pool.shutdown(wait=False)

@@ -495,7 +495,7 @@ class GpuBackend:
 
         def drain():
             _t.sleep(0.01)
-            while core.late_steps() > 0:
+            while core.late_steps > 0:
                 _t.sleep(0.005)
             with self._lock:
                 self.quarantined.discard("core")

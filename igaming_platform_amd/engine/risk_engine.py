@@ -1000,19 +1000,24 @@ def make_abuse_gpu(cfg: Config, local, abuse_model):
 
 
 def serve_shard(cfg: Config, comm, backend: str = "gpu", capacity: Optional[int] = None, fraud_model=None,
-                abuse_model=None, capture: bool = True, ingress=None):
+                abuse_model=None, capture: bool = True, ingress=None, on_node=None):
     """Worker rank (>= 1) of an SPMD group: build the same local shard as rank 0 and serve
     its cold ops until rank 0 stops the group; ``ingress(node)``, when given, runs this rank's
     own traffic through its serving core on a thread meanwhile. Returns (ops served, rows
     this shard scored)."""
     from ..parallel.spmd import run_worker
     node = worker_node(cfg, comm, backend, capacity, fraud_model, capture)
+    started = on_node(node) if on_node is not None else None  # e.g. this rank's gRPC listener
     if ingress is not None:  # this rank's own traffic, beside the cold-op loop
         import threading
         th = threading.Thread(target=ingress, args=(node,), name=f"ingress-{comm.rank}", daemon=True)
         th.start()
     abuse_gpu = make_abuse_gpu(cfg, node.local, abuse_model if abuse_model is not None else cfg.abuse_model.path)
-    out = run_worker(comm, node.local, abuse_gpu, node.core)
+    try:
+        out = run_worker(comm, node.local, abuse_gpu, node.core)
+    finally:
+        if started is not None and hasattr(started, "stop"):
+            started.stop(1.0)
     if ingress is not None:
         th.join(60)
     return out

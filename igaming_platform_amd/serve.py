@@ -47,6 +47,9 @@ def main(argv=None) -> int:
     ap.add_argument("--snapshot-dir", default=os.environ.get("RISK_SNAPSHOT_DIR", ""))
     ap.add_argument("--snapshot-every-s", type=float, default=300.0)
     ap.add_argument("--no-batching", action="store_true")
+    ap.add_argument("--internal-port-offset", type=int, default=1000,
+                    help="multi-GPU: rank 0 also listens on grpc_port + this for the cold RPCs the other "
+                         "ranks forward")
     ap.add_argument("--audit-flush-every-s", type=float, default=2.0,
                     help="drain the risk_scores / ltv_predictions rings into AUDIT_DB this often")
     a = ap.parse_args(argv)
@@ -63,7 +66,8 @@ def main(argv=None) -> int:
     log = setup_logger(cfg.server.log_level)
     comm = None
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        # one process per GPU (torchrun): rank 0 serves the API, the others own their shards
+        # one process per GPU (torchrun): every rank serves the hot RPCs through its own core;
+        # rank 0 also runs the control plane and the cold RPCs
         import torch
         from .parallel.comm import init_from_env
         backend = a.backend if a.backend != "auto" else ("gpu" if torch.cuda.is_available() else "cpu")
@@ -74,9 +78,17 @@ def main(argv=None) -> int:
         # down); GPU shards move their rows over RCCL communicators of their own
         comm = init_from_env("gloo")
         if comm.rank != 0:
+            # every rank ingests: this rank's own risk.v1 listener (same port, SO_REUSEPORT)
+            # serves ScoreBatch / ScoreTransaction through its serving core and forwards the
+            # cold RPCs to rank 0's internal port
+            from .api.grpc_server import IngressServer
             from .engine.risk_engine import serve_shard
+
+            def listen(node):
+                return IngressServer(node, f"127.0.0.1:{cfg.server.grpc_port + a.internal_port_offset}",
+                                     port=cfg.server.grpc_port, host=a.host).start()
             n, rows = serve_shard(cfg, comm, backend=backend, capacity=a.accounts or None,
-                                  fraud_model=_fraud_model(a, cfg))
+                                  fraud_model=_fraud_model(a, cfg), on_node=listen)
             log.info("shard worker stopped", extra={"fields": dict(rank=comm.rank, ops=n, rows_scored=rows)})
             return 0
     from .api.grpc_server import RiskServer
@@ -85,7 +97,9 @@ def main(argv=None) -> int:
     if a.snapshot_dir and os.path.exists(os.path.join(a.snapshot_dir, "registry.json")):
         n = eng.restore(a.snapshot_dir)
         log.info("feature store restored", extra={"fields": dict(accounts=n, dir=a.snapshot_dir)})
-    gs = RiskServer(eng, port=cfg.server.grpc_port, host=a.host, batching=not a.no_batching).start()
+    multi = comm is not None and comm.world > 1
+    gs = RiskServer(eng, port=cfg.server.grpc_port, host=a.host, batching=not a.no_batching, reuseport=multi,
+                    extra_ports=[cfg.server.grpc_port + a.internal_port_offset] if multi else ()).start()
     hs = HttpServer(eng, port=cfg.server.http_port, host=a.host, timeout_s=cfg.server.http_timeout_s).start()
     stop = threading.Event()
 

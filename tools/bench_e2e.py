@@ -222,6 +222,104 @@ def _client(i, port, kind, accounts, batch, n_payloads, t_start, t_end, q):
     q.put((lat, errs, per))
 
 
+def _open_loop_client(i, port, accounts, rates, seconds, t_start, q):
+    """One load-generator process: open-loop unary ScoreTransaction over grpc.aio. Calls are
+    issued on a fixed schedule (rate / clients per second) whatever the server's pace, up to
+    4096 in flight; a call's latency counts from its SCHEDULED send time, so a server that
+    falls behind shows up as growing latency, not as a lower offered load."""
+    import asyncio
+    import grpc
+    from igaming_platform_amd.proto import risk_v1 as P
+    payloads = tx_payloads(accounts, 8192, seed=300 + i)
+
+    async def main():
+        ch = grpc.aio.insecure_channel(f"127.0.0.1:{port}")
+        call = ch.unary_unary(P.method_path("ScoreTransaction"))
+        for k in range(200):  # connect + warm
+            await call(payloads[k], timeout=30)
+        out = []
+        t_level = t_start
+        for rate in rates:
+            while time.time() < t_level:
+                await asyncio.sleep(0.001)
+            lat, errs, sent = [], [0], 0
+            sem = asyncio.Semaphore(4096)
+            loop = asyncio.get_running_loop()
+            t0 = loop.time()
+            interval = 1.0 / rate
+
+            async def one(t_sched, body):
+                try:
+                    await call(body, timeout=30)
+                    lat.append((loop.time() - t_sched) * 1e3)
+                except Exception:
+                    errs[0] += 1
+                finally:
+                    sem.release()
+            tasks = []
+            while True:
+                t_sched = t0 + sent * interval
+                if t_sched >= t0 + seconds:
+                    break
+                d = t_sched - loop.time()
+                if d > 0:
+                    await asyncio.sleep(d)
+                await sem.acquire()
+                tasks.append(asyncio.ensure_future(one(t_sched, payloads[sent % len(payloads)])))
+                sent += 1
+            await asyncio.gather(*tasks)
+            out.append((rate, sent, lat, errs[0], loop.time() - t0))
+            t_level += seconds + 2.0
+        await ch.close()
+        return out
+    q.put(asyncio.run(main()))
+
+
+def run_grpc_open_loop(a) -> dict:
+    """Unary ScoreTransaction throughput vs latency: offered load stepped through ``--rates``
+    (whole-node calls/s, split over ``--clients`` processes), open loop."""
+    import multiprocessing as mp
+    from igaming_platform_amd.api.grpc_server import RiskServer
+    eng = build_engine(a.accounts, a.batch, a.backend)
+    srv = RiskServer(eng, port=0, batching=True, workers=16).start()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    rates = [int(x) for x in a.rates.split(",")]
+    lead = 30.0
+    t_start = time.time() + lead
+    per = [r / a.clients for r in rates]
+    procs = [ctx.Process(target=_open_loop_client, args=(i, srv.port, a.accounts, per, a.seconds, t_start, q))
+             for i in range(a.clients)]
+    [p.start() for p in procs]
+    res = [q.get(timeout=lead + len(rates) * (a.seconds + 2) + 300) for _ in procs]
+    [p.join() for p in procs]
+    st = eng.core.stats(False) if getattr(eng, "core", None) is not None else None
+    srv.stop(0.5)
+    eng.close()
+    curve = []
+    for li, rate in enumerate(rates):
+        lat = [x for r in res for x in r[li][2]]
+        sent = sum(r[li][1] for r in res)
+        errs = sum(r[li][3] for r in res)
+        dur = max(r[li][4] for r in res)
+        curve.append(dict(offered_per_s=rate, achieved_per_s=round(len(lat) / dur, 1), calls=sent, errors=errs,
+                          p50_ms=round(float(np.percentile(lat, 50)), 3) if lat else None,
+                          p99_ms=round(float(np.percentile(lat, 99)), 3) if lat else None))
+    ok = [c for c in curve if c["p99_ms"] is not None and c["p99_ms"] < BASELINE_P99_MS and c["errors"] == 0
+          and c["achieved_per_s"] >= 0.95 * c["offered_per_s"]]
+    best = max(ok, key=lambda c: c["achieved_per_s"]) if ok else None
+    return dict(metric="unary risk.v1.ScoreTransaction over gRPC: throughput vs latency (open loop)",
+                value=best["achieved_per_s"] if best else 0.0, unit="calls/s",
+                value_is="highest offered rate answered in full with p99 < 50 ms", scope="grpc_unary_open_loop",
+                n_gpus=1 if a.backend == "gpu" else 0, data="synthetic (UUID ids, random-init cfg3 weights)",
+                config=dict(model="cfg3 GBDT(100,d7,128f)+MLP(32-256-1)", clients=a.clients, seconds_per_level=a.seconds,
+                            server="grpc.aio, raw-bytes handlers, native serving core FIFO (NativeUnary)",
+                            client="grpc.aio open loop, latency from the scheduled send time"),
+                curve=curve, best=best,
+                mean_rows_per_device_step=(round(st["rows"] / max(st["steps"], 1), 1) if st else None),
+                latency_baseline_ms=BASELINE_P99_MS)
+
+
 def run_grpc(a) -> dict:
     import multiprocessing as mp
     from igaming_platform_amd.api.grpc_server import RiskServer
@@ -278,9 +376,15 @@ def main(argv=None) -> int:
     ap.add_argument("--clients", type=int, default=8)
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--open-loop", action="store_true", help="--scope grpc --rpc tx: offered-load curve")
+    ap.add_argument("--rates", default="5000,10000,20000,40000,60000,80000",
+                    help="--open-loop: offered whole-node unary calls/s per level")
     a = ap.parse_args(argv)
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-    out = {"e2e": run_e2e, "grpc": run_grpc, "engine_batched": run_cold_engine}[a.scope](a)
+    if a.scope == "grpc" and a.rpc == "tx" and a.open_loop:
+        out = run_grpc_open_loop(a)
+    else:
+        out = {"e2e": run_e2e, "grpc": run_grpc, "engine_batched": run_cold_engine}[a.scope](a)
     line = json.dumps(out)
     print(line, flush=True)
     if a.json_out:
