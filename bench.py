@@ -67,7 +67,7 @@ def parse():
                          "owner-routed RCCL exchange steps for N > 1, GPU pipeline) -> response bytes with the "
                          "FeatureVector, every rank ingesting; engine_only: pre-resolved ReqRec rows into the "
                          "device pipeline (device-pipeline number); e2e / grpc: tools/bench_e2e.py")
-    ap.add_argument("--threads", type=int, default=8, help="serving scope: ingress threads per rank")
+    ap.add_argument("--threads", type=int, default=12, help="serving scope: ingress threads per rank")
     ap.add_argument("--requests", type=int, default=0, help="serving scope: transactions per ScoreBatch request "
                     "(default: the config's micro-batch)")
     ap.add_argument("--rpc", default="batch", choices=["batch", "tx"], help="--scope grpc: ScoreBatch or unary "
