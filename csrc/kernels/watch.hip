@@ -1,21 +1,18 @@
-// Batch watchdog: deadline waits on HIP events without polling, plus a bounded stall kernel
-// that the fault-injection tests use to make a real device batch overrun its deadline.
+// Batch watchdog: deadline waits on HIP events, plus a bounded stall kernel that the
+// fault-injection tests use to make a real device batch overrun its deadline.
 //
-// hipEventSynchronize has no timeout, so one watcher thread per EventWatch blocks in it (GIL
-// released, FIFO over the requests) and signals a condition variable; the caller sleeps on that
-// variable until the event completes or its deadline passes. A request that overran keeps being
-// waited on, so a late batch is still observed (engine/backends.py drains the quarantined slot).
-// The watcher's state is shared with the thread: destroying an EventWatch whose watcher is stuck
-// in a hung event detaches it instead of blocking (reference: the Go service bounds each score
-// with a context deadline, services/risk/internal/scoring/engine.go:279-282).
+// hipEventSynchronize has no timeout, so wait_for polls the caller's own event with
+// hipEventQuery (GIL released): a short spin, then a back-off of 20 us -> 1 ms sleeps. Every
+// wait is independent: a hung batch delays only the callers waiting on THAT batch (an earlier
+// design queued every request on one watcher thread blocked in hipEventSynchronize, so one
+// overrun cascaded into false timeouts for later batches), and nothing keeps a raw event after
+// wait_for returns, so the event's owner may go away at once (reference: the Go service bounds
+// each score with a context deadline, services/risk/internal/scoring/engine.go:279-282).
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 
+#include <atomic>
 #include <chrono>
-#include <condition_variable>
-#include <deque>
-#include <memory>
-#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -25,81 +22,45 @@ namespace py = pybind11;
 namespace igp {
 namespace {
 
-struct WatchReq {
-  hipEvent_t ev;
-  bool done = false;
-  hipError_t err = hipSuccess;
-};
-
-struct WatchState {
-  std::mutex mu;
-  std::condition_variable cv;       // new request / stop
-  std::condition_variable done_cv;  // a request completed
-  std::deque<std::shared_ptr<WatchReq>> q;
-  bool stop = false;
-  int64_t completed = 0;
-};
-
-void watch_loop(std::shared_ptr<WatchState> s) {
-  std::unique_lock<std::mutex> lk(s->mu);
-  for (;;) {
-    s->cv.wait(lk, [&] { return s->stop || !s->q.empty(); });
-    if (s->q.empty()) return;  // stop requested, nothing left to observe
-    auto r = s->q.front();
-    lk.unlock();
-    const hipError_t err = hipEventSynchronize(r->ev);
-    lk.lock();
-    r->err = err;
-    r->done = true;
-    s->q.pop_front();
-    ++s->completed;
-    s->done_cv.notify_all();
-    if (s->stop) return;
-  }
-}
-
 class EventWatch {
  public:
-  EventWatch() : s_(std::make_shared<WatchState>()) { std::thread(watch_loop, s_).detach(); }
-  ~EventWatch() {
-    {
-      std::lock_guard<std::mutex> lk(s_->mu);
-      s_->stop = true;
-    }
-    s_->cv.notify_all();
-  }
-
-  // true once the event completed; false when `timeout_ms` passed first (the watcher goes on
-  // waiting for it: pending() counts such requests until they finish)
+  // true once the event completed; false when `timeout_ms` passed first
   bool wait_for(uintptr_t event, double timeout_ms) {
     hipEvent_t ev = reinterpret_cast<hipEvent_t>(event);
-    const hipError_t q = hipEventQuery(ev);
+    hipError_t q = hipEventQuery(ev);
     if (q == hipSuccess) return true;
     if (q != hipErrorNotReady) throw std::runtime_error(std::string("EventWatch: ") + hipGetErrorString(q));
-    auto r = std::make_shared<WatchReq>();
-    r->ev = ev;
     py::gil_scoped_release nogil;
-    std::unique_lock<std::mutex> lk(s_->mu);
-    s_->q.push_back(r);
-    s_->cv.notify_all();
-    const bool ok = s_->done_cv.wait_for(lk, std::chrono::duration<double, std::milli>(timeout_ms),
-                                         [&] { return r->done; });
-    if (ok && r->err != hipSuccess)
-      throw std::runtime_error(std::string("EventWatch: batch failed: ") + hipGetErrorString(r->err));
-    return ok;
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double, std::milli>(timeout_ms);
+    int64_t sleep_us = 20;
+    for (int spin = 0;; ++spin) {
+      q = hipEventQuery(ev);
+      if (q == hipSuccess) {
+        completed_.fetch_add(1);
+        return true;
+      }
+      if (q != hipErrorNotReady) {
+        py::gil_scoped_acquire gil;
+        throw std::runtime_error(std::string("EventWatch: batch failed: ") + hipGetErrorString(q));
+      }
+      const auto now = std::chrono::steady_clock::now();
+      if (now >= t_end) {
+        timeouts_.fetch_add(1);
+        return false;
+      }
+      if (spin < 256) continue;
+      const auto left = std::chrono::duration_cast<std::chrono::microseconds>(t_end - now).count();
+      std::this_thread::sleep_for(std::chrono::microseconds(std::min<int64_t>(sleep_us, std::max<int64_t>(left, 1))));
+      sleep_us = std::min<int64_t>(sleep_us * 2, 1000);
+    }
   }
 
-  int pending() {
-    std::lock_guard<std::mutex> lk(s_->mu);
-    return (int)s_->q.size();
-  }
-  int64_t completed() {
-    std::lock_guard<std::mutex> lk(s_->mu);
-    return s_->completed;
-  }
+  // waits that gave up at their deadline / that saw their event complete
+  int64_t timeouts() const { return timeouts_.load(); }
+  int64_t completed() const { return completed_.load(); }
 
  private:
-  std::shared_ptr<WatchState> s_;
+  std::atomic<int64_t> timeouts_{0}, completed_{0};
 };
 
 // One wave that sleeps until `ticks` of the 100 MHz constant clock have passed (bounded: the
@@ -126,7 +87,7 @@ void register_watch(py::module_& m) {
   py::class_<EventWatch>(m, "EventWatch")
       .def(py::init<>())
       .def("wait_for", &EventWatch::wait_for, py::arg("event"), py::arg("timeout_ms"))
-      .def("pending", &EventWatch::pending)
+      .def("timeouts", &EventWatch::timeouts)
       .def("completed", &EventWatch::completed);
   m.def("stall", &stall, py::arg("stream"), py::arg("us"),
         "Enqueue a one-wave kernel that sleeps for `us` microseconds on `stream` (fault injection).");

@@ -103,10 +103,15 @@ def plan_importance(plan, width: int) -> Dict[str, float]:
     score = np.zeros(width, np.float64)
     trees = [s for s in plan.steps if s.kind == "tree"]
     if trees:
-        for t in trees:  # complete layout: padding nodes have +inf thresholds
-            nodes = np.asarray(t.nodes_np, np.float32).reshape(-1, 2)
-            real = np.isfinite(nodes[:, 0])
-            feat = nodes[:, 1].view(np.uint32)[real] & 0xFFFF
+        for t in trees:
+            if t.layout == "sparse":  # pointer layout: [N][4] int32 {meta, thr, left, right}, leaves mode 7
+                nodes = np.asarray(t.nodes_np, np.int32).reshape(-1, 4)
+                meta = nodes[:, 0].view(np.uint32)
+                feat = meta[((meta >> 16) & 7) != 7] & 0xFFFF
+            else:  # complete layout: [T][2^D-1][2] f32 {thr, meta}, padding nodes have +inf thresholds
+                nodes = np.asarray(t.nodes_np, np.float32).reshape(-1, 2)
+                real = np.isfinite(nodes[:, 0])
+                feat = nodes[:, 1].view(np.uint32)[real] & 0xFFFF
             score += np.bincount(feat.astype(np.int64), minlength=width)[:width]
     else:
         first = next((s for s in plan.steps if s.kind in ("dense", "head")), None)

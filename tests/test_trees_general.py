@@ -79,3 +79,33 @@ def test_validate_sparse_rejects_bad_layouts():
     bad.depth = 2                                                           # path longer than depth
     with pytest.raises(PlanError):
         validate_sparse(bad)
+
+
+@pytest.mark.parametrize("kind", ["gb_d16", "rf_unbalanced"])
+def test_feature_importance_of_sparse_layout_ensembles(kind):
+    """GetFeatureImportance (onnx_model.go:329-345) of deep / unbalanced ensembles that lower to
+    the pointer layout: split counts per input column, equal to the sklearn trees' own."""
+    from igaming_platform_amd.features.store_ops import input_names, plan_importance
+    from igaming_platform_amd.models.plan import compile_onnx
+    from igaming_platform_amd.native import native
+    from tests import tree_models as TM
+    m, _ = TM.build(kind)
+    plan = compile_onnx(native().OnnxModel.from_bytes(m.SerializeToString()))
+    assert any(s.kind == "tree" and s.layout == "sparse" for s in plan.steps)
+    imp = plan_importance(plan, TM.N_FEAT)
+    # sklearn's own split features
+    from sklearn.ensemble import GradientBoostingClassifier, RandomForestRegressor
+    X, y, _ = TM.data()
+    if kind == "gb_d16":
+        est = GradientBoostingClassifier(n_estimators=25, max_depth=16, learning_rate=0.2, random_state=0).fit(X, y > 0)
+        trees = [e[0].tree_ for e in est.estimators_]
+    else:
+        est = RandomForestRegressor(n_estimators=30, max_depth=None, max_features=0.5, random_state=0).fit(X, y)
+        trees = [e.tree_ for e in est.estimators_]
+    cnt = np.zeros(TM.N_FEAT)
+    for t in trees:
+        f = t.feature[t.feature >= 0]
+        cnt += np.bincount(f, minlength=TM.N_FEAT)
+    names = input_names(TM.N_FEAT)
+    got = np.array([imp.get(n, 0.0) for n in names])
+    np.testing.assert_allclose(got, cnt / cnt.sum(), rtol=1e-12)
