@@ -454,6 +454,7 @@ PYBIND11_MODULE(_hipk, m) {
       a.N[l] = geti(d, (p + "N").c_str());
       a.K[l] = geti(d, (p + "K").c_str());
       a.act[l] = geti(d, (p + "act").c_str());
+      a.W_lo[l] = ptr<const uint16_t*>(d, (p + "Wlo").c_str());
       if (!a.W[l]) throw std::runtime_error("mlp_chain: missing weights");
       if (a.N[l] < 64 || a.N[l] > 512 || a.N[l] % 64) throw std::runtime_error("mlp_chain: N must be 64..512, % 64");
       if (a.K[l] < 64 || a.K[l] > 512 || a.K[l] % 64) throw std::runtime_error("mlp_chain: K must be 64..512, % 64");
@@ -472,6 +473,12 @@ PYBIND11_MODULE(_hipk, m) {
     if (a.waves != 4 && a.waves != 8) throw std::runtime_error("mlp_chain: 4 or 8 waves");
     for (int l = 0; l < a.n_layers; ++l)
       if (a.N[l] % (16 * a.waves)) throw std::runtime_error("mlp_chain: N must be a multiple of 16 x waves");
+    a.split = geti(d, "split", 0);
+    if (a.split) {
+      for (int l = 0; l < a.n_layers; ++l)
+        if (!a.W_lo[l]) throw std::runtime_error("mlp_chain: split mode needs every layer's residual weights");
+      if (a.rows_per_block != 32) throw std::runtime_error("mlp_chain: split mode runs 32 rows per block");
+    }
     if (!a.w2) throw std::runtime_error("mlp_chain: head weights required");
     if (!a.slots && !a.X) throw std::runtime_error("mlp_chain: input");
     if (a.slots && !a.pf_tab) throw std::runtime_error("mlp_chain: LTV gather needs the profile table");

@@ -294,6 +294,8 @@ struct MlpChainArgs {
   float* ltv_out;           // [rows][6] K9 output (nullable; needs slots + pf_tab)
   int32_t rows_per_block;   // 16, 32 (default) or 64 rows per workgroup
   int32_t waves;            // 4 (default) or 8 (32 rows; each wave owns N/8 columns)
+  const uint16_t* W_lo[MC_MAX_LAYERS];  // split (f32-faithful) mode: bf16 residuals w - bf16(w)
+  int32_t split;            // 1: three-MFMA bf16 pairs (hi*hi + hi*lo + lo*hi)
 };
 void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st);
 

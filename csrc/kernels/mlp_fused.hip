@@ -17,6 +17,13 @@
 //
 // Numerics = the unfused bf16 path (gemm.hip / mlp_head): bf16 weights and activations, f32
 // accumulation, bf16 rounding of each hidden activation.
+//
+// SPLIT (the ONNX model's f32 contract, default for fp32 plans): every weight and activation is
+// carried as a pair of bf16 values hi + lo (hi = bf16(x), lo = bf16(x - hi), ~17 significant
+// bits), and each product runs as three MFMAs, hi*hi + hi*lo + lo*hi (lo*lo, ~2^-18 relative,
+// is dropped), accumulated in f32: f32-faithful to ~1e-5 relative at bf16 MFMA rates, where the
+// f32 MFMA (v_mfma_f32_16x16x4_f32) would run the chain ~16x slower. The hi and lo activation
+// tiles both live in LDS (4 x 32 x 520 bf16 = 133 KB).
 #include "common.h"
 #include "launch.h"
 #include "ltv.h"
@@ -42,9 +49,48 @@ __device__ __forceinline__ float mc_act(float v, int act) {
 // holding W[16 nt + (l & 15)][32 ks + 8 (l >> 4) .. +8], so each B-fragment load is one fully
 // coalesced 1 KB wave read (row-major W made it 16 half-used 128-B lines per instruction and
 // the texture path, not the MFMA, set the pace: 92 -> see profiles/NOTES.md).
-template <int NKS, int MT, int JT>
-__device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, const uint16_t* __restrict__ W, int K,
+template <int NKS, int MT, int JT, bool SPLIT>
+__device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, const uint16_t* __restrict__ Hlo,
+                                             const uint16_t* __restrict__ W, const uint16_t* __restrict__ Wlo, int K,
                                              int colw, int NT, int lane, mc_f32x4 (&acc)[MT][JT]) {
+  if constexpr (SPLIT) {
+    // hi*hi + hi*lo + lo*hi per k-step; both weight halves prefetched one k-step ahead
+    mc_bf16x8 fh[2][JT], fl[2][JT];
+    const int kq = 8 * (lane >> 4);
+    const size_t woff = ((size_t)(colw >> 4) * NKS) * 512 + lane * 8;
+    int jt[JT];
+#pragma unroll
+    for (int j = 0; j < JT; ++j) jt[j] = (j < NT ? j : NT - 1) * NKS;
+    auto load = [&](int ks, mc_bf16x8 (&dh)[JT], mc_bf16x8 (&dl)[JT]) {
+#pragma unroll
+      for (int j = 0; j < JT; ++j) {
+        dh[j] = *reinterpret_cast<const mc_bf16x8*>(W + woff + ((size_t)jt[j] + ks) * 512);
+        dl[j] = *reinterpret_cast<const mc_bf16x8*>(Wlo + woff + ((size_t)jt[j] + ks) * 512);
+      }
+    };
+    load(0, fh[0], fl[0]);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      if (ks + 1 < NKS) load(ks + 1, fh[(ks + 1) & 1], fl[(ks + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      mc_bf16x8 ah[MT], al[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int o = (16 * m + (lane & 15)) * MC_LDA + ks * 32 + kq;
+        ah[m] = *reinterpret_cast<const mc_bf16x8*>(&Hin[o]);
+        al[m] = *reinterpret_cast<const mc_bf16x8*>(&Hlo[o]);
+      }
+#pragma unroll
+      for (int j = 0; j < JT; ++j)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[m], fh[ks & 1][j], acc[m][j], 0, 0, 0);
+          acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[m], fl[ks & 1][j], acc[m][j], 0, 0, 0);
+          acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[m], fh[ks & 1][j], acc[m][j], 0, 0, 0);
+        }
+    }
+    return;
+  }
   mc_bf16x8 fb[3][JT];
   const int kq = 8 * (lane >> 4);
   const uint16_t* wt = W + ((size_t)(colw >> 4) * NKS) * 512 + lane * 8;  // this wave's first n-tile
@@ -77,13 +123,20 @@ __device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, c
   }
 }
 
-template <int MC_ROWS, int WAVES>
+// the bf16 pair of an f32 value: hi = bf16(x), lo = bf16(x - hi)
+__device__ __forceinline__ void mc_split(float x, uint16_t& hi, uint16_t& lo) {
+  hi = f32_to_bf16(x);
+  lo = f32_to_bf16(x - __uint_as_float((uint32_t)hi << 16));
+}
+
+template <int MC_ROWS, int WAVES, bool SPLIT>
 __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
   constexpr int MT = MC_ROWS / 16;            // 16-row MFMA tiles per wave
   constexpr int THREADS = 64 * WAVES;
   constexpr int PARTS = THREADS / MC_ROWS;    // staging threads per row
   constexpr int JT = 32 / WAVES;              // 16-column tiles per wave at N = 512
-  __shared__ __attribute__((aligned(16))) uint16_t H[2][MC_ROWS * MC_LDA];
+  // [0..1]: hi tiles (ping-pong); SPLIT: [2..3] the matching lo tiles
+  __shared__ __attribute__((aligned(16))) uint16_t H[SPLIT ? 4 : 2][MC_ROWS * MC_LDA];
   __shared__ float part[WAVES][MC_ROWS];
   __shared__ float mlv[MC_ROWS];
   __shared__ float pfl[MC_ROWS][P_NCOLS];  // raw profile rows for the K9 epilogue
@@ -126,7 +179,11 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
           if (a.ltv_out) pfl[r][c] = x;
           x = copysignf(log1pf(fabsf(x)), x);  // [sign*log1p|profile| (25) | extended features]
         }
-        H[0][r * MC_LDA + c] = f32_to_bf16(x);
+        if constexpr (SPLIT) {
+          mc_split(x, H[0][r * MC_LDA + c], H[2][r * MC_LDA + c]);
+        } else {
+          H[0][r * MC_LDA + c] = f32_to_bf16(x);
+        }
       }
     }
   }
@@ -142,21 +199,24 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
 #pragma unroll
       for (int j = 0; j < JT; ++j) acc[m][j] = mc_f32x4{0.f, 0.f, 0.f, 0.f};
     const uint16_t* Hin = H[cur];
+    const uint16_t* Hlo = H[SPLIT ? 2 + cur : cur];
+    const uint16_t* Wl = SPLIT ? a.W_lo[l] : nullptr;
     switch (K >> 5) {  // K-steps of 32 (the host allows 2..16)
-      case 2: mc_layer_mma<2, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
-      case 4: mc_layer_mma<4, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
-      case 6: mc_layer_mma<6, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
-      case 8: mc_layer_mma<8, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
-      case 10: mc_layer_mma<10, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
-      case 12: mc_layer_mma<12, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
-      case 14: mc_layer_mma<14, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
-      default: mc_layer_mma<16, MT, JT>(Hin, a.W[l], K, colw, NT, lane, acc); break;
+      case 2: mc_layer_mma<2, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      case 4: mc_layer_mma<4, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      case 6: mc_layer_mma<6, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      case 8: mc_layer_mma<8, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      case 10: mc_layer_mma<10, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      case 12: mc_layer_mma<12, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      case 14: mc_layer_mma<14, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      default: mc_layer_mma<16, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
     }
     const float* bias = a.bias[l];
     const int act = a.act[l];
     if (l + 1 < a.n_layers) {
       // hidden layer: bias + act -> bf16 -> the next layer's LDS tile
       uint16_t* Hout = H[cur ^ 1];
+      uint16_t* Hout_lo = H[SPLIT ? 2 + (cur ^ 1) : (cur ^ 1)];
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -165,8 +225,12 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
           const int col = colw + j * 16 + (lane & 15);
           const float b = bias ? bias[col] : 0.f;
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            Hout[(m * 16 + 4 * (lane >> 4) + q) * MC_LDA + col] = f32_to_bf16(mc_act(acc[m][j][q] + b, act));
+          for (int q = 0; q < 4; ++q) {
+            const int o = (m * 16 + 4 * (lane >> 4) + q) * MC_LDA + col;
+            const float v = mc_act(acc[m][j][q] + b, act);
+            if constexpr (SPLIT) mc_split(v, Hout[o], Hout_lo[o]);
+            else Hout[o] = f32_to_bf16(v);
+          }
         }
       __syncthreads();
       cur ^= 1;
@@ -216,14 +280,21 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
 void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
   const int r = a.rows_per_block;
+  if (a.split) {  // f32-faithful: 32 rows per block (hi + lo tiles fill the LDS)
+    if (a.waves == 8)
+      IGP_LAUNCH((mlp_chain_kernel<32, 8, true>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
+    else
+      IGP_LAUNCH((mlp_chain_kernel<32, 4, true>), dim3((a.n_rows + 31) / 32), dim3(256), 0, st, a);
+    return;
+  }
   if (a.waves == 8)
-    IGP_LAUNCH((mlp_chain_kernel<32, 8>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
+    IGP_LAUNCH((mlp_chain_kernel<32, 8, false>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
   else if (r == 64)
-    IGP_LAUNCH((mlp_chain_kernel<64, 4>), dim3((a.n_rows + 63) / 64), dim3(256), 0, st, a);
+    IGP_LAUNCH((mlp_chain_kernel<64, 4, false>), dim3((a.n_rows + 63) / 64), dim3(256), 0, st, a);
   else if (r == 16)
-    IGP_LAUNCH((mlp_chain_kernel<16, 4>), dim3((a.n_rows + 15) / 16), dim3(256), 0, st, a);
+    IGP_LAUNCH((mlp_chain_kernel<16, 4, false>), dim3((a.n_rows + 15) / 16), dim3(256), 0, st, a);
   else
-    IGP_LAUNCH((mlp_chain_kernel<32, 4>), dim3((a.n_rows + 31) / 32), dim3(256), 0, st, a);
+    IGP_LAUNCH((mlp_chain_kernel<32, 4, false>), dim3((a.n_rows + 31) / 32), dim3(256), 0, st, a);
 }
 
 }  // namespace igp

@@ -42,6 +42,9 @@ class InvalidArgument(ValueError):
     pass
 
 
+HOT = {"ScoreTransaction", "ScoreBatch"}  # the scoring RPCs (fast metrics path)
+
+
 # ============================================================================ interceptors
 def _wrap_unary(h, fn_wrap):
     if h is None or h.unary_unary is None:
@@ -363,7 +366,8 @@ def _with_deps(fname: str):
 class AioInterceptor(grpc.aio.ServerInterceptor):
     """The reference's interceptor chain (main.go:303-353) as one async wrapper: recovery
     (exceptions -> INTERNAL "internal server error"), metrics, logging (OK at debug, errors
-    at info)."""
+    at info). The scoring RPCs' successful calls only bump plain counters
+    (``Metrics.fast_rpc``): no prometheus label lookup, lock or histogram search per call."""
 
     def __init__(self, metrics):
         self.m = metrics
@@ -375,6 +379,19 @@ class AioInterceptor(grpc.aio.ServerInterceptor):
         inner, method = h.unary_unary, details.method
         short = method.rsplit("/", 1)[-1]
         m = self.m
+        fast = m.fast_rpc(short) if short in HOT else None
+
+        def account(code: str, dt: float) -> None:
+            if code == "OK" and fast is not None:
+                fast.observe(dt)
+                return
+            m.requests.labels(method=short, code=code).inc()
+            m.latency.labels(method=short).observe(dt)
+            if code != "OK":
+                log.info("grpc request failed", extra={"fields": dict(method=method, code=code,
+                                                                      duration_ms=round(dt * 1e3, 3))})
+            elif log.isEnabledFor(10):
+                log.debug("grpc request", extra={"fields": dict(method=method, duration_ms=round(dt * 1e3, 3))})
 
         async def call(req, ctx):
             t0 = time.perf_counter()
@@ -393,14 +410,7 @@ class AioInterceptor(grpc.aio.ServerInterceptor):
                 log.error("panic recovered", exc_info=True, extra={"fields": dict(method=method)})
                 await ctx.abort(grpc.StatusCode.INTERNAL, "internal server error")
             finally:
-                dt = time.perf_counter() - t0
-                m.requests.labels(method=short, code=code).inc()
-                m.latency.labels(method=short).observe(dt)
-                if code != "OK":
-                    log.info("grpc request failed", extra={"fields": dict(method=method, code=code,
-                                                                          duration_ms=round(dt * 1e3, 3))})
-                elif log.isEnabledFor(10):
-                    log.debug("grpc request", extra={"fields": dict(method=method, duration_ms=round(dt * 1e3, 3))})
+                account(code, time.perf_counter() - t0)
 
         return grpc.unary_unary_rpc_method_handler(call, request_deserializer=h.request_deserializer,
                                                    response_serializer=h.response_serializer)

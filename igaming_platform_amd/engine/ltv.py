@@ -125,9 +125,13 @@ class LtvGpu:
             plan is not None and any(st.kind == "gru" for st in plan.steps))
         self._pull_copy = os.environ.get("IGP_PULL_COPY", "0") == "1"
         self.chain = None
-        if (plan is not None and plan.precision == "bf16" and os.environ.get("IGP_MLP_FUSED", "1") != "0"
+        # the fused chain (mlp_fused.hip): bf16 plans as bf16 MFMA, fp32 plans in its split
+        # mode (bf16 hi/lo pairs, three MFMAs per product: f32-faithful); IGP_MLP_SPLIT=0 sends
+        # fp32 plans to the per-layer f32 MFMA kernels instead
+        split_ok = os.environ.get("IGP_MLP_SPLIT", "1") != "0"
+        if (plan is not None and (plan.precision == "bf16" or split_ok) and os.environ.get("IGP_MLP_FUSED", "1") != "0"
                 and K.MlpChainPack.eligible(plan.steps)):
-            self.chain = K.MlpChainPack(plan.steps, self.device)
+            self.chain = K.MlpChainPack(plan.steps, self.device, split=plan.precision != "bf16")
         dev = self.device
         self.capacity = int(capacity)
         self.pf_tab = torch.zeros((self.capacity, N_COLS), dtype=torch.float32, device=dev)

@@ -29,6 +29,7 @@ class Metrics:
         self._n = self._ml_high = self._bl = 0
         # native serving cores count their own decisions (engine/serving.py core_metrics)
         self.sources = []
+        self._fast = {}
         r.register(_DecisionCollector(self))
         self.batch_size = Histogram("gpu_batch_size", "rows per device micro-batch",
                                     buckets=(1, 8, 64, 256, 1024, 4096, 8192), registry=r)
@@ -41,6 +42,13 @@ class Metrics:
                                      "audit rows dropped from the ring before a flush", registry=r)
         self.fallbacks = Counter("risk_fallback_total", "rows scored by the CPU fallback", ["reason"], registry=r)
         self.accounts = Gauge("risk_accounts", "accounts resident in the feature store", ["gpu"], registry=r)
+
+    def fast_rpc(self, method: str) -> "_FastRpc":
+        """risk_requests_total{OK} / risk_latency_seconds children of a hot RPC, resolved once."""
+        f = self._fast.get(method)
+        if f is None:
+            f = self._fast[method] = _FastRpc(self, method)
+        return f
 
     def observe_results(self, res: np.ndarray, feats=None) -> None:
         """Decision accounting from ResultRec rows (uint32 [n,2])."""
@@ -106,3 +114,16 @@ class _DecisionCollector:
         c = CounterMetricFamily("risk_blacklist_hits", "requests matching the blacklist")
         c.add_metric([], bl)
         yield c
+
+
+
+class _FastRpc:
+    """OK calls of one hot RPC through pre-resolved metric children (no label lookup per call)."""
+
+    def __init__(self, m: "Metrics", method: str):
+        self._count = m.requests.labels(method=method, code="OK")
+        self._lat = m.latency.labels(method=method)
+
+    def observe(self, dt: float) -> None:
+        self._count.inc()
+        self._lat.observe(dt)

@@ -556,19 +556,26 @@ class MlpChainPack:
             return False
         return all(ks[i] == widths[i - 1] for i in range(1, len(ks)))
 
-    def __init__(self, steps, device):
+    def __init__(self, steps, device, split: bool = False):
+        """``split``: f32-faithful mode - each weight also as its bf16 residual w - bf16(w), and
+        the kernel runs three MFMAs per product on (hi, lo) pairs (mlp_fused.hip SPLIT)."""
         import numpy as np
         if not self.eligible(steps):
             raise ValueError("mlp_chain: the plan is not a dense chain the fused kernel covers")
         dev = as_device(device)
+        self.split = bool(split)
         self.layers = []
         for s in steps:
-            w = s.w1_np if s.kind == "head" else s.w_np
+            w = np.asarray(s.w1_np if s.kind == "head" else s.w_np, np.float32)
             b = s.b1_np if s.kind == "head" else s.b_np
             n, k = w.shape
             kp = -(-k // 64) * 64
             # MFMA B-fragment order (pack_fragments): one 1 KB contiguous wave load per 16x32 tile
-            self.layers.append(dict(W=pack_fragments(w, kp).to(dev),
+            lo = None
+            if self.split:
+                hi = torch.from_numpy(np.ascontiguousarray(w)).to(torch.bfloat16).float().numpy()
+                lo = pack_fragments(w - hi, kp).to(dev)
+            self.layers.append(dict(W=pack_fragments(w, kp).to(dev), Wlo=lo,
                                     b=None if b is None else torch.from_numpy(np.ascontiguousarray(b, np.float32)).to(dev),
                                     N=n, K=kp, act=ACT[s.act1 if s.kind == "head" else s.act]))
         head = steps[-1]
@@ -616,6 +623,10 @@ def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, s
         raise ValueError("mlp_chain: nothing to write")
     for i, l in enumerate(pk.layers):
         d[f"l{i}_W"] = _need(l["W"], "W", torch.bfloat16, l["N"] * l["K"], dev)
+        if pk.split:
+            d[f"l{i}_Wlo"] = _need(l["Wlo"], "Wlo", torch.bfloat16, l["N"] * l["K"], dev)
         d[f"l{i}_b"] = _opt(l["b"], "b", dtype=torch.float32, min_numel=l["N"], device=dev)
         d[f"l{i}_N"], d[f"l{i}_K"], d[f"l{i}_act"] = l["N"], l["K"], l["act"]
+    if pk.split:
+        d.update(split=1, rows_per_block=32)
     _mod().mlp_chain(d, _stream())

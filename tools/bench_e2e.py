@@ -242,7 +242,7 @@ def _open_loop_client(i, port, accounts, rates, seconds, t_start, q):
         for rate in rates:
             while time.time() < t_level:
                 await asyncio.sleep(0.001)
-            lat, errs, sent = [], [0], 0
+            lat, errs, sent, kinds = [], [0], 0, {}
             sem = asyncio.Semaphore(4096)
             loop = asyncio.get_running_loop()
             t0 = loop.time()
@@ -252,8 +252,10 @@ def _open_loop_client(i, port, accounts, rates, seconds, t_start, q):
                 try:
                     await call(body, timeout=30)
                     lat.append((loop.time() - t_sched) * 1e3)
-                except Exception:
+                except Exception as e:
                     errs[0] += 1
+                    k = str(getattr(e, "code", lambda: type(e).__name__)())
+                    kinds[k] = kinds.get(k, 0) + 1
                 finally:
                     sem.release()
             tasks = []
@@ -268,7 +270,7 @@ def _open_loop_client(i, port, accounts, rates, seconds, t_start, q):
                 tasks.append(asyncio.ensure_future(one(t_sched, payloads[sent % len(payloads)])))
                 sent += 1
             await asyncio.gather(*tasks)
-            out.append((rate, sent, lat, errs[0], loop.time() - t0))
+            out.append((rate, sent, lat, errs[0], loop.time() - t0, kinds))
             t_level += seconds + 2.0
         await ch.close()
         return out
@@ -302,7 +304,12 @@ def run_grpc_open_loop(a) -> dict:
         sent = sum(r[li][1] for r in res)
         errs = sum(r[li][3] for r in res)
         dur = max(r[li][4] for r in res)
+        kinds = {}
+        for r in res:
+            for k, v in r[li][5].items():
+                kinds[k] = kinds.get(k, 0) + v
         curve.append(dict(offered_per_s=rate, achieved_per_s=round(len(lat) / dur, 1), calls=sent, errors=errs,
+                          error_kinds=kinds,
                           p50_ms=round(float(np.percentile(lat, 50)), 3) if lat else None,
                           p99_ms=round(float(np.percentile(lat, 99)), 3) if lat else None))
     ok = [c for c in curve if c["p99_ms"] is not None and c["p99_ms"] < BASELINE_P99_MS and c["errors"] == 0
@@ -377,7 +384,7 @@ def main(argv=None) -> int:
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--json-out", default="")
     ap.add_argument("--open-loop", action="store_true", help="--scope grpc --rpc tx: offered-load curve")
-    ap.add_argument("--rates", default="5000,10000,20000,40000,60000,80000",
+    ap.add_argument("--rates", default="2000,5000,8000,12000,16000,24000",
                     help="--open-loop: offered whole-node unary calls/s per level")
     a = ap.parse_args(argv)
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
