@@ -55,8 +55,8 @@ def parse():
                          "|| model(i-2) (measured slower on ROCm 7.2 than the default three-stream pipeline: "
                          "~35 us between consecutive multi-branch graph launches)")
     ap.add_argument("--numerics", default="auto", choices=["auto", "fp32", "bf16"],
-                    help="dense-layer numerics: fp32 = the ONNX model's f32 contract (default for the fraud "
-                         "scorers), bf16 = bf16 MFMA with f32 accumulate (default for cfg4 / cfg5)")
+                    help="dense-layer numerics: fp32 = the ONNX model's f32 contract (default; f32 MFMA heads, "
+                         "split bf16x3 MFMA for the cfg4 chain and the cfg5 GRU), bf16 = bf16 MFMA with f32 accumulate")
     ap.add_argument("--dp-mode", default="exchange", choices=["exchange", "replicas"],
                     help="N > 1: exchange = every rank ingests 8192 rows/step spread over all owners and "
                          "the owner-routed RCCL exchange (the serving path, engine/dp.py) moves each row to "
@@ -74,19 +74,19 @@ def parse():
                     "ScoreTransaction through the micro-batcher")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
-    if a.numerics == "auto":
-        a.numerics = "bf16" if a.config in ("cfg4", "cfg5") else "fp32"
-    if a.config == "cfg5" and a.numerics != "bf16":
-        ap.error("cfg5's GRU kernel runs bf16 weights (f32 state / accumulate) only")
+    if a.numerics == "auto":  # the ONNX models' f32 contract everywhere (cfg4 / cfg5: split MFMA)
+        a.numerics = "fp32"
     return a
 
 
 def numerics_desc(a) -> str:
+    split = ("f32-faithful: bf16 hi/lo pairs of every weight and activation, three bf16 MFMAs per product "
+             "(hi*hi + hi*lo + lo*hi), fp32 accumulate")
     if a.config == "cfg5":
-        return "bf16 MFMA weights/activations, fp32 accumulate and state"
+        return (split + " and fp32 hidden state" if a.numerics == "fp32"
+                else "bf16 MFMA weights/activations, fp32 accumulate and state")
     if a.config == "cfg4":
-        return ("bf16 MFMA weights/activations, fp32 accumulate" if a.numerics == "bf16"
-                else "fp32 MFMA (v_mfma_f32_16x16x4_f32) end to end")
+        return split if a.numerics == "fp32" else "bf16 MFMA weights/activations, fp32 accumulate"
     dense = ("fp32 MFMA (v_mfma_f32_16x16x4_f32) MLP" if a.numerics == "fp32"
              else "bf16 MFMA MLP (fp32 accumulate)")
     return f"fp32 features+trees, {dense}, fp64 ensemble"

@@ -390,6 +390,8 @@ PYBIND11_MODULE(_hipk, m) {
       a.layer[l].bias = ptr<const float*>(d, (p + "bias").c_str());
       a.layer[l].kx_pad = geti(d, (p + "kx_pad").c_str());
       a.layer[l].lbr = geti(d, (p + "lbr").c_str());
+      a.layer[l].W_lo = ptr<const uint16_t*>(d, (p + "Wlo").c_str());
+      a.layer[l].R_lo = ptr<const uint16_t*>(d, (p + "Rlo").c_str());
       if (!a.layer[l].W || !a.layer[l].R || !a.layer[l].bias) throw std::runtime_error("gru: missing layer weights");
     }
     a.H = geti(d, "H");
@@ -419,6 +421,12 @@ PYBIND11_MODULE(_hipk, m) {
     a.ws_part = ptr<float*>(d, "ws_part");
     a.ws_err = ptr<int32_t*>(d, "ws_err");
     a.ws_trace = ptr<int64_t*>(d, "ws_trace");
+    a.split = geti(d, "split");
+    if (a.split) {
+      for (int l = 0; l < a.n_layers; ++l)
+        if (!a.layer[l].W_lo || !a.layer[l].R_lo) throw std::runtime_error("gru: split mode needs residual weights");
+      a.ws = 0;
+    }
     if (a.tile_rows != 0 && a.tile_rows != 16 && a.tile_rows != 32) throw std::runtime_error("gru: tile_rows 16|32");
     if (a.H != 64 && a.H != 128 && a.H != 256) throw std::runtime_error("gru: H must be 64, 128 or 256");
     if (a.layer[0].kx_pad != 32 && a.layer[0].kx_pad != 64) throw std::runtime_error("gru: input dim must pad to 32 or 64");

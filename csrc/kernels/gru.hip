@@ -190,6 +190,133 @@ __device__ __forceinline__ void layer_step(const WFrag& gW, const WFrag& gR, con
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// f32-faithful split mode (the ONNX model's f32 contract, default for fp32 plans): weights and
+// activations are bf16 pairs hi + lo (hi = bf16(x), lo = bf16(x - hi)), each product runs as
+// three MFMAs (lo*hi + hi*lo + hi*hi; lo*lo ~2^-18 relative is dropped) into f32 accumulators,
+// and the hidden state stays f32 in registers. ~1e-5 relative to fp32 at 3x the bf16 MFMA
+// count; the f32 MFMA (v_mfma_f32_16x16x4_f32) would be ~16x slower than bf16.
+__device__ __forceinline__ void gru_split(float x, uint16_t& hi, uint16_t& lo) {
+  hi = f32_to_bf16(x);
+  lo = f32_to_bf16(x - __uint_as_float((uint32_t)hi << 16));
+}
+
+#define GRU_MMA3(acc, ah, al, bh, bl)                                      \
+  do {                                                                     \
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);   \
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);   \
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);   \
+  } while (0)
+
+template <int RT, int KSX, int KSH, int LBR, int NW>
+__device__ __forceinline__ void layer_step_x3(const WFrag& gW, const WFrag& gWl, const WFrag& gR, const WFrag& gRl,
+                                              const float* bias, const uint16_t* in, const uint16_t* inl, int in_stride,
+                                              const uint16_t* hprev, const uint16_t* hprevl, uint16_t* hnext,
+                                              uint16_t* hnextl, uint16_t* rb, uint16_t* rbl,
+                                              float (&hs)[KSH * 2 / NW][RT][4], int lane, int wave) {
+  constexpr int HT = KSH * 2;
+  constexpr int HTW = HT / NW;
+  constexpr int H = KSH * 32;
+  constexpr int HS = H + GRU_PAD;
+  const int arow = lane & 15, akof = 8 * (lane >> 4);
+  const int crow = (lane >> 4) * 4, ccol = lane & 15;
+  float zk[LBR ? 1 : HTW][RT][4];
+  float xk[LBR ? 1 : HTW][RT][4];
+#pragma unroll
+  for (int i = 0; i < HTW; ++i) {
+    const int ht = wave + NW * i;
+    f32x4 az[RT], ar[RT], ax[RT], ah[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) az[rt] = ar[rt] = ax[rt] = ah[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KSX; ++ks) {  // x_t . W^T
+      const bf16x8 bz = ld_frag(gW, ht, KSX, ks), bzl = ld_frag(gWl, ht, KSX, ks);
+      const bf16x8 br = ld_frag(gW, HT + ht, KSX, ks), brl = ld_frag(gWl, HT + ht, KSX, ks);
+      const bf16x8 bh = ld_frag(gW, 2 * HT + ht, KSX, ks), bhl = ld_frag(gWl, 2 * HT + ht, KSX, ks);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const bf16x8 a = lds_frag(in, in_stride, rt * 16 + arow, ks * 32 + akof);
+        const bf16x8 al = lds_frag(inl, in_stride, rt * 16 + arow, ks * 32 + akof);
+        GRU_MMA3(az[rt], a, al, bz, bzl);
+        GRU_MMA3(ar[rt], a, al, br, brl);
+        GRU_MMA3(ax[rt], a, al, bh, bhl);
+      }
+    }
+#pragma unroll 2
+    for (int ks = 0; ks < KSH; ++ks) {  // h_{t-1} . R^T
+      const bf16x8 bz = ld_frag(gR, ht, KSH, ks), bzl = ld_frag(gRl, ht, KSH, ks);
+      const bf16x8 br = ld_frag(gR, HT + ht, KSH, ks), brl = ld_frag(gRl, HT + ht, KSH, ks);
+      bf16x8 bh, bhl;
+      if constexpr (LBR != 0) {
+        bh = ld_frag(gR, 2 * HT + ht, KSH, ks);
+        bhl = ld_frag(gRl, 2 * HT + ht, KSH, ks);
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const bf16x8 a = lds_frag(hprev, HS, rt * 16 + arow, ks * 32 + akof);
+        const bf16x8 al = lds_frag(hprevl, HS, rt * 16 + arow, ks * 32 + akof);
+        GRU_MMA3(az[rt], a, al, bz, bzl);
+        GRU_MMA3(ar[rt], a, al, br, brl);
+        if constexpr (LBR != 0) GRU_MMA3(ah[rt], a, al, bh, bhl);
+      }
+    }
+    const int j = ht * 16 + ccol;
+    const float bz_ = bias[j] + bias[3 * H + j];
+    const float br_ = bias[H + j] + bias[4 * H + j];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = sig_(az[rt][r] + bz_);
+        const float rr = sig_(ar[rt][r] + br_);
+        const int o = (rt * 16 + crow + r) * HS + j;
+        if constexpr (LBR != 0) {
+          const float hh = tanh_(ax[rt][r] + bias[2 * H + j] + rr * (ah[rt][r] + bias[5 * H + j]));
+          const float h = (1.f - z) * hh + z * hs[i][rt][r];
+          hs[i][rt][r] = h;
+          gru_split(h, hnext[o], hnextl[o]);
+        } else {
+          zk[i][rt][r] = z;
+          xk[i][rt][r] = ax[rt][r];
+          gru_split(rr * hs[i][rt][r], rb[o], rbl[o]);
+        }
+      }
+  }
+  if constexpr (LBR == 0) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < HTW; ++i) {
+      const int ht = wave + NW * i;
+      f32x4 ah[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) ah[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+      for (int ks = 0; ks < KSH; ++ks) {
+        const bf16x8 bh = ld_frag(gR, 2 * HT + ht, KSH, ks), bhl = ld_frag(gRl, 2 * HT + ht, KSH, ks);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const bf16x8 a = lds_frag(rb, HS, rt * 16 + arow, ks * 32 + akof);
+          const bf16x8 al = lds_frag(rbl, HS, rt * 16 + arow, ks * 32 + akof);
+          GRU_MMA3(ah[rt], a, al, bh, bhl);
+        }
+      }
+      const int j = ht * 16 + ccol;
+      const float bxh = bias[2 * H + j], bhh = bias[5 * H + j];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float hh = tanh_(xk[i][rt][r] + bxh + ah[rt][r] + bhh);
+          const float z = zk[i][rt][r];
+          const float h = (1.f - z) * hh + z * hs[i][rt][r];
+          hs[i][rt][r] = h;
+          const int o = (rt * 16 + crow + r) * HS + j;
+          gru_split(h, hnext[o], hnextl[o]);
+        }
+    }
+  }
+}
+
 }  // namespace
 
 template <int RT, int KSH, int NW>
@@ -348,6 +475,143 @@ __global__ void __launch_bounds__(NW * 64) gru_kernel(GruArgs a) {
     emit_outputs<RT, KSH, NW>(a, hs0, red, row0, n_live, lane, wave, tid);
 #undef HB
 #undef XB
+}
+
+// Batch-parallel recurrence in split mode (layer_step_x3): the same structure as gru_kernel,
+// with every LDS activation tile doubled into hi / lo halves (16 rows per workgroup keeps it
+// within the LDS: ~96 KB at H = 256).
+template <int RT, int KSX, int KSH, int LBR, int NW>
+__global__ void __launch_bounds__(NW * 64) gru_x3_kernel(GruArgs a) {
+  constexpr int M = RT * 16;
+  constexpr int H = KSH * 32;
+  constexpr int HS = H + GRU_PAD;
+  constexpr int XS = KSX * 32 + GRU_PAD;
+  constexpr int HTW = KSH * 2 / NW;
+  constexpr int NT = NW * 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n_live = a.m_ptr ? min(*a.m_ptr, a.n_rows) : a.n_rows;
+  const int row0 = blockIdx.x * M;
+  if (row0 >= n_live) return;
+  const size_t wx = (size_t)3 * H * KSX * 32, wh = (size_t)3 * H * H;
+  const WFrag w0 = wfrag(a.layer[0].W, wx, lane), w0l = wfrag(a.layer[0].W_lo, wx, lane);
+  const WFrag r0 = wfrag(a.layer[0].R, wh, lane), r0l = wfrag(a.layer[0].R_lo, wh, lane);
+  const WFrag w1 = wfrag(a.layer[1].W, wh, lane), w1l = wfrag(a.layer[1].W_lo, wh, lane);
+  const WFrag r1 = wfrag(a.layer[1].R, wh, lane), r1l = wfrag(a.layer[1].R_lo, wh, lane);
+
+  // LDS: hb[2 halves][layer][pingpong][M][HS] | xb[2 halves][pingpong][M][XS] | rb[2 halves][M][HS]
+  //      | bias[2][6H] | red[NW][M]
+  uint16_t* const hb = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* const xb = hb + 8 * M * HS;
+  uint16_t* const rb = xb + 4 * M * XS;
+  float* const bias = reinterpret_cast<float*>(rb + 2 * M * HS);
+  float* const red = bias + 12 * H;
+#define HB(half, l, b) (hb + ((half) * 4 + (l) * 2 + (b)) * (M * HS))
+#define XB(half, b) (xb + ((half) * 2 + (b)) * (M * XS))
+  {
+    uint32_t* z = reinterpret_cast<uint32_t*>(smem);
+    const int words = (8 * M * HS + 4 * M * XS) / 2;
+    for (int i = tid; i < words; i += NT) z[i] = 0u;
+  }
+  for (int i = tid; i < 6 * H; i += NT) bias[i] = a.layer[0].bias[i];
+  if (a.n_layers == 2)
+    for (int i = tid; i < 6 * H; i += NT) bias[6 * H + i] = a.layer[1].bias[i];
+
+  const int I = a.I;
+  const int chunks = I >> 3;
+  const int my_rr = tid / max(chunks, 1), my_c = tid - my_rr * max(chunks, 1);
+  const bool stager = chunks > 0 && my_rr < M;
+  const int grow = row0 + my_rr;
+  int slot = -1, head = 0, valid_from = a.T;
+  if (stager && grow < n_live) {
+    if (a.mode == 1) {
+      slot = a.slots[grow];
+      if (slot >= 0) {
+        const AcctRT r = a.rt[slot];
+        head = r.ev_head;
+        valid_from = a.T - min(r.ev_count, a.T);
+      }
+    } else {
+      valid_from = 0;
+    }
+  }
+  // x_t as (hi, lo) bf16 halves: the event ring holds bf16 values (lo = 0); dense f32 input splits
+  auto load_x = [&](int t, uint4& hi, uint4& lo) {
+    hi = lo = make_uint4(0, 0, 0, 0);
+    if (!stager || t < valid_from || t >= a.T) return;
+    if (a.mode == 1) {
+      int idx = (head - a.T + t) % a.ev_ring;
+      if (idx < 0) idx += a.ev_ring;
+      hi = *reinterpret_cast<const uint4*>(a.ev + (((size_t)slot * a.ev_ring + idx) * I + my_c * 8));
+    } else {
+      const float* src = a.X + (((size_t)t * a.x_rows + grow) * I + my_c * 8);
+      uint16_t h8[8], l8[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gru_split(src[e], h8[e], l8[e]);
+      hi = make_uint4(h8[0] | (uint32_t)h8[1] << 16, h8[2] | (uint32_t)h8[3] << 16, h8[4] | (uint32_t)h8[5] << 16,
+                      h8[6] | (uint32_t)h8[7] << 16);
+      lo = make_uint4(l8[0] | (uint32_t)l8[1] << 16, l8[2] | (uint32_t)l8[3] << 16, l8[4] | (uint32_t)l8[5] << 16,
+                      l8[6] | (uint32_t)l8[7] << 16);
+    }
+  };
+  __syncthreads();
+  if (stager) {
+    uint4 h, l;
+    load_x(0, h, l);
+    *reinterpret_cast<uint4*>(XB(0, 0) + my_rr * XS + my_c * 8) = h;
+    *reinterpret_cast<uint4*>(XB(1, 0) + my_rr * XS + my_c * 8) = l;
+  }
+  float hs0[HTW][RT][4], hs1[HTW][RT][4];
+#pragma unroll
+  for (int i = 0; i < HTW; ++i)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hs0[i][rt][r] = hs1[i][rt][r] = 0.f;
+  __syncthreads();
+
+  for (int t = 0; t < a.T; ++t) {
+    const int pb = t & 1, nb = pb ^ 1;
+    uint4 xh, xl;
+    load_x(t + 1, xh, xl);
+    layer_step_x3<RT, KSX, KSH, LBR, NW>(w0, w0l, r0, r0l, bias, XB(0, pb), XB(1, pb), XS, HB(0, 0, pb), HB(1, 0, pb),
+                                         HB(0, 0, nb), HB(1, 0, nb), rb, rb + M * HS, hs0, lane, wave);
+    __syncthreads();
+    if (a.n_layers == 2) {
+      layer_step_x3<RT, KSH, KSH, LBR, NW>(w1, w1l, r1, r1l, bias + 6 * H, HB(0, 0, nb), HB(1, 0, nb), HS,
+                                           HB(0, 1, pb), HB(1, 1, pb), HB(0, 1, nb), HB(1, 1, nb), rb, rb + M * HS,
+                                           hs1, lane, wave);
+    }
+    if (stager && t + 1 < a.T) {
+      *reinterpret_cast<uint4*>(XB(0, nb) + my_rr * XS + my_c * 8) = xh;
+      *reinterpret_cast<uint4*>(XB(1, nb) + my_rr * XS + my_c * 8) = xl;
+    }
+    __syncthreads();
+  }
+  if (a.n_layers == 2)
+    emit_outputs<RT, KSH, NW>(a, hs1, red, row0, n_live, lane, wave, tid);
+  else
+    emit_outputs<RT, KSH, NW>(a, hs0, red, row0, n_live, lane, wave, tid);
+#undef HB
+#undef XB
+}
+
+static size_t gru_x3_lds_bytes(int RT, int KSX, int KSH, int NW) {
+  const int M = RT * 16, H = KSH * 32, HS = H + GRU_PAD, XS = KSX * 32 + GRU_PAD;
+  return (size_t)8 * M * HS * 2 + (size_t)4 * M * XS * 2 + (size_t)2 * M * HS * 2 + (size_t)2 * 6 * H * 4 +
+         (size_t)NW * M * 4;
+}
+
+template <int KSX, int KSH>
+static void launch_gru_x3(const GruArgs& a, hipStream_t st) {
+  constexpr int NW = KSH >= 4 ? 8 : 4;
+  const dim3 grid((a.n_rows + 15) / 16), block(NW * 64);
+  const size_t lds = gru_x3_lds_bytes(1, KSX, KSH, NW);
+  if (a.layer[0].lbr)
+    IGP_LAUNCH((gru_x3_kernel<1, KSX, KSH, 1, NW>), grid, block, lds, st, a);
+  else
+    IGP_LAUNCH((gru_x3_kernel<1, KSX, KSH, 0, NW>), grid, block, lds, st, a);
 }
 
 // Two stacked layers, layer-pipelined: waves [0, NW/2) run layer 1 at step t while waves
@@ -571,6 +835,15 @@ static void launch_gru_h(const GruArgs& a, hipStream_t st) {
 
 void launch_gru(const GruArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
+  if (a.split) {  // f32-faithful: the batch-parallel split kernel, 16 rows per workgroup
+    const int ksx = a.layer[0].kx_pad / 32;
+    switch (a.H) {
+      case 64: if (ksx == 1) launch_gru_x3<1, 2>(a, st); else launch_gru_x3<2, 2>(a, st); break;
+      case 128: if (ksx == 1) launch_gru_x3<1, 4>(a, st); else launch_gru_x3<2, 4>(a, st); break;
+      default: if (ksx == 1) launch_gru_x3<1, 8>(a, st); else launch_gru_x3<2, 8>(a, st); break;
+    }
+    return;
+  }
   // weight-stationary clusters while all of them fit one wave of the chip (1 workgroup per CU);
   // beyond that the batch-parallel kernel at 32 rows per workgroup streams weights at a better
   // rate than two waves of clusters (tools/gru_bench.py: 8192 rows 5.6 M vs 4.5 M seq/s)

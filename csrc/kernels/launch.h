@@ -207,6 +207,8 @@ struct GruLayerArgs {
   const float* bias;        // [6H]: Wb z,r,h | Rb z,r,h
   int32_t kx_pad;
   int32_t lbr;              // linear_before_reset
+  const uint16_t* W_lo;     // split mode: bf16 residuals (w - bf16(w)), same fragment order
+  const uint16_t* R_lo;
 };
 struct GruArgs {
   GruLayerArgs layer[2];
@@ -238,6 +240,7 @@ struct GruArgs {
   float* ws_part;           // [ws_clusters][8][128] head partials
   int32_t* ws_err;          // [1] set when a cluster was not co-resident (bounded wait expired)
   int64_t* ws_trace;        // [64][6] phase timestamps of workgroup 0 (nullable; tools/gru_bench.py)
+  int32_t split;            // 1: f32-faithful bf16 hi/lo pairs, three MFMAs per product (gru.hip x3)
 };
 void launch_gru(const GruArgs& a, hipStream_t st);
 bool gru_ws_eligible(const GruArgs& a);

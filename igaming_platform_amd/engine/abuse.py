@@ -96,7 +96,8 @@ class AbuseGpu:
         steps = plan.steps
         n = sum(1 for s in steps if s.kind == "gru")
         head = steps[n] if n < len(steps) else None
-        self.gp = K.GruPack(steps[:n], head, self.device)
+        # fp32 plans (the ONNX f32 contract, default): the f32-faithful split GRU; bf16 plans: bf16 MFMA
+        self.gp = K.GruPack(steps[:n], head, self.device, split=getattr(plan, "precision", "fp32") != "bf16")
         if self.gp.head_w is None:
             raise ValueError("abuse model must end in an N=1 head (probability)")
         self.T = steps[0].seq or store.ev.shape[1]

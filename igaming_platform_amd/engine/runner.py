@@ -61,7 +61,7 @@ class DeviceModel:
             head = steps[n] if n < len(steps) and steps[n].kind == "dense" and steps[n].n == 1 else None
             if n == 0 or n + (head is not None) != len(steps):
                 raise ValueError("sequence model must be GRU layers followed by at most an N=1 head")
-            self.gru = K.GruPack(steps[:n], head, self.device)
+            self.gru = K.GruPack(steps[:n], head, self.device, split=plan.precision != "bf16")
             self.gru_steps = len(steps)
             self.seq_len = steps[0].seq
         self.out = self.step_out[-1] if self.step_out else None

@@ -412,7 +412,9 @@ def pack_fragments(w, k_pad: int) -> torch.Tensor:
 class GruPack:
     """Device weights of a 1-2 layer GRU chain (+ optional N=1 head) for the K4 kernel."""
 
-    def __init__(self, layers, head=None, device="cuda"):
+    def __init__(self, layers, head=None, device="cuda", split: bool = False):
+        """``split``: f32-faithful mode (gru.hip layer_step_x3): each weight also as its bf16
+        residual w - bf16(w); the kernel runs three MFMAs per product on (hi, lo) pairs."""
         import numpy as np
         if not 1 <= len(layers) <= 2:
             raise ValueError("gru: 1 or 2 stacked layers are lowered")
@@ -429,10 +431,17 @@ class GruPack:
         self.waves = 0
         self.lbr = int(layers[0].linear_before_reset)
         dev = as_device(device)
+        self.split = bool(split)
         self.layers = []
+
+        def residual(w):
+            w = np.ascontiguousarray(w, np.float32)
+            return w - torch.from_numpy(w).to(torch.bfloat16).float().numpy()
         for i, l in enumerate(layers):
             kx = H if i == 1 else (32 if l.in_dim <= 32 else 64)
             self.layers.append(dict(W=pack_fragments(l.w_np, kx).to(dev), R=pack_fragments(l.r_np, H).to(dev),
+                                    Wlo=pack_fragments(residual(l.w_np), kx).to(dev) if self.split else None,
+                                    Rlo=pack_fragments(residual(l.r_np), H).to(dev) if self.split else None,
                                     bias=torch.from_numpy(np.ascontiguousarray(l.b_np, np.float32)).to(dev),
                                     kx_pad=kx, lbr=self.lbr))
         self.head_w = self.head_b = None
@@ -445,7 +454,8 @@ class GruPack:
             self.head_act = ACT[head.act]
         self.device = dev
         # weight-stationary cluster kernel (csrc/kernels/gru_ws.hip) for 2 x 256, lbr = 1, I <= 32
-        self.ws_ok = self.n_layers == 2 and H == 256 and self.lbr == 1 and self.I <= 32
+        # (bf16 only: its stationary weights fill the register file)
+        self.ws_ok = self.n_layers == 2 and H == 256 and self.lbr == 1 and self.I <= 32 and not self.split
         self._ws = None
         self._ws_old = []  # superseded workspaces stay alive: captured graphs keep their pointers
         self.ws_err = torch.zeros(1, dtype=torch.int32, device=dev) if self.ws_ok else None
@@ -506,9 +516,14 @@ def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh
         d.update(ws=int(ws), ws_clusters=w["clusters"], ws_sync=w["sync"].data_ptr(), ws_x=w["x"].data_ptr(),
                  ws_part=w["part"].data_ptr(), ws_err=gp.ws_err.data_ptr(),
                  ws_trace=_opt(ws_trace, "ws_trace", dtype=torch.int64, min_numel=64 * 8 + 4, device=dev))
+    if gp.split:
+        d["split"] = 1
     for i, l in enumerate(gp.layers):
         d[f"l{i}_W"] = _need(l["W"], "W", torch.bfloat16, device=dev)
         d[f"l{i}_R"] = _need(l["R"], "R", torch.bfloat16, device=dev)
+        if gp.split:
+            d[f"l{i}_Wlo"] = _need(l["Wlo"], "Wlo", torch.bfloat16, device=dev)
+            d[f"l{i}_Rlo"] = _need(l["Rlo"], "Rlo", torch.bfloat16, device=dev)
         d[f"l{i}_bias"] = _need(l["bias"], "bias", torch.float32, 6 * gp.H, dev)
         d[f"l{i}_kx_pad"] = l["kx_pad"]
         d[f"l{i}_lbr"] = l["lbr"]

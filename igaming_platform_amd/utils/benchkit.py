@@ -168,7 +168,8 @@ def build_model(config: str, batch: int, accounts: int, dev, rank: int = 0, dept
         rt[:, head_col] = torch.randint(0, fc.event_ring, (accounts,), generator=g, device=dev, dtype=torch.int32)
         rt[:, cnt_col] = fc.event_ring
         m = N.OnnxModel.from_bytes(builders.build("gru", seq=100, in_dim=16, hidden=256).SerializeToString())
-        runner = AbuseGpu(store, to_device(compile_onnx(m), dev), buckets=[B], use_graphs=use_graphs, depth=depth)
+        runner = AbuseGpu(store, to_device(compile_onnx(m), dev, precision), buckets=[B], use_graphs=use_graphs,
+                          depth=depth)
     torch.cuda.synchronize(dev)
     runner.capture()
     pool = [rng.integers(0, accounts, B).astype(np.int32) for _ in range(n_pool)]
