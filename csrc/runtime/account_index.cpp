@@ -235,4 +235,12 @@ std::string AccountIndex::id_of(int32_t slot) const {
   return std::string(p + 4, len);
 }
 
+std::string_view AccountIndex::id_view(int32_t slot) const {
+  if (slot < 0 || slot >= size()) return {};
+  const char* p = arena_ + size_t(slot_off_[slot]) * 8;
+  uint32_t len;
+  std::memcpy(&len, p, 4);
+  return std::string_view(p + 4, len);
+}
+
 }  // namespace igp

@@ -47,6 +47,8 @@ class AccountIndex {
   int64_t capacity() const { return hdr_->cap; }
   int64_t collisions() const { return hdr_->collisions.load(std::memory_order_relaxed); }
   std::string id_of(int32_t slot) const;
+  // the id bytes in the arena (no copy); empty for an out-of-range slot
+  std::string_view id_view(int32_t slot) const;
   bool shared() const { return region_.shared_mapping(); }
   void unlink_shared() { region_.unlink(); }
 

@@ -8,6 +8,7 @@
 #include <memory>
 
 #include "account_index.h"
+#include "audit.h"
 #include "cpu_device.h"
 #include "cpu_scorer.h"
 #include "serve_core.h"
@@ -564,6 +565,53 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("rows_scored", &ShmXchgDevice::rows_scored)
       .def("unlink_shared", &ShmXchgDevice::unlink_shared);
 
+  py::class_<AuditRing, std::shared_ptr<AuditRing>>(m, "AuditRing")
+      .def(py::init<int64_t>(), py::arg("capacity"))
+      .def("pending", &AuditRing::pending)
+      .def("append", [](AuditRing& a, py::array_t<uint32_t, py::array::c_style> res,
+                        py::array_t<int32_t, py::array::c_style> slots, int owner, int64_t t_ms, int version) {
+        const size_t n = size_t(slots.size());
+        if (res.ndim() != 2 || size_t(res.shape(0)) != n || res.shape(1) != 2)
+          throw std::runtime_error("AuditRing.append: res must be uint32[n,2] for n slots");
+        const ResultRec* r = reinterpret_cast<const ResultRec*>(res.data());
+        const int32_t* s = slots.data();
+        py::gil_scoped_release rel;
+        a.append(r, s, 1, owner, n, t_ms, uint16_t(version));
+      }, py::arg("res"), py::arg("slots"), py::arg("owner"), py::arg("t_ms"), py::arg("version"))
+      .def_property_readonly("evicted", &AuditRing::evicted)
+      .def_property_readonly("appended", &AuditRing::appended)
+      .def("flush_sqlite", [](AuditRing& a, const std::string& path, const std::string& schema,
+                              std::vector<std::shared_ptr<AccountIndex>> idx) {
+        py::gil_scoped_release rel;
+        return a.flush_sqlite(path, schema, idx);
+      })
+      .def_property_readonly("capacity", &AuditRing::capacity)
+      .def("flush_segment", [](AuditRing& a, const std::string& dir, const std::string& tag,
+                               std::vector<std::shared_ptr<AccountIndex>> idx) {
+        py::gil_scoped_release rel;
+        return a.flush_segment(dir, tag, idx);
+      })
+      .def("peek", [](const AuditRing& a, int64_t max) {
+        auto v = a.peek(max);
+        py::dict d;
+        std::vector<int64_t> t(v.size());
+        std::vector<int32_t> sl(v.size()), ow(v.size()), ver(v.size());
+        std::vector<uint32_t> pk(v.size());
+        std::vector<float> ml(v.size());
+        for (size_t i = 0; i < v.size(); ++i) {
+          t[i] = v[i].t_ms; sl[i] = v[i].slot; ow[i] = v[i].owner; ver[i] = v[i].model_version;
+          pk[i] = v[i].packed; ml[i] = v[i].ml;
+        }
+        d["t_ms"] = vec_np(t); d["slot"] = vec_np(sl); d["owner"] = vec_np(ow); d["model_version"] = vec_np(ver);
+        d["packed"] = vec_np(pk); d["ml"] = vec_np(ml);
+        return d;
+      }, py::arg("max") = 1 << 20);
+
+  m.def("audit_load_segment", [](const std::string& seg, const std::string& db, const std::string& schema) {
+    py::gil_scoped_release rel;
+    return audit_load_segment(seg, db, schema);
+  }, py::arg("segment"), py::arg("db"), py::arg("schema"));
+
   py::class_<PyServe, std::shared_ptr<PyServe>>(m, "ServeCore")
       .def(py::init([](std::vector<std::shared_ptr<AccountIndex>> idx, py::object dev, int rank,
                        std::shared_ptr<StepClock> clock, int max_wait_us, int64_t timeout_us, int finishers,
@@ -665,6 +713,8 @@ PYBIND11_MODULE(_native, m) {
       .def("stop", [](PyServe& s) { py::gil_scoped_release rel; s.core->stop(); })
       .def("abort", [](PyServe& s) { py::gil_scoped_release rel; s.core->abort(); })
       .def("set_links", [](PyServe& s, std::shared_ptr<LinkIndex> l) { s.core->set_links(std::move(l)); })
+      .def("set_audit", [](PyServe& s, std::shared_ptr<AuditRing> a) { s.core->set_audit(std::move(a)); })
+      .def("set_model_version", [](PyServe& s, int v) { s.core->set_model_version(v); })
       .def("pending_items", [](PyServe& s) { return s.core->pending_items(); })
       .def_property_readonly("issued", [](const PyServe& s) { return s.core->issued(); })
       .def_property_readonly("seq", [](const PyServe& s) { return s.core->seq(); })

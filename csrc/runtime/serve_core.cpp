@@ -584,6 +584,7 @@ void ServeCore::finish_seg(const Step& st, const Seg& s) {
       if (f) std::memcpy(it->feat + s.item_pos, f + s.dev_pos, size_t(s.count) * kFeatBytes);
     }
     record_decisions(r, s.count);
+    audit_seg(r, it->rows.data() + s.item_pos, 0, s.count);
     return;
   }
   const size_t W = kResBytes + (st.wf ? kFeatBytes : 0);
@@ -597,6 +598,15 @@ void ServeCore::finish_seg(const Step& st, const Seg& s) {
     if (it->feat && f) it->feat[dst] = f[i];
   }
   record_decisions(r, s.count);
+  audit_seg(r, it->rows.data() + s.item_pos, s.owner, s.count);
+}
+
+void ServeCore::audit_seg(const ResultRec* r, const ReqRec* rows, int owner, int n) {
+  AuditRing* a = audit_.get();
+  if (!a || n <= 0) return;
+  const int64_t t_ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                           std::chrono::system_clock::now().time_since_epoch()).count();
+  a->append(r, &rows[0].slot, sizeof(ReqRec) / sizeof(int32_t), owner, size_t(n), t_ms, model_ver_.load());
 }
 
 // decision counters of /metrics (obs/metrics.py): score deciles, actions, ML high-risk and

@@ -38,6 +38,7 @@
 #include "../include/device_ops.h"
 #include "../include/records.h"
 #include "account_index.h"
+#include "audit.h"
 #include "link_index.h"
 #include "shm.h"
 #include "wire.h"
@@ -128,6 +129,10 @@ class ServeCore {
   void abort();
 
   void set_links(std::shared_ptr<LinkIndex> links) { links_ = std::move(links); }
+  // risk_scores audit: every result row the core hands back is appended to the ring, stamped
+  // with the model version in force (set_model_version on every hot reload)
+  void set_audit(std::shared_ptr<AuditRing> ring) { audit_ = std::move(ring); }
+  void set_model_version(int v) { model_ver_.store(uint16_t(v)); }
   ServeStats stats(bool reset);
   int64_t issued() const { return issued_.load(); }
   int32_t seq() const { return seq_; }
@@ -170,6 +175,7 @@ class ServeCore {
   void resolve_rows(std::vector<wire::TxRow>& rows, Item* it);
   void converge(int64_t gen);
   void record_decisions(const ResultRec* r, int n);
+  void audit_seg(const ResultRec* r, const ReqRec* rows, int owner, int n);
 
   std::vector<std::shared_ptr<AccountIndex>> idx_;
   const IgpDeviceOps* dev_;
@@ -179,6 +185,8 @@ class ServeCore {
   std::shared_ptr<StepClock> clock_;
   Options opt_;
   std::shared_ptr<LinkIndex> links_;
+  std::shared_ptr<AuditRing> audit_;
+  std::atomic<uint16_t> model_ver_{1};
 
   // queue + slots (q_mu_)
   std::mutex q_mu_;

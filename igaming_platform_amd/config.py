@@ -157,6 +157,9 @@ class ServerConfig:
     shutdown_grace_s: float = 30.0
     http_timeout_s: float = 10.0
     audit_db: str = ""           # SQLite file the risk_scores audit ring drains into ("" = in-memory only)
+    audit_ring_rows: int = 1 << 24  # native audit ring of the serving core (24 B/row: 384 MiB at 16.7M rows)
+    audit_mode: str = "auto"     # auto | sqlite | segments (engine/audit.py)
+    audit_direct_max: int = 262144  # auto: larger native backlogs go through segment files
 
 
 @dataclass
@@ -212,6 +215,8 @@ class Config:
         s.http_port = geti("HTTP_PORT", s.http_port)
         s.log_level = env.get("LOG_LEVEL", s.log_level) or s.log_level
         s.audit_db = env.get("AUDIT_DB", s.audit_db)
+        s.audit_ring_rows = int(env.get("AUDIT_RING_ROWS", s.audit_ring_rows))
+        s.audit_mode = env.get("AUDIT_MODE", s.audit_mode)
         sc = self.scoring
         sc.block_threshold = geti("BLOCK_THRESHOLD", sc.block_threshold)
         sc.review_threshold = geti("REVIEW_THRESHOLD", sc.review_threshold)

@@ -97,7 +97,7 @@ class CpuBackend:
         self.store.ip_intel = {int(k): int(x) for k, x in zip(t.keys.view(np.uint64), t.vals) if int(k) != 0}
         self._tables_version = v
 
-    def swap_model(self, fm, mkind: str) -> None:
+    def swap_model(self, fm, mkind: str, version: Optional[int] = None) -> None:
         """Model hot-reload: the next batch scores with the new model (feature state kept)."""
         spec = cpu_model_spec(self.cfg, fm, mkind)
         with self._lock:
@@ -319,10 +319,11 @@ class GpuBackend:
         self.core = core
         self._core_pool = cf.ThreadPoolExecutor(max_workers=8, thread_name_prefix=f"core-{self.device}")
 
-    def swap_model(self, fm, mkind: str) -> None:
+    def swap_model(self, fm, mkind: str, version: Optional[int] = None) -> None:
         """Model hot-reload: drain the shard, build a scorer for the new plan on the same HBM
         feature store (new graphs, same store, batch sequence and metrics carried over so the
-        dedup region ring stays consistent), swap it in. Scoring resumes with the new model."""
+        dedup region ring stays consistent), swap it in. Scoring resumes with the new model;
+        ``version`` becomes the serving core's audit stamp while nothing is in flight."""
         from ..models.plan import compile_onnx, to_device
         torch = self.torch
         plan = to_device(compile_onnx(fm), self.device, self.cfg.fraud_model.precision) if mkind == "onnx" else None
@@ -347,6 +348,8 @@ class GpuBackend:
                 self.scorer = sc
                 if core is not None:
                     core.set_device(self.native_device())
+                    if version is not None:
+                        core.set_model_version(int(version))
             finally:
                 for lk in self._slot_locks:
                     lk.release()
@@ -666,14 +669,24 @@ class NativeCpuBackend:
         d = getattr(self, "_device", None)
         return int(d.rows_scored) if d is not None and hasattr(d, "rows_scored") else 0
 
-    def swap_model(self, fm, mkind: str) -> None:
-        """Model hot-reload: the C++ scorer's executor is replaced between batches."""
+    def swap_model(self, fm, mkind: str, version: Optional[int] = None) -> None:
+        """Model hot-reload: the C++ scorer's executor is replaced between batches (with the
+        serving core paused, so ``version`` stamps exactly the rows of the new model)."""
         spec = cpu_model_spec(self.cfg, fm, mkind)
+        core = self.core
         with self._lock:
-            self.model = spec["model"]
-            self.sc.set_model(spec["executor"] if self.model == "plan" else None, spec["input_name"],
-                              spec["output_name"], spec["ml_col"])
-            self.refresh_config()
+            if core is not None:
+                core.pause()
+            try:
+                self.model = spec["model"]
+                self.sc.set_model(spec["executor"] if self.model == "plan" else None, spec["input_name"],
+                                  spec["output_name"], spec["ml_col"])
+                self.refresh_config()
+                if core is not None and version is not None:
+                    core.set_model_version(int(version))
+            finally:
+                if core is not None:
+                    core.resume()
 
     def refresh_config(self, scoring=None) -> None:
         from ..layouts import MODEL_HEURISTIC, MODEL_NONE, MODEL_OUTPUT, score_cfg

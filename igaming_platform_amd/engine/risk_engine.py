@@ -104,7 +104,7 @@ class RiskEngine:
         self._lock = threading.RLock()
         self.scoring = cfg.scoring
         # risk_scores / ltv_predictions audit (engine/audit.py): on when AUDIT_DB is configured
-        self.auditlog = AuditLog(enabled=bool(cfg.server.audit_db))
+        self.auditlog = make_auditlog(cfg, "r0")
         from ..features.store_ops import KVStore
         self.kv = KVStore()  # IncrementCounter / SetFeature / GetFeature keys (redis_store.go:206-227)
 
@@ -146,6 +146,8 @@ class RiskEngine:
             self.local = local
             self.core = node.core
             self.core.set_links(self.links)
+            self.auditlog = node.audit  # the node's core writes its native ring
+            self._audit_evicted_seen = 0
             from . import serving
             self.metrics.sources.append(lambda c=node.core: serving.core_metrics(c))
             abuse_gpu = make_abuse_gpu(cfg, local, self._abuse_am)
@@ -247,13 +249,19 @@ class RiskEngine:
         core.set_links(self.links)
         be.attach_core(core)
         self.core = core
+        self._attach_audit(core, indexes if indexes is not None else [self.registry.index[0]])
         self.metrics.sources.append(lambda c=core: serving.core_metrics(c))
 
+    def _attach_audit(self, core, indexes) -> None:
+        """risk_scores audit of the core's rows: its native ring (csrc/runtime/audit.cpp),
+        drained by :meth:`flush_audit` next to the Python rings."""
+        attach_audit_ring(self.auditlog, self.cfg, core, indexes, int(self.model_version))
+        self._audit_evicted_seen = 0
+
     def _native_ok(self) -> bool:
-        """Whether a request may take the all-native path (the Python path keeps the audit
-        ring, fault injection and the degraded-shard fallback)."""
-        return (self.core is not None and all(self.healthy) and not self.auditlog.enabled
-                and not self.faults.any_active())
+        """Whether a request may take the all-native path (the Python path keeps fault
+        injection and the degraded-shard fallback)."""
+        return self.core is not None and all(self.healthy) and not self.faults.any_active()
 
     def _cpu_backend(self, mkind, fm, kind: str = "cpu", capacity: int = 1):
         if kind == "cpu":
@@ -287,13 +295,15 @@ class RiskEngine:
                     feats = feats.view(FEATREC).reshape(-1) if feats is not None else None
                 except RuntimeError as e:  # a peer missed the step deadline: the group failed
                     raise g.fail(e) from e
+                audited = self.auditlog.native is not None  # the core's ring has these rows
             except GroupFailure:
                 # the batch died with the group (some rows may have been applied on their
                 # shards): answer all of it from the stateless fallback; later batches go to
                 # the local and re-homed shards (_group_failed)
                 res, feats = self._fallback_score(req, now, want_features, "group_failed")
+                audited = False
             self._add_links(rb, slots, owners)
-            self._observe(rb, res, version)
+            self._observe(rb, res, version, audited)
             return res, feats, slots, owners
         res = np.zeros((n, 2), np.uint32)
         feats = np.zeros(n, FEATREC) if want_features else None
@@ -304,8 +314,11 @@ class RiskEngine:
             if len(sub) == 0:
                 continue
             pend.append((o, sel, sub, self._submit(o, sub, now, want_features)))
+        # rows the serving core scored are in its native audit ring already (world 1 only)
+        audited = self.auditlog.native is not None
         for o, sel, sub, p in pend:
-            r, f = self._collect(o, sub, now, want_features, p)
+            r, f, via_core = self._collect(o, sub, now, want_features, p)
+            audited = audited and via_core
             if sel is None:
                 res[:], feats = r, f
             else:
@@ -313,7 +326,7 @@ class RiskEngine:
                 if want_features:
                     feats[sel] = f
         self._add_links(rb, slots, owners)
-        self._observe(rb, res, version)
+        self._observe(rb, res, version, audited)
         return res, feats, slots, owners
 
     def _add_links(self, rb, slots: np.ndarray, owners: np.ndarray) -> None:
@@ -333,13 +346,14 @@ class RiskEngine:
         for f in pend:
             f.result()
 
-    def _observe(self, rb, res: np.ndarray, version: int) -> None:
+    def _observe(self, rb, res: np.ndarray, version: int, audited: bool = False) -> None:
         """Metrics + the risk_scores audit entry of one scored batch (every scoring entry point
         goes through :meth:`_score_parsed`, so ScoreWithExplanation and /debug/score are logged
-        too). ``version`` is the model version the batch was scored with."""
+        too). ``version`` is the model version the batch was scored with; ``audited``: the
+        serving core's native ring holds the batch already."""
         self.metrics.observe_results(res)
         self.metrics.batch_size.observe(len(res))
-        if self.auditlog.enabled:
+        if self.auditlog.enabled and not audited:
             before = self.auditlog.evicted_rows
             self.auditlog.record_scores(rb.account_id, res, version)
             if self.auditlog.evicted_rows != before:
@@ -367,11 +381,14 @@ class RiskEngine:
             be, h = h
             try:
                 if be.kind == "gpu":
-                    return be.collect(h, timeout_s=self.cfg.gpu.batch_timeout_ms / 1e3)
-                return be.collect(h)
+                    r, f = be.collect(h, timeout_s=self.cfg.gpu.batch_timeout_ms / 1e3)
+                else:
+                    r, f = be.collect(h)
+                return r, f, getattr(be, "core", None) is not None
             except Exception as e:
                 self._mark_unhealthy(o, e)
-        return self._fallback_score(sub, now, want_features, "shard_unhealthy", shard=o)
+        r, f = self._fallback_score(sub, now, want_features, "shard_unhealthy", shard=o)
+        return r, f, False
 
     def _fallback_score(self, sub: np.ndarray, now: int, want_features: bool, reason: str, shard=None):
         if self.fallback is None:
@@ -573,7 +590,15 @@ class RiskEngine:
         ``ltv_predictions`` (deploy/schema.sql; the reference declares both tables,
         init-db.sql:122-155, and never writes them). Rows survive a failed write. Returns the
         number of rows written."""
-        return self.auditlog.flush(path)
+        try:
+            return self.auditlog.flush(path)
+        finally:
+            ring = self.auditlog.native
+            if ring is not None:  # native-ring evictions -> the Prometheus counter
+                ev = int(ring.evicted)
+                if ev > self._audit_evicted_seen:
+                    self.metrics.audit_evicted.inc(ev - self._audit_evicted_seen)
+                    self._audit_evicted_seen = ev
 
     # ================================================================== python-level API
     def _tx_bytes(self, tx: Dict) -> bytes:
@@ -664,7 +689,7 @@ class RiskEngine:
                 self.group.reload_model(raw)
             else:
                 for be in self.backends:
-                    be.swap_model(fm, mkind)
+                    be.swap_model(fm, mkind, version=self.model_version + 1)
             if self.fallback is not None:
                 self.fallback.swap_model(fm, mkind)
             self.fraud_onnx, self.model_kind = fm, mkind
@@ -858,6 +883,7 @@ class RiskEngine:
             self.group = None
         elif self.core is not None:
             self.core.stop()
+        self.auditlog.close()  # the segment loader (segments left over resume on the next start)
 
     def health(self) -> Dict:
         fo = self.failover
@@ -937,7 +963,7 @@ class DeadShard:
     def refresh_config(self, scoring=None) -> None:
         pass
 
-    def swap_model(self, fm, mkind: str) -> None:
+    def swap_model(self, fm, mkind: str, version=None) -> None:
         pass
 
     def metrics(self):
@@ -1023,6 +1049,26 @@ def serve_shard(cfg: Config, comm, backend: str = "gpu", capacity: Optional[int]
     return out
 
 
+def make_auditlog(cfg: Config, tag: str) -> AuditLog:
+    """The risk_scores / ltv_predictions audit log of a process (on when AUDIT_DB is set);
+    segments an earlier process left behind are loaded in the background."""
+    s = cfg.server
+    log_ = AuditLog(enabled=bool(s.audit_db), mode=s.audit_mode, direct_max=s.audit_direct_max,
+                    tag=f"{tag}-p{os.getpid()}")
+    if log_.enabled:
+        log_.resume_loading(s.audit_db)
+    return log_
+
+
+def attach_audit_ring(auditlog: AuditLog, cfg: Config, core, indexes, model_version: int = 1) -> None:
+    if not auditlog.enabled:
+        return
+    ring = native().AuditRing(int(cfg.server.audit_ring_rows))
+    core.set_audit(ring)
+    core.set_model_version(int(model_version))
+    auditlog.attach_native(ring, indexes)
+
+
 def worker_node(cfg: Config, comm, backend: str = "gpu", capacity: Optional[int] = None, fraud_model=None,
                 capture: bool = True) -> "SpmdNode":
     """The serving objects of a worker rank (>= 1): local shard, node-shared registry, core."""
@@ -1082,6 +1128,33 @@ class SpmdNode:
         seq0 = self.local.scorer._seq if self.local.kind == "gpu" else 0
         self.core = serving.make_core(self.registry.index, dev, cfg, rank=rank, clock=self.clock, seq0=seq0)
         self.local.attach_core(self.core)
+        self.cfg = cfg
+        # risk_scores audit of the rows this rank ingests (each rank drains its own ring)
+        self.audit = make_auditlog(cfg, f"r{rank}")
+        attach_audit_ring(self.audit, cfg, self.core, self.registry.index)
+
+    def flush_audit(self, path: str) -> int:
+        return self.audit.flush(path)
+
+    def start_audit_flusher(self, every_s: float, log=None) -> None:
+        """Worker ranks: drain the audit ring every ``every_s`` (rank 0's serve loop does its own)."""
+        if not self.audit.enabled:
+            return
+        from .audit import flush_if_configured
+        self._audit_stop = threading.Event()
+
+        def loop():
+            while not self._audit_stop.wait(every_s):
+                flush_if_configured(self, log)
+            flush_if_configured(self, log)
+        self._audit_thread = threading.Thread(target=loop, name="audit-flush", daemon=True)
+        self._audit_thread.start()
+
+    def stop_audit_flusher(self) -> None:
+        if getattr(self, "_audit_stop", None) is not None:
+            self._audit_stop.set()
+            self._audit_thread.join(60)
+        self.audit.close()
 
     def score_batch_bytes(self, data: bytes, now: Optional[int] = None) -> bytes:
         """This rank's ingress: ScoreBatch request bytes -> response bytes."""

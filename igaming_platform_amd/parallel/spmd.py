@@ -100,6 +100,7 @@ class ShardRunner:
         self.rank = comm.rank
         self.abuse_gpu = abuse_gpu
         self.core = core  # this rank's serving core (paused around snapshots / restores)
+        self.model_version = 1  # fraud-model reloads applied (audit stamp of the core's rows)
         self.snapshot_dir = None  # the directory of the last OP_SNAPSHOT (final snapshot on failure)
         self.used = [0] * comm.world  # slots in use per rank (the shared registry, via OP_PING)
 
@@ -164,7 +165,9 @@ class ShardRunner:
         if op == OP_RELOAD:  # payload: ONNX bytes (empty: built-in heuristic)
             from ..native import native
             fm = native().OnnxModel.from_bytes(payload) if payload else None
-            self.be.swap_model(fm, "onnx" if fm is not None else "heuristic")
+            # every rank counts the reloads it applied: the same audit version stamp group-wide
+            self.model_version += 1
+            self.be.swap_model(fm, "onnx" if fm is not None else "heuristic", version=self.model_version)
             return None
         if op == OP_TABLES:
             _load_tables(payload, self.be.blacklist, self.be.ipintel)

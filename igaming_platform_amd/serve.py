@@ -84,11 +84,17 @@ def main(argv=None) -> int:
             from .api.grpc_server import IngressServer
             from .engine.risk_engine import serve_shard
 
+            nodes = []
+
             def listen(node):
+                nodes.append(node)
+                node.start_audit_flusher(a.audit_flush_every_s, log)  # AUDIT_DB: this rank's rows
                 return IngressServer(node, f"127.0.0.1:{cfg.server.grpc_port + a.internal_port_offset}",
                                      port=cfg.server.grpc_port, host=a.host).start()
             n, rows = serve_shard(cfg, comm, backend=backend, capacity=a.accounts or None,
                                   fraud_model=_fraud_model(a, cfg), on_node=listen)
+            for node in nodes:
+                node.stop_audit_flusher()
             log.info("shard worker stopped", extra={"fields": dict(rank=comm.rank, ops=n, rows_scored=rows)})
             return 0
     from .api.grpc_server import RiskServer

@@ -6,7 +6,8 @@ cd $GRAFT_REPO_ROOT
 O=gpurun_out/r3d
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_mlp_fused_gpu.py tests/test_gru_gpu.py tests/test_engine_gpu.py -m gpu -v --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1
-echo "tests rc=$?" >> $O/status.txt
+rc=$?; echo "tests rc=$rc" >> $O/status.txt
+[ $rc -le 1 ] || exit 2  # timeout / abort / fault: nothing more on the GPU
 for c in cfg4 cfg5; do
   for nm in fp32 bf16; do
     timeout -k 10 300 python bench.py --config $c --numerics $nm --steps 300 --warmup 30 --json-out $O/bench_${c}_$nm.json > $O/bench_${c}_$nm.log 2>&1 || exit 3
