@@ -61,8 +61,9 @@ def parse():
                     help="N > 1: exchange = every rank ingests 8192 rows/step spread over all owners and "
                          "the owner-routed RCCL exchange (the serving path, engine/dp.py) moves each row to "
                          "its owner and the results back; replicas = N independent single-GPU pipelines")
-    ap.add_argument("--scope", default="serving", choices=["serving", "engine_only", "e2e", "grpc"],
-                    help="serving (default): the serving objects of every rank - risk.v1 ScoreBatch request bytes "
+    ap.add_argument("--scope", default="auto", choices=["auto", "serving", "engine_only", "e2e", "grpc"],
+                    help="auto (default): serving for the fraud configs, engine_only for cfg4 / cfg5 (LTV and "
+                         "abuse models are not ScoreBatch traffic); serving: the serving objects of every rank - risk.v1 ScoreBatch request bytes "
                          "(UUID account ids) -> the rank's native serving core (C++ parse, node-shared AccountIndex, "
                          "owner-routed RCCL exchange steps for N > 1, GPU pipeline) -> response bytes with the "
                          "FeatureVector, every rank ingesting; engine_only: pre-resolved ReqRec rows into the "
@@ -76,6 +77,8 @@ def parse():
     a = ap.parse_args()
     if a.numerics == "auto":  # the ONNX models' f32 contract everywhere (cfg4 / cfg5: split MFMA)
         a.numerics = "fp32"
+    if a.scope == "auto":
+        a.scope = "engine_only" if a.config in ("cfg4", "cfg5") else "serving"
     return a
 
 

@@ -222,7 +222,7 @@ PYBIND11_MODULE(_hipk, m) {
     }, s, "feature_update");
   });
 
-  m.def("tree_ensemble", [](py::dict d, uintptr_t s) {
+  auto tree_args = [](const py::dict& d) {
     TreeArgs a{};
     a.hdr = ptr<const BatchHdr*>(d, "hdr");
     a.X = ptr<const float*>(d, "X");
@@ -243,6 +243,11 @@ PYBIND11_MODULE(_hipk, m) {
     a.no_finish = geti(d, "no_finish", 0);
     a.all_leq = geti(d, "all_leq", 0);
     a.trace = ptr<int64_t*>(d, "trace");
+    return a;
+  };
+
+  m.def("tree_ensemble", [tree_args](py::dict d, uintptr_t s) {
+    TreeArgs a = tree_args(d);
     const int groups = geti(d, "groups", 1);
     float* partial = ptr<float*>(d, "partial");
     if (d.contains("ens") && !d["ens"].is_none()) {
@@ -318,7 +323,7 @@ PYBIND11_MODULE(_hipk, m) {
     launch_or_record([a](hipStream_t st) { launch_gemv(a, st); }, s, "gemv");
   });
 
-  m.def("mlp_head", [](py::dict d, uintptr_t s) {
+  auto head_args = [](const py::dict& d) {
     HeadArgs a{};
     a.X = ptr<const void*>(d, "X");
     a.W1 = ptr<const void*>(d, "W1");
@@ -349,7 +354,25 @@ PYBIND11_MODULE(_hipk, m) {
       if (!a.ens.hdr || !a.ens.cfg || !a.ens.feat || !a.ens.out) throw std::runtime_error("mlp_head: ensemble args");
     }
     if (a.k_pad % 32 || a.k_pad < a.K) throw std::runtime_error("mlp_head: k_pad must be a multiple of 32 >= K");
+    return a;
+  };
+
+  m.def("mlp_head", [head_args](py::dict d, uintptr_t s) {
+    const HeadArgs a = head_args(d);
     launch_or_record([a](hipStream_t st) { launch_mlp_head(a, st); }, s, "mlp_head");
+  });
+
+  m.def("tree_head", [tree_args, head_args](py::dict dt, py::dict dh, uintptr_t s) {
+    const TreeArgs a = tree_args(dt);
+    const HeadArgs h = head_args(dh);
+    const int groups = geti(dt, "groups", 1);
+    float* partial = ptr<float*>(dt, "partial");
+    unsigned int* cnt = ptr<unsigned int*>(dt, "tile_cnt");
+    if (!partial || !cnt || h.partial != partial || h.groups != groups)
+      throw std::runtime_error("tree_head: partial slab / tile counters");
+    if (!tree_head_supported(a, h, groups)) throw std::runtime_error("tree_head: unsupported tree/head shape");
+    launch_or_record([a, h, groups, partial, cnt](hipStream_t st) { launch_tree_head(a, h, groups, partial, cnt, st); },
+                     s, "tree_head");
   });
 
   m.def("ensemble", [](py::dict d, uintptr_t s) {
@@ -422,6 +445,7 @@ PYBIND11_MODULE(_hipk, m) {
     a.ws_err = ptr<int32_t*>(d, "ws_err");
     a.ws_trace = ptr<int64_t*>(d, "ws_trace");
     a.split = geti(d, "split");
+    a.reverse = geti(d, "reverse", 0);
     if (a.split) {
       for (int l = 0; l < a.n_layers; ++l)
         if (!a.layer[l].W_lo || !a.layer[l].R_lo) throw std::runtime_error("gru: split mode needs residual weights");

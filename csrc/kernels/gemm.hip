@@ -8,24 +8,15 @@
 // two LDS buffers: tile k+1 is loaded to registers while tile k's MFMAs run.
 #include "common.h"
 #include "ensemble.h"
+#include "head_f32.h"
 #include "launch.h"
 
 namespace igp {
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 constexpr int G_BK = 64;
 constexpr int G_PAD = 8;  // bf16 elements of row padding (144-byte rows)
-
-__device__ __forceinline__ float act_fn(float v, int act) {
-  switch (act) {
-    case 1: return v > 0.f ? v : 0.f;
-    case 2: return 1.f / (1.f + expf(-v));
-    case 3: return tanhf(v);
-    default: return v;
-  }
-}
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
@@ -452,15 +443,6 @@ __global__ void __launch_bounds__(256) mlp_head_kernel(HeadArgs a, int w_lds) {
 // on v_mfma_f32_16x16x4_f32: lane l supplies A[l & 15][k] and B[k][l & 15] with
 // k = 4 (l >> 4) + j for the j-th of four consecutive MFMAs, so one 16-B LDS read per operand
 // feeds four MFMAs and four MFMAs cover 16 k (the sum over k is order-free up to rounding).
-typedef __attribute__((ext_vector_type(4))) float f32v4;
-
-__device__ __forceinline__ f32x4 mfma4_f32(const float4& av, const float4& bv, f32x4 acc) {
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc, 0, 0, 0);
-  return acc;
-}
 
 // mlp_head in f32: same blocking as the bf16 kernel (32 rows per block, 4 waves x 16 hidden
 // columns per 64-column chunk), A tile and W1 (f32 [n1p][k_pad]) staged in LDS with rows

@@ -427,7 +427,8 @@ __global__ void __launch_bounds__(NW * 64) gru_kernel(GruArgs a) {
   }
   auto load_x = [&](int t) -> uint4 {
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (!stager || t < valid_from) return v;
+    if (a.reverse) t = a.T - 1 - t;  // direction=reverse: forward over the time-reversed sequence
+    if (!stager || t < valid_from || t < 0) return v;
     if (a.mode == 1) {
       int idx = (head - a.T + t) % a.ev_ring;
       if (idx < 0) idx += a.ev_ring;
@@ -539,7 +540,9 @@ __global__ void __launch_bounds__(NW * 64) gru_x3_kernel(GruArgs a) {
   // x_t as (hi, lo) bf16 halves: the event ring holds bf16 values (lo = 0); dense f32 input splits
   auto load_x = [&](int t, uint4& hi, uint4& lo) {
     hi = lo = make_uint4(0, 0, 0, 0);
-    if (!stager || t < valid_from || t >= a.T) return;
+    if (t >= a.T) return;
+    if (a.reverse) t = a.T - 1 - t;
+    if (!stager || t < valid_from) return;
     if (a.mode == 1) {
       int idx = (head - a.T + t) % a.ev_ring;
       if (idx < 0) idx += a.ev_ring;
@@ -674,7 +677,9 @@ __global__ void __launch_bounds__(NW * 64) gru2_pipe_kernel(GruArgs a) {
   }
   auto load_x = [&](int t) -> uint4 {
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (!stager || t < valid_from || t >= a.T) return v;
+    if (t >= a.T) return v;
+    if (a.reverse) t = a.T - 1 - t;
+    if (!stager || t < valid_from) return v;
     if (a.mode == 1) {
       int idx = (head - a.T + t) % a.ev_ring;
       if (idx < 0) idx += a.ev_ring;

@@ -262,7 +262,9 @@ __global__ void __launch_bounds__(256, 1) gru_ws_kernel(GruArgs a) {
     uint4 v = make_uint4(0, 0, 0, 0);
     const int2 m = xmeta[c];
     const int from = m.y >> 16;
-    if (t >= T || t < from) return v;
+    if (t >= T) return v;
+    if (a.reverse) t = T - 1 - t;  // direction=reverse: forward over the time-reversed sequence
+    if (t < from) return v;
     const int row = c / chunks, q = c - row * chunks;
     if (a.mode == 1) {
       if (m.x < 0) return v;

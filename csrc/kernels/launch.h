@@ -195,6 +195,13 @@ struct HeadArgs {
 };
 void launch_mlp_head(const HeadArgs& a, hipStream_t st);
 
+// cfg3 stacked model in one launch (trees.hip tree_head_kernel): grouped K = 32 tree ensemble
+// whose last-arriving group block per 64-row tile runs the f32 head (+ fused K5) on the tile.
+// h.partial / h.groups describe the slab the tree blocks write; tile_cnt: zeroed uint32 per tile.
+bool tree_head_supported(const TreeArgs& a, const HeadArgs& h, int groups);
+void launch_tree_head(const TreeArgs& a, const HeadArgs& h, int groups, float* partial, unsigned int* tile_cnt,
+                      hipStream_t st);
+
 void launch_ensemble(const EnsembleArgs& a, hipStream_t st);
 
 // ---- K4 GRU sequence (recurrent weights resident in VGPRs)
@@ -241,6 +248,7 @@ struct GruArgs {
   int32_t* ws_err;          // [1] set when a cluster was not co-resident (bounded wait expired)
   int64_t* ws_trace;        // [64][6] phase timestamps of workgroup 0 (nullable; tools/gru_bench.py)
   int32_t split;            // 1: f32-faithful bf16 hi/lo pairs, three MFMAs per product (gru.hip x3)
+  int32_t reverse;          // 1: ONNX direction=reverse (every layer): time steps read last to first
 };
 void launch_gru(const GruArgs& a, hipStream_t st);
 bool gru_ws_eligible(const GruArgs& a);

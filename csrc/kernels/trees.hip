@@ -13,6 +13,7 @@
 // finisher (or the consuming mlp_head kernel) adds base values and the post transform.
 #include "common.h"
 #include "ensemble.h"
+#include "head_f32.h"
 #include "launch.h"
 #include "tree_post.h"
 
@@ -20,6 +21,7 @@ namespace igp {
 
 constexpr int TR_ROWS = 64;
 constexpr int TR_ILP = 4;
+typedef unsigned int tr_u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int tree_step(int i, float x, float2 nd) {
   const uint32_t m = __float_as_uint(nd.y);
@@ -67,11 +69,13 @@ __device__ __forceinline__ int tree_next(int i, float x, float2 nd) {
   else return tree_step(i, x, nd);
 }
 
-template <int K, bool LEQ>
-__global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_group, int feat_w,
-                                                   int nodes_in_lds, float* partial) {
+// One workgroup's share of the ensemble: its 64-row tile x its tree group (blockIdx.y).
+// WT: the group partials are stored write-through (sc1) for an in-launch consumer
+// (tree_head_kernel); otherwise plain stores for the next kernel.
+template <int K, bool LEQ, bool WT>
+__device__ __forceinline__ void tree_block(const TreeArgs& a, int trees_per_group, int feat_w, int nodes_in_lds,
+                                           float* partial, char* smem) {
   constexpr bool TWO_PHASE = K >= 16;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   const int xs = feat_w + 1;
   float* sx = reinterpret_cast<float*>(smem);                       // [64][feat_w+1]
   const size_t x_bytes = ((size_t)TR_ROWS * xs * 4 + 15) & ~size_t(15);
@@ -270,7 +274,15 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
       const int row = row0 + r;
       if (row >= a.n_rows) continue;
       if (partial) {
-        *reinterpret_cast<float4*>(partial + ((size_t)g * a.n_rows + row) * K + 4 * k4) = v[j];
+        if constexpr (WT) {
+          // 16-B write-through store: the line leaves this XCD's L2, so the tile's last-arriving
+          // group block (any XCD, behind its agent acquire) reads it fresh
+          const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(partial, 0, 0x7fffffff, 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(tr_u32x4, v[j]), prs,
+                                                 (int)((((size_t)g * a.n_rows + row) * K + 4 * k4) * 4), 0, 16);
+        } else {
+          *reinterpret_cast<float4*>(partial + ((size_t)g * a.n_rows + row) * K + 4 * k4) = v[j];
+        }
       } else if (rowwise) {
         *reinterpret_cast<float4*>(red + r * K + 4 * k4) = v[j];
       } else {
@@ -315,6 +327,189 @@ __global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_gro
 }
 
 #undef TR_MARK
+
+template <int K, bool LEQ>
+__global__ void __launch_bounds__(256) tree_kernel(TreeArgs a, int trees_per_group, int feat_w,
+                                                   int nodes_in_lds, float* partial) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  tree_block<K, LEQ, false>(a, trees_per_group, feat_w, nodes_in_lds, partial, smem);
+}
+
+// ---------------------------------------------------------------------------------------------
+// cfg3 stacked model in one launch: TreeEnsemble (K = 32 leaf vectors, grouped) -> f32 MLP head
+// -> K5 ensemble. Every group block stores its [64][32] partial write-through and takes a ticket
+// on its tile's counter; the tile's last arriver (whichever XCD it runs on) runs one agent-scope
+// acquire, reduces the group partials in group order (+ base, / T: the same sums as
+// head_a_f32), and runs the head of the reference-precision kernel (mlp_head_f32_fast_kernel:
+// the same MFMA sequence per 16-row fragment, the same hidden-chunk and wave order, so Y is
+// bit-identical) and the fused K5 on its 64 rows. Removes the head launch and its hand-off;
+// the partial slab is read once, by one block per tile.
+constexpr int TH_LR = 32 + 4;  // LDS row stride of the A tile and W1 (floats)
+
+template <bool LEQ, int ACT>
+__global__ void __launch_bounds__(256) tree_head_kernel(TreeArgs a, HeadArgs h, int trees_per_group, int feat_w,
+                                                        int nodes_in_lds, float* partial, int groups,
+                                                        unsigned int* tile_cnt) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  tree_block<32, LEQ, true>(a, trees_per_group, feat_w, nodes_in_lds, partial, smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n1p = (h.N1 + 63) & ~63;
+  float* sA = reinterpret_cast<float*>(smem);  // [64][TH_LR]
+  float* sW = sA + TR_ROWS * TH_LR;             // [n1p][TH_LR]
+  float* sred = sW + n1p * TH_LR;               // [4][64]
+  float* sb1 = sred + 4 * TR_ROWS;              // [n1p]
+  float* sw2 = sb1 + n1p;                       // [n1p]
+  unsigned int* ecnt = reinterpret_cast<unsigned int*>(sw2 + n1p);  // [MET_N]
+  int* sflag = reinterpret_cast<int*>(ecnt + MET_N);
+  // publish: every wave's partial stores complete, then one ticket per block
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned int old = __hip_atomic_fetch_add(&tile_cnt[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (unsigned int)(groups - 1);
+    if (last) __hip_atomic_store(&tile_cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sflag[0] = last;
+  }
+  __syncthreads();
+  if (!sflag[0]) return;
+  const int M = h.m_ptr ? min(*h.m_ptr, h.M) : h.M;
+  const int row0 = blockIdx.x * TR_ROWS;
+  const bool fm = h.fuse_ens && h.ens.metrics;
+  if (row0 >= M) {  // no live row in this tile: the fused ensemble still writes the inert rows
+    if (h.fuse_ens)
+      for (int r = row0 + tid; r < min(row0 + TR_ROWS, h.ens.n_rows); r += 256) ensemble_row(h.ens, r, true, 0.f, nullptr);
+    return;
+  }
+  // weights first (read-only: no acquire needed), in flight across the acquire
+  const float* const W1 = reinterpret_cast<const float*>(h.W1);
+  constexpr int KQ = 8;  // float4 chunks per 32-float W1 row
+  const int total = n1p * KQ;
+  float4 wv[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int ch = u * 256 + tid;
+    wv[u] = ch < total ? *reinterpret_cast<const float4*>(W1 + (size_t)(ch / KQ) * 32 + (ch % KQ) * 4)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  if (fm)
+    for (int i = tid; i < MET_N; i += 256) ecnt[i] = 0;
+  __syncthreads();
+  // A tile: sum_g partial[g][row][k] in group order (+ base, / T), 2 x 16-B chunks per thread;
+  // up to 8 groups' loads in flight per round (the weights go to LDS under the first round)
+  const int gl = groups - 1;
+  float fa[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  for (int g0 = 0; g0 < groups; g0 += 8) {
+    float4 p[2][8];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int ch = c * 256 + tid, r = ch >> 3, kc = (ch & 7) * 4;
+#pragma unroll
+      for (int g = 0; g < 8; ++g)
+        p[c][g] = *reinterpret_cast<const float4*>(
+            partial + ((size_t)min(g0 + g, gl) * a.n_rows + min(row0 + r, a.n_rows - 1)) * 32 + kc);
+    }
+    if (g0 == 0) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int ch = u * 256 + tid;
+        if (ch < total) *reinterpret_cast<float4*>(&sW[(ch / KQ) * TH_LR + (ch % KQ) * 4]) = wv[u];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int g = 0; g < 8; ++g)
+        if (g0 + g <= gl) {
+          fa[c][0] += p[c][g].x; fa[c][1] += p[c][g].y; fa[c][2] += p[c][g].z; fa[c][3] += p[c][g].w;
+        }
+  }
+  for (int ch = 8 * 256 + tid; ch < total; ch += 256)
+    *reinterpret_cast<float4*>(&sW[(ch / KQ) * TH_LR + (ch % KQ) * 4]) =
+        *reinterpret_cast<const float4*>(W1 + (size_t)(ch / KQ) * 32 + (ch % KQ) * 4);
+  for (int n = tid; n < n1p; n += 256) {
+    sb1[n] = (n < h.N1 && h.b1) ? h.b1[n] : 0.f;
+    sw2[n] = n < h.N1 ? h.w2[n] : 0.f;
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int ch = c * 256 + tid, r = ch >> 3, kc = (ch & 7) * 4;
+    float f[4] = {0.f, 0.f, 0.f, 0.f};
+    if (row0 + r < M) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f[j] = fa[c][j];
+        if (h.p_average) f[j] /= (float)h.p_ntrees;
+        f[j] += h.pbase ? h.pbase[kc + j] : 0.f;
+      }
+    }
+    *reinterpret_cast<float4*>(&sA[r * TH_LR + kc]) = make_float4(f[0], f[1], f[2], f[3]);
+  }
+  __syncthreads();
+  // 4 row fragments of 16 x (4 waves x 16 hidden columns per 64-column chunk)
+  float4 av[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      av[i][s] = *reinterpret_cast<const float4*>(&sA[(i * 16 + (lane & 15)) * TH_LR + s * 16 + 4 * (lane >> 4)]);
+  float part[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) part[i][q] = 0.f;
+  for (int c0 = 0; c0 < h.N1; c0 += 64) {
+    const int n = c0 + wave * 16 + (lane & 15);
+    float4 bv[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) bv[s] = *reinterpret_cast<const float4*>(&sW[n * TH_LR + s * 16 + 4 * (lane >> 4)]);
+    const float b1 = sb1[n];
+    const float w2 = sw2[n];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) acc = mfma4_f32(av[i][s], bv[s], acc);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) part[i][q] += act_fn(acc[q] + b1, ACT) * w2;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v = part[i][q];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      part[i][q] = v;
+    }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sred[wave * TR_ROWS + i * 16 + (lane >> 4) * 4 + q] = part[i][q];
+  }
+  __syncthreads();
+  if (tid < TR_ROWS) {
+    const int row = row0 + tid;
+    float y = 0.f;
+    if (row < M) {
+      const float v = sred[tid] + sred[TR_ROWS + tid] + sred[2 * TR_ROWS + tid] + sred[3 * TR_ROWS + tid];
+      y = act_fn(v + h.b2, h.act2);
+      h.Y[(size_t)row * h.ldy] = y;
+    }
+    if (h.fuse_ens && row < h.ens.n_rows) ensemble_row(h.ens, row, true, y, fm ? ecnt : nullptr);
+  }
+  if (fm) {
+    __syncthreads();
+    ensemble_metrics_flush(h.ens, ecnt, tid, 256);
+  }
+}
 
 __global__ void tree_finish_kernel(TreeArgs a, const float* partial, int groups) {
   const int row = blockIdx.x * blockDim.x + threadIdx.x;
@@ -421,5 +616,36 @@ void launch_tree_ensemble_grouped(const TreeArgs& a, int groups, float* partial,
 }
 
 void launch_tree_ensemble(const TreeArgs& a, hipStream_t st) { launch_tree_ensemble_grouped(a, 1, nullptr, st); }
+
+bool tree_head_supported(const TreeArgs& a, const HeadArgs& h, int groups) {
+  return a.k == 32 && groups > 1 && groups <= 16 && a.post == 0 && a.binary_class < 0 && h.w1_f32 && h.k_pad == 32 &&
+         h.K == 32 && h.N1 > 0 && h.N1 <= 512 && h.act1 >= 0 && h.act1 <= 3 && h.M == a.n_rows && !h.trace;
+}
+
+void launch_tree_head(const TreeArgs& a, const HeadArgs& h, int groups, float* partial, unsigned int* tile_cnt,
+                      hipStream_t st) {
+  const int tpg = (a.n_trees + groups - 1) / groups;
+  const int feat_w = a.x_stride;
+  const int n_int = (1 << a.depth) - 1;
+  const size_t x_bytes = ((size_t)TR_ROWS * (feat_w + 1) * 4 + 15) & ~size_t(15);
+  const size_t red_bytes = (size_t)TR_ROWS * 32 * 4;
+  const size_t node_bytes = ((size_t)tpg * n_int * 8 + 15) & ~size_t(15);
+  const size_t leaf_bytes = (size_t)TR_ROWS * tpg * 2;
+  const size_t base = x_bytes > red_bytes ? x_bytes : red_bytes;
+  const int in_lds = (base + node_bytes + leaf_bytes) <= 96 * 1024;
+  const size_t tree_lds = base + (in_lds ? node_bytes : 0) + leaf_bytes;
+  const size_t n1p = (size_t)((h.N1 + 63) & ~63);
+  const size_t head_lds = ((size_t)TR_ROWS + n1p) * TH_LR * 4 + 4 * TR_ROWS * 4 + 2 * n1p * 4 + MET_N * 4 + 16;
+  const size_t lds = tree_lds > head_lds ? tree_lds : head_lds;
+  dim3 grid((a.n_rows + TR_ROWS - 1) / TR_ROWS, groups);
+#define TH_CASE(L, ACT) \
+  if (a.all_leq == L && h.act1 == ACT) { \
+    IGP_LAUNCH((tree_head_kernel<L, ACT>), grid, dim3(256), lds, st, a, h, tpg, feat_w, in_lds, partial, groups, tile_cnt); \
+    return; \
+  }
+  TH_CASE(true, 0) TH_CASE(true, 1) TH_CASE(true, 2) TH_CASE(true, 3)
+  TH_CASE(false, 0) TH_CASE(false, 1) TH_CASE(false, 2) TH_CASE(false, 3)
+#undef TH_CASE
+}
 
 }  // namespace igp

@@ -126,19 +126,28 @@ Tensor matmul(const Tensor& A, const Tensor& B) {
   return Y;
 }
 
-// ONNX GRU (gates z, r, h), layout 0, activations sigmoid/tanh.
+// ONNX GRU (gates z, r, h), activations sigmoid/tanh, directions forward / reverse /
+// bidirectional. layout 0: X [S][B][I], Y [S][D][B][H], Y_h / initial_h [D][B][H];
+// layout 1 (batch-major): X [B][S][I], Y [B][S][D][H], Y_h / initial_h [B][D][H].
 void gru(const onnx::Node& n, const Tensor& X, const Tensor& W, const Tensor& R, const Tensor* Bp,
          const Tensor* h0, Tensor& Y, Tensor& Yh) {
   const int64_t H = n.geti("hidden_size", R.dims.back());
   const bool lbr = n.geti("linear_before_reset", 0);
-  if (n.geti("layout", 0) != 0) throw std::runtime_error("GRU: layout=1 is not supported");
+  const int64_t layout = n.geti("layout", 0);
+  if (layout != 0 && layout != 1) throw std::runtime_error("GRU: layout must be 0 or 1");
   std::string dir = n.gets("direction", "forward");
+  if (dir != "forward" && dir != "reverse" && dir != "bidirectional") throw std::runtime_error("GRU: direction");
   const int64_t D = dir == "bidirectional" ? 2 : 1;
-  const int64_t S = X.dims[0], Bn = X.dims[1], I = X.dims[2];
+  if (X.dims.size() != 3) throw std::runtime_error("GRU: X must be rank 3");
+  const int64_t S = layout ? X.dims[1] : X.dims[0], Bn = layout ? X.dims[0] : X.dims[1], I = X.dims[2];
   if (W.dims[0] != D || W.dims[1] != 3 * H || W.dims[2] != I) throw std::runtime_error("GRU: W shape");
   if (R.dims[0] != D || R.dims[1] != 3 * H || R.dims[2] != H) throw std::runtime_error("GRU: R shape");
-  Y = make({S, D, Bn, H});
-  Yh = make({D, Bn, H});
+  Y = layout ? make({Bn, S, D, H}) : make({S, D, Bn, H});
+  Yh = layout ? make({Bn, D, H}) : make({D, Bn, H});
+  // element offsets of (t, b) in X, (t, d, b) in Y and (d, b) in Y_h / initial_h
+  auto xo = [&](int64_t t, int64_t b) { return (layout ? b * S + t : t * Bn + b) * I; };
+  auto yo = [&](int64_t t, int64_t d, int64_t b) { return (layout ? (b * S + t) * D + d : (t * D + d) * Bn + b) * H; };
+  auto ho = [&](int64_t d, int64_t b) { return (layout ? b * D + d : d * Bn + b) * H; };
   std::vector<double> hz(H), hr(H), hh(H), xz(H), xr(H), xh(H);
   for (int64_t d = 0; d < D; ++d) {
     const bool rev = dir == "reverse" || (D == 2 && d == 1);
@@ -148,10 +157,10 @@ void gru(const onnx::Node& n, const Tensor& X, const Tensor& W, const Tensor& R,
     if (Bp) std::copy(Bp->f.begin() + d * 6 * H, Bp->f.begin() + (d + 1) * 6 * H, bias.begin());
     for (int64_t b = 0; b < Bn; ++b) {
       std::vector<float> h(H, 0.f);
-      if (h0) std::copy(h0->f.begin() + (d * Bn + b) * H, h0->f.begin() + (d * Bn + b + 1) * H, h.begin());
+      if (h0) std::copy(h0->f.begin() + ho(d, b), h0->f.begin() + ho(d, b) + H, h.begin());
       for (int64_t st = 0; st < S; ++st) {
         const int64_t t = rev ? S - 1 - st : st;
-        const float* x = &X.f[(t * Bn + b) * I];
+        const float* x = &X.f[xo(t, b)];
         for (int64_t j = 0; j < H; ++j) {
           double az = 0, ar = 0, ah = 0, bz = 0, br = 0, bh = 0;
           for (int64_t k = 0; k < I; ++k) {
@@ -185,9 +194,9 @@ void gru(const onnx::Node& n, const Tensor& X, const Tensor& W, const Tensor& R,
           float nt = std::tanh(float(xh[j] + bias[2 * H + j] + hh[j]));
           h[j] = (1.f - zg[j]) * nt + zg[j] * h[j];
         }
-        std::copy(h.begin(), h.end(), Y.f.begin() + ((t * D + d) * Bn + b) * H);
+        std::copy(h.begin(), h.end(), Y.f.begin() + yo(t, d, b));
       }
-      std::copy(h.begin(), h.end(), Yh.f.begin() + (d * Bn + b) * H);
+      std::copy(h.begin(), h.end(), Yh.f.begin() + ho(d, b));
     }
   }
 }

@@ -94,12 +94,13 @@ class AbuseGpu:
         self.store = store
         self.device = store.device
         steps = plan.steps
-        n = sum(1 for s in steps if s.kind == "gru")
-        head = steps[n] if n < len(steps) else None
+        from .runner import GruModel
         # fp32 plans (the ONNX f32 contract, default): the f32-faithful split GRU; bf16 plans: bf16 MFMA
-        self.gp = K.GruPack(steps[:n], head, self.device, split=getattr(plan, "precision", "fp32") != "bf16")
-        if self.gp.head_w is None:
+        bmax_ = max([int(b) for b in buckets] or [bmax])
+        self.gm = GruModel(steps, self.device, getattr(plan, "precision", "fp32") != "bf16", bmax_)
+        if not self.gm.has_head:
             raise ValueError("abuse model must end in an N=1 head (probability)")
+        self.gp = self.gm.packs[0]  # (the weight-stationary path and its fallback live on this pack)
         self.T = steps[0].seq or store.ev.shape[1]
         if self.T > store.ev.shape[1]:
             raise ValueError(f"abuse model sequence length {self.T} exceeds the event ring {store.ev.shape[1]}")
@@ -122,7 +123,7 @@ class AbuseGpu:
 
     def _body(self, slot: int, b: int) -> None:
         self.dev_slab[:16 + 4 * b].copy_(self.host[slot][:16 + 4 * b], non_blocking=True)
-        self.K.gru(self.gp, b, self.T, out=self.out, store=self.store, slots=self.slots, m_ptr=self.n_ptr)
+        self.gm.run(b, self.T, self.out, store=self.store, slots=self.slots, m_ptr=self.n_ptr)
         self.host_out[slot][:b].copy_(self.out[:b], non_blocking=True)
 
     def _pack(self, slot: int, slots: np.ndarray, b: int) -> None:

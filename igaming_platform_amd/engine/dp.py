@@ -33,6 +33,31 @@ from .scorer import HDR_BYTES, GpuScorer
 
 REQ = REQREC.itemsize
 
+# Per-rank stream -> hardware-queue map of the exchange pipeline. HIP multiplexes a process's
+# streams onto GPU_MAX_HW_QUEUES hardware queues (4 on the boxes, HIP's default); a fifth
+# stream would share a queue with one of these and serialise behind it. The default layout
+# (IGP_XCHG_STREAMS=3) therefore puts the two RCCL all-to-alls on the copy and model streams:
+#   default  allocations, cold reads (GetFeatures readouts order on the state stream)
+#   copy     H2D chunks + header, row all-to-all (communicator 0), compaction, dedup insert
+#   state    K1 feature assembly + state update (owns the HBM feature store)
+#   model    trees / head / K5, result scatter, result all-to-all (communicator 1), D2H
+# Communicators per rank: the two exchange RcclComms (rows, results; their kernels run on the
+# streams above, RCCL opens no stream of its own for them) and the gloo control plane (CPU).
+# No torch NCCL process group exists on the serving path. IGP_XCHG_STREAMS=5 gives the
+# all-to-alls two CU-masked streams of their own (6 streams: an A/B knob, over the budget).
+HW_QUEUES = 4
+EXCHANGE_COMMUNICATORS = 2
+
+
+def stream_roles(mode: Optional[str] = None) -> dict:
+    """role -> the stream that carries it (``mode``: IGP_XCHG_STREAMS, default "3")."""
+    mode = mode if mode is not None else os.environ.get("IGP_XCHG_STREAMS", "3")
+    roles = dict(default="default", h2d="copy", rows_a2a="copy", compact="copy", features="state",
+                 model="model", results_a2a="model", d2h="model")
+    if mode == "5":
+        roles.update(rows_a2a="xs", results_a2a="ys")
+    return roles
+
 
 @dataclass
 class XPending:
@@ -92,6 +117,15 @@ class DpGpuScorer(GpuScorer):
         self.xgraphs = {}
         self.xdriver = None
         self._watch = None
+
+    def stream_map(self) -> dict:
+        """role -> HIP stream handle actually used by this rank (see :func:`stream_roles`)."""
+        st = dict(default=torch.cuda.default_stream(self.device), copy=self.cstream, state=self.stream,
+                  model=self.mstream, xs=self.xstream, ys=self.ystream)
+        h = {k: v.cuda_stream for k, v in st.items()}
+        roles = dict(default="default", h2d="copy", rows_a2a="xs", compact="copy", features="state",
+                     model="model", results_a2a="ys", d2h="ys")
+        return {r: h[s] for r, s in roles.items()}
 
     # ------------------------------------------------------------------ graph bodies
     @staticmethod

@@ -27,6 +27,62 @@ def tree_groups(step, bucket: int) -> int:
     return max(1, min(max(1, step.n_trees // 8), -(-512 // tiles)))
 
 
+class GruModel:
+    """The GRU part of a plan on the device (K4, csrc/kernels/gru*.hip):
+
+    * forward or reverse layers (1-2, stacked): one launch, the N=1 head fused in its epilogue;
+    * one bidirectional layer: a forward and a reverse launch, each writing its final state
+      into its half of a [rows, 2H] buffer (the ONNX Y_h in [N, 2, H] order), then the N=1
+      head as a dense launch.
+
+    Input: dense X f32 [T, rows, I] (the ONNX layout-0 order; layout-1 plans are fed the same,
+    see :meth:`DeviceModel.run`) or the store's event rings for ``slots``."""
+
+    def __init__(self, steps, device, split: bool, bmax: int):
+        n = 0
+        while n < len(steps) and steps[n].kind == "gru":
+            n += 1
+        head = steps[n] if n < len(steps) and steps[n].kind == "dense" and steps[n].n == 1 else None
+        if n == 0 or n + (head is not None) != len(steps):
+            raise ValueError("sequence model must be GRU layers followed by at most an N=1 head")
+        g = steps[0]
+        self.H = g.hidden
+        self.seq = g.seq
+        self.bidirectional = g.bidirectional
+        self.head = head
+        if g.bidirectional:
+            if n != 1:
+                raise ValueError("bidirectional GRU: one layer")
+            self.packs = [K.GruPack([g.direction(0)], None, device, split=split),
+                          K.GruPack([g.direction(1)], None, device, split=split, reverse=True)]
+            self.yh = [torch.zeros((bmax, self.H), dtype=torch.float32, device=device) for _ in range(2)]
+            self.cat = torch.zeros((bmax, 2 * self.H), dtype=torch.float32, device=device)
+        else:
+            self.packs = [K.GruPack(steps[:n], head, device, split=split, reverse=g.reverse)]
+
+    @property
+    def has_head(self) -> bool:
+        return self.head is not None
+
+    def run(self, n_rows: int, T: int, out: torch.Tensor, X: Optional[torch.Tensor] = None, store=None,
+            slots: Optional[torch.Tensor] = None, m_ptr: Optional[torch.Tensor] = None) -> None:
+        """``out``: [rows] probabilities with a head, else [rows, H * directions] final states."""
+        if not self.bidirectional:
+            gp = self.packs[0]
+            if self.head is not None:
+                K.gru(gp, n_rows, T, out=out, X=X, store=store, slots=slots, m_ptr=m_ptr)
+            else:
+                K.gru(gp, n_rows, T, yh=out, X=X, store=store, slots=slots, m_ptr=m_ptr)
+            return
+        for gp, yh in zip(self.packs, self.yh):
+            K.gru(gp, n_rows, T, yh=yh, X=X, store=store, slots=slots, m_ptr=m_ptr)
+        dst = self.cat if self.head is not None else out
+        torch.cat([self.yh[0][:n_rows], self.yh[1][:n_rows]], dim=1, out=dst[:n_rows])
+        if self.head is not None:
+            h = self.head
+            K.dense(self.cat, h.w, h.b, out, n_rows, 1, 2 * self.H, act=h.act, m_ptr=m_ptr)
+
+
 class DeviceModel:
     def __init__(self, plan: Plan, device, buckets: Sequence[int]):
         self.plan = plan
@@ -51,17 +107,15 @@ class DeviceModel:
                     self.tree_groups[b] = g
                     need = max(need, g * b * s.k)
                 self.tree_partial = torch.zeros(max(need, 1), dtype=torch.float32, device=self.device)
+        # tree -> head pairs that run as one launch (trees.hip tree_head_kernel) need one ticket
+        # counter per 64-row tile (the kernel returns them to zero)
+        self.tile_cnt = torch.zeros(-(-B // 64), dtype=torch.int32, device=self.device)
         # sequence models: the GRU layers (+ an N=1 head) run as ONE fused K4 launch
-        self.gru: Optional[K.GruPack] = None
+        # (a bidirectional layer: two launches + the head, GruModel)
+        self.gru: Optional[GruModel] = None
         self.gru_steps = 0
         if any(s.kind == "gru" for s in steps):
-            n = 0
-            while n < len(steps) and steps[n].kind == "gru":
-                n += 1
-            head = steps[n] if n < len(steps) and steps[n].kind == "dense" and steps[n].n == 1 else None
-            if n == 0 or n + (head is not None) != len(steps):
-                raise ValueError("sequence model must be GRU layers followed by at most an N=1 head")
-            self.gru = K.GruPack(steps[:n], head, self.device, split=plan.precision != "bf16")
+            self.gru = GruModel(steps, self.device, plan.precision != "bf16", B)
             self.gru_steps = len(steps)
             self.seq_len = steps[0].seq
         self.out = self.step_out[-1] if self.step_out else None
@@ -92,15 +146,18 @@ class DeviceModel:
         if ens is not None and not self.fuses_ensemble(bucket):
             raise ValueError("this plan cannot fuse the ensemble")
         if self.gru is not None:
-            T = X.shape[0]
-            if self.gru.head_w is not None:
-                K.gru(self.gru, bucket, T, out=self.out, X=X, m_ptr=m_ptr)
-            else:
-                K.gru(self.gru, bucket, T, yh=self.out, X=X, m_ptr=m_ptr)
+            if self.plan.steps[0].layout == 1:  # batch-major model input [rows, T, I]
+                X = X.transpose(0, 1).contiguous()
+            self.gru.run(bucket, X.shape[0], self.out, X=X, m_ptr=m_ptr)
             return self.out
         cur = X
         fused_partial = None
+        skip = -1
+        one_launch = os.environ.get("IGP_TREE_HEAD", "1") != "0"
         for i, (s, out) in enumerate(zip(steps, self.step_out)):
+            if i == skip:
+                cur = out
+                continue
             if s.kind == "tree" and s.layout == "sparse":
                 K.tree_sparse(s, cur, out, bucket, partial=self.tree_partial, groups=self.tree_groups.get(bucket, 1))
                 fused_partial = None
@@ -108,6 +165,13 @@ class DeviceModel:
                 g = self.tree_groups.get(bucket, 1)
                 fuse = (g > 1 and i + 1 < len(steps) and steps[i + 1].kind == "head" and s.post == 0
                         and s.binary_class < 0 and steps[i + 1].k == s.k)
+                if fuse and one_launch and K.tree_head_ok(s, steps[i + 1], g):
+                    # the head (and the K5 of a last head) in the tree kernel's last-arriving blocks
+                    K.tree_head(s, steps[i + 1], cur, self.step_out[i + 1], bucket, self.tree_partial, g,
+                                self.tile_cnt, m_ptr=m_ptr, ens=ens if i + 1 == len(steps) - 1 else None)
+                    skip = i + 1
+                    cur = out
+                    continue
                 K.tree_ensemble(s, cur, None if fuse else out, bucket, partial=self.tree_partial,
                                 groups=g, no_finish=fuse, ens=ens if i == len(steps) - 1 else None)
                 fused_partial = (self.tree_partial, g, s) if fuse else None

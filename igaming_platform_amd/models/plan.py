@@ -145,10 +145,24 @@ class GRUStep:
     seq: int = 0
     dev: Dict[str, Any] = field(default_factory=dict)
     kind: str = "gru"
+    reverse: bool = False      # direction=reverse: the sequence is read last step first
+    layout: int = 0            # ONNX layout attribute (1: batch-major X / Y / Y_h)
+    bidirectional: bool = False
+    w_rev_np: Optional[np.ndarray] = None  # bidirectional: the reverse direction's W / R / B
+    r_rev_np: Optional[np.ndarray] = None
+    b_rev_np: Optional[np.ndarray] = None
 
     @property
     def out_width(self) -> int:
-        return self.hidden
+        return self.hidden * (2 if self.bidirectional else 1)
+
+    def direction(self, d: int) -> "GRUStep":
+        """One direction of a bidirectional layer as a unidirectional step (d = 1: reverse)."""
+        if d == 0:
+            return GRUStep(self.hidden, self.in_dim, self.linear_before_reset, self.w_np, self.r_np, self.b_np,
+                           seq=self.seq, layout=self.layout)
+        return GRUStep(self.hidden, self.in_dim, self.linear_before_reset, self.w_rev_np, self.r_rev_np,
+                       self.b_rev_np, seq=self.seq, reverse=True, layout=self.layout)
 
 
 @dataclass
@@ -212,6 +226,7 @@ def compile_onnx(model, input_name: str = "input", output_name: str = "output",
     width = in_width
     ml_col = 0
     visited = set()
+    bidir_pending = False  # a layout-0 bidirectional Y_h still in [D, N, H] order
     while cur != output_name:
         cons = [n for n in _consumers(nodes, cur) if id(n) not in visited]
         if len(cons) != 1:
@@ -315,25 +330,53 @@ def compile_onnx(model, input_name: str = "input", output_name: str = "output",
             continue
         if op in ("Squeeze", "Reshape", "Unsqueeze"):
             # shape-only between GRU layers / before the head (validated by the CPU executor)
+            if op == "Reshape" and bidir_pending:
+                raise PlanError("bidirectional GRU: Y_h [2, N, H] must be transposed to [N, 2, H] before reshaping")
+            cur = n["outputs"][0]
+            continue
+        if op == "Transpose":
+            # only the direction <-> batch swap of a layout-0 GRU's Y_h ([D, N, H] -> [N, D, H])
+            perm = [int(x) for x in a.get("perm", [])]
+            if not steps or steps[-1].kind != "gru" or steps[-1].layout != 0 or perm != [1, 0, 2]:
+                raise PlanError("Transpose is lowered only as perm [1, 0, 2] on a GRU's final states")
+            bidir_pending = False
             cur = n["outputs"][0]
             continue
         if op == "GRU":
-            if a.get("direction", "forward") != "forward" or int(a.get("layout", 0)) != 0:
-                raise PlanError("GRU: only forward, layout 0 is lowered")
+            direction = a.get("direction", "forward")
+            layout = int(a.get("layout", 0))
+            if direction not in ("forward", "reverse", "bidirectional") or layout not in (0, 1):
+                raise PlanError(f"GRU: direction {direction!r} / layout {layout} is not lowered")
             if len(n["inputs"]) > 4 and n["inputs"][4]:
                 raise PlanError("GRU: sequence_lens is not lowered")
-            W = np.asarray(const(n["inputs"][1]), np.float32)[0]
-            R = np.asarray(const(n["inputs"][2]), np.float32)[0]
-            H = int(a.get("hidden_size", R.shape[-1]))
-            B = (np.asarray(const(n["inputs"][3]), np.float32)[0] if len(n["inputs"]) > 3 and n["inputs"][3]
-                 else np.zeros(6 * H, np.float32))
-            steps.append(GRUStep(hidden=H, in_dim=int(W.shape[1]),
+            if len(n["inputs"]) > 5 and n["inputs"][5]:
+                raise PlanError("GRU: initial_h is not lowered (the device starts every sequence at zero)")
+            prev = [s for s in steps if s.kind == "gru"]
+            if prev and (direction == "bidirectional" or prev[0].bidirectional
+                         or prev[0].reverse != (direction == "reverse") or prev[0].layout != layout):
+                raise PlanError("GRU: stacked layers must share direction and layout (bidirectional: one layer)")
+            Wa = np.asarray(const(n["inputs"][1]), np.float32)
+            Ra = np.asarray(const(n["inputs"][2]), np.float32)
+            H = int(a.get("hidden_size", Ra.shape[-1]))
+            D = 2 if direction == "bidirectional" else 1
+            Ba = (np.asarray(const(n["inputs"][3]), np.float32).reshape(D, 6 * H)
+                  if len(n["inputs"]) > 3 and n["inputs"][3] else np.zeros((D, 6 * H), np.float32))
+            if Wa.shape[0] != D or Ra.shape[0] != D:
+                raise PlanError("GRU: weight direction count does not match the direction attribute")
+            seq = dims[1] if layout == 1 else dims[0]
+            steps.append(GRUStep(hidden=H, in_dim=int(Wa.shape[2]),
                                  linear_before_reset=int(a.get("linear_before_reset", 0)),
-                                 w_np=W, r_np=R, b_np=B, seq=int(dims[0]) if dims[0] > 0 else 0))
-            width = H
+                                 w_np=Wa[0], r_np=Ra[0], b_np=Ba[0], seq=int(seq) if seq > 0 else 0,
+                                 reverse=direction == "reverse", layout=layout, bidirectional=D == 2,
+                                 w_rev_np=Wa[1] if D == 2 else None, r_rev_np=Ra[1] if D == 2 else None,
+                                 b_rev_np=Ba[1] if D == 2 else None))
+            width = H * D
             # continue on Y (chained GRU) or Y_h (head)
             y, yh = n["outputs"][0], (n["outputs"][1] if len(n["outputs"]) > 1 else "")
             y_used = bool(y) and any(id(c) not in visited for c in _consumers(nodes, y))
+            if D == 2 and y_used:
+                raise PlanError("bidirectional GRU: only the final states (Y_h) are lowered")
+            bidir_pending = D == 2 and layout == 0
             cur = y if y_used else yh
             continue
         raise PlanError(f"op {op} is not lowered to the device")

@@ -130,22 +130,41 @@ def _gru_weights(rng, in_dim: int, hidden: int):
 
 
 def gru(seq: int = 100, in_dim: int = 16, hidden: int = 256, seed: int = 5, layers: int = 2,
-        linear_before_reset: int = 1, head: bool = True):
+        linear_before_reset: int = 1, head: bool = True, direction: str = "forward", layout: int = 0):
+    """GRU sequence classifier. ``direction`` forward / reverse / bidirectional (one layer),
+    ``layout`` 0 ([seq, N, in]) or 1 (batch-major [N, seq, in])."""
     rng = np.random.default_rng(seed)
-    w1, r1, b1 = _gru_weights(rng, in_dim, hidden)
-    wh = (rng.standard_normal((hidden, 1)) * np.sqrt(1.0 / hidden)).astype(np.float32)
+    D = 2 if direction == "bidirectional" else 1
+    if D == 2 and layers != 1:
+        raise ValueError("bidirectional: one layer")
+
+    def weights(i):
+        ws = [_gru_weights(rng, i, hidden) for _ in range(D)]
+        return tuple(np.concatenate([w[k] for w in ws], 0) for k in range(3))
+    w1, r1, b1 = weights(in_dim)
+    wh = (rng.standard_normal((D * hidden, 1)) * np.sqrt(1.0 / (D * hidden))).astype(np.float32)
     bh = np.array([0.0], np.float32)
     lbr = int(linear_before_reset)
-    nodes = [node("GRU", ["input", "W1", "R1", "B1"], ["Y1", "Yh1"], hidden_size=hidden, linear_before_reset=lbr)]
+    attrs = dict(hidden_size=hidden, linear_before_reset=lbr)
+    if direction != "forward":
+        attrs["direction"] = direction
+    if layout:
+        attrs["layout"] = int(layout)
+    nodes = [node("GRU", ["input", "W1", "R1", "B1"], ["Y1", "Yh1"], **attrs)]
+    # Y: layout 0 [seq, D, N, H] -> squeeze axis 1; layout 1 [N, seq, D, H] -> squeeze axis 2
     inits = [tensor("W1", w1), tensor("R1", r1), tensor("B1", b1),
-             tensor("ax1", np.array([1], np.int64)), tensor("shp", np.array([-1, hidden], np.int64))]
+             tensor("ax1", np.array([2 if layout else 1], np.int64)),
+             tensor("shp", np.array([-1, D * hidden], np.int64))]
     last_h = "Yh1"
     if layers == 2:
-        w2, r2, b2 = _gru_weights(rng, hidden, hidden)
+        w2, r2, b2 = weights(hidden)
         nodes += [node("Squeeze", ["Y1", "ax1"], ["X2"]),
-                  node("GRU", ["X2", "W2", "R2", "B2"], ["Y2", "Yh2"], hidden_size=hidden, linear_before_reset=lbr)]
+                  node("GRU", ["X2", "W2", "R2", "B2"], ["Y2", "Yh2"], **attrs)]
         inits += [tensor("W2", w2), tensor("R2", r2), tensor("B2", b2)]
         last_h = "Yh2"
+    if D == 2 and not layout:  # Y_h [2, N, H] -> [N, 2, H] -> [N, 2H]
+        nodes.append(node("Transpose", [last_h], ["hT"], perm=[1, 0, 2]))
+        last_h = "hT"
     if head:
         nodes += [node("Reshape", [last_h, "shp"], ["h"]), node("Gemm", ["h", "Wh", "Bh"], ["logit"]),
                   node("Sigmoid", ["logit"], ["output"])]
@@ -153,9 +172,11 @@ def gru(seq: int = 100, in_dim: int = 16, hidden: int = 256, seed: int = 5, laye
         out_vi = value_info("output", S.FLOAT, ["N", 1])
     else:
         nodes.append(node("Reshape", [last_h, "shp"], ["output"]))
-        out_vi = value_info("output", S.FLOAT, ["N", hidden])
-    return model(nodes, [value_info("input", S.FLOAT, [seq, "N", in_dim])], [out_vi], inits, name="abuse_gru",
-                 metadata={"family": "gru", "layers": str(layers), "hidden": str(hidden), "seq": str(seq)})
+        out_vi = value_info("output", S.FLOAT, ["N", D * hidden])
+    x_dims = ["N", seq, in_dim] if layout else [seq, "N", in_dim]
+    return model(nodes, [value_info("input", S.FLOAT, x_dims)], [out_vi], inits, name="abuse_gru",
+                 metadata={"family": "gru", "layers": str(layers), "hidden": str(hidden), "seq": str(seq),
+                           "direction": direction, "layout": str(layout)})
 
 
 BUILDERS = {"logistic": logistic, "gbdt": gbdt, "stacked": stacked, "ltv_mlp": ltv_mlp, "gru": gru}

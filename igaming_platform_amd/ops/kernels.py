@@ -194,13 +194,8 @@ def update_segments(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int,
 
 
 # --------------------------------------------------------------------------- K2
-def tree_ensemble(tp, X: torch.Tensor, out: Optional[torch.Tensor], n_rows: int,
-                  partial: Optional[torch.Tensor] = None, groups: int = 1, no_finish: bool = False,
-                  trace: Optional[torch.Tensor] = None, ens: Optional[dict] = None) -> None:
-    """``tp``: models.plan.TreeStep with device tensors. ``trace``: int64 [64] phase timestamps
-    (wall_clock64) of 8 sample workgroups, for tools/tree_bench.py. ``ens``
-    (:func:`ensemble_args` with ``ml`` = ``out``, grouped launches only): the scorer's K5
-    ensemble runs in the finish kernel's epilogue."""
+def _tree_dict(tp, X: torch.Tensor, out: Optional[torch.Tensor], n_rows: int, partial, groups: int,
+               no_finish: bool, trace, ens) -> dict:
     dev = X.device
     if tp.k not in (1, 2, 4, 8, 16, 32, 64):
         raise ValueError(f"tree kernel built for K in 1,2,4,8,16,32,64; got {tp.k}")
@@ -229,7 +224,41 @@ def tree_ensemble(tp, X: torch.Tensor, out: Optional[torch.Tensor], n_rows: int,
         raise ValueError("leaf table smaller than n_trees * 2^depth * K")
     if tp.n_trees * (1 << tp.depth) * tp.k >= 2 ** 31:
         raise ValueError("leaf table too large for the kernel's 32-bit offsets")
-    _mod().tree_ensemble(d, _stream())
+    return d
+
+
+def tree_ensemble(tp, X: torch.Tensor, out: Optional[torch.Tensor], n_rows: int,
+                  partial: Optional[torch.Tensor] = None, groups: int = 1, no_finish: bool = False,
+                  trace: Optional[torch.Tensor] = None, ens: Optional[dict] = None) -> None:
+    """``tp``: models.plan.TreeStep with device tensors. ``trace``: int64 [64] phase timestamps
+    (wall_clock64) of 8 sample workgroups, for tools/tree_bench.py. ``ens``
+    (:func:`ensemble_args` with ``ml`` = ``out``, grouped launches only): the scorer's K5
+    ensemble runs in the finish kernel's epilogue."""
+    _mod().tree_ensemble(_tree_dict(tp, X, out, n_rows, partial, groups, no_finish, trace, ens), _stream())
+
+
+def tree_head_ok(tp, hs, groups: int) -> bool:
+    """Whether :func:`tree_head` runs this tree -> head pair in one launch (K = 32 leaf vectors
+    without a post transform, grouped, f32 head with k_pad 32)."""
+    return (tp.layout != "sparse" and tp.k == 32 and 1 < groups <= 16 and tp.post == 0 and tp.binary_class < 0
+            and hs.k == 32 and hs.w1.dtype == torch.float32 and hs.w1.shape[1] == 32 and 0 < hs.n1 <= 512
+            and ACT.get(hs.act1, -1) in (0, 1, 2, 3))
+
+
+def tree_head(tp, hs, X: torch.Tensor, Y: torch.Tensor, n_rows: int, partial: torch.Tensor, groups: int,
+              tile_cnt: torch.Tensor, m_ptr: Optional[torch.Tensor] = None, ens: Optional[dict] = None) -> None:
+    """K2 -> K3 -> K5 of the stacked model in ONE launch (trees.hip tree_head_kernel): the
+    grouped tree ensemble's last-arriving block per 64-row tile reduces the tile's group
+    partials and runs the f32 head and the fused ensemble on it. ``tile_cnt``: int32 zeros,
+    one per 64-row tile (the kernel leaves them zero)."""
+    if not tree_head_ok(tp, hs, groups):
+        raise ValueError("tree_head: unsupported tree / head shapes")
+    if tile_cnt.dtype != torch.int32 or tile_cnt.numel() < -(-n_rows // 64) or tile_cnt.device != X.device:
+        raise ValueError("tree_head: tile counters")
+    dt = _tree_dict(tp, X, None, n_rows, partial, groups, True, None, None)
+    dt["tile_cnt"] = tile_cnt.data_ptr()
+    dh = _head_dict(hs, None, Y, n_rows, m_ptr, (partial, groups, tp), None, ens)
+    _mod().tree_head(dt, dh, _stream())
 
 
 def tree_sparse(tp, X: torch.Tensor, out: torch.Tensor, n_rows: int, partial: Optional[torch.Tensor] = None,
@@ -296,6 +325,10 @@ def mlp_head(hs, X: Optional[torch.Tensor], Y: torch.Tensor, M: int, m_ptr: Opti
     group partials [groups, M, K]; the head reduces them while staging (no finisher launch).
     ``ens``: :func:`ensemble_args` of the scorer's K5 on this Y (model column 0): the head's
     epilogue runs the ensemble of its rows, replacing the standalone ensemble launch."""
+    _mod().mlp_head(_head_dict(hs, X, Y, M, m_ptr, tree_partial, trace, ens), _stream())
+
+
+def _head_dict(hs, X, Y, M, m_ptr, tree_partial, trace, ens) -> dict:
     if tree_partial is not None:
         slab, groups, ts = tree_partial
         if ts.k != hs.k or slab.numel() < groups * M * hs.k or ts.post != 0 or ts.binary_class >= 0:
@@ -331,7 +364,7 @@ def mlp_head(hs, X: Optional[torch.Tensor], Y: torch.Tensor, M: int, m_ptr: Opti
         if ens["n_rows"] > M:
             raise ValueError("mlp_head: fused ensemble covers more rows than the head")
         d["ens"] = ens
-    _mod().mlp_head(d, _stream())
+    return d
 
 
 # --------------------------------------------------------------------------- K5 / K10
@@ -412,9 +445,11 @@ def pack_fragments(w, k_pad: int) -> torch.Tensor:
 class GruPack:
     """Device weights of a 1-2 layer GRU chain (+ optional N=1 head) for the K4 kernel."""
 
-    def __init__(self, layers, head=None, device="cuda", split: bool = False):
+    def __init__(self, layers, head=None, device="cuda", split: bool = False, reverse: bool = False):
         """``split``: f32-faithful mode (gru.hip layer_step_x3): each weight also as its bf16
-        residual w - bf16(w); the kernel runs three MFMAs per product on (hi, lo) pairs."""
+        residual w - bf16(w); the kernel runs three MFMAs per product on (hi, lo) pairs.
+        ``reverse``: ONNX direction=reverse for every layer (the kernels read the sequence last
+        step first: forward recurrences over the time-reversed input give the same states)."""
         import numpy as np
         if not 1 <= len(layers) <= 2:
             raise ValueError("gru: 1 or 2 stacked layers are lowered")
@@ -428,6 +463,7 @@ class GruPack:
         if len({int(l.linear_before_reset) for l in layers}) != 1:
             raise ValueError("gru: layers must share linear_before_reset")
         self.H, self.I, self.n_layers = H, layers[0].in_dim, len(layers)
+        self.reverse = bool(reverse)
         self.waves = 0
         self.lbr = int(layers[0].linear_before_reset)
         dev = as_device(device)
@@ -518,6 +554,8 @@ def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh
                  ws_trace=_opt(ws_trace, "ws_trace", dtype=torch.int64, min_numel=64 * 8 + 4, device=dev))
     if gp.split:
         d["split"] = 1
+    if gp.reverse:
+        d["reverse"] = 1
     for i, l in enumerate(gp.layers):
         d[f"l{i}_W"] = _need(l["W"], "W", torch.bfloat16, device=dev)
         d[f"l{i}_R"] = _need(l["R"], "R", torch.bfloat16, device=dev)

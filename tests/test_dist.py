@@ -235,3 +235,14 @@ def test_multi_ingress_every_rank_ingests_and_matches_single_process(world):
     assert next(m[4] for m in msgs if m[0] == "ok") == per_owner
     served = {m[1]: m[4] for m in msgs if m[0] == "ingress"}
     assert [served[r] for r in range(1, world)] == per_owner[1:]
+
+
+def test_exchange_stream_plan_fits_four_hardware_queues():
+    """The exchange pipeline's stream -> hardware-queue map (engine/dp.py stream_roles): the
+    default layout uses 4 distinct streams (= GPU_MAX_HW_QUEUES on the boxes); the 5-stream A/B
+    layout is documented as over budget."""
+    from igaming_platform_amd.engine import dp as DP
+    assert set(DP.stream_roles("3").values()) == {"default", "copy", "state", "model"}
+    assert len(set(DP.stream_roles("3").values())) == DP.HW_QUEUES
+    assert len(set(DP.stream_roles("5").values())) > DP.HW_QUEUES
+    assert DP.EXCHANGE_COMMUNICATORS == 2

@@ -159,3 +159,22 @@ def test_exchange_kernels_multi_sender_layout(world, C):
     got = send.cpu().numpy().reshape(world, C * 136)
     mask = scatter_results(np.ones((n, 2), np.uint32), np.ones(n, FEATREC), route_ref, world, C) != 0
     np.testing.assert_array_equal(got[mask], want[mask])
+
+
+def test_exchange_rank_fits_the_hardware_queue_budget():
+    """one exchange rank runs on at most GPU_MAX_HW_QUEUES (4) distinct
+    streams, default stream included, and owns exactly two communicators (the exchange's rows
+    and results RcclComms); no torch NCCL process group is created (engine/dp.py stream map)."""
+    import torch
+    import torch.distributed as dist
+    from igaming_platform_amd.engine import dp as DP
+    from igaming_platform_amd.parallel.exchange import rccl_comms
+    cfg, pop, mk_store, plan, dev = _setup()
+    sc = DP.DpGpuScorer(cfg, mk_store(), rccl_comms(0, 1), world=1, rank=0, senders=1, cbuckets=[64, 256],
+                        plan=plan, model="plan", device=dev, pipeline_depth=3)
+    sc.capture()
+    m = sc.stream_map()
+    assert len(set(m.values())) == len(set(DP.stream_roles().values())) <= DP.HW_QUEUES == 4
+    assert m["rows_a2a"] == m["h2d"] and m["results_a2a"] == m["model"]  # the collectives share streams
+    assert len(sc.comms) == DP.EXCHANGE_COMMUNICATORS == 2
+    assert not dist.is_initialized() or dist.get_backend() != "nccl"

@@ -378,3 +378,34 @@ def test_gpu_watchdog_quarantines_stalled_batch_then_drains():
         assert int(g["tx_sum_1h"]) == int(c["tx_sum_1h"])
     r2 = eng.score(txs, now=NOW + 3)
     assert [x["score"] for x in r2] == [x["score"] for x in ref.score(txs, now=NOW + 3)]
+
+
+@pytest.mark.parametrize("bucket", [8192, 1024])
+def test_tree_head_one_launch_matches_two_kernels(monkeypatch, bucket):
+    """cfg3 in one launch (trees.hip tree_head_kernel: the tile's last-arriving group block
+    runs the f32 head + K5) gives bit-identical result records, model outputs and metrics to
+    the tree kernel + mlp_head_f32 pair (IGP_TREE_HEAD=0), for full and partial batches; 8192
+    rows run 4 tree groups, 1024 rows 12 (two reduction rounds)."""
+    import torch
+    from igaming_platform_amd.engine.runner import tree_groups
+    from igaming_platform_amd.utils import benchkit
+    from igaming_platform_amd.utils.synth import NOW0, make_requests
+    dev = torch.device("cuda", 0)
+    monkeypatch.setenv("IGP_TREE_HEAD", "0")
+    A = benchkit.build("cfg3", bucket, 1 << 16, dev, depth=2, history_batches=2, hot_frac=0.1)
+    monkeypatch.setenv("IGP_TREE_HEAD", "1")
+    B = benchkit.build("cfg3", bucket, 1 << 16, dev, depth=2, history_batches=2, hot_frac=0.1)
+    step = B.scorer.slots[0].model.plan.steps[0]
+    assert tree_groups(step, bucket) == (4 if bucket == 8192 else 12)
+    rng = np.random.default_rng(21)
+    for i, n in enumerate((bucket, bucket - 777, bucket, 33)):
+        r = make_requests(A.pop, n, rng, NOW0, hot_frac=0.1)
+        ra, _ = A.scorer.wait(A.scorer.submit(r, now=NOW0 + i), unpack=False)
+        rb, _ = B.scorer.wait(B.scorer.submit(r, now=NOW0 + i), unpack=False)
+        np.testing.assert_array_equal(ra, rb)
+        torch.cuda.synchronize()
+        sa, sb = A.scorer.slots[A.scorer._cur], B.scorer.slots[B.scorer._cur]
+        assert torch.equal(sa.res, sb.res)
+        assert torch.equal(sa.model.step_out[-1][:n], sb.model.step_out[-1][:n])
+        assert int(sb.model.tile_cnt.abs().sum()) == 0  # every tile's counter back at zero
+    assert torch.equal(A.scorer.metrics, B.scorer.metrics)

@@ -36,6 +36,30 @@ def test_gru_dense_input_matches_executor(kw):
         assert np.abs(got - ref).mean() < 2e-3
 
 
+@pytest.mark.parametrize("kw", [
+    dict(seq=20, hidden=256, layers=2, linear_before_reset=1, direction="reverse"),
+    dict(seq=16, hidden=128, layers=1, linear_before_reset=0, direction="bidirectional"),
+    dict(seq=12, hidden=64, layers=2, linear_before_reset=1, layout=1),
+    dict(seq=12, hidden=64, layers=1, linear_before_reset=1, direction="bidirectional", layout=1),
+])
+def test_gru_directions_and_layout_match_executor(kw):
+    """reverse (K4 reading the sequence last step first), bidirectional (a
+    forward and a reverse launch + the head over [N, 2H]) and layout-1 GRUs on the device vs the
+    fp32 executor, split (f32-faithful) numerics."""
+    import torch
+    from igaming_platform_amd.engine.runner import DeviceModel
+    N, m, plan = _model(**kw)
+    T, I = kw["seq"], 16
+    rng = np.random.default_rng(3)
+    for rows in (7, 700):
+        X = rng.standard_normal((T, rows, I)).astype(np.float32)
+        feed = np.ascontiguousarray(X.transpose(1, 0, 2)) if kw.get("layout") else X
+        ref = N.Executor(m).run({"input": feed})["output"]
+        dm = DeviceModel(plan, "cuda", [rows])
+        got = dm.run(torch.from_numpy(feed).cuda(), rows)[:rows].cpu().numpy().reshape(ref.shape)
+        np.testing.assert_allclose(got, ref, rtol=0, atol=1e-4)
+
+
 def test_gru_event_ring_input_matches_executor():
     import torch
     from igaming_platform_amd.config import FeatureConfig
