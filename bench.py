@@ -34,6 +34,7 @@ import time
 
 import numpy as np
 
+DATA_PG = None  # replicas mode: the RCCL group of the results all-gather (None: the default group)
 BASELINE_P99_MS = 50.0  # README.md:58 "< 50ms latency" (the only published number)
 
 CONFIGS = ("cfg3", "cfg2", "cfg1", "heuristic", "cfg4", "cfg5")  # igaming_platform_amd/utils/benchkit.py
@@ -68,7 +69,7 @@ def parse():
                          "owner-routed RCCL exchange steps for N > 1, GPU pipeline) -> response bytes with the "
                          "FeatureVector, every rank ingesting; engine_only: pre-resolved ReqRec rows into the "
                          "device pipeline (device-pipeline number); e2e / grpc: tools/bench_e2e.py")
-    ap.add_argument("--threads", type=int, default=12, help="serving scope: ingress threads per rank")
+    ap.add_argument("--threads", type=int, default=16, help="serving scope: ingress threads per rank (the box gives each GPU 16 CPUs)")
     ap.add_argument("--requests", type=int, default=0, help="serving scope: transactions per ScoreBatch request "
                     "(default: the config's micro-batch)")
     ap.add_argument("--rpc", default="batch", choices=["batch", "tx"], help="--scope grpc: ScoreBatch or unary "
@@ -136,23 +137,31 @@ def main():
     local_dev = local % ndev if backend != "nccl" else local
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-
     from igaming_platform_amd.utils import benchkit
     from igaming_platform_amd.utils.synth import NOW0
+
+    exchange = ((world > 1 and a.dp_mode == "exchange" and a.config not in benchkit.MODEL_CONFIGS
+                 and not (a.stream and not a.no_graphs)) or os.environ.get("IGP_FORCE_EXCHANGE") == "1")
+    if world > 1:
+        if exchange or backend != "nccl":
+            # the exchange moves rows over its own two RCCL communicators; the process group is
+            # only the control plane (barriers, the final max-reduce), on the CPU over gloo: no
+            # third communicator or its stream competes for the 4 hardware queues
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     if a.config in benchkit.MODEL_CONFIGS:
         return model_bench(a, world, rank, dev)
 
     if a.stream and not a.no_graphs:
         return stream_bench(a, world, rank, dev)
-    if (world > 1 and a.dp_mode == "exchange") or os.environ.get("IGP_FORCE_EXCHANGE") == "1":
+    if exchange:
         if dp_bench(a, world, rank, dev) is not None:  # (forced at N = 1: RCCL's single-rank path, for tests)
             return
+    global DATA_PG
+    if world > 1 and backend == "nccl" and dist.get_backend() != "nccl":
+        DATA_PG = dist.new_group(backend="nccl")  # replicas fallback: results all-gather over RCCL
     S = benchkit.build(a.config, a.batch, a.accounts, dev, rank=rank, depth=a.depth,
                        use_graphs=not a.no_graphs, precision=a.numerics)
     sc, pool, B = S.scorer, S.pool, S.batch
@@ -178,10 +187,10 @@ def main():
         if world > 1 and not a.no_gather:
             with torch.cuda.stream(sc.mstream):  # results / metrics live on the model stream
                 gather_work[slot] = dist.all_gather_into_tensor(gathered, sc.slots[slot].res[:B].reshape(-1),
-                                                                async_op=True)
+                                                                async_op=True, group=DATA_PG)
                 if i % 16 == 15:
                     met_sum.copy_(sc.metrics)
-                    dist.all_reduce(met_sum)
+                    dist.all_reduce(met_sum, group=DATA_PG)
                 if p.event is not None:
                     p.event.record(sc.mstream)
         return p
@@ -219,7 +228,7 @@ def main():
     elapsed = time.perf_counter() - t0
     host = sc.driver.stats() if sc.driver is not None else {}
     stats = torch.tensor([elapsed, float(np.percentile(lat, 99)), float(np.percentile(lat, 50))],
-                         dtype=torch.float64, device=dev)
+                         dtype=torch.float64, device=dev if dist.is_initialized() and dist.get_backend() == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
     elapsed, p99, p50 = (float(x) for x in stats.cpu())
@@ -300,7 +309,7 @@ def dp_bench(a, world: int, rank: int, dev) -> None:
     if comms is None:
         err = box.get("err", "communicator set-up timed out")
     if world > 1:
-        bad = torch.tensor([0 if comms is not None else 1], dtype=torch.int32, device=dev)
+        bad = torch.tensor([0 if comms is not None else 1], dtype=torch.int32)  # control plane (gloo, CPU)
         dist.all_reduce(bad, op=dist.ReduceOp.MAX)
         if int(bad.item()):
             print(json.dumps({"warning": "exchange communicators failed; replicas fallback", "rank": rank,
@@ -312,17 +321,11 @@ def dp_bench(a, world: int, rank: int, dev) -> None:
     S = benchkit.build(a.config, a.batch, a.accounts, dev, rank=rank, depth=a.depth, precision=a.numerics,
                        dp=dict(world=world, comms=comms))
     sc, pool, B, C = S.scorer, S.pool, S.batch, S.chunk
-    met_sum = torch.zeros(128, dtype=torch.int64, device=dev)
 
     def step(i: int, now: int):
         slot = sc.next_slot()
         chunks, n = pool[i % len(pool)]
-        p = sc.submit_chunks(slot, C, now, chunks, n=n)
-        if world > 1 and i % 16 == 15:  # device metrics of every shard summed (feeds /metrics in serving)
-            with torch.cuda.stream(sc.mstream):
-                met_sum.copy_(sc.metrics)
-                dist.all_reduce(met_sum)
-        return p
+        return sc.submit_chunks(slot, C, now, chunks, n=n)
 
     # probe: two steps under a deadline (event wait; past it the communicators are aborted), so a
     # broken or hung exchange on a new node falls back to replicas instead of hanging the bench
@@ -334,7 +337,7 @@ def dp_bench(a, world: int, rank: int, dev) -> None:
         ok, err = 0, f"{type(e).__name__}: {e}"
         sc.abort_exchange()
     if world > 1:
-        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+        flag = torch.tensor([ok], dtype=torch.int32)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         ok = int(flag.item())
     if not ok:
@@ -371,14 +374,17 @@ def dp_bench(a, world: int, rank: int, dev) -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     host = sc.xdriver.stats()
-    stats = torch.tensor([elapsed, float(np.percentile(lat, 99)), float(np.percentile(lat, 50))],
-                         dtype=torch.float64, device=dev)
-    total = torch.tensor([rows], dtype=torch.int64, device=dev)
-    over = torch.tensor([sc.route_overflow(s, C) for s in range(sc.depth)], dtype=torch.int64, device=dev)
+    stats = torch.tensor([elapsed, float(np.percentile(lat, 99)), float(np.percentile(lat, 50))], dtype=torch.float64)
+    total = torch.tensor([rows], dtype=torch.int64)
+    over = torch.tensor([sc.route_overflow(s, C) for s in range(sc.depth)], dtype=torch.int64)
+    # device metrics of every shard, summed once after the timed window over the control plane
+    # (in serving they feed /metrics through the core's own counters)
+    met = sc.metrics.cpu()
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
         dist.all_reduce(total)
         dist.all_reduce(over)
+        dist.all_reduce(met)
     elapsed, p99, p50 = (float(x) for x in stats.cpu())
     total = int(total.item())
     out = {
@@ -392,6 +398,8 @@ def dp_bench(a, world: int, rank: int, dev) -> None:
                    "driver": "native exchange (XchgDriver; two RCCL all-to-alls per step"
                              + (", captured in the hipGraphs)" if sc.captured else ", issued by the driver)"),
                    "dp_mode": "exchange", "chunk_capacity": C, "rows_scored": total,
+                   "rows_scored_device_metrics": int(met[106]),
+                   "control_plane": "gloo (CPU)" if world > 1 else "none",
                    "rows_dropped_by_route": int(over.sum().item()),
                    "numerics": numerics_desc(a),
                    # collective / queue knobs in effect, so a scaling curve is self-describing

@@ -64,6 +64,11 @@ class GruModel:
     def has_head(self) -> bool:
         return self.head is not None
 
+    @property
+    def split(self) -> bool:
+        """f32-faithful (bf16 hi/lo, three MFMAs per product) weights."""
+        return self.packs[0].split
+
     def run(self, n_rows: int, T: int, out: torch.Tensor, X: Optional[torch.Tensor] = None, store=None,
             slots: Optional[torch.Tensor] = None, m_ptr: Optional[torch.Tensor] = None) -> None:
         """``out``: [rows] probabilities with a head, else [rows, H * directions] final states."""
