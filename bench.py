@@ -485,7 +485,9 @@ def serving_bench(a) -> None:
         node = SpmdNode(cfg, comm, kind, n_acc + 4096, _load_onnx(fm), "onnx",
                         Blacklist(cfg.gpu.blacklist_capacity), IPIntel(cfg.gpu.blacklist_capacity))
         core, registry, backend = node.core, node.registry, node.local
-        mode = "native serving core per rank, owner-routed RCCL exchange (every rank ingests)"
+        mode = ("native serving core per rank, owner-routed RCCL exchange (every rank ingests), results via "
+                + ("per-GPU D2H into node-shared pinned memory" if node.results_mode == "d2h"
+                   else "the result all-to-all"))
     if core is None:
         raise RuntimeError("no native serving core (IGP native driver disabled?)")
     # this rank's accounts: the global population is world x n_acc UUIDs; a rank loads the

@@ -9,7 +9,7 @@
 #pragma once
 #include <stdint.h>
 
-#define IGP_DEVICE_OPS_ABI 3
+#define IGP_DEVICE_OPS_ABI 4
 
 #ifdef __cplusplus
 extern "C" {
@@ -33,11 +33,16 @@ typedef struct IgpDeviceOps {
   // block until the slot's batch completed: 0 ok, 1 timeout (timeout_us >= 0), -1 error
   int32_t (*wait)(void* ctx, int32_t slot, int64_t timeout_us, char* err, int32_t errlen);
   // results of the slot's last batch. exchange == 0: ResultRec[n] and FeatRec[n] (features may
-  // be null when not requested). exchange == 1: the returned chunks, [world][cap * W] bytes
+  // be null when not requested). exchange == 1: the returned chunks, [world][cap * W] bytes (or
+  // res_owner_stride apart)
   // with W = 8 (+128 with features): cap ResultRec, then cap FeatRec per owner; features()
   // is unused.
   const void* (*results)(void* ctx, int32_t slot);
   const void* (*features)(void* ctx, int32_t slot);
+  // exchange == 1: bytes from one owner's chunk to the next in results() (0: cap * W, the
+  // chunks back to back). The per-GPU D2H result path hands out a node-shared region laid out
+  // [owner][sender][cap * W], so a sender's chunks are world * cap * W apart.
+  int64_t res_owner_stride;
 } IgpDeviceOps;
 
 #ifdef __cplusplus

@@ -25,6 +25,7 @@
 #include <dlfcn.h>
 
 #include <chrono>
+#include <algorithm>
 #include <thread>
 #include <cstring>
 #include <memory>
@@ -263,6 +264,7 @@ class XchgDriver {
     ev_.resize(6 * depth);
     for (auto& e : ev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event create");
     done_recorded_.assign(depth, false);
+    gen_.assign(size_t(depth), 0);
     slots_.resize(depth);
     // A/B experiment at world 1 only: device copies instead of the RCCL all-to-alls
     const char* co = getenv("IGP_XCHG_COPY_ONLY");
@@ -362,9 +364,18 @@ class XchgDriver {
         return -1;
       }
       hipEvent_t e = d->E(slot, 5);
+      const auto t_start = std::chrono::steady_clock::now();
+      auto owners = [&]() -> int32_t {
+        if (!d->rshm_) return 0;
+        int64_t left = -1;
+        if (timeout_us >= 0)
+          left = std::max<int64_t>(0, timeout_us - std::chrono::duration_cast<std::chrono::microseconds>(
+                                                       std::chrono::steady_clock::now() - t_start).count());
+        return d->wait_owners(slot, left, err, errlen);
+      };
       if (timeout_us < 0) {
         const hipError_t r = hipEventSynchronize(e);
-        if (r == hipSuccess) return 0;
+        if (r == hipSuccess) return owners();
         if (err && errlen > 0) {
           std::strncpy(err, hipGetErrorString(r), size_t(errlen) - 1);
           err[errlen - 1] = 0;
@@ -374,7 +385,7 @@ class XchgDriver {
       const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
       for (int spin = 0;; ++spin) {
         const hipError_t q = hipEventQuery(e);
-        if (q == hipSuccess) return 0;
+        if (q == hipSuccess) return owners();
         if (q != hipErrorNotReady) {
           if (err && errlen > 0) {
             std::strncpy(err, hipGetErrorString(q), size_t(errlen) - 1);
@@ -387,14 +398,59 @@ class XchgDriver {
       }
     };
     ops_.results = [](void* ctx, int32_t slot) -> const void* {
-      return static_cast<XchgDriver*>(ctx)->slots_[slot].host_rr;
+      auto* d = static_cast<XchgDriver*>(ctx);
+      if (d->rshm_) return d->rshm_ + size_t(slot) * d->rshm_slot_stride_ + size_t(d->rank_) * d->ops_C_ * kResFeatW;
+      return d->slots_[slot].host_rr;
     };
     ops_.features = [](void*, int32_t) -> const void* { return nullptr; };
+    ops_.res_owner_stride = rshm_ ? int64_t(rshm_owner_stride_) : 0;
     return reinterpret_cast<uintptr_t>(&ops_);
+  }
+
+  // Per-GPU D2H result path (instead of the result all-to-all): every owner copies its scored
+  // rows for ALL senders ([sender][C][W], the scatter's layout) into its block of a node-shared
+  // pinned host region [slot][owner][sender][C][W]; a sender reads its chunk of every owner's
+  // block. Completion is two-level: the slot's local event (this rank's D2H landed), then one
+  // release-published generation per (slot, owner) in the region's flag lines, polled until
+  // every owner reached the step. Reuse of a block is ordered by the next step's row
+  // all-to-all (no owner can copy step k + depth before every sender issued it, i.e. finished
+  // reading step k). The copy itself is a node of the captured model graph (engine/dp.py).
+  void set_results_shm(uintptr_t base, size_t slot_stride, size_t owner_stride, uintptr_t flags, int rank) {
+    if (!base || !flags || rank < 0 || rank >= world_) throw std::runtime_error("XchgDriver: results region");
+    rshm_ = reinterpret_cast<char*>(base);
+    rshm_slot_stride_ = slot_stride;
+    rshm_owner_stride_ = owner_stride;
+    rflags_ = reinterpret_cast<int64_t*>(flags);
+    rank_ = rank;
+    // a driver replacing another on the same region (model hot reload, every rank paused at the
+    // same step): continue from the generation this owner published last
+    for (int s = 0; s < depth_; ++s)
+      gen_[size_t(s)] = __atomic_load_n(&rflags_[(size_t(s) * world_ + rank_) * 8], __ATOMIC_ACQUIRE);
+  }
+
+  // d2h mode, inside wait(slot): publish this owner's generation, then wait for every owner's
+  int32_t wait_owners(int slot, int64_t timeout_us, char* err, int32_t errlen) {
+    const int64_t g = gen_[size_t(slot)];
+    __atomic_store_n(&rflags_[(size_t(slot) * world_ + rank_) * 8], g, __ATOMIC_RELEASE);
+    const auto t_end = timeout_us >= 0 ? std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us)
+                                       : std::chrono::steady_clock::time_point::max();
+    for (int spin = 0;; ++spin) {
+      bool all = true;
+      for (int o = 0; o < world_ && all; ++o)
+        all = __atomic_load_n(&rflags_[(size_t(slot) * world_ + o) * 8], __ATOMIC_ACQUIRE) >= g;
+      if (all) return 0;
+      if (std::chrono::steady_clock::now() >= t_end) {
+        if (timeout_us < 0 && err && errlen > 0) std::strncpy(err, "results region: owner never published", size_t(errlen) - 1);
+        return 1;
+      }
+      if (spin > 4096) std::this_thread::sleep_for(std::chrono::microseconds(5));
+    }
   }
 
   void submit_impl(int slot, int C, int seq, int64_t now, uintptr_t src, size_t nbytes, bool with_features) {
     auto it = graphs_.find(key(C, slot));
+    ++gen_[size_t(slot)];  // every rank submits the same steps on the same slots: the same generations
+    if (rshm_ && !captured_) throw std::runtime_error("XchgDriver: the D2H result path needs the captured graphs");
     if (it == graphs_.end()) throw std::runtime_error("XchgDriver: no graphs for this chunk capacity / slot");
     const Graphs g = it->second;
     const Slot& sl = slots_[slot];
@@ -550,6 +606,13 @@ class XchgDriver {
   IgpDeviceOps ops_{};
   int ops_C_ = 0;
   int device_ = 0;
+  static constexpr size_t kResFeatW = sizeof(ResultRec) + sizeof(FeatRec);
+  // per-GPU D2H result path (set_results_shm)
+  char* rshm_ = nullptr;
+  size_t rshm_slot_stride_ = 0, rshm_owner_stride_ = 0;
+  int64_t* rflags_ = nullptr;
+  int rank_ = 0;
+  std::vector<int64_t> gen_;
 };
 
 template <class T>
@@ -584,6 +647,7 @@ void register_exchange(py::module_& m) {
       .def("set_ops", &XchgDriver::set_ops)
       .def("set_state_ops", &XchgDriver::set_state_ops)
       .def("set_captured", &XchgDriver::set_captured)
+      .def("set_results_shm", &XchgDriver::set_results_shm)
       .def("submit", &XchgDriver::submit)
       .def("device_ops", &XchgDriver::device_ops)
       .def("wait", &XchgDriver::wait)
@@ -591,6 +655,13 @@ void register_exchange(py::module_& m) {
       .def("state_event", &XchgDriver::state_event)
       .def("done_event", &XchgDriver::done_event)
       .def("stats", &XchgDriver::stats);
+  // page-lock a host range (the node-shared result region of the D2H result path) so device
+  // copies into it are asynchronous DMA and capturable
+  m.def("host_register", [](uintptr_t p, size_t n) {
+    const hipError_t e = hipHostRegister(reinterpret_cast<void*>(p), n, hipHostRegisterDefault);
+    if (e != hipSuccess) throw std::runtime_error(std::string("hipHostRegister: ") + hipGetErrorString(e));
+  });
+  m.def("host_unregister", [](uintptr_t p) { (void)hipHostUnregister(reinterpret_cast<void*>(p)); });
   // kernel launches (captured into the exchange graphs from Python)
   m.def("exchange_compact", [](uintptr_t recv, uintptr_t rows, uintptr_t hdr, uintptr_t route, int N, int C, int cap,
                                uintptr_t stream) {

@@ -635,12 +635,20 @@ PYBIND11_MODULE(_native, m) {
       .def("score_batch", [](PyServe& s, py::bytes data, int64_t now, int64_t t0_ns) {
         char* p; py::ssize_t n;
         PYBIND11_BYTES_AS_STRING_AND_SIZE(data.ptr(), &p, &n);
-        std::string out;
+        std::string_view out;
         {
           py::gil_scoped_release rel;
-          out = s.core->score_batch(p, size_t(n), now, t0_ns);
+          out = s.core->score_batch_view(p, size_t(n), now, t0_ns);
         }
-        return py::bytes(out);
+        // allocate the result object under the GIL, fill it without: the MB-sized copy of a
+        // batch response would otherwise serialise every ingress thread on the GIL
+        PyObject* b = PyBytes_FromStringAndSize(nullptr, py::ssize_t(out.size()));
+        if (!b) throw py::error_already_set();
+        {
+          py::gil_scoped_release rel;
+          if (!out.empty()) std::memcpy(PyBytes_AS_STRING(b), out.data(), out.size());
+        }
+        return py::reinterpret_steal<py::bytes>(b);
       }, py::arg("data"), py::arg("now") = -1, py::arg("t0_ns") = 0)
       .def("score_rows", [](PyServe& s, py::array req, py::object owners, int64_t now, bool want_features) {
         if (req.nbytes() % sizeof(ReqRec)) throw std::runtime_error("score_rows: ReqRec rows expected");

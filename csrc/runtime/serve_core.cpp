@@ -213,14 +213,18 @@ void ServeCore::wait_item(Item* it) {
 }
 
 std::string ServeCore::score_batch(const char* data, size_t n, int64_t now, int64_t t0_ns) {
+  const std::string_view v = score_batch_view(data, n, now, t0_ns);
+  return std::string(v.data(), v.size());
+}
+
+std::string_view ServeCore::score_batch_view(const char* data, size_t n, int64_t now, int64_t t0_ns) {
   const int64_t t0 = t0_ns > 0 ? t0_ns : now_ns();
   thread_local std::vector<wire::TxRow> rows;
   rows.clear();
   const int64_t ta = now_ns();
   wire::parse_batch_rows(data, n, rows);
   const int64_t tb = now_ns();
-  std::string out;
-  if (rows.empty()) return out;
+  if (rows.empty()) return {};
   Item it;
   it.kind = 0;
   it.now = now >= 0 ? now : wall_s();
@@ -237,7 +241,7 @@ std::string ServeCore::score_batch(const char* data, size_t n, int64_t now, int6
   wait_item(&it);
   if (it.failed) throw std::runtime_error("ServeCore: batch failed: " + it.err);
   const int64_t td = now_ns();
-  wire::append_batch_response(out, it.res, it.feat, nullptr, (td - t0) / 1000000, it.n);
+  const std::string_view out = wire::batch_response_scratch(it.res, it.feat, nullptr, (td - t0) / 1000000, it.n);
   const int64_t te = now_ns();
   a_parse_.fetch_add(tb - ta, std::memory_order_relaxed);
   a_resolve_.fetch_add(tc - tb, std::memory_order_relaxed);
@@ -588,7 +592,8 @@ void ServeCore::finish_seg(const Step& st, const Seg& s) {
     return;
   }
   const size_t W = kResBytes + (st.wf ? kFeatBytes : 0);
-  const char* chunk = base + size_t(s.owner) * size_t(cap_) * W;
+  const size_t ostride = dev_->res_owner_stride > 0 ? size_t(dev_->res_owner_stride) : size_t(cap_) * W;
+  const char* chunk = base + size_t(s.owner) * ostride;
   const ResultRec* r = reinterpret_cast<const ResultRec*>(chunk) + s.dev_pos;
   const FeatRec* f = st.wf ? reinterpret_cast<const FeatRec*>(chunk + size_t(cap_) * kResBytes) + s.dev_pos : nullptr;
   const int32_t* perm = it->perm.empty() ? nullptr : it->perm.data() + s.item_pos;

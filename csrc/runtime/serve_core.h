@@ -104,6 +104,9 @@ class ServeCore {
 
   // ScoreBatch: request bytes -> response bytes (blocking; callable from many threads)
   std::string score_batch(const char* data, size_t n, int64_t now, int64_t t0_ns);
+  // the same, the response left in the calling thread's scratch buffer (valid until the
+  // thread's next call): the binding copies it into the Python bytes object without the GIL
+  std::string_view score_batch_view(const char* data, size_t n, int64_t now, int64_t t0_ns);
   // pre-resolved rows (REQREC with slots; owners[] per row when world > 1): results in row order
   void score_rows(const ReqRec* rows, const int32_t* owners, size_t n, int64_t now, bool want_features,
                   ResultRec* res, FeatRec* feat);

@@ -234,20 +234,9 @@ size_t write_tx_response(char* out, const ResultRec& r, const FeatRec* f, int64_
   return size_t(o.p - out);
 }
 
-void append_batch_response(std::string& out, const ResultRec* r, const FeatRec* f, const int64_t* ms, int64_t ms_all,
-                           size_t n) {
-  // worst case per row into an uninitialised per-thread scratch buffer, then one append of
-  // the bytes actually written (a zero-filled resize of the worst case costs more than the
-  // whole serialisation)
-  thread_local std::unique_ptr<char[]> scratch;
-  thread_local size_t scratch_cap = 0;
-  const size_t need = n * (kMaxTxResponse + 8);
-  if (scratch_cap < need) {
-    scratch.reset(new char[need]);
-    scratch_cap = need;
-  }
-  char* const start = scratch.get();
-  char* p = start;
+size_t write_batch_response(char* dst, const ResultRec* r, const FeatRec* f, const int64_t* ms, int64_t ms_all,
+                            size_t n) {
+  char* p = dst;
   char body[kMaxTxResponse];
   for (size_t i = 0; i < n; ++i) {
     const size_t len = write_tx_response(body, r[i], f ? f + i : nullptr, ms ? ms[i] : ms_all);
@@ -257,7 +246,27 @@ void append_batch_response(std::string& out, const ResultRec* r, const FeatRec* 
     o.bytes(body, len);
     p = o.p;
   }
-  out.append(start, size_t(p - start));
+  return size_t(p - dst);
+}
+
+std::string_view batch_response_scratch(const ResultRec* r, const FeatRec* f, const int64_t* ms, int64_t ms_all,
+                                        size_t n) {
+  // worst case per row into an uninitialised, grow-only per-thread buffer (its pages stay
+  // resident across requests: a fresh multi-MB buffer per response pays a page fault per 4 KB)
+  thread_local std::unique_ptr<char[]> scratch;
+  thread_local size_t scratch_cap = 0;
+  const size_t need = n * kMaxBatchRowBytes;
+  if (scratch_cap < need) {
+    scratch.reset(new char[need]);
+    scratch_cap = need;
+  }
+  return std::string_view(scratch.get(), write_batch_response(scratch.get(), r, f, ms, ms_all, n));
+}
+
+void append_batch_response(std::string& out, const ResultRec* r, const FeatRec* f, const int64_t* ms, int64_t ms_all,
+                           size_t n) {
+  const std::string_view v = batch_response_scratch(r, f, ms, ms_all, n);
+  out.append(v.data(), v.size());
 }
 
 std::string serialize_feature_vector(const FeatRec& x) {

@@ -65,6 +65,13 @@ std::string serialize_feature_vector(const FeatRec& f);
 // (tag + length + body) at most kMaxTxResponse + 8.
 constexpr size_t kMaxTxResponse = 1024;
 size_t write_tx_response(char* out, const ResultRec& r, const FeatRec* f, int64_t ms);
+constexpr size_t kMaxBatchRowBytes = kMaxTxResponse + 8;
+// ScoreBatchResponse of n rows written at dst (capacity n * kMaxBatchRowBytes); returns its size
+size_t write_batch_response(char* dst, const ResultRec* r, const FeatRec* f, const int64_t* ms, int64_t ms_all,
+                            size_t n);
+// the same into this thread's grow-only scratch buffer (valid until its next call on the thread)
+std::string_view batch_response_scratch(const ResultRec* r, const FeatRec* f, const int64_t* ms, int64_t ms_all,
+                                        size_t n);
 // ScoreBatchResponse of n rows appended to `out`
 void append_batch_response(std::string& out, const ResultRec* r, const FeatRec* f, const int64_t* ms, int64_t ms_all,
                            size_t n);

@@ -358,10 +358,13 @@ class GpuBackend:
 
     def _make_scorer(self, plan, model: str, depth: int, use_graphs=None):
         if self.exchange is not None:
-            from .dp import DpGpuScorer
+            from .dp import DpGpuScorer, map_results_region
             x = self.exchange
+            if isinstance(x.get("results_shm"), str):  # mapped once; a hot reload's scorer reuses it
+                x["results_shm"] = map_results_region(x["results_shm"], depth, x["world"], max(x["cbuckets"]))
             return DpGpuScorer(self.cfg, self.store, x["comms"], x["world"], self.rank, x["senders"], x["cbuckets"],
-                               plan=plan, model=model, device=self.device, pipeline_depth=depth)
+                               plan=plan, model=model, device=self.device, pipeline_depth=depth,
+                               results_shm=x.get("results_shm"))
         from .scorer import GpuScorer
         return GpuScorer(self.cfg, self.store, plan=plan, model=model, device=self.device, pipeline_depth=depth,
                          owner_filter=self.owner_filter, rank=self.rank, use_graphs=use_graphs)

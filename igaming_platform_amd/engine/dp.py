@@ -49,6 +49,33 @@ HW_QUEUES = 4
 EXCHANGE_COMMUNICATORS = 2
 
 
+def map_results_region(name: str, depth: int, world: int, cmax: int) -> dict:
+    """The node-shared result region of the per-GPU D2H result path (IGP_XCHG_RESULTS=d2h):
+    [depth][owner][sender][cmax][W] result chunks + one 64-B flag line per (slot, owner).
+    Every rank opens the same name (O_CREAT, same size: no creation order needed); the group's
+    creator unlinks it once every rank mapped it. Page-locked, so the owners' device copies into
+    it are asynchronous DMA (and nodes of the captured model graphs)."""
+    import ctypes
+    import mmap
+    W = RES_BYTES + FEAT_BYTES
+    owner_stride = world * cmax * W
+    slot_stride = world * owner_stride
+    data = depth * slot_stride
+    size = data + depth * world * 64
+    path = "/dev/shm/" + name.lstrip("/")
+    fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o600)
+    try:
+        if os.fstat(fd).st_size < size:
+            os.ftruncate(fd, size)
+        mm = mmap.mmap(fd, size)
+    finally:
+        os.close(fd)
+    base = ctypes.addressof(ctypes.c_char.from_buffer(mm))
+    hipk().host_register(base, size)
+    return dict(name=name, path=path, mm=mm, base=base, size=size, owner_stride=owner_stride, slot_stride=slot_stride,
+                flags=base + data, depth=depth, world=world, cmax=cmax)
+
+
 def stream_roles(mode: Optional[str] = None) -> dict:
     """role -> the stream that carries it (``mode``: IGP_XCHG_STREAMS, default "3")."""
     mode = mode if mode is not None else os.environ.get("IGP_XCHG_STREAMS", "3")
@@ -75,7 +102,11 @@ class DpGpuScorer(GpuScorer):
 
     def __init__(self, cfg, store, comms: Sequence, world: int, rank: int, senders: int,
                  cbuckets: Sequence[int], plan=None, model: str = "plan", device=None, pipeline_depth: int = 3,
-                 update_features: bool = True):
+                 update_features: bool = True, results_shm: Optional[str] = None):
+        """``results_shm``: name of a node-shared /dev/shm region for the per-GPU D2H result
+        path (every rank opens the same name; the creator of the group unlinks it once all
+        mapped it): owners copy their results for every sender into it instead of the result
+        all-to-all (IGP_XCHG_RESULTS=d2h, :meth:`_attach_results_shm`)."""
         self.world, self.senders = int(world), int(senders)
         if not 1 <= self.senders <= self.world:
             raise ValueError("senders must be in [1, world]")
@@ -117,6 +148,12 @@ class DpGpuScorer(GpuScorer):
         self.xgraphs = {}
         self.xdriver = None
         self._watch = None
+        self.rshm = None
+        if results_shm:
+            self.rshm = (results_shm if isinstance(results_shm, dict)
+                         else map_results_region(results_shm, self.depth, self.world, self.cbuckets[-1]))
+            if (self.rshm["depth"], self.rshm["world"], self.rshm["cmax"]) != (self.depth, self.world, self.cbuckets[-1]):
+                raise ValueError("results region shape does not match the scorer")
 
     def stream_map(self) -> dict:
         """role -> HIP stream handle actually used by this rank (see :func:`stream_roles`)."""
@@ -182,6 +219,14 @@ class DpGpuScorer(GpuScorer):
 
     def _model_results_body(self, slot: int, C: int, with_features: bool) -> None:
         self._xmodel_body(slot, C, with_features)
+        if self.rshm is not None:
+            # per-GPU D2H: this owner's result chunks for every sender -> its block of the
+            # node-shared region (the senders read their chunk of every owner's block)
+            r, sb = self.rshm, self.slots[slot]
+            hipk().memcpy_async(r["base"] + slot * r["slot_stride"] + self.rank * r["owner_stride"],
+                                sb.rsend.data_ptr(), self.world * C * result_width(with_features),
+                                torch.cuda.current_stream().cuda_stream)
+            return
         self._a2a_results(slot, C, with_features)
 
     def capture(self) -> None:
@@ -256,6 +301,11 @@ class DpGpuScorer(GpuScorer):
                         self._state_body(slot, self.cap(C))
                     d.set_state_ops(C, slot, r.ops)
         d.set_captured(self.captured)
+        if self.rshm is not None:
+            if not self.captured:
+                raise RuntimeError("the D2H result path needs the captured exchange graphs")
+            r = self.rshm
+            d.set_results_shm(r["base"], r["slot_stride"], r["owner_stride"], r["flags"], self.rank)
         self.xdriver = d
         self.driver = None  # the three-graph driver of the single-GPU path is not used here
 

@@ -980,7 +980,8 @@ class DeadShard:
 
 # ============================================================================ shard construction
 def make_local_backend(cfg: Config, kind: str, capacity: int, fm, mkind: str, blacklist, ipintel,
-                       owner_filter: bool = False, rank: int = 0, capture: bool = True, comm=None):
+                       owner_filter: bool = False, rank: int = 0, capture: bool = True, comm=None,
+                       results_shm: Optional[str] = None):
     """The backend of THIS process's shard (used by SPMD rank 0 and by every worker rank).
     ``comm``: the SPMD group; a GPU shard then joins the owner-routed RCCL exchange (two
     communicators of its own, created collectively here) and scores only its own rows."""
@@ -996,6 +997,8 @@ def make_local_backend(cfg: Config, kind: str, capacity: int, fm, mkind: str, bl
             # every rank ingests: each step carries up to C rows per (sender, owner) pair
             exchange = dict(comms=rccl_comms(comm.rank, comm.world), world=comm.world, senders=comm.world,
                             cbuckets=[chunk_capacity(max(cfg.gpu.buckets), comm.world)])
+            if results_shm:  # per-GPU D2H result path instead of the result all-to-all
+                exchange["results_shm"] = results_shm
         return GpuBackend(cfg, capacity, dev, plan=plan, model=model, blacklist=blacklist, ipintel=ipintel,
                           capture=capture, owner_filter=owner_filter, rank=rank, exchange=exchange)
     N = native()
@@ -1099,8 +1102,16 @@ class SpmdNode:
         rank, world = comm.rank, comm.world
         self.rank, self.world = rank, world
         prefix = comm.bcast_bytes(serving.shm_token().encode() if rank == 0 else None, 0).decode()
+        # IGP_XCHG_RESULTS=d2h: results return through a node-shared pinned region (each owner
+        # copies its rows for every sender D2H) instead of the result all-to-all over xGMI
+        self.results_mode = os.environ.get("IGP_XCHG_RESULTS", "a2a")
+        if self.results_mode not in ("a2a", "d2h"):
+            raise ValueError("IGP_XCHG_RESULTS must be a2a or d2h")
+        rshm = f"{prefix}-res" if (backend == "gpu" and self.results_mode == "d2h") else None
+        if backend != "gpu":
+            self.results_mode = "a2a"  # the CPU exchange (/dev/shm) has one result path
         self.local = make_local_backend(cfg, backend, capacity, fm, mkind, blacklist, ipintel, rank=rank,
-                                        capture=capture, comm=comm if backend == "gpu" else None)
+                                        capture=capture, comm=comm if backend == "gpu" else None, results_shm=rshm)
         C = chunk_capacity(max(cfg.gpu.buckets), world)
         op_t = getattr(comm, "op_timeout", None)
         timeout_s = min(cfg.gpu.exchange_timeout_s, op_t.total_seconds()) if op_t else cfg.gpu.exchange_timeout_s
@@ -1125,6 +1136,11 @@ class SpmdNode:
             self.clock.unlink_shared()
             if hasattr(dev, "unlink_shared"):
                 dev.unlink_shared()
+            if rshm:  # every rank mapped it while building its shard (before the barriers)
+                try:
+                    os.unlink("/dev/shm/" + rshm)
+                except FileNotFoundError:
+                    pass
         seq0 = self.local.scorer._seq if self.local.kind == "gpu" else 0
         self.core = serving.make_core(self.registry.index, dev, cfg, rank=rank, clock=self.clock, seq0=seq0)
         self.local.attach_core(self.core)

@@ -81,9 +81,14 @@ def _free_port():
     return p
 
 
-def test_spmd_engine_world1_matches_plain_gpu_engine():
+@pytest.mark.parametrize("results", ["a2a", "d2h"])
+def test_spmd_engine_world1_matches_plain_gpu_engine(monkeypatch, results):
+    """The SPMD serving engine at world 1 (its native core driving the exchange pipeline)
+    answers exactly like the plain GPU engine, with the results returning through the result
+    all-to-all or through the per-GPU D2H copies into the node-shared region (IGP_XCHG_RESULTS)."""
     import torch
     import torch.distributed as dist
+    monkeypatch.setenv("IGP_XCHG_RESULTS", results)
     from igaming_platform_amd.config import Config
     from igaming_platform_amd.engine.risk_engine import RiskEngine
     from igaming_platform_amd.parallel.comm import TorchComm
@@ -95,6 +100,9 @@ def test_spmd_engine_world1_matches_plain_gpu_engine():
         spmd = RiskEngine(cfg, backend="gpu", capacity=1024, spmd=TorchComm("nccl", "cuda:0"))
         plain = RiskEngine(cfg, backend="gpu", capacity=1024)
         assert spmd.local.scorer.__class__.__name__ == "DpGpuScorer"
+        assert (spmd.local.scorer.rshm is not None) == (results == "d2h")
+        if results == "d2h":
+            assert not os.path.exists(spmd.local.scorer.rshm["path"])  # unlinked once every rank mapped it
         rng = np.random.default_rng(2)
         types = ["deposit", "withdraw", "bet", "win"]
         for e in (spmd, plain):
