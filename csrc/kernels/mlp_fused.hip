@@ -34,6 +34,7 @@ typedef __attribute__((ext_vector_type(8))) short mc_bf16x8;
 typedef __attribute__((ext_vector_type(4))) float mc_f32x4;
 
 constexpr int MC_LDA = 512 + 8;  // bf16 elements per LDS row (1040 B)
+constexpr int MC_PF = 5;  // k-steps of weight fragments prefetched ahead (bf16 path; IGP_MC_PF=2: the r2 depth)
 
 __device__ __forceinline__ float mc_act(float v, int act) {
   switch (act) {
@@ -49,7 +50,7 @@ __device__ __forceinline__ float mc_act(float v, int act) {
 // holding W[16 nt + (l & 15)][32 ks + 8 (l >> 4) .. +8], so each B-fragment load is one fully
 // coalesced 1 KB wave read (row-major W made it 16 half-used 128-B lines per instruction and
 // the texture path, not the MFMA, set the pace: 92 -> see profiles/NOTES.md).
-template <int NKS, int MT, int JT, bool SPLIT>
+template <int NKS, int MT, int JT, bool SPLIT, int PFD = MC_PF>
 __device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, const uint16_t* __restrict__ Hlo,
                                              const uint16_t* __restrict__ W, const uint16_t* __restrict__ Wlo, int K,
                                              int colw, int NT, int lane, mc_f32x4 (&acc)[MT][JT]) {
@@ -91,7 +92,11 @@ __device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, c
     }
     return;
   }
-  mc_bf16x8 fb[3][JT];
+  // PF k-steps of B fragments in flight: a k-step is only JT x MT MFMAs (8 x 8 cycles at 8
+  // waves), so covering the ~700-cycle L2 latency needs ~5 steps ahead, not 2
+  constexpr int PF = PFD < NKS ? PFD : NKS - 1;
+  constexpr int RING = PF + 1;
+  mc_bf16x8 fb[RING][JT];
   const int kq = 8 * (lane >> 4);
   const uint16_t* wt = W + ((size_t)(colw >> 4) * NKS) * 512 + lane * 8;  // this wave's first n-tile
   // branch-free: tiles j >= NT (layers narrower than 512) re-load tile NT-1 and their
@@ -103,11 +108,11 @@ __device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, c
 #pragma unroll
     for (int j = 0; j < JT; ++j) dst[j] = *reinterpret_cast<const mc_bf16x8*>(wt + ((size_t)jt[j] + ks) * 512);
   };
-  load(0, fb[0]);
-  if (NKS > 1) load(1, fb[1]);
+#pragma unroll
+  for (int p = 0; p < PF; ++p) load(p, fb[p]);
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
-    if (ks + 2 < NKS) load(ks + 2, fb[(ks + 2) % 3]);
+    if (ks + PF < NKS) load(ks + PF, fb[(ks + PF) % RING]);
     // keep the prefetch at the top of the step: without this fence the scheduler sank each
     // load next to its MFMAs and the loop ran at vmcnt(1) (one load in flight per wave)
     __builtin_amdgcn_sched_barrier(0);
@@ -119,7 +124,7 @@ __device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, c
     for (int j = 0; j < JT; ++j)
 #pragma unroll
       for (int m = 0; m < MT; ++m)
-        acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[ks % 3][j], acc[m][j], 0, 0, 0);
+        acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[ks % RING][j], acc[m][j], 0, 0, 0);
   }
 }
 
@@ -129,7 +134,7 @@ __device__ __forceinline__ void mc_split(float x, uint16_t& hi, uint16_t& lo) {
   lo = f32_to_bf16(x - __uint_as_float((uint32_t)hi << 16));
 }
 
-template <int MC_ROWS, int WAVES, bool SPLIT>
+template <int MC_ROWS, int WAVES, bool SPLIT, int PFD = MC_PF>
 __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
   constexpr int MT = MC_ROWS / 16;            // 16-row MFMA tiles per wave
   constexpr int THREADS = 64 * WAVES;
@@ -202,14 +207,14 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
     const uint16_t* Hlo = H[SPLIT ? 2 + cur : cur];
     const uint16_t* Wl = SPLIT ? a.W_lo[l] : nullptr;
     switch (K >> 5) {  // K-steps of 32 (the host allows 2..16)
-      case 2: mc_layer_mma<2, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
-      case 4: mc_layer_mma<4, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
-      case 6: mc_layer_mma<6, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
-      case 8: mc_layer_mma<8, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
-      case 10: mc_layer_mma<10, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
-      case 12: mc_layer_mma<12, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
-      case 14: mc_layer_mma<14, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
-      default: mc_layer_mma<16, MT, JT, SPLIT>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      case 2: mc_layer_mma<2, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      case 4: mc_layer_mma<4, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      case 6: mc_layer_mma<6, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      case 8: mc_layer_mma<8, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      case 10: mc_layer_mma<10, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      case 12: mc_layer_mma<12, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      case 14: mc_layer_mma<14, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      default: mc_layer_mma<16, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
     }
     const float* bias = a.bias[l];
     const int act = a.act[l];
@@ -287,7 +292,13 @@ void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st) {
       IGP_LAUNCH((mlp_chain_kernel<32, 4, true>), dim3((a.n_rows + 31) / 32), dim3(256), 0, st, a);
     return;
   }
-  if (a.waves == 8)
+  static const int pf = [] {  // same-box A/B of the weight prefetch depth
+    const char* e = getenv("IGP_MC_PF");
+    return e ? atoi(e) : MC_PF;
+  }();
+  if (a.waves == 8 && pf == 2)
+    IGP_LAUNCH((mlp_chain_kernel<32, 8, false, 2>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
+  else if (a.waves == 8)
     IGP_LAUNCH((mlp_chain_kernel<32, 8, false>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
   else if (r == 64)
     IGP_LAUNCH((mlp_chain_kernel<64, 4, false>), dim3((a.n_rows + 63) / 64), dim3(256), 0, st, a);

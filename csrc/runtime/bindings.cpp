@@ -9,6 +9,7 @@
 
 #include "account_index.h"
 #include "audit.h"
+#include "h2grpc.h"
 #include "cpu_device.h"
 #include "cpu_scorer.h"
 #include "serve_core.h"
@@ -82,6 +83,21 @@ py::array_t<T> vec_np(const std::vector<T>& v) { return py::array_t<T>(v.size(),
 struct PyServe {
   std::shared_ptr<ServeCore> core;
   py::object dev;
+};
+
+// the native gRPC server; stopped without the GIL (its cold threads may be waiting for it)
+struct PyGrpc {
+  std::unique_ptr<GrpcServer> srv;
+  py::object core;  // keeps the PyServe (and its device) alive
+  ~PyGrpc() {
+    if (srv) {
+      {
+        py::gil_scoped_release rel;
+        srv->stop();
+      }
+      srv.reset();  // drops the Python callable: with the GIL
+    }
+  }
 };
 
 const IgpDeviceOps* device_ops_of(py::object dev) {
@@ -611,6 +627,61 @@ PYBIND11_MODULE(_native, m) {
     py::gil_scoped_release rel;
     return audit_load_segment(seg, db, schema);
   }, py::arg("segment"), py::arg("db"), py::arg("schema"));
+
+  py::class_<PyGrpc>(m, "GrpcServer")
+      .def(py::init([](py::object core, py::function cold, int cold_threads, int batch_threads) {
+             auto p = std::make_unique<PyGrpc>();
+             std::shared_ptr<ServeCore> c;
+             if (!core.is_none()) {
+               c = core.cast<PyServe&>().core;
+               p->core = core;
+             }
+             // cold RPC: cold(path: str, body: bytes) -> bytes, or (grpc status, message)
+             GrpcServer::ColdFn fn = [cb = py::function(cold)](const std::string& path, std::string body) {
+               py::gil_scoped_acquire g;
+               GrpcReply r;
+               try {
+                 py::object out = cb(py::str(path), py::bytes(body));
+                 if (py::isinstance<py::bytes>(out)) {
+                   r.body = out.cast<std::string>();
+                 } else {
+                   auto t = out.cast<py::tuple>();
+                   r.status = t[0].cast<int>();
+                   r.message = t[1].cast<std::string>();
+                 }
+               } catch (py::error_already_set& e) {
+                 r.status = 13;
+                 r.message = e.what();
+               } catch (const std::exception& e) {
+                 r.status = 13;
+                 r.message = e.what();
+               }
+               return r;
+             };
+             p->srv = std::make_unique<GrpcServer>(c, std::move(fn), cold_threads, batch_threads);
+             return p;
+           }),
+           py::arg("core"), py::arg("cold"), py::arg("cold_threads") = 4, py::arg("batch_threads") = 8)
+      .def("start", [](PyGrpc& s, const std::string& host, int port, int workers) {
+        py::gil_scoped_release rel;
+        return s.srv->start(host, port, workers);
+      }, py::arg("host"), py::arg("port"), py::arg("workers") = 4)
+      .def("stop", [](PyGrpc& s) {
+        py::gil_scoped_release rel;
+        s.srv->stop();
+      })
+      .def("set_hot", [](PyGrpc& s, bool on) { s.srv->set_hot(on); })
+      .def("stats", [](PyGrpc& s) {
+        const auto st = s.srv->stats();
+        py::dict d;
+        d["calls"] = st.calls;
+        d["hot_tx"] = st.hot_tx;
+        d["hot_batch"] = st.hot_batch;
+        d["cold"] = st.cold;
+        d["errors"] = st.errors;
+        d["connections"] = st.connections;
+        return d;
+      });
 
   py::class_<PyServe, std::shared_ptr<PyServe>>(m, "ServeCore")
       .def(py::init([](std::vector<std::shared_ptr<AccountIndex>> idx, py::object dev, int rank,

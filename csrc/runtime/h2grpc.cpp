@@ -1,0 +1,652 @@
+#include "h2grpc.h"
+
+#include <arpa/inet.h>
+#include <dlfcn.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+#include <unordered_map>
+
+namespace igp {
+
+// ---------------------------------------------------------------------------- libnghttp2 (dlopen)
+// The ABI-stable subset of nghttp2.h this server uses (libnghttp2.so.14).
+namespace {
+
+struct NgFrameHd {
+  size_t length;
+  int32_t stream_id;
+  uint8_t type;
+  uint8_t flags;
+  uint8_t reserved;
+};
+struct NgNv {
+  const uint8_t* name;
+  const uint8_t* value;
+  size_t namelen;
+  size_t valuelen;
+  uint8_t flags;
+};
+union NgDataSource {
+  int fd;
+  void* ptr;
+};
+typedef ssize_t (*NgReadCb)(void* session, int32_t stream_id, uint8_t* buf, size_t length, uint32_t* data_flags,
+                            NgDataSource* source, void* user_data);
+struct NgDataProvider {
+  NgDataSource source;
+  NgReadCb read_callback;
+};
+struct NgSettingsEntry {
+  int32_t settings_id;
+  uint32_t value;
+};
+constexpr uint8_t kFrameData = 0, kFrameHeaders = 1, kFlagEndStream = 0x01;
+constexpr uint32_t kDataEof = 0x01, kDataNoEndStream = 0x02;
+constexpr int32_t kSettingsMaxStreams = 0x03, kSettingsInitialWindow = 0x04;
+
+struct Ng {
+  int (*callbacks_new)(void**);
+  void (*callbacks_del)(void*);
+  void (*set_on_begin_headers)(void*, int (*)(void*, const void*, void*));
+  void (*set_on_header)(void*, int (*)(void*, const void*, const uint8_t*, size_t, const uint8_t*, size_t, uint8_t, void*));
+  void (*set_on_data_chunk_recv)(void*, int (*)(void*, uint8_t, int32_t, const uint8_t*, size_t, void*));
+  void (*set_on_frame_recv)(void*, int (*)(void*, const void*, void*));
+  void (*set_on_stream_close)(void*, int (*)(void*, int32_t, uint32_t, void*));
+  int (*server_new)(void**, const void*, void*);
+  void (*session_del)(void*);
+  ssize_t (*mem_recv)(void*, const uint8_t*, size_t);
+  ssize_t (*mem_send)(void*, const uint8_t**);
+  int (*submit_settings)(void*, uint8_t, const NgSettingsEntry*, size_t);
+  int (*submit_response)(void*, int32_t, const NgNv*, size_t, const NgDataProvider*);
+  int (*submit_trailer)(void*, int32_t, const NgNv*, size_t);
+  int (*want_read)(void*);
+  int (*want_write)(void*);
+  int (*set_local_window_size)(void*, uint8_t, int32_t, int32_t);  // optional (nghttp2 >= 1.11)
+};
+
+const Ng& ng() {
+  static Ng n{};
+  static bool loaded = false;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> g(mu);
+  if (loaded) return n;
+  void* h = dlopen("libnghttp2.so.14", RTLD_NOW | RTLD_LOCAL);
+  if (!h) throw std::runtime_error(std::string("grpc server: cannot load libnghttp2: ") + dlerror());
+  auto sym = [&](const char* name) {
+    void* f = dlsym(h, name);
+    if (!f) throw std::runtime_error(std::string("grpc server: libnghttp2 lacks ") + name);
+    return f;
+  };
+#define NG_SYM(field, name) n.field = reinterpret_cast<decltype(n.field)>(sym(name))
+  NG_SYM(callbacks_new, "nghttp2_session_callbacks_new");
+  NG_SYM(callbacks_del, "nghttp2_session_callbacks_del");
+  NG_SYM(set_on_begin_headers, "nghttp2_session_callbacks_set_on_begin_headers_callback");
+  NG_SYM(set_on_header, "nghttp2_session_callbacks_set_on_header_callback");
+  NG_SYM(set_on_data_chunk_recv, "nghttp2_session_callbacks_set_on_data_chunk_recv_callback");
+  NG_SYM(set_on_frame_recv, "nghttp2_session_callbacks_set_on_frame_recv_callback");
+  NG_SYM(set_on_stream_close, "nghttp2_session_callbacks_set_on_stream_close_callback");
+  NG_SYM(server_new, "nghttp2_session_server_new");
+  NG_SYM(session_del, "nghttp2_session_del");
+  NG_SYM(mem_recv, "nghttp2_session_mem_recv");
+  NG_SYM(mem_send, "nghttp2_session_mem_send");
+  NG_SYM(submit_settings, "nghttp2_submit_settings");
+  NG_SYM(submit_response, "nghttp2_submit_response");
+  NG_SYM(submit_trailer, "nghttp2_submit_trailer");
+  NG_SYM(want_read, "nghttp2_session_want_read");
+  NG_SYM(want_write, "nghttp2_session_want_write");
+#undef NG_SYM
+  n.set_local_window_size = reinterpret_cast<decltype(n.set_local_window_size)>(dlsym(h, "nghttp2_session_set_local_window_size"));
+  loaded = true;
+  return n;
+}
+
+NgNv nv(const char* name, const std::string& value) {
+  return NgNv{reinterpret_cast<const uint8_t*>(name), reinterpret_cast<const uint8_t*>(value.data()), std::strlen(name),
+              value.size(), 0};
+}
+
+// grpc-message is percent-encoded (printable ASCII except '%' passes through)
+std::string pct(const std::string& s) {
+  static const char* hex = "0123456789ABCDEF";
+  std::string o;
+  for (unsigned char c : s) {
+    if (c >= 0x20 && c <= 0x7e && c != '%') {
+      o += char(c);
+    } else {
+      o += '%';
+      o += hex[c >> 4];
+      o += hex[c & 15];
+    }
+  }
+  return o;
+}
+
+int64_t mono_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+constexpr uint64_t kTagListen = 1, kTagEvent = 2, kFirstConn = 16;
+constexpr int kWorkerShift = 40;
+constexpr uint64_t kTokenMask = (uint64_t(1) << kWorkerShift) - 1;
+const std::string kPathTx = "/risk.v1.RiskService/ScoreTransaction";
+const std::string kPathBatch = "/risk.v1.RiskService/ScoreBatch";
+
+}  // namespace
+
+// ---------------------------------------------------------------------------- worker
+struct GrpcServer::Worker {
+  struct Stream {
+    std::string path;
+    std::string data;
+    std::string out;  // 5-byte prefix + response message
+    size_t off = 0;
+  };
+  struct Conn {
+    Worker* w = nullptr;
+    uint64_t id = 0;
+    int fd = -1;
+    void* sess = nullptr;
+    std::unordered_map<int32_t, Stream> streams;
+    std::string wbuf;
+    size_t woff = 0;
+    bool epollout = false;
+  };
+  struct Done {
+    uint64_t token;  // hot unary: pending-table token; 0: conn / stream below
+    uint64_t conn;
+    int32_t stream;
+    GrpcReply reply;
+  };
+
+  GrpcServer* srv;
+  int idx;
+  int lfd = -1, ep = -1, evfd = -1;
+  std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns;
+  uint64_t next_conn = kFirstConn;
+  std::unordered_map<uint64_t, std::pair<uint64_t, int32_t>> pending;  // token -> (conn, stream)
+  uint64_t next_token = 1;
+  std::mutex qmu;
+  std::vector<Done> q;
+  std::atomic<bool> stop{false};
+  void* cbs = nullptr;
+
+  Worker(GrpcServer* s, int i) : srv(s), idx(i) {}
+  ~Worker() {
+    for (auto& kv : conns) close_conn_raw(*kv.second);
+    conns.clear();
+    if (cbs) ng().callbacks_del(cbs);
+    if (lfd >= 0) ::close(lfd);
+    if (ep >= 0) ::close(ep);
+    if (evfd >= 0) ::close(evfd);
+  }
+
+  void post(Done&& d) {
+    {
+      std::lock_guard<std::mutex> g(qmu);
+      q.push_back(std::move(d));
+    }
+    const uint64_t one = 1;
+    ssize_t r = ::write(evfd, &one, sizeof one);
+    (void)r;
+  }
+
+  // ---- nghttp2 callbacks (user_data = Conn*)
+  static int on_begin_headers(void*, const void* frame, void* ud) {
+    auto* c = static_cast<Conn*>(ud);
+    const auto* hd = static_cast<const NgFrameHd*>(frame);
+    if (hd->type == kFrameHeaders) c->streams[hd->stream_id];
+    return 0;
+  }
+  static int on_header(void*, const void* frame, const uint8_t* name, size_t namelen, const uint8_t* value,
+                       size_t valuelen, uint8_t, void* ud) {
+    auto* c = static_cast<Conn*>(ud);
+    const auto* hd = static_cast<const NgFrameHd*>(frame);
+    if (hd->type != kFrameHeaders) return 0;
+    if (namelen == 5 && std::memcmp(name, ":path", 5) == 0) {
+      auto it = c->streams.find(hd->stream_id);
+      if (it != c->streams.end()) it->second.path.assign(reinterpret_cast<const char*>(value), valuelen);
+    }
+    return 0;
+  }
+  static int on_data(void*, uint8_t, int32_t sid, const uint8_t* data, size_t len, void* ud) {
+    auto* c = static_cast<Conn*>(ud);
+    auto it = c->streams.find(sid);
+    if (it != c->streams.end()) {
+      if (it->second.data.size() + len > (size_t(64) << 20)) return -902;  // NGHTTP2_ERR_CALLBACK_FAILURE
+      it->second.data.append(reinterpret_cast<const char*>(data), len);
+    }
+    return 0;
+  }
+  static int on_frame(void*, const void* frame, void* ud) {
+    auto* c = static_cast<Conn*>(ud);
+    const auto* hd = static_cast<const NgFrameHd*>(frame);
+    if ((hd->type == kFrameData || hd->type == kFrameHeaders) && (hd->flags & kFlagEndStream))
+      c->w->dispatch(*c, hd->stream_id);
+    return 0;
+  }
+  static int on_close(void*, int32_t sid, uint32_t, void* ud) {
+    static_cast<Conn*>(ud)->streams.erase(sid);
+    return 0;
+  }
+  static ssize_t read_body(void* sess, int32_t sid, uint8_t* buf, size_t len, uint32_t* flags, NgDataSource* src,
+                           void*) {
+    auto* st = static_cast<Stream*>(src->ptr);
+    const size_t n = std::min(len, st->out.size() - st->off);
+    std::memcpy(buf, st->out.data() + st->off, n);
+    st->off += n;
+    if (st->off == st->out.size()) {
+      *flags |= kDataEof | kDataNoEndStream;
+      static const std::string ok = "0";
+      const NgNv tr[1] = {nv("grpc-status", ok)};
+      ng().submit_trailer(sess, sid, tr, 1);
+    }
+    return ssize_t(n);
+  }
+
+  void init(const std::string& host, int port) {
+    const Ng& n = ng();
+    if (n.callbacks_new(&cbs) != 0) throw std::runtime_error("grpc server: nghttp2 callbacks");
+    n.set_on_begin_headers(cbs, on_begin_headers);
+    n.set_on_header(cbs, on_header);
+    n.set_on_data_chunk_recv(cbs, on_data);
+    n.set_on_frame_recv(cbs, on_frame);
+    n.set_on_stream_close(cbs, on_close);
+    lfd = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+    if (lfd < 0) throw std::runtime_error("grpc server: socket");
+    int one = 1;
+    ::setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    ::setsockopt(lfd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof one);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons(uint16_t(port));
+    if (host.empty() || host == "0.0.0.0" || host == "[::]") a.sin_addr.s_addr = htonl(INADDR_ANY);
+    else if (::inet_pton(AF_INET, host == "localhost" ? "127.0.0.1" : host.c_str(), &a.sin_addr) != 1)
+      throw std::runtime_error("grpc server: bad host " + host);
+    if (::bind(lfd, reinterpret_cast<sockaddr*>(&a), sizeof a) != 0)
+      throw std::runtime_error(std::string("grpc server: bind: ") + std::strerror(errno));
+    if (::listen(lfd, 1024) != 0) throw std::runtime_error("grpc server: listen");
+    ep = ::epoll_create1(EPOLL_CLOEXEC);
+    evfd = ::eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    if (ep < 0 || evfd < 0) throw std::runtime_error("grpc server: epoll / eventfd");
+    epoll_event e{};
+    e.events = EPOLLIN;
+    e.data.u64 = kTagListen;
+    ::epoll_ctl(ep, EPOLL_CTL_ADD, lfd, &e);
+    e.data.u64 = kTagEvent;
+    ::epoll_ctl(ep, EPOLL_CTL_ADD, evfd, &e);
+  }
+  int bound_port() const {
+    sockaddr_in a{};
+    socklen_t l = sizeof a;
+    ::getsockname(lfd, reinterpret_cast<sockaddr*>(&a), &l);
+    return ntohs(a.sin_port);
+  }
+
+  void run() {
+    epoll_event evs[64];
+    std::vector<char> rbuf(size_t(256) << 10);
+    while (!stop.load(std::memory_order_relaxed)) {
+      const int n = ::epoll_wait(ep, evs, 64, 100);
+      for (int i = 0; i < n; ++i) {
+        const uint64_t tag = evs[i].data.u64;
+        if (tag == kTagListen) {
+          accept_all();
+        } else if (tag == kTagEvent) {
+          uint64_t v;
+          ssize_t r = ::read(evfd, &v, sizeof v);
+          (void)r;
+          drain_done();
+        } else {
+          auto it = conns.find(tag);
+          if (it == conns.end()) continue;
+          Conn& c = *it->second;
+          bool ok = true;
+          if (evs[i].events & EPOLLIN) ok = read_conn(c, rbuf);
+          if (ok && (evs[i].events & (EPOLLERR | EPOLLHUP)) && !(evs[i].events & EPOLLIN)) ok = false;
+          if (ok) ok = flush(c);
+          if (!ok) close_conn(tag);
+        }
+      }
+    }
+  }
+
+  void accept_all() {
+    for (;;) {
+      const int fd = ::accept4(lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+      if (fd < 0) return;
+      int one = 1;
+      ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+      auto c = std::make_unique<Conn>();
+      c->w = this;
+      c->id = next_conn++;
+      c->fd = fd;
+      const Ng& n = ng();
+      if (n.server_new(&c->sess, cbs, c.get()) != 0) {
+        ::close(fd);
+        continue;
+      }
+      const NgSettingsEntry iv[2] = {{kSettingsMaxStreams, 4096}, {kSettingsInitialWindow, 8u << 20}};
+      n.submit_settings(c->sess, 0, iv, 2);
+      if (n.set_local_window_size) n.set_local_window_size(c->sess, 0, 0, 64 << 20);
+      epoll_event e{};
+      e.events = EPOLLIN;
+      e.data.u64 = c->id;
+      ::epoll_ctl(ep, EPOLL_CTL_ADD, fd, &e);
+      srv->conns_.fetch_add(1, std::memory_order_relaxed);
+      Conn& ref = *c;
+      conns.emplace(c->id, std::move(c));
+      if (!flush(ref)) close_conn(ref.id);
+    }
+  }
+
+  bool read_conn(Conn& c, std::vector<char>& buf) {
+    for (;;) {
+      const ssize_t r = ::read(c.fd, buf.data(), buf.size());
+      if (r == 0) return false;
+      if (r < 0) return errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR;
+      const ssize_t k = ng().mem_recv(c.sess, reinterpret_cast<const uint8_t*>(buf.data()), size_t(r));
+      if (k < 0) return false;
+    }
+  }
+
+  // write what nghttp2 has queued; the remainder waits for EPOLLOUT
+  bool flush(Conn& c) {
+    const Ng& n = ng();
+    auto write_some = [&](const char* p, size_t len) -> size_t {
+      size_t done = 0;
+      while (done < len) {
+        const ssize_t w = ::send(c.fd, p + done, len - done, MSG_NOSIGNAL);
+        if (w < 0) {
+          if (errno == EINTR) continue;
+          if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+          return size_t(-1);
+        }
+        done += size_t(w);
+      }
+      return done;
+    };
+    if (c.woff < c.wbuf.size()) {
+      const size_t w = write_some(c.wbuf.data() + c.woff, c.wbuf.size() - c.woff);
+      if (w == size_t(-1)) return false;
+      c.woff += w;
+      if (c.woff < c.wbuf.size()) return set_out(c, true);
+      c.wbuf.clear();
+      c.woff = 0;
+    }
+    for (;;) {
+      const uint8_t* p = nullptr;
+      const ssize_t len = n.mem_send(c.sess, &p);
+      if (len < 0) return false;
+      if (len == 0) break;
+      const size_t w = write_some(reinterpret_cast<const char*>(p), size_t(len));
+      if (w == size_t(-1)) return false;
+      if (w < size_t(len)) {
+        c.wbuf.assign(reinterpret_cast<const char*>(p) + w, size_t(len) - w);
+        c.woff = 0;
+        return set_out(c, true);
+      }
+    }
+    if (!n.want_read(c.sess) && !n.want_write(c.sess)) return false;
+    return set_out(c, false);
+  }
+  bool set_out(Conn& c, bool on) {
+    if (c.epollout == on) return true;
+    epoll_event e{};
+    e.events = EPOLLIN | (on ? EPOLLOUT : 0u);
+    e.data.u64 = c.id;
+    ::epoll_ctl(ep, EPOLL_CTL_MOD, c.fd, &e);
+    c.epollout = on;
+    return true;
+  }
+
+  void close_conn_raw(Conn& c) {
+    if (c.sess) ng().session_del(c.sess);
+    c.sess = nullptr;
+    if (c.fd >= 0) ::close(c.fd);
+    c.fd = -1;
+  }
+  void close_conn(uint64_t id) {
+    auto it = conns.find(id);
+    if (it == conns.end()) return;
+    ::epoll_ctl(ep, EPOLL_CTL_DEL, it->second->fd, nullptr);
+    close_conn_raw(*it->second);
+    conns.erase(it);
+    srv->conns_.fetch_sub(1, std::memory_order_relaxed);
+  }
+
+  void dispatch(Conn& c, int32_t sid) {
+    auto it = c.streams.find(sid);
+    if (it == c.streams.end()) return;
+    Stream& st = it->second;
+    srv->calls_.fetch_add(1, std::memory_order_relaxed);
+    const std::string& d = st.data;
+    GrpcReply bad;
+    if (d.size() < 5) {
+      bad.status = 13;
+      bad.message = "grpc: missing message frame";
+    } else if (d[0] != 0) {
+      bad.status = 12;
+      bad.message = "grpc: compressed messages are not supported";
+    } else {
+      const uint32_t len = (uint32_t(uint8_t(d[1])) << 24) | (uint32_t(uint8_t(d[2])) << 16) |
+                           (uint32_t(uint8_t(d[3])) << 8) | uint32_t(uint8_t(d[4]));
+      if (size_t(len) + 5 != d.size()) {
+        bad.status = 13;
+        bad.message = "grpc: message length mismatch";
+      }
+    }
+    if (bad.status) {
+      respond(c, sid, bad);
+      return;
+    }
+    const bool hot = srv->hot_.load(std::memory_order_relaxed) && srv->core_;
+    if (hot && st.path == kPathTx) {
+      const uint64_t token = next_token++ & kTokenMask;
+      pending[token] = {c.id, sid};
+      srv->hot_tx_.fetch_add(1, std::memory_order_relaxed);
+      srv->core_->submit_tx(d.data() + 5, d.size() - 5, ServeCore::kSinkTag | (uint64_t(idx) << kWorkerShift) | token,
+                            -1, mono_ns());
+      return;
+    }
+    Job j{idx, c.id, sid, st.path, d.substr(5)};
+    {
+      std::lock_guard<std::mutex> g(srv->jmu_);
+      if (hot && st.path == kPathBatch && srv->n_batch_ > 0) {
+        srv->hot_batch_.fetch_add(1, std::memory_order_relaxed);
+        srv->batch_q_.push_back(std::move(j));
+      } else {
+        srv->cold_n_.fetch_add(1, std::memory_order_relaxed);
+        srv->cold_q_.push_back(std::move(j));
+      }
+    }
+    srv->jcv_.notify_all();
+    st.data.clear();
+    st.data.shrink_to_fit();
+  }
+
+  void respond(Conn& c, int32_t sid, const GrpcReply& r) {
+    auto it = c.streams.find(sid);
+    if (it == c.streams.end()) return;  // the client reset the stream meanwhile
+    Stream& st = it->second;
+    const Ng& n = ng();
+    static const std::string s200 = "200", ct = "application/grpc";
+    if (r.status != 0) {
+      srv->errors_.fetch_add(1, std::memory_order_relaxed);
+      const std::string code = std::to_string(r.status), msg = pct(r.message);
+      const NgNv h[4] = {nv(":status", s200), nv("content-type", ct), nv("grpc-status", code), nv("grpc-message", msg)};
+      n.submit_response(c.sess, sid, h, 4, nullptr);  // Trailers-Only
+      return;
+    }
+    st.out.resize(5 + r.body.size());
+    const uint32_t len = uint32_t(r.body.size());
+    st.out[0] = 0;
+    st.out[1] = char(len >> 24);
+    st.out[2] = char(len >> 16);
+    st.out[3] = char(len >> 8);
+    st.out[4] = char(len);
+    std::memcpy(&st.out[5], r.body.data(), r.body.size());
+    st.off = 0;
+    const NgNv h[2] = {nv(":status", s200), nv("content-type", ct)};
+    NgDataProvider prd{};
+    prd.source.ptr = &st;
+    prd.read_callback = read_body;
+    n.submit_response(c.sess, sid, h, 2, &prd);
+  }
+
+  void drain_done() {
+    std::vector<Done> items;
+    {
+      std::lock_guard<std::mutex> g(qmu);
+      items.swap(q);
+    }
+    std::vector<uint64_t> touched;
+    for (Done& d : items) {
+      uint64_t cid = d.conn;
+      int32_t sid = d.stream;
+      if (d.token) {
+        auto p = pending.find(d.token);
+        if (p == pending.end()) continue;
+        cid = p->second.first;
+        sid = p->second.second;
+        pending.erase(p);
+      }
+      auto it = conns.find(cid);
+      if (it == conns.end()) continue;
+      respond(*it->second, sid, d.reply);
+      touched.push_back(cid);
+    }
+    for (uint64_t cid : touched) {
+      auto it = conns.find(cid);
+      if (it != conns.end() && !flush(*it->second)) close_conn(cid);
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------- server
+GrpcServer::GrpcServer(std::shared_ptr<ServeCore> core, ColdFn cold, int cold_threads, int batch_threads)
+    : core_(std::move(core)), cold_(std::move(cold)), n_cold_(std::max(1, cold_threads)),
+      n_batch_(core_ ? std::max(0, batch_threads) : 0) {
+  ng();  // fail early without libnghttp2
+}
+
+GrpcServer::~GrpcServer() { stop(); }
+
+int GrpcServer::start(const std::string& host, int port, int workers) {
+  if (running_.exchange(true)) throw std::runtime_error("grpc server: already started");
+  workers = std::max(1, workers);
+  int bound = port;
+  for (int i = 0; i < workers; ++i) {
+    auto w = std::make_unique<Worker>(this, i);
+    w->init(host, bound);
+    if (i == 0) bound = w->bound_port();
+    workers_.push_back(std::move(w));
+  }
+  if (core_) {
+    core_->set_sink([this](std::vector<ServeCore::Done>&& outs) {
+      sink_active_.fetch_add(1, std::memory_order_acq_rel);
+      struct Exit {
+        std::atomic<int>& a;
+        ~Exit() { a.fetch_sub(1, std::memory_order_acq_rel); }
+      } exit_guard{sink_active_};
+      if (!running_.load(std::memory_order_acquire)) return;
+      for (auto& d : outs) {
+        const int wi = int((d.tag & ~ServeCore::kSinkTag) >> kWorkerShift);
+        if (wi < 0 || size_t(wi) >= workers_.size()) continue;
+        GrpcReply r;
+        if (!d.err.empty()) {
+          r.status = d.err.find("pb:") != std::string::npos ? 3 : 13;
+          r.message = d.err;
+        } else {
+          r.body = std::move(d.bytes);
+        }
+        workers_[size_t(wi)]->post(Worker::Done{d.tag & kTokenMask, 0, 0, std::move(r)});
+      }
+    });
+  }
+  for (auto& w : workers_) threads_.emplace_back([p = w.get()] { p->run(); });
+  for (int i = 0; i < n_cold_; ++i) threads_.emplace_back([this] { cold_loop(); });
+  for (int i = 0; i < n_batch_; ++i) threads_.emplace_back([this] { batch_loop(); });
+  return bound;
+}
+
+void GrpcServer::stop() {
+  if (!running_.exchange(false)) return;
+  {
+    std::lock_guard<std::mutex> g(jmu_);
+    jstop_ = true;
+  }
+  jcv_.notify_all();
+  for (auto& w : workers_) w->stop.store(true);
+  if (core_) core_->set_sink(nullptr);
+  while (sink_active_.load(std::memory_order_acquire) > 0) std::this_thread::yield();  // a finisher inside the sink
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  threads_.clear();
+  workers_.clear();
+}
+
+void GrpcServer::post(int worker, uint64_t conn, int32_t stream, GrpcReply&& r) {
+  if (worker < 0 || size_t(worker) >= workers_.size()) return;
+  workers_[size_t(worker)]->post(Worker::Done{0, conn, stream, std::move(r)});
+}
+
+void GrpcServer::cold_loop() {
+  for (;;) {
+    Job j;
+    {
+      std::unique_lock<std::mutex> l(jmu_);
+      jcv_.wait(l, [&] { return jstop_ || !cold_q_.empty(); });
+      if (cold_q_.empty()) return;
+      j = std::move(cold_q_.front());
+      cold_q_.pop_front();
+    }
+    GrpcReply r;
+    try {
+      r = cold_(j.path, std::move(j.body));
+    } catch (const std::exception& e) {
+      r.status = 13;
+      r.message = e.what();
+    }
+    post(j.worker, j.conn, j.stream, std::move(r));
+  }
+}
+
+void GrpcServer::batch_loop() {
+  for (;;) {
+    Job j;
+    {
+      std::unique_lock<std::mutex> l(jmu_);
+      jcv_.wait(l, [&] { return jstop_ || !batch_q_.empty(); });
+      if (batch_q_.empty()) return;
+      j = std::move(batch_q_.front());
+      batch_q_.pop_front();
+    }
+    GrpcReply r;
+    try {
+      const std::string_view v = core_->score_batch_view(j.body.data(), j.body.size(), -1, mono_ns());
+      r.body.assign(v.data(), v.size());
+    } catch (const std::exception& e) {
+      r.status = std::strstr(e.what(), "pb:") ? 3 : 13;
+      r.message = e.what();
+    }
+    post(j.worker, j.conn, j.stream, std::move(r));
+  }
+}
+
+GrpcServer::Stats GrpcServer::stats() const {
+  return Stats{calls_.load(), hot_tx_.load(), hot_batch_.load(), cold_n_.load(), errors_.load(), conns_.load()};
+}
+
+}  // namespace igp

@@ -303,14 +303,37 @@ void ServeCore::submit_tx(const char* data, size_t n, uint64_t tag, int64_t now,
     resolve_rows(rows, it);
     enqueue(it);
   } catch (const std::exception& e) {
-    Done d{tag, std::string(), e.what()};
+    std::vector<Done> d;
+    d.push_back(Done{tag, std::string(), e.what()});
     delete it;
-    {
-      std::lock_guard<std::mutex> g(out_mu_);
-      outq_.push_back(std::move(d));
-    }
-    out_cv_.notify_one();
+    deliver(std::move(d));
   }
+}
+
+void ServeCore::deliver(std::vector<Done>&& outs) {
+  Sink sink;
+  {
+    std::lock_guard<std::mutex> g(out_mu_);
+    sink = sink_;
+    if (!sink) {
+      for (auto& d : outs) outq_.push_back(std::move(d));
+      outs.clear();
+    } else {
+      // tags of the native server go to its sink, the others to poll()
+      size_t k = 0;
+      for (size_t i = 0; i < outs.size(); ++i) {
+        if (outs[i].tag & kSinkTag) {
+          if (k != i) outs[k] = std::move(outs[i]);  // (a self-move would empty the strings)
+          ++k;
+        } else {
+          outq_.push_back(std::move(outs[i]));
+        }
+      }
+      outs.resize(k);
+    }
+  }
+  out_cv_.notify_all();
+  if (sink && !outs.empty()) sink(std::move(outs));
 }
 
 size_t ServeCore::poll(std::vector<Done>& out, size_t max, int64_t timeout_us) {
@@ -676,11 +699,7 @@ void ServeCore::finisher_loop() {
     a_serialize_.fetch_add(now_ns() - t, std::memory_order_relaxed);
     a_items_.fetch_add(int64_t(outs.size()), std::memory_order_relaxed);
     a_rows_.fetch_add(int64_t(outs.size()), std::memory_order_relaxed);
-    {
-      std::lock_guard<std::mutex> g(out_mu_);
-      for (auto& d : outs) outq_.push_back(std::move(d));
-    }
-    out_cv_.notify_all();
+    deliver(std::move(outs));
   }
 }
 

@@ -26,6 +26,7 @@
 // per-step header on the hot path (VERDICT r2 "step clock").
 #pragma once
 #include <atomic>
+#include <functional>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -120,6 +121,15 @@ class ServeCore {
     std::string err;
   };
   size_t poll(std::vector<Done>& out, size_t max, int64_t timeout_us);
+  // completions whose tag has bit 63 set go to `sink` (called on a finisher thread, must not
+  // block) instead of the poll() queue: the native gRPC server (h2grpc.cpp) routes them back to
+  // the connection that asked
+  using Sink = std::function<void(std::vector<Done>&&)>;
+  static constexpr uint64_t kSinkTag = uint64_t(1) << 63;
+  void set_sink(Sink sink) {
+    std::lock_guard<std::mutex> g(out_mu_);
+    sink_ = std::move(sink);
+  }
 
   // stop issuing new steps (exchange: every rank converges to the same step count) and wait
   // until every issued step completed; set_device() is allowed while paused
@@ -169,6 +179,7 @@ class ServeCore {
   void stepper_loop();
   void completion_loop();
   void finisher_loop();
+  void deliver(std::vector<Done>&& outs);
   void link_loop();
   void enqueue(Item* it);
   void wait_item(Item* it);
@@ -189,6 +200,7 @@ class ServeCore {
   Options opt_;
   std::shared_ptr<LinkIndex> links_;
   std::shared_ptr<AuditRing> audit_;
+  Sink sink_;
   std::atomic<uint16_t> model_ver_{1};
 
   // queue + slots (q_mu_)

@@ -50,6 +50,11 @@ def main(argv=None) -> int:
     ap.add_argument("--internal-port-offset", type=int, default=1000,
                     help="multi-GPU: rank 0 also listens on grpc_port + this for the cold RPCs the other "
                          "ranks forward")
+    ap.add_argument("--grpc-server", default=os.environ.get("RISK_GRPC_SERVER", "native"), choices=["native", "aio"],
+                    help="native: the C++ HTTP/2 server owns the public port (unary RPCs, ScoreTransaction "
+                         "straight into the serving core) and the grpc.aio server serves streaming / "
+                         "reflection on grpc_port + --internal-port-offset; aio: grpc.aio on the public port")
+    ap.add_argument("--grpc-workers", type=int, default=4, help="native server: epoll worker threads")
     ap.add_argument("--audit-flush-every-s", type=float, default=2.0,
                     help="drain the risk_scores / ltv_predictions rings into AUDIT_DB this often")
     a = ap.parse_args(argv)
@@ -89,8 +94,12 @@ def main(argv=None) -> int:
             def listen(node):
                 nodes.append(node)
                 node.start_audit_flusher(a.audit_flush_every_s, log)  # AUDIT_DB: this rank's rows
-                return IngressServer(node, f"127.0.0.1:{cfg.server.grpc_port + a.internal_port_offset}",
-                                     port=cfg.server.grpc_port, host=a.host).start()
+                up = f"127.0.0.1:{cfg.server.grpc_port + a.internal_port_offset}"
+                if a.grpc_server == "native":
+                    from .api.native_grpc import NativeIngressServer
+                    return NativeIngressServer(node, up, port=cfg.server.grpc_port, host=a.host,
+                                               workers=a.grpc_workers).start()
+                return IngressServer(node, up, port=cfg.server.grpc_port, host=a.host).start()
             n, rows = serve_shard(cfg, comm, backend=backend, capacity=a.accounts or None,
                                   fraud_model=_fraud_model(a, cfg), on_node=listen)
             for node in nodes:
@@ -104,8 +113,18 @@ def main(argv=None) -> int:
         n = eng.restore(a.snapshot_dir)
         log.info("feature store restored", extra={"fields": dict(accounts=n, dir=a.snapshot_dir)})
     multi = comm is not None and comm.world > 1
-    gs = RiskServer(eng, port=cfg.server.grpc_port, host=a.host, batching=not a.no_batching, reuseport=multi,
-                    extra_ports=[cfg.server.grpc_port + a.internal_port_offset] if multi else ()).start()
+    internal = cfg.server.grpc_port + a.internal_port_offset
+    ngs = None
+    if a.grpc_server == "native":
+        # public port: the native server (every rank, SO_REUSEPORT); the grpc.aio server keeps
+        # the streaming RPCs (health Watch, reflection) and the worker ranks' forwarded cold RPCs
+        from .api.native_grpc import NativeRiskServer
+        ngs = NativeRiskServer(eng, port=cfg.server.grpc_port, host=a.host, workers=a.grpc_workers,
+                               batching=not a.no_batching).start()
+        gs = RiskServer(eng, port=internal, host=a.host, batching=not a.no_batching).start()
+    else:
+        gs = RiskServer(eng, port=cfg.server.grpc_port, host=a.host, batching=not a.no_batching, reuseport=multi,
+                        extra_ports=[internal] if multi else ()).start()
     hs = HttpServer(eng, port=cfg.server.http_port, host=a.host, timeout_s=cfg.server.http_timeout_s).start()
     stop = threading.Event()
 
@@ -124,6 +143,8 @@ def main(argv=None) -> int:
         if time.time() - last_flush >= a.audit_flush_every_s:  # AUDIT_DB set: drain the audit rings
             flush_if_configured(eng, log)
             last_flush = time.time()
+    if ngs is not None:
+        ngs.stop()
     gs.stop(cfg.server.shutdown_grace_s)
     hs.stop()
     flush_if_configured(eng, log)  # rows scored during the grace period

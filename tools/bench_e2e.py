@@ -277,13 +277,28 @@ def _open_loop_client(i, port, accounts, rates, seconds, t_start, q):
     q.put(asyncio.run(main()))
 
 
+def make_server(a, eng, batching: bool):
+    """--server native (default): the C++ HTTP/2 server (api/native_grpc.py); aio: grpc.aio."""
+    if a.server == "native":
+        from igaming_platform_amd.api.native_grpc import NativeRiskServer
+        return NativeRiskServer(eng, port=0, workers=a.server_workers, batching=batching).start()
+    from igaming_platform_amd.api.grpc_server import RiskServer
+    return RiskServer(eng, port=0, batching=batching, workers=16).start()
+
+
+def server_desc(a) -> str:
+    if a.server == "native":
+        return (f"native HTTP/2 (libnghttp2, {a.server_workers} epoll workers, SO_REUSEPORT); ScoreTransaction "
+                "straight into the serving core")
+    return "grpc.aio, raw-bytes handlers, native serving core FIFO (NativeUnary)"
+
+
 def run_grpc_open_loop(a) -> dict:
     """Unary ScoreTransaction throughput vs latency: offered load stepped through ``--rates``
     (whole-node calls/s, split over ``--clients`` processes), open loop."""
     import multiprocessing as mp
-    from igaming_platform_amd.api.grpc_server import RiskServer
     eng = build_engine(a.accounts, a.batch, a.backend)
-    srv = RiskServer(eng, port=0, batching=True, workers=16).start()
+    srv = make_server(a, eng, batching=True)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     rates = [int(x) for x in a.rates.split(",")]
@@ -296,7 +311,7 @@ def run_grpc_open_loop(a) -> dict:
     res = [q.get(timeout=lead + len(rates) * (a.seconds + 2) + 300) for _ in procs]
     [p.join() for p in procs]
     st = eng.core.stats(False) if getattr(eng, "core", None) is not None else None
-    srv.stop(0.5)
+    srv.stop(0.5) if a.server != "native" else srv.stop()
     eng.close()
     curve = []
     for li, rate in enumerate(rates):
@@ -320,7 +335,7 @@ def run_grpc_open_loop(a) -> dict:
                 value_is="highest offered rate answered in full with p99 < 50 ms", scope="grpc_unary_open_loop",
                 n_gpus=1 if a.backend == "gpu" else 0, data="synthetic (UUID ids, random-init cfg3 weights)",
                 config=dict(model="cfg3 GBDT(100,d7,128f)+MLP(32-256-1)", clients=a.clients, seconds_per_level=a.seconds,
-                            server="grpc.aio, raw-bytes handlers, native serving core FIFO (NativeUnary)",
+                            server=server_desc(a),
                             client="grpc.aio open loop, latency from the scheduled send time"),
                 curve=curve, best=best,
                 mean_rows_per_device_step=(round(st["rows"] / max(st["steps"], 1), 1) if st else None),
@@ -329,10 +344,9 @@ def run_grpc_open_loop(a) -> dict:
 
 def run_grpc(a) -> dict:
     import multiprocessing as mp
-    from igaming_platform_amd.api.grpc_server import RiskServer
     cold = a.rpc in ("ltv", "abuse")
     eng = build_cold_engine(a.accounts, a.backend) if cold else build_engine(a.accounts, a.batch, a.backend)
-    srv = RiskServer(eng, port=0, batching=a.rpc != "batch", workers=16).start()
+    srv = make_server(a, eng, batching=a.rpc != "batch")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     lead = 25.0  # client start-up (import + payload generation) happens before the window
@@ -343,7 +357,9 @@ def run_grpc(a) -> dict:
     [p.start() for p in procs]
     res = [q.get(timeout=a.seconds + lead + 300) for _ in procs]
     [p.join() for p in procs]
-    srv.stop(0.5)
+    batcher = None if a.server == "native" else {"tx": srv.batcher, "ltv": srv.ltv_batcher,
+                                                 "abuse": srv.abuse_batcher}.get(a.rpc)
+    srv.stop(0.5) if a.server != "native" else srv.stop()
     eng.close()
     lat = [x for r in res for x in r[0]]
     per = res[0][2]
@@ -352,7 +368,6 @@ def run_grpc(a) -> dict:
              "tx": "fraud scores/sec (unary risk.v1.ScoreTransaction over gRPC, micro-batched)",
              "ltv": "PredictLTV answers/sec (unary over gRPC, micro-batched)",
              "abuse": "CheckBonusAbuse answers/sec (unary over gRPC, micro-batched)"}
-    batcher = {"tx": srv.batcher, "ltv": srv.ltv_batcher, "abuse": srv.abuse_batcher}.get(a.rpc)
     mean_batch = (batcher.items / max(batcher.batches, 1)) if batcher is not None else None
     return dict(metric=names[a.rpc], mean_device_batch=mean_batch,
                 value=calls * per / a.seconds, unit="scores/s", scope="grpc", n_gpus=1 if a.backend == "gpu" else 0,
@@ -361,8 +376,7 @@ def run_grpc(a) -> dict:
                                    " + rule signals"}.get(a.rpc, "cfg3 GBDT(100,d7,128f)+MLP(32-256-1)"),
                             rpc=a.rpc, clients=a.clients,
                             seconds=a.seconds, transactions_per_call=per, accounts=a.accounts,
-                            server="grpc.aio, raw-bytes handlers, C++ codec"
-                                   + (", MicroBatcher" if a.rpc == "tx" else "")),
+                            server=server_desc(a)),
                 calls=calls, errors=sum(r[1] for r in res),
                 p50_latency_ms=float(np.percentile(lat, 50)), p99_latency_ms=float(np.percentile(lat, 99)),
                 latency_baseline_ms=BASELINE_P99_MS,
@@ -384,6 +398,8 @@ def main(argv=None) -> int:
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--json-out", default="")
     ap.add_argument("--open-loop", action="store_true", help="--scope grpc --rpc tx: offered-load curve")
+    ap.add_argument("--server", default="native", choices=["native", "aio"], help="--scope grpc: the gRPC server")
+    ap.add_argument("--server-workers", type=int, default=4, help="--server native: epoll worker threads")
     ap.add_argument("--rates", default="2000,5000,8000,12000,16000,24000",
                     help="--open-loop: offered whole-node unary calls/s per level")
     a = ap.parse_args(argv)
