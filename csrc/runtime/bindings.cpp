@@ -683,6 +683,23 @@ PYBIND11_MODULE(_native, m) {
         return d;
       });
 
+  m.def("grpc_load", [](const std::string& host, int port, const std::string& path, std::vector<std::string> payloads,
+                        double rate, double seconds, int conns, int max_inflight) {
+    LoadResult r;
+    {
+      py::gil_scoped_release rel;
+      r = grpc_load(host, port, path, payloads, rate, seconds, conns, max_inflight);
+    }
+    py::dict d;
+    d["latency_ms"] = vec_np(r.latency_ms);
+    d["errors"] = r.errors;
+    d["sent"] = r.sent;
+    d["seconds"] = r.seconds;
+    d["elapsed"] = r.elapsed;
+    return d;
+  }, py::arg("host"), py::arg("port"), py::arg("path"), py::arg("payloads"), py::arg("rate"), py::arg("seconds"),
+     py::arg("conns") = 8, py::arg("max_inflight") = 4096);
+
   py::class_<PyServe, std::shared_ptr<PyServe>>(m, "ServeCore")
       .def(py::init([](std::vector<std::shared_ptr<AccountIndex>> idx, py::object dev, int rank,
                        std::shared_ptr<StepClock> clock, int max_wait_us, int64_t timeout_us, int finishers,

@@ -64,6 +64,9 @@ struct Ng {
   void (*set_on_frame_recv)(void*, int (*)(void*, const void*, void*));
   void (*set_on_stream_close)(void*, int (*)(void*, int32_t, uint32_t, void*));
   int (*server_new)(void**, const void*, void*);
+  int (*client_new)(void**, const void*, void*);
+  int32_t (*submit_request)(void*, const void*, const NgNv*, size_t, const NgDataProvider*, void*);
+  void* (*stream_user_data)(void*, int32_t);
   void (*session_del)(void*);
   ssize_t (*mem_recv)(void*, const uint8_t*, size_t);
   ssize_t (*mem_send)(void*, const uint8_t**);
@@ -97,6 +100,9 @@ const Ng& ng() {
   NG_SYM(set_on_frame_recv, "nghttp2_session_callbacks_set_on_frame_recv_callback");
   NG_SYM(set_on_stream_close, "nghttp2_session_callbacks_set_on_stream_close_callback");
   NG_SYM(server_new, "nghttp2_session_server_new");
+  NG_SYM(client_new, "nghttp2_session_client_new");
+  NG_SYM(submit_request, "nghttp2_submit_request");
+  NG_SYM(stream_user_data, "nghttp2_session_get_stream_user_data");
   NG_SYM(session_del, "nghttp2_session_del");
   NG_SYM(mem_recv, "nghttp2_session_mem_recv");
   NG_SYM(mem_send, "nghttp2_session_mem_send");
@@ -647,6 +653,187 @@ void GrpcServer::batch_loop() {
 
 GrpcServer::Stats GrpcServer::stats() const {
   return Stats{calls_.load(), hot_tx_.load(), hot_batch_.load(), cold_n_.load(), errors_.load(), conns_.load()};
+}
+
+// ---------------------------------------------------------------------------- load generator
+// Open-loop unary gRPC load over `conns` HTTP/2 connections (one thread each): calls are issued
+// on a fixed schedule (rate / conns per connection) whatever the server's pace, up to
+// max_inflight per connection; latency counts from the SCHEDULED send time, so a server that
+// falls behind shows growing latency, not a lower offered load (tools/bench_e2e.py
+// --client native: the Python clients topped out before the native server did).
+namespace {
+
+struct LoadConn {
+  struct Call {
+    int64_t t_sched;
+    std::string body;  // 5-byte prefix + message
+    size_t off = 0;
+    int status = -1;
+  };
+  void* sess = nullptr;
+  std::unordered_map<int32_t, std::unique_ptr<Call>> calls;  // heap calls: the providers point at them
+  std::vector<double>* lat = nullptr;
+  int64_t* errors = nullptr;
+  int64_t* done = nullptr;
+  int64_t* last = nullptr;  // latest completion (mono ns)
+
+  static ssize_t read_req(void*, int32_t, uint8_t* buf, size_t len, uint32_t* flags, NgDataSource* src, void*) {
+    auto* c = static_cast<Call*>(src->ptr);
+    const size_t n = std::min(len, c->body.size() - c->off);
+    std::memcpy(buf, c->body.data() + c->off, n);
+    c->off += n;
+    if (c->off == c->body.size()) *flags |= kDataEof;
+    return ssize_t(n);
+  }
+  static int on_header(void*, const void* frame, const uint8_t* name, size_t namelen, const uint8_t* value,
+                       size_t valuelen, uint8_t, void* ud) {
+    auto* lc = static_cast<LoadConn*>(ud);
+    const auto* hd = static_cast<const NgFrameHd*>(frame);
+    if (namelen == 11 && std::memcmp(name, "grpc-status", 11) == 0) {
+      auto it = lc->calls.find(hd->stream_id);
+      if (it != lc->calls.end()) it->second->status = std::atoi(std::string(reinterpret_cast<const char*>(value), valuelen).c_str());
+    }
+    return 0;
+  }
+  static int on_close(void*, int32_t sid, uint32_t err, void* ud) {
+    auto* lc = static_cast<LoadConn*>(ud);
+    auto it = lc->calls.find(sid);
+    if (it == lc->calls.end()) return 0;
+    const int64_t t = mono_ns();
+    if (t > *lc->last) *lc->last = t;
+    if (err == 0 && it->second->status == 0) lc->lat->push_back(double(t - it->second->t_sched) * 1e-6);
+    else ++*lc->errors;
+    ++*lc->done;
+    lc->calls.erase(it);
+    return 0;
+  }
+};
+
+}  // namespace
+
+LoadResult grpc_load(const std::string& host, int port, const std::string& path, const std::vector<std::string>& payloads,
+                     double rate, double seconds, int conns, int max_inflight) {
+  const Ng& n = ng();
+  if (payloads.empty() || rate <= 0 || conns < 1) throw std::runtime_error("grpc_load: arguments");
+  LoadResult out;
+  std::vector<std::vector<double>> lats(static_cast<size_t>(conns));
+  std::vector<int64_t> errs(static_cast<size_t>(conns), 0), sent(static_cast<size_t>(conns), 0),
+      done(static_cast<size_t>(conns), 0), last(static_cast<size_t>(conns), 0);
+  std::vector<std::string> frames(payloads.size());
+  for (size_t i = 0; i < payloads.size(); ++i) {
+    const uint32_t len = uint32_t(payloads[i].size());
+    std::string f(5, '\0');
+    f[1] = char(len >> 24); f[2] = char(len >> 16); f[3] = char(len >> 8); f[4] = char(len);
+    frames[i] = f + payloads[i];
+  }
+  const std::string authority = host + ":" + std::to_string(port);
+  const int64_t t0 = mono_ns() + 20000000;  // 20 ms for the connections to come up
+  const int64_t t_end = t0 + int64_t(seconds * 1e9);
+  std::vector<std::thread> th;
+  std::atomic<int> failed{0};
+  for (int ci = 0; ci < conns; ++ci) {
+    th.emplace_back([&, ci] {
+      const int fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+      sockaddr_in a{};
+      a.sin_family = AF_INET;
+      a.sin_port = htons(uint16_t(port));
+      ::inet_pton(AF_INET, host == "localhost" ? "127.0.0.1" : host.c_str(), &a.sin_addr);
+      if (fd < 0 || ::connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof a) != 0) {
+        failed.fetch_add(1);
+        if (fd >= 0) ::close(fd);
+        return;
+      }
+      int one = 1;
+      ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+      ::fcntl(fd, F_SETFL, ::fcntl(fd, F_GETFL) | O_NONBLOCK);
+      void* cbs = nullptr;
+      n.callbacks_new(&cbs);
+      n.set_on_header(cbs, LoadConn::on_header);
+      n.set_on_stream_close(cbs, LoadConn::on_close);
+      LoadConn lc;
+      lc.lat = &lats[size_t(ci)];
+      lc.errors = &errs[size_t(ci)];
+      lc.done = &done[size_t(ci)];
+      lc.last = &last[size_t(ci)];
+      n.client_new(&lc.sess, cbs, &lc);
+      n.callbacks_del(cbs);
+      const NgSettingsEntry iv[2] = {{kSettingsMaxStreams, 100000}, {kSettingsInitialWindow, 8u << 20}};
+      n.submit_settings(lc.sess, 0, iv, 2);
+      const double interval = double(conns) / rate * 1e9;  // ns between this connection's calls
+      int64_t k = 0;
+      std::vector<char> rbuf(size_t(256) << 10);
+      std::string wpend;
+      static const std::string post = "POST", scheme = "http", ct = "application/grpc", te = "trailers";
+      bool ok = true;
+      while (ok) {
+        const int64_t now = mono_ns();
+        if (now > t_end + 10000000000LL) break;  // 10 s grace for stragglers
+        // issue every call whose scheduled time has come
+        while (true) {
+          const int64_t ts = t0 + int64_t(double(k) * interval) + int64_t(double(ci) * interval / conns);
+          if (ts > now || ts >= t_end) break;
+          if (int(lc.calls.size()) >= max_inflight) break;
+          auto c = std::make_unique<LoadConn::Call>();
+          c->t_sched = ts;
+          c->body = frames[size_t((k * conns + ci) % int64_t(frames.size()))];
+          const NgNv h[6] = {nv(":method", post), nv(":scheme", scheme), nv(":path", path),
+                             nv(":authority", authority), nv("content-type", ct), nv("te", te)};
+          NgDataProvider prd{};
+          prd.read_callback = LoadConn::read_req;
+          prd.source.ptr = c.get();
+          const int32_t sid = n.submit_request(lc.sess, nullptr, h, 6, &prd, nullptr);
+          ++k;
+          if (sid < 0) {
+            ++errs[size_t(ci)];
+            continue;
+          }
+          lc.calls.emplace(sid, std::move(c));
+          ++sent[size_t(ci)];
+        }
+        const uint8_t* p = nullptr;
+        for (;;) {
+          const ssize_t len = n.mem_send(lc.sess, &p);
+          if (len <= 0) break;
+          wpend.append(reinterpret_cast<const char*>(p), size_t(len));
+        }
+        while (!wpend.empty()) {
+          const ssize_t w = ::send(fd, wpend.data(), wpend.size(), MSG_NOSIGNAL);
+          if (w < 0) {
+            if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+            ok = false;
+            break;
+          }
+          wpend.erase(0, size_t(w));
+        }
+        const ssize_t r = ::recv(fd, rbuf.data(), rbuf.size(), 0);
+        if (r > 0) {
+          if (n.mem_recv(lc.sess, reinterpret_cast<const uint8_t*>(rbuf.data()), size_t(r)) < 0) ok = false;
+        } else if (r == 0) {
+          ok = false;
+        } else if (errno != EAGAIN && errno != EWOULDBLOCK) {
+          ok = false;
+        } else {
+          if (now >= t_end && lc.calls.empty()) break;
+          std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+      }
+      errs[size_t(ci)] += int64_t(lc.calls.size());  // unanswered at the end
+      n.session_del(lc.sess);
+      ::close(fd);
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int ci = 0; ci < conns; ++ci) {
+    out.latency_ms.insert(out.latency_ms.end(), lats[size_t(ci)].begin(), lats[size_t(ci)].end());
+    out.errors += errs[size_t(ci)];
+    out.sent += sent[size_t(ci)];
+  }
+  out.errors += int64_t(failed.load()) * int64_t(rate * seconds / conns);
+  out.seconds = seconds;
+  int64_t lastc = t0;
+  for (int64_t v : last) lastc = std::max(lastc, v);
+  out.elapsed = std::max(seconds, double(lastc - t0) * 1e-9);
+  return out;
 }
 
 }  // namespace igp

@@ -84,4 +84,14 @@ class GrpcServer {
   mutable std::atomic<int64_t> calls_{0}, hot_tx_{0}, hot_batch_{0}, cold_n_{0}, errors_{0}, conns_{0};
 };
 
+// open-loop unary gRPC load generator (tools/bench_e2e.py --client native)
+struct LoadResult {
+  std::vector<double> latency_ms;  // per answered call, from its scheduled send time
+  int64_t errors = 0, sent = 0;
+  double seconds = 0;
+  double elapsed = 0;  // schedule start -> last completion (>= seconds)
+};
+LoadResult grpc_load(const std::string& host, int port, const std::string& path, const std::vector<std::string>& payloads,
+                     double rate, double seconds, int conns, int max_inflight);
+
 }  // namespace igp

@@ -157,3 +157,15 @@ def test_many_connections_and_a_large_batch(nstack):
     for c in chans:
         c.close()
     assert srv.stats()["connections"] >= 1
+
+
+def test_native_load_generator_against_the_native_server(nstack):
+    """csrc/runtime/h2grpc.cpp grpc_load (the open-loop client of tools/bench_e2e.py): every
+    scheduled call answered, latencies from the scheduled send times."""
+    from igaming_platform_amd.native import native
+    eng, srv, cli = nstack
+    body = [P.ScoreTransactionRequest(account_id=f"lg-{i}", amount=100, transaction_type="bet").SerializeToString()
+            for i in range(64)]
+    r = native().grpc_load("127.0.0.1", srv.port, P.method_path("ScoreTransaction"), body, 1000.0, 1.0, 4, 512)
+    assert r["errors"] == 0 and r["sent"] == 1000 and len(r["latency_ms"]) == 1000
+    assert float(np.median(r["latency_ms"])) < 1000 and r["elapsed"] >= 1.0

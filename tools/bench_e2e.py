@@ -299,9 +299,11 @@ def run_grpc_open_loop(a) -> dict:
     import multiprocessing as mp
     eng = build_engine(a.accounts, a.batch, a.backend)
     srv = make_server(a, eng, batching=True)
+    rates = [int(x) for x in a.rates.split(",")]
+    if a.client == "native":
+        return _native_open_loop(a, eng, srv, rates)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    rates = [int(x) for x in a.rates.split(",")]
     lead = 30.0
     t_start = time.time() + lead
     per = [r / a.clients for r in rates]
@@ -340,6 +342,47 @@ def run_grpc_open_loop(a) -> dict:
                 curve=curve, best=best,
                 mean_rows_per_device_step=(round(st["rows"] / max(st["steps"], 1), 1) if st else None),
                 latency_baseline_ms=BASELINE_P99_MS)
+
+
+def _curve_result(a, curve, st) -> dict:
+    ok = [c for c in curve if c["p99_ms"] is not None and c["p99_ms"] < BASELINE_P99_MS and c["errors"] == 0
+          and c["achieved_per_s"] >= 0.95 * c["offered_per_s"]]
+    best = max(ok, key=lambda c: c["achieved_per_s"]) if ok else None
+    return dict(metric="unary risk.v1.ScoreTransaction over gRPC: throughput vs latency (open loop)",
+                value=best["achieved_per_s"] if best else 0.0, unit="calls/s",
+                value_is="highest offered rate answered in full with p99 < 50 ms", scope="grpc_unary_open_loop",
+                n_gpus=1 if a.backend == "gpu" else 0, data="synthetic (UUID ids, random-init cfg3 weights)",
+                config=dict(model="cfg3 GBDT(100,d7,128f)+MLP(32-256-1)", clients=a.clients, seconds_per_level=a.seconds,
+                            server=server_desc(a),
+                            client=("native HTTP/2 open loop (libnghttp2, one connection per thread)" if a.client == "native"
+                                    else "grpc.aio open loop") + ", latency from the scheduled send time"),
+                curve=curve, best=best,
+                mean_rows_per_device_step=(round(st["rows"] / max(st["steps"], 1), 1) if st else None),
+                latency_baseline_ms=BASELINE_P99_MS)
+
+
+def _native_open_loop(a, eng, srv, rates) -> dict:
+    """The offered-load curve from the C++ load generator (csrc/runtime/h2grpc.cpp grpc_load):
+    ``--clients`` HTTP/2 connections, each on its own thread."""
+    from igaming_platform_amd.native import native
+    from igaming_platform_amd.proto import risk_v1 as P
+    payloads = tx_payloads(a.accounts, 8192, seed=300)
+    path = P.method_path("ScoreTransaction")
+    native().grpc_load("127.0.0.1", srv.port, path, payloads, 2000.0, 1.0, a.clients, 4096)  # warm
+    curve = []
+    for rate in rates:
+        r = native().grpc_load("127.0.0.1", srv.port, path, payloads, float(rate), a.seconds, a.clients, 8192)
+        lat = np.asarray(r["latency_ms"])
+        curve.append(dict(offered_per_s=rate, achieved_per_s=round(len(lat) / float(r["elapsed"]), 1), calls=int(r["sent"]),
+                          errors=int(r["errors"]), error_kinds={},
+                          p50_ms=round(float(np.percentile(lat, 50)), 3) if len(lat) else None,
+                          p99_ms=round(float(np.percentile(lat, 99)), 3) if len(lat) else None))
+        print(json.dumps(curve[-1]), flush=True)
+        time.sleep(1.0)
+    st = eng.core.stats(False) if getattr(eng, "core", None) is not None else None
+    srv.stop()
+    eng.close()
+    return _curve_result(a, curve, st)
 
 
 def run_grpc(a) -> dict:
@@ -400,6 +443,8 @@ def main(argv=None) -> int:
     ap.add_argument("--open-loop", action="store_true", help="--scope grpc --rpc tx: offered-load curve")
     ap.add_argument("--server", default="native", choices=["native", "aio"], help="--scope grpc: the gRPC server")
     ap.add_argument("--server-workers", type=int, default=4, help="--server native: epoll worker threads")
+    ap.add_argument("--client", default="native", choices=["native", "aio"],
+                    help="--open-loop load generator: C++ HTTP/2 (default) or grpc.aio processes")
     ap.add_argument("--rates", default="2000,5000,8000,12000,16000,24000",
                     help="--open-loop: offered whole-node unary calls/s per level")
     a = ap.parse_args(argv)

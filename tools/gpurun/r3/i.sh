@@ -11,7 +11,7 @@ rc=$?; echo "tests rc=$rc" >> $O/status.txt
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 3
 timeout -k 10 300 python bench.py --json-out $O/bench_default.json > $O/bench_default.log 2>&1 || exit 4
 echo "bench $(tail -c 300 $O/bench_default.json)" >> $O/status.txt
-timeout -k 10 400 python tools/bench_e2e.py --scope grpc --rpc tx --open-loop --clients 8 --seconds 4 --rates 5000,20000,50000,100000,150000 --json-out $O/grpc_tx_native_curve.json > $O/grpc_tx_native_curve.log 2>&1 || exit 5
+timeout -k 10 400 python tools/bench_e2e.py --scope grpc --rpc tx --open-loop --clients 8 --seconds 4 --rates 10000,50000,100000,200000,400000 --json-out $O/grpc_tx_native_curve.json > $O/grpc_tx_native_curve.log 2>&1 || exit 5
 timeout -k 10 300 python tools/bench_e2e.py --scope grpc --rpc batch --clients 8 --seconds 8 --json-out $O/grpc_batch_native.json > $O/grpc_batch_native.log 2>&1 || exit 6
 for pf in 2 5 2 5; do
   IGP_MC_PF=$pf timeout -k 10 200 python bench.py --config cfg4 --numerics bf16 --steps 400 --warmup 50 >> $O/cfg4_pf_ab.log 2>&1 || exit 7
