@@ -217,6 +217,7 @@ class Config:
         s.audit_db = env.get("AUDIT_DB", s.audit_db)
         s.audit_ring_rows = int(env.get("AUDIT_RING_ROWS", s.audit_ring_rows))
         s.audit_mode = env.get("AUDIT_MODE", s.audit_mode)
+        s.audit_direct_max = int(env.get("AUDIT_DIRECT_MAX", s.audit_direct_max))
         sc = self.scoring
         sc.block_threshold = geti("BLOCK_THRESHOLD", sc.block_threshold)
         sc.review_threshold = geti("REVIEW_THRESHOLD", sc.review_threshold)
