@@ -446,6 +446,7 @@ PYBIND11_MODULE(_hipk, m) {
     a.ws_trace = ptr<int64_t*>(d, "ws_trace");
     a.split = geti(d, "split");
     a.reverse = geti(d, "reverse", 0);
+    a.ws_stagger = geti(d, "ws_stagger", 0);
     if (a.split) {
       for (int l = 0; l < a.n_layers; ++l)
         if (!a.layer[l].W_lo || !a.layer[l].R_lo) throw std::runtime_error("gru: split mode needs residual weights");

@@ -858,7 +858,11 @@ void launch_gru(const GruArgs& a, hipStream_t st) {
     hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
     return v > 0 ? v : 256;
   }();
-  if (a.ws && gru_ws_eligible(a) && gru_ws_clusters(a.n_rows) * 8 <= n_cu) return launch_gru_ws(a, st);
+  if (a.ws && gru_ws_eligible(a)) {
+    // ws = 3: two 64-row clusters per CU (all co-resident at <= 2 workgroups per CU)
+    if (a.ws == 3 ? gru_ws2_clusters(a.n_rows) * 8 <= 2 * n_cu : gru_ws_clusters(a.n_rows) * 8 <= n_cu)
+      return launch_gru_ws(a, st);
+  }
   // rows per workgroup: every CU streams the full weight set each step (a per-CU L2 bandwidth
   // bound, tools/gru_bench.py), so 32 rows amortise each fragment over two MFMA row tiles once
   // the batch fills the 256 CUs at 32 rows; below that 16 keeps more CUs streaming.

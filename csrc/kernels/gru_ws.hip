@@ -570,13 +570,381 @@ __global__ void __launch_bounds__(256, 1) gru_ws_kernel(GruArgs a) {
   }
 }
 
+// ============================================================================================
+// Two clusters per CU (ws = 3): 64-row clusters, 4 waves per workgroup, TWO co-resident
+// workgroups per CU (80 KB LDS each, <= 256 VGPRs per wave). Same member split and hand-off
+// protocol as above, but every SIMD now hosts two waves of two independent clusters, so one
+// cluster's hand-off (sc1 stores draining, counter poll, gather) and gate epilogue issue while
+// the other cluster's wave keeps the MFMA pipe busy - the hardware interleaves what the
+// single-wave kernel had to serialise (NOTES: 9.4 us/step = 5.5 compute + 3.9 hand-off).
+// Layer balance: a layer-2 wave issues 192 MFMAs per step, a layer-1 wave 108; the second
+// wave of blocks (b >> 8 odd: under breadth-first dispatch the partner on the same CU) swaps
+// the layer <-> wave assignment so a SIMD tends to host one wave of each layer.
+constexpr int W2_M = 64;
+constexpr int W2_RT = W2_M / 16;
+constexpr int W2_SLICE = 2 * W2_M * WS_UW;  // bf16 per member slice (both layers)
+constexpr int W2_CH = W2_SLICE / 8;         // 16-B chunks per slice (512)
+constexpr int W2_BLK = W2_M * WS_UW;        // bf16 per (layer, member) block of the LDS image (4 KB)
+// LDS image of h (per layer): [member][64 rows][32 columns] bf16, member-major so that a k-step
+// of 32 is one member's block and a handed-off slice is 2 contiguous 4-KB blocks - gathered
+// with global_load_lds (1 KB per wave instruction, no registers: the stationary weights leave
+// none). The 16-B chunk (row, q) sits at row * 4 + (q ^ ((row >> 2) & 3)): a 16-row A-fragment
+// read then touches 16 distinct chunks of every 256-B bank row (conflict-free), and the swizzle
+// is the same in every member's block, so slices are copied verbatim.
+__device__ __forceinline__ int w2_chunk(int row, int q) { return row * 4 + (q ^ ((row >> 2) & 3)); }
+
+// one row tile of one layer's step: acc = A(rt) . [Wz | Wr | Wh] over NK k-steps
+template <int L>
+__device__ __forceinline__ void w2_tile(const bf16x8 (&wz)[16], const bf16x8 (&wr)[16], const bf16x8 (&wh)[16],
+                                        const uint16_t* X, const uint16_t* H1, const uint16_t* H2, int rt, int lane,
+                                        f32x4 (&acc)[4]) {
+  constexpr int NK = L == 0 ? 9 : 16;
+  constexpr int NX = L == 0 ? 1 : 8;
+  const int arow = rt * 16 + (lane & 15), akof = 8 * (lane >> 4);
+  const int hoff = w2_chunk(arow, lane >> 4) * 8;  // k-step ks reads member block ks
+  auto hfrag = [&](const uint16_t* Hb, int blk) -> bf16x8 {
+    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Hb + blk * W2_BLK + hoff));
+  };
+  auto afrag = [&](int ks) -> bf16x8 {
+    if constexpr (L == 0) {
+      return ks == 0 ? lds_frag(X, WS_XS, arow, akof) : hfrag(H1, ks - 1);
+    } else {
+      return ks < 8 ? hfrag(H1, ks) : hfrag(H2, ks - 8);
+    }
+  };
+#pragma unroll
+  for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 cur = afrag(0);
+#pragma unroll
+  for (int ks = 0; ks < NK; ++ks) {
+    const bf16x8 nxt = ks + 1 < NK ? afrag(ks + 1) : cur;
+    // one k-step ahead only: left alone the scheduler hoists every A read of the tile (and
+    // runs out of the ~60 registers the stationary weights leave)
+    __builtin_amdgcn_sched_barrier(0);
+    acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur, wz[ks], acc[0], 0, 0, 0);
+    acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur, wr[ks], acc[1], 0, 0, 0);
+    if (ks < NX) acc[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur, wh[ks], acc[2], 0, 0, 0);
+    else acc[3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur, wh[ks], acc[3], 0, 0, 0);
+    cur = nxt;
+  }
+}
+
+template <int L>
+__device__ __forceinline__ void w2_layer(const bf16x8 (&wz)[16], const bf16x8 (&wr)[16], const bf16x8 (&wh)[16],
+                                         const uint16_t* X, const uint16_t* H1, const uint16_t* H2,
+                                         float (&hs)[W2_RT][4], const float (&bv)[4], int lane) {
+#pragma unroll
+  for (int rt = 0; rt < W2_RT; ++rt) {
+    f32x4 acc[4];
+    w2_tile<L>(wz, wr, wh, X, H1, H2, rt, lane, acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float z = sig_(acc[0][r] + bv[0]);
+      const float rr = sig_(acc[1][r] + bv[1]);
+      const float hh = tanh_(acc[2][r] + bv[2] + rr * (acc[3][r] + bv[3]));
+      hs[rt][r] = (1.f - z) * hh + z * hs[rt][r];
+    }
+  }
+}
+
+template <int L>
+struct W2Layer {
+  static constexpr int value = L;
+};
+
+__global__ void __launch_bounds__(256, 2) gru_ws2_kernel(GruArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // LDS: H1[8 blocks] | H2[8 blocks] (swizzled images) | X[2][M][XS] (bf16) | red[2][M] f32 | xmeta[4M] | flag
+  uint16_t* const H1 = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* const H2 = H1 + WS_CL * W2_BLK;
+  uint16_t* const Xb = H2 + WS_CL * W2_BLK;
+  float* const red = reinterpret_cast<float*>(Xb + 2 * W2_M * WS_XS);
+  int2* const xmeta = reinterpret_cast<int2*>(red + 2 * W2_M);
+  int* const sflag = reinterpret_cast<int*>(xmeta + 4 * W2_M);
+
+  const int b = blockIdx.x;
+  const int mem = (b >> 3) & 7;
+  const int cl = (b >> 6) * 8 + (b & 7);
+  const int row0 = cl * W2_M;
+  const int n_live = a.m_ptr ? min(*a.m_ptr, a.n_rows) : a.n_rows;
+  if (row0 >= n_live || cl >= 2 * a.ws_clusters) return;  // uniform over the cluster's 8 members
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int layer = (wave >> 1) ^ ((b >> 8) & 1);
+  const int tile = wave & 1;
+  const int ht = mem * 2 + tile;
+  const int crow = (lane >> 4) * 4, ccol = lane & 15;
+  const int j = ht * 16 + ccol;
+  const int T = a.T;
+  int32_t* const cnt = a.ws_sync + cl * 16;
+  if (a.head_w && mem == 0 && tid < W2_M && row0 + tid < n_live) a.out[row0 + tid] = __builtin_nanf("");
+  if (a.yh)
+    for (int e = tid; e < W2_M * WS_UW; e += 256) {
+      const int row = row0 + e / WS_UW;
+      if (row < n_live) a.yh[(size_t)row * WS_H + mem * WS_UW + e % WS_UW] = __builtin_nanf("");
+    }
+  {
+    uint32_t* z = reinterpret_cast<uint32_t*>(smem);
+    const int words = (2 * WS_CL * W2_BLK + 2 * W2_M * WS_XS) / 2;
+    for (int i = tid; i < words; i += 256) z[i] = 0u;
+  }
+  const int I = a.I;
+  const int chunks = I >> 3;
+  const int nchunk = W2_M * chunks;  // <= 256
+  for (int c = tid; c < nchunk; c += 256) {
+    const int grow = row0 + c / chunks;
+    int slot = -1, head = 0, from = T;
+    if (grow < n_live) {
+      if (a.mode == 1) {
+        slot = a.slots[grow];
+        if (slot >= 0) {
+          const AcctRT r = a.rt[slot];
+          head = r.ev_head;
+          from = T - min(r.ev_count, T);
+        }
+      } else {
+        from = 0;
+      }
+    }
+    xmeta[c] = make_int2(slot, head | (from << 16));
+  }
+  auto load_x = [&](int c, int t) -> uint4 {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    const int2 m = xmeta[c];
+    const int from = m.y >> 16;
+    if (t >= T) return v;
+    if (a.reverse) t = T - 1 - t;
+    if (t < from) return v;
+    const int row = c / chunks, q = c - row * chunks;
+    if (a.mode == 1) {
+      if (m.x < 0) return v;
+      int idx = ((m.y & 0xffff) - T + t) % a.ev_ring;
+      if (idx < 0) idx += a.ev_ring;
+      v = *reinterpret_cast<const uint4*>(a.ev + (((size_t)m.x * a.ev_ring + idx) * I + q * 8));
+    } else {
+      const float* src = a.X + (((size_t)t * a.x_rows + row0 + row) * I + q * 8);
+      const float4 f0 = *reinterpret_cast<const float4*>(src);
+      const float4 f1 = *reinterpret_cast<const float4*>(src + 4);
+      v.x = (uint32_t)f32_to_bf16(f0.x) | ((uint32_t)f32_to_bf16(f0.y) << 16);
+      v.y = (uint32_t)f32_to_bf16(f0.z) | ((uint32_t)f32_to_bf16(f0.w) << 16);
+      v.z = (uint32_t)f32_to_bf16(f1.x) | ((uint32_t)f32_to_bf16(f1.y) << 16);
+      v.w = (uint32_t)f32_to_bf16(f1.z) | ((uint32_t)f32_to_bf16(f1.w) << 16);
+    }
+    return v;
+  };
+  auto x_slot = [&](int buf, int c) -> uint4* {
+    const int row = c / chunks, q = c - row * chunks;
+    return reinterpret_cast<uint4*>(Xb + buf * (W2_M * WS_XS) + row * WS_XS + q * 8);
+  };
+  const int ltid = tid & 127;  // thread index among the two layer-0 waves
+  __syncthreads();
+  if (layer == 0)
+    for (int c = ltid; c < nchunk; c += 128) *x_slot(0, c) = load_x(c, 0);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      a.ws_x + (size_t)cl * 2 * WS_CL * W2_SLICE, 0, 2 * WS_CL * W2_SLICE * 2, 0x00020000);
+  int64_t* const trace = (a.ws_trace && b == 0 && tid == 0) ? a.ws_trace : nullptr;
+
+  // the whole recurrence, specialised per layer: each wave runs exactly one instantiation, so
+  // the register allocator sees one set of stationary weights (192 registers for layer 2, 108
+  // for layer 1) instead of both sets merged across a branch. Both instantiations execute the
+  // same sequence of workgroup barriers.
+  auto run = [&](auto Lc) -> bool {
+    constexpr int L = decltype(Lc)::value;
+    bf16x8 wz[16], wr[16], wh[16];
+    if constexpr (L == 0) {
+      const uint16_t* W = a.layer[0].W;
+      const uint16_t* R = a.layer[0].R;
+      wz[0] = wfrag(W, ht, 1, 0, lane);
+      wr[0] = wfrag(W, WS_HT + ht, 1, 0, lane);
+      wh[0] = wfrag(W, 2 * WS_HT + ht, 1, 0, lane);
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        wz[1 + ks] = wfrag(R, ht, 8, ks, lane);
+        wr[1 + ks] = wfrag(R, WS_HT + ht, 8, ks, lane);
+        wh[1 + ks] = wfrag(R, 2 * WS_HT + ht, 8, ks, lane);
+      }
+    } else {
+      const uint16_t* W = a.layer[1].W;
+      const uint16_t* R = a.layer[1].R;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        wz[ks] = wfrag(W, ht, 8, ks, lane);
+        wr[ks] = wfrag(W, WS_HT + ht, 8, ks, lane);
+        wh[ks] = wfrag(W, 2 * WS_HT + ht, 8, ks, lane);
+        wz[8 + ks] = wfrag(R, ht, 8, ks, lane);
+        wr[8 + ks] = wfrag(R, WS_HT + ht, 8, ks, lane);
+        wh[8 + ks] = wfrag(R, 2 * WS_HT + ht, 8, ks, lane);
+      }
+    }
+    float bv[4];
+    {
+      const float* bs = a.layer[L].bias;
+      bv[0] = bs[j] + bs[3 * WS_H + j];
+      bv[1] = bs[WS_H + j] + bs[4 * WS_H + j];
+      bv[2] = bs[2 * WS_H + j];
+      bv[3] = bs[5 * WS_H + j];
+    }
+    float hs[W2_RT][4];
+#pragma unroll
+    for (int rt = 0; rt < W2_RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hs[rt][r] = 0.f;
+    uint16_t* const Hl = L == 0 ? H1 : H2;
+    __syncthreads();
+    // phase offset between the two clusters that share a CU: in lockstep both compute, then
+    // both hand off, and the SIMDs idle through the hand-offs; half a step apart, one
+    // cluster's hand-off runs under the other's MFMAs
+    if (a.ws_stagger > 0 && ((b >> 8) & 1)) {
+      const uint64_t t0 = wall_clock64();
+      while (wall_clock64() - t0 < (uint64_t)a.ws_stagger) __builtin_amdgcn_s_sleep(2);
+    }
+#define WS_MARK(t, k) \
+  if (trace && (t) < 64) trace[(t) * 6 + (k)] = (int64_t)wall_clock64()
+    for (int t = 0; t <= T; ++t) {
+      WS_MARK(t, 0);
+      const bool act = L == 0 ? (t < T) : (t >= 1);
+      if constexpr (L == 0) {
+        uint4 xn[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int c = ltid + 128 * u;
+          xn[u] = c < nchunk ? load_x(c, t + 1) : make_uint4(0, 0, 0, 0);
+        }
+        if (act) w2_layer<0>(wz, wr, wh, Xb + (t & 1) * (W2_M * WS_XS), H1, H2, hs, bv, lane);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int c = ltid + 128 * u;
+          if (c < nchunk) *x_slot((t + 1) & 1, c) = xn[u];
+        }
+      } else {
+        if (act) w2_layer<1>(wz, wr, wh, Xb, H1, H2, hs, bv, lane);
+      }
+      __syncthreads();  // every wave is done reading H1 / H2 / X of this step
+      WS_MARK(t, 1);
+      if (t == T) break;
+      if (act) {
+        const int cq = (tile * 16 + ccol) >> 3, ce = ccol & 7;  // this lane's column in the member block
+#pragma unroll
+        for (int rt = 0; rt < W2_RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = rt * 16 + crow + r;
+            Hl[mem * W2_BLK + w2_chunk(row, cq) * 8 + ce] = f32_to_bf16(hs[rt][r]);
+          }
+      }
+      __syncthreads();
+      const int par = t & 1;
+      // publish: this member's two blocks, verbatim (512 chunks, 2 per thread)
+#pragma unroll
+      for (int i = 0; i < W2_CH / 256; ++i) {
+        const int c = i * 256 + tid;
+        const uint16_t* src = ((c >> 8) ? H2 : H1) + mem * W2_BLK + (c & 255) * 8;
+        const u32x4 v = __builtin_bit_cast(u32x4, *reinterpret_cast<const uint4*>(src));
+        __builtin_amdgcn_raw_buffer_store_b128(v, xr, c * 16, ((par * WS_CL + mem) * W2_SLICE) * 2, SC1);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      WS_MARK(t, 2);
+      if (tid == 0) {
+        __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool ok = ws_wait(cnt, WS_CL * (t + 1));
+        if (!ok) atomicExch(a.ws_err, 1);
+        *sflag = ok;
+      }
+      __syncthreads();
+      WS_MARK(t, 3);
+      if (!*sflag) return false;
+      // the other 7 members' slices straight into the LDS image: 7 x 8 KB = 56 global_load_lds
+      // of 1 KB (14 per wave), sc1 (L2-coherent); the barrier below waits vmcnt(0) for them
+      {
+        const uint16_t* slab = a.ws_x + (size_t)cl * 2 * WS_CL * W2_SLICE + (size_t)par * WS_CL * W2_SLICE;
+#pragma unroll
+        for (int i = 0; i < 14; ++i) {
+          const int g = wave * 14 + i;
+          const int m2i = g >> 3;
+          const int m2 = m2i + (m2i >= mem);
+          const int Lg = (g >> 2) & 1, kb = g & 3;
+          const uint16_t* src = slab + (size_t)m2 * W2_SLICE + Lg * W2_BLK + kb * 512 + lane * 8;
+          uint16_t* dst = (Lg ? H2 : H1) + m2 * W2_BLK + kb * 512;
+          __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src),
+                                           (__attribute__((address_space(3))) void*)(dst), 16, 0, SC1);
+        }
+      }
+      __syncthreads();
+      WS_MARK(t, 4);
+    }
+#undef WS_MARK
+    if constexpr (L == 1) {
+      if (a.yh) {
+#pragma unroll
+        for (int rt = 0; rt < W2_RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = row0 + rt * 16 + crow + r;
+            if (row < n_live) a.yh[(size_t)row * WS_H + j] = hs[rt][r];
+          }
+      }
+      if (a.head_w) {
+        const float w = a.head_w[j];
+#pragma unroll
+        for (int rt = 0; rt < W2_RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = hs[rt][r] * w;
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+            if (ccol == 0) red[tile * W2_M + rt * 16 + crow + r] = v;
+          }
+      }
+    }
+    return true;
+  };
+  const bool ok_run = layer == 0 ? run(W2Layer<0>{}) : run(W2Layer<1>{});
+  if (!ok_run) return;
+
+  float* const part = a.ws_part + (size_t)cl * WS_CL * W2_M;
+  if (a.head_w) {
+    __syncthreads();
+    if (tid < W2_M) {
+      const float v = red[tid] + red[W2_M + tid];
+      __hip_atomic_store(part + mem * W2_M + tid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool ok = true;
+    if (mem == 0) {
+      ok = ws_wait(cnt, WS_CL * (T + 1));
+      if (!ok) atomicExch(a.ws_err, 1);
+    }
+    *sflag = ok;
+  }
+  __syncthreads();
+  if (mem != 0 || !*sflag) return;
+  if (a.head_w && tid < W2_M && row0 + tid < n_live) {
+    float v = a.head_b;
+#pragma unroll
+    for (int m2 = 0; m2 < WS_CL; ++m2)
+      v += __hip_atomic_load(part + m2 * W2_M + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.head_act == 2) v = 1.f / (1.f + expf(-v));
+    a.out[row0 + tid] = v;
+  }
+  if (tid == 0) __hip_atomic_exchange(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
 
 size_t gru_ws_lds_bytes() {
   return (size_t)2 * WS_M * WS_HS * 2 + (size_t)2 * WS_M * WS_XS * 2 + (size_t)2 * WS_M * 4 + (size_t)4 * WS_M * 8 + 16;
 }
+static size_t gru_ws2_lds_bytes() {
+  return (size_t)2 * WS_CL * W2_BLK * 2 + (size_t)2 * W2_M * WS_XS * 2 + (size_t)2 * W2_M * 4 + (size_t)4 * W2_M * 8 + 16;
+}
 
 int gru_ws_clusters(int n_rows) { return (n_rows + WS_M - 1) / WS_M; }
+int gru_ws2_clusters(int n_rows) { return (n_rows + W2_M - 1) / W2_M; }
 
 bool gru_ws_eligible(const GruArgs& a) {
   return a.ws_x && a.ws_sync && a.ws_err && a.n_layers == 2 && a.H == WS_H && a.layer[0].lbr == 1 &&
@@ -587,6 +955,11 @@ bool gru_ws_eligible(const GruArgs& a) {
 
 // grid: 64 workgroups per 8 clusters (b = 64 q + 8 member + g, cluster = 8 q + g)
 void launch_gru_ws(const GruArgs& a, hipStream_t st) {
+  if (a.ws == 3) {
+    const int ncl2 = gru_ws2_clusters(a.n_rows);
+    IGP_LAUNCH(gru_ws2_kernel, dim3(((ncl2 + 7) / 8) * 64), dim3(256), gru_ws2_lds_bytes(), st, a);
+    return;
+  }
   const int ncl = gru_ws_clusters(a.n_rows);
   const int grid = ((ncl + 7) / 8) * 64;
   if (a.ws == 2) IGP_LAUNCH(gru_ws_kernel<true>, dim3(grid), dim3(256), gru_ws_lds_bytes(), st, a);

@@ -240,20 +240,23 @@ struct GruArgs {
   int32_t pipeline;         // 2 layers: layer-pipelined kernel (layer 1 @ t || layer 2 @ t-1)
   // weight-stationary cluster path (gru_ws.hip), used when the workspace is given and the
   // model is the 2 x 256, linear_before_reset = 1, input <= 32 shape
-  int32_t ws;               // 0 off | 1 use when eligible
+  int32_t ws;               // 0 off | 1 use when eligible | 2 two-half pipeline | 3 two 64-row clusters per CU
   int32_t ws_clusters;      // workspace capacity in 128-row clusters
-  int32_t* ws_sync;         // [ws_clusters][16] step counters (zeroed per launch)
+  int32_t* ws_sync;         // [2 ws_clusters][16] step counters (back to 0 after every launch)
   uint16_t* ws_x;           // [ws_clusters][2][8][2][128][32] bf16 hand-off slabs
   float* ws_part;           // [ws_clusters][8][128] head partials
   int32_t* ws_err;          // [1] set when a cluster was not co-resident (bounded wait expired)
   int64_t* ws_trace;        // [64][6] phase timestamps of workgroup 0 (nullable; tools/gru_bench.py)
   int32_t split;            // 1: f32-faithful bf16 hi/lo pairs, three MFMAs per product (gru.hip x3)
   int32_t reverse;          // 1: ONNX direction=reverse (every layer): time steps read last to first
+  int32_t ws_stagger;       // ws = 3: wall-clock ticks (10 ns) by which the second half of the grid
+                            // (the co-resident partner cluster under breadth-first dispatch) starts late
 };
 void launch_gru(const GruArgs& a, hipStream_t st);
 bool gru_ws_eligible(const GruArgs& a);
 void launch_gru_ws(const GruArgs& a, hipStream_t st);
 int gru_ws_clusters(int n_rows);
+int gru_ws2_clusters(int n_rows);  // 64-row clusters (ws = 3)
 
 // ---- K9 LTV / churn / segment
 struct LtvArgs {

@@ -275,7 +275,7 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
     const float y = mc_act(sum + a.b2, a.act2);
     mlv[tid] = y;
     const int row = row0 + tid;
-    if (row < a.n_rows) {
+    if (row < n_live) {  // rows past the device live count stay untouched
       if (a.ml) a.ml[row] = y;
       if (a.ltv_out) ltv_row(pfl[tid], &mlv[tid], a.ltv_out + (size_t)row * 6);  // K9, learned LTV
     }
@@ -292,11 +292,18 @@ void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st) {
       IGP_LAUNCH((mlp_chain_kernel<32, 4, true>), dim3((a.n_rows + 31) / 32), dim3(256), 0, st, a);
     return;
   }
-  static const int pf = [] {  // same-box A/B of the weight prefetch depth
-    const char* e = getenv("IGP_MC_PF");
-    return e ? atoi(e) : MC_PF;
-  }();
-  if (a.waves == 8 && pf == 2)
+  const char* pfe = getenv("IGP_MC_PF");  // same-box A/B of the weight prefetch depth (per call: tests flip it)
+  const int pf = pfe ? atoi(pfe) : MC_PF;
+  if (a.waves == 8 && r == 64) {
+    // 64 rows x 8 waves (4 x 4 MFMA tiles per wave): per k-step a CU issues as many MFMA cycles
+    // as it needs L1 cycles for the 32 KB of weight fragments (32 rows: half), so the weight
+    // stream stops bounding the MFMA rate; a batch then occupies half the CUs and the per-slot
+    // streams keep two batches in flight
+    if (pf == 3)
+      IGP_LAUNCH((mlp_chain_kernel<64, 8, false, 3>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
+    else
+      IGP_LAUNCH((mlp_chain_kernel<64, 8, false>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
+  } else if (a.waves == 8 && pf == 2)
     IGP_LAUNCH((mlp_chain_kernel<32, 8, false, 2>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
   else if (a.waves == 8)
     IGP_LAUNCH((mlp_chain_kernel<32, 8, false>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);

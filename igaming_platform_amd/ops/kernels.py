@@ -506,7 +506,8 @@ class GruPack:
                 self._ws_old.append(self._ws)
             dev = self.device
             self._ws = dict(clusters=ncl,
-                            sync=torch.zeros(ncl * 16, dtype=torch.int32, device=dev),
+                            # 16 counters per 128-row cluster, or per 64-row cluster (ws = 3)
+                            sync=torch.zeros(ncl * 32, dtype=torch.int32, device=dev),
                             x=torch.zeros(ncl * 2 * 8 * 2 * 128 * 32, dtype=torch.int16, device=dev),
                             part=torch.zeros(ncl * 8 * 128, dtype=torch.float32, device=dev))
         return self._ws
@@ -529,6 +530,10 @@ class GruPack:
 _GRU_WS = os.environ.get("IGP_GRU_WS", "1") != "0"  # 0: always the batch-parallel K4 (A/B runs)
 # 1: the cluster kernel runs its 128 sequences as two software-pipelined halves (gru_ws.hip SPLIT)
 _GRU_SPLIT = os.environ.get("IGP_GRU_SPLIT", "0") == "1"
+# default cluster layout: 1 one 128-row cluster per CU, 3 two 64-row clusters per CU
+_GRU_WS_MODE = int(os.environ.get("IGP_GRU_WS_MODE", "3"))
+# ws = 3: start offset (10-ns ticks) of the second cluster on each CU (gru_ws.hip ws_stagger)
+_GRU_STAGGER = int(os.environ.get("IGP_GRU_STAGGER", "0"))
 
 
 def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh: Optional[torch.Tensor] = None,
@@ -537,19 +542,19 @@ def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh
         ws: Optional[int] = None, ws_trace: Optional[torch.Tensor] = None) -> None:
     """K4. Input either dense ``X`` f32 [T, rows, I] or the store's event rings for ``slots``.
     ``ws``: 0 the batch-parallel kernel; 1 the weight-stationary cluster kernel when the model
-    shape allows it; 2 the same with its two-half hand-off pipeline; None: 1, or 2 under
-    IGP_GRU_SPLIT=1."""
+    shape allows it; 2 the same with its two-half hand-off pipeline; 3 two 64-row clusters per
+    CU (gru_ws2_kernel); None: 1, or 2 under IGP_GRU_SPLIT=1."""
     if ws is None:
-        ws = 2 if _GRU_SPLIT else 1
-    if ws not in (0, 1, 2):
-        raise ValueError("gru: ws must be 0, 1 or 2")
+        ws = 2 if _GRU_SPLIT else _GRU_WS_MODE
+    if ws not in (0, 1, 2, 3):
+        raise ValueError("gru: ws must be 0, 1, 2 or 3")
     dev = gp.device
     d = dict(n_layers=gp.n_layers, H=gp.H, T=int(T), I=gp.I, n_rows=int(n_rows),
              m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32, device=dev), tile_rows=int(tile_rows),
              waves=int(waves or gp.waves), pipeline=int(pipeline))
     w = gp.workspace(n_rows) if ws and _GRU_WS else None
     if w is not None:
-        d.update(ws=int(ws), ws_clusters=w["clusters"], ws_sync=w["sync"].data_ptr(), ws_x=w["x"].data_ptr(),
+        d.update(ws=int(ws), ws_stagger=_GRU_STAGGER, ws_clusters=w["clusters"], ws_sync=w["sync"].data_ptr(), ws_x=w["x"].data_ptr(),
                  ws_part=w["part"].data_ptr(), ws_err=gp.ws_err.data_ptr(),
                  ws_trace=_opt(ws_trace, "ws_trace", dtype=torch.int64, min_numel=64 * 8 + 4, device=dev))
     if gp.split:
@@ -653,7 +658,7 @@ def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, s
     [rows] and/or the K9 rows ``ltv_out`` [rows, 6]."""
     dev = pk.device
     d = dict(n_rows=int(n_rows), n_layers=len(pk.layers), in_w=pk.in_w, in_live=pk.in_live,
-             rows_per_block=int(os.environ.get("IGP_MLP_ROWS", "32")), waves=pk.waves(),
+             rows_per_block=int(os.environ.get("IGP_MLP_ROWS", "64")), waves=pk.waves(),
              m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32, device=dev), w2=_need(pk.w2, "w2", torch.float32, device=dev),
              b2=pk.b2, act2=pk.act2,
              ml=_opt(ml, "ml", dtype=torch.float32, min_numel=n_rows, device=dev),

@@ -146,6 +146,30 @@ def test_gru_weight_stationary_matches_batch_parallel(rows):
         np.testing.assert_allclose(a, ref, rtol=0, atol=1e-2)
 
 
+@pytest.mark.parametrize("rows", [1, 100, 4096, 8000])
+def test_gru_two_clusters_per_cu_matches_one(rows):
+    """ws=3 (64-row clusters, two per CU, member-major swizzled LDS image gathered with
+    global_load_lds) computes every row exactly as the 128-row cluster kernel: same bf16
+    operands, same k order, same epilogue and head order -> bit-identical outputs, also from
+    the event rings and on repeated launches (counters returned to 0). 8000 rows exceed the
+    two-per-CU capacity: the launcher falls back to the batch-parallel kernel."""
+    import torch
+    from igaming_platform_amd.ops import kernels as K
+    T = 24
+    N, m, gp = _ws_pack(T)
+    rng = np.random.default_rng(rows + 11)
+    Xd = torch.from_numpy(rng.standard_normal((T, rows, 16)).astype(np.float32)).cuda()
+    o1 = torch.full((rows,), -9.0, device="cuda")
+    o3 = torch.full((rows,), -9.0, device="cuda")
+    K.gru(gp, rows, T, out=o1, X=Xd, ws=1 if rows <= 4096 else 0)
+    for _ in range(2):
+        o3.fill_(-9.0)
+        K.gru(gp, rows, T, out=o3, X=Xd, ws=3)
+        torch.cuda.synchronize()
+        assert not gp.ws_failed()
+        assert torch.equal(o1, o3)
+
+
 @pytest.mark.parametrize("rows", [130, 4096, 4500])
 def test_gru_weight_stationary_split_matches_unsplit(rows):
     """The cluster kernel's two-half pipeline (ws=2: one half's hand-off beside the other

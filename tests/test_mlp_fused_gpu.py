@@ -45,6 +45,40 @@ def test_mlp_chain_dense_input_matches_reference():
     np.testing.assert_allclose(got[:n - 5], ref.cpu().numpy()[:n - 5], atol=2e-3, rtol=2e-3)
 
 
+@pytest.mark.parametrize("pf", ["5", "3"])
+def test_mlp_chain_64_row_tiles_match_32(monkeypatch, pf):
+    """64 rows x 8 waves per workgroup (4 x 4 MFMA tiles per wave) computes every row with the
+    same bf16 operands in the same k order as the 32-row tiles: bit-identical outputs, also
+    with a live count that ends inside a tile."""
+    import torch
+    from igaming_platform_amd.models.plan import DenseStep, HeadStep
+    from igaming_platform_amd.ops import kernels as K
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(5)
+    dims = [(256, 512), (512, 512), (512, 512), (512, 512)]
+    steps = [DenseStep(n=n, k=k, act="relu", w_np=rng.normal(0, 0.05, (n, k)).astype(np.float32),
+                       b_np=rng.normal(0, 0.1, n).astype(np.float32)) for k, n in dims[:-1]]
+    steps.append(HeadStep(n1=512, k=512, act1="relu", act2="none",
+                          w1_np=rng.normal(0, 0.05, (512, 512)).astype(np.float32),
+                          b1_np=rng.normal(0, 0.1, 512).astype(np.float32),
+                          w2_np=rng.normal(0, 0.1, 512).astype(np.float32), b2=0.2))
+    pk = K.MlpChainPack(steps, dev)
+    assert pk.waves() == 8
+    n = 1000
+    X = torch.from_numpy(rng.normal(0, 1, (n, 256)).astype(np.float32)).to(dev)
+    m_ptr = torch.tensor([n - 23], dtype=torch.int32, device=dev)
+    outs = {}
+    for rows in ("32", "64"):
+        monkeypatch.setenv("IGP_MLP_ROWS", rows)
+        monkeypatch.setenv("IGP_MC_PF", pf)
+        ml = torch.full((n,), -7.0, device=dev)
+        K.mlp_chain(pk, n, X=X, ml=ml, m_ptr=m_ptr)
+        torch.cuda.synchronize()
+        outs[rows] = ml.cpu()
+    assert torch.equal(outs["32"], outs["64"])
+    assert torch.all(outs["64"][n - 23:] == -7.0) and not torch.any(outs["64"][:n - 23] == -7.0)
+
+
 def _ltv_gpu(fused: bool, plan, dev, cap):
     from igaming_platform_amd.engine.ltv import LtvGpu
     old = os.environ.get("IGP_MLP_FUSED")

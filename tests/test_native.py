@@ -270,6 +270,56 @@ def test_wire_serialize_matches_python_protobuf():
     assert [P.ScoreTransactionResponse.FromString(b).score for b in many] == list(u["score"])
 
 
+def test_wire_serialize_bytes_equal_python_protobuf():
+    """The branch-free response writer (wire.cpp FastOut) emits exactly the bytes of Python
+    protobuf's serializer: random zero / small / large / negative integers, -0.0 and ordinary
+    floats, every reason-code combination, and bodies longer than 127 bytes (two-byte lengths)."""
+    from igaming_platform_amd.layouts import FEATREC, pack_results, unpack_results
+    from igaming_platform_amd.config import REASON_CODES
+    n = 3000
+    rng = np.random.default_rng(7)
+    res = pack_results(rng.integers(0, 101, n), rng.integers(0, 101, n), rng.integers(0, 4, n),
+                       rng.integers(0, 4096, n), rng.choice([0.0, -0.0, 0.5, 1e-30, 0.999], n).astype(np.float32),
+                       np.ones(n, bool))
+    f = np.zeros(n, FEATREC)
+    pick = lambda vals: rng.choice(np.asarray(vals), n)  # noqa: E731
+    for k, t in FEATREC.descr:
+        if k in ("flags", "tx_type", "slot", "amount", "rule_reasons", "rule_score"):
+            continue
+        if t == "<f4":
+            f[k] = pick([0.0, -0.0, 1.5, 3.25e7, -2.0, 1e-40]).astype(np.float32)
+        elif t == "<i8":
+            f[k] = pick([0, 1, 127, 128, 16383, 16384, 2**35, 2**55, 2**56, 2**62, -1, -(2**40)]).astype(np.int64)
+        else:
+            f[k] = pick([0, 1, 127, 128, 300, 2**20, 2**31 - 1, -1, -(2**31)]).astype(np.int32)
+    f["flags"] = rng.integers(0, 64, n)
+    ms = rng.choice(np.array([0, 3, 200, 2**40], np.int64), n)
+    got = N.serialize_batch_response(res, f.view(np.int32).reshape(n, 32), ms)
+    u = unpack_results(res)
+    fv = lambda i: P.FeatureVector(  # noqa: E731
+        tx_count_1m=int(f["tx_count_1m"][i]), tx_count_5m=int(f["tx_count_5m"][i]), tx_count_1h=int(f["tx_count_1h"][i]),
+        tx_sum_1h=int(f["tx_sum_1h"][i]), tx_avg_1h=float(f["tx_avg_1h"][i]),
+        unique_devices_24h=int(f["unique_devices_24h"][i]), unique_ips_24h=int(f["unique_ips_24h"][i]),
+        ip_country_changes_7d=int(f["ip_country_changes_7d"][i]), device_age_days=int(f["device_age_days"][i]),
+        account_age_days=int(f["account_age_days"][i]), total_deposits=int(f["total_deposits"][i]),
+        total_withdrawals=int(f["total_withdrawals"][i]), net_deposit=int(f["net_deposit"][i]),
+        deposit_count=int(f["deposit_count"][i]), withdraw_count=int(f["withdraw_count"][i]),
+        time_since_last_tx_sec=int(f["time_since_last_tx_sec"][i]),
+        session_duration_sec=int(f["session_duration_sec"][i]), avg_bet_size=float(f["avg_bet_size"][i]),
+        win_rate=float(f["win_rate"][i]), is_vpn=bool(f["flags"][i] & 1), is_proxy=bool(f["flags"][i] & 2),
+        is_tor=bool(f["flags"][i] & 4), disposable_email=bool(f["flags"][i] & 8),
+        bonus_claim_count=int(f["bonus_claim_count"][i]),
+        bonus_wager_completion_rate=float(f["bonus_wager_completion_rate"][i]),
+        bonus_only_player=bool(f["flags"][i] & 16))
+    want = P.ScoreBatchResponse(results=[
+        P.ScoreTransactionResponse(score=int(u["score"][i]), action=int(u["action"][i]),
+                                   reason_codes=[REASON_CODES[b] for b in range(12) if u["reasons"][i] >> b & 1],
+                                   rule_score=int(u["rule_score"][i]), ml_score=float(u["ml"][i]),
+                                   response_time_ms=int(ms[i]), features=fv(i))
+        for i in range(n)]).SerializeToString()
+    assert got == want
+
+
 def test_wire_rejects_truncated_input():
     data = P.ScoreBatchRequest(transactions=_batch(3)).SerializeToString()
     rb = N.RequestBatch()

@@ -19,9 +19,13 @@ def main() -> int:
     R = S.runner
     res = []
     ref = {}
-    for B in (512, 4096, 8192):
+    batches = [int(b) for b in os.environ.get("GRU_BATCHES", "512,4096,8192").split(",")]
+    variants = ((16, 0, 1, 1), (16, 0, 1, 3), (16, 4, 0, 0), (16, 8, 0, 0), (32, 4, 0, 0), (16, 0, 1, 0), (32, 0, 1, 0))
+    if os.environ.get("GRU_WS_ONLY"):  # the cluster kernels and the default batch-parallel one
+        variants = ((16, 0, 1, 1), (16, 0, 1, 3), (16, 0, 1, 0))
+    for B in batches:
         slots = torch.from_numpy(np.random.default_rng(B).integers(0, 1 << 18, B).astype(np.int32)).to(dev)
-        for tr, w, pipe, ws in ((16, 0, 1, 1), (16, 4, 0, 0), (16, 8, 0, 0), (32, 4, 0, 0), (16, 0, 1, 0), (32, 0, 1, 0)):
+        for tr, w, pipe, ws in variants:
             if True:
                 out = torch.zeros(B, device=dev)
                 run = lambda: K.gru(R.gp, B, R.T, out=out, store=R.store, slots=slots, tile_rows=tr, waves=w,  # noqa

@@ -16,6 +16,7 @@ def main() -> int:
     from igaming_platform_amd.utils import benchkit
     from igaming_platform_amd.ops import kernels as K
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    ws = int(sys.argv[2]) if len(sys.argv) > 2 else 1  # 1: one cluster per CU, 3: two 64-row clusters per CU
     dev = torch.device("cuda", 0)
     S = benchkit.build_model("cfg5", B, 1 << 16, dev, use_graphs=False)
     R = S.runner
@@ -23,7 +24,7 @@ def main() -> int:
     out = torch.zeros(B, device=dev)
     tr = torch.zeros(64 * 8 + 4, dtype=torch.int64, device=dev)
     for _ in range(3):
-        K.gru(R.gp, B, R.T, out=out, store=R.store, slots=slots, ws=1, ws_trace=tr)
+        K.gru(R.gp, B, R.T, out=out, store=R.store, slots=slots, ws=ws, ws_trace=tr)
     torch.cuda.synchronize()
     raw = tr.cpu().numpy()
     t = raw[:64 * 6].reshape(64, 6).astype(np.float64) / 100.0  # us
