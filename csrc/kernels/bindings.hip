@@ -446,7 +446,6 @@ PYBIND11_MODULE(_hipk, m) {
     a.ws_trace = ptr<int64_t*>(d, "ws_trace");
     a.split = geti(d, "split");
     a.reverse = geti(d, "reverse", 0);
-    a.ws_stagger = geti(d, "ws_stagger", 0);
     if (a.split) {
       for (int l = 0; l < a.n_layers; ++l)
         if (!a.layer[l].W_lo || !a.layer[l].R_lo) throw std::runtime_error("gru: split mode needs residual weights");
@@ -465,6 +464,7 @@ PYBIND11_MODULE(_hipk, m) {
     check("gru");
   });
   m.def("gru_ws_clusters", [](int n_rows) { return gru_ws_clusters(n_rows); });
+  m.def("mlp_pair_clusters", [](int n_rows) { return mlp_pair_clusters(n_rows); });
 
   m.def("mlp_chain", [](py::dict d, uintptr_t s) {
     MlpChainArgs a{};
@@ -507,6 +507,11 @@ PYBIND11_MODULE(_hipk, m) {
     for (int l = 0; l < a.n_layers; ++l)
       if (a.N[l] % (16 * a.waves)) throw std::runtime_error("mlp_chain: N must be a multiple of 16 x waves");
     a.split = geti(d, "split", 0);
+    a.pair_x = ptr<uint16_t*>(d, "pair_x");
+    a.pair_sync = ptr<int32_t*>(d, "pair_sync");
+    a.pair_part = ptr<float*>(d, "pair_part");
+    a.pair_err = ptr<int32_t*>(d, "pair_err");
+    a.pair_clusters = geti(d, "pair_clusters", 0);
     if (a.split) {
       for (int l = 0; l < a.n_layers; ++l)
         if (!a.W_lo[l]) throw std::runtime_error("mlp_chain: split mode needs every layer's residual weights");

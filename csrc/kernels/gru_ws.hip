@@ -743,6 +743,10 @@ __global__ void __launch_bounds__(256, 2) gru_ws2_kernel(GruArgs a) {
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       a.ws_x + (size_t)cl * 2 * WS_CL * W2_SLICE, 0, 2 * WS_CL * W2_SLICE * 2, 0x00020000);
   int64_t* const trace = (a.ws_trace && b == 0 && tid == 0) ? a.ws_trace : nullptr;
+  // placement record (trace runs only): which XCD / SE / CU / SIMD each workgroup's wave 0 got
+  if (a.ws_trace && tid == 0 && b < 1024)
+    a.ws_trace[64 * 8 + 4 + b] = ((int64_t)__builtin_amdgcn_s_getreg(0xF814) << 32) |
+                                 (uint32_t)__builtin_amdgcn_s_getreg(0xF804);  // XCC_ID | HW_ID
 
   // the whole recurrence, specialised per layer: each wave runs exactly one instantiation, so
   // the register allocator sees one set of stationary weights (192 registers for layer 2, 108
@@ -791,13 +795,6 @@ __global__ void __launch_bounds__(256, 2) gru_ws2_kernel(GruArgs a) {
       for (int r = 0; r < 4; ++r) hs[rt][r] = 0.f;
     uint16_t* const Hl = L == 0 ? H1 : H2;
     __syncthreads();
-    // phase offset between the two clusters that share a CU: in lockstep both compute, then
-    // both hand off, and the SIMDs idle through the hand-offs; half a step apart, one
-    // cluster's hand-off runs under the other's MFMAs
-    if (a.ws_stagger > 0 && ((b >> 8) & 1)) {
-      const uint64_t t0 = wall_clock64();
-      while (wall_clock64() - t0 < (uint64_t)a.ws_stagger) __builtin_amdgcn_s_sleep(2);
-    }
 #define WS_MARK(t, k) \
   if (trace && (t) < 64) trace[(t) * 6 + (k)] = (int64_t)wall_clock64()
     for (int t = 0; t <= T; ++t) {
@@ -832,8 +829,8 @@ __global__ void __launch_bounds__(256, 2) gru_ws2_kernel(GruArgs a) {
             Hl[mem * W2_BLK + w2_chunk(row, cq) * 8 + ce] = f32_to_bf16(hs[rt][r]);
           }
       }
-      __syncthreads();
       const int par = t & 1;
+      __syncthreads();
       // publish: this member's two blocks, verbatim (512 chunks, 2 per thread)
 #pragma unroll
       for (int i = 0; i < W2_CH / 256; ++i) {

@@ -4,11 +4,11 @@
 // K9 churn / segment / next-best-action epilogue.
 //
 // One workgroup = 32 rows, 4 waves (8192 rows -> 256 workgroups, one per CU). The 32-row
-// activation tile lives in LDS for the whole chain (bf16, two 32 x 520 buffers ping-ponged
+// activation tile lives in LDS for the whole chain (bf16, two 32 x 512 buffers ping-ponged
 // between layers: 66.5 KB), so hidden activations never touch HBM and the chain is one launch
 // instead of five. Each wave owns a quarter of a layer's output columns (N/4 <= 128: eight
 // 16-column MFMA tiles x two 16-row tiles, v_mfma_f32_16x16x32_bf16, f32 accumulators). A
-// fragments come from LDS (ds_read_b128; the 1040-byte row pitch spreads a 16-row read over all
+// fragments come from LDS (ds_read_b128; 16-B chunks XOR-swizzled by row, mc_idx, spread a read over all
 // 64 banks); B fragments are 16-byte loads straight from the weights [N][K] (L2-resident: the
 // whole 4 x 512 chain is 1.8 MB bf16, every workgroup reads it), prefetched two K-steps ahead
 // into a 3-deep register ring. Bias + activation + bf16 rounding of a hidden layer happen in
@@ -23,7 +23,7 @@
 // bits), and each product runs as three MFMAs, hi*hi + hi*lo + lo*hi (lo*lo, ~2^-18 relative,
 // is dropped), accumulated in f32: f32-faithful to ~1e-5 relative at bf16 MFMA rates, where the
 // f32 MFMA (v_mfma_f32_16x16x4_f32) would run the chain ~16x slower. The hi and lo activation
-// tiles both live in LDS (4 x 32 x 520 bf16 = 133 KB).
+// tiles both live in LDS (4 x 32 x 512 bf16 = 128 KB).
 #include "common.h"
 #include "launch.h"
 #include "ltv.h"
@@ -33,7 +33,15 @@ namespace igp {
 typedef __attribute__((ext_vector_type(8))) short mc_bf16x8;
 typedef __attribute__((ext_vector_type(4))) float mc_f32x4;
 
-constexpr int MC_LDA = 512 + 8;  // bf16 elements per LDS row (1040 B)
+constexpr int MC_LDA = 512;  // bf16 elements per LDS row (1024 B, 64 chunks of 16 B, swizzled)
+// element (row, col) of an LDS activation tile: 16-B chunk col / 8 of the row stored at chunk
+// (col / 8) ^ (row & 15). ds_read_b128 serves a wave in 4 lane groups ({0-3, 12-15, 20-27}, ...,
+// MI355X_MICROARCH.md LDS table); with the old 1040-B pitch rows r and r + 12 of one group hit
+// the same bank (SQ_LDS_BANK_CONFLICT ~2 cycles per LDS instruction, profiles/r3/n); swizzled,
+// every group of an A-fragment read touches 16 distinct 16-B bank slots.
+__device__ __forceinline__ int mc_idx(int row, int col) {
+  return row * MC_LDA + ((((col >> 3) ^ (row & 15))) << 3) + (col & 7);
+}
 constexpr int MC_PF = 5;  // k-steps of weight fragments prefetched ahead (bf16 path; IGP_MC_PF=2: the r2 depth)
 
 __device__ __forceinline__ float mc_act(float v, int act) {
@@ -52,21 +60,22 @@ __device__ __forceinline__ float mc_act(float v, int act) {
 // the texture path, not the MFMA, set the pace: 92 -> see profiles/NOTES.md).
 template <int NKS, int MT, int JT, bool SPLIT, int PFD = MC_PF>
 __device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, const uint16_t* __restrict__ Hlo,
-                                             const uint16_t* __restrict__ W, const uint16_t* __restrict__ Wlo, int K,
+                                             const uint16_t* __restrict__ W, const uint16_t* __restrict__ Wlo, int N,
                                              int colw, int NT, int lane, mc_f32x4 (&acc)[MT][JT]) {
+  const int NTT = N >> 4;  // column tiles of the layer: a k-step's tiles are NTT x 1 KB contiguous
   if constexpr (SPLIT) {
     // hi*hi + hi*lo + lo*hi per k-step; both weight halves prefetched one k-step ahead
     mc_bf16x8 fh[2][JT], fl[2][JT];
     const int kq = 8 * (lane >> 4);
-    const size_t woff = ((size_t)(colw >> 4) * NKS) * 512 + lane * 8;
+    const size_t woff = (size_t)(colw >> 4) * 512 + lane * 8;
     int jt[JT];
 #pragma unroll
-    for (int j = 0; j < JT; ++j) jt[j] = (j < NT ? j : NT - 1) * NKS;
+    for (int j = 0; j < JT; ++j) jt[j] = j < NT ? j : NT - 1;
     auto load = [&](int ks, mc_bf16x8 (&dh)[JT], mc_bf16x8 (&dl)[JT]) {
 #pragma unroll
       for (int j = 0; j < JT; ++j) {
-        dh[j] = *reinterpret_cast<const mc_bf16x8*>(W + woff + ((size_t)jt[j] + ks) * 512);
-        dl[j] = *reinterpret_cast<const mc_bf16x8*>(Wlo + woff + ((size_t)jt[j] + ks) * 512);
+        dh[j] = *reinterpret_cast<const mc_bf16x8*>(W + woff + ((size_t)ks * NTT + jt[j]) * 512);
+        dl[j] = *reinterpret_cast<const mc_bf16x8*>(Wlo + woff + ((size_t)ks * NTT + jt[j]) * 512);
       }
     };
     load(0, fh[0], fl[0]);
@@ -77,7 +86,7 @@ __device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, c
       mc_bf16x8 ah[MT], al[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        const int o = (16 * m + (lane & 15)) * MC_LDA + ks * 32 + kq;
+        const int o = mc_idx(16 * m + (lane & 15), ks * 32 + kq);
         ah[m] = *reinterpret_cast<const mc_bf16x8*>(&Hin[o]);
         al[m] = *reinterpret_cast<const mc_bf16x8*>(&Hlo[o]);
       }
@@ -92,21 +101,22 @@ __device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, c
     }
     return;
   }
-  // PF k-steps of B fragments in flight: a k-step is only JT x MT MFMAs (8 x 8 cycles at 8
-  // waves), so covering the ~700-cycle L2 latency needs ~5 steps ahead, not 2
+  // PF k-steps of B fragments in flight: a k-step is only JT x MT MFMAs, so covering the L2
+  // latency of lines every CU of the XCD requests at once (~1 us, tools/mlp_bench.py) needs
+  // 8-10 steps ahead
   constexpr int PF = PFD < NKS ? PFD : NKS - 1;
   constexpr int RING = PF + 1;
   mc_bf16x8 fb[RING][JT];
   const int kq = 8 * (lane >> 4);
-  const uint16_t* wt = W + ((size_t)(colw >> 4) * NKS) * 512 + lane * 8;  // this wave's first n-tile
+  const uint16_t* wt = W + (size_t)(colw >> 4) * 512 + lane * 8;  // this wave's first n-tile
   // branch-free: tiles j >= NT (layers narrower than 512) re-load tile NT-1 and their
   // accumulators are never read; a guarded load made hipcc branch and wait vmcnt(0) per load
   int jt[JT];
 #pragma unroll
-  for (int j = 0; j < JT; ++j) jt[j] = (j < NT ? j : NT - 1) * NKS;
+  for (int j = 0; j < JT; ++j) jt[j] = j < NT ? j : NT - 1;
   auto load = [&](int ks, mc_bf16x8 (&dst)[JT]) {
 #pragma unroll
-    for (int j = 0; j < JT; ++j) dst[j] = *reinterpret_cast<const mc_bf16x8*>(wt + ((size_t)jt[j] + ks) * 512);
+    for (int j = 0; j < JT; ++j) dst[j] = *reinterpret_cast<const mc_bf16x8*>(wt + ((size_t)ks * NTT + jt[j]) * 512);
   };
 #pragma unroll
   for (int p = 0; p < PF; ++p) load(p, fb[p]);
@@ -119,7 +129,7 @@ __device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, c
     mc_bf16x8 fa[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
-      fa[m] = *reinterpret_cast<const mc_bf16x8*>(&Hin[(16 * m + (lane & 15)) * MC_LDA + ks * 32 + kq]);
+      fa[m] = *reinterpret_cast<const mc_bf16x8*>(&Hin[mc_idx(16 * m + (lane & 15), ks * 32 + kq)]);
 #pragma unroll
     for (int j = 0; j < JT; ++j)
 #pragma unroll
@@ -185,9 +195,9 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
           x = copysignf(log1pf(fabsf(x)), x);  // [sign*log1p|profile| (25) | extended features]
         }
         if constexpr (SPLIT) {
-          mc_split(x, H[0][r * MC_LDA + c], H[2][r * MC_LDA + c]);
+          mc_split(x, H[0][mc_idx(r, c)], H[2][mc_idx(r, c)]);
         } else {
-          H[0][r * MC_LDA + c] = f32_to_bf16(x);
+          H[0][mc_idx(r, c)] = f32_to_bf16(x);
         }
       }
     }
@@ -207,14 +217,14 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
     const uint16_t* Hlo = H[SPLIT ? 2 + cur : cur];
     const uint16_t* Wl = SPLIT ? a.W_lo[l] : nullptr;
     switch (K >> 5) {  // K-steps of 32 (the host allows 2..16)
-      case 2: mc_layer_mma<2, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
-      case 4: mc_layer_mma<4, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
-      case 6: mc_layer_mma<6, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
-      case 8: mc_layer_mma<8, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
-      case 10: mc_layer_mma<10, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
-      case 12: mc_layer_mma<12, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
-      case 14: mc_layer_mma<14, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
-      default: mc_layer_mma<16, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, K, colw, NT, lane, acc); break;
+      case 2: mc_layer_mma<2, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, N, colw, NT, lane, acc); break;
+      case 4: mc_layer_mma<4, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, N, colw, NT, lane, acc); break;
+      case 6: mc_layer_mma<6, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, N, colw, NT, lane, acc); break;
+      case 8: mc_layer_mma<8, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, N, colw, NT, lane, acc); break;
+      case 10: mc_layer_mma<10, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, N, colw, NT, lane, acc); break;
+      case 12: mc_layer_mma<12, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, N, colw, NT, lane, acc); break;
+      case 14: mc_layer_mma<14, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, N, colw, NT, lane, acc); break;
+      default: mc_layer_mma<16, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, N, colw, NT, lane, acc); break;
     }
     const float* bias = a.bias[l];
     const int act = a.act[l];
@@ -231,7 +241,7 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
           const float b = bias ? bias[col] : 0.f;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const int o = (m * 16 + 4 * (lane >> 4) + q) * MC_LDA + col;
+            const int o = mc_idx(m * 16 + 4 * (lane >> 4) + q, col);
             const float v = mc_act(acc[m][j][q] + b, act);
             if constexpr (SPLIT) mc_split(v, Hout[o], Hout_lo[o]);
             else Hout[o] = f32_to_bf16(v);
@@ -284,6 +294,7 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
 
 void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
+  if (mlp_pair_eligible(a)) return launch_mlp_pair(a, st);
   const int r = a.rows_per_block;
   if (a.split) {  // f32-faithful: 32 rows per block (hi + lo tiles fill the LDS)
     if (a.waves == 8)
@@ -293,20 +304,27 @@ void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st) {
     return;
   }
   const char* pfe = getenv("IGP_MC_PF");  // same-box A/B of the weight prefetch depth (per call: tests flip it)
-  const int pf = pfe ? atoi(pfe) : MC_PF;
+  const int pf = pfe ? atoi(pfe) : 0;      // 0: the default depth of the tile shape
   if (a.waves == 8 && r == 64) {
     // 64 rows x 8 waves (4 x 4 MFMA tiles per wave): per k-step a CU issues as many MFMA cycles
-    // as it needs L1 cycles for the 32 KB of weight fragments (32 rows: half), so the weight
-    // stream stops bounding the MFMA rate; a batch then occupies half the CUs and the per-slot
-    // streams keep two batches in flight
-    if (pf == 3)
-      IGP_LAUNCH((mlp_chain_kernel<64, 8, false, 3>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
+    // as it needs L1 cycles for the 32 KB of weight fragments (32 rows: half); a batch then
+    // occupies half the CUs and the per-slot streams keep two batches in flight
+    if (pf == 5)
+      IGP_LAUNCH((mlp_chain_kernel<64, 8, false, 5>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
     else
-      IGP_LAUNCH((mlp_chain_kernel<64, 8, false>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
-  } else if (a.waves == 8 && pf == 2)
-    IGP_LAUNCH((mlp_chain_kernel<32, 8, false, 2>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
-  else if (a.waves == 8)
-    IGP_LAUNCH((mlp_chain_kernel<32, 8, false>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
+      IGP_LAUNCH((mlp_chain_kernel<64, 8, false, 8>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
+  } else if (a.waves == 8) {
+    // 32 rows x 8 waves: a k-step is 8 MFMAs per wave (~0.11 us at two waves per SIMD) against
+    // ~1 us of L2 latency for the weight fragments every CU of the XCD reads at the same time
+    // (tools/mlp_bench.py: the launch time hardly changes from 4096 to 8192 rows): the prefetch
+    // ring holds 10 k-steps (11 x 4 fragments, 176 VGPRs)
+    if (pf == 5)
+      IGP_LAUNCH((mlp_chain_kernel<32, 8, false, 5>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
+    else if (pf == 8)
+      IGP_LAUNCH((mlp_chain_kernel<32, 8, false, 8>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
+    else
+      IGP_LAUNCH((mlp_chain_kernel<32, 8, false, 10>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
+  }
   else if (r == 64)
     IGP_LAUNCH((mlp_chain_kernel<64, 4, false>), dim3((a.n_rows + 63) / 64), dim3(256), 0, st, a);
   else if (r == 16)

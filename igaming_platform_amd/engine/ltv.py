@@ -26,9 +26,13 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from ..golden import ltv as GL
+from ..obs.logging import get_logger
 
 N_COLS = len(GL.PLAYER_COLUMNS)
 
+
+
+log = get_logger("ltv")
 
 def ltv_model_input(pf: np.ndarray, ext: Optional[np.ndarray], width: int) -> np.ndarray:
     pf = np.asarray(pf, np.float32).reshape(-1, N_COLS)
@@ -183,7 +187,7 @@ class LtvGpu:
         nout = b * self.out.shape[1] * self.out.element_size()
         if self.chain is not None:
             K.mlp_chain(self.chain, b, slots=self.slots, pf_tab=self.pf_tab, ext_tab=self.ext_tab,
-                        ltv_out=self.out, m_ptr=self.n_ptr)
+                        ltv_out=self.out, m_ptr=self.n_ptr, ws_key=slot % len(self._slabs))
             cp(self.host_out[slot], self.out, nout)
             return
         ml = None
@@ -265,10 +269,31 @@ class LtvGpu:
         slot, n, ev = p
         try:
             ev.synchronize()
-            return self.host_out[slot][:n].numpy().copy()
+            out = self.host_out[slot][:n].numpy().copy()
+            if self.chain is not None and self.chain.pair_ok and n and np.isnan(out).any():
+                out = self._pair_fallback(slot, n)
+            return out
         finally:
             if release:
                 self._slot_locks[slot].release()
+
+    def _pair_fallback(self, slot: int, n: int) -> np.ndarray:
+        """A pair-cluster launch gave up (its two workgroups were not co-resident): switch the
+        chain to the one-workgroup kernel, re-capture, and recompute the batch."""
+        torch = self.torch
+        log.error("LTV chain: pair kernel timed out; falling back to the one-workgroup kernel")
+        with self._lock:
+            torch.cuda.synchronize(self.device)
+            self.chain.disable_pair()
+            b = self.bucket_for(max(n, 1))
+            self._use(slot)
+            with torch.cuda.stream(self.stream):
+                self._body(slot, b)
+            self.stream.synchronize()
+            out = self.host_out[slot][:n].numpy().copy()
+            self.graphs.clear()
+            self.capture()
+        return out
 
     def predict_slots(self, slots: np.ndarray) -> np.ndarray:
         """slots -> [n, 6] (ltv, churn, survival, confidence, segment, nba)."""

@@ -11,7 +11,7 @@ import contextlib
 
 import os
 
-from typing import Optional
+from typing import Dict, Optional
 
 import torch
 
@@ -427,9 +427,13 @@ def ltv_assemble(slots: torch.Tensor, pf_tab: torch.Tensor, ext_tab: Optional[to
 
 
 # --------------------------------------------------------------------------- K4
-def pack_fragments(w, k_pad: int) -> torch.Tensor:
+def pack_fragments(w, k_pad: int, ks_major: bool = False) -> torch.Tensor:
     """[N, K] float -> bf16 MFMA B-fragment order P[N/16][k_pad/32][64 lanes][8]
-    (lane l of tile (nt, ks) holds W[nt*16 + (l&15)][ks*32 + 8*(l>>4) .. +8])."""
+    (lane l of tile (nt, ks) holds W[nt*16 + (l&15)][ks*32 + 8*(l>>4) .. +8]).
+    ``ks_major``: P[k_pad/32][N/16][64][8] - the tiles one k-step reads across all columns are
+    contiguous. The chain kernels stream weights that way: every CU of an XCD reads the same
+    k-step at about the same time, and with N/16-major order those 1-KB tiles sat NKS KB apart,
+    i.e. on the same few L2 channels."""
     import numpy as np
     w = np.asarray(w, np.float32)
     n, k = w.shape
@@ -439,6 +443,8 @@ def pack_fragments(w, k_pad: int) -> torch.Tensor:
     buf[:, :k] = w
     # [nt, 16 rows, ks, 4 kgroups, 8] -> [nt, ks, kgroup, row, 8] (lane = kgroup*16 + row)
     t = buf.reshape(n // 16, 16, k_pad // 32, 4, 8).transpose(0, 2, 3, 1, 4)
+    if ks_major:
+        t = t.transpose(1, 0, 2, 3, 4)
     return torch.from_numpy(np.ascontiguousarray(t).reshape(-1)).to(torch.bfloat16)
 
 
@@ -532,8 +538,6 @@ _GRU_WS = os.environ.get("IGP_GRU_WS", "1") != "0"  # 0: always the batch-parall
 _GRU_SPLIT = os.environ.get("IGP_GRU_SPLIT", "0") == "1"
 # default cluster layout: 1 one 128-row cluster per CU, 3 two 64-row clusters per CU
 _GRU_WS_MODE = int(os.environ.get("IGP_GRU_WS_MODE", "3"))
-# ws = 3: start offset (10-ns ticks) of the second cluster on each CU (gru_ws.hip ws_stagger)
-_GRU_STAGGER = int(os.environ.get("IGP_GRU_STAGGER", "0"))
 
 
 def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh: Optional[torch.Tensor] = None,
@@ -543,20 +547,20 @@ def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh
     """K4. Input either dense ``X`` f32 [T, rows, I] or the store's event rings for ``slots``.
     ``ws``: 0 the batch-parallel kernel; 1 the weight-stationary cluster kernel when the model
     shape allows it; 2 the same with its two-half hand-off pipeline; 3 two 64-row clusters per
-    CU (gru_ws2_kernel); None: 1, or 2 under IGP_GRU_SPLIT=1."""
+    CU (gru_ws2_kernel); None: IGP_GRU_WS_MODE (3), or 2 under IGP_GRU_SPLIT=1."""
     if ws is None:
         ws = 2 if _GRU_SPLIT else _GRU_WS_MODE
     if ws not in (0, 1, 2, 3):
-        raise ValueError("gru: ws must be 0, 1, 2 or 3")
+        raise ValueError("gru: ws must be 0..3")
     dev = gp.device
     d = dict(n_layers=gp.n_layers, H=gp.H, T=int(T), I=gp.I, n_rows=int(n_rows),
              m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32, device=dev), tile_rows=int(tile_rows),
              waves=int(waves or gp.waves), pipeline=int(pipeline))
     w = gp.workspace(n_rows) if ws and _GRU_WS else None
     if w is not None:
-        d.update(ws=int(ws), ws_stagger=_GRU_STAGGER, ws_clusters=w["clusters"], ws_sync=w["sync"].data_ptr(), ws_x=w["x"].data_ptr(),
+        d.update(ws=int(ws), ws_clusters=w["clusters"], ws_sync=w["sync"].data_ptr(), ws_x=w["x"].data_ptr(),
                  ws_part=w["part"].data_ptr(), ws_err=gp.ws_err.data_ptr(),
-                 ws_trace=_opt(ws_trace, "ws_trace", dtype=torch.int64, min_numel=64 * 8 + 4, device=dev))
+                 ws_trace=_opt(ws_trace, "ws_trace", dtype=torch.int64, min_numel=64 * 8 + 4 + 1024, device=dev))
     if gp.split:
         d["split"] = 1
     if gp.reverse:
@@ -628,12 +632,13 @@ class MlpChainPack:
             b = s.b1_np if s.kind == "head" else s.b_np
             n, k = w.shape
             kp = -(-k // 64) * 64
-            # MFMA B-fragment order (pack_fragments): one 1 KB contiguous wave load per 16x32 tile
+            # MFMA B-fragment order (pack_fragments, k-step major): one 1 KB contiguous wave load
+            # per 16x32 tile, a k-step's tiles of all columns contiguous
             lo = None
             if self.split:
                 hi = torch.from_numpy(np.ascontiguousarray(w)).to(torch.bfloat16).float().numpy()
-                lo = pack_fragments(w - hi, kp).to(dev)
-            self.layers.append(dict(W=pack_fragments(w, kp).to(dev), Wlo=lo,
+                lo = pack_fragments(w - hi, kp, ks_major=True).to(dev)
+            self.layers.append(dict(W=pack_fragments(w, kp, ks_major=True).to(dev), Wlo=lo,
                                     b=None if b is None else torch.from_numpy(np.ascontiguousarray(b, np.float32)).to(dev),
                                     N=n, K=kp, act=ACT[s.act1 if s.kind == "head" else s.act]))
         head = steps[-1]
@@ -642,6 +647,44 @@ class MlpChainPack:
         self.in_live = steps[0].k
         self.in_w = self.layers[0]["K"]
         self.device = dev
+        # pair-cluster form (csrc/kernels/mlp_pair.hip, IGP_MLP_PAIR=1): two CUs per 128 rows,
+        # each streaming half of every layer's weights; bf16 chains whose layers are all 512
+        # wide. Off by default: its per-layer L2 hand-offs cost more than the weight bytes it
+        # saves (profiles/NOTES.md, round 3 late). One workspace per key (the LTV pipeline's
+        # slots run concurrently on their own streams).
+        self.pair_ok = (not self.split and all(l["N"] == 512 for l in self.layers)
+                        and os.environ.get("IGP_MLP_PAIR", "0") == "1")
+        self._pair: Dict[int, dict] = {}
+        self._pair_old = []  # superseded workspaces stay alive: captured graphs keep their pointers
+        self.pair_err = torch.zeros(1, dtype=torch.int32, device=dev) if self.pair_ok else None
+
+    def pair_workspace(self, n_rows: int, key: int = 0):
+        """Hand-off slabs / counters / head partials of the pair kernel for ``n_rows`` (grow-only)."""
+        if not self.pair_ok:
+            return None
+        ncl = -(-int(n_rows) // 128)
+        w = self._pair.get(key)
+        if w is None or w["clusters"] < ncl:
+            if w is not None:
+                self._pair_old.append(w)
+            dev = self.device
+            w = dict(clusters=ncl, x=torch.zeros(ncl * 4 * 128 * 256, dtype=torch.int16, device=dev),
+                     sync=torch.zeros(ncl * 16, dtype=torch.int32, device=dev),
+                     part=torch.zeros(ncl * 2 * 128, dtype=torch.float32, device=dev))
+            self._pair[key] = w
+        return w
+
+    def pair_failed(self) -> bool:
+        return bool(self.pair_err is not None and int(self.pair_err.item()) != 0)
+
+    def disable_pair(self) -> None:
+        """After a pair launch gave up (its workgroups were not co-resident): counters back to 0
+        and every later launch on the one-workgroup kernel (callers re-capture their graphs)."""
+        self.pair_ok = False
+        for w in list(self._pair.values()) + self._pair_old:
+            w["sync"].zero_()
+        if self.pair_err is not None:
+            self.pair_err.zero_()
 
     def waves(self) -> int:
         """Waves per workgroup: 8 needs every layer width to be a multiple of 128."""
@@ -652,10 +695,11 @@ class MlpChainPack:
 def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, slots: Optional[torch.Tensor] = None,
               pf_tab: Optional[torch.Tensor] = None, ext_tab: Optional[torch.Tensor] = None,
               ml: Optional[torch.Tensor] = None, ltv_out: Optional[torch.Tensor] = None,
-              m_ptr: Optional[torch.Tensor] = None) -> None:
+              m_ptr: Optional[torch.Tensor] = None, ws_key: int = 0) -> None:
     """Fused dense chain + N=1 head over ``n_rows`` rows. Input: dense ``X`` [rows, >= in] f32, or
     the LTV gather (``slots`` into ``pf_tab`` [C, 25] / ``ext_tab`` [C, ext_w]); outputs ``ml``
-    [rows] and/or the K9 rows ``ltv_out`` [rows, 6]."""
+    [rows] and/or the K9 rows ``ltv_out`` [rows, 6]. ``ws_key``: which pair-kernel workspace
+    (launches that may run concurrently need different keys)."""
     dev = pk.device
     d = dict(n_rows=int(n_rows), n_layers=len(pk.layers), in_w=pk.in_w, in_live=pk.in_live,
              rows_per_block=int(os.environ.get("IGP_MLP_ROWS", "64")), waves=pk.waves(),
@@ -687,4 +731,8 @@ def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, s
         d[f"l{i}_N"], d[f"l{i}_K"], d[f"l{i}_act"] = l["N"], l["K"], l["act"]
     if pk.split:
         d.update(split=1, rows_per_block=32)
+    w = pk.pair_workspace(n_rows, ws_key)
+    if w is not None:
+        d.update(pair_x=w["x"].data_ptr(), pair_sync=w["sync"].data_ptr(), pair_part=w["part"].data_ptr(),
+                 pair_err=pk.pair_err.data_ptr(), pair_clusters=w["clusters"])
     _mod().mlp_chain(d, _stream())

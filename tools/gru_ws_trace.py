@@ -40,6 +40,22 @@ def main() -> int:
                       "ws_failed": R.gp.ws_failed()}))
     for s in range(0, 8):
         print(s, np.round(np.diff(t[s, :5]), 2).tolist())
+    if ws == 3:  # which workgroups share a CU (HW_ID: cu_id bits 8..11, sh 12, se 13..15; XCC_ID)
+        hw = raw[64 * 8 + 4:64 * 8 + 4 + 1024]
+        nwg = ((-(-B // 64) + 7) // 8) * 64  # 64-row clusters, 8 members, groups of 8 clusters
+        where = {}
+        for b in range(min(nwg, 1024)):
+            v = int(hw[b])
+            key = (v >> 32, (v >> 13) & 7, (v >> 12) & 1, (v >> 8) & 15)
+            where.setdefault(key, []).append(b)
+        pairs = [tuple(bs) for bs in where.values() if len(bs) > 1]
+        deltas = {}
+        for bs in pairs:
+            d = bs[1] - bs[0]
+            deltas[d] = deltas.get(d, 0) + 1
+        print(json.dumps({"cus_used": len(where), "co_resident_pairs": len(pairs),
+                          "pair_blockidx_deltas": dict(sorted(deltas.items(), key=lambda kv: -kv[1])[:6]),
+                          "first_pairs": pairs[:6]}))
     return 0
 
 
