@@ -143,7 +143,8 @@ static_assert(offsetof(ScoreCfg, bl_mask) == 132 && offsetof(ScoreCfg, ip_max_pr
 // contiguous slab [BatchHdr | ReqRec x n]: one H2D copy per micro-batch.
 struct ReqRec {
   int32_t slot;       // feature-store slot on this GPU (-1 = unknown account)
-  int32_t tx_type;    // TxType in bits 0..7, owner rank in bits 8..15 (broadcast serving mode)
+  int32_t tx_type;    // TxType in bits 0..7, owner rank in bits 8..15 (broadcast serving mode),
+                      // bit 16 FV_ENC_BIT: the request wants response bytes (encoded features)
   int64_t amount;     // cents
   uint64_t dev_hash;  // XXH64 digests, 0 = absent
   uint64_t fp_hash;
@@ -151,6 +152,13 @@ struct ReqRec {
   int64_t ts;         // event time (unix s) used by feature_update
 };
 static_assert(sizeof(ReqRec) == 48, "ReqRec must be 48 bytes");
+
+// ReqRec.tx_type bit 16: the device writes the row's risk.v1 FeatureVector body, encoded, as the
+// row's 128-byte D2H feature image instead of the raw FeatRec (features.hip write_fenc). The
+// image's byte 127 tells them apart: 0x80 | length for an encoded body (<= 126 bytes), 0 for a
+// raw FeatRec (the top byte of its rule score).
+constexpr int32_t FV_ENC_BIT = 1 << 16;
+constexpr uint8_t FV_IMG_ENCODED = 0x80;
 
 // Per-batch header in device memory (written by one H2D copy per batch, read by every
 // kernel of the captured graph): the number of live rows and the scoring clock.

@@ -150,6 +150,7 @@ PYBIND11_MODULE(_hipk, m) {
     if (!a.hll_lc) throw std::runtime_error("feature_assemble: hll_lc table required");
     a.X = ptr<float*>(d, "X");
     a.feat = ptr<FeatRec*>(d, "feat");
+    a.fenc = ptr<uint8_t*>(d, "fenc");
     a.dbuf = ptr<int32_t*>(d, "dbuf");
     a.dcap = geti(d, "dcap");
     a.dmax = geti(d, "dmax");

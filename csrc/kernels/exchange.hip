@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void exchange_compact_kernel(XchgCompactArgs a
   int4* out = reinterpret_cast<int4*>(a.rows + dst);
   int4 q0 = src[0];
   const int4 q1 = src[1], q2 = src[2];
-  q0.y &= 0xff;  // owner bits of tx_type: this GPU owns every row it receives
+  q0.y &= 0xff | FV_ENC_BIT;  // owner bits of tx_type: this GPU owns every row it receives
   out[0] = q0;
   out[1] = q1;
   out[2] = q2;
@@ -111,7 +111,7 @@ struct XchgScatterArgs {
   const BatchHdr* hdr;
   const int32_t* route;
   const ResultRec* res;  // [cap]
-  const FeatRec* feat;   // [cap] (nullable: results only)
+  const FeatRec* feat;   // [cap] feature images (raw or encoded, features.hip write_fenc; nullable: results only)
   uint8_t* send;         // [N][C * W]: C ResultRec, then (features) C FeatRec per peer
   int32_t C, cap;
 };

@@ -148,12 +148,133 @@ __device__ __forceinline__ void apply_event_q(const UpdateArgs& a, const ScoreCf
   if (ql == 0) a.rt[s] = r;
 }
 
-// inert row (graph padding / another rank's request): zero inputs, FeatRec with slot -1
+// inert row (graph padding / another rank's request): zero inputs, FeatRec with slot -1 (also
+// as the row's D2H image)
 __device__ __forceinline__ void inert_row(const AssembleArgs& a, float* xr, int row, int ql, int ext_w, int flag) {
   for (int j = ql; j < 30 + ext_w; j += K1_QL) xr[j] = 0.f;
   int32_t* fr = reinterpret_cast<int32_t*>(a.feat + row);
   fr[ql] = ql == 3 ? flag : 0;
   fr[ql + 16] = ql + 16 == 27 ? -1 : 0;
+  if (a.fenc) {
+    int32_t* fe = reinterpret_cast<int32_t*>(a.fenc + (size_t)row * sizeof(FeatRec));
+    fe[ql] = ql == 3 ? flag : 0;
+    fe[ql + 16] = ql + 16 == 27 ? -1 : 0;
+  }
+}
+
+// ---- risk.v1 FeatureVector body, encoded on the device (the D2H image of a row whose request
+// wants response bytes: ReqRec.tx_type bit FV_ENC_BIT). The serving core then copies these bytes
+// into ScoreTransactionResponse.features instead of serialising ~26 fields per row on a host
+// thread. Same bytes as the host writer (wire.cpp FastOut, byte-exact with protobuf): proto3
+// zero suppression, int32 sign-extended to 64-bit varints, int64 varints, fixed32 floats,
+// bools as 1, one-byte tags for fields 1-15, two-byte tags for 16-26. Image: bytes [0, len),
+// byte 127 = 0x80 | len; a body longer than 126 bytes (large negative values) leaves the raw
+// FeatRec instead (its byte 127 is the top byte of the rule score, 0), which the host serialises.
+// FeatRec words: 0-2 tx counts, 3 flags, 4-5 tx_sum_1h, 6 tx_avg_1h, 7-11 i32 fields, 12-17 the
+// three i64 totals, 18-21 i32, 22-23 f32, 24 i32, 25 f32 (records.h).
+__device__ __forceinline__ void fv_put(uint64_t& lo, uint64_t& hi, int& n, uint32_t byte) {
+  if (n < 8) lo |= (uint64_t)byte << (8 * n);
+  else hi |= (uint64_t)byte << (8 * (n - 8));
+  ++n;
+}
+
+// bytes of FeatureVector field `field` (1-based) into lo / hi; returns the byte count (0: omitted)
+__device__ __forceinline__ int fv_field(const uint32_t* w, int field, uint64_t& lo, uint64_t& hi) {
+  int word = 0, kind = 0;  // kind 0 int32, 1 int64, 2 float, 3 bool (flag bit in `bit`)
+  uint32_t bit = 0;
+  switch (field) {
+    case 1: word = 0; break;
+    case 2: word = 1; break;
+    case 3: word = 2; break;
+    case 4: word = 4; kind = 1; break;
+    case 5: word = 6; kind = 2; break;
+    case 6: word = 7; break;
+    case 7: word = 8; break;
+    case 8: word = 9; break;
+    case 9: word = 10; break;
+    case 10: word = 11; break;
+    case 11: word = 12; kind = 1; break;
+    case 12: word = 14; kind = 1; break;
+    case 13: word = 16; kind = 1; break;
+    case 14: word = 18; break;
+    case 15: word = 19; break;
+    case 16: word = 20; break;
+    case 17: word = 21; break;
+    case 18: word = 22; kind = 2; break;
+    case 19: word = 23; kind = 2; break;
+    case 20: kind = 3; bit = FR_VPN; break;
+    case 21: kind = 3; bit = FR_PROXY; break;
+    case 22: kind = 3; bit = FR_TOR; break;
+    case 23: kind = 3; bit = FR_DISPOSABLE; break;
+    case 24: word = 24; break;
+    case 25: word = 25; kind = 2; break;
+    default: kind = 3; bit = FR_BONUS_ONLY; break;  // 26
+  }
+  uint64_t v;
+  if (kind == 0) v = (uint64_t)(int64_t)(int32_t)w[word];
+  else if (kind == 1) v = (uint64_t)w[word] | ((uint64_t)w[word + 1] << 32);
+  else if (kind == 2) v = w[word];
+  else v = (w[3] & bit) ? 1u : 0u;
+  lo = hi = 0;
+  int n = 0;
+  if (v == 0) return 0;
+  const uint32_t t = ((uint32_t)field << 3) | (kind == 2 ? 5u : 0u);
+  if (t < 128) {
+    fv_put(lo, hi, n, t);
+  } else {
+    fv_put(lo, hi, n, (t & 0x7f) | 0x80);
+    fv_put(lo, hi, n, t >> 7);
+  }
+  if (kind == 2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fv_put(lo, hi, n, (uint32_t)(v >> (8 * i)) & 0xffu);
+  } else {
+    do {
+      uint32_t byte = (uint32_t)v & 0x7fu;
+      v >>= 7;
+      if (v) byte |= 0x80u;
+      fv_put(lo, hi, n, byte);
+    } while (v);
+  }
+  return n;
+}
+
+// exclusive prefix sum over the 16 lanes of a quarter (lane ql gets the sum of lanes < ql)
+__device__ __forceinline__ int qscan_excl(int v, int ql) {
+  int s = v;
+#pragma unroll
+  for (int d = 1; d < 16; d <<= 1) {
+    const int u = __shfl_up(s, d, 16);
+    if (ql >= d) s += u;
+  }
+  return s - v;
+}
+
+// the row's D2H image (a.fenc): the encoded body when the request asked for it and it fits,
+// else the raw FeatRec staged in LDS (fw)
+__device__ __forceinline__ void write_fenc(const AssembleArgs& a, int row, int ql, bool enc, const uint32_t* fw,
+                                           uint8_t* se) {
+  uint2* const out = reinterpret_cast<uint2*>(a.fenc + (size_t)row * sizeof(FeatRec));
+  if (enc) {
+    uint64_t lo0, hi0, lo1 = 0, hi1 = 0;
+    const int n0 = fv_field(fw, ql + 1, lo0, hi0);
+    const int n1 = ql < 10 ? fv_field(fw, ql + 17, lo1, hi1) : 0;
+    const int off0 = qscan_excl(n0, ql);
+    const int tot0 = __shfl(off0 + n0, 15, 16);
+    const int off1 = tot0 + qscan_excl(n1, ql);
+    const int total = __shfl(off1 + n1, 15, 16);
+    if (total <= 126) {
+      for (int i = 0; i < n0; ++i) se[off0 + i] = (uint8_t)((i < 8 ? lo0 >> (8 * i) : hi0 >> (8 * (i - 8))) & 0xff);
+      for (int i = 0; i < n1; ++i) se[off1 + i] = (uint8_t)((i < 8 ? lo1 >> (8 * i) : hi1 >> (8 * (i - 8))) & 0xff);
+      if (ql == 0) se[127] = (uint8_t)(0x80 | total);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      out[ql] = reinterpret_cast<const uint2*>(se)[ql];
+      return;
+    }
+  }
+  out[ql] = reinterpret_cast<const uint2*>(fw)[ql];
 }
 
 // Loads are organised in two dependency levels (under a full grid each dependent global-load
@@ -187,6 +308,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
   // per-request staging of the X row (30 + up to 112 ext floats) and the FeatRec
   __shared__ __attribute__((aligned(16))) float s_xst[16][144];
   __shared__ __attribute__((aligned(16))) uint2 s_fst[16][16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_enc[16][128];  // encoded FeatureVector bodies
   const int lc0 = a.hll_lc[threadIdx.x];
   const int lc1 = threadIdx.x == 0 ? a.hll_lc[256] : 0;
   // ---- level 1
@@ -493,6 +615,9 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     for (int j = ql + 112; j < ext_w; j += K1_QL) xr[30 + j] = has ? a.ext[(size_t)s * ext_w + j] : 0.f;
     K1_MARK(3);
     reinterpret_cast<uint2*>(a.feat + row)[ql] = s_fst[threadIdx.x >> 4][ql];
+    if (a.fenc)
+      write_fenc(a, row, ql, (rq.tx_type & FV_ENC_BIT) != 0, reinterpret_cast<const uint32_t*>(s_fst[threadIdx.x >> 4]),
+                 s_enc[threadIdx.x >> 4]);
 
     // ---- score-then-update (engine.go:486-488)
     if (a.dbuf && has) {

@@ -65,6 +65,9 @@ struct AssembleArgs {
   const int32_t* hll_lc;    // [257]: floor(256 ln(256 / v) + 0.5), HLL linear counting by zero count v
   float* X;                 // [n_rows][x_stride]
   FeatRec* feat;            // [n_rows]
+  // [n_rows][128 B] D2H image of each row (nullable): the raw FeatRec, or for a request with
+  // ReqRec.tx_type bit FV_ENC_BIT the encoded risk.v1 FeatureVector body (features.hip write_fenc)
+  uint8_t* fenc;
   int32_t* dbuf;            // dedup regions (nullable: no score-then-update)
   int32_t dcap;
   int32_t dmax;

@@ -101,9 +101,7 @@ __device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, c
     }
     return;
   }
-  // PF k-steps of B fragments in flight: a k-step is only JT x MT MFMAs, so covering the L2
-  // latency of lines every CU of the XCD requests at once (~1 us, tools/mlp_bench.py) needs
-  // 8-10 steps ahead
+  // PF k-steps of B fragments in flight (5 by default: deeper rings spill, r3/q)
   constexpr int PF = PFD < NKS ? PFD : NKS - 1;
   constexpr int RING = PF + 1;
   mc_bf16x8 fb[RING][JT];
@@ -309,21 +307,22 @@ void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st) {
     // 64 rows x 8 waves (4 x 4 MFMA tiles per wave): per k-step a CU issues as many MFMA cycles
     // as it needs L1 cycles for the 32 KB of weight fragments (32 rows: half); a batch then
     // occupies half the CUs and the per-slot streams keep two batches in flight
-    if (pf == 5)
-      IGP_LAUNCH((mlp_chain_kernel<64, 8, false, 5>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
-    else
+    // prefetch 5 k-steps; 8 spills (28 VGPRs) and ran 78 -> 93 us alone (tools/mlp_bench.py, r3/q)
+    if (pf == 8)
       IGP_LAUNCH((mlp_chain_kernel<64, 8, false, 8>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
+    else
+      IGP_LAUNCH((mlp_chain_kernel<64, 8, false, 5>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
   } else if (a.waves == 8) {
     // 32 rows x 8 waves: a k-step is 8 MFMAs per wave (~0.11 us at two waves per SIMD) against
     // ~1 us of L2 latency for the weight fragments every CU of the XCD reads at the same time
-    // (tools/mlp_bench.py: the launch time hardly changes from 4096 to 8192 rows): the prefetch
-    // ring holds 10 k-steps (11 x 4 fragments, 176 VGPRs)
-    if (pf == 5)
-      IGP_LAUNCH((mlp_chain_kernel<32, 8, false, 5>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
+    // (tools/mlp_bench.py: the launch time hardly changes from 4096 to 8192 rows); deeper rings
+    // (8 / 10 k-steps) do not fit the registers without spills and measured no better (r3/q)
+    if (pf == 10)
+      IGP_LAUNCH((mlp_chain_kernel<32, 8, false, 10>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
     else if (pf == 8)
       IGP_LAUNCH((mlp_chain_kernel<32, 8, false, 8>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
     else
-      IGP_LAUNCH((mlp_chain_kernel<32, 8, false, 10>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
+      IGP_LAUNCH((mlp_chain_kernel<32, 8, false, 5>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
   }
   else if (r == 64)
     IGP_LAUNCH((mlp_chain_kernel<64, 4, false>), dim3((a.n_rows + 63) / 64), dim3(256), 0, st, a);

@@ -45,7 +45,7 @@ constexpr int MP_ROWS = 128;
 constexpr int MP_HALF = 256;                 // columns per member
 constexpr int MP_BLK = MP_ROWS * MP_HALF;    // bf16 per half image (64 KB)
 constexpr int MP_CH = MP_BLK / 8;            // 16-B chunks per half (4096)
-constexpr int MP_PF = 12;                    // weight k-steps in flight (2 fragments each)
+constexpr int MP_PF = 4;                     // weight k-steps in flight (2 fragments each; 8 / 12 spill)
 constexpr int MP_SC1 = 16;
 constexpr uint64_t MP_WAIT_TICKS = 20000000;  // 200 ms of wall_clock64: never hang the GPU
 
@@ -322,9 +322,7 @@ void launch_mlp_pair(const MlpChainArgs& a, hipStream_t st) {
   const int ncl = mlp_pair_clusters(a.n_rows);
   const char* pfe = getenv("IGP_MP_PF");  // A/B of the weight prefetch depth
   const int pf = pfe ? atoi(pfe) : MP_PF;
-  if (pf == 4)
-    IGP_LAUNCH(mlp_pair_kernel<4>, dim3(((ncl + 7) / 8) * 16), dim3(512), mlp_pair_lds_bytes(), st, a);
-  else if (pf == 8)
+  if (pf == 8)
     IGP_LAUNCH(mlp_pair_kernel<8>, dim3(((ncl + 7) / 8) * 16), dim3(512), mlp_pair_lds_bytes(), st, a);
   else
     IGP_LAUNCH(mlp_pair_kernel<MP_PF>, dim3(((ncl + 7) / 8) * 16), dim3(512), mlp_pair_lds_bytes(), st, a);

@@ -112,6 +112,9 @@ ServeCore::~ServeCore() {
 // ---------------------------------------------------------------------------- ingress
 void ServeCore::resolve_rows(std::vector<wire::TxRow>& rows, Item* it) {
   const size_t n = rows.size();
+  // rows of a request that is answered with response bytes: GPU devices return each row's
+  // FeatureVector already encoded (records.h FV_ENC_BIT; CPU devices ignore the bit)
+  const int32_t enc = it->wf ? FV_ENC_BIT : 0;
   it->n = n;
   it->rows.resize(n);
   thread_local std::vector<std::string_view> ids;
@@ -129,6 +132,7 @@ void ServeCore::resolve_rows(std::vector<wire::TxRow>& rows, Item* it) {
     for (size_t k = 0; k < n; ++k) {
       it->rows[k] = rows[k].rec;
       it->rows[k].slot = slots[k];
+      it->rows[k].tx_type |= enc;
     }
     it->ocur.assign(1, 0);
     it->ostart = {0, int32_t(n)};  // one owner (a world-1 exchange reads the owner ranges too)
@@ -158,6 +162,7 @@ void ServeCore::resolve_rows(std::vector<wire::TxRow>& rows, Item* it) {
     for (size_t pos = 0; pos < n; ++pos) {
       it->rows[pos] = rows[it->perm[pos]].rec;
       it->rows[pos].slot = slots[pos];
+      it->rows[pos].tx_type |= enc;
     }
   }
   if (links_ && n) {  // (device, account) co-occurrences, off the scoring path

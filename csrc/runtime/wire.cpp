@@ -345,10 +345,18 @@ inline char* write_tx_body(char* out, const ResultRec& r, const FeatRec* f, int6
   o.i64(T1(6, 0), 1, ms);
   if (f) {
     *o.p = char(T1(7, pb::LEN));
-    char* slot = o.p + 1;
-    o.p = slot + 1;
-    write_feature_vector(o, *f);
-    o.p = close_len(slot, o.p);
+    const uint8_t img = reinterpret_cast<const uint8_t*>(f)[sizeof(FeatRec) - 1];
+    if (img & FV_IMG_ENCODED) {  // the device encoded the body (features.hip write_fenc): <= 126 bytes
+      const size_t len = img & 0x7f;
+      o.p[1] = char(len);
+      std::memcpy(o.p + 2, f, 128);  // whole image (the buffer has the slack): one fixed-size copy
+      o.p += 2 + len;
+    } else {
+      char* slot = o.p + 1;
+      o.p = slot + 1;
+      write_feature_vector(o, *f);
+      o.p = close_len(slot, o.p);
+    }
   }
   return o.p;
 }

@@ -196,7 +196,8 @@ class DpGpuScorer(GpuScorer):
             ml = sb.model.run(sb.X, b, m_ptr=sb.n_ptr) if sb.model is not None else None
             K.ensemble(sb.hdr, self.cfg_dev, sb.feat, sb.X, ml, sb.res, b, self.metrics)
         hipk().exchange_scatter(sb.dev_slab.data_ptr(), sb.route.data_ptr(), sb.res.data_ptr(),
-                                sb.feat.data_ptr() if with_features else 0, sb.rsend.data_ptr(), C, b,
+                                (sb.fenc if sb.fenc is not None else sb.feat).data_ptr() if with_features else 0,
+                                sb.rsend.data_ptr(), C, b,
                                 torch.cuda.current_stream().cuda_stream)
 
     # ---- collectives captured into the graphs (RCCL stream capture, IGP_XCHG_CAPTURE=1)

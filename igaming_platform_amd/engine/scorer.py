@@ -70,6 +70,8 @@ def _destroy_cu_streams() -> None:
     _CU_STREAMS.clear()
 
 
+_FEAT_ENC = os.environ.get("IGP_FEAT_ENC", "1") != "0"
+
 class _Slot:
     """Device buffers of one pipeline slot (slab, model input/output, results)."""
 
@@ -215,6 +217,10 @@ class GpuScorer:
         sb.req = sb.dev_slab[HDR_BYTES:]
         sb.X = torch.zeros((B, self.width), dtype=torch.float32, device=dev)
         sb.feat = torch.zeros((B, 32), dtype=torch.int32, device=dev)
+        # the rows' 128-B D2H feature images: K1 writes the raw FeatRec, or the encoded risk.v1
+        # FeatureVector body for rows the serving core marked (FV_ENC_BIT: its response writer
+        # then copies bytes instead of serialising 26 fields per row). IGP_FEAT_ENC=0: raw only
+        sb.fenc = torch.zeros((B, 32), dtype=torch.int32, device=dev) if _FEAT_ENC else None
         sb.res = torch.zeros((B, 2), dtype=torch.int32, device=dev)
         sb.model = None
         if self.plan is not None:
@@ -269,7 +275,8 @@ class GpuScorer:
         batch seq+3 (part "update")."""
         sb, upd = self.slots[slot], self.update_features
         if part in ("all", "k1"):
-            K.feature_assemble(self.store, sb.hdr, self.cfg_dev, sb.req, sb.X, sb.feat, bucket, dedup=upd)
+            K.feature_assemble(self.store, sb.hdr, self.cfg_dev, sb.req, sb.X, sb.feat, bucket, dedup=upd,
+                               fenc=sb.fenc)
         if upd and part in ("all", "update"):
             K.update_segments(self.store, self.cfg_dev, sb.req, bucket, sb.hdr)
 
@@ -289,7 +296,8 @@ class GpuScorer:
         if host is None:
             K.memcpy_async(self.host_res[slot], sb.res, bucket * sb.res[0].numel() * sb.res.element_size())
         if with_features:
-            K.memcpy_async(self.host_feat[slot], sb.feat, bucket * sb.feat[0].numel() * sb.feat.element_size())
+            img = sb.fenc if sb.fenc is not None else sb.feat
+            K.memcpy_async(self.host_feat[slot], img, bucket * img[0].numel() * img.element_size())
 
     def capture(self) -> None:
         """Capture the copy, state, model and model+features graphs per (bucket, pipeline

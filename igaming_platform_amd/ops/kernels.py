@@ -117,10 +117,12 @@ def _opt(t: Optional[torch.Tensor], name: str, **kw):
 # --------------------------------------------------------------------------- K1
 def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch.Tensor,
                      X: torch.Tensor, feat: torch.Tensor, n_rows: int, dedup: bool = False,
-                     trace: Optional[torch.Tensor] = None) -> None:
+                     trace: Optional[torch.Tensor] = None, fenc: Optional[torch.Tensor] = None) -> None:
     """K1. ``dedup=True``: score-then-update. :func:`dedup_insert` must have registered the
     batch first; K1 then applies each single-event account's event and opens the segments
-    that :func:`update_segments` applies afterwards (dedup ring region by batch seq)."""
+    that :func:`update_segments` applies afterwards (dedup ring region by batch seq).
+    ``fenc`` [rows, 32] int32: each row's 128-byte D2H feature image - the raw FeatRec, or the
+    encoded risk.v1 FeatureVector body for rows whose ReqRec.tx_type carries FV_ENC_BIT."""
     dev = store.device
     if X.dim() != 2 or X.shape[1] < 30 + store.ext_width:
         raise ValueError("X must be [rows, >= 30 + ext_width]")
@@ -137,6 +139,7 @@ def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch
         hll_lc=_need(store.hll_lc, "hll_lc", torch.int32, 257),
         X=_need(X, "X", torch.float32, X.shape[1] * n_rows, dev),
         feat=_need(feat, "feat", torch.int32, 32 * n_rows, dev),
+        fenc=_need(fenc, "fenc", torch.int32, 32 * n_rows, dev) if fenc is not None else None,
         dbuf=_need(store.dbuf, "dbuf", torch.int32) if dedup else None, dcap=int(store.dcap), dmax=int(store.dmax),
         x_stride=int(X.shape[1]), ring_size=int(store.ring_ts.shape[1]), n_rows=int(n_rows),
         trace=_opt(trace, "trace", dtype=torch.int64, min_numel=64, device=dev),

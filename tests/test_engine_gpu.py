@@ -409,3 +409,38 @@ def test_tree_head_one_launch_matches_two_kernels(monkeypatch, bucket):
         assert torch.equal(sa.model.step_out[-1][:n], sb.model.step_out[-1][:n])
         assert int(sb.model.tile_cnt.abs().sum()) == 0  # every tile's counter back at zero
     assert torch.equal(A.scorer.metrics, B.scorer.metrics)
+
+
+def test_device_encoded_features_equal_host_serialised(monkeypatch):
+    """ScoreBatch bytes through the native serving core: with FV_ENC_BIT rows K1 writes each
+    row's risk.v1 FeatureVector body encoded (features.hip write_fenc) and the response writer
+    copies it; the responses must equal those of an engine whose device returns raw FeatRecs
+    that the host serialises (wire.cpp), field for field and byte for byte in `features`, over
+    a stream whose feature values cover zeros, large sums and negative net deposits."""
+    from igaming_platform_amd.engine import scorer as S
+    from igaming_platform_amd.proto import risk_v1 as P
+    engines = {}
+    for enc in (True, False):
+        monkeypatch.setattr(S, "_FEAT_ENC", enc)
+        engines[enc] = _engines()[0]
+    assert engines[True].core is not None and engines[False].core is not None
+    rng = np.random.default_rng(11)
+    encoded_rows = 0
+    for step in range(4):
+        txs = _txs(500, rng)
+        for t in txs[::7]:
+            t["amount"] = 3_000_000_000  # sums past 2^31, net deposits below zero for some accounts
+        data = P.ScoreBatchRequest(transactions=[P.ScoreTransactionRequest(**t) for t in txs]).SerializeToString()
+        out = {}
+        for enc, e in engines.items():
+            out[enc] = P.ScoreBatchResponse.FromString(e.score_batch_bytes(data, now=NOW + step * 40)).results
+        if step == 3:  # the last batch's D2H images: most rows came back encoded
+            sc = engines[True].backends[0].scorer
+            img = np.stack([h.numpy().view(np.uint8).reshape(-1, 128) for h in sc.host_feat])
+            encoded_rows = int(((img[:, :, 127] & 0x80) != 0).sum())
+        for a, b in zip(out[True], out[False]):
+            assert (a.score, a.action, list(a.reason_codes), a.rule_score, a.ml_score) == \
+                   (b.score, b.action, list(b.reason_codes), b.rule_score, b.ml_score)
+            assert a.features.SerializeToString() == b.features.SerializeToString()
+            assert a.features == b.features
+    assert encoded_rows > 0

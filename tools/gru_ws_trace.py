@@ -22,7 +22,7 @@ def main() -> int:
     R = S.runner
     slots = torch.from_numpy(np.random.default_rng(B).integers(0, 1 << 16, B).astype(np.int32)).to(dev)
     out = torch.zeros(B, device=dev)
-    tr = torch.zeros(64 * 8 + 4, dtype=torch.int64, device=dev)
+    tr = torch.zeros(64 * 8 + 4 + 1024, dtype=torch.int64, device=dev)  # phases | clocks | placement
     for _ in range(3):
         K.gru(R.gp, B, R.T, out=out, store=R.store, slots=slots, ws=ws, ws_trace=tr)
     torch.cuda.synchronize()
