@@ -6,19 +6,23 @@ default config = cfg 3, the data-parallel headline: GBDT+MLP stacked ensemble
 (ONNX TreeEnsembleRegressor(100 trees, depth 7, 128 features, 32 targets) -> Gemm(32x256)
 -> Relu -> Gemm(256x1) -> Sigmoid), micro-batch 8192 per GPU, DP over all GPUs with RCCL.
 
-One timed step per GPU = one full scoring micro-batch, nothing skipped:
-  host: pack 8192 requests (48 B ReqRec) into a pinned slab
-  GPU, three streams driven by the native driver (engine/scorer.py, csrc/kernels/driver.hip;
-  stage kernels issued directly from recorded op lists):
+Default scope (serving), per rank: 16 ingress threads each send risk.v1 ScoreBatch request bytes
+(8192 transactions, UUID account ids) into the rank's native serving core and get response bytes
+back: C++ parse, node-shared AccountIndex resolve, micro-batch step clock, the GPU pipeline below,
+response writer (FeatureVector bodies encoded on the device). One timed step = one round of
+requests, one per ingress thread (16 x 8192 transactions per rank), nothing skipped.
+Device micro-batch (per GPU, 8192 rows), three streams driven by the native driver
+(engine/scorer.py, csrc/kernels/driver.hip; stage kernels issued from recorded op lists):
       copy:  H2D slab -> dedup insert
       state: feature_assemble (ring windows, HLL, blacklist, ip-intel, rules, single-event
-             score-then-update) -> multi-event update segments
-      model: tree ensemble -> fused f32-MFMA dense+GEMV+sigmoid -> ensemble/action (+metrics)
+             score-then-update, FeatureVector encode) -> multi-event update segments
+      model: tree ensemble -> f32-MFMA head -> ensemble/action (+metrics), one launch
              -> results into pinned host memory
       batches i, i+1, i+2 overlap across the three stages
-  N > 1 (default --dp-mode exchange): the owner-routed RCCL exchange (two all-to-alls per step)
-  moves every row to the rank owning its account and the results back (dp_bench below)
-Per-GPU work is fixed as N grows (weak scaling): global batch = 8192 x N per step.
+  N > 1: every rank ingests; the owner-routed RCCL exchange (two all-to-alls per device step)
+  moves every row to the rank owning its account and the results back (engine/dp.py)
+Per-GPU work is fixed as N grows (weak scaling). --scope engine_only: pre-resolved rows into the
+device pipeline, one step = one 8192-row micro-batch (the device-pipeline number).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|heuristic]
 For N > 1 run under torchrun (the driver does), or this script launches torchrun itself.
@@ -540,12 +544,15 @@ def serving_bench(a) -> None:
         if comm is not None:
             comm.barrier()
 
-    run(max(a.warmup, a.threads), NOW0 - 3600, False)   # history + warm graphs / caches
+    # a serving step = one round of ScoreBatch requests, one per ingress thread (16 concurrent
+    # 8192-transaction requests per rank): timing single requests (the driver's --steps 20)
+    # would measure the threads' ramp up and down around ~2 requests per thread
+    run(max(a.warmup, 1) * a.threads, NOW0 - 3600, False)   # history + warm graphs / caches
     barrier()
     sync()
     core.stats(True)
     t0 = time.perf_counter()
-    run(a.steps, NOW0, True)
+    run(a.steps * a.threads, NOW0, True)
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -563,11 +570,13 @@ def serving_bench(a) -> None:
         elapsed, p99, p50 = (float(x) for x in mx)
     out = {
         "metric": "fraud scores/sec (whole node) + p99 score latency",
-        "value": world * a.steps * B / elapsed, "unit": "scores/s", "n_gpus": world, "steps": a.steps,
+        "value": world * a.steps * a.threads * B / elapsed, "unit": "scores/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": a.numerics, "data": "synthetic (UUID account ids, random-init weights)",
-        "config": {"model": c["desc"], "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
-                   "per_gpu_batch": B, "transactions_per_request": B, "accounts_per_gpu": n_acc,
+        "config": {"model": c["desc"], "global_batch": B * a.threads * world, "seq_len": 1, "parallelism": f"dp{world}",
+                   "per_gpu_batch": B, "transactions_per_request": B, "requests_per_step_per_rank": a.threads,
+                   "step": "one 8192-transaction ScoreBatch request per ingress thread (concurrent); device "
+                           "micro-batches of per_gpu_batch rows", "accounts_per_gpu": n_acc,
                    "ingress_threads_per_rank": a.threads, "pipeline_depth": a.depth, "serving": mode,
                    "numerics": numerics_desc(a),
                    "comm_env": {k: v for k, v in sorted(os.environ.items())

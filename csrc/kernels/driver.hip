@@ -16,6 +16,7 @@
 // (pool selection, bookkeeping, the wait for an older batch) overlaps the ~40 us of HIP calls
 // instead of adding to them. wait(slot) / query(slot) / model_event(slot) first wait for the
 // slot's queued batch to be issued; issue errors resurface on the next call.
+#include "hostwait.h"
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 
@@ -69,14 +70,7 @@ void bind_device(int d) {
 // event wait with a deadline (hipEventSynchronize has none): query with a short back-off
 bool poll_event(hipEvent_t e, int64_t timeout_us) {
   const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
-  for (int spin = 0;; ++spin) {
-    const hipError_t q = hipEventQuery(e);
-    if (q == hipSuccess) return true;
-    if (q != hipErrorNotReady) hip_ok(q, "event query");
-    if (std::chrono::steady_clock::now() >= t_end) return false;
-    // spin first (a batch completes within a few hundred us), then back off
-    if (spin > 4096) std::this_thread::sleep_for(std::chrono::microseconds(10));
-  }
+  return poll_event_until(e, t_end, [](hipError_t q) { hip_ok(q, "event query"); });
 }
 
 class PipeDriver {

@@ -19,6 +19,7 @@
 // RCCL is the copy torch already loaded (torch/lib/librccl.so.1), resolved with dlopen, so the
 // process holds one RCCL whether or not torch.distributed uses it; our communicators are our
 // own (ncclCommInitRank over a unique id that Python broadcasts once).
+#include "hostwait.h"
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 
@@ -383,19 +384,16 @@ class XchgDriver {
         return -1;
       }
       const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
-      for (int spin = 0;; ++spin) {
-        const hipError_t q = hipEventQuery(e);
-        if (q == hipSuccess) return owners();
-        if (q != hipErrorNotReady) {
-          if (err && errlen > 0) {
-            std::strncpy(err, hipGetErrorString(q), size_t(errlen) - 1);
-            err[errlen - 1] = 0;
-          }
-          return -1;
+      bool failed = false;
+      const bool done = poll_event_until(e, t_end, [&](hipError_t q) {
+        failed = true;
+        if (err && errlen > 0) {
+          std::strncpy(err, hipGetErrorString(q), size_t(errlen) - 1);
+          err[errlen - 1] = 0;
         }
-        if (std::chrono::steady_clock::now() >= t_end) return 1;
-        if (spin > 4096) std::this_thread::sleep_for(std::chrono::microseconds(10));
-      }
+      });
+      if (done) return owners();
+      return failed ? -1 : 1;
     };
     ops_.results = [](void* ctx, int32_t slot) -> const void* {
       auto* d = static_cast<XchgDriver*>(ctx);
@@ -434,7 +432,8 @@ class XchgDriver {
     __atomic_store_n(&rflags_[(size_t(slot) * world_ + rank_) * 8], g, __ATOMIC_RELEASE);
     const auto t_end = timeout_us >= 0 ? std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us)
                                        : std::chrono::steady_clock::time_point::max();
-    for (int spin = 0;; ++spin) {
+    const auto t_spin = std::chrono::steady_clock::now() + std::chrono::microseconds(wait_spin_us());
+    for (;;) {
       bool all = true;
       for (int o = 0; o < world_ && all; ++o)
         all = __atomic_load_n(&rflags_[(size_t(slot) * world_ + o) * 8], __ATOMIC_ACQUIRE) >= g;
@@ -443,7 +442,7 @@ class XchgDriver {
         if (timeout_us < 0 && err && errlen > 0) std::strncpy(err, "results region: owner never published", size_t(errlen) - 1);
         return 1;
       }
-      if (spin > 4096) std::this_thread::sleep_for(std::chrono::microseconds(5));
+      wait_backoff(t_spin);
     }
   }
 
