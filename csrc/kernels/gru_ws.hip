@@ -577,9 +577,8 @@ __global__ void __launch_bounds__(256, 1) gru_ws_kernel(GruArgs a) {
 // cluster's hand-off (sc1 stores draining, counter poll, gather) and gate epilogue issue while
 // the other cluster's wave keeps the MFMA pipe busy - the hardware interleaves what the
 // single-wave kernel had to serialise (NOTES: 9.4 us/step = 5.5 compute + 3.9 hand-off).
-// Layer balance: a layer-2 wave issues 192 MFMAs per step, a layer-1 wave 108; the second
-// wave of blocks (b >> 8 odd: under breadth-first dispatch the partner on the same CU) swaps
-// the layer <-> wave assignment so a SIMD tends to host one wave of each layer.
+// Layer balance: a layer-2 wave issues 192 MFMAs per step, a layer-1 wave 108; roles follow the
+// wave's SIMD so that every SIMD hosts one wave of each layer (see the kernel's prologue).
 constexpr int W2_M = 64;
 constexpr int W2_RT = W2_M / 16;
 constexpr int W2_SLICE = 2 * W2_M * WS_UW;  // bf16 per member slice (both layers)
@@ -670,8 +669,21 @@ __global__ void __launch_bounds__(256, 2) gru_ws2_kernel(GruArgs a) {
   if (row0 >= n_live || cl >= 2 * a.ws_clusters) return;  // uniform over the cluster's 8 members
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int layer = (wave >> 1) ^ ((b >> 8) & 1);
-  const int tile = wave & 1;
+  // Roles by SIMD: a layer-2 wave issues 192 MFMAs per step, a layer-1 wave 108, and the two
+  // co-resident workgroups of a CU are blocks b and b + 256 (breadth-first dispatch, recorded by
+  // tools/gru_ws_trace.py). A workgroup's four waves sit on four different SIMDs, in an order
+  // whose start varies, so the roles follow the SIMD the wave got (HW_ID bits 5:4): SIMDs 0-1
+  // run layer 1 and SIMDs 2-3 layer 2 in the first half of the grid, the other way round in the
+  // second, and every SIMD hosts one wave of each layer (300 MFMAs per step, not up to 384).
+  // When the four SIMD ids are not distinct, roles fall back to the wave index.
+  int* const ssid = sflag + 4;
+  const int sid = (int)((__builtin_amdgcn_s_getreg(0xF804) >> 4) & 3u);  // HW_ID.SIMD_ID
+  if (lane == 0) ssid[wave] = sid;
+  __syncthreads();
+  const bool by_simd = ((1 << ssid[0]) | (1 << ssid[1]) | (1 << ssid[2]) | (1 << ssid[3])) == 15;
+  const int role = __builtin_amdgcn_readfirstlane(by_simd ? sid : wave);
+  const int layer = (role >> 1) ^ ((b >> 8) & 1);
+  const int tile = role & 1;
   const int ht = mem * 2 + tile;
   const int crow = (lane >> 4) * 4, ccol = lane & 15;
   const int j = ht * 16 + ccol;
@@ -736,7 +748,7 @@ __global__ void __launch_bounds__(256, 2) gru_ws2_kernel(GruArgs a) {
     const int row = c / chunks, q = c - row * chunks;
     return reinterpret_cast<uint4*>(Xb + buf * (W2_M * WS_XS) + row * WS_XS + q * 8);
   };
-  const int ltid = tid & 127;  // thread index among the two layer-0 waves
+  const int ltid = tile * 64 + lane;  // thread index among the two layer-0 waves
   __syncthreads();
   if (layer == 0)
     for (int c = ltid; c < nchunk; c += 128) *x_slot(0, c) = load_x(c, 0);
@@ -936,8 +948,8 @@ __global__ void __launch_bounds__(256, 2) gru_ws2_kernel(GruArgs a) {
 size_t gru_ws_lds_bytes() {
   return (size_t)2 * WS_M * WS_HS * 2 + (size_t)2 * WS_M * WS_XS * 2 + (size_t)2 * WS_M * 4 + (size_t)4 * WS_M * 8 + 16;
 }
-static size_t gru_ws2_lds_bytes() {
-  return (size_t)2 * WS_CL * W2_BLK * 2 + (size_t)2 * W2_M * WS_XS * 2 + (size_t)2 * W2_M * 4 + (size_t)4 * W2_M * 8 + 16;
+static size_t gru_ws2_lds_bytes() {  // ... | flag word, 3 spare | 4 SIMD ids
+  return (size_t)2 * WS_CL * W2_BLK * 2 + (size_t)2 * W2_M * WS_XS * 2 + (size_t)2 * W2_M * 4 + (size_t)4 * W2_M * 8 + 32;
 }
 
 int gru_ws_clusters(int n_rows) { return (n_rows + WS_M - 1) / WS_M; }
