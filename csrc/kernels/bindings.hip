@@ -516,7 +516,8 @@ PYBIND11_MODULE(_hipk, m) {
     if (a.split) {
       for (int l = 0; l < a.n_layers; ++l)
         if (!a.W_lo[l]) throw std::runtime_error("mlp_chain: split mode needs every layer's residual weights");
-      if (a.rows_per_block != 32) throw std::runtime_error("mlp_chain: split mode runs 32 rows per block");
+      if (a.rows_per_block != 32 && !(a.rows_per_block == 64 && a.waves == 8))
+        throw std::runtime_error("mlp_chain: split mode runs 32 rows per block (64 with 8 waves)");
     }
     if (!a.w2) throw std::runtime_error("mlp_chain: head weights required");
     if (!a.slots && !a.X) throw std::runtime_error("mlp_chain: input");

@@ -142,14 +142,17 @@ __device__ __forceinline__ void mc_split(float x, uint16_t& hi, uint16_t& lo) {
   lo = f32_to_bf16(x - __uint_as_float((uint32_t)hi << 16));
 }
 
-template <int MC_ROWS, int WAVES, bool SPLIT, int PFD = MC_PF>
+// NBUF = 2: the activation tile is ping-ponged between layers; NBUF = 1 (64-row split tiles,
+// whose hi + lo tiles fill 128 KB of LDS once): a layer's outputs wait in the accumulators until
+// every wave has read its input, then overwrite the tile in place (one more barrier per layer).
+template <int MC_ROWS, int WAVES, bool SPLIT, int PFD = MC_PF, int NBUF = 2>
 __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
   constexpr int MT = MC_ROWS / 16;            // 16-row MFMA tiles per wave
   constexpr int THREADS = 64 * WAVES;
   constexpr int PARTS = THREADS / MC_ROWS;    // staging threads per row
   constexpr int JT = 32 / WAVES;              // 16-column tiles per wave at N = 512
-  // [0..1]: hi tiles (ping-pong); SPLIT: [2..3] the matching lo tiles
-  __shared__ __attribute__((aligned(16))) uint16_t H[SPLIT ? 4 : 2][MC_ROWS * MC_LDA];
+  // [0, NBUF): hi tiles (ping-pong when NBUF = 2); SPLIT: [NBUF, 2 NBUF) the matching lo tiles
+  __shared__ __attribute__((aligned(16))) uint16_t H[(SPLIT ? 2 : 1) * NBUF][MC_ROWS * MC_LDA];
   __shared__ float part[WAVES][MC_ROWS];
   __shared__ float mlv[MC_ROWS];
   __shared__ float pfl[MC_ROWS][P_NCOLS];  // raw profile rows for the K9 epilogue
@@ -193,7 +196,7 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
           x = copysignf(log1pf(fabsf(x)), x);  // [sign*log1p|profile| (25) | extended features]
         }
         if constexpr (SPLIT) {
-          mc_split(x, H[0][mc_idx(r, c)], H[2][mc_idx(r, c)]);
+          mc_split(x, H[0][mc_idx(r, c)], H[NBUF][mc_idx(r, c)]);
         } else {
           H[0][mc_idx(r, c)] = f32_to_bf16(x);
         }
@@ -212,7 +215,7 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
 #pragma unroll
       for (int j = 0; j < JT; ++j) acc[m][j] = mc_f32x4{0.f, 0.f, 0.f, 0.f};
     const uint16_t* Hin = H[cur];
-    const uint16_t* Hlo = H[SPLIT ? 2 + cur : cur];
+    const uint16_t* Hlo = H[SPLIT ? NBUF + cur : cur];
     const uint16_t* Wl = SPLIT ? a.W_lo[l] : nullptr;
     switch (K >> 5) {  // K-steps of 32 (the host allows 2..16)
       case 2: mc_layer_mma<2, MT, JT, SPLIT, PFD>(Hin, Hlo, a.W[l], Wl, N, colw, NT, lane, acc); break;
@@ -228,8 +231,10 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
     const int act = a.act[l];
     if (l + 1 < a.n_layers) {
       // hidden layer: bias + act -> bf16 -> the next layer's LDS tile
-      uint16_t* Hout = H[cur ^ 1];
-      uint16_t* Hout_lo = H[SPLIT ? 2 + (cur ^ 1) : (cur ^ 1)];
+      const int nxt = NBUF == 2 ? cur ^ 1 : 0;
+      uint16_t* Hout = H[nxt];
+      uint16_t* Hout_lo = H[SPLIT ? NBUF + nxt : nxt];
+      if constexpr (NBUF == 1) __syncthreads();  // every wave has read this layer's input tile
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -246,7 +251,7 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
           }
         }
       __syncthreads();
-      cur ^= 1;
+      cur = nxt;
       continue;
     }
     // last hidden layer: y[r] = act2(sum_n act(h[r][n] + b[n]) * w2[n] + b2)
@@ -294,8 +299,10 @@ void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
   if (mlp_pair_eligible(a)) return launch_mlp_pair(a, st);
   const int r = a.rows_per_block;
-  if (a.split) {  // f32-faithful: 32 rows per block (hi + lo tiles fill the LDS)
-    if (a.waves == 8)
+  if (a.split) {  // f32-faithful: hi + lo tiles fill the LDS (64 rows: each tile once, NBUF = 1)
+    if (a.waves == 8 && r == 64)
+      IGP_LAUNCH((mlp_chain_kernel<64, 8, true, MC_PF, 1>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
+    else if (a.waves == 8)
       IGP_LAUNCH((mlp_chain_kernel<32, 8, true>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
     else
       IGP_LAUNCH((mlp_chain_kernel<32, 4, true>), dim3((a.n_rows + 31) / 32), dim3(256), 0, st, a);

@@ -733,7 +733,10 @@ def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, s
         d[f"l{i}_b"] = _opt(l["b"], "b", dtype=torch.float32, min_numel=l["N"], device=dev)
         d[f"l{i}_N"], d[f"l{i}_K"], d[f"l{i}_act"] = l["N"], l["K"], l["act"]
     if pk.split:
-        d.update(split=1, rows_per_block=32)
+        # 64 rows x 8 waves (hi + lo tiles in LDS once): 123-128 vs 91 M predictions/s for 32
+        # rows, same box (profiles/r3/x); 4-wave chains keep 32
+        rows = int(os.environ.get("IGP_MLP_SPLIT_ROWS", "64" if d["waves"] == 8 else "32"))
+        d.update(split=1, rows_per_block=rows if d["waves"] == 8 else 32)
     w = pk.pair_workspace(n_rows, ws_key)
     if w is not None:
         d.update(pair_x=w["x"].data_ptr(), pair_sync=w["sync"].data_ptr(), pair_part=w["part"].data_ptr(),

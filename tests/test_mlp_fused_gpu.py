@@ -192,6 +192,35 @@ def test_mlp_chain_split_mode_matches_fp32_reference():
     assert errs[True] < errs[False] / 20, errs   # the split mode is far closer to fp32 than bf16
 
 
+def test_mlp_chain_split_64_row_tiles_match_32(monkeypatch):
+    """The f32-faithful split chain at 64 rows per workgroup (hi + lo tiles in LDS once, each
+    overwritten in place after every wave read it) equals the 32-row split chain bit for bit."""
+    import torch
+    from igaming_platform_amd.models.plan import DenseStep, HeadStep
+    from igaming_platform_amd.ops import kernels as K
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(8)
+    steps = [DenseStep(n=512, k=k, act="relu", w_np=rng.normal(0, 1 / np.sqrt(k), (512, k)).astype(np.float32),
+                       b_np=rng.normal(0, 0.05, 512).astype(np.float32)) for k in (256, 512, 512)]
+    steps.append(HeadStep(n1=512, k=512, act1="relu", act2="none",
+                          w1_np=rng.normal(0, 1 / np.sqrt(512), (512, 512)).astype(np.float32),
+                          b1_np=rng.normal(0, 0.05, 512).astype(np.float32),
+                          w2_np=rng.normal(0, 1 / np.sqrt(512), 512).astype(np.float32), b2=0.1))
+    pk = K.MlpChainPack(steps, dev, split=True)
+    n = 1500
+    X = torch.from_numpy(rng.normal(0, 1, (n, 256)).astype(np.float32)).to(dev)
+    m_ptr = torch.tensor([n - 29], dtype=torch.int32, device=dev)
+    outs = {}
+    for rows in ("32", "64"):
+        monkeypatch.setenv("IGP_MLP_SPLIT_ROWS", rows)
+        ml = torch.full((n,), -7.0, device=dev)
+        K.mlp_chain(pk, n, X=X, ml=ml, m_ptr=m_ptr)
+        torch.cuda.synchronize()
+        outs[rows] = ml.cpu()
+    assert torch.equal(outs["32"], outs["64"])
+    assert torch.all(outs["64"][n - 29:] == -7.0) and not torch.any(outs["64"][:n - 29] == -7.0)
+
+
 def test_ltv_fp32_plan_runs_the_split_chain_and_matches_the_executor():
     """An fp32 LTV plan takes the fused chain in split mode; over 12288 players (table gather in
     the kernel) its model output matches the C++ fp32 executor of the ONNX model (the reference

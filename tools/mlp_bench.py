@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """cfg 4 LTV chain kernel alone (256 -> 4 x 512 -> 1, bf16), one launch at a time on one stream:
 microseconds per launch and TFLOP/s for the one-workgroup kernel (32 / 64 rows per workgroup)
-and the pair-cluster kernel (csrc/kernels/mlp_pair.hip), at several batch sizes. Checks that the
+and the pair-cluster kernel (csrc/kernels/mlp_pair.hip); SPLIT=1: the f32-faithful chain at 32 / 64 rows, at several batch sizes. Checks that the
 variants agree. Usage: python tools/mlp_bench.py [batches, default 8192,4096,16384]"""
 import json
 import os
@@ -25,15 +25,18 @@ def main() -> int:
                           b1_np=rng.normal(0, 0.1, 512).astype(np.float32),
                           w2_np=rng.normal(0, 0.1, 512).astype(np.float32), b2=0.1))
     os.environ["IGP_MLP_PAIR"] = "1"  # allocate the pair workspace; each variant sets pair_ok itself
-    pk = K.MlpChainPack(steps, dev)
+    split = os.environ.get("SPLIT", "0") == "1"  # the f32-faithful chain (hi/lo bf16 pairs)
+    pk = K.MlpChainPack(steps, dev, split=split)
     flop_row = 2 * (256 * 512 + 3 * 512 * 512 + 512)
     batches = [int(b) for b in (sys.argv[1] if len(sys.argv) > 1 else "8192,4096,16384").split(",")]
     res = []
     for B in batches:
         X = torch.from_numpy(rng.normal(0, 1, (B, 256)).astype(np.float32)).to(dev)
         ref = None
-        for name, rows, pair in (("wg32", "32", False), ("wg64", "64", False), ("pair", "64", True)):
-            os.environ["IGP_MLP_ROWS"] = rows
+        variants = ((("split32", "32", False), ("split64", "64", False)) if split else
+                    (("wg32", "32", False), ("wg64", "64", False), ("pair", "64", True)))
+        for name, rows, pair in variants:
+            os.environ["IGP_MLP_SPLIT_ROWS" if split else "IGP_MLP_ROWS"] = rows
             pk.pair_ok = pair
             ml = torch.zeros(B, device=dev)
             run = lambda: K.mlp_chain(pk, B, X=X, ml=ml)  # noqa: E731
