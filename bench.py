@@ -697,9 +697,11 @@ def model_bench(a, world: int, rank: int, dev) -> None:
     def step(i: int):
         p = R.submit(S.pool[i % len(S.pool)])
         if world > 1 and not a.no_gather:
-            with torch.cuda.stream(R.stream):
-                dist.all_gather_into_tensor(gathered, R.out[:B].reshape(-1))
-                p[2].record(R.stream)
+            st = R.slot_stream(p[0]) if hasattr(R, "slot_stream") else R.stream
+            ob = R.slot_out(p[0]) if hasattr(R, "slot_out") else R.out
+            with torch.cuda.stream(st):
+                dist.all_gather_into_tensor(gathered, ob[:B].reshape(-1))
+                p[2].record(st)
         return p
 
     inflight, lat = [], []

@@ -502,11 +502,11 @@ __global__ void __launch_bounds__(NW * 64) gru_x3_kernel(GruArgs a) {
   const WFrag r1 = wfrag(a.layer[1].R, wh, lane), r1l = wfrag(a.layer[1].R_lo, wh, lane);
 
   // LDS: hb[2 halves][layer][pingpong][M][HS] | xb[2 halves][pingpong][M][XS] | rb[2 halves][M][HS]
-  //      | bias[2][6H] | red[NW][M]
+  //      (LBR = 0 only) | bias[2][6H] | red[NW][M]
   uint16_t* const hb = reinterpret_cast<uint16_t*>(smem);
   uint16_t* const xb = hb + 8 * M * HS;
   uint16_t* const rb = xb + 4 * M * XS;
-  float* const bias = reinterpret_cast<float*>(rb + 2 * M * HS);
+  float* const bias = reinterpret_cast<float*>(rb + (LBR ? 0 : 2 * M * HS));
   float* const red = bias + 12 * H;
 #define HB(half, l, b) (hb + ((half) * 4 + (l) * 2 + (b)) * (M * HS))
 #define XB(half, b) (xb + ((half) * 2 + (b)) * (M * XS))
@@ -600,18 +600,29 @@ __global__ void __launch_bounds__(NW * 64) gru_x3_kernel(GruArgs a) {
 #undef XB
 }
 
-static size_t gru_x3_lds_bytes(int RT, int KSX, int KSH, int NW) {
+static size_t gru_x3_lds_bytes(int RT, int KSX, int KSH, int NW, int lbr) {
   const int M = RT * 16, H = KSH * 32, HS = H + GRU_PAD, XS = KSX * 32 + GRU_PAD;
-  return (size_t)8 * M * HS * 2 + (size_t)4 * M * XS * 2 + (size_t)2 * M * HS * 2 + (size_t)2 * 6 * H * 4 +
-         (size_t)NW * M * 4;
+  return (size_t)8 * M * HS * 2 + (size_t)4 * M * XS * 2 + (lbr ? 0 : (size_t)2 * M * HS * 2) +
+         (size_t)2 * 6 * H * 4 + (size_t)NW * M * 4;
 }
 
+// rows per workgroup (GruArgs.tile_rows: 0 / 16 -> 16): 32 rows (RT = 2, linear_before_reset, tiles
+// within the LDS: 155 KB at H = 256) feed every streamed hi / lo weight fragment to two row
+// tiles; a 4096-row batch then fills 128 CUs, which pays only when another slot's batch runs
+// beside it (the cfg5 bench's per-slot streams, engine/abuse.py overlap).
 template <int KSX, int KSH>
 static void launch_gru_x3(const GruArgs& a, hipStream_t st) {
   constexpr int NW = KSH >= 4 ? 8 : 4;
-  const dim3 grid((a.n_rows + 15) / 16), block(NW * 64);
-  const size_t lds = gru_x3_lds_bytes(1, KSX, KSH, NW);
-  if (a.layer[0].lbr)
+  const dim3 block(NW * 64);
+  const int lbr = a.layer[0].lbr ? 1 : 0;
+  if (lbr && a.tile_rows == 32 && gru_x3_lds_bytes(2, KSX, KSH, NW, 1) <= 160 * 1024) {
+    IGP_LAUNCH((gru_x3_kernel<2, KSX, KSH, 1, NW>), dim3((a.n_rows + 31) / 32), block,
+               gru_x3_lds_bytes(2, KSX, KSH, NW, 1), st, a);
+    return;
+  }
+  const dim3 grid((a.n_rows + 15) / 16);
+  const size_t lds = gru_x3_lds_bytes(1, KSX, KSH, NW, lbr);
+  if (lbr)
     IGP_LAUNCH((gru_x3_kernel<1, KSX, KSH, 1, NW>), grid, block, lds, st, a);
   else
     IGP_LAUNCH((gru_x3_kernel<1, KSX, KSH, 0, NW>), grid, block, lds, st, a);

@@ -477,6 +477,7 @@ class GruPack:
         self.lbr = int(layers[0].linear_before_reset)
         dev = as_device(device)
         self.split = bool(split)
+        self.x3_rows = 16  # rows per workgroup of the split kernel (32: see AbuseGpu overlap)
         self.layers = []
 
         def residual(w):
@@ -566,6 +567,8 @@ def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh
                  ws_trace=_opt(ws_trace, "ws_trace", dtype=torch.int64, min_numel=64 * 8 + 4 + 1024, device=dev))
     if gp.split:
         d["split"] = 1
+        if not tile_rows:
+            d["tile_rows"] = int(gp.x3_rows)
     if gp.reverse:
         d["reverse"] = 1
     for i, l in enumerate(gp.layers):

@@ -124,7 +124,7 @@ class ModelSetup:
 
 
 def build_model(config: str, batch: int, accounts: int, dev, rank: int = 0, depth: int = 2,
-                use_graphs: bool = True, n_pool: int = 8, precision: str = "bf16") -> ModelSetup:
+                use_graphs: bool = True, n_pool: int = 8, precision: str = "bf16", overlap: bool = True) -> ModelSetup:
     import torch
 
     from ..config import FeatureConfig
@@ -169,7 +169,7 @@ def build_model(config: str, batch: int, accounts: int, dev, rank: int = 0, dept
         rt[:, cnt_col] = fc.event_ring
         m = N.OnnxModel.from_bytes(builders.build("gru", seq=100, in_dim=16, hidden=256).SerializeToString())
         runner = AbuseGpu(store, to_device(compile_onnx(m), dev, precision), buckets=[B], use_graphs=use_graphs,
-                          depth=depth)
+                          depth=depth, overlap=overlap)
     torch.cuda.synchronize(dev)
     runner.capture()
     pool = [rng.integers(0, accounts, B).astype(np.int32) for _ in range(n_pool)]

@@ -299,3 +299,47 @@ def test_gru_split_mode_fp32_faithful_over_100_steps(lbr):
     assert e_split < e_bf16 / 10, (e_split, e_bf16)
     thr = float(np.median(ref))
     assert np.array_equal(outs["split"] > thr, ref > thr)
+
+
+def test_gru_split_32_row_tiles_match_16():
+    """The f32-faithful split GRU at 32 rows per workgroup (two row tiles share every streamed
+    hi / lo weight fragment; linear_before_reset, H = 256; the cfg5 bench runs it with one
+    stream per pipeline slot) equals the 16-row kernel bit for bit, with a batch that ends
+    inside a workgroup."""
+    import torch
+    from igaming_platform_amd.engine.runner import DeviceModel
+    from igaming_platform_amd.models.plan import compile_onnx, to_device
+    from igaming_platform_amd.native import native
+    from igaming_platform_amd.onnx import builders
+    m = native().OnnxModel.from_bytes(builders.build("gru", seq=40, in_dim=16, hidden=256, layers=2,
+                                                     linear_before_reset=1, head=True).SerializeToString())
+    plan = to_device(compile_onnx(m), "cuda", "fp32")
+    rows = 1000
+    Xd = torch.from_numpy(np.random.default_rng(9).standard_normal((40, rows, 16)).astype(np.float32)).cuda()
+    outs = {}
+    for tile in (16, 32):
+        dm = DeviceModel(plan, "cuda", [rows])
+        assert dm.gru.split
+        dm.gru.packs[0].x3_rows = tile
+        outs[tile] = dm.run(Xd, rows)[:rows].reshape(-1).cpu().numpy().copy()
+    assert np.all(np.isfinite(outs[32]))
+    np.testing.assert_array_equal(outs[16], outs[32])
+
+
+def test_abuse_gpu_overlapped_slots_match_one_stream():
+    """cfg5's AbuseGpu with one stream per pipeline slot (overlap, 32-row split tiles) returns
+    the same probabilities as the single-stream runner, with batches in flight on every slot."""
+    import torch
+    from igaming_platform_amd.utils import benchkit
+    dev = torch.device("cuda", 0)
+    res = {}
+    for overlap in (False, True):
+        S = benchkit.build_model("cfg5", 1024, 8192, dev, depth=3, use_graphs=True, precision="fp32", overlap=overlap)
+        R = S.runner
+        if overlap:
+            from igaming_platform_amd.engine.abuse import AbuseGpu
+            assert isinstance(R, AbuseGpu) and R.n_streams == 3 and R.gp.x3_rows == 32
+        ps = [R.submit(S.pool[i % len(S.pool)]) for i in range(3)]
+        res[overlap] = [R.wait(p) for p in ps]
+    for a, b in zip(res[False], res[True]):
+        np.testing.assert_array_equal(a, b)
