@@ -149,6 +149,10 @@ class LtvGpu:
         # buffers and stream, so batch i+1's H2D / kernel overlap batch i's kernel / D2H (the
         # layer-kernel path shares the DeviceModel activations and stays on one stream)
         n_bufs = depth if self.chain is not None else 1
+        # the chain's K9 epilogue stores each row's 6 outputs into the slot's pinned host buffer
+        # (24 B per row through the fabric) instead of device memory + a D2H copy kernel: cfg4
+        # fp32 124-129 -> 136-137 M/s, bf16 189-190 -> 200 M/s (profiles/r3/zb). 0: the copy
+        self._host_out = self.chain is not None and os.environ.get("IGP_LTV_HOST_OUT", "1") == "1"
         self._slabs = [torch.zeros(16 + 4 * B, dtype=torch.uint8, device=dev) for _ in range(n_bufs)]
         self._outs = [torch.zeros((B, 6), dtype=torch.float32, device=dev) for _ in range(n_bufs)]
         self._streams = [torch.cuda.Stream(device=dev) for _ in range(n_bufs)]
@@ -186,6 +190,10 @@ class LtvGpu:
         cp(self.dev_slab, self.host[slot], 16 + 4 * b)
         nout = b * self.out.shape[1] * self.out.element_size()
         if self.chain is not None:
+            if self._host_out:  # the epilogue writes the slot's pinned rows: no D2H copy kernel
+                K.mlp_chain(self.chain, b, slots=self.slots, pf_tab=self.pf_tab, ext_tab=self.ext_tab,
+                            ltv_out=self.host_out[slot], m_ptr=self.n_ptr, ws_key=slot % len(self._slabs))
+                return
             K.mlp_chain(self.chain, b, slots=self.slots, pf_tab=self.pf_tab, ext_tab=self.ext_tab,
                         ltv_out=self.out, m_ptr=self.n_ptr, ws_key=slot % len(self._slabs))
             cp(self.host_out[slot], self.out, nout)

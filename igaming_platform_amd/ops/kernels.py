@@ -114,6 +114,15 @@ def _opt(t: Optional[torch.Tensor], name: str, **kw):
     return None if t is None else _need(t, name, **kw)
 
 
+def _host_or_dev(t: Optional[torch.Tensor], name: str, min_numel: int, device):
+    """f32 output pointer: a GPU tensor on ``device`` or a pinned (device-mapped) host tensor."""
+    if t is None or t.is_cuda:
+        return _opt(t, name, dtype=torch.float32, min_numel=min_numel, device=device)
+    if not t.is_pinned() or not t.is_contiguous() or t.dtype != torch.float32 or t.numel() < min_numel:
+        raise ValueError(f"{name}: host output must be a contiguous pinned f32 tensor of >= {min_numel} elements")
+    return t.data_ptr()
+
+
 # --------------------------------------------------------------------------- K1
 def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch.Tensor,
                      X: torch.Tensor, feat: torch.Tensor, n_rows: int, dedup: bool = False,
@@ -704,15 +713,16 @@ def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, s
               m_ptr: Optional[torch.Tensor] = None, ws_key: int = 0) -> None:
     """Fused dense chain + N=1 head over ``n_rows`` rows. Input: dense ``X`` [rows, >= in] f32, or
     the LTV gather (``slots`` into ``pf_tab`` [C, 25] / ``ext_tab`` [C, ext_w]); outputs ``ml``
-    [rows] and/or the K9 rows ``ltv_out`` [rows, 6]. ``ws_key``: which pair-kernel workspace
-    (launches that may run concurrently need different keys)."""
+    [rows] and/or the K9 rows ``ltv_out`` [rows, 6] (a GPU tensor, or a pinned host tensor that
+    the epilogue writes through the fabric: no D2H copy). ``ws_key``: which pair-kernel
+    workspace (launches that may run concurrently need different keys)."""
     dev = pk.device
     d = dict(n_rows=int(n_rows), n_layers=len(pk.layers), in_w=pk.in_w, in_live=pk.in_live,
              rows_per_block=int(os.environ.get("IGP_MLP_ROWS", "64")), waves=pk.waves(),
              m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32, device=dev), w2=_need(pk.w2, "w2", torch.float32, device=dev),
              b2=pk.b2, act2=pk.act2,
              ml=_opt(ml, "ml", dtype=torch.float32, min_numel=n_rows, device=dev),
-             ltv_out=_opt(ltv_out, "ltv_out", dtype=torch.float32, min_numel=6 * n_rows, device=dev))
+             ltv_out=_host_or_dev(ltv_out, "ltv_out", 6 * n_rows, dev))
     if slots is not None:
         if pf_tab is None or pf_tab.dim() != 2 or pf_tab.shape[1] != 25:
             raise ValueError("mlp_chain: LTV gather needs the [C, 25] profile table")

@@ -258,3 +258,29 @@ def test_ltv_fp32_plan_runs_the_split_chain_and_matches_the_executor():
     o = out.cpu().numpy()
     want = [GL.predict(GL.PlayerFeatures.from_row(pf[i]), ltv_override=float(ref[i])) for i in range(cap)]
     assert [int(x) for x in o[:, 4]] == [w.segment for w in want]
+
+
+def test_ltv_chain_host_outputs_equal_device_outputs(monkeypatch):
+    """IGP_LTV_HOST_OUT=1: the chain's K9 epilogue stores the rows into the slot's pinned host
+    buffer (no D2H copy); results equal the device-buffer + copy path, slot by slot."""
+    import torch
+    from igaming_platform_amd.models.plan import compile_onnx, to_device
+    from igaming_platform_amd.native import native
+    from igaming_platform_amd.onnx import builders
+    dev = torch.device("cuda", 0)
+    m = native().OnnxModel.from_bytes(builders.build("ltv_mlp", n_features=256, width=512, layers=4).SerializeToString())
+    plan = to_device(compile_onnx(m), dev, "fp32")
+    cap = 4096
+    rng = np.random.default_rng(4)
+    pf = np.floor(rng.uniform(0, 1, (cap, 25)) * 700).astype(np.float32)
+    ext = rng.normal(0, 1, (cap, 231)).astype(np.float32)
+    batches = [rng.integers(0, cap, 1000 + 300 * i).astype(np.int32) for i in range(4)]
+    outs = {}
+    for host in ("0", "1"):
+        monkeypatch.setenv("IGP_LTV_HOST_OUT", host)
+        g = _ltv_gpu(True, plan, dev, cap)
+        assert g._host_out == (host == "1")
+        g.set_rows(np.arange(cap), pf, ext)
+        outs[host] = [g.predict_slots(s) for s in batches]
+    for a, b in zip(outs["0"], outs["1"]):
+        np.testing.assert_array_equal(a, b)
