@@ -153,6 +153,10 @@ class LtvGpu:
         # (24 B per row through the fabric) instead of device memory + a D2H copy kernel: cfg4
         # fp32 124-129 -> 136-137 M/s, bf16 189-190 -> 200 M/s (profiles/r3/zb). 0: the copy
         self._host_out = self.chain is not None and os.environ.get("IGP_LTV_HOST_OUT", "1") == "1"
+        # IGP_LTV_HOST_IN=1: the chain also reads the request slab ([n | slots], 4 B per row) from
+        # the slot's pinned buffer, skipping the H2D copy (the slot lock keeps it unchanged until
+        # the batch was waited for)
+        self._host_in = self._host_out and os.environ.get("IGP_LTV_HOST_IN", "0") == "1"
         self._slabs = [torch.zeros(16 + 4 * B, dtype=torch.uint8, device=dev) for _ in range(n_bufs)]
         self._outs = [torch.zeros((B, 6), dtype=torch.float32, device=dev) for _ in range(n_bufs)]
         self._streams = [torch.cuda.Stream(device=dev) for _ in range(n_bufs)]
@@ -187,10 +191,17 @@ class LtvGpu:
     def _body(self, slot: int, b: int) -> None:
         K = self.K
         cp = K.pull_copy if self._pull_copy else K.memcpy_async
-        cp(self.dev_slab, self.host[slot], 16 + 4 * b)
+        if not self._host_in:
+            cp(self.dev_slab, self.host[slot], 16 + 4 * b)
         nout = b * self.out.shape[1] * self.out.element_size()
         if self.chain is not None:
             if self._host_out:  # the epilogue writes the slot's pinned rows: no D2H copy kernel
+                if self._host_in:  # ... and the kernel reads [n | slots] from the pinned slab: no H2D
+                    hs = self.host[slot]
+                    K.mlp_chain(self.chain, b, slots=hs[16:16 + 4 * b].view(self.torch.int32),
+                                pf_tab=self.pf_tab, ext_tab=self.ext_tab, ltv_out=self.host_out[slot],
+                                m_ptr=hs[:4].view(self.torch.int32), ws_key=slot % len(self._slabs))
+                    return
                 K.mlp_chain(self.chain, b, slots=self.slots, pf_tab=self.pf_tab, ext_tab=self.ext_tab,
                             ltv_out=self.host_out[slot], m_ptr=self.n_ptr, ws_key=slot % len(self._slabs))
                 return

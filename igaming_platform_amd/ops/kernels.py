@@ -114,12 +114,13 @@ def _opt(t: Optional[torch.Tensor], name: str, **kw):
     return None if t is None else _need(t, name, **kw)
 
 
-def _host_or_dev(t: Optional[torch.Tensor], name: str, min_numel: int, device):
-    """f32 output pointer: a GPU tensor on ``device`` or a pinned (device-mapped) host tensor."""
+def _host_or_dev(t: Optional[torch.Tensor], name: str, min_numel: int, device, dtype=torch.float32):
+    """Pointer to a GPU tensor on ``device`` or to a pinned (device-mapped) host tensor that the
+    kernel reads / writes through the fabric."""
     if t is None or t.is_cuda:
-        return _opt(t, name, dtype=torch.float32, min_numel=min_numel, device=device)
-    if not t.is_pinned() or not t.is_contiguous() or t.dtype != torch.float32 or t.numel() < min_numel:
-        raise ValueError(f"{name}: host output must be a contiguous pinned f32 tensor of >= {min_numel} elements")
+        return _opt(t, name, dtype=dtype, min_numel=min_numel, device=device)
+    if not t.is_pinned() or not t.is_contiguous() or t.dtype != dtype or t.numel() < min_numel:
+        raise ValueError(f"{name}: host tensor must be contiguous, pinned, {dtype}, >= {min_numel} elements")
     return t.data_ptr()
 
 
@@ -719,7 +720,7 @@ def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, s
     dev = pk.device
     d = dict(n_rows=int(n_rows), n_layers=len(pk.layers), in_w=pk.in_w, in_live=pk.in_live,
              rows_per_block=int(os.environ.get("IGP_MLP_ROWS", "64")), waves=pk.waves(),
-             m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32, device=dev), w2=_need(pk.w2, "w2", torch.float32, device=dev),
+             m_ptr=_host_or_dev(m_ptr, "m_ptr", 1, dev, torch.int32), w2=_need(pk.w2, "w2", torch.float32, device=dev),
              b2=pk.b2, act2=pk.act2,
              ml=_opt(ml, "ml", dtype=torch.float32, min_numel=n_rows, device=dev),
              ltv_out=_host_or_dev(ltv_out, "ltv_out", 6 * n_rows, dev))
@@ -729,7 +730,10 @@ def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, s
         ext_w = 0 if ext_tab is None else int(ext_tab.shape[1])
         if 25 + ext_w < pk.in_live:
             raise ValueError("mlp_chain: tables narrower than the model input")
-        d.update(slots=_need(slots, "slots", torch.int32, n_rows, dev), pf_tab=_need(pf_tab, "pf_tab", torch.float32, device=dev),
+        if slots is None:
+            raise ValueError("slots: tensor required")
+        d.update(slots=_host_or_dev(slots, "slots", n_rows, dev, torch.int32),
+                 pf_tab=_need(pf_tab, "pf_tab", torch.float32, device=dev),
                  ext_tab=_opt(ext_tab, "ext_tab", dtype=torch.float32, device=dev), ext_w=ext_w)
     else:
         if X is None or X.dim() != 2 or X.shape[1] < pk.in_live or X.shape[0] < n_rows:

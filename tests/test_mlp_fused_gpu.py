@@ -262,7 +262,8 @@ def test_ltv_fp32_plan_runs_the_split_chain_and_matches_the_executor():
 
 def test_ltv_chain_host_outputs_equal_device_outputs(monkeypatch):
     """IGP_LTV_HOST_OUT=1: the chain's K9 epilogue stores the rows into the slot's pinned host
-    buffer (no D2H copy); results equal the device-buffer + copy path, slot by slot."""
+    buffer (no D2H copy); IGP_LTV_HOST_IN=1 also reads [n | slots] from the pinned slab (no
+    H2D); results equal the device-buffer + copy path, batch by batch."""
     import torch
     from igaming_platform_amd.models.plan import compile_onnx, to_device
     from igaming_platform_amd.native import native
@@ -276,11 +277,13 @@ def test_ltv_chain_host_outputs_equal_device_outputs(monkeypatch):
     ext = rng.normal(0, 1, (cap, 231)).astype(np.float32)
     batches = [rng.integers(0, cap, 1000 + 300 * i).astype(np.int32) for i in range(4)]
     outs = {}
-    for host in ("0", "1"):
-        monkeypatch.setenv("IGP_LTV_HOST_OUT", host)
+    for host in ("0", "1", "in"):
+        monkeypatch.setenv("IGP_LTV_HOST_OUT", "0" if host == "0" else "1")
+        monkeypatch.setenv("IGP_LTV_HOST_IN", "1" if host == "in" else "0")
         g = _ltv_gpu(True, plan, dev, cap)
-        assert g._host_out == (host == "1")
+        assert g._host_out == (host != "0") and g._host_in == (host == "in")
         g.set_rows(np.arange(cap), pf, ext)
         outs[host] = [g.predict_slots(s) for s in batches]
-    for a, b in zip(outs["0"], outs["1"]):
+    for a, b, c in zip(outs["0"], outs["1"], outs["in"]):
         np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(a, c)

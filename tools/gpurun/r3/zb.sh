@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 3, pass zb: LTV chain writing its K9 rows straight into pinned host memory (no D2H copy
+# round 3, pass zb: LTV chain with host-resident outputs (and inputs, zc): parity test, cfg4 A/B
 # kernel): parity test, cfg4 fp32 / bf16 engine A/B
 set -o pipefail
 cd $GRAFT_REPO_ROOT
