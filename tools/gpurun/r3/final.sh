@@ -3,7 +3,7 @@
 # command (twice), every config's default run, rocprof kernel statistics of the headline
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r3final
+O=gpurun_out/${R3FINAL:-r3final}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/tests.txt 2>&1
 rc=$?; echo "tests rc=$rc $(tail -1 $O/tests.txt)" >> $O/status.txt
