@@ -688,6 +688,10 @@ def model_bench(a, world: int, rank: int, dev) -> None:
     import torch
     import torch.distributed as dist
     from igaming_platform_amd.utils import benchkit
+    if world > 1 and not a.no_gather:
+        # the results are all-gathered from the device output buffers: keep the LTV rows there
+        # (IGP_LTV_HOST_OUT=1, the 1-GPU default, writes them straight to pinned host memory)
+        os.environ["IGP_LTV_HOST_OUT"] = "0"
     S = benchkit.build_model(a.config, a.batch, a.accounts, dev, rank=rank, depth=a.depth,
                              use_graphs=not a.no_graphs, precision=a.numerics)
     R, B = S.runner, S.batch
