@@ -55,10 +55,6 @@ def parse():
     ap.add_argument("--depth", type=int, default=3, help="pipeline depth (batches in flight)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the per-step RCCL all_gather")
-    ap.add_argument("--stream", action="store_true",
-                    help="scorer configs: streaming mode, one launch per batch running copy(i) || state(i-1) "
-                         "|| model(i-2) (measured slower on ROCm 7.2 than the default three-stream pipeline: "
-                         "~35 us between consecutive multi-branch graph launches)")
     ap.add_argument("--numerics", default="auto", choices=["auto", "fp32", "bf16"],
                     help="dense-layer numerics: fp32 = the ONNX model's f32 contract (default; f32 MFMA heads, "
                          "split bf16x3 MFMA for the cfg4 chain and the cfg5 GRU), bf16 = bf16 MFMA with f32 accumulate")
@@ -68,16 +64,23 @@ def parse():
                          "its owner and the results back; replicas = N independent single-GPU pipelines")
     ap.add_argument("--scope", default="auto", choices=["auto", "serving", "engine_only", "e2e", "grpc"],
                     help="auto (default): serving for the fraud configs, engine_only for cfg4 / cfg5 (LTV and "
-                         "abuse models are not ScoreBatch traffic); serving: the serving objects of every rank - risk.v1 ScoreBatch request bytes "
-                         "(UUID account ids) -> the rank's native serving core (C++ parse, node-shared AccountIndex, "
+                         "abuse models are not ScoreBatch traffic); serving: the serving objects of every rank - "
+                         "risk.v1 ScoreBatch request bytes (UUID account ids) -> the rank's native serving core "
+                         "(C++ parse, node-shared AccountIndex, "
                          "owner-routed RCCL exchange steps for N > 1, GPU pipeline) -> response bytes with the "
                          "FeatureVector, every rank ingesting; engine_only: pre-resolved ReqRec rows into the "
                          "device pipeline (device-pipeline number); e2e / grpc: tools/bench_e2e.py")
-    ap.add_argument("--threads", type=int, default=16, help="serving scope: ingress threads per rank (the box gives each GPU 16 CPUs)")
+    ap.add_argument("--threads", type=int, default=16,
+                    help="serving scope: ingress threads per rank (the box gives each GPU 16 CPUs)")
     ap.add_argument("--requests", type=int, default=0, help="serving scope: transactions per ScoreBatch request "
                     "(default: the config's micro-batch)")
     ap.add_argument("--rpc", default="batch", choices=["batch", "tx"], help="--scope grpc: ScoreBatch or unary "
                     "ScoreTransaction through the micro-batcher")
+    ap.add_argument("--rates", default="25000,50000,100000,150000,200000,300000",
+                    help="--scope serving with cfg4 / cfg5: offered PredictLTV / CheckBonusAbuse calls/s per level "
+                         "(open loop over the native gRPC server)")
+    ap.add_argument("--seconds", type=float, default=5.0, help="cfg4 / cfg5 serving: seconds per offered-load level")
+    ap.add_argument("--zipf", type=float, default=0.0, help="cfg4 / cfg5 serving: Zipf exponent of the account ids")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
     if a.numerics == "auto":  # the ONNX models' f32 contract everywhere (cfg4 / cfg5: split MFMA)
@@ -108,8 +111,26 @@ def maybe_launch_torchrun(a) -> None:
         sys.exit(subprocess.call(cmd))
 
 
+def acct_serving_bench(a) -> None:
+    """cfg4 / cfg5 through the serving path, 1 GPU: unary PredictLTV / CheckBonusAbuse calls over
+    the native HTTP/2 server (bytes in -> the native account router -> micro-batches on the LTV
+    chain / abuse step -> response bytes) from the native open-loop load generator, stepped
+    through --rates; the value is the highest offered rate answered in full with p99 < 50 ms
+    (tools/bench_e2e.py _native_open_loop)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+    import bench_e2e
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or a.gpus > 1:
+        raise SystemExit("cfg4 / cfg5 --scope serving runs on 1 GPU (multi-GPU: --scope engine_only)")
+    argv = ["--scope", "grpc", "--rpc", "ltv" if a.config == "cfg4" else "abuse", "--open-loop", "--accounts",
+            str(a.accounts), "--rates", a.rates, "--seconds", str(a.seconds), "--numerics", a.numerics,
+            "--zipf", str(a.zipf)] + (["--json-out", a.json_out] if a.json_out else [])
+    return bench_e2e.main(argv)
+
+
 def main():
     a = parse()
+    if a.scope == "serving" and a.config in ("cfg4", "cfg5"):
+        return acct_serving_bench(a)
     if a.scope == "serving":
         maybe_launch_torchrun(a)
         return serving_bench(a)
@@ -144,8 +165,8 @@ def main():
     from igaming_platform_amd.utils import benchkit
     from igaming_platform_amd.utils.synth import NOW0
 
-    exchange = ((world > 1 and a.dp_mode == "exchange" and a.config not in benchkit.MODEL_CONFIGS
-                 and not (a.stream and not a.no_graphs)) or os.environ.get("IGP_FORCE_EXCHANGE") == "1")
+    exchange = ((world > 1 and a.dp_mode == "exchange" and a.config not in benchkit.MODEL_CONFIGS)
+                or os.environ.get("IGP_FORCE_EXCHANGE") == "1")
     if world > 1:
         if exchange or backend != "nccl":
             # the exchange moves rows over its own two RCCL communicators; the process group is
@@ -158,8 +179,6 @@ def main():
     if a.config in benchkit.MODEL_CONFIGS:
         return model_bench(a, world, rank, dev)
 
-    if a.stream and not a.no_graphs:
-        return stream_bench(a, world, rank, dev)
     if exchange:
         if dp_bench(a, world, rank, dev) is not None:  # (forced at N = 1: RCCL's single-rank path, for tests)
             return
@@ -610,77 +629,6 @@ def _emit(a, world: int, rank: int, out: dict) -> None:
                 f.write(line + "\n")
     if world > 1:
         dist.destroy_process_group()
-
-
-def stream_bench(a, world: int, rank: int, dev) -> None:
-    """Scorer configs in streaming mode (engine/scorer.py capture_pipelined): launch p runs
-    copy + dedup insert of batch p || feature assembly + store update of batch p-1 || model +
-    ensemble + D2H of batch p-2, one hipGraphLaunch per micro-batch. The timed region starts
-    with an empty pipeline and ends after the two drain launches: every timed batch is fully
-    scored and its results are on the host."""
-    import torch
-    import torch.distributed as dist
-    from igaming_platform_amd.utils import benchkit
-    from igaming_platform_amd.utils.synth import NOW0
-    S = benchkit.build(a.config, a.batch, a.accounts, dev, rank=rank, depth=3, use_graphs=True,
-                       precision=a.numerics)
-    sc, pool, B = S.scorer, S.pool, S.batch
-    sc.capture_pipelined()
-    gathered = torch.zeros(world * B * 2, dtype=torch.int32, device=dev) if world > 1 else None
-    met_sum = torch.zeros(128, dtype=torch.int64, device=dev)
-    lat: list = []
-    scored = [0]
-
-    def step(i: int, now: int):
-        slot, done = sc.pipe_reserve()
-        sc.pack(slot, pool[i % len(pool)])  # the wire decoder's output: raw REQREC rows
-        sc.pipe_launch(B, now)
-        if world > 1 and not a.no_gather:
-            with torch.cuda.stream(sc.pstream):  # results of the batch this launch finished
-                dist.all_gather_into_tensor(gathered, sc.slots[(slot + 1) % 3].res[:B].reshape(-1))
-                if i % 16 == 15:
-                    met_sum.copy_(sc.metrics)
-                    dist.all_reduce(met_sum)
-        return done
-
-    def account(done):
-        for n, _, ms in done:
-            scored[0] += n
-            lat.append(ms)
-
-    for i in range(a.warmup):
-        step(i, NOW0 + i // 50)
-    sc.pipe_drain()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        account(step(a.warmup + i, NOW0 + (a.warmup + i) // 50))
-    account(sc.pipe_drain())
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    assert scored[0] == B * a.steps, (scored[0], B * a.steps)
-    stats = torch.tensor([elapsed, float(np.percentile(lat, 99)), float(np.percentile(lat, 50))],
-                         dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-    elapsed, p99, p50 = (float(x) for x in stats.cpu())
-    out = {
-        "metric": "fraud scores/sec (whole node) + p99 score latency",
-        "value": world * B * a.steps / elapsed, "unit": "scores/s", "n_gpus": world, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": a.numerics, "data": "synthetic",
-        "config": {"model": S.desc, "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
-                   "per_gpu_batch": B, "accounts_per_gpu": a.accounts, "pipeline": "streaming (1 launch/batch)",
-                   "graphs": True,
-                   "numerics": numerics_desc(a)},
-        "p99_latency_ms": p99, "p50_latency_ms": p50, "latency_baseline_ms": BASELINE_P99_MS,
-        "latency_vs_baseline": BASELINE_P99_MS / p99 if p99 > 0 else None,
-    }
-    _emit(a, world, rank, out)
 
 
 def model_bench(a, world: int, rank: int, dev) -> None:

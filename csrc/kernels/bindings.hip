@@ -111,9 +111,9 @@ StopEvent& stop_event() {
 
 namespace igp {
 void register_driver(py::module_& m);
+void register_model_driver(py::module_& m);
 void register_exchange(py::module_& m);
 void register_watch(py::module_& m);
-void register_copy(py::module_& m);
 }
 
 PYBIND11_MODULE(_hipk, m) {
@@ -127,9 +127,9 @@ PYBIND11_MODULE(_hipk, m) {
   m.attr("DEDUP_LIST") = DEDUP_LIST;
   m.attr("DEDUP_REGIONS") = DEDUP_RING + 1;
   igp::register_driver(m);
+  igp::register_model_driver(m);
   igp::register_exchange(m);
   igp::register_watch(m);
-  igp::register_copy(m);
 
   m.def("feature_assemble", [](py::dict d, uintptr_t s) {
     AssembleArgs a{};
@@ -465,7 +465,6 @@ PYBIND11_MODULE(_hipk, m) {
     check("gru");
   });
   m.def("gru_ws_clusters", [](int n_rows) { return gru_ws_clusters(n_rows); });
-  m.def("mlp_pair_clusters", [](int n_rows) { return mlp_pair_clusters(n_rows); });
 
   m.def("mlp_chain", [](py::dict d, uintptr_t s) {
     MlpChainArgs a{};
@@ -508,11 +507,6 @@ PYBIND11_MODULE(_hipk, m) {
     for (int l = 0; l < a.n_layers; ++l)
       if (a.N[l] % (16 * a.waves)) throw std::runtime_error("mlp_chain: N must be a multiple of 16 x waves");
     a.split = geti(d, "split", 0);
-    a.pair_x = ptr<uint16_t*>(d, "pair_x");
-    a.pair_sync = ptr<int32_t*>(d, "pair_sync");
-    a.pair_part = ptr<float*>(d, "pair_part");
-    a.pair_err = ptr<int32_t*>(d, "pair_err");
-    a.pair_clusters = geti(d, "pair_clusters", 0);
     if (a.split) {
       for (int l = 0; l < a.n_layers; ++l)
         if (!a.W_lo[l]) throw std::runtime_error("mlp_chain: split mode needs every layer's residual weights");

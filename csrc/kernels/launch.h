@@ -311,17 +311,7 @@ struct MlpChainArgs {
   int32_t waves;            // 4 (default) or 8 (32 rows; each wave owns N/8 columns)
   const uint16_t* W_lo[MC_MAX_LAYERS];  // split (f32-faithful) mode: bf16 residuals w - bf16(w)
   int32_t split;            // 1: three-MFMA bf16 pairs (hi*hi + hi*lo + lo*hi)
-  // pair-cluster form (mlp_pair.hip: two CUs per 128 rows, each streaming half of every
-  // layer's weights); used when the workspace is given and every layer is 512 wide
-  uint16_t* pair_x;         // [pair_clusters][2 parity][2 members][128 x 256] bf16 hand-off slabs
-  int32_t* pair_sync;       // [pair_clusters][16] counters (back to 0 after every launch)
-  float* pair_part;         // [pair_clusters][2][128] head partials
-  int32_t* pair_err;        // [1] set when a pair was not co-resident (bounded wait expired)
-  int32_t pair_clusters;    // workspace capacity in 128-row pairs
 };
 void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st);
-bool mlp_pair_eligible(const MlpChainArgs& a);
-void launch_mlp_pair(const MlpChainArgs& a, hipStream_t st);
-int mlp_pair_clusters(int n_rows);
 
 }  // namespace igp

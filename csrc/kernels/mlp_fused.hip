@@ -297,7 +297,6 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
 
 void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
-  if (mlp_pair_eligible(a)) return launch_mlp_pair(a, st);
   const int r = a.rows_per_block;
   if (a.split) {  // f32-faithful: hi + lo tiles fill the LDS (64 rows: each tile once, NBUF = 1)
     if (a.waves == 8 && r == 64)

@@ -8,6 +8,8 @@
 #include <memory>
 
 #include "account_index.h"
+#include "acct_core.h"
+#include "acct_devices.h"
 #include "audit.h"
 #include "h2grpc.h"
 #include "cpu_device.h"
@@ -85,10 +87,38 @@ struct PyServe {
   py::object dev;
 };
 
+// Python handle of the account-RPC router: keeps the model devices (whose function tables its
+// cores call) alive for as long as the cores may use them
+struct PyAcct {
+  std::shared_ptr<AcctRouter> router;
+  std::vector<py::object> devs;
+  ~PyAcct() {
+    if (router) {
+      py::gil_scoped_release rel;
+      router->stop();
+    }
+  }
+};
+
+const IgpModelOps* model_ops_of(py::object dev) {
+  const uintptr_t p = dev.attr("model_ops")().cast<uintptr_t>();
+  if (!p) throw std::runtime_error("model_ops(): null function table");
+  return reinterpret_cast<const IgpModelOps*>(p);
+}
+
+py::dict acct_stats_dict(const AcctStats& t) {
+  py::dict d;
+  d["items"] = t.items; d["steps"] = t.steps; d["rows"] = t.rows; d["device_ns"] = t.device_ns;
+  d["queue_ns"] = t.queue_ns; d["finish_ns"] = t.finish_ns; d["wait_errors"] = t.wait_errors;
+  d["max_step_rows"] = t.max_step_rows;
+  return d;
+}
+
 // the native gRPC server; stopped without the GIL (its cold threads may be waiting for it)
 struct PyGrpc {
   std::unique_ptr<GrpcServer> srv;
   py::object core;  // keeps the PyServe (and its device) alive
+  py::object acct;  // keeps the PyAcct alive
   ~PyGrpc() {
     if (srv) {
       {
@@ -385,6 +415,10 @@ PYBIND11_MODULE(_native, m) {
 
   py::class_<LinkIndex, std::shared_ptr<LinkIndex>>(m, "LinkIndex")
       .def(py::init<int, int64_t>(), py::arg("per_key") = 8, py::arg("buckets") = int64_t(1) << 18)
+      .def(py::init<int, int64_t, const std::string&, bool>(), py::arg("per_key"), py::arg("buckets"),
+           py::arg("shm_name"), py::arg("create"))
+      .def("unlink_shared", &LinkIndex::unlink_shared)
+      .def_property_readonly("shared", &LinkIndex::shared)
       .def("add", [](LinkIndex& ix, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> dev,
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> acct) {
         if (dev.size() != acct.size()) throw std::runtime_error("LinkIndex.add: length mismatch");
@@ -629,12 +663,17 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("segment"), py::arg("db"), py::arg("schema"));
 
   py::class_<PyGrpc>(m, "GrpcServer")
-      .def(py::init([](py::object core, py::function cold, int cold_threads, int batch_threads) {
+      .def(py::init([](py::object core, py::function cold, int cold_threads, int batch_threads, py::object acct) {
              auto p = std::make_unique<PyGrpc>();
              std::shared_ptr<ServeCore> c;
              if (!core.is_none()) {
                c = core.cast<PyServe&>().core;
                p->core = core;
+             }
+             std::shared_ptr<AcctRouter> ar;
+             if (!acct.is_none()) {
+               ar = acct.cast<PyAcct&>().router;
+               p->acct = acct;
              }
              // cold RPC: cold(path: str, body: bytes) -> bytes, or (grpc status, message)
              GrpcServer::ColdFn fn = [cb = py::function(cold)](const std::string& path, std::string body) {
@@ -658,10 +697,11 @@ PYBIND11_MODULE(_native, m) {
                }
                return r;
              };
-             p->srv = std::make_unique<GrpcServer>(c, std::move(fn), cold_threads, batch_threads);
+             p->srv = std::make_unique<GrpcServer>(c, std::move(fn), cold_threads, batch_threads, ar);
              return p;
            }),
-           py::arg("core"), py::arg("cold"), py::arg("cold_threads") = 4, py::arg("batch_threads") = 8)
+           py::arg("core"), py::arg("cold"), py::arg("cold_threads") = 4, py::arg("batch_threads") = 8,
+           py::arg("acct") = py::none())
       .def("start", [](PyGrpc& s, const std::string& host, int port, int workers) {
         py::gil_scoped_release rel;
         return s.srv->start(host, port, workers);
@@ -680,8 +720,11 @@ PYBIND11_MODULE(_native, m) {
         d["cold"] = st.cold;
         d["errors"] = st.errors;
         d["connections"] = st.connections;
+        d["hot_acct"] = st.hot_acct;
+        d["hot_failures"] = st.hot_failures;
         return d;
-      });
+      })
+      .def("last_failure", [](PyGrpc& s) { return s.srv->last_failure(); });
 
   m.def("grpc_load", [](const std::string& host, int port, const std::string& path, std::vector<std::string> payloads,
                         double rate, double seconds, int conns, int max_inflight) {
@@ -831,4 +874,126 @@ PYBIND11_MODULE(_native, m) {
         return d;
       }, py::arg("reset") = false)
       .def_static("now_ns", &ServeCore::now_ns);
+
+  // ---- account RPCs (acct_core.h): PredictLTV / GetPlayerSegment / CheckBonusAbuse
+  m.attr("RPC_LTV") = int(RPC_LTV);
+  m.attr("RPC_SEGMENT") = int(RPC_SEGMENT);
+  m.attr("RPC_ABUSE") = int(RPC_ABUSE);
+  py::class_<CpuLtvDevice, std::shared_ptr<CpuLtvDevice>>(m, "CpuLtvDevice")
+      .def(py::init([](py::array rows, py::array present, py::object ext, py::object model, std::string in_name,
+                       std::string out_name, int width, int depth, int cap) {
+             // the arrays stay owned by the caller (engine/ltv.py PlayerTable), which keeps them alive
+             auto r = py::array_t<float, py::array::c_style>::ensure(rows);
+             auto pr = py::array_t<uint8_t, py::array::c_style>::ensure(present);
+             if (!r || !pr || r.ndim() != 2 || r.shape(1) != 25 || pr.size() != r.shape(0))
+               throw std::runtime_error("CpuLtvDevice: rows [C, 25] f32 and present [C] (bool / uint8) expected");
+             if (static_cast<const void*>(r.data()) != rows.data() || static_cast<const void*>(pr.data()) != present.data())
+               throw std::runtime_error("CpuLtvDevice: the tables must be C-contiguous (no copies)");
+             const float* ep = nullptr;
+             int ew = 0;
+             if (!ext.is_none()) {
+               auto e = py::array_t<float, py::array::c_style>::ensure(ext);
+               if (!e || static_cast<const void*>(e.data()) != ext.cast<py::array>().data() || e.ndim() != 2 ||
+                   e.shape(0) != r.shape(0))
+                 throw std::runtime_error("CpuLtvDevice: ext [C, w] f32, C-contiguous");
+               ep = e.data();
+               ew = int(e.shape(1));
+             }
+             std::shared_ptr<exec::Executor> ex;
+             if (!model.is_none()) ex = model.cast<std::shared_ptr<exec::Executor>>();
+             return std::make_shared<CpuLtvDevice>(r.data(), pr.data(), ep, ew, int64_t(r.shape(0)), ex, in_name,
+                                                   out_name, width, depth, cap);
+           }),
+           py::arg("rows"), py::arg("present"), py::arg("ext"), py::arg("model"), py::arg("in_name") = "input",
+           py::arg("out_name") = "output", py::arg("width") = 0, py::arg("depth") = 2, py::arg("cap") = 4096)
+      .def("model_ops", [](const CpuLtvDevice& d) { return reinterpret_cast<uintptr_t>(d.ops()); });
+  py::class_<CpuAbuseDevice, std::shared_ptr<CpuAbuseDevice>>(m, "CpuAbuseDevice")
+      .def(py::init<std::shared_ptr<CpuScorer>, std::shared_ptr<exec::Executor>, std::string, std::string, int, int>(),
+           py::arg("scorer"), py::arg("model"), py::arg("in_name") = "input", py::arg("out_name") = "output",
+           py::arg("depth") = 2, py::arg("cap") = 4096)
+      .def("model_ops", [](const CpuAbuseDevice& d) { return reinterpret_cast<uintptr_t>(d.ops()); });
+
+  py::class_<PyAcct, std::shared_ptr<PyAcct>>(m, "AcctRouter")
+      .def(py::init([](std::vector<std::shared_ptr<AccountIndex>> idx, int rank, std::string mailbox, bool create) {
+             auto p = std::make_shared<PyAcct>();
+             py::gil_scoped_release rel;
+             p->router = std::make_shared<AcctRouter>(std::move(idx), rank, mailbox, create);
+             return p;
+           }),
+           py::arg("indexes"), py::arg("rank") = 0, py::arg("mailbox") = "", py::arg("create") = false)
+      .def("attach", [](PyAcct& a, py::object dev, int max_wait_us, int64_t timeout_us, int finishers) {
+        AcctCore::Options o;
+        o.max_wait_us = max_wait_us;
+        o.timeout_us = timeout_us;
+        o.finishers = finishers;
+        const IgpModelOps* ops = model_ops_of(dev);
+        a.devs.push_back(dev);
+        py::gil_scoped_release rel;
+        a.router->attach(ops, o);
+      }, py::arg("device"), py::arg("max_wait_us") = 200, py::arg("timeout_us") = -1, py::arg("finishers") = 2)
+      .def("set_device", [](PyAcct& a, py::object dev) {
+        const IgpModelOps* ops = model_ops_of(dev);
+        a.devs.push_back(dev);  // the old table may still be read by a step in flight: keep it
+        py::gil_scoped_release rel;
+        a.router->set_device(ops->kind, ops);
+      })
+      .def("set_links", [](PyAcct& a, std::shared_ptr<LinkIndex> l) { a.router->set_links(std::move(l)); })
+      .def("set_abuse", [](PyAcct& a, int max_devices, int max_ips, int max_tx_per_minute, double threshold,
+                           std::vector<double> weights, int linked_limit) {
+        AbuseParams p;
+        p.max_devices_per_day = max_devices;
+        p.max_ips_per_day = max_ips;
+        p.max_tx_per_minute = max_tx_per_minute;
+        p.threshold = threshold;
+        if (weights.size() != 7) throw std::runtime_error("set_abuse: 7 signal weights");
+        for (int k = 0; k < 7; ++k) p.w[k] = weights[size_t(k)];
+        p.linked_limit = linked_limit;
+        a.router->set_abuse(p);
+      }, py::arg("max_devices"), py::arg("max_ips"), py::arg("max_tx_per_minute"), py::arg("threshold"),
+         py::arg("weights"), py::arg("linked_limit") = 16)
+      .def("serves", [](PyAcct& a, int rpc) { return a.router->serves(uint8_t(rpc)); })
+      .def("submit", [](PyAcct& a, int rpc, py::bytes data, uint64_t tag, int64_t t0_ns, int64_t now) {
+        char* p; py::ssize_t n;
+        PYBIND11_BYTES_AS_STRING_AND_SIZE(data.ptr(), &p, &n);
+        a.router->submit(uint8_t(rpc), p, size_t(n), tag, t0_ns, now);
+      }, py::arg("rpc"), py::arg("data"), py::arg("tag"), py::arg("t0_ns") = 0, py::arg("now") = -1)
+      .def("submit_many", [](PyAcct& a, int rpc, py::list items, py::list tags, int64_t now) {
+        const size_t n = items.size();
+        if (tags.size() != n) throw std::runtime_error("submit_many: lengths");
+        std::vector<std::string> bufs(n);
+        std::vector<uint64_t> tg(n);
+        for (size_t k = 0; k < n; ++k) {
+          bufs[k] = items[k].cast<std::string>();
+          tg[k] = tags[k].cast<uint64_t>();
+        }
+        py::gil_scoped_release rel;
+        const int64_t t0 = ServeCore::now_ns();
+        for (size_t k = 0; k < n; ++k) a.router->submit(uint8_t(rpc), bufs[k].data(), bufs[k].size(), tg[k], t0, now);
+      }, py::arg("rpc"), py::arg("items"), py::arg("tags"), py::arg("now") = -1)
+      .def("poll", [](PyAcct& a, size_t max, int64_t timeout_us) {
+        std::vector<AcctRouter::Done> out;
+        {
+          py::gil_scoped_release rel;
+          a.router->poll(out, max, timeout_us);
+        }
+        py::list l;
+        for (auto& d : out) {
+          if (d.err.empty()) l.append(py::make_tuple(d.tag, py::bytes(d.bytes), py::none()));
+          else l.append(py::make_tuple(d.tag, py::none(), py::str(d.err)));
+        }
+        return l;
+      }, py::arg("max") = 4096, py::arg("timeout_us") = 1000)
+      .def("stop", [](PyAcct& a) {
+        py::gil_scoped_release rel;
+        a.router->stop();
+      })
+      .def("unlink_shared", [](PyAcct& a) { a.router->unlink_shared(); })
+      .def("stats", [](PyAcct& a, int kind, bool reset) { return acct_stats_dict(a.router->stats(kind, reset)); },
+           py::arg("kind"), py::arg("reset") = false)
+      .def_property_readonly("remote_out", [](const PyAcct& a) { return a.router->remote_out(); })
+      .def_property_readonly("remote_expired", [](const PyAcct& a) { return a.router->remote_expired(); })
+      .def_property_readonly("world", [](const PyAcct& a) { return a.router->world(); })
+      .def_property_readonly("rank", [](const PyAcct& a) { return a.router->rank(); })
+      .def_property("remote_timeout_us", [](const PyAcct& a) { return a.router->remote_timeout_us; },
+                    [](PyAcct& a, int64_t v) { a.router->remote_timeout_us = v; });
 }

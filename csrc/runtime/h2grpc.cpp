@@ -148,6 +148,26 @@ constexpr int kWorkerShift = 40;
 constexpr uint64_t kTokenMask = (uint64_t(1) << kWorkerShift) - 1;
 const std::string kPathTx = "/risk.v1.RiskService/ScoreTransaction";
 const std::string kPathBatch = "/risk.v1.RiskService/ScoreBatch";
+const std::string kPathLtv = "/risk.v1.RiskService/PredictLTV";
+const std::string kPathSeg = "/risk.v1.RiskService/GetPlayerSegment";
+const std::string kPathAbuse = "/risk.v1.RiskService/CheckBonusAbuse";
+
+// the account RPC a path names (0: none)
+uint8_t acct_rpc(const std::string& path) {
+  if (path == kPathLtv) return RPC_LTV;
+  if (path == kPathSeg) return RPC_SEGMENT;
+  if (path == kPathAbuse) return RPC_ABUSE;
+  return 0;
+}
+
+// a failed hot call: malformed requests answer INVALID_ARGUMENT; anything else (a device error or
+// deadline inside a core) is retried through the cold handler table
+bool invalid_request(const std::string& err) {
+  return err.rfind("invalid: ", 0) == 0 || err.find("pb:") != std::string::npos;
+}
+std::string invalid_message(const std::string& err) {
+  return err.rfind("invalid: ", 0) == 0 ? err.substr(9) : err;
+}
 
 }  // namespace
 
@@ -168,12 +188,20 @@ struct GrpcServer::Worker {
     std::string wbuf;
     size_t woff = 0;
     bool epollout = false;
+    size_t buffered = 0;  // request bytes held by this connection's streams
   };
   struct Done {
     uint64_t token;  // hot unary: pending-table token; 0: conn / stream below
     uint64_t conn;
     int32_t stream;
     GrpcReply reply;
+    bool retry = false;  // a failed hot call: run it again through the cold handler table
+  };
+  struct Pend {  // a hot unary call in a core: where to answer, and its request for a retry
+    uint64_t conn;
+    int32_t stream;
+    std::string path;
+    std::string body;
   };
 
   GrpcServer* srv;
@@ -181,7 +209,7 @@ struct GrpcServer::Worker {
   int lfd = -1, ep = -1, evfd = -1;
   std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns;
   uint64_t next_conn = kFirstConn;
-  std::unordered_map<uint64_t, std::pair<uint64_t, int32_t>> pending;  // token -> (conn, stream)
+  std::unordered_map<uint64_t, Pend> pending;  // token -> the call
   uint64_t next_token = 1;
   std::mutex qmu;
   std::vector<Done> q;
@@ -230,8 +258,12 @@ struct GrpcServer::Worker {
     auto* c = static_cast<Conn*>(ud);
     auto it = c->streams.find(sid);
     if (it != c->streams.end()) {
-      if (it->second.data.size() + len > (size_t(64) << 20)) return -902;  // NGHTTP2_ERR_CALLBACK_FAILURE
+      // per-stream (64 MiB) and per-connection (kMaxConnBuffered) request bytes: past either the
+      // connection fails (NGHTTP2_ERR_CALLBACK_FAILURE) instead of the server allocating without
+      // bound
+      if (it->second.data.size() + len > (size_t(64) << 20) || c->buffered + len > kMaxConnBuffered) return -902;
       it->second.data.append(reinterpret_cast<const char*>(data), len);
+      c->buffered += len;
     }
     return 0;
   }
@@ -243,7 +275,12 @@ struct GrpcServer::Worker {
     return 0;
   }
   static int on_close(void*, int32_t sid, uint32_t, void* ud) {
-    static_cast<Conn*>(ud)->streams.erase(sid);
+    auto* c = static_cast<Conn*>(ud);
+    auto it = c->streams.find(sid);
+    if (it != c->streams.end()) {
+      c->buffered -= std::min(c->buffered, it->second.data.size());
+      c->streams.erase(it);
+    }
     return 0;
   }
   static ssize_t read_body(void* sess, int32_t sid, uint8_t* buf, size_t len, uint32_t* flags, NgDataSource* src,
@@ -343,7 +380,7 @@ struct GrpcServer::Worker {
         ::close(fd);
         continue;
       }
-      const NgSettingsEntry iv[2] = {{kSettingsMaxStreams, 4096}, {kSettingsInitialWindow, 8u << 20}};
+      const NgSettingsEntry iv[2] = {{kSettingsMaxStreams, kMaxStreams}, {kSettingsInitialWindow, 8u << 20}};
       n.submit_settings(c->sess, 0, iv, 2);
       if (n.set_local_window_size) n.set_local_window_size(c->sess, 0, 0, 64 << 20);
       epoll_event e{};
@@ -457,15 +494,29 @@ struct GrpcServer::Worker {
       respond(c, sid, bad);
       return;
     }
-    const bool hot = srv->hot_.load(std::memory_order_relaxed) && srv->core_;
-    if (hot && st.path == kPathTx) {
+    const bool hot = srv->hot_.load(std::memory_order_relaxed);
+    const uint8_t arpc = hot && srv->router_ ? acct_rpc(st.path) : 0;
+    if ((hot && srv->core_ && st.path == kPathTx) || (arpc && srv->router_->serves(arpc))) {
       const uint64_t token = next_token++ & kTokenMask;
-      pending[token] = {c.id, sid};
-      srv->hot_tx_.fetch_add(1, std::memory_order_relaxed);
-      srv->core_->submit_tx(d.data() + 5, d.size() - 5, ServeCore::kSinkTag | (uint64_t(idx) << kWorkerShift) | token,
-                            -1, mono_ns());
+      const uint64_t tag = ServeCore::kSinkTag | (uint64_t(idx) << kWorkerShift) | token;
+      c.buffered -= std::min(c.buffered, st.data.size());
+      Pend& p = pending[token];
+      p.conn = c.id;
+      p.stream = sid;
+      p.path = st.path;
+      p.body = std::move(st.data);  // kept for a retry through the cold table
+      const char* body = p.body.data() + 5;
+      const size_t blen = p.body.size() - 5;
+      if (arpc) {
+        srv->hot_acct_.fetch_add(1, std::memory_order_relaxed);
+        srv->router_->submit(arpc, body, blen, tag, mono_ns());
+      } else {
+        srv->hot_tx_.fetch_add(1, std::memory_order_relaxed);
+        srv->core_->submit_tx(body, blen, tag, -1, mono_ns());
+      }
       return;
     }
+    c.buffered -= std::min(c.buffered, st.data.size());
     Job j{idx, c.id, sid, st.path, d.substr(5)};
     {
       std::lock_guard<std::mutex> g(srv->jmu_);
@@ -524,8 +575,20 @@ struct GrpcServer::Worker {
       if (d.token) {
         auto p = pending.find(d.token);
         if (p == pending.end()) continue;
-        cid = p->second.first;
-        sid = p->second.second;
+        cid = p->second.conn;
+        sid = p->second.stream;
+        if (d.retry) {  // the native path failed: the cold table answers (engine fallback)
+          Pend pd = std::move(p->second);
+          pending.erase(p);
+          srv->note_failure(d.reply.message);
+          {
+            std::lock_guard<std::mutex> g(srv->jmu_);
+            srv->cold_n_.fetch_add(1, std::memory_order_relaxed);
+            srv->cold_q_.push_back(Job{idx, cid, sid, pd.path + "#retry:" + d.reply.message, pd.body.substr(5)});
+          }
+          srv->jcv_.notify_one();
+          continue;
+        }
         pending.erase(p);
       }
       auto it = conns.find(cid);
@@ -541,10 +604,44 @@ struct GrpcServer::Worker {
 };
 
 // ---------------------------------------------------------------------------- server
-GrpcServer::GrpcServer(std::shared_ptr<ServeCore> core, ColdFn cold, int cold_threads, int batch_threads)
-    : core_(std::move(core)), cold_(std::move(cold)), n_cold_(std::max(1, cold_threads)),
+GrpcServer::GrpcServer(std::shared_ptr<ServeCore> core, ColdFn cold, int cold_threads, int batch_threads,
+                       std::shared_ptr<AcctRouter> router)
+    : core_(std::move(core)), router_(std::move(router)), cold_(std::move(cold)), n_cold_(std::max(1, cold_threads)),
       n_batch_(core_ ? std::max(0, batch_threads) : 0) {
   ng();  // fail early without libnghttp2
+}
+
+void GrpcServer::note_failure(const std::string& msg) {
+  hot_fail_.fetch_add(1, std::memory_order_relaxed);
+  std::lock_guard<std::mutex> g(fail_mu_);
+  last_failure_ = msg;
+}
+
+std::string GrpcServer::last_failure() const {
+  std::lock_guard<std::mutex> g(fail_mu_);
+  return last_failure_;
+}
+
+// completions of hot unary calls (a core's finisher thread): to the worker owning the connection
+void GrpcServer::route_done(std::vector<ServeCore::Done>&& outs) {
+  for (auto& d : outs) {
+    const int wi = int((d.tag & ~ServeCore::kSinkTag) >> kWorkerShift);
+    if (wi < 0 || size_t(wi) >= workers_.size()) continue;
+    Worker::Done w{d.tag & kTokenMask, 0, 0, GrpcReply{}, false};
+    if (!d.err.empty()) {
+      if (invalid_request(d.err)) {
+        w.reply.status = 3;
+        w.reply.message = invalid_message(d.err);
+      } else {
+        w.reply.status = 13;
+        w.reply.message = d.err;
+        w.retry = true;
+      }
+    } else {
+      w.reply.body = std::move(d.bytes);
+    }
+    workers_[size_t(wi)]->post(std::move(w));
+  }
 }
 
 GrpcServer::~GrpcServer() { stop(); }
@@ -559,28 +656,16 @@ int GrpcServer::start(const std::string& host, int port, int workers) {
     if (i == 0) bound = w->bound_port();
     workers_.push_back(std::move(w));
   }
-  if (core_) {
-    core_->set_sink([this](std::vector<ServeCore::Done>&& outs) {
-      sink_active_.fetch_add(1, std::memory_order_acq_rel);
-      struct Exit {
-        std::atomic<int>& a;
-        ~Exit() { a.fetch_sub(1, std::memory_order_acq_rel); }
-      } exit_guard{sink_active_};
-      if (!running_.load(std::memory_order_acquire)) return;
-      for (auto& d : outs) {
-        const int wi = int((d.tag & ~ServeCore::kSinkTag) >> kWorkerShift);
-        if (wi < 0 || size_t(wi) >= workers_.size()) continue;
-        GrpcReply r;
-        if (!d.err.empty()) {
-          r.status = d.err.find("pb:") != std::string::npos ? 3 : 13;
-          r.message = d.err;
-        } else {
-          r.body = std::move(d.bytes);
-        }
-        workers_[size_t(wi)]->post(Worker::Done{d.tag & kTokenMask, 0, 0, std::move(r)});
-      }
-    });
-  }
+  gate_ = std::make_shared<SinkGate>();
+  gate_->srv = this;
+  // the sink holds the gate, not the server: a finisher that copied it before stop() finds the
+  // gate closed (srv null) instead of a destroyed server
+  auto sink = [gate = gate_](std::vector<ServeCore::Done>&& outs) {
+    std::shared_lock<std::shared_mutex> g(gate->mu);
+    if (gate->srv) gate->srv->route_done(std::move(outs));
+  };
+  if (core_) core_->set_sink(sink);
+  if (router_) router_->set_sink(sink);
   for (auto& w : workers_) threads_.emplace_back([p = w.get()] { p->run(); });
   for (int i = 0; i < n_cold_; ++i) threads_.emplace_back([this] { cold_loop(); });
   for (int i = 0; i < n_batch_; ++i) threads_.emplace_back([this] { batch_loop(); });
@@ -596,7 +681,11 @@ void GrpcServer::stop() {
   jcv_.notify_all();
   for (auto& w : workers_) w->stop.store(true);
   if (core_) core_->set_sink(nullptr);
-  while (sink_active_.load(std::memory_order_acquire) > 0) std::this_thread::yield();  // a finisher inside the sink
+  if (router_) router_->set_sink(nullptr);
+  if (gate_) {  // waits for sink calls in progress; later ones (copies taken earlier) see it closed
+    std::unique_lock<std::shared_mutex> g(gate_->mu);
+    gate_->srv = nullptr;
+  }
   for (auto& t : threads_)
     if (t.joinable()) t.join();
   threads_.clear();
@@ -605,7 +694,7 @@ void GrpcServer::stop() {
 
 void GrpcServer::post(int worker, uint64_t conn, int32_t stream, GrpcReply&& r) {
   if (worker < 0 || size_t(worker) >= workers_.size()) return;
-  workers_[size_t(worker)]->post(Worker::Done{0, conn, stream, std::move(r)});
+  workers_[size_t(worker)]->post(Worker::Done{0, conn, stream, std::move(r), false});
 }
 
 void GrpcServer::cold_loop() {
@@ -644,15 +733,27 @@ void GrpcServer::batch_loop() {
       const std::string_view v = core_->score_batch_view(j.body.data(), j.body.size(), -1, mono_ns());
       r.body.assign(v.data(), v.size());
     } catch (const std::exception& e) {
-      r.status = std::strstr(e.what(), "pb:") ? 3 : 13;
-      r.message = e.what();
+      if (std::strstr(e.what(), "pb:")) {
+        r.status = 3;
+        r.message = e.what();
+      } else {  // the core failed it: the cold table (engine fallback) answers instead
+        note_failure(e.what());
+        cold_n_.fetch_add(1, std::memory_order_relaxed);
+        try {
+          r = cold_(j.path + "#retry:" + e.what(), std::move(j.body));
+        } catch (const std::exception& e2) {
+          r.status = 13;
+          r.message = e2.what();
+        }
+      }
     }
     post(j.worker, j.conn, j.stream, std::move(r));
   }
 }
 
 GrpcServer::Stats GrpcServer::stats() const {
-  return Stats{calls_.load(), hot_tx_.load(), hot_batch_.load(), cold_n_.load(), errors_.load(), conns_.load()};
+  return Stats{calls_.load(), hot_tx_.load(), hot_batch_.load(), cold_n_.load(), errors_.load(), conns_.load(),
+               hot_acct_.load(), hot_fail_.load()};
 }
 
 // ---------------------------------------------------------------------------- load generator

@@ -8,12 +8,24 @@
 // (move-to-front on repeat). Memory is fixed at construction, an insert touches one or two
 // cache lines per table, and the batch insert prefetches the buckets of upcoming rows: it is
 // on the scoring hot path (every ScoreBatch / micro-batch), ~8192 rows per call.
+//
+// The tables live in a memory region: process-private, or node-shared (/dev/shm) so that every
+// rank of a one-process-per-GPU group records the traffic it ingests into ONE index and every
+// rank's CheckBonusAbuse sees the links of all of them (a device shared by accounts that reached
+// different ingress ranks). A spin lock in the region serialises writers and readers across the
+// processes (a batch insert holds it ~1 ms per 8192 rows; readers are single lookups).
 #pragma once
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstring>
-#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
 #include <vector>
+
+#include "shm.h"
 
 namespace igp {
 
@@ -21,32 +33,30 @@ class LinkIndex {
  public:
   static constexpr int kMaxPerKey = 16;
 
-  explicit LinkIndex(int per_key = 8, int64_t buckets = int64_t(1) << 18)
-      : per_key_(std::max(1, std::min(per_key, kMaxPerKey))) {
-    int64_t b = 1;
-    while (b < buckets) b <<= 1;
-    dev_.init(b);
-    acct_.init(b);
+  explicit LinkIndex(int per_key = 8, int64_t buckets = int64_t(1) << 18) { init(per_key, buckets, "", false); }
+  // node-shared index in /dev/shm/<name> (create: this process sizes it; the others map it)
+  LinkIndex(int per_key, int64_t buckets, const std::string& shm_name, bool create) {
+    init(per_key, buckets, shm_name, create);
   }
 
   void add(const uint64_t* dev, const int64_t* acct, size_t n) {
     constexpr size_t kAhead = 8;
-    std::lock_guard<std::mutex> g(mu_);
+    Guard g(hdr_->lock);
     for (size_t i = 0; i < n; ++i) {
       if (i + kAhead < n) {
         dev_.prefetch(dev[i + kAhead]);
         acct_.prefetch(akey(acct[i + kAhead]));
       }
       if (dev[i] == 0 || acct[i] < 0) continue;
-      ++clock_;
-      push(dev_.touch(dev[i], clock_), acct[i]);
-      push(acct_.touch(akey(acct[i]), clock_), int64_t(dev[i]));
+      const uint32_t now = ++hdr_->clock;
+      push(dev_.touch(dev[i], now, hdr_->dev_used), acct[i]);
+      push(acct_.touch(akey(acct[i]), now, hdr_->acct_used), int64_t(dev[i]));
     }
   }
 
   // accounts sharing at least one device with `acct` (excluding itself), most recent first
   std::vector<int64_t> linked(int64_t acct, size_t limit) const {
-    std::lock_guard<std::mutex> g(mu_);
+    Guard g(hdr_->lock);
     std::vector<int64_t> out;
     CEntry a;
     if (!acct_.find(akey(acct), a)) return out;
@@ -64,17 +74,62 @@ class LinkIndex {
   }
 
   std::vector<int64_t> devices_of(int64_t acct) const {
-    std::lock_guard<std::mutex> g(mu_);
+    Guard g(hdr_->lock);
     CEntry a;
     return acct_.find(akey(acct), a) ? std::vector<int64_t>(a.v, a.v + a.n) : std::vector<int64_t>{};
   }
 
   size_t n_devices() const {
-    std::lock_guard<std::mutex> g(mu_);
-    return dev_.used;
+    Guard g(hdr_->lock);
+    return size_t(hdr_->dev_used);
+  }
+  bool shared() const { return region_.shared_mapping(); }
+  void unlink_shared() { region_.unlink(); }
+
+  // insert tickets (process-local): a producer that queues an insert for later (the serving
+  // core's link thread) takes a ticket; a reader that must see every insert queued before it
+  // (CheckBonusAbuse's linked_accounts) waits until the tickets handed out before its own were
+  // completed
+  uint64_t ticket() const { return enq_.load(std::memory_order_acquire); }
+  void note_queued() { enq_.fetch_add(1, std::memory_order_acq_rel); }
+  void note_done() { done_.fetch_add(1, std::memory_order_acq_rel); }
+  bool wait_done(uint64_t ticket, int64_t timeout_us) const {
+    if (done_.load(std::memory_order_acquire) >= ticket) return true;
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
+    while (done_.load(std::memory_order_acquire) < ticket) {
+      if (std::chrono::steady_clock::now() >= t_end) return false;
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    return true;
   }
 
  private:
+  static constexpr uint64_t kMagic = 0x49475031494e4b31ULL;  // "IGP1INK1"
+  struct alignas(64) Hdr {
+    uint64_t magic;
+    int64_t buckets;
+    int32_t per_key;
+    std::atomic<uint32_t> lock;
+    uint32_t clock;
+    int32_t pad0;
+    uint64_t dev_used, acct_used;
+    char pad[16];
+  };
+  static_assert(sizeof(Hdr) == 64, "LinkIndex header must be one line");
+  // cross-process spin lock (the region's word); short critical sections
+  struct Guard {
+    std::atomic<uint32_t>& l;
+    explicit Guard(std::atomic<uint32_t>& x) : l(x) {
+      for (int spin = 0;; ++spin) {
+        uint32_t z = 0;
+        if (l.compare_exchange_weak(z, 1, std::memory_order_acquire, std::memory_order_relaxed)) return;
+        if (spin > 256) std::this_thread::sleep_for(std::chrono::microseconds(5));
+        else if (spin > 32) std::this_thread::yield();
+      }
+    }
+    ~Guard() { l.store(0, std::memory_order_release); }
+  };
+
   // table keys are never 0 (empty): device digests are non-zero, account keys are stored + 1
   static uint64_t akey(int64_t acct) { return uint64_t(acct) + 1; }
   // bucket = 4 key slots in one 64-byte line; the value lists live in a parallel array and are
@@ -98,13 +153,15 @@ class LinkIndex {
     int32_t n;
   };
   struct Table {
-    std::vector<Bucket> b;
-    std::vector<int64_t> vals;  // [buckets * 4][kMaxPerKey]
+    Bucket* b = nullptr;
+    int64_t* vals = nullptr;  // [buckets * 4][kMaxPerKey]
     uint64_t mask = 0;
-    size_t used = 0;
-    void init(int64_t buckets) {
-      b.assign(size_t(buckets), Bucket{});
-      vals.assign(size_t(buckets) * 4 * kMaxPerKey, 0);
+    static size_t bytes(int64_t buckets) {
+      return sizeof(Bucket) * size_t(buckets) + sizeof(int64_t) * size_t(buckets) * 4 * kMaxPerKey;
+    }
+    void map(char* base, int64_t buckets) {
+      b = reinterpret_cast<Bucket*>(base);
+      vals = reinterpret_cast<int64_t*>(base + sizeof(Bucket) * size_t(buckets));
       mask = uint64_t(buckets - 1);
     }
     static uint64_t mix(uint64_t k) {
@@ -122,7 +179,7 @@ class LinkIndex {
         }
       return false;
     }
-    Entry touch(uint64_t key, uint32_t now) {
+    Entry touch(uint64_t key, uint32_t now, uint64_t& used) {
       const size_t bi = mix(key) & mask;
       Key* k = b[bi].k;
       int victim = 0;
@@ -139,6 +196,28 @@ class LinkIndex {
       return Entry{k + victim, &vals[(bi * 4 + victim) * kMaxPerKey]};
     }
   };
+
+  void init(int per_key, int64_t buckets, const std::string& shm_name, bool create) {
+    int64_t nb = 1;
+    while (nb < buckets) nb <<= 1;
+    const size_t tb = Table::bytes(nb);
+    const size_t total = sizeof(Hdr) + 2 * tb;
+    const bool fresh = shm_name.empty() || create;
+    region_ = shm_name.empty() ? Region::anon(total) : Region::shared(shm_name, total, create);
+    char* base = static_cast<char*>(region_.base());
+    hdr_ = reinterpret_cast<Hdr*>(base);
+    if (fresh) {  // zero pages (anonymous / a fresh sparse file): empty tables
+      hdr_->buckets = nb;
+      hdr_->per_key = std::max(1, std::min(per_key, kMaxPerKey));
+      hdr_->magic = kMagic;
+    } else if (hdr_->magic != kMagic || hdr_->buckets != nb) {
+      throw std::runtime_error("LinkIndex: " + shm_name + " has another layout");
+    }
+    per_key_ = hdr_->per_key;
+    dev_.map(base + sizeof(Hdr), nb);
+    acct_.map(base + sizeof(Hdr) + tb, nb);
+  }
+
   void push(Entry en, int64_t x) {
     int32_t& n = en.n();
     for (int k = 0; k < n; ++k)
@@ -154,10 +233,12 @@ class LinkIndex {
     }
     en.v[n++] = x;
   }
-  int per_key_;
-  uint32_t clock_ = 0;
+
+  Region region_;
+  Hdr* hdr_ = nullptr;
+  int per_key_ = 8;
   Table dev_, acct_;
-  mutable std::mutex mu_;
+  std::atomic<uint64_t> enq_{0}, done_{0};
 };
 
 }  // namespace igp

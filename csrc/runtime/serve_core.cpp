@@ -175,6 +175,7 @@ void ServeCore::resolve_rows(std::vector<wire::TxRow>& rows, Item* it) {
     }
     std::lock_guard<std::mutex> g(l_mu_);
     if (lq_.size() < 16) {  // bounded: links are best-effort under overload
+      links_->note_queued();  // (a reader of linked accounts waits for the inserts queued before it)
       lq_.emplace_back(std::move(d), std::move(a));
       l_cv_.notify_one();
     }
@@ -364,9 +365,20 @@ int ServeCore::pending_items() {
 // ---------------------------------------------------------------------------- stepper
 // Takes rows from the FIFO into the next free slot and launches it. Called with q_mu_ held
 // (released around the copy into the pinned buffer and the device calls).
+// The pipeline slot the next step runs on, or -1 when it is busy. Exchange mode: slot =
+// step index % depth on EVERY rank (steps are issued in the same sequence everywhere), so a step
+// uses the same slot index on all ranks - the per-GPU D2H result path indexes its node-shared
+// region and generation flags by slot (with a free-slot stack, ranks released steps in
+// different orders and could run one step on different slots). Direct mode: any free slot.
+int ServeCore::next_slot_locked() const {
+  if (!exchange_) return free_slots_.empty() ? -1 : free_slots_.back();
+  const int s = int(issued_.load() % int64_t(depth_));
+  return std::find(free_slots_.begin(), free_slots_.end(), s) != free_slots_.end() ? s : -1;
+}
+
 bool ServeCore::issue_step(std::unique_lock<std::mutex>& lk, bool allow_empty) {
-  if (free_slots_.empty()) return false;
-  const int slot = free_slots_.back();
+  const int slot = next_slot_locked();
+  if (slot < 0) return false;
   Step* st = steps_[slot].get();
   st->slot = slot;
   st->segs.clear();
@@ -416,7 +428,7 @@ bool ServeCore::issue_step(std::unique_lock<std::mutex>& lk, bool allow_empty) {
     }
   }
   if (n == 0 && !allow_empty) return false;
-  free_slots_.pop_back();
+  free_slots_.erase(std::find(free_slots_.begin(), free_slots_.end(), slot));
   queued_rows_ -= n;
   ++inflight_;
   st->n = n;
@@ -501,7 +513,7 @@ void ServeCore::stepper_loop() {
         hold_since = now_ns();
       }
       if (peer_ahead) {
-        if (!free_slots_.empty()) {
+        if (next_slot_locked() >= 0) {
           issue_step(lk, true);
           continue;
         }
@@ -527,7 +539,7 @@ void ServeCore::stepper_loop() {
       q_cv_.wait_for(lk, std::chrono::microseconds(exchange_ ? 50 : 1000));
       continue;
     }
-    const bool slot = !free_slots_.empty();
+    const bool slot = next_slot_locked() >= 0;
     if (slot && (queued_rows_ > 0 || peer_ahead)) {
       const int64_t age = queue_.empty() ? 0 : now_ns() - queue_.front()->t_enq;
       if (peer_ahead || inflight_ == 0 || queued_rows_ >= full_rows || age >= max_wait) {
@@ -718,7 +730,10 @@ void ServeCore::link_loop() {
       job = std::move(lq_.front());
       lq_.pop_front();
     }
-    if (links_) links_->add(job.first.data(), job.second.data(), job.first.size());
+    if (links_) {
+      links_->add(job.first.data(), job.second.data(), job.first.size());
+      links_->note_done();
+    }
   }
 }
 
@@ -771,13 +786,13 @@ void ServeCore::abort() {
   }
   q_cv_.notify_all();
   // queued items never reach a step: fail them now (rows already in steps fail or finish with
-  // their steps)
+  // their steps). Unary failures go through deliver(): sink-tagged calls (the native gRPC
+  // server) reach their connection instead of the poll() queue nobody drains
+  std::vector<Done> unary;
   for (Item* it : dropped) {
     if (it->kind == 1) {
-      Done d{it->tag, std::string(), "ServeCore: aborted"};
+      unary.push_back(Done{it->tag, std::string(), "ServeCore: aborted"});
       delete it;
-      std::lock_guard<std::mutex> g(out_mu_);
-      outq_.push_back(std::move(d));
       continue;
     }
     std::lock_guard<std::mutex> g(it->m);
@@ -786,7 +801,7 @@ void ServeCore::abort() {
     it->aborted_rows = int64_t(it->n) - it->taken;
     it->cv.notify_one();
   }
-  out_cv_.notify_all();
+  deliver(std::move(unary));
   stop();
 }
 

@@ -184,6 +184,7 @@ class ServeCore {
   void enqueue(Item* it);
   void wait_item(Item* it);
   bool issue_step(std::unique_lock<std::mutex>& lk, bool allow_empty);
+  int next_slot_locked() const;
   void finish_seg(const Step& st, const Seg& s);
   void release_step_ref(Step* st);
   void resolve_rows(std::vector<wire::TxRow>& rows, Item* it);

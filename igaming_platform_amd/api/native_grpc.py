@@ -8,9 +8,17 @@ dlopen, one epoll loop per worker thread, SO_REUSEPORT listeners):
 * ScoreTransaction goes from the HTTP/2 DATA frame straight into the engine's serving core
   (C++ parse, AccountIndex, micro-batch FIFO) and back - no Python, no GIL;
 * ScoreBatch runs ``ServeCore.score_batch`` on native batch threads;
-* every other unary RPC (LTV, segments, bonus abuse, blacklist, features, thresholds,
-  grpc.health.v1 Check) calls the same :class:`RiskServicer` handlers as the Python server,
-  bytes in / bytes out, on native cold threads that take the GIL.
+* PredictLTV, GetPlayerSegment and CheckBonusAbuse go to the engine's native account router
+  (engine/acct.py, csrc/runtime/acct_core.cpp): C++ parse, owner routing, micro-batches on the
+  LTV chain / abuse step of the owner's GPU, response bytes written in C++ - no Python;
+* every other unary RPC (blacklist, features, thresholds, grpc.health.v1 Check) - and the three
+  above while the router is absent - calls the same :class:`RiskServicer` handlers as the Python
+  server, bytes in / bytes out, on native cold threads that take the GIL.
+
+A hot call that fails inside a native core (device error, step deadline) comes back through
+the cold table with its path suffixed ``#retry:<error>``: the engine marks the shard unhealthy
+(or fails the SPMD group over), so this call and the later ones are answered by the Python
+path and its fallback, and the watcher turns the hot flag off.
 
 While the engine must not take the native path (degraded shard, fault injection, audit-less
 fallback...) a watcher flips the server's hot flag and the scoring RPCs go through the
@@ -56,11 +64,13 @@ class NativeRiskServer:
         self._table = self._handlers()
         self._host, self._port_req, self._workers = host, port, workers
         core = getattr(engine, "core", None)
-        self.srv = native().GrpcServer(core, self._cold, int(cold_threads), int(batch_threads if core is not None else 0))
+        acct = getattr(engine, "acct", None)
+        self.srv = native().GrpcServer(core, self._cold, int(cold_threads), int(batch_threads if core is not None else 0),
+                                       acct=acct.router if acct is not None else None)
         self.port = 0
         self._stop = threading.Event()
         self._watch: Optional[threading.Thread] = None
-        self._seen = dict(hot_tx=0, hot_batch=0)
+        self._seen = dict(hot_tx=0, hot_batch=0, hot_acct=0)
 
     # ------------------------------------------------------------------ cold handler table
     def _handlers(self) -> Dict[str, Callable[[bytes], bytes]]:
@@ -81,6 +91,12 @@ class NativeRiskServer:
         return table
 
     def _cold(self, path: str, body: bytes):
+        if "#retry:" in path:  # a hot call the native path failed: fail the shard over, then serve it here
+            path, msg = path.split("#retry:", 1)
+            try:
+                self.engine.on_core_failure(msg)
+            except Exception:
+                log.error("core failure handling", exc_info=True)
         f = self._table.get(path)
         short = path.rsplit("/", 1)[-1]
         m = self.engine.metrics
@@ -120,7 +136,8 @@ class NativeRiskServer:
             try:
                 self.srv.set_hot(bool(e._native_ok()))
                 st = self.srv.stats()
-                for k, method in (("hot_tx", "ScoreTransaction"), ("hot_batch", "ScoreBatch")):
+                for k, method in (("hot_tx", "ScoreTransaction"), ("hot_batch", "ScoreBatch"),
+                                  ("hot_acct", "AccountRPC")):
                     d = int(st[k]) - self._seen[k]
                     if d > 0:
                         m.requests.labels(method=method, code="OK").inc(d)
@@ -169,6 +186,8 @@ class NativeIngressServer:
     serving core, every other unary RPC forwarded byte-for-byte to rank 0's internal port."""
 
     def __init__(self, node, upstream: str, port: int, host: str = "0.0.0.0", workers: int = 4):
+        # PredictLTV / GetPlayerSegment / CheckBonusAbuse: this rank's native account router
+        # (owner-routed over /dev/shm); the rest of the cold RPCs go to rank 0
         opts = [("grpc.max_receive_message_length", 64 << 20), ("grpc.max_send_message_length", 64 << 20)]
         self._up = grpc.insecure_channel(upstream, options=opts)
         self.upstream = upstream
@@ -176,10 +195,12 @@ class NativeIngressServer:
         self.health.set(P.SERVICE, "SERVING")
         self._calls: Dict[str, Callable] = {}
         self._host, self._port_req, self._workers = host, port, workers
-        self.srv = native().GrpcServer(node.core, self._cold, 4, 8)
+        acct = getattr(node, "acct", None)
+        self.srv = native().GrpcServer(node.core, self._cold, 4, 8, acct=acct.router if acct is not None else None)
         self.port = 0
 
     def _cold(self, path: str, body: bytes):
+        path = path.split("#retry:", 1)[0]  # a failed hot call: rank 0 answers it on its Python path
         if path == f"/{HV.SERVICE}/Check":
             try:
                 return self.health.Check(HV.HealthCheckRequest.FromString(body), _Ctx()).SerializeToString()

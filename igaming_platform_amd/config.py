@@ -147,6 +147,10 @@ class GPUConfig:
     serve_depth: int = 3          # pipeline slots (batches in flight) of a shard's device
     serve_finishers: int = 2      # unary response threads
     exchange_timeout_s: float = 10.0  # multi-rank step deadline: a peer that misses it failed
+    # native account RPCs (csrc/runtime/acct_core.cpp, engine/acct.py): PredictLTV,
+    # GetPlayerSegment, CheckBonusAbuse micro-batched on the owner's model devices
+    native_acct: bool = True
+    acct_depth: int = 2           # pipeline slots of each account-model device
 
 
 @dataclass
@@ -238,6 +242,9 @@ class Config:
         ns = env.get("RISK_NATIVE_SERVING")
         if ns not in (None, ""):
             self.gpu.native_serving = ns.strip().lower() not in ("0", "false", "no", "off")
+        na = env.get("RISK_NATIVE_ACCT")
+        if na is not None:
+            self.gpu.native_acct = na.strip().lower() not in ("0", "false", "no", "off")
         lt = env.get("RISK_LOG_TRANSFORM")
         if lt:
             self.features.log_transform = lt

@@ -100,6 +100,8 @@ class DpGpuScorer(GpuScorer):
     """GpuScorer whose batches arrive through the exchange. ``cbuckets``: chunk capacities
     (rows per owner per sender); the scorer graphs run ``senders * C`` rows."""
 
+    fenc_to_host = False  # the result all-to-all carries the device feature images to the senders
+
     def __init__(self, cfg, store, comms: Sequence, world: int, rank: int, senders: int,
                  cbuckets: Sequence[int], plan=None, model: str = "plan", device=None, pipeline_depth: int = 3,
                  update_features: bool = True, results_shm: Optional[str] = None):

@@ -97,6 +97,8 @@ class PlayerTable:
             rows = self.rows[owner][s].copy()
             ext = self.ext[owner][s].copy() if self.ext[owner] is not None else None
         rows[~present] = 0
+        if ext is not None:
+            ext[~present] = 0  # an empty profile has no extra features either (the device gathers zeros)
         return rows, present, ext
 
 
@@ -127,7 +129,6 @@ class LtvGpu:
         # nodes, profiles/r2/direct3)
         self.direct = os.environ.get("IGP_LTV_DIRECT", "0") == "1" and not (
             plan is not None and any(st.kind == "gru" for st in plan.steps))
-        self._pull_copy = os.environ.get("IGP_PULL_COPY", "0") == "1"
         self.chain = None
         # the fused chain (mlp_fused.hip): bf16 plans as bf16 MFMA, fp32 plans in its split
         # mode (bf16 hi/lo pairs, three MFMAs per product: f32-faithful); IGP_MLP_SPLIT=0 sends
@@ -190,7 +191,7 @@ class LtvGpu:
     # ---- the step
     def _body(self, slot: int, b: int) -> None:
         K = self.K
-        cp = K.pull_copy if self._pull_copy else K.memcpy_async
+        cp = K.memcpy_async
         if not self._host_in:
             cp(self.dev_slab, self.host[slot], 16 + 4 * b)
         nout = b * self.out.shape[1] * self.out.element_size()
@@ -288,31 +289,10 @@ class LtvGpu:
         slot, n, ev = p
         try:
             ev.synchronize()
-            out = self.host_out[slot][:n].numpy().copy()
-            if self.chain is not None and self.chain.pair_ok and n and np.isnan(out).any():
-                out = self._pair_fallback(slot, n)
-            return out
+            return self.host_out[slot][:n].numpy().copy()
         finally:
             if release:
                 self._slot_locks[slot].release()
-
-    def _pair_fallback(self, slot: int, n: int) -> np.ndarray:
-        """A pair-cluster launch gave up (its two workgroups were not co-resident): switch the
-        chain to the one-workgroup kernel, re-capture, and recompute the batch."""
-        torch = self.torch
-        log.error("LTV chain: pair kernel timed out; falling back to the one-workgroup kernel")
-        with self._lock:
-            torch.cuda.synchronize(self.device)
-            self.chain.disable_pair()
-            b = self.bucket_for(max(n, 1))
-            self._use(slot)
-            with torch.cuda.stream(self.stream):
-                self._body(slot, b)
-            self.stream.synchronize()
-            out = self.host_out[slot][:n].numpy().copy()
-            self.graphs.clear()
-            self.capture()
-        return out
 
     def predict_slots(self, slots: np.ndarray) -> np.ndarray:
         """slots -> [n, 6] (ltv, churn, survival, confidence, segment, nba)."""
@@ -321,14 +301,24 @@ class LtvGpu:
 
 
 class LtvService:
+    """``gpu``: the LtvGpu of each local owner (indexed owner % len). ``group`` (SPMD rank 0): the
+    rows and predictions of accounts owned by other ranks go to their rank (OP_LTVROWS / OP_LTV
+    over the control plane); ``rank``: the owner this process holds (SPMD)."""
+
     def __init__(self, registry, world: int = 1, gpu: Optional[List[LtvGpu]] = None, executor=None,
-                 model_width: int = 0, output_name: str = "output", input_name: str = "input"):
+                 model_width: int = 0, output_name: str = "output", input_name: str = "input", group=None,
+                 rank: Optional[int] = None):
         self.registry = registry
         self.table = PlayerTable(registry.capacity, world, ext_width=max(model_width - N_COLS, 0))
         self.gpu = gpu
         self.executor = executor
         self.model_width = model_width
         self.input_name, self.output_name = input_name, output_name
+        self.group = group
+        self.rank = rank
+
+    def _remote(self, o: int) -> bool:
+        return self.group is not None and self.rank is not None and int(o) != self.rank
 
     def set_players(self, account_ids: Sequence[str], features: Sequence[GL.PlayerFeatures],
                     ext: Optional[np.ndarray] = None) -> None:
@@ -337,12 +327,30 @@ class LtvService:
         self.set_rows(slots, owners, rows, ext)
 
     def set_rows(self, slots: np.ndarray, owners: np.ndarray, rows: np.ndarray, ext=None) -> None:
+        slots, owners = np.asarray(slots, np.int32), np.asarray(owners, np.int32)
+        rows = np.asarray(rows, np.float32).reshape(-1, N_COLS)
+        if self.group is not None and self.rank is not None:
+            remote = (owners != self.rank) & (slots >= 0)
+            if remote.any():  # every rank applies the rows it owns (one control-plane op)
+                self.group.ltv_rows(slots[remote], owners[remote], rows[remote],
+                                    None if ext is None else np.asarray(ext, np.float32)[remote])
         for o in np.unique(owners):
+            if self._remote(o):
+                continue
             sel = np.nonzero((owners == o) & (slots >= 0))[0]
             e = None if ext is None else np.asarray(ext)[sel]
             self.table.set(int(o), slots[sel], rows[sel], e)
             if self.gpu is not None:
                 self.gpu[int(o) % len(self.gpu)].set_rows(slots[sel], rows[sel], e)
+
+    def predict_owner_slots(self, o: int, slots: np.ndarray):
+        """[n, 6] rows (ltv, churn, survival, confidence, segment, nba) of owner ``o``'s ``slots``
+        on this process's shard, and the profile-present mask."""
+        rows, present, ext = self.table.get(int(o), np.asarray(slots, np.int32), with_rows=self.gpu is None)
+        if self.gpu is not None:
+            return self.gpu[int(o) % len(self.gpu)].predict_slots(np.where(present, slots, -1)), present
+        X = ltv_model_input(rows, ext, self.model_width) if self.model_width else None
+        return self._cpu(rows, X), present
 
     def predict(self, account_ids: Sequence[str]) -> List[LtvResult]:
         slots, owners = self.registry.resolve_ids(list(account_ids), insert=False)
@@ -350,12 +358,10 @@ class LtvService:
         nba = GL.NBA_CODES
         for o in np.unique(owners):
             sel = np.nonzero(owners == o)[0]
-            rows, present, ext = self.table.get(int(o), slots[sel], with_rows=self.gpu is None)
-            if self.gpu is not None:
-                res = self.gpu[int(o) % len(self.gpu)].predict_slots(np.where(present, slots[sel], -1))
+            if self._remote(o):
+                res, present = self.group.ltv_predict(slots[sel], np.full(len(sel), o, np.int32))
             else:
-                X = ltv_model_input(rows, ext, self.model_width) if self.model_width else None
-                res = self._cpu(rows, X)
+                res, present = self.predict_owner_slots(int(o), slots[sel])
             # columns -> Python scalars in bulk (tolist) before building the per-account results
             ltv, churn, surv, conf = (res[:, c].astype(np.float64).tolist() for c in (0, 1, 2, 3))
             seg, act = res[:, 4].astype(np.int64).tolist(), res[:, 5].astype(np.int64).tolist()

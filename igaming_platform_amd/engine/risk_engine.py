@@ -145,7 +145,7 @@ class RiskEngine:
             local = node.local
             self.local = local
             self.core = node.core
-            self.core.set_links(self.links)
+            self.links = node.links  # node-shared: links recorded by every rank's ingress
             self.auditlog = node.audit  # the node's core writes its native ring
             self._audit_evicted_seen = 0
             from . import serving
@@ -198,7 +198,9 @@ class RiskEngine:
                 g.capture()
                 lg = [g]
             self.ltv = LtvService(self.registry, world, gpu=lg, model_width=ltv_width,
-                                  executor=N.Executor(lm) if (lm is not None and lg is None) else None)
+                                  executor=N.Executor(lm) if (lm is not None and lg is None) else None,
+                                  group=self.group, rank=0)
+            self.group.runner.ltv = self.ltv
             self.abuse = AbuseService(self, threshold=cfg.abuse.threshold, group=self.group,
                                       executor=N.Executor(am) if (am is not None and backend != "gpu") else None,
                                       group_model=am is not None and backend == "gpu")
@@ -226,6 +228,12 @@ class RiskEngine:
                                   model_width=ltv_width)
             self.abuse = AbuseService(self, threshold=cfg.abuse.threshold,
                                       executor=N.Executor(am) if am is not None else None)
+        # ---- native account RPCs (engine/acct.py, csrc/runtime/acct_core.cpp): PredictLTV,
+        # GetPlayerSegment and CheckBonusAbuse bytes -> bytes without Python, micro-batched on this
+        # process's model devices (SPMD: the node's router, owner-routed over /dev/shm)
+        self.acct = None
+        if cfg.gpu.native_acct and backend != "golden" and (spmd is not None or (world == 1 and cfg.gpu.native_serving)):
+            self._attach_acct(spmd is not None, am)
         self.started_at = time.time()
         if self.group is not None:
             self.group.start_heartbeat()
@@ -257,6 +265,40 @@ class RiskEngine:
         drained by :meth:`flush_audit` next to the Python rings."""
         attach_audit_ring(self.auditlog, self.cfg, core, indexes, int(self.model_version))
         self._audit_evicted_seen = 0
+
+    def _attach_acct(self, spmd: bool, am) -> None:
+        from . import acct as A
+        try:
+            if spmd:
+                acct = self.node.acct
+                local, owner = self.local, 0
+            else:
+                acct = A.NativeAcct([self.registry.index[0]])
+                local, owner = self.backends[0], 0
+            plan = A.abuse_device_plan(self.cfg, am, local.device) if (am is not None and local.kind == "gpu") else None
+            A.attach_models(acct, self.cfg, local, ltv=self.ltv, owner=owner, abuse_model=am, abuse_plan=plan,
+                            audit=self.auditlog.enabled, rank=0)
+            acct.router.set_links(self.links)
+            self.acct = acct
+            if spmd:
+                self.group.runner.acct = acct
+        except Exception as e:  # the Python path keeps serving these RPCs
+            log.error("native account RPCs unavailable", extra={"fields": dict(error=str(e))})
+            self.acct = None
+
+    def on_core_failure(self, msg: str) -> None:
+        """A hot call failed inside a native core (device error / deadline): the same handling
+        as :meth:`score_batch_bytes` - the group fails over (SPMD) or the shard is marked
+        unhealthy, so later calls take the Python path with its fallback."""
+        e = RuntimeError(f"native serving failure: {msg}")
+        g = self.group
+        if g is not None:
+            try:
+                g.fail(e)
+            except Exception:  # GroupFailure: the failover runs in _group_failed
+                pass
+        else:
+            self._mark_unhealthy(0, e)
 
     def _native_ok(self) -> bool:
         """Whether a request may take the all-native path (the Python path keeps fault
@@ -705,12 +747,16 @@ class RiskEngine:
 
     def _push_config(self) -> None:
         if self.group is not None:
-            self.backends[0].refresh_config(self.scoring)
+            self.backends[0].refresh_config(self.scoring)  # every rank's runner refreshes its router too
             return
         for be in self.backends:
             be.refresh_config(self.scoring)
         if self.fallback is not None:
             self.fallback.refresh_config(self.scoring)
+        acct = getattr(self, "acct", None)
+        if acct is not None:
+            acct.set_abuse(self.scoring, self.cfg.abuse.threshold)
+            acct.refresh()
 
     # ---- blacklist (risk.proto:151-181; redis_store.go:251-293)
     def add_to_blacklist(self, type_: str, value: str, reason: str = "", created_by: str = "",
@@ -878,6 +924,8 @@ class RiskEngine:
     # ---- health / durability
     def close(self) -> None:
         """Release the SPMD workers (rank 0 only) and stop the serving core."""
+        if getattr(self, "acct", None) is not None:
+            self.acct.stop()
         if self.group is not None:
             self.group.stop()  # also stops this rank's core (every rank converges)
             self.group = None
@@ -1028,14 +1076,45 @@ def make_abuse_gpu(cfg: Config, local, abuse_model):
     return g
 
 
+def worker_acct(cfg: Config, node, ltv_model=None, abuse_model=None):
+    """A worker rank's LTV shard (the profile rows of the accounts it owns) and its native
+    account-RPC router with the LTV / abuse devices attached. Returns (ltv, acct or None)."""
+    from .ltv import LtvGpu, LtvService
+    lm = _load_onnx(ltv_model if ltv_model is not None else cfg.ltv_model.path)
+    am = _load_onnx(abuse_model if abuse_model is not None else cfg.abuse_model.path)
+    width = int(lm.inputs()[0][2][-1]) if lm is not None else 0
+    local = node.local
+    gpu = None
+    if local.kind == "gpu":
+        from ..models.plan import compile_onnx, to_device
+        lp = to_device(compile_onnx(lm), str(local.device), cfg.ltv_model.precision) if lm is not None else None
+        g = LtvGpu(str(local.device), node.registry.capacity, lp, buckets=cfg.gpu.buckets, in_width=width)
+        g.capture()
+        gpu = [g]
+    ltv = LtvService(node.registry, node.world, gpu=gpu, model_width=width, rank=node.rank,
+                     executor=native().Executor(lm) if (lm is not None and gpu is None) else None)
+    acct = node.acct if cfg.gpu.native_acct else None
+    if acct is not None:
+        from . import acct as A
+        try:
+            plan = A.abuse_device_plan(cfg, am, local.device) if (am is not None and local.kind == "gpu") else None
+            A.attach_models(acct, cfg, local, ltv=ltv, owner=node.rank, abuse_model=am, abuse_plan=plan,
+                            audit=bool(cfg.server.audit_db), rank=node.rank)
+        except Exception as e:
+            log.error("native account RPCs unavailable on this rank", extra={"fields": dict(error=str(e))})
+            acct = None
+    return ltv, acct
+
+
 def serve_shard(cfg: Config, comm, backend: str = "gpu", capacity: Optional[int] = None, fraud_model=None,
-                abuse_model=None, capture: bool = True, ingress=None, on_node=None):
+                abuse_model=None, capture: bool = True, ingress=None, on_node=None, ltv_model=None):
     """Worker rank (>= 1) of an SPMD group: build the same local shard as rank 0 and serve
     its cold ops until rank 0 stops the group; ``ingress(node)``, when given, runs this rank's
     own traffic through its serving core on a thread meanwhile. Returns (ops served, rows
     this shard scored)."""
     from ..parallel.spmd import run_worker
     node = worker_node(cfg, comm, backend, capacity, fraud_model, capture)
+    ltv, acct = worker_acct(cfg, node, ltv_model, abuse_model)
     started = on_node(node) if on_node is not None else None  # e.g. this rank's gRPC listener
     if ingress is not None:  # this rank's own traffic, beside the cold-op loop
         import threading
@@ -1043,7 +1122,8 @@ def serve_shard(cfg: Config, comm, backend: str = "gpu", capacity: Optional[int]
         th.start()
     abuse_gpu = make_abuse_gpu(cfg, node.local, abuse_model if abuse_model is not None else cfg.abuse_model.path)
     try:
-        out = run_worker(comm, node.local, abuse_gpu, node.core)
+        out = run_worker(comm, node.local, abuse_gpu, node.core, ltv=ltv, acct=acct,
+                         abuse_threshold=cfg.abuse.threshold)
     finally:
         if started is not None and hasattr(started, "stop"):
             started.stop(1.0)
@@ -1119,6 +1199,13 @@ class SpmdNode:
         def regions(create: bool):
             reg = AccountRegistry(capacity, world, shm_prefix=prefix, create=create)
             clock = native().StepClock(f"{prefix}-clock", world, rank, create)
+            # the account-RPC mailbox (engine/acct.py): PredictLTV / GetPlayerSegment /
+            # CheckBonusAbuse of accounts another rank owns travel to it over /dev/shm
+            from .acct import NativeAcct
+            self.acct = NativeAcct(reg.index, rank, f"{prefix}-acct", create) if backend != "golden" else None
+            # the device <-> account link index every rank's ingress records into and every
+            # rank's CheckBonusAbuse reads (linked_accounts across ingress ranks)
+            self.links = native().LinkIndex(8, 1 << 18, f"{prefix}-links", create)
             if self.local.kind == "gpu":
                 dev = self.local.native_device()
             else:
@@ -1134,6 +1221,9 @@ class SpmdNode:
         if rank == 0:
             self.registry.unlink_shared()
             self.clock.unlink_shared()
+            if self.acct is not None:
+                self.acct.router.unlink_shared()
+            self.links.unlink_shared()
             if hasattr(dev, "unlink_shared"):
                 dev.unlink_shared()
             if rshm:  # every rank mapped it while building its shard (before the barriers)
@@ -1143,6 +1233,9 @@ class SpmdNode:
                     pass
         seq0 = self.local.scorer._seq if self.local.kind == "gpu" else 0
         self.core = serving.make_core(self.registry.index, dev, cfg, rank=rank, clock=self.clock, seq0=seq0)
+        self.core.set_links(self.links)
+        if self.acct is not None:
+            self.acct.router.set_links(self.links)
         self.local.attach_core(self.core)
         self.cfg = cfg
         # risk_scores audit of the rows this rank ingests (each rank drains its own ring)

@@ -71,6 +71,11 @@ def _destroy_cu_streams() -> None:
 
 
 _FEAT_ENC = os.environ.get("IGP_FEAT_ENC", "1") != "0"
+# K1 stores each row's 128-B feature image straight into the slot's pinned host buffer (one
+# coalesced store per row through the fabric) instead of device memory + a D2H copy on the model
+# stream: that copy ran as a 20 us blit kernel per serving step. The
+# exchange scorer (engine/dp.py) keeps the device image: its all-to-all sends it to the sender.
+_FEAT_HOST = os.environ.get("IGP_FEAT_HOST", "1") != "0"
 
 class _Slot:
     """Device buffers of one pipeline slot (slab, model input/output, results)."""
@@ -88,6 +93,8 @@ class Pending:
 
 
 class GpuScorer:
+    fenc_to_host = _FEAT_HOST  # K1 writes the D2H feature images into host_feat[slot] directly
+
     def __init__(self, cfg: Config, store, plan: Optional[Plan] = None, model: str = "plan",
                  device=None, pipeline_depth: int = 2, update_features: bool = True,
                  use_graphs: Optional[bool] = None, owner_filter: bool = False, rank: int = 0):
@@ -103,7 +110,6 @@ class GpuScorer:
             model = "none"
         self.model = model
         self.update_features = update_features
-        self._pull_copy = os.environ.get("IGP_PULL_COPY", "0") == "1"
         self.direct = False
         self.serial = False
         self.use_graphs = cfg.gpu.use_graphs if use_graphs is None else use_graphs
@@ -265,8 +271,7 @@ class GpuScorer:
     def _copy_body(self, slot: int, bucket: int) -> None:
         sb = self.slots[slot]
         nbytes = HDR_BYTES + REQ_BYTES * bucket
-        # IGP_PULL_COPY=1: a kernel on the copy stream pulls the slab from pinned memory
-        (K.pull_copy if self._pull_copy else K.memcpy_async)(sb.dev_slab, self.host_slab[slot], nbytes)
+        K.memcpy_async(sb.dev_slab, self.host_slab[slot], nbytes)
         if self.update_features:
             K.dedup_insert(self.store, self.cfg_dev, sb.req, bucket, sb.hdr)
 
@@ -276,7 +281,7 @@ class GpuScorer:
         sb, upd = self.slots[slot], self.update_features
         if part in ("all", "k1"):
             K.feature_assemble(self.store, sb.hdr, self.cfg_dev, sb.req, sb.X, sb.feat, bucket, dedup=upd,
-                               fenc=sb.fenc)
+                               fenc=self._fenc_out(slot))
         if upd and part in ("all", "update"):
             K.update_segments(self.store, self.cfg_dev, sb.req, bucket, sb.hdr)
 
@@ -295,9 +300,17 @@ class GpuScorer:
             K.ensemble(sb.hdr, self.cfg_dev, sb.feat, sb.X, ml, sb.res, bucket, self.metrics, host_out=host)
         if host is None:
             K.memcpy_async(self.host_res[slot], sb.res, bucket * sb.res[0].numel() * sb.res.element_size())
-        if with_features:
+        if with_features and not self._fenc_host():
             img = sb.fenc if sb.fenc is not None else sb.feat
             K.memcpy_async(self.host_feat[slot], img, bucket * img[0].numel() * img.element_size())
+
+    def _fenc_host(self) -> bool:
+        return self.fenc_to_host and _FEAT_ENC
+
+    def _fenc_out(self, slot: int):
+        """Where K1 writes the slot's feature images: the pinned host rows (default) or the
+        slot's device buffer (copied by the model stage when features are requested)."""
+        return self.host_feat[slot] if self._fenc_host() else self.slots[slot].fenc
 
     def capture(self) -> None:
         """Capture the copy, state, model and model+features graphs per (bucket, pipeline
@@ -372,99 +385,6 @@ class GpuScorer:
             if os.environ.get("IGP_ASYNC_SUBMIT", "0") == "1":
                 d.set_async(True)
             self.driver = d
-
-    # ------------------------------------------------------------------ streaming (one launch per batch)
-    def capture_pipelined(self) -> None:
-        """Streaming mode: per bucket, three graphs; graph p runs copy(slot p) || state(slot
-        p-1) || model(slot p-2) on three forked capture streams, so a saturated stream costs
-        ONE hipGraphLaunch per micro-batch instead of three launches plus six event operations
-        (the host, not the GPU, bounded the three-graph pipeline: tools/host_probe.py).
-        Ordering is the graph sequence itself: launch p+1 starts after every branch of
-        launch p, which gives copy(q) -> state(q) -> model(q) and store updates in batch
-        order; dedup regions rotate as in the three-stream mode (K1 of batch q clears the
-        region of q+2, which no branch of its launch touches)."""
-        if self.depth != 3:
-            raise ValueError("streaming mode needs pipeline_depth=3")
-        if not self.graphs:
-            self.capture()  # eager warm-up of every body
-        dev = self.device
-        s0, s1, s2 = self.cstream, self.stream, self.mstream  # no extra streams (hardware queues)
-        self.pstream = s0
-        self.pgraphs: Dict[tuple, object] = {}
-        with torch.cuda.device(dev):
-            for b in self.buckets:
-                for p in range(3):
-                    g = torch.cuda.CUDAGraph()
-                    s0.wait_stream(torch.cuda.current_stream())
-                    with K.graph_capture(g, s0):
-                        s1.wait_stream(s0)
-                        s2.wait_stream(s0)
-                        self._copy_body(p, b)
-                        with torch.cuda.stream(s1):
-                            self._state_body((p + 2) % 3, b)
-                        with torch.cuda.stream(s2):
-                            self._model_body((p + 1) % 3, b)
-                        s0.wait_stream(s1)
-                        s0.wait_stream(s2)
-                    self.pgraphs[(b, p)] = g
-            torch.cuda.synchronize(dev)
-        self._pstep = 0
-        self._pev: collections.deque = collections.deque()   # (step, event) of launches in flight
-        self._pbatch: Dict[int, tuple] = {}                   # step -> (n, bucket, t_submit)
-
-    def pipe_reserve(self, max_inflight: int = 2):
-        """Wait until at most ``max_inflight - 1`` launches are in flight, so the next step's
-        slot (its pinned slab last read by launch p-3) may be packed. Returns (slot, the
-        completions that wait produced: (n, result rows, latency_ms) per finished batch)."""
-        p = self._pstep
-        done = []
-        while self._pev and self._pev[0][0] <= p - max_inflight:
-            done += self.pipe_launch_wait()
-        return p % 3, done
-
-    def pipe_launch(self, n: int, now: int) -> None:
-        """Launch streaming step p: batch p's rows are packed in ``slab_view(p % 3, n)`` after
-        :meth:`pipe_reserve`; n = 0 launches an empty batch (drain)."""
-        p = self._pstep
-        slot = p % 3
-        b = self.bucket_for(max(n, 1))
-        # one launch runs three batches' stages: the largest of their buckets (padded rows are inert)
-        for q in (p - 1, p - 2):
-            if q in self._pbatch:
-                b = max(b, self._pbatch[q][1])
-        self._seq += 1
-        self._write_hdr(slot, n, now)
-        with torch.cuda.stream(self.pstream):
-            self.pgraphs[(b, slot)].replay()
-            ev = torch.cuda.Event()
-            ev.record(self.pstream)
-        self._pev.append((p, ev))
-        if n > 0:
-            self._pbatch[p] = (n, b, time.perf_counter())
-        self._pstep = p + 1
-        self.batches += 1
-
-    def pipe_drain(self):
-        """Two empty launches finish the batches in flight; returns their completions."""
-        done = []
-        for _ in range(2):
-            done += self.pipe_reserve()[1]
-            self.pipe_launch(0, 0)
-        while self._pev:
-            done += self.pipe_launch_wait()
-        return done
-
-    def pipe_launch_wait(self):
-        q, ev = self._pev.popleft()
-        ev.synchronize()
-        t = time.perf_counter()
-        out = []
-        bq = q - 2  # launch q finished batch q-2
-        if bq in self._pbatch:
-            nb, _, ts = self._pbatch.pop(bq)
-            # a copy: the pinned rows are overwritten by batch bq+3's D2H
-            out.append((nb, self.host_res[bq % 3][:nb].numpy().copy(), (t - ts) * 1e3))
-        return out
 
     def bucket_for(self, n: int) -> int:
         for b in self.buckets:

@@ -11,7 +11,7 @@ import contextlib
 
 import os
 
-from typing import Dict, Optional
+from typing import Optional
 
 import torch
 
@@ -70,16 +70,6 @@ def graph_capture(g, stream):
             gc.enable()
 
 
-def pull_copy(dst: torch.Tensor, src: torch.Tensor, nbytes: int) -> None:
-    """Copy ``nbytes`` with a kernel on the current stream that reads / writes the pinned host
-    side directly (csrc/kernels/copy.hip): no DMA-engine hand-off; recordable."""
-    if nbytes > dst.numel() * dst.element_size() or nbytes > src.numel() * src.element_size():
-        raise ValueError("pull_copy: nbytes exceeds a tensor")
-    if not (dst.is_contiguous() and src.is_contiguous()):
-        raise ValueError("pull_copy: tensors must be contiguous")
-    _mod().pull_copy(dst.data_ptr(), src.data_ptr(), int(nbytes), _stream())
-
-
 class Recorder:
     """``with Recorder() as r: body()`` -> ``r.ops``: the body's launches as a native op list
     (nothing runs on the device while recording)."""
@@ -132,7 +122,9 @@ def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch
     batch first; K1 then applies each single-event account's event and opens the segments
     that :func:`update_segments` applies afterwards (dedup ring region by batch seq).
     ``fenc`` [rows, 32] int32: each row's 128-byte D2H feature image - the raw FeatRec, or the
-    encoded risk.v1 FeatureVector body for rows whose ReqRec.tx_type carries FV_ENC_BIT."""
+    encoded risk.v1 FeatureVector body for rows whose ReqRec.tx_type carries FV_ENC_BIT. A pinned
+    host tensor is written through the fabric (one coalesced 128-B store per row), so the image
+    needs no D2H copy."""
     dev = store.device
     if X.dim() != 2 or X.shape[1] < 30 + store.ext_width:
         raise ValueError("X must be [rows, >= 30 + ext_width]")
@@ -149,7 +141,7 @@ def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch
         hll_lc=_need(store.hll_lc, "hll_lc", torch.int32, 257),
         X=_need(X, "X", torch.float32, X.shape[1] * n_rows, dev),
         feat=_need(feat, "feat", torch.int32, 32 * n_rows, dev),
-        fenc=_need(fenc, "fenc", torch.int32, 32 * n_rows, dev) if fenc is not None else None,
+        fenc=_host_or_dev(fenc, "fenc", 32 * n_rows, dev, torch.int32),
         dbuf=_need(store.dbuf, "dbuf", torch.int32) if dedup else None, dcap=int(store.dcap), dmax=int(store.dmax),
         x_stride=int(X.shape[1]), ring_size=int(store.ring_ts.shape[1]), n_rows=int(n_rows),
         trace=_opt(trace, "trace", dtype=torch.int64, min_numel=64, device=dev),
@@ -548,8 +540,6 @@ class GruPack:
 
 
 _GRU_WS = os.environ.get("IGP_GRU_WS", "1") != "0"  # 0: always the batch-parallel K4 (A/B runs)
-# 1: the cluster kernel runs its 128 sequences as two software-pipelined halves (gru_ws.hip SPLIT)
-_GRU_SPLIT = os.environ.get("IGP_GRU_SPLIT", "0") == "1"
 # default cluster layout: 1 one 128-row cluster per CU, 3 two 64-row clusters per CU
 _GRU_WS_MODE = int(os.environ.get("IGP_GRU_WS_MODE", "3"))
 
@@ -561,9 +551,9 @@ def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh
     """K4. Input either dense ``X`` f32 [T, rows, I] or the store's event rings for ``slots``.
     ``ws``: 0 the batch-parallel kernel; 1 the weight-stationary cluster kernel when the model
     shape allows it; 2 the same with its two-half hand-off pipeline; 3 two 64-row clusters per
-    CU (gru_ws2_kernel); None: IGP_GRU_WS_MODE (3), or 2 under IGP_GRU_SPLIT=1."""
+    CU (gru_ws2_kernel); None: IGP_GRU_WS_MODE (3)."""
     if ws is None:
-        ws = 2 if _GRU_SPLIT else _GRU_WS_MODE
+        ws = _GRU_WS_MODE
     if ws not in (0, 1, 2, 3):
         raise ValueError("gru: ws must be 0..3")
     dev = gp.device
@@ -663,44 +653,6 @@ class MlpChainPack:
         self.in_live = steps[0].k
         self.in_w = self.layers[0]["K"]
         self.device = dev
-        # pair-cluster form (csrc/kernels/mlp_pair.hip, IGP_MLP_PAIR=1): two CUs per 128 rows,
-        # each streaming half of every layer's weights; bf16 chains whose layers are all 512
-        # wide. Off by default: its per-layer L2 hand-offs cost more than the weight bytes it
-        # saves (profiles/NOTES.md, round 3 late). One workspace per key (the LTV pipeline's
-        # slots run concurrently on their own streams).
-        self.pair_ok = (not self.split and all(l["N"] == 512 for l in self.layers)
-                        and os.environ.get("IGP_MLP_PAIR", "0") == "1")
-        self._pair: Dict[int, dict] = {}
-        self._pair_old = []  # superseded workspaces stay alive: captured graphs keep their pointers
-        self.pair_err = torch.zeros(1, dtype=torch.int32, device=dev) if self.pair_ok else None
-
-    def pair_workspace(self, n_rows: int, key: int = 0):
-        """Hand-off slabs / counters / head partials of the pair kernel for ``n_rows`` (grow-only)."""
-        if not self.pair_ok:
-            return None
-        ncl = -(-int(n_rows) // 128)
-        w = self._pair.get(key)
-        if w is None or w["clusters"] < ncl:
-            if w is not None:
-                self._pair_old.append(w)
-            dev = self.device
-            w = dict(clusters=ncl, x=torch.zeros(ncl * 4 * 128 * 256, dtype=torch.int16, device=dev),
-                     sync=torch.zeros(ncl * 16, dtype=torch.int32, device=dev),
-                     part=torch.zeros(ncl * 2 * 128, dtype=torch.float32, device=dev))
-            self._pair[key] = w
-        return w
-
-    def pair_failed(self) -> bool:
-        return bool(self.pair_err is not None and int(self.pair_err.item()) != 0)
-
-    def disable_pair(self) -> None:
-        """After a pair launch gave up (its workgroups were not co-resident): counters back to 0
-        and every later launch on the one-workgroup kernel (callers re-capture their graphs)."""
-        self.pair_ok = False
-        for w in list(self._pair.values()) + self._pair_old:
-            w["sync"].zero_()
-        if self.pair_err is not None:
-            self.pair_err.zero_()
 
     def waves(self) -> int:
         """Waves per workgroup: 8 needs every layer width to be a multiple of 128."""
@@ -715,8 +667,8 @@ def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, s
     """Fused dense chain + N=1 head over ``n_rows`` rows. Input: dense ``X`` [rows, >= in] f32, or
     the LTV gather (``slots`` into ``pf_tab`` [C, 25] / ``ext_tab`` [C, ext_w]); outputs ``ml``
     [rows] and/or the K9 rows ``ltv_out`` [rows, 6] (a GPU tensor, or a pinned host tensor that
-    the epilogue writes through the fabric: no D2H copy). ``ws_key``: which pair-kernel
-    workspace (launches that may run concurrently need different keys)."""
+    the epilogue writes through the fabric: no D2H copy). ``ws_key`` is accepted for call-site
+    compatibility (the one-workgroup chain keeps no workspace)."""
     dev = pk.device
     d = dict(n_rows=int(n_rows), n_layers=len(pk.layers), in_w=pk.in_w, in_live=pk.in_live,
              rows_per_block=int(os.environ.get("IGP_MLP_ROWS", "64")), waves=pk.waves(),
@@ -754,8 +706,4 @@ def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, s
         # rows, same box (profiles/r3/x); 4-wave chains keep 32
         rows = int(os.environ.get("IGP_MLP_SPLIT_ROWS", "64" if d["waves"] == 8 else "32"))
         d.update(split=1, rows_per_block=rows if d["waves"] == 8 else 32)
-    w = pk.pair_workspace(n_rows, ws_key)
-    if w is not None:
-        d.update(pair_x=w["x"].data_ptr(), pair_sync=w["sync"].data_ptr(), pair_part=w["part"].data_ptr(),
-                 pair_err=pk.pair_err.data_ptr(), pair_clusters=w["clusters"])
     _mod().mlp_chain(d, _stream())

@@ -42,8 +42,9 @@ from ..config import RuleWeights, ScoringConfig
 from ..layouts import ACCTBATCH, FEATREC, REQREC  # noqa: F401  (REQREC: OP_INGEST rows)
 
 OP_INGEST, OP_CONFIG, OP_TABLES, OP_BATCH, OP_EXT, OP_FEATURES, OP_RESET, OP_STOP, OP_EVHIST, \
-    OP_ABUSE, OP_SNAPSHOT, OP_RESTORE, OP_RELOAD, OP_FEATMANY, OP_PING, OP_METRICS = range(2, 18)
-MUTATING = (OP_INGEST, OP_CONFIG, OP_TABLES, OP_BATCH, OP_EXT, OP_RESET, OP_RELOAD)
+    OP_ABUSE, OP_SNAPSHOT, OP_RESTORE, OP_RELOAD, OP_FEATMANY, OP_PING, OP_METRICS, OP_LTVROWS, OP_LTV = range(2, 20)
+MUTATING = (OP_INGEST, OP_CONFIG, OP_TABLES, OP_BATCH, OP_EXT, OP_RESET, OP_RELOAD, OP_LTVROWS)
+LTV_COLS = 25  # golden.ltv.PLAYER_COLUMNS
 MET_WORDS = 128   # K10 device counter block (csrc/include/records.h MET_*); [106] = rows scored
 
 log = logging.getLogger("igaming_platform_amd.spmd")
@@ -94,12 +95,15 @@ def scoring_from_json(b: bytes) -> ScoringConfig:
 class ShardRunner:
     """What every rank (0 included) executes for one cold op on its local backend."""
 
-    def __init__(self, comm, backend, abuse_gpu=None, core=None):
+    def __init__(self, comm, backend, abuse_gpu=None, core=None, ltv=None):
         self.comm = comm
         self.be = backend
         self.rank = comm.rank
         self.abuse_gpu = abuse_gpu
         self.core = core  # this rank's serving core (paused around snapshots / restores)
+        self.ltv = ltv    # this rank's LTV shard (engine/ltv.py LtvService holding its own accounts)
+        self.acct = None  # this rank's native account-RPC router (engine/acct.py NativeAcct)
+        self.abuse_threshold = 0.7
         self.model_version = 1  # fraud-model reloads applied (audit stamp of the core's rows)
         self.snapshot_dir = None  # the directory of the last OP_SNAPSHOT (final snapshot on failure)
         self.used = [0] * comm.world  # slots in use per rank (the shared registry, via OP_PING)
@@ -160,7 +164,11 @@ class ShardRunner:
                 self.be.ingest(ev[mine])
             return None
         if op == OP_CONFIG:
-            self.be.refresh_config(scoring_from_json(payload))
+            sc = scoring_from_json(payload)
+            self.be.refresh_config(sc)
+            if self.acct is not None:  # the abuse signal limits of this rank's native router
+                self.acct.set_abuse(sc, self.abuse_threshold)
+                self.acct.refresh()
             return None
         if op == OP_RELOAD:  # payload: ONNX bytes (empty: built-in heuristic)
             from ..native import native
@@ -172,6 +180,8 @@ class ShardRunner:
         if op == OP_TABLES:
             _load_tables(payload, self.be.blacklist, self.be.ipintel)
             self.be.refresh_config(None)
+            if self.acct is not None:
+                self.acct.refresh()
             return None
         if op in (OP_BATCH, OP_EXT, OP_RESET):
             slots = np.frombuffer(payload[:4 * n], np.int32)
@@ -214,6 +224,26 @@ class ShardRunner:
             if np.any(mine) and self.abuse_gpu is not None:
                 out[mine] = self.abuse_gpu.score_slots(slots[mine])
             return self.comm.sum_i64(np.pad(out, (0, n % 2)).view(np.int64))
+        if op == OP_LTVROWS:  # payload: slots | owners | rows [n, 25] f32 | ext [n, aux] f32
+            slots = np.frombuffer(payload[:4 * n], np.int32)
+            owners = np.frombuffer(payload[4 * n:8 * n], np.int32)
+            rows = np.frombuffer(payload[8 * n:8 * n + 4 * LTV_COLS * n], np.float32).reshape(n, LTV_COLS)
+            ext = np.frombuffer(payload[8 * n + 4 * LTV_COLS * n:], np.float32).reshape(n, aux) if aux else None
+            mine = self._mine(owners)
+            if np.any(mine) and self.ltv is not None:
+                self.ltv.set_rows(slots[mine], owners[mine], rows[mine], None if ext is None else ext[mine])
+            return None
+        if op == OP_LTV:  # payload: slots | owners -> [n, 7] f32 (6 outputs + profile present), sum-reduced
+            slots = np.frombuffer(payload[:4 * n], np.int32)
+            owners = np.frombuffer(payload[4 * n:8 * n], np.int32)
+            out = np.zeros((n, 7), np.float32)
+            mine = self._mine(owners)
+            if np.any(mine) and self.ltv is not None:
+                res, present = self.ltv.predict_owner_slots(self.rank, slots[mine])
+                out[mine, :6] = res
+                out[mine, 6] = present
+            flat = out.reshape(-1)
+            return self.comm.sum_i64(np.pad(flat, (0, len(flat) % 2)).view(np.int64))
         if op in (OP_SNAPSHOT, OP_RESTORE):  # payload: {"dir": ..., "used": [slots in use per rank]}
             import os
             meta = json.loads(payload.decode())
@@ -386,6 +416,22 @@ class SpmdGroup:
                           n=n)
         return out.view(np.float32)[:n].copy()
 
+    def ltv_rows(self, slots, owners, rows, ext=None) -> None:
+        n = len(slots)
+        w = 0 if ext is None else int(np.asarray(ext).shape[1])
+        body = np.ascontiguousarray(rows, np.float32).tobytes()
+        if ext is not None:
+            body += np.ascontiguousarray(ext, np.float32).tobytes()
+        self._issue(OP_LTVROWS, np.asarray(slots, np.int32).tobytes() + np.asarray(owners, np.int32).tobytes() + body,
+                    n=n, aux=w)
+
+    def ltv_predict(self, slots, owners):
+        """[n, 6] LTV rows of accounts owned by any rank, and their profile-present mask."""
+        n = len(slots)
+        out = self._issue(OP_LTV, np.asarray(slots, np.int32).tobytes() + np.asarray(owners, np.int32).tobytes(), n=n)
+        v = out.view(np.float32)[:7 * n].reshape(n, 7)
+        return v[:, :6].copy(), v[:, 6] > 0.5
+
     def shard_metrics(self) -> np.ndarray:
         """[world, 128] device counters of every shard (one all-reduce; /metrics)."""
         return self._issue(OP_METRICS)
@@ -423,13 +469,14 @@ class SpmdGroup:
             log.warning("destroy_process_group after failure: %s", e)
 
 
-def run_worker(comm, backend, abuse_gpu=None, core=None):
+def run_worker(comm, backend, abuse_gpu=None, core=None, ltv=None, acct=None, abuse_threshold: float = 0.7):
     """Cold-op loop of ranks >= 1 until rank 0 sends STOP (the rank's serving core keeps
     ingesting and stepping on its own threads meanwhile). Returns (ops served, rows scored).
     When a collective fails (rank 0 or a peer died / the group was torn down), the shard
     aborts its core, writes its final snapshot (if rank 0 ever sent a snapshot directory) and
     the loop returns."""
-    runner = ShardRunner(comm, backend, abuse_gpu, core)
+    runner = ShardRunner(comm, backend, abuse_gpu, core, ltv)
+    runner.acct, runner.abuse_threshold = acct, float(abuse_threshold)
     served = 0
     while True:
         try:
@@ -438,6 +485,8 @@ def run_worker(comm, backend, abuse_gpu=None, core=None):
             hdr = comm.bcast_i64(np.zeros(8, np.int64), 0, deadline=False)
             op = int(hdr[0])
             if op == OP_STOP:
+                if acct is not None:
+                    acct.stop()
                 if core is not None:
                     core.stop()
                 return served, runner.rows_scored

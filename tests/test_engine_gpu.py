@@ -132,39 +132,6 @@ def test_gpu_snapshot_restore(tmp_path):
         assert g.get_features(f"acc-{i}", now=NOW + 3).tobytes() == h.get_features(f"acc-{i}", now=NOW + 3).tobytes()
 
 
-def test_streaming_mode_matches_three_stream_mode():
-    """capture_pipelined (one launch per batch: copy(p) || state(p-1) || model(p-2)) gives the
-    same results and leaves the same feature store as the three-graph / three-stream pipeline,
-    including hot accounts with several events per batch and mixed batch sizes."""
-    import torch
-    from igaming_platform_amd.utils import benchkit
-    from igaming_platform_amd.utils.synth import NOW0, make_requests
-    dev = torch.device("cuda", 0)
-    A = benchkit.build("cfg3", 512, 4096, dev, depth=3, history_batches=4, hot_frac=0.2)
-    B = benchkit.build("cfg3", 512, 4096, dev, depth=3, history_batches=4, hot_frac=0.2)
-    rng = np.random.default_rng(3)
-    batches = [make_requests(A.pop, n, rng, NOW0, hot_frac=0.2) for n in (512, 300, 512, 17, 512, 512, 200)]
-    ref = []
-    for i, r in enumerate(batches):
-        res, _ = A.scorer.wait(A.scorer.submit(r, now=NOW0 + i), unpack=False)
-        ref.append(res)
-    sc = B.scorer
-    sc.capture_pipelined()
-    out = []  # completions arrive in batch order
-    for i, r in enumerate(batches):
-        slot, done = sc.pipe_reserve()
-        sc.pack(slot, r)
-        sc.pipe_launch(len(r), NOW0 + i)
-        out += [rows for _, rows, _ in done]
-    out += [rows for _, rows, _ in sc.pipe_drain()]
-    assert [len(x) for x in out] == [len(r) for r in batches]
-    for a, b in zip(ref, out):
-        np.testing.assert_array_equal(a, b)
-    torch.cuda.synchronize()
-    for name in ("rt", "ring_ts", "ring_amt", "hll"):
-        assert torch.equal(getattr(A.store, name), getattr(B.store, name)), name
-
-
 @pytest.mark.parametrize("env", [dict(IGP_DIRECT_LAUNCH="1", IGP_SPLIT_STATE="1", IGP_SERIAL_MAX_BUCKET="0"),
                                  dict(IGP_DIRECT_LAUNCH="1", IGP_SPLIT_STATE="0", IGP_SERIAL_MAX_BUCKET="0"),
                                  dict(IGP_DIRECT_LAUNCH="1", IGP_SERIAL_MAX_BUCKET="4096"),

@@ -79,43 +79,6 @@ def test_mlp_chain_64_row_tiles_match_32(monkeypatch, pf):
     assert torch.all(outs["64"][n - 23:] == -7.0) and not torch.any(outs["64"][:n - 23] == -7.0)
 
 
-@pytest.mark.parametrize("n", [100, 1000, 8192])
-def test_mlp_pair_kernel_matches_one_workgroup(n, monkeypatch):
-    """Pair-cluster chain (mlp_pair.hip: two CUs per 128 rows, each streaming half of every
-    layer's weights and swapping activation halves through L2) vs the one-workgroup kernel:
-    the hidden layers are computed with the same operands in the same k order, only the final
-    N -> 1 sum is ordered differently; live-row handling; repeated launches reuse counters."""
-    import torch
-    from igaming_platform_amd.models.plan import DenseStep, HeadStep
-    from igaming_platform_amd.ops import kernels as K
-    dev = torch.device("cuda", 0)
-    rng = np.random.default_rng(9)
-    steps = [DenseStep(n=512, k=k, act="relu", w_np=rng.normal(0, 0.05, (512, k)).astype(np.float32),
-                       b_np=rng.normal(0, 0.1, 512).astype(np.float32)) for k in (256, 512, 512)]
-    steps.append(HeadStep(n1=512, k=512, act1="relu", act2="sigmoid",
-                          w1_np=rng.normal(0, 0.05, (512, 512)).astype(np.float32),
-                          b1_np=rng.normal(0, 0.1, 512).astype(np.float32),
-                          w2_np=rng.normal(0, 0.1, 512).astype(np.float32), b2=0.2))
-    monkeypatch.setenv("IGP_MLP_PAIR", "1")
-    pk = K.MlpChainPack(steps, dev)
-    assert pk.pair_ok
-    X = torch.from_numpy(rng.normal(0, 1, (n, 256)).astype(np.float32)).to(dev)
-    live = n - 3
-    m_ptr = torch.tensor([live], dtype=torch.int32, device=dev)
-    outs = []
-    for pair in (False, True, True):
-        pk.pair_ok = pair
-        ml = torch.full((n,), -7.0, device=dev)
-        K.mlp_chain(pk, n, X=X, ml=ml, m_ptr=m_ptr)
-        torch.cuda.synchronize()
-        outs.append(ml.cpu())
-    assert not pk.pair_failed()
-    ref, p1, p2 = outs
-    assert torch.equal(p1, p2)
-    assert torch.all(p1[live:] == -7.0)
-    np.testing.assert_allclose(p1[:live].numpy(), ref[:live].numpy(), rtol=0, atol=2e-6)
-
-
 def _ltv_gpu(fused: bool, plan, dev, cap):
     from igaming_platform_amd.engine.ltv import LtvGpu
     old = os.environ.get("IGP_MLP_FUSED")

@@ -192,7 +192,7 @@ def test_plan_lowers_gru_directions_and_layout():
                    for g in grus)
         assert plan.steps[-1].kind == "dense" and plan.steps[-1].k == 64 * (2 if direction == "bidirectional" else 1)
     # a bidirectional Y_h reshaped without the batch-major transpose would mix rows
-    from igaming_platform_amd.onnx.writer import model, node, tensor, value_info
+    from igaming_platform_amd.onnx.writer import model, value_info
     from igaming_platform_amd.onnx import schema as S
     good = builders.build("gru", seq=4, in_dim=8, hidden=64, layers=1, direction="bidirectional")
     nodes = [n for n in good.graph.node if n.op_type != "Transpose"]

@@ -2,7 +2,6 @@
 clients: every unary risk.v1 RPC and health Check, error statuses, ScoreTransaction through the
 serving core without Python, the engine's Python path while the native path is off, concurrency
 over many connections and a multi-MB ScoreBatch. Reference: services/risk/cmd/main.go:72-258."""
-import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
 

@@ -63,25 +63,57 @@ def tx_payloads(n_accounts: int, n: int, seed: int):
             for a in rng.integers(0, n_accounts, n)]
 
 
-def build_cold_engine(accounts: int, backend: str):
+def build_cold_engine(accounts: int, backend: str, precision: str = "fp32"):
     """Engine with the cfg 4 LTV MLP and the cfg 5 abuse GRU loaded, player profiles for every
-    account (PredictLTV / GetPlayerSegment / CheckBonusAbuse benches)."""
+    account and (GPU) full 100-event histories in the HBM event rings (PredictLTV /
+    GetPlayerSegment / CheckBonusAbuse benches). ``precision``: the models' dense numerics
+    (fp32 = the ONNX f32 contract: split bf16x3 MFMA; bf16)."""
     from igaming_platform_amd.config import Config
     from igaming_platform_amd.engine.risk_engine import RiskEngine
     from igaming_platform_amd.onnx import builders
     cfg = Config()
     cfg.gpu.buckets = [64, 512, 4096]
     cfg.gpu.max_batch = 4096
+    cfg.ltv_model.precision = cfg.abuse_model.precision = precision
     eng = RiskEngine(cfg, backend=backend, capacity=accounts + 1024,
                      ltv_model=builders.build("ltv_mlp", n_features=256, width=512, layers=4).SerializeToString(),
                      abuse_model=builders.build("gru", seq=100, in_dim=16, hidden=256).SerializeToString())
     rng = np.random.default_rng(5)
     ids = [account_id(i) for i in range(accounts)]
     slots, owners = eng.registry.resolve_ids(ids, insert=True)
-    rows = np.floor(rng.uniform(0, 1, (accounts, 25)) * np.array(
-        [900, 90, 60, 500, 10, 120, 1e5, 8e4, 3e4, 500, 8, 5e3, 2e5, 1.8e5, 3000, 1, 80, 60, 20, 15, 1, 1, 1, 1, 8]))
-    eng.ltv.set_rows(slots, owners, rows.astype(np.float32), rng.normal(0, 1, (accounts, 231)).astype(np.float32))
+    step = 1 << 18
+    for s0 in range(0, accounts, step):
+        n = min(step, accounts - s0)
+        rows = np.floor(rng.uniform(0, 1, (n, 25)) * np.array(
+            [900, 90, 60, 500, 10, 120, 1e5, 8e4, 3e4, 500, 8, 5e3, 2e5, 1.8e5, 3000, 1, 80, 60, 20, 15, 1, 1, 1, 1, 8]))
+        eng.ltv.set_rows(slots[s0:s0 + n], owners[s0:s0 + n], rows.astype(np.float32),
+                         rng.normal(0, 1, (n, 231)).astype(np.float32))
+    if backend == "gpu":  # full histories: the GRU runs its 100 steps over real-looking events
+        import torch
+        from igaming_platform_amd.layouts import ACCTRT
+        store = eng.backends[0].store
+        g = torch.Generator(device=store.device)
+        g.manual_seed(77)
+        for s0 in range(0, accounts, 1 << 16):
+            n = min(1 << 16, accounts - s0)
+            ev = torch.randn((n, store.ev.shape[1], store.ev.shape[2]), generator=g, device=store.device)
+            store.ev[s0:s0 + n].copy_(ev.to(torch.bfloat16).view(torch.int16))
+        rt = store.rt.view(-1, store.rt.shape[1])
+        rt[:accounts, ACCTRT.fields["ev_count"][1] // 4] = store.ev.shape[1]
+        torch.cuda.synchronize(store.device)
     return eng
+
+
+def acct_payloads(accounts: int, rpc: str, n: int, seed: int, zipf: float = 0.0):
+    """Request bodies of PredictLTV / GetPlayerSegment / CheckBonusAbuse over the population:
+    uniform account ids, or Zipf-distributed ranks with exponent ``zipf`` (> 1)."""
+    from igaming_platform_amd.proto import risk_v1 as P
+    rng = np.random.default_rng(seed)
+    acc = (rng.zipf(zipf, n) - 1) % accounts if zipf > 1 else rng.integers(0, accounts, n)
+    mk = {"ltv": lambda a: P.PredictLTVRequest(account_id=a),
+          "segment": lambda a: P.GetPlayerSegmentRequest(account_id=a),
+          "abuse": lambda a: P.CheckBonusAbuseRequest(account_id=a, bonus_id="welcome")}[rpc]
+    return [mk(account_id(int(a))).SerializeToString() for a in acc]
 
 
 def run_cold_engine(a) -> dict:
@@ -344,15 +376,26 @@ def run_grpc_open_loop(a) -> dict:
                 latency_baseline_ms=BASELINE_P99_MS)
 
 
+RPC_PATHS = {"tx": "ScoreTransaction", "ltv": "PredictLTV", "segment": "GetPlayerSegment", "abuse": "CheckBonusAbuse"}
+RPC_MODELS = {"tx": "cfg3 GBDT(100,d7,128f)+MLP(32-256-1)",
+              "ltv": "cfg4 LTV MLP 4x512 over 256 features (HBM tables) + K9, fused chain",
+              "segment": "cfg4 LTV MLP 4x512 over 256 features (HBM tables) + K9, fused chain",
+              "abuse": "cfg5 GRU 2x256 over the last 100 events (HBM event rings) + K1 rule signals + links"}
+
+
 def _curve_result(a, curve, st) -> dict:
     ok = [c for c in curve if c["p99_ms"] is not None and c["p99_ms"] < BASELINE_P99_MS and c["errors"] == 0
           and c["achieved_per_s"] >= 0.95 * c["offered_per_s"]]
     best = max(ok, key=lambda c: c["achieved_per_s"]) if ok else None
-    return dict(metric="unary risk.v1.ScoreTransaction over gRPC: throughput vs latency (open loop)",
+    rpc = RPC_PATHS[a.rpc]
+    return dict(metric=f"unary risk.v1.{rpc} over gRPC: throughput vs latency (open loop)",
                 value=best["achieved_per_s"] if best else 0.0, unit="calls/s",
                 value_is="highest offered rate answered in full with p99 < 50 ms", scope="grpc_unary_open_loop",
-                n_gpus=1 if a.backend == "gpu" else 0, data="synthetic (UUID ids, random-init cfg3 weights)",
-                config=dict(model="cfg3 GBDT(100,d7,128f)+MLP(32-256-1)", clients=a.clients, seconds_per_level=a.seconds,
+                n_gpus=1 if a.backend == "gpu" else 0,
+                data=f"synthetic (UUID ids over {a.accounts} accounts"
+                     + (f", Zipf({a.zipf}) account ranks" if a.zipf > 1 else ", uniform") + ", random-init weights)",
+                dtype=getattr(a, "numerics", "fp32"),
+                config=dict(model=RPC_MODELS[a.rpc], clients=a.clients, seconds_per_level=a.seconds,
                             server=server_desc(a),
                             client=("native HTTP/2 open loop (libnghttp2, one connection per thread)" if a.client == "native"
                                     else "grpc.aio open loop") + ", latency from the scheduled send time"),
@@ -366,8 +409,9 @@ def _native_open_loop(a, eng, srv, rates) -> dict:
     ``--clients`` HTTP/2 connections, each on its own thread."""
     from igaming_platform_amd.native import native
     from igaming_platform_amd.proto import risk_v1 as P
-    payloads = tx_payloads(a.accounts, 8192, seed=300)
-    path = P.method_path("ScoreTransaction")
+    payloads = (tx_payloads(a.accounts, 8192, seed=300) if a.rpc == "tx"
+                else acct_payloads(a.accounts, a.rpc, 1 << 16, 300, a.zipf))
+    path = P.method_path(RPC_PATHS[a.rpc])
     native().grpc_load("127.0.0.1", srv.port, path, payloads, 2000.0, 1.0, a.clients, 4096)  # warm
     curve = []
     for rate in rates:
@@ -379,10 +423,17 @@ def _native_open_loop(a, eng, srv, rates) -> dict:
                           p99_ms=round(float(np.percentile(lat, 99)), 3) if len(lat) else None))
         print(json.dumps(curve[-1]), flush=True)
         time.sleep(1.0)
-    st = eng.core.stats(False) if getattr(eng, "core", None) is not None else None
+    if a.rpc == "tx":
+        st = eng.core.stats(False) if getattr(eng, "core", None) is not None else None
+    else:  # the native account router's device steps (None: served on the Python path)
+        acct = getattr(eng, "acct", None)
+        st = acct.router.stats(3 if a.rpc == "abuse" else 1) if acct is not None else None
+    out_srv = srv.stats()
     srv.stop()
     eng.close()
-    return _curve_result(a, curve, st)
+    res = _curve_result(a, curve, st)
+    res["server_stats"] = out_srv
+    return res
 
 
 def run_grpc(a) -> dict:
@@ -429,7 +480,9 @@ def run_grpc(a) -> dict:
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--scope", default="e2e", choices=["e2e", "grpc", "engine_batched"])
-    ap.add_argument("--rpc", default="batch", choices=["batch", "tx", "ltv", "abuse"])
+    ap.add_argument("--rpc", default="batch", choices=["batch", "tx", "ltv", "segment", "abuse"])
+    ap.add_argument("--zipf", type=float, default=0.0, help="account-id distribution: Zipf exponent (> 1), 0 uniform")
+    ap.add_argument("--numerics", default="fp32", choices=["fp32", "bf16"], help="cfg4 / cfg5 model numerics")
     ap.add_argument("--backend", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--accounts", type=int, default=1 << 20)
     ap.add_argument("--batch", type=int, default=8192)
@@ -449,7 +502,10 @@ def main(argv=None) -> int:
                     help="--open-loop: offered whole-node unary calls/s per level")
     a = ap.parse_args(argv)
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-    if a.scope == "grpc" and a.rpc == "tx" and a.open_loop:
+    if a.scope == "grpc" and a.rpc in ("ltv", "segment", "abuse") and a.open_loop:
+        eng = build_cold_engine(a.accounts, a.backend, a.numerics)
+        out = _native_open_loop(a, eng, make_server(a, eng, batching=True), [int(x) for x in a.rates.split(",")])
+    elif a.scope == "grpc" and a.rpc == "tx" and a.open_loop:
         out = run_grpc_open_loop(a)
     else:
         out = {"e2e": run_e2e, "grpc": run_grpc, "engine_batched": run_cold_engine}[a.scope](a)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """cfg 4 LTV chain kernel alone (256 -> 4 x 512 -> 1, bf16), one launch at a time on one stream:
-microseconds per launch and TFLOP/s for the one-workgroup kernel (32 / 64 rows per workgroup)
-and the pair-cluster kernel (csrc/kernels/mlp_pair.hip); SPLIT=1: the f32-faithful chain at 32 / 64 rows, at several batch sizes. Checks that the
+microseconds per launch and TFLOP/s for the one-workgroup kernel (32 / 64 rows per workgroup);
+SPLIT=1: the f32-faithful chain at 32 / 64 rows, at several batch sizes. Checks that the
 variants agree. Usage: python tools/mlp_bench.py [batches, default 8192,4096,16384]"""
 import json
 import os
@@ -24,7 +24,6 @@ def main() -> int:
                           w1_np=rng.normal(0, 0.05, (512, 512)).astype(np.float32),
                           b1_np=rng.normal(0, 0.1, 512).astype(np.float32),
                           w2_np=rng.normal(0, 0.1, 512).astype(np.float32), b2=0.1))
-    os.environ["IGP_MLP_PAIR"] = "1"  # allocate the pair workspace; each variant sets pair_ok itself
     split = os.environ.get("SPLIT", "0") == "1"  # the f32-faithful chain (hi/lo bf16 pairs)
     pk = K.MlpChainPack(steps, dev, split=split)
     flop_row = 2 * (256 * 512 + 3 * 512 * 512 + 512)
@@ -34,10 +33,9 @@ def main() -> int:
         X = torch.from_numpy(rng.normal(0, 1, (B, 256)).astype(np.float32)).to(dev)
         ref = None
         variants = ((("split32", "32", False), ("split64", "64", False)) if split else
-                    (("wg32", "32", False), ("wg64", "64", False), ("pair", "64", True)))
-        for name, rows, pair in variants:
+                    (("wg32", "32", False), ("wg64", "64", False)))
+        for name, rows, _ in variants:
             os.environ["IGP_MLP_SPLIT_ROWS" if split else "IGP_MLP_ROWS"] = rows
-            pk.pair_ok = pair
             ml = torch.zeros(B, device=dev)
             run = lambda: K.mlp_chain(pk, B, X=X, ml=ml)  # noqa: E731
             for _ in range(3):
@@ -56,8 +54,7 @@ def main() -> int:
                 ts.append(e0.elapsed_time(e1) * 1e3)
             us = float(np.median(ts))
             r = dict(batch=B, kernel=name, us=round(us, 2), tflops=round(flop_row * B / us / 1e6, 1),
-                     pct_of_2500=round(flop_row * B / us / 1e6 / 25.0, 1), max_diff=diff,
-                     pair_failed=pk.pair_failed() if pair else None)
+                     pct_of_2500=round(flop_row * B / us / 1e6 / 25.0, 1), max_diff=diff)
             res.append(r)
             print(json.dumps(r), flush=True)
     with open(os.environ.get("OUT", "gpurun_out/mlp_bench.json"), "w") as f:
