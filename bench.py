@@ -80,7 +80,9 @@ def parse():
                     help="--scope serving with cfg4 / cfg5: offered PredictLTV / CheckBonusAbuse calls/s per level "
                          "(open loop over the native gRPC server)")
     ap.add_argument("--seconds", type=float, default=5.0, help="cfg4 / cfg5 serving: seconds per offered-load level")
-    ap.add_argument("--zipf", type=float, default=0.0, help="cfg4 / cfg5 serving: Zipf exponent of the account ids")
+    ap.add_argument("--zipf", type=float, default=0.0, help="serving: Zipf exponent of the account ids (0: uniform)")
+    ap.add_argument("--payloads", type=int, default=128, help="serving: distinct ScoreBatch requests per rank "
+                    "(their account ids spread over the whole population)")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
     if a.numerics == "auto":  # the ONNX models' f32 contract everywhere (cfg4 / cfg5: split MFMA)
@@ -533,9 +535,14 @@ def serving_bench(a) -> None:
         backend.set_batch_rows(slots[ok], rows[ok])
         if c["width"] > 30:
             backend.set_ext(slots[ok], pop.ext[(s0 + mine)[ok] % n_acc])
-    payloads = bench_e2e.make_payloads(total, 6, B, seed=11 + rank)
+    # the request stream covers the population (6 replayed payloads kept 4.7 % of the
+    # accounts hot): --payloads distinct requests, account ids uniform (default) or Zipf(--zipf)
+    spread = {}
+    payloads = bench_e2e.spread_payloads(total, a.payloads, B, seed=11 + rank, zipf=a.zipf, stats=spread)
     lat = []
+    stage_rows = []  # per request: parse, resolve, queue, device, serialize, total (ns)
     lock = threading.Lock()
+    timings = type(core).last_timings
 
     def run(n_req: int, t_base: int, record: bool):
         counter = {"i": 0}
@@ -550,11 +557,13 @@ def serving_bench(a) -> None:
                 t0 = time.perf_counter_ns()
                 out = core.score_batch(payloads[i % len(payloads)], t_base + i // 50, t0)
                 dt = (time.perf_counter_ns() - t0) / 1e6
+                tm = timings()
                 if len(out) < B:
                     raise RuntimeError("short response")
                 if record:
                     with lock:
                         lat.append(dt)
+                        stage_rows.append(tm[:6])
         th = [threading.Thread(target=worker) for _ in range(a.threads)]
         [t.start() for t in th]
         [t.join() for t in th]
@@ -583,6 +592,12 @@ def serving_bench(a) -> None:
                   device_steps=int(st["steps"]), empty_steps=int(st["empty_steps"]),
                   mean_rows_per_device_step=round(st["rows"] / max(int(st["steps"]), 1), 1))
     p99, p50 = float(np.percentile(lat, 99)), float(np.percentile(lat, 50))
+    # where a request's time goes, per request (tails, not sums): queue = enqueue -> its first
+    # device step formed, device = that step formed -> all its rows back
+    sr = np.asarray(stage_rows, np.float64) / 1e6
+    stage_tails = {name: {"p50": round(float(np.percentile(sr[:, k], 50)), 3),
+                          "p99": round(float(np.percentile(sr[:, k], 99)), 3)}
+                   for k, name in enumerate(("parse", "resolve", "queue", "device", "serialize", "total"))}
     if comm is not None:  # the slowest rank's clock and latencies
         mx = torch.tensor([elapsed, p99, p50], dtype=torch.float64)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -597,6 +612,10 @@ def serving_bench(a) -> None:
                    "step": "one 8192-transaction ScoreBatch request per ingress thread (concurrent); device "
                            "micro-batches of per_gpu_batch rows", "accounts_per_gpu": n_acc,
                    "ingress_threads_per_rank": a.threads, "pipeline_depth": a.depth, "serving": mode,
+                   "account_spread": {"distribution": f"zipf({a.zipf})" if a.zipf > 1 else "uniform",
+                                      "population": total, "requests_in_stream_per_rank": a.payloads,
+                                      "distinct_accounts_in_stream_rank0": spread.get("distinct_accounts"),
+                                      "transactions_in_stream_per_rank": spread.get("transactions")},
                    "numerics": numerics_desc(a),
                    "comm_env": {k: v for k, v in sorted(os.environ.items())
                                 if k.startswith(("NCCL_", "RCCL_")) or k == "GPU_MAX_HW_QUEUES"}},
@@ -605,6 +624,7 @@ def serving_bench(a) -> None:
         "out, including the serving core's micro-batch queueing",
         "latency_baseline_ms": BASELINE_P99_MS, "latency_vs_baseline": BASELINE_P99_MS / p99 if p99 > 0 else None,
         "host_stages_rank0": stages,
+        "request_stage_ms_rank0": stage_tails,
     }
     if rank == 0:
         line = json.dumps(out)

@@ -9,7 +9,7 @@
 namespace igp {
 namespace {
 
-constexpr uint64_t kMagic = 0x3158444954434341ull;  // "ACCTIDX1"
+constexpr uint64_t kMagic = 0x3258444954434341ull;  // "ACCTIDX2" (32-byte entries with inline keys)
 constexpr int64_t kArenaPerAccount = 64;            // bytes reserved per slot (4-byte length + id, 8-aligned)
 
 int64_t table_size(int64_t capacity) {
@@ -93,6 +93,47 @@ int32_t AccountIndex::published(const Entry& e) const {
   return st > 0 ? st - 1 : -1;
 }
 
+static int hexv(char c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  return -1;  // upper case is not the canonical form: such ids take the non-UUID encoding
+}
+
+uint32_t AccountIndex::encode_key(std::string_view id, uint8_t key[16]) {
+  std::memset(key, 0, 16);
+  if (id.size() == 36 && id[8] == '-' && id[13] == '-' && id[18] == '-' && id[23] == '-') {
+    int b = 0, hi = -1;
+    bool ok = true;
+    for (size_t i = 0; i < 36 && ok; ++i) {
+      if (i == 8 || i == 13 || i == 18 || i == 23) continue;
+      const int v = hexv(id[i]);
+      if (v < 0) {
+        ok = false;
+      } else if (hi < 0) {
+        hi = v;
+      } else {
+        key[b++] = uint8_t(hi << 4 | v);
+        hi = -1;
+      }
+    }
+    if (ok) return kExact | kUuid;
+    std::memset(key, 0, 16);
+  }
+  if (id.size() <= 15) {
+    key[0] = uint8_t(id.size());
+    std::memcpy(key + 1, id.data(), id.size());
+    return kExact;
+  }
+  std::memcpy(key, id.data(), 16);  // prefix of a long id: a fast reject before the arena compare
+  return 0;
+}
+
+bool AccountIndex::key_equal(const Entry& e, std::string_view id, uint32_t form, const uint8_t* key) const {
+  if ((e.off8 & (kExact | kUuid)) != form) return false;  // the encoding form is a function of the id
+  if (std::memcmp(e.key, key, 16) != 0) return false;
+  return (form & kExact) || id_equal(e.off8 & kOffMask, id);
+}
+
 bool AccountIndex::id_equal(uint32_t off8, std::string_view id) const {
   const char* p = arena_ + size_t(off8) * 8;
   uint32_t len;
@@ -101,13 +142,15 @@ bool AccountIndex::id_equal(uint32_t off8, std::string_view id) const {
 }
 
 int32_t AccountIndex::find_from(int64_t i, std::string_view id, uint64_t h) const {
+  uint8_t key[16];
+  const uint32_t form = encode_key(id, key);
   for (int64_t probes = 0; probes <= mask_; ++probes, i = (i + 1) & mask_) {
     const Entry& e = tab_[size_t(i)];
     const uint64_t hv = e.h.load(std::memory_order_acquire);
     if (hv == 0) return -1;
     if (hv != h) continue;
     const int32_t s = published(e);
-    if (s >= 0 && id_equal(e.off8, id)) return s;
+    if (s >= 0 && key_equal(e, id, form, key)) return s;
   }
   return -1;
 }
@@ -120,6 +163,8 @@ int32_t AccountIndex::find(std::string_view id, uint64_t h) const {
 int32_t AccountIndex::insert(std::string_view id, uint64_t h, bool* inserted) {
   if (inserted) *inserted = false;
   if (h == 0) return -1;
+  uint8_t key[16];
+  const uint32_t form = encode_key(id, key);
   int64_t i = int64_t(h & uint64_t(mask_));
   for (int64_t probes = 0; probes <= mask_; ++probes, i = (i + 1) & mask_) {
     Entry& e = tab_[size_t(i)];
@@ -142,7 +187,12 @@ int32_t AccountIndex::insert(std::string_view id, uint64_t h, bool* inserted) {
         const uint32_t len = uint32_t(id.size());
         std::memcpy(p, &len, 4);
         std::memcpy(p + 4, id.data(), id.size());
-        e.off8 = uint32_t(off / 8);
+        if (off / 8 > int64_t(kOffMask)) {
+          e.state.store(-1, std::memory_order_release);
+          return -1;
+        }
+        std::memcpy(e.key, key, 16);
+        e.off8 = uint32_t(off / 8) | form;
         slot_off_[s] = uint32_t(off / 8);
         e.state.store(int32_t(s + 1), std::memory_order_release);
         if (inserted) *inserted = true;
@@ -153,7 +203,7 @@ int32_t AccountIndex::insert(std::string_view id, uint64_t h, bool* inserted) {
     if (hv != h) continue;
     const int32_t s = published(e);
     if (s >= 0) {
-      if (id_equal(e.off8, id)) return s;
+      if (key_equal(e, id, form, key)) return s;
       hdr_->collisions.fetch_add(1, std::memory_order_relaxed);
     }
   }
@@ -178,48 +228,56 @@ void AccountIndex::lookup(const std::vector<std::string>& ids, const std::vector
 void AccountIndex::lookup_views(const std::string_view* ids, const uint64_t* h, size_t n, bool insert_, int32_t* slots,
                                 uint8_t* fresh, const uint8_t* sel) {
   constexpr size_t kAhead = 16;  // probe lines in flight
-  // pass 1: probe every row (prefetched), remember the first digest match and prefetch its id
-  std::vector<int64_t> cand(n, -1);
+  // pass 1: probe every row (prefetched); an exact inline key settles the row on the spot (one
+  // miss per row); long ids remember their candidate and prefetch its arena bytes
+  std::vector<int64_t> cand;
+  std::vector<uint32_t> later;
   const Entry* t = tab_;
   for (size_t k = 0; k < std::min(n, kAhead); ++k) __builtin_prefetch(t + (h[k] & uint64_t(mask_)));
+  uint8_t key[16];
   for (size_t k = 0; k < n; ++k) {
     if (k + kAhead < n) __builtin_prefetch(t + (h[k + kAhead] & uint64_t(mask_)));
     if (fresh) fresh[k] = 0;
     slots[k] = -1;
     if (h[k] == 0 || (sel && !sel[k])) continue;
+    const uint32_t form = encode_key(ids[k], key);
     int64_t i = int64_t(h[k] & uint64_t(mask_));
+    bool settled = false, deferred = false;
     for (int64_t probes = 0; probes <= mask_; ++probes, i = (i + 1) & mask_) {
-      const uint64_t hv = t[size_t(i)].h.load(std::memory_order_acquire);
+      const Entry& e = t[size_t(i)];
+      const uint64_t hv = e.h.load(std::memory_order_acquire);
       if (hv == 0) break;
-      if (hv == h[k]) {
+      if (hv != h[k]) continue;
+      if (!(form & kExact)) {  // confirm against the arena in pass 2
+        if (e.state.load(std::memory_order_acquire) > 0) __builtin_prefetch(arena_ + size_t(e.off8 & kOffMask) * 8);
+        if (cand.empty()) cand.assign(n, -1);
         cand[k] = i;
-        const int32_t st = t[size_t(i)].state.load(std::memory_order_acquire);
-        if (st > 0) __builtin_prefetch(arena_ + size_t(t[size_t(i)].off8) * 8);
+        later.push_back(uint32_t(k));
+        deferred = true;
+        break;
+      }
+      const int32_t s = published(e);
+      if (s >= 0 && key_equal(e, ids[k], form, key)) {
+        slots[k] = s;
+        settled = true;
         break;
       }
     }
+    if (!settled && !deferred && insert_) later.push_back(uint32_t(k));
   }
-  // pass 2: confirm the candidates against the stored ids (lines already in flight)
+  // pass 2: long ids against the stored bytes (lines already in flight), then inserts in row
+  // order (a batch's new accounts get slots in arrival order)
   std::vector<uint32_t> miss;
-  for (size_t k = 0; k < n; ++k) {
-    if (h[k] == 0 || (sel && !sel[k])) continue;
-    if (cand[k] >= 0) {
-      const Entry& e = t[size_t(cand[k])];
-      const int32_t s = published(e);
-      if (s >= 0 && id_equal(e.off8, ids[k])) {
-        slots[k] = s;
-        continue;
-      }
-      // digest collision (or a dead entry): the rest of the probe chain
-      const int32_t s2 = find_from((cand[k] + 1) & mask_, ids[k], h[k]);
+  for (uint32_t k : later) {
+    if (!cand.empty() && cand[k] >= 0) {
+      const int32_t s2 = find_from(cand[k], ids[k], h[k]);
       if (s2 >= 0) {
         slots[k] = s2;
         continue;
       }
     }
-    if (insert_) miss.push_back(uint32_t(k));
+    if (insert_) miss.push_back(k);
   }
-  // pass 3: inserts in row order (a batch's new accounts get slots in arrival order)
   for (uint32_t k : miss) {
     bool ins = false;
     slots[k] = insert(ids[k], h[k], &ins);

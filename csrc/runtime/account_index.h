@@ -3,10 +3,15 @@
 // Replaces the per-account Redis key namespace ``features:<uuid>:*`` of
 // services/risk/internal/features/redis_store.go:25-35.
 //
-// Lock-free open addressing over 16-byte entries {XXH64 digest, state, id offset}; the id
-// bytes live in an append-only arena, so identity is the exact id string (a digest match is
-// always confirmed against the stored bytes: two ids that collide on 64 bits get two slots,
-// and the collision is counted). Inserts claim an empty entry with one 64-bit CAS, take the
+// Lock-free open addressing over 32-byte entries {XXH64 digest, state, id offset, inline key};
+// the id bytes live in an append-only arena, so identity is the exact id string (a digest match
+// is always confirmed against the id: two ids that collide on 64 bits get two slots, and the
+// collision is counted). The inline key makes that confirmation free for the common ids: a
+// canonical UUID string (36 chars, lower-case hex) is stored as its 16 binary bytes and a short
+// id (<= 15 bytes) verbatim, both exact encodings of the string, so a lookup costs ONE cache
+// miss (the entry) instead of two (entry + arena); longer ids keep a 16-byte prefix for a
+// fast reject and are confirmed against the arena (uniform traffic over 1 M
+// accounts made the second miss the resolve cost). Inserts claim an empty entry with one 64-bit CAS, take the
 // next slot with a fetch_add, write the id, then publish the slot with a release store;
 // readers that meet a claimed-but-unpublished entry spin until it is published.
 //
@@ -69,9 +74,16 @@ class AccountIndex {
   struct Entry {
     std::atomic<uint64_t> h;      // 0 = empty
     std::atomic<int32_t> state;   // 0 = claimed, not yet published; s + 1 = slot s; -1 = dead (index full)
-    uint32_t off8;                // id offset in the arena, 8-byte units
+    uint32_t off8;                // id offset in the arena, 8-byte units | kExact | kUuid
+    uint8_t key[16];              // inline key (written before the publish)
   };
-  static_assert(sizeof(Entry) == 16, "AccountIndex entry must be 16 bytes");
+  static_assert(sizeof(Entry) == 32, "AccountIndex entry must be 32 bytes");
+  static constexpr uint32_t kExact = 1u << 31, kUuid = 1u << 30, kOffMask = (1u << 30) - 1;
+ public:
+  // the inline key of an id: returns kExact [| kUuid] when the key IS the id (exact encoding)
+  static uint32_t encode_key(std::string_view id, uint8_t key[16]);
+ private:
+  bool key_equal(const Entry& e, std::string_view id, uint32_t form, const uint8_t* key) const;
 
   void layout(void* base);
   void init_fresh(int64_t capacity);

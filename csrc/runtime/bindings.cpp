@@ -398,14 +398,19 @@ PYBIND11_MODULE(_native, m) {
         }
         return py::make_tuple(slots, fresh);
       }, py::arg("batch"), py::arg("insert") = true, py::arg("sel") = py::none())
-      .def("lookup", [](AccountIndex& ix, const std::vector<std::string>& ids, bool insert) {
+      .def("lookup", [](AccountIndex& ix, const std::vector<std::string>& ids, bool insert, py::object hashes) {
         std::vector<uint64_t> h(ids.size());
-        for (size_t k = 0; k < ids.size(); ++k) h[k] = id_hash(ids[k], SEED_ACCOUNT);
+        if (hashes.is_none()) {
+          for (size_t k = 0; k < ids.size(); ++k) h[k] = id_hash(ids[k], SEED_ACCOUNT);
+        } else {  // explicit digests (tests: forced collisions)
+          h = hashes.cast<std::vector<uint64_t>>();
+          if (h.size() != ids.size()) throw std::runtime_error("lookup: hashes length");
+        }
         py::array_t<int32_t> slots(ids.size());
         py::array_t<uint8_t> fresh(ids.size());
         ix.lookup(ids, h, insert, slots.mutable_data(), fresh.mutable_data());
         return py::make_tuple(slots, fresh);
-      }, py::arg("ids"), py::arg("insert") = false)
+      }, py::arg("ids"), py::arg("insert") = false, py::arg("hashes") = py::none())
       .def("__len__", &AccountIndex::size)
       .def_property_readonly("capacity", &AccountIndex::capacity)
       .def_property_readonly("collisions", &AccountIndex::collisions)
@@ -735,6 +740,7 @@ PYBIND11_MODULE(_native, m) {
     }
     py::dict d;
     d["latency_ms"] = vec_np(r.latency_ms);
+    d["sched_ms"] = vec_np(r.sched_ms);
     d["errors"] = r.errors;
     d["sent"] = r.sent;
     d["seconds"] = r.seconds;
@@ -873,7 +879,11 @@ PYBIND11_MODULE(_native, m) {
         d["ml_high"] = t.ml_high; d["blacklisted"] = t.blacklisted; d["scored"] = t.scored;
         return d;
       }, py::arg("reset") = false)
-      .def_static("now_ns", &ServeCore::now_ns);
+      .def_static("now_ns", &ServeCore::now_ns)
+      .def_static("last_timings", []() {  // this thread's last score_batch call, ns per stage
+        const CallTimings& t = last_timings_tl();
+        return py::make_tuple(t.parse, t.resolve, t.queue, t.device, t.serialize, t.total, t.rows);
+      });
 
   // ---- account RPCs (acct_core.h): PredictLTV / GetPlayerSegment / CheckBonusAbuse
   m.attr("RPC_LTV") = int(RPC_LTV);

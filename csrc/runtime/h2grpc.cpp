@@ -774,6 +774,8 @@ struct LoadConn {
   void* sess = nullptr;
   std::unordered_map<int32_t, std::unique_ptr<Call>> calls;  // heap calls: the providers point at them
   std::vector<double>* lat = nullptr;
+  std::vector<double>* sched = nullptr;
+  int64_t t0 = 0;
   int64_t* errors = nullptr;
   int64_t* done = nullptr;
   int64_t* last = nullptr;  // latest completion (mono ns)
@@ -802,8 +804,12 @@ struct LoadConn {
     if (it == lc->calls.end()) return 0;
     const int64_t t = mono_ns();
     if (t > *lc->last) *lc->last = t;
-    if (err == 0 && it->second->status == 0) lc->lat->push_back(double(t - it->second->t_sched) * 1e-6);
-    else ++*lc->errors;
+    if (err == 0 && it->second->status == 0) {
+      lc->lat->push_back(double(t - it->second->t_sched) * 1e-6);
+      lc->sched->push_back(double(it->second->t_sched - lc->t0) * 1e-6);
+    } else {
+      ++*lc->errors;
+    }
     ++*lc->done;
     lc->calls.erase(it);
     return 0;
@@ -817,7 +823,7 @@ LoadResult grpc_load(const std::string& host, int port, const std::string& path,
   const Ng& n = ng();
   if (payloads.empty() || rate <= 0 || conns < 1) throw std::runtime_error("grpc_load: arguments");
   LoadResult out;
-  std::vector<std::vector<double>> lats(static_cast<size_t>(conns));
+  std::vector<std::vector<double>> lats(static_cast<size_t>(conns)), scheds(static_cast<size_t>(conns));
   std::vector<int64_t> errs(static_cast<size_t>(conns), 0), sent(static_cast<size_t>(conns), 0),
       done(static_cast<size_t>(conns), 0), last(static_cast<size_t>(conns), 0);
   std::vector<std::string> frames(payloads.size());
@@ -828,7 +834,7 @@ LoadResult grpc_load(const std::string& host, int port, const std::string& path,
     frames[i] = f + payloads[i];
   }
   const std::string authority = host + ":" + std::to_string(port);
-  const int64_t t0 = mono_ns() + 20000000;  // 20 ms for the connections to come up
+  const int64_t t0 = mono_ns() + 200000000;  // 200 ms for the connections to come up (HTTP/2 preface, settings)
   const int64_t t_end = t0 + int64_t(seconds * 1e9);
   std::vector<std::thread> th;
   std::atomic<int> failed{0};
@@ -853,6 +859,8 @@ LoadResult grpc_load(const std::string& host, int port, const std::string& path,
       n.set_on_stream_close(cbs, LoadConn::on_close);
       LoadConn lc;
       lc.lat = &lats[size_t(ci)];
+      lc.sched = &scheds[size_t(ci)];
+      lc.t0 = t0;
       lc.errors = &errs[size_t(ci)];
       lc.done = &done[size_t(ci)];
       lc.last = &last[size_t(ci)];
@@ -926,6 +934,7 @@ LoadResult grpc_load(const std::string& host, int port, const std::string& path,
   for (auto& t : th) t.join();
   for (int ci = 0; ci < conns; ++ci) {
     out.latency_ms.insert(out.latency_ms.end(), lats[size_t(ci)].begin(), lats[size_t(ci)].end());
+    out.sched_ms.insert(out.sched_ms.end(), scheds[size_t(ci)].begin(), scheds[size_t(ci)].end());
     out.errors += errs[size_t(ci)];
     out.sent += sent[size_t(ci)];
   }

@@ -115,6 +115,7 @@ class GrpcServer {
 // open-loop unary gRPC load generator (tools/bench_e2e.py --client native)
 struct LoadResult {
   std::vector<double> latency_ms;  // per answered call, from its scheduled send time
+  std::vector<double> sched_ms;    // that call's scheduled send time, from the schedule start
   int64_t errors = 0, sent = 0;
   double seconds = 0;
   double elapsed = 0;  // schedule start -> last completion (>= seconds)

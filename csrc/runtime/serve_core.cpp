@@ -55,6 +55,7 @@ struct ServeCore::Item {
   FeatRec feat1{};
   uint64_t tag = 0;
   int64_t t0 = 0, t_enq = 0;
+  int64_t t_issue = 0;          // the first step holding rows of this item was formed (q_mu_)
   // completion hand-off (m)
   std::mutex m;
   std::condition_variable cv;
@@ -244,11 +245,15 @@ std::string_view ServeCore::score_batch_view(const char* data, size_t n, int64_t
   it.res = res.data();
   it.feat = it.wf ? feat.data() : nullptr;
   enqueue(&it);
+  const int64_t tq = it.t_enq;
   wait_item(&it);
   if (it.failed) throw std::runtime_error("ServeCore: batch failed: " + it.err);
   const int64_t td = now_ns();
   const std::string_view out = wire::batch_response_scratch(it.res, it.feat, nullptr, (td - t0) / 1000000, it.n);
   const int64_t te = now_ns();
+  // this call's stage times (last_timings(): per-request tails, not only sums)
+  CallTimings& ct = last_timings_tl();
+  ct = CallTimings{tb - ta, tc - tb, it.t_issue - tq, td - it.t_issue, te - td, te - t0, int64_t(it.n)};
   a_parse_.fetch_add(tb - ta, std::memory_order_relaxed);
   a_resolve_.fetch_add(tc - tb, std::memory_order_relaxed);
   a_serialize_.fetch_add(te - td, std::memory_order_relaxed);
@@ -396,6 +401,7 @@ bool ServeCore::issue_step(std::unique_lock<std::mutex>& lk, bool allow_empty) {
       it->ocur[0] += take;
       it->remaining -= take;
       it->taken += take;
+      if (!it->t_issue) it->t_issue = now_ns();
       n += take;
       now = std::max(now, it->now);
       st->wf |= it->wf;
@@ -415,6 +421,7 @@ bool ServeCore::issue_step(std::unique_lock<std::mutex>& lk, bool allow_empty) {
         it->ocur[o] += take;
         it->remaining -= take;
         it->taken += take;
+        if (!it->t_issue) it->t_issue = now_ns();
         fill[o] += take;
         n += take;
         if (fill[o] == cap_) ++full;

@@ -73,6 +73,17 @@ class StepClock {
   int world_ = 1, rank_ = 0;
 };
 
+// stage times of one ScoreBatch call (ns): parse, resolve, queue (enqueue -> its first device
+// step formed), device (first step formed -> every row back, incl. the copy out), serialize, total
+struct CallTimings {
+  int64_t parse = 0, resolve = 0, queue = 0, device = 0, serialize = 0, total = 0, rows = 0;
+};
+// the calling thread's last score_batch / score_batch_view timings
+inline CallTimings& last_timings_tl() {
+  thread_local CallTimings t;
+  return t;
+}
+
 struct ServeStats {
   int64_t items = 0, rows = 0, steps = 0, empty_steps = 0, unary = 0;
   int64_t parse_ns = 0, resolve_ns = 0, pack_ns = 0, device_ns = 0, copy_ns = 0, serialize_ns = 0, queue_ns = 0;

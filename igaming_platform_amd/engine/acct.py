@@ -127,6 +127,11 @@ class AbuseNativeDevice:
             self.gm = GruModel(plan.steps, dev, getattr(plan, "precision", "fp32") != "bf16", B)
             if not self.gm.has_head:
                 raise ValueError("abuse model must end in an N=1 head (probability)")
+            # batch-parallel K4 only: the weight-stationary cluster kernel (gru_ws.hip) needs every
+            # workgroup of the launch co-resident, which a serving rank sharing the chip with the
+            # scoring pipeline cannot promise (and a recorded graph cannot fall back)
+            for gp in self.gm.packs:
+                gp.disable_ws()
             self.T = plan.steps[0].seq or store.ev.shape[1]
         self.req_off = 16 + 4 * B
         nb = self.req_off + 48 * B

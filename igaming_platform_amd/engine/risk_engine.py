@@ -218,7 +218,7 @@ class RiskEngine:
             if am is not None:
                 ag = []
                 for r, d in enumerate(self.devices):
-                    ap = to_device(compile_onnx(am), f"cuda:{d}")
+                    ap = to_device(compile_onnx(am), f"cuda:{d}", cfg.abuse_model.precision)
                     g = AbuseGpu(self.backends[r].store, ap, buckets=cfg.gpu.buckets, use_graphs=capture)
                     g.capture()
                     ag.append(g)
@@ -1071,7 +1071,8 @@ def make_abuse_gpu(cfg: Config, local, abuse_model):
         return None
     from ..models.plan import compile_onnx, to_device
     from .abuse import AbuseGpu
-    g = AbuseGpu(local.store, to_device(compile_onnx(am), str(local.device)), buckets=cfg.gpu.buckets)
+    g = AbuseGpu(local.store, to_device(compile_onnx(am), str(local.device), cfg.abuse_model.precision),
+                 buckets=cfg.gpu.buckets)
     g.capture()
     return g
 

@@ -245,7 +245,7 @@ def test_mailbox_routes_accounts_to_their_owner_rank():
     tabs = []
     for o in range(2):
         mine = [a for a, w in zip(ids, owners) if w == o]
-        slots = idx[o].lookup(mine, True)
+        slots, _ = idx[o].lookup(mine, True)
         rows = np.zeros((64, 25), np.float32)
         present = np.zeros(64, np.uint8)
         for s, a in zip(slots, mine):

@@ -363,3 +363,35 @@ def test_account_index_batch_lookup_with_owner_mask():
     assert list(s) == [0, -1, 0, 1] and list(f) == [1, 0, 0, 1]
     s, _ = ix.lookup_batch(rb, False)
     assert list(s) == [0, -1, 0, 1] and ix.id_of(1) == "z" and list(rb.account_id) == ["x", "y", "x", "z"]
+
+
+def test_account_index_inline_keys_keep_exact_identity():
+    """32-byte entries with inline keys (account_index.h): canonical UUIDs are stored as 16
+    binary bytes, short ids verbatim, long ids as a prefix confirmed against the arena. Identity
+    stays the exact string under forced digest collisions: case variants of a UUID, ids that
+    share a 16-byte prefix and short ids are all distinct slots; repeats resolve to their slot
+    through the batch path and the single-id path alike."""
+    from igaming_platform_amd.native import native
+    N = native()
+    ix = N.AccountIndex(64)
+    ids = ["3f2b8c1e-9a4d-4e2b-8f6a-0c1d2e3f4a5b", "3F2B8C1E-9A4D-4E2B-8F6A-0C1D2E3F4A5B",
+           "3f2b8c1e-9a4d-4e2b-8f6a-0c1d2e3f4a5c", "short-1", "short-2", "",
+           "a-long-account-identifier-0001", "a-long-account-identifier-0002", "3f2b8c1e9a4d4e2b8f6a0c1d2e3f4a5b",
+           "3f2b8c1e-9a4d-4e2b-8f6a-0c1d2e3f4a5g"]  # not hex: the non-UUID encoding
+    forced = [0x1234] * len(ids)           # every id on one digest: only the key / arena tells them apart
+    forced[5] = 0                          # the empty id has digest 0 (absent)
+    slots, fresh = ix.lookup(ids, True, forced)
+    live = [s for i, s in enumerate(slots) if i != 5]
+    assert slots[5] == -1 and len(set(live)) == len(live) and all(fresh[i] for i in range(len(ids)) if i != 5)
+    again, fresh2 = ix.lookup(ids[::-1], False, forced[::-1])
+    assert list(again[::-1]) == list(slots) and not any(fresh2)
+    for i, a in enumerate(ids):
+        if i != 5:
+            assert ix.id_of(int(slots[i])) == a
+    assert ix.collisions >= len(live) - 1
+    # the batch path (RequestBatch digests) agrees with the single-id path on real digests
+    ix2 = N.AccountIndex(256)
+    real = [f"{i:08x}-1111-4222-8333-{i:012x}" for i in range(100)] + [f"user-{i}" for i in range(50)]
+    s1, _ = ix2.lookup(real, True)
+    s2, f2 = ix2.lookup(real, False)
+    assert list(s1) == list(s2) and not any(f2) and sorted(s1) == list(range(150))
