@@ -723,24 +723,6 @@ __global__ void update_single_kernel(UpdateArgs a) {
   if (r.slot >= 0 && row_owned(r, *a.cfg)) update_event(a, upd_region(a), i, r.slot);
 }
 
-// account s has more events in the batch than its dedup list holds: find them in row order
-// (64 rows per ballot) and apply them one by one on lane 0 (degenerate traffic only)
-__device__ void apply_scan_serial(const UpdateArgs& a, int s, int lane) {
-  const int n = upd_n(a);
-  AcctRT r = a.rt[s];
-  for (int base = 0; base < n; base += 64) {
-    const int i = base + lane;
-    const bool m = i < n && a.req[i].slot == s && row_owned(a.req[i], *a.cfg);
-    uint64_t b = __ballot(m);
-    while (b) {
-      const int l = __ffsll((long long)b) - 1;
-      b &= b - 1;
-      if (lane == 0) apply_event(a, base + l, r);
-    }
-  }
-  if (lane == 0) a.rt[s] = r;
-}
-
 // PFADD of up to 64 same-account events at once: the per-register winner writes the max,
 // each event learns whether it raised its register (the GRU's new-device/new-ip feature)
 // exactly as the sequential order would have.
@@ -775,24 +757,12 @@ __device__ __forceinline__ uint32_t hll_segment(const UpdateArgs& a, uint8_t* rg
   return (uint32_t)(tlast + a.cfg->hll_ttl);
 }
 
-// the c (>= 2) events of account s (dedup hash slot h) in row order, by one wave holding the
-// account's pre-batch AcctRT `r`: events sorted in registers and applied in parallel when
-// the segment spans less than the shortest TTL (then no key can expire mid-segment);
-// otherwise lane 0 applies them one by one; more than DEDUP_LIST events: ordered batch scan.
-__device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h, int c, int s, AcctRT r,
-                                   int lane) {
-  if (c > DEDUP_LIST) {
-    apply_scan_serial(a, s, lane);
-    return;
-  }
-  // sort the (distinct) row indices: rank = #smaller, then push each to lane `rank`
-  // sc1 load: the entries come from other waves of the same launch (feature_assemble hand-off)
-  const int raw = __hip_atomic_load(&t.list[(size_t)h * DEDUP_LIST + lane], __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);  // all 64 lanes: no wait on c first
-  const int key = lane < c ? raw : (0x7fffffc0 | lane);
-  int rank = 0;
-  for (int y = 0; y < c; ++y) rank += __shfl(key, y, 64) < key;  // lanes >= c hold sentinels
-  const int j = __builtin_amdgcn_ds_permute(rank * 4, key);
+// Apply c (1..64) events of account s, held in row order by lanes 0..c-1 (`j` = the lane's
+// request row), to the account's AcctRT `r` (the same value in every lane, updated in place):
+// in parallel when the events span less than the shortest TTL (then no key can expire
+// mid-chunk: on the scorer path every event of a batch happens at the batch clock, span 0);
+// otherwise lane 0 applies them one by one. The caller stores r.
+__device__ void apply_chunk(const UpdateArgs& a, int s, AcctRT& r, int j, int c, int lane) {
   const bool act = lane < c;
   ReqRec ev{};
   if (act) ev = a.req[j];
@@ -804,14 +774,24 @@ __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h
   const int64_t big = 0x3fffffffffffffffLL;
   const int64_t tmx = wave_max(act ? ts : -big);
   const int64_t tmn = -wave_max(act ? -ts : -big);
-  // parallel apply is exact when the segment spans less than the shortest TTL (no key can
-  // expire mid-segment); otherwise lane 0 applies the sorted events one by one
   if (tmx - tmn >= (int64_t)min_ttl) {
     for (int x = 0; x < c; ++x) {
       const int jx = __shfl(j, x, 64);
       if (lane == 0) apply_event(a, jx, r);
     }
-    if (lane == 0) a.rt[s] = r;
+    // every lane continues with lane 0's state
+    r.ring_head = __shfl(r.ring_head, 0, 64);
+    r.ev_head = __shfl(r.ev_head, 0, 64);
+    r.ev_count = __shfl(r.ev_count, 0, 64);
+    r.sum_compat = __shfl(r.sum_compat, 0, 64);
+    r.sum_exp = (uint32_t)__shfl((int)r.sum_exp, 0, 64);
+    r.hll_dev_exp = (uint32_t)__shfl((int)r.hll_dev_exp, 0, 64);
+    r.hll_ip_exp = (uint32_t)__shfl((int)r.hll_ip_exp, 0, 64);
+    r.last_tx = (uint32_t)__shfl((int)r.last_tx, 0, 64);
+    r.last_tx_exp = (uint32_t)__shfl((int)r.last_tx_exp, 0, 64);
+    r.session_start = (uint32_t)__shfl((int)r.session_start, 0, 64);
+    r.session_exp = (uint32_t)__shfl((int)r.session_exp, 0, 64);
+    r.last_event_ts = (uint32_t)__shfl((int)r.last_event_ts, 0, 64);
     return;
   }
   const int64_t amt = act ? ev.amount : 0;
@@ -833,6 +813,8 @@ __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h
   const int pi = iq ? (int)regs[256 + (iq & 255u)] : 0;
   r.hll_dev_exp = hll_segment(a, regs, r.hll_dev_exp, dq, ts, lane, new_dev, pd);
   r.hll_ip_exp = hll_segment(a, regs + 256, r.hll_ip_exp, iq, ts, lane, new_ip, pi);
+  // the next chunk re-reads registers this one wrote (other lanes' stores)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   // last tx / session
   if (ts0 >= (int64_t)r.session_exp || r.session_start == 0) r.session_start = (uint32_t)ts0;
   r.session_exp = (uint32_t)(tsl + cfg.session_ttl);
@@ -852,6 +834,59 @@ __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h
   }
   r.ring_head = (r.ring_head + c) % a.ring_size;
   r.last_event_ts = (uint32_t)tsl;
+}
+
+// account s has more events in the batch than its dedup list holds (a hot account: Zipf
+// traffic gives the top account hundreds of rows in an 8192-row batch): scan the batch 64 rows
+// per ballot, compact the account's rows (row order) into a 64-event chunk in registers and
+// apply full chunks in parallel (apply_chunk); the chunk carries over between windows.
+__device__ void apply_scan_chunks(const UpdateArgs& a, int s, AcctRT r, int lane) {
+  const int n = upd_n(a);
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes below this one
+  int pj = 0, p = 0;  // pending chunk: lane k < p holds its k-th row
+  for (int base = 0; base < n; base += 64) {
+    const int i = base + lane;
+    const bool m = i < n && a.req[i].slot == s && row_owned(a.req[i], *a.cfg);
+    const uint64_t b = __ballot(m);
+    if (!b) continue;
+    const int cw = __popcll(b);
+    // the window's rows compacted to lanes 0..cw-1 (a push permute; other lanes fill behind)
+    const int dst = m ? __popcll(b & lt) : cw + __popcll(~b & lt);
+    const int wj = __builtin_amdgcn_ds_permute(dst * 4, i);
+    // append to the pending chunk: lanes p..p+cw-1 take window rows 0..cw-1
+    const int take = __shfl(wj, lane >= p ? lane - p : 0, 64);
+    if (lane >= p && lane < p + cw) pj = take;
+    if (p + cw < 64) {
+      p += cw;
+      continue;
+    }
+    apply_chunk(a, s, r, pj, 64, lane);
+    const int over = p + cw - 64;  // window rows that did not fit: the next chunk's head
+    const int rest = __shfl(wj, min(lane + 64 - p, 63), 64);
+    if (lane < over) pj = rest;
+    p = over;
+  }
+  if (p > 0) apply_chunk(a, s, r, pj, p, lane);
+  if (lane == 0) a.rt[s] = r;
+}
+
+// the c (>= 2) events of account s (dedup hash slot h) in row order, by one wave holding the
+// account's pre-batch AcctRT `r`; more than DEDUP_LIST events: the chunked batch scan.
+__device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h, int c, int s, AcctRT r,
+                                   int lane) {
+  if (c > DEDUP_LIST) {
+    apply_scan_chunks(a, s, r, lane);
+    return;
+  }
+  // sort the (distinct) row indices: rank = #smaller, then push each to lane `rank`
+  // sc1 load: the entries come from other waves of the same launch (feature_assemble hand-off)
+  const int raw = __hip_atomic_load(&t.list[(size_t)h * DEDUP_LIST + lane], __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);  // all 64 lanes: no wait on c first
+  const int key = lane < c ? raw : (0x7fffffc0 | lane);
+  int rank = 0;
+  for (int y = 0; y < c; ++y) rank += __shfl(key, y, 64) < key;  // lanes >= c hold sentinels
+  const int j = __builtin_amdgcn_ds_permute(rank * 4, key);
+  apply_chunk(a, s, r, j, c, lane);
   if (lane == 0) a.rt[s] = r;
 }
 

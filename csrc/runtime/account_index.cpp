@@ -93,32 +93,34 @@ int32_t AccountIndex::published(const Entry& e) const {
   return st > 0 ? st - 1 : -1;
 }
 
-static int hexv(char c) {
-  if (c >= '0' && c <= '9') return c - '0';
-  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
-  return -1;  // upper case is not the canonical form: such ids take the non-UUID encoding
-}
+namespace {
+// char -> hex digit value; 0x10 marks a char that is not a lower-case hex digit (upper case is not
+// the canonical UUID form: such ids take the non-UUID encoding)
+struct HexTable {
+  uint8_t v[256];
+  constexpr HexTable() : v() {
+    for (int i = 0; i < 256; ++i) v[i] = 0x10;
+    for (int i = 0; i < 10; ++i) v['0' + i] = uint8_t(i);
+    for (int i = 0; i < 6; ++i) v['a' + i] = uint8_t(10 + i);
+  }
+};
+constexpr HexTable kHex;
+// byte k of a canonical UUID = hex pair at these string positions (hyphens at 8, 13, 18, 23)
+constexpr uint8_t kPos[16] = {0, 2, 4, 6, 9, 11, 14, 16, 19, 21, 24, 26, 28, 30, 32, 34};
+}  // namespace
 
 uint32_t AccountIndex::encode_key(std::string_view id, uint8_t key[16]) {
-  std::memset(key, 0, 16);
-  if (id.size() == 36 && id[8] == '-' && id[13] == '-' && id[18] == '-' && id[23] == '-') {
-    int b = 0, hi = -1;
-    bool ok = true;
-    for (size_t i = 0; i < 36 && ok; ++i) {
-      if (i == 8 || i == 13 || i == 18 || i == 23) continue;
-      const int v = hexv(id[i]);
-      if (v < 0) {
-        ok = false;
-      } else if (hi < 0) {
-        hi = v;
-      } else {
-        key[b++] = uint8_t(hi << 4 | v);
-        hi = -1;
-      }
+  const unsigned char* c = reinterpret_cast<const unsigned char*>(id.data());
+  if (id.size() == 36 && c[8] == '-' && c[13] == '-' && c[18] == '-' && c[23] == '-') {
+    uint32_t bad = 0;  // branch-free: 32 table lookups, one check at the end
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t hi = kHex.v[c[kPos[k]]], lo = kHex.v[c[kPos[k] + 1]];
+      bad |= hi | lo;
+      key[k] = uint8_t(hi << 4 | lo);
     }
-    if (ok) return kExact | kUuid;
-    std::memset(key, 0, 16);
+    if (!(bad & 0x10)) return kExact | kUuid;
   }
+  std::memset(key, 0, 16);
   if (id.size() <= 15) {
     key[0] = uint8_t(id.size());
     std::memcpy(key + 1, id.data(), id.size());

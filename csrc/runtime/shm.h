@@ -35,6 +35,7 @@ class Region {
     Region r;
     void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
     if (p == MAP_FAILED) throw std::runtime_error("Region: anonymous mmap of " + std::to_string(bytes) + " bytes failed");
+    hugepages(p, bytes);
     r.base_ = p;
     r.bytes_ = bytes;
     return r;
@@ -69,6 +70,7 @@ class Region {
     void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_NORESERVE, fd, 0);
     ::close(fd);
     if (p == MAP_FAILED) throw std::runtime_error("Region: mmap " + r.path_ + " failed");
+    hugepages(p, bytes);
     r.base_ = p;
     r.bytes_ = bytes;
     return r;
@@ -78,6 +80,12 @@ class Region {
   void unlink() {
     if (!path_.empty()) ::unlink(path_.c_str());
     unlink_ = false;
+  }
+  // transparent huge pages for large tables: the hash tables are probed at random (an
+  // AccountIndex lookup per request row), so with 4 KiB pages nearly every probe also misses the
+  // TLB; a no-op where THP is off (shmem THP follows /sys/kernel/mm/transparent_hugepage/shmem_enabled)
+  static void hugepages(void* p, size_t bytes) {
+    if (bytes >= (size_t(8) << 20)) (void)madvise(p, bytes, MADV_HUGEPAGE);
   }
   void* base() const { return base_; }
   size_t bytes() const { return bytes_; }
