@@ -882,7 +882,8 @@ PYBIND11_MODULE(_native, m) {
       .def_static("now_ns", &ServeCore::now_ns)
       .def_static("last_timings", []() {  // this thread's last score_batch call, ns per stage
         const CallTimings& t = last_timings_tl();
-        return py::make_tuple(t.parse, t.resolve, t.queue, t.device, t.serialize, t.total, t.rows);
+        return py::make_tuple(t.parse, t.resolve, t.queue, t.device, t.serialize, t.total, t.rows, t.seq_first,
+                              t.seq_last);
       });
 
   // ---- account RPCs (acct_core.h): PredictLTV / GetPlayerSegment / CheckBonusAbuse

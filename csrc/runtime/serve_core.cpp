@@ -56,6 +56,7 @@ struct ServeCore::Item {
   uint64_t tag = 0;
   int64_t t0 = 0, t_enq = 0;
   int64_t t_issue = 0;          // the first step holding rows of this item was formed (q_mu_)
+  int32_t seq_first = 0, seq_last = 0;  // batch sequence numbers of its first / last step (q_mu_)
   // completion hand-off (m)
   std::mutex m;
   std::condition_variable cv;
@@ -253,7 +254,8 @@ std::string_view ServeCore::score_batch_view(const char* data, size_t n, int64_t
   const int64_t te = now_ns();
   // this call's stage times (last_timings(): per-request tails, not only sums)
   CallTimings& ct = last_timings_tl();
-  ct = CallTimings{tb - ta, tc - tb, it.t_issue - tq, td - it.t_issue, te - td, te - t0, int64_t(it.n)};
+  ct = CallTimings{tb - ta, tc - tb, it.t_issue - tq, td - it.t_issue, te - td, te - t0, int64_t(it.n), it.seq_first,
+                   it.seq_last};
   a_parse_.fetch_add(tb - ta, std::memory_order_relaxed);
   a_resolve_.fetch_add(tc - tb, std::memory_order_relaxed);
   a_serialize_.fetch_add(te - td, std::memory_order_relaxed);
@@ -444,6 +446,10 @@ bool ServeCore::issue_step(std::unique_lock<std::mutex>& lk, bool allow_empty) {
   if (now == 0) now = wall_s();
   const int32_t seq = ++seq_;
   st->seq = seq;
+  for (const Seg& sg : st->segs) {  // the steps an item's rows ride in (the ordering contract, dp.py)
+    if (!sg.item->seq_first) sg.item->seq_first = seq;
+    sg.item->seq_last = seq;
+  }
   lk.unlock();
   // pack the rows into the slot's pinned buffer (outside the queue lock)
   const int64_t t0 = now_ns();

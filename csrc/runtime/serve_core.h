@@ -77,6 +77,7 @@ class StepClock {
 // step formed), device (first step formed -> every row back, incl. the copy out), serialize, total
 struct CallTimings {
   int64_t parse = 0, resolve = 0, queue = 0, device = 0, serialize = 0, total = 0, rows = 0;
+  int32_t seq_first = 0, seq_last = 0;  // the batch sequence numbers of the first / last step of its rows
 };
 // the calling thread's last score_batch / score_batch_view timings
 inline CallTimings& last_timings_tl() {

@@ -14,6 +14,21 @@ row-count read-back):
 Each GPU scores only its own accounts' rows (``senders * C`` rows at most per batch: one
 sender for the serving front end on rank 0, every rank in ``bench.py --gpus N``). With a
 world of 1 the same code runs through RCCL's single-rank path (tests on a 1-GPU box).
+
+Ordering contract for one account reached through several ingress ranks (two wallet
+connections landing on different ranks under SO_REUSEPORT). Every rank issues the same
+sequence of exchange steps (the step clock). A request's rows ride in the step its rank's
+serving core formed when it took them from its FIFO (``ServeCore.last_timings()`` reports the
+step); within a step the owner compacts the rows by sender rank, then by the sender's row order
+(the sender's FIFO order, then the request's row order), scores every row of the step against
+the account state the previous steps left (score-then-update, engine.go:485-488, batch
+semantics: rows of one step do not see each other), and applies the rows' events in that same
+(step, sender rank, row) order, each exactly once. The responses and the resulting state are
+therefore those of a single engine fed, step by step, the senders' rows concatenated in rank
+order (tests/test_dist.py ``test_cross_ingress_ordering_contract_same_accounts``,
+tests/test_dp_gpu.py ``test_exchange_world1_same_accounts_in_one_step_follow_fifo_order``).
+Which step a request lands in depends on arrival time, exactly as the order of two
+independent connections to one server does.
 """
 from __future__ import annotations
 

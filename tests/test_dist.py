@@ -246,3 +246,122 @@ def test_exchange_stream_plan_fits_four_hardware_queues():
     assert len(set(DP.stream_roles("3").values())) == DP.HW_QUEUES
     assert len(set(DP.stream_roles("5").values())) > DP.HW_QUEUES
     assert DP.EXCHANGE_COMMUNICATORS == 2
+
+
+# ----------------------------------------------------------------------------- ordering contract
+SHARED_ROUNDS = 5
+
+
+def _shared_payload(rank, rnd, n=30):
+    """ScoreBatchRequest bytes over the SAME 10 accounts on every rank (cross-ingress traffic)."""
+    from igaming_platform_amd.proto import risk_v1 as P
+    rng = np.random.default_rng(7000 + 100 * rank + rnd)
+    types = ["deposit", "withdraw", "bet", "win"]
+    txs = [P.ScoreTransactionRequest(account_id=f"shared-{int(a)}", amount=int(rng.choice([500, 150000, 2_000_000])),
+                                     transaction_type=types[int(rng.integers(0, 4))], device_id=f"sd{rank}-{int(a) % 3}",
+                                     ip_address=f"10.9.{rank}.{int(a)}")
+           for a in rng.integers(0, 10, n)]
+    return P.ScoreBatchRequest(transactions=txs).SerializeToString()
+
+
+def _shared_worker(rank, world, port, q, barrier):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.engine.risk_engine import RiskEngine, serve_shard
+    from igaming_platform_amd.parallel.comm import TorchComm
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = TorchComm("gloo")
+
+    def rounds(core):
+        import threading
+        import time
+        out = []
+        for k in range(SHARED_ROUNDS):
+            barrier.wait(60)
+            box = {}
+
+            def call():
+                box["resp"] = core.score_batch(_shared_payload(rank, k), NOW + 10 * k, 0)
+                box["t"] = type(core).last_timings()
+            if k % 2:
+                # odd rounds: every rank's request is queued before any rank issues the step, so
+                # the owners receive rows of the same accounts from several senders in ONE step
+                core.pause()
+                th = threading.Thread(target=call)
+                th.start()
+                while core.pending_items() < 1:
+                    time.sleep(0.001)
+                barrier.wait(60)
+                core.resume()
+                th.join()
+            else:  # even rounds: free-running (each rank's request may get a step of its own)
+                call()
+            t = box["t"]
+            out.append((k, int(t[7]), int(t[8]), _decode(box["resp"])))
+            barrier.wait(60)
+        return out
+    try:
+        if rank == 0:
+            eng = RiskEngine(Config(), backend="cpu", capacity=256, spmd=comm)
+            got = rounds(eng.core)
+            feats = [_noslot(eng.get_features(f"shared-{i}", now=NOW + 100)) for i in range(10)]
+            eng.close()
+            q.put(("ok", 0, got, feats))
+        else:
+            box = {}
+
+            def ingress(node):
+                box["got"] = rounds(node.core)
+            serve_shard(Config(), comm, backend="cpu", capacity=256, ingress=ingress)
+            q.put(("ingress", rank, box["got"], None))
+    except Exception:  # pragma: no cover - surfaced by the parent
+        import traceback
+        q.put(("err", traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_cross_ingress_ordering_contract_same_accounts(world):
+    """Every rank ingests transactions of the SAME accounts in the same rounds.
+    The contract (engine/dp.py): an owner applies the rows of one exchange step in (step,
+    sender-rank, row) order, and every row of a step is scored against the state left by the
+    previous steps. So the responses and the final features must equal a single-process engine
+    fed, step by step, the concatenation of the senders' requests in rank order - every row
+    applied exactly once, each response seeing exactly the events ordered before it."""
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.engine.risk_engine import RiskEngine
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    barrier = ctx.Barrier(world)
+    port = _free_port()
+    procs = [ctx.Process(target=_shared_worker, args=(r, world, port, q, barrier)) for r in range(world)]
+    [p.start() for p in procs]
+    msgs = [q.get(timeout=240) for _ in range(world)]
+    [p.join(timeout=60) for p in procs]
+    errs = [m[1] for m in msgs if m[0] == "err"]
+    assert not errs, errs[0]
+    by_rank = {m[1]: m[2] for m in msgs}
+    # every request rode in exactly one exchange step; group the requests by step
+    steps = {}
+    for r, got in by_rank.items():
+        for k, s0, s1, resp in got:
+            assert s0 == s1 and s0 > 0, (r, k, s0, s1)
+            steps.setdefault(s0, []).append((r, k, resp))
+    ref = RiskEngine(Config(), backend="cpu", capacity=256, shards=world)
+    from igaming_platform_amd.proto import risk_v1 as P
+    for seq in sorted(steps):
+        members = sorted(steps[seq])                          # sender-rank order within the step
+        assert len({k for _, k, _ in members}) == 1           # one round per step (barriers)
+        k = members[0][1]
+        txs = [t for r, _, _ in members for t in P.ScoreBatchRequest.FromString(_shared_payload(r, k)).transactions]
+        want = _decode(ref.score_batch_bytes(P.ScoreBatchRequest(transactions=txs).SerializeToString(), now=NOW + 10 * k))
+        off = 0
+        for r, _, resp in members:
+            assert resp == want[off:off + len(resp)], f"step {seq}: rank {r}'s responses differ"
+            off += len(resp)
+    feats = next(m[3] for m in msgs if m[0] == "ok")
+    assert feats == [_noslot(ref.get_features(f"shared-{i}", now=NOW + 100)) for i in range(10)]
+    # the shared accounts really were hit by several ranks within one step
+    assert any(len(v) > 1 for v in steps.values())

@@ -186,3 +186,66 @@ def test_exchange_rank_fits_the_hardware_queue_budget():
     assert m["rows_a2a"] == m["h2d"] and m["results_a2a"] == m["model"]  # the collectives share streams
     assert len(sc.comms) == DP.EXCHANGE_COMMUNICATORS == 2
     assert not dist.is_initialized() or dist.get_backend() != "nccl"
+
+
+def test_exchange_world1_same_accounts_in_one_step_follow_fifo_order():
+    """The ordering contract on the GPU exchange (engine/dp.py) at world 1: two ScoreBatch
+    requests over the same accounts queued into ONE exchange step are applied in FIFO (then row)
+    order and scored against the pre-step state - equal to a plain GPU engine scoring their
+    concatenation as one batch; the next step sees both."""
+    import threading
+    import time
+    import torch
+    import torch.distributed as dist
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.engine.risk_engine import RiskEngine
+    from igaming_platform_amd.parallel.comm import TorchComm
+    from igaming_platform_amd.proto import risk_v1 as P
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        cfg = Config()
+        cfg.gpu.buckets = [64, 256]
+        spmd = RiskEngine(cfg, backend="gpu", capacity=1024, spmd=TorchComm("nccl", "cuda:0"))
+        plain = RiskEngine(cfg, backend="gpu", capacity=1024)
+        rng = np.random.default_rng(4)
+        types = ["deposit", "withdraw", "bet", "win"]
+
+        def payload(n):
+            return P.ScoreBatchRequest(transactions=[
+                P.ScoreTransactionRequest(account_id=f"same-{int(a)}", amount=int(rng.choice([500, 150000, 2_000_000])),
+                                          transaction_type=types[int(rng.integers(0, 4))],
+                                          device_id=f"dv-{int(rng.integers(0, 9))}", ip_address=f"10.7.{int(a)}.1")
+                for a in rng.integers(0, 6, n)]).SerializeToString()
+
+        def decode(b):
+            out = []
+            for x in P.ScoreBatchResponse.FromString(b).results:
+                x.response_time_ms = 0
+                out.append(x.SerializeToString())
+            return out
+        core = spmd.core
+        for rnd in range(3):
+            reqs = [payload(40), payload(25)]
+            now = NOW + 30 * rnd
+            got, seqs = [None, None], [None, None]
+
+            def call(i):
+                got[i] = decode(core.score_batch(reqs[i], now, 0))
+                seqs[i] = type(core).last_timings()[7]
+            core.pause()
+            th = []
+            for i in range(2):  # queued in this order, both before the step is formed
+                th.append(threading.Thread(target=call, args=(i,)))
+                th[-1].start()
+                while core.pending_items() < i + 1:
+                    time.sleep(0.001)
+            core.resume()
+            [t.join() for t in th]
+            assert seqs[0] == seqs[1]  # one exchange step
+            txs = [t for r in reqs for t in P.ScoreBatchRequest.FromString(r).transactions]
+            want = decode(plain.score_batch_bytes(P.ScoreBatchRequest(transactions=txs).SerializeToString(), now=now))
+            assert got[0] + got[1] == want
+        spmd.close()
+    finally:
+        dist.destroy_process_group()
