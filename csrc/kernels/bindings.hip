@@ -323,6 +323,27 @@ PYBIND11_MODULE(_hipk, m) {
     const GemmArgs a = gemm_args(d);
     launch_or_record([a](hipStream_t st) { launch_gemv(a, st); }, s, "gemv");
   });
+  m.def("join", [](py::dict d, uintptr_t s) {
+    JoinArgs a{};
+    a.A = ptr<const void*>(d, "A");
+    a.B = ptr<const void*>(d, "B");
+    a.Y = ptr<void*>(d, "Y");
+    a.m_ptr = ptr<const int32_t*>(d, "m_ptr");
+    a.M = geti(d, "M");
+    a.na = geti(d, "na");
+    a.nb = geti(d, "nb");
+    a.op = geti(d, "op");
+    a.lda = geti(d, "lda");
+    a.ldb = geti(d, "ldb");
+    a.ldy = geti(d, "ldy");
+    a.a_bf16 = geti(d, "a_bf16");
+    a.b_bf16 = geti(d, "b_bf16");
+    a.y_bf16 = geti(d, "y_bf16");
+    if (!a.A || !a.B || !a.Y || a.na < 1 || (a.op != 0 && a.op != 1)) throw std::runtime_error("join: args");
+    if (a.op == 0 && a.nb != a.na) throw std::runtime_error("join: add needs equal widths");
+    if (a.op == 1 && a.nb < 1) throw std::runtime_error("join: concat widths");
+    launch_or_record([a](hipStream_t st) { launch_join(a, st); }, s, "join");
+  });
 
   auto head_args = [](const py::dict& d) {
     HeadArgs a{};

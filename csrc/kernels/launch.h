@@ -169,6 +169,18 @@ struct GemmArgs {
 void launch_gemm(const GemmArgs& a, hipStream_t st);
 void launch_gemv(const GemmArgs& a, hipStream_t st);  // N == 1 heads
 
+// DAG join of two branches (join.hip): op 0 Y = A + B (na columns), op 1 Y = [A | B]
+struct JoinArgs {
+  const void* A;
+  const void* B;
+  void* Y;
+  const int32_t* m_ptr;     // live rows in device memory (nullable -> M)
+  int32_t M, na, nb, op;
+  int32_t lda, ldb, ldy;
+  int32_t a_bf16, b_bf16, y_bf16;
+};
+void launch_join(const JoinArgs& a, hipStream_t st);
+
 // dense(N1) + act1 + dense(N1 -> 1) + act2 fused; W1 bf16 [N1_pad(64)][k_pad(32)]
 // ---- K5 ensemble + action + metrics
 struct HeadArgs {

@@ -10,6 +10,7 @@ enum TreePostKind : int { TP_NONE = 0, TP_LOGISTIC = 1, TP_SOFTMAX = 2, TP_SOFTM
 
 // Giles' single-precision erfinv (same coefficients and order as the executor)
 __device__ __forceinline__ float tp_erfinv(float x) {
+  if (!(fabsf(x) < 1.0f)) return isnan(x) ? x : copysignf(INFINITY, x);  // the domain edge (p = 0 or 1)
   float w = -logf((1.0f - x) * (1.0f + x)), p;
   if (w < 5.0f) {
     w -= 2.5f;

@@ -201,6 +201,102 @@ void gru(const onnx::Node& n, const Tensor& X, const Tensor& W, const Tensor& R,
   }
 }
 
+// ---- ai.onnx.ml linear models and preprocessing (sklearn-style pipelines: Scaler ->
+// LinearClassifier -> ZipMap; Normalizer; LinearRegressor). Semantics follow the ai.onnx.ml
+// operator definitions; ORT itself is not available offline, so exact ORT parity is unpinned
+// (tests compare against numpy references of the definitions below).
+
+int32_t post_code(const onnx::Node& n) {
+  const std::string p = n.gets("post_transform", "NONE");
+  if (p == "NONE") return trees::NONE;
+  if (p == "LOGISTIC") return trees::LOGISTIC;
+  if (p == "SOFTMAX") return trees::SOFTMAX;
+  if (p == "SOFTMAX_ZERO") return trees::SOFTMAX_ZERO;
+  if (p == "PROBIT") return trees::PROBIT;
+  throw std::runtime_error(n.op_type + ": unknown post_transform " + p);
+}
+
+// one row of K scores through a post transform, in place
+void post_row(int32_t post, float* z, int64_t k) {
+  if (post == trees::LOGISTIC) {
+    for (int64_t c = 0; c < k; ++c) z[c] = sigmoid(z[c]);
+  } else if (post == trees::SOFTMAX || post == trees::SOFTMAX_ZERO) {
+    const bool zero = post == trees::SOFTMAX_ZERO;
+    float m = -INFINITY;
+    for (int64_t c = 0; c < k; ++c) if (!(zero && z[c] == 0.f)) m = std::max(m, z[c]);
+    double s = 0;
+    for (int64_t c = 0; c < k; ++c) {
+      if (zero && z[c] == 0.f) continue;
+      z[c] = std::exp(z[c] - m);
+      s += z[c];
+    }
+    for (int64_t c = 0; c < k; ++c) z[c] = (zero && z[c] == 0.f) || s <= 0 ? 0.f : float(z[c] / s);
+  } else if (post == trees::PROBIT) {
+    for (int64_t c = 0; c < k; ++c) z[c] = 1.41421356f * trees::erfinv(2 * z[c] - 1);
+  }
+}
+
+// rows of X ([N][C], or one row [C]) times coefficient rows W [E][C] plus intercepts: [N][E]
+std::vector<float> linear_rows(const std::string& op, const Tensor& X, const std::vector<float>& W,
+                               const std::vector<float>& b, int64_t E, int64_t& N) {
+  const auto x = as_float(X);
+  const int64_t C = X.dims.empty() ? 1 : X.dims.back();
+  N = X.dims.size() <= 1 ? 1 : X.numel() / std::max<int64_t>(C, 1);
+  if (E < 1 || int64_t(W.size()) != E * C) throw std::runtime_error(op + ": coefficients do not match [E][C]");
+  if (!b.empty() && int64_t(b.size()) != E) throw std::runtime_error(op + ": intercepts do not match E");
+  std::vector<float> y(size_t(N * E));
+  for (int64_t i = 0; i < N; ++i)
+    for (int64_t e = 0; e < E; ++e) {
+      double s = b.empty() ? 0.0 : double(b[e]);
+      for (int64_t c = 0; c < C; ++c) s += double(W[e * C + c]) * double(x[i * C + c]);
+      y[i * E + e] = float(s);
+    }
+  return y;
+}
+
+const std::vector<float>& attr_floats(const onnx::Node& n, const char* name) {
+  static const std::vector<float> none;
+  auto a = n.attr(name);
+  return a ? a->floats : none;
+}
+
+// LinearClassifier: outputs (label [N] int64, scores [N][K]). One coefficient row is the binary
+// case: raw score s becomes the two columns [-s, s] before the post transform (LOGISTIC then
+// gives [sigmoid(-s), sigmoid(s)]) and the label is classlabels[s > 0]. E rows: label =
+// classlabels[argmax raw]. String class labels yield the class index as the label.
+void linear_classifier(const onnx::Node& n, const Tensor& X, Tensor& labels, Tensor& scores) {
+  const auto& W = attr_floats(n, "coefficients");
+  const auto& b = attr_floats(n, "intercepts");
+  const int64_t C = X.dims.empty() ? 1 : X.dims.back();
+  const int64_t E = !b.empty() ? int64_t(b.size()) : int64_t(W.size()) / std::max<int64_t>(C, 1);
+  std::vector<int64_t> cl;
+  if (auto a = n.attr("classlabels_ints")) cl = a->ints;
+  else if (auto s = n.attr("classlabels_strings"))
+    for (size_t k = 0; k < s->strings.size(); ++k) cl.push_back(int64_t(k));
+  int64_t N = 0;
+  auto raw = linear_rows(n.op_type, X, W, b, E, N);
+  const int32_t post = post_code(n);
+  const int64_t K = E == 1 ? 2 : E;
+  labels = make({N}, INT64);
+  scores = make({N, K});
+  for (int64_t i = 0; i < N; ++i) {
+    float* z = &scores.f[i * K];
+    int64_t best = 0;
+    if (E == 1) {
+      z[0] = -raw[i];
+      z[1] = raw[i];
+      best = raw[i] > 0.f ? 1 : 0;
+    } else {
+      for (int64_t e = 0; e < E; ++e) {
+        z[e] = raw[i * E + e];
+        if (z[e] > z[best]) best = e;
+      }
+    }
+    post_row(post, z, K);
+    labels.i[i] = best < int64_t(cl.size()) ? cl[best] : best;
+  }
+}
+
 }  // namespace
 
 Executor::Executor(onnx::Model model) : model_(std::move(model)) {
@@ -404,6 +500,62 @@ std::map<std::string, Tensor> Executor::run(const std::map<std::string, Tensor>&
         vals[n.outputs[0]] = probs;
       }
       continue;
+    } else if (op == "LinearClassifier") {
+      Tensor labels, scores;
+      linear_classifier(n, get(n.inputs[0]), labels, scores);
+      vals[n.outputs[0]] = std::move(labels);
+      if (n.outputs.size() > 1) vals[n.outputs[1]] = std::move(scores);
+      continue;
+    } else if (op == "LinearRegressor") {
+      const Tensor& x = get(n.inputs[0]);
+      const int64_t E = n.geti("targets", 1);
+      int64_t N = 0;
+      auto y = linear_rows(op, x, attr_floats(n, "coefficients"), attr_floats(n, "intercepts"), E, N);
+      const int32_t post = post_code(n);
+      out = make({N, E});
+      out.f = std::move(y);
+      for (int64_t i = 0; i < N; ++i) post_row(post, &out.f[i * E], E);
+    } else if (op == "Scaler") {
+      // Y = (X - offset) * scale, offset / scale per column (or one value for all)
+      const Tensor& x = get(n.inputs[0]);
+      const auto& off = attr_floats(n, "offset");
+      const auto& sc = attr_floats(n, "scale");
+      const int64_t C = x.dims.empty() ? 1 : x.dims.back();
+      auto ok = [C](size_t s) { return s == 0 || s == 1 || int64_t(s) == C; };
+      if (!ok(off.size()) || !ok(sc.size())) throw std::runtime_error("Scaler: offset / scale length must be 1 or C");
+      auto xf = as_float(x);
+      out = make(x.dims);
+      for (int64_t e = 0; e < x.numel(); ++e) {
+        const int64_t c = e % C;
+        const float o = off.empty() ? 0.f : off[off.size() == 1 ? 0 : c];
+        const float s = sc.empty() ? 1.f : sc[sc.size() == 1 ? 0 : c];
+        out.f[e] = (xf[e] - o) * s;
+      }
+    } else if (op == "Normalizer") {
+      // per row (last axis): MAX divides by the row maximum, L1 by sum |x|, L2 by sqrt(sum x^2);
+      // a zero denominator leaves the row unchanged
+      const Tensor& x = get(n.inputs[0]);
+      const std::string norm = n.gets("norm", "MAX");
+      if (norm != "MAX" && norm != "L1" && norm != "L2") throw std::runtime_error("Normalizer: norm " + norm);
+      const int64_t C = x.dims.empty() ? 1 : x.dims.back();
+      out = make(x.dims);
+      out.f = as_float(x);
+      for (int64_t r = 0; r < x.numel() / std::max<int64_t>(C, 1); ++r) {
+        float* z = &out.f[r * C];
+        double d = norm == "MAX" ? -INFINITY : 0.0;
+        for (int64_t c = 0; c < C; ++c)
+          d = norm == "MAX" ? std::max(d, double(z[c])) : norm == "L1" ? d + std::fabs(double(z[c]))
+                                                                        : d + double(z[c]) * z[c];
+        if (norm == "L2") d = std::sqrt(d);
+        if (d != 0.0 && std::isfinite(d))
+          for (int64_t c = 0; c < C; ++c) z[c] = float(double(z[c]) / d);
+      }
+    } else if (op == "ZipMap") {
+      // seq(map(label -> probability)) is represented densely: the [N][K] probability tensor,
+      // columns in classlabels order (what every consumer of the model output reads)
+      const Tensor& x = get(n.inputs[0]);
+      out = make(x.dims);
+      out.f = as_float(x);
     } else if (op == "GRU") {
       Tensor Y, Yh;
       gru(n, get(n.inputs[0]), get(n.inputs[1]), get(n.inputs[2]), opt(n, 3),

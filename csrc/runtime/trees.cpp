@@ -55,7 +55,11 @@ inline bool go_true(float x, float thr, uint8_t mode, uint8_t miss) {
   return c || (miss && std::isnan(x));
 }
 
+
+}  // namespace
+
 float erfinv(float x) {  // Giles' single-precision approximation (PROBIT post transform)
+  if (!(std::fabs(x) < 1.0f)) return std::isnan(x) ? x : std::copysign(INFINITY, x);
   float w = -std::log((1.0f - x) * (1.0f + x)), p;
   if (w < 5.0f) {
     w -= 2.5f;
@@ -70,8 +74,6 @@ float erfinv(float x) {  // Giles' single-precision approximation (PROBIT post t
   }
   return p * x;
 }
-
-}  // namespace
 
 Ensemble compile(const onnx::Node& node) {
   Ensemble e;

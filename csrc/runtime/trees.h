@@ -46,6 +46,8 @@ struct Ensemble {
 };
 
 Ensemble compile(const onnx::Node& node);
+// single-precision inverse error function (the PROBIT post transform: sqrt(2) * erfinv(2p - 1))
+float erfinv(float x);
 
 // Per-sample raw scores [N][K] (aggregated, + base values, before post transform).
 void eval_raw(const Ensemble& e, const float* X, int64_t n, int64_t n_feat, float* scores);

@@ -51,13 +51,8 @@ def cpu_model_spec(cfg: Config, fm, mkind: str) -> dict:
     built-in model kind ("heuristic" / "none")."""
     if mkind != "onnx":
         return dict(model=mkind, executor=None, input_name="input", output_name=cfg.fraud_model.output_name, ml_col=0)
-    from ..models.plan import compile_onnx
-    ml_col, out_name = 0, cfg.fraud_model.output_name
-    try:
-        p = compile_onnx(fm)
-        ml_col, out_name = p.ml_col, p.output_name
-    except Exception:
-        pass
+    from ..models.plan import executor_output
+    ml_col, out_name = executor_output(fm, cfg.fraud_model.output_name)
     from ..native import native
     return dict(model="plan", executor=native().Executor(fm), input_name=fm.inputs()[0][0], output_name=out_name,
                 ml_col=ml_col)

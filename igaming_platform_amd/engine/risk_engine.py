@@ -309,13 +309,8 @@ class RiskEngine:
         if kind == "cpu":
             return make_local_backend(self.cfg, "cpu", capacity, fm, mkind, self.blacklist, self.ipintel)
         if mkind == "onnx":
-            ml_col, out_name = 0, self.cfg.fraud_model.output_name
-            try:
-                from ..models.plan import compile_onnx
-                p = compile_onnx(fm)
-                ml_col, out_name = p.ml_col, p.output_name
-            except Exception:
-                pass
+            from ..models.plan import executor_output
+            ml_col, out_name = executor_output(fm, self.cfg.fraud_model.output_name)
             in_name = fm.inputs()[0][0]
             return CpuBackend(self.cfg, model="plan", executor=self.N.Executor(fm), input_name=in_name,
                               output_name=out_name, ml_col=ml_col, blacklist=self.blacklist, ipintel=self.ipintel)
@@ -1053,13 +1048,8 @@ def make_local_backend(cfg: Config, kind: str, capacity: int, fm, mkind: str, bl
     cls = CpuBackend if kind == "golden" else NativeCpuBackend
     kw = {} if kind == "golden" else {"capacity": capacity}
     if mkind == "onnx":
-        from ..models.plan import compile_onnx
-        ml_col, out_name = 0, cfg.fraud_model.output_name
-        try:
-            p = compile_onnx(fm)
-            ml_col, out_name = p.ml_col, p.output_name
-        except Exception:
-            pass
+        from ..models.plan import executor_output
+        ml_col, out_name = executor_output(fm, cfg.fraud_model.output_name)
         return cls(cfg, model="plan", executor=N.Executor(fm), input_name=fm.inputs()[0][0],
                    output_name=out_name, ml_col=ml_col, blacklist=blacklist, ipintel=ipintel, **kw)
     return cls(cfg, model=mkind, blacklist=blacklist, ipintel=ipintel, **kw)

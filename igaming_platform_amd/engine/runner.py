@@ -13,7 +13,7 @@ from typing import Dict, List, Optional, Sequence
 
 import torch
 
-from ..models.plan import Plan
+from ..models.plan import Plan, step_consumers, step_inputs
 from ..ops import kernels as K
 
 
@@ -98,11 +98,13 @@ class DeviceModel:
         self.tree_partial: Optional[torch.Tensor] = None
         self.tree_groups: Dict[int, int] = {}
         steps = plan.steps
+        self.consumers = step_consumers(steps)
         for i, s in enumerate(steps):
             last = i == len(steps) - 1
-            feeds_mma = (not last) and steps[i + 1].kind in ("dense", "head")
-            # bf16 plans hand bf16 activations to the next MFMA layer; fp32 plans stay f32
-            dt = (torch.bfloat16 if (s.kind in ("dense", "gru") and feeds_mma and plan.precision == "bf16")
+            cons = self.consumers[i]
+            feeds_mma = (not last) and bool(cons) and all(steps[j].kind in ("dense", "head", "join") for j in cons)
+            # bf16 plans hand bf16 activations to the MFMA layers reading them; fp32 plans stay f32
+            dt = (torch.bfloat16 if (s.kind in ("dense", "gru", "join") and feeds_mma and plan.precision == "bf16")
                   else torch.float32)
             self.step_out.append(torch.zeros((B, s.out_width), dtype=dt, device=self.device))
             if s.kind == "tree":
@@ -159,17 +161,27 @@ class DeviceModel:
         fused_partial = None
         skip = -1
         one_launch = os.environ.get("IGP_TREE_HEAD", "1") != "0"
+
+        def value(k):
+            return X if k < 0 else self.step_out[k]
         for i, (s, out) in enumerate(zip(steps, self.step_out)):
             if i == skip:
                 cur = out
                 continue
+            if s.kind == "join":  # two branches of a DAG model meet
+                K.join(s.op, value(s.a), value(s.b), out, bucket, s.na, s.nb, m_ptr=m_ptr)
+                fused_partial = None
+                cur = out
+                continue
+            cur = value(step_inputs(steps, i)[0])
             if s.kind == "tree" and s.layout == "sparse":
                 K.tree_sparse(s, cur, out, bucket, partial=self.tree_partial, groups=self.tree_groups.get(bucket, 1))
                 fused_partial = None
             elif s.kind == "tree":
                 g = self.tree_groups.get(bucket, 1)
                 fuse = (g > 1 and i + 1 < len(steps) and steps[i + 1].kind == "head" and s.post == 0
-                        and s.binary_class < 0 and steps[i + 1].k == s.k)
+                        and s.binary_class < 0 and steps[i + 1].k == s.k and self.consumers[i] == [i + 1]
+                        and step_inputs(steps, i + 1) == (i,))
                 if fuse and one_launch and K.tree_head_ok(s, steps[i + 1], g):
                     # the head (and the K5 of a last head) in the tree kernel's last-arriving blocks
                     K.tree_head(s, steps[i + 1], cur, self.step_out[i + 1], bucket, self.tree_partial, g,

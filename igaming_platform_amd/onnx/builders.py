@@ -179,7 +179,116 @@ def gru(seq: int = 100, in_dim: int = 16, hidden: int = 256, seed: int = 5, laye
                            "direction": direction, "layout": str(layout)})
 
 
-BUILDERS = {"logistic": logistic, "gbdt": gbdt, "stacked": stacked, "ltv_mlp": ltv_mlp, "gru": gru}
+def _scaler(rng, n_features: int):
+    """sklearn StandardScaler as ai.onnx.ml Scaler: (x - mean) * (1 / std)."""
+    mean = rng.uniform(-0.5, 0.5, n_features).astype(np.float32)
+    scale = rng.uniform(0.5, 2.0, n_features).astype(np.float32)
+    return node("Scaler", ["input"], ["scaled"], domain=ML_DOMAIN, offset=mean, scale=scale)
+
+
+def sklearn_linear(n_features: int = 32, classes: int = 2, post: str = "LOGISTIC", seed: int = 6,
+                   scaler: bool = True, zipmap: bool = True, string_labels: bool = False):
+    """sklearn-onnx style linear pipeline: [Scaler] -> LinearClassifier -> [ZipMap].
+    ``classes`` 2 writes one coefficient row (sklearn's binary LogisticRegression); more write
+    one row per class."""
+    rng = np.random.default_rng(seed)
+    E = 1 if classes == 2 else classes
+    coef = (rng.standard_normal((E, n_features)) * 0.3).astype(np.float32)
+    icpt = (rng.standard_normal(E) * 0.1).astype(np.float32)
+    labels = (dict(classlabels_strings=[f"c{i}" for i in range(classes)]) if string_labels
+              else dict(classlabels_ints=np.arange(classes, dtype=np.int64)))
+    nodes = [_scaler(rng, n_features)] if scaler else []
+    x = "scaled" if scaler else "input"
+    probs = "probabilities" if zipmap else "output"
+    nodes.append(node("LinearClassifier", [x], ["label", probs], domain=ML_DOMAIN, coefficients=coef.ravel(),
+                      intercepts=icpt, post_transform=post, multi_class=0, **labels))
+    if zipmap:
+        zl = (dict(classlabels_strings=labels["classlabels_strings"]) if string_labels
+              else dict(classlabels_int64s=np.arange(classes, dtype=np.int64)))
+        nodes.append(node("ZipMap", [probs], ["output"], domain=ML_DOMAIN, **zl))
+    return model(nodes, [value_info("input", S.FLOAT, ["N", n_features])],
+                 [value_info("label", S.INT64, ["N"]), value_info("output", S.FLOAT, ["N", classes])],
+                 name="sklearn_linear", metadata={"family": "linear", "classes": str(classes)})
+
+
+def linear_regressor(n_features: int = 32, targets: int = 1, post: str = "NONE", seed: int = 7):
+    rng = np.random.default_rng(seed)
+    coef = (rng.standard_normal((targets, n_features)) * 0.3).astype(np.float32)
+    icpt = (rng.standard_normal(targets) * 0.1).astype(np.float32)
+    nodes = [_scaler(rng, n_features),
+             node("LinearRegressor", ["scaled"], ["output"], domain=ML_DOMAIN, coefficients=coef.ravel(),
+                  intercepts=icpt, targets=targets, post_transform=post)]
+    return model(nodes, [value_info("input", S.FLOAT, ["N", n_features])],
+                 [value_info("output", S.FLOAT, ["N", targets])], name="linear_regressor",
+                 metadata={"family": "linear"})
+
+
+def mlp_classifier(n_features: int = 32, hidden: int = 64, seed: int = 8):
+    """sklearn MLPClassifier-style pipeline: Scaler -> Gemm -> Relu -> LinearClassifier (binary,
+    LOGISTIC) -> ZipMap. On the device: the Scaler folds into the first layer's weights and the
+    two layers run as one fused head."""
+    rng = np.random.default_rng(seed)
+    w = (rng.standard_normal((n_features, hidden)) * np.sqrt(2.0 / n_features)).astype(np.float32)
+    b = (rng.standard_normal(hidden) * 0.01).astype(np.float32)
+    coef = (rng.standard_normal(hidden) * np.sqrt(1.0 / hidden)).astype(np.float32)
+    nodes = [_scaler(rng, n_features), node("Gemm", ["scaled", "W", "B"], ["h"]), node("Relu", ["h"], ["a"]),
+             node("LinearClassifier", ["a"], ["label", "probabilities"], domain=ML_DOMAIN, coefficients=coef,
+                  intercepts=np.array([-0.1], np.float32), post_transform="LOGISTIC",
+                  classlabels_ints=np.array([0, 1], np.int64)),
+             node("ZipMap", ["probabilities"], ["output"], domain=ML_DOMAIN,
+                  classlabels_int64s=np.array([0, 1], np.int64))]
+    return model(nodes, [value_info("input", S.FLOAT, ["N", n_features])],
+                 [value_info("label", S.INT64, ["N"]), value_info("output", S.FLOAT, ["N", 2])],
+                 [tensor("W", w), tensor("B", b)], name="mlp_classifier", metadata={"family": "mlp"})
+
+
+def wide_deep(n_features: int = 32, hidden: int = 128, deep_out: int = 64, wide: int = 16, seed: int = 9):
+    """DAG: a deep tower (Gemm -> Relu -> Gemm -> Relu) and a wide linear branch read the same
+    input; Concat -> Gemm -> Sigmoid."""
+    rng = np.random.default_rng(seed)
+
+    def lin(k, n, name):
+        return [tensor(f"W{name}", (rng.standard_normal((k, n)) * np.sqrt(2.0 / k)).astype(np.float32)),
+                tensor(f"B{name}", (rng.standard_normal(n) * 0.01).astype(np.float32))]
+    inits = lin(n_features, hidden, "d1") + lin(hidden, deep_out, "d2") + lin(n_features, wide, "w") + \
+        lin(deep_out + wide, 1, "o")
+    nodes = [node("Gemm", ["input", "Wd1", "Bd1"], ["d1"]), node("Relu", ["d1"], ["a1"]),
+             node("Gemm", ["a1", "Wd2", "Bd2"], ["d2"]), node("Relu", ["d2"], ["a2"]),
+             node("Gemm", ["input", "Ww", "Bw"], ["wide"]),
+             node("Concat", ["a2", "wide"], ["cat"], axis=1),
+             node("Gemm", ["cat", "Wo", "Bo"], ["logit"]), node("Sigmoid", ["logit"], ["output"])]
+    return model(nodes, [value_info("input", S.FLOAT, ["N", n_features])],
+                 [value_info("output", S.FLOAT, ["N", 1])], inits, name="wide_deep", metadata={"family": "mlp"})
+
+
+def residual_mlp(n_features: int = 32, width: int = 128, blocks: int = 2, seed: int = 10):
+    """DAG: h = Relu(x W0 + b0); per block h = h + Relu(Relu(h W1 + b1) W2 + b2) (MatMul + Add
+    pairs); head Gemm -> Sigmoid."""
+    rng = np.random.default_rng(seed)
+    inits = [tensor("W0", (rng.standard_normal((n_features, width)) * np.sqrt(2.0 / n_features)).astype(np.float32)),
+             tensor("B0", np.zeros(width, np.float32))]
+    nodes = [node("Gemm", ["input", "W0", "B0"], ["z0"]), node("Relu", ["z0"], ["h0"])]
+    h = "h0"
+    for i in range(blocks):
+        for j in (1, 2):
+            inits += [tensor(f"W{i}_{j}", (rng.standard_normal((width, width)) * np.sqrt(1.0 / width)).astype(np.float32)),
+                      tensor(f"B{i}_{j}", (rng.standard_normal(width) * 0.01).astype(np.float32))]
+        nodes += [node("MatMul", [h, f"W{i}_1"], [f"m{i}_1"]), node("Add", [f"m{i}_1", f"B{i}_1"], [f"z{i}_1"]),
+                  node("Relu", [f"z{i}_1"], [f"a{i}_1"]),
+                  node("MatMul", [f"a{i}_1", f"W{i}_2"], [f"m{i}_2"]), node("Add", [f"m{i}_2", f"B{i}_2"], [f"z{i}_2"]),
+                  node("Relu", [f"z{i}_2"], [f"a{i}_2"]),
+                  node("Add", [h, f"a{i}_2"], [f"h{i + 1}"])]
+        h = f"h{i + 1}"
+    inits += [tensor("Wh", (rng.standard_normal((width, 1)) * np.sqrt(1.0 / width)).astype(np.float32)),
+              tensor("Bh", np.array([-0.2], np.float32))]
+    nodes += [node("Gemm", [h, "Wh", "Bh"], ["logit"]), node("Sigmoid", ["logit"], ["output"])]
+    return model(nodes, [value_info("input", S.FLOAT, ["N", n_features])],
+                 [value_info("output", S.FLOAT, ["N", 1])], inits, name="residual_mlp", metadata={"family": "mlp"})
+
+
+BUILDERS = {"logistic": logistic, "gbdt": gbdt, "stacked": stacked, "ltv_mlp": ltv_mlp, "gru": gru,
+            "sklearn_linear": sklearn_linear, "linear_regressor": linear_regressor,
+            "mlp_classifier": mlp_classifier, "wide_deep": wide_deep, "residual_mlp": residual_mlp}
 
 
 def build(kind: str, **kw):

@@ -323,6 +323,28 @@ def dense(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], Y: tor
         _mod().gemm(d, _stream())
 
 
+JOIN_OPS = {"add": 0, "concat": 1}
+
+
+def join(op: str, A: torch.Tensor, B: torch.Tensor, Y: torch.Tensor, M: int, na: int, nb: int,
+         m_ptr: Optional[torch.Tensor] = None) -> None:
+    """DAG join (join.hip): ``add`` Y[:M, :na] = A + B; ``concat`` Y[:M, :na+nb] = [A | B]."""
+    dev = Y.device
+    for t, name in ((A, "A"), (B, "B"), (Y, "Y")):
+        if t.dim() != 2 or t.dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"join: {name} must be 2-D float32 or bfloat16")
+    width = na if op == "add" else na + nb
+    if op not in JOIN_OPS or (op == "add" and na != nb):
+        raise ValueError("join: op add (equal widths) or concat")
+    if A.shape[1] < na or B.shape[1] < nb or Y.shape[1] < width or min(A.shape[0], B.shape[0], Y.shape[0]) < M:
+        raise ValueError("join: operand shapes smaller than M / widths")
+    d = dict(A=_need(A, "A", device=dev), B=_need(B, "B", device=dev), Y=_need(Y, "Y", device=dev),
+             m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32), M=int(M), na=int(na), nb=int(nb), op=JOIN_OPS[op],
+             lda=int(A.shape[1]), ldb=int(B.shape[1]), ldy=int(Y.shape[1]), a_bf16=int(A.dtype == torch.bfloat16),
+             b_bf16=int(B.dtype == torch.bfloat16), y_bf16=int(Y.dtype == torch.bfloat16))
+    _mod().join(d, _stream())
+
+
 def mlp_head(hs, X: Optional[torch.Tensor], Y: torch.Tensor, M: int, m_ptr: Optional[torch.Tensor] = None,
              tree_partial=None, trace: Optional[torch.Tensor] = None, ens: Optional[dict] = None) -> None:
     """``hs``: models.plan.HeadStep. Y[:M, 0] = act2(act1(X W1^T + b1) . w2 + b2).
@@ -616,6 +638,8 @@ class MlpChainPack:
     def eligible(steps) -> bool:
         if not steps or steps[-1].kind != "head" or any(s.kind != "dense" for s in steps[:-1]):
             return False
+        if any(getattr(s, "src", None) is not None for s in steps):
+            return False  # DAG plans run step by step (engine/runner.py)
         if len(steps) > MlpChainPack.MAX_LAYERS:
             return False
         widths = [s.n for s in steps[:-1]] + [steps[-1].n1]
