@@ -182,18 +182,27 @@ def run_cold_engine(a) -> dict:
                 p50_latency_ms=float(np.percentile(lat, 50)), p99_latency_ms=float(np.percentile(lat, 99)))
 
 
-def build_engine(accounts: int, batch: int, backend: str):
+FRAUD_MODELS = {"cfg3": ("cfg3 GBDT(100,d7,128f)+MLP(32-256-1)", 128),
+                "cfg1": ("cfg1 logistic regression over 32 features (Gemm -> Sigmoid)", 32)}
+
+
+def fraud_model_bytes(model: str) -> bytes:
+    from igaming_platform_amd.onnx import builders
+    if model == "cfg1":
+        return builders.build("logistic", n_features=32).SerializeToString()
+    return builders.build("stacked").SerializeToString()
+
+
+def build_engine(accounts: int, batch: int, backend: str, model: str = "cfg3"):
     from igaming_platform_amd.config import Config
     from igaming_platform_amd.engine.risk_engine import RiskEngine
     from igaming_platform_amd.layouts import ACCTBATCH
-    from igaming_platform_amd.onnx import builders
     from igaming_platform_amd.utils.synth import make_population
     cfg = Config()
-    cfg.features.width = 128
+    cfg.features.width = FRAUD_MODELS[model][1]
     cfg.gpu.buckets = sorted({64, 512, 2048, batch})
     cfg.gpu.max_batch = batch
-    eng = RiskEngine(cfg, backend=backend, capacity=accounts + 1024,
-                     fraud_model=builders.build("stacked").SerializeToString())
+    eng = RiskEngine(cfg, backend=backend, capacity=accounts + 1024, fraud_model=fraud_model_bytes(model))
     pop = make_population(accounts, 98, seed=3, fast_hash=True)
     ids = [account_id(i) for i in range(accounts)]
     step = 1 << 18
@@ -372,7 +381,7 @@ def run_grpc_open_loop(a) -> dict:
     """Unary ScoreTransaction throughput vs latency: offered load stepped through ``--rates``
     (whole-node calls/s, split over ``--clients`` processes), open loop."""
     import multiprocessing as mp
-    eng = build_engine(a.accounts, a.batch, a.backend)
+    eng = build_engine(a.accounts, a.batch, a.backend, a.model)
     srv = make_server(a, eng, batching=True)
     rates = [int(x) for x in a.rates.split(",")]
     if a.client == "native":
@@ -411,7 +420,7 @@ def run_grpc_open_loop(a) -> dict:
                 value=best["achieved_per_s"] if best else 0.0, unit="calls/s",
                 value_is="highest offered rate answered in full with p99 < 50 ms", scope="grpc_unary_open_loop",
                 n_gpus=1 if a.backend == "gpu" else 0, data="synthetic (UUID ids, random-init cfg3 weights)",
-                config=dict(model="cfg3 GBDT(100,d7,128f)+MLP(32-256-1)", clients=a.clients, seconds_per_level=a.seconds,
+                config=dict(model=FRAUD_MODELS[a.model][0], clients=a.clients, seconds_per_level=a.seconds,
                             server=server_desc(a),
                             client="grpc.aio open loop, latency from the scheduled send time"),
                 curve=curve, best=best,
@@ -438,7 +447,8 @@ def _curve_result(a, curve, st) -> dict:
                 data=f"synthetic (UUID ids over {a.accounts} accounts"
                      + (f", Zipf({a.zipf}) account ranks" if a.zipf > 1 else ", uniform") + ", random-init weights)",
                 dtype=getattr(a, "numerics", "fp32"),
-                config=dict(model=RPC_MODELS[a.rpc], clients=a.clients, seconds_per_level=a.seconds,
+                config=dict(model=FRAUD_MODELS[a.model][0] if a.rpc == "tx" else RPC_MODELS[a.rpc],
+                            clients=a.clients, seconds_per_level=a.seconds, backend=a.backend,
                             server=server_desc(a),
                             client=("native HTTP/2 open loop (libnghttp2, one connection per thread)" if a.client == "native"
                                     else "grpc.aio open loop") + ", latency from the scheduled send time"),
@@ -527,6 +537,8 @@ def main(argv=None) -> int:
     ap.add_argument("--zipf", type=float, default=0.0, help="account-id distribution: Zipf exponent (> 1), 0 uniform")
     ap.add_argument("--numerics", default="fp32", choices=["fp32", "bf16"], help="cfg4 / cfg5 model numerics")
     ap.add_argument("--backend", default="gpu", choices=["gpu", "cpu"])
+    ap.add_argument("--model", default="cfg3", choices=sorted(FRAUD_MODELS),
+                    help="fraud model of the ScoreTransaction / ScoreBatch scopes (cfg1: CPU logistic, BASELINE config 1)")
     ap.add_argument("--accounts", type=int, default=1 << 20)
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--payloads", type=int, default=6)
