@@ -65,13 +65,6 @@ UpdateArgs update_args(const py::dict& d) {
   a.dcap = geti(d, "dcap");
   a.dmax = geti(d, "dmax");
   a.region = geti(d, "region", DEDUP_STANDALONE);
-  {
-    static const int pf = [] {  // IGP_K1_PREFETCH (features.hip dedup_insert_list_kernel)
-      const char* e = getenv("IGP_K1_PREFETCH");
-      return e ? atoi(e) : 0;
-    }();
-    a.prefetch = pf;
-  }
   if (!a.dbuf || !a.cfg || !a.req || !a.rt) throw std::runtime_error("update args: missing pointers");
   if (a.n_max > a.dmax || a.dcap < 2 * a.dmax) throw std::runtime_error("update args: dedup scratch too small");
   if (a.ev && a.ev_dim != 16) throw std::runtime_error("update args: event dim must be 16");

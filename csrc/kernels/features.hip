@@ -685,19 +685,6 @@ __global__ void __launch_bounds__(64) dedup_insert_list_kernel(UpdateArgs a) {
   const int2 r = *reinterpret_cast<const int2*>(a.req + i);  // {slot, tx_type}
   const ScoreCfg& cfg = *a.cfg;
   if (r.x < 0 || (cfg.owner_filter && ((r.y >> 8) & 0xff) != cfg.my_rank)) return;
-  // IGP_K1_PREFETCH: touch one word per 128-B line of the account's tx ring, HLL registers and
-  // runtime record, so K1 (next on the state queue) finds them in the memory-side cache instead
-  // of HBM (cold accounts on rotating batches: K1 is ~3x its hot-cache time). Issued before the
-  // CAS chain, whose atomic latency they overlap; consumed by an empty asm, so the loads stay.
-  uint32_t pf = 0;
-  if (a.prefetch && a.ring_ts && a.hll) {  // kernel-uniform
-    const uint32_t* ts = a.ring_ts + (size_t)r.x * a.ring_size;
-    for (int l = 0; l < a.ring_size; l += 32) pf += ts[l];
-    const uint32_t* hl = reinterpret_cast<const uint32_t*>(a.hll + (size_t)r.x * 512);
-#pragma unroll
-    for (int l = 0; l < 128; l += 32) pf += hl[l];
-    pf += reinterpret_cast<const uint32_t*>(a.rt + r.x)[0];
-  }
   uint32_t h = mix32((uint32_t)r.x) & (uint32_t)(t.cap - 1);
   for (int p = 0; p < t.cap; ++p) {
     const int prev = atomicCAS(&t.keys[h], -1, r.x);
@@ -713,7 +700,6 @@ __global__ void __launch_bounds__(64) dedup_insert_list_kernel(UpdateArgs a) {
     }
     h = (h + 1) & (uint32_t)(t.cap - 1);
   }
-  asm volatile("" ::"v"(pf));
 }
 
 __global__ void update_single_kernel(UpdateArgs a) {

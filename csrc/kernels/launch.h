@@ -45,7 +45,6 @@ struct UpdateArgs {
   int32_t dcap;             // power of two >= 2 * dmax
   int32_t dmax;
   int32_t region;           // -1: hdr->seq & 1; else fixed region (2 = standalone)
-  int32_t prefetch;         // dedup insert touches each account's tx ring / HLL / RT lines
 };
 
 struct AssembleArgs {
