@@ -618,6 +618,8 @@ PYBIND11_MODULE(_native, m) {
            py::arg("create"), py::arg("timeout_s") = 60.0, py::keep_alive<1, 2>())
       .def("device_ops", [](const ShmXchgDevice& d) { return reinterpret_cast<uintptr_t>(d.ops()); })
       .def_property_readonly("rows_scored", &ShmXchgDevice::rows_scored)
+      .def_property_readonly("slot_violations", &ShmXchgDevice::slot_violations)
+      .def_property_readonly("steps", &ShmXchgDevice::steps)
       .def("unlink_shared", &ShmXchgDevice::unlink_shared);
 
   py::class_<AuditRing, std::shared_ptr<AuditRing>>(m, "AuditRing")

@@ -133,10 +133,14 @@ void ShmXchgDevice::step(int slot, int64_t now) {
   Slot& s = slots_[slot];
   const int q = int(k_ % kRing);
   const size_t stride = size_t(C_) + 1;
-  // 1. post my owner chunks
+  // 1. post my owner chunks (and the slot this step runs on: every rank must use the same one)
+  if (slot != int(k_ % int64_t(slots_.size()))) slot_violations_.fetch_add(1);
   std::memcpy(send_area(rank_, q), s.send.data(), send_bytes_);
+  counters_[rank_].slot.store(slot, std::memory_order_relaxed);
   counters_[rank_].posted.store(k_ + 1, std::memory_order_release);
   wait_all(&Counter::posted, k_ + 1);
+  for (int p = 0; p < world_; ++p)  // a peer cannot post step k + 2 before this rank scored k + 1
+    if (counters_[p].slot.load(std::memory_order_relaxed) != slot) slot_violations_.fetch_add(1);
   // 2. compact the rows every sender routed to me (sender order, then row order)
   size_t n = 0;
   int64_t t = 0;  // the step's clock: the latest clock of the senders that sent rows

@@ -49,6 +49,10 @@ class ShmXchgDevice {
                 bool create, double timeout_s);
   const IgpDeviceOps* ops() const { return &ops_; }
   int64_t rows_scored() const { return rows_scored_.load(); }
+  // steps whose pipeline slot differed from step index % depth here, or from the slot a peer ran
+  // the same step on (the serving core's exchange-mode slot contract, serve_core.cpp)
+  int64_t slot_violations() const { return slot_violations_.load(); }
+  int64_t steps() const { return k_; }
   void unlink_shared() { region_.unlink(); }
 
  private:
@@ -56,7 +60,8 @@ class ShmXchgDevice {
   struct alignas(64) Counter {
     std::atomic<int64_t> posted;
     std::atomic<int64_t> scored;
-    char pad[48];
+    std::atomic<int32_t> slot;  // pipeline slot of the step last posted
+    char pad[44];
   };
   struct Slot {
     std::vector<ReqRec> send;   // [world][C + 1]
@@ -86,6 +91,7 @@ class ShmXchgDevice {
   std::vector<ResultRec> res_;
   std::vector<FeatRec> feat_;
   std::atomic<int64_t> rows_scored_{0};
+  std::atomic<int64_t> slot_violations_{0};
   IgpDeviceOps ops_{};
 };
 

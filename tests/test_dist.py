@@ -365,3 +365,77 @@ def test_cross_ingress_ordering_contract_same_accounts(world):
     assert feats == [_noslot(ref.get_features(f"shared-{i}", now=NOW + 100)) for i in range(10)]
     # the shared accounts really were hit by several ranks within one step
     assert any(len(v) > 1 for v in steps.values())
+
+
+def _slot_worker(rank, world, port, q):
+    """Concurrent ScoreBatch calls of mixed sizes on every rank: items spanning several exchange
+    steps and single-step items finish (and free their slots) in arbitrary order."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import threading
+    import torch.distributed as dist
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.engine.risk_engine import RiskEngine, serve_shard
+    from igaming_platform_amd.parallel.comm import TorchComm
+    from igaming_platform_amd.proto import risk_v1 as P
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = TorchComm("gloo")
+    cfg = Config()
+    cfg.gpu.buckets = [64, 256]
+    cfg.gpu.max_batch = 256
+
+    def hammer(core, dev):
+        errs = []
+
+        def worker(t):
+            rng = np.random.default_rng(100 * rank + t)
+            for i in range(12):
+                n = int(rng.choice([1, 7, 90, 300, 700]))
+                txs = [P.ScoreTransactionRequest(account_id=f"slot-{int(a)}", amount=1000 + int(a),
+                                                 transaction_type="bet") for a in rng.integers(0, 500, n)]
+                resp = P.ScoreBatchResponse.FromString(core.score_batch(
+                    P.ScoreBatchRequest(transactions=txs).SerializeToString(), NOW + i, 0))
+                if len(resp.results) != n:
+                    errs.append((t, i, n, len(resp.results)))
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
+        [th.start() for th in ths]
+        [th.join() for th in ths]
+        return errs, int(dev.slot_violations), int(dev.steps)
+    try:
+        if rank == 0:
+            eng = RiskEngine(cfg, backend="cpu", capacity=1024, spmd=comm)
+            out = hammer(eng.core, eng.node.local._device)
+            eng.close()
+        else:
+            box = {}
+
+            def ingress(node):
+                box["out"] = hammer(node.core, node.local._device)
+            serve_shard(cfg, comm, backend="cpu", capacity=1024, ingress=ingress)
+            out = box["out"]
+        q.put(("ok", rank) + out)
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put(("err", rank, traceback.format_exc() + repr(e), 0, 0))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_steps_run_on_the_same_slot_on_every_rank():
+    """with a free-slot stack, ranks that released steps in different orders ran one
+    exchange step on different pipeline slots (the D2H result path indexes its shared region by
+    slot). The core now issues step k on slot k % depth everywhere; the CPU exchange device
+    checks it against its own step count and against every peer's slot for the same step."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world = 2
+    port = _free_port()
+    procs = [ctx.Process(target=_slot_worker, args=(r, world, port, q)) for r in range(world)]
+    [p.start() for p in procs]
+    msgs = [q.get(timeout=240) for _ in range(world)]
+    [p.join(timeout=60) for p in procs]
+    errs = [m[2] for m in msgs if m[0] == "err"]
+    assert not errs, errs[0]
+    for _, rank, call_errs, violations, steps in msgs:
+        assert not call_errs, (rank, call_errs[:3])
+        assert violations == 0, (rank, violations)
+        assert steps > 20, (rank, steps)
