@@ -724,29 +724,32 @@ class MlpLayerPack:
         self.rows = 0
         self.ws = None
 
-    def reserve(self, rows: int) -> None:
-        """Workspace for batches of up to ``rows``: two activation buffers (+ lo planes) and the
-        head partials. Reallocating invalidates graphs captured on the old buffers."""
-        if rows <= self.rows:
+    def reserve(self, rows: int, n_ws: int = 1) -> None:
+        """``n_ws`` workspaces (one per pipeline slot that may run concurrently) for batches of up
+        to ``rows``: two activation buffers (+ lo planes) and the head partials each.
+        Reallocating invalidates graphs captured on the old buffers."""
+        if rows <= self.rows and n_ws <= len(self.ws or ()):
             return
+        rows = max(int(rows), self.rows)
         planes = 2 if self.split else 1
-        act = torch.zeros((planes, 2, rows, self.width), dtype=torch.bfloat16, device=self.device)
-        part = torch.zeros((self.layers[-1]["N"] // 128, rows), dtype=torch.float32, device=self.device)
-        self.ws, self.rows = (act, part), int(rows)
+        self.ws = [(torch.zeros((planes, 2, rows, self.width), dtype=torch.bfloat16, device=self.device),
+                    torch.zeros((self.layers[-1]["N"] // 128, rows), dtype=torch.float32, device=self.device))
+                   for _ in range(max(int(n_ws), len(self.ws or ())))]
+        self.rows = rows
 
 
 def mlp_layers(pk: MlpLayerPack, n_rows: int, X: Optional[torch.Tensor] = None, slots: Optional[torch.Tensor] = None,
                pf_tab: Optional[torch.Tensor] = None, ext_tab: Optional[torch.Tensor] = None,
                ml: Optional[torch.Tensor] = None, ltv_out: Optional[torch.Tensor] = None,
-               m_ptr: Optional[torch.Tensor] = None) -> None:
+               m_ptr: Optional[torch.Tensor] = None, ws_key: int = 0) -> None:
     """The same chain as :func:`mlp_chain` (same inputs and outputs), one GEMM launch per layer +
-    a finish launch. ``n_rows`` must be within :meth:`MlpLayerPack.reserve`."""
+    a finish launch, on workspace ``ws_key``. ``n_rows`` must be within :meth:`MlpLayerPack.reserve`."""
     dev = pk.device
-    if pk.ws is None or n_rows > pk.rows:
-        raise ValueError(f"mlp_layers: workspace reserved for {pk.rows} rows < {n_rows}")
+    if pk.ws is None or n_rows > pk.rows or not 0 <= ws_key < len(pk.ws):
+        raise ValueError(f"mlp_layers: no workspace {ws_key} for {n_rows} rows (reserved: {pk.rows})")
     if ml is None and ltv_out is None:
         raise ValueError("mlp_layers: nothing to write")
-    act, part = pk.ws
+    act, part = pk.ws[ws_key]
     mp = _host_or_dev(m_ptr, "m_ptr", 1, dev, torch.int32)
     src = {}
     if slots is not None:
