@@ -340,11 +340,12 @@ struct MlpLayerArgs {
   const float* ext_tab;     // [C][ext_w] (nullable)
   int32_t ext_w;
   int32_t in_live;          // src 1 / 2: real input columns (the rest of K is zero)
-  const uint16_t* W;        // bf16 [N_pad(128)][K] row-major (row n = output column n)
-  const uint16_t* W_lo;     // split: residuals
+  const uint16_t* W;        // bf16 fragment-packed, k-step major [K/32][N/16][64][8] (pack_fragments)
+  const uint16_t* W_lo;     // split: residuals, same layout
   const float* bias;        // [N] (nullable)
   int32_t M, K, act;        // rows (grid coverage), K multiple of 64
-  int32_t tiles, col_tiles; // row tiles x column tiles; col_tiles = N / 128
+  int32_t tiles, col_tiles; // row tiles x column tiles (mlp_layer_tile_rows / _cols per mode)
+  int32_t n_tiles;          // N / 16: column tiles of the fragment-packed weights
   const int32_t* m_ptr;     // live rows (nullable)
   uint16_t* Y;              // epi 0: [M][ldy] bf16 (hi)
   uint16_t* Y_lo;           // epi 0, split
@@ -355,8 +356,11 @@ struct MlpLayerArgs {
   int32_t act2;
   float* ml;                // finish: [M] (nullable)
   float* ltv_out;           // finish: [M][6] K9 rows (nullable; needs slots + pf_tab)
+  int64_t* trace;           // [64 blocks][8] phase wall-clock marks (nullable)
 };
 void launch_mlp_layer(const MlpLayerArgs& a, hipStream_t st);
+int mlp_layer_tile_rows(int split);  // 128 (bf16) / 64 (split)
+int mlp_layer_tile_cols(int split);  // 128 (bf16) / 256 (split)
 void launch_mlp_layer_finish(const MlpLayerArgs& a, hipStream_t st);
 
 }  // namespace igp

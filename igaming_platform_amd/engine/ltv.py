@@ -143,7 +143,7 @@ class LtvGpu:
         # layer-wise from IGP_MLP_LAYERS_MIN rows)
         self.layers = None
         design = os.environ.get("IGP_MLP_DESIGN", "chain")
-        if self.chain is not None and design != "chain" and K.MlpLayerPack.eligible(plan.steps):
+        if self.chain is not None and design != "chain" and K.MlpLayerPack.eligible(plan.steps, self.chain.split):
             self.layers = K.MlpLayerPack(plan.steps, self.device, split=self.chain.split)
             self.layers_min = 1 if design == "layers" else int(os.environ.get("IGP_MLP_LAYERS_MIN", "2048"))
         dev = self.device

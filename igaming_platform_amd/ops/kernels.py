@@ -686,21 +686,27 @@ class MlpChainPack:
 
 class MlpLayerPack:
     """Device weights of a dense chain for the layer-wise kernels (csrc/kernels/mlp_layers.hip):
-    each layer a 128 x 128-tile GEMM launch, the N -> 1 head as partial dots in the last layer's
-    epilogue plus a finish launch (head sum, K9). Weights row-major bf16 [N][K_pad 64] (+ the
-    residuals in split mode); activations between layers live in a per-pack workspace sized by
-    :meth:`reserve` (before any graph capture)."""
+    each layer one GEMM launch over the whole chip (bf16 128 x 128 tiles, split 64 x 256), the
+    N -> 1 head as partial dots in the last layer's epilogue plus a finish launch (head sum, K9).
+    Weights fragment-packed k-step major (:func:`pack_fragments`, + the residuals in split mode);
+    activations between layers live in per-slot workspaces sized by :meth:`reserve` (before any
+    graph capture)."""
 
     @staticmethod
-    def eligible(steps) -> bool:
+    def tile_cols(split: bool) -> int:
+        return 256 if split else 128
+
+    @staticmethod
+    def eligible(steps, split: bool = False) -> bool:
         if not MlpChainPack.eligible(steps):
             return False
-        return all((s.n1 if s.kind == "head" else s.n) % 128 == 0 for s in steps)
+        bn = MlpLayerPack.tile_cols(split)
+        return all((s.n1 if s.kind == "head" else s.n) % bn == 0 for s in steps)
 
     def __init__(self, steps, device, split: bool = False):
         import numpy as np
-        if not self.eligible(steps):
-            raise ValueError("mlp_layers: every layer width must be a multiple of 128 (<= 512)")
+        if not self.eligible(steps, split):
+            raise ValueError("mlp_layers: every layer width must fill whole column tiles (<= 512)")
         dev = as_device(device)
         self.split = bool(split)
         self.layers = []
@@ -709,11 +715,12 @@ class MlpLayerPack:
             b = s.b1_np if s.kind == "head" else s.b_np
             n, k = w.shape
             kp = -(-k // 64) * 64
-            buf = np.zeros((n, kp), np.float32)
-            buf[:, :k] = w
-            hi = torch.from_numpy(buf).to(torch.bfloat16)
-            lo = (torch.from_numpy(buf) - hi.float()).to(torch.bfloat16).to(dev) if self.split else None
-            self.layers.append(dict(W=hi.to(dev), Wlo=lo, N=n, K=kp, act=ACT[s.act1 if s.kind == "head" else s.act],
+            lo = None
+            if self.split:
+                hi = torch.from_numpy(np.ascontiguousarray(w)).to(torch.bfloat16).float().numpy()
+                lo = pack_fragments(w - hi, kp, ks_major=True).to(dev)
+            self.layers.append(dict(W=pack_fragments(w, kp, ks_major=True).to(dev), Wlo=lo, N=n, K=kp,
+                                    act=ACT[s.act1 if s.kind == "head" else s.act],
                                     b=None if b is None else torch.from_numpy(np.ascontiguousarray(b, np.float32)).to(dev)))
         head = steps[-1]
         self.w2 = torch.from_numpy(np.ascontiguousarray(head.w2_np, np.float32)).to(dev)
@@ -732,8 +739,9 @@ class MlpLayerPack:
             return
         rows = max(int(rows), self.rows)
         planes = 2 if self.split else 1
+        tiles = self.layers[-1]["N"] // self.tile_cols(self.split)
         self.ws = [(torch.zeros((planes, 2, rows, self.width), dtype=torch.bfloat16, device=self.device),
-                    torch.zeros((self.layers[-1]["N"] // 128, rows), dtype=torch.float32, device=self.device))
+                    torch.zeros((tiles, rows), dtype=torch.float32, device=self.device))
                    for _ in range(max(int(n_ws), len(self.ws or ())))]
         self.rows = rows
 
@@ -741,7 +749,7 @@ class MlpLayerPack:
 def mlp_layers(pk: MlpLayerPack, n_rows: int, X: Optional[torch.Tensor] = None, slots: Optional[torch.Tensor] = None,
                pf_tab: Optional[torch.Tensor] = None, ext_tab: Optional[torch.Tensor] = None,
                ml: Optional[torch.Tensor] = None, ltv_out: Optional[torch.Tensor] = None,
-               m_ptr: Optional[torch.Tensor] = None, ws_key: int = 0) -> None:
+               m_ptr: Optional[torch.Tensor] = None, ws_key: int = 0, trace: Optional[torch.Tensor] = None) -> None:
     """The same chain as :func:`mlp_chain` (same inputs and outputs), one GEMM launch per layer +
     a finish launch, on workspace ``ws_key``. ``n_rows`` must be within :meth:`MlpLayerPack.reserve`."""
     dev = pk.device
@@ -772,9 +780,9 @@ def mlp_layers(pk: MlpLayerPack, n_rows: int, X: Optional[torch.Tensor] = None, 
     L = len(pk.layers)
     for i, l in enumerate(pk.layers):
         d = dict(base, W=_need(l["W"], "W", torch.bfloat16, l["N"] * l["K"], dev),
-                 W_lo=_opt(l["Wlo"], "Wlo", dtype=torch.bfloat16, device=dev),
+                 W_lo=_opt(l["Wlo"], "Wlo", dtype=torch.bfloat16, min_numel=l["N"] * l["K"], device=dev),
                  bias=_opt(l["b"], "b", dtype=torch.float32, min_numel=l["N"], device=dev),
-                 K=l["K"], act=l["act"], col_tiles=l["N"] // 128)
+                 K=l["K"], N=l["N"], act=l["act"])
         if i == 0:
             d.update(src, in_live=pk.in_live)
         else:
@@ -784,8 +792,10 @@ def mlp_layers(pk: MlpLayerPack, n_rows: int, X: Optional[torch.Tensor] = None, 
             d.update(epi=0, Y=act[0, i & 1].data_ptr(), Y_lo=act[1, i & 1].data_ptr() if pk.split else None, ldy=W)
         else:
             d.update(epi=1, w2=_need(pk.w2, "w2", torch.float32, l["N"], dev), part=part.data_ptr())
+        if trace is not None:  # [layers][64][8] int64 phase marks (tools/mlp_layerwise_bench.py --trace)
+            d["trace"] = _need(trace, "trace", torch.int64, (i + 1) * 512, dev) + i * 512 * 8
         _mod().mlp_layer(d, _stream())
-    f = dict(base, part=part.data_ptr(), col_tiles=pk.layers[-1]["N"] // 128, b2=pk.b2, act2=pk.act2,
+    f = dict(base, part=part.data_ptr(), N=pk.layers[-1]["N"], b2=pk.b2, act2=pk.act2,
              ml=_opt(ml, "ml", dtype=torch.float32, min_numel=n_rows, device=dev),
              ltv_out=_host_or_dev(ltv_out, "ltv_out", 6 * n_rows, dev))
     if ltv_out is not None:

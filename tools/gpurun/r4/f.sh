@@ -15,6 +15,7 @@ step() {
 }
 step tests 300 python -u -m pytest tests/test_mlp_fused_gpu.py -v --timeout 120 --timeout-method thread -p no:cacheprovider
 export OUT=$R/$O/mlp_layerwise.json
+step trace 200 python tools/mlp_layerwise_bench.py 8192 --trace
 step layerwise 300 python tools/mlp_layerwise_bench.py 8192,16384
 cd /tmp
 export OUT=/tmp/lw.json

@@ -39,13 +39,20 @@ def _time_graph(torch, fn, reps=50):
         fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ts = []
-    for _ in range(reps):
+    with torch.cuda.stream(s):  # replay() launches on the current stream: time it there
+        for _ in range(reps):
+            e0.record(s)
+            g.replay()
+            e1.record(s)
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        # back to back (the throughput a stream of batches sees: launch gaps overlap)
         e0.record(s)
-        g.replay()
+        for _ in range(reps):
+            g.replay()
         e1.record(s)
         e1.synchronize()
-        ts.append(e0.elapsed_time(e1) * 1e3)
-    return float(np.median(ts)), g
+    return float(np.median(ts)), g, e0.elapsed_time(e1) * 1e3 / reps
 
 
 def main() -> int:
@@ -58,8 +65,28 @@ def main() -> int:
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(0)
     steps = _steps(rng)
-    batches = [int(b) for b in (sys.argv[1] if len(sys.argv) > 1 else "8192,16384").split(",")]
+    args = [x for x in sys.argv[1:] if not x.startswith("--")]
+    batches = [int(b) for b in (args[0] if args else "8192,16384").split(",")]
     out = []
+    if "--trace" in sys.argv:  # per-phase wall clock of the layer kernels (blocks 0..63, wave 0)
+        for precision in ("bf16", "fp32"):
+            B = batches[0]
+            lp = K.MlpLayerPack(steps, dev, split=precision == "fp32")
+            lp.reserve(B)
+            X = torch.from_numpy(rng.normal(0, 1, (B, 256)).astype(np.float32)).to(dev)
+            ml = torch.zeros(B, device=dev)
+            tr = torch.zeros((len(lp.layers), 64, 8), dtype=torch.int64, device=dev)
+            for _ in range(3):
+                K.mlp_layers(lp, B, X=X, ml=ml, trace=tr)
+            torch.cuda.synchronize()
+            t = tr.cpu().numpy().astype(np.float64) / 100.0  # 100 MHz ticks -> us
+            for li in range(t.shape[0]):
+                m = t[li]
+                ph = {f"p{k}{k + 1}": round(float(np.median(m[:, k + 1] - m[:, k])), 2) for k in range(5)}
+                r = dict(trace=True, precision=precision, batch=B, layer=li, start_skew_us=round(float(np.ptp(m[:, 0])), 2),
+                         span_us=round(float(m[:, 5].max() - m[:, 0].min()), 2), **ph)
+                out.append(r)
+                print(json.dumps(r), flush=True)
     for precision in ("bf16", "fp32"):
         pk = K.MlpChainPack(steps, dev, split=precision == "fp32")
         plan = to_device(Plan(family="mlp", in_width=256, steps=copy.deepcopy(steps), out_width=1, ml_col=0,
@@ -67,22 +94,24 @@ def main() -> int:
         for B in batches:
             X = torch.from_numpy(rng.normal(0, 1, (B, 256)).astype(np.float32)).to(dev)
             ml = torch.zeros(B, device=dev)
-            us_c, _g1 = _time_graph(torch, lambda: K.mlp_chain(pk, B, X=X, ml=ml))
+            us_c, _g1, bb_c = _time_graph(torch, lambda: K.mlp_chain(pk, B, X=X, ml=ml))
             ref = ml.clone()
-            lp = K.MlpLayerPack(steps, dev, split=precision == "fp32")
+            lp = K.MlpLayerPack(steps, dev, split=precision == "fp32")  # noqa: F841
             lp.reserve(B)
             ml2 = torch.zeros(B, device=dev)
-            us_k, _g3 = _time_graph(torch, lambda: K.mlp_layers(lp, B, X=X, ml=ml2))
+            us_k, _g3, bb_k = _time_graph(torch, lambda: K.mlp_layers(lp, B, X=X, ml=ml2))
             diff_k = float((ml2 - ref).abs().max())
             dm = DeviceModel(plan, dev, [B])
             res = {}
 
             def layerwise():
                 res["y"] = dm.run(X, B)
-            us_l, _g2 = _time_graph(torch, layerwise)
+            us_l, _g2, bb_l = _time_graph(torch, layerwise)
             diff = float((res["y"][:B, 0].float() - ref).abs().max())
-            for name, us, dd in (("chain", us_c, 0.0), ("layerwise_generic", us_l, diff), ("mlp_layers", us_k, diff_k)):
-                r = dict(design=name, precision=precision, batch=B, us=round(us, 2),
+            for name, us, bb, dd in (("chain", us_c, bb_c, 0.0), ("layerwise_generic", us_l, bb_l, diff),
+                                     ("mlp_layers", us_k, bb_k, diff_k)):
+                r = dict(design=name, precision=precision, batch=B, us=round(us, 2), us_back_to_back=round(bb, 2),
+                         predictions_per_s_back_to_back=round(B / bb * 1e6),
                          predictions_per_s=round(B / us * 1e6), tflops=round(FLOP_ROW * B / us / 1e6, 1),
                          layers={"chain": "fused chain (mlp_fused.hip)",
                                  "layerwise_generic": "runner plan: " + plan.describe(),
