@@ -14,6 +14,9 @@
 //   abuse  H2D of the live rows -> K1 (features.hip, FeatRec images stored into pinned host
 //          rows) -> K4 GRU over the HBM event rings (gru.hip / gru_ws.hip) -> score D2H
 // Completion: one event per slot, polled by the core's completion thread with the deadline.
+// Streams: one per slot (or one shared): the account-RPC micro-batches are small (a few hundred
+// rows fill a few dozen CUs), so consecutive slots' steps run side by side on the chip instead of
+// queueing behind each other on one stream.
 #include "hostwait.h"
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
@@ -55,9 +58,11 @@ void bind_device(int d) {
 
 class ModelDriver {
  public:
-  ModelDriver(uintptr_t stream, int kind, int depth, int cap, int has_model, int rank, py::list slabs, py::list out0,
+  ModelDriver(py::list streams, int kind, int depth, int cap, int has_model, int rank, py::list slabs, py::list out0,
               py::list out1)
-      : st_(reinterpret_cast<hipStream_t>(stream)), depth_(depth), cap_(cap), rank_(rank) {
+      : depth_(depth), cap_(cap), rank_(rank) {
+    for (auto s : streams) st_.push_back(reinterpret_cast<hipStream_t>(s.cast<uintptr_t>()));
+    if (st_.empty() || (st_.size() != 1 && (int)st_.size() != depth)) throw std::runtime_error("ModelDriver: one stream or one per slot");
     if (kind != IGP_MODEL_LTV && kind != IGP_MODEL_ABUSE) throw std::runtime_error("ModelDriver: kind");
     if (depth < 1 || cap < 1 || (int)slabs.size() != depth || (int)out0.size() != depth)
       throw std::runtime_error("ModelDriver: one slab / output per slot");
@@ -175,16 +180,17 @@ class ModelDriver {
       }
     }
     const StepBody& b = it->second;
+    hipStream_t st = st_[st_.size() == 1 ? 0 : slot];
     if (b.ops) {
-      if (!b.ops->run_recording(st_, ev_[slot])) hip_ok(hipEventRecord(ev_[slot], st_), "record");
+      if (!b.ops->run_recording(st, ev_[slot])) hip_ok(hipEventRecord(ev_[slot], st), "record");
     } else {
-      hip_ok(hipGraphLaunch(b.graph, st_), "graph launch");
-      hip_ok(hipEventRecord(ev_[slot], st_), "record");
+      hip_ok(hipGraphLaunch(b.graph, st), "graph launch");
+      hip_ok(hipEventRecord(ev_[slot], st), "record");
     }
     ++submits_;
   }
 
-  hipStream_t st_;
+  std::vector<hipStream_t> st_;
   int depth_, cap_, rank_;
   int device_ = 0;
   int32_t seq_ = 0;
@@ -203,7 +209,7 @@ void register_model_driver(py::module_& m) {
   m.attr("MODEL_LTV") = int(IGP_MODEL_LTV);
   m.attr("MODEL_ABUSE") = int(IGP_MODEL_ABUSE);
   py::class_<ModelDriver, std::shared_ptr<ModelDriver>>(m, "ModelDriver")
-      .def(py::init<uintptr_t, int, int, int, int, int, py::list, py::list, py::list>(), py::arg("stream"),
+      .def(py::init<py::list, int, int, int, int, int, py::list, py::list, py::list>(), py::arg("streams"),
            py::arg("kind"), py::arg("depth"), py::arg("cap"), py::arg("has_model"), py::arg("rank"), py::arg("slabs"),
            py::arg("out0"), py::arg("out1"))
       .def("set_ops", &ModelDriver::set_ops)

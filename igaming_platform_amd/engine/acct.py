@@ -48,8 +48,13 @@ class LtvNativeDevice:
         self.slabs = [torch.zeros(16 + 4 * B, dtype=torch.uint8).pin_memory() for _ in range(self.depth)]
         self.outs = [torch.zeros((B, 6), dtype=torch.float32).pin_memory() for _ in range(self.depth)]
         self.stream = torch.cuda.Stream(device=dev)
+        # one stream per slot when the step is the recorded chain (no shared scratch): small
+        # micro-batches of consecutive slots then run side by side
+        self.streams = [self.stream] + ([torch.cuda.Stream(device=dev) for _ in range(self.depth - 1)]
+                                        if g.chain is not None else [])
         m = K._mod()
-        self.driver = m.ModelDriver(self.stream.cuda_stream, m.MODEL_LTV, self.depth, B, 1 if g.plan is not None else 0,
+        self.driver = m.ModelDriver([st.cuda_stream for st in self.streams], m.MODEL_LTV, self.depth, B,
+                                    1 if g.plan is not None else 0,
                                     0, [t.data_ptr() for t in self.slabs], [t.data_ptr() for t in self.outs], [])
         self.graphs = []
         self._dev = None
@@ -154,12 +159,19 @@ class AbuseNativeDevice:
         self.cfg_dev = sc.cfg_dev.clone()
         width = sc.width
         self.stream = torch.cuda.Stream(device=dev)
+        # one stream per slot: a few hundred rows of 100-step GRU fill a few dozen CUs, so the
+        # slots' steps run side by side (a bidirectional model shares the pack's direction
+        # buffers between slots and keeps one stream)
+        shared = self.gm is not None and self.gm.bidirectional
+        self.streams = [self.stream] if shared else [self.stream] + [
+            torch.cuda.Stream(device=dev) for _ in range(self.depth - 1)]
         self.bufs = [dict(slab=torch.zeros(nb, dtype=torch.uint8, device=dev),
                           X=torch.zeros((B, width), dtype=torch.float32, device=dev),
                           feat=torch.zeros((B, 32), dtype=torch.int32, device=dev),
                           out=torch.zeros(B, dtype=torch.float32, device=dev)) for _ in range(self.depth)]
         m = K._mod()
-        self.driver = m.ModelDriver(self.stream.cuda_stream, m.MODEL_ABUSE, self.depth, B, 1 if self.gm else 0,
+        self.driver = m.ModelDriver([st.cuda_stream for st in self.streams], m.MODEL_ABUSE, self.depth, B,
+                                    1 if self.gm else 0,
                                     int(rank), [t.data_ptr() for t in self.slabs], [t.data_ptr() for t in self.out0],
                                     [t.data_ptr() for t in self.out1])
         self.graphs = []
@@ -188,7 +200,7 @@ class AbuseNativeDevice:
         from ..ops import kernels as K
         h = self.slabs[slot].numpy()
         h[:4].view(np.int32)[0] = 0
-        s = self.stream
+        s = self.streams[slot % len(self.streams)]
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             self._body(slot, b)

@@ -14,6 +14,7 @@ step() {
   case $rc in 124|134|137|139) exit $rc;; esac
   return 0
 }
+step acct_tests 300 python -u -m pytest tests/test_acct_gpu.py tests/test_mlp_fused_gpu.py -v --timeout 120 --timeout-method thread -p no:cacheprovider
 export OUT=$R/$O/mlp_trace.json
 step trace 200 python tools/mlp_layerwise_bench.py 8192 --trace
 export OUT=$R/$O/mlp_layerwise.json
