@@ -156,10 +156,6 @@ PYBIND11_MODULE(_hipk, m) {
       if (a.upd.region >= 0 || a.upd.dbuf != a.dbuf) throw std::runtime_error("feature_assemble: upd region");
     }
     a.trace = ptr<int64_t*>(d, "trace");
-    {
-      const char* xe = getenv("IGP_K1_EXP");
-      a.exp_flags = xe ? atoi(xe) : 0;
-    }
     launch_or_record([a](hipStream_t st) { launch_feature_assemble(a, st); }, s, "feature_assemble");
   });
 

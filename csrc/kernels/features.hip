@@ -355,11 +355,8 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     const int n4 = rs / 4;
     const uint4* ts4 = reinterpret_cast<const uint4*>(a.ring_ts + (size_t)sc * rs);
     uint4 tsv[4];
-    // A/B experiment (IGP_K1_EXP bit 0): only the first 64 ring entries -> upper bound of what a
-    // recent-first ring layout saves (results differ for accounts with > 64 events)
-    const int n_ld = (a.exp_flags & 1) ? 1 : 4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) tsv[i] = i < n_ld ? ts4[min(ql + 16 * i, n4 - 1)] : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < 4; ++i) tsv[i] = ts4[min(ql + 16 * i, n4 - 1)];
     const uint32_t* hreg = reinterpret_cast<const uint32_t*>(a.hll + (size_t)sc * 512);
     uint32_t wd[4], wi[4];
 #pragma unroll

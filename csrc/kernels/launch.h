@@ -78,7 +78,6 @@ struct AssembleArgs {
   // each wave applies its request's event when it is the account's only one in the batch
   // and opens the segment of a multi-event account (applied by update_segments after K1)
   UpdateArgs upd;
-  int32_t exp_flags;        // A/B experiment bits for same-box comparisons (env IGP_K1_EXP): 1 = tier-A ring only
 };
 
 

@@ -42,7 +42,7 @@ constexpr int MC_LDA = 512;  // bf16 elements per LDS row (1024 B, 64 chunks of 
 __device__ __forceinline__ int mc_idx(int row, int col) {
   return row * MC_LDA + ((((col >> 3) ^ (row & 15))) << 3) + (col & 7);
 }
-constexpr int MC_PF = 5;  // k-steps of weight fragments prefetched ahead (bf16 path; IGP_MC_PF=2: the r2 depth)
+constexpr int MC_PF = 5;  // k-steps of weight fragments prefetched ahead
 
 __device__ __forceinline__ float mc_act(float v, int act) {
   switch (act) {
@@ -307,28 +307,16 @@ void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st) {
       IGP_LAUNCH((mlp_chain_kernel<32, 4, true>), dim3((a.n_rows + 31) / 32), dim3(256), 0, st, a);
     return;
   }
-  const char* pfe = getenv("IGP_MC_PF");  // same-box A/B of the weight prefetch depth (per call: tests flip it)
-  const int pf = pfe ? atoi(pfe) : 0;      // 0: the default depth of the tile shape
   if (a.waves == 8 && r == 64) {
     // 64 rows x 8 waves (4 x 4 MFMA tiles per wave): per k-step a CU issues as many MFMA cycles
     // as it needs L1 cycles for the 32 KB of weight fragments (32 rows: half); a batch then
-    // occupies half the CUs and the per-slot streams keep two batches in flight
-    // prefetch 5 k-steps; 8 spills (28 VGPRs) and ran 78 -> 93 us alone (tools/mlp_bench.py, r3/q)
-    if (pf == 8)
-      IGP_LAUNCH((mlp_chain_kernel<64, 8, false, 8>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
-    else
-      IGP_LAUNCH((mlp_chain_kernel<64, 8, false, 5>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
+    // occupies half the CUs and the per-slot streams keep two batches in flight. Weights
+    // prefetched 5 k-steps ahead: deeper rings (8 / 10) spilled and ran slower (r3/q)
+    IGP_LAUNCH((mlp_chain_kernel<64, 8, false, 5>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
   } else if (a.waves == 8) {
     // 32 rows x 8 waves: a k-step is 8 MFMAs per wave (~0.11 us at two waves per SIMD) against
     // ~1 us of L2 latency for the weight fragments every CU of the XCD reads at the same time
-    // (tools/mlp_bench.py: the launch time hardly changes from 4096 to 8192 rows); deeper rings
-    // (8 / 10 k-steps) do not fit the registers without spills and measured no better (r3/q)
-    if (pf == 10)
-      IGP_LAUNCH((mlp_chain_kernel<32, 8, false, 10>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
-    else if (pf == 8)
-      IGP_LAUNCH((mlp_chain_kernel<32, 8, false, 8>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
-    else
-      IGP_LAUNCH((mlp_chain_kernel<32, 8, false, 5>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
+    IGP_LAUNCH((mlp_chain_kernel<32, 8, false, 5>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
   }
   else if (r == 64)
     IGP_LAUNCH((mlp_chain_kernel<64, 4, false>), dim3((a.n_rows + 63) / 64), dim3(256), 0, st, a);

@@ -121,14 +121,10 @@ class LtvGpu:
         if plan is not None and self.w < N_COLS:
             raise ValueError(f"LTV model input ({self.w}) must hold the {N_COLS} profile columns")
         self.model = DeviceModel(plan, self.device, self.buckets) if plan is not None else None
-        # a dense chain (cfg 4: 256 -> 4 x 512 -> 1, bf16) runs as ONE fused kernel with the
-        # table gather and K9 in it (csrc/kernels/mlp_fused.hip); IGP_MLP_FUSED=0: layer kernels
-        # IGP_LTV_DIRECT=1: the step's recorded launches (csrc/kernels/oplist.h) instead of a graph
-        # replay. Off by default: cfg4 same box 96.4 vs 172.7 M/s for graphs (the step is one
-        # fused kernel between two small copies; as stream copies they cost more than as graph
-        # nodes, profiles/r2/direct3)
-        self.direct = os.environ.get("IGP_LTV_DIRECT", "0") == "1" and not (
-            plan is not None and any(st.kind == "gru" for st in plan.steps))
+        # a dense chain (cfg 4: 256 -> 4 x 512 -> 1) runs as ONE fused kernel with the table
+        # gather and K9 in it (csrc/kernels/mlp_fused.hip); IGP_MLP_FUSED=0: layer kernels. The
+        # step replays a captured graph (recorded direct launches measured slower here: cfg4 96.4
+        # vs 172.7 M/s, profiles/r2/direct3; the native account device records them instead)
         self.chain = None
         # the fused chain (mlp_fused.hip): bf16 plans as bf16 MFMA, fp32 plans in its split
         # mode (bf16 hi/lo pairs, three MFMAs per product: f32-faithful); IGP_MLP_SPLIT=0 sends
@@ -247,11 +243,6 @@ class LtvGpu:
                     with torch.cuda.stream(s):
                         self._body(slot, b)
                     torch.cuda.current_stream().wait_stream(s)
-                    if self.direct:  # recorded launches (csrc/kernels/oplist.h), no graph replay
-                        with self.K.Recorder() as r:
-                            self._body(slot, b)
-                        self.graphs[(b, slot)] = r.ops
-                        continue
                     g = torch.cuda.CUDAGraph()
                     with self.K.graph_capture(g, s):
                         self._body(slot, b)
@@ -285,8 +276,6 @@ class LtvGpu:
             g = self.graphs.get((b, slot))
             if g is None:
                 self._body(slot, b)
-            elif self.direct:
-                g.run(self.stream.cuda_stream)
             else:
                 g.replay()
             ev = torch.cuda.Event()
