@@ -94,6 +94,7 @@ def test_spmd_engine_world1_matches_plain_gpu_engine(monkeypatch, results):
     from igaming_platform_amd.parallel.comm import TorchComm
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    spmd = plain = None
     try:
         cfg = Config()
         cfg.gpu.buckets = [64, 256]
@@ -117,8 +118,10 @@ def test_spmd_engine_world1_matches_plain_gpu_engine(monkeypatch, results):
                        (y["score"], y["action"], y["reason_codes"], y["rule_score"], y["ml_score"])
                 assert x["features"].tobytes() == y["features"].tobytes()
         assert spmd.group.runner.rows_scored == 600
-        spmd.close()
     finally:
+        for e in (spmd, plain):
+            if e is not None:
+                e.close()
         dist.destroy_process_group()
 
 
@@ -203,6 +206,7 @@ def test_exchange_world1_same_accounts_in_one_step_follow_fifo_order():
     from igaming_platform_amd.proto import risk_v1 as P
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    spmd = plain = None
     try:
         cfg = Config()
         cfg.gpu.buckets = [64, 256]
@@ -246,6 +250,10 @@ def test_exchange_world1_same_accounts_in_one_step_follow_fifo_order():
             txs = [t for r in reqs for t in P.ScoreBatchRequest.FromString(r).transactions]
             want = decode(plain.score_batch_bytes(P.ScoreBatchRequest(transactions=txs).SerializeToString(), now=now))
             assert got[0] + got[1] == want
-        spmd.close()
     finally:
+        # the engines stop their exchange / cores before the process group goes away, also when
+        # an assertion failed (destroying the group under a running exchange aborts the process)
+        for e in (spmd, plain):
+            if e is not None:
+                e.close()
         dist.destroy_process_group()
