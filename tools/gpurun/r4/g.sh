@@ -19,6 +19,10 @@ export OUT=$R/$O/mlp_trace.json
 step trace 200 python tools/mlp_layerwise_bench.py 8192 --trace
 export OUT=$R/$O/mlp_layerwise.json
 step layerwise 300 python tools/mlp_layerwise_bench.py 8192,16384
+cd /tmp
+export OUT=/tmp/lw.json
+step prof_cfg4 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof_cfg4 -o lw -- python $R/tools/mlp_layerwise_bench.py 8192
+cd $R
 for rpc in ltv segment abuse; do
   step curve_$rpc 400 python -u tools/bench_e2e.py --scope grpc --rpc $rpc --open-loop --rates 50000,100000,150000,200000 \
     --seconds 4 --clients 8 --json-out $R/$O/${rpc}_curve.json

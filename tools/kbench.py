@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--hot", type=float, default=0.02, help="fraction of requests on 16 hot accounts")
     ap.add_argument("--only", default="", help="comma-separated op names to run")
+    ap.add_argument("--cold", action="store_true",
+                    help="rotating K1 batches draw fresh uniform account slots each round (cold state)")
     a = ap.parse_args()
     import torch
     from igaming_platform_amd.ops import kernels as K
@@ -107,6 +109,8 @@ def main():
       for i in range(24):
           vv = sc.slab_view(slot, B)
           vv[:] = S.pool[i % len(S.pool)]
+          if a.cold:  # every round a fresh uniform draw over the population: cold account lines
+              vv["slot"] = np.random.default_rng(1000 + i).integers(0, a.accounts, B).astype(np.int32)
           vv["ts"] = NOW0 + 1 + i
           sc._seq += 1
           sc._write_hdr(slot, B, NOW0 + 1 + i)
