@@ -268,20 +268,17 @@ class GpuScorer:
         self.cfg_dev.copy_(torch.from_numpy(c.view(np.uint8).copy()))
 
     # ------------------------------------------------------------------ the step
-    def _copy_body(self, slot: int, bucket: int, dedup: bool = True) -> None:
+    def _copy_body(self, slot: int, bucket: int) -> None:
         sb = self.slots[slot]
         nbytes = HDR_BYTES + REQ_BYTES * bucket
         K.memcpy_async(sb.dev_slab, self.host_slab[slot], nbytes)
-        if self.update_features and dedup:
+        if self.update_features:
             K.dedup_insert(self.store, self.cfg_dev, sb.req, bucket, sb.hdr)
 
-    def _state_body(self, slot: int, bucket: int, part: str = "all", dedup: bool = False) -> None:
+    def _state_body(self, slot: int, bucket: int, part: str = "all") -> None:
         """K1 (part "k1"), then the multi-event update that also clears the dedup region of
-        batch seq+3 (part "update"). ``dedup``: the batch's dedup insert runs here, right before
-        K1 on the state stream, instead of on the copy stream."""
+        batch seq+3 (part "update")."""
         sb, upd = self.slots[slot], self.update_features
-        if upd and dedup and part in ("all", "k1"):
-            K.dedup_insert(self.store, self.cfg_dev, sb.req, bucket, sb.hdr)
         if part in ("all", "k1"):
             K.feature_assemble(self.store, sb.hdr, self.cfg_dev, sb.req, sb.X, sb.feat, bucket, dedup=upd,
                                fenc=self._fenc_out(slot))
@@ -364,12 +361,9 @@ class GpuScorer:
                             # the state stage split in two (IGP_SPLIT_STATE, default on): the
                             # model waits for K1 only, the multi-event update runs beside it
                             split = os.environ.get("IGP_SPLIT_STATE", "1") == "1"
-                            # IGP_DEDUP_STATE=1: the dedup insert on the state stream before K1
-                            # (one same-queue kernel boundary instead of a copy -> state hand-off)
-                            ds = os.environ.get("IGP_DEDUP_STATE", "0") == "1"
                             lists = []
-                            for body in (lambda: self._copy_body(slot, b, dedup=not ds),
-                                         lambda: self._state_body(slot, b, "k1" if split else "all", dedup=ds),
+                            for body in (lambda: self._copy_body(slot, b),
+                                         lambda: self._state_body(slot, b, "k1" if split else "all"),
                                          lambda: self._model_body(slot, b),
                                          lambda: self._model_body(slot, b, with_features=True),
                                          lambda: self._state_body(slot, b, "update")):
