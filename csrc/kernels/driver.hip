@@ -375,7 +375,7 @@ class PipeDriver {
     // the state stage of batch seq - DEDUP_AHEAD cleared this batch's dedup region: wait for it
     // unless the host already sees it complete (an event query instead of a queue wait)
     if ((int)hist_.size() == DEDUP_AHEAD && (!query_skip_ || hipEventQuery(pe_[hist_.front()]) != hipSuccess))
-      hip_ok(hipStreamWaitEvent(cs_, pe_[hist_.front()], 0), "wait state-ahead");
+      hip_ok(hipStreamWaitEvent(cs_, pe_[hist_.front()], 0), "wait state-3");
     const auto t2 = clk::now();
     const bool cb = stage_rec(g.c, g.oc, cs_, ce, "copy graph");
     const auto t3 = clk::now();
@@ -387,7 +387,7 @@ class PipeDriver {
     if (!sb) hip_ok(hipEventRecord(se, ss_), "record state");
     hip_ok(hipStreamWaitEvent(ms_, se, 0), "wait state");
     // split state stage (direct launch): the model waited for K1 only; the multi-event update
-    // (which also clears the dedup region of batch seq + DEDUP_AHEAD) follows on the state stream and its
+    // (which also clears the dedup region of batch seq+3) follows on the state stream and its
     // own event gates that region's reuse
     const bool pb = g.osu && ext_events_ && g.osu->run_recording(ss_, pe_[slot]);
     if (g.osu && !ext_events_) g.osu->run(ss_);

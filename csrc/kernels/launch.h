@@ -16,11 +16,11 @@ constexpr int DEDUP_LIST = 64;
 // scorer batches rotate over DEDUP_RING dedup regions by BatchHdr::seq: batch q's state stage
 // clears the region of batch q + DEDUP_AHEAD, so batch q+1's dedup insert (copy stream) can run
 // while batch q is still in K1 / update_segments on the state stream. The copy of batch q waits
-// for the state stage of batch q - DEDUP_AHEAD; with five regions that batch is four back, and
-// the native driver skips the wait when the host already sees it complete (with up to four
-// batches in flight it always does: the host waited for batch q - 4 before submitting q into
-// its slot). Region DEDUP_STANDALONE: event ingestion.
-constexpr int DEDUP_RING = 5;
+// for the state stage of batch q - DEDUP_AHEAD; with four regions that batch is three back, and
+// the native driver skips the wait when the host already sees it complete (it usually does: the
+// host waited for batch q - 3's model before submitting q). Region DEDUP_STANDALONE: event
+// ingestion.
+constexpr int DEDUP_RING = 4;
 constexpr int DEDUP_AHEAD = DEDUP_RING - 1;
 constexpr int DEDUP_STANDALONE = DEDUP_RING;
 __host__ __device__ inline int dedup_ring_region(int seq) { return (int)((unsigned)seq % DEDUP_RING); }

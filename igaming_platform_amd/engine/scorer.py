@@ -10,7 +10,7 @@ One micro-batch = three captured hipGraphs on three HIP streams:
     K1   feature_assemble (+blacklist, +ip-intel, +HLL counts, +rules) -> X, FeatRec, then
          score-then-update of every account with one event in the batch
     K6b  update_multi: the multi-event accounts' events in row order (one wave each), then
-         clear the dedup region of batch seq+4 (five-region ring)
+         clear the dedup region of batch seq+3 (four-region ring)
   model stream (reads only the slot's X / FeatRec; never touches the store)
     K2/K3 model steps of the compiled ONNX plan                            -> ml
     K5   ensemble + action (+K10 metrics histogram)                        -> ResultRec
@@ -277,7 +277,7 @@ class GpuScorer:
 
     def _state_body(self, slot: int, bucket: int, part: str = "all") -> None:
         """K1 (part "k1"), then the multi-event update that also clears the dedup region of
-        batch seq+4 (part "update")."""
+        batch seq+3 (part "update")."""
         sb, upd = self.slots[slot], self.update_features
         if part in ("all", "k1"):
             K.feature_assemble(self.store, sb.hdr, self.cfg_dev, sb.req, sb.X, sb.feat, bucket, dedup=upd,
@@ -428,7 +428,7 @@ class GpuScorer:
         g = self.graphs.get((b, slot))
         with torch.cuda.stream(self.cstream):
             self.cstream.wait_event(self._model_ev[slot])  # the slot's device buffers are free
-            # batch seq-4's state stage cleared this batch's dedup region; seq-2's comes after it
+            # batch seq-3's state stage cleared this batch's dedup region; seq-2's comes after it
             if len(self._state_hist) == 2:
                 self.cstream.wait_event(self._state_hist[0])
             if g is not None:

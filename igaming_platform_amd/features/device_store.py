@@ -32,8 +32,8 @@ from ..layouts import ACCTBATCH, ACCTRT
 from .tables import Blacklist, IPIntel
 
 DEDUP_LIST = 64  # events per account per batch kept in a dedup list (launch.h DEDUP_LIST)
-DEDUP_REGIONS = 6  # 5 scorer ring regions (by batch seq) + 1 standalone ingestion region
-DEDUP_STANDALONE = 5
+DEDUP_REGIONS = 5  # 4 scorer ring regions (by batch seq) + 1 standalone ingestion region
+DEDUP_STANDALONE = 4
 
 
 def _pow2_at_least(n: int) -> int:
