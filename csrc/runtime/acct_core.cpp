@@ -395,6 +395,21 @@ void AcctCore::set_device(const IgpModelOps* dev) {
   q_cv_.notify_all();
 }
 
+void AcctCore::pause() {
+  std::unique_lock<std::mutex> lk(q_mu_);
+  hold_ = true;
+  q_cv_.notify_all();
+  idle_cv_.wait(lk, [&] { return inflight_ == 0 || stopped_; });
+}
+
+void AcctCore::resume() {
+  {
+    std::lock_guard<std::mutex> lk(q_mu_);
+    hold_ = false;
+  }
+  q_cv_.notify_all();
+}
+
 void AcctCore::stop() {
   {
     std::lock_guard<std::mutex> lk(q_mu_);
@@ -576,6 +591,16 @@ void AcctRouter::set_device(int kind, const IgpModelOps* dev) {
   AcctCore* c = kind == IGP_MODEL_LTV ? ltv_.get() : abuse_.get();
   if (!c) throw std::runtime_error("AcctRouter.set_device: no core of that kind");
   c->set_device(dev);
+}
+
+void AcctRouter::pause() {
+  for (AcctCore* c : {ltv_.get(), abuse_.get()})
+    if (c) c->pause();
+}
+
+void AcctRouter::resume() {
+  for (AcctCore* c : {ltv_.get(), abuse_.get()})
+    if (c) c->resume();
 }
 
 void AcctRouter::set_abuse(const AbuseParams& p) {

@@ -95,6 +95,10 @@ class AcctCore {
   void stop();
   // swap the device function table (hot model reload): blocks new steps, drains, swaps
   void set_device(const IgpModelOps* dev);
+  // no new device steps until resume(); returns once every step in flight finished (a device's
+  // shared state - its config block - can then be rewritten without a step reading it)
+  void pause();
+  void resume();
   int kind() const { return kind_; }
   AcctStats stats(bool reset);
 
@@ -227,6 +231,8 @@ class AcctRouter {
   // the local model devices (kind from the table): LTV serves PredictLTV + GetPlayerSegment
   void attach(const IgpModelOps* dev, AcctCore::Options opt);
   void set_device(int kind, const IgpModelOps* dev);
+  void pause();   // every local core (AcctCore::pause)
+  void resume();
   void set_links(std::shared_ptr<LinkIndex> l) { links_ = std::move(l); }
   void set_abuse(const AbuseParams& p);
   AbuseParams abuse() const;

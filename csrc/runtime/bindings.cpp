@@ -950,6 +950,11 @@ PYBIND11_MODULE(_native, m) {
         py::gil_scoped_release rel;
         a.router->set_device(ops->kind, ops);
       })
+      .def("pause", [](PyAcct& a) {
+        py::gil_scoped_release rel;
+        a.router->pause();
+      })
+      .def("resume", [](PyAcct& a) { a.router->resume(); })
       .def("set_links", [](PyAcct& a, std::shared_ptr<LinkIndex> l) { a.router->set_links(std::move(l)); })
       .def("set_abuse", [](PyAcct& a, int max_devices, int max_ips, int max_tx_per_minute, double threshold,
                            std::vector<double> weights, int linked_limit) {

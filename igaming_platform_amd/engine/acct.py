@@ -256,9 +256,17 @@ class NativeAcct:
                               [float(SIGNAL_WEIGHTS[k]) for k in SIGNAL_ORDER])
 
     def refresh(self) -> None:
-        for d in self.devices:
-            if hasattr(d, "refresh"):
+        """Re-copy the devices' config blocks with no step in flight (a device's slots run on
+        their own streams, so a copy on one stream could otherwise overlap a step on another)."""
+        devs = [d for d in self.devices if hasattr(d, "refresh")]
+        if not devs:
+            return
+        self.router.pause()
+        try:
+            for d in devs:
                 d.refresh()
+        finally:
+            self.router.resume()
 
     def serves(self, rpc: int) -> bool:
         return bool(self.router.serves(int(rpc)))

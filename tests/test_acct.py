@@ -359,3 +359,30 @@ def test_every_rank_serves_account_rpcs_owner_routed(world):
         if m[3] is not None:
             assert m[3] == want  # rank 0's SPMD Python path (OP_LTV / OP_ABUSE / OP_FEATMANY)
     ref.close()
+
+
+def test_router_pause_holds_new_steps_until_resume():
+    """AcctRouter.pause (used by a config refresh: the devices' config blocks are rewritten with
+    no step in flight) holds every new device step; resume releases them, nothing is lost."""
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.engine.risk_engine import RiskEngine
+    from igaming_platform_amd.onnx import builders
+    lm = builders.build("ltv_mlp", n_features=64, width=64, layers=2).SerializeToString()
+    eng = RiskEngine(Config(), backend="cpu", capacity=256, ltv_model=lm)
+    ids = _populate(eng)
+    reqs = [x for x in _requests(ids) if x[0] == 1][:8]
+    r = eng.acct.router
+    r.pause()
+    for i, (rpc, m) in enumerate(reqs):
+        r.submit(rpc, m.SerializeToString(), i, 0, NOW)
+    assert r.poll(64, 200000) == []            # held: no step issued while paused
+    r.resume()
+    got = {}
+    t_end = time.time() + 20
+    while len(got) < len(reqs) and time.time() < t_end:
+        for tag, b, e in r.poll(64, 50000):
+            got[int(tag)] = (b, e)
+    assert sorted(got) == list(range(len(reqs))) and all(e is None for _, e in got.values())
+    eng.acct.refresh()                          # pause / refresh / resume round trip
+    assert len(_ask(r, reqs)) == len(reqs)
+    eng.close()
