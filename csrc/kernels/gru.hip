@@ -615,6 +615,22 @@ static void launch_gru_x3(const GruArgs& a, hipStream_t st) {
   constexpr int NW = KSH >= 4 ? 8 : 4;
   const dim3 block(NW * 64);
   const int lbr = a.layer[0].lbr ? 1 : 0;
+  if constexpr (KSH == 8) {
+    // 16 waves (one hidden tile each, four waves per SIMD): twice the weight loads in flight
+    // per CU at the same LDS footprint (tools/gru_x3_bench.py)
+    if (a.waves == 16 && lbr) {
+      const int rt = a.tile_rows == 32 ? 2 : 1;
+      const size_t lds = gru_x3_lds_bytes(rt, KSX, KSH, 16, 1);
+      if (rt == 2 && lds <= 160 * 1024) {
+        IGP_LAUNCH((gru_x3_kernel<2, KSX, KSH, 1, 16>), dim3((a.n_rows + 31) / 32), dim3(1024), lds, st, a);
+        return;
+      }
+      if (rt == 1) {
+        IGP_LAUNCH((gru_x3_kernel<1, KSX, KSH, 1, 16>), dim3((a.n_rows + 15) / 16), dim3(1024), lds, st, a);
+        return;
+      }
+    }
+  }
   if (lbr && a.tile_rows == 32 && gru_x3_lds_bytes(2, KSX, KSH, NW, 1) <= 160 * 1024) {
     IGP_LAUNCH((gru_x3_kernel<2, KSX, KSH, 1, NW>), dim3((a.n_rows + 31) / 32), block,
                gru_x3_lds_bytes(2, KSX, KSH, NW, 1), st, a);

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""cfg5 f32-faithful GRU (gru_x3_kernel) occupancy sweep: rows per workgroup (16 / 32) x batch x
+"""cfg5 f32-faithful GRU (gru_x3_kernel) occupancy sweep: rows per workgroup (16 / 32) x waves
+per workgroup (8 / 16) x batch x
 concurrent launches on separate streams (1 = the serving rank's single stream, 2-3 = the
 bench's per-slot streams). Reports per-launch ms, checks/s and per-CU row rate so the two tile
 sizes can be compared on the same box; every variant's scores are compared with the first."""
@@ -28,11 +29,11 @@ def main() -> int:
             slots = [torch.from_numpy(np.random.default_rng(B + i).integers(0, 1 << 18, B).astype(np.int32)).to(dev)
                      for i in range(conc)]
             outs = [torch.zeros(B, device=dev) for _ in range(conc)]
-            for tr in (16, 32):
+            for tr, nw in ((16, 8), (32, 8), (16, 16), (32, 16)):
                 def run():
                     for s, sl, o in zip(streams, slots, outs):
                         with torch.cuda.stream(s):
-                            K.gru(R.gp, B, R.T, out=o, store=R.store, slots=sl, tile_rows=tr, ws=0)
+                            K.gru(R.gp, B, R.T, out=o, store=R.store, slots=sl, tile_rows=tr, waves=nw, ws=0)
                 run()
                 torch.cuda.synchronize()
                 key = (B, conc)
@@ -54,7 +55,7 @@ def main() -> int:
                     ts.append(e0.elapsed_time(e1))
                 ms = float(np.median(ts[1:]))
                 wgs = conc * ((B + tr - 1) // tr)
-                r = dict(batch=B, concurrent=conc, tile_rows=tr, workgroups=wgs, cus=cus, ms=round(ms, 3),
+                r = dict(batch=B, concurrent=conc, tile_rows=tr, waves=nw, workgroups=wgs, cus=cus, ms=round(ms, 3),
                          checks_per_s=round(conc * B / ms * 1e3), us_per_step=round(ms * 1e3 / R.T, 2),
                          max_diff_vs_16=diff)
                 res.append(r)
