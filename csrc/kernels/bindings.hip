@@ -573,16 +573,15 @@ PYBIND11_MODULE(_hipk, m) {
     a.waves = geti(d, "waves", 4);
     if (a.rows_per_block != 16 && a.rows_per_block != 32 && a.rows_per_block != 64)
       throw std::runtime_error("mlp_chain: 16, 32 or 64 rows per block");
-    if (a.waves != 4 && a.waves != 8 && !(a.waves == 16 && a.rows_per_block == 64))
-      throw std::runtime_error("mlp_chain: 4 or 8 waves (16 at 64 rows)");
+    if (a.waves != 4 && a.waves != 8) throw std::runtime_error("mlp_chain: 4 or 8 waves");
     for (int l = 0; l < a.n_layers; ++l)
       if (a.N[l] % (16 * a.waves)) throw std::runtime_error("mlp_chain: N must be a multiple of 16 x waves");
     a.split = geti(d, "split", 0);
     if (a.split) {
       for (int l = 0; l < a.n_layers; ++l)
         if (!a.W_lo[l]) throw std::runtime_error("mlp_chain: split mode needs every layer's residual weights");
-      if (a.rows_per_block != 32 && !(a.rows_per_block == 64 && a.waves >= 8))
-        throw std::runtime_error("mlp_chain: split mode runs 32 rows per block (64 with 8 or 16 waves)");
+      if (a.rows_per_block != 32 && !(a.rows_per_block == 64 && a.waves == 8))
+        throw std::runtime_error("mlp_chain: split mode runs 32 rows per block (64 with 8 waves)");
     }
     if (!a.w2) throw std::runtime_error("mlp_chain: head weights required");
     if (!a.slots && !a.X) throw std::runtime_error("mlp_chain: input");

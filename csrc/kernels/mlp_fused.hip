@@ -169,11 +169,10 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
     const int r = tid / PARTS, row = row0 + r;
     const bool live = row < n_live;
     const int s = (live && a.slots) ? a.slots[row] : -1;
-    constexpr int CW = WAVES >= 16 ? 16 : 32;  // columns per staging chunk (16 waves: 128 VGPRs)
-    for (int c0 = (tid % PARTS) * CW; c0 < K0; c0 += PARTS * CW) {
-      float v[CW];
+    for (int c0 = (tid % PARTS) * 32; c0 < K0; c0 += PARTS * 32) {
+      float v[32];
 #pragma unroll
-      for (int i = 0; i < CW; ++i) {
+      for (int i = 0; i < 32; ++i) {
         const int c = c0 + i;
         float x = 0.f;
         if (live && c < a.in_live) {
@@ -189,7 +188,7 @@ __global__ void __launch_bounds__(64 * WAVES) mlp_chain_kernel(MlpChainArgs a) {
         v[i] = x;
       }
 #pragma unroll
-      for (int i = 0; i < CW; ++i) {
+      for (int i = 0; i < 32; ++i) {
         const int c = c0 + i;
         float x = v[i];
         if (a.slots && c < P_NCOLS) {
@@ -300,9 +299,7 @@ void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
   const int r = a.rows_per_block;
   if (a.split) {  // f32-faithful: hi + lo tiles fill the LDS (64 rows: each tile once, NBUF = 1)
-    if (a.waves == 16 && r == 64)
-      IGP_LAUNCH((mlp_chain_kernel<64, 16, true, 1, 1>), dim3((a.n_rows + 63) / 64), dim3(1024), 0, st, a);
-    else if (a.waves == 8 && r == 64)
+    if (a.waves == 8 && r == 64)
       IGP_LAUNCH((mlp_chain_kernel<64, 8, true, MC_PF, 1>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
     else if (a.waves == 8)
       IGP_LAUNCH((mlp_chain_kernel<32, 8, true>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
@@ -310,11 +307,7 @@ void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st) {
       IGP_LAUNCH((mlp_chain_kernel<32, 4, true>), dim3((a.n_rows + 31) / 32), dim3(256), 0, st, a);
     return;
   }
-  if (a.waves == 16 && r == 64) {
-    // 64 rows x 16 waves (4 x 2 MFMA tiles per wave, four waves per SIMD): the same weight
-    // bytes per CU with twice the waves keeping fragment loads in flight
-    IGP_LAUNCH((mlp_chain_kernel<64, 16, false, 2>), dim3((a.n_rows + 63) / 64), dim3(1024), 0, st, a);
-  } else if (a.waves == 8 && r == 64) {
+  if (a.waves == 8 && r == 64) {
     // 64 rows x 8 waves (4 x 4 MFMA tiles per wave): per k-step a CU issues as many MFMA cycles
     // as it needs L1 cycles for the 32 KB of weight fragments (32 rows: half); a batch then
     // occupies half the CUs and the per-slot streams keep two batches in flight. Weights

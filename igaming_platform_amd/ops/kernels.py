@@ -838,9 +838,6 @@ def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, s
         d.update(X=_need(X, "X", torch.float32, device=dev), ldx=int(X.shape[1]))
     if ml is None and ltv_out is None:
         raise ValueError("mlp_chain: nothing to write")
-    if d["waves"] == 16 and (pk.split and os.environ.get("IGP_MLP_SPLIT_ROWS", "64") != "64"
-                             or not pk.split and d["rows_per_block"] != 64):
-        d["waves"] = 8  # 16 waves run 64-row tiles only
     for i, l in enumerate(pk.layers):
         d[f"l{i}_W"] = _need(l["W"], "W", torch.bfloat16, l["N"] * l["K"], dev)
         if pk.split:
@@ -850,6 +847,6 @@ def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, s
     if pk.split:
         # 64 rows x 8 waves (hi + lo tiles in LDS once): 123-128 vs 91 M predictions/s for 32
         # rows, same box (profiles/r3/x); 4-wave chains keep 32
-        rows = int(os.environ.get("IGP_MLP_SPLIT_ROWS", "64" if d["waves"] >= 8 else "32"))
-        d.update(split=1, rows_per_block=rows if d["waves"] >= 8 else 32)
+        rows = int(os.environ.get("IGP_MLP_SPLIT_ROWS", "64" if d["waves"] == 8 else "32"))
+        d.update(split=1, rows_per_block=rows if d["waves"] == 8 else 32)
     _mod().mlp_chain(d, _stream())

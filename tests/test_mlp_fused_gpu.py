@@ -75,15 +75,6 @@ def test_mlp_chain_64_row_tiles_match_32(monkeypatch):
         outs[rows] = ml.cpu()
     assert torch.equal(outs["32"], outs["64"])
     assert torch.all(outs["64"][n - 23:] == -7.0) and not torch.any(outs["64"][:n - 23] == -7.0)
-    # 16 waves at 64 rows (4 x 2 tiles per wave): hidden layers identical, the head's partial
-    # sums reduce over 16 waves instead of 8 (summation order only)
-    monkeypatch.setenv("IGP_MLP_WAVES", "16")
-    assert pk.waves() == 16
-    ml = torch.full((n,), -7.0, device=dev)
-    K.mlp_chain(pk, n, X=X, ml=ml, m_ptr=m_ptr)
-    torch.cuda.synchronize()
-    np.testing.assert_allclose(ml.cpu().numpy()[:n - 23], outs["64"].numpy()[:n - 23], rtol=1e-5, atol=1e-6)
-    assert torch.all(ml.cpu()[n - 23:] == -7.0)
 
 
 def _ltv_gpu(fused: bool, plan, dev, cap):
@@ -189,13 +180,6 @@ def test_mlp_chain_split_64_row_tiles_match_32(monkeypatch):
         outs[rows] = ml.cpu()
     assert torch.equal(outs["32"], outs["64"])
     assert torch.all(outs["64"][n - 29:] == -7.0) and not torch.any(outs["64"][:n - 29] == -7.0)
-    monkeypatch.setenv("IGP_MLP_WAVES", "16")  # 16 waves: head summation order only
-    assert pk.waves() == 16
-    ml = torch.full((n,), -7.0, device=dev)
-    K.mlp_chain(pk, n, X=X, ml=ml, m_ptr=m_ptr)
-    torch.cuda.synchronize()
-    np.testing.assert_allclose(ml.cpu().numpy()[:n - 29], outs["64"].numpy()[:n - 29], rtol=1e-5, atol=1e-6)
-    assert torch.all(ml.cpu()[n - 29:] == -7.0)
 
 
 def test_ltv_fp32_plan_runs_the_split_chain_and_matches_the_executor():
