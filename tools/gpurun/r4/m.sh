@@ -20,3 +20,12 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke o
 step bench 400 python bench.py --steps 20 --warmup 5 --json-out $R/$O/bench.json
 step engine 400 python bench.py --steps 20 --warmup 5 --scope engine_only --json-out $R/$O/engine.json
 OUT=$R/$O/gru_x3_sweep.json step gru_x3 300 python tools/gru_x3_bench.py
+# cfg4 chain: 8 vs 16 waves per 64-row workgroup, interleaved, fp32 (split) and bf16
+for i in 1 2; do
+  for w in 8 16; do
+    IGP_MLP_WAVES=$w step cfg4_fp32_w${w}_$i 300 python bench.py --config cfg4 --steps 20 --warmup 5 --json-out $R/$O/cfg4_fp32_w${w}_$i.json
+  done
+done
+for w in 8 16; do
+  IGP_MLP_WAVES=$w step cfg4_bf16_w$w 300 python bench.py --config cfg4 --numerics bf16 --steps 20 --warmup 5 --json-out $R/$O/cfg4_bf16_w$w.json
+done
