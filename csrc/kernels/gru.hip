@@ -616,9 +616,11 @@ static void launch_gru_x3(const GruArgs& a, hipStream_t st) {
   const dim3 block(NW * 64);
   const int lbr = a.layer[0].lbr ? 1 : 0;
   if constexpr (KSH == 8) {
-    // 16 waves (one hidden tile each, four waves per SIMD): twice the weight loads in flight
-    // per CU at the same LDS footprint (tools/gru_x3_bench.py)
-    if (a.waves == 16 && lbr) {
+    // H = 256: 16 waves (one hidden tile each, four waves per SIMD) keep twice the weight loads
+    // in flight per CU at the same LDS footprint: +16 % at 16 rows on one stream, +3-8 % at 32
+    // rows with the slots' streams overlapped (tools/gru_x3_bench.py, profiles/r4/m); waves = 8
+    // keeps the 8-wave kernel
+    if (a.waves != 8 && lbr) {
       const int rt = a.tile_rows == 32 ? 2 : 1;
       const size_t lds = gru_x3_lds_bytes(rt, KSX, KSH, 16, 1);
       if (rt == 2 && lds <= 160 * 1024) {

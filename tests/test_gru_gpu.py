@@ -305,7 +305,8 @@ def test_gru_split_32_row_tiles_match_16():
     """The f32-faithful split GRU at 32 rows per workgroup (two row tiles share every streamed
     hi / lo weight fragment; linear_before_reset, H = 256; the cfg5 bench runs it with one
     stream per pipeline slot) equals the 16-row kernel bit for bit, with a batch that ends
-    inside a workgroup; the 16-wave variants agree to 1e-6."""
+    inside a workgroup (16 waves per workgroup by default at H = 256; the 8-wave kernel agrees to
+    1e-6)."""
     import torch
     from igaming_platform_amd.engine.runner import DeviceModel
     from igaming_platform_amd.models.plan import compile_onnx, to_device
@@ -317,7 +318,7 @@ def test_gru_split_32_row_tiles_match_16():
     rows = 1000
     Xd = torch.from_numpy(np.random.default_rng(9).standard_normal((40, rows, 16)).astype(np.float32)).cuda()
     outs = {}
-    for tile, waves in ((16, 0), (32, 0), (16, 16), (32, 16)):
+    for tile, waves in ((16, 8), (32, 8), (16, 0), (32, 0)):
         dm = DeviceModel(plan, "cuda", [rows])
         assert dm.gru.split
         dm.gru.packs[0].x3_rows = tile
@@ -325,10 +326,11 @@ def test_gru_split_32_row_tiles_match_16():
         outs[tile, waves] = dm.run(Xd, rows)[:rows].reshape(-1).cpu().numpy().copy()
     assert np.all(np.isfinite(outs[32, 0]))
     np.testing.assert_array_equal(outs[16, 0], outs[32, 0])
-    # 16 waves (one hidden tile each): same recurrence per unit, the head's partial sums reduce
-    # over 16 waves instead of 8 (summation order only)
+    np.testing.assert_array_equal(outs[16, 8], outs[32, 8])
+    # default 16 waves (one hidden tile each) vs 8: same recurrence per unit, the head's partial
+    # sums reduce over 16 waves instead of 8 (summation order only)
     for tile in (16, 32):
-        np.testing.assert_allclose(outs[tile, 16], outs[16, 0], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(outs[tile, 0], outs[16, 8], rtol=0, atol=1e-6)
 
 
 def test_abuse_gpu_overlapped_slots_match_one_stream():
