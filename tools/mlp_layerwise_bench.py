@@ -2,7 +2,8 @@
 """cfg 4 design comparison: the fused LTV chain kernel (one launch, 64-row
 tiles, weights streamed from L2 per tile) against a layer-wise plan (one large-tile MFMA GEMM per
 layer, 8192 x 512 activations staying in L2 / MALL between launches, the N=1 head last), both
-captured in a hipGraph and replayed on one stream, same weights, same inputs; and the dedicated layer-wise kernels (mlp_layers.hip).
+captured in a hipGraph and replayed on one stream, same weights, same inputs; and the dedicated
+layer-wise kernels (mlp_layers.hip).
 
 Prints one JSON line per (design, precision, batch): microseconds per forward, predictions/s,
 TFLOP/s, max |diff| against the chain. Usage: python tools/mlp_layerwise_bench.py [8192,16384]"""
