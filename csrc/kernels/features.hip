@@ -706,10 +706,18 @@ __global__ void update_single_kernel(UpdateArgs a) {
   if (r.slot >= 0 && row_owned(r, *a.cfg)) update_event(a, upd_region(a), i, r.slot);
 }
 
+// lane `l` (wave-uniform) of a 64-bit value, via two v_readlane
+__device__ __forceinline__ int64_t rdlane64(int64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // PFADD of up to 64 same-account events at once: the per-register winner writes the max,
 // each event learns whether it raised its register (the GRU's new-device/new-ip feature)
 // exactly as the sequential order would have.
 // pre: the lane's register byte rg[hq & 255], loaded by the caller beside the other HLL's
+template <bool LDSR>
 __device__ __forceinline__ uint32_t hll_segment(const UpdateArgs& a, uint8_t* rg, uint32_t exp, uint64_t hq,
                                                 int64_t ts, int lane, bool& changed, int pre) {
   const bool has = hq != 0;
@@ -717,20 +725,53 @@ __device__ __forceinline__ uint32_t hll_segment(const UpdateArgs& a, uint8_t* rg
   if (!any) return exp;
   const int fl = __ffsll((long long)any) - 1;
   const int ll = 63 - __clzll((long long)any);
-  const int64_t tfirst = __shfl(ts, fl, 64), tlast = __shfl(ts, ll, 64);
+  const int64_t tfirst = rdlane64(ts, fl), tlast = rdlane64(ts, ll);
   const bool reset = tfirst >= (int64_t)exp;
   const int idx = has ? (int)(hq & 255u) : -1;
   const int rank = has ? hll_rank(hq) : 0;
   const int before = (has && !reset) ? pre : 0;
   if (reset) {
     reinterpret_cast<uint32_t*>(rg)[lane] = 0u;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    if constexpr (LDSR) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // one wave's LDS: in order
+    else __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   }
   int pm = before;
   bool win = has;
-  for (int y = 0; y <= ll; ++y) {  // events occupy lanes 0..ll
-    const int iy = __shfl(idx, y, 64), ry = __shfl(rank, y, 64);
-    if (has && iy == idx && y != lane) {
+  // one pass per distinct register index among the events (a few per account: its devices /
+  // ips), not per event. Lanes of a group share idx; when they also share the rank (the same
+  // hash repeated, the common case) the group's first lane is the only one that can raise the
+  // register and the later ones see its rank; a group of different ranks (distinct hashes on
+  // one register) walks its lanes. Wave-uniform lanes come through v_readlane.
+  uint64_t rem = any;
+  for (int ng = 0; rem && ng < 8; ++ng) {
+    const int lead = __ffsll((long long)rem) - 1;
+    const int v = __builtin_amdgcn_readlane(idx, lead), rl = __builtin_amdgcn_readlane(rank, lead);
+    const bool in = has && idx == v;
+    const uint64_t g = __ballot(in);
+    rem &= ~g;
+    if (__ballot(in && rank == rl) == g) {
+      if (in && lane != lead) {
+        pm = max(pm, rl);
+        win = false;
+      }
+    } else {
+      for (uint64_t q = g; q; q &= q - 1) {
+        const int y = __ffsll((long long)q) - 1;
+        const int ry = __builtin_amdgcn_readlane(rank, y);
+        if (in && y != lane) {
+          if (y < lane) pm = max(pm, ry);
+          if (ry > rank || (ry == rank && y < lane)) win = false;
+        }
+      }
+    }
+  }
+  // more than 8 distinct registers in the chunk: the rest lane by lane (groups leave whole, so
+  // a remaining lane's group mates are all in `rem`)
+  const bool left = has && ((rem >> lane) & 1ull);
+  for (uint64_t q = rem; q; q &= q - 1) {
+    const int y = __ffsll((long long)q) - 1;
+    const int iy = __builtin_amdgcn_readlane(idx, y), ry = __builtin_amdgcn_readlane(rank, y);
+    if (left && iy == idx && y != lane) {
       if (y < lane) pm = max(pm, ry);
       if (ry > rank || (ry == rank && y < lane)) win = false;
     }
@@ -744,23 +785,33 @@ __device__ __forceinline__ uint32_t hll_segment(const UpdateArgs& a, uint8_t* rg
 // request row), to the account's AcctRT `r` (the same value in every lane, updated in place):
 // in parallel when the events span less than the shortest TTL (then no key can expire
 // mid-chunk: on the scorer path every event of a batch happens at the batch clock, span 0);
-// otherwise lane 0 applies them one by one. The caller stores r.
-__device__ void apply_chunk(const UpdateArgs& a, int s, AcctRT& r, int j, int c, int lane) {
+// otherwise lane 0 applies them one by one. The caller stores r. `regs`: the account's HLL
+// registers in the store, or (LDSR) the wave's LDS copy that a hot account's chunks share.
+// A hot account's chunk k0 of ctot events (the scan below): a tx-ring entry or GRU event row
+// that a later event of the same batch overwrites (event k < ctot - ring size) is not written.
+template <bool LDSR>
+__device__ void apply_chunk(const UpdateArgs& a, int s, AcctRT& r, int j, int c, int lane, uint8_t* regs,
+                            int k0 = 0, int ctot = 0) {
   const bool act = lane < c;
   ReqRec ev{};
   if (act) ev = a.req[j];
+  // scorer path: every event happens at the batch clock, whose hour-of-day word the batch's
+  // dedup insert already computed (region ctr[1])
+  const int64_t hour_word = (a.hdr && a.ev) ? (int64_t)(uint32_t)upd_region(a).ctr[1] : -1;
   const int64_t ts = act ? event_ts(a, ev) : 0;
   const ScoreCfg& cfg = *a.cfg;
   const int min_ttl = min(min(cfg.session_ttl, cfg.sum_ttl), min(cfg.hll_ttl, cfg.last_tx_ttl));
-  const int64_t ts0 = __shfl(ts, 0, 64);
-  const int64_t tsl = __shfl(ts, c - 1, 64);
+  const int64_t ts0 = rdlane64(ts, 0);
+  const int64_t tsl = rdlane64(ts, c - 1);
   const int64_t big = 0x3fffffffffffffffLL;
-  const int64_t tmx = wave_max(act ? ts : -big);
-  const int64_t tmn = -wave_max(act ? -ts : -big);
+  // every event at one clock (the scorer path): span 0 without the two 64-bit wave reductions
+  const bool one_clock = __ballot(act && ts != ts0) == 0ull;
+  const int64_t tmx = one_clock ? ts0 : wave_max(act ? ts : -big);
+  const int64_t tmn = one_clock ? ts0 : -wave_max(act ? -ts : -big);
   if (tmx - tmn >= (int64_t)min_ttl) {
     for (int x = 0; x < c; ++x) {
-      const int jx = __shfl(j, x, 64);
-      if (lane == 0) apply_event(a, jx, r);
+      const int jx = __builtin_amdgcn_readlane(j, x);
+      if (lane == 0) apply_event(a, jx, r, regs);
     }
     // every lane continues with lane 0's state
     r.ring_head = __shfl(r.ring_head, 0, 64);
@@ -775,11 +826,12 @@ __device__ void apply_chunk(const UpdateArgs& a, int s, AcctRT& r, int j, int c,
     r.session_start = (uint32_t)__shfl((int)r.session_start, 0, 64);
     r.session_exp = (uint32_t)__shfl((int)r.session_exp, 0, 64);
     r.last_event_ts = (uint32_t)__shfl((int)r.last_event_ts, 0, 64);
+    if constexpr (LDSR) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // lane 0's register writes
     return;
   }
   const int64_t amt = act ? ev.amount : 0;
   // tx ring: consecutive positions from the head
-  if (act) {
+  if (act && k0 + lane >= ctot - a.ring_size) {
     const int pos = (r.ring_head + lane) % a.ring_size;
     a.ring_ts[(size_t)s * a.ring_size + pos] = (uint32_t)ts;
     a.ring_amt[(size_t)s * a.ring_size + pos] = amt;
@@ -789,15 +841,15 @@ __device__ void apply_chunk(const UpdateArgs& a, int s, AcctRT& r, int j, int c,
   r.sum_compat = (ts0 >= (int64_t)r.sum_exp ? 0 : r.sum_compat) + tot;
   r.sum_exp = (uint32_t)(tsl + cfg.sum_ttl);
   // HyperLogLogs
-  uint8_t* regs = a.hll + (size_t)s * 512;
   bool new_dev = false, new_ip = false;
   const uint64_t dq = act ? ev.dev_hash : 0, iq = act ? ev.ip_hash : 0;
   const int pd = dq ? (int)regs[dq & 255u] : 0;  // both registers in one memory round trip
   const int pi = iq ? (int)regs[256 + (iq & 255u)] : 0;
-  r.hll_dev_exp = hll_segment(a, regs, r.hll_dev_exp, dq, ts, lane, new_dev, pd);
-  r.hll_ip_exp = hll_segment(a, regs + 256, r.hll_ip_exp, iq, ts, lane, new_ip, pi);
+  r.hll_dev_exp = hll_segment<LDSR>(a, regs, r.hll_dev_exp, dq, ts, lane, new_dev, pd);
+  r.hll_ip_exp = hll_segment<LDSR>(a, regs + 256, r.hll_ip_exp, iq, ts, lane, new_ip, pi);
   // the next chunk re-reads registers this one wrote (other lanes' stores)
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  if constexpr (LDSR) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  else __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   // last tx / session
   if (ts0 >= (int64_t)r.session_exp || r.session_start == 0) r.session_start = (uint32_t)ts0;
   r.session_exp = (uint32_t)(tsl + cfg.session_ttl);
@@ -806,10 +858,10 @@ __device__ void apply_chunk(const UpdateArgs& a, int s, AcctRT& r, int j, int c,
   // event ring: event x's predecessor is event x-1 (event 0's is the stored last event)
   const int64_t up = __shfl(ts, lane > 0 ? lane - 1 : 0, 64);
   const int64_t prev = lane == 0 ? (int64_t)r.last_event_ts : up;
-  if (a.ev && act) {
+  if (a.ev && act && k0 + lane >= ctot - a.ev_ring) {
     const int pos = (r.ev_head + lane) % a.ev_ring;
     write_event_row(a.ev + ((size_t)s * a.ev_ring + pos) * a.ev_dim, amt, ev.tx_type & 0xff, ts, prev, new_dev,
-                    new_ip);
+                    new_ip, hour_word);
   }
   if (a.ev) {
     r.ev_head = (r.ev_head + c) % a.ev_ring;
@@ -822,43 +874,70 @@ __device__ void apply_chunk(const UpdateArgs& a, int s, AcctRT& r, int j, int c,
 // account s has more events in the batch than its dedup list holds (a hot account: Zipf
 // traffic gives the top account hundreds of rows in an 8192-row batch): scan the batch 64 rows
 // per ballot, compact the account's rows (row order) into a 64-event chunk in registers and
-// apply full chunks in parallel (apply_chunk); the chunk carries over between windows.
-__device__ void apply_scan_chunks(const UpdateArgs& a, int s, AcctRT r, int lane) {
+// apply full chunks in parallel (apply_chunk); the chunk carries over between windows. The
+// {slot, tx_type} words of SCAN_W windows are loaded at once (one memory round trip per 512
+// rows instead of per 64), and the account's HLL registers stay in the wave's LDS slice `lr`
+// (128 words) for all its chunks: a chunk's register reads and writes are LDS operations, and
+// the store's copy is written back once at the end.
+constexpr int SCAN_W = 8;
+__device__ void apply_scan_chunks(const UpdateArgs& a, int s, AcctRT r, int lane, uint32_t* lr, int ctot) {
   const int n = upd_n(a);
+  const ScoreCfg& cfg = *a.cfg;
+  const bool filt = cfg.owner_filter != 0;
+  const int me = cfg.my_rank;
+  uint32_t* const g = reinterpret_cast<uint32_t*>(a.hll + (size_t)s * 512);
+  lr[lane] = g[lane];
+  lr[64 + lane] = g[64 + lane];
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  uint8_t* const regs = reinterpret_cast<uint8_t*>(lr);
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes below this one
   int pj = 0, p = 0;  // pending chunk: lane k < p holds its k-th row
-  for (int base = 0; base < n; base += 64) {
-    const int i = base + lane;
-    const bool m = i < n && a.req[i].slot == s && row_owned(a.req[i], *a.cfg);
-    const uint64_t b = __ballot(m);
-    if (!b) continue;
-    const int cw = __popcll(b);
-    // the window's rows compacted to lanes 0..cw-1 (a push permute; other lanes fill behind)
-    const int dst = m ? __popcll(b & lt) : cw + __popcll(~b & lt);
-    const int wj = __builtin_amdgcn_ds_permute(dst * 4, i);
-    // append to the pending chunk: lanes p..p+cw-1 take window rows 0..cw-1
-    const int take = __shfl(wj, lane >= p ? lane - p : 0, 64);
-    if (lane >= p && lane < p + cw) pj = take;
-    if (p + cw < 64) {
-      p += cw;
-      continue;
+  int k0 = 0;         // the account's events applied so far
+  for (int base0 = 0; base0 < n; base0 += 64 * SCAN_W) {
+    int2 kv[SCAN_W];
+#pragma unroll
+    for (int u = 0; u < SCAN_W; ++u) {
+      const int i = base0 + 64 * u + lane;
+      kv[u] = i < n ? *reinterpret_cast<const int2*>(a.req + i) : make_int2(-1, 0);  // {slot, tx_type}
     }
-    apply_chunk(a, s, r, pj, 64, lane);
-    const int over = p + cw - 64;  // window rows that did not fit: the next chunk's head
-    const int rest = __shfl(wj, min(lane + 64 - p, 63), 64);
-    if (lane < over) pj = rest;
-    p = over;
+#pragma unroll
+    for (int u = 0; u < SCAN_W; ++u) {
+      const int i = base0 + 64 * u + lane;
+      const bool m = kv[u].x == s && (!filt || ((kv[u].y >> 8) & 0xff) == me);
+      const uint64_t b = __ballot(m);
+      if (!b) continue;
+      const int cw = __popcll(b);
+      // the window's rows compacted to lanes 0..cw-1 (a push permute; other lanes fill behind)
+      const int dst = m ? __popcll(b & lt) : cw + __popcll(~b & lt);
+      const int wj = __builtin_amdgcn_ds_permute(dst * 4, i);
+      // append to the pending chunk: lanes p..p+cw-1 take window rows 0..cw-1
+      const int take = __shfl(wj, lane >= p ? lane - p : 0, 64);
+      if (lane >= p && lane < p + cw) pj = take;
+      if (p + cw < 64) {
+        p += cw;
+        continue;
+      }
+      apply_chunk<true>(a, s, r, pj, 64, lane, regs, k0, ctot);
+      k0 += 64;
+      const int over = p + cw - 64;  // window rows that did not fit: the next chunk's head
+      const int rest = __shfl(wj, min(lane + 64 - p, 63), 64);
+      if (lane < over) pj = rest;
+      p = over;
+    }
   }
-  if (p > 0) apply_chunk(a, s, r, pj, p, lane);
+  if (p > 0) apply_chunk<true>(a, s, r, pj, p, lane, regs, k0, ctot);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  g[lane] = lr[lane];
+  g[64 + lane] = lr[64 + lane];
   if (lane == 0) a.rt[s] = r;
 }
 
 // the c (>= 2) events of account s (dedup hash slot h) in row order, by one wave holding the
 // account's pre-batch AcctRT `r`; more than DEDUP_LIST events: the chunked batch scan.
 __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h, int c, int s, AcctRT r,
-                                   int lane) {
+                                   int lane, uint32_t* lr) {
   if (c > DEDUP_LIST) {
-    apply_scan_chunks(a, s, r, lane);
+    apply_scan_chunks(a, s, r, lane, lr, c);
     return;
   }
   // sort the (distinct) row indices: rank = #smaller, then push each to lane `rank`
@@ -867,9 +946,9 @@ __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h
                                     __HIP_MEMORY_SCOPE_AGENT);  // all 64 lanes: no wait on c first
   const int key = lane < c ? raw : (0x7fffffc0 | lane);
   int rank = 0;
-  for (int y = 0; y < c; ++y) rank += __shfl(key, y, 64) < key;  // lanes >= c hold sentinels
+  for (int y = 0; y < c; ++y) rank += __builtin_amdgcn_readlane(key, y) < key;  // lanes >= c: sentinels
   const int j = __builtin_amdgcn_ds_permute(rank * 4, key);
-  apply_chunk(a, s, r, j, c, lane);
+  apply_chunk<false>(a, s, r, j, c, lane, a.hll + (size_t)s * 512);
   if (lane == 0) a.rt[s] = r;
 }
 
@@ -879,6 +958,7 @@ constexpr int UPD_MULTI_BLOCKS = 64;  // 256 waves loop over the list (any count
 // list} -> request rows -> both HLL registers -> stores (the pair carries the account slot, so
 // count, AcctRT and the row list are loaded together)
 __global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
+  __shared__ uint32_t s_regs[4][128];  // per wave: a hot account's HLL registers
   const int lane = threadIdx.x & 63;
   const DedupTab t = upd_region(a);
   const int npair = t.nmax >> 1;
@@ -895,7 +975,7 @@ __global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
     const int c = t.count[h];
     const AcctRT r = a.rt[s];
     if (c < 2) continue;
-    apply_segment_wave(a, t, h, c, s, r, lane);
+    apply_segment_wave(a, t, h, c, s, r, lane, s_regs[threadIdx.x >> 6]);
   }
   // scorer ring: clear the region of batch seq + DEDUP_AHEAD (= seq-1's, consumed by now) for
   // its insert; the copy of that batch waits for this batch's state stage

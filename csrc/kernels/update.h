@@ -129,12 +129,14 @@ __device__ __forceinline__ uint32_t event_word(int k, int64_t amt, int tt, int64
   }
 }
 
-// encode + store one GRU event row (one thread), dim 16 bf16 = 32 B
+// encode + store one GRU event row (one thread), dim 16 bf16 = 32 B; `hour_word` >= 0: word 4
+// precomputed for `now` (the scorer's batch clock: dedup_insert_list_kernel), no sin / cos here
 __device__ __forceinline__ void write_event_row(uint16_t* e, int64_t amt, int tt, int64_t now, int64_t prev,
-                                                bool new_dev, bool new_ip) {
+                                                bool new_dev, bool new_ip, int64_t hour_word = -1) {
   uint32_t w[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) w[k] = event_word(k, amt, tt, now, prev, new_dev, new_ip);
+  for (int k = 0; k < 8; ++k)
+    w[k] = (k == 4 && hour_word >= 0) ? (uint32_t)hour_word : event_word(k, amt, tt, now, prev, new_dev, new_ip);
   uint4* e4 = reinterpret_cast<uint4*>(e);
   e4[0] = make_uint4(w[0], w[1], w[2], w[3]);
   e4[1] = make_uint4(w[4], w[5], w[6], w[7]);
@@ -146,8 +148,9 @@ __device__ __forceinline__ int64_t event_ts(const UpdateArgs& a, const ReqRec& e
   return a.hdr ? a.hdr->now : ev.ts;
 }
 
-// apply one event to an account whose AcctRT `r` the caller holds in registers
-__device__ __forceinline__ void apply_event(const UpdateArgs& a, int j, AcctRT& r) {
+// apply one event to an account whose AcctRT `r` the caller holds in registers; `regs` = the
+// account's 512 HLL register bytes (the store's, or a wave's LDS copy of them)
+__device__ __forceinline__ void apply_event(const UpdateArgs& a, int j, AcctRT& r, uint8_t* regs) {
   const ReqRec ev = a.req[j];
   const int s = ev.slot;
   const int64_t now = event_ts(a, ev);
@@ -161,7 +164,6 @@ __device__ __forceinline__ void apply_event(const UpdateArgs& a, int j, AcctRT& 
   r.sum_compat += amt;
   r.sum_exp = (uint32_t)(now + cfg.sum_ttl);
   bool new_dev = false, new_ip = false;
-  uint8_t* regs = a.hll + (size_t)s * 512;
   if (ev.dev_hash) hll_add(regs, r.hll_dev_exp, ev.dev_hash, now, cfg.hll_ttl, new_dev);
   if (ev.ip_hash) hll_add(regs + 256, r.hll_ip_exp, ev.ip_hash, now, cfg.hll_ttl, new_ip);
   r.last_tx = (uint32_t)now;
@@ -175,6 +177,10 @@ __device__ __forceinline__ void apply_event(const UpdateArgs& a, int j, AcctRT& 
     r.ev_count = r.ev_count + 1 > a.ev_ring ? a.ev_ring : r.ev_count + 1;
   }
   r.last_event_ts = (uint32_t)now;
+}
+
+__device__ __forceinline__ void apply_event(const UpdateArgs& a, int j, AcctRT& r) {
+  apply_event(a, j, r, a.hll + (size_t)a.req[j].slot * 512);
 }
 
 // event i of a multi-event account (hash slot h): append it to the account's list; the
