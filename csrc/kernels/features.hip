@@ -665,7 +665,10 @@ __global__ void dedup_insert_kernel(UpdateArgs a) {
   if (i == 0 && a.hdr) upd_region(a).ctr[1] = (int32_t)event_word(4, 0, 0, a.hdr->now, 0, false, false);
   if (i >= upd_n(a)) return;
   const ReqRec& r = a.req[i];
-  if (r.slot >= 0 && row_owned(r, *a.cfg)) dedup_insert(upd_region(a), r.slot, i);
+  const DedupTab t = upd_region(a);
+  const bool mine = r.slot >= 0 && row_owned(r, *a.cfg);
+  if (i < t.nmax) t.rows[i] = mine ? r.slot : -1;
+  if (mine) dedup_insert(t, r.slot, i);
 }
 
 // Scorer head: register the batch's events in its dedup region (cleared two batches ahead by
@@ -681,7 +684,9 @@ __global__ void __launch_bounds__(64) dedup_insert_list_kernel(UpdateArgs a) {
   if (i >= upd_n(a)) return;
   const int2 r = *reinterpret_cast<const int2*>(a.req + i);  // {slot, tx_type}
   const ScoreCfg& cfg = *a.cfg;
-  if (r.x < 0 || (cfg.owner_filter && ((r.y >> 8) & 0xff) != cfg.my_rank)) return;
+  const bool mine = r.x >= 0 && !(cfg.owner_filter && ((r.y >> 8) & 0xff) != cfg.my_rank);
+  if (i < t.nmax) t.rows[i] = mine ? r.x : -1;  // compact account column for hot-account scans
+  if (!mine) return;
   uint32_t h = mix32((uint32_t)r.x) & (uint32_t)(t.cap - 1);
   for (int p = 0; p < t.cap; ++p) {
     const int prev = atomicCAS(&t.keys[h], -1, r.x);
@@ -874,17 +879,15 @@ __device__ void apply_chunk(const UpdateArgs& a, int s, AcctRT& r, int j, int c,
 // account s has more events in the batch than its dedup list holds (a hot account: Zipf
 // traffic gives the top account hundreds of rows in an 8192-row batch): scan the batch 64 rows
 // per ballot, compact the account's rows (row order) into a 64-event chunk in registers and
-// apply full chunks in parallel (apply_chunk); the chunk carries over between windows. The
-// {slot, tx_type} words of SCAN_W windows are loaded at once (one memory round trip per 512
-// rows instead of per 64), and the account's HLL registers stay in the wave's LDS slice `lr`
-// (128 words) for all its chunks: a chunk's register reads and writes are LDS operations, and
-// the store's copy is written back once at the end.
-constexpr int SCAN_W = 8;
-__device__ void apply_scan_chunks(const UpdateArgs& a, int s, AcctRT r, int lane, uint32_t* lr, int ctot) {
-  const int n = upd_n(a);
-  const ScoreCfg& cfg = *a.cfg;
-  const bool filt = cfg.owner_filter != 0;
-  const int me = cfg.my_rank;
+// apply full chunks in parallel (apply_chunk); the chunk carries over between windows. The scan
+// reads the insert's compact row -> account column (4 B per row instead of a 48-B request
+// record), SCAN_W windows per memory round trip, and the account's HLL registers stay in the
+// wave's LDS slice `lr` (128 words) for all its chunks: a chunk's register reads and writes are
+// LDS operations, and the store's copy is written back once at the end.
+constexpr int SCAN_W = 16;
+__device__ void apply_scan_chunks(const UpdateArgs& a, const DedupTab& t, int s, AcctRT r, int lane, uint32_t* lr,
+                                  int ctot) {
+  const int n = min(upd_n(a), t.nmax);
   uint32_t* const g = reinterpret_cast<uint32_t*>(a.hll + (size_t)s * 512);
   lr[lane] = g[lane];
   lr[64 + lane] = g[64 + lane];
@@ -894,16 +897,17 @@ __device__ void apply_scan_chunks(const UpdateArgs& a, int s, AcctRT r, int lane
   int pj = 0, p = 0;  // pending chunk: lane k < p holds its k-th row
   int k0 = 0;         // the account's events applied so far
   for (int base0 = 0; base0 < n; base0 += 64 * SCAN_W) {
-    int2 kv[SCAN_W];
+    // the insert's compact row -> account column (4 B per row; -1: not applied here)
+    int kv[SCAN_W];
 #pragma unroll
     for (int u = 0; u < SCAN_W; ++u) {
       const int i = base0 + 64 * u + lane;
-      kv[u] = i < n ? *reinterpret_cast<const int2*>(a.req + i) : make_int2(-1, 0);  // {slot, tx_type}
+      kv[u] = i < n ? t.rows[i] : -1;  // written by the batch's insert launch
     }
 #pragma unroll
     for (int u = 0; u < SCAN_W; ++u) {
       const int i = base0 + 64 * u + lane;
-      const bool m = kv[u].x == s && (!filt || ((kv[u].y >> 8) & 0xff) == me);
+      const bool m = kv[u] == s;
       const uint64_t b = __ballot(m);
       if (!b) continue;
       const int cw = __popcll(b);
@@ -937,7 +941,7 @@ __device__ void apply_scan_chunks(const UpdateArgs& a, int s, AcctRT r, int lane
 __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h, int c, int s, AcctRT r,
                                    int lane, uint32_t* lr) {
   if (c > DEDUP_LIST) {
-    apply_scan_chunks(a, s, r, lane, lr, c);
+    apply_scan_chunks(a, t, s, r, lane, lr, c);
     return;
   }
   // sort the (distinct) row indices: rank = #smaller, then push each to lane `rank`

@@ -83,8 +83,9 @@ class DeviceFeatureStore:
         self.dmax = self.max_events
         self.dcap = _pow2_at_least(2 * self.max_events)
         # per region (csrc/kernels/update.h dedup_region): keys/first/count/fill/done [cap],
-        # per-account event lists [cap][DEDUP_LIST], multi-account list [dmax], 2 counters
-        self.dregion = (5 * self.dcap + self.dcap * DEDUP_LIST + self.dmax + 2 + 15) & ~15
+        # per-account event lists [cap][DEDUP_LIST], multi-account list [dmax], 2 counters, the
+        # batch's row -> applied account slot array [dmax] (update.h dedup_region_size)
+        self.dregion = (5 * self.dcap + self.dcap * DEDUP_LIST + 2 * self.dmax + 2 + 15) & ~15
         self.dbuf = torch.empty(DEDUP_REGIONS * self.dregion, dtype=torch.int32, **z)
         self.reset_dedup()
 
