@@ -91,6 +91,35 @@ def test_gpu_hot_accounts_with_hundreds_of_events_per_batch_match_cpu():
         np.testing.assert_array_equal(hg, hc)
 
 
+def test_gpu_hot_accounts_with_many_devices_match_cpu():
+    """Hot accounts whose events carry hundreds of distinct devices / ips: a 64-event chunk then
+    touches more than 8 HLL registers (the per-lane fallback after the register groups) and
+    distinct hashes land on one register with different ranks (a group walked lane by lane);
+    store and scores must still equal the CPU engine's sequential apply."""
+    from igaming_platform_amd.onnx import builders
+    am = builders.build("gru", seq=100, hidden=64, layers=2).SerializeToString()
+    g, c = _engines(abuse_model=am)
+    rng = np.random.default_rng(11)
+    types = ["deposit", "withdraw", "bet", "win"]
+    for step in range(3):
+        acc = np.where(rng.random(1024) < 0.7, rng.integers(0, 2, 1024), rng.integers(2, 30, 1024))
+        txs = [dict(account_id=f"acc-{int(a)}", amount=int(rng.integers(1, 300000)),
+                    transaction_type=types[int(rng.integers(0, 4))], device_id=f"dev-{int(rng.integers(0, 400))}",
+                    ip_address=f"10.3.{int(rng.integers(0, 20))}.{int(rng.integers(0, 20))}") for a in acc]
+        a = g.score(txs, now=NOW + step * 20)
+        b = c.score(txs, now=NOW + step * 20)
+        assert [(x["score"], x["action"], x["reason_codes"]) for x in a] == \
+               [(y["score"], y["action"], y["reason_codes"]) for y in b]
+    for i in range(30):
+        fg, fc = g.get_features(f"acc-{i}", now=NOW + 100), c.get_features(f"acc-{i}", now=NOW + 100)
+        for k in ("tx_count_1h", "tx_sum_1h", "unique_devices_24h", "unique_ips_24h", "session_duration_sec"):
+            assert fg[k] == fc[k], (i, k)
+    for i in range(3):
+        hg = g.backends[0].event_history(g.registry.resolve_ids([f"acc-{i}"], insert=False)[0][0])
+        hc = c.backends[0].event_history(c.registry.resolve_ids([f"acc-{i}"], insert=False)[0][0])
+        np.testing.assert_array_equal(hg, hc)
+
+
 def test_gpu_engine_with_stacked_model_close_to_cpu():
     from igaming_platform_amd.onnx import builders
     cfg_w = 128
