@@ -677,30 +677,61 @@ __global__ void dedup_insert_kernel(UpdateArgs a) {
 // row). One thread per row, 64-thread workgroups spread over the chip: the kernel is a chain
 // of memory-side atomics (CAS, add, add), not work.
 __global__ void __launch_bounds__(64) dedup_insert_list_kernel(UpdateArgs a) {
-  const int i = blockIdx.x * 64 + threadIdx.x;
+  // the wave's rows grouped by account first (a 128-entry LDS table): one global probe and one
+  // count add per account and wave, not per row - under Zipf traffic the top account's rows
+  // (~1 in 5) otherwise queue their CAS / add on one hash slot
+  __shared__ int s_key[128], s_cnt[128], s_min[128], s_base[128], s_h[128];
+  const int lane = threadIdx.x;
+  const int i = blockIdx.x * 64 + lane;
   const DedupTab t = upd_region(a);
   // the batch clock's hour-of-day event-row word (sin/cos in double), once per batch for K1
   if (i == 0) t.ctr[1] = (int32_t)event_word(4, 0, 0, a.hdr->now, 0, false, false);
-  if (i >= upd_n(a)) return;
-  const int2 r = *reinterpret_cast<const int2*>(a.req + i);  // {slot, tx_type}
+  s_key[lane] = s_key[64 + lane] = -1;
+  s_cnt[lane] = s_cnt[64 + lane] = 0;
+  s_min[lane] = s_min[64 + lane] = 0x7fffffff;
+  const bool live = i < upd_n(a);
+  const int2 r = live ? *reinterpret_cast<const int2*>(a.req + i) : make_int2(-1, 0);  // {slot, tx_type}
   const ScoreCfg& cfg = *a.cfg;
   const bool mine = r.x >= 0 && !(cfg.owner_filter && ((r.y >> 8) & 0xff) != cfg.my_rank);
-  if (i < t.nmax) t.rows[i] = mine ? r.x : -1;  // compact account column for hot-account scans
-  if (!mine) return;
-  uint32_t h = mix32((uint32_t)r.x) & (uint32_t)(t.cap - 1);
-  for (int p = 0; p < t.cap; ++p) {
-    const int prev = atomicCAS(&t.keys[h], -1, r.x);
-    if (prev == -1 || prev == r.x) {
-      atomicMin(&t.first[h], i);
-      const int pos = atomicAdd(&t.count[h], 1);
-      if (pos < DEDUP_LIST) t.list[(size_t)h * DEDUP_LIST + pos] = i;
-      if (pos == 1) {
-        const int m = atomicAdd(&t.ctr[0], 1);
-        if (2 * m + 1 < t.nmax) *reinterpret_cast<int2*>(t.mlist + 2 * m) = make_int2((int)h, r.x);
-      }
-      break;
+  if (live && i < t.nmax) t.rows[i] = mine ? r.x : -1;  // compact account column for hot-account scans
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  int e = 0, lp = 0;
+  if (mine) {  // at most 64 keys in 128 entries: the probe always ends
+    e = (int)(mix32((uint32_t)r.x) & 127u);
+    for (int q = 0; q < 128; ++q) {
+      const int prev = atomicCAS(&s_key[e], -1, r.x);
+      if (prev == -1 || prev == r.x) break;
+      e = (e + 1) & 127;
     }
-    h = (h + 1) & (uint32_t)(t.cap - 1);
+    lp = atomicAdd(&s_cnt[e], 1);
+    atomicMin(&s_min[e], i);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (mine && lp == 0) {  // the account's first row in this wave probes the region for everyone
+    uint32_t h = mix32((uint32_t)r.x) & (uint32_t)(t.cap - 1);
+    for (int p = 0; p < t.cap; ++p) {
+      const int prev = atomicCAS(&t.keys[h], -1, r.x);
+      if (prev == -1 || prev == r.x) break;
+      h = (h + 1) & (uint32_t)(t.cap - 1);
+    }
+    atomicMin(&t.first[h], s_min[e]);
+    s_base[e] = atomicAdd(&t.count[h], s_cnt[e]);
+    s_h[e] = (int)h;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (!mine) return;
+  const int h = s_h[e];
+  const int pos = s_base[e] + lp;  // list order is arbitrary: the apply sorts the rows
+  if (pos < DEDUP_LIST) t.list[(size_t)h * DEDUP_LIST + pos] = i;
+  if (pos == 1) {  // the account's second row registers it as a multi-event account
+    const int m = atomicAdd(&t.ctr[0], 1);
+    if (2 * m + 1 < t.nmax) *reinterpret_cast<int2*>(t.mlist + 2 * m) = make_int2(h, r.x);
   }
 }
 
