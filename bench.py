@@ -72,6 +72,9 @@ def parse():
                          "device pipeline (device-pipeline number); e2e / grpc: tools/bench_e2e.py")
     ap.add_argument("--threads", type=int, default=16,
                     help="serving scope: ingress threads per rank (the box gives each GPU 16 CPUs)")
+    ap.add_argument("--rounds", type=int, default=16,
+                    help="serving scope: ScoreBatch requests per ingress thread in one timed step (a step of "
+                         "threads x rounds requests per rank keeps the driver's --steps 20 window >= 0.5 s)")
     ap.add_argument("--requests", type=int, default=0, help="serving scope: transactions per ScoreBatch request "
                     "(default: the config's micro-batch)")
     ap.add_argument("--rpc", default="batch", choices=["batch", "tx"], help="--scope grpc: ScoreBatch or unary "
@@ -453,9 +456,10 @@ def serving_bench(a) -> None:
         FeatureVector per transaction (nothing skipped: parse, resolve, routing, feature
         assembly + store update, trees, MLP, ensemble, results back, serialization)
 
-    A step = one ScoreBatch request per rank (K per rank timed, W untimed first); the value is
-    the whole job's transactions per second, the latency the per-request bytes-in -> bytes-out
-    time (it includes the micro-batch queueing inside the core)."""
+    A step = ``--rounds`` ScoreBatch requests per ingress thread (threads x rounds requests per
+    rank; K steps timed, W untimed first); the value is the whole job's transactions per second,
+    the latency the per-request bytes-in -> bytes-out time (it includes the micro-batch queueing
+    inside the core)."""
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     import threading
     import torch
@@ -572,15 +576,17 @@ def serving_bench(a) -> None:
         if comm is not None:
             comm.barrier()
 
-    # a serving step = one round of ScoreBatch requests, one per ingress thread (16 concurrent
-    # 8192-transaction requests per rank): timing single requests (the driver's --steps 20)
-    # would measure the threads' ramp up and down around ~2 requests per thread
-    run(max(a.warmup, 1) * a.threads, NOW0 - 3600, False)   # history + warm graphs / caches
+    # a serving step = --rounds rounds of ScoreBatch requests, one per ingress thread per round
+    # (16 concurrent 8192-transaction requests per rank per round): timing single requests (the
+    # driver's --steps 20) would measure the threads' ramp up and down, and one round per step
+    # made the driver's timed window ~32 ms
+    per_step = a.threads * max(1, a.rounds)
+    run(max(a.warmup, 1) * per_step, NOW0 - 3600, False)   # history + warm graphs / caches
     barrier()
     sync()
     core.stats(True)
     t0 = time.perf_counter()
-    run(a.steps * a.threads, NOW0, True)
+    run(a.steps * per_step, NOW0, True)
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -604,13 +610,15 @@ def serving_bench(a) -> None:
         elapsed, p99, p50 = (float(x) for x in mx)
     out = {
         "metric": "fraud scores/sec (whole node) + p99 score latency",
-        "value": world * a.steps * a.threads * B / elapsed, "unit": "scores/s", "n_gpus": world, "steps": a.steps,
+        "value": world * a.steps * per_step * B / elapsed, "unit": "scores/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": a.numerics, "data": "synthetic (UUID account ids, random-init weights)",
-        "config": {"model": c["desc"], "global_batch": B * a.threads * world, "seq_len": 1, "parallelism": f"dp{world}",
-                   "per_gpu_batch": B, "transactions_per_request": B, "requests_per_step_per_rank": a.threads,
-                   "step": "one 8192-transaction ScoreBatch request per ingress thread (concurrent); device "
-                           "micro-batches of per_gpu_batch rows", "accounts_per_gpu": n_acc,
+        "config": {"model": c["desc"], "global_batch": B * per_step * world, "seq_len": 1, "parallelism": f"dp{world}",
+                   "per_gpu_batch": B, "transactions_per_request": B, "requests_per_step_per_rank": per_step,
+                   "step": f"{max(1, a.rounds)} rounds of one 8192-transaction ScoreBatch request per ingress thread "
+                           "(concurrent); device micro-batches of per_gpu_batch rows",
+                   "synthetic_clock": "request i of a run is scored at NOW0 + i // 50 (s)",
+                   "accounts_per_gpu": n_acc,
                    "ingress_threads_per_rank": a.threads, "pipeline_depth": a.depth, "serving": mode,
                    "account_spread": {"distribution": f"zipf({a.zipf})" if a.zipf > 1 else "uniform",
                                       "population": total, "requests_in_stream_per_rank": a.payloads,

@@ -476,66 +476,6 @@ PYBIND11_MODULE(_hipk, m) {
   });
   m.def("gru_ws_clusters", [](int n_rows) { return gru_ws_clusters(n_rows); });
 
-  // layer-wise MLP (mlp_layers.hip): one 128 x 128-tile GEMM per call; "finish" = the head sum + K9
-  auto layer_args = [](const py::dict& d) {
-    MlpLayerArgs a{};
-    a.src = geti(d, "src");
-    a.epi = geti(d, "epi");
-    a.split = geti(d, "split");
-    a.A = ptr<const uint16_t*>(d, "A");
-    a.A_lo = ptr<const uint16_t*>(d, "A_lo");
-    a.lda = geti(d, "lda");
-    a.X = ptr<const float*>(d, "X");
-    a.ldx = geti(d, "ldx");
-    a.slots = ptr<const int32_t*>(d, "slots");
-    a.pf_tab = ptr<const float*>(d, "pf_tab");
-    a.ext_tab = ptr<const float*>(d, "ext_tab");
-    a.ext_w = geti(d, "ext_w");
-    a.in_live = geti(d, "in_live");
-    a.W = ptr<const uint16_t*>(d, "W");
-    a.W_lo = ptr<const uint16_t*>(d, "W_lo");
-    a.bias = ptr<const float*>(d, "bias");
-    a.M = geti(d, "M");
-    a.K = geti(d, "K");
-    a.act = geti(d, "act");
-    a.n_tiles = geti(d, "N") / 16;
-    a.col_tiles = geti(d, "N") / mlp_layer_tile_cols(a.split);
-    a.tiles = ((a.M + mlp_layer_tile_rows(a.split) - 1) / mlp_layer_tile_rows(a.split)) * a.col_tiles;
-    a.m_ptr = ptr<const int32_t*>(d, "m_ptr");
-    a.Y = ptr<uint16_t*>(d, "Y");
-    a.Y_lo = ptr<uint16_t*>(d, "Y_lo");
-    a.ldy = geti(d, "ldy");
-    a.w2 = ptr<const float*>(d, "w2");
-    a.part = ptr<float*>(d, "part");
-    a.b2 = d.contains("b2") ? d["b2"].cast<float>() : 0.f;
-    a.act2 = geti(d, "act2");
-    a.ml = ptr<float*>(d, "ml");
-    a.ltv_out = ptr<float*>(d, "ltv_out");
-    a.trace = ptr<int64_t*>(d, "trace");
-    return a;
-  };
-  m.def("mlp_layer", [layer_args](py::dict d, uintptr_t s) {
-    const MlpLayerArgs a = layer_args(d);
-    if (a.src < 0 || a.src > 2 || a.epi < 0 || a.epi > 1) throw std::runtime_error("mlp_layer: src / epi");
-    if (a.K < 64 || a.K > 512 || a.K % 64 || a.col_tiles < 1 || !a.W || (a.split && !a.W_lo))
-      throw std::runtime_error("mlp_layer: weights");
-    if (geti(d, "N") % mlp_layer_tile_cols(a.split)) throw std::runtime_error("mlp_layer: N must fill whole column tiles");
-    if (a.src == 0 && (!a.A || (a.split && !a.A_lo) || a.lda < a.K || a.lda % 8)) throw std::runtime_error("mlp_layer: A");
-    if (a.src == 1 && (!a.X || a.ldx < a.in_live)) throw std::runtime_error("mlp_layer: X");
-    if (a.src == 2 && (!a.slots || !a.pf_tab)) throw std::runtime_error("mlp_layer: gather tables");
-    if (a.src != 0 && (a.in_live < 1 || a.in_live > a.K)) throw std::runtime_error("mlp_layer: input width");
-    if (a.epi == 0 && (!a.Y || (a.split && !a.Y_lo) || a.ldy < geti(d, "N") || a.ldy % 8))
-      throw std::runtime_error("mlp_layer: Y");
-    if (a.epi == 1 && (!a.w2 || !a.part)) throw std::runtime_error("mlp_layer: head");
-    launch_or_record([a](hipStream_t st) { launch_mlp_layer(a, st); }, s, "mlp_layer");
-  });
-  m.def("mlp_layer_finish", [layer_args](py::dict d, uintptr_t s) {
-    const MlpLayerArgs a = layer_args(d);
-    if (!a.part || a.col_tiles < 1 || a.col_tiles * mlp_layer_tile_cols(a.split) != geti(d, "N") || (!a.ml && !a.ltv_out) ||
-        (a.ltv_out && (!a.slots || !a.pf_tab)))
-      throw std::runtime_error("mlp_layer_finish: args");
-    launch_or_record([a](hipStream_t st) { launch_mlp_layer_finish(a, st); }, s, "mlp_layer_finish");
-  });
   m.def("mlp_chain", [](py::dict d, uintptr_t s) {
     MlpChainArgs a{};
     a.X = ptr<const float*>(d, "X");

@@ -98,8 +98,6 @@ class PipeDriver {
     host_done_.assign(depth, 0);
     const char* xe = getenv("IGP_EXT_EVENTS");
     ext_events_ = !(xe && atoi(xe) == 0);
-    const char* qe = getenv("IGP_DEDUP_QUERY");  // 0: always queue the dedup-region wait
-    query_skip_ = !(qe && atoi(qe) == 0);
   }
   ~PipeDriver() {
     stop_worker();
@@ -374,7 +372,7 @@ class PipeDriver {
       hip_ok(hipStreamWaitEvent(cs_, pe_[slot], 0), "wait slot update");
     // the state stage of batch seq - DEDUP_AHEAD cleared this batch's dedup region: wait for it
     // unless the host already sees it complete (an event query instead of a queue wait)
-    if ((int)hist_.size() == DEDUP_AHEAD && (!query_skip_ || hipEventQuery(pe_[hist_.front()]) != hipSuccess))
+    if ((int)hist_.size() == DEDUP_AHEAD && (hipEventQuery(pe_[hist_.front()]) != hipSuccess))
       hip_ok(hipStreamWaitEvent(cs_, pe_[hist_.front()], 0), "wait state-3");
     const auto t2 = clk::now();
     const bool cb = stage_rec(g.c, g.oc, cs_, ce, "copy graph");
@@ -472,7 +470,6 @@ class PipeDriver {
   // async issue
   bool async_ = false;
   bool ext_events_ = true;
-  bool query_skip_ = true;
   bool stop_ = false;
   std::thread worker_;
   std::mutex mu_;

@@ -835,11 +835,7 @@ void launch_mlp_head(const HeadArgs& a, hipStream_t st) {
     const size_t lds = ((size_t)HD_ROWS + (w_lds ? n1p : 0)) * lds_row * 4 + 4 * HD_ROWS * sizeof(float) +
                        2 * n1p * sizeof(float);
     const dim3 grid((a.M + HD_ROWS - 1) / HD_ROWS);
-    static const bool generic = [] {  // A/B switch: IGP_HEAD_GENERIC=1 runs the generic kernel
-      const char* e = getenv("IGP_HEAD_GENERIC");
-      return e && atoi(e) != 0;
-    }();
-    if (w_lds && (a.k_pad == 32 || a.k_pad == 64) && a.act1 >= 0 && a.act1 <= 3 && !generic) {
+    if (w_lds && (a.k_pad == 32 || a.k_pad == 64) && a.act1 >= 0 && a.act1 <= 3) {
 #define HQ_CASE(KP, ACT) \
   if (a.k_pad == KP && a.act1 == ACT) { IGP_LAUNCH((mlp_head_f32_fast_kernel<KP, ACT>), grid, dim3(256), lds, st, a); return; }
       HQ_CASE(32, 0) HQ_CASE(32, 1) HQ_CASE(32, 2) HQ_CASE(32, 3)

@@ -157,7 +157,7 @@ __device__ __forceinline__ bool ws_wait(int32_t* cnt, int target) {
 }
 
 // SPLIT: the cluster's 128 sequences as two independent 64-row halves in a software pipeline
-// (IGP_GRU_SPLIT): the hand-off of one half (sc1 stores draining, counter, gather) runs beside
+// (GruArgs.ws == 2): the hand-off of one half (sc1 stores draining, counter, gather) runs beside
 // the other half's MFMAs; counters cnt[0] (half A) and cnt[8] (half B).
 template <bool SPLIT>
 __global__ void __launch_bounds__(256, 1) gru_ws_kernel(GruArgs a) {

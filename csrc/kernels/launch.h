@@ -324,42 +324,4 @@ struct MlpChainArgs {
 };
 void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st);
 
-// ---- K3 layer-wise MLP (mlp_layers.hip): one 128 x 128-tile GEMM launch per layer + a finish
-struct MlpLayerArgs {
-  int32_t src;              // A: 0 bf16 activations, 1 dense f32 X, 2 LTV gather (slots -> tables)
-  int32_t epi;              // 0 act -> bf16 Y, 1 N -> 1 head partials (part)
-  int32_t split;            // f32-faithful bf16 pairs, three MFMAs per product
-  const uint16_t* A;        // src 0: [M][lda] bf16 (hi)
-  const uint16_t* A_lo;     // src 0, split: residuals
-  int32_t lda;
-  const float* X;           // src 1: [M][ldx]
-  int32_t ldx;
-  const int32_t* slots;     // src 2 / K9: player slots [M] (-1: empty profile)
-  const float* pf_tab;      // [C][25]
-  const float* ext_tab;     // [C][ext_w] (nullable)
-  int32_t ext_w;
-  int32_t in_live;          // src 1 / 2: real input columns (the rest of K is zero)
-  const uint16_t* W;        // bf16 fragment-packed, k-step major [K/32][N/16][64][8] (pack_fragments)
-  const uint16_t* W_lo;     // split: residuals, same layout
-  const float* bias;        // [N] (nullable)
-  int32_t M, K, act;        // rows (grid coverage), K multiple of 64
-  int32_t tiles, col_tiles; // row tiles x column tiles (mlp_layer_tile_rows / _cols per mode)
-  int32_t n_tiles;          // N / 16: column tiles of the fragment-packed weights
-  const int32_t* m_ptr;     // live rows (nullable)
-  uint16_t* Y;              // epi 0: [M][ldy] bf16 (hi)
-  uint16_t* Y_lo;           // epi 0, split
-  int32_t ldy;
-  const float* w2;          // epi 1: head [N]
-  float* part;              // epi 1: [col_tiles][M]
-  float b2;                 // finish: head bias / activation
-  int32_t act2;
-  float* ml;                // finish: [M] (nullable)
-  float* ltv_out;           // finish: [M][6] K9 rows (nullable; needs slots + pf_tab)
-  int64_t* trace;           // [64 blocks][8] phase wall-clock marks (nullable)
-};
-void launch_mlp_layer(const MlpLayerArgs& a, hipStream_t st);
-int mlp_layer_tile_rows(int split);  // 128 (bf16) / 64 (split)
-int mlp_layer_tile_cols(int split);  // 128 (bf16) / 256 (split)
-void launch_mlp_layer_finish(const MlpLayerArgs& a, hipStream_t st);
-
 }  // namespace igp

@@ -143,7 +143,7 @@ void AcctCore::submit(uint8_t rpc, int32_t slot, std::string_view account, uint6
   Item it{rpc, int16_t(origin), slot, tag, now, t0_ns, mono_ns(), link_ticket, std::string(account)};
   {
     std::lock_guard<std::mutex> lk(q_mu_);
-    if (stopping_ || stopped_) throw std::runtime_error("AcctCore: stopped");
+    if (stopping_ || stopped_) throw std::runtime_error(std::string(kColdPrefix) + "AcctCore: stopped");
     queue_.push_back(std::move(it));
   }
   q_cv_.notify_all();
@@ -523,8 +523,19 @@ bool AcctMailbox::send_rep(int sender, uint64_t tag, int32_t status, std::string
   RepMsg& m = rep_msgs(rank_, sender)[head % uint64_t(rep_cap_)];
   m.tag = tag;
   m.status = status;
-  m.len = int32_t(std::min(data.size(), kRepData));
-  std::memcpy(m.data, data.data(), size_t(m.len));
+  if (data.size() > kRepData) {
+    // never a truncated answer marked OK (e.g. CheckBonusAbuse with 16 long linked ids): the
+    // ingress serves the call through its cold path instead
+    oversize_.fetch_add(1, std::memory_order_relaxed);
+    const std::string msg = std::string(kColdPrefix) + "reply of " + std::to_string(data.size()) +
+                            " bytes exceeds the mailbox record";
+    m.status = status ? status : kInternal;
+    m.len = int32_t(std::min(msg.size(), kRepData));
+    std::memcpy(m.data, msg.data(), size_t(m.len));
+  } else {
+    m.len = int32_t(data.size());
+    std::memcpy(m.data, data.data(), size_t(m.len));
+  }
   h->head.v.store(head + 1, std::memory_order_release);
   return true;
 }
@@ -679,7 +690,8 @@ void AcctRouter::local(uint8_t rpc, int32_t slot, std::string_view account, uint
                        int64_t t0, uint64_t ticket) {
   AcctCore* c = core_for(rpc);
   if (!c) {
-    answer_now(origin, tag, std::string(), "model core not attached on this rank");
+    answer_now(origin, tag, std::string(), std::string(kColdPrefix) + "no native model core for this RPC on rank " +
+                                               std::to_string(rank_));
     return;
   }
   if (rpc == RPC_ABUSE && slot < 0) {

@@ -194,6 +194,7 @@ class AcctMailbox {
   size_t poll_rep(const std::function<void(int owner, const RepMsg&)>& fn);
   void unlink_shared() { region_.unlink(); }
   int world() const { return world_; }
+  int64_t oversize() const { return oversize_.load(); }  // replies too long for a record (sent as cold)
 
  private:
   struct alignas(64) Ctr {
@@ -213,6 +214,7 @@ class AcctMailbox {
   int world_, rank_, req_cap_, rep_cap_;
   size_t req_ring_bytes_, rep_ring_bytes_, rep_off_;
   std::vector<std::unique_ptr<std::mutex>> req_mu_, rep_mu_;
+  std::atomic<int64_t> oversize_{0};
 };
 
 // This rank's entry point for the three RPCs: parse, route (local core or mailbox), deliver.
@@ -254,6 +256,7 @@ class AcctRouter {
   AcctStats stats(int kind, bool reset);
   int64_t remote_out() const { return remote_out_.load(); }
   int64_t remote_expired() const { return expired_.load(); }
+  int64_t reply_oversize() const { return mb_ ? mb_->oversize() : 0; }
 
   // used by the cores
   void deliver(int origin, std::vector<Done>&& outs);

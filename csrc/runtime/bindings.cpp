@@ -435,7 +435,9 @@ PYBIND11_MODULE(_native, m) {
       })
       .def("linked", &LinkIndex::linked, py::arg("acct"), py::arg("limit") = 16)
       .def("devices_of", &LinkIndex::devices_of)
-      .def("n_devices", &LinkIndex::n_devices);
+      .def("n_devices", &LinkIndex::n_devices)
+      .def("_debug_acquire_and_leak", &LinkIndex::debug_acquire_and_leak)
+      .def_property_readonly("takeovers", &LinkIndex::takeovers);
 
   py::class_<CpuScorer, std::shared_ptr<CpuScorer>>(m, "CpuScorer")
       .def(py::init<int64_t, int, int, int, int>(), py::arg("capacity"), py::arg("ring_size") = 256,
@@ -1010,6 +1012,7 @@ PYBIND11_MODULE(_native, m) {
            py::arg("kind"), py::arg("reset") = false)
       .def_property_readonly("remote_out", [](const PyAcct& a) { return a.router->remote_out(); })
       .def_property_readonly("remote_expired", [](const PyAcct& a) { return a.router->remote_expired(); })
+      .def_property_readonly("reply_oversize", [](const PyAcct& a) { return a.router->reply_oversize(); })
       .def_property_readonly("world", [](const PyAcct& a) { return a.router->world(); })
       .def_property_readonly("rank", [](const PyAcct& a) { return a.router->rank(); })
       .def_property("remote_timeout_us", [](const PyAcct& a) { return a.router->remote_timeout_us; },

@@ -196,6 +196,7 @@ struct GrpcServer::Worker {
     int32_t stream;
     GrpcReply reply;
     bool retry = false;  // a failed hot call: run it again through the cold handler table
+    bool cold = false;   // ... because no native core can serve it (no failover: kColdPrefix)
   };
   struct Pend {  // a hot unary call in a core: where to answer, and its request for a retry
     uint64_t conn;
@@ -580,11 +581,14 @@ struct GrpcServer::Worker {
         if (d.retry) {  // the native path failed: the cold table answers (engine fallback)
           Pend pd = std::move(p->second);
           pending.erase(p);
-          srv->note_failure(d.reply.message);
+          // a core failure fails the shard over ("#retry:"); a call no native core serves (the
+          // owner has no model core of that kind, or it is stopping) only takes the cold path
+          if (!d.cold) srv->note_failure(d.reply.message);
           {
             std::lock_guard<std::mutex> g(srv->jmu_);
             srv->cold_n_.fetch_add(1, std::memory_order_relaxed);
-            srv->cold_q_.push_back(Job{idx, cid, sid, pd.path + "#retry:" + d.reply.message, pd.body.substr(5)});
+            srv->cold_q_.push_back(
+                Job{idx, cid, sid, pd.path + (d.cold ? "#cold:" : "#retry:") + d.reply.message, pd.body.substr(5)});
           }
           srv->jcv_.notify_one();
           continue;
@@ -636,6 +640,7 @@ void GrpcServer::route_done(std::vector<ServeCore::Done>&& outs) {
         w.reply.status = 13;
         w.reply.message = d.err;
         w.retry = true;
+        w.cold = d.err.rfind(kColdPrefix, 0) == 0;
       }
     } else {
       w.reply.body = std::move(d.bytes);

@@ -13,10 +13,14 @@
 // rank of a one-process-per-GPU group records the traffic it ingests into ONE index and every
 // rank's CheckBonusAbuse sees the links of all of them (a device shared by accounts that reached
 // different ingress ranks). A spin lock in the region serialises writers and readers across the
-// processes (a batch insert holds it ~1 ms per 8192 rows; readers are single lookups).
+// processes (a batch insert holds it ~1 ms per 8192 rows; readers are single lookups). The lock
+// word holds its owner's pid: a waiter that finds the owner process gone (SIGKILL, abort while
+// inside a critical section) takes the lock over instead of spinning forever, and readers wait
+// a bounded time (kReadWaitUs) and then answer "no links".
 #pragma once
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <chrono>
 #include <cstdint>
 #include <cstring>
@@ -25,6 +29,9 @@
 #include <thread>
 #include <vector>
 
+#include <signal.h>
+#include <unistd.h>
+
 #include "shm.h"
 
 namespace igp {
@@ -32,6 +39,7 @@ namespace igp {
 class LinkIndex {
  public:
   static constexpr int kMaxPerKey = 16;
+  static constexpr int64_t kReadWaitUs = 50000;  // a reader gives up (no links) after this long
 
   explicit LinkIndex(int per_key = 8, int64_t buckets = int64_t(1) << 18) { init(per_key, buckets, "", false); }
   // node-shared index in /dev/shm/<name> (create: this process sizes it; the others map it)
@@ -41,7 +49,7 @@ class LinkIndex {
 
   void add(const uint64_t* dev, const int64_t* acct, size_t n) {
     constexpr size_t kAhead = 8;
-    Guard g(hdr_->lock);
+    Guard g(hdr_->lock, -1);
     for (size_t i = 0; i < n; ++i) {
       if (i + kAhead < n) {
         dev_.prefetch(dev[i + kAhead]);
@@ -56,8 +64,9 @@ class LinkIndex {
 
   // accounts sharing at least one device with `acct` (excluding itself), most recent first
   std::vector<int64_t> linked(int64_t acct, size_t limit) const {
-    Guard g(hdr_->lock);
+    Guard g(hdr_->lock, kReadWaitUs);
     std::vector<int64_t> out;
+    if (!g.held) return out;
     CEntry a;
     if (!acct_.find(akey(acct), a)) return out;
     for (int d = a.n - 1; d >= 0; --d) {
@@ -74,15 +83,18 @@ class LinkIndex {
   }
 
   std::vector<int64_t> devices_of(int64_t acct) const {
-    Guard g(hdr_->lock);
+    Guard g(hdr_->lock, kReadWaitUs);
     CEntry a;
-    return acct_.find(akey(acct), a) ? std::vector<int64_t>(a.v, a.v + a.n) : std::vector<int64_t>{};
+    return g.held && acct_.find(akey(acct), a) ? std::vector<int64_t>(a.v, a.v + a.n) : std::vector<int64_t>{};
   }
 
   size_t n_devices() const {
-    Guard g(hdr_->lock);
+    Guard g(hdr_->lock, kReadWaitUs);
     return size_t(hdr_->dev_used);
   }
+  // tests: take the lock and keep it (a process that dies inside a critical section)
+  void debug_acquire_and_leak() { Guard(hdr_->lock, -1).leak(); }
+  int64_t takeovers() const { return takeovers_.load(); }
   bool shared() const { return region_.shared_mapping(); }
   void unlink_shared() { region_.unlink(); }
 
@@ -116,18 +128,45 @@ class LinkIndex {
     char pad[16];
   };
   static_assert(sizeof(Hdr) == 64, "LinkIndex header must be one line");
-  // cross-process spin lock (the region's word); short critical sections
+  // cross-process spin lock (the region's word = the owner's pid, 0: free); short critical
+  // sections. timeout_us < 0: wait until acquired. A waiter checks every ~1 ms whether the owner
+  // process still exists and takes the word over (CAS owner -> self) when it does not.
+  static std::atomic<int64_t> takeovers_;
   struct Guard {
     std::atomic<uint32_t>& l;
-    explicit Guard(std::atomic<uint32_t>& x) : l(x) {
+    bool held = false;
+    Guard(std::atomic<uint32_t>& x, int64_t timeout_us) : l(x) {
+      const uint32_t me = uint32_t(::getpid());
+      const auto t0 = std::chrono::steady_clock::now();
+      auto next_check = t0 + std::chrono::milliseconds(1);
       for (int spin = 0;; ++spin) {
         uint32_t z = 0;
-        if (l.compare_exchange_weak(z, 1, std::memory_order_acquire, std::memory_order_relaxed)) return;
+        if (l.compare_exchange_weak(z, me, std::memory_order_acquire, std::memory_order_relaxed)) {
+          held = true;
+          return;
+        }
         if (spin > 256) std::this_thread::sleep_for(std::chrono::microseconds(5));
         else if (spin > 32) std::this_thread::yield();
+        if (spin > 32) {
+          const auto t = std::chrono::steady_clock::now();
+          if (t >= next_check) {
+            next_check = t + std::chrono::milliseconds(1);
+            uint32_t owner = l.load(std::memory_order_relaxed);
+            if (owner != 0 && owner != me && ::kill(pid_t(owner), 0) != 0 && errno == ESRCH &&
+                l.compare_exchange_strong(owner, me, std::memory_order_acquire, std::memory_order_relaxed)) {
+              takeovers_.fetch_add(1, std::memory_order_relaxed);
+              held = true;
+              return;
+            }
+          }
+          if (timeout_us >= 0 && t - t0 >= std::chrono::microseconds(timeout_us)) return;
+        }
       }
     }
-    ~Guard() { l.store(0, std::memory_order_release); }
+    void leak() { held = false; }
+    ~Guard() {
+      if (held) l.store(0, std::memory_order_release);
+    }
   };
 
   // table keys are never 0 (empty): device digests are non-zero, account keys are stored + 1
@@ -240,5 +279,7 @@ class LinkIndex {
   Table dev_, acct_;
   std::atomic<uint64_t> enq_{0}, done_{0};
 };
+
+inline std::atomic<int64_t> LinkIndex::takeovers_{0};
 
 }  // namespace igp

@@ -46,6 +46,8 @@
 
 namespace igp {
 
+inline constexpr const char* kColdPrefix = "cold: ";
+
 // Per-rank step counters shared by the ranks of one node (/dev/shm).
 class StepClock {
  public:
@@ -132,6 +134,9 @@ class ServeCore {
     std::string bytes;
     std::string err;
   };
+  // error texts starting with kColdPrefix: no native core can serve the call (none attached on
+  // the owner, or it is stopping): the ingress answers it through its cold (Python) path and
+  // does NOT treat it as a core failure (h2grpc.cpp route_done, api/native_grpc.py _cold)
   size_t poll(std::vector<Done>& out, size_t max, int64_t timeout_us);
   // completions whose tag has bit 63 set go to `sink` (called on a finisher thread, must not
   // block) instead of the poll() queue: the native gRPC server (h2grpc.cpp) routes them back to

@@ -91,7 +91,9 @@ class NativeRiskServer:
         return table
 
     def _cold(self, path: str, body: bytes):
-        if "#retry:" in path:  # a hot call the native path failed: fail the shard over, then serve it here
+        if "#cold:" in path:  # no native core serves this call (owner without one, or stopping): no failover
+            path = path.split("#cold:", 1)[0]
+        elif "#retry:" in path:  # a hot call the native path failed: fail the shard over, then serve it here
             path, msg = path.split("#retry:", 1)
             try:
                 self.engine.on_core_failure(msg)

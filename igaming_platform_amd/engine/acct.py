@@ -58,27 +58,17 @@ class LtvNativeDevice:
                                     0, [t.data_ptr() for t in self.slabs], [t.data_ptr() for t in self.outs], [])
         self.graphs = []
         self._dev = None
-        # big buckets layer-wise (LtvGpu.layers, mlp_layers.hip) on this device's own workspaces
-        lp = None
-        if getattr(g, "layers", None) is not None:
-            import copy
-            lp = copy.copy(g.layers)
-            lp.ws, lp.rows = None, 0
-            lp.reserve(B, self.depth)
         with torch.cuda.device(dev):
             for b in g.buckets:
                 for slot in range(self.depth):
                     if g.chain is not None:
                         # [n | slots] read from the pinned slab, 6 outputs per row stored into the
-                        # pinned rows (no H2D / D2H copy): one fused kernel, or the layer kernels
+                        # pinned rows (no H2D / D2H copy): one fused kernel
                         hs = self.slabs[slot]
                         kw = dict(slots=hs[16:16 + 4 * b].view(torch.int32), pf_tab=g.pf_tab, ext_tab=g.ext_tab,
                                   ltv_out=self.outs[slot], m_ptr=hs[:4].view(torch.int32))
                         with K.Recorder() as r:
-                            if lp is not None and b >= g.layers_min:
-                                K.mlp_layers(lp, b, ws_key=slot, **kw)
-                            else:
-                                K.mlp_chain(g.chain, b, **kw)
+                            K.mlp_chain(g.chain, b, **kw)
                         self.driver.set_ops(b, slot, r.ops)
                     else:
                         self.driver.set_graph(b, slot, self._capture(slot, b))

@@ -133,15 +133,6 @@ class LtvGpu:
         if (plan is not None and (plan.precision == "bf16" or split_ok) and os.environ.get("IGP_MLP_FUSED", "1") != "0"
                 and K.MlpChainPack.eligible(plan.steps)):
             self.chain = K.MlpChainPack(plan.steps, self.device, split=plan.precision != "bf16")
-        # big batches run the same chain layer-wise (mlp_layers.hip: one 128 x 128-tile GEMM per
-        # layer over the whole chip, the gather in the first, K9 in the finish kernel): the fused
-        # chain re-streams every weight per 64 rows. IGP_MLP_DESIGN=chain|layers|auto (auto:
-        # layer-wise from IGP_MLP_LAYERS_MIN rows)
-        self.layers = None
-        design = os.environ.get("IGP_MLP_DESIGN", "chain")
-        if self.chain is not None and design != "chain" and K.MlpLayerPack.eligible(plan.steps, self.chain.split):
-            self.layers = K.MlpLayerPack(plan.steps, self.device, split=self.chain.split)
-            self.layers_min = 1 if design == "layers" else int(os.environ.get("IGP_MLP_LAYERS_MIN", "2048"))
         dev = self.device
         self.capacity = int(capacity)
         self.pf_tab = torch.zeros((self.capacity, N_COLS), dtype=torch.float32, device=dev)
@@ -163,8 +154,6 @@ class LtvGpu:
         # the slot's pinned buffer, skipping the H2D copy (the slot lock keeps it unchanged until
         # the batch was waited for)
         self._host_in = self._host_out and os.environ.get("IGP_LTV_HOST_IN", "0") == "1"
-        if self.layers is not None:
-            self.layers.reserve(B, n_bufs)
         self._slabs = [torch.zeros(16 + 4 * B, dtype=torch.uint8, device=dev) for _ in range(n_bufs)]
         self._outs = [torch.zeros((B, 6), dtype=torch.float32, device=dev) for _ in range(n_bufs)]
         self._streams = [torch.cuda.Stream(device=dev) for _ in range(n_bufs)]
@@ -204,12 +193,8 @@ class LtvGpu:
         nout = b * self.out.shape[1] * self.out.element_size()
         if self.chain is not None:
             ws = slot % len(self._slabs)
-            if self.layers is not None and b >= self.layers_min:
-                def run(**kw):
-                    K.mlp_layers(self.layers, b, pf_tab=self.pf_tab, ext_tab=self.ext_tab, ws_key=ws, **kw)
-            else:
-                def run(**kw):
-                    K.mlp_chain(self.chain, b, pf_tab=self.pf_tab, ext_tab=self.ext_tab, ws_key=ws, **kw)
+            def run(**kw):
+                K.mlp_chain(self.chain, b, pf_tab=self.pf_tab, ext_tab=self.ext_tab, ws_key=ws, **kw)
             if self._host_out:  # the epilogue writes the slot's pinned rows: no D2H copy kernel
                 if self._host_in:  # ... and the kernel reads [n | slots] from the pinned slab: no H2D
                     hs = self.host[slot]

@@ -277,7 +277,7 @@ class RiskEngine:
                 local, owner = self.backends[0], 0
             plan = A.abuse_device_plan(self.cfg, am, local.device) if (am is not None and local.kind == "gpu") else None
             A.attach_models(acct, self.cfg, local, ltv=self.ltv, owner=owner, abuse_model=am, abuse_plan=plan,
-                            audit=self.auditlog.enabled, rank=0)
+                            audit=bool(self.cfg.server.audit_db), rank=0)  # as every worker rank
             acct.router.set_links(self.links)
             self.acct = acct
             if spmd:

@@ -136,9 +136,9 @@ class GpuScorer:
         self._cur = 0  # slot of the last submitted batch (the un-indexed buffer properties)
         self.metrics = torch.zeros(128, dtype=torch.int64, device=dev)
         self.stream = torch.cuda.Stream(device=dev)    # state stream (feature store owner)
-        # H2D + dedup insert; IGP_STREAMS=2 runs them in order on the state stream (one
-        # cross-queue wait per batch fewer, copy no longer beside K1)
-        self.cstream = self.stream if os.environ.get("IGP_STREAMS", "3") == "2" else torch.cuda.Stream(device=dev)
+        # H2D + dedup insert beside K1 (in order on the state stream instead: 78 vs 100 M
+        # scores/s, profiles/NOTES.md "Model stream")
+        self.cstream = torch.cuda.Stream(device=dev)
         self.mstream = torch.cuda.Stream(device=dev)   # model / result stream
         # state/copy streams and the model stream on disjoint CU halves (CU-masked HIP streams):
         # K1 and the tree/MLP kernels slowed each other 2-7x when sharing CUs (rocprofv3

@@ -684,125 +684,6 @@ class MlpChainPack:
         return w if all(l["N"] % (16 * w) == 0 for l in self.layers) else 4
 
 
-class MlpLayerPack:
-    """Device weights of a dense chain for the layer-wise kernels (csrc/kernels/mlp_layers.hip):
-    each layer one GEMM launch over the whole chip (bf16 128 x 128 tiles, split 64 x 256), the
-    N -> 1 head as partial dots in the last layer's epilogue plus a finish launch (head sum, K9).
-    Weights fragment-packed k-step major (:func:`pack_fragments`, + the residuals in split mode);
-    activations between layers live in per-slot workspaces sized by :meth:`reserve` (before any
-    graph capture)."""
-
-    @staticmethod
-    def tile_cols(split: bool) -> int:
-        return 256 if split else 128
-
-    @staticmethod
-    def eligible(steps, split: bool = False) -> bool:
-        if not MlpChainPack.eligible(steps):
-            return False
-        bn = MlpLayerPack.tile_cols(split)
-        return all((s.n1 if s.kind == "head" else s.n) % bn == 0 for s in steps)
-
-    def __init__(self, steps, device, split: bool = False):
-        import numpy as np
-        if not self.eligible(steps, split):
-            raise ValueError("mlp_layers: every layer width must fill whole column tiles (<= 512)")
-        dev = as_device(device)
-        self.split = bool(split)
-        self.layers = []
-        for s in steps:
-            w = np.asarray(s.w1_np if s.kind == "head" else s.w_np, np.float32)
-            b = s.b1_np if s.kind == "head" else s.b_np
-            n, k = w.shape
-            kp = -(-k // 64) * 64
-            lo = None
-            if self.split:
-                hi = torch.from_numpy(np.ascontiguousarray(w)).to(torch.bfloat16).float().numpy()
-                lo = pack_fragments(w - hi, kp, ks_major=True).to(dev)
-            self.layers.append(dict(W=pack_fragments(w, kp, ks_major=True).to(dev), Wlo=lo, N=n, K=kp,
-                                    act=ACT[s.act1 if s.kind == "head" else s.act],
-                                    b=None if b is None else torch.from_numpy(np.ascontiguousarray(b, np.float32)).to(dev)))
-        head = steps[-1]
-        self.w2 = torch.from_numpy(np.ascontiguousarray(head.w2_np, np.float32)).to(dev)
-        self.b2, self.act2 = float(head.b2), ACT[head.act2]
-        self.in_live = steps[0].k
-        self.width = max(l["N"] for l in self.layers)
-        self.device = dev
-        self.rows = 0
-        self.ws = None
-
-    def reserve(self, rows: int, n_ws: int = 1) -> None:
-        """``n_ws`` workspaces (one per pipeline slot that may run concurrently) for batches of up
-        to ``rows``: two activation buffers (+ lo planes) and the head partials each.
-        Reallocating invalidates graphs captured on the old buffers."""
-        if rows <= self.rows and n_ws <= len(self.ws or ()):
-            return
-        rows = max(int(rows), self.rows)
-        planes = 2 if self.split else 1
-        tiles = self.layers[-1]["N"] // self.tile_cols(self.split)
-        self.ws = [(torch.zeros((planes, 2, rows, self.width), dtype=torch.bfloat16, device=self.device),
-                    torch.zeros((tiles, rows), dtype=torch.float32, device=self.device))
-                   for _ in range(max(int(n_ws), len(self.ws or ())))]
-        self.rows = rows
-
-
-def mlp_layers(pk: MlpLayerPack, n_rows: int, X: Optional[torch.Tensor] = None, slots: Optional[torch.Tensor] = None,
-               pf_tab: Optional[torch.Tensor] = None, ext_tab: Optional[torch.Tensor] = None,
-               ml: Optional[torch.Tensor] = None, ltv_out: Optional[torch.Tensor] = None,
-               m_ptr: Optional[torch.Tensor] = None, ws_key: int = 0, trace: Optional[torch.Tensor] = None) -> None:
-    """The same chain as :func:`mlp_chain` (same inputs and outputs), one GEMM launch per layer +
-    a finish launch, on workspace ``ws_key``. ``n_rows`` must be within :meth:`MlpLayerPack.reserve`."""
-    dev = pk.device
-    if pk.ws is None or n_rows > pk.rows or not 0 <= ws_key < len(pk.ws):
-        raise ValueError(f"mlp_layers: no workspace {ws_key} for {n_rows} rows (reserved: {pk.rows})")
-    if ml is None and ltv_out is None:
-        raise ValueError("mlp_layers: nothing to write")
-    act, part = pk.ws[ws_key]
-    mp = _host_or_dev(m_ptr, "m_ptr", 1, dev, torch.int32)
-    src = {}
-    if slots is not None:
-        if pf_tab is None or pf_tab.dim() != 2 or pf_tab.shape[1] != 25:
-            raise ValueError("mlp_layers: LTV gather needs the [C, 25] profile table")
-        ext_w = 0 if ext_tab is None else int(ext_tab.shape[1])
-        if 25 + ext_w < pk.in_live:
-            raise ValueError("mlp_layers: tables narrower than the model input")
-        src = dict(src=2, slots=_host_or_dev(slots, "slots", n_rows, dev, torch.int32),
-                   pf_tab=_need(pf_tab, "pf_tab", torch.float32, device=dev),
-                   ext_tab=_opt(ext_tab, "ext_tab", dtype=torch.float32, device=dev), ext_w=ext_w)
-    else:
-        if X is None or X.dim() != 2 or X.shape[1] < pk.in_live or X.shape[0] < n_rows:
-            raise ValueError("mlp_layers: X must be [>= rows, >= model input]")
-        if ltv_out is not None:
-            raise ValueError("mlp_layers: the K9 epilogue needs slots")
-        src = dict(src=1, X=_need(X, "X", torch.float32, device=dev), ldx=int(X.shape[1]))
-    W = pk.width
-    base = dict(M=int(n_rows), m_ptr=mp, split=int(pk.split))
-    L = len(pk.layers)
-    for i, l in enumerate(pk.layers):
-        d = dict(base, W=_need(l["W"], "W", torch.bfloat16, l["N"] * l["K"], dev),
-                 W_lo=_opt(l["Wlo"], "Wlo", dtype=torch.bfloat16, min_numel=l["N"] * l["K"], device=dev),
-                 bias=_opt(l["b"], "b", dtype=torch.float32, min_numel=l["N"], device=dev),
-                 K=l["K"], N=l["N"], act=l["act"])
-        if i == 0:
-            d.update(src, in_live=pk.in_live)
-        else:
-            d.update(src=0, A=act[0, (i - 1) & 1].data_ptr(), lda=W,
-                     A_lo=act[1, (i - 1) & 1].data_ptr() if pk.split else None)
-        if i + 1 < L:
-            d.update(epi=0, Y=act[0, i & 1].data_ptr(), Y_lo=act[1, i & 1].data_ptr() if pk.split else None, ldy=W)
-        else:
-            d.update(epi=1, w2=_need(pk.w2, "w2", torch.float32, l["N"], dev), part=part.data_ptr())
-        if trace is not None:  # [layers][64][8] int64 phase marks (tools/mlp_layerwise_bench.py --trace)
-            d["trace"] = _need(trace, "trace", torch.int64, (i + 1) * 512, dev) + i * 512 * 8
-        _mod().mlp_layer(d, _stream())
-    f = dict(base, part=part.data_ptr(), N=pk.layers[-1]["N"], b2=pk.b2, act2=pk.act2,
-             ml=_opt(ml, "ml", dtype=torch.float32, min_numel=n_rows, device=dev),
-             ltv_out=_host_or_dev(ltv_out, "ltv_out", 6 * n_rows, dev))
-    if ltv_out is not None:
-        f.update(slots=src["slots"], pf_tab=src["pf_tab"])
-    _mod().mlp_layer_finish(f, _stream())
-
-
 def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, slots: Optional[torch.Tensor] = None,
               pf_tab: Optional[torch.Tensor] = None, ext_tab: Optional[torch.Tensor] = None,
               ml: Optional[torch.Tensor] = None, ltv_out: Optional[torch.Tensor] = None,

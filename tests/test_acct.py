@@ -281,6 +281,55 @@ def test_mailbox_routes_accounts_to_their_owner_rank():
         r1.stop()
 
 
+def test_owner_without_core_and_oversize_replies_take_the_cold_path():
+    """a call whose owner has no model core of that kind, or whose answer does not fit
+    one mailbox record (CheckBonusAbuse with 15 linked ids of 150 bytes), comes back to the
+    ingress as an error marked ``cold: `` - the native gRPC server then answers it through its
+    cold (Python) path WITHOUT failing the shard over - never as a truncated response marked OK."""
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.engine.acct import cpu_abuse_device
+    from igaming_platform_amd.engine.risk_engine import RiskEngine
+    from igaming_platform_amd.engine.serving import shm_token
+    from igaming_platform_amd.native import native
+    from igaming_platform_amd.proto import risk_v1 as P
+    from igaming_platform_amd.utils.hashing import SEED_ACCOUNT, id_hash
+    N = native()
+    eng = RiskEngine(Config(), backend="cpu", capacity=256)   # rank 1's shard: its CPU scorer + index
+    idx = [N.AccountIndex(256), eng.registry.index[0]]
+    name = shm_token() + "-mb"
+    r0 = N.AcctRouter(idx, 0, name, True)
+    r1 = N.AcctRouter(idx, 1, name, False)
+    r0.unlink_shared()
+    try:
+        r1.attach(cpu_abuse_device(eng.backends[0], None, 64))   # rank 1: abuse core only, no LTV core
+        short = next(a for a in (f"short-{i}" for i in range(100)) if id_hash(a, SEED_ACCOUNT) % 2 == 1)
+        longs = [("L%03d-" % i) + "x" * 145 for i in range(15)]
+        keys = []
+        for a in [short] + longs:
+            o = id_hash(a, SEED_ACCOUNT) % 2
+            sl, _ = idx[o].lookup([a], True)
+            keys.append((o << 32) | int(sl[0]))
+        L = N.LinkIndex(16)
+        L.add(np.full(len(keys), 777, np.uint64), np.array(keys, np.int64))   # one shared device
+        r1.set_links(L)
+        # PredictLTV for an account of rank 1 asked on rank 0: no LTV core on the owner
+        (b, e), = _ask(r0, [(N.RPC_LTV, P.PredictLTVRequest(account_id=short))])
+        assert b is None and e.startswith("cold: ") and "no native model core" in e
+        # CheckBonusAbuse: asked on the owner the answer is whole (15 linked ids, ~2.3 KB) ...
+        ask = [(N.RPC_ABUSE, P.CheckBonusAbuseRequest(account_id=short, bonus_id="b"))]
+        (b1, e1), = _ask(r1, ask)
+        assert e1 is None and len(b1) > 2032
+        assert sorted(P.CheckBonusAbuseResponse.FromString(b1).linked_accounts) == sorted(longs)
+        # ... asked on rank 0 it does not fit a reply record: marked cold, never truncated
+        (b0, e0), = _ask(r0, ask)
+        assert b0 is None and e0.startswith("cold: ") and "exceeds the mailbox record" in e0
+        assert r1.reply_oversize == 1
+    finally:
+        r0.stop()
+        r1.stop()
+        eng.close()
+
+
 # ----------------------------------------------------------------------------- multi-process
 def _free_port():
     s = socket.socket()

@@ -1,5 +1,8 @@
 """T1: the C++ host runtime — hashing, ONNX reader/writer, CPU executor (vs numpy, sklearn,
 torch), wire codec (vs the Python protobuf runtime), account/link indexes, record layouts."""
+import os
+import time
+
 import numpy as np
 import pytest
 
@@ -352,6 +355,38 @@ def test_link_index_account_zero_and_bounded_buckets():
     L.add(np.arange(100, 300, dtype=np.uint64), np.arange(1000, 1200, dtype=np.int64))
     assert L.n_devices() <= 16   # fixed memory: old keys were evicted
     assert L.linked(1199, 4) == [] and L.devices_of(1199) == [299]
+
+
+def test_link_index_lock_taken_over_from_a_dead_owner():
+    """the node-shared LinkIndex lock word holds its owner's pid. A process killed
+    while it holds the lock (SIGKILL inside a critical section) must not wedge every other rank:
+    the next writer takes the lock over, readers wait a bounded time."""
+    import signal
+    import subprocess
+    import sys
+    from igaming_platform_amd.engine.serving import shm_token
+    name = shm_token() + "-lk"
+    L = N.LinkIndex(4, 64, name, True)
+    try:
+        code = ("import sys, time; from igaming_platform_amd.native import native; "
+                f"L = native().LinkIndex(4, 64, {name!r}, False); L._debug_acquire_and_leak(); "
+                "print('held', flush=True); time.sleep(60)")
+        child = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True,
+                                 cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        try:
+            assert child.stdout.readline().strip() == "held"
+            t0 = time.monotonic()
+            assert L.linked(1, 4) == []              # live owner: the reader gives up (bounded)
+            assert time.monotonic() - t0 < 2.0
+            child.send_signal(signal.SIGKILL)
+            child.wait(10)
+        finally:
+            if child.poll() is None:
+                child.kill()
+        L.add(np.array([5, 5], np.uint64), np.array([1, 2], np.int64))   # takes the dead owner's lock
+        assert L.linked(1, 4) == [2] and L.takeovers >= 1
+    finally:
+        L.unlink_shared()
 
 
 def test_account_index_batch_lookup_with_owner_mask():
