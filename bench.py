@@ -38,6 +38,9 @@ import time
 
 import numpy as np
 
+# kernel arguments in device memory (igaming_platform_amd/__init__.py): set before any GPU call
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 DATA_PG = None  # replicas mode: the RCCL group of the results all-gather (None: the default group)
 BASELINE_P99_MS = 50.0  # README.md:58 "< 50ms latency" (the only published number)
 

@@ -17,6 +17,43 @@ __device__ __forceinline__ int as_vgpr(int x) {
   return x;
 }
 
+// A kernel's argument struct read with VECTOR loads from the kernarg segment (one dword per
+// lane, issued with the kernel's first loads) and rebuilt in SGPRs by v_readlane. The default
+// lowering reads it with scalar loads that the compiler re-issues whenever SGPR pressure evicts
+// a field (K1: 15 kernarg loads, 39 SGPR spills), each an s_waitcnt lgkmcnt(0) round trip to the
+// kernarg segment - measured at ~1,700-2,700 cycles per scalar load on MI355X (SmemLatency,
+// profiles/r5/NOTES: "K1's fixed cost"). Here the words stay in one or two VGPRs and a field the
+// compiler drops is re-read by v_readlane, not from memory. T must be <= 512 bytes.
+template <class T>
+__device__ __forceinline__ T kernarg_vgpr() {
+  static_assert(sizeof(T) % 4 == 0 && sizeof(T) <= 512, "kernarg_vgpr: 4-byte multiple, <= 512 B");
+  constexpr int NW = (int)(sizeof(T) / 4);
+  typedef const uint32_t __attribute__((address_space(4)))* kptr_t;  // the constant address space
+  const kptr_t kp = (kptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+  const int lane = (int)(threadIdx.x & 63);
+  uint32_t w[(NW + 63) / 64];
+#pragma unroll
+  for (int r = 0; r < (NW + 63) / 64; ++r) {
+    const int i = as_vgpr(64 * r + lane);
+    w[r] = kp[i < NW ? i : 0];
+  }
+  T out;
+  uint32_t* ow = reinterpret_cast<uint32_t*>(&out);
+#pragma unroll
+  for (int k = 0; k < NW; ++k) ow[k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k >> 6], k & 63);
+  return out;
+}
+
+// A generic pointer re-derived from a global (address space 1) one: pointers rebuilt from
+// integer words (kernarg_vgpr) lose the address space the compiler infers for kernel arguments,
+// and their loads / stores would be issued as flat_* instructions (out of order, counted in both
+// vmcnt and lgkmcnt); this cast lets the address-space inference see them as global again.
+template <class P>
+__device__ __forceinline__ void as_global(P*& p) {
+  typedef __attribute__((address_space(1))) P* gptr_t;
+  p = (P*)(gptr_t)(uintptr_t)(p);  // int -> global -> generic: the inference sees the global origin
+}
+
 // Mark a loaded value as used here: keeps the compiler from sinking its load below a branch
 // (the load then issues together with the other first-level loads).
 __device__ __forceinline__ void keep_issued(int x) { asm volatile("" ::"v"(x)); }

@@ -41,6 +41,7 @@
 #include "launch.h"
 #include "oplist.h"
 #include "roctx.h"
+#include "state_clock.h"
 
 namespace py = pybind11;
 
@@ -219,6 +220,8 @@ class PipeDriver {
     g.om = std::move(m);
     g.omf = std::move(mf);
   }
+  // readers of the feature store order themselves after the last published state stage
+  void set_state_clock(std::shared_ptr<StateClock> c) { clock_ = std::move(c); }
   // direct launch with a split state stage: `s` of set_ops holds K1 only, `su` the update
   void set_state_update(int bucket, int slot, std::shared_ptr<OpList> su) {
     if (slot < 0 || slot >= depth_) throw std::runtime_error("PipeDriver: bad slot");
@@ -350,6 +353,7 @@ class PipeDriver {
       if (g.osu) g.osu->run(cs_);
       (with_features ? g.omf : g.om)->run(cs_);
       hip_ok(hipEventRecord(pe_[slot], cs_), "record post");
+      if (clock_) clock_->publish(pe_[slot]);  // the batch's whole state stage (read-your-writes)
       hip_ok(hipEventRecord(me, cs_), "record model");
       st_[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
       st_[2] += std::chrono::duration<double, std::micro>(clk::now() - ts).count();
@@ -390,6 +394,7 @@ class PipeDriver {
     const bool pb = g.osu && ext_events_ && g.osu->run_recording(ss_, pe_[slot]);
     if (g.osu && !ext_events_) g.osu->run(ss_);
     if (!pb) hip_ok(hipEventRecord(pe_[slot], ss_), "record post");
+    if (clock_) clock_->publish(pe_[slot]);  // K1 + the multi-event update of this batch
     const auto t6 = clk::now();
     const bool mb = stage_rec(with_features ? g.mf : g.m, with_features ? g.omf : g.om, ms_, me, "model graph");
     const auto t7 = clk::now();
@@ -464,6 +469,7 @@ class PipeDriver {
   std::vector<bool> recorded_;
   std::vector<uint8_t> host_done_;  // wait(slot) returned since the slot's last submit (bytes: set by waiter threads)
   std::vector<int> hist_;  // slots of the last DEDUP_AHEAD submitted batches, oldest first
+  std::shared_ptr<StateClock> clock_;
   std::unordered_map<int64_t, Graphs> graphs_;
   int serial_max_ = 0;
   bool serial_hist_ = false;  // the last issued batch ran in serial mode
@@ -487,7 +493,15 @@ class PipeDriver {
 }  // namespace
 
 void register_driver(py::module_& m) {
+  py::class_<StateClock, std::shared_ptr<StateClock>>(m, "StateClock")
+      .def(py::init<>())
+      .def("wait", [](StateClock& c, uintptr_t stream) { c.wait(reinterpret_cast<hipStream_t>(stream)); },
+           py::arg("stream"))
+      .def_property_readonly("published", &StateClock::published)
+      .def_property_readonly("waits", &StateClock::waits)
+      .def_property_readonly("skips", &StateClock::skips);
   py::class_<PipeDriver>(m, "PipeDriver")
+      .def("set_state_clock", &PipeDriver::set_state_clock)
       .def(py::init<uintptr_t, uintptr_t, uintptr_t, int, py::list>())
       .def("set_graphs", &PipeDriver::set_graphs)
       .def("set_host_results", &PipeDriver::set_host_results)

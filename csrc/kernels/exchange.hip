@@ -39,6 +39,7 @@
 #include "../include/records.h"
 #include "oplist.h"
 #include "roctx.h"
+#include "state_clock.h"
 
 namespace py = pybind11;
 
@@ -489,6 +490,7 @@ class XchgDriver {
       hip_ok(hipStreamWaitEvent(ss_, e_post, 0), "wait post");
       stage(g.state, g.ostate, ss_, "state graph");  // recorded launches when set (set_state_ops)
       hip_ok(hipEventRecord(e_state, ss_), "record state");
+      if (clock_) clock_->publish(e_state);  // K1 + multi-event update: readers order after it
       hip_ok(hipStreamWaitEvent(ms_, e_state, 0), "wait state");
       hip_ok(hipGraphLaunch(with_features ? g.model_f : g.model, ms_), "model+results graph");
       hip_ok(hipEventRecord(e_done, ms_), "record done");
@@ -513,6 +515,7 @@ class XchgDriver {
     hip_ok(hipStreamWaitEvent(ss_, e_post, 0), "wait post");
     stage(g.state, g.ostate, ss_, "state graph");
     hip_ok(hipEventRecord(e_state, ss_), "record state");
+    if (clock_) clock_->publish(e_state);
     hip_ok(hipStreamWaitEvent(ms_, e_state, 0), "wait state");
     stage(with_features ? g.model_f : g.model, with_features ? g.omodel_f : g.omodel, ms_, "model graph");
     hop(ms_, ys_, e_model, "model -> y");
@@ -547,6 +550,7 @@ class XchgDriver {
   }
   // last submitted batch's state-stream event (snapshot ordering)
   uintptr_t state_event(int slot) const { return reinterpret_cast<uintptr_t>(ev_[6 * slot + 3]); }
+  void set_state_clock(std::shared_ptr<StateClock> c) { clock_ = std::move(c); }
   // the slot's completion event (the watchdog's deadline wait, watch.hip)
   uintptr_t done_event(int slot) const { return reinterpret_cast<uintptr_t>(E(slot, 5)); }
 
@@ -591,6 +595,7 @@ class XchgDriver {
     if (s < 0 || s >= depth_) throw std::runtime_error("XchgDriver: bad slot");
   }
   hipStream_t cs_, ss_, ms_, xs_, ys_;
+  std::shared_ptr<StateClock> clock_;
   int depth_, world_;
   uintptr_t cx_, cy_;
   const Rccl& r_;
@@ -652,6 +657,7 @@ void register_exchange(py::module_& m) {
       .def("wait", &XchgDriver::wait)
       .def("query", &XchgDriver::query)
       .def("state_event", &XchgDriver::state_event)
+      .def("set_state_clock", &XchgDriver::set_state_clock)
       .def("done_event", &XchgDriver::done_event)
       .def("stats", &XchgDriver::stats);
   // page-lock a host range (the node-shared result region of the D2H result path) so device

@@ -288,9 +288,13 @@ __device__ __forceinline__ void write_fenc(const AssembleArgs& a, int row, int q
 // account's events - put chains of device-scope atomics and dependent loads at the end of
 // K1: a 20 us tail behind 14 us of work at B=8192.)
 __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
-  // phase trace of 8 sample waves (wave ids 0, 293, ...): [wave][phase] wall_clock64
-  const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  int64_t* const trow = (a.trace && (threadIdx.x & 63) == 0 && gw % 293 == 0 && gw / 293 < 8) ? a.trace + (gw / 293) * 8 : nullptr;
+  // phase trace of every wave: [wave][16] = wall_clock64 marks 0..7, [8] HW_ID, [9] XCC_ID
+  const int gw = (int)((blockIdx.x * 256 + threadIdx.x) >> 6);  // launched with 256 threads
+  int64_t* const trow = (a.trace && (threadIdx.x & 63) == 0) ? a.trace + (size_t)gw * 16 : nullptr;
+  if (trow) {
+    trow[8] = (int64_t)__builtin_amdgcn_s_getreg(0xF804);  // HW_ID
+    trow[9] = (int64_t)__builtin_amdgcn_s_getreg(0xF814);  // XCC_ID
+  }
 #define K1_MARK(k) \
   if (trow) trow[k] = (int64_t)wall_clock64()
   K1_MARK(0);
@@ -344,6 +348,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     inert_row(a, xr, row, ql, ext_w, foreign ? FR_NOT_OWNED : 0);
   }
   int h = -1, s = -1, dcount = 0;
+  K1_MARK(6);
   if (live) {
     s = rq.slot;
     const int64_t amount = rq.amount;
@@ -354,25 +359,36 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     const int rs = a.ring_size;  // multiple of 64: lane ql holds entries 4 (ql + 16 i) .. +3
     const int n4 = rs / 4;
     const uint4* ts4 = reinterpret_cast<const uint4*>(a.ring_ts + (size_t)sc * rs);
-    uint4 tsv[4];
+    uint4 tsv[4] = {};
+    if (!(a.ablate & 32)) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) tsv[i] = ts4[min(ql + 16 * i, n4 - 1)];
-    const uint32_t* hreg = reinterpret_cast<const uint32_t*>(a.hll + (size_t)sc * 512);
-    uint32_t wd[4], wi[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      wd[i] = hreg[ql + 16 * i];
-      wi[i] = hreg[64 + ql + 16 * i];
+      for (int i = 0; i < 4; ++i) tsv[i] = ts4[min(ql + 16 * i, n4 - 1)];
     }
-    AcctRT rt = a.rt[sc];
-    AcctBatch bt = a.batch[sc];
-    const float* e = a.ext + (size_t)sc * ext_w;
-    float extv[7];  // ext widths up to 112 preloaded; wider rows finish in a loop at the end
+    const uint32_t* hreg = reinterpret_cast<const uint32_t*>(a.hll + (size_t)sc * 512);
+    const int abl = a.ablate;
+    uint32_t wd[4] = {0, 0, 0, 0}, wi[4] = {0, 0, 0, 0};
+    if (!(abl & 1)) {
 #pragma unroll
-    for (int u = 0; u < 7; ++u) extv[u] = e[max(0, min(ql + 16 * u, ext_w - 1))];
+      for (int i = 0; i < 4; ++i) {
+        wd[i] = hreg[ql + 16 * i];
+        wi[i] = hreg[64 + ql + 16 * i];
+      }
+    }
+    AcctRT rt{};
+    AcctBatch bt{};
+    if (!(abl & 64)) {
+      rt = a.rt[sc];
+      bt = a.batch[sc];
+    }
+    const float* e = a.ext + (size_t)sc * ext_w;
+    float extv[7] = {0, 0, 0, 0, 0, 0, 0};  // ext widths up to 112 preloaded; wider rows finish in a loop at the end
+    if (!(abl & 16)) {
+#pragma unroll
+      for (int u = 0; u < 7; ++u) extv[u] = e[max(0, min(ql + 16 * u, ext_w - 1))];
+    }
     uint32_t dh = 0, hour_word = 0;
     int dkey = -1, dfirst = -1;
-    if (a.dbuf) {  // kernel-uniform
+    if (a.dbuf && !(abl & 2)) {  // kernel-uniform
       const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
       dh = mix32((uint32_t)sc) & (uint32_t)(t.cap - 1);
       dkey = t.keys[dh];
@@ -385,7 +401,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     if (ql == 0) key = rq.dev_hash;
     else if (ql == 1) key = rq.fp_hash;
     else if (ql == 2 || ql == 3) key = rq.ip_hash;
-    const bool tabs = a.bl_keys && a.ip_keys;  // kernel-uniform
+    const bool tabs = a.bl_keys && a.ip_keys && !(abl & 4);  // kernel-uniform
     const bool bl_lane = tabs && ql < 3 && key != 0;
     const bool ip_lane = tabs && ql == 3 && key != 0;
     const uint64_t* pkeys = ql < 3 ? a.bl_keys : a.ip_keys;
@@ -398,6 +414,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       pk = pkeys[pi];
       pv = pvals[pi];
     }
+    K1_MARK(7);
     // ---- mask what a missing account / short ring must not see
     if (!has) {
 #pragma unroll
@@ -440,7 +457,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       // third dependent level in exchange for ~half the HBM traffic of the gather (same-box
       // A/B, cfg3 bench: 109.6 vs 106.1 M scores/s for the full-ring load)
       const int64_t* amp = a.ring_amt + (size_t)s * rs;
-      const bool want_amt = !cfg.sum_compat;
+      const bool want_amt = !cfg.sum_compat && !(abl & 8);
       long long av[16];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -472,6 +489,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       c60 = qsum(c60);
       s60 = qsum(s60);
       // ---- K8: HyperLogLog counts (p = 8; 16 registers per lane)
+      if (!(abl & 1)) {
       double zd = 0, zi = 0;
       int vd = 0, vi = 0;
 #pragma unroll
@@ -493,6 +511,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       const int ci = (ei <= 2.5 * m && vi > 0) ? li : (int)floor(ei + 0.5);
       hll_dev = now < (int64_t)rt.hll_dev_exp ? cd : 0;
       hll_ip = now < (int64_t)rt.hll_ip_exp ? ci : 0;
+      }
     }
 
     // ---- assemble raw features (quarter-uniform values)
@@ -603,7 +622,8 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int wst = 30 + min(ext_w, 112);
-    if (((wst | (int)a.x_stride) & 3) == 0) {
+    if (abl & 128) {
+    } else if (((wst | (int)a.x_stride) & 3) == 0) {
       for (int c = ql; c < (wst >> 2); c += K1_QL)
         reinterpret_cast<float4*>(xr)[c] = reinterpret_cast<const float4*>(sx)[c];
     } else {
@@ -611,13 +631,13 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     }
     for (int j = ql + 112; j < ext_w; j += K1_QL) xr[30 + j] = has ? a.ext[(size_t)s * ext_w + j] : 0.f;
     K1_MARK(3);
-    reinterpret_cast<uint2*>(a.feat + row)[ql] = s_fst[threadIdx.x >> 4][ql];
-    if (a.fenc)
+    if (!(abl & 128)) reinterpret_cast<uint2*>(a.feat + row)[ql] = s_fst[threadIdx.x >> 4][ql];
+    if (a.fenc && !(abl & 128))
       write_fenc(a, row, ql, (rq.tx_type & FV_ENC_BIT) != 0, reinterpret_cast<const uint32_t*>(s_fst[threadIdx.x >> 4]),
                  s_enc[threadIdx.x >> 4]);
 
     // ---- score-then-update (engine.go:486-488)
-    if (a.dbuf && has) {
+    if (a.dbuf && has && !(abl & 2)) {
       const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
       h = (int)dh;
       if (dkey != s) {  // probe collision: walk the chain
@@ -639,7 +659,23 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
 #undef K1_MARK
 }
 
-__global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs a) { feature_assemble_body(a); }
+__device__ __forceinline__ void globalize(UpdateArgs& u) {
+  as_global(u.cfg); as_global(u.hdr); as_global(u.req); as_global(u.ring_ts); as_global(u.ring_amt);
+  as_global(u.hll); as_global(u.rt); as_global(u.ev); as_global(u.dbuf);
+}
+__device__ __forceinline__ void globalize(AssembleArgs& a) {
+  as_global(a.hdr); as_global(a.cfg); as_global(a.req); as_global(a.ring_ts); as_global(a.ring_amt);
+  as_global(a.hll); as_global(a.rt); as_global(a.batch); as_global(a.ext); as_global(a.bl_keys);
+  as_global(a.bl_exp); as_global(a.ip_keys); as_global(a.ip_flags); as_global(a.hll_lc); as_global(a.X);
+  as_global(a.feat); as_global(a.fenc); as_global(a.dbuf); as_global(a.trace);
+  globalize(a.upd);
+}
+
+__global__ void __launch_bounds__(256) feature_assemble_kernel(AssembleArgs) {
+  AssembleArgs a = kernarg_vgpr<AssembleArgs>();
+  globalize(a);
+  feature_assemble_body(a);
+}
 
 // ---------------------------------------------------------------------------------- K6
 __device__ __forceinline__ int upd_n(const UpdateArgs& a) {

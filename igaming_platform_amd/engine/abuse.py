@@ -94,6 +94,9 @@ class AbuseGpu:
         self.torch, self.K = torch, K
         self.store = store
         self.device = store.device
+        # the shard's _native.StateClock when it also scores (engine/backends.py wait_state): each
+        # batch then reads the store after every scoring batch issued before it
+        self.state_clock = None
         steps = plan.steps
         from .runner import GruModel
         # fp32 plans (the ONNX f32 contract, default): the f32-faithful split GRU; bf16 plans: bf16 MFMA
@@ -191,6 +194,8 @@ class AbuseGpu:
         b = self.bucket_for(max(n, 1))
         st = self.slot_stream(slot)
         with torch.cuda.stream(st):
+            if self.state_clock is not None:
+                self.state_clock.wait(st.cuda_stream)
             g = self.graphs.get((b, slot))
             if g is not None:
                 g.replay()

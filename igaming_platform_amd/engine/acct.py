@@ -164,6 +164,9 @@ class AbuseNativeDevice:
                                     1 if self.gm else 0,
                                     int(rank), [t.data_ptr() for t in self.slabs], [t.data_ptr() for t in self.out0],
                                     [t.data_ptr() for t in self.out1])
+        # every step reads the store after the scoring batches issued before it (state_clock.h)
+        if getattr(backend, "state_clock", None) is not None:
+            self.driver.set_state_clock(backend.state_clock)
         self.graphs = []
         with torch.cuda.device(dev):
             for b in self.buckets:

@@ -288,6 +288,12 @@ class GpuBackend:
         self.store = DeviceFeatureStore(capacity, cfg.features, self.device, events=True,
                                         blacklist=blacklist, ipintel=ipintel, max_events=dmax)
         self.blacklist, self.ipintel = self.store.blacklist, self.store.ipintel
+        # read-your-writes for every reader of this shard's store (GetFeatures, event history,
+        # CheckBonusAbuse steps): each scoring driver publishes its batches' state-stage events
+        # here, a reader's stream waits for the latest one (csrc/kernels/state_clock.h). One clock
+        # per shard, kept across scorer rebuilds (failover, hot reload)
+        from ..ops import kernels as _K
+        self.state_clock = _K._mod().StateClock()
         self.scorer = self._make_scorer(plan, model, (cfg.gpu.serve_depth if cfg.gpu.native_serving else 2)
                                          if exchange is None else 3)
         if capture and self.scorer.use_graphs:
@@ -357,12 +363,20 @@ class GpuBackend:
             x = self.exchange
             if isinstance(x.get("results_shm"), str):  # mapped once; a hot reload's scorer reuses it
                 x["results_shm"] = map_results_region(x["results_shm"], depth, x["world"], max(x["cbuckets"]))
-            return DpGpuScorer(self.cfg, self.store, x["comms"], x["world"], self.rank, x["senders"], x["cbuckets"],
-                               plan=plan, model=model, device=self.device, pipeline_depth=depth,
-                               results_shm=x.get("results_shm"))
-        from .scorer import GpuScorer
-        return GpuScorer(self.cfg, self.store, plan=plan, model=model, device=self.device, pipeline_depth=depth,
-                         owner_filter=self.owner_filter, rank=self.rank, use_graphs=use_graphs)
+            sc = DpGpuScorer(self.cfg, self.store, x["comms"], x["world"], self.rank, x["senders"], x["cbuckets"],
+                             plan=plan, model=model, device=self.device, pipeline_depth=depth,
+                             results_shm=x.get("results_shm"))
+        else:
+            from .scorer import GpuScorer
+            sc = GpuScorer(self.cfg, self.store, plan=plan, model=model, device=self.device, pipeline_depth=depth,
+                           owner_filter=self.owner_filter, rank=self.rank, use_graphs=use_graphs)
+        sc.state_clock = self.state_clock  # before capture(), which makes the native driver
+        return sc
+
+    def wait_state(self, stream) -> None:
+        """Order ``stream`` (a torch stream) after the last scoring batch's state stage issued so
+        far on this shard (read-your-writes, csrc/kernels/state_clock.h)."""
+        self.state_clock.wait(stream.cuda_stream)
 
     def exchange_score(self, req: Optional[np.ndarray], owners: Optional[np.ndarray], C: int, now: int,
                        want_features: bool, timeout_s: Optional[float] = None) -> Result:
@@ -575,11 +589,18 @@ class GpuBackend:
         slots = np.asarray(slots, np.int32)
         out = np.zeros(len(slots), FEATREC)
         R = self.FX_ROWS
+        st = self.scorer.stream
         with self._lock:
             if self._fx is None:
-                self._fx = dict(slab=torch.zeros(16 + 48 * R, dtype=torch.uint8, device=self.device),
-                                X=torch.zeros((R, self.cfg.features.width), dtype=torch.float32, device=self.device),
-                                feat=torch.zeros((R, 32), dtype=torch.int32, device=self.device))
+                # zero-filled ON the stream that uses them: torch.zeros on the default stream
+                # raced the first read's slab copy on the state stream (the fill landed after the
+                # copy: n = 0, every row inert -> the one-off all-zero GetFeatures of round 4,
+                # profiles/NOTES.md "read consistency")
+                with torch.cuda.stream(st):
+                    self._fx = dict(slab=torch.zeros(16 + 48 * R, dtype=torch.uint8, device=self.device),
+                                    X=torch.zeros((R, self.cfg.features.width), dtype=torch.float32,
+                                                  device=self.device),
+                                    feat=torch.zeros((R, 32), dtype=torch.int32, device=self.device))
             fx = self._fx
             for i in range(0, len(slots), R):
                 sl = slots[i:i + R]
@@ -590,7 +611,8 @@ class GpuBackend:
                 r["slot"], r["tx_type"], r["ts"] = sl, 255 | (self.scorer.rank << 8), now
                 buf = np.concatenate([h.view(np.uint8), r.view(np.uint8)])
                 bucket = 64 if n <= 64 else R
-                with torch.cuda.stream(self.scorer.stream):
+                with torch.cuda.stream(st):
+                    self.wait_state(st)  # every scoring batch issued before this read (read-your-writes)
                     fx["slab"][:len(buf)].copy_(torch.from_numpy(buf))
                     K.feature_assemble(self.store, fx["slab"][:16].view(torch.int64), self.scorer.cfg_dev,
                                        fx["slab"][16:16 + 48 * bucket], fx["X"], fx["feat"], bucket)
@@ -600,7 +622,10 @@ class GpuBackend:
 
     def event_history(self, slot: int) -> np.ndarray:
         """[event_ring, event_dim] f32, oldest first, right-aligned (GRU input)."""
-        with self._lock:
+        torch = self.torch
+        st = self.scorer.stream
+        with self._lock, torch.cuda.stream(st):
+            self.wait_state(st)  # after the state stage of every batch issued so far
             raw = self.store.ev[slot].cpu().numpy()
             rt = self.store.read_rt(slot)
         ev = (raw.view(np.uint16).astype(np.uint32) << 16).view(np.float32)

@@ -324,6 +324,8 @@ class DpGpuScorer(GpuScorer):
                 raise RuntimeError("the D2H result path needs the captured exchange graphs")
             r = self.rshm
             d.set_results_shm(r["base"], r["slot_stride"], r["owner_stride"], r["flags"], self.rank)
+        if getattr(self, "state_clock", None) is not None:
+            d.set_state_clock(self.state_clock)
         self.xdriver = d
         self.driver = None  # the three-graph driver of the single-GPU path is not used here
 

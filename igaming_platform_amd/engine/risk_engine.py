@@ -220,6 +220,7 @@ class RiskEngine:
                 for r, d in enumerate(self.devices):
                     ap = to_device(compile_onnx(am), f"cuda:{d}", cfg.abuse_model.precision)
                     g = AbuseGpu(self.backends[r].store, ap, buckets=cfg.gpu.buckets, use_graphs=capture)
+                    g.state_clock = getattr(self.backends[r], "state_clock", None)
                     g.capture()
                     ag.append(g)
             self.abuse = AbuseService(self, threshold=cfg.abuse.threshold, gpu=ag)
@@ -1063,6 +1064,7 @@ def make_abuse_gpu(cfg: Config, local, abuse_model):
     from .abuse import AbuseGpu
     g = AbuseGpu(local.store, to_device(compile_onnx(am), str(local.device), cfg.abuse_model.precision),
                  buckets=cfg.gpu.buckets)
+    g.state_clock = getattr(local, "state_clock", None)
     g.capture()
     return g
 

@@ -99,6 +99,9 @@ class GpuScorer:
                  device=None, pipeline_depth: int = 2, update_features: bool = True,
                  use_graphs: Optional[bool] = None, owner_filter: bool = False, rank: int = 0):
         self.cfg = cfg
+        # _native.StateClock of the shard (engine/backends.py): the driver publishes each batch's
+        # state-stage event into it, feature-store readers wait on it (csrc/kernels/state_clock.h)
+        self.state_clock = None
         # broadcast serving (multi-GPU): every rank sees the whole batch, scores only the rows
         # whose owner byte (ReqRec.tx_type bits 8-15) is its rank, zeroes the rest
         self.owner_filter = bool(owner_filter)
@@ -347,6 +350,8 @@ class GpuScorer:
                                     self.depth, [t.data_ptr() for t in self.host_slab])
             for slot in range(self.depth):  # what the native serving core reads after a wait
                 d.set_host_results(slot, self.host_res[slot].data_ptr(), self.host_feat[slot].data_ptr())
+            if self.state_clock is not None:
+                d.set_state_clock(self.state_clock)
             for (b, slot), g in self.graphs.items():
                 d.set_graphs(b, slot, g[0].raw_cuda_graph_exec(), g[1].raw_cuda_graph_exec(),
                              g[2].raw_cuda_graph_exec(), g[3].raw_cuda_graph_exec())

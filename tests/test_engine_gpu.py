@@ -110,9 +110,8 @@ def test_gpu_hot_accounts_with_many_devices_match_cpu():
         b = c.score(txs, now=NOW + step * 20)
         assert [(x["score"], x["action"], x["reason_codes"]) for x in a] == \
                [(y["score"], y["action"], y["reason_codes"]) for y in b]
-    # the final store, after the last batch's state stage (it may still run when score() returns)
-    import torch
-    torch.cuda.synchronize()
+    # no device sync: GetFeatures / the event history wait on the shard's state clock for the last
+    # batch's state stage (csrc/kernels/state_clock.h), which may still run when score() returns
     for i in range(30):
         fg, fc = g.get_features(f"acc-{i}", now=NOW + 100), c.get_features(f"acc-{i}", now=NOW + 100)
         for k in ("tx_count_1h", "tx_sum_1h", "unique_devices_24h", "unique_ips_24h", "session_duration_sec"):
@@ -121,6 +120,58 @@ def test_gpu_hot_accounts_with_many_devices_match_cpu():
         hg = g.backends[0].event_history(g.registry.resolve_ids([f"acc-{i}"], insert=False)[0][0])
         hc = c.backends[0].event_history(c.registry.resolve_ids([f"acc-{i}"], insert=False)[0][0])
         np.testing.assert_array_equal(hg, hc)
+
+
+def test_gpu_reads_see_every_batch_delivered_before_them():
+    """Read-your-writes: ScoreBatch on hot accounts (most rows of each batch,
+    so their events are applied by the multi-event update that runs AFTER the model stage has
+    delivered the response), then at once - no device sync - GetFeatures, the GRU event history
+    and the native CheckBonusAbuse of those accounts. Every read must see the batch it follows:
+    equal to the CPU engine's sequential state after the same batch, batch after batch."""
+    from igaming_platform_amd.onnx import builders
+    from igaming_platform_amd.proto import risk_v1 as P
+    am = builders.build("gru", seq=100, hidden=64, layers=2).SerializeToString()
+    g, c = _engines(abuse_model=am)
+    rng = np.random.default_rng(23)
+    types = ["deposit", "withdraw", "bet", "win"]
+    keys = ("tx_count_1m", "tx_count_5m", "tx_count_1h", "tx_sum_1h", "unique_devices_24h", "unique_ips_24h",
+            "time_since_last_tx_sec", "session_duration_sec")
+    for step in range(6):
+        acc = np.where(rng.random(1024) < 0.8, rng.integers(0, 4, 1024), rng.integers(4, 40, 1024))
+        txs = [dict(account_id=f"acc-{int(a)}", amount=int(rng.integers(1, 300000)),
+                    transaction_type=types[int(rng.integers(0, 4))], device_id=f"dev-{int(rng.integers(0, 60))}",
+                    ip_address=f"10.4.{int(a)}.{int(rng.integers(0, 9))}") for a in acc]
+        now = NOW + step * 7
+        a = g.score(txs, now=now)
+        b = c.score(txs, now=now)
+        assert [(x["score"], x["action"]) for x in a] == [(y["score"], y["action"]) for y in b]
+        for i in (0, 1, 2, 3, 17):
+            fg, fc = g.get_features(f"acc-{i}", now=now), c.get_features(f"acc-{i}", now=now)
+            for k in keys:
+                assert fg[k] == fc[k], (step, i, k, fg[k], fc[k])
+        sg = g.registry.resolve_ids(["acc-0"], insert=False)[0][0]
+        sc_ = c.registry.resolve_ids(["acc-0"], insert=False)[0][0]
+        np.testing.assert_array_equal(g.backends[0].event_history(sg), c.backends[0].event_history(sc_))
+        if g.acct is not None:  # the native CheckBonusAbuse step (its own streams) right behind the batch
+            ids = [f"acc-{i}" for i in range(4)]
+            for i, a_id in enumerate(ids):
+                g.acct.router.submit(3, P.CheckBonusAbuseRequest(account_id=a_id, bonus_id="b").SerializeToString(),
+                                     i, 0, now)
+                c.acct.router.submit(3, P.CheckBonusAbuseRequest(account_id=a_id, bonus_id="b").SerializeToString(),
+                                     i, 0, now)
+            got = {}
+            for e, key in ((g, "g"), (c, "c")):
+                while sum(1 for k in got if k[0] == key) < len(ids):
+                    for tag, body, err in e.acct.router.poll(64, 200000):
+                        assert err is None, err
+                        got[(key, int(tag))] = P.CheckBonusAbuseResponse.FromString(body)
+            for i in range(len(ids)):
+                x, y = got[("g", i)], got[("c", i)]
+                assert list(x.signals) == list(y.signals), (step, i)
+                assert x.abuse_score == pytest.approx(y.abuse_score, abs=1e-4)
+    assert g.backends[0].state_clock.published > 0
+    g.close()
+    c.close()
 
 
 def test_gpu_engine_with_stacked_model_close_to_cpu():

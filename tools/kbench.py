@@ -70,6 +70,10 @@ def main():
     if a.only:
         keep = set(a.only.split(","))
         ops = {k: v for k, v in ops.items() if k in keep}
+    from igaming_platform_amd.native import hipk
+
+    def stall():  # a 300-us device spin ahead of the timed region (the Python launch path takes ~50 us)
+        hipk().stall(torch.cuda.current_stream().cuda_stream, 300.0)
     times = {k: [] for k in ops}
     for r in range(a.rounds):
         # a fresh batch sequence number per round, as the scorer does per micro-batch
@@ -80,13 +84,14 @@ def main():
                 sc._seq += 1
                 sc._write_hdr(slot, B, NOW0)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            stall()  # the device reaches e0 only after the host enqueued the op: device time only
             e0.record()
             f()
             e1.record()
             e1.synchronize()
             times[k].append(e0.elapsed_time(e1) * 1e3)
     # K1 phase trace of 8 sample waves (wall_clock64, 100 MHz -> us from the earliest start)
-    tr = torch.zeros(64, dtype=torch.int64, device=dev)
+    trw = torch.zeros(((B + 15) // 16) * 4 * 16, dtype=torch.int64, device=dev)  # every wave: 16 int64
     for dd in (True, False):
         for _ in range(3):
             sc._seq += 1
@@ -94,17 +99,22 @@ def main():
             sc.dev_slab[:nb].copy_(sc.host_slab[slot][:nb])
             if dd:
                 K.dedup_insert(sc.store, sc.cfg_dev, sc.req, B, sc.hdr)
-            tr.zero_()
-            K.feature_assemble(sc.store, sc.hdr, sc.cfg_dev, sc.req, sc.X, sc.feat, B, dedup=dd, trace=tr)
+            trw.zero_()
+            K.feature_assemble(sc.store, sc.hdr, sc.cfg_dev, sc.req, sc.X, sc.feat, B, dedup=dd, trace=trw)
             torch.cuda.synchronize()
-        t = tr.cpu().numpy().reshape(8, 8)[:, :6].astype(np.float64)
+        t = trw.cpu().numpy().reshape(-1, 16)[[w * 293 for w in range(7)]][:, [0, 1, 6, 7, 2, 3, 4, 5]].astype(np.float64)
         t0 = t[t > 0].min()
-        print(f"K1 trace (update={dd}) us: start / level1 / level2 / compute / stores / end")
-        for w in range(8):
+        print(f"K1 trace (update={dd}) us: start / level1 / live / l2-issued / level2 / compute / stores / end")
+        for w in range(7):
             print("   wave", w * 293, [round((x - t0) / 100.0, 2) if x > 0 else None for x in t[w]])
     # K1 with the update on rotating pool batches (the bench's access pattern): event timing
     # of the kernel alone + phase trace of the last one
-    for var in os.environ.get("KB_K1_MODES", "full").split(","):  # full | nodedup | noseg
+    # KB_ABLATE: comma-separated K1 skip masks (features.hip AssembleArgs.ablate; 512 = also store
+    # the D2H feature images into pinned host memory, as the serving path does)
+    fenc_host = torch.zeros((B, 32), dtype=torch.int32).pin_memory()
+    modes = [(v, 0) for v in os.environ.get("KB_K1_MODES", "full").split(",") if v not in ("", "-")]
+    modes += [("full", int(m)) for m in os.environ.get("KB_ABLATE", "").split(",") if m]
+    for var, abl in modes:  # full | nodedup | noseg
       ts_k1 = []
       for i in range(24):
           vv = sc.slab_view(slot, B)
@@ -117,21 +127,29 @@ def main():
           sc.dev_slab[:nb].copy_(sc.host_slab[slot][:nb])
           if var != "nodedup":
               K.dedup_insert(sc.store, sc.cfg_dev, sc.req, B, sc.hdr)
-          tr.zero_()
+          trw.zero_()
           e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+          stall()
           e0.record()
-          K.feature_assemble(sc.store, sc.hdr, sc.cfg_dev, sc.req, sc.X, sc.feat, B, dedup=var != "nodedup", trace=tr)
+          K.feature_assemble(sc.store, sc.hdr, sc.cfg_dev, sc.req, sc.X, sc.feat, B, dedup=var != "nodedup", trace=trw,
+                             fenc=fenc_host if abl & 512 else None, ablate=abl & 511)
+          if abl & 1024:  # the same launch again right behind it (instruction caches warm): 2 launches timed
+              K.feature_assemble(sc.store, sc.hdr, sc.cfg_dev, sc.req, sc.X, sc.feat, B, dedup=False,
+                                 fenc=fenc_host if abl & 512 else None, ablate=(abl & 511) | 2)
           e1.record()
           e1.synchronize()
           ts_k1.append(e0.elapsed_time(e1) * 1e3)
           if var not in ("nodedup", "noseg"):
               K.update_segments(sc.store, sc.cfg_dev, sc.req, B, sc.hdr)
-      print(f"[{var}] K1+update on rotating pool batches: median {np.median(ts_k1[8:]):.1f} us "
+      full = trw.cpu().numpy().reshape(-1, 16)
+      if os.environ.get("KB_TRACE_OUT"):
+          np.save(os.environ["KB_TRACE_OUT"] + f"_a{abl}.npy", full)
+      print(f"[{var} ablate={abl}] K1+update on rotating pool batches: median {np.median(ts_k1[8:]):.1f} us "
             f"(first pass {np.median(ts_k1[:8]):.1f})")
-      t = tr.cpu().numpy().reshape(8, 8)[:, :6].astype(np.float64)
+      t = full[[w * 293 for w in range(7)]][:, [0, 1, 6, 7, 2, 3, 4, 5]].astype(np.float64)
       t0 = t[t > 0].min()
-      print("K1 trace (update, rotating batches) us: start / level1 / level2 / compute / stores / end")
-      for w in range(8):
+      print("K1 trace (update, rotating batches) us: start / level1 / live / l2-issued / level2 / compute / stores / end")
+      for w in range(7):
           print("   wave", w * 293, [round((x - t0) / 100.0, 2) if x > 0 else None for x in t[w]])
     # mlp_head (8 sample blocks) phase trace
     tr = torch.zeros(64, dtype=torch.int64, device=dev)
