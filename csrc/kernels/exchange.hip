@@ -211,10 +211,16 @@ class RcclComm {
   // communicators live until destroy() or process exit: destroying one from a static
   // destructor after the HIP runtime began tearing down faults (seen under rocprofv3)
   ~RcclComm() = default;
+  // the owner drained the streams and destroyed every graph that captured this communicator's
+  // collectives first (engine/dp.py DpGpuScorer.close): RCCL waits for those graph references
   void destroy() {
-    if (comm_) (void)r_.comm_destroy(comm_);
+    if (!comm_) return;
+    void* c = comm_;
     comm_ = nullptr;
+    py::gil_scoped_release nogil;
+    (void)r_.comm_destroy(c);
   }
+  bool alive() const { return comm_ != nullptr; }
   uintptr_t ptr() const { return reinterpret_cast<uintptr_t>(comm_); }
   int rank() const { return rank_; }
   int world() const { return world_; }
@@ -642,6 +648,7 @@ void register_exchange(py::module_& m) {
       .def("all_to_all", &RcclComm::all_to_all)
       .def("async_error", &RcclComm::async_error)
       .def("destroy", &RcclComm::destroy)
+      .def_property_readonly("alive", &RcclComm::alive)
       .def("abort", &RcclComm::abort);
   py::class_<XchgDriver>(m, "XchgDriver")
       .def(py::init<uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int, const RcclComm&, const RcclComm&>(),

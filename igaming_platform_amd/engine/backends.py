@@ -542,6 +542,13 @@ class GpuBackend:
                 cb(self)
         threading.Thread(target=drain, daemon=True, name=f"gpu-drain-{self.device}").start()
 
+    def close(self) -> None:
+        """Release the exchange (graphs, then the RCCL communicators) once the serving core that
+        issues its steps has stopped; a plain single-GPU shard holds nothing to release."""
+        sc = self.scorer
+        if self.exchange is not None and hasattr(sc, "close"):
+            sc.close()
+
     def leave_exchange(self, timeout_s: float = 5.0) -> None:
         """Failover (rank 0 of a failed SPMD group): abort the RCCL exchange and serve this
         shard through the plain single-GPU pipeline on the same HBM store (new scorer and
@@ -558,6 +565,7 @@ class GpuBackend:
             if not hipk().EventWatch().wait_for(int(ev.cuda_event), timeout_s * 1e3):
                 raise TimeoutError("the exchange streams did not drain after the abort")
             torch.cuda.synchronize(self.device)
+            old.release_graphs()  # their references to the aborted communicators go now, not at GC
             self.exchange = None
             sc = self._make_scorer(old.plan, old.model, 2, use_graphs=old.use_graphs)
             sc._seq = old._seq

@@ -400,6 +400,33 @@ class DpGpuScorer(GpuScorer):
     def done(self, p) -> bool:
         return self.xdriver.query(p.slot)
 
+    def release_graphs(self) -> None:
+        """Destroy the exchange graphs / op lists and the driver that replays them. RCCL keeps a
+        reference on a communicator for every graph that captured one of its collectives, and
+        ncclCommDestroy waits until those graphs are gone: destroying the communicators while the
+        scorer still held its graphs is the hang of round 4 (reverted e878694)."""
+        self.xdriver = None
+        for gs in self.xgraphs.values():
+            for g in gs:
+                if hasattr(g, "reset"):  # torch.cuda.CUDAGraph: hipGraphExecDestroy + hipGraphDestroy
+                    g.reset()
+        self.xgraphs.clear()
+
+    def close(self) -> None:
+        """Ordered teardown (the reference drains and stops,
+        services/risk/cmd/main.go:239-257): the serving core that issues steps must be stopped by
+        the caller first; then the device drains, the graphs holding communicator references are
+        destroyed, and both communicators are destroyed (ncclCommDestroy). Idempotent."""
+        if getattr(self, "_closed", False):
+            return
+        self._closed = True
+        import torch
+        torch.cuda.synchronize(self.device)  # every issued step (collectives included) finished
+        self.release_graphs()
+        torch.cuda.synchronize(self.device)
+        for c in self.comms:
+            c.destroy()
+
     def abort_exchange(self) -> List[int]:
         """Failover: abort both communicators (cancels collectives still waiting on a dead peer
         so the streams drain). Returns their async error codes read before the abort."""

@@ -925,6 +925,8 @@ class RiskEngine:
         if self.group is not None:
             self.group.stop()  # also stops this rank's core (every rank converges)
             self.group = None
+            if getattr(self, "node", None) is not None:
+                self.node.close()  # the exchange graphs, then the RCCL communicators
         elif self.core is not None:
             self.core.stop()
         self.auditlog.close()  # the segment loader (segments left over resume on the next start)
@@ -1122,6 +1124,8 @@ def serve_shard(cfg: Config, comm, backend: str = "gpu", capacity: Optional[int]
             started.stop(1.0)
     if ingress is not None:
         th.join(60)
+    if node.local.kind == "gpu" and getattr(node.local.scorer, "comms", None):
+        node.close()  # graphs, then the communicators (no leak across the process lifetime)
     return out
 
 
@@ -1251,6 +1255,18 @@ class SpmdNode:
             flush_if_configured(self, log)
         self._audit_thread = threading.Thread(target=loop, name="audit-flush", daemon=True)
         self._audit_thread.start()
+
+    def close(self) -> None:
+        """Ordered shutdown of this rank: the account router and the serving core stop issuing
+        device steps, then the local shard releases its exchange (graphs, then the RCCL
+        communicators: engine/dp.py DpGpuScorer.close). Idempotent."""
+        acct = getattr(self, "acct", None)
+        if acct is not None:
+            acct.stop()
+        if self.core is not None:
+            self.core.stop()
+        if hasattr(self.local, "close"):
+            self.local.close()
 
     def stop_audit_flusher(self) -> None:
         if getattr(self, "_audit_stop", None) is not None:

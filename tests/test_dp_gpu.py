@@ -71,6 +71,9 @@ def test_exchange_scorer_matches_plain_pipeline():
     # device metrics count exactly the rows this GPU scored
     m_ref, m_dp = ref.read_metrics(), dp.read_metrics()
     np.testing.assert_array_equal(m_ref, m_dp)
+    # ordered teardown: graphs holding communicator references first, then ncclCommDestroy
+    dp.close()
+    assert not any(c.alive for c in dp.comms)
 
 
 def _free_port():
@@ -123,6 +126,44 @@ def test_spmd_engine_world1_matches_plain_gpu_engine(monkeypatch, results):
             if e is not None:
                 e.close()
         dist.destroy_process_group()
+
+
+def test_spmd_engines_close_and_destroy_their_communicators():
+    """two SPMD world-1 engines created and closed one after the other in one
+    process. Each close stops the serving core, destroys the exchange graphs (RCCL keeps a
+    reference on a communicator per graph that captured its collectives) and then both RCCL
+    communicators; the second engine's set-up, scoring and teardown then run in a process with
+    no communicator left over from the first."""
+    import torch
+    import torch.distributed as dist
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.engine.risk_engine import RiskEngine
+    from igaming_platform_amd.parallel.comm import TorchComm
+    for round_ in range(2):
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+        dist.init_process_group("gloo", rank=0, world_size=1)
+        eng = None
+        try:
+            cfg = Config()
+            cfg.gpu.buckets = [64, 256]
+            eng = RiskEngine(cfg, backend="gpu", capacity=1024, spmd=TorchComm("gloo"))
+            sc = eng.local.scorer
+            assert sc.__class__.__name__ == "DpGpuScorer" and all(c.alive for c in sc.comms)
+            rng = np.random.default_rng(round_)
+            txs = [dict(account_id=f"acc-{int(a)}", amount=5000, transaction_type="bet", device_id=f"d-{int(a)}",
+                        ip_address="10.0.0.1") for a in rng.integers(0, 60, 200)]
+            out = eng.score(txs, now=NOW + round_)
+            assert len(out) == 200
+            comms = list(sc.comms)
+            eng.close()
+            eng = None
+            assert not any(c.alive for c in comms), round_
+            assert not sc.xgraphs
+        finally:
+            if eng is not None:
+                eng.close()
+            dist.destroy_process_group()
+        torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("world,C", [(2, 64), (3, 40), (8, 16)])

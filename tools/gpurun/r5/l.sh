@@ -22,3 +22,5 @@ step engine 400 python bench.py --steps 300 --warmup 30 --scope engine_only --js
 echo "prof rc=$?" >> $R/$O/status.txt
 timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py tests/test_acct_gpu.py -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > $R/$O/gpu_tests.log 2>&1
 echo "gpu tests rc=$?" >> $R/$O/status.txt
+timeout -k 10 400 python -u -m pytest tests/test_dp_gpu.py -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider > $R/$O/dp_tests.log 2>&1
+echo "dp tests rc=$?" >> $R/$O/status.txt
