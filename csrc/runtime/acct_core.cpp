@@ -9,6 +9,7 @@
 
 #include "pb.h"
 #include "xxh64.h"
+#include "thread_name.h"
 
 namespace igp {
 
@@ -126,9 +127,20 @@ AcctCore::AcctCore(AcctRouter* router, const IgpModelOps* dev, Options opt) : ro
     steps_[s] = std::make_unique<Step>();
     free_slots_.push_back(depth_ - 1 - s);
   }
-  threads_.emplace_back([this] { stepper_loop(); });
-  threads_.emplace_back([this] { completion_loop(); });
-  for (int i = 0; i < std::max(1, opt_.finishers); ++i) threads_.emplace_back([this] { finisher_loop(); });
+  const std::string k = kind_ == IGP_MODEL_LTV ? "ltv" : "abuse";
+  threads_.emplace_back([this, k] {
+    name_thread("acct-" + k + "-step");
+    stepper_loop();
+  });
+  threads_.emplace_back([this, k] {
+    name_thread("acct-" + k + "-done");
+    completion_loop();
+  });
+  for (int i = 0; i < std::max(1, opt_.finishers); ++i)
+    threads_.emplace_back([this, k] {
+      name_thread("acct-" + k + "-fin");
+      finisher_loop();
+    });
 }
 
 AcctCore::~AcctCore() {
@@ -580,7 +592,10 @@ AcctRouter::AcctRouter(std::vector<std::shared_ptr<AccountIndex>> indexes, int r
   if (world_ > 1) {
     if (mailbox.empty()) throw std::runtime_error("AcctRouter: world > 1 needs a mailbox name");
     mb_ = std::make_unique<AcctMailbox>(mailbox, world_, rank_, req_cap, rep_cap, create);
-    mb_thread_ = std::thread([this] { mailbox_loop(); });
+    mb_thread_ = std::thread([this] {
+      name_thread("acct-mailbox");
+      mailbox_loop();
+    });
   }
 }
 

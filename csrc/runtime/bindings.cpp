@@ -18,6 +18,7 @@
 #include "link_index.h"
 #include "executor.h"
 #include "onnx_model.h"
+#include "sampler.h"
 #include "trees.h"
 #include "wire.h"
 #include "xxh64.h"
@@ -735,6 +736,21 @@ PYBIND11_MODULE(_native, m) {
       })
       .def("last_failure", [](PyGrpc& s) { return s.srv->last_failure(); });
 
+  // host CPU sampler (csrc/runtime/sampler.h): tools/host_profile.py --sample
+  m.def("sampler_start", [](int hz, size_t capacity) { sampler::start(hz, capacity); }, py::arg("hz") = 4000,
+        py::arg("capacity") = size_t(1) << 20);
+  m.def("sampler_stop", []() {
+    const auto v = sampler::stop();
+    py::array_t<uint64_t> pc(v.size());
+    py::array_t<int32_t> tid(v.size());
+    auto p = pc.mutable_unchecked<1>();
+    auto t = tid.mutable_unchecked<1>();
+    for (size_t i = 0; i < v.size(); ++i) {
+      p(i) = v[i].pc;
+      t(i) = v[i].tid;
+    }
+    return py::make_tuple(pc, tid);
+  });
   m.def("grpc_load", [](const std::string& host, int port, const std::string& path, std::vector<std::string> payloads,
                         double rate, double seconds, int conns, int max_inflight) {
     LoadResult r;

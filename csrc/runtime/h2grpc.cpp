@@ -1,4 +1,5 @@
 #include "h2grpc.h"
+#include "thread_name.h"
 
 #include <arpa/inet.h>
 #include <dlfcn.h>
@@ -227,11 +228,30 @@ struct GrpcServer::Worker {
     if (evfd >= 0) ::close(evfd);
   }
 
+  // completions from other threads; the eventfd is written only when the queue was empty (a
+  // non-empty queue already has a wake-up pending and drain_done takes all of it): one syscall
+  // per burst of completions instead of one per call
   void post(Done&& d) {
+    bool wake;
     {
       std::lock_guard<std::mutex> g(qmu);
+      wake = q.empty();
       q.push_back(std::move(d));
     }
+    if (wake) notify();
+  }
+  void post_many(std::vector<Done>& ds) {
+    if (ds.empty()) return;
+    bool wake;
+    {
+      std::lock_guard<std::mutex> g(qmu);
+      wake = q.empty();
+      for (auto& d : ds) q.push_back(std::move(d));
+    }
+    ds.clear();
+    if (wake) notify();
+  }
+  void notify() {
     const uint64_t one = 1;
     ssize_t r = ::write(evfd, &one, sizeof one);
     (void)r;
@@ -402,6 +422,9 @@ struct GrpcServer::Worker {
       if (r < 0) return errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR;
       const ssize_t k = ng().mem_recv(c.sess, reinterpret_cast<const uint8_t*>(buf.data()), size_t(r));
       if (k < 0) return false;
+      // a short read drained the socket: no second read() just to see EAGAIN (level-triggered
+      // epoll reports the connection again when more bytes arrive)
+      if (size_t(r) < buf.size()) return true;
     }
   }
 
@@ -429,18 +452,32 @@ struct GrpcServer::Worker {
       c.wbuf.clear();
       c.woff = 0;
     }
+    // everything nghttp2 has queued (a unary response is three frames: HEADERS, DATA, trailer
+    // HEADERS; a drain of many completions is many of them) goes out in ONE send(): one syscall
+    // per connection and flush instead of one per frame (tools/host_profile.py: send() was ~45 %
+    // of the HTTP/2 workers' CPU)
+    bool more = false;  // stopped at the size bound with frames still queued
     for (;;) {
       const uint8_t* p = nullptr;
       const ssize_t len = n.mem_send(c.sess, &p);
       if (len < 0) return false;
       if (len == 0) break;
-      const size_t w = write_some(reinterpret_cast<const char*>(p), size_t(len));
+      c.wbuf.append(reinterpret_cast<const char*>(p), size_t(len));
+      if (c.wbuf.size() >= (size_t(1) << 20)) {  // bounded; the rest goes out on EPOLLOUT
+        more = true;
+        break;
+      }
+    }
+    if (!c.wbuf.empty()) {
+      const size_t w = write_some(c.wbuf.data(), c.wbuf.size());
       if (w == size_t(-1)) return false;
-      if (w < size_t(len)) {
-        c.wbuf.assign(reinterpret_cast<const char*>(p) + w, size_t(len) - w);
-        c.woff = 0;
+      if (w < c.wbuf.size()) {
+        c.woff = w;
         return set_out(c, true);
       }
+      c.wbuf.clear();
+      c.woff = 0;
+      if (more) return set_out(c, true);
     }
     if (!n.want_read(c.sess) && !n.want_write(c.sess)) return false;
     return set_out(c, false);
@@ -628,6 +665,8 @@ std::string GrpcServer::last_failure() const {
 
 // completions of hot unary calls (a core's finisher thread): to the worker owning the connection
 void GrpcServer::route_done(std::vector<ServeCore::Done>&& outs) {
+  thread_local std::vector<std::vector<Worker::Done>> per;  // per worker, posted once per batch
+  if (per.size() < workers_.size()) per.resize(workers_.size());
   for (auto& d : outs) {
     const int wi = int((d.tag & ~ServeCore::kSinkTag) >> kWorkerShift);
     if (wi < 0 || size_t(wi) >= workers_.size()) continue;
@@ -645,8 +684,9 @@ void GrpcServer::route_done(std::vector<ServeCore::Done>&& outs) {
     } else {
       w.reply.body = std::move(d.bytes);
     }
-    workers_[size_t(wi)]->post(std::move(w));
+    per[size_t(wi)].push_back(std::move(w));
   }
+  for (size_t i = 0; i < workers_.size(); ++i) workers_[i]->post_many(per[i]);
 }
 
 GrpcServer::~GrpcServer() { stop(); }
@@ -671,9 +711,21 @@ int GrpcServer::start(const std::string& host, int port, int workers) {
   };
   if (core_) core_->set_sink(sink);
   if (router_) router_->set_sink(sink);
-  for (auto& w : workers_) threads_.emplace_back([p = w.get()] { p->run(); });
-  for (int i = 0; i < n_cold_; ++i) threads_.emplace_back([this] { cold_loop(); });
-  for (int i = 0; i < n_batch_; ++i) threads_.emplace_back([this] { batch_loop(); });
+  for (auto& w : workers_)
+    threads_.emplace_back([p = w.get()] {
+      name_thread("h2-worker");
+      p->run();
+    });
+  for (int i = 0; i < n_cold_; ++i)
+    threads_.emplace_back([this] {
+      name_thread("h2-cold");
+      cold_loop();
+    });
+  for (int i = 0; i < n_batch_; ++i)
+    threads_.emplace_back([this] {
+      name_thread("h2-batch");
+      batch_loop();
+    });
   return bound;
 }
 
@@ -845,6 +897,7 @@ LoadResult grpc_load(const std::string& host, int port, const std::string& path,
   std::atomic<int> failed{0};
   for (int ci = 0; ci < conns; ++ci) {
     th.emplace_back([&, ci] {
+      name_thread("h2-loadgen");
       const int fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
       sockaddr_in a{};
       a.sin_family = AF_INET;

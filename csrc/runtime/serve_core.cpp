@@ -1,4 +1,5 @@
 #include "serve_core.h"
+#include "thread_name.h"
 
 #include <algorithm>
 #include <chrono>
@@ -98,10 +99,23 @@ ServeCore::ServeCore(std::vector<std::shared_ptr<AccountIndex>> indexes, const I
   }
   if (clock_) issued_.store(clock_->issued(rank_));
   seq_ = opt_.seq0;
-  threads_.emplace_back([this] { stepper_loop(); });
-  threads_.emplace_back([this] { completion_loop(); });
-  for (int i = 0; i < std::max(1, opt_.finishers); ++i) threads_.emplace_back([this] { finisher_loop(); });
-  threads_.emplace_back([this] { link_loop(); });
+  threads_.emplace_back([this] {
+    name_thread("core-step");
+    stepper_loop();
+  });
+  threads_.emplace_back([this] {
+    name_thread("core-done");
+    completion_loop();
+  });
+  for (int i = 0; i < std::max(1, opt_.finishers); ++i)
+    threads_.emplace_back([this] {
+      name_thread("core-fin");
+      finisher_loop();
+    });
+  threads_.emplace_back([this] {
+    name_thread("core-link");
+    link_loop();
+  });
 }
 
 ServeCore::~ServeCore() {
