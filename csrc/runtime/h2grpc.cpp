@@ -228,6 +228,14 @@ struct GrpcServer::Worker {
     if (evfd >= 0) ::close(evfd);
   }
 
+  // unary ScoreTransaction calls completed by one read() (dispatch), handed to the core at once
+  std::vector<ServeCore::TxCall> txq;
+  void submit_txq() {
+    if (txq.empty()) return;
+    srv->core_->submit_tx_many(txq.data(), txq.size(), -1);
+    txq.clear();
+  }
+
   // completions from other threads; the eventfd is written only when the queue was empty (a
   // non-empty queue already has a wake-up pending and drain_done takes all of it): one syscall
   // per burst of completions instead of one per call
@@ -383,6 +391,7 @@ struct GrpcServer::Worker {
           if (!ok) close_conn(tag);
         }
       }
+      submit_txq();  // (calls dispatched outside a read, if any)
     }
   }
 
@@ -421,6 +430,7 @@ struct GrpcServer::Worker {
       if (r == 0) return false;
       if (r < 0) return errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR;
       const ssize_t k = ng().mem_recv(c.sess, reinterpret_cast<const uint8_t*>(buf.data()), size_t(r));
+      submit_txq();  // the unary calls this chunk completed, as one batch
       if (k < 0) return false;
       // a short read drained the socket: no second read() just to see EAGAIN (level-triggered
       // epoll reports the connection again when more bytes arrive)
@@ -550,7 +560,7 @@ struct GrpcServer::Worker {
         srv->router_->submit(arpc, body, blen, tag, mono_ns());
       } else {
         srv->hot_tx_.fetch_add(1, std::memory_order_relaxed);
-        srv->core_->submit_tx(body, blen, tag, -1, mono_ns());
+        txq.push_back(ServeCore::TxCall{body, blen, tag, mono_ns()});  // handed over after this read
       }
       return;
     }

@@ -337,6 +337,119 @@ void ServeCore::submit_tx(const char* data, size_t n, uint64_t tag, int64_t now,
   }
 }
 
+void ServeCore::submit_tx_many(const TxCall* calls, size_t n, int64_t now) {
+  if (n == 0) return;
+  thread_local std::vector<wire::TxRow> rows;
+  thread_local std::vector<Item*> items;
+  thread_local std::vector<std::string_view> ids;
+  thread_local std::vector<uint64_t> hs;
+  thread_local std::vector<int32_t> slots;
+  thread_local std::vector<uint8_t> ok;
+  rows.resize(n);
+  items.assign(n, nullptr);
+  ok.assign(n, 0);
+  std::vector<Done> bad;
+  const int64_t wnow = now >= 0 ? now : wall_s();
+  const int32_t enc = opt_.features ? FV_ENC_BIT : 0;
+  for (size_t k = 0; k < n; ++k) {
+    try {
+      wire::parse_tx_row(calls[k].data, calls[k].n, rows[k]);
+      ok[k] = 1;
+    } catch (const std::exception& e) {
+      bad.push_back(Done{calls[k].tag, std::string(), e.what()});
+    }
+  }
+  if (world_ == 1) {  // one batched lookup for the account ids of every call
+    ids.resize(n);
+    hs.resize(n);
+    slots.assign(n, -1);
+    size_t m = 0;
+    for (size_t k = 0; k < n; ++k)
+      if (ok[k]) {
+        ids[m] = rows[k].account;
+        hs[m] = rows[k].account_hash;
+        ++m;
+      }
+    idx_[0]->lookup_views(ids.data(), hs.data(), m, true, slots.data(), nullptr);
+    m = 0;
+    for (size_t k = 0; k < n; ++k) {
+      if (!ok[k]) continue;
+      auto* it = new Item();
+      it->kind = 1;
+      it->tag = calls[k].tag;
+      it->t0 = calls[k].t0_ns > 0 ? calls[k].t0_ns : now_ns();
+      it->now = wnow;
+      it->wf = opt_.features;
+      it->res = &it->res1;
+      it->feat = it->wf ? &it->feat1 : nullptr;
+      it->n = 1;
+      it->rows.resize(1);
+      it->rows[0] = rows[k].rec;
+      it->rows[0].slot = slots[m++];
+      it->rows[0].tx_type |= enc;
+      it->ocur.assign(1, 0);
+      it->ostart = {0, 1};
+      items[k] = it;
+    }
+    if (links_ && m) {  // (device, account) co-occurrences of every call: ONE link job for the batch
+      std::vector<uint64_t> d;
+      std::vector<int64_t> acc;
+      d.reserve(m);
+      acc.reserve(m);
+      for (Item* it : items)
+        if (it) {
+          d.push_back(it->rows[0].dev_hash);
+          acc.push_back(it->rows[0].slot >= 0 ? int64_t(it->rows[0].slot) : -1);
+        }
+      std::lock_guard<std::mutex> g(l_mu_);
+      if (lq_.size() < 16) {  // bounded: links are best-effort under overload (as resolve_rows)
+        links_->note_queued();
+        lq_.emplace_back(std::move(d), std::move(acc));
+        l_cv_.notify_one();
+      }
+    }
+  } else {  // owner routing per call (resolve_rows sorts one call's row by owner)
+    for (size_t k = 0; k < n; ++k) {
+      if (!ok[k]) continue;
+      auto* it = new Item();
+      it->kind = 1;
+      it->tag = calls[k].tag;
+      it->t0 = calls[k].t0_ns > 0 ? calls[k].t0_ns : now_ns();
+      it->now = wnow;
+      it->wf = opt_.features;
+      it->res = &it->res1;
+      it->feat = it->wf ? &it->feat1 : nullptr;
+      std::vector<wire::TxRow> one(1, rows[k]);
+      resolve_rows(one, it);
+      items[k] = it;
+    }
+  }
+  const int64_t t_enq = now_ns();
+  bool stopped = false;
+  {
+    std::lock_guard<std::mutex> lk(q_mu_);
+    stopped = stopping_ || stopped_;
+    if (!stopped)
+      for (Item* it : items)
+        if (it) {
+          it->remaining = int64_t(it->n);
+          it->t_enq = t_enq;
+          queue_.push_back(it);
+          queued_rows_ += int64_t(it->n);
+        }
+  }
+  if (stopped) {
+    for (size_t k = 0; k < n; ++k)
+      if (items[k]) {
+        bad.push_back(Done{items[k]->tag, std::string(), "ServeCore: stopped"});
+        delete items[k];
+      }
+  } else {
+    q_cv_.notify_all();
+  }
+  if (!bad.empty()) deliver(std::move(bad));
+}
+
 void ServeCore::deliver(std::vector<Done>&& outs) {
   Sink sink;
   {

@@ -127,6 +127,15 @@ class ServeCore {
                   ResultRec* res, FeatRec* feat);
   // unary ScoreTransaction: enqueue (non-blocking); the response comes back from poll() with `tag`
   void submit_tx(const char* data, size_t n, uint64_t tag, int64_t now, int64_t t0_ns);
+  // many unary calls at once (the HTTP/2 worker hands over every call one read() delivered): one
+  // batched account lookup, one queue lock and one stepper wake-up for all of them
+  struct TxCall {
+    const char* data;
+    size_t n;
+    uint64_t tag;
+    int64_t t0_ns;
+  };
+  void submit_tx_many(const TxCall* calls, size_t n, int64_t now);
   // completed unary responses (tag, response bytes, error text: empty on success); blocks up
   // to timeout_us for the first one
   struct Done {
