@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "launch.h"
+#include "update.h"
 #include "oplist.h"
 
 namespace py = pybind11;
@@ -119,6 +120,7 @@ PYBIND11_MODULE(_hipk, m) {
   m.attr("SIZEOF_REQREC") = (int)sizeof(ReqRec);
   m.attr("DEDUP_LIST") = DEDUP_LIST;
   m.attr("DEDUP_REGIONS") = DEDUP_RING + 1;
+  m.def("dedup_region_size", [](int cap, int n_max) { return (int64_t)dedup_region_size(cap, n_max); });
   igp::register_driver(m);
   igp::register_model_driver(m);
   igp::register_exchange(m);

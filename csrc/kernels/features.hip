@@ -692,7 +692,7 @@ __global__ void dedup_reset_kernel(UpdateArgs a) {
   const DedupTab t = upd_region(a);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < t.cap) { t.keys[i] = -1; t.first[i] = 0x7fffffff; t.count[i] = 0; t.fill[i] = 0; t.done[i] = 0; }
-  if (i < 2) t.ctr[i] = 0;
+  if (i < 4) t.ctr[i] = 0;
 }
 
 __global__ void dedup_insert_kernel(UpdateArgs a) {
@@ -768,6 +768,10 @@ __global__ void __launch_bounds__(64) dedup_insert_list_kernel(UpdateArgs a) {
   if (pos == 1) {  // the account's second row registers it as a multi-event account
     const int m = atomicAdd(&t.ctr[0], 1);
     if (2 * m + 1 < t.nmax) *reinterpret_cast<int2*>(t.mlist + 2 * m) = make_int2(h, r.x);
+  }
+  if (pos == DEDUP_LIST) {  // ... and its (DEDUP_LIST + 1)-th as a hot account (update_hot_kernel)
+    const int m = atomicAdd(&t.ctr[2], 1);
+    if (m < t.hot_cap) *reinterpret_cast<int2*>(t.hot + 2 * m) = make_int2(h, r.x);
   }
 }
 
@@ -1046,6 +1050,7 @@ __global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
     const int c = t.count[h];
     const AcctRT r = a.rt[s];
     if (c < 2) continue;
+    if (c > DEDUP_LIST && a.region < 0) continue;  // scorer path: update_hot_kernel applies it
     apply_segment_wave(a, t, h, c, s, r, lane, s_regs[threadIdx.x >> 6]);
   }
   // scorer ring: clear the region of batch seq + DEDUP_AHEAD (= seq-1's, consumed by now) for
@@ -1059,7 +1064,156 @@ __global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
       reinterpret_cast<int4*>(nt.first)[e4] = big;
       reinterpret_cast<int4*>(nt.count)[e4] = z;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) nt.ctr[0] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      nt.ctr[0] = 0;
+      nt.ctr[2] = 0;
+    }
+  }
+}
+
+// Hot accounts on the scorer path (more than DEDUP_LIST events in one batch: Zipf traffic gives
+// the top account ~1 in 5 rows), one 512-thread workgroup per account instead of one wave that
+// scans the batch and applies 64-event chunks one after another. Every event of
+// a scoring batch happens at the batch clock, so the account's events split in two:
+//   bulk  ranks 0 .. ctot-T-1 (row order): their effects commute except the tx-ring positions,
+//         which are head + rank: ring entries (only the last ring_size events are kept), the
+//         1 h sum, HLL registers as a per-register max (LDS atomicMax), and the scalar state
+//         (last tx, session, heads) once for all of them. Their GRU event rows are overwritten by
+//         the tail's (T >= ev_ring), so no per-event flags are needed.
+//   tail  the last T events (T = ev_ring rounded up to 64): exact sequential semantics through
+//         apply_chunk (new-device / new-ip flags against the registers after the bulk, GRU rows).
+// The ranks come from one ordered pass over the batch's compact row -> account column: per 512-row
+// block a ballot per wave and a 16-entry scan of the wave counts. Equal to the CPU engine's
+// sequential apply byte for byte (tests/test_engine_gpu.py hot-account tests).
+constexpr int HOT_THREADS = 512;
+constexpr int HOT_BLOCKS = 64;
+constexpr int HOT_TAIL_MAX = 192;
+
+__global__ void __launch_bounds__(HOT_THREADS) update_hot_kernel(UpdateArgs a) {
+  __shared__ uint32_t s_regs[128];  // the account's HLL registers: dev words 0..63, ip 64..127
+  __shared__ uint32_t s_pre[512];   // per register: max rank over the bulk events
+  __shared__ int s_tail[HOT_TAIL_MAX];
+  __shared__ int s_wcnt[HOT_THREADS / 64];
+  __shared__ long long s_wamt[HOT_THREADS / 64];
+  __shared__ int s_any[2];
+  const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  constexpr int NW = HOT_THREADS / 64;
+  if (upd_n(a) <= 0) return;
+  const DedupTab t = upd_region(a);
+  const int n = min(upd_n(a), t.nmax);
+  const int nh = min(t.ctr[2], t.hot_cap);
+  const ScoreCfg& cfg = *a.cfg;
+  const int64_t now = a.hdr->now;
+  const int R = a.ring_size;
+  const int T = a.ev ? min(((max(a.ev_ring, 1) + 63) / 64) * 64, HOT_TAIL_MAX) : 64;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int w = blockIdx.x; w < nh; w += gridDim.x) {
+    const int2 hs = *reinterpret_cast<const int2*>(t.hot + 2 * w);
+    const int h = hs.x, s = hs.y;
+    if (h < 0 || h >= t.cap || s < 0) continue;
+    const int ctot = t.count[h];
+    if (ctot <= DEDUP_LIST) continue;
+    const int Tn = min(T, ctot);
+    const int Nb = ctot - Tn;  // bulk events
+    AcctRT r = a.rt[s];
+    uint32_t* const g = reinterpret_cast<uint32_t*>(a.hll + (size_t)s * 512);
+    if (tid < 128) s_regs[tid] = g[tid];
+    if (tid < 512) s_pre[tid] = 0u;
+    if (tid < 2) s_any[tid] = 0;
+    __syncthreads();
+    long long amt = 0;
+    bool any_dev = false, any_ip = false;
+    int k_base = 0;  // the account's events in the earlier row blocks
+    for (int b0 = 0; b0 < n; b0 += HOT_THREADS) {
+      const int i = b0 + tid;
+      const bool m = i < n && t.rows[i] == s;
+      const uint64_t bal = __ballot(m);
+      if (lane == 0) s_wcnt[wv] = __popcll(bal);
+      __syncthreads();
+      int off = 0, blk = 0;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const int cq = s_wcnt[q];
+        off += q < wv ? cq : 0;
+        blk += cq;
+      }
+      __syncthreads();  // s_wcnt is rewritten by the next block
+      if (m) {
+        const int k = k_base + off + __popcll(bal & lt);  // the event's rank in row order
+        if (k >= Nb) {
+          s_tail[k - Nb] = i;
+        } else {
+          const ReqRec ev = a.req[i];
+          amt += ev.amount;
+          if (k >= ctot - R) {  // ring entries a later event of the batch overwrites are not written
+            const int pos = (r.ring_head + k) % R;
+            a.ring_ts[(size_t)s * R + pos] = (uint32_t)now;
+            a.ring_amt[(size_t)s * R + pos] = ev.amount;
+          }
+          if (ev.dev_hash) {
+            any_dev = true;
+            atomicMax(&s_pre[ev.dev_hash & 255u], (uint32_t)hll_rank(ev.dev_hash));
+          }
+          if (ev.ip_hash) {
+            any_ip = true;
+            atomicMax(&s_pre[256 + (ev.ip_hash & 255u)], (uint32_t)hll_rank(ev.ip_hash));
+          }
+        }
+      }
+      k_base += blk;
+    }
+    amt = wave_sum(amt);
+    const bool wd = __ballot(any_dev) != 0ull, wi = __ballot(any_ip) != 0ull;
+    if (lane == 0) {
+      s_wamt[wv] = amt;
+      if (wd) atomicOr(&s_any[0], 1);
+      if (wi) atomicOr(&s_any[1], 1);
+    }
+    __syncthreads();
+    long long tot = 0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) tot += s_wamt[q];
+    const bool ad = s_any[0] != 0, ai = s_any[1] != 0;
+    // the bulk's registers: a key expired at the batch clock was reset by its first PFADD
+    if (tid < 512) {
+      const bool ip = tid >= 256;
+      if (ip ? ai : ad) {
+        uint8_t* const rb = reinterpret_cast<uint8_t*>(s_regs);
+        const uint32_t exp = ip ? r.hll_ip_exp : r.hll_dev_exp;
+        const uint32_t base = now >= (int64_t)exp ? 0u : (uint32_t)rb[tid];
+        rb[tid] = (uint8_t)max(base, s_pre[tid]);
+      }
+    }
+    __syncthreads();
+    if (Nb > 0) {  // the bulk's scalar state, as its events applied one by one at `now`
+      r.ring_head = (r.ring_head + Nb) % R;
+      if (now >= (int64_t)r.sum_exp) r.sum_compat = 0;
+      r.sum_compat += tot;
+      r.sum_exp = (uint32_t)(now + cfg.sum_ttl);
+      if (ad) r.hll_dev_exp = (uint32_t)(now + cfg.hll_ttl);
+      if (ai) r.hll_ip_exp = (uint32_t)(now + cfg.hll_ttl);
+      r.last_tx = (uint32_t)now;
+      r.last_tx_exp = (uint32_t)(now + cfg.last_tx_ttl);
+      if (now >= (int64_t)r.session_exp || r.session_start == 0) r.session_start = (uint32_t)now;
+      r.session_exp = (uint32_t)(now + cfg.session_ttl);
+      if (a.ev) {
+        r.ev_head = (r.ev_head + Nb) % a.ev_ring;
+        r.ev_count = r.ev_count + Nb > a.ev_ring ? a.ev_ring : r.ev_count + Nb;
+      }
+      r.last_event_ts = (uint32_t)now;
+    }
+    if (wv == 0) {  // the tail, exact, 64 events at a time
+      for (int q = 0; q < Tn; q += 64) {
+        const int c = min(64, Tn - q);
+        const int pj = lane < c ? s_tail[q + lane] : 0;
+        apply_chunk<true>(a, s, r, pj, c, lane, reinterpret_cast<uint8_t*>(s_regs), Nb + q, ctot);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      g[lane] = s_regs[lane];
+      g[64 + lane] = s_regs[64 + lane];
+      if (lane == 0) a.rt[s] = r;
+    }
+    __syncthreads();  // the LDS is the next hot account's
   }
 }
 
@@ -1077,7 +1231,9 @@ void launch_dedup_insert(const UpdateArgs& a, hipStream_t st) {
 
 void launch_update_segments(const UpdateArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
-  // one wave per multi-event account, 256 waves looping over the region's list
+  // scorer path: the hot accounts (> DEDUP_LIST events) one workgroup each, then one wave per
+  // other multi-event account, 256 waves looping over the region's list
+  if (a.region < 0) IGP_LAUNCH(update_hot_kernel, dim3(HOT_BLOCKS), dim3(HOT_THREADS), 0, st, a);
   IGP_LAUNCH(update_multi_kernel, dim3(UPD_MULTI_BLOCKS), dim3(256), 0, st, a);
 }
 

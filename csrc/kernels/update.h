@@ -18,14 +18,20 @@ struct DedupTab {
   int32_t* done;    // scorer path: rows of the account whose reads are complete
   int32_t* list;    // [cap][DEDUP_LIST]
   int32_t* mlist;   // [n_max / 2] pairs {hash slot, account slot} of multi-event accounts
-  int32_t* ctr;     // [0] multi-account count, [1] the batch clock's hour-of-day event word
+  int32_t* ctr;     // [0] multi-account count, [1] the batch clock's hour-of-day event word,
+                    // [2] hot-account count, [3] spare
   int32_t* rows;    // [n_max]: row i's account slot if this rank applies it, else -1 (hot scans)
+  int32_t* hot;     // [hot_cap] pairs {hash slot, account slot}: accounts with > DEDUP_LIST events
   int32_t cap;
   int32_t nmax;     // ints in mlist (n_max / 2 pairs: each listed account has >= 2 events)
+  int32_t hot_cap;  // pairs in hot (n_max / (DEDUP_LIST + 1) + 1)
 };
 
+__host__ __device__ inline int dedup_hot_cap(int n_max) { return n_max / (DEDUP_LIST + 1) + 1; }
+
 __host__ __device__ inline size_t dedup_region_size(int cap, int n_max) {
-  return ((size_t)5 * cap + (size_t)cap * DEDUP_LIST + 2 * (size_t)n_max + 2 + 15) & ~size_t(15);
+  return ((size_t)5 * cap + (size_t)cap * DEDUP_LIST + 2 * (size_t)n_max + 4 + 2 * (size_t)dedup_hot_cap(n_max) +
+          15) & ~size_t(15);
 }
 
 __device__ __forceinline__ DedupTab dedup_region(int32_t* buf, int cap, int n_max, int region) {
@@ -39,9 +45,11 @@ __device__ __forceinline__ DedupTab dedup_region(int32_t* buf, int cap, int n_ma
   t.list = b + 5 * cap;
   t.mlist = t.list + (size_t)cap * DEDUP_LIST;
   t.ctr = t.mlist + n_max;
-  t.rows = t.ctr + 2;
+  t.rows = t.ctr + 4;
+  t.hot = t.rows + n_max;
   t.cap = cap;
   t.nmax = n_max;
+  t.hot_cap = dedup_hot_cap(n_max);
   return t;
 }
 

@@ -36,6 +36,16 @@ DEDUP_REGIONS = 5  # 4 scorer ring regions (by batch seq) + 1 standalone ingesti
 DEDUP_STANDALONE = 4
 
 
+def dedup_hot_cap(n_max: int) -> int:
+    """Hot-account pairs per region (update.h dedup_hot_cap)."""
+    return n_max // (DEDUP_LIST + 1) + 1
+
+
+def dedup_region_size(cap: int, n_max: int) -> int:
+    """int32 words of one dedup region (update.h dedup_region_size)."""
+    return (5 * cap + cap * DEDUP_LIST + 2 * n_max + 4 + 2 * dedup_hot_cap(n_max) + 15) & ~15
+
+
 def _pow2_at_least(n: int) -> int:
     c = 1
     while c < n:
@@ -83,9 +93,10 @@ class DeviceFeatureStore:
         self.dmax = self.max_events
         self.dcap = _pow2_at_least(2 * self.max_events)
         # per region (csrc/kernels/update.h dedup_region): keys/first/count/fill/done [cap],
-        # per-account event lists [cap][DEDUP_LIST], multi-account list [dmax], 2 counters, the
-        # batch's row -> applied account slot array [dmax] (update.h dedup_region_size)
-        self.dregion = (5 * self.dcap + self.dcap * DEDUP_LIST + 2 * self.dmax + 2 + 15) & ~15
+        # per-account event lists [cap][DEDUP_LIST], multi-account list [dmax], 4 counters, the
+        # batch's row -> applied account slot array [dmax], the hot-account list [hot_cap] pairs
+        # (update.h dedup_region_size; checked against the extension by layouts.check_layouts)
+        self.dregion = dedup_region_size(self.dcap, self.dmax)
         self.dbuf = torch.empty(DEDUP_REGIONS * self.dregion, dtype=torch.int32, **z)
         self.reset_dedup()
 

@@ -69,10 +69,13 @@ def check_layouts(mod) -> None:
         want = getattr(mod, "SIZEOF_" + name)
         if dt.itemsize != want:
             raise RuntimeError(f"layout drift: {name} is {dt.itemsize} B in Python, {want} B in C")
-    from .features.device_store import DEDUP_LIST, DEDUP_REGIONS
+    from .features.device_store import DEDUP_LIST, DEDUP_REGIONS, dedup_region_size
     if (getattr(mod, "DEDUP_LIST", DEDUP_LIST), getattr(mod, "DEDUP_REGIONS", DEDUP_REGIONS)) != (DEDUP_LIST,
                                                                                                  DEDUP_REGIONS):
         raise RuntimeError("layout drift: dedup scratch layout differs between Python and C")
+    f = getattr(mod, "dedup_region_size", None)
+    if f is not None and any(f(c, n) != dedup_region_size(c, n) for c, n in ((16384, 8192), (1024, 300), (64, 1))):
+        raise RuntimeError("layout drift: dedup region size differs between Python and C")
 
 
 def score_cfg(cfg: Config, model_kind: int, ml_col: int = 0, ml_stride: int = 1,
