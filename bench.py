@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="per-GPU micro-batch (default: the config's)")
     ap.add_argument("--accounts", type=int, default=1 << 20, help="feature-store accounts per GPU")
-    ap.add_argument("--depth", type=int, default=3, help="pipeline depth (batches in flight)")
+    ap.add_argument("--depth", type=int, default=4, help="pipeline depth (batches in flight; up to 7, launch.h DEDUP_AHEAD)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the per-step RCCL all_gather")
     ap.add_argument("--numerics", default="auto", choices=["auto", "fp32", "bf16"],
@@ -75,7 +75,7 @@ def parse():
                          "device pipeline (device-pipeline number); e2e / grpc: tools/bench_e2e.py")
     ap.add_argument("--threads", type=int, default=16,
                     help="serving scope: ingress threads per rank (the box gives each GPU 16 CPUs)")
-    ap.add_argument("--rounds", type=int, default=16,
+    ap.add_argument("--rounds", type=int, default=32,
                     help="serving scope: ScoreBatch requests per ingress thread in one timed step (a step of "
                          "threads x rounds requests per rank keeps the driver's --steps 20 window >= 0.5 s)")
     ap.add_argument("--requests", type=int, default=0, help="serving scope: transactions per ScoreBatch request "

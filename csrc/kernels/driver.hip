@@ -23,6 +23,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -93,8 +94,11 @@ class PipeDriver {
     ev_.resize(3 * depth);
     for (size_t i = 0; i < ev_.size(); ++i)
       hip_ok(hipEventCreateWithFlags(&ev_[i], i % 3 == 2 ? hipEventDisableTiming : dev_flags), "event create");
-    pe_.resize(depth);
+    if (depth > DEDUP_AHEAD)  // batch q's dedup region was cleared by batch q - DEDUP_AHEAD's update
+      throw std::runtime_error("PipeDriver: depth exceeds the dedup ring (DEDUP_AHEAD)");
     for (auto& e : pe_) hip_ok(hipEventCreateWithFlags(&e, dev_flags), "event create");
+    pe_seq_.fill(-1);
+    slot_seq_.assign(depth, -1);
     recorded_.assign(3 * depth, false);
     host_done_.assign(depth, 0);
     const char* xe = getenv("IGP_EXT_EVENTS");
@@ -338,11 +342,16 @@ class PipeDriver {
     h->now = now;
     hipEvent_t ce = ev_[3 * slot], se = ev_[3 * slot + 1], me = ev_[3 * slot + 2];
     const bool serial = cmd.bucket <= serial_max_ && g.oc && g.os && g.om && g.omf;
-    if (serial && !hist_.empty() && !serial_hist_) {
+    if (serial && last_seq_ >= 0 && !serial_hist_) {
       // the previous batch ran as three stages: its state work (store updates) comes first
-      hip_ok(hipStreamWaitEvent(cs_, pe_[hist_.back()], 0), "wait previous state");
+      if (hipEvent_t e = post_event(last_seq_)) hip_ok(hipStreamWaitEvent(cs_, e, 0), "wait previous state");
     }
     serial_hist_ = serial;
+    const int prev_seq = slot_seq_[slot];
+    hipEvent_t pe = pe_[ring(seq)];
+    pe_seq_[ring(seq)] = seq;
+    slot_seq_[slot] = seq;
+    last_seq_ = seq;
     if (serial) {
       // serial mode (small micro-batches): every stage on the copy stream in order - no
       // cross-queue waits (~12 us each when unsatisfied) and no event calls but the completion
@@ -352,16 +361,14 @@ class PipeDriver {
       g.os->run(cs_);
       if (g.osu) g.osu->run(cs_);
       (with_features ? g.omf : g.om)->run(cs_);
-      hip_ok(hipEventRecord(pe_[slot], cs_), "record post");
-      if (clock_) clock_->publish(pe_[slot]);  // the batch's whole state stage (read-your-writes)
+      hip_ok(hipEventRecord(pe, cs_), "record post");
+      if (clock_) clock_->publish(pe);  // the batch's whole state stage (read-your-writes)
       hip_ok(hipEventRecord(me, cs_), "record model");
       st_[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
       st_[2] += std::chrono::duration<double, std::micro>(clk::now() - ts).count();
       st_[5] += 1;
       host_done_[slot] = 0;
       recorded_[3 * slot] = recorded_[3 * slot + 1] = recorded_[3 * slot + 2] = true;
-      hist_.push_back(slot);
-      if ((int)hist_.size() > DEDUP_AHEAD) hist_.erase(hist_.begin());
       return;
     }
     // the slot's previous batch: skipped when the host already saw it complete (wait(slot))
@@ -369,15 +376,13 @@ class PipeDriver {
     host_done_[slot] = 0;
     // the slot's previous batch's split update stage (state stream, after K1) also reads the
     // slot's device header and rows: the model event above does not cover it (the model only
-    // waited for K1), and the dedup-ring wait below only covers batch seq - DEDUP_AHEAD, so with
-    // fewer slots than DEDUP_AHEAD the copy must wait for that update itself (an event query
-    // first: no queue wait when it already finished)
-    if (recorded_[3 * slot + 1] && hipEventQuery(pe_[slot]) != hipSuccess)
-      hip_ok(hipStreamWaitEvent(cs_, pe_[slot], 0), "wait slot update");
-    // the state stage of batch seq - DEDUP_AHEAD cleared this batch's dedup region: wait for it
-    // unless the host already sees it complete (an event query instead of a queue wait)
-    if ((int)hist_.size() == DEDUP_AHEAD && (hipEventQuery(pe_[hist_.front()]) != hipSuccess))
-      hip_ok(hipStreamWaitEvent(cs_, pe_[hist_.front()], 0), "wait state-3");
+    // waited for K1). An event query first: no queue wait when it already finished.
+    if (hipEvent_t e = post_event(prev_seq); e && hipEventQuery(e) != hipSuccess)
+      hip_ok(hipStreamWaitEvent(cs_, e, 0), "wait slot update");
+    // the state stage of batch seq - DEDUP_AHEAD cleared this batch's dedup region (the post
+    // events are kept per batch in a ring of DEDUP_RING, so this is exact at any depth <= AHEAD)
+    if (hipEvent_t e = post_event(seq - DEDUP_AHEAD); e && hipEventQuery(e) != hipSuccess)
+      hip_ok(hipStreamWaitEvent(cs_, e, 0), "wait state-ahead");
     const auto t2 = clk::now();
     const bool cb = stage_rec(g.c, g.oc, cs_, ce, "copy graph");
     const auto t3 = clk::now();
@@ -391,10 +396,10 @@ class PipeDriver {
     // split state stage (direct launch): the model waited for K1 only; the multi-event update
     // (which also clears the dedup region of batch seq+3) follows on the state stream and its
     // own event gates that region's reuse
-    const bool pb = g.osu && ext_events_ && g.osu->run_recording(ss_, pe_[slot]);
+    const bool pb = g.osu && ext_events_ && g.osu->run_recording(ss_, pe);
     if (g.osu && !ext_events_) g.osu->run(ss_);
-    if (!pb) hip_ok(hipEventRecord(pe_[slot], ss_), "record post");
-    if (clock_) clock_->publish(pe_[slot]);  // K1 + the multi-event update of this batch
+    if (!pb) hip_ok(hipEventRecord(pe, ss_), "record post");
+    if (clock_) clock_->publish(pe);  // K1 + the multi-event update of this batch
     const auto t6 = clk::now();
     const bool mb = stage_rec(with_features ? g.mf : g.m, with_features ? g.omf : g.om, ms_, me, "model graph");
     const auto t7 = clk::now();
@@ -408,8 +413,12 @@ class PipeDriver {
     st_[4] += us(t6, t7);                          // model graph launch
     st_[5] += 1;
     recorded_[3 * slot] = recorded_[3 * slot + 1] = recorded_[3 * slot + 2] = true;
-    hist_.push_back(slot);
-    if ((int)hist_.size() > DEDUP_AHEAD) hist_.erase(hist_.begin());
+  }
+  static int ring(int seq) { return (int)((unsigned)seq % DEDUP_RING); }
+  // the post-state event of batch `seq` if this driver issued it (and the ring still holds it)
+  hipEvent_t post_event(int seq) const {
+    if (seq < 0) return nullptr;
+    return pe_seq_[ring(seq)] == seq ? pe_[ring(seq)] : nullptr;
   }
 
  public:
@@ -465,10 +474,13 @@ class PipeDriver {
   int depth_;
   std::vector<char*> slabs_;
   std::vector<hipEvent_t> ev_;
-  std::vector<hipEvent_t> pe_;  // per slot: the state stream's work of the batch is complete
+  // per batch (ring of DEDUP_RING by seq): the state stream's work of the batch is complete
+  std::array<hipEvent_t, DEDUP_RING> pe_{};
+  std::array<int, DEDUP_RING> pe_seq_{};  // the batch each ring event was last recorded for
+  std::vector<int> slot_seq_;             // the slot's last batch
+  int last_seq_ = -1;
   std::vector<bool> recorded_;
   std::vector<uint8_t> host_done_;  // wait(slot) returned since the slot's last submit (bytes: set by waiter threads)
-  std::vector<int> hist_;  // slots of the last DEDUP_AHEAD submitted batches, oldest first
   std::shared_ptr<StateClock> clock_;
   std::unordered_map<int64_t, Graphs> graphs_;
   int serial_max_ = 0;

@@ -6,6 +6,7 @@
 //   write path  redis_store.go:119-168
 //   rules       scoring/engine.go:420-483
 //   blacklist   redis_store.go:267-293
+#include <cstdlib>
 #include <stdexcept>
 
 #include "update.h"
@@ -1032,18 +1033,20 @@ constexpr int UPD_MULTI_BLOCKS = 64;  // 256 waves loop over the list (any count
 // dependent memory round trips per account: {list count, first pair} -> {count, AcctRT, row
 // list} -> request rows -> both HLL registers -> stores (the pair carries the account slot, so
 // count, AcctRT and the row list are loaded together)
-__global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
-  __shared__ uint32_t s_regs[4][128];  // per wave: a hot account's HLL registers
+// The multi-event accounts: wave w0 of `nwaves` loops over the region's list; thread `gt` of
+// `nthreads` also clears the dedup region batch seq + DEDUP_AHEAD will insert into (scorer ring).
+template <int WPB>
+__device__ __forceinline__ void update_multi_body(const UpdateArgs& a, int w0, int nwaves, int gt, int nthreads,
+                                                  uint32_t (*s_regs)[128]) {
   const int lane = threadIdx.x & 63;
   const DedupTab t = upd_region(a);
   const int npair = t.nmax >> 1;
-  const int w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   int2 hs = w0 < npair ? *reinterpret_cast<const int2*>(t.mlist + 2 * w0) : make_int2(-1, -1);  // speculative
   // a batch with no live rows (graph warm-up, an empty padded launch) applies nothing: the
   // region's list may still hold the previous user of the region (a scorer that took over
   // the store carries the batch sequence over)
   const int nm = upd_n(a) > 0 ? min(t.ctr[0], npair) : 0;
-  for (int w = w0; w < nm; w += UPD_MULTI_BLOCKS * 4) {
+  for (int w = w0; w < nm; w += nwaves) {
     if (w != w0) hs = *reinterpret_cast<const int2*>(t.mlist + 2 * w);
     const int h = hs.x, s = hs.y;
     if (h < 0 || h >= t.cap || s < 0) continue;
@@ -1051,7 +1054,7 @@ __global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
     const AcctRT r = a.rt[s];
     if (c < 2) continue;
     if (c > DEDUP_LIST && a.region < 0) continue;  // scorer path: update_hot_kernel applies it
-    apply_segment_wave(a, t, h, c, s, r, lane, s_regs[threadIdx.x >> 6]);
+    apply_segment_wave(a, t, h, c, s, r, lane, s_regs[(threadIdx.x >> 6) & (WPB - 1)]);
   }
   // scorer ring: clear the region of batch seq + DEDUP_AHEAD (= seq-1's, consumed by now) for
   // its insert; the copy of that batch waits for this batch's state stage
@@ -1059,16 +1062,22 @@ __global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
     const DedupTab nt = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(a.hdr->seq + DEDUP_AHEAD));
     const int4 m1 = make_int4(-1, -1, -1, -1), big = make_int4(0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff);
     const int4 z = make_int4(0, 0, 0, 0);
-    for (int e4 = blockIdx.x * 256 + threadIdx.x; e4 < (nt.cap >> 2); e4 += UPD_MULTI_BLOCKS * 256) {
+    for (int e4 = gt; e4 < (nt.cap >> 2); e4 += nthreads) {
       reinterpret_cast<int4*>(nt.keys)[e4] = m1;
       reinterpret_cast<int4*>(nt.first)[e4] = big;
       reinterpret_cast<int4*>(nt.count)[e4] = z;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (gt == 0) {
       nt.ctr[0] = 0;
       nt.ctr[2] = 0;
     }
   }
+}
+
+__global__ void __launch_bounds__(256) update_multi_kernel(UpdateArgs a) {
+  __shared__ uint32_t s_regs[4][128];  // per wave: a multi-event account's HLL registers
+  const int w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  update_multi_body<4>(a, w0, UPD_MULTI_BLOCKS * 4, blockIdx.x * 256 + threadIdx.x, UPD_MULTI_BLOCKS * 256, s_regs);
 }
 
 // Hot accounts on the scorer path (more than DEDUP_LIST events in one batch: Zipf traffic gives
@@ -1089,13 +1098,23 @@ constexpr int HOT_THREADS = 512;
 constexpr int HOT_BLOCKS = 64;
 constexpr int HOT_TAIL_MAX = 192;
 
-__global__ void __launch_bounds__(HOT_THREADS) update_hot_kernel(UpdateArgs a) {
-  __shared__ uint32_t s_regs[128];  // the account's HLL registers: dev words 0..63, ip 64..127
-  __shared__ uint32_t s_pre[512];   // per register: max rank over the bulk events
-  __shared__ int s_tail[HOT_TAIL_MAX];
-  __shared__ int s_wcnt[HOT_THREADS / 64];
-  __shared__ long long s_wamt[HOT_THREADS / 64];
-  __shared__ int s_any[2];
+struct HotLds {
+  uint32_t regs[128];  // the account's HLL registers: dev words 0..63, ip 64..127
+  uint32_t pre[512];   // per register: max rank over the bulk events
+  int tail[HOT_TAIL_MAX];
+  int wcnt[HOT_THREADS / 64];
+  long long wamt[HOT_THREADS / 64];
+  int any[2];
+};
+
+// hot accounts w = hb, hb + nhb, ... of the region's hot list, one HOT_THREADS workgroup each
+__device__ __forceinline__ void update_hot_body(const UpdateArgs& a, int hb, int nhb, HotLds& L) {
+  uint32_t* const s_regs = L.regs;
+  uint32_t* const s_pre = L.pre;
+  int* const s_tail = L.tail;
+  int* const s_wcnt = L.wcnt;
+  long long* const s_wamt = L.wamt;
+  int* const s_any = L.any;
   const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
   constexpr int NW = HOT_THREADS / 64;
   if (upd_n(a) <= 0) return;
@@ -1107,7 +1126,7 @@ __global__ void __launch_bounds__(HOT_THREADS) update_hot_kernel(UpdateArgs a) {
   const int R = a.ring_size;
   const int T = a.ev ? min(((max(a.ev_ring, 1) + 63) / 64) * 64, HOT_TAIL_MAX) : 64;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (int w = blockIdx.x; w < nh; w += gridDim.x) {
+  for (int w = hb; w < nh; w += nhb) {
     const int2 hs = *reinterpret_cast<const int2*>(t.hot + 2 * w);
     const int h = hs.x, s = hs.y;
     if (h < 0 || h >= t.cap || s < 0) continue;
@@ -1217,6 +1236,33 @@ __global__ void __launch_bounds__(HOT_THREADS) update_hot_kernel(UpdateArgs a) {
   }
 }
 
+__global__ void __launch_bounds__(HOT_THREADS) update_hot_kernel(UpdateArgs a) {
+  __shared__ HotLds L;
+  update_hot_body(a, blockIdx.x, gridDim.x, L);
+}
+
+// The scorer path's whole post-K1 update in one launch (the hot and the other multi-event
+// accounts are disjoint sets): workgroups [0, UPD_SEG_MULTI) run the multi-event list as 8 waves
+// each (256 waves, as update_multi_kernel) and clear the next region; workgroups
+// [UPD_SEG_MULTI, + HOT_BLOCKS) take the hot accounts. One dispatch instead of two back to back on
+// the state stream (each paid its argument fetch, the dependent header / counter loads and the
+// queue's inter-dispatch gap: ~7 us per batch, r5n timeline).
+constexpr int UPD_SEG_MULTI = UPD_MULTI_BLOCKS / 2;
+__global__ void __launch_bounds__(HOT_THREADS) update_segments_kernel(UpdateArgs a) {
+  __shared__ union {
+    HotLds hot;
+    uint32_t regs[HOT_THREADS / 64][128];
+  } L;
+  const int b = (int)blockIdx.x;
+  if (b < UPD_SEG_MULTI) {
+    const int w0 = __builtin_amdgcn_readfirstlane(b * (HOT_THREADS / 64) + (int)(threadIdx.x >> 6));
+    update_multi_body<HOT_THREADS / 64>(a, w0, UPD_SEG_MULTI * (HOT_THREADS / 64), b * HOT_THREADS + threadIdx.x,
+                                        UPD_SEG_MULTI * HOT_THREADS, L.regs);
+  } else {
+    update_hot_body(a, b - UPD_SEG_MULTI, HOT_BLOCKS, L.hot);
+  }
+}
+
 // ---------------------------------------------------------------------------------- launch
 void launch_feature_assemble(const AssembleArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
@@ -1233,6 +1279,14 @@ void launch_update_segments(const UpdateArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
   // scorer path: the hot accounts (> DEDUP_LIST events) one workgroup each, then one wave per
   // other multi-event account, 256 waves looping over the region's list
+  static const int fused = [] {
+    const char* e = std::getenv("IGP_UPD_FUSED");
+    return e ? std::atoi(e) : 1;
+  }();
+  if (a.region < 0 && fused) {
+    IGP_LAUNCH(update_segments_kernel, dim3(UPD_SEG_MULTI + HOT_BLOCKS), dim3(HOT_THREADS), 0, st, a);
+    return;
+  }
   if (a.region < 0) IGP_LAUNCH(update_hot_kernel, dim3(HOT_BLOCKS), dim3(HOT_THREADS), 0, st, a);
   IGP_LAUNCH(update_multi_kernel, dim3(UPD_MULTI_BLOCKS), dim3(256), 0, st, a);
 }

@@ -14,13 +14,13 @@ namespace igp {
 constexpr int DEDUP_LIST = 64;
 
 // scorer batches rotate over DEDUP_RING dedup regions by BatchHdr::seq: batch q's state stage
-// clears the region of batch q + DEDUP_AHEAD, so batch q+1's dedup insert (copy stream) can run
-// while batch q is still in K1 / update_segments on the state stream. The copy of batch q waits
-// for the state stage of batch q - DEDUP_AHEAD; with four regions that batch is three back, and
-// the native driver skips the wait when the host already sees it complete (it usually does: the
-// host waited for batch q - 3's model before submitting q). Region DEDUP_STANDALONE: event
-// ingestion.
-constexpr int DEDUP_RING = 4;
+// clears the region of batch q + DEDUP_AHEAD (= q - 1's, consumed by then), so batch q+1's dedup
+// insert (copy stream) can run while batch q is still in K1 / update_segments on the state stream.
+// The copy of batch q waits for the state stage of batch q - DEDUP_AHEAD (the native driver keeps
+// one post-state event per ring entry and only queues the wait when the host does not already see
+// that batch complete). Eight regions let the pipeline run up to seven batches deep without that
+// wait: with four, depth 4 collapsed (r4 NOTES). Region DEDUP_STANDALONE: event ingestion.
+constexpr int DEDUP_RING = 8;
 constexpr int DEDUP_AHEAD = DEDUP_RING - 1;
 constexpr int DEDUP_STANDALONE = DEDUP_RING;
 __host__ __device__ inline int dedup_ring_region(int seq) { return (int)((unsigned)seq % DEDUP_RING); }

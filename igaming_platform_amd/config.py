@@ -144,7 +144,7 @@ class GPUConfig:
     # native serving core (csrc/runtime/serve_core.cpp, engine/serving.py): request bytes ->
     # response bytes without Python on the hot path; the unary micro-batcher is its FIFO
     native_serving: bool = True
-    serve_depth: int = 3          # pipeline slots (batches in flight) of a shard's device
+    serve_depth: int = 4          # pipeline slots (batches in flight) of a shard's device (<= 7)
     serve_finishers: int = 2      # unary response threads
     exchange_timeout_s: float = 10.0  # multi-rank step deadline: a peer that misses it failed
     # native account RPCs (csrc/runtime/acct_core.cpp, engine/acct.py): PredictLTV,

@@ -10,7 +10,7 @@ One micro-batch = three captured hipGraphs on three HIP streams:
     K1   feature_assemble (+blacklist, +ip-intel, +HLL counts, +rules) -> X, FeatRec, then
          score-then-update of every account with one event in the batch
     K6b  update_multi: the multi-event accounts' events in row order (one wave each), then
-         clear the dedup region of batch seq+3 (four-region ring)
+         clear the dedup region of batch seq+7 (eight-region ring, launch.h DEDUP_RING)
   model stream (reads only the slot's X / FeatRec; never touches the store)
     K2/K3 model steps of the compiled ONNX plan                            -> ml
     K5   ensemble + action (+K10 metrics histogram)                        -> ResultRec
@@ -19,9 +19,10 @@ One micro-batch = three captured hipGraphs on three HIP streams:
 Score-then-update (engine.go:486-488) needs only the batch's own requests and the state K1
 read, so the whole store read-modify-write finishes in the state graph, and the next batch's
 K1 starts while this batch's trees / MLP / ensemble still run on the model stream; its copy
-and dedup insert run even earlier, under this batch's K1 (dedup regions rotate over three by
-batch seq; the state graph of batch q clears the region of batch q+2, so the copy of batch q
-waits for the state graph of batch q-2). Each pipeline slot has its own device slab, X,
+and dedup insert run even earlier, under this batch's K1 (dedup regions rotate over eight by
+batch seq; the state graph of batch q clears the region of batch q+7, so the copy of batch q
+needs the state graph of batch q-7: the native driver keeps one event per ring entry, this
+Python path waits for batch q-2's, which covers it). Each pipeline slot has its own device slab, X,
 FeatRec, result and model activation buffers; a slot is reused only after the model graph
 that last read it.
 
@@ -280,7 +281,7 @@ class GpuScorer:
 
     def _state_body(self, slot: int, bucket: int, part: str = "all") -> None:
         """K1 (part "k1"), then the multi-event update that also clears the dedup region of
-        batch seq+3 (part "update")."""
+        batch seq + DEDUP_AHEAD (part "update")."""
         sb, upd = self.slots[slot], self.update_features
         if part in ("all", "k1"):
             K.feature_assemble(self.store, sb.hdr, self.cfg_dev, sb.req, sb.X, sb.feat, bucket, dedup=upd,

@@ -32,8 +32,8 @@ from ..layouts import ACCTBATCH, ACCTRT
 from .tables import Blacklist, IPIntel
 
 DEDUP_LIST = 64  # events per account per batch kept in a dedup list (launch.h DEDUP_LIST)
-DEDUP_REGIONS = 5  # 4 scorer ring regions (by batch seq) + 1 standalone ingestion region
-DEDUP_STANDALONE = 4
+DEDUP_REGIONS = 9  # 8 scorer ring regions (by batch seq) + 1 standalone ingestion region (launch.h)
+DEDUP_STANDALONE = 8
 
 
 def dedup_hot_cap(n_max: int) -> int:

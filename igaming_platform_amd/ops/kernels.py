@@ -195,7 +195,7 @@ def dedup_insert(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, hd
 
 def update_segments(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, hdr: torch.Tensor) -> None:
     """Scorer tail (after K1): ordered apply of the multi-event accounts (insert before K1,
-    single-event accounts in K1), then clear the dedup region of batch seq+3."""
+    single-event accounts in K1), then clear the dedup region of batch seq + DEDUP_AHEAD (launch.h)."""
     d = update_args(store, cfg_dev, req, n_max, hdr=hdr, region=-1)
     d["segments_only"] = 1
     _mod().feature_update(d, _stream())

@@ -84,6 +84,20 @@ def _free_port():
     return p
 
 
+def _init_pg(backend, **kw):
+    """init_process_group on a fresh local port; a port handed out by the kernel can be taken
+    again before the store binds it (EADDRINUSE): then another one."""
+    import torch.distributed as dist
+    for attempt in range(5):
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+        try:
+            dist.init_process_group(backend, rank=0, world_size=1, **kw)
+            return
+        except dist.DistNetworkError:
+            if attempt == 4:
+                raise
+
+
 @pytest.mark.parametrize("results", ["a2a", "d2h"])
 def test_spmd_engine_world1_matches_plain_gpu_engine(monkeypatch, results):
     """The SPMD serving engine at world 1 (its native core driving the exchange pipeline)
@@ -95,8 +109,7 @@ def test_spmd_engine_world1_matches_plain_gpu_engine(monkeypatch, results):
     from igaming_platform_amd.config import Config
     from igaming_platform_amd.engine.risk_engine import RiskEngine
     from igaming_platform_amd.parallel.comm import TorchComm
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    _init_pg("nccl", device_id=torch.device("cuda", 0))
     spmd = plain = None
     try:
         cfg = Config()
@@ -140,8 +153,7 @@ def test_spmd_engines_close_and_destroy_their_communicators():
     from igaming_platform_amd.engine.risk_engine import RiskEngine
     from igaming_platform_amd.parallel.comm import TorchComm
     for round_ in range(2):
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
-        dist.init_process_group("gloo", rank=0, world_size=1)
+        _init_pg("gloo")
         eng = None
         try:
             cfg = Config()
@@ -245,8 +257,7 @@ def test_exchange_world1_same_accounts_in_one_step_follow_fifo_order():
     from igaming_platform_amd.engine.risk_engine import RiskEngine
     from igaming_platform_amd.parallel.comm import TorchComm
     from igaming_platform_amd.proto import risk_v1 as P
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    _init_pg("nccl", device_id=torch.device("cuda", 0))
     spmd = plain = None
     try:
         cfg = Config()
