@@ -79,7 +79,10 @@ struct AcctRT {
   int32_t ring_head;        // next tx-ring write position
   int32_t ev_head;          // next event-ring write position
   int32_t ev_count;
-  int32_t pad[3];
+  // padding as scalars, not an array: a kernel-local copy of a struct with an array member became
+  // an LDS-promoted alloca indexed by the flat work-item id, i.e. one read of the dispatch packet
+  // (host memory) per wave for the work-group size (K1, the update kernels)
+  int32_t pad0, pad1, pad2;
 };
 static_assert(sizeof(AcctRT) == 64, "AcctRT must be 64 bytes");
 
@@ -98,7 +101,7 @@ struct AcctBatch {
   int32_t bonus_claim_count;
   float bonus_wager_complete;
   int32_t present;          // 0 = batch features unavailable (partial features, quirk Q10)
-  int32_t pad[2];
+  int32_t pad0, pad1;
 };
 static_assert(sizeof(AcctBatch) == 80, "AcctBatch must be 80 bytes");
 
@@ -131,7 +134,7 @@ struct ScoreCfg {
   int32_t ext_width;        // feature-vector columns beyond the 30 reference ones
   int32_t owner_filter;     // 1: rows whose owner (ReqRec.tx_type bits 8..15) != my_rank are skipped
   int32_t my_rank;
-  int32_t pad[3];
+  int32_t pad0, pad1, pad2;
 };
 static_assert(sizeof(ScoreCfg) == 176, "ScoreCfg must be 176 bytes");
 // feature_assemble reads ScoreCfg bytes 128..159 as two int4 (csrc/kernels/features.hip)

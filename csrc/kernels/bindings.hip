@@ -143,7 +143,6 @@ PYBIND11_MODULE(_hipk, m) {
     a.ip_flags = ptr<const uint32_t*>(d, "ip_flags");
     a.hll_lc = ptr<const int32_t*>(d, "hll_lc");
     if (!a.hll_lc) throw std::runtime_error("feature_assemble: hll_lc table required");
-    a.ablate = d.contains("ablate") ? d["ablate"].cast<int>() : 0;
     a.X = ptr<float*>(d, "X");
     a.feat = ptr<FeatRec*>(d, "feat");
     a.fenc = ptr<uint8_t*>(d, "fenc");

@@ -6,7 +6,6 @@
 //   write path  redis_store.go:119-168
 //   rules       scoring/engine.go:420-483
 //   blacklist   redis_store.go:267-293
-#include <cstdlib>
 #include <stdexcept>
 
 #include "update.h"
@@ -146,7 +145,7 @@ __device__ __forceinline__ void apply_event_q(const UpdateArgs& a, const ScoreCf
     r.ev_count = r.ev_count + 1 > a.ev_ring ? a.ev_ring : r.ev_count + 1;
   }
   r.last_event_ts = (uint32_t)now;
-  if (ql == 0) a.rt[s] = r;
+  if (ql == 0) store_rt(a.rt + s, r);
 }
 
 // inert row (graph padding / another rank's request): zero inputs, FeatRec with slot -1 (also
@@ -354,66 +353,70 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     s = rq.slot;
     const int64_t amount = rq.amount;
     const int tx_type = rq.tx_type & 0xff;
-    // ---- level 2 (clamped addresses, masked afterwards)
+    // ---- level 2 (clamped addresses, masked afterwards). Every load below is unconditional
+    // but for the kernel-uniform table / dedup switches: a data-dependent branch around a load
+    // makes the count of outstanding loads path-dependent, and the compiler then waits for all
+    // of them (vmcnt(0)) at the first use of any.
     const bool has = s >= 0;
     const int sc = has ? s : 0;
-    const int rs = a.ring_size;  // multiple of 64: lane ql holds entries 4 (ql + 16 i) .. +3
-    const int n4 = rs / 4;
-    const uint4* ts4 = reinterpret_cast<const uint4*>(a.ring_ts + (size_t)sc * rs);
-    uint4 tsv[4] = {};
-    if (!(a.ablate & 32)) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) tsv[i] = ts4[min(ql + 16 * i, n4 - 1)];
-    }
-    const uint32_t* hreg = reinterpret_cast<const uint32_t*>(a.hll + (size_t)sc * 512);
-    const int abl = a.ablate;
-    uint32_t wd[4] = {0, 0, 0, 0}, wi[4] = {0, 0, 0, 0};
-    if (!(abl & 1)) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        wd[i] = hreg[ql + 16 * i];
-        wi[i] = hreg[64 + ql + 16 * i];
-      }
-    }
-    AcctRT rt{};
-    AcctBatch bt{};
-    if (!(abl & 64)) {
-      rt = a.rt[sc];
-      bt = a.batch[sc];
-    }
-    const float* e = a.ext + (size_t)sc * ext_w;
-    float extv[7] = {0, 0, 0, 0, 0, 0, 0};  // ext widths up to 112 preloaded; wider rows finish in a loop at the end
-    if (!(abl & 16)) {
-#pragma unroll
-      for (int u = 0; u < 7; ++u) extv[u] = e[max(0, min(ql + 16 * u, ext_w - 1))];
-    }
-    uint32_t dh = 0, hour_word = 0;
-    int dkey = -1, dfirst = -1;
-    if (a.dbuf && !(abl & 2)) {  // kernel-uniform
-      const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
-      dh = mix32((uint32_t)sc) & (uint32_t)(t.cap - 1);
-      dkey = t.keys[dh];
-      dfirst = t.first[dh];
-      dcount = t.count[dh];
-      hour_word = (uint32_t)t.ctr[1];
-    }
-    // K7: blacklist (lanes 0..2: device, fingerprint, ip) and IP intelligence (lane 3)
+    // K7 first probe slots: blacklist (lanes 0..2: device, fingerprint, ip) and IP intelligence
+    // (lane 3); their addresses need only the request row and the config block
     uint64_t key = 0;
     if (ql == 0) key = rq.dev_hash;
     else if (ql == 1) key = rq.fp_hash;
     else if (ql == 2 || ql == 3) key = rq.ip_hash;
-    const bool tabs = a.bl_keys && a.ip_keys && !(abl & 4);  // kernel-uniform
+    const bool tabs = a.bl_keys && a.ip_keys;  // kernel-uniform
     const bool bl_lane = tabs && ql < 3 && key != 0;
     const bool ip_lane = tabs && ql == 3 && key != 0;
     const uint64_t* pkeys = ql < 3 ? a.bl_keys : a.ip_keys;
     const uint32_t* pvals = ql < 3 ? a.bl_exp : a.ip_flags;
     const uint32_t pmask = (uint32_t)(ql < 3 ? c8.y : c8.w);
     uint32_t pi = (bl_lane || ip_lane) ? ((uint32_t)key & pmask) : 0u;
-    uint64_t pk = 0;
-    uint32_t pv = 0;
-    if (tabs) {
-      pk = pkeys[pi];
-      pv = pvals[pi];
+    // without tables the probe reads the request row instead (a valid address; masked below)
+    const uint64_t* pk0 = tabs ? pkeys + pi : reinterpret_cast<const uint64_t*>(a.req);
+    const uint32_t* pv0 = tabs ? pvals + pi : reinterpret_cast<const uint32_t*>(a.req);
+    uint64_t pk = *pk0;
+    uint32_t pv = *pv0;
+    if (!tabs) pk = pv = 0;
+    const int rs = a.ring_size;  // multiple of 64: lane ql holds entries 4 (ql + 16 i) .. +3
+    const int n4 = rs / 4;
+    const uint4* ts4 = reinterpret_cast<const uint4*>(a.ring_ts + (size_t)sc * rs);
+    uint4 tsv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tsv[i] = ts4[min(ql + 16 * i, n4 - 1)];
+    const uint32_t* hreg = reinterpret_cast<const uint32_t*>(a.hll + (size_t)sc * 512);
+    uint32_t wd[4], wi[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      wd[i] = hreg[ql + 16 * i];
+      wi[i] = hreg[64 + ql + 16 * i];
+    }
+    AcctRT rt = load_rt(a.rt + sc);
+    AcctBatch bt = a.batch[sc];
+    const float* e = a.ext + (size_t)sc * ext_w;
+    float extv[7];  // ext widths up to 112 preloaded; wider rows finish in a loop at the end
+#pragma unroll
+    for (int u = 0; u < 7; ++u) extv[u] = e[max(0, min(ql + 16 * u, ext_w - 1))];
+    // dedup probe (without a dedup region: the batch header, masked below)
+    uint32_t dh = 0;
+    const int32_t *pkey, *pfirst, *pcount, *phour;
+    if (a.dbuf) {  // kernel-uniform
+      const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
+      dh = mix32((uint32_t)sc) & (uint32_t)(t.cap - 1);
+      pkey = t.keys + dh;
+      pfirst = t.first + dh;
+      pcount = t.count + dh;
+      phour = t.ctr + 1;
+    } else {
+      pkey = pfirst = pcount = phour = reinterpret_cast<const int32_t*>(a.hdr);
+    }
+    int dkey = *pkey, dfirst = *pfirst;
+    dcount = *pcount;
+    uint32_t hour_word = (uint32_t)*phour;
+    if (!a.dbuf) {
+      dkey = dfirst = -1;
+      dcount = 0;
+      hour_word = 0;
     }
     K1_MARK(7);
     // ---- mask what a missing account / short ring must not see
@@ -458,7 +461,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       // third dependent level in exchange for ~half the HBM traffic of the gather (same-box
       // A/B, cfg3 bench: 109.6 vs 106.1 M scores/s for the full-ring load)
       const int64_t* amp = a.ring_amt + (size_t)s * rs;
-      const bool want_amt = !cfg.sum_compat && !(abl & 8);
+      const bool want_amt = !cfg.sum_compat;
       long long av[16];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -490,7 +493,6 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       c60 = qsum(c60);
       s60 = qsum(s60);
       // ---- K8: HyperLogLog counts (p = 8; 16 registers per lane)
-      if (!(abl & 1)) {
       double zd = 0, zi = 0;
       int vd = 0, vi = 0;
 #pragma unroll
@@ -512,7 +514,6 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       const int ci = (ei <= 2.5 * m && vi > 0) ? li : (int)floor(ei + 0.5);
       hll_dev = now < (int64_t)rt.hll_dev_exp ? cd : 0;
       hll_ip = now < (int64_t)rt.hll_ip_exp ? ci : 0;
-      }
     }
 
     // ---- assemble raw features (quarter-uniform values)
@@ -623,8 +624,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int wst = 30 + min(ext_w, 112);
-    if (abl & 128) {
-    } else if (((wst | (int)a.x_stride) & 3) == 0) {
+    if (((wst | (int)a.x_stride) & 3) == 0) {
       for (int c = ql; c < (wst >> 2); c += K1_QL)
         reinterpret_cast<float4*>(xr)[c] = reinterpret_cast<const float4*>(sx)[c];
     } else {
@@ -632,13 +632,13 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     }
     for (int j = ql + 112; j < ext_w; j += K1_QL) xr[30 + j] = has ? a.ext[(size_t)s * ext_w + j] : 0.f;
     K1_MARK(3);
-    if (!(abl & 128)) reinterpret_cast<uint2*>(a.feat + row)[ql] = s_fst[threadIdx.x >> 4][ql];
-    if (a.fenc && !(abl & 128))
+    reinterpret_cast<uint2*>(a.feat + row)[ql] = s_fst[threadIdx.x >> 4][ql];
+    if (a.fenc)
       write_fenc(a, row, ql, (rq.tx_type & FV_ENC_BIT) != 0, reinterpret_cast<const uint32_t*>(s_fst[threadIdx.x >> 4]),
                  s_enc[threadIdx.x >> 4]);
 
     // ---- score-then-update (engine.go:486-488)
-    if (a.dbuf && has && !(abl & 2)) {
+    if (a.dbuf && has) {
       const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(seq));
       h = (int)dh;
       if (dkey != s) {  // probe collision: walk the chain
@@ -770,7 +770,7 @@ __global__ void __launch_bounds__(64) dedup_insert_list_kernel(UpdateArgs a) {
     const int m = atomicAdd(&t.ctr[0], 1);
     if (2 * m + 1 < t.nmax) *reinterpret_cast<int2*>(t.mlist + 2 * m) = make_int2(h, r.x);
   }
-  if (pos == DEDUP_LIST) {  // ... and its (DEDUP_LIST + 1)-th as a hot account (update_hot_kernel)
+  if (pos == DEDUP_LIST) {  // ... and its (DEDUP_LIST + 1)-th as a hot account (update_segments_kernel)
     const int m = atomicAdd(&t.ctr[2], 1);
     if (m < t.hot_cap) *reinterpret_cast<int2*>(t.hot + 2 * m) = make_int2(h, r.x);
   }
@@ -1005,7 +1005,7 @@ __device__ void apply_scan_chunks(const UpdateArgs& a, const DedupTab& t, int s,
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   g[lane] = lr[lane];
   g[64 + lane] = lr[64 + lane];
-  if (lane == 0) a.rt[s] = r;
+  if (lane == 0) store_rt(a.rt + s, r);
 }
 
 // the c (>= 2) events of account s (dedup hash slot h) in row order, by one wave holding the
@@ -1025,7 +1025,7 @@ __device__ void apply_segment_wave(const UpdateArgs& a, const DedupTab& t, int h
   for (int y = 0; y < c; ++y) rank += __builtin_amdgcn_readlane(key, y) < key;  // lanes >= c: sentinels
   const int j = __builtin_amdgcn_ds_permute(rank * 4, key);
   apply_chunk<false>(a, s, r, j, c, lane, a.hll + (size_t)s * 512);
-  if (lane == 0) a.rt[s] = r;
+  if (lane == 0) store_rt(a.rt + s, r);
 }
 
 // standalone ingestion: one wave per multi-event account listed by update_single
@@ -1051,9 +1051,9 @@ __device__ __forceinline__ void update_multi_body(const UpdateArgs& a, int w0, i
     const int h = hs.x, s = hs.y;
     if (h < 0 || h >= t.cap || s < 0) continue;
     const int c = t.count[h];
-    const AcctRT r = a.rt[s];
+    const AcctRT r = load_rt(a.rt + s);
     if (c < 2) continue;
-    if (c > DEDUP_LIST && a.region < 0) continue;  // scorer path: update_hot_kernel applies it
+    if (c > DEDUP_LIST && a.region < 0) continue;  // scorer path: the hot workgroups of update_segments_kernel apply it
     apply_segment_wave(a, t, h, c, s, r, lane, s_regs[(threadIdx.x >> 6) & (WPB - 1)]);
   }
   // scorer ring: clear the region of batch seq + DEDUP_AHEAD (= seq-1's, consumed by now) for
@@ -1134,7 +1134,7 @@ __device__ __forceinline__ void update_hot_body(const UpdateArgs& a, int hb, int
     if (ctot <= DEDUP_LIST) continue;
     const int Tn = min(T, ctot);
     const int Nb = ctot - Tn;  // bulk events
-    AcctRT r = a.rt[s];
+    AcctRT r = load_rt(a.rt + s);
     uint32_t* const g = reinterpret_cast<uint32_t*>(a.hll + (size_t)s * 512);
     if (tid < 128) s_regs[tid] = g[tid];
     if (tid < 512) s_pre[tid] = 0u;
@@ -1230,15 +1230,10 @@ __device__ __forceinline__ void update_hot_body(const UpdateArgs& a, int hb, int
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       g[lane] = s_regs[lane];
       g[64 + lane] = s_regs[64 + lane];
-      if (lane == 0) a.rt[s] = r;
+      if (lane == 0) store_rt(a.rt + s, r);
     }
     __syncthreads();  // the LDS is the next hot account's
   }
-}
-
-__global__ void __launch_bounds__(HOT_THREADS) update_hot_kernel(UpdateArgs a) {
-  __shared__ HotLds L;
-  update_hot_body(a, blockIdx.x, gridDim.x, L);
 }
 
 // The scorer path's whole post-K1 update in one launch (the hot and the other multi-event
@@ -1279,15 +1274,10 @@ void launch_update_segments(const UpdateArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
   // scorer path: the hot accounts (> DEDUP_LIST events) one workgroup each, then one wave per
   // other multi-event account, 256 waves looping over the region's list
-  static const int fused = [] {
-    const char* e = std::getenv("IGP_UPD_FUSED");
-    return e ? std::atoi(e) : 1;
-  }();
-  if (a.region < 0 && fused) {
+  if (a.region < 0) {
     IGP_LAUNCH(update_segments_kernel, dim3(UPD_SEG_MULTI + HOT_BLOCKS), dim3(HOT_THREADS), 0, st, a);
     return;
   }
-  if (a.region < 0) IGP_LAUNCH(update_hot_kernel, dim3(HOT_BLOCKS), dim3(HOT_THREADS), 0, st, a);
   IGP_LAUNCH(update_multi_kernel, dim3(UPD_MULTI_BLOCKS), dim3(256), 0, st, a);
 }
 

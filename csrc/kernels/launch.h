@@ -74,7 +74,6 @@ struct AssembleArgs {
   int32_t ring_size;
   int32_t n_rows;           // rows covered by the launch (graph bucket)
   int64_t* trace;           // [8 waves][8] phase timestamps (nullable; tools/kbench.py --trace)
-  int32_t ablate;           // attribution experiments only (tools/kbench.py KB_ABLATE): skip bits, 0 in production
   // score-then-update (dbuf != null): the batch's dedup insert ran before K1 (dedup_insert);
   // each wave applies its request's event when it is the account's only one in the batch
   // and opens the segment of a multi-event account (applied by update_segments after K1)

@@ -34,6 +34,40 @@ __host__ __device__ inline size_t dedup_region_size(int cap, int n_max) {
           15) & ~size_t(15);
 }
 
+// AcctRT record without its three pad words: a kernel-local copy that carries them (64-byte load,
+// 64-byte store back) left them in a 12-byte alloca that the compiler promoted to LDS, indexed by
+// the flat work-item id - one scalar read of the dispatch packet (host memory, behind every wave's
+// other scalar loads) per wave in K1 and the update kernels.
+__device__ __forceinline__ AcctRT load_rt(const AcctRT* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  const uint4 a = q[0], b = q[1], c = q[2];
+  const int32_t d = reinterpret_cast<const int32_t*>(p)[12];
+  AcctRT r;
+  r.hll_dev_exp = a.x;
+  r.hll_ip_exp = a.y;
+  r.last_tx = a.z;
+  r.last_tx_exp = a.w;
+  r.session_start = b.x;
+  r.session_exp = b.y;
+  r.sum_exp = b.z;
+  r.last_event_ts = b.w;
+  r.sum_compat = (int64_t)(((uint64_t)c.y << 32) | c.x);
+  r.ring_head = (int32_t)c.z;
+  r.ev_head = (int32_t)c.w;
+  r.ev_count = d;
+  r.pad0 = r.pad1 = r.pad2 = 0;
+  return r;
+}
+
+__device__ __forceinline__ void store_rt(AcctRT* p, const AcctRT& r) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4(r.hll_dev_exp, r.hll_ip_exp, r.last_tx, r.last_tx_exp);
+  q[1] = make_uint4(r.session_start, r.session_exp, r.sum_exp, r.last_event_ts);
+  q[2] = make_uint4((uint32_t)(uint64_t)r.sum_compat, (uint32_t)((uint64_t)r.sum_compat >> 32), (uint32_t)r.ring_head,
+                    (uint32_t)r.ev_head);
+  reinterpret_cast<int32_t*>(p)[12] = r.ev_count;
+}
+
 __device__ __forceinline__ DedupTab dedup_region(int32_t* buf, int cap, int n_max, int region) {
   int32_t* b = buf + dedup_region_size(cap, n_max) * region;
   DedupTab t;
@@ -210,9 +244,9 @@ __device__ __forceinline__ void update_event(const UpdateArgs& a, const DedupTab
   if (h < 0) return;
   const int c = t.count[h];
   if (c == 1) {
-    AcctRT r = a.rt[s];
+    AcctRT r = load_rt(a.rt + s);
     apply_event(a, i, r);
-    a.rt[s] = r;
+    store_rt(a.rt + s, r);
   } else {
     note_multi_event(t, h, s, i, t.first[h] == i);
   }

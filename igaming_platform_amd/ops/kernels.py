@@ -117,8 +117,7 @@ def _host_or_dev(t: Optional[torch.Tensor], name: str, min_numel: int, device, d
 # --------------------------------------------------------------------------- K1
 def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch.Tensor,
                      X: torch.Tensor, feat: torch.Tensor, n_rows: int, dedup: bool = False,
-                     trace: Optional[torch.Tensor] = None, fenc: Optional[torch.Tensor] = None,
-                     ablate: int = 0) -> None:
+                     trace: Optional[torch.Tensor] = None, fenc: Optional[torch.Tensor] = None) -> None:
     """K1. ``dedup=True``: score-then-update. :func:`dedup_insert` must have registered the
     batch first; K1 then applies each single-event account's event and opens the segments
     that :func:`update_segments` applies afterwards (dedup ring region by batch seq).
@@ -147,7 +146,6 @@ def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch
         x_stride=int(X.shape[1]), ring_size=int(store.ring_ts.shape[1]), n_rows=int(n_rows),
         # every wave's 16 trace words (features.hip): 4 waves per 16 rows
         trace=_opt(trace, "trace", dtype=torch.int64, min_numel=((int(n_rows) + 15) // 16) * 64, device=dev),
-        ablate=int(ablate),
     )
     if dedup:
         d["upd"] = update_args(store, cfg_dev, req, n_rows, hdr=hdr, region=-1)

@@ -109,11 +109,11 @@ def main():
             print("   wave", w * 293, [round((x - t0) / 100.0, 2) if x > 0 else None for x in t[w]])
     # K1 with the update on rotating pool batches (the bench's access pattern): event timing
     # of the kernel alone + phase trace of the last one
-    # KB_ABLATE: comma-separated K1 skip masks (features.hip AssembleArgs.ablate; 512 = also store
-    # the D2H feature images into pinned host memory, as the serving path does)
+    # KB_VARIANTS: comma-separated masks (512 = also store the D2H feature images into pinned host
+    # memory, as the serving path does; 1024 = a second launch right behind the first)
     fenc_host = torch.zeros((B, 32), dtype=torch.int32).pin_memory()
     modes = [(v, 0) for v in os.environ.get("KB_K1_MODES", "full").split(",") if v not in ("", "-")]
-    modes += [("full", int(m)) for m in os.environ.get("KB_ABLATE", "").split(",") if m]
+    modes += [("full", int(m)) for m in os.environ.get("KB_VARIANTS", "").split(",") if m]
     for var, abl in modes:  # full | nodedup | noseg
       ts_k1 = []
       for i in range(24):
@@ -132,10 +132,10 @@ def main():
           stall()
           e0.record()
           K.feature_assemble(sc.store, sc.hdr, sc.cfg_dev, sc.req, sc.X, sc.feat, B, dedup=var != "nodedup", trace=trw,
-                             fenc=fenc_host if abl & 512 else None, ablate=abl & 511)
+                             fenc=fenc_host if abl & 512 else None)
           if abl & 1024:  # the same launch again right behind it (instruction caches warm): 2 launches timed
               K.feature_assemble(sc.store, sc.hdr, sc.cfg_dev, sc.req, sc.X, sc.feat, B, dedup=False,
-                                 fenc=fenc_host if abl & 512 else None, ablate=(abl & 511) | 2)
+                                 fenc=fenc_host if abl & 512 else None)
           e1.record()
           e1.synchronize()
           ts_k1.append(e0.elapsed_time(e1) * 1e3)
@@ -144,7 +144,7 @@ def main():
       full = trw.cpu().numpy().reshape(-1, 16)
       if os.environ.get("KB_TRACE_OUT"):
           np.save(os.environ["KB_TRACE_OUT"] + f"_a{abl}.npy", full)
-      print(f"[{var} ablate={abl}] K1+update on rotating pool batches: median {np.median(ts_k1[8:]):.1f} us "
+      print(f"[{var} variant={abl}] K1+update on rotating pool batches: median {np.median(ts_k1[8:]):.1f} us "
             f"(first pass {np.median(ts_k1[:8]):.1f})")
       t = full[[w * 293 for w in range(7)]][:, [0, 1, 6, 7, 2, 3, 4, 5]].astype(np.float64)
       t0 = t[t > 0].min()
