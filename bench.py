@@ -66,8 +66,9 @@ def parse():
                          "the owner-routed RCCL exchange (the serving path, engine/dp.py) moves each row to "
                          "its owner and the results back; replicas = N independent single-GPU pipelines")
     ap.add_argument("--scope", default="auto", choices=["auto", "serving", "engine_only", "e2e", "grpc"],
-                    help="auto (default): serving for the fraud configs, engine_only for cfg4 / cfg5 (LTV and "
-                         "abuse models are not ScoreBatch traffic); serving: the serving objects of every rank - "
+                    help="auto (default): serving; for cfg4 / cfg5 that is PredictLTV / CheckBonusAbuse bytes "
+                         "through every rank's native account router, owner-routed (acct_dp_bench); serving for "
+                         "the fraud configs: the serving objects of every rank - "
                          "risk.v1 ScoreBatch request bytes (UUID account ids) -> the rank's native serving core "
                          "(C++ parse, node-shared AccountIndex, "
                          "owner-routed RCCL exchange steps for N > 1, GPU pipeline) -> response bytes with the "
@@ -82,9 +83,14 @@ def parse():
                     "(default: the config's micro-batch)")
     ap.add_argument("--rpc", default="batch", choices=["batch", "tx"], help="--scope grpc: ScoreBatch or unary "
                     "ScoreTransaction through the micro-batcher")
-    ap.add_argument("--rates", default="25000,50000,100000,150000,200000,300000",
-                    help="--scope serving with cfg4 / cfg5: offered PredictLTV / CheckBonusAbuse calls/s per level "
-                         "(open loop over the native gRPC server)")
+    ap.add_argument("--rates", default="",
+                    help="--scope serving with cfg4 / cfg5, 1 GPU: offered PredictLTV / CheckBonusAbuse calls/s per "
+                         "level, open loop over the native gRPC server (e.g. 25000,50000,100000,200000); without it "
+                         "the owner-routed DP bench (every rank's account router, closed loop)")
+    ap.add_argument("--calls", type=int, default=65536, help="cfg4 / cfg5 serving: calls per rank per step")
+    ap.add_argument("--inflight", type=int, default=16384, help="cfg4 / cfg5 serving: outstanding calls per rank")
+    ap.add_argument("--check-out", default="", help="cfg4 / cfg5 serving: after the timed run every rank answers "
+                    "the same fixed calls and writes them to <check-out>.<rank>.json (tests/test_bench_acct.py)")
     ap.add_argument("--seconds", type=float, default=5.0, help="cfg4 / cfg5 serving: seconds per offered-load level")
     ap.add_argument("--zipf", type=float, default=0.0, help="serving: Zipf exponent of the account ids (0: uniform)")
     ap.add_argument("--payloads", type=int, default=128, help="serving: distinct ScoreBatch requests per rank "
@@ -93,8 +99,8 @@ def parse():
     a = ap.parse_args()
     if a.numerics == "auto":  # the ONNX models' f32 contract everywhere (cfg4 / cfg5: split MFMA)
         a.numerics = "fp32"
-    if a.scope == "auto":
-        a.scope = "engine_only" if a.config in ("cfg4", "cfg5") else "serving"
+    if a.scope == "auto":  # cfg4 / cfg5: the account-RPC serving path, owner-routed over every rank
+        a.scope = "serving"
     return a
 
 
@@ -120,25 +126,202 @@ def maybe_launch_torchrun(a) -> None:
 
 
 def acct_serving_bench(a) -> None:
-    """cfg4 / cfg5 through the serving path, 1 GPU: unary PredictLTV / CheckBonusAbuse calls over
-    the native HTTP/2 server (bytes in -> the native account router -> micro-batches on the LTV
-    chain / abuse step -> response bytes) from the native open-loop load generator, stepped
-    through --rates; the value is the highest offered rate answered in full with p99 < 50 ms
-    (tools/bench_e2e.py _native_open_loop)."""
+    """cfg4 / cfg5 offered-load curve, 1 GPU (--rates): unary PredictLTV / CheckBonusAbuse calls
+    over the native HTTP/2 server (bytes in -> the native account router -> micro-batches on the
+    LTV chain / abuse step -> response bytes) from the native open-loop load generator; the value
+    is the highest offered rate answered in full with p99 < 50 ms (tools/bench_e2e.py
+    _native_open_loop)."""
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
     import bench_e2e
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or a.gpus > 1:
-        raise SystemExit("cfg4 / cfg5 --scope serving runs on 1 GPU (multi-GPU: --scope engine_only)")
     argv = ["--scope", "grpc", "--rpc", "ltv" if a.config == "cfg4" else "abuse", "--open-loop", "--accounts",
             str(a.accounts), "--rates", a.rates, "--seconds", str(a.seconds), "--numerics", a.numerics,
             "--zipf", str(a.zipf)] + (["--json-out", a.json_out] if a.json_out else [])
     return bench_e2e.main(argv)
 
 
+NOW_ACCT = 1_760_000_000  # the account benches' clock (fixed: answers comparable across runs)
+
+
+def acct_models(numerics: str, small: bool = False):
+    """The cfg4 LTV MLP 4x512 over 256 features and the cfg5 abuse GRU 2x256 over the last 100
+    events (random-init, deterministic), as ONNX bytes; the config they run under. ``small``:
+    narrow models of the same structure (CPU protocol rehearsals only, never a benchmark)."""
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.onnx import builders
+    cfg = Config()
+    cfg.gpu.buckets = [64, 512, 4096]
+    cfg.gpu.max_batch = 4096
+    cfg.gpu.spmd_heartbeat_s = 0.0
+    cfg.ltv_model.precision = cfg.abuse_model.precision = numerics
+    w, h = (32, 16) if small else (512, 256)
+    lm = builders.build("ltv_mlp", n_features=256, width=w, layers=4).SerializeToString()
+    am = builders.build("gru", seq=100, in_dim=16, hidden=h).SerializeToString()
+    return cfg, lm, am
+
+
+def acct_dp_bench(a) -> None:
+    """cfg4 / cfg5 through the account-RPC serving path on every rank (BASELINE
+    config 5 "DP=8 over xGMI"): each rank runs its shard (its accounts' profile rows and HBM
+    event rings) and its native ``AcctRouter``; every rank ingests PredictLTV / CheckBonusAbuse
+    request bytes for account ids spread over ALL owners, and the router sends each call to the
+    owner's model device over the node-shared /dev/shm mailbox (the owner micro-batches the
+    calls of every sender into its LTV chain / abuse GRU step and mails the answer bytes back).
+    No replicas, no all-gather: each call is computed once, on the GPU that holds its account.
+
+    A step = ``--calls`` calls per rank, driven in-process closed-loop (``AcctRouter.drive``:
+    at most ``--inflight`` outstanding, bytes in -> answer bytes out, no Python per call); the
+    value is the whole job's answered calls per second, the latency per call submit -> answer.
+    IGP_BENCH_BACKEND=cpu: the same objects on CPU shards (tests/test_bench_acct.py)."""
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+    import bench_e2e
+    from igaming_platform_amd.layouts import ACCTBATCH
+    from igaming_platform_amd.native import native
+    from igaming_platform_amd.utils import benchkit
+    from igaming_platform_amd.utils.hashing import SEED_ACCOUNT
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    kind = os.environ.get("IGP_BENCH_BACKEND", "gpu")
+    if kind == "gpu":
+        torch.cuda.set_device(local)
+    comm = None
+    if world > 1:
+        dist.init_process_group("gloo")
+        from igaming_platform_amd.parallel.comm import TorchComm
+        comm = TorchComm("gloo")
+    rpc_name = "ltv" if a.config == "cfg4" else "abuse"
+    rpc = native().RPC_LTV if rpc_name == "ltv" else native().RPC_ABUSE
+    small = os.environ.get("IGP_BENCH_SMALL_MODELS") == "1"  # CPU rehearsal (tests/test_bench_acct.py)
+    if small and kind == "gpu":
+        raise SystemExit("IGP_BENCH_SMALL_MODELS is for the CPU rehearsal only")
+    cfg, lm, am = acct_models(a.numerics, small)
+    n_acc = a.accounts
+    if world == 1:
+        from igaming_platform_amd.engine.risk_engine import RiskEngine
+        eng = RiskEngine(cfg, backend=kind, capacity=n_acc + 1024, ltv_model=lm, abuse_model=am)
+        acct, registry, ltv, backend = eng.acct, eng.registry, eng.ltv, eng.backends[0]
+    else:
+        from igaming_platform_amd.engine.risk_engine import worker_acct, worker_node
+        node = worker_node(cfg, comm, kind, n_acc + 1024)
+        ltv, acct = worker_acct(cfg, node, lm, am)
+        registry, backend = node.registry, node.local
+    if acct is None or not acct.serves(rpc):
+        raise RuntimeError("no native account router for this RPC")
+    router = acct.router
+    # this rank's accounts: the global population is world x n_acc UUIDs, owner = XXH64(id) % world
+    # (an account's profile depends on its index only, not on the world size or its owner)
+    total = n_acc * world
+    step = 1 << 16
+    for s0 in range(0, total, step):
+        ids = [bench_e2e.account_id(i) for i in range(s0, min(total, s0 + step))]
+        h = native().id_hashes(ids, SEED_ACCOUNT)
+        mine = np.nonzero((h % np.uint64(world)).astype(np.int64) == rank)[0]
+        if not len(mine):
+            continue
+        rng = np.random.default_rng(1000 + s0)
+        rows = np.floor(rng.uniform(0, 1, (len(ids), 25)) * bench_e2e.PROFILE_SCALE).astype(np.float32)
+        ext = rng.normal(0, 1, (len(ids), 231)).astype(np.float32)
+        slots, owners = registry.resolve_ids([ids[i] for i in mine], insert=True)
+        ltv.set_rows(slots, owners, rows[mine], ext[mine])
+        # warehouse rows (the abuse rules' bonus / wager / deposit inputs)
+        g = (s0 + mine).astype(np.int64)
+        wb = np.zeros(len(mine), ACCTBATCH)
+        wb["present"] = 1
+        wb["total_deposits"] = (g % 97) * 700
+        wb["total_bets"] = (g % 89) * 1300
+        wb["bonus_claim_count"] = g % 6
+        wb["bonus_wager_complete"] = (g % 5) / 5.0
+        wb["account_created_at"] = NOW_ACCT - (g % 40) * 86400
+        backend.set_batch_rows(slots, wb)
+    if kind == "gpu":  # full 100-event histories in the shard's HBM event rings
+        bench_e2e.fill_event_rings(backend.store, seed=77 + rank)
+    if comm is not None:
+        comm.barrier()
+    payloads = bench_e2e.acct_payloads(total, rpc_name, 1 << 16, 300 + rank, a.zipf)
+    per_step = a.calls
+    now = NOW_ACCT
+    router.drive(rpc, payloads, max(a.warmup, 1) * per_step, a.inflight, now)  # warm: graphs, caches
+    if comm is not None:
+        comm.barrier()
+    t0 = time.perf_counter()
+    r = router.drive(rpc, payloads, a.steps * per_step, a.inflight, now)
+    if comm is not None:
+        comm.barrier()
+    elapsed = time.perf_counter() - t0
+    lat = np.asarray(r["latency_ns"], np.float64)
+    ok = lat[lat >= 0] / 1e6
+    p99 = float(np.percentile(ok, 99)) if len(ok) else float("nan")
+    p50 = float(np.percentile(ok, 50)) if len(ok) else float("nan")
+    errors, cold = int(r["errors"]), int(r["cold"])
+    st = router.stats(3 if rpc_name == "abuse" else 1)
+    if comm is not None:  # the slowest rank's clock and latencies, every rank's errors
+        mx = torch.tensor([elapsed, p99, p50], dtype=torch.float64)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        elapsed, p99, p50 = (float(x) for x in mx)
+        ec = torch.tensor([errors, cold, int(router.remote_out)], dtype=torch.int64)
+        dist.all_reduce(ec)
+        errors, cold, remote = (int(x) for x in ec)
+    else:
+        remote = int(router.remote_out)
+    c = benchkit.MODEL_CONFIGS[a.config]
+    out = {
+        "metric": c["metric"], "value": world * a.steps * per_step / elapsed, "unit": c["unit"], "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": a.numerics,
+        "data": "synthetic (UUID account ids, random-init weights, random 100-event histories)",
+        "config": {"model": c["desc"], "global_batch": per_step * world, "seq_len": 100 if a.config == "cfg5" else 1,
+                   "parallelism": f"dp{world} (owner-routed: each call computed once, on its account's GPU)",
+                   "calls_per_step_per_rank": per_step, "inflight_per_rank": a.inflight,
+                   "device_micro_batch_max": max(cfg.gpu.buckets), "accounts_per_gpu": n_acc,
+                   "account_spread": f"zipf({a.zipf})" if a.zipf > 1 else "uniform",
+                   "numerics": numerics_desc(a), "backend": kind,
+                   **({"models": "SMALL rehearsal models (not the cfg4 / cfg5 sizes)"} if small else {})},
+        "scope": "serving (risk.v1 request bytes in -> answer bytes out through every rank's native account "
+                 "router and the /dev/shm owner mailbox, in-process closed loop)",
+        "p99_latency_ms": p99, "p50_latency_ms": p50, "latency_what": "per call, submit -> answer bytes",
+        "errors": errors, "cold_path_calls": cold, "remote_calls_rank_sum": remote,
+        "device_steps_rank0": int(st.get("steps", 0)), "rows_per_device_step_rank0":
+            round(st.get("items", 0) / max(int(st.get("steps", 1)), 1), 1),
+    }
+    if errors:
+        raise RuntimeError(f"{errors} calls failed ({cold} cold-path replies)")
+    if a.check_out:  # every rank asks the same calls (accounts 0..47 + an unknown id) and dumps the answers
+        check = [bench_e2e.acct_request(rpc_name, bench_e2e.account_id(i)) for i in range(min(total, 48))]
+        check.append(bench_e2e.acct_request(rpc_name, "nobody"))
+        for i, b in enumerate(check):
+            router.submit(rpc, b, i, 0, now)
+        got, t_end = {}, time.time() + 60
+        while len(got) < len(check) and time.time() < t_end:
+            for tag, b, e in router.poll(4096, 50000):
+                got[int(tag)] = b.hex() if e is None else "error: " + e
+        with open(f"{a.check_out}.{rank}.json", "w") as f:
+            json.dump({"rank": rank, "world": world, "answers": [got.get(i) for i in range(len(check))]}, f)
+        if comm is not None:
+            comm.barrier()
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        router.stop()
+        dist.destroy_process_group()
+    else:
+        eng.close()
+
+
 def main():
     a = parse()
     if a.scope == "serving" and a.config in ("cfg4", "cfg5"):
-        return acct_serving_bench(a)
+        if a.rates:  # the 1-GPU offered-load curve over HTTP/2
+            return acct_serving_bench(a)
+        maybe_launch_torchrun(a)
+        return acct_dp_bench(a)
     if a.scope == "serving":
         maybe_launch_torchrun(a)
         return serving_bench(a)

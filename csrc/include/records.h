@@ -170,5 +170,6 @@ struct BatchHdr {
   int32_t seq;    // batch sequence number (dedup-table ping-pong parity)
   int64_t now;
 };
+static_assert(sizeof(BatchHdr) == 16, "BatchHdr must be 16 bytes (dedup_insert_list_kernel reads it as one int4)");
 
 }  // namespace igp

@@ -66,6 +66,8 @@ UpdateArgs update_args(const py::dict& d) {
   a.dcap = geti(d, "dcap");
   a.dmax = geti(d, "dmax");
   a.region = geti(d, "region", DEDUP_STANDALONE);
+  a.src = ptr<const char*>(d, "src");
+  if (a.src && (a.region >= 0 || !a.hdr)) throw std::runtime_error("update args: slab source needs the scorer ring");
   if (!a.dbuf || !a.cfg || !a.req || !a.rt) throw std::runtime_error("update args: missing pointers");
   if (a.n_max > a.dmax || a.dcap < 2 * a.dmax) throw std::runtime_error("update args: dedup scratch too small");
   if (a.ev && a.ev_dim != 16) throw std::runtime_error("update args: event dim must be 16");

@@ -713,6 +713,9 @@ __global__ void dedup_insert_kernel(UpdateArgs a) {
 // row's add returned) and the list of multi-event accounts (added by the account's second
 // row). One thread per row, 64-thread workgroups spread over the chip: the kernel is a chain
 // of memory-side atomics (CAS, add, add), not work.
+// With a.src (the scorer's copy stage) the batch comes straight from the pinned host slab: each
+// thread reads its row through the fabric and writes the device copy K1 and the update read, the
+// first thread the header - no H2D copy (an SDMA job and a launch per batch) ahead of it.
 __global__ void __launch_bounds__(64) dedup_insert_list_kernel(UpdateArgs a) {
   // the wave's rows grouped by account first (a 128-entry LDS table): one global probe and one
   // count add per account and wave, not per row - under Zipf traffic the top account's rows
@@ -720,14 +723,34 @@ __global__ void __launch_bounds__(64) dedup_insert_list_kernel(UpdateArgs a) {
   __shared__ int s_key[128], s_cnt[128], s_min[128], s_base[128], s_h[128];
   const int lane = threadIdx.x;
   const int i = blockIdx.x * 64 + lane;
-  const DedupTab t = upd_region(a);
+  // the batch header {n, seq, now}: from the host slab (every lane the same 16 bytes: one
+  // request per wave) or the device copy
+  const int4 hv = *reinterpret_cast<const int4*>(a.src ? reinterpret_cast<const void*>(a.src)
+                                                       : reinterpret_cast<const void*>(a.hdr));
+  const int n = min(hv.x, a.n_max);  // as upd_n: the header's live count
+  const int64_t now = (int64_t)(((uint64_t)(uint32_t)hv.w << 32) | (uint32_t)hv.z);
+  const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(hv.y));
+  const bool live = i < n;
+  int2 r = make_int2(-1, 0);  // {slot, tx_type}
+  if (a.src) {
+    if (i == 0) *reinterpret_cast<int4*>(const_cast<BatchHdr*>(a.hdr)) = hv;
+    if (live) {
+      const uint4* sp = reinterpret_cast<const uint4*>(a.src + sizeof(BatchHdr)) + 3 * (size_t)i;
+      uint4* dp = reinterpret_cast<uint4*>(const_cast<ReqRec*>(a.req + i));
+      const uint4 q0 = sp[0], q1 = sp[1], q2 = sp[2];
+      dp[0] = q0;
+      dp[1] = q1;
+      dp[2] = q2;
+      r = make_int2((int)q0.x, (int)q0.y);
+    }
+  } else if (live) {
+    r = *reinterpret_cast<const int2*>(a.req + i);
+  }
   // the batch clock's hour-of-day event-row word (sin/cos in double), once per batch for K1
-  if (i == 0) t.ctr[1] = (int32_t)event_word(4, 0, 0, a.hdr->now, 0, false, false);
+  if (i == 0) t.ctr[1] = (int32_t)event_word(4, 0, 0, now, 0, false, false);
   s_key[lane] = s_key[64 + lane] = -1;
   s_cnt[lane] = s_cnt[64 + lane] = 0;
   s_min[lane] = s_min[64 + lane] = 0x7fffffff;
-  const bool live = i < upd_n(a);
-  const int2 r = live ? *reinterpret_cast<const int2*>(a.req + i) : make_int2(-1, 0);  // {slot, tx_type}
   const ScoreCfg& cfg = *a.cfg;
   const bool mine = r.x >= 0 && !(cfg.owner_filter && ((r.y >> 8) & 0xff) != cfg.my_rank);
   if (live && i < t.nmax) t.rows[i] = mine ? r.x : -1;  // compact account column for hot-account scans

@@ -45,6 +45,9 @@ struct UpdateArgs {
   int32_t dcap;             // power of two >= 2 * dmax
   int32_t dmax;
   int32_t region;           // -1: hdr->seq & 1; else fixed region (2 = standalone)
+  // scorer dedup insert only (nullable): the pinned host slab [BatchHdr | ReqRec x n]; the kernel
+  // reads the batch from it and writes the device copy (hdr, req) for the later stages
+  const char* src;
 };
 
 struct AssembleArgs {

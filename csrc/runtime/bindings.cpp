@@ -1019,6 +1019,58 @@ PYBIND11_MODULE(_native, m) {
         }
         return l;
       }, py::arg("max") = 4096, py::arg("timeout_us") = 1000)
+      // in-process closed-loop load (bench.py --config cfg4|cfg5 --scope serving): `n` calls
+      // cycling over `payloads`, at most `inflight` outstanding, submitted and answered on this
+      // thread without the GIL. Returns per-call latency (submit -> answer, ns) of the answered
+      // calls, the error count, the cold-path count ("cold: " replies) and the elapsed seconds.
+      .def("drive", [](PyAcct& a, int rpc, py::list payloads, int64_t n, int64_t inflight, int64_t now) {
+        const size_t np_ = payloads.size();
+        if (np_ == 0 || n <= 0 || inflight <= 0) throw std::runtime_error("drive: payloads, n and inflight > 0");
+        std::vector<std::string> bufs(np_);
+        for (size_t k = 0; k < np_; ++k) bufs[k] = payloads[k].cast<std::string>();
+        std::vector<int64_t> t_sub(size_t(n), 0);
+        py::array_t<int64_t> lat(n);
+        int64_t* L = lat.mutable_data();
+        int64_t sent = 0, got = 0, errors = 0, cold = 0;
+        double elapsed = 0;
+        {
+          py::gil_scoped_release rel;
+          std::vector<AcctRouter::Done> out;
+          const int64_t t0 = ServeCore::now_ns();
+          while (got < n) {
+            const int64_t room = std::min<int64_t>(n - sent, inflight - (sent - got));
+            if (room > 0) {
+              const int64_t ts = ServeCore::now_ns();
+              for (int64_t k = 0; k < room; ++k, ++sent) {
+                const std::string& b = bufs[size_t(sent) % np_];
+                t_sub[size_t(sent)] = ts;
+                a.router->submit(uint8_t(rpc), b.data(), b.size(), uint64_t(sent), ts, now);
+              }
+            }
+            out.clear();
+            a.router->poll(out, size_t(inflight), 2000);
+            const int64_t tr = ServeCore::now_ns();
+            for (auto& d : out) {
+              const size_t i = size_t(d.tag);
+              if (i >= size_t(n)) continue;
+              if (!d.err.empty()) {
+                ++errors;
+                if (d.err.compare(0, std::strlen(kColdPrefix), kColdPrefix) == 0) ++cold;
+                L[got++] = -1;
+              } else {
+                L[got++] = tr - t_sub[i];
+              }
+            }
+          }
+          elapsed = double(ServeCore::now_ns() - t0) / 1e9;
+        }
+        py::dict r;
+        r["latency_ns"] = lat;
+        r["errors"] = errors;
+        r["cold"] = cold;
+        r["elapsed"] = elapsed;
+        return r;
+      }, py::arg("rpc"), py::arg("payloads"), py::arg("n"), py::arg("inflight") = 8192, py::arg("now") = -1)
       .def("stop", [](PyAcct& a) {
         py::gil_scoped_release rel;
         a.router->stop();

@@ -274,10 +274,11 @@ class GpuScorer:
     # ------------------------------------------------------------------ the step
     def _copy_body(self, slot: int, bucket: int) -> None:
         sb = self.slots[slot]
-        nbytes = HDR_BYTES + REQ_BYTES * bucket
-        K.memcpy_async(sb.dev_slab, self.host_slab[slot], nbytes)
         if self.update_features:
-            K.dedup_insert(self.store, self.cfg_dev, sb.req, bucket, sb.hdr)
+            # the dedup insert reads the batch from the pinned slab and writes the device copy
+            K.dedup_insert(self.store, self.cfg_dev, sb.req, bucket, sb.hdr, src=self.host_slab[slot])
+            return
+        K.memcpy_async(sb.dev_slab, self.host_slab[slot], HDR_BYTES + REQ_BYTES * bucket)
 
     def _state_body(self, slot: int, bucket: int, part: str = "all") -> None:
         """K1 (part "k1"), then the multi-event update that also clears the dedup region of

@@ -183,10 +183,15 @@ def feature_update(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, 
     _mod().feature_update(d, _stream())
 
 
-def dedup_insert(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, hdr: torch.Tensor) -> None:
+def dedup_insert(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, hdr: torch.Tensor,
+                 src: Optional[torch.Tensor] = None) -> None:
     """Scorer head: register the batch's accounts in its dedup region (before K1), with the
-    per-account row lists and the multi-event account list :func:`update_segments` reads."""
+    per-account row lists and the multi-event account list :func:`update_segments` reads.
+    ``src``: the pinned host slab [BatchHdr | ReqRec x n_max] - the kernel reads the batch from
+    it and writes ``hdr`` / ``req`` itself (no H2D copy before it)."""
     d = update_args(store, cfg_dev, req, n_max, hdr=hdr, region=-1)
+    if src is not None:
+        d["src"] = _host_or_dev(src, "src", 16 + 48 * n_max, store.device, torch.uint8)
     d["insert_only"] = 1
     _mod().feature_update(d, _stream())
 

@@ -106,6 +106,28 @@ def tx_payloads(n_accounts: int, n: int, seed: int):
             for a in rng.integers(0, n_accounts, n)]
 
 
+# per-column scale of the synthetic 25-column player profile (uniform in [0, scale))
+PROFILE_SCALE = np.array([900, 90, 60, 500, 10, 120, 1e5, 8e4, 3e4, 500, 8, 5e3, 2e5, 1.8e5, 3000, 1, 80, 60, 20, 15,
+                          1, 1, 1, 1, 8])
+
+
+def fill_event_rings(store, seed: int = 77) -> None:
+    """Full 100-event histories in a GPU shard's HBM event rings (random bf16 events for every
+    slot, ring counts full): the GRU runs its 100 steps over real-looking inputs."""
+    import torch
+    from igaming_platform_amd.layouts import ACCTRT
+    g = torch.Generator(device=store.device)
+    g.manual_seed(seed)
+    cap = store.ev.shape[0]
+    for s0 in range(0, cap, 1 << 16):
+        n = min(1 << 16, cap - s0)
+        ev = torch.randn((n, store.ev.shape[1], store.ev.shape[2]), generator=g, device=store.device)
+        store.ev[s0:s0 + n].copy_(ev.to(torch.bfloat16).view(torch.int16))
+    rt = store.rt.view(-1, store.rt.shape[1])
+    rt[:, ACCTRT.fields["ev_count"][1] // 4] = store.ev.shape[1]
+    torch.cuda.synchronize(store.device)
+
+
 def build_cold_engine(accounts: int, backend: str, precision: str = "fp32"):
     """Engine with the cfg 4 LTV MLP and the cfg 5 abuse GRU loaded, player profiles for every
     account and (GPU) full 100-event histories in the HBM event rings (PredictLTV /
@@ -127,36 +149,29 @@ def build_cold_engine(accounts: int, backend: str, precision: str = "fp32"):
     step = 1 << 18
     for s0 in range(0, accounts, step):
         n = min(step, accounts - s0)
-        rows = np.floor(rng.uniform(0, 1, (n, 25)) * np.array(
-            [900, 90, 60, 500, 10, 120, 1e5, 8e4, 3e4, 500, 8, 5e3, 2e5, 1.8e5, 3000, 1, 80, 60, 20, 15, 1, 1, 1, 1, 8]))
+        rows = np.floor(rng.uniform(0, 1, (n, 25)) * PROFILE_SCALE)
         eng.ltv.set_rows(slots[s0:s0 + n], owners[s0:s0 + n], rows.astype(np.float32),
                          rng.normal(0, 1, (n, 231)).astype(np.float32))
-    if backend == "gpu":  # full histories: the GRU runs its 100 steps over real-looking events
-        import torch
-        from igaming_platform_amd.layouts import ACCTRT
-        store = eng.backends[0].store
-        g = torch.Generator(device=store.device)
-        g.manual_seed(77)
-        for s0 in range(0, accounts, 1 << 16):
-            n = min(1 << 16, accounts - s0)
-            ev = torch.randn((n, store.ev.shape[1], store.ev.shape[2]), generator=g, device=store.device)
-            store.ev[s0:s0 + n].copy_(ev.to(torch.bfloat16).view(torch.int16))
-        rt = store.rt.view(-1, store.rt.shape[1])
-        rt[:accounts, ACCTRT.fields["ev_count"][1] // 4] = store.ev.shape[1]
-        torch.cuda.synchronize(store.device)
+    if backend == "gpu":
+        fill_event_rings(eng.backends[0].store)
     return eng
+
+
+def acct_request(rpc: str, account: str) -> bytes:
+    """One PredictLTV / GetPlayerSegment / CheckBonusAbuse request body."""
+    from igaming_platform_amd.proto import risk_v1 as P
+    m = {"ltv": lambda a: P.PredictLTVRequest(account_id=a),
+         "segment": lambda a: P.GetPlayerSegmentRequest(account_id=a),
+         "abuse": lambda a: P.CheckBonusAbuseRequest(account_id=a, bonus_id="welcome")}[rpc](account)
+    return m.SerializeToString()
 
 
 def acct_payloads(accounts: int, rpc: str, n: int, seed: int, zipf: float = 0.0):
     """Request bodies of PredictLTV / GetPlayerSegment / CheckBonusAbuse over the population:
     uniform account ids, or Zipf-distributed ranks with exponent ``zipf`` (> 1)."""
-    from igaming_platform_amd.proto import risk_v1 as P
     rng = np.random.default_rng(seed)
     acc = (rng.zipf(zipf, n) - 1) % accounts if zipf > 1 else rng.integers(0, accounts, n)
-    mk = {"ltv": lambda a: P.PredictLTVRequest(account_id=a),
-          "segment": lambda a: P.GetPlayerSegmentRequest(account_id=a),
-          "abuse": lambda a: P.CheckBonusAbuseRequest(account_id=a, bonus_id="welcome")}[rpc]
-    return [mk(account_id(int(a))).SerializeToString() for a in acc]
+    return [acct_request(rpc, account_id(int(a))) for a in acc]
 
 
 def run_cold_engine(a) -> dict:
