@@ -464,7 +464,6 @@ PYBIND11_MODULE(_hipk, m) {
     if (a.split) {
       for (int l = 0; l < a.n_layers; ++l)
         if (!a.layer[l].W_lo || !a.layer[l].R_lo) throw std::runtime_error("gru: split mode needs residual weights");
-      a.ws = 0;
     }
     if (a.tile_rows != 0 && a.tile_rows != 16 && a.tile_rows != 32) throw std::runtime_error("gru: tile_rows 16|32");
     if (a.H != 64 && a.H != 128 && a.H != 256) throw std::runtime_error("gru: H must be 64, 128 or 256");

@@ -87,9 +87,8 @@ class PipeDriver {
     // the copy / state / post-state events only order work between this device's queues: no
     // system-scope fence (cache writeback + invalidate at the stage's end, which also slows the
     // kernels running beside it); the model event keeps it (the host reads results from pinned
-    // memory after it). IGP_EVENT_DEVSCOPE=0 restores system scope everywhere.
-    const char* ds = getenv("IGP_EVENT_DEVSCOPE");
-    const unsigned dev_flags = hipEventDisableTiming | ((ds && atoi(ds) == 0) ? 0u : (unsigned)hipEventDisableSystemFence);
+    // memory after it).
+    const unsigned dev_flags = hipEventDisableTiming | (unsigned)hipEventDisableSystemFence;
     hip_ok(hipGetDevice(&device_), "get device");  // the serving core's threads bind to it
     ev_.resize(3 * depth);
     for (size_t i = 0; i < ev_.size(); ++i)

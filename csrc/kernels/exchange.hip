@@ -274,9 +274,6 @@ class XchgDriver {
     done_recorded_.assign(depth, false);
     gen_.assign(size_t(depth), 0);
     slots_.resize(depth);
-    // A/B experiment at world 1 only: device copies instead of the RCCL all-to-alls
-    const char* co = getenv("IGP_XCHG_COPY_ONLY");
-    copy_only_ = co && co[0] == '1' && world == 1;
   }
   ~XchgDriver() {
     for (auto& e : ev_) (void)hipEventDestroy(e);
@@ -511,8 +508,7 @@ class XchgDriver {
     if (done_recorded_[slot]) hip_ok(hipStreamWaitEvent(xs_, e_done, 0), "wait done");
     stage(g.send, g.osend, xs_, "send graph");
     const auto t2 = clk::now();
-    if (copy_only_) hip_ok(hipMemcpyAsync(sl.xrecv, sl.xsend, xbytes, hipMemcpyDeviceToDevice, xs_), "rows D2D");
-    else nccl_ok(r_, r_.all_to_all(sl.xsend, sl.xrecv, xbytes, kUint8, reinterpret_cast<void*>(cx_), xs_), "all_to_all rows");
+    nccl_ok(r_, r_.all_to_all(sl.xsend, sl.xrecv, xbytes, kUint8, reinterpret_cast<void*>(cx_), xs_), "all_to_all rows");
     const auto t3 = clk::now();
     hop(xs_, cs_, e_x, "x -> copy");
     if (hist_.size() == 2) hip_ok(hipStreamWaitEvent(cs_, E(hist_.front(), 3), 0), "wait state-2");
@@ -526,8 +522,7 @@ class XchgDriver {
     stage(with_features ? g.model_f : g.model, with_features ? g.omodel_f : g.omodel, ms_, "model graph");
     hop(ms_, ys_, e_model, "model -> y");
     const auto t4 = clk::now();
-    if (copy_only_) hip_ok(hipMemcpyAsync(sl.rrecv, sl.rsend, rbytes, hipMemcpyDeviceToDevice, ys_), "results D2D");
-    else nccl_ok(r_, r_.all_to_all(sl.rsend, sl.rrecv, rbytes, kUint8, reinterpret_cast<void*>(cy_), ys_), "all_to_all results");
+    nccl_ok(r_, r_.all_to_all(sl.rsend, sl.rrecv, rbytes, kUint8, reinterpret_cast<void*>(cy_), ys_), "all_to_all results");
     const auto t5 = clk::now();
     hip_ok(hipMemcpyAsync(sl.host_rr, sl.rrecv, (size_t)world_ * rbytes, hipMemcpyDeviceToHost, ys_), "results D2H");
     hip_ok(hipEventRecord(e_done, ys_), "record done");
@@ -611,7 +606,6 @@ class XchgDriver {
   std::vector<Slot> slots_;
   std::unordered_map<int64_t, Graphs> graphs_;
   double st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  bool copy_only_ = false;
   bool captured_ = false;
   IgpDeviceOps ops_{};
   int ops_C_ = 0;

@@ -869,7 +869,19 @@ static void launch_gru_h(const GruArgs& a, hipStream_t st) {
 
 void launch_gru(const GruArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
-  if (a.split) {  // f32-faithful: the batch-parallel split kernel, 16 rows per workgroup
+  static int n_cu = [] {
+    int dev = 0, v = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    return v > 0 ? v : 256;
+  }();
+  if (a.split) {
+    // small micro-batches: the weight-stationary split clusters (16 workgroups per 32 rows, a
+    // whole CU each), while a launch takes at most half the chip (the serving abuse device runs
+    // them on one stream, so the scorer's kernels keep the other half and every cluster becomes
+    // resident; its bounded waits only guard against what cannot); larger ones: the
+    // batch-parallel split kernel
+    if (a.ws && gru_wsx_eligible(a) && gru_wsx_clusters(a.n_rows) * 16 <= n_cu / 2) return launch_gru_wsx(a, st);
     const int ksx = a.layer[0].kx_pad / 32;
     switch (a.H) {
       case 64: if (ksx == 1) launch_gru_x3<1, 2>(a, st); else launch_gru_x3<2, 2>(a, st); break;
@@ -881,12 +893,6 @@ void launch_gru(const GruArgs& a, hipStream_t st) {
   // weight-stationary clusters while all of them fit one wave of the chip (1 workgroup per CU);
   // beyond that the batch-parallel kernel at 32 rows per workgroup streams weights at a better
   // rate than two waves of clusters (tools/gru_bench.py: 8192 rows 5.6 M vs 4.5 M seq/s)
-  static int n_cu = [] {
-    int dev = 0, v = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
-    return v > 0 ? v : 256;
-  }();
   if (a.ws && gru_ws_eligible(a)) {
     // ws = 3: two 64-row clusters per CU (all co-resident at <= 2 workgroups per CU)
     if (a.ws == 3 ? gru_ws2_clusters(a.n_rows) * 8 <= 2 * n_cu : gru_ws_clusters(a.n_rows) * 8 <= n_cu)

@@ -271,6 +271,12 @@ bool gru_ws_eligible(const GruArgs& a);
 void launch_gru_ws(const GruArgs& a, hipStream_t st);
 int gru_ws_clusters(int n_rows);
 int gru_ws2_clusters(int n_rows);  // 64-row clusters (ws = 3)
+// split (f32-faithful) weight-stationary clusters of 16 workgroups x 32 rows (gru_wsx.hip);
+// the workspace is then sized in 32-row clusters: ws_sync [clusters][16], ws_x
+// [clusters][2][16][4][32][16] bf16, ws_part [clusters][16][32]
+bool gru_wsx_eligible(const GruArgs& a);
+void launch_gru_wsx(const GruArgs& a, hipStream_t st);
+int gru_wsx_clusters(int n_rows);
 
 // ---- K9 LTV / churn / segment
 struct LtvArgs {

@@ -22,6 +22,7 @@
 #include <pybind11/pybind11.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -74,6 +75,8 @@ class ModelDriver {
       o1_.push_back(kind == IGP_MODEL_ABUSE ? reinterpret_cast<void*>(out1[s].cast<uintptr_t>()) : nullptr);
     }
     hip_ok(hipGetDevice(&device_), "get device");
+    last_n_.assign(depth, 0);
+    last_key_.assign(depth, -1);
     ev_.resize(depth);
     for (auto& e : ev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event create");
     ops_.abi = IGP_MODEL_OPS_ABI;
@@ -106,6 +109,7 @@ class ModelDriver {
           const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
           if (!poll_event_until(e, t_end, [](hipError_t q) { hip_ok(q, "event query"); })) return 1;
         }
+        d->check_fallback(slot);
       } catch (const std::exception& e) {
         copy_err(err, errlen, e.what());
         return -1;
@@ -127,7 +131,24 @@ class ModelDriver {
     check(bucket, slot);
     steps_[key(bucket, slot)].graph = reinterpret_cast<hipGraphExec_t>(exec);
   }
+  // the same step without the weight-stationary GRU clusters (gru_wsx.hip): a cluster that
+  // could not become co-resident gives up after a bounded wait and leaves NaN scores; wait()
+  // then re-runs the slot's step on this body and every later step uses it
+  void set_alt_graph(int bucket, int slot, uintptr_t exec) {
+    check(bucket, slot);
+    steps_[key(bucket, slot)].alt = reinterpret_cast<hipGraphExec_t>(exec);
+  }
+  bool fell_back() const { return fallback_.load(); }
+  // small buckets (the weight-stationary GRU clusters, up to half the chip per launch) all run
+  // on one extra stream, one launch at a time; larger ones on the slot's own stream
+  void set_small_stream(uintptr_t stream, int max_rows) {
+    small_st_ = reinterpret_cast<hipStream_t>(stream);
+    shared_max_ = max_rows;
+  }
+  int64_t fallbacks() const { return fallbacks_; }
   uintptr_t model_ops() {
+    has_alt_ = false;
+    for (auto& kv : steps_) has_alt_ = has_alt_ || kv.second.alt != nullptr;
     buckets_.clear();
     for (auto& kv : steps_) {
       const int b = int(kv.first >> 8);
@@ -147,7 +168,26 @@ class ModelDriver {
   struct StepBody {
     std::shared_ptr<OpList> ops;
     hipGraphExec_t graph = nullptr;
+    hipGraphExec_t alt = nullptr;
   };
+  // completion of an abuse step: NaN scores mean a cluster launch gave up - switch to the
+  // alternative bodies and recompute this slot's rows (the step only reads the store)
+  void check_fallback(int slot) {
+    if (ops_.kind != IGP_MODEL_ABUSE || !has_alt_) return;
+    const int n = last_n_[slot];
+    const float* o = static_cast<const float*>(o0_[slot]);
+    bool nan = false;
+    for (int i = 0; i < n && !nan; ++i) nan = o[i] != o[i];
+    if (!nan) return;
+    fallback_.store(true);
+    auto it = steps_.find(last_key_[slot]);
+    if (it == steps_.end() || !it->second.alt) throw std::runtime_error("abuse step gave up and has no fallback body");
+    hipStream_t st = stream_for(int(last_key_[slot] >> 8), slot);
+    hip_ok(hipGraphLaunch(it->second.alt, st), "fallback graph launch");
+    hip_ok(hipEventRecord(ev_[slot], st), "record");
+    hip_ok(hipEventSynchronize(ev_[slot]), "sync fallback");
+    ++fallbacks_;
+  }
   static int64_t key(int bucket, int slot) { return (int64_t(bucket) << 8) | slot; }
   void check(int bucket, int slot) const {
     if (slot < 0 || slot >= depth_ || bucket < 1 || bucket > cap_) throw std::runtime_error("ModelDriver: bucket / slot");
@@ -182,11 +222,16 @@ class ModelDriver {
       }
     }
     const StepBody& b = it->second;
-    hipStream_t st = st_[st_.size() == 1 ? 0 : slot];
+    hipStream_t st = stream_for(bucket, slot);
+    last_n_[slot] = n;
+    last_key_[slot] = key(bucket, slot);
     // the abuse step reads the feature store (K1 rule signals, the GRU event rings): it sees every
     // scoring batch issued before this call (state_clock.h), without a host sync
     if (ops_.kind == IGP_MODEL_ABUSE && clock_) clock_->wait(st);
-    if (b.ops) {
+    if (b.alt && fallback_.load()) {
+      hip_ok(hipGraphLaunch(b.alt, st), "graph launch");
+      hip_ok(hipEventRecord(ev_[slot], st), "record");
+    } else if (b.ops) {
       if (!b.ops->run_recording(st, ev_[slot])) hip_ok(hipEventRecord(ev_[slot], st), "record");
     } else {
       hip_ok(hipGraphLaunch(b.graph, st), "graph launch");
@@ -205,6 +250,17 @@ class ModelDriver {
   std::vector<hipEvent_t> ev_;
   std::map<int64_t, StepBody> steps_;
   std::vector<int> buckets_;
+  std::vector<int> last_n_;
+  std::vector<int64_t> last_key_;
+  bool has_alt_ = false;
+  int shared_max_ = 0;  // buckets up to this many rows run on small_st_
+  hipStream_t small_st_ = nullptr;
+  hipStream_t stream_for(int bucket, int slot) const {
+    if (small_st_ && bucket <= shared_max_) return small_st_;
+    return st_[st_.size() == 1 ? 0 : slot];
+  }
+  std::atomic<bool> fallback_{false};
+  int64_t fallbacks_ = 0;
   IgpModelOps ops_{};
   std::shared_ptr<StateClock> clock_;
 };
@@ -220,6 +276,10 @@ void register_model_driver(py::module_& m) {
            py::arg("out0"), py::arg("out1"))
       .def("set_ops", &ModelDriver::set_ops)
       .def("set_graph", &ModelDriver::set_graph)
+      .def("set_alt_graph", &ModelDriver::set_alt_graph)
+      .def("set_small_stream", &ModelDriver::set_small_stream)
+      .def_property_readonly("fell_back", &ModelDriver::fell_back)
+      .def_property_readonly("fallbacks", [](const ModelDriver& d) { return d.fallbacks(); })
       .def("model_ops", &ModelDriver::model_ops)
       .def("set_state_clock", &ModelDriver::set_state_clock)
       .def_property_readonly("submits", &ModelDriver::submits);

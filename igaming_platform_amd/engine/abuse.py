@@ -118,9 +118,8 @@ class AbuseGpu:
         # 256 CUs at 4096 rows). The weight-stationary cluster kernel needs the whole chip
         # co-resident and a bidirectional model shares its intermediates: both stay on one
         # stream, as does a serving rank (its streams are budgeted to the 4 hardware queues,
-        # engine/dp.py). IGP_ABUSE_STREAMS=1 forces one.
-        multi = (overlap and not self.gp.ws_ok and not self.gm.bidirectional and depth > 1
-                 and os.environ.get("IGP_ABUSE_STREAMS", "") != "1")
+        # engine/dp.py).
+        multi = overlap and not self.gp.ws_ok and not self.gm.bidirectional and depth > 1
         self.n_streams = depth if multi else 1
         if self.gm.split:  # 32-row split tiles leave half the chip to the next slot's batch
             rows = int(os.environ.get("IGP_GRU_X3_ROWS", "32" if multi else "16"))
@@ -217,7 +216,7 @@ class AbuseGpu:
         try:
             ev.synchronize()
             out = self.host_out[slot][:n].numpy().copy()
-            if self.gp.ws_ok and n and np.isnan(out).any():
+            if (self.gp.ws_ok or self.gp.wsx_ok) and n and np.isnan(out).any():
                 out = self._ws_fallback(slot, n)
             return out
         finally:

@@ -133,11 +133,17 @@ class AbuseNativeDevice:
             self.gm = GruModel(plan.steps, dev, getattr(plan, "precision", "fp32") != "bf16", B)
             if not self.gm.has_head:
                 raise ValueError("abuse model must end in an N=1 head (probability)")
-            # batch-parallel K4 only: the weight-stationary cluster kernel (gru_ws.hip) needs every
-            # workgroup of the launch co-resident, which a serving rank sharing the chip with the
-            # scoring pipeline cannot promise (and a recorded graph cannot fall back)
+            # the bf16 cluster kernel (gru_ws.hip) needs the whole chip co-resident, which a
+            # serving rank sharing it with the scoring pipeline cannot promise: off. The split
+            # clusters for small batches (gru_wsx.hip, <= a quarter of the chip per launch) stay,
+            # with a second graph per step on the batch-parallel kernel that the driver switches
+            # to if a cluster ever gives up (NaN scores, model_driver.hip check_fallback)
             for gp in self.gm.packs:
-                gp.disable_ws()
+                gp.disable_ws(keep_wsx=True)
+            if any(gp.wsx_ok for gp in self.gm.packs):
+                # 128- and 256-row buckets: micro-batches up to 256 rows run on the clusters
+                # (8 x 16 CUs at 256 rows)
+                self.buckets = sorted(set(self.buckets) | {b for b in (128, 256) if b < B})
             self.T = plan.steps[0].seq or store.ev.shape[1]
         self.req_off = 16 + 4 * B
         nb = self.req_off + 48 * B
@@ -167,11 +173,25 @@ class AbuseNativeDevice:
         # every step reads the store after the scoring batches issued before it (state_clock.h)
         if getattr(backend, "state_clock", None) is not None:
             self.driver.set_state_clock(backend.state_clock)
+        if self.gm is not None and any(gp.wsx_ok for gp in self.gm.packs):
+            # the split GRU clusters (buckets <= 256: up to half the chip per launch) run one
+            # launch at a time on a stream of their own; larger buckets keep a stream per slot
+            self.small_stream = torch.cuda.Stream(device=dev)
+            self.driver.set_small_stream(self.small_stream.cuda_stream, 256)
         self.graphs = []
+        wsx = self.gm is not None and any(gp.wsx_ok for gp in self.gm.packs)
         with torch.cuda.device(dev):
             for b in self.buckets:
                 for slot in range(self.depth):
                     self.driver.set_graph(b, slot, self._capture(slot, b))
+                    if wsx:  # the same step on the batch-parallel kernel (the fallback body)
+                        for gp in self.gm.packs:
+                            gp.wsx_ok = False
+                        try:
+                            self.driver.set_alt_graph(b, slot, self._capture(slot, b))
+                        finally:
+                            for gp in self.gm.packs:
+                                gp.wsx_ok = True
             torch.cuda.synchronize(dev)
 
     def _body(self, slot: int, b: int) -> None:

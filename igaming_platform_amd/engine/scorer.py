@@ -166,7 +166,7 @@ class GpuScorer:
         self.cfg_dev = torch.zeros(176, dtype=torch.uint8, device=dev)
         self.refresh_config()
         self.graphs: Dict[tuple, tuple] = {}
-        self._host_results = os.environ.get("IGP_HOST_RESULTS", "1") != "0"
+        self._host_results = True  # K5 writes the result rows straight into pinned host memory
         self.driver = None
         self._slot = 0
         self._seq = 0
@@ -293,9 +293,9 @@ class GpuScorer:
     def _model_body(self, slot: int, bucket: int, with_features: bool = False) -> None:
         sb = self.slots[slot]
         # K5 writes the result rows straight into the slot's pinned host buffer as well (no
-        # D2H copy node on the model stream); IGP_HOST_RESULTS=0 restores the copy
+        # D2H copy node on the model stream)
         host = self.host_res[slot] if self._host_results else None
-        if sb.model is not None and sb.model.fuses_ensemble(bucket) and os.environ.get("IGP_FUSE_ENS", "1") != "0":
+        if sb.model is not None and sb.model.fuses_ensemble(bucket):
             # K5 in the MLP head's (or the grouped trees' finish kernel's) epilogue: one launch fewer
             ens = K.ensemble_args(sb.hdr, self.cfg_dev, sb.feat, sb.X, sb.model.step_out[-1], sb.res, bucket,
                                   self.metrics, host_out=host)

@@ -529,15 +529,28 @@ class GruPack:
             self.head_b = float(head.b_np[0]) if head.b_np is not None else 0.0
             self.head_act = ACT[head.act]
         self.device = dev
-        # weight-stationary cluster kernel (csrc/kernels/gru_ws.hip) for 2 x 256, lbr = 1, I <= 32
-        # (bf16 only: its stationary weights fill the register file)
-        self.ws_ok = self.n_layers == 2 and H == 256 and self.lbr == 1 and self.I <= 32 and not self.split
+        # weight-stationary cluster kernels for 2 x 256, lbr = 1, I <= 32: bf16 (gru_ws.hip, 8
+        # members per 128 / 64 rows) and, for small f32-faithful batches, the split variant
+        # (gru_wsx.hip, 16 members per 32 rows; the launcher picks it up to n_cu / 4 workgroups)
+        shape_ok = self.n_layers == 2 and H == 256 and self.lbr == 1 and self.I <= 32
+        self.ws_ok = shape_ok and not self.split
+        self.wsx_ok = shape_ok and self.split
         self._ws = None
         self._ws_old = []  # superseded workspaces stay alive: captured graphs keep their pointers
-        self.ws_err = torch.zeros(1, dtype=torch.int32, device=dev) if self.ws_ok else None
+        self.ws_err = torch.zeros(1, dtype=torch.int32, device=dev) if (self.ws_ok or self.wsx_ok) else None
 
     def workspace(self, n_rows: int):
         """Hand-off slabs / counters / head partials for ``n_rows`` (grow-only)."""
+        if self.wsx_ok:  # 32-row clusters of 16 members: [2 parities][16][4 blocks][32][16] bf16
+            ncl = -(-int(n_rows) // 32)
+            if self._ws is None or self._ws["clusters"] < ncl:
+                if self._ws is not None:
+                    self._ws_old.append(self._ws)
+                dev = self.device
+                self._ws = dict(clusters=ncl, sync=torch.zeros(ncl * 16, dtype=torch.int32, device=dev),
+                                x=torch.zeros(ncl * 2 * 16 * 4 * 32 * 16, dtype=torch.int16, device=dev),
+                                part=torch.zeros(ncl * 16 * 32, dtype=torch.float32, device=dev))
+            return self._ws
         if not self.ws_ok:
             return None
         ncl = -(-int(n_rows) // 128)
@@ -556,10 +569,14 @@ class GruPack:
         """True if a cluster launch ever timed out waiting for a non-resident member."""
         return bool(self.ws_err is not None and int(self.ws_err.item()) != 0)
 
-    def disable_ws(self) -> None:
+    def disable_ws(self, keep_wsx: bool = False) -> None:
         """After a failed cluster launch (NaN outputs / ws_err): counters back to 0 and every
-        later launch on the batch-parallel kernel (callers re-capture their graphs)."""
+        later launch on the batch-parallel kernel (callers re-capture their graphs).
+        ``keep_wsx``: only the bf16 cluster kernel (a caller that falls back on its own)."""
         self.ws_ok = False
+        if keep_wsx:
+            return
+        self.wsx_ok = False
         for w in [self._ws] + self._ws_old:
             if w is not None:
                 w["sync"].zero_()
@@ -567,7 +584,6 @@ class GruPack:
             self.ws_err.zero_()
 
 
-_GRU_WS = os.environ.get("IGP_GRU_WS", "1") != "0"  # 0: always the batch-parallel K4 (A/B runs)
 # default cluster layout: 1 one 128-row cluster per CU, 3 two 64-row clusters per CU
 _GRU_WS_MODE = int(os.environ.get("IGP_GRU_WS_MODE", "3"))
 
@@ -588,7 +604,7 @@ def gru(gp: GruPack, n_rows: int, T: int, out: Optional[torch.Tensor] = None, yh
     d = dict(n_layers=gp.n_layers, H=gp.H, T=int(T), I=gp.I, n_rows=int(n_rows),
              m_ptr=_opt(m_ptr, "m_ptr", dtype=torch.int32, device=dev), tile_rows=int(tile_rows),
              waves=int(waves or gp.waves), pipeline=int(pipeline))
-    w = gp.workspace(n_rows) if ws and _GRU_WS else None
+    w = gp.workspace(n_rows) if ws else None
     if w is not None:
         d.update(ws=int(ws), ws_clusters=w["clusters"], ws_sync=w["sync"].data_ptr(), ws_x=w["x"].data_ptr(),
                  ws_part=w["part"].data_ptr(), ws_err=gp.ws_err.data_ptr(),
@@ -686,8 +702,8 @@ class MlpChainPack:
 
     def waves(self) -> int:
         """Waves per workgroup: 8 needs every layer width to be a multiple of 128."""
-        w = int(os.environ.get("IGP_MLP_WAVES", "8"))  # 8: +11 % cfg4 over 4 (same-box A/B, NOTES.md)
-        return w if all(l["N"] % (16 * w) == 0 for l in self.layers) else 4
+        # 8: +11 % cfg4 over 4 (same-box A/B, NOTES.md)
+        return 8 if all(l["N"] % 128 == 0 for l in self.layers) else 4
 
 
 def mlp_chain(pk: MlpChainPack, n_rows: int, X: Optional[torch.Tensor] = None, slots: Optional[torch.Tensor] = None,

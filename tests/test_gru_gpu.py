@@ -350,3 +350,87 @@ def test_abuse_gpu_overlapped_slots_match_one_stream():
         res[overlap] = [R.wait(p) for p in ps]
     for a, b in zip(res[False], res[True]):
         np.testing.assert_array_equal(a, b)
+
+
+def _split_pack(seq, head=True):
+    from igaming_platform_amd.models.plan import compile_onnx, to_device
+    from igaming_platform_amd.native import native
+    from igaming_platform_amd.ops import kernels as K
+    from igaming_platform_amd.onnx import builders
+    N = native()
+    m = N.OnnxModel.from_bytes(builders.build("gru", seq=seq, in_dim=16, hidden=256, layers=2, linear_before_reset=1,
+                                              head=head).SerializeToString())
+    plan = to_device(compile_onnx(m), "cuda", "fp32")
+    gp = K.GruPack([s for s in plan.steps if s.kind == "gru"], plan.steps[-1] if head else None, "cuda", split=True)
+    assert gp.wsx_ok and not gp.ws_ok
+    return N, m, plan, gp
+
+
+@pytest.mark.parametrize("rows", [1, 31, 32, 100, 128])
+def test_gru_split_clusters_match_batch_parallel(rows):
+    """gru_wsx.hip (16-workgroup clusters per 32 rows, hi + lo weights
+    stationary in registers, K split over two waves per layer, sc1 hand-offs of hi / lo state)
+    equals the batch-parallel split kernel to f32 rounding and the float64 reference to 1e-4 over
+    100 steps, for one row, a partial / full cluster and four clusters; repeated launches reuse the
+    counters the kernel returns to 0."""
+    import torch
+    from igaming_platform_amd.ops import kernels as K
+    T = 100
+    N, m, plan, gp = _split_pack(T)
+    plan.steps[-1].w_np = plan.steps[-1].w_np * 40.0  # spread the scores over (0, 1)
+    gp.head_w = torch.from_numpy(np.ascontiguousarray(plan.steps[-1].w_np[0], np.float32)).cuda()
+    rng = np.random.default_rng(rows + 5)
+    Xd = torch.from_numpy(rng.standard_normal((T, rows, 16)).astype(np.float32)).cuda()
+    o_x = torch.full((rows,), -9.0, device="cuda")
+    o_bp = torch.full((rows,), -9.0, device="cuda")
+    for _ in range(2):
+        o_x.fill_(-9.0)
+        K.gru(gp, rows, T, out=o_x, X=Xd, ws=3)
+        torch.cuda.synchronize()
+        assert not gp.ws_failed()
+        assert bool(torch.all(torch.isfinite(o_x))) and bool(torch.all(o_x != -9.0))
+    # the cluster kernel ran (only it writes the per-member head partials of its workspace)
+    assert bool(torch.any(gp.workspace(rows)["part"] != 0))
+    K.gru(gp, rows, T, out=o_bp, X=Xd, ws=0)
+    torch.cuda.synchronize()
+    a, b = o_x.cpu().numpy(), o_bp.cpu().numpy()
+    np.testing.assert_allclose(a, b, rtol=0, atol=1e-5)
+    ref = _gru_f64(plan, Xd)
+    assert float(np.abs(a - ref).max()) <= 1e-4
+
+
+def test_gru_split_clusters_event_rings_yh_and_live_rows():
+    """The split cluster kernel from the HBM event rings (right-aligned histories, empty slots),
+    Y_h without a head, and a device live count below the launch rows: equal to the batch-parallel
+    split kernel; rows past the live count untouched."""
+    import torch
+    from igaming_platform_amd.config import FeatureConfig
+    from igaming_platform_amd.features.device_store import DeviceFeatureStore
+    from igaming_platform_amd.layouts import ACCTRT
+    from igaming_platform_amd.ops import kernels as K
+    fc = FeatureConfig()
+    C, R, D = 400, fc.event_ring, fc.event_dim
+    N, m, plan, gp = _split_pack(R, head=False)
+    store = DeviceFeatureStore(C, fc, "cuda", events=True, max_events=64)
+    rng = np.random.default_rng(12)
+    store.ev.copy_(torch.from_numpy(rng.standard_normal((C, R, D)).astype(np.float32)).to(torch.bfloat16)
+                   .view(torch.int16).cuda())
+    rt = np.zeros(C, ACCTRT)
+    rt["ev_head"] = rng.integers(0, R, C)
+    rt["ev_count"] = rng.integers(0, R + 1, C)
+    store.rt.copy_(torch.from_numpy(rt.view(np.int32).reshape(C, -1).copy()).cuda())
+    rows, live = 128, 77
+    slots = rng.integers(0, C, rows).astype(np.int32)
+    slots[::9] = -1
+    sd = torch.from_numpy(slots).cuda()
+    n = torch.tensor([live], dtype=torch.int32, device="cuda")
+    y_x = torch.full((rows, 256), 5.0, device="cuda")
+    y_bp = torch.full((rows, 256), 5.0, device="cuda")
+    K.gru(gp, rows, R, yh=y_x, store=store, slots=sd, m_ptr=n, ws=3)
+    K.gru(gp, rows, R, yh=y_bp, store=store, slots=sd, m_ptr=n, ws=0)
+    torch.cuda.synchronize()
+    assert not gp.ws_failed()
+    assert torch.all(y_x[live:] == 5.0)
+    np.testing.assert_allclose(y_x[:live].cpu().numpy(), y_bp[:live].cpu().numpy(), rtol=0, atol=1e-5)
+    # a different kernel (the two K halves are summed in another order): not bit-identical
+    assert not torch.equal(y_x[:live], y_bp[:live])

@@ -161,6 +161,7 @@ def main():
     stop_names.set()
     names.update({t: n for t, (n, _) in after.items()})
     lat = np.asarray(r["latency_ms"])
+    sched = np.asarray(r["sched_ms"]) if "sched_ms" in r else None
     calls = max(len(lat), 1)
     by = collections.defaultdict(float)
     nthreads = collections.Counter()
@@ -172,9 +173,27 @@ def main():
     total = (proc1.user + proc1.system) - (proc0.user + proc0.system)
     by["h2-loadgen (exited threads)"] = max(0.0, total - sum(by.values()))
     core = eng.core.stats(False) if getattr(eng, "core", None) is not None else {}
+    acct_st = None
+    if a.rpc != "tx" and getattr(eng, "acct", None) is not None:
+        st = eng.acct.router.stats(3 if a.rpc == "abuse" else 1)
+        steps = max(int(st["steps"]), 1)
+        acct_st = dict(steps=int(st["steps"]), rows_per_step=round(st["rows"] / steps, 1),
+                       max_step_rows=int(st["max_step_rows"]), device_us_per_step=round(st["device_ns"] / steps / 1e3, 1),
+                       queue_us_per_item=round(st["queue_ns"] / max(int(st["items"]), 1) / 1e3, 1),
+                       wait_errors=int(st["wait_errors"]))
+        drv = getattr(getattr(eng.acct, "devices", [None])[-1], "driver", None)
+        if drv is not None and hasattr(drv, "fallbacks"):
+            acct_st["cluster_fallbacks"] = int(drv.fallbacks)
     res = dict(backend=a.backend, rpc=a.rpc, offered_per_s=a.rate, achieved_per_s=round(len(lat) / float(r["elapsed"]), 1),
                errors=int(r["errors"]), p50_ms=round(float(np.percentile(lat, 50)), 3) if len(lat) else None,
                p99_ms=round(float(np.percentile(lat, 99)), 3) if len(lat) else None, wall_s=round(wall, 2),
+               latency_ms_pct={str(q): round(float(np.percentile(lat, q)), 3) for q in (10, 50, 90, 95, 99, 99.9)}
+               if len(lat) else None, account_router=acct_st,
+               # the slowest call of every 100-ms window of the schedule: a periodic stall shows as
+               # a few windows far above the rest
+               window_max_ms=[round(float(lat[(sched >= w) & (sched < w + 100)].max()), 2)
+                              for w in range(0, int(sched.max()) + 1, 100) if np.any((sched >= w) & (sched < w + 100))]
+               if sched is not None and len(lat) else None,
                clients=a.clients, workers=a.workers,
                cpu_us_per_call={k: round(v / calls * 1e6, 2) for k, v in sorted(by.items(), key=lambda x: -x[1])},
                cpu_cores_busy={k: round(v / wall, 2) for k, v in sorted(by.items(), key=lambda x: -x[1])},
