@@ -89,6 +89,7 @@ def parse():
                          "the owner-routed DP bench (every rank's account router, closed loop)")
     ap.add_argument("--calls", type=int, default=65536, help="cfg4 / cfg5 serving: calls per rank per step")
     ap.add_argument("--inflight", type=int, default=16384, help="cfg4 / cfg5 serving: outstanding calls per rank")
+    ap.add_argument("--drive-threads", type=int, default=4, help="cfg4 / cfg5 serving: threads submitting calls per rank")
     ap.add_argument("--check-out", default="", help="cfg4 / cfg5 serving: after the timed run every rank answers "
                     "the same fixed calls and writes them to <check-out>.<rank>.json (tests/test_bench_acct.py)")
     ap.add_argument("--seconds", type=float, default=5.0, help="cfg4 / cfg5 serving: seconds per offered-load level")
@@ -244,11 +245,11 @@ def acct_dp_bench(a) -> None:
     payloads = bench_e2e.acct_payloads(total, rpc_name, 1 << 16, 300 + rank, a.zipf)
     per_step = a.calls
     now = NOW_ACCT
-    router.drive(rpc, payloads, max(a.warmup, 1) * per_step, a.inflight, now)  # warm: graphs, caches
+    router.drive(rpc, payloads, max(a.warmup, 1) * per_step, a.inflight, now, a.drive_threads)  # warm
     if comm is not None:
         comm.barrier()
     t0 = time.perf_counter()
-    r = router.drive(rpc, payloads, a.steps * per_step, a.inflight, now)
+    r = router.drive(rpc, payloads, a.steps * per_step, a.inflight, now, a.drive_threads)
     if comm is not None:
         comm.barrier()
     elapsed = time.perf_counter() - t0
@@ -276,6 +277,7 @@ def acct_dp_bench(a) -> None:
         "config": {"model": c["desc"], "global_batch": per_step * world, "seq_len": 100 if a.config == "cfg5" else 1,
                    "parallelism": f"dp{world} (owner-routed: each call computed once, on its account's GPU)",
                    "calls_per_step_per_rank": per_step, "inflight_per_rank": a.inflight,
+                   "submit_threads_per_rank": a.drive_threads,
                    "device_micro_batch_max": max(cfg.gpu.buckets), "accounts_per_gpu": n_acc,
                    "account_spread": f"zipf({a.zipf})" if a.zipf > 1 else "uniform",
                    "numerics": numerics_desc(a), "backend": kind,

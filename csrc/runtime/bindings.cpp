@@ -4,8 +4,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <atomic>
 #include <cstring>
 #include <memory>
+#include <thread>
 
 #include "account_index.h"
 #include "acct_core.h"
@@ -1020,36 +1022,61 @@ PYBIND11_MODULE(_native, m) {
         return l;
       }, py::arg("max") = 4096, py::arg("timeout_us") = 1000)
       // in-process closed-loop load (bench.py --config cfg4|cfg5 --scope serving): `n` calls
-      // cycling over `payloads`, at most `inflight` outstanding, submitted and answered on this
-      // thread without the GIL. Returns per-call latency (submit -> answer, ns) of the answered
-      // calls, the error count, the cold-path count ("cold: " replies) and the elapsed seconds.
-      .def("drive", [](PyAcct& a, int rpc, py::list payloads, int64_t n, int64_t inflight, int64_t now) {
+      // cycling over `payloads`, at most `inflight` outstanding, submitted by `threads` threads
+      // (call i by thread i % threads) and answered on this thread, all without the GIL. Returns
+      // per-call latency (submit -> answer, ns; -1 for an error), the error count, the cold-path
+      // count ("cold: " replies) and the elapsed seconds.
+      .def("drive", [](PyAcct& a, int rpc, py::list payloads, int64_t n, int64_t inflight, int64_t now, int threads) {
         const size_t np_ = payloads.size();
-        if (np_ == 0 || n <= 0 || inflight <= 0) throw std::runtime_error("drive: payloads, n and inflight > 0");
+        if (np_ == 0 || n <= 0 || inflight <= 0 || threads < 1 || threads > 64)
+          throw std::runtime_error("drive: payloads, n and inflight > 0, 1..64 threads");
         std::vector<std::string> bufs(np_);
         for (size_t k = 0; k < np_; ++k) bufs[k] = payloads[k].cast<std::string>();
         std::vector<int64_t> t_sub(size_t(n), 0);
         py::array_t<int64_t> lat(n);
         int64_t* L = lat.mutable_data();
-        int64_t sent = 0, got = 0, errors = 0, cold = 0;
+        int64_t got = 0, errors = 0, cold = 0;
         double elapsed = 0;
         {
           py::gil_scoped_release rel;
-          std::vector<AcctRouter::Done> out;
+          const int T = threads;
+          const int64_t cap = std::max<int64_t>(1, inflight / T);
+          std::vector<std::atomic<int64_t>> done(static_cast<size_t>(T));
+          for (auto& d : done) d.store(0);
+          std::atomic<bool> abort{false};
           const int64_t t0 = ServeCore::now_ns();
-          while (got < n) {
-            const int64_t room = std::min<int64_t>(n - sent, inflight - (sent - got));
-            if (room > 0) {
-              const int64_t ts = ServeCore::now_ns();
-              for (int64_t k = 0; k < room; ++k, ++sent) {
-                const std::string& b = bufs[size_t(sent) % np_];
-                t_sub[size_t(sent)] = ts;
-                a.router->submit(uint8_t(rpc), b.data(), b.size(), uint64_t(sent), ts, now);
+          std::vector<std::thread> subs;
+          for (int j = 0; j < T; ++j) {
+            subs.emplace_back([&, j] {
+              int64_t sent = 0;  // calls j, j + T, j + 2T, ... of this thread
+              for (int64_t i = j; i < n && !abort.load(std::memory_order_relaxed); i += T) {
+                while (sent - done[size_t(j)].load(std::memory_order_acquire) >= cap) {
+                  if (abort.load(std::memory_order_relaxed)) return;
+                  std::this_thread::sleep_for(std::chrono::microseconds(20));
+                }
+                const std::string& b = bufs[size_t(i) % np_];
+                const int64_t ts = ServeCore::now_ns();
+                t_sub[size_t(i)] = ts;
+                a.router->submit(uint8_t(rpc), b.data(), b.size(), uint64_t(i), ts, now);
+                ++sent;
               }
-            }
+            });
+          }
+          std::vector<AcctRouter::Done> out;
+          int64_t idle_since = 0;
+          while (got < n) {
             out.clear();
-            a.router->poll(out, size_t(inflight), 2000);
+            a.router->poll(out, size_t(std::max<int64_t>(inflight, 1024)), 2000);
             const int64_t tr = ServeCore::now_ns();
+            if (out.empty()) {
+              if (!idle_since) idle_since = tr;
+              if (tr - idle_since > 60000000000LL) {  // nothing answered for a minute: give up
+                abort.store(true);
+                break;
+              }
+              continue;
+            }
+            idle_since = 0;
             for (auto& d : out) {
               const size_t i = size_t(d.tag);
               if (i >= size_t(n)) continue;
@@ -1060,9 +1087,13 @@ PYBIND11_MODULE(_native, m) {
               } else {
                 L[got++] = tr - t_sub[i];
               }
+              done[i % size_t(T)].fetch_add(1, std::memory_order_release);
             }
           }
+          for (auto& t : subs) t.join();
           elapsed = double(ServeCore::now_ns() - t0) / 1e9;
+          for (int64_t k = got; k < n; ++k) L[k] = -1;
+          errors += n - got;
         }
         py::dict r;
         r["latency_ns"] = lat;
@@ -1070,7 +1101,8 @@ PYBIND11_MODULE(_native, m) {
         r["cold"] = cold;
         r["elapsed"] = elapsed;
         return r;
-      }, py::arg("rpc"), py::arg("payloads"), py::arg("n"), py::arg("inflight") = 8192, py::arg("now") = -1)
+      }, py::arg("rpc"), py::arg("payloads"), py::arg("n"), py::arg("inflight") = 8192, py::arg("now") = -1,
+         py::arg("threads") = 1)
       .def("stop", [](PyAcct& a) {
         py::gil_scoped_release rel;
         a.router->stop();
