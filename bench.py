@@ -89,7 +89,7 @@ def parse():
                          "the owner-routed DP bench (every rank's account router, closed loop)")
     ap.add_argument("--calls", type=int, default=65536, help="cfg4 / cfg5 serving: calls per rank per step")
     ap.add_argument("--inflight", type=int, default=16384, help="cfg4 / cfg5 serving: outstanding calls per rank")
-    ap.add_argument("--drive-threads", type=int, default=4, help="cfg4 / cfg5 serving: threads submitting calls per rank")
+    ap.add_argument("--drive-threads", type=int, default=1, help="cfg4 / cfg5 serving: threads submitting calls per rank")
     ap.add_argument("--check-out", default="", help="cfg4 / cfg5 serving: after the timed run every rank answers "
                     "the same fixed calls and writes them to <check-out>.<rank>.json (tests/test_bench_acct.py)")
     ap.add_argument("--seconds", type=float, default=5.0, help="cfg4 / cfg5 serving: seconds per offered-load level")
@@ -672,10 +672,16 @@ def serving_bench(a) -> None:
         if kind == "gpu":
             torch.cuda.synchronize(local)
     comm = None
-    if world > 1:
+    # IGP_BENCH_SPMD=1: the multi-GPU serving objects (SpmdNode: owner-routed RCCL exchange,
+    # node-shared registry, step clock) at world 1 too - the N = 1 point of the exchange path
+    spmd = world > 1 or os.environ.get("IGP_BENCH_SPMD") == "1"
+    if spmd:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(29400 + os.getpid() % 1000))
         # the control plane (shm names, barriers, RCCL unique ids, result reduce) runs over gloo;
         # the hot path moves rows over the exchange's own RCCL communicators
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", **({} if world > 1 else dict(rank=0, world_size=1)))
         from igaming_platform_amd.parallel.comm import TorchComm
         comm = TorchComm("gloo")
     if a.config not in benchkit.CONFIGS or benchkit.CONFIGS[a.config]["model"] == "heuristic":
@@ -691,7 +697,7 @@ def serving_bench(a) -> None:
     cfg.gpu.spmd_heartbeat_s = 0.0
     n_acc = a.accounts
     fm = builders.build(c["model"]).SerializeToString()
-    if world == 1:
+    if not spmd:
         from igaming_platform_amd.engine.risk_engine import RiskEngine
         eng = RiskEngine(cfg, backend=kind, capacity=n_acc + 4096, fraud_model=fm)
         core, registry, backend = eng.core, eng.registry, eng.backends[0]
@@ -773,11 +779,31 @@ def serving_bench(a) -> None:
     barrier()
     sync()
     core.stats(True)
+    # IGP_BENCH_THREADS_OUT=<path>: per-thread CPU time over the timed run (rank 0; thread names
+    # from csrc/runtime/thread_name.h) - which host thread, if any, is saturated
+    threads_out = os.environ.get("IGP_BENCH_THREADS_OUT") if rank == 0 else None
+    if threads_out:
+        import host_profile
+        cpu0, proc0 = host_profile.thread_cpu(), os.times()
     t0 = time.perf_counter()
     run(a.steps * per_step, NOW0, True)
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    if threads_out:
+        cpu1, proc1 = host_profile.thread_cpu(), os.times()
+        busy, alive = {}, 0.0
+        for tid, (name, cpu) in cpu1.items():
+            d = cpu - cpu0.get(tid, (name, 0.0))[1]
+            alive += d
+            if d > 0:
+                busy.setdefault(name, []).append(round(d / elapsed, 3))
+        # the ingress threads exit with run(): their share is the process total minus the rest
+        total = (proc1.user + proc1.system) - (proc0.user + proc0.system)
+        with open(threads_out, "w") as f:
+            json.dump({"elapsed_s": elapsed, "cpu_fraction_by_thread_name": busy,
+                       "ingress_threads_cores": round(max(0.0, total - alive) / elapsed, 2),
+                       "process_cores": round(total / elapsed, 2)}, f)
     st = core.stats(True)
     rows = max(int(st["rows"]), 1)
     stages = {k[:-3] + "_ns_per_row": round(st[k] / rows, 1)
@@ -828,8 +854,10 @@ def serving_bench(a) -> None:
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
-    if world > 1:
+    if spmd:
         node.core.stop()
+        if world == 1:
+            node.close()  # (N > 1: the communicators go with the processes; no teardown to wait on)
         dist.destroy_process_group()
     else:
         eng.close()

@@ -37,6 +37,7 @@
 
 #include "../include/device_ops.h"
 #include "../include/records.h"
+#include "launch.h"
 #include "oplist.h"
 #include "roctx.h"
 #include "state_clock.h"
@@ -104,9 +105,13 @@ __global__ __launch_bounds__(256) void exchange_compact_kernel(XchgCompactArgs a
 // abort (a peer died inside the collective, ncclCommAbort) the kernels queued behind the
 // all-to-all still run; with the counts cleared they compact zero rows instead of replaying a
 // stale chunk of an older batch into the feature store.
-__global__ __launch_bounds__(64) void exchange_clear_kernel(ReqRec* recv, int32_t N, int32_t C) {
+// also copies the batch header {n, seq, now} from the pinned host slab to the device slab
+// (nullable): one thread of a kernel that runs anyway instead of a 16-byte copy job per step
+__global__ __launch_bounds__(64) void exchange_clear_kernel(ReqRec* recv, int32_t N, int32_t C, const int4* hdr_src,
+                                                            int4* hdr_dst) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p < N) recv[(size_t)p * (C + 1)].slot = 0;
+  if (p == 0 && hdr_src) *hdr_dst = *hdr_src;
 }
 
 struct XchgScatterArgs {
@@ -268,6 +273,8 @@ class XchgDriver {
       : cs_(S(cs)), ss_(S(ss)), ms_(S(ms)), xs_(S(xs)), ys_(S(ys)), depth_(depth), world_(world),
         cx_(cx.ptr()), cy_(cy.ptr()), r_(rccl("")) {
     if (cx.world() != world || cy.world() != world) throw std::runtime_error("XchgDriver: communicator world");
+    if (depth < 1 || depth > DEDUP_AHEAD)  // the copy of batch q relies on batch q - depth's state stage
+      throw std::runtime_error("XchgDriver: depth exceeds the dedup ring (DEDUP_AHEAD)");
     hip_ok(hipGetDevice(&device_), "get device");  // the serving core's threads bind to it
     ev_.resize(6 * depth);
     for (auto& e : ev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event create");
@@ -298,24 +305,6 @@ class XchgDriver {
     g.state = G(state);
     g.model = G(model);
     g.model_f = G(model_f);
-  }
-  // captured mode with the state stage (K1 + update, no collectives) as recorded launches
-  void set_state_ops(int C, int slot, std::shared_ptr<OpList> state) {
-    check_slot(slot);
-    graphs_[key(C, slot)].ostate = std::move(state);
-  }
-  // direct launch: the five stage bodies as recorded op lists; the driver issues the two
-  // all-to-alls and the D2H itself (the uncaptured path)
-  void set_ops(int C, int slot, std::shared_ptr<OpList> send, std::shared_ptr<OpList> post,
-               std::shared_ptr<OpList> state, std::shared_ptr<OpList> model, std::shared_ptr<OpList> model_f) {
-    check_slot(slot);
-    if (!send || !post || !state || !model || !model_f) throw std::runtime_error("XchgDriver: set_ops needs five lists");
-    Graphs& g = graphs_[key(C, slot)];
-    g.osend = std::move(send);
-    g.opost = std::move(post);
-    g.ostate = std::move(state);
-    g.omodel = std::move(model);
-    g.omodel_f = std::move(model_f);
   }
 
   // src: nbytes of prebuilt chunks ([N][C+1] ReqRec) copied into the slot's pinned buffer
@@ -409,14 +398,14 @@ class XchgDriver {
     return reinterpret_cast<uintptr_t>(&ops_);
   }
 
-  // Per-GPU D2H result path (instead of the result all-to-all): every owner copies its scored
-  // rows for ALL senders ([sender][C][W], the scatter's layout) into its block of a node-shared
-  // pinned host region [slot][owner][sender][C][W]; a sender reads its chunk of every owner's
-  // block. Completion is two-level: the slot's local event (this rank's D2H landed), then one
-  // release-published generation per (slot, owner) in the region's flag lines, polled until
-  // every owner reached the step. Reuse of a block is ordered by the next step's row
-  // all-to-all (no owner can copy step k + depth before every sender issued it, i.e. finished
-  // reading step k). The copy itself is a node of the captured model graph (engine/dp.py).
+  // Per-GPU D2H result path (instead of the result all-to-all): every owner's scatter kernel
+  // writes its scored rows for ALL senders ([sender][C][W]) straight into its block of a
+  // node-shared pinned host region [slot][owner][sender][C][W] (no copy job); a sender reads its
+  // chunk of every owner's block. Completion is two-level: the slot's local event (this rank's
+  // model stage, scatter included, finished), then one release-published generation per
+  // (slot, owner) in the region's flag lines, polled until every owner reached the step. Reuse
+  // of a block is ordered by the next step's row all-to-all (no owner can write step k + depth
+  // before every sender issued it, i.e. finished reading step k).
   void set_results_shm(uintptr_t base, size_t slot_stride, size_t owner_stride, uintptr_t flags, int rank) {
     if (!base || !flags || rank < 0 || rank >= world_) throw std::runtime_error("XchgDriver: results region");
     rshm_ = reinterpret_cast<char*>(base);
@@ -453,7 +442,6 @@ class XchgDriver {
   void submit_impl(int slot, int C, int seq, int64_t now, uintptr_t src, size_t nbytes, bool with_features) {
     auto it = graphs_.find(key(C, slot));
     ++gen_[size_t(slot)];  // every rank submits the same steps on the same slots: the same generations
-    if (rshm_ && !captured_) throw std::runtime_error("XchgDriver: the D2H result path needs the captured graphs");
     if (it == graphs_.end()) throw std::runtime_error("XchgDriver: no graphs for this chunk capacity / slot");
     const Graphs g = it->second;
     const Slot& sl = slots_[slot];
@@ -462,9 +450,7 @@ class XchgDriver {
     const size_t rbytes = (size_t)C * W;
     if (nbytes > sl.host_x_bytes || (size_t)world_ * xbytes > sl.host_x_bytes) throw std::runtime_error("XchgDriver: chunks exceed the slot buffer");
     if ((size_t)world_ * rbytes > sl.host_rr_bytes) throw std::runtime_error("XchgDriver: results exceed the slot buffer");
-    const bool direct = g.osend != nullptr;
-    if (with_features && !g.model_f && !direct) throw std::runtime_error("XchgDriver: no feature graph");
-    if (captured_ && direct) throw std::runtime_error("XchgDriver: direct launch needs set_captured(False)");
+    if (with_features && !g.model_f) throw std::runtime_error("XchgDriver: no feature graph");
     Range range("igp.xsubmit");
     const auto t0 = clk::now();
     if (src) std::memcpy(sl.host_x, reinterpret_cast<const void*>(src), nbytes);
@@ -486,12 +472,14 @@ class XchgDriver {
     if (captured_) {
       // the collectives and the D2H copy are nodes of the graphs (RCCL stream capture): three
       // launches per batch, the same shape as the single-GPU pipeline
+      // the slot's previous batch (q - depth) finished: its buffers are free, and its state
+      // stage - with every earlier one, the state stream runs in order - cleared this batch's
+      // dedup region (cleared by batch q - DEDUP_AHEAD, and depth <= DEDUP_AHEAD)
       if (done_recorded_[slot]) hip_ok(hipStreamWaitEvent(cs_, e_done, 0), "wait done");
-      if (hist_.size() == 2) hip_ok(hipStreamWaitEvent(cs_, E(hist_.front(), 3), 0), "wait state-2");
       hip_ok(hipGraphLaunch(g.send, cs_), "send+post graph");
       hip_ok(hipEventRecord(e_post, cs_), "record post");
       hip_ok(hipStreamWaitEvent(ss_, e_post, 0), "wait post");
-      stage(g.state, g.ostate, ss_, "state graph");  // recorded launches when set (set_state_ops)
+      hip_ok(hipGraphLaunch(g.state, ss_), "state graph");
       hip_ok(hipEventRecord(e_state, ss_), "record state");
       if (clock_) clock_->publish(e_state);  // K1 + multi-event update: readers order after it
       hip_ok(hipStreamWaitEvent(ms_, e_state, 0), "wait state");
@@ -501,25 +489,32 @@ class XchgDriver {
       st_[1] += std::chrono::duration<double, std::micro>(clk::now() - t1).count();
       st_[3] += 1;
       done_recorded_[slot] = true;
-      hist_.push_back(slot);
-      if (hist_.size() > 2) hist_.erase(hist_.begin());
       return;
     }
     if (done_recorded_[slot]) hip_ok(hipStreamWaitEvent(xs_, e_done, 0), "wait done");
-    stage(g.send, g.osend, xs_, "send graph");
+    hip_ok(hipGraphLaunch(g.send, xs_), "send graph");
     const auto t2 = clk::now();
     nccl_ok(r_, r_.all_to_all(sl.xsend, sl.xrecv, xbytes, kUint8, reinterpret_cast<void*>(cx_), xs_), "all_to_all rows");
     const auto t3 = clk::now();
     hop(xs_, cs_, e_x, "x -> copy");
-    if (hist_.size() == 2) hip_ok(hipStreamWaitEvent(cs_, E(hist_.front(), 3), 0), "wait state-2");
-    stage(g.post, g.opost, cs_, "post graph");
+    hip_ok(hipGraphLaunch(g.post, cs_), "post graph");
     hip_ok(hipEventRecord(e_post, cs_), "record post");
     hip_ok(hipStreamWaitEvent(ss_, e_post, 0), "wait post");
-    stage(g.state, g.ostate, ss_, "state graph");
+    hip_ok(hipGraphLaunch(g.state, ss_), "state graph");
     hip_ok(hipEventRecord(e_state, ss_), "record state");
     if (clock_) clock_->publish(e_state);
     hip_ok(hipStreamWaitEvent(ms_, e_state, 0), "wait state");
-    stage(with_features ? g.model_f : g.model, with_features ? g.omodel_f : g.omodel, ms_, "model graph");
+    hip_ok(hipGraphLaunch(with_features ? g.model_f : g.model, ms_), "model graph");
+    if (rshm_) {  // node-shared results: the model stage's scatter wrote them into the region
+      hip_ok(hipEventRecord(e_done, ms_), "record done");
+      auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+      st_[0] += us(t0, t1);
+      st_[1] += us(t1, t2) + us(t3, clk::now());
+      st_[2] += us(t2, t3);
+      st_[3] += 1;
+      done_recorded_[slot] = true;
+      return;
+    }
     hop(ms_, ys_, e_model, "model -> y");
     const auto t4 = clk::now();
     nccl_ok(r_, r_.all_to_all(sl.rsend, sl.rrecv, rbytes, kUint8, reinterpret_cast<void*>(cy_), ys_), "all_to_all results");
@@ -533,8 +528,6 @@ class XchgDriver {
     st_[2] += us(t2, t3) + us(t4, t5);
     st_[3] += 1;
     done_recorded_[slot] = true;
-    hist_.push_back(slot);
-    if (hist_.size() > 2) hist_.erase(hist_.begin());
   }
 
   void wait(int slot) {
@@ -571,13 +564,7 @@ class XchgDriver {
   using clk = std::chrono::steady_clock;
   struct Graphs {
     hipGraphExec_t send = nullptr, post = nullptr, state = nullptr, model = nullptr, model_f = nullptr;
-    // direct-launch mode (oplist.h): recorded stage launches instead of graph replays
-    std::shared_ptr<OpList> osend, opost, ostate, omodel, omodel_f;
   };
-  static void stage(hipGraphExec_t g, const std::shared_ptr<OpList>& ops, hipStream_t st, const char* what) {
-    if (ops) ops->run(st);
-    else hip_ok(hipGraphLaunch(g, st), what);
-  }
   struct Slot {
     char* host_hdr;
     char* host_x;
@@ -602,7 +589,6 @@ class XchgDriver {
   const Rccl& r_;
   std::vector<hipEvent_t> ev_;
   std::vector<bool> done_recorded_;
-  std::vector<int> hist_;
   std::vector<Slot> slots_;
   std::unordered_map<int64_t, Graphs> graphs_;
   double st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -649,8 +635,6 @@ void register_exchange(py::module_& m) {
            py::keep_alive<1, 9>(), py::keep_alive<1, 10>())
       .def("set_slot", &XchgDriver::set_slot)
       .def("set_graphs", &XchgDriver::set_graphs)
-      .def("set_ops", &XchgDriver::set_ops)
-      .def("set_state_ops", &XchgDriver::set_state_ops)
       .def("set_captured", &XchgDriver::set_captured)
       .def("set_results_shm", &XchgDriver::set_results_shm)
       .def("submit", &XchgDriver::submit)
@@ -684,17 +668,22 @@ void register_exchange(py::module_& m) {
     f(P<hipStream_t>(stream));
     hip_ok(hipGetLastError(), "exchange_compact");
   });
-  m.def("exchange_clear", [](uintptr_t recv, int N, int C, uintptr_t stream) {
+  m.def("exchange_clear", [](uintptr_t recv, int N, int C, uintptr_t stream, uintptr_t hdr_src, uintptr_t hdr_dst) {
     if (N < 1 || N > XCHG_MAX_WORLD || C < 1) throw std::runtime_error("exchange_clear: bad sizes");
+    if (!hdr_src != !hdr_dst) throw std::runtime_error("exchange_clear: header source and destination together");
     ReqRec* r = P<ReqRec*>(recv);
-    auto f = [r, N, C](hipStream_t st) { IGP_LAUNCH(exchange_clear_kernel, dim3(1), dim3(64), 0, st, r, N, C); };
+    const int4* hs = P<const int4*>(hdr_src);
+    int4* hd = P<int4*>(hdr_dst);
+    auto f = [r, N, C, hs, hd](hipStream_t st) {
+      IGP_LAUNCH(exchange_clear_kernel, dim3(1), dim3(64), 0, st, r, N, C, hs, hd);
+    };
     if (OpList* rec = recording()) {
       rec->ops.emplace_back(f);
       return;
     }
     f(P<hipStream_t>(stream));
     hip_ok(hipGetLastError(), "exchange_clear");
-  });
+  }, py::arg("recv"), py::arg("N"), py::arg("C"), py::arg("stream"), py::arg("hdr_src") = 0, py::arg("hdr_dst") = 0);
   m.def("exchange_scatter", [](uintptr_t hdr, uintptr_t route, uintptr_t res, uintptr_t feat, uintptr_t send, int C,
                                int cap, uintptr_t stream) {
     if (C < 1 || cap < 1) throw std::runtime_error("exchange_scatter: bad sizes");

@@ -184,7 +184,7 @@ class DpGpuScorer(GpuScorer):
     # ------------------------------------------------------------------ graph bodies
     @staticmethod
     def _direct_default() -> bool:
-        return os.environ.get("IGP_XCHG_DIRECT", "0") == "1"
+        return False  # the exchange stages are graph replays (see capture); CU masks pay for them
 
     def cap(self, C: int) -> int:
         return self.senders * C
@@ -192,10 +192,11 @@ class DpGpuScorer(GpuScorer):
     def _send_body(self, slot: int, C: int) -> None:
         sb, nb = self.slots[slot], self.world * (C + 1) * REQ
         K.memcpy_async(sb.xsend, self.host_x[slot], nb)
-        K.memcpy_async(sb.dev_slab, self.host_slab[slot], HDR_BYTES)
         # the receive buffer's chunk counts are zeroed ahead of the all-to-all: an aborted
-        # collective (failover) then leaves zero rows to compact instead of a stale chunk
-        hipk().exchange_clear(sb.xrecv.data_ptr(), self.world, C, torch.cuda.current_stream().cuda_stream)
+        # collective (failover) then leaves zero rows to compact instead of a stale chunk; the
+        # same kernel brings the batch header from the pinned slab (no 16-byte copy job)
+        hipk().exchange_clear(sb.xrecv.data_ptr(), self.world, C, torch.cuda.current_stream().cuda_stream,
+                              self.host_slab[slot].data_ptr(), sb.dev_slab.data_ptr())
 
     def _post_body(self, slot: int, C: int) -> None:
         sb, b = self.slots[slot], self.cap(C)
@@ -204,7 +205,10 @@ class DpGpuScorer(GpuScorer):
         if self.update_features:
             K.dedup_insert(self.store, self.cfg_dev, sb.req, b, sb.hdr)
 
-    def _xmodel_body(self, slot: int, C: int, with_features: bool) -> None:
+    def _xmodel_body(self, slot: int, C: int, with_features: bool, send: int = 0) -> None:
+        """The model, K5, and the scatter of each row's result (+ feature image) into its
+        sender's chunk of ``send`` (default: the slot's device buffer for the result
+        all-to-all)."""
         sb, b = self.slots[slot], self.cap(C)
         if sb.model is not None and sb.model.fuses_ensemble(b):
             ens = K.ensemble_args(sb.hdr, self.cfg_dev, sb.feat, sb.X, sb.model.step_out[-1], sb.res, b, self.metrics)
@@ -214,7 +218,7 @@ class DpGpuScorer(GpuScorer):
             K.ensemble(sb.hdr, self.cfg_dev, sb.feat, sb.X, ml, sb.res, b, self.metrics)
         hipk().exchange_scatter(sb.dev_slab.data_ptr(), sb.route.data_ptr(), sb.res.data_ptr(),
                                 (sb.fenc if sb.fenc is not None else sb.feat).data_ptr() if with_features else 0,
-                                sb.rsend.data_ptr(), C, b,
+                                send or sb.rsend.data_ptr(), C, b,
                                 torch.cuda.current_stream().cuda_stream)
 
     # ---- collectives captured into the graphs (RCCL stream capture, IGP_XCHG_CAPTURE=1)
@@ -235,16 +239,19 @@ class DpGpuScorer(GpuScorer):
         self._a2a_rows(slot, C)
         self._post_body(slot, C)
 
+    def _region(self, slot: int) -> int:
+        """This owner's block of the node-shared results region for ``slot`` (0: no region)."""
+        r = self.rshm
+        return 0 if r is None else r["base"] + slot * r["slot_stride"] + self.rank * r["owner_stride"]
+
     def _model_results_body(self, slot: int, C: int, with_features: bool) -> None:
-        self._xmodel_body(slot, C, with_features)
         if self.rshm is not None:
-            # per-GPU D2H: this owner's result chunks for every sender -> its block of the
-            # node-shared region (the senders read their chunk of every owner's block)
-            r, sb = self.rshm, self.slots[slot]
-            hipk().memcpy_async(r["base"] + slot * r["slot_stride"] + self.rank * r["owner_stride"],
-                                sb.rsend.data_ptr(), self.world * C * result_width(with_features),
-                                torch.cuda.current_stream().cuda_stream)
+            # node-shared results: the scatter writes this owner's rows for every sender straight
+            # into its block of the pinned host region (the senders read their chunk of every
+            # owner's block) - no result all-to-all and no D2H copy job
+            self._xmodel_body(slot, C, with_features, send=self._region(slot))
             return
+        self._xmodel_body(slot, C, with_features)
         self._a2a_results(slot, C, with_features)
 
     def capture(self) -> None:
@@ -253,12 +260,12 @@ class DpGpuScorer(GpuScorer):
         IGP_XCHG_CAPTURE=1 (default) the two all-to-alls and the D2H copy are captured into the
         send and model graphs too (three graph launches per batch)."""
         dev = self.device
-        # IGP_XCHG_DIRECT=1: the stage bodies as recorded launch lists (csrc/kernels/oplist.h)
-        # with the collectives issued by the driver. Off by default: same-box world-1 A/B 67.4 vs
-        # 100.9 M scores/s for the captured graphs (RCCL inside the graphs beats driver-issued
-        # collectives, profiles/r2/direct3)
-        self.direct = os.environ.get("IGP_XCHG_DIRECT", "0") == "1"
-        self.captured = (not self.direct and os.environ.get("IGP_XCHG_CAPTURE", "1") == "1"
+        # the stages are always graph replays: recorded direct launches with driver-issued
+        # collectives measured 67.4 vs 100.9 M scores/s at world 1 (profiles/r2/direct3), and the
+        # collective-free state stage as recorded launches 91.7 / 90.4 vs 90.7 / 104.0
+        # (profiles/r2/xab); both were removed in round 5
+        self.direct = False
+        self.captured = (os.environ.get("IGP_XCHG_CAPTURE", "1") == "1"
                          and self.xstream is self.cstream and self.ystream is self.mstream)
         with torch.cuda.device(dev):
             for C in self.cbuckets:
@@ -275,8 +282,8 @@ class DpGpuScorer(GpuScorer):
                         bodies = ((lambda: self._send_body(slot, C), self.xstream),
                                   (lambda: self._post_body(slot, C), self.cstream),
                                   (lambda: self._state_body(slot, self.cap(C)), self.stream),
-                                  (lambda: self._xmodel_body(slot, C, False), self.mstream),
-                                  (lambda: self._xmodel_body(slot, C, True), self.mstream))
+                                  (lambda: self._xmodel_body(slot, C, False, self._region(slot)), self.mstream),
+                                  (lambda: self._xmodel_body(slot, C, True, self._region(slot)), self.mstream))
                     for item in bodies:
                         if item is None:
                             gs.append(None)
@@ -286,11 +293,6 @@ class DpGpuScorer(GpuScorer):
                         with torch.cuda.stream(s):
                             body()
                         torch.cuda.current_stream().wait_stream(s)
-                        if self.direct:
-                            with K.Recorder() as r:
-                                body()
-                            gs.append(r.ops)
-                            continue
                         g = torch.cuda.CUDAGraph()
                         with K.graph_capture(g, s):
                             body()
@@ -306,22 +308,9 @@ class DpGpuScorer(GpuScorer):
                        self.host_rr[slot].data_ptr(), sb.xsend.data_ptr(), sb.xrecv.data_ptr(), sb.rsend.data_ptr(),
                        sb.rrecv.data_ptr(), self.xbytes_max, self.rbytes_max)
         for (C, slot), g in self.xgraphs.items():
-            if self.direct:
-                d.set_ops(C, slot, *g)
-            else:
-                d.set_graphs(C, slot, *[0 if x is None else x.raw_cuda_graph_exec() for x in g])
-        # IGP_XCHG_STATE_DIRECT=1 (captured mode): the collective-free state stage as recorded
-        # launches, the two stages with RCCL inside stay graphs
-        if self.captured and os.environ.get("IGP_XCHG_STATE_DIRECT", "0") == "1":
-            with torch.cuda.device(dev):
-                for (C, slot) in self.xgraphs:
-                    with K.Recorder() as r:
-                        self._state_body(slot, self.cap(C))
-                    d.set_state_ops(C, slot, r.ops)
+            d.set_graphs(C, slot, *[0 if x is None else x.raw_cuda_graph_exec() for x in g])
         d.set_captured(self.captured)
         if self.rshm is not None:
-            if not self.captured:
-                raise RuntimeError("the D2H result path needs the captured exchange graphs")
             r = self.rshm
             d.set_results_shm(r["base"], r["slot_stride"], r["owner_stride"], r["flags"], self.rank)
         if getattr(self, "state_clock", None) is not None:

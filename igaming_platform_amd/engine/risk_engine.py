@@ -1179,8 +1179,9 @@ class SpmdNode:
         rank, world = comm.rank, comm.world
         self.rank, self.world = rank, world
         prefix = comm.bcast_bytes(serving.shm_token().encode() if rank == 0 else None, 0).decode()
-        # IGP_XCHG_RESULTS=d2h: results return through a node-shared pinned region (each owner
-        # copies its rows for every sender D2H) instead of the result all-to-all over xGMI
+        # IGP_XCHG_RESULTS=d2h: results return through a node-shared pinned region (each owner's
+        # scatter kernel writes its rows for every sender into it over PCIe) instead of the result
+        # all-to-all over xGMI
         self.results_mode = os.environ.get("IGP_XCHG_RESULTS", "a2a")
         if self.results_mode not in ("a2a", "d2h"):
             raise ValueError("IGP_XCHG_RESULTS must be a2a or d2h")
