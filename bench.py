@@ -811,6 +811,12 @@ def serving_bench(a) -> None:
     stages.update(device_us_per_step=round(st["device_ns"] / max(int(st["steps"]), 1) / 1e3, 1),
                   device_steps=int(st["steps"]), empty_steps=int(st["empty_steps"]),
                   mean_rows_per_device_step=round(st["rows"] / max(int(st["steps"]), 1), 1))
+    # a step slot's cycle and the stepper's waits with rows queued (serve_core.h ServeStats)
+    stages.update({k[:-3] + "_us_per_step": round(st[k] / max(int(st["steps"]), 1) / 1e3, 1)
+                   for k in ("release_ns", "slot_wait_ns", "rows_wait_ns", "pack_ns", "submit_ns") if k in st})
+    if st.get("slot_waits"):
+        stages.update(slot_waits_per_step=round(st["slot_waits"] / max(int(st["steps"]), 1), 2),
+                      inflight_at_slot_wait=round(st["slot_wait_inflight"] / st["slot_waits"], 2))
     p99, p50 = float(np.percentile(lat, 99)), float(np.percentile(lat, 50))
     # where a request's time goes, per request (tails, not sums): queue = enqueue -> its first
     # device step formed, device = that step formed -> all its rows back

@@ -277,7 +277,12 @@ class XchgDriver {
       throw std::runtime_error("XchgDriver: depth exceeds the dedup ring (DEDUP_AHEAD)");
     hip_ok(hipGetDevice(&device_), "get device");  // the serving core's threads bind to it
     ev_.resize(6 * depth);
-    for (auto& e : ev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event create");
+    // the hop / post / state / model events only order work between this device's queues: no
+    // system-scope fence at the stage's end (as PipeDriver, driver.hip); the done event keeps it
+    // (the host reads the results from pinned memory after it)
+    const unsigned dev_flags = hipEventDisableTiming | (unsigned)hipEventDisableSystemFence;
+    for (size_t i = 0; i < ev_.size(); ++i)
+      hip_ok(hipEventCreateWithFlags(&ev_[i], i % 6 == 5 ? hipEventDisableTiming : dev_flags), "event create");
     done_recorded_.assign(depth, false);
     gen_.assign(size_t(depth), 0);
     slots_.resize(depth);
@@ -305,6 +310,21 @@ class XchgDriver {
     g.state = G(state);
     g.model = G(model);
     g.model_f = G(model_f);
+  }
+
+  // captured mode: the collective-free stages as recorded launches (oplist.h) instead of graph
+  // replays - the state stage (K1 + update), and with node-shared results the model stages too
+  // (model_f / model null: those stay graphs). A hipGraphLaunch costs ~20 us of host time even
+  // for a two-kernel graph (rocprofv3 HIP API trace, profiles/NOTES.md round 5), and the serving
+  // core issues every step from one thread.
+  void set_stage_ops(int C, int slot, std::shared_ptr<OpList> state, std::shared_ptr<OpList> model,
+                     std::shared_ptr<OpList> model_f) {
+    check_slot(slot);
+    if (!state || !model != !model_f) throw std::runtime_error("XchgDriver: set_stage_ops lists");
+    Graphs& g = graphs_[key(C, slot)];
+    g.ostate = std::move(state);
+    g.omodel = std::move(model);
+    g.omodel_f = std::move(model_f);
   }
 
   // src: nbytes of prebuilt chunks ([N][C+1] ReqRec) copied into the slot's pinned buffer
@@ -479,12 +499,22 @@ class XchgDriver {
       hip_ok(hipGraphLaunch(g.send, cs_), "send+post graph");
       hip_ok(hipEventRecord(e_post, cs_), "record post");
       hip_ok(hipStreamWaitEvent(ss_, e_post, 0), "wait post");
-      hip_ok(hipGraphLaunch(g.state, ss_), "state graph");
-      hip_ok(hipEventRecord(e_state, ss_), "record state");
+      // recorded stages bind their end event to their last kernel (no marker command)
+      if (g.ostate) {
+        if (!g.ostate->run_recording(ss_, e_state)) hip_ok(hipEventRecord(e_state, ss_), "record state");
+      } else {
+        hip_ok(hipGraphLaunch(g.state, ss_), "state graph");
+        hip_ok(hipEventRecord(e_state, ss_), "record state");
+      }
       if (clock_) clock_->publish(e_state);  // K1 + multi-event update: readers order after it
       hip_ok(hipStreamWaitEvent(ms_, e_state, 0), "wait state");
-      hip_ok(hipGraphLaunch(with_features ? g.model_f : g.model, ms_), "model+results graph");
-      hip_ok(hipEventRecord(e_done, ms_), "record done");
+      const std::shared_ptr<OpList>& om = with_features ? g.omodel_f : g.omodel;
+      if (om) {
+        if (!om->run_recording(ms_, e_done)) hip_ok(hipEventRecord(e_done, ms_), "record done");
+      } else {
+        hip_ok(hipGraphLaunch(with_features ? g.model_f : g.model, ms_), "model+results graph");
+        hip_ok(hipEventRecord(e_done, ms_), "record done");
+      }
       st_[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
       st_[1] += std::chrono::duration<double, std::micro>(clk::now() - t1).count();
       st_[3] += 1;
@@ -564,6 +594,7 @@ class XchgDriver {
   using clk = std::chrono::steady_clock;
   struct Graphs {
     hipGraphExec_t send = nullptr, post = nullptr, state = nullptr, model = nullptr, model_f = nullptr;
+    std::shared_ptr<OpList> ostate, omodel, omodel_f;  // set_stage_ops (captured mode)
   };
   struct Slot {
     char* host_hdr;
@@ -636,6 +667,8 @@ void register_exchange(py::module_& m) {
       .def("set_slot", &XchgDriver::set_slot)
       .def("set_graphs", &XchgDriver::set_graphs)
       .def("set_captured", &XchgDriver::set_captured)
+      .def("set_stage_ops", &XchgDriver::set_stage_ops, py::arg("C"), py::arg("slot"), py::arg("state"),
+           py::arg("model") = nullptr, py::arg("model_f") = nullptr)
       .def("set_results_shm", &XchgDriver::set_results_shm)
       .def("submit", &XchgDriver::submit)
       .def("device_ops", &XchgDriver::device_ops)

@@ -894,6 +894,8 @@ PYBIND11_MODULE(_native, m) {
         d["unary"] = t.unary; d["parse_ns"] = t.parse_ns; d["resolve_ns"] = t.resolve_ns; d["pack_ns"] = t.pack_ns;
         d["device_ns"] = t.device_ns; d["copy_ns"] = t.copy_ns; d["serialize_ns"] = t.serialize_ns;
         d["submit_ns"] = t.submit_ns; d["wait_errors"] = t.wait_errors; d["max_step_rows"] = t.max_step_rows;
+        d["release_ns"] = t.release_ns; d["slot_wait_ns"] = t.slot_wait_ns; d["rows_wait_ns"] = t.rows_wait_ns;
+        d["slot_waits"] = t.slot_waits; d["slot_wait_inflight"] = t.slot_wait_inflight;
         d["actions"] = py::make_tuple(t.actions[0], t.actions[1], t.actions[2], t.actions[3]);
         py::list dl;
         for (int k = 0; k < 11; ++k) dl.append(t.deciles[k]);

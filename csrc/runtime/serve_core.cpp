@@ -631,6 +631,11 @@ bool ServeCore::issue_step(std::unique_lock<std::mutex>& lk, bool allow_empty) {
   return true;
 }
 
+void ServeCore::note_wait(int64_t ServeStats::*field, int64_t ns) {
+  std::lock_guard<std::mutex> g(st_mu_);
+  st_.*field += ns;
+}
+
 void ServeCore::stepper_loop() {
   std::unique_lock<std::mutex> lk(q_mu_);
   const int64_t max_wait = int64_t(opt_.max_wait_us) * 1000;
@@ -686,12 +691,21 @@ void ServeCore::stepper_loop() {
         issue_step(lk, peer_ahead);
         continue;
       }
+      const int64_t w0 = now_ns();
       q_cv_.wait_for(lk, std::chrono::nanoseconds(std::max<int64_t>(max_wait - age, 1000)));
+      note_wait(&ServeStats::rows_wait_ns, now_ns() - w0);
       continue;
     }
     // nothing to issue: sleep until new work / a free slot; exchange ranks also watch the peers
+    const bool blocked = !slot && queued_rows_ > 0;
+    const int64_t w0 = blocked ? now_ns() : 0;
     if (exchange_) q_cv_.wait_for(lk, std::chrono::microseconds(50));
     else q_cv_.wait_for(lk, std::chrono::milliseconds(100));
+    if (blocked) {
+      note_wait(&ServeStats::slot_wait_ns, now_ns() - w0);
+      note_wait(&ServeStats::slot_waits, 1);
+      note_wait(&ServeStats::slot_wait_inflight, inflight_);
+    }
   }
 }
 
@@ -719,6 +733,7 @@ void ServeCore::completion_loop() {
       }
     }
     const int64_t t = now_ns();
+    st->t_done = t;
     {
       std::lock_guard<std::mutex> g(st_mu_);
       st_.device_ns += t - st->t_submit;
@@ -816,6 +831,11 @@ void ServeCore::record_decisions(const ResultRec* r, int n) {
 
 void ServeCore::release_step_ref(Step* st) {
   if (st->refs.fetch_sub(1) != 1) return;
+  if (st->t_done) {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.release_ns += now_ns() - st->t_done;
+  }
+  st->t_done = 0;
   {
     std::lock_guard<std::mutex> lk(q_mu_);
     free_slots_.push_back(st->slot);

@@ -91,6 +91,10 @@ struct ServeStats {
   int64_t items = 0, rows = 0, steps = 0, empty_steps = 0, unary = 0;
   int64_t parse_ns = 0, resolve_ns = 0, pack_ns = 0, device_ns = 0, copy_ns = 0, serialize_ns = 0, queue_ns = 0;
   int64_t submit_ns = 0, wait_errors = 0, max_step_rows = 0;
+  // where a step's slot spends its cycle: device wait returned -> every segment finished (the
+  // slot is free again), and the stepper's waits with rows queued: for the next slot (in-order
+  // slots of the exchange) or for more rows (a step is formed at 7/8 full or after max_wait)
+  int64_t release_ns = 0, slot_wait_ns = 0, rows_wait_ns = 0, slot_waits = 0, slot_wait_inflight = 0;
   // cumulative decision counters (never reset)
   int64_t actions[4] = {0, 0, 0, 0};
   int64_t deciles[11] = {0};
@@ -195,7 +199,7 @@ class ServeCore {
     int32_t seq = 0;
     int n = 0;
     bool wf = false;
-    int64_t t_submit = 0;
+    int64_t t_submit = 0, t_done = 0;
     std::vector<Seg> segs;
     std::atomic<int> refs{0};
     bool failed = false;
@@ -203,6 +207,7 @@ class ServeCore {
   };
 
   void stepper_loop();
+  void note_wait(int64_t ServeStats::*field, int64_t ns);
   void completion_loop();
   void finisher_loop();
   void deliver(std::vector<Done>&& outs);

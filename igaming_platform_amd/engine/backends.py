@@ -294,8 +294,10 @@ class GpuBackend:
         # per shard, kept across scorer rebuilds (failover, hot reload)
         from ..ops import kernels as _K
         self.state_clock = _K._mod().StateClock()
-        self.scorer = self._make_scorer(plan, model, (cfg.gpu.serve_depth if cfg.gpu.native_serving else 2)
-                                         if exchange is None else 3)
+        # the exchange scorer too runs serve_depth slots (it was pinned to 3 while the dedup ring
+        # held 4 regions; at 3 the serving core's stepper waited ~50 us per step for a slot,
+        # round-5 slot-cycle stats)
+        self.scorer = self._make_scorer(plan, model, cfg.gpu.serve_depth if cfg.gpu.native_serving else 2)
         if capture and self.scorer.use_graphs:
             self.scorer.capture()
         self._lock = threading.RLock()

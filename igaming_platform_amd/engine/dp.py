@@ -184,7 +184,10 @@ class DpGpuScorer(GpuScorer):
     # ------------------------------------------------------------------ graph bodies
     @staticmethod
     def _direct_default() -> bool:
-        return False  # the exchange stages are graph replays (see capture); CU masks pay for them
+        # the state / model stages are recorded launches (see capture): no CU masks (same-box
+        # world-1 A/B, 3 runs each: none 77.9 / 78.1 / 71.7 vs half 68.3 / 69.0 / 74.4 M
+        # scores/s, profiles/r5/xchg)
+        return True
 
     def cap(self, C: int) -> int:
         return self.senders * C
@@ -309,6 +312,25 @@ class DpGpuScorer(GpuScorer):
                        sb.rrecv.data_ptr(), self.xbytes_max, self.rbytes_max)
         for (C, slot), g in self.xgraphs.items():
             d.set_graphs(C, slot, *[0 if x is None else x.raw_cuda_graph_exec() for x in g])
+        # captured mode: the collective-free stages also as recorded launches (oplist.h), which
+        # the driver issues instead of their graphs - the state stage always, the model stages
+        # when the results go through the node-shared region (no result all-to-all inside them).
+        # A two-kernel hipGraphLaunch costs ~20 us of host time and one thread issues every step
+        # (profiles/NOTES.md round 5). GRU plans keep graphs (as the single-GPU pipeline).
+        self.stage_ops = self.captured and not any(s.kind == "gru" for s in (self.plan.steps if self.plan else []))
+        if self.stage_ops:
+            with torch.cuda.device(dev):
+                for (C, slot) in self.xgraphs:
+                    lists = []
+                    bodies = [lambda: self._state_body(slot, self.cap(C))]
+                    if self.rshm is not None:
+                        bodies += [lambda: self._xmodel_body(slot, C, False, self._region(slot)),
+                                   lambda: self._xmodel_body(slot, C, True, self._region(slot))]
+                    for body in bodies:
+                        with K.Recorder() as r:
+                            body()
+                        lists.append(r.ops)
+                    d.set_stage_ops(C, slot, *lists)
         d.set_captured(self.captured)
         if self.rshm is not None:
             r = self.rshm

@@ -118,6 +118,7 @@ def test_spmd_engine_world1_matches_plain_gpu_engine(monkeypatch, results):
         plain = RiskEngine(cfg, backend="gpu", capacity=1024)
         assert spmd.local.scorer.__class__.__name__ == "DpGpuScorer"
         assert (spmd.local.scorer.rshm is not None) == (results == "d2h")
+        assert spmd.local.scorer.stage_ops  # state (+ d2h: model) stages as recorded launches
         if results == "d2h":
             assert not os.path.exists(spmd.local.scorer.rshm["path"])  # unlinked once every rank mapped it
         rng = np.random.default_rng(2)
