@@ -1182,7 +1182,8 @@ class SpmdNode:
         # IGP_XCHG_RESULTS=d2h: results return through a node-shared pinned region (each owner's
         # scatter kernel writes its rows for every sender into it over PCIe) instead of the result
         # all-to-all over xGMI
-        self.results_mode = os.environ.get("IGP_XCHG_RESULTS", "a2a")
+        # (default: same-box world-1 A/B 95 vs 86 M scores/s, profiles/r5/xchg)
+        self.results_mode = os.environ.get("IGP_XCHG_RESULTS", "d2h")
         if self.results_mode not in ("a2a", "d2h"):
             raise ValueError("IGP_XCHG_RESULTS must be a2a or d2h")
         rshm = f"{prefix}-res" if (backend == "gpu" and self.results_mode == "d2h") else None
