@@ -9,13 +9,8 @@
 // objects, replay bookkeeping) while the GPU needs ~60 us, so the host bounded throughput
 // (rocprofv3 timeline: GPU 58 % busy). The driver issues the same sequence with raw HIP calls
 // on the graphs' exec handles, writes the batch header and copies the packed request rows
-// into the pinned slab itself, all with the GIL released.
-//
-// Asynchronous issue (set_async(true)): submit() only queues the batch; a driver thread of its
-// own does the row copy, the header and the launches, so the caller's per-batch Python work
-// (pool selection, bookkeeping, the wait for an older batch) overlaps the ~40 us of HIP calls
-// instead of adding to them. wait(slot) / query(slot) / model_event(slot) first wait for the
-// slot's queued batch to be issued; issue errors resurface on the next call.
+// into the pinned slab itself, all with the GIL released. (An asynchronous issue thread and a
+// one-stream serial mode were measured slower and removed in round 5: profiles/NOTES.md.)
 #include "hostwait.h"
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
@@ -25,15 +20,10 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
-#include <condition_variable>
 #include <cstring>
-#include <deque>
-#include <exception>
 #include <memory>
-#include <mutex>
 #include <stdexcept>
 #include <string>
-#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -104,29 +94,13 @@ class PipeDriver {
     ext_events_ = !(xe && atoi(xe) == 0);
   }
   ~PipeDriver() {
-    stop_worker();
     for (auto& e : ev_) (void)hipEventDestroy(e);
     for (auto& e : pe_) (void)hipEventDestroy(e);
   }
 
-  // serial mode: batches of up to `max_bucket` rows run all stages on one stream (direct launch
-  // only); larger ones keep the three-stream pipeline
-  void set_serial(int max_bucket) { serial_max_ = max_bucket; }
-
   // stage-end events bound to the stages' last kernels (oplist.h) instead of recorded markers
   void set_ext_events(bool on) { ext_events_ = on; }
   bool ext_events() const { return ext_events_; }
-
-  void set_async(bool on) {
-    if (on && !worker_.joinable()) {
-      pending_.assign(depth_, 0);
-      stop_ = false;
-      worker_ = std::thread([this] { loop(); });
-    } else if (!on) {
-      stop_worker();
-    }
-    async_ = on;
-  }
 
   // the slot's pinned result rows (ResultRec [bucket]) and FeatRec rows: what the native
   // serving core reads after wait (device_ops)
@@ -183,7 +157,6 @@ class PipeDriver {
       auto* d = static_cast<PipeDriver*>(ctx);
       try {
         bind_device(d->device_);
-        d->drain_slot(slot);
         hipEvent_t e = d->ev_[3 * slot + 2];
         if (timeout_us < 0) {
           hip_ok(hipEventSynchronize(e), "sync model");
@@ -240,16 +213,6 @@ class PipeDriver {
     auto it = graphs_.find(key(bucket, slot));
     if (it == graphs_.end()) throw std::runtime_error("PipeDriver: no graphs for this bucket/slot");
     const Cmd c{slot, bucket, n, seq, now, rows, with_features, it->second};
-    if (async_) {
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        rethrow_locked();
-        q_.push_back(c);
-        ++pending_[slot];
-      }
-      cv_.notify_one();
-      return;
-    }
     py::gil_scoped_release nogil;
     issue(c);
   }
@@ -280,50 +243,6 @@ class PipeDriver {
     Graphs g;
   };
 
-  void loop() {
-    std::unique_lock<std::mutex> lk(mu_);
-    for (;;) {
-      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
-      if (q_.empty()) return;
-      const Cmd c = q_.front();
-      q_.pop_front();
-      lk.unlock();
-      std::exception_ptr err;
-      try {
-        issue(c);
-      } catch (...) {
-        err = std::current_exception();
-      }
-      lk.lock();
-      if (err && !err_) err_ = err;
-      --pending_[c.slot];
-      done_cv_.notify_all();
-    }
-  }
-  void stop_worker() {
-    if (!worker_.joinable()) return;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    worker_.join();
-  }
-  void rethrow_locked() {
-    if (err_) {
-      std::exception_ptr e = err_;
-      err_ = nullptr;
-      std::rethrow_exception(e);
-    }
-  }
-  // async mode: block until the slot's queued batches are issued
-  void drain_slot(int slot) {
-    if (!async_) return;
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return pending_[slot] == 0; });
-    rethrow_locked();
-  }
-
   void issue(const Cmd& cmd) {
     const int slot = cmd.slot, n = cmd.n, seq = cmd.seq;
     const int64_t now = cmd.now;
@@ -340,36 +259,10 @@ class PipeDriver {
     h->seq = seq;
     h->now = now;
     hipEvent_t ce = ev_[3 * slot], se = ev_[3 * slot + 1], me = ev_[3 * slot + 2];
-    const bool serial = cmd.bucket <= serial_max_ && g.oc && g.os && g.om && g.omf;
-    if (serial && last_seq_ >= 0 && !serial_hist_) {
-      // the previous batch ran as three stages: its state work (store updates) comes first
-      if (hipEvent_t e = post_event(last_seq_)) hip_ok(hipStreamWaitEvent(cs_, e, 0), "wait previous state");
-    }
-    serial_hist_ = serial;
     const int prev_seq = slot_seq_[slot];
     hipEvent_t pe = pe_[ring(seq)];
     pe_seq_[ring(seq)] = seq;
     slot_seq_[slot] = seq;
-    last_seq_ = seq;
-    if (serial) {
-      // serial mode (small micro-batches): every stage on the copy stream in order - no
-      // cross-queue waits (~12 us each when unsatisfied) and no event calls but the completion
-      // record; stream order gives the slot / dedup-region / store ordering
-      const auto ts = clk::now();
-      g.oc->run(cs_);
-      g.os->run(cs_);
-      if (g.osu) g.osu->run(cs_);
-      (with_features ? g.omf : g.om)->run(cs_);
-      hip_ok(hipEventRecord(pe, cs_), "record post");
-      if (clock_) clock_->publish(pe);  // the batch's whole state stage (read-your-writes)
-      hip_ok(hipEventRecord(me, cs_), "record model");
-      st_[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
-      st_[2] += std::chrono::duration<double, std::micro>(clk::now() - ts).count();
-      st_[5] += 1;
-      host_done_[slot] = 0;
-      recorded_[3 * slot] = recorded_[3 * slot + 1] = recorded_[3 * slot + 2] = true;
-      return;
-    }
     // the slot's previous batch: skipped when the host already saw it complete (wait(slot))
     if (recorded_[3 * slot + 2] && !host_done_[slot]) hip_ok(hipStreamWaitEvent(cs_, me, 0), "wait model");
     host_done_[slot] = 0;
@@ -424,7 +317,6 @@ class PipeDriver {
   void wait(int slot) {
     if (slot < 0 || slot >= depth_) throw std::runtime_error("PipeDriver: bad slot");
     py::gil_scoped_release nogil;
-    drain_slot(slot);
     Range range("igp.wait");
     const auto t0 = clk::now();
     hip_ok(hipEventSynchronize(ev_[3 * slot + 2]), "sync model");
@@ -449,19 +341,11 @@ class PipeDriver {
   }
 
   bool query(int slot) {
-    if (async_) {
-      std::lock_guard<std::mutex> lk(mu_);
-      if (pending_[slot] > 0) return false;
-    }
     return hipEventQuery(ev_[3 * slot + 2]) == hipSuccess;
   }
 
-  // the slot's model-stream event (completes with its batch; async mode: after it is issued)
+  // the slot's model-stream event (completes with its batch)
   uintptr_t model_event(int slot) {
-    {
-      py::gil_scoped_release nogil;
-      drain_slot(slot);
-    }
     return reinterpret_cast<uintptr_t>(ev_[3 * slot + 2]);
   }
 
@@ -477,23 +361,11 @@ class PipeDriver {
   std::array<hipEvent_t, DEDUP_RING> pe_{};
   std::array<int, DEDUP_RING> pe_seq_{};  // the batch each ring event was last recorded for
   std::vector<int> slot_seq_;             // the slot's last batch
-  int last_seq_ = -1;
   std::vector<bool> recorded_;
   std::vector<uint8_t> host_done_;  // wait(slot) returned since the slot's last submit (bytes: set by waiter threads)
   std::shared_ptr<StateClock> clock_;
   std::unordered_map<int64_t, Graphs> graphs_;
-  int serial_max_ = 0;
-  bool serial_hist_ = false;  // the last issued batch ran in serial mode
-  // async issue
-  bool async_ = false;
   bool ext_events_ = true;
-  bool stop_ = false;
-  std::thread worker_;
-  std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
-  std::deque<Cmd> q_;
-  std::vector<int> pending_;
-  std::exception_ptr err_;
   // native serving core interface
   std::vector<char*> host_res_, host_feat_;
   std::vector<int> buckets_;
@@ -519,14 +391,12 @@ void register_driver(py::module_& m) {
       .def("device_ops", &PipeDriver::device_ops)
       .def("set_ops", &PipeDriver::set_ops)
       .def("set_state_update", &PipeDriver::set_state_update)
-      .def("set_serial", &PipeDriver::set_serial)
       .def("set_ext_events", &PipeDriver::set_ext_events)
       .def_property_readonly("ext_events", &PipeDriver::ext_events)
       .def("submit", &PipeDriver::submit)
       .def("wait", &PipeDriver::wait)
       .def("query", &PipeDriver::query)
       .def("model_event", &PipeDriver::model_event)
-      .def("set_async", &PipeDriver::set_async)
       .def("stats", &PipeDriver::stats);
 }
 

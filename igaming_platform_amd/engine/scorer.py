@@ -115,7 +115,6 @@ class GpuScorer:
         self.model = model
         self.update_features = update_features
         self.direct = False
-        self.serial = False
         self.use_graphs = cfg.gpu.use_graphs if use_graphs is None else use_graphs
         self.buckets = sorted(set(int(b) for b in cfg.gpu.buckets))
         self.bmax = self.buckets[-1]
@@ -150,8 +149,6 @@ class GpuScorer:
         # Only with a model plan: the heuristic model stream is just the ensemble.
         split = os.environ.get("IGP_CU_SPLIT", "auto")
         if split == "auto":
-            # serial mode (small micro-batches, see capture) runs every stage on one stream: give
-            # that stream the whole GPU
             # With direct launch the masks no longer pay (same-box A/Bs, 3000-step runs: no split
             # 107.6 vs half 101.8 M scores/s, 5 x 600 steps on another box: median 130.5 vs 127.5;
             # profiles/r2/cu, cu3): they were a win for the graph-replay pipeline only
@@ -380,17 +377,9 @@ class GpuScorer:
                             d.set_ops(b, slot, *lists[:4])
                             if split:
                                 d.set_state_update(b, slot, lists[4])
-            # serial mode (IGP_SERIAL_MAX_BUCKET > 0): batches up to that many rows run the three
-            # stages back to back on one stream. Off: the overlap of batch i+1's K1 with batch i's
-            # model is worth more than the hand-offs it costs even at 1024 rows (same box: cfg2
-            # 22.6 vs 11.0 M scores/s, cfg3 107 vs 57 M; profiles/r2/serial)
-            smax = int(os.environ.get("IGP_SERIAL_MAX_BUCKET", "0")) if self.direct else 0
-            self.serial = self.direct and self.bmax <= smax   # every bucket of this scorer runs serially
-            if self.direct and smax > 0:
-                d.set_serial(smax)  # buckets <= smax serial, larger ones three-stream
-            # IGP_ASYNC_SUBMIT=1: the driver's own thread issues each batch (csrc/kernels/driver.hip)
-            if os.environ.get("IGP_ASYNC_SUBMIT", "0") == "1":
-                d.set_async(True)
+            # (round 5 removed the one-stream serial mode - cfg2 22.6 vs 11.0 M, cfg3 107 vs 57 M,
+            # profiles/r2/serial - and the asynchronous issue thread - cfg3 118 vs 127 M,
+            # profiles/r2/direct3: both measured slower)
             self.driver = d
 
     def bucket_for(self, n: int) -> int:

@@ -46,8 +46,6 @@ def gpu_device(scorer):
     if getattr(scorer, "xdriver", None) is not None:
         return XchgDevice(scorer, scorer.cbuckets[-1])
     d = getattr(scorer, "driver", None)
-    if d is None or getattr(scorer, "serial", False):
-        return None
     return d
 
 

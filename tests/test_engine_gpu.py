@@ -245,30 +245,27 @@ def test_gpu_snapshot_restore(tmp_path):
         assert g.get_features(f"acc-{i}", now=NOW + 3).tobytes() == h.get_features(f"acc-{i}", now=NOW + 3).tobytes()
 
 
-@pytest.mark.parametrize("env", [dict(IGP_DIRECT_LAUNCH="1", IGP_SPLIT_STATE="1", IGP_SERIAL_MAX_BUCKET="0"),
-                                 dict(IGP_DIRECT_LAUNCH="1", IGP_SPLIT_STATE="0", IGP_SERIAL_MAX_BUCKET="0"),
-                                 dict(IGP_DIRECT_LAUNCH="1", IGP_SERIAL_MAX_BUCKET="4096"),
-                                 dict(IGP_DIRECT_LAUNCH="1", IGP_SERIAL_MAX_BUCKET="64"),  # mixed
-                                 dict(IGP_DIRECT_LAUNCH="1", IGP_ASYNC_SUBMIT="1", IGP_SERIAL_MAX_BUCKET="0"),
-                                 dict(IGP_DIRECT_LAUNCH="1", IGP_EXT_EVENTS="0", IGP_SERIAL_MAX_BUCKET="0")])
-def test_direct_launch_and_async_issue_match_graph_replay(env, monkeypatch):
+@pytest.mark.parametrize("env", [dict(IGP_DIRECT_LAUNCH="1", IGP_SPLIT_STATE="1"),
+                                 dict(IGP_DIRECT_LAUNCH="1", IGP_SPLIT_STATE="0"),
+                                 dict(IGP_DIRECT_LAUNCH="1", IGP_EXT_EVENTS="0")])
+def test_direct_launch_matches_graph_replay(env, monkeypatch):
     """The native driver's direct-launch mode (recorded kernel launches instead of graph
-    replays, csrc/kernels/oplist.h) and its asynchronous issue thread give bit-identical results,
-    features and feature-store state to the graph-replay pipeline (mixed batch sizes, hot
-    accounts with several events per batch)."""
+    replays, csrc/kernels/oplist.h), with the state stage split or whole and the stage-end
+    events bound to kernels or recorded, gives bit-identical results, features and
+    feature-store state to the graph-replay pipeline (mixed batch sizes, hot accounts with
+    several events per batch)."""
     import torch
     from igaming_platform_amd.utils import benchkit
     from igaming_platform_amd.utils.synth import NOW0, make_requests
     dev = torch.device("cuda", 0)
     monkeypatch.setenv("IGP_DIRECT_LAUNCH", "0")       # the reference: graph replay
-    bk = [64, 512]  # with IGP_SERIAL_MAX_BUCKET=64 small batches run serially, large ones on 3 streams
+    bk = [64, 512]
     A = benchkit.build("cfg3", 512, 4096, dev, depth=3, history_batches=4, hot_frac=0.2, buckets=bk)
     assert not A.scorer.direct
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     B = benchkit.build("cfg3", 512, 4096, dev, depth=3, history_batches=4, hot_frac=0.2, buckets=bk)
     assert B.scorer.direct
-    assert B.scorer.serial == (int(env["IGP_SERIAL_MAX_BUCKET"]) >= 512)
     assert B.scorer.driver.ext_events == (env.get("IGP_EXT_EVENTS", "1") != "0")
     rng = np.random.default_rng(5)
     batches = [make_requests(A.pop, n, rng, NOW0, hot_frac=0.2) for n in (512, 300, 512, 17, 512, 64, 200)]
@@ -297,7 +294,6 @@ def test_pipelined_direct_launch_matches_graph_replay(ext, monkeypatch):
     from igaming_platform_amd.utils.synth import NOW0, make_requests
     dev = torch.device("cuda", 0)
     monkeypatch.setenv("IGP_DIRECT_LAUNCH", "0")
-    monkeypatch.setenv("IGP_SERIAL_MAX_BUCKET", "0")
     A = benchkit.build("cfg3", 2048, 4096, dev, depth=3, history_batches=4, hot_frac=0.3, buckets=[2048])
     monkeypatch.setenv("IGP_DIRECT_LAUNCH", "1")
     monkeypatch.setenv("IGP_EXT_EVENTS", ext)
