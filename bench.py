@@ -630,6 +630,19 @@ def dp_bench(a, world: int, rank: int, dev) -> None:
     return out
 
 
+def _hot_by_thread(samples, names) -> dict:
+    """{thread name: [(function, samples)]} from the native SIGPROF sampler (tools/host_profile.py)."""
+    import collections
+    import host_profile
+    pcs, tids = samples
+    maps, base = host_profile._maps()
+    syms = host_profile.symbolise(pcs, maps, base)
+    hot = collections.defaultdict(collections.Counter)
+    for sym, tid in zip(syms, tids):
+        hot[names.get(int(tid), ("exited", 0))[0]][sym] += 1
+    return {k: c.most_common(12) for k, c in hot.items()}
+
+
 def serving_bench(a) -> None:
     """The serving objects end to end, every rank ingesting (bench.py --gpus N runs
     the serving path, not a hand-built scorer). Per rank:
@@ -785,12 +798,19 @@ def serving_bench(a) -> None:
     if threads_out:
         import host_profile
         cpu0, proc0 = host_profile.thread_cpu(), os.times()
+        if os.environ.get("IGP_BENCH_SAMPLE") == "1":  # + the hottest functions per thread name
+            from igaming_platform_amd.native import native as _nat
+            _nat().sampler_start(4000, 1 << 21)
     t0 = time.perf_counter()
     run(a.steps * per_step, NOW0, True)
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
     if threads_out:
+        samples = None
+        if os.environ.get("IGP_BENCH_SAMPLE") == "1":
+            from igaming_platform_amd.native import native as _nat
+            samples = _nat().sampler_stop()
         cpu1, proc1 = host_profile.thread_cpu(), os.times()
         busy, alive = {}, 0.0
         for tid, (name, cpu) in cpu1.items():
@@ -803,7 +823,8 @@ def serving_bench(a) -> None:
         with open(threads_out, "w") as f:
             json.dump({"elapsed_s": elapsed, "cpu_fraction_by_thread_name": busy,
                        "ingress_threads_cores": round(max(0.0, total - alive) / elapsed, 2),
-                       "process_cores": round(total / elapsed, 2)}, f)
+                       "process_cores": round(total / elapsed, 2),
+                       "hot": _hot_by_thread(samples, cpu1) if samples is not None else None}, f)
     st = core.stats(True)
     rows = max(int(st["rows"]), 1)
     stages = {k[:-3] + "_ns_per_row": round(st[k] / rows, 1)
