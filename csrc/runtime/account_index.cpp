@@ -229,7 +229,7 @@ void AccountIndex::lookup(const std::vector<std::string>& ids, const std::vector
 
 void AccountIndex::lookup_views(const std::string_view* ids, const uint64_t* h, size_t n, bool insert_, int32_t* slots,
                                 uint8_t* fresh, const uint8_t* sel) {
-  constexpr size_t kAhead = 16;  // probe lines in flight
+  constexpr size_t kAhead = 16;  // probe lines in flight (32: same, 64: slower; profiles/r5/host)
   // pass 1: probe every row (prefetched); an exact inline key settles the row on the spot (one
   // miss per row); long ids remember their candidate and prefetch its arena bytes
   std::vector<int64_t> cand;
