@@ -1,5 +1,7 @@
 #include "account_index.h"
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -109,16 +111,54 @@ constexpr HexTable kHex;
 constexpr uint8_t kPos[16] = {0, 2, 4, 6, 9, 11, 14, 16, 19, 21, 24, 26, 28, 30, 32, 34};
 }  // namespace
 
-uint32_t AccountIndex::encode_key(std::string_view id, uint8_t key[16]) {
+// The 32 hex digits of a canonical lower-case UUID -> 16 key bytes, SSSE3: three unaligned loads,
+// byte shuffles that drop the hyphens, a range check and a nibble pack (the table loop above was
+// ~13 % of the ingress threads' samples; resolve 42 -> 35 ns/row, serving throughput unchanged:
+// not ingress-bound, profiles/r5/host/keys). false: not 32 lower-case hex digits.
+__attribute__((target("ssse3"))) static bool uuid_hex_simd(const unsigned char* c, uint8_t key[16]) {
+  const __m128i v0 = _mm_loadu_si128(reinterpret_cast<const __m128i*>(c));       // chars 0..15
+  const __m128i v1 = _mm_loadu_si128(reinterpret_cast<const __m128i*>(c + 16));  // chars 16..31
+  const __m128i v2 = _mm_loadu_si128(reinterpret_cast<const __m128i*>(c + 20));  // chars 20..35
+  const char z = char(0x80);
+  // key bytes 0..7 <- chars 0-7, 9-12, 14-17; key bytes 8..15 <- chars 19-22, 24-35
+  const __m128i a = _mm_or_si128(
+      _mm_shuffle_epi8(v0, _mm_setr_epi8(0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 11, 12, 14, 15, z, z)),
+      _mm_shuffle_epi8(v1, _mm_setr_epi8(z, z, z, z, z, z, z, z, z, z, z, z, z, z, 0, 1)));
+  const __m128i b = _mm_or_si128(
+      _mm_shuffle_epi8(v1, _mm_setr_epi8(3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15, z, z, z, z)),
+      _mm_shuffle_epi8(v2, _mm_setr_epi8(z, z, z, z, z, z, z, z, z, z, z, z, 12, 13, 14, 15)));
+  auto nibbles = [](__m128i v, __m128i& ok) {
+    const __m128i d = _mm_sub_epi8(v, _mm_set1_epi8('0'));
+    const __m128i h = _mm_sub_epi8(v, _mm_set1_epi8('a'));
+    const __m128i is_d = _mm_cmpeq_epi8(_mm_min_epu8(d, _mm_set1_epi8(9)), d);  // d <= 9 unsigned
+    const __m128i is_h = _mm_cmpeq_epi8(_mm_min_epu8(h, _mm_set1_epi8(5)), h);  // h <= 5 unsigned
+    ok = _mm_and_si128(ok, _mm_or_si128(is_d, is_h));
+    return _mm_or_si128(_mm_and_si128(is_d, d), _mm_and_si128(is_h, _mm_add_epi8(h, _mm_set1_epi8(10))));
+  };
+  __m128i ok = _mm_set1_epi8(char(0xff));
+  const __m128i na = nibbles(a, ok), nb = nibbles(b, ok);
+  if (_mm_movemask_epi8(ok) != 0xffff) return false;
+  const __m128i w = _mm_set1_epi16(0x0110);  // even char x 16 + odd char
+  const __m128i packed = _mm_packus_epi16(_mm_maddubs_epi16(na, w), _mm_maddubs_epi16(nb, w));
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(key), packed);
+  return true;
+}
+
+// the scalar decode (table lookups): the reference the SIMD path is tested against
+static bool uuid_hex_scalar(const unsigned char* c, uint8_t key[16]) {
+  uint32_t bad = 0;
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t hi = kHex.v[c[kPos[k]]], lo = kHex.v[c[kPos[k] + 1]];
+    bad |= hi | lo;
+    key[k] = uint8_t(hi << 4 | lo);
+  }
+  return !(bad & 0x10);
+}
+
+uint32_t AccountIndex::encode_key(std::string_view id, uint8_t key[16], bool scalar) {
   const unsigned char* c = reinterpret_cast<const unsigned char*>(id.data());
   if (id.size() == 36 && c[8] == '-' && c[13] == '-' && c[18] == '-' && c[23] == '-') {
-    uint32_t bad = 0;  // branch-free: 32 table lookups, one check at the end
-    for (int k = 0; k < 16; ++k) {
-      const uint32_t hi = kHex.v[c[kPos[k]]], lo = kHex.v[c[kPos[k] + 1]];
-      bad |= hi | lo;
-      key[k] = uint8_t(hi << 4 | lo);
-    }
-    if (!(bad & 0x10)) return kExact | kUuid;
+    if (scalar ? uuid_hex_scalar(c, key) : uuid_hex_simd(c, key)) return kExact | kUuid;
   }
   std::memset(key, 0, 16);
   if (id.size() <= 15) {

@@ -81,7 +81,7 @@ class AccountIndex {
   static constexpr uint32_t kExact = 1u << 31, kUuid = 1u << 30, kOffMask = (1u << 30) - 1;
  public:
   // the inline key of an id: returns kExact [| kUuid] when the key IS the id (exact encoding)
-  static uint32_t encode_key(std::string_view id, uint8_t key[16]);
+  static uint32_t encode_key(std::string_view id, uint8_t key[16], bool scalar = false);
  private:
   bool key_equal(const Entry& e, std::string_view id, uint32_t form, const uint8_t* key) const;
 

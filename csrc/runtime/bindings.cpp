@@ -378,6 +378,12 @@ PYBIND11_MODULE(_native, m) {
     return out;
   });
 
+  // the inline key of an id (form bits, 16 bytes); scalar: the table decode the SSSE3 path replaced
+  m.def("account_key", [](const std::string& id, bool scalar) {
+    uint8_t key[16];
+    const uint32_t form = AccountIndex::encode_key(id, key, scalar);
+    return py::make_tuple(form, py::bytes(reinterpret_cast<const char*>(key), 16));
+  }, py::arg("id"), py::arg("scalar") = false);
   py::class_<AccountIndex, std::shared_ptr<AccountIndex>>(m, "AccountIndex")
       .def(py::init<int64_t>())
       // node-shared index (/dev/shm/<shm_name>): one creator sizes it, the other ranks open it

@@ -430,3 +430,39 @@ def test_account_index_inline_keys_keep_exact_identity():
     s1, _ = ix2.lookup(real, True)
     s2, f2 = ix2.lookup(real, False)
     assert list(s1) == list(s2) and not any(f2) and sorted(s1) == list(range(150))
+
+
+def _account_key_ref(s: str):
+    """Python reference of AccountIndex::encode_key (csrc/runtime/account_index.cpp)."""
+    b = s.encode()
+    hexd = set(b"0123456789abcdef")
+    if len(b) == 36 and all(b[i] == ord("-") for i in (8, 13, 18, 23)):
+        digits = b[0:8] + b[9:13] + b[14:18] + b[19:23] + b[24:36]
+        if all(ch in hexd for ch in digits):
+            return (1 << 31) | (1 << 30), bytes.fromhex(digits.decode())
+    if len(b) <= 15:
+        return 1 << 31, bytes([len(b)]) + b + bytes(15 - len(b))
+    return 0, b[:16]
+
+
+def test_account_key_simd_uuid_decode_matches_scalar_and_reference():
+    """The SSSE3 UUID decode of the inline account key equals the table decode and a Python
+    reference on canonical UUIDs, on every single-character corruption class (upper case,
+    characters just outside '0'-'9' / 'a'-'f', hyphens moved) and on non-UUID ids."""
+    import uuid
+    rng = np.random.default_rng(11)
+    ids = [str(uuid.UUID(bytes=rng.bytes(16))) for _ in range(2000)]
+    ids += ["00000000-0000-0000-0000-000000000000", "ffffffff-ffff-ffff-ffff-ffffffffffff"]
+    bad = []
+    for u in ids[:200]:
+        for pos in (0, 7, 9, 12, 14, 17, 19, 22, 24, 30, 35):
+            for ch in "/:`g@AFG- \x80":
+                bad.append(u[:pos] + ch + u[pos + 1:])
+        bad.append(u.upper())
+        bad.append(u.replace("-", "_", 1))
+    others = ["", "a", "acc-17", "x" * 15, "y" * 16, "player-0000000000000000000001", ids[0] + "0", ids[0][:-1]]
+    for s in ids + bad + others:
+        want = _account_key_ref(s)
+        got = native().account_key(s)
+        assert (got[0], got[1]) == want, s
+        assert tuple(native().account_key(s, True)) == tuple(got), s
