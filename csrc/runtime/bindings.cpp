@@ -1053,8 +1053,47 @@ PYBIND11_MODULE(_native, m) {
           for (auto& d : done) d.store(0);
           std::atomic<bool> abort{false};
           const int64_t t0 = ServeCore::now_ns();
+          if (T == 1) {
+            // one thread submits every free window slot, then polls (no hand-off between a
+            // submitting and a polling thread: the submitter's back-off sleeps left the window
+            // part-empty, cfg5 1.92 -> 1.18 M checks/s)
+            int64_t sent = 0, idle_since = 0;
+            std::vector<AcctRouter::Done> out;
+            while (got < n) {
+              const int64_t room = std::min<int64_t>(n - sent, inflight - (sent - got));
+              for (int64_t k = 0; k < room; ++k, ++sent) {
+                const std::string& b = bufs[size_t(sent) % np_];
+                const int64_t ts = ServeCore::now_ns();
+                t_sub[size_t(sent)] = ts;
+                a.router->submit(uint8_t(rpc), b.data(), b.size(), uint64_t(sent), ts, now);
+              }
+              out.clear();
+              a.router->poll(out, size_t(std::max<int64_t>(inflight, 1024)), 2000);
+              const int64_t tr = ServeCore::now_ns();
+              if (out.empty()) {
+                if (!idle_since) idle_since = tr;
+                if (tr - idle_since > 60000000000LL) break;  // nothing answered for a minute: give up
+                continue;
+              }
+              idle_since = 0;
+              for (auto& d : out) {
+                const size_t i = size_t(d.tag);
+                if (i >= size_t(n)) continue;
+                if (!d.err.empty()) {
+                  ++errors;
+                  if (d.err.compare(0, std::strlen(kColdPrefix), kColdPrefix) == 0) ++cold;
+                  L[got++] = -1;
+                } else {
+                  L[got++] = tr - t_sub[i];
+                }
+              }
+            }
+            elapsed = double(ServeCore::now_ns() - t0) / 1e9;
+            for (int64_t k = got; k < n; ++k) L[k] = -1;
+            errors += n - got;
+          }
           std::vector<std::thread> subs;
-          for (int j = 0; j < T; ++j) {
+          for (int j = 0; j < T && T > 1; ++j) {
             subs.emplace_back([&, j] {
               int64_t sent = 0;  // calls j, j + T, j + 2T, ... of this thread
               for (int64_t i = j; i < n && !abort.load(std::memory_order_relaxed); i += T) {
@@ -1072,7 +1111,7 @@ PYBIND11_MODULE(_native, m) {
           }
           std::vector<AcctRouter::Done> out;
           int64_t idle_since = 0;
-          while (got < n) {
+          while (T > 1 && got < n) {
             out.clear();
             a.router->poll(out, size_t(std::max<int64_t>(inflight, 1024)), 2000);
             const int64_t tr = ServeCore::now_ns();
@@ -1099,9 +1138,11 @@ PYBIND11_MODULE(_native, m) {
             }
           }
           for (auto& t : subs) t.join();
-          elapsed = double(ServeCore::now_ns() - t0) / 1e9;
-          for (int64_t k = got; k < n; ++k) L[k] = -1;
-          errors += n - got;
+          if (T > 1) {
+            elapsed = double(ServeCore::now_ns() - t0) / 1e9;
+            for (int64_t k = got; k < n; ++k) L[k] = -1;
+            errors += n - got;
+          }
         }
         py::dict r;
         r["latency_ns"] = lat;
