@@ -272,7 +272,9 @@ class GpuScorer:
     def _copy_body(self, slot: int, bucket: int) -> None:
         sb = self.slots[slot]
         if self.update_features:
-            # the dedup insert reads the batch from the pinned slab and writes the device copy
+            # the dedup insert reads the batch from the pinned slab and writes the device copy (an
+            # H2D copy first and the insert from HBM: same engine_only / serving, round-5 A/B
+            # profiles/r5/eng/dedup_src)
             K.dedup_insert(self.store, self.cfg_dev, sb.req, bucket, sb.hdr, src=self.host_slab[slot])
             return
         K.memcpy_async(sb.dev_slab, self.host_slab[slot], HDR_BYTES + REQ_BYTES * bucket)
