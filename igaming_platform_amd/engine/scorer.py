@@ -138,6 +138,8 @@ class GpuScorer:
         self.slots = [self._alloc_slot() for _ in range(self.depth)]
         self._cur = 0  # slot of the last submitted batch (the un-indexed buffer properties)
         self.metrics = torch.zeros(128, dtype=torch.int64, device=dev)
+        # equal stream priorities: a high-priority state, model or copy stream measured the same
+        # (round-5 A/B, profiles/r5/eng/prio)
         self.stream = torch.cuda.Stream(device=dev)    # state stream (feature store owner)
         # H2D + dedup insert beside K1 (in order on the state stream instead: 78 vs 100 M
         # scores/s, profiles/NOTES.md "Model stream")
