@@ -19,12 +19,16 @@ from ..ops import kernels as K
 
 def tree_groups(step, bucket: int) -> int:
     """Split the trees of one ensemble into ``g`` groups so a small batch still fills the
-    256 CUs (>= ~512 workgroups), without shrinking a group below 8 trees."""
+    256 CUs (>= 256 workgroups, one per CU), without shrinking a group below 8 trees. The
+    target was 512 workgroups until round 5: at 8192 rows, 2 groups instead of 4 leave more of
+    the chip to the K1 / dedup-insert kernels running beside the trees - engine_only 151 vs 139 M
+    scores/s, serving unchanged (5 interleaved pairs 117.7 vs 117.8 M); 1 group (128
+    workgroups) drops to 91 M (profiles/r5/eng/groups)."""
     forced = int(os.environ.get("IGP_TREE_GROUPS", "0"))  # same-box A/B override
     if forced > 0:
         return max(1, min(forced, step.n_trees))
     tiles = -(-bucket // 64)
-    return max(1, min(max(1, step.n_trees // 8), -(-512 // tiles)))
+    return max(1, min(max(1, step.n_trees // 8), -(-256 // tiles)))
 
 
 class GruModel:
