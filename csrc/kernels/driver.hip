@@ -94,6 +94,10 @@ class PipeDriver {
     ext_events_ = !(xe && atoi(xe) == 0);
   }
   ~PipeDriver() {
+    if (clock_) {  // the shard's clock may still hold one of these events
+      clock_->retract(ev_.data(), ev_.size());
+      clock_->retract(pe_.data(), pe_.size());
+    }
     for (auto& e : ev_) (void)hipEventDestroy(e);
     for (auto& e : pe_) (void)hipEventDestroy(e);
   }
@@ -382,7 +386,8 @@ void register_driver(py::module_& m) {
            py::arg("stream"))
       .def_property_readonly("published", &StateClock::published)
       .def_property_readonly("waits", &StateClock::waits)
-      .def_property_readonly("skips", &StateClock::skips);
+      .def_property_readonly("skips", &StateClock::skips)
+      .def_property_readonly("retracts", &StateClock::retracts);
   py::class_<PipeDriver>(m, "PipeDriver")
       .def("set_state_clock", &PipeDriver::set_state_clock)
       .def(py::init<uintptr_t, uintptr_t, uintptr_t, int, py::list>())

@@ -41,6 +41,7 @@
 #include "oplist.h"
 #include "roctx.h"
 #include "state_clock.h"
+#include "../include/results_region.h"
 
 namespace py = pybind11;
 
@@ -288,6 +289,7 @@ class XchgDriver {
     slots_.resize(depth);
   }
   ~XchgDriver() {
+    if (clock_) clock_->retract(ev_.data(), ev_.size());  // before the events go
     for (auto& e : ev_) (void)hipEventDestroy(e);
   }
 
@@ -431,32 +433,27 @@ class XchgDriver {
     rshm_ = reinterpret_cast<char*>(base);
     rshm_slot_stride_ = slot_stride;
     rshm_owner_stride_ = owner_stride;
-    rflags_ = reinterpret_cast<int64_t*>(flags);
+    owners_ = OwnerGenerations(reinterpret_cast<int64_t*>(flags), world_, rank);
     rank_ = rank;
     // a driver replacing another on the same region (model hot reload, every rank paused at the
     // same step): continue from the generation this owner published last
-    for (int s = 0; s < depth_; ++s)
-      gen_[size_t(s)] = __atomic_load_n(&rflags_[(size_t(s) * world_ + rank_) * 8], __ATOMIC_ACQUIRE);
+    for (int s = 0; s < depth_; ++s) gen_[size_t(s)] = owners_.published(s, rank_);
   }
+  // the longest a step waits for the other owners when its caller gives no deadline (the serving
+  // core's drain of a step that already overran its own): the engine sets it from the serving
+  // deadline (engine/dp.py), so a dead or hung owner fails the step instead of hanging it
+  void set_owner_deadline_us(int64_t us) {
+    if (us <= 0) throw std::runtime_error("XchgDriver: the owner deadline must be finite and positive");
+    owner_deadline_us_ = us;
+  }
+  int64_t owner_deadline_us() const { return owner_deadline_us_; }
 
-  // d2h mode, inside wait(slot): publish this owner's generation, then wait for every owner's
+  // d2h mode, inside wait(slot): publish this owner's generation, then wait for every owner's.
+  // 1 = an owner missed the deadline (err names it); timeout_us < 0: the owner deadline.
   int32_t wait_owners(int slot, int64_t timeout_us, char* err, int32_t errlen) {
     const int64_t g = gen_[size_t(slot)];
-    __atomic_store_n(&rflags_[(size_t(slot) * world_ + rank_) * 8], g, __ATOMIC_RELEASE);
-    const auto t_end = timeout_us >= 0 ? std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us)
-                                       : std::chrono::steady_clock::time_point::max();
-    const auto t_spin = std::chrono::steady_clock::now() + std::chrono::microseconds(wait_spin_us());
-    for (;;) {
-      bool all = true;
-      for (int o = 0; o < world_ && all; ++o)
-        all = __atomic_load_n(&rflags_[(size_t(slot) * world_ + o) * 8], __ATOMIC_ACQUIRE) >= g;
-      if (all) return 0;
-      if (std::chrono::steady_clock::now() >= t_end) {
-        if (timeout_us < 0 && err && errlen > 0) std::strncpy(err, "results region: owner never published", size_t(errlen) - 1);
-        return 1;
-      }
-      wait_backoff(t_spin);
-    }
+    owners_.publish(slot, g);
+    return owners_.wait(slot, g, timeout_us >= 0 ? timeout_us : owner_deadline_us_, wait_spin_us(), err, errlen);
   }
 
   void submit_impl(int slot, int C, int seq, int64_t now, uintptr_t src, size_t nbytes, bool with_features) {
@@ -631,7 +628,8 @@ class XchgDriver {
   // per-GPU D2H result path (set_results_shm)
   char* rshm_ = nullptr;
   size_t rshm_slot_stride_ = 0, rshm_owner_stride_ = 0;
-  int64_t* rflags_ = nullptr;
+  OwnerGenerations owners_;
+  int64_t owner_deadline_us_ = 10000000;  // set_owner_deadline_us (engine: from the serving deadline)
   int rank_ = 0;
   std::vector<int64_t> gen_;
 };
@@ -670,6 +668,8 @@ void register_exchange(py::module_& m) {
       .def("set_stage_ops", &XchgDriver::set_stage_ops, py::arg("C"), py::arg("slot"), py::arg("state"),
            py::arg("model") = nullptr, py::arg("model_f") = nullptr)
       .def("set_results_shm", &XchgDriver::set_results_shm)
+      .def("set_owner_deadline_us", &XchgDriver::set_owner_deadline_us)
+      .def_property_readonly("owner_deadline_us", &XchgDriver::owner_deadline_us)
       .def("submit", &XchgDriver::submit)
       .def("device_ops", &XchgDriver::device_ops)
       .def("wait", &XchgDriver::wait)

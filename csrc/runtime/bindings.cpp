@@ -446,7 +446,8 @@ PYBIND11_MODULE(_native, m) {
       .def("devices_of", &LinkIndex::devices_of)
       .def("n_devices", &LinkIndex::n_devices)
       .def("_debug_acquire_and_leak", &LinkIndex::debug_acquire_and_leak)
-      .def_property_readonly("takeovers", &LinkIndex::takeovers);
+      .def_property_readonly("takeovers", &LinkIndex::takeovers)
+      .def_property_readonly("read_timeouts", &LinkIndex::read_timeouts);
 
   py::class_<CpuScorer, std::shared_ptr<CpuScorer>>(m, "CpuScorer")
       .def(py::init<int64_t, int, int, int, int>(), py::arg("capacity"), py::arg("ring_size") = 256,
@@ -631,6 +632,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("rows_scored", &ShmXchgDevice::rows_scored)
       .def_property_readonly("slot_violations", &ShmXchgDevice::slot_violations)
       .def_property_readonly("steps", &ShmXchgDevice::steps)
+      .def("debug_stall_results_when", &ShmXchgDevice::debug_stall_results_when)
       .def("unlink_shared", &ShmXchgDevice::unlink_shared);
 
   py::class_<AuditRing, std::shared_ptr<AuditRing>>(m, "AuditRing")

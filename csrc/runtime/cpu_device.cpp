@@ -1,5 +1,7 @@
 #include "cpu_device.h"
 
+#include <unistd.h>
+
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -69,8 +71,11 @@ const void* CpuDevice::features_fn(void* ctx, int32_t slot) {
 }
 
 // ============================================================================ ShmXchgDevice
-// shm layout: [world] Counter | per rank r, ring q: send [world][C + 1] ReqRec | per rank r,
-// ring q: results [world][C * W] (C ResultRec, then C FeatRec per destination rank)
+// shm layout: [world] Counter | [kRing][world] owner generation lines (results_region.h) |
+// per rank r, ring q: send [world][C + 1] ReqRec | per rank r, ring q: results [world][C * W]
+// (C ResultRec, then C FeatRec per destination rank). A step completes as on the GPU exchange's
+// node-shared results region: each owner publishes the step's generation after writing its rows,
+// and every rank waits for all owners with a finite deadline (OwnerGenerations).
 ShmXchgDevice::ShmXchgDevice(std::shared_ptr<CpuScorer> sc, const std::string& shm_name, int world, int rank, int depth,
                              int C, bool create, double timeout_s)
     : sc_(std::move(sc)), world_(world), rank_(rank), C_(C), timeout_s_(timeout_s) {
@@ -79,10 +84,13 @@ ShmXchgDevice::ShmXchgDevice(std::shared_ptr<CpuScorer> sc, const std::string& s
   W_ = sizeof(ResultRec) + sizeof(FeatRec);
   send_bytes_ = size_t(world) * size_t(C + 1) * sizeof(ReqRec);
   res_bytes_ = size_t(world) * size_t(C) * W_;
-  const size_t bytes = sizeof(Counter) * size_t(world) + size_t(world) * kRing * (send_bytes_ + res_bytes_);
+  const size_t flag_bytes = sizeof(int64_t) * OwnerGenerations::kLineWords * kRing * size_t(world);
+  const size_t bytes = sizeof(Counter) * size_t(world) + flag_bytes + size_t(world) * kRing * (send_bytes_ + res_bytes_);
   region_ = Region::shared(shm_name, bytes, create);
   counters_ = reinterpret_cast<Counter*>(region_.base());
-  data_ = reinterpret_cast<char*>(region_.base()) + sizeof(Counter) * size_t(world);
+  char* flags = reinterpret_cast<char*>(region_.base()) + sizeof(Counter) * size_t(world);
+  owners_ = OwnerGenerations(reinterpret_cast<int64_t*>(flags), world, rank);
+  data_ = flags + flag_bytes;
   slots_.resize(depth);
   for (auto& s : slots_) {
     s.send.resize(size_t(world) * size_t(C + 1));
@@ -167,8 +175,13 @@ void ShmXchgDevice::step(int slot, int64_t now) {
     std::memcpy(base + size_t(j) * sizeof(ResultRec), &res_[i], sizeof(ResultRec));
     std::memcpy(base + size_t(C_) * sizeof(ResultRec) + size_t(j) * sizeof(FeatRec), &feat_[i], sizeof(FeatRec));
   }
-  counters_[rank_].scored.store(k_ + 1, std::memory_order_release);
-  wait_all(&Counter::scored, k_ + 1);
+  // fault injection (FAULT_INJECT=xchg_stall_results): an owner that keeps stepping but never
+  // publishes its results - a hung device, alive enough that the posts keep coming
+  if (!stall_file_.empty() && !stalled_) stalled_ = ::access(stall_file_.c_str(), F_OK) == 0;
+  if (!stalled_) owners_.publish(q, k_ + 1);
+  char err[256] = {0};
+  if (owners_.wait(q, k_ + 1, int64_t(timeout_s_ * 1e6), 30, err, sizeof err) != 0)
+    throw std::runtime_error(std::string("ShmXchgDevice: ") + err);
   // 5. gather my rows' results from every owner
   for (int p = 0; p < world_; ++p)
     std::memcpy(s.recv.data() + size_t(p) * size_t(C_) * W_, res_area(p, q) + size_t(rank_) * size_t(C_) * W_,

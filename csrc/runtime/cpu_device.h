@@ -16,6 +16,7 @@
 
 #include "../include/device_ops.h"
 #include "../include/records.h"
+#include "../include/results_region.h"
 #include "cpu_scorer.h"
 #include "shm.h"
 
@@ -53,6 +54,10 @@ class ShmXchgDevice {
   // the same step on (the serving core's exchange-mode slot contract, serve_core.cpp)
   int64_t slot_violations() const { return slot_violations_.load(); }
   int64_t steps() const { return k_; }
+  // fault injection: once the file `path` exists this rank keeps posting its rows but never
+  // publishes its results again (the peers' steps must fail within the deadline;
+  // tests/test_failover.py)
+  void debug_stall_results_when(const std::string& path) { stall_file_ = path; }
   void unlink_shared() { region_.unlink(); }
 
  private:
@@ -85,6 +90,9 @@ class ShmXchgDevice {
   size_t W_, send_bytes_, res_bytes_;
   double timeout_s_;
   int64_t k_ = 0;  // steps done
+  std::string stall_file_;
+  bool stalled_ = false;
+  OwnerGenerations owners_;
   std::vector<Slot> slots_;
   std::vector<ReqRec> compact_;
   std::vector<int32_t> route_;

@@ -16,7 +16,8 @@
 // processes (a batch insert holds it ~1 ms per 8192 rows; readers are single lookups). The lock
 // word holds its owner's pid: a waiter that finds the owner process gone (SIGKILL, abort while
 // inside a critical section) takes the lock over instead of spinning forever, and readers wait
-// a bounded time (kReadWaitUs) and then answer "no links".
+// a bounded time (kReadWaitUs) and then answer "no links"; such answers are counted
+// (read_timeouts, exported as a metric) so abuse-score drift from lock timeouts is visible.
 #pragma once
 #include <algorithm>
 #include <atomic>
@@ -66,7 +67,10 @@ class LinkIndex {
   std::vector<int64_t> linked(int64_t acct, size_t limit) const {
     Guard g(hdr_->lock, kReadWaitUs);
     std::vector<int64_t> out;
-    if (!g.held) return out;
+    if (!g.held) {
+      read_timeouts_.fetch_add(1, std::memory_order_relaxed);
+      return out;
+    }
     CEntry a;
     if (!acct_.find(akey(acct), a)) return out;
     for (int d = a.n - 1; d >= 0; --d) {
@@ -84,6 +88,7 @@ class LinkIndex {
 
   std::vector<int64_t> devices_of(int64_t acct) const {
     Guard g(hdr_->lock, kReadWaitUs);
+    if (!g.held) read_timeouts_.fetch_add(1, std::memory_order_relaxed);
     CEntry a;
     return g.held && acct_.find(akey(acct), a) ? std::vector<int64_t>(a.v, a.v + a.n) : std::vector<int64_t>{};
   }
@@ -95,6 +100,8 @@ class LinkIndex {
   // tests: take the lock and keep it (a process that dies inside a critical section)
   void debug_acquire_and_leak() { Guard(hdr_->lock, -1).leak(); }
   int64_t takeovers() const { return takeovers_.load(); }
+  // lookups answered "no links" because the lock was not free within kReadWaitUs
+  int64_t read_timeouts() const { return read_timeouts_.load(); }
   bool shared() const { return region_.shared_mapping(); }
   void unlink_shared() { region_.unlink(); }
 
@@ -132,6 +139,7 @@ class LinkIndex {
   // sections. timeout_us < 0: wait until acquired. A waiter checks every ~1 ms whether the owner
   // process still exists and takes the word over (CAS owner -> self) when it does not.
   static std::atomic<int64_t> takeovers_;
+  static std::atomic<int64_t> read_timeouts_;
   struct Guard {
     std::atomic<uint32_t>& l;
     bool held = false;
@@ -281,5 +289,6 @@ class LinkIndex {
 };
 
 inline std::atomic<int64_t> LinkIndex::takeovers_{0};
+inline std::atomic<int64_t> LinkIndex::read_timeouts_{0};
 
 }  // namespace igp

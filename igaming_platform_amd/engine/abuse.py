@@ -120,6 +120,12 @@ class AbuseGpu:
         # stream, as does a serving rank (its streams are budgeted to the 4 hardware queues,
         # engine/dp.py).
         multi = overlap and not self.gp.ws_ok and not self.gm.bidirectional and depth > 1
+        if multi:
+            # the split cluster kernel (gru_wsx) keeps one workspace per pack (counters, hand-off
+            # slab, head partials): launches on several streams at once would share it (ADVICE
+            # r5), so with one stream per slot every bucket runs the batch-parallel kernel
+            for gp in self.gm.packs:
+                gp.wsx_ok = False
         self.n_streams = depth if multi else 1
         if self.gm.split:  # 32-row split tiles leave half the chip to the next slot's batch
             rows = int(os.environ.get("IGP_GRU_X3_ROWS", "32" if multi else "16"))

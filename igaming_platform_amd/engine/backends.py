@@ -694,6 +694,10 @@ class NativeCpuBackend:
         from ..native import native
         self._device = native().ShmXchgDevice(self.sc, shm_name, int(world), int(rank), int(depth), int(C),
                                               bool(create), float(timeout_s))
+        from ..utils.faults import Faults
+        f = Faults()  # FAULT_INJECT=xchg_stall_results:file=P - this owner stops publishing results
+        if f.active("xchg_stall_results"):
+            self._device.debug_stall_results_when(f.params("xchg_stall_results")["file"])
         return self._device
 
     @property

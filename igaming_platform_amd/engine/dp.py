@@ -335,6 +335,11 @@ class DpGpuScorer(GpuScorer):
         if self.rshm is not None:
             r = self.rshm
             d.set_results_shm(r["base"], r["slot_stride"], r["owner_stride"], r["flags"], self.rank)
+            # every wait for the other owners is bounded (a hung owner fails the step, then the
+            # group fails over): the serving deadline's headroom for the late-step drain
+            ms = getattr(getattr(self, "cfg", None), "gpu", None)
+            ms = int(ms.batch_timeout_ms) if ms is not None and ms.batch_timeout_ms > 0 else 5000
+            d.set_owner_deadline_us(2 * ms * 1000)
         if getattr(self, "state_clock", None) is not None:
             d.set_state_clock(self.state_clock)
         self.xdriver = d

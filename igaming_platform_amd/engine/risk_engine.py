@@ -96,6 +96,7 @@ class RiskEngine:
         self.blacklist = Blacklist(cfg.gpu.blacklist_capacity)
         self.ipintel = IPIntel(cfg.gpu.blacklist_capacity)
         self.links = N.LinkIndex(8)  # 8 most recent accounts per device / devices per account
+        self.metrics.links = self.links
         # link inserts run off the scoring path on one background thread (C++, GIL released);
         # linked_accounts() waits for the inserts already queued
         import concurrent.futures as _cf
@@ -146,6 +147,7 @@ class RiskEngine:
             self.local = local
             self.core = node.core
             self.links = node.links  # node-shared: links recorded by every rank's ingress
+            self.metrics.links = self.links
             self.auditlog = node.audit  # the node's core writes its native ring
             self._audit_evicted_seen = 0
             from . import serving

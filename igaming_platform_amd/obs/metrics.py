@@ -30,6 +30,8 @@ class Metrics:
         # native serving cores count their own decisions (engine/serving.py core_metrics)
         self.sources = []
         self._fast = {}
+        # the engine's LinkIndex (CheckBonusAbuse linked_accounts): its lock counters at scrape
+        self.links = None
         r.register(_DecisionCollector(self))
         self.batch_size = Histogram("gpu_batch_size", "rows per device micro-batch",
                                     buckets=(1, 8, 64, 256, 1024, 4096, 8192), registry=r)
@@ -114,6 +116,15 @@ class _DecisionCollector:
         c = CounterMetricFamily("risk_blacklist_hits", "requests matching the blacklist")
         c.add_metric([], bl)
         yield c
+        links = m.links
+        if links is not None:
+            c = CounterMetricFamily("risk_link_read_timeouts", "linked-account lookups answered empty because "
+                                    "the link index lock was busy past its bounded wait")
+            c.add_metric([], int(links.read_timeouts))
+            yield c
+            c = CounterMetricFamily("risk_link_lock_takeovers", "link index locks taken over from a dead process")
+            c.add_metric([], int(links.takeovers))
+            yield c
 
 
 

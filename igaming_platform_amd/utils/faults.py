@@ -4,7 +4,10 @@ Names used by the engine: ``backend_error`` (a shard's scoring step raises -> th
 marked unhealthy and its rows go to the CPU fallback), ``gpu_timeout:ms=N`` (a real N ms
 device stall is queued ahead of the shard's batch, so the watchdog deadline fires),
 ``model_error`` (ML fails -> ml_error_score, engine.go:279-282),
-``feature_store_down`` (features unavailable -> partial features, engine.go:267-270).
+``feature_store_down`` (features unavailable -> partial features, engine.go:267-270),
+``xchg_stall_results:file=P`` (once file P exists, a CPU exchange owner keeps stepping but
+stops publishing its results: its peers' steps fail at the deadline, then the group fails
+over; tests/test_failover.py).
 """
 from __future__ import annotations
 

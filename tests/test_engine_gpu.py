@@ -387,7 +387,18 @@ def test_gpu_model_hot_reload():
         fa, fb = a.get_features(f"acc-{i}", now=NOW + 5), b.get_features(f"acc-{i}", now=NOW + 5)
         diff = [k for k in fa.dtype.names if fa[k] != fb[k]]
         assert not diff, ("before reload", i, [(k, fa[k], fb[k]) for k in diff])
+    import gc
+    import weakref
+    old = weakref.ref(a.backends[0].scorer.driver)
     assert a.reload_model(m) == 2
+    gc.collect()
+    # reads right after the swap, before the new scorer published a state stage: the shard's
+    # StateClock must not hand out the dropped driver's events (retract on destroy)
+    for i in range(40):
+        fa, fb = a.get_features(f"acc-{i}", now=NOW + 5), b.get_features(f"acc-{i}", now=NOW + 5)
+        assert fa.tobytes() == fb.tobytes(), ("right after reload", i)
+    if old() is None:  # the old driver is gone: it retracted its events from the clock first
+        assert a.backends[0].state_clock.retracts >= 1
     ra, rb = a.score(t2, now=NOW + 20), b.score(t2, now=NOW + 20)
     assert [(x["score"], x["action"], x["ml_score"]) for x in ra] == [(x["score"], x["action"], x["ml_score"]) for x in rb]
     for i in range(40):

@@ -187,3 +187,103 @@ def test_heartbeat_detects_dead_worker_while_idle(tmp_path):
     assert out["rehomed"]
     assert out["health"]["healthy"] == [True, True]
     assert out["health"]["failover"]["rehomed"] == [1]
+
+
+# ---- an owner that stops publishing its results
+#
+# The owner stays alive and keeps posting its rows (a hung device, not a dead process), so the
+# other ranks pass the row hand-off and block in the results wait - the GPU exchange's
+# node-shared results region protocol (csrc/include/results_region.h, shared by exchange.hip
+# XchgDriver::wait_owners and the CPU ShmXchgDevice). That wait is bounded: the in-flight
+# batch fails within the deadline with an error naming the owner, the group fails over, and
+# scoring continues on the re-homed shards.
+
+def _rank0_stall(world, port, snap, stall_file, q, ev_ready, ev_stalled):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE=str(world))
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.engine.risk_engine import RiskEngine
+    from igaming_platform_amd.parallel.comm import init_from_env
+    comm = init_from_env("gloo", timeout_s=30, op_timeout_s=5)
+    cfg = Config()
+    cfg.gpu.spmd_heartbeat_s = 0.0
+    cfg.gpu.rehome_grace_s = 10.0
+    cfg.gpu.exchange_timeout_s = 2.0
+    eng = RiskEngine(cfg, backend="cpu", capacity=256, spmd=comm)
+    accts = [f"acct-{i}" for i in range(48)]
+    out = {}
+    try:
+        for step in range(3):
+            eng.score(_txs(accts, step), now=NOW + step)
+        eng.snapshot(snap)
+        ev_ready.set()
+        ev_stalled.wait(60)
+        fb0 = eng.metrics.fallbacks.labels(reason="group_failed")._value.get()
+        t0 = time.time()
+        r = eng.score(_txs(accts, 8), now=NOW + 40)   # in flight when owner 2 stops publishing
+        out["first_s"] = time.time() - t0
+        out["n_first"] = len(r)
+        out["fallback_rows"] = eng.metrics.fallbacks.labels(reason="group_failed")._value.get() - fb0
+        out["group_failed"] = eng.failover["group_failed"]
+        out["error"] = eng.failover["error"]
+        out["rehomed"] = eng.rehome_done.wait(60)
+        out["health"] = eng.health()
+        out["rehome_errors"] = dict(eng.failover["rehome_errors"])
+        r = eng.score(_txs(accts, 9), now=NOW + 50)
+        out["second_tx_count_1h"] = [int(x["features"]["tx_count_1h"]) for x in r]
+        q.put(("ok", out))
+    except Exception:
+        import traceback
+        q.put(("err", traceback.format_exc()))
+    finally:
+        eng.close()
+
+
+def _worker_stall(rank, world, port, q, fault):
+    if fault:
+        os.environ["FAULT_INJECT"] = fault
+    _worker(rank, world, port, q)
+
+
+def test_owner_that_stops_publishing_fails_the_step_within_the_deadline(tmp_path):
+    world, victim = 3, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ev_ready, ev_stalled = ctx.Event(), ctx.Event()
+    port = _free_port()
+    snap = str(tmp_path / "snap")
+    stall_file = str(tmp_path / "stall")
+    p0 = ctx.Process(target=_rank0_stall, args=(world, port, snap, stall_file, q, ev_ready, ev_stalled))
+    ws = {r: ctx.Process(target=_worker_stall,
+                         args=(r, world, port, q, f"xchg_stall_results:file={stall_file}" if r == victim else ""))
+          for r in range(1, world)}
+    p0.start()
+    [p.start() for p in ws.values()]
+    msgs = []
+    try:
+        assert ev_ready.wait(240), "rank 0 never reached the stall point"
+        open(stall_file, "w").close()   # owner 2 keeps stepping, never publishes again
+        ev_stalled.set()
+        deadline = time.time() + 180
+        while time.time() < deadline and not any(m[0] in ("ok", "err") for m in msgs):
+            msgs.append(q.get(timeout=max(1, deadline - time.time())))
+        for p in ws.values():   # every worker, the stalled one included, leaves on its own
+            p.join(60)
+            assert p.exitcode == 0, f"worker exit {p.exitcode}"
+        while not q.empty():
+            msgs.append(q.get())
+    finally:
+        for p in [p0, *ws.values()]:
+            if p.is_alive():
+                p.kill()
+    errs = [m[1] for m in msgs if m[0] == "err"]
+    assert not errs, errs[0]
+    out = next(m[1] for m in msgs if m[0] == "ok")
+    # the in-flight batch: answered (stateless fallback, every row) within the step deadline
+    assert out["n_first"] == 60 and out["fallback_rows"] == 60
+    assert out["first_s"] < 2.0 + 8.0, out["first_s"]
+    assert out["group_failed"]
+    assert "did not publish generation" in out["error"] and "owner(s) 2" in out["error"], out["error"]
+    # failover: every remote shard re-homed, scoring continues with feature state
+    assert out["rehomed"] and not out["rehome_errors"]
+    assert out["health"]["healthy"] == [True] * world
+    assert sum(c > 0 for c in out["second_tx_count_1h"]) >= 50

@@ -399,6 +399,35 @@ def test_gru_split_clusters_match_batch_parallel(rows):
     assert float(np.abs(a - ref).max()) <= 1e-4
 
 
+def test_gru_split_clusters_start_from_zeroed_counters():
+    """a cluster launch that timed out leaves its counters part-advanced. Every
+    cluster launch now starts with a memset of its counters (a node of the captured graph), so
+    a launch after such leftovers - here: counters poisoned by hand - still waits for every
+    member and equals the batch-parallel kernel (without the reset its first waits would pass
+    early and read slices that were never published)."""
+    import torch
+    from igaming_platform_amd.ops import kernels as K
+    T, rows = 100, 64
+    N, m, plan, gp = _split_pack(T)
+    plan.steps[-1].w_np = plan.steps[-1].w_np * 40.0
+    gp.head_w = torch.from_numpy(np.ascontiguousarray(plan.steps[-1].w_np[0], np.float32)).cuda()
+    rng = np.random.default_rng(77)
+    Xd = torch.from_numpy(rng.standard_normal((T, rows, 16)).astype(np.float32)).cuda()
+    o_x = torch.full((rows,), -9.0, device="cuda")
+    o_bp = torch.full((rows,), -9.0, device="cuda")
+    ws = gp.workspace(rows)
+    for poison in (16 * 37, 5):
+        ws["sync"].fill_(poison)
+        o_x.fill_(-9.0)
+        K.gru(gp, rows, T, out=o_x, X=Xd, ws=3)
+        torch.cuda.synchronize()
+        assert not gp.ws_failed()
+        assert int(ws["sync"].abs().sum()) == 0  # member 0 of every cluster returned them to 0
+    K.gru(gp, rows, T, out=o_bp, X=Xd, ws=0)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(o_x.cpu().numpy(), o_bp.cpu().numpy(), rtol=0, atol=1e-5)
+
+
 def test_gru_split_clusters_event_rings_yh_and_live_rows():
     """The split cluster kernel from the HBM event rings (right-aligned histories, empty slots),
     Y_h without a head, and a device live count below the launch rows: equal to the batch-parallel

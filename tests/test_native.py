@@ -376,8 +376,10 @@ def test_link_index_lock_taken_over_from_a_dead_owner():
         try:
             assert child.stdout.readline().strip() == "held"
             t0 = time.monotonic()
+            before = L.read_timeouts
             assert L.linked(1, 4) == []              # live owner: the reader gives up (bounded)
             assert time.monotonic() - t0 < 2.0
+            assert L.read_timeouts == before + 1     # ... and the "no links" answer is counted
             child.send_signal(signal.SIGKILL)
             child.wait(10)
         finally:
