@@ -29,7 +29,9 @@ class OwnerGenerations {
   static constexpr int kLineWords = 8;  // int64 words per flag line
 
   OwnerGenerations() = default;
-  OwnerGenerations(int64_t* flags, int world, int rank) : flags_(flags), world_(world), rank_(rank) {}
+  // `what`: how a timeout names the ranks behind ("results region: owner(s)", "rows region: sender(s)")
+  OwnerGenerations(int64_t* flags, int world, int rank, const char* what = "results region: owner(s)")
+      : flags_(flags), world_(world), rank_(rank), what_(what) {}
   bool valid() const { return flags_ != nullptr; }
   int world() const { return world_; }
 
@@ -72,7 +74,7 @@ class OwnerGenerations {
       if (published(slot, o) < gen) owners += (owners.empty() ? "" : ",") + std::to_string(o);
     char buf[256];
     std::snprintf(buf, sizeof buf,
-                  "results region: owner(s) %s did not publish generation %lld of slot %d within %.1f ms",
+                  "%s %s did not publish generation %lld of slot %d within %.1f ms", what_,
                   owners.empty() ? "?" : owners.c_str(), (long long)gen, slot, double(timeout_us) / 1e3);
     std::strncpy(err, buf, size_t(errlen) - 1);
     err[errlen - 1] = 0;
@@ -80,6 +82,7 @@ class OwnerGenerations {
 
   int64_t* flags_ = nullptr;
   int world_ = 0, rank_ = 0;
+  const char* what_ = "results region: owner(s)";
 };
 
 }  // namespace igp

@@ -51,19 +51,25 @@ constexpr int XCHG_MAX_WORLD = 64;
 
 // ------------------------------------------------------------------------------- kernels
 struct XchgCompactArgs {
-  const ReqRec* recv;  // [N][C + 1]: header record (slot = row count) + C rows per sender
+  const ReqRec* recv;  // sender p's chunk at recv + p * pstride: header record (slot = row count) + C rows
   ReqRec* rows;        // scorer slab rows [cap]
   BatchHdr* hdr;       // n written here (seq / now came with the batch header copy)
   int32_t* route;      // [cap + 1]: route[i] = peer * C + index; route[cap] = rows over cap
   int32_t N, C, cap;
+  int64_t pstride;     // records between two senders' chunks: C + 1 (all-to-all receive buffer) or
+                       // world * (C + 1) (the node-shared rows region: [sender][owner][C + 1])
+  const int4* hdr_src; // nullable: the batch header {n, seq, now} in the pinned slab, copied first
 };
 
 __global__ __launch_bounds__(256) void exchange_compact_kernel(XchgCompactArgs a) {
   __shared__ int cnt[XCHG_MAX_WORLD];
   __shared__ int pre[XCHG_MAX_WORLD + 1];
+  __shared__ int64_t tsp[XCHG_MAX_WORLD];
   if (threadIdx.x < (unsigned)a.N) {
-    const int c = a.recv[(size_t)threadIdx.x * (a.C + 1)].slot;
+    const ReqRec* h = a.recv + (size_t)threadIdx.x * a.pstride;
+    const int c = h->slot;
     cnt[threadIdx.x] = c < 0 ? 0 : (c > a.C ? a.C : c);
+    tsp[threadIdx.x] = h->ts;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -74,11 +80,11 @@ __global__ __launch_bounds__(256) void exchange_compact_kernel(XchgCompactArgs a
       s += cnt[p];
       // senders of the serving core stamp their step clock into the chunk header: the step is
       // scored at the latest clock among the senders that sent rows (0: keep the batch header's)
-      const int64_t ts = a.recv[(size_t)p * (a.C + 1)].ts;
-      if (cnt[p] > 0 && ts > t) t = ts;
+      if (cnt[p] > 0 && tsp[p] > t) t = tsp[p];
     }
     pre[a.N] = s;
     if (blockIdx.x == 0) {
+      if (a.hdr_src) *reinterpret_cast<int4*>(a.hdr) = *a.hdr_src;
       a.hdr->n = s < a.cap ? s : a.cap;
       if (t > 0) a.hdr->now = t;
       a.route[a.cap] = s > a.cap ? s - a.cap : 0;
@@ -91,7 +97,7 @@ __global__ __launch_bounds__(256) void exchange_compact_kernel(XchgCompactArgs a
   if (p >= a.N || j >= cnt[p]) return;
   const int dst = pre[p] + j;
   if (dst >= a.cap) return;
-  const int4* src = reinterpret_cast<const int4*>(a.recv + (size_t)p * (a.C + 1) + 1 + j);
+  const int4* src = reinterpret_cast<const int4*>(a.recv + (size_t)p * a.pstride + 1 + j);
   int4* out = reinterpret_cast<int4*>(a.rows + dst);
   int4 q0 = src[0];
   const int4 q1 = src[1], q2 = src[2];
@@ -269,11 +275,14 @@ class RcclComm {
 // xs / ys run on CUs reserved for communication (engine/dp.py IGP_XCHG_COMM_CUS).
 class XchgDriver {
  public:
+  // cx / cy: the row and result communicators; both null for the node-shared rows + results
+  // regions (set_rows_shm + set_results_shm: no collective on the hot path)
   XchgDriver(uintptr_t cs, uintptr_t ss, uintptr_t ms, uintptr_t xs, uintptr_t ys, int depth, int world,
-             const RcclComm& cx, const RcclComm& cy)
+             const RcclComm* cx, const RcclComm* cy)
       : cs_(S(cs)), ss_(S(ss)), ms_(S(ms)), xs_(S(xs)), ys_(S(ys)), depth_(depth), world_(world),
-        cx_(cx.ptr()), cy_(cy.ptr()), r_(rccl("")) {
-    if (cx.world() != world || cy.world() != world) throw std::runtime_error("XchgDriver: communicator world");
+        cx_(cx ? cx->ptr() : 0), cy_(cy ? cy->ptr() : 0), r_(cx ? &rccl("") : nullptr) {
+    if (!cx != !cy) throw std::runtime_error("XchgDriver: both communicators or neither");
+    if (cx && (cx->world() != world || cy->world() != world)) throw std::runtime_error("XchgDriver: communicator world");
     if (depth < 1 || depth > DEDUP_AHEAD)  // the copy of batch q relies on batch q - depth's state stage
       throw std::runtime_error("XchgDriver: depth exceeds the dedup ring (DEDUP_AHEAD)");
     hip_ok(hipGetDevice(&device_), "get device");  // the serving core's threads bind to it
@@ -448,6 +457,33 @@ class XchgDriver {
   }
   int64_t owner_deadline_us() const { return owner_deadline_us_; }
 
+  // Node-shared rows region (no row all-to-all): [slot][sender][owner][C + 1] ReqRec in page-
+  // locked /dev/shm plus one generation line per (slot, sender). A sender packs its chunks for
+  // every owner straight into its block (the serving core through device_ops().rows, or
+  // submit()'s copy) and publishes the step's generation; an owner waits on the host until
+  // every sender of the step published (finite deadline, results_region.h), then its copy
+  // stage compacts its chunk of every sender's block straight from host memory (zero copy,
+  // one kernel) and inserts the batch into the dedup region - three recorded stages per step,
+  // no collective. A block is reused (step k + depth) only after the sender's wait(slot) of
+  // step k saw every owner's results, i.e. after every owner's copy stage of step k finished.
+  void set_rows_shm(uintptr_t base, size_t slot_stride, size_t sender_stride, uintptr_t flags) {
+    if (!rshm_) throw std::runtime_error("XchgDriver: the rows region needs the results region (set_results_shm first)");
+    if (!base || !flags || sender_stride == 0 || slot_stride < size_t(world_) * sender_stride)
+      throw std::runtime_error("XchgDriver: rows region");
+    rows_ = reinterpret_cast<char*>(base);
+    senders_ = OwnerGenerations(reinterpret_cast<int64_t*>(flags), world_, rank_, "rows region: sender(s)");
+    for (int s = 0; s < depth_; ++s) {
+      slots_[size_t(s)].host_x = rows_ + size_t(s) * slot_stride + size_t(rank_) * sender_stride;
+      slots_[size_t(s)].host_x_bytes = sender_stride;
+    }
+  }
+  // the copy stage of the rows-region mode (compact from the region + dedup insert)
+  void set_copy_ops(int C, int slot, std::shared_ptr<OpList> copy) {
+    check_slot(slot);
+    if (!copy) throw std::runtime_error("XchgDriver: set_copy_ops list");
+    graphs_[key(C, slot)].ocopy = std::move(copy);
+  }
+
   // d2h mode, inside wait(slot): publish this owner's generation, then wait for every owner's.
   // 1 = an owner missed the deadline (err names it); timeout_us < 0: the owner deadline.
   int32_t wait_owners(int slot, int64_t timeout_us, char* err, int32_t errlen) {
@@ -478,6 +514,42 @@ class XchgDriver {
     const auto t1 = clk::now();
     hipEvent_t e_send = E(slot, 0), e_x = E(slot, 1), e_post = E(slot, 2), e_state = E(slot, 3), e_model = E(slot, 4),
                e_done = E(slot, 5);
+    if (rows_) {
+      if (!g.ocopy || !(g.ostate || g.state) || !((with_features ? g.omodel_f : g.omodel) || (with_features ? g.model_f : g.model)))
+        throw std::runtime_error("XchgDriver: rows-region mode lacks a stage body");
+      // this sender's chunks are in its block: publish, then wait for every sender of the step
+      senders_.publish(slot, gen_[size_t(slot)]);
+      char err[256] = {0};
+      if (senders_.wait(slot, gen_[size_t(slot)], owner_deadline_us_, wait_spin_us(), err, sizeof err) != 0)
+        throw std::runtime_error(err);
+      const auto t2 = clk::now();
+      // the slot's previous batch (q - depth) finished: its device rows / route / dedup region are free
+      if (done_recorded_[slot]) hip_ok(hipStreamWaitEvent(cs_, e_done, 0), "wait done");
+      if (!g.ocopy->run_recording(cs_, e_post)) hip_ok(hipEventRecord(e_post, cs_), "record post");
+      hip_ok(hipStreamWaitEvent(ss_, e_post, 0), "wait post");
+      if (g.ostate) {
+        if (!g.ostate->run_recording(ss_, e_state)) hip_ok(hipEventRecord(e_state, ss_), "record state");
+      } else {
+        hip_ok(hipGraphLaunch(g.state, ss_), "state graph");
+        hip_ok(hipEventRecord(e_state, ss_), "record state");
+      }
+      if (clock_) clock_->publish(e_state);
+      hip_ok(hipStreamWaitEvent(ms_, e_state, 0), "wait state");
+      const std::shared_ptr<OpList>& om = with_features ? g.omodel_f : g.omodel;
+      if (om) {
+        if (!om->run_recording(ms_, e_done)) hip_ok(hipEventRecord(e_done, ms_), "record done");
+      } else {
+        hip_ok(hipGraphLaunch(with_features ? g.model_f : g.model, ms_), "model graph");
+        hip_ok(hipEventRecord(e_done, ms_), "record done");
+      }
+      auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+      st_[0] += us(t0, t1);
+      st_[1] += us(t2, clk::now());
+      st_[2] += us(t1, t2);  // the wait for the other senders' rows (host)
+      st_[3] += 1;
+      done_recorded_[slot] = true;
+      return;
+    }
     (void)e_send;
     // a hop between two streams costs an event record + wait; when the exchange runs its
     // collectives on the copy / model streams themselves (IGP_XCHG_STREAMS=3) there is none
@@ -521,7 +593,8 @@ class XchgDriver {
     if (done_recorded_[slot]) hip_ok(hipStreamWaitEvent(xs_, e_done, 0), "wait done");
     hip_ok(hipGraphLaunch(g.send, xs_), "send graph");
     const auto t2 = clk::now();
-    nccl_ok(r_, r_.all_to_all(sl.xsend, sl.xrecv, xbytes, kUint8, reinterpret_cast<void*>(cx_), xs_), "all_to_all rows");
+    if (!r_) throw std::runtime_error("XchgDriver: no communicators for the row all-to-all");
+    nccl_ok(*r_, r_->all_to_all(sl.xsend, sl.xrecv, xbytes, kUint8, reinterpret_cast<void*>(cx_), xs_), "all_to_all rows");
     const auto t3 = clk::now();
     hop(xs_, cs_, e_x, "x -> copy");
     hip_ok(hipGraphLaunch(g.post, cs_), "post graph");
@@ -544,7 +617,7 @@ class XchgDriver {
     }
     hop(ms_, ys_, e_model, "model -> y");
     const auto t4 = clk::now();
-    nccl_ok(r_, r_.all_to_all(sl.rsend, sl.rrecv, rbytes, kUint8, reinterpret_cast<void*>(cy_), ys_), "all_to_all results");
+    nccl_ok(*r_, r_->all_to_all(sl.rsend, sl.rrecv, rbytes, kUint8, reinterpret_cast<void*>(cy_), ys_), "all_to_all results");
     const auto t5 = clk::now();
     hip_ok(hipMemcpyAsync(sl.host_rr, sl.rrecv, (size_t)world_ * rbytes, hipMemcpyDeviceToHost, ys_), "results D2H");
     hip_ok(hipEventRecord(e_done, ys_), "record done");
@@ -592,6 +665,7 @@ class XchgDriver {
   struct Graphs {
     hipGraphExec_t send = nullptr, post = nullptr, state = nullptr, model = nullptr, model_f = nullptr;
     std::shared_ptr<OpList> ostate, omodel, omodel_f;  // set_stage_ops (captured mode)
+    std::shared_ptr<OpList> ocopy;                     // set_copy_ops (rows-region mode)
   };
   struct Slot {
     char* host_hdr;
@@ -614,7 +688,7 @@ class XchgDriver {
   std::shared_ptr<StateClock> clock_;
   int depth_, world_;
   uintptr_t cx_, cy_;
-  const Rccl& r_;
+  const Rccl* r_;
   std::vector<hipEvent_t> ev_;
   std::vector<bool> done_recorded_;
   std::vector<Slot> slots_;
@@ -629,6 +703,8 @@ class XchgDriver {
   char* rshm_ = nullptr;
   size_t rshm_slot_stride_ = 0, rshm_owner_stride_ = 0;
   OwnerGenerations owners_;
+  OwnerGenerations senders_;  // rows-region mode: the generation lines of the senders
+  char* rows_ = nullptr;
   int64_t owner_deadline_us_ = 10000000;  // set_owner_deadline_us (engine: from the serving deadline)
   int rank_ = 0;
   std::vector<int64_t> gen_;
@@ -660,8 +736,10 @@ void register_exchange(py::module_& m) {
       .def_property_readonly("alive", &RcclComm::alive)
       .def("abort", &RcclComm::abort);
   py::class_<XchgDriver>(m, "XchgDriver")
-      .def(py::init<uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int, const RcclComm&, const RcclComm&>(),
+      .def(py::init<uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int, const RcclComm*, const RcclComm*>(),
            py::keep_alive<1, 9>(), py::keep_alive<1, 10>())
+      .def("set_rows_shm", &XchgDriver::set_rows_shm)
+      .def("set_copy_ops", &XchgDriver::set_copy_ops)
       .def("set_slot", &XchgDriver::set_slot)
       .def("set_graphs", &XchgDriver::set_graphs)
       .def("set_captured", &XchgDriver::set_captured)
@@ -687,9 +765,12 @@ void register_exchange(py::module_& m) {
   m.def("host_unregister", [](uintptr_t p) { (void)hipHostUnregister(reinterpret_cast<void*>(p)); });
   // kernel launches (captured into the exchange graphs from Python)
   m.def("exchange_compact", [](uintptr_t recv, uintptr_t rows, uintptr_t hdr, uintptr_t route, int N, int C, int cap,
-                               uintptr_t stream) {
+                               uintptr_t stream, int64_t pstride, uintptr_t hdr_src) {
     if (N < 1 || N > XCHG_MAX_WORLD || C < 1 || cap < 1) throw std::runtime_error("exchange_compact: bad sizes");
-    XchgCompactArgs a{P<const ReqRec*>(recv), P<ReqRec*>(rows), P<BatchHdr*>(hdr), P<int32_t*>(route), N, C, cap};
+    if (pstride == 0) pstride = C + 1;
+    if (pstride < C + 1) throw std::runtime_error("exchange_compact: sender stride below the chunk size");
+    XchgCompactArgs a{P<const ReqRec*>(recv), P<ReqRec*>(rows), P<BatchHdr*>(hdr), P<int32_t*>(route), N, C, cap,
+                      pstride, P<const int4*>(hdr_src)};
     const int threads = N * C;
     auto f = [a, threads](hipStream_t st) {
       IGP_LAUNCH(exchange_compact_kernel, dim3((threads + 255) / 256), dim3(256), 0, st, a);
@@ -700,7 +781,8 @@ void register_exchange(py::module_& m) {
     }
     f(P<hipStream_t>(stream));
     hip_ok(hipGetLastError(), "exchange_compact");
-  });
+  }, py::arg("recv"), py::arg("rows"), py::arg("hdr"), py::arg("route"), py::arg("N"), py::arg("C"), py::arg("cap"),
+        py::arg("stream"), py::arg("pstride") = 0, py::arg("hdr_src") = 0);
   m.def("exchange_clear", [](uintptr_t recv, int N, int C, uintptr_t stream, uintptr_t hdr_src, uintptr_t hdr_dst) {
     if (N < 1 || N > XCHG_MAX_WORLD || C < 1) throw std::runtime_error("exchange_clear: bad sizes");
     if (!hdr_src != !hdr_dst) throw std::runtime_error("exchange_clear: header source and destination together");

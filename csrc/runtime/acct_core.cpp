@@ -650,6 +650,11 @@ void AcctRouter::set_sink(Sink s) {
   sink_ = std::move(s);
 }
 
+AcctRouter::Sink AcctRouter::sink() const {
+  std::lock_guard<std::mutex> g(out_mu_);
+  return sink_;
+}
+
 void AcctRouter::deliver(int origin, std::vector<Done>&& outs) {
   if (origin >= 0) {  // answers to another rank's ingress: its reply ring
     for (auto& d : outs) {

@@ -245,6 +245,7 @@ class AcctRouter {
   // now: the clock the account's features are read at (unix s; < 0: the wall clock)
   void submit(uint8_t rpc, const char* data, size_t n, uint64_t tag, int64_t t0_ns, int64_t now = -1);
   void set_sink(Sink s);
+  Sink sink() const;
   size_t poll(std::vector<Done>& out, size_t max, int64_t timeout_us);
 
   void stop();
@@ -279,7 +280,7 @@ class AcctRouter {
   mutable std::mutex p_mu_;
   AbuseParams abuse_params_;
 
-  std::mutex out_mu_;
+  mutable std::mutex out_mu_;
   std::condition_variable out_cv_;
   std::deque<Done> outq_;
   Sink sink_;

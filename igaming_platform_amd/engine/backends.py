@@ -364,7 +364,8 @@ class GpuBackend:
             from .dp import DpGpuScorer, map_results_region
             x = self.exchange
             if isinstance(x.get("results_shm"), str):  # mapped once; a hot reload's scorer reuses it
-                x["results_shm"] = map_results_region(x["results_shm"], depth, x["world"], max(x["cbuckets"]))
+                x["results_shm"] = map_results_region(x["results_shm"], depth, x["world"], max(x["cbuckets"]),
+                                                      rows=bool(x.get("rows_shm")))
             sc = DpGpuScorer(self.cfg, self.store, x["comms"], x["world"], self.rank, x["senders"], x["cbuckets"],
                              plan=plan, model=model, device=self.device, pipeline_depth=depth,
                              results_shm=x.get("results_shm"))

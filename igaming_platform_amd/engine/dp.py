@@ -50,23 +50,42 @@ REQ = REQREC.itemsize
 
 # Per-rank stream -> hardware-queue map of the exchange pipeline. HIP multiplexes a process's
 # streams onto GPU_MAX_HW_QUEUES hardware queues (4 on the boxes, HIP's default); a fifth
-# stream would share a queue with one of these and serialise behind it. The default layout
-# (IGP_XCHG_STREAMS=3) therefore puts the two RCCL all-to-alls on the copy and model streams:
+# stream would share a queue with one of these and serialise behind it. The two RCCL
+# all-to-alls (IGP_XCHG_ROWS=rccl) therefore run on the copy and model streams:
 #   default  allocations, cold reads (GetFeatures readouts order on the state stream)
 #   copy     H2D chunks + header, row all-to-all (communicator 0), compaction, dedup insert
 #   state    K1 feature assembly + state update (owns the HBM feature store)
 #   model    trees / head / K5, result scatter, result all-to-all (communicator 1), D2H
 # Communicators per rank: the two exchange RcclComms (rows, results; their kernels run on the
 # streams above, RCCL opens no stream of its own for them) and the gloo control plane (CPU).
-# No torch NCCL process group exists on the serving path. IGP_XCHG_STREAMS=5 gives the
-# all-to-alls two CU-masked streams of their own (6 streams: an A/B knob, over the budget).
+# With the node-shared rows and results regions (IGP_XCHG_ROWS=shm, IGP_XCHG_RESULTS=d2h: the
+# serving default) a rank has no RCCL communicator at all: copy = compact from the rows region
+# + dedup insert, state, model + scatter into the results region - three streams + default.
+# No torch NCCL process group exists on the serving path. (Round 5's A/B mode with two
+# CU-masked streams of their own for the collectives was removed: it exceeded the queue budget.)
 HW_QUEUES = 4
 EXCHANGE_COMMUNICATORS = 2
 
 
-def map_results_region(name: str, depth: int, world: int, cmax: int) -> dict:
+def rows_mode() -> str:
+    """How rows reach their owners (IGP_XCHG_ROWS): ``shm`` (default) through the node-shared
+    rows region - every sender packs its per-owner chunks into page-locked /dev/shm and each
+    owner's copy stage compacts its chunks straight from host memory (the rows cross PCIe once,
+    host -> owner, as in the single-GPU pipeline; no collective on the hot path); ``rccl``: an
+    H2D copy to the ingress GPU, then the RCCL row all-to-all over xGMI. The requests arrive in
+    host memory either way, so the all-to-all adds a hop: at world 1 the exchange path measured
+    94 M scores/s against 129 M for the plain pipeline on the same box (profiles/r6/a)."""
+    m = os.environ.get("IGP_XCHG_ROWS", "shm")
+    if m not in ("shm", "rccl"):
+        raise ValueError("IGP_XCHG_ROWS must be shm or rccl")
+    return m
+
+
+def map_results_region(name: str, depth: int, world: int, cmax: int, rows: bool = False) -> dict:
     """The node-shared result region of the per-GPU D2H result path (IGP_XCHG_RESULTS=d2h):
-    [depth][owner][sender][cmax][W] result chunks + one 64-B flag line per (slot, owner).
+    [depth][owner][sender][cmax][W] result chunks + one 64-B flag line per (slot, owner); with
+    ``rows`` also the rows region (IGP_XCHG_ROWS=shm): [depth][sender][owner][cmax + 1] ReqRec
+    chunks + one 64-B flag line per (slot, sender).
     Every rank opens the same name (O_CREAT, same size: no creation order needed); the group's
     creator unlinks it once every rank mapped it. Page-locked, so the owners' device copies into
     it are asynchronous DMA (and nodes of the captured model graphs)."""
@@ -76,7 +95,11 @@ def map_results_region(name: str, depth: int, world: int, cmax: int) -> dict:
     owner_stride = world * cmax * W
     slot_stride = world * owner_stride
     data = depth * slot_stride
-    size = data + depth * world * 64
+    sender_stride = world * (cmax + 1) * REQ
+    rows_slot_stride = world * sender_stride
+    rows_at = data + depth * world * 64
+    rows_flags_at = rows_at + depth * rows_slot_stride
+    size = rows_flags_at + depth * world * 64 if rows else data + depth * world * 64
     path = "/dev/shm/" + name.lstrip("/")
     fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o600)
     try:
@@ -87,18 +110,18 @@ def map_results_region(name: str, depth: int, world: int, cmax: int) -> dict:
         os.close(fd)
     base = ctypes.addressof(ctypes.c_char.from_buffer(mm))
     hipk().host_register(base, size)
-    return dict(name=name, path=path, mm=mm, base=base, size=size, owner_stride=owner_stride, slot_stride=slot_stride,
-                flags=base + data, depth=depth, world=world, cmax=cmax)
+    out = dict(name=name, path=path, mm=mm, base=base, size=size, owner_stride=owner_stride, slot_stride=slot_stride,
+               flags=base + data, depth=depth, world=world, cmax=cmax, rows=None)
+    if rows:
+        out["rows"] = dict(base=base + rows_at, slot_stride=rows_slot_stride, sender_stride=sender_stride,
+                           flags=base + rows_flags_at, offset=rows_at)
+    return out
 
 
-def stream_roles(mode: Optional[str] = None) -> dict:
-    """role -> the stream that carries it (``mode``: IGP_XCHG_STREAMS, default "3")."""
-    mode = mode if mode is not None else os.environ.get("IGP_XCHG_STREAMS", "3")
-    roles = dict(default="default", h2d="copy", rows_a2a="copy", compact="copy", features="state",
-                 model="model", results_a2a="model", d2h="model")
-    if mode == "5":
-        roles.update(rows_a2a="xs", results_a2a="ys")
-    return roles
+def stream_roles() -> dict:
+    """role -> the stream that carries it."""
+    return dict(default="default", h2d="copy", rows_a2a="copy", compact="copy", features="state",
+                model="model", results_a2a="model", d2h="model")
 
 
 @dataclass
@@ -132,15 +155,9 @@ class DpGpuScorer(GpuScorer):
         self.cbuckets = sorted(set(int(c) for c in cbuckets))
         cfg = copy.deepcopy(cfg)
         cfg.gpu.buckets = [self.senders * c for c in self.cbuckets]
-        # CUs reserved for the RCCL streams (collective kernels poll: sharing CUs with K1 slowed
-        # both ~2x in the rocprofv3 timeline)
-        self._comm_cus = (int(os.environ.get("IGP_XCHG_COMM_CUS", "8"))
-                          if os.environ.get("IGP_XCHG_STREAMS", "3") == "5" else 0)
         super().__init__(cfg, store, plan=plan, model=model, device=device, pipeline_depth=pipeline_depth,
                          update_features=update_features, use_graphs=True, owner_filter=False, rank=rank)
-        self.comms = list(comms)
-        if len(self.comms) != 2:
-            raise ValueError("the exchange needs two RCCL communicators (rows, results)")
+        self.comms = list(comms or [])
         cmax, dev = self.cbuckets[-1], self.device
         self.xbytes_max = self.world * (cmax + 1) * REQ
         self.rbytes_max = self.world * cmax * (RES_BYTES + FEAT_BYTES)
@@ -153,15 +170,9 @@ class DpGpuScorer(GpuScorer):
         self.host_x = [torch.zeros(self.xbytes_max, dtype=torch.uint8).pin_memory() for _ in range(self.depth)]
         self.host_x_np = [t.numpy() for t in self.host_x]
         self.host_rr = [torch.zeros(self.rbytes_max, dtype=torch.uint8).pin_memory() for _ in range(self.depth)]
-        cs = getattr(self, "comm_streams", ())
-        if os.environ.get("IGP_XCHG_STREAMS", "3") == "3":
-            # the row all-to-all on the copy stream, the result all-to-all + D2H on the model
-            # stream: two cross-stream hops per batch, as in the single-GPU pipeline
-            self.xstream, self.ystream = self.cstream, self.mstream
-        elif len(cs) == 2:
-            self.xstream, self.ystream = cs
-        else:  # no CU split (IGP_CU_SPLIT=none / heuristic model)
-            self.xstream, self.ystream = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+        # the row all-to-all on the copy stream, the result all-to-all + D2H on the model stream:
+        # two cross-stream hops per batch, as in the single-GPU pipeline
+        self.xstream, self.ystream = self.cstream, self.mstream
         self.xgraphs = {}
         self.xdriver = None
         self._watch = None
@@ -171,6 +182,16 @@ class DpGpuScorer(GpuScorer):
                          else map_results_region(results_shm, self.depth, self.world, self.cbuckets[-1]))
             if (self.rshm["depth"], self.rshm["world"], self.rshm["cmax"]) != (self.depth, self.world, self.cbuckets[-1]):
                 raise ValueError("results region shape does not match the scorer")
+        # rows through the node-shared rows region (IGP_XCHG_ROWS=shm): no communicator at all
+        self.rows_shm = self.rshm is not None and self.rshm.get("rows") is not None
+        if self.rows_shm:
+            r = self.rshm["rows"]
+            # this sender's block of each slot: submit_rows packs its chunks there directly
+            self.host_x_np = [np.frombuffer(self.rshm["mm"], np.uint8, r["sender_stride"],
+                                            r["offset"] + s * r["slot_stride"] + self.rank * r["sender_stride"])
+                              for s in range(self.depth)]
+        elif len(self.comms) != 2:
+            raise ValueError("the exchange needs two RCCL communicators (rows, results)")
 
     def stream_map(self) -> dict:
         """role -> HIP stream handle actually used by this rank (see :func:`stream_roles`)."""
@@ -208,6 +229,17 @@ class DpGpuScorer(GpuScorer):
         if self.update_features:
             K.dedup_insert(self.store, self.cfg_dev, sb.req, b, sb.hdr)
 
+    def _rows_post_body(self, slot: int, C: int) -> None:
+        """Rows-region copy stage: this owner's chunk of every sender's block, compacted straight
+        from page-locked host memory (the batch header comes along), then the dedup insert."""
+        sb, b, r = self.slots[slot], self.cap(C), self.rshm["rows"]
+        first = r["base"] + slot * r["slot_stride"] + self.rank * (C + 1) * REQ
+        hipk().exchange_compact(first, sb.req.data_ptr(), sb.dev_slab.data_ptr(), sb.route.data_ptr(),
+                                self.world, C, b, torch.cuda.current_stream().cuda_stream,
+                                r["sender_stride"] // REQ, self.host_slab[slot].data_ptr())
+        if self.update_features:
+            K.dedup_insert(self.store, self.cfg_dev, sb.req, b, sb.hdr)
+
     def _xmodel_body(self, slot: int, C: int, with_features: bool, send: int = 0) -> None:
         """The model, K5, and the scatter of each row's result (+ feature image) into its
         sender's chunk of ``send`` (default: the slot's device buffer for the result
@@ -224,7 +256,7 @@ class DpGpuScorer(GpuScorer):
                                 send or sb.rsend.data_ptr(), C, b,
                                 torch.cuda.current_stream().cuda_stream)
 
-    # ---- collectives captured into the graphs (RCCL stream capture, IGP_XCHG_CAPTURE=1)
+    # ---- collectives captured into the graphs (RCCL stream capture)
     def _a2a_rows(self, slot: int, C: int) -> None:
         sb = self.slots[slot]
         self.comms[0].all_to_all(sb.xsend.data_ptr(), sb.xrecv.data_ptr(), (C + 1) * REQ,
@@ -259,17 +291,18 @@ class DpGpuScorer(GpuScorer):
 
     def capture(self) -> None:
         """Capture send / post / state / model / model+features graphs per (C, slot), each on
-        the stream it replays on, and hand them to the native exchange driver. With
-        IGP_XCHG_CAPTURE=1 (default) the two all-to-alls and the D2H copy are captured into the
-        send and model graphs too (three graph launches per batch)."""
+        the stream it replays on, and hand them to the native exchange driver. The two all-to-alls
+        and the D2H copy are captured into the send and model graphs too (three graph launches
+        per batch)."""
         dev = self.device
+        if self.rows_shm:
+            return self._capture_rows_shm()
         # the stages are always graph replays: recorded direct launches with driver-issued
         # collectives measured 67.4 vs 100.9 M scores/s at world 1 (profiles/r2/direct3), and the
         # collective-free state stage as recorded launches 91.7 / 90.4 vs 90.7 / 104.0
         # (profiles/r2/xab); both were removed in round 5
         self.direct = False
-        self.captured = (os.environ.get("IGP_XCHG_CAPTURE", "1") == "1"
-                         and self.xstream is self.cstream and self.ystream is self.mstream)
+        self.captured = True
         with torch.cuda.device(dev):
             for C in self.cbuckets:
                 for slot in range(self.depth):
@@ -344,6 +377,64 @@ class DpGpuScorer(GpuScorer):
             d.set_state_clock(self.state_clock)
         self.xdriver = d
         self.driver = None  # the three-graph driver of the single-GPU path is not used here
+
+    def _capture_rows_shm(self) -> None:
+        """Rows and results through the node-shared regions: the three stages as recorded
+        launches (oplist.h) issued by the native driver - copy (compact from the rows region +
+        dedup insert), state (K1 + update), model (trees / head / K5 + scatter into the results
+        region). GRU plans keep graphs for the state / model stages (not recordable)."""
+        dev = self.device
+        self.direct = False
+        self.captured = False
+        self.stage_ops = not any(s.kind == "gru" for s in (self.plan.steps if self.plan else []))
+        m = hipk()
+        d = m.XchgDriver(self.cstream.cuda_stream, self.stream.cuda_stream, self.mstream.cuda_stream,
+                         self.xstream.cuda_stream, self.ystream.cuda_stream, self.depth, self.world, None, None)
+        for slot, sb in enumerate(self.slots):
+            d.set_slot(slot, self.host_slab[slot].data_ptr(), self.host_x[slot].data_ptr(),
+                       self.host_rr[slot].data_ptr(), sb.xsend.data_ptr(), sb.xrecv.data_ptr(), sb.rsend.data_ptr(),
+                       sb.rrecv.data_ptr(), self.xbytes_max, self.rbytes_max)
+        with torch.cuda.device(dev):
+            for C in self.cbuckets:
+                for slot in range(self.depth):
+                    self._write_hdr(slot, 0, 0)
+                    with K.Recorder() as r:
+                        self._rows_post_body(slot, C)
+                    d.set_copy_ops(C, slot, r.ops)
+                    stages = [lambda: self._state_body(slot, self.cap(C)),
+                              lambda: self._xmodel_body(slot, C, False, self._region(slot)),
+                              lambda: self._xmodel_body(slot, C, True, self._region(slot))]
+                    if self.stage_ops:
+                        lists = []
+                        for body in stages:
+                            with K.Recorder() as r:
+                                body()
+                            lists.append(r.ops)
+                        d.set_stage_ops(C, slot, *lists)
+                        continue
+                    gs = []
+                    for body, st in zip(stages, (self.stream, self.mstream, self.mstream)):
+                        st.wait_stream(torch.cuda.current_stream())
+                        with torch.cuda.stream(st):
+                            body()
+                        torch.cuda.current_stream().wait_stream(st)
+                        g = torch.cuda.CUDAGraph()
+                        with K.graph_capture(g, st):
+                            body()
+                        gs.append(g)
+                    self.xgraphs[(C, slot)] = (None, None, *gs)
+                    d.set_graphs(C, slot, 0, 0, *[g.raw_cuda_graph_exec() for g in gs])
+            torch.cuda.synchronize(dev)
+        rs = self.rshm
+        d.set_results_shm(rs["base"], rs["slot_stride"], rs["owner_stride"], rs["flags"], self.rank)
+        ms = self.cfg.gpu.batch_timeout_ms if self.cfg.gpu.batch_timeout_ms > 0 else 5000
+        d.set_owner_deadline_us(int(2 * ms * 1000))
+        rw = rs["rows"]
+        d.set_rows_shm(rw["base"], rw["slot_stride"], rw["sender_stride"], rw["flags"])
+        if getattr(self, "state_clock", None) is not None:
+            d.set_state_clock(self.state_clock)
+        self.xdriver = d
+        self.driver = None
 
     # ------------------------------------------------------------------ batches
     def cbucket_for(self, c: int) -> int:

@@ -1042,9 +1042,14 @@ def make_local_backend(cfg: Config, kind: str, capacity: int, fm, mkind: str, bl
         exchange = None
         if comm is not None:
             from ..parallel.exchange import chunk_capacity, rccl_comms
+            from .dp import rows_mode
+            # rows and results through the node-shared regions: no communicator (engine/dp.py
+            # rows_mode); otherwise the two RCCL communicators of the all-to-alls
+            rows_shm = bool(results_shm) and rows_mode() == "shm"
             # every rank ingests: each step carries up to C rows per (sender, owner) pair
-            exchange = dict(comms=rccl_comms(comm.rank, comm.world), world=comm.world, senders=comm.world,
-                            cbuckets=[chunk_capacity(max(cfg.gpu.buckets), comm.world)])
+            exchange = dict(comms=[] if rows_shm else rccl_comms(comm.rank, comm.world), world=comm.world,
+                            senders=comm.world, cbuckets=[chunk_capacity(max(cfg.gpu.buckets), comm.world)],
+                            rows_shm=rows_shm)
             if results_shm:  # per-GPU D2H result path instead of the result all-to-all
                 exchange["results_shm"] = results_shm
         return GpuBackend(cfg, capacity, dev, plan=plan, model=model, blacklist=blacklist, ipintel=ipintel,

@@ -190,11 +190,6 @@ class GpuScorer:
         else:
             a, b = (int(x) for x in arg.split("/"))
             st = [i % b < a for i in range(n_cu)]
-        # the data-parallel exchange (engine/dp.py) reserves CUs [0, comm) of the state side for
-        # its RCCL streams, so collective kernels never share CUs with K1 / the model
-        comm = int(getattr(self, "_comm_cus", 0))
-        cm = [i < comm for i in range(n_cu)]
-        st = [x and not c for x, c in zip(st, cm)]
 
         def words(sel):
             w = [0] * ((n_cu + 31) // 32)
@@ -203,18 +198,17 @@ class GpuScorer:
                     w[i // 32] |= 1 << (i % 32)
             return w
 
-        model = [not x and not c for x, c in zip(st, cm)]
-        key = (self.device.index, kind, arg, comm)
+        model = [not x for x in st]
+        key = (self.device.index, kind, arg)
         if key not in _CU_STREAMS:  # HIP streams live for the process: reused by later scorers
-            masks = (st, st, model) + ((cm, cm) if comm else ())
+            masks = (st, st, model)
             with torch.cuda.device(self.device):
                 _CU_STREAMS[key] = tuple(torch.cuda.ExternalStream(K._mod().cu_stream(words(m)), device=self.device)
                                          for m in masks)
             if len(_CU_STREAMS) == 1:
                 import atexit
                 atexit.register(_destroy_cu_streams)
-        self.stream, self.cstream, self.mstream = _CU_STREAMS[key][:3]
-        self.comm_streams = _CU_STREAMS[key][3:]
+        self.stream, self.cstream, self.mstream = _CU_STREAMS[key]
 
     # ------------------------------------------------------------------ buffers / config
     def _alloc_slot(self) -> "_Slot":

@@ -17,14 +17,14 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(tmp_path, config, world, population=3000):
+def _run(tmp_path, config, world, population=3000, threads=1):
     out = str(tmp_path / f"{config}-w{world}")
     env = dict(os.environ, IGP_BENCH_BACKEND="cpu", IGP_BENCH_SMALL_MODELS="1", MASTER_ADDR="127.0.0.1")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--config", config,
            "--accounts", str(population // world), "--steps", "2", "--warmup", "1", "--calls", "300",
-           "--inflight", "256", "--check-out", out]
+           "--inflight", "256", "--check-out", out, "--drive-threads", str(threads)]
     r = subprocess.run(cmd, env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
@@ -54,8 +54,10 @@ def test_acct_dp_bench_answers_equal_single_process(tmp_path, config, worlds):
     want = _norm(config, ans1)
     assert len(set(want)) > 1  # the fixed calls do not all have the same answer
     for w in worlds:
-        res, per_rank = _run(tmp_path, config, w)
+        # world 2: three submitting threads per rank (answers through the router's sink)
+        res, per_rank = _run(tmp_path, config, w, threads=3 if w == 2 else 1)
         assert res["n_gpus"] == w and res["errors"] == 0 and res["cold_path_calls"] == 0
+        assert res["config"]["submit_threads_per_rank"] == (3 if w == 2 else 1)
         # calls of every rank crossed the mailbox to other owners
         assert res["remote_calls_rank_sum"] > 0
         assert res["config"]["parallelism"].startswith(f"dp{w}")

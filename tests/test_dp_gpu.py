@@ -98,14 +98,17 @@ def _init_pg(backend, **kw):
                 raise
 
 
-@pytest.mark.parametrize("results", ["a2a", "d2h"])
-def test_spmd_engine_world1_matches_plain_gpu_engine(monkeypatch, results):
+@pytest.mark.parametrize("results,rows", [("a2a", "rccl"), ("d2h", "rccl"), ("d2h", "shm")])
+def test_spmd_engine_world1_matches_plain_gpu_engine(monkeypatch, results, rows):
     """The SPMD serving engine at world 1 (its native core driving the exchange pipeline)
     answers exactly like the plain GPU engine, with the results returning through the result
-    all-to-all or through the per-GPU D2H copies into the node-shared region (IGP_XCHG_RESULTS)."""
+    all-to-all or through the per-GPU D2H copies into the node-shared region (IGP_XCHG_RESULTS),
+    and the rows reaching their owner through the RCCL row all-to-all or the node-shared rows
+    region (IGP_XCHG_ROWS; shm: no communicator at all)."""
     import torch
     import torch.distributed as dist
     monkeypatch.setenv("IGP_XCHG_RESULTS", results)
+    monkeypatch.setenv("IGP_XCHG_ROWS", rows)
     from igaming_platform_amd.config import Config
     from igaming_platform_amd.engine.risk_engine import RiskEngine
     from igaming_platform_amd.parallel.comm import TorchComm
@@ -119,6 +122,8 @@ def test_spmd_engine_world1_matches_plain_gpu_engine(monkeypatch, results):
         assert spmd.local.scorer.__class__.__name__ == "DpGpuScorer"
         assert (spmd.local.scorer.rshm is not None) == (results == "d2h")
         assert spmd.local.scorer.stage_ops  # state (+ d2h: model) stages as recorded launches
+        assert spmd.local.scorer.rows_shm == (rows == "shm")
+        assert len(spmd.local.scorer.comms) == (0 if rows == "shm" else 2)
         if results == "d2h":
             assert not os.path.exists(spmd.local.scorer.rshm["path"])  # unlinked once every rank mapped it
         rng = np.random.default_rng(2)
@@ -142,7 +147,7 @@ def test_spmd_engine_world1_matches_plain_gpu_engine(monkeypatch, results):
         dist.destroy_process_group()
 
 
-def test_spmd_engines_close_and_destroy_their_communicators():
+def test_spmd_engines_close_and_destroy_their_communicators(monkeypatch):
     """two SPMD world-1 engines created and closed one after the other in one
     process. Each close stops the serving core, destroys the exchange graphs (RCCL keeps a
     reference on a communicator per graph that captured its collectives) and then both RCCL
@@ -153,6 +158,7 @@ def test_spmd_engines_close_and_destroy_their_communicators():
     from igaming_platform_amd.config import Config
     from igaming_platform_amd.engine.risk_engine import RiskEngine
     from igaming_platform_amd.parallel.comm import TorchComm
+    monkeypatch.setenv("IGP_XCHG_ROWS", "rccl")  # the communicator lifecycle (rows region: none)
     for round_ in range(2):
         _init_pg("gloo")
         eng = None
@@ -224,6 +230,48 @@ def test_exchange_kernels_multi_sender_layout(world, C):
     got = send.cpu().numpy().reshape(world, C * 136)
     mask = scatter_results(np.ones((n, 2), np.uint32), np.ones(n, FEATREC), route_ref, world, C) != 0
     np.testing.assert_array_equal(got[mask], want[mask])
+
+
+@pytest.mark.parametrize("world,C", [(1, 64), (3, 40), (8, 16)])
+def test_exchange_compact_from_the_node_shared_rows_region(world, C):
+    """The rows-region copy stage: exchange_compact reading this owner's chunk of every sender's
+    block straight from page-locked host memory ([sender][owner][C + 1], sender stride
+    world * (C + 1)) and copying the batch header along equals the host twin over the chunks
+    this owner would have received from the all-to-all."""
+    import torch
+    from igaming_platform_amd.layouts import REQREC
+    from igaming_platform_amd.native import hipk
+    from igaming_platform_amd.parallel.exchange import build_chunks, compact
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(100 + world)
+    me = world - 1
+    region = torch.zeros(world * world * (C + 1) * 48, dtype=torch.uint8).pin_memory()
+    blocks = region.numpy().view(REQREC).reshape(world, world * (C + 1))
+    for p in range(world):  # sender p's block: its chunks for every owner (<= C rows each)
+        owners = np.repeat(np.arange(world), rng.integers(0, C + 1, world))
+        rng.shuffle(owners)
+        n = len(owners)
+        rows = np.zeros(n, REQREC)
+        rows["slot"] = rng.integers(0, 1000, n)
+        rows["tx_type"] = rng.integers(0, 4, n) | (p << 8)
+        rows["amount"] = rng.integers(1, 10**6, n)
+        rows["ts"] = NOW + p
+        blocks[p] = build_chunks(rows, owners, world, C)[0]
+    recv = np.concatenate([blocks[p, me * (C + 1):(me + 1) * (C + 1)] for p in range(world)])
+    cap = world * C
+    slab = torch.zeros(16 + 48 * cap, dtype=torch.uint8, device=dev)
+    route = torch.full((cap + 1,), -7, dtype=torch.int32, device=dev)
+    hdr = torch.tensor([0, 4242, NOW & 0xFFFFFFFF, NOW >> 32], dtype=torch.int32).pin_memory()
+    first = region.data_ptr() + me * (C + 1) * 48
+    hipk().exchange_compact(first, slab.data_ptr() + 16, slab.data_ptr(), route.data_ptr(), world, C, cap,
+                            torch.cuda.current_stream().cuda_stream, world * (C + 1), hdr.data_ptr())
+    torch.cuda.synchronize()
+    rows_ref, route_ref = compact(recv, world, C)
+    n = int(slab[:4].view(torch.int32).item())
+    assert n == len(rows_ref) and int(slab[4:8].view(torch.int32).item()) == 4242
+    got = slab[16:16 + 48 * n].cpu().numpy().view(REQREC)
+    np.testing.assert_array_equal(got.view(np.uint8), rows_ref.view(np.uint8))
+    np.testing.assert_array_equal(route[:n].cpu().numpy(), route_ref)
 
 
 def test_exchange_rank_fits_the_hardware_queue_budget():

@@ -1,0 +1,172 @@
+#!/usr/bin/env python3
+"""Mixed traffic on one GPU: the serving bench's ScoreBatch load plus open-loop
+CheckBonusAbuse and unary ScoreTransaction over the native HTTP/2 server, all at once.
+
+The reference calls CheckBonusAbuse from the node that scores wallet traffic
+(/root/reference/services/bonus/internal/service/bonus_engine.go:268-275 for the award path,
+services/wallet/internal/service/wallet_service.go:261-279 for the per-transaction risk check).
+Here one engine holds the cfg3 fraud model, the cfg4 LTV MLP and the cfg5 abuse GRU; the run is
+
+  phase A  ScoreBatch alone: ``--threads`` in-process ingress threads, 8192-transaction requests
+           through the native serving core (as bench.py's serving scope) for ``--seconds``
+  phase B  the same ScoreBatch load + ``--abuse-rate`` CheckBonusAbuse/s + ``--tx-rate``
+           ScoreTransaction/s, open loop from the native load generator (C++ HTTP/2 clients,
+           latency from the scheduled send time) over ``--clients`` connections each
+
+and reports the ScoreBatch throughput of both phases (the loss the unary traffic costs it), the
+unary p50 / p99, the abuse device's cluster fallbacks (gru_wsx clusters that did not become
+co-resident) and the device steps of each path. One JSON line (``--json-out``).
+
+Usage: python tools/bench_mixed.py [--seconds 5] [--abuse-rate 100000] [--tx-rate 200000]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
+
+def build(accounts: int):
+    """One engine: cfg3 fraud model (8192-row micro-batches), cfg4 LTV MLP, cfg5 abuse GRU; warehouse
+    rows + ext rows for every account, profile rows for the LTV model, full event rings."""
+    import bench_e2e as E
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.engine.risk_engine import RiskEngine
+    from igaming_platform_amd.layouts import ACCTBATCH
+    from igaming_platform_amd.onnx import builders
+    from igaming_platform_amd.utils.synth import make_population
+    cfg = Config()
+    cfg.features.width = 128
+    cfg.gpu.buckets = [64, 512, 2048, 8192]
+    cfg.gpu.max_batch = 8192
+    eng = RiskEngine(cfg, backend="gpu", capacity=accounts + 4096, fraud_model=E.fraud_model_bytes("cfg3"),
+                     ltv_model=builders.build("ltv_mlp", n_features=256, width=512, layers=4).SerializeToString(),
+                     abuse_model=builders.build("gru", seq=100, in_dim=16, hidden=256).SerializeToString())
+    pop = make_population(accounts, 98, seed=3, fast_hash=True)
+    ids = [E.account_id(i) for i in range(accounts)]
+    rng = np.random.default_rng(5)
+    step = 1 << 18
+    for s in range(0, accounts, step):
+        eng.load_batch_features(ids[s:s + step], np.asarray(pop.batch[s:s + step], ACCTBATCH))
+        eng.load_ext_features(ids[s:s + step], pop.ext[s:s + step])
+        slots, owners = eng.registry.resolve_ids(ids[s:s + step], insert=True)
+        n = len(slots)
+        eng.ltv.set_rows(slots, owners, np.floor(rng.uniform(0, 1, (n, 25)) * E.PROFILE_SCALE).astype(np.float32),
+                         rng.normal(0, 1, (n, 231)).astype(np.float32))
+    E.fill_event_rings(eng.backends[0].store)
+    return eng
+
+
+def batch_load(eng, payloads, threads: int, seconds: float, t_base: int, stop_evt=None):
+    """Closed-loop ScoreBatch from ``threads`` ingress threads for ``seconds``: (rows/s, p50, p99 ms)."""
+    core = eng.core
+    lock = threading.Lock()
+    lat, rows = [], [0]
+    t_end = time.perf_counter() + seconds
+    counter = [0]
+
+    def worker():
+        while time.perf_counter() < t_end:
+            with lock:
+                i = counter[0]
+                counter[0] += 1
+            t0 = time.perf_counter_ns()
+            out = core.score_batch(payloads[i % len(payloads)], t_base + i // 50, t0)
+            dt = (time.perf_counter_ns() - t0) / 1e6
+            with lock:
+                lat.append(dt)
+                rows[0] += len(out)
+    th = [threading.Thread(target=worker) for _ in range(threads)]
+    t0 = time.perf_counter()
+    [t.start() for t in th]
+    [t.join() for t in th]
+    el = time.perf_counter() - t0
+    return rows[0] / el, float(np.percentile(lat, 50)), float(np.percentile(lat, 99)), counter[0]
+
+
+def open_loop(port: int, rpc: str, payloads, rate: float, seconds: float, conns: int, out: dict):
+    from igaming_platform_amd.native import native
+    from igaming_platform_amd.proto import risk_v1 as P
+    path = P.method_path({"abuse": "CheckBonusAbuse", "tx": "ScoreTransaction"}[rpc])
+    r = native().grpc_load("127.0.0.1", port, path, payloads, float(rate), float(seconds), int(conns), 8192)
+    lat = np.asarray(r["latency_ms"])
+    out[rpc] = dict(offered_per_s=rate, achieved_per_s=round(len(lat) / float(r["elapsed"]), 1), calls=int(r["sent"]),
+                    errors=int(r["errors"]),
+                    p50_ms=round(float(np.percentile(lat, 50)), 3) if len(lat) else None,
+                    p99_ms=round(float(np.percentile(lat, 99)), 3) if len(lat) else None)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--accounts", type=int, default=1 << 20)
+    ap.add_argument("--seconds", type=float, default=5.0)
+    ap.add_argument("--threads", type=int, default=8, help="ScoreBatch ingress threads")
+    ap.add_argument("--abuse-rate", type=float, default=100000.0)
+    ap.add_argument("--tx-rate", type=float, default=200000.0)
+    ap.add_argument("--clients", type=int, default=4, help="HTTP/2 connections per open-loop RPC")
+    ap.add_argument("--server-workers", type=int, default=4)
+    ap.add_argument("--json-out", default="")
+    a = ap.parse_args(argv)
+    import bench_e2e as E
+    from igaming_platform_amd.api.native_grpc import NativeRiskServer
+    from igaming_platform_amd.utils.synth import NOW0
+    eng = build(a.accounts)
+    srv = NativeRiskServer(eng, port=0, workers=a.server_workers, batching=True).start()
+    payloads = E.spread_payloads(a.accounts, 64, 8192, seed=11)
+    abuse_p = E.acct_payloads(a.accounts, "abuse", 1 << 16, 300)
+    tx_p = E.tx_payloads(a.accounts, 8192, seed=300)
+    # warm: graphs, histories, both unary paths
+    batch_load(eng, payloads, a.threads, 2.0, NOW0 - 3600)
+    warm = {}
+    open_loop(srv.port, "abuse", abuse_p, 2000, 1.0, a.clients, warm)
+    open_loop(srv.port, "tx", tx_p, 2000, 1.0, a.clients, warm)
+    dev = [d for d in eng.acct.devices if hasattr(d, "driver") and hasattr(d.driver, "fallbacks")]
+    fb0 = sum(int(d.driver.fallbacks) for d in dev)
+    acct0 = eng.acct.router.stats(3, True)
+    alone = batch_load(eng, payloads, a.threads, a.seconds, NOW0)
+    time.sleep(1.0)
+    eng.acct.router.stats(3, True)
+    res = {}
+    th = [threading.Thread(target=open_loop, args=(srv.port, "abuse", abuse_p, a.abuse_rate, a.seconds, a.clients, res)),
+          threading.Thread(target=open_loop, args=(srv.port, "tx", tx_p, a.tx_rate, a.seconds, a.clients, res))]
+    [t.start() for t in th]
+    mixed = batch_load(eng, payloads, a.threads, a.seconds, NOW0 + 600)
+    [t.join() for t in th]
+    st = eng.acct.router.stats(3, False)
+    fb = sum(int(d.driver.fallbacks) for d in dev) - fb0
+    out = dict(metric="mixed traffic on one GPU: ScoreBatch load + open-loop CheckBonusAbuse + ScoreTransaction",
+               n_gpus=1, seconds=a.seconds, data="synthetic (UUID ids over %d accounts, random-init cfg3/cfg4/cfg5 "
+                                                "weights, full 100-event histories)" % a.accounts,
+               scorebatch_alone=dict(scores_per_s=round(alone[0], 1), p50_ms=round(alone[1], 3), p99_ms=round(alone[2], 3),
+                                     requests=alone[3]),
+               scorebatch_mixed=dict(scores_per_s=round(mixed[0], 1), p50_ms=round(mixed[1], 3), p99_ms=round(mixed[2], 3),
+                                     requests=mixed[3]),
+               scorebatch_loss_pct=round(100.0 * (1 - mixed[0] / alone[0]), 2),
+               check_bonus_abuse=res.get("abuse"), score_transaction=res.get("tx"),
+               abuse_cluster_fallbacks=fb,
+               abuse_rows_per_device_step=round(st.get("items", 0) / max(int(st.get("steps", 1)), 1), 1),
+               config=dict(scorebatch_threads=a.threads, clients_per_rpc=a.clients, server_workers=a.server_workers,
+                           models="cfg3 GBDT(100,d7,128f)+MLP(32-256-1) fp32; cfg5 GRU 2x256 x 100 events fp32 split"),
+               server_stats=srv.stats())
+    srv.stop()
+    eng.close()
+    line = json.dumps(out)
+    print(line, flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            f.write(line + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
