@@ -100,6 +100,9 @@ def parse():
     ap.add_argument("--zipf", type=float, default=0.0, help="serving: Zipf exponent of the account ids (0: uniform)")
     ap.add_argument("--payloads", type=int, default=128, help="serving: distinct ScoreBatch requests per rank "
                     "(their account ids spread over the whole population)")
+    ap.add_argument("--sum-mode", default="sliding", choices=["sliding", "compat"],
+                    help="fraud configs: the 1h amount sum - sliding (exact, from the tx ring: default) or compat "
+                         "(the reference's INCRBY-with-TTL running sum, redis_store.go:136-138; quirk Q8)")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
     if a.numerics == "auto":  # the ONNX models' f32 contract everywhere (cfg4 / cfg5: split MFMA)
@@ -385,7 +388,7 @@ def main():
     if world > 1 and backend == "nccl" and dist.get_backend() != "nccl":
         DATA_PG = dist.new_group(backend="nccl")  # replicas fallback: results all-gather over RCCL
     S = benchkit.build(a.config, a.batch, a.accounts, dev, rank=rank, depth=a.depth,
-                       use_graphs=not a.no_graphs, precision=a.numerics)
+                       use_graphs=not a.no_graphs, precision=a.numerics, sum_mode=a.sum_mode)
     sc, pool, B = S.scorer, S.pool, S.batch
     c = dict(desc=S.desc)
     n_acc = a.accounts
@@ -481,6 +484,7 @@ def main():
             "driver": "native" if sc.driver is not None else "python",
             "dp_mode": a.dp_mode if world > 1 else "none",
             "numerics": numerics_desc(a),
+            "sum_mode": a.sum_mode,
         },
         "scope": "engine_only",
         "p99_latency_ms": p99,
@@ -709,6 +713,7 @@ def serving_bench(a) -> None:
     B = a.requests or a.batch or c["batch"]
     cfg = Config()
     cfg.features.width = c["width"]
+    cfg.features.sum_mode = a.sum_mode
     cfg.fraud_model.precision = a.numerics
     cfg.gpu.buckets = sorted({64, 512, 2048, B})
     cfg.gpu.max_batch = B
@@ -871,7 +876,7 @@ def serving_bench(a) -> None:
                                       "population": total, "requests_in_stream_per_rank": a.payloads,
                                       "distinct_accounts_in_stream_rank0": spread.get("distinct_accounts"),
                                       "transactions_in_stream_per_rank": spread.get("transactions")},
-                   "numerics": numerics_desc(a),
+                   "numerics": numerics_desc(a), "sum_mode": a.sum_mode,
                    "comm_env": {k: v for k, v in sorted(os.environ.items())
                                 if k.startswith(("NCCL_", "RCCL_")) or k == "GPU_MAX_HW_QUEUES"}},
         "scope": "serving (risk.v1 ScoreBatch bytes in -> bytes out, in-process, every rank ingesting)",

@@ -79,10 +79,14 @@ struct AcctRT {
   int32_t ring_head;        // next tx-ring write position
   int32_t ev_head;          // next event-ring write position
   int32_t ev_count;
-  // padding as scalars, not an array: a kernel-local copy of a struct with an array member became
+  // HyperLogLog estimates of the two register files (before the TTL check), kept by every path
+  // that changes a register (PFCOUNT on a cached cardinality, as Redis keeps it in the HLL header,
+  // redis_store.go:80-81): feature assembly reads these 8 bytes instead of 512 register bytes
+  int32_t hll_dev_n, hll_ip_n;
+  // padding as a scalar, not an array: a kernel-local copy of a struct with an array member became
   // an LDS-promoted alloca indexed by the flat work-item id, i.e. one read of the dispatch packet
   // (host memory) per wave for the work-group size (K1, the update kernels)
-  int32_t pad0, pad1, pad2;
+  int32_t pad0;
 };
 static_assert(sizeof(AcctRT) == 64, "AcctRT must be 64 bytes");
 

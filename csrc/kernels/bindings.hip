@@ -67,6 +67,8 @@ UpdateArgs update_args(const py::dict& d) {
   a.dmax = geti(d, "dmax");
   a.region = geti(d, "region", DEDUP_STANDALONE);
   a.src = ptr<const char*>(d, "src");
+  a.hll_lc = ptr<const int32_t*>(d, "hll_lc");
+  if (!a.hll_lc) throw std::runtime_error("update args: hll_lc table required (cached HLL estimates)");
   if (a.src && (a.region >= 0 || !a.hdr)) throw std::runtime_error("update args: slab source needs the scorer ring");
   if (!a.dbuf || !a.cfg || !a.req || !a.rt) throw std::runtime_error("update args: missing pointers");
   if (a.n_max > a.dmax || a.dcap < 2 * a.dmax) throw std::runtime_error("update args: dedup scratch too small");

@@ -71,29 +71,50 @@ __device__ __forceinline__ T qsum(T v) {
   return v;
 }
 
-__device__ __forceinline__ uint32_t pick4(const uint32_t (&w)[4], int i) {
-  return i == 0 ? w[0] : i == 1 ? w[1] : i == 2 ? w[2] : w[3];
+// HLL estimate of a register file held as 4 words (16 registers) per lane of a quarter (lane ql
+// holds words ql + 16 i); every lane of the quarter gets it
+__device__ __forceinline__ int hll_count_q(const uint32_t (&w)[4], const int32_t* lc) {
+  double z = 0;
+  int v = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int r = (w[i] >> (8 * b)) & 0xff;
+      z += exp2_neg(r);
+      v += r == 0;
+    }
+  return hll_estimate(qsum(z), qsum(v), lc);
 }
 
-// PFADD on a register file held as 4 words (16 registers) per lane of a quarter: lane ql holds
-// words ql + 16 i. The owner lane of the register updates and stores its word; an expired key
-// (TTL) is rewritten as zeros first. Returns whether the register rose (golden new_device).
-__device__ __forceinline__ bool hll_add_q(uint32_t* words, const uint32_t (&w)[4], uint32_t& exp, uint64_t h,
-                                          int64_t now, int ttl, int ql, int qb) {
+// PFADD by the 16 lanes of a quarter that hold only the event's register word `w1` (the same
+// word in every lane: one load per account instead of the 512-byte file). An expired key (TTL)
+// is rewritten as zeros first; a raised register updates the account's cached estimate `cnt`:
+// after a reset directly (one non-zero register), otherwise from the file, read only then (a
+// register rises on an account's first events of a device / ip, not on repeats). Returns
+// whether the register rose (golden new_device).
+__device__ __forceinline__ bool hll_add_q(uint32_t* words, uint32_t w1, uint32_t& exp, int32_t& cnt, uint64_t h,
+                                          int64_t now, int ttl, int ql, const int32_t* lc) {
   const bool reset = now >= (int64_t)exp;
   const int idx = (int)(h & 255u);
   const int rank = hll_rank(h);
   const int wix = idx >> 2, sh = 8 * (idx & 3);
-  const bool own = ql == (wix & 15);
-  uint32_t cur = reset ? 0u : pick4(w, wix >> 4);
-  const bool mine = own && rank > (int)((cur >> sh) & 0xffu);
+  const uint32_t cur = reset ? 0u : w1;
+  const bool rise = rank > (int)((cur >> sh) & 0xffu);  // quarter-uniform
+  const uint32_t nw = (cur & ~(0xffu << sh)) | ((uint32_t)rank << sh);
   if (reset) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) words[ql + 16 * i] = 0u;
+    for (int i = 0; i < 4; ++i) words[ql + 16 * i] = ql + 16 * i == wix ? nw : 0u;
+    cnt = hll_estimate(255.0 + exp2_neg(rank), 255, lc);
+  } else if (rise) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = ql + 16 * i == wix ? nw : words[ql + 16 * i];
+    if (ql == (wix & 15)) words[wix] = nw;
+    cnt = hll_count_q(w, lc);
   }
-  if (mine) words[wix] = (cur & ~(0xffu << sh)) | ((uint32_t)rank << sh);
   exp = (uint32_t)(now + ttl);
-  return qballot(mine, qb) != 0u;
+  return rise;
 }
 
 // apply_event (update.h) by the 16 lanes of a quarter that already hold the account's AcctRT
@@ -101,8 +122,7 @@ __device__ __forceinline__ bool hll_add_q(uint32_t* words, const uint32_t (&w)[4
 // (one word each) with a single double log1p pass (lane 0: amount, lane 3: dt) and the
 // batch's precomputed hour-of-day word `hour_word` (dedup_insert_kernel).
 __device__ __forceinline__ void apply_event_q(const UpdateArgs& a, const ScoreCfg& cfg, const ReqRec& ev, AcctRT r,
-                                              const uint32_t (&wd)[4], const uint32_t (&wi)[4], int ql, int qb,
-                                              uint32_t hour_word) {
+                                              uint32_t wd, uint32_t wi, int ql, uint32_t hour_word, const int32_t* lc) {
   const int s = ev.slot;
   const int64_t now = event_ts(a, ev);
   const int64_t amt = ev.amount;
@@ -117,8 +137,8 @@ __device__ __forceinline__ void apply_event_q(const UpdateArgs& a, const ScoreCf
   r.sum_exp = (uint32_t)(now + cfg.sum_ttl);
   uint32_t* regs = reinterpret_cast<uint32_t*>(a.hll + (size_t)s * 512);
   bool new_dev = false, new_ip = false;
-  if (ev.dev_hash) new_dev = hll_add_q(regs, wd, r.hll_dev_exp, ev.dev_hash, now, cfg.hll_ttl, ql, qb);
-  if (ev.ip_hash) new_ip = hll_add_q(regs + 64, wi, r.hll_ip_exp, ev.ip_hash, now, cfg.hll_ttl, ql, qb);
+  if (ev.dev_hash) new_dev = hll_add_q(regs, wd, r.hll_dev_exp, r.hll_dev_n, ev.dev_hash, now, cfg.hll_ttl, ql, lc);
+  if (ev.ip_hash) new_ip = hll_add_q(regs + 64, wi, r.hll_ip_exp, r.hll_ip_n, ev.ip_hash, now, cfg.hll_ttl, ql, lc);
   r.last_tx = (uint32_t)now;
   r.last_tx_exp = (uint32_t)(now + cfg.last_tx_ttl);
   if (now >= (int64_t)r.session_exp || r.session_start == 0) r.session_start = (uint32_t)now;
@@ -384,13 +404,11 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     uint4 tsv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) tsv[i] = ts4[min(ql + 16 * i, n4 - 1)];
+    // HLL: the cardinalities come cached in AcctRT; only the two register words the request's
+    // own PFADDs touch are read (one address per quarter), for the single-event apply below
     const uint32_t* hreg = reinterpret_cast<const uint32_t*>(a.hll + (size_t)sc * 512);
-    uint32_t wd[4], wi[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      wd[i] = hreg[ql + 16 * i];
-      wi[i] = hreg[64 + ql + 16 * i];
-    }
+    uint32_t wd = hreg[(uint32_t)(rq.dev_hash & 255u) >> 2];
+    uint32_t wi = hreg[64 + ((uint32_t)(rq.ip_hash & 255u) >> 2)];
     AcctRT rt = load_rt(a.rt + sc);
     AcctBatch bt = a.batch[sc];
     const float* e = a.ext + (size_t)sc * ext_w;
@@ -422,7 +440,8 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
     // ---- mask what a missing account / short ring must not see
     if (!has) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { tsv[i] = make_uint4(0, 0, 0, 0); wd[i] = wi[i] = 0u; }
+      for (int i = 0; i < 4; ++i) tsv[i] = make_uint4(0, 0, 0, 0);
+      wd = wi = 0u;
       rt = AcctRT{};
       bt = AcctBatch{};
 #pragma unroll
@@ -447,7 +466,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       }
     }
     const bool blacklisted = qballot(hit, qb) != 0u;
-    if (trow) keep_issued((int)rt.ring_head + (int)tsv[0].x + (int)wd[0] + (int)bt.present + (int)extv[0]);
+    if (trow) keep_issued((int)rt.ring_head + (int)tsv[0].x + (int)wd + (int)bt.present + (int)extv[0]);
     K1_MARK(2);
     ipf = __shfl(ipf, qb + 3, 64);
 
@@ -492,28 +511,9 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       c5 = qsum(c5);
       c60 = qsum(c60);
       s60 = qsum(s60);
-      // ---- K8: HyperLogLog counts (p = 8; 16 registers per lane)
-      double zd = 0, zi = 0;
-      int vd = 0, vi = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const int rd = (wd[i] >> (8 * b)) & 0xff, ri = (wi[i] >> (8 * b)) & 0xff;
-          zd += exp2_neg(rd); vd += rd == 0;
-          zi += exp2_neg(ri); vi += ri == 0;
-        }
-      zd = qsum(zd); zi = qsum(zi);
-      vd = qsum(vd); vi = qsum(vi);
-      // linear counting (E <= 2.5 m, V > 0): floor(m ln(m / V) + 0.5) from the host-computed
-      // table (libm log, as the golden model); otherwise the harmonic estimate
-      const double m = 256.0, alpha = 0.7213 / (1.0 + 1.079 / 256.0);
-      const double ed = alpha * m * m / zd, ei = alpha * m * m / zi;
-      const int ld = s_lc[vd], li = s_lc[vi];
-      const int cd = (ed <= 2.5 * m && vd > 0) ? ld : (int)floor(ed + 0.5);
-      const int ci = (ei <= 2.5 * m && vi > 0) ? li : (int)floor(ei + 0.5);
-      hll_dev = now < (int64_t)rt.hll_dev_exp ? cd : 0;
-      hll_ip = now < (int64_t)rt.hll_ip_exp ? ci : 0;
+      // ---- K8: HyperLogLog counts (PFCOUNT): the estimates every register change keeps in AcctRT
+      hll_dev = now < (int64_t)rt.hll_dev_exp ? rt.hll_dev_n : 0;
+      hll_ip = now < (int64_t)rt.hll_ip_exp ? rt.hll_ip_n : 0;
     }
 
     // ---- assemble raw features (quarter-uniform values)
@@ -647,7 +647,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       }
       if (h >= 0) {
         if (dcount == 1) {
-          apply_event_q(a.upd, cfg, rq, rt, wd, wi, ql, qb, hour_word);
+          apply_event_q(a.upd, cfg, rq, rt, wd, wi, ql, hour_word, s_lc);
         }
       }
     }
@@ -662,7 +662,7 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
 
 __device__ __forceinline__ void globalize(UpdateArgs& u) {
   as_global(u.cfg); as_global(u.hdr); as_global(u.req); as_global(u.ring_ts); as_global(u.ring_amt);
-  as_global(u.hll); as_global(u.rt); as_global(u.ev); as_global(u.dbuf);
+  as_global(u.hll); as_global(u.rt); as_global(u.ev); as_global(u.dbuf); as_global(u.hll_lc);
 }
 __device__ __forceinline__ void globalize(AssembleArgs& a) {
   as_global(a.hdr); as_global(a.cfg); as_global(a.req); as_global(a.ring_ts); as_global(a.ring_amt);
@@ -881,6 +881,15 @@ __device__ __forceinline__ uint32_t hll_segment(const UpdateArgs& a, uint8_t* rg
   return (uint32_t)(tlast + a.cfg->hll_ttl);
 }
 
+// the estimate of 256 register bytes (the store's or a wave's LDS copy) by a whole wave: every
+// quarter reads the file as K1's layout (lane ql: words ql + 16 i) and all lanes get the value
+__device__ __forceinline__ int hll_count_wave(const uint8_t* rg, int lane, const int32_t* lc) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(rg);
+  const int ql = lane & 15;
+  const uint32_t q[4] = {w[ql], w[ql + 16], w[ql + 32], w[ql + 48]};
+  return hll_count_q(q, lc);
+}
+
 // Apply c (1..64) events of account s, held in row order by lanes 0..c-1 (`j` = the lane's
 // request row), to the account's AcctRT `r` (the same value in every lane, updated in place):
 // in parallel when the events span less than the shortest TTL (then no key can expire
@@ -926,6 +935,8 @@ __device__ void apply_chunk(const UpdateArgs& a, int s, AcctRT& r, int j, int c,
     r.session_start = (uint32_t)__shfl((int)r.session_start, 0, 64);
     r.session_exp = (uint32_t)__shfl((int)r.session_exp, 0, 64);
     r.last_event_ts = (uint32_t)__shfl((int)r.last_event_ts, 0, 64);
+    r.hll_dev_n = __shfl(r.hll_dev_n, 0, 64);
+    r.hll_ip_n = __shfl(r.hll_ip_n, 0, 64);
     if constexpr (LDSR) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // lane 0's register writes
     return;
   }
@@ -950,6 +961,9 @@ __device__ void apply_chunk(const UpdateArgs& a, int s, AcctRT& r, int j, int c,
   // the next chunk re-reads registers this one wrote (other lanes' stores)
   if constexpr (LDSR) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   else __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  // a raised register (or a reset, which raises one) refreshes the cached estimate
+  if (__ballot(new_dev)) r.hll_dev_n = hll_count_wave(regs, lane, a.hll_lc);
+  if (__ballot(new_ip)) r.hll_ip_n = hll_count_wave(regs + 256, lane, a.hll_lc);
   // last tx / session
   if (ts0 >= (int64_t)r.session_exp || r.session_start == 0) r.session_start = (uint32_t)ts0;
   r.session_exp = (uint32_t)(tsl + cfg.session_ttl);
@@ -1245,6 +1259,10 @@ __device__ __forceinline__ void update_hot_body(const UpdateArgs& a, int hb, int
       r.last_event_ts = (uint32_t)now;
     }
     if (wv == 0) {  // the tail, exact, 64 events at a time
+      // the bulk's raised registers: the cached estimates first (the tail refreshes them again
+      // only if one of its own events raises a register)
+      if (ad) r.hll_dev_n = hll_count_wave(reinterpret_cast<const uint8_t*>(s_regs), lane, a.hll_lc);
+      if (ai) r.hll_ip_n = hll_count_wave(reinterpret_cast<const uint8_t*>(s_regs + 64), lane, a.hll_lc);
       for (int q = 0; q < Tn; q += 64) {
         const int c = min(64, Tn - q);
         const int pj = lane < c ? s_tail[q + lane] : 0;

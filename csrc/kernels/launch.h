@@ -48,6 +48,7 @@ struct UpdateArgs {
   // scorer dedup insert only (nullable): the pinned host slab [BatchHdr | ReqRec x n]; the kernel
   // reads the batch from it and writes the device copy (hdr, req) for the later stages
   const char* src;
+  const int32_t* hll_lc;    // [257] linear-counting table (the cached HLL estimates, AcctRT)
 };
 
 struct AssembleArgs {

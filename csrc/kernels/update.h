@@ -40,8 +40,7 @@ __host__ __device__ inline size_t dedup_region_size(int cap, int n_max) {
 // other scalar loads) per wave in K1 and the update kernels.
 __device__ __forceinline__ AcctRT load_rt(const AcctRT* p) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
-  const uint4 a = q[0], b = q[1], c = q[2];
-  const int32_t d = reinterpret_cast<const int32_t*>(p)[12];
+  const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
   AcctRT r;
   r.hll_dev_exp = a.x;
   r.hll_ip_exp = a.y;
@@ -54,8 +53,10 @@ __device__ __forceinline__ AcctRT load_rt(const AcctRT* p) {
   r.sum_compat = (int64_t)(((uint64_t)c.y << 32) | c.x);
   r.ring_head = (int32_t)c.z;
   r.ev_head = (int32_t)c.w;
-  r.ev_count = d;
-  r.pad0 = r.pad1 = r.pad2 = 0;
+  r.ev_count = (int32_t)d.x;
+  r.hll_dev_n = (int32_t)d.y;
+  r.hll_ip_n = (int32_t)d.z;
+  r.pad0 = 0;
   return r;
 }
 
@@ -65,7 +66,7 @@ __device__ __forceinline__ void store_rt(AcctRT* p, const AcctRT& r) {
   q[1] = make_uint4(r.session_start, r.session_exp, r.sum_exp, r.last_event_ts);
   q[2] = make_uint4((uint32_t)(uint64_t)r.sum_compat, (uint32_t)((uint64_t)r.sum_compat >> 32), (uint32_t)r.ring_head,
                     (uint32_t)r.ev_head);
-  reinterpret_cast<int32_t*>(p)[12] = r.ev_count;
+  q[3] = make_uint4((uint32_t)r.ev_count, (uint32_t)r.hll_dev_n, (uint32_t)r.hll_ip_n, 0u);
 }
 
 __device__ __forceinline__ DedupTab dedup_region(int32_t* buf, int cap, int n_max, int region) {
@@ -130,6 +131,33 @@ __device__ __forceinline__ void dedup_clear_range(const DedupTab& t, int e0, int
 __device__ __forceinline__ int hll_rank(uint64_t h) {
   const uint64_t wv = h >> 8;
   return wv ? (__clzll((long long)wv) - 8 + 1) : 57;
+}
+
+// HLL estimate (p = 8) from the register sum z = sum 2^-r and the zero-register count v:
+// linear counting from the host table `lc` (floor(256 ln(256 / v) + 0.5), libm log as the golden
+// model) while the raw estimate is <= 2.5 m and a register is still zero, else the harmonic mean.
+// Every partial sum of 2^-r (r <= ~44) is exact in double, so any summation order gives the same z.
+__device__ __forceinline__ int hll_estimate(double z, int v, const int32_t* lc) {
+  const double m = 256.0, alpha = 0.7213 / (1.0 + 1.079 / 256.0);
+  const double e = alpha * m * m / z;
+  return (e <= 2.5 * m && v > 0) ? lc[v] : (int)floor(e + 0.5);
+}
+
+// one thread over the 256 register bytes (the sequential event path)
+__device__ __forceinline__ int hll_count_bytes(const uint8_t* rg, const int32_t* lc) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(rg);  // 4-byte aligned (store or LDS copy)
+  double z = 0;
+  int v = 0;
+  for (int k = 0; k < 64; ++k) {
+    const uint32_t q = w[k];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int r = (q >> (8 * b)) & 0xff;
+      z += exp2_neg(r);
+      v += r == 0;
+    }
+  }
+  return hll_estimate(z, v, lc);
 }
 
 __device__ __forceinline__ void hll_add(uint8_t* rg, uint32_t& exp, uint64_t h, int64_t now, int ttl,
@@ -210,6 +238,9 @@ __device__ __forceinline__ void apply_event(const UpdateArgs& a, int j, AcctRT& 
   bool new_dev = false, new_ip = false;
   if (ev.dev_hash) hll_add(regs, r.hll_dev_exp, ev.dev_hash, now, cfg.hll_ttl, new_dev);
   if (ev.ip_hash) hll_add(regs + 256, r.hll_ip_exp, ev.ip_hash, now, cfg.hll_ttl, new_ip);
+  // the cached estimates follow every register change (a reset always ends in a raised register)
+  if (new_dev) r.hll_dev_n = hll_count_bytes(regs, a.hll_lc);
+  if (new_ip) r.hll_ip_n = hll_count_bytes(regs + 256, a.hll_lc);
   r.last_tx = (uint32_t)now;
   r.last_tx_exp = (uint32_t)(now + cfg.last_tx_ttl);
   if (now >= (int64_t)r.session_exp || r.session_start == 0) r.session_start = (uint32_t)now;

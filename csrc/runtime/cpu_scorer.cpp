@@ -312,6 +312,11 @@ void CpuScorer::apply(const ReqRec& q, int64_t now) {
   };
   if (q.dev_hash) hll_add(rg, r.hll_dev_exp, q.dev_hash, new_dev);
   if (q.ip_hash) hll_add(rg + HLL_M, r.hll_ip_exp, q.ip_hash, new_ip);
+  // the cached estimates (AcctRT hll_dev_n / hll_ip_n) follow every raised register, as on the
+  // device; the read path below still counts from the registers, so GPU / CPU parity tests check
+  // the device's cache against the definition
+  if (new_dev) r.hll_dev_n = hll_count(rg);
+  if (new_ip) r.hll_ip_n = hll_count(rg + HLL_M);
   r.last_tx = (uint32_t)now;
   r.last_tx_exp = (uint32_t)(now + c.last_tx_ttl);
   if (now >= (int64_t)r.session_exp || r.session_start == 0) r.session_start = (uint32_t)now;

@@ -793,12 +793,20 @@ class NativeCpuBackend:
         import os
         st = self.sc.state()
         tmp = path + ".tmp.npz"
-        np.savez(tmp, version=np.array([1]), ring_size=np.array([self.cfg.features.ring_size]), **st)
+        # version 2: AcctRT carries the cached HLL estimates (version 1 files get them rebuilt)
+        np.savez(tmp, version=np.array([2]), ring_size=np.array([self.cfg.features.ring_size]), **st)
         os.replace(tmp, path)
 
     def restore(self, path: str) -> int:
         with np.load(path, allow_pickle=False) as z:
             if int(z["ring_size"][0]) != self.cfg.features.ring_size:
                 raise ValueError("snapshot ring size differs from the configured ring size")
-            self.sc.load_state({k: z[k] for k in ("ring_ts", "ring_amt", "hll", "rt", "batch", "ext", "ev")})
+            st = {k: z[k] for k in ("ring_ts", "ring_amt", "hll", "rt", "batch", "ext", "ev")}
+            if int(z["version"][0]) < 2 and st["rt"].size:  # before AcctRT cached the HLL estimates
+                from ..golden.hll import refresh_cached_counts
+                from ..layouts import ACCTRT
+                rt = np.ascontiguousarray(st["rt"]).copy()
+                refresh_cached_counts(st["hll"], rt.view(np.uint8).reshape(-1, ACCTRT.itemsize).view(ACCTRT).reshape(-1))
+                st["rt"] = rt
+            self.sc.load_state(st)
         return self.sc.capacity

@@ -190,7 +190,8 @@ class DeviceFeatureStore:
         """Versioned snapshot of the first ``n_used`` slots (device -> host -> file)."""
         n = self.capacity if n_used is None else int(n_used)
         arrs = {
-            "version": np.array([1], np.int32),
+            # version 2: AcctRT carries the cached HLL estimates (version 1 files get them rebuilt)
+            "version": np.array([2], np.int32),
             "ring_size": np.array([self.cfg.ring_size], np.int32),
             "ring_ts": self.ring_ts[:n].cpu().numpy(), "ring_amt": self.ring_amt[:n].cpu().numpy(),
             "hll": self.hll[:n].cpu().numpy(), "rt": self.rt[:n].cpu().numpy(),
@@ -209,8 +210,14 @@ class DeviceFeatureStore:
             n = z["ring_ts"].shape[0]
             if n > self.capacity:
                 raise ValueError("snapshot larger than the store capacity")
-            for name in ("ring_ts", "ring_amt", "hll", "rt", "batch", "ext"):
+            rt = z["rt"].copy()
+            if int(z["version"][0]) < 2 and n:  # written before AcctRT cached the HLL estimates
+                from ..golden.hll import refresh_cached_counts
+                v = rt.reshape(n, -1).view(ACCTRT).reshape(-1)
+                refresh_cached_counts(z["hll"], v)
+            for name in ("ring_ts", "ring_amt", "hll", "batch", "ext"):
                 getattr(self, name)[:n].copy_(self.torch.from_numpy(z[name]))
+            self.rt[:n].copy_(self.torch.from_numpy(rt))
             if self.ev is not None and "ev" in z:
                 self.ev[:n].copy_(self.torch.from_numpy(z["ev"]))
         return n

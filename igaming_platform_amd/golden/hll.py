@@ -52,3 +52,29 @@ def count(regs) -> int:
     if e <= 2.5 * M and v > 0:
         e = M * math.log(M / v)
     return int(math.floor(e + 0.5))
+
+
+def count_many(regs) -> "np.ndarray":
+    """:func:`count` of every row of ``regs`` (uint8 [n, 256]) at once (numpy; the same sums:
+    every partial sum of 2^-r is exact in double). Used to rebuild the cached estimates of
+    AcctRT (hll_dev_n / hll_ip_n) when a snapshot is loaded."""
+    import numpy as np
+    r = np.asarray(regs, np.uint8).reshape(-1, M).astype(np.int64)
+    z = np.ldexp(1.0, -r).sum(axis=1)
+    v = (r == 0).sum(axis=1)
+    e = ALPHA * M * M / z
+    lc = np.array([0] + [linear_count(k) for k in range(1, M + 1)], np.int64)
+    out = np.floor(e + 0.5).astype(np.int64)
+    small = (e <= 2.5 * M) & (v > 0)
+    out[small] = lc[v[small]]
+    return out.astype(np.int32)
+
+
+def refresh_cached_counts(hll, rt) -> None:
+    """Rewrite AcctRT's cached estimates (structured ``rt`` [n] ACCTRT, in place) from the
+    register files ``hll`` (uint8 [n, 512]: device HLL then ip HLL)."""
+    import numpy as np
+    h = np.asarray(hll, np.uint8).reshape(len(rt), 2, M)
+    rt["hll_dev_n"] = count_many(h[:, 0])
+    rt["hll_ip_n"] = count_many(h[:, 1])
+

@@ -27,7 +27,7 @@ ACCTRT = np.dtype([
     ("hll_dev_exp", "<u4"), ("hll_ip_exp", "<u4"), ("last_tx", "<u4"), ("last_tx_exp", "<u4"),
     ("session_start", "<u4"), ("session_exp", "<u4"), ("sum_exp", "<u4"), ("last_event_ts", "<u4"),
     ("sum_compat", "<i8"), ("ring_head", "<i4"), ("ev_head", "<i4"), ("ev_count", "<i4"),
-    ("pad", "<i4", (3,)),
+    ("hll_dev_n", "<i4"), ("hll_ip_n", "<i4"), ("pad", "<i4"),
 ])
 
 ACCTBATCH = np.dtype([

@@ -172,6 +172,7 @@ def update_args(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, n: 
         ev_ring=int(store.ev.shape[1]) if store.ev is not None else 0,
         ev_dim=int(store.ev.shape[2]) if store.ev is not None else 0,
         dbuf=_need(store.dbuf, "dbuf", torch.int32), dcap=int(store.dcap), dmax=int(store.dmax), region=int(region),
+        hll_lc=_need(store.hll_lc, "hll_lc", torch.int32, 257),
     )
 
 

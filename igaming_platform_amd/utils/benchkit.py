@@ -30,7 +30,8 @@ class Setup:
 
 def build(config: str, batch: int, accounts: int, dev, rank: int = 0, depth: int = 2,
           use_graphs: bool = True, history_batches: int = 24, n_pool: int = 8,
-          hot_frac: float = 0.02, precision: str = "fp32", dp: dict = None, buckets=None) -> Setup:
+          hot_frac: float = 0.02, precision: str = "fp32", dp: dict = None, buckets=None,
+          sum_mode: str = "sliding") -> Setup:
     """``dp=dict(world=N, comms=[2 RcclComm])``: this rank is one of N ingress ranks of the
     owner-routed exchange (engine/dp.py): its pool entries are (chunks, rows) whose rows are
     spread over every owner uniformly at random, as hash routing spreads real accounts."""
@@ -49,6 +50,7 @@ def build(config: str, batch: int, accounts: int, dev, rank: int = 0, depth: int
     B = batch or c["batch"]
     cfg = Config()
     cfg.features.width = c["width"]
+    cfg.features.sum_mode = sum_mode
     cfg.gpu.buckets = sorted(set(buckets)) if buckets else [B]
     cfg.gpu.max_batch = B
     world = dp["world"] if dp else 1
