@@ -44,6 +44,11 @@ EnsembleArgs ensemble_args(const py::dict& d) {
   a.host_out = ptr<ResultRec*>(d, "host_out");
   a.metrics = ptr<unsigned long long*>(d, "metrics");
   a.n_rows = geti(d, "n_rows");
+  a.route = ptr<const int32_t*>(d, "route");
+  a.route_c = geti(d, "route_c");
+  a.route_stride = geti(d, "route_stride");
+  if (a.route && (!a.host_out || a.route_c < 1 || a.route_stride < a.route_c * (int)sizeof(ResultRec)))
+    throw std::runtime_error("ensemble: routed host rows need host_out, route_c and route_stride");
   return a;
 }
 
@@ -69,6 +74,15 @@ UpdateArgs update_args(const py::dict& d) {
   a.src = ptr<const char*>(d, "src");
   a.hll_lc = ptr<const int32_t*>(d, "hll_lc");
   if (!a.hll_lc) throw std::runtime_error("update args: hll_lc table required (cached HLL estimates)");
+  a.xrecv = ptr<const ReqRec*>(d, "xrecv");
+  a.route = ptr<int32_t*>(d, "route");
+  a.xhdr = ptr<const int4*>(d, "xhdr");
+  a.xn = geti(d, "xn");
+  a.xc = geti(d, "xc");
+  a.xpstride = geti(d, "xpstride");
+  if (a.xrecv && (a.src || !a.route || !a.xhdr || a.xn < 1 || a.xn > 64 || a.xc < 1 || a.xpstride < a.xc + 1 ||
+                  a.xn * a.xc > a.n_max || a.region >= 0 || !a.hdr))
+    throw std::runtime_error("update args: rows-region source (xrecv, route, xhdr, 1 <= xn <= 64, xc, stride)");
   if (a.src && (a.region >= 0 || !a.hdr)) throw std::runtime_error("update args: slab source needs the scorer ring");
   if (!a.dbuf || !a.cfg || !a.req || !a.rt) throw std::runtime_error("update args: missing pointers");
   if (a.n_max > a.dmax || a.dcap < 2 * a.dmax) throw std::runtime_error("update args: dedup scratch too small");
@@ -150,6 +164,11 @@ PYBIND11_MODULE(_hipk, m) {
     a.X = ptr<float*>(d, "X");
     a.feat = ptr<FeatRec*>(d, "feat");
     a.fenc = ptr<uint8_t*>(d, "fenc");
+    a.fenc_route = ptr<const int32_t*>(d, "fenc_route");
+    a.fenc_c = geti(d, "fenc_c");
+    a.fenc_stride = geti(d, "fenc_stride");
+    if (a.fenc_route && (!a.fenc || a.fenc_c < 1 || a.fenc_stride < a.fenc_c * (int)sizeof(FeatRec)))
+      throw std::runtime_error("feature_assemble: routed images need fenc, fenc_c and fenc_stride");
     a.dbuf = ptr<int32_t*>(d, "dbuf");
     a.dcap = geti(d, "dcap");
     a.dmax = geti(d, "dmax");

@@ -34,7 +34,7 @@ __device__ __forceinline__ void ensemble_row(const EnsembleArgs& a, int row, boo
   const int n_live = a.hdr->n;
   if (row >= n_live || (a.feat[row].flags & FR_NOT_OWNED)) {
     a.out[row] = ResultRec{0u, 0.f};  // padding / another rank's request: zero (merge by sum)
-    if (a.host_out) a.host_out[row] = ResultRec{0u, 0.f};
+    if (a.host_out && !a.route) a.host_out[row] = ResultRec{0u, 0.f};
     return;
   }
   const ScoreCfg& cfg = *a.cfg;
@@ -63,7 +63,16 @@ __device__ __forceinline__ void ensemble_row(const EnsembleArgs& a, int row, boo
   a.out[row] = ResultRec{packed, (float)ml};
   // host copy: 8-B stores over the bus, visible to the host once the kernel's completion
   // signal (system-scope release) is
-  if (a.host_out) a.host_out[row] = ResultRec{packed, (float)ml};
+  if (a.host_out) {
+    ResultRec* dst = a.host_out + row;
+    if (a.route) {  // the row's place in its sender's chunk of the results region
+      const int d = a.route[row];
+      const int p = d / a.route_c;
+      dst = reinterpret_cast<ResultRec*>(reinterpret_cast<char*>(a.host_out) + (size_t)p * a.route_stride) +
+            (d - p * a.route_c);
+    }
+    *dst = ResultRec{packed, (float)ml};
+  }
   if (cnt) {
     atomicAdd(&cnt[MET_HIST + (fin < 0 ? 0 : fin)], 1u);
     atomicAdd(&cnt[MET_ACTION + action], 1u);

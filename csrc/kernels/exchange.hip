@@ -503,7 +503,7 @@ class XchgDriver {
     const size_t rbytes = (size_t)C * W;
     if (nbytes > sl.host_x_bytes || (size_t)world_ * xbytes > sl.host_x_bytes) throw std::runtime_error("XchgDriver: chunks exceed the slot buffer");
     if ((size_t)world_ * rbytes > sl.host_rr_bytes) throw std::runtime_error("XchgDriver: results exceed the slot buffer");
-    if (with_features && !g.model_f) throw std::runtime_error("XchgDriver: no feature graph");
+    if (with_features && !g.model_f && !g.omodel_f) throw std::runtime_error("XchgDriver: no feature graph");
     Range range("igp.xsubmit");
     const auto t0 = clk::now();
     if (src) std::memcpy(sl.host_x, reinterpret_cast<const void*>(src), nbytes);

@@ -175,7 +175,7 @@ __device__ __forceinline__ void inert_row(const AssembleArgs& a, float* xr, int 
   int32_t* fr = reinterpret_cast<int32_t*>(a.feat + row);
   fr[ql] = ql == 3 ? flag : 0;
   fr[ql + 16] = ql + 16 == 27 ? -1 : 0;
-  if (a.fenc) {
+  if (a.fenc && !a.fenc_route) {  // (routed images: padding rows have no sender chunk)
     int32_t* fe = reinterpret_cast<int32_t*>(a.fenc + (size_t)row * sizeof(FeatRec));
     fe[ql] = ql == 3 ? flag : 0;
     fe[ql + 16] = ql + 16 == 27 ? -1 : 0;
@@ -274,7 +274,13 @@ __device__ __forceinline__ int qscan_excl(int v, int ql) {
 // else the raw FeatRec staged in LDS (fw)
 __device__ __forceinline__ void write_fenc(const AssembleArgs& a, int row, int ql, bool enc, const uint32_t* fw,
                                            uint8_t* se) {
-  uint2* const out = reinterpret_cast<uint2*>(a.fenc + (size_t)row * sizeof(FeatRec));
+  uint8_t* base = a.fenc + (size_t)row * sizeof(FeatRec);
+  if (a.fenc_route) {  // the row's place in its sender's chunk of the results region
+    const int d = a.fenc_route[row];
+    const int p = d / a.fenc_c;
+    base = a.fenc + (size_t)p * a.fenc_stride + (size_t)(d - p * a.fenc_c) * sizeof(FeatRec);
+  }
+  uint2* const out = reinterpret_cast<uint2*>(base);
   if (enc) {
     uint64_t lo0, hi0, lo1 = 0, hi1 = 0;
     const int n0 = fv_field(fw, ql + 1, lo0, hi0);
@@ -668,7 +674,7 @@ __device__ __forceinline__ void globalize(AssembleArgs& a) {
   as_global(a.hdr); as_global(a.cfg); as_global(a.req); as_global(a.ring_ts); as_global(a.ring_amt);
   as_global(a.hll); as_global(a.rt); as_global(a.batch); as_global(a.ext); as_global(a.bl_keys);
   as_global(a.bl_exp); as_global(a.ip_keys); as_global(a.ip_flags); as_global(a.hll_lc); as_global(a.X);
-  as_global(a.feat); as_global(a.fenc); as_global(a.dbuf); as_global(a.trace);
+  as_global(a.feat); as_global(a.fenc); as_global(a.fenc_route); as_global(a.dbuf); as_global(a.trace);
   globalize(a.upd);
 }
 
@@ -723,16 +729,65 @@ __global__ void __launch_bounds__(64) dedup_insert_list_kernel(UpdateArgs a) {
   __shared__ int s_key[128], s_cnt[128], s_min[128], s_base[128], s_h[128];
   const int lane = threadIdx.x;
   const int i = blockIdx.x * 64 + lane;
-  // the batch header {n, seq, now}: from the host slab (every lane the same 16 bytes: one
-  // request per wave) or the device copy
-  const int4 hv = *reinterpret_cast<const int4*>(a.src ? reinterpret_cast<const void*>(a.src)
-                                                       : reinterpret_cast<const void*>(a.hdr));
+  int2 r = make_int2(-1, 0);  // {slot, tx_type}
+  int4 hv;
+  if (a.xrecv) {
+    // rows-region exchange: compact this owner's chunk of every sender's block (host memory)
+    // here instead of a separate compact kernel and a device round trip of the rows. Lane p < xn
+    // reads sender p's header record; a wave scan of the counts places every row.
+    int cnt = 0;
+    int64_t ts = 0;
+    if (lane < a.xn) {
+      const ReqRec* h = a.xrecv + (size_t)lane * a.xpstride;
+      const int c = h->slot;
+      cnt = c < 0 ? 0 : (c > a.xc ? a.xc : c);
+      ts = cnt > 0 ? h->ts : 0;
+    }
+    const int4 h0 = *a.xhdr;
+    int incl = cnt;  // inclusive prefix over the lanes (senders)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    const int excl = incl - cnt;
+    const int total = __shfl(incl, 63, 64);
+    const int64_t t = wave_max(ts);
+    hv = make_int4(min(total, a.n_max), h0.y, t > 0 ? (int)(uint32_t)(uint64_t)t : h0.z,
+                   t > 0 ? (int)(uint32_t)((uint64_t)t >> 32) : h0.w);
+    if (i == 0) {
+      *reinterpret_cast<int4*>(const_cast<BatchHdr*>(a.hdr)) = hv;
+      a.route[a.n_max] = total > a.n_max ? total - a.n_max : 0;
+    }
+    int p = 0;  // the last sender whose rows start at or before row i (the whole wave: converged)
+    for (int q = 1; q < a.xn; ++q)
+      if (__builtin_amdgcn_readlane(excl, q) <= i && __builtin_amdgcn_readlane(cnt, q) > 0) p = q;
+    const int j = i - __shfl(excl, p, 64);
+    if (i < hv.x) {
+      const uint4* sp = reinterpret_cast<const uint4*>(a.xrecv + (size_t)p * a.xpstride + 1 + j);
+      uint4* dp = reinterpret_cast<uint4*>(const_cast<ReqRec*>(a.req + i));
+      uint4 q0 = sp[0];
+      const uint4 q1 = sp[1], q2 = sp[2];
+      q0.y &= 0xffu | (uint32_t)FV_ENC_BIT;  // owner bits of tx_type: this GPU owns every row it receives
+      dp[0] = q0;
+      dp[1] = q1;
+      dp[2] = q2;
+      a.route[i] = p * a.xc + j;
+      r = make_int2((int)q0.x, (int)q0.y);
+    }
+  } else {
+    // the batch header {n, seq, now}: from the host slab (every lane the same 16 bytes: one
+    // request per wave) or the device copy
+    hv = *reinterpret_cast<const int4*>(a.src ? reinterpret_cast<const void*>(a.src)
+                                              : reinterpret_cast<const void*>(a.hdr));
+  }
   const int n = min(hv.x, a.n_max);  // as upd_n: the header's live count
   const int64_t now = (int64_t)(((uint64_t)(uint32_t)hv.w << 32) | (uint32_t)hv.z);
   const DedupTab t = dedup_region(a.dbuf, a.dcap, a.dmax, dedup_ring_region(hv.y));
   const bool live = i < n;
-  int2 r = make_int2(-1, 0);  // {slot, tx_type}
-  if (a.src) {
+  if (a.xrecv) {
+    // (rows, route and header written above)
+  } else if (a.src) {
     if (i == 0) *reinterpret_cast<int4*>(const_cast<BatchHdr*>(a.hdr)) = hv;
     if (live) {
       const uint4* sp = reinterpret_cast<const uint4*>(a.src + sizeof(BatchHdr)) + 3 * (size_t)i;

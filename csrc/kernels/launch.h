@@ -49,6 +49,16 @@ struct UpdateArgs {
   // reads the batch from it and writes the device copy (hdr, req) for the later stages
   const char* src;
   const int32_t* hll_lc;    // [257] linear-counting table (the cached HLL estimates, AcctRT)
+  // scorer dedup insert of the rows-region exchange only (nullable): the rows come from this
+  // owner's chunk of every sender's block of the node-shared rows region (sender p's chunk at
+  // xrecv + p * xpstride: header record {slot = count, ts = sender clock} + up to xc rows); the
+  // kernel compacts them into req (sender order, then row order), writes route[i] = p * xc + j,
+  // route[n_max] = rows over capacity, and the header {n, seq (from xhdr), now}
+  const ReqRec* xrecv;
+  int32_t* route;
+  const int4* xhdr;
+  int32_t xn, xc;
+  int32_t xpstride;
 };
 
 struct AssembleArgs {
@@ -71,6 +81,11 @@ struct AssembleArgs {
   // [n_rows][128 B] D2H image of each row (nullable): the raw FeatRec, or for a request with
   // ReqRec.tx_type bit FV_ENC_BIT the encoded risk.v1 FeatureVector body (features.hip write_fenc)
   uint8_t* fenc;
+  // nullable: fenc is routed like EnsembleArgs::route - live row i's image goes to
+  // fenc + p * fenc_stride + j * 128 bytes (route[i] = p * fenc_c + j); padding rows write none
+  const int32_t* fenc_route;
+  int32_t fenc_c;
+  int32_t fenc_stride;
   int32_t* dbuf;            // dedup regions (nullable: no score-then-update)
   int32_t dcap;
   int32_t dmax;
@@ -105,6 +120,12 @@ struct EnsembleArgs {
   ResultRec* host_out;      // nullable: pinned host rows written directly (no D2H copy node)
   unsigned long long* metrics;  // [128] score histogram(101) | actions(4) | ml_high | rows (nullable)
   int32_t n_rows;
+  // nullable: host_out is routed - live row i goes to host_out + (p * route_stride bytes) + j rows,
+  // route[i] = p * route_c + j (the exchange's compacted rows back into their senders' chunks of
+  // the node-shared results region; padding rows are not written)
+  const int32_t* route;
+  int32_t route_c;
+  int32_t route_stride;
 };
 struct TreeArgs {
   const BatchHdr* hdr;      // nullable: all n_rows live

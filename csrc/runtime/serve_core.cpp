@@ -184,7 +184,7 @@ void ServeCore::resolve_rows(std::vector<wire::TxRow>& rows, Item* it) {
   bool link_room = false;
   if (links_ && n) {  // bounded: links are best-effort under overload (no copy for a full queue)
     std::lock_guard<std::mutex> g(l_mu_);
-    link_room = lq_.size() < 16;
+    link_room = lq_.size() < kLinkQueue;
   }
   if (link_room) {  // (device, account) co-occurrences, off the scoring path
     std::vector<uint64_t> d(n);
@@ -195,7 +195,7 @@ void ServeCore::resolve_rows(std::vector<wire::TxRow>& rows, Item* it) {
       a[pos] = it->rows[pos].slot >= 0 ? ((int64_t(o) << 32) | it->rows[pos].slot) : -1;
     }
     std::lock_guard<std::mutex> g(l_mu_);
-    if (lq_.size() < 16) {
+    if (lq_.size() < kLinkQueue) {
       links_->note_queued();  // (a reader of linked accounts waits for the inserts queued before it)
       lq_.emplace_back(std::move(d), std::move(a));
       l_cv_.notify_one();
@@ -418,7 +418,7 @@ void ServeCore::submit_tx_many(const TxCall* calls, size_t n, int64_t now) {
           acc.push_back(it->rows[0].slot >= 0 ? int64_t(it->rows[0].slot) : -1);
         }
       std::lock_guard<std::mutex> g(l_mu_);
-      if (lq_.size() < 16) {  // bounded: links are best-effort under overload (as resolve_rows)
+      if (lq_.size() < kLinkQueue) {  // bounded: links are best-effort under overload (as resolve_rows)
         links_->note_queued();
         lq_.emplace_back(std::move(d), std::move(acc));
         l_cv_.notify_one();

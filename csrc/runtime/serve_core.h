@@ -270,6 +270,10 @@ class ServeCore {
   // links (background)
   std::mutex l_mu_;
   std::condition_variable l_cv_;
+  // link inserts queued for the link thread: bounded, so the inserts a CheckBonusAbuse call
+  // waits for (LinkIndex tickets) lag the ingress by at most a few ms; under overload batches
+  // beyond it are not linked (links are best effort)
+  static constexpr size_t kLinkQueue = 4;
   std::deque<std::pair<std::vector<uint64_t>, std::vector<int64_t>>> lq_;
   bool l_stop_ = false;
 

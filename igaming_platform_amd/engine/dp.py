@@ -230,21 +230,51 @@ class DpGpuScorer(GpuScorer):
             K.dedup_insert(self.store, self.cfg_dev, sb.req, b, sb.hdr)
 
     def _rows_post_body(self, slot: int, C: int) -> None:
-        """Rows-region copy stage: this owner's chunk of every sender's block, compacted straight
-        from page-locked host memory (the batch header comes along), then the dedup insert."""
+        """Rows-region copy stage, one kernel: the dedup insert reads this owner's chunk of every
+        sender's block straight from page-locked host memory, compacts the rows (with their route
+        and the batch header) into the slot's device rows and registers them - as the
+        single-GPU pipeline's insert reads its pinned slab."""
         sb, b, r = self.slots[slot], self.cap(C), self.rshm["rows"]
         first = r["base"] + slot * r["slot_stride"] + self.rank * (C + 1) * REQ
+        if self.update_features:
+            K.dedup_insert(self.store, self.cfg_dev, sb.req, b, sb.hdr,
+                           xsrc=dict(recv=first, pstride=r["sender_stride"] // REQ, N=self.world, C=C,
+                                     route=sb.route, hdr=self.host_slab[slot].data_ptr()))
+            return
         hipk().exchange_compact(first, sb.req.data_ptr(), sb.dev_slab.data_ptr(), sb.route.data_ptr(),
                                 self.world, C, b, torch.cuda.current_stream().cuda_stream,
                                 r["sender_stride"] // REQ, self.host_slab[slot].data_ptr())
-        if self.update_features:
-            K.dedup_insert(self.store, self.cfg_dev, sb.req, b, sb.hdr)
+
+    def _routed(self, slot: int, C: int, with_features: bool) -> Optional[dict]:
+        """Rows-region exchange with feature images: K5 writes each result and K1 each image
+        straight into the row's sender chunk of the results region (no scatter kernel, no device
+        copy of the images): dict(base, route, C, stride) of the result rows, else None."""
+        if not (self.rows_shm and with_features):
+            return None
+        return dict(base=self._region(slot), route=self.slots[slot].route, C=C, stride=C * (RES_BYTES + FEAT_BYTES))
+
+    def _fenc_route(self, slot: int, bucket: int):
+        if not self.rows_shm:
+            return None
+        C = bucket // self.senders
+        r = self._routed(slot, C, True)
+        return dict(r, base=r["base"] + C * RES_BYTES)
 
     def _xmodel_body(self, slot: int, C: int, with_features: bool, send: int = 0) -> None:
         """The model, K5, and the scatter of each row's result (+ feature image) into its
         sender's chunk of ``send`` (default: the slot's device buffer for the result
-        all-to-all)."""
+        all-to-all). Rows-region exchange with features: K5 writes the rows in place (routed)."""
         sb, b = self.slots[slot], self.cap(C)
+        routed = self._routed(slot, C, with_features)
+        if routed is not None:
+            if sb.model is not None and sb.model.fuses_ensemble(b):
+                ens = K.ensemble_args(sb.hdr, self.cfg_dev, sb.feat, sb.X, sb.model.step_out[-1], sb.res, b,
+                                      self.metrics, host_route=routed)
+                sb.model.run(sb.X, b, m_ptr=sb.n_ptr, ens=ens)
+            else:
+                ml = sb.model.run(sb.X, b, m_ptr=sb.n_ptr) if sb.model is not None else None
+                K.ensemble(sb.hdr, self.cfg_dev, sb.feat, sb.X, ml, sb.res, b, self.metrics, host_route=routed)
+            return
         if sb.model is not None and sb.model.fuses_ensemble(b):
             ens = K.ensemble_args(sb.hdr, self.cfg_dev, sb.feat, sb.X, sb.model.step_out[-1], sb.res, b, self.metrics)
             sb.model.run(sb.X, b, m_ptr=sb.n_ptr, ens=ens)

@@ -280,8 +280,9 @@ class GpuScorer:
         batch seq + DEDUP_AHEAD (part "update")."""
         sb, upd = self.slots[slot], self.update_features
         if part in ("all", "k1"):
+            route = self._fenc_route(slot, bucket)
             K.feature_assemble(self.store, sb.hdr, self.cfg_dev, sb.req, sb.X, sb.feat, bucket, dedup=upd,
-                               fenc=self._fenc_out(slot))
+                               fenc=None if route is not None else self._fenc_out(slot), fenc_route=route)
         if upd and part in ("all", "update"):
             K.update_segments(self.store, self.cfg_dev, sb.req, bucket, sb.hdr)
 
@@ -306,6 +307,11 @@ class GpuScorer:
 
     def _fenc_host(self) -> bool:
         return self.fenc_to_host and _FEAT_ENC
+
+    def _fenc_route(self, slot: int, bucket: int):
+        """K1 writes the feature images straight into their senders' chunks of a results region
+        (engine/dp.py, the rows-region exchange); None here."""
+        return None
 
     def _fenc_out(self, slot: int):
         """Where K1 writes the slot's feature images: the pinned host rows (default) or the

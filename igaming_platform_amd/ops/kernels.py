@@ -117,14 +117,17 @@ def _host_or_dev(t: Optional[torch.Tensor], name: str, min_numel: int, device, d
 # --------------------------------------------------------------------------- K1
 def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch.Tensor,
                      X: torch.Tensor, feat: torch.Tensor, n_rows: int, dedup: bool = False,
-                     trace: Optional[torch.Tensor] = None, fenc: Optional[torch.Tensor] = None) -> None:
+                     trace: Optional[torch.Tensor] = None, fenc: Optional[torch.Tensor] = None,
+                     fenc_route: Optional[dict] = None) -> None:
     """K1. ``dedup=True``: score-then-update. :func:`dedup_insert` must have registered the
     batch first; K1 then applies each single-event account's event and opens the segments
     that :func:`update_segments` applies afterwards (dedup ring region by batch seq).
     ``fenc`` [rows, 32] int32: each row's 128-byte D2H feature image - the raw FeatRec, or the
     encoded risk.v1 FeatureVector body for rows whose ReqRec.tx_type carries FV_ENC_BIT. A pinned
     host tensor is written through the fabric (one coalesced 128-B store per row), so the image
-    needs no D2H copy."""
+    needs no D2H copy. ``fenc_route``: dict(base=host address, route=int32 tensor, C=, stride=):
+    the images go to their senders' chunks of the exchange's node-shared results region instead
+    (row i at base + p * stride + j * 128, route[i] = p * C + j)."""
     dev = store.device
     if X.dim() != 2 or X.shape[1] < 30 + store.ext_width:
         raise ValueError("X must be [rows, >= 30 + ext_width]")
@@ -149,6 +152,11 @@ def feature_assemble(store, hdr: torch.Tensor, cfg_dev: torch.Tensor, req: torch
     )
     if dedup:
         d["upd"] = update_args(store, cfg_dev, req, n_rows, hdr=hdr, region=-1)
+    if fenc_route is not None:
+        if fenc is not None:
+            raise ValueError("feature_assemble: fenc or fenc_route")
+        d.update(fenc=int(fenc_route["base"]), fenc_route=_need(fenc_route["route"], "route", torch.int32, n_rows, dev),
+                 fenc_c=int(fenc_route["C"]), fenc_stride=int(fenc_route["stride"]))
     _mod().feature_assemble(d, _stream())
 
 
@@ -185,14 +193,20 @@ def feature_update(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, 
 
 
 def dedup_insert(store, cfg_dev: torch.Tensor, req: torch.Tensor, n_max: int, hdr: torch.Tensor,
-                 src: Optional[torch.Tensor] = None) -> None:
+                 src: Optional[torch.Tensor] = None, xsrc: Optional[dict] = None) -> None:
     """Scorer head: register the batch's accounts in its dedup region (before K1), with the
     per-account row lists and the multi-event account list :func:`update_segments` reads.
     ``src``: the pinned host slab [BatchHdr | ReqRec x n_max] - the kernel reads the batch from
-    it and writes ``hdr`` / ``req`` itself (no H2D copy before it)."""
+    it and writes ``hdr`` / ``req`` itself (no H2D copy before it). ``xsrc``: the rows-region
+    exchange - dict(recv=host address of sender 0's chunk for this owner, pstride=records between
+    senders, N=senders, C=chunk capacity, route=int32 [n_max + 1], hdr=host address of the batch
+    header): the kernel compacts the chunks into ``req`` itself (launch.h UpdateArgs)."""
     d = update_args(store, cfg_dev, req, n_max, hdr=hdr, region=-1)
     if src is not None:
         d["src"] = _host_or_dev(src, "src", 16 + 48 * n_max, store.device, torch.uint8)
+    if xsrc is not None:
+        d.update(xrecv=int(xsrc["recv"]), xpstride=int(xsrc["pstride"]), xn=int(xsrc["N"]), xc=int(xsrc["C"]),
+                 route=_need(xsrc["route"], "route", torch.int32, n_max + 1, store.device), xhdr=int(xsrc["hdr"]))
     d["insert_only"] = 1
     _mod().feature_update(d, _stream())
 
@@ -403,9 +417,12 @@ def _head_dict(hs, X, Y, M, m_ptr, tree_partial, trace, ens) -> dict:
 
 # --------------------------------------------------------------------------- K5 / K10
 def ensemble_args(hdr, cfg_dev, feat, X, ml: Optional[torch.Tensor], out, n_rows: int,
-                  metrics: Optional[torch.Tensor] = None, host_out: Optional[torch.Tensor] = None) -> dict:
+                  metrics: Optional[torch.Tensor] = None, host_out: Optional[torch.Tensor] = None,
+                  host_route: Optional[dict] = None) -> dict:
     """``host_out``: pinned host int32 [>= n_rows, 2] rows the kernel also writes (the D2H
-    copy of the results is then not needed)."""
+    copy of the results is then not needed). ``host_route``: dict(base=host address,
+    route=int32 tensor, C=, stride=): the live rows go to their senders' chunks of the exchange's
+    results region instead (row i at base + p * stride + j * 8, route[i] = p * C + j)."""
     dev = feat.device
     d = dict(hdr=_need(hdr, "hdr", torch.int64, 2, dev), cfg=_need(cfg_dev, "cfg", torch.uint8, 176, dev),
              feat=_need(feat, "feat", torch.int32, 32 * n_rows, dev),
@@ -419,12 +436,18 @@ def ensemble_args(hdr, cfg_dev, feat, X, ml: Optional[torch.Tensor], out, n_rows
                 not host_out.is_contiguous() or host_out.numel() < 2 * n_rows:
             raise ValueError("ensemble: host_out must be pinned contiguous int32 [>= n_rows, 2]")
         d["host_out"] = host_out.data_ptr()
+    if host_route is not None:
+        if host_out is not None:
+            raise ValueError("ensemble: host_out or host_route")
+        d.update(host_out=int(host_route["base"]), route=_need(host_route["route"], "route", torch.int32, n_rows, dev),
+                 route_c=int(host_route["C"]), route_stride=int(host_route["stride"]))
     return d
 
 
 def ensemble(hdr, cfg_dev, feat, X, ml: Optional[torch.Tensor], out, n_rows: int,
-             metrics: Optional[torch.Tensor] = None, host_out: Optional[torch.Tensor] = None) -> None:
-    _mod().ensemble(ensemble_args(hdr, cfg_dev, feat, X, ml, out, n_rows, metrics, host_out), _stream())
+             metrics: Optional[torch.Tensor] = None, host_out: Optional[torch.Tensor] = None,
+             host_route: Optional[dict] = None) -> None:
+    _mod().ensemble(ensemble_args(hdr, cfg_dev, feat, X, ml, out, n_rows, metrics, host_out, host_route), _stream())
 
 
 # --------------------------------------------------------------------------- K9

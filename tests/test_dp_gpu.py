@@ -272,6 +272,21 @@ def test_exchange_compact_from_the_node_shared_rows_region(world, C):
     got = slab[16:16 + 48 * n].cpu().numpy().view(REQREC)
     np.testing.assert_array_equal(got.view(np.uint8), rows_ref.view(np.uint8))
     np.testing.assert_array_equal(route[:n].cpu().numpy(), route_ref)
+    # the serving copy stage: the dedup insert compacts the same chunks itself (one kernel)
+    from igaming_platform_amd.engine.scorer import GpuScorer
+    from igaming_platform_amd.ops import kernels as K
+    cfg, pop, mk_store, plan, dev = _setup()
+    store = mk_store()
+    sc = GpuScorer(cfg, store, plan=plan, model="plan", device=dev, pipeline_depth=2)
+    slab2 = torch.zeros(16 + 48 * cap, dtype=torch.uint8, device=dev)
+    route2 = torch.full((cap + 1,), -7, dtype=torch.int32, device=dev)
+    K.dedup_insert(store, sc.cfg_dev, slab2[16:], cap, slab2[:16].view(torch.int64),
+                   xsrc=dict(recv=first, pstride=world * (C + 1), N=world, C=C, route=route2, hdr=hdr.data_ptr()))
+    torch.cuda.synchronize()
+    assert int(slab2[:4].view(torch.int32).item()) == n and int(slab2[4:8].view(torch.int32).item()) == 4242
+    np.testing.assert_array_equal(slab2[16:16 + 48 * n].cpu().numpy(), got.view(np.uint8))
+    np.testing.assert_array_equal(route2[:n].cpu().numpy(), route_ref)
+    assert int(route2[cap].item()) == 0
 
 
 def test_exchange_rank_fits_the_hardware_queue_budget():

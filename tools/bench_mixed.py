@@ -67,7 +67,7 @@ def build(accounts: int):
     return eng
 
 
-def batch_load(eng, payloads, threads: int, seconds: float, t_base: int, stop_evt=None):
+def batch_load(eng, payloads, threads: int, seconds: float, t_base: int, rows_per_request: int = 8192):
     """Closed-loop ScoreBatch from ``threads`` ingress threads for ``seconds``: (rows/s, p50, p99 ms)."""
     core = eng.core
     lock = threading.Lock()
@@ -83,9 +83,11 @@ def batch_load(eng, payloads, threads: int, seconds: float, t_base: int, stop_ev
             t0 = time.perf_counter_ns()
             out = core.score_batch(payloads[i % len(payloads)], t_base + i // 50, t0)
             dt = (time.perf_counter_ns() - t0) / 1e6
+            if not out:
+                raise RuntimeError("empty ScoreBatch response")
             with lock:
                 lat.append(dt)
-                rows[0] += len(out)
+                rows[0] += rows_per_request
     th = [threading.Thread(target=worker) for _ in range(threads)]
     t0 = time.perf_counter()
     [t.start() for t in th]
@@ -135,6 +137,13 @@ def main(argv=None) -> int:
     acct0 = eng.acct.router.stats(3, True)
     alone = batch_load(eng, payloads, a.threads, a.seconds, NOW0)
     time.sleep(1.0)
+    # the unary load alone (the same two open loops, no ScoreBatch): what the GPU sharing costs it
+    solo = {}
+    th = [threading.Thread(target=open_loop, args=(srv.port, "abuse", abuse_p, a.abuse_rate, a.seconds, a.clients, solo)),
+          threading.Thread(target=open_loop, args=(srv.port, "tx", tx_p, a.tx_rate, a.seconds, a.clients, solo))]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    time.sleep(1.0)
     eng.acct.router.stats(3, True)
     res = {}
     th = [threading.Thread(target=open_loop, args=(srv.port, "abuse", abuse_p, a.abuse_rate, a.seconds, a.clients, res)),
@@ -153,6 +162,7 @@ def main(argv=None) -> int:
                                      requests=mixed[3]),
                scorebatch_loss_pct=round(100.0 * (1 - mixed[0] / alone[0]), 2),
                check_bonus_abuse=res.get("abuse"), score_transaction=res.get("tx"),
+               unary_without_scorebatch=dict(check_bonus_abuse=solo.get("abuse"), score_transaction=solo.get("tx")),
                abuse_cluster_fallbacks=fb,
                abuse_rows_per_device_step=round(st.get("items", 0) / max(int(st.get("steps", 1)), 1), 1),
                config=dict(scorebatch_threads=a.threads, clients_per_rpc=a.clients, server_workers=a.server_workers,
