@@ -255,6 +255,7 @@ def acct_dp_bench(a) -> None:
     per_step = a.calls
     now = NOW_ACCT
     router.drive(rpc, payloads, max(a.warmup, 1) * per_step, a.inflight, now, a.drive_threads)  # warm
+    router.stats(3 if rpc_name == "abuse" else 1, True)  # the timed run's device steps only
     if comm is not None:
         comm.barrier()
     t0 = time.perf_counter()
@@ -297,6 +298,13 @@ def acct_dp_bench(a) -> None:
         "errors": errors, "cold_path_calls": cold, "remote_calls_rank_sum": remote,
         "device_steps_rank0": int(st.get("steps", 0)), "rows_per_device_step_rank0":
             round(st.get("items", 0) / max(int(st.get("steps", 1)), 1), 1),
+        # where a call's time goes on rank 0 (acct_core.h AcctStats): queueing before its step,
+        # the step on the device, the answer writing
+        "device_us_per_step_rank0": round(st.get("device_ns", 0) / max(int(st.get("steps", 1)), 1) / 1e3, 1),
+        "queue_us_per_call_rank0": round(st.get("queue_ns", 0) / max(int(st.get("items", 1)), 1) / 1e3, 1),
+        "max_step_rows_rank0": int(st.get("max_step_rows", 0)),
+        "cluster_fallbacks_rank0": sum(int(getattr(getattr(d, "driver", None), "fallbacks", 0) or 0)
+                                       for d in getattr(acct, "devices", [])),
     }
     if errors:
         raise RuntimeError(f"{errors} calls failed ({cold} cold-path replies)")

@@ -450,7 +450,7 @@ void ServeCore::submit_tx_many(const TxCall* calls, size_t n, int64_t now) {
         if (it) {
           it->remaining = int64_t(it->n);
           it->t_enq = t_enq;
-          queue_.push_back(it);
+          uqueue_.push_back(it);
           queued_rows_ += int64_t(it->n);
         }
   }
@@ -509,7 +509,7 @@ size_t ServeCore::poll(std::vector<Done>& out, size_t max, int64_t timeout_us) {
 
 int ServeCore::pending_items() {
   std::lock_guard<std::mutex> lk(q_mu_);
-  return int(queue_.size());
+  return int(queue_.size() + uqueue_.size());
 }
 
 // ---------------------------------------------------------------------------- stepper
@@ -539,44 +539,48 @@ bool ServeCore::issue_step(std::unique_lock<std::mutex>& lk, bool allow_empty) {
   int n = 0;
   thread_local std::vector<int32_t> fill;
   if (!exchange_) {
-    while (!queue_.empty() && n < cap_) {
-      Item* it = queue_.front();
-      const int take = int(std::min<int64_t>(it->remaining, cap_ - n));
-      st->segs.push_back(Seg{it, 0, it->ocur[0], n, take});
-      it->ocur[0] += take;
-      it->remaining -= take;
-      it->taken += take;
-      if (!it->t_issue) it->t_issue = now_ns();
-      n += take;
-      now = std::max(now, it->now);
-      st->wf |= it->wf;
-      if (it->remaining == 0) queue_.pop_front();
+    for (std::deque<Item*>* q : {&uqueue_, &queue_}) {  // unary calls first
+      while (!q->empty() && n < cap_) {
+        Item* it = q->front();
+        const int take = int(std::min<int64_t>(it->remaining, cap_ - n));
+        st->segs.push_back(Seg{it, 0, it->ocur[0], n, take});
+        it->ocur[0] += take;
+        it->remaining -= take;
+        it->taken += take;
+        if (!it->t_issue) it->t_issue = now_ns();
+        n += take;
+        now = std::max(now, it->now);
+        st->wf |= it->wf;
+        if (it->remaining == 0) q->pop_front();
+      }
     }
   } else {
     fill.assign(world_, 0);
     int full = 0;
-    for (auto qi = queue_.begin(); qi != queue_.end() && full < world_;) {
-      Item* it = *qi;
-      bool took = false;
-      for (int o = 0; o < world_; ++o) {
-        const int avail = it->ostart[o + 1] - it->ocur[o];
-        if (avail <= 0 || fill[o] >= cap_) continue;
-        const int take = std::min(avail, cap_ - fill[o]);
-        st->segs.push_back(Seg{it, o, it->ocur[o], fill[o], take});
-        it->ocur[o] += take;
-        it->remaining -= take;
-        it->taken += take;
-        if (!it->t_issue) it->t_issue = now_ns();
-        fill[o] += take;
-        n += take;
-        if (fill[o] == cap_) ++full;
-        took = true;
+    for (std::deque<Item*>* q : {&uqueue_, &queue_}) {  // unary calls first
+      for (auto qi = q->begin(); qi != q->end() && full < world_;) {
+        Item* it = *qi;
+        bool took = false;
+        for (int o = 0; o < world_; ++o) {
+          const int avail = it->ostart[o + 1] - it->ocur[o];
+          if (avail <= 0 || fill[o] >= cap_) continue;
+          const int take = std::min(avail, cap_ - fill[o]);
+          st->segs.push_back(Seg{it, o, it->ocur[o], fill[o], take});
+          it->ocur[o] += take;
+          it->remaining -= take;
+          it->taken += take;
+          if (!it->t_issue) it->t_issue = now_ns();
+          fill[o] += take;
+          n += take;
+          if (fill[o] == cap_) ++full;
+          took = true;
+        }
+        if (took) {
+          now = std::max(now, it->now);
+          st->wf |= it->wf;
+        }
+        qi = it->remaining == 0 ? q->erase(qi) : qi + 1;
       }
-      if (took) {
-        now = std::max(now, it->now);
-        st->wf |= it->wf;
-      }
-      qi = it->remaining == 0 ? queue_.erase(qi) : qi + 1;
     }
   }
   if (n == 0 && !allow_empty) return false;
@@ -665,7 +669,7 @@ void ServeCore::stepper_loop() {
     }
     const bool peer_ahead = exchange_ && clock_->max_issued() > issued_.load();
     // pause / stop: converge on a generation (exchange: every rank at the same step count)
-    const bool draining = stopping_ && queue_.empty();
+    const bool draining = stopping_ && queue_.empty() && uqueue_.empty();
     if (pause_req_ || draining) {
       const int64_t gen = hold_gen_;
       if (!held_) {
@@ -702,7 +706,9 @@ void ServeCore::stepper_loop() {
     }
     const bool slot = next_slot_locked() >= 0;
     if (slot && (queued_rows_ > 0 || peer_ahead)) {
-      const int64_t age = queue_.empty() ? 0 : now_ns() - queue_.front()->t_enq;
+      const int64_t t_front = std::min(queue_.empty() ? INT64_MAX : queue_.front()->t_enq,
+                                       uqueue_.empty() ? INT64_MAX : uqueue_.front()->t_enq);
+      const int64_t age = t_front == INT64_MAX ? 0 : now_ns() - t_front;
       if (peer_ahead || inflight_ == 0 || queued_rows_ >= full_rows || age >= max_wait) {
         issue_step(lk, peer_ahead);
         continue;
@@ -958,6 +964,8 @@ void ServeCore::abort() {
     aborting_ = true;
     stopping_ = true;
     dropped.swap(queue_);
+    dropped.insert(dropped.end(), uqueue_.begin(), uqueue_.end());
+    uqueue_.clear();
     queued_rows_ = 0;
   }
   q_cv_.notify_all();

@@ -239,6 +239,11 @@ class ServeCore {
   std::mutex q_mu_;
   std::condition_variable q_cv_;      // stepper: new items / free slot / peers / state
   std::deque<Item*> queue_;
+  // unary calls (ScoreTransaction, one row each) form steps ahead of queued ScoreBatch rows:
+  // under a saturating batch load a unary call otherwise waits behind every batch request
+  // queued before it (mixed-traffic run, profiles/r6/d: ScoreTransaction p99 286 ms). Two
+  // concurrent requests have no defined order between them (engine/dp.py ordering contract).
+  std::deque<Item*> uqueue_;
   int64_t queued_rows_ = 0;
   std::vector<int> free_slots_;
   std::vector<std::unique_ptr<Step>> steps_;  // by slot

@@ -168,8 +168,17 @@ class ServerConfig:
 
 @dataclass
 class AbuseConfig:
-    """CheckBonusAbuse decision threshold (engine/abuse.py documents the signal weights)."""
+    """CheckBonusAbuse decision threshold (engine/abuse.py documents the signal weights) and the
+    native abuse device's micro-batching on a GPU shard that also scores transactions:
+    ``max_batch`` caps the rows of one device step (0: the shard's largest batch bucket) - at
+    <= 256 every step runs the weight-stationary split GRU clusters (gru_wsx.hip), which read no
+    weights per step and so do not compete with the scoring kernels for L2; ``high_priority``
+    creates the abuse streams at high queue priority. Off by default: on the box it made the
+    abuse path slower, not faster - unary CheckBonusAbuse p99 391 ms at high priority vs 1.9 ms
+    at normal priority with no ScoreBatch load (tools/bench_mixed.py, profiles/r6/f)."""
     threshold: float = 0.7
+    max_batch: int = 0
+    high_priority: bool = False
 
 
 @dataclass

@@ -117,7 +117,8 @@ class AbuseNativeDevice:
     """The CheckBonusAbuse step of one GPU shard for the native core: K1 feature rows of the
     accounts (the rule signals) and, with an abuse model, the GRU over their event rings."""
 
-    def __init__(self, backend, plan=None, buckets=(64, 512, 4096), depth: int = 2, rank: int = 0):
+    def __init__(self, backend, plan=None, buckets=(64, 512, 4096), depth: int = 2, rank: int = 0,
+                 max_batch: int = 0, priority: int = 0):
         import torch
         from ..ops import kernels as K
         from .runner import GruModel
@@ -125,6 +126,8 @@ class AbuseNativeDevice:
         store, sc = backend.store, backend.scorer
         dev = store.device
         self.buckets = sorted(set(int(b) for b in buckets))
+        if max_batch > 0:  # AbuseConfig.max_batch: smaller device steps (the cluster kernel's range)
+            self.buckets = sorted({b for b in self.buckets if b < max_batch} | {int(max_batch)})
         B = self.cap = self.buckets[-1]
         if B > store.dmax:
             raise ValueError("abuse bucket larger than the store's batch capacity")
@@ -154,13 +157,13 @@ class AbuseNativeDevice:
         # block) while these graphs keep their pointers (refresh() re-copies it)
         self.cfg_dev = sc.cfg_dev.clone()
         width = sc.width
-        self.stream = torch.cuda.Stream(device=dev)
+        self.stream = torch.cuda.Stream(device=dev, priority=priority)
         # one stream per slot: a few hundred rows of 100-step GRU fill a few dozen CUs, so the
         # slots' steps run side by side (a bidirectional model shares the pack's direction
         # buffers between slots and keeps one stream)
         shared = self.gm is not None and self.gm.bidirectional
         self.streams = [self.stream] if shared else [self.stream] + [
-            torch.cuda.Stream(device=dev) for _ in range(self.depth - 1)]
+            torch.cuda.Stream(device=dev, priority=priority) for _ in range(self.depth - 1)]
         self.bufs = [dict(slab=torch.zeros(nb, dtype=torch.uint8, device=dev),
                           X=torch.zeros((B, width), dtype=torch.float32, device=dev),
                           feat=torch.zeros((B, 32), dtype=torch.int32, device=dev),
@@ -176,7 +179,7 @@ class AbuseNativeDevice:
         if self.gm is not None and any(gp.wsx_ok for gp in self.gm.packs):
             # the split GRU clusters (buckets <= 256: up to half the chip per launch) run one
             # launch at a time on a stream of their own; larger buckets keep a stream per slot
-            self.small_stream = torch.cuda.Stream(device=dev)
+            self.small_stream = torch.cuda.Stream(device=dev, priority=priority)
             self.driver.set_small_stream(self.small_stream.cuda_stream, 256)
         self.graphs = []
         wsx = self.gm is not None and any(gp.wsx_ok for gp in self.gm.packs)
@@ -300,7 +303,10 @@ def attach_models(acct: NativeAcct, cfg, backend, ltv=None, owner: int = 0, abus
         elif backend.kind == "cpu":
             acct.attach(cpu_ltv_device(ltv, owner, max(cfg.gpu.buckets), depth), cfg)
     if backend.kind == "gpu":
-        acct.attach(AbuseNativeDevice(backend, abuse_plan, buckets=cfg.gpu.buckets, depth=depth, rank=rank), cfg)
+        # (torch maps a large negative priority to the highest the device allows)
+        acct.attach(AbuseNativeDevice(backend, abuse_plan, buckets=cfg.gpu.buckets, depth=depth, rank=rank,
+                                      max_batch=int(cfg.abuse.max_batch),
+                                      priority=-100 if cfg.abuse.high_priority else 0), cfg)
     elif backend.kind == "cpu" and hasattr(backend, "sc"):
         acct.attach(cpu_abuse_device(backend, abuse_model, max(cfg.gpu.buckets),
                                      cfg.abuse_model.input_name, cfg.abuse_model.output_name, depth), cfg)

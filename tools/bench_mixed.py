@@ -36,7 +36,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 
 
-def build(accounts: int):
+def build(accounts: int, abuse_max_batch: int = 0, abuse_priority: bool = True):
     """One engine: cfg3 fraud model (8192-row micro-batches), cfg4 LTV MLP, cfg5 abuse GRU; warehouse
     rows + ext rows for every account, profile rows for the LTV model, full event rings."""
     import bench_e2e as E
@@ -49,6 +49,8 @@ def build(accounts: int):
     cfg.features.width = 128
     cfg.gpu.buckets = [64, 512, 2048, 8192]
     cfg.gpu.max_batch = 8192
+    cfg.abuse.max_batch = abuse_max_batch
+    cfg.abuse.high_priority = abuse_priority
     eng = RiskEngine(cfg, backend="gpu", capacity=accounts + 4096, fraud_model=E.fraud_model_bytes("cfg3"),
                      ltv_model=builders.build("ltv_mlp", n_features=256, width=512, layers=4).SerializeToString(),
                      abuse_model=builders.build("gru", seq=100, in_dim=16, hidden=256).SerializeToString())
@@ -67,28 +69,42 @@ def build(accounts: int):
     return eng
 
 
-def batch_load(eng, payloads, threads: int, seconds: float, t_base: int, rows_per_request: int = 8192):
-    """Closed-loop ScoreBatch from ``threads`` ingress threads for ``seconds``: (rows/s, p50, p99 ms)."""
+def batch_load(eng, payloads, threads: int, seconds: float, t_base: int, rows_per_request: int = 8192,
+               rate: float = 0.0):
+    """ScoreBatch from ``threads`` ingress threads for ``seconds``: closed loop, or paced open
+    loop at ``rate`` requests/s (request k of thread w due at t0 + (k * threads + w) / rate;
+    latency from the due time). Returns (rows/s, p50, p99 ms, requests)."""
     core = eng.core
     lock = threading.Lock()
     lat, rows = [], [0]
-    t_end = time.perf_counter() + seconds
+    t_start = time.perf_counter()
+    t_end = t_start + seconds
     counter = [0]
 
-    def worker():
+    def worker(w):
+        k = 0
         while time.perf_counter() < t_end:
+            due = None
+            if rate > 0:
+                due = t_start + (k * threads + w) / rate
+                k += 1
+                if due >= t_end:
+                    return
+                wait = due - time.perf_counter()
+                if wait > 0:
+                    time.sleep(wait)
             with lock:
                 i = counter[0]
                 counter[0] += 1
-            t0 = time.perf_counter_ns()
-            out = core.score_batch(payloads[i % len(payloads)], t_base + i // 50, t0)
+            t0 = time.perf_counter_ns() if due is None else int(due * 1e9)
+            out = core.score_batch(payloads[i % len(payloads)], t_base + i // 50, time.perf_counter_ns())
             dt = (time.perf_counter_ns() - t0) / 1e6
             if not out:
                 raise RuntimeError("empty ScoreBatch response")
             with lock:
                 lat.append(dt)
                 rows[0] += rows_per_request
-    th = [threading.Thread(target=worker) for _ in range(threads)]
+    th = [threading.Thread(target=worker, args=(w,)) for w in range(threads)]
     t0 = time.perf_counter()
     [t.start() for t in th]
     [t.join() for t in th]
@@ -117,12 +133,16 @@ def main(argv=None) -> int:
     ap.add_argument("--tx-rate", type=float, default=200000.0)
     ap.add_argument("--clients", type=int, default=4, help="HTTP/2 connections per open-loop RPC")
     ap.add_argument("--server-workers", type=int, default=4)
+    ap.add_argument("--abuse-max-batch", type=int, default=0, help="AbuseConfig.max_batch (0: the largest bucket)")
+    ap.add_argument("--abuse-priority", type=int, default=0, help="AbuseConfig.high_priority")
+    ap.add_argument("--batch-rate", type=float, default=0.0,
+                    help="ScoreBatch requests/s, paced open loop over --threads (0: closed loop)")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args(argv)
     import bench_e2e as E
     from igaming_platform_amd.api.native_grpc import NativeRiskServer
     from igaming_platform_amd.utils.synth import NOW0
-    eng = build(a.accounts)
+    eng = build(a.accounts, a.abuse_max_batch, bool(a.abuse_priority))
     srv = NativeRiskServer(eng, port=0, workers=a.server_workers, batching=True).start()
     payloads = E.spread_payloads(a.accounts, 64, 8192, seed=11)
     abuse_p = E.acct_payloads(a.accounts, "abuse", 1 << 16, 300)
@@ -135,7 +155,7 @@ def main(argv=None) -> int:
     dev = [d for d in eng.acct.devices if hasattr(d, "driver") and hasattr(d.driver, "fallbacks")]
     fb0 = sum(int(d.driver.fallbacks) for d in dev)
     acct0 = eng.acct.router.stats(3, True)
-    alone = batch_load(eng, payloads, a.threads, a.seconds, NOW0)
+    alone = batch_load(eng, payloads, a.threads, a.seconds, NOW0, rate=a.batch_rate)
     time.sleep(1.0)
     # the unary load alone (the same two open loops, no ScoreBatch): what the GPU sharing costs it
     solo = {}
@@ -149,7 +169,7 @@ def main(argv=None) -> int:
     th = [threading.Thread(target=open_loop, args=(srv.port, "abuse", abuse_p, a.abuse_rate, a.seconds, a.clients, res)),
           threading.Thread(target=open_loop, args=(srv.port, "tx", tx_p, a.tx_rate, a.seconds, a.clients, res))]
     [t.start() for t in th]
-    mixed = batch_load(eng, payloads, a.threads, a.seconds, NOW0 + 600)
+    mixed = batch_load(eng, payloads, a.threads, a.seconds, NOW0 + 600, rate=a.batch_rate)
     [t.join() for t in th]
     st = eng.acct.router.stats(3, False)
     fb = sum(int(d.driver.fallbacks) for d in dev) - fb0
@@ -165,7 +185,17 @@ def main(argv=None) -> int:
                unary_without_scorebatch=dict(check_bonus_abuse=solo.get("abuse"), score_transaction=solo.get("tx")),
                abuse_cluster_fallbacks=fb,
                abuse_rows_per_device_step=round(st.get("items", 0) / max(int(st.get("steps", 1)), 1), 1),
+               # where an abuse call's time goes in the mixed phase (acct_core.h AcctStats): queueing
+               # before its step, the step on the device, the answer writing (link lookups included)
+               abuse_device_us_per_step=round(st.get("device_ns", 0) / max(int(st.get("steps", 1)), 1) / 1e3, 1),
+               abuse_queue_us_per_call=round(st.get("queue_ns", 0) / max(int(st.get("items", 1)), 1) / 1e3, 1),
+               abuse_finish_us_per_step=round(st.get("finish_ns", 0) / max(int(st.get("steps", 1)), 1) / 1e3, 1),
+               abuse_steps=int(st.get("steps", 0)),
+               link_read_timeouts=int(getattr(eng.links, "read_timeouts", 0) or 0) if getattr(eng, "links", None) else None,
+               link_lock_takeovers=int(getattr(eng.links, "takeovers", 0) or 0) if getattr(eng, "links", None) else None,
                config=dict(scorebatch_threads=a.threads, clients_per_rpc=a.clients, server_workers=a.server_workers,
+                           scorebatch_offered_per_s=(a.batch_rate * 8192 if a.batch_rate > 0 else "closed loop"),
+                           abuse_max_batch=a.abuse_max_batch, abuse_high_priority=bool(a.abuse_priority),
                            models="cfg3 GBDT(100,d7,128f)+MLP(32-256-1) fp32; cfg5 GRU 2x256 x 100 events fp32 split"),
                server_stats=srv.stats())
     srv.stop()
