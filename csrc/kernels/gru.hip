@@ -867,15 +867,6 @@ static void launch_gru_h(const GruArgs& a, hipStream_t st) {
   }
 }
 
-// Cluster counters start every launch at 0: a cluster that timed out leaves its
-// counters part-advanced (only member 0 of a finished cluster resets them), and a launch queued
-// behind it on the same stream would otherwise pass its first waits early and read slices that
-// were never published. A memset node in the captured step graph, ahead of the kernel.
-static void reset_cluster_counters(int32_t* sync, size_t n, hipStream_t st) {
-  const hipError_t e = hipMemsetAsync(sync, 0, n * sizeof(int32_t), st);
-  if (e != hipSuccess) throw std::runtime_error(std::string("gru: counter reset: ") + hipGetErrorString(e));
-}
-
 void launch_gru(const GruArgs& a, hipStream_t st) {
   if (a.n_rows <= 0) return;
   static int n_cu = [] {
@@ -891,7 +882,6 @@ void launch_gru(const GruArgs& a, hipStream_t st) {
     // resident; its bounded waits only guard against what cannot); larger ones: the
     // batch-parallel split kernel
     if (a.ws && gru_wsx_eligible(a) && gru_wsx_clusters(a.n_rows) * 16 <= n_cu / 2) {
-      reset_cluster_counters(a.ws_sync, size_t(a.ws_clusters) * 16, st);
       return launch_gru_wsx(a, st);
     }
     const int ksx = a.layer[0].kx_pad / 32;
@@ -908,7 +898,6 @@ void launch_gru(const GruArgs& a, hipStream_t st) {
   if (a.ws && gru_ws_eligible(a)) {
     // ws = 3: two 64-row clusters per CU (all co-resident at <= 2 workgroups per CU)
     if (a.ws == 3 ? gru_ws2_clusters(a.n_rows) * 8 <= 2 * n_cu : gru_ws_clusters(a.n_rows) * 8 <= n_cu) {
-      reset_cluster_counters(a.ws_sync, size_t(a.ws_clusters) * 32, st);
       return launch_gru_ws(a, st);
     }
   }

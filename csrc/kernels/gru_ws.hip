@@ -144,15 +144,21 @@ __device__ __forceinline__ void ws_layer(const bf16x8 (&wz)[16], const bf16x8 (&
 }
 #undef MFMA
 
-// bounded poll of the cluster counter by one lane; returns false on timeout
-__device__ __forceinline__ bool ws_wait(int32_t* cnt, int target) {
+// bounded poll of a cluster counter by one lane; returns false on timeout, after poisoning both
+// counters of the cluster (`base`: cnt[0] and cnt[8], gru.hip kClusterPoison) so that no member
+// still to arrive and no launch queued behind this one passes a wait on a part-advanced count
+__device__ __forceinline__ bool ws_wait(int32_t* cnt, int target, int32_t* base) {
   const uint64_t t0 = wall_clock64();
   for (;;) {
     for (int n = 0; n < 64; ++n) {
       if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
       __builtin_amdgcn_s_sleep(1);
     }
-    if (wall_clock64() - t0 > WS_WAIT_TICKS) return false;
+    if (wall_clock64() - t0 > WS_WAIT_TICKS) {
+      __hip_atomic_exchange(base, kClusterPoison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_exchange(base + 8, kClusterPoison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
   }
 }
 
@@ -354,7 +360,7 @@ __global__ void __launch_bounds__(256, 1) gru_ws_kernel(GruArgs a) {
         if (arrive) __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         bool ok = true;
         if (target > 0) {
-          ok = ws_wait(c, target);
+          ok = ws_wait(c, target, cnt);
           if (!ok) atomicExch(a.ws_err, 1);
         }
         *sflag = ok;
@@ -476,7 +482,7 @@ __global__ void __launch_bounds__(256, 1) gru_ws_kernel(GruArgs a) {
     WS_MARK(t, 2);
     if (tid == 0) {
       __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const bool ok = ws_wait(cnt, WS_CL * (t + 1));
+      const bool ok = ws_wait(cnt, WS_CL * (t + 1), cnt);
       if (!ok) atomicExch(a.ws_err, 1);
       *sflag = ok;
     }
@@ -549,7 +555,7 @@ __global__ void __launch_bounds__(256, 1) gru_ws_kernel(GruArgs a) {
     __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bool ok = true;
     if (mem == 0) {
-      ok = ws_wait(cnt, WS_CL * (T + 1));
+      ok = ws_wait(cnt, WS_CL * (T + 1), cnt);
       if (!ok) atomicExch(a.ws_err, 1);
     }
     *sflag = ok;
@@ -856,7 +862,7 @@ __global__ void __launch_bounds__(256, 2) gru_ws2_kernel(GruArgs a) {
       WS_MARK(t, 2);
       if (tid == 0) {
         __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool ok = ws_wait(cnt, WS_CL * (t + 1));
+        const bool ok = ws_wait(cnt, WS_CL * (t + 1), cnt);
         if (!ok) atomicExch(a.ws_err, 1);
         *sflag = ok;
       }
@@ -925,7 +931,7 @@ __global__ void __launch_bounds__(256, 2) gru_ws2_kernel(GruArgs a) {
     __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bool ok = true;
     if (mem == 0) {
-      ok = ws_wait(cnt, WS_CL * (T + 1));
+      ok = ws_wait(cnt, WS_CL * (T + 1), cnt);
       if (!ok) atomicExch(a.ws_err, 1);
     }
     *sflag = ok;

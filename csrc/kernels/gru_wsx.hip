@@ -77,7 +77,9 @@ __device__ __forceinline__ bf16x8 xlds(const uint16_t* p) {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);   \
   } while (0)
 
-// bounded poll of the cluster counter by one lane; false on timeout
+// bounded poll of the cluster counter by one lane; false on timeout, after poisoning the
+// counter (gru.hip kClusterPoison): the members still to arrive and every launch queued behind
+// this one then fail their waits too instead of passing them early on a part-advanced count
 __device__ __forceinline__ bool xwait(int32_t* cnt, int target) {
   const uint64_t t0 = wall_clock64();
   for (;;) {
@@ -85,7 +87,10 @@ __device__ __forceinline__ bool xwait(int32_t* cnt, int target) {
       if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
       __builtin_amdgcn_s_sleep(1);
     }
-    if (wall_clock64() - t0 > X_WAIT_TICKS) return false;
+    if (wall_clock64() - t0 > X_WAIT_TICKS) {
+      __hip_atomic_exchange(cnt, kClusterPoison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
   }
 }
 

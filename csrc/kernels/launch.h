@@ -242,6 +242,13 @@ void launch_tree_head(const TreeArgs& a, const HeadArgs& h, int groups, float* p
 
 void launch_ensemble(const EnsembleArgs& a, hipStream_t st);
 
+// Cluster counters of the weight-stationary GRU kernels (gru_ws.hip, gru_wsx.hip): a member
+// whose bounded wait times out stores this value into its cluster's counters before it exits.
+// Every later wait on them then fails as well (no launch can add its way back to a target from
+// here), so counters that a failed launch left part-advanced are never passed early; the host
+// zeroes them when it falls back (GruPack.disable_ws) - a successful launch leaves them at 0.
+constexpr int32_t kClusterPoison = -(1 << 30);
+
 // ---- K4 GRU sequence (recurrent weights resident in VGPRs)
 // ---- K4 GRU (1-2 stacked ONNX GRU layers, forward, layout 0) + optional N=1 head
 // Weights are fragment-packed on the host: P[nt][ks][lane][8] = W[nt*16 + (lane&15)]

@@ -56,9 +56,12 @@ struct AbuseParams {
   double threshold = 0.7;
   double w[7] = {0.35, 0.2, 0.15, 0.1, 0.1, 0.1, 0.25};
   int32_t linked_limit = 16;
-  // wait at most this long for link inserts queued before the request (the serving core keeps at
-  // most kLinkQueue batch inserts queued, ~1 ms each: a longer wait only adds latency under load)
-  int64_t link_wait_us = 2000;
+  // wait at most this long for link inserts queued before the request (AbuseConfig.link_wait_us).
+  // The serving core keeps at most kLinkQueue batch inserts queued (~1 ms each) and drops the
+  // rest under overload, so links are best-effort there anyway; a long wait only adds latency:
+  // 2 ms put ~0.4-1.3 ms of link waiting on every CheckBonusAbuse micro-batch under ScoreBatch
+  // load (tools/bench_mixed.py abuse_finish_us_per_step, profiles/r6/j)
+  int64_t link_wait_us = 500;
 };
 
 namespace acctwire {

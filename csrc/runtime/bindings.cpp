@@ -987,7 +987,7 @@ PYBIND11_MODULE(_native, m) {
       .def("resume", [](PyAcct& a) { a.router->resume(); })
       .def("set_links", [](PyAcct& a, std::shared_ptr<LinkIndex> l) { a.router->set_links(std::move(l)); })
       .def("set_abuse", [](PyAcct& a, int max_devices, int max_ips, int max_tx_per_minute, double threshold,
-                           std::vector<double> weights, int linked_limit) {
+                           std::vector<double> weights, int linked_limit, int64_t link_wait_us) {
         AbuseParams p;
         p.max_devices_per_day = max_devices;
         p.max_ips_per_day = max_ips;
@@ -996,9 +996,10 @@ PYBIND11_MODULE(_native, m) {
         if (weights.size() != 7) throw std::runtime_error("set_abuse: 7 signal weights");
         for (int k = 0; k < 7; ++k) p.w[k] = weights[size_t(k)];
         p.linked_limit = linked_limit;
+        p.link_wait_us = link_wait_us;
         a.router->set_abuse(p);
       }, py::arg("max_devices"), py::arg("max_ips"), py::arg("max_tx_per_minute"), py::arg("threshold"),
-         py::arg("weights"), py::arg("linked_limit") = 16)
+         py::arg("weights"), py::arg("linked_limit") = 16, py::arg("link_wait_us") = AbuseParams().link_wait_us)
       .def("serves", [](PyAcct& a, int rpc) { return a.router->serves(uint8_t(rpc)); })
       .def("submit", [](PyAcct& a, int rpc, py::bytes data, uint64_t tag, int64_t t0_ns, int64_t now) {
         char* p; py::ssize_t n;

@@ -170,15 +170,22 @@ class ServerConfig:
 class AbuseConfig:
     """CheckBonusAbuse decision threshold (engine/abuse.py documents the signal weights) and the
     native abuse device's micro-batching on a GPU shard that also scores transactions:
-    ``max_batch`` caps the rows of one device step (0: the shard's largest batch bucket) - at
-    <= 256 every step runs the weight-stationary split GRU clusters (gru_wsx.hip), which read no
-    weights per step and so do not compete with the scoring kernels for L2; ``high_priority``
-    creates the abuse streams at high queue priority. Off by default: on the box it made the
-    abuse path slower, not faster - unary CheckBonusAbuse p99 391 ms at high priority vs 1.9 ms
-    at normal priority with no ScoreBatch load (tools/bench_mixed.py, profiles/r6/f)."""
+    ``max_batch`` caps the rows of one device step (0: the shard's largest batch bucket);
+    ``cluster_kernel`` runs steps of <= 256 rows on the weight-stationary split GRU clusters
+    (gru_wsx.hip), which read no weights per timestep: the batch-parallel kernel streams the
+    2.5 MB weight set through L2 every timestep of every workgroup, and beside a ScoreBatch
+    load that cost the scoring path 64-79 % of its throughput (profiles/r6/i);
+    ``high_priority`` creates the abuse streams at high queue priority, off by default: on the
+    box it made the abuse path slower, not faster - unary CheckBonusAbuse p99 391 ms at high
+    priority vs 1.9 ms at normal priority with no ScoreBatch load (tools/bench_mixed.py,
+    profiles/r6/f)."""
     threshold: float = 0.7
     max_batch: int = 0
     high_priority: bool = False
+    cluster_kernel: bool = True
+    # longest wait of a CheckBonusAbuse micro-batch for the link inserts queued before its calls
+    # (acct_core.h AbuseParams.link_wait_us)
+    link_wait_us: int = 500
 
 
 @dataclass

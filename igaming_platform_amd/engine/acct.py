@@ -118,7 +118,7 @@ class AbuseNativeDevice:
     accounts (the rule signals) and, with an abuse model, the GRU over their event rings."""
 
     def __init__(self, backend, plan=None, buckets=(64, 512, 4096), depth: int = 2, rank: int = 0,
-                 max_batch: int = 0, priority: int = 0):
+                 max_batch: int = 0, priority: int = 0, cluster_kernel: bool = True):
         import torch
         from ..ops import kernels as K
         from .runner import GruModel
@@ -138,11 +138,14 @@ class AbuseNativeDevice:
                 raise ValueError("abuse model must end in an N=1 head (probability)")
             # the bf16 cluster kernel (gru_ws.hip) needs the whole chip co-resident, which a
             # serving rank sharing it with the scoring pipeline cannot promise: off. The split
-            # clusters for small batches (gru_wsx.hip, <= a quarter of the chip per launch) stay,
-            # with a second graph per step on the batch-parallel kernel that the driver switches
-            # to if a cluster ever gives up (NaN scores, model_driver.hip check_fallback)
+            # clusters for small batches (gru_wsx.hip, <= half the chip per launch) with
+            # ``cluster_kernel`` (AbuseConfig, default on), with a second graph per step on the
+            # batch-parallel kernel that the driver switches to if a cluster gives up (NaN
+            # scores, model_driver.hip check_fallback). The step graphs hold no counter-reset
+            # memset: with one, cluster launches stalled up to their 200 ms bound (cfg5 serving
+            # 0.22 M checks/s at p99 204 ms vs 1.14 M at p99 15 ms without, profiles/r6/g, r6/i)
             for gp in self.gm.packs:
-                gp.disable_ws(keep_wsx=True)
+                gp.disable_ws(keep_wsx=cluster_kernel)
             if any(gp.wsx_ok for gp in self.gm.packs):
                 # 128- and 256-row buckets: micro-batches up to 256 rows run on the clusters
                 # (8 x 16 CUs at 256 rows)
@@ -266,10 +269,10 @@ class NativeAcct:
                            finishers=int(g.serve_finishers))
         self.devices.append(device)
 
-    def set_abuse(self, scoring, threshold: float) -> None:
+    def set_abuse(self, scoring, threshold: float, link_wait_us: int = 500) -> None:
         self.router.set_abuse(int(scoring.max_devices_per_day), int(scoring.max_ips_per_day),
                               int(scoring.max_tx_per_minute), float(threshold),
-                              [float(SIGNAL_WEIGHTS[k]) for k in SIGNAL_ORDER])
+                              [float(SIGNAL_WEIGHTS[k]) for k in SIGNAL_ORDER], link_wait_us=int(link_wait_us))
 
     def refresh(self) -> None:
         """Re-copy the devices' config blocks with no step in flight (a device's slots run on
@@ -306,11 +309,12 @@ def attach_models(acct: NativeAcct, cfg, backend, ltv=None, owner: int = 0, abus
         # (torch maps a large negative priority to the highest the device allows)
         acct.attach(AbuseNativeDevice(backend, abuse_plan, buckets=cfg.gpu.buckets, depth=depth, rank=rank,
                                       max_batch=int(cfg.abuse.max_batch),
-                                      priority=-100 if cfg.abuse.high_priority else 0), cfg)
+                                      priority=-100 if cfg.abuse.high_priority else 0,
+                                      cluster_kernel=bool(cfg.abuse.cluster_kernel)), cfg)
     elif backend.kind == "cpu" and hasattr(backend, "sc"):
         acct.attach(cpu_abuse_device(backend, abuse_model, max(cfg.gpu.buckets),
                                      cfg.abuse_model.input_name, cfg.abuse_model.output_name, depth), cfg)
-    acct.set_abuse(cfg.scoring, cfg.abuse.threshold)
+    acct.set_abuse(cfg.scoring, cfg.abuse.threshold, cfg.abuse.link_wait_us)
 
 
 def abuse_device_plan(cfg, abuse_model, device) -> Optional[object]:

@@ -753,7 +753,7 @@ class RiskEngine:
             self.fallback.refresh_config(self.scoring)
         acct = getattr(self, "acct", None)
         if acct is not None:
-            acct.set_abuse(self.scoring, self.cfg.abuse.threshold)
+            acct.set_abuse(self.scoring, self.cfg.abuse.threshold, self.cfg.abuse.link_wait_us)
             acct.refresh()
 
     # ---- blacklist (risk.proto:151-181; redis_store.go:251-293)
@@ -1125,7 +1125,8 @@ def serve_shard(cfg: Config, comm, backend: str = "gpu", capacity: Optional[int]
     abuse_gpu = make_abuse_gpu(cfg, node.local, abuse_model if abuse_model is not None else cfg.abuse_model.path)
     try:
         out = run_worker(comm, node.local, abuse_gpu, node.core, ltv=ltv, acct=acct,
-                         abuse_threshold=cfg.abuse.threshold)
+                         abuse_threshold=cfg.abuse.threshold,
+                         abuse_link_wait_us=cfg.abuse.link_wait_us)
     finally:
         if started is not None and hasattr(started, "stop"):
             started.stop(1.0)

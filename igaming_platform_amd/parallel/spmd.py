@@ -104,6 +104,7 @@ class ShardRunner:
         self.ltv = ltv    # this rank's LTV shard (engine/ltv.py LtvService holding its own accounts)
         self.acct = None  # this rank's native account-RPC router (engine/acct.py NativeAcct)
         self.abuse_threshold = 0.7
+        self.abuse_link_wait_us = 500
         self.model_version = 1  # fraud-model reloads applied (audit stamp of the core's rows)
         self.snapshot_dir = None  # the directory of the last OP_SNAPSHOT (final snapshot on failure)
         self.used = [0] * comm.world  # slots in use per rank (the shared registry, via OP_PING)
@@ -167,7 +168,7 @@ class ShardRunner:
             sc = scoring_from_json(payload)
             self.be.refresh_config(sc)
             if self.acct is not None:  # the abuse signal limits of this rank's native router
-                self.acct.set_abuse(sc, self.abuse_threshold)
+                self.acct.set_abuse(sc, self.abuse_threshold, self.abuse_link_wait_us)
                 self.acct.refresh()
             return None
         if op == OP_RELOAD:  # payload: ONNX bytes (empty: built-in heuristic)
@@ -469,7 +470,8 @@ class SpmdGroup:
             log.warning("destroy_process_group after failure: %s", e)
 
 
-def run_worker(comm, backend, abuse_gpu=None, core=None, ltv=None, acct=None, abuse_threshold: float = 0.7):
+def run_worker(comm, backend, abuse_gpu=None, core=None, ltv=None, acct=None, abuse_threshold: float = 0.7,
+               abuse_link_wait_us: int = 500):
     """Cold-op loop of ranks >= 1 until rank 0 sends STOP (the rank's serving core keeps
     ingesting and stepping on its own threads meanwhile). Returns (ops served, rows scored).
     When a collective fails (rank 0 or a peer died / the group was torn down), the shard
@@ -477,6 +479,7 @@ def run_worker(comm, backend, abuse_gpu=None, core=None, ltv=None, acct=None, ab
     the loop returns."""
     runner = ShardRunner(comm, backend, abuse_gpu, core, ltv)
     runner.acct, runner.abuse_threshold = acct, float(abuse_threshold)
+    runner.abuse_link_wait_us = int(abuse_link_wait_us)
     served = 0
     while True:
         try:

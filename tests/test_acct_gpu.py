@@ -76,6 +76,39 @@ def test_gpu_native_abuse_matches_cpu_engine():
     c.close()
 
 
+@pytest.mark.parametrize("cluster_kernel", [False, True])
+def test_gpu_native_abuse_cluster_kernel_option(cluster_kernel):
+    """AbuseConfig.cluster_kernel: the 2 x 256 GRU's small steps on the split clusters
+    (gru_wsx.hip, with the batch-parallel fallback graphs) or, by default, always on the
+    batch-parallel split kernel - the same scores either way (both f32-faithful), no fallback."""
+    from igaming_platform_amd.config import Config
+    from igaming_platform_amd.engine.acct import AbuseNativeDevice
+    from igaming_platform_amd.engine.risk_engine import RiskEngine
+    from igaming_platform_amd.onnx import builders
+    from igaming_platform_amd.proto import risk_v1 as P
+    am = builders.build("gru", seq=100, in_dim=16, hidden=256).SerializeToString()
+    cfg = Config()
+    cfg.gpu.buckets = [64, 512]
+    cfg.abuse.cluster_kernel = cluster_kernel
+    g = RiskEngine(cfg, backend="gpu", capacity=256, abuse_model=am)
+    c = RiskEngine(cfg, backend="cpu", capacity=256, abuse_model=am)
+    dev = next(d for d in g.acct.devices if isinstance(d, AbuseNativeDevice))
+    assert any(gp.wsx_ok for gp in dev.gm.packs) == cluster_kernel
+    assert (128 in dev.buckets) == cluster_kernel  # the cluster kernel's 128 / 256-row buckets
+    ids = _populate(g)
+    _populate(c)
+    reqs = [x for x in _requests(ids) if x[0] == 3]
+    a = _ask(g.acct.router, reqs)
+    b = _ask(c.acct.router, reqs)
+    for (x, _), (y, _) in zip(a, b):
+        rx, ry = P.CheckBonusAbuseResponse.FromString(x), P.CheckBonusAbuseResponse.FromString(y)
+        assert list(rx.signals) == list(ry.signals)
+        assert rx.abuse_score == pytest.approx(ry.abuse_score, abs=1e-4)
+    assert dev.driver.fallbacks == 0
+    g.close()
+    c.close()
+
+
 def test_gpu_native_ltv_through_grpc_under_load():
     """Many concurrent PredictLTV calls over the native HTTP/2 server (open loop, native load
     generator): every call answered, micro-batched (fewer device steps than calls)."""

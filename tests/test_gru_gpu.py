@@ -399,12 +399,15 @@ def test_gru_split_clusters_match_batch_parallel(rows):
     assert float(np.abs(a - ref).max()) <= 1e-4
 
 
-def test_gru_split_clusters_start_from_zeroed_counters():
-    """a cluster launch that timed out leaves its counters part-advanced. Every
-    cluster launch now starts with a memset of its counters (a node of the captured graph), so
-    a launch after such leftovers - here: counters poisoned by hand - still waits for every
-    member and equals the batch-parallel kernel (without the reset its first waits would pass
-    early and read slices that were never published)."""
+def test_gru_split_clusters_never_pass_a_wait_on_leftover_counters():
+    """a cluster launch that timed out must not leave counters that let a later
+    launch pass its waits early (reading slices that were never published). A member whose wait
+    times out poisons its cluster's counters (launch.h kClusterPoison), so the launches behind
+    it give up too - NaN outputs and ws_err, which the hosts turn into the batch-parallel
+    fallback (model_driver.hip check_fallback, engine/abuse.py) - instead of returning wrong
+    numbers; zeroed counters (GruPack.disable_ws, or a successful launch) run clean again. No
+    memset per launch: as a node of the serving step graphs it stalled cluster launches up to
+    their 200 ms bound (profiles/r6/i)."""
     import torch
     from igaming_platform_amd.ops import kernels as K
     T, rows = 100, 64
@@ -416,15 +419,22 @@ def test_gru_split_clusters_start_from_zeroed_counters():
     o_x = torch.full((rows,), -9.0, device="cuda")
     o_bp = torch.full((rows,), -9.0, device="cuda")
     ws = gp.workspace(rows)
-    for poison in (16 * 37, 5):
-        ws["sync"].fill_(poison)
-        o_x.fill_(-9.0)
-        K.gru(gp, rows, T, out=o_x, X=Xd, ws=3)
-        torch.cuda.synchronize()
-        assert not gp.ws_failed()
-        assert int(ws["sync"].abs().sum()) == 0  # member 0 of every cluster returned them to 0
     K.gru(gp, rows, T, out=o_bp, X=Xd, ws=0)
+    K.gru(gp, rows, T, out=o_x, X=Xd, ws=3)  # clean run: counters back to 0
     torch.cuda.synchronize()
+    assert not gp.ws_failed() and int(ws["sync"].abs().sum()) == 0
+    np.testing.assert_allclose(o_x.cpu().numpy(), o_bp.cpu().numpy(), rtol=0, atol=1e-5)
+    ws["sync"].fill_(-(1 << 30))  # what a timed-out member leaves behind
+    o_x.fill_(-9.0)
+    K.gru(gp, rows, T, out=o_x, X=Xd, ws=3)  # gives up after the bounded wait (200 ms)
+    torch.cuda.synchronize()
+    assert gp.ws_failed() and bool(torch.isnan(o_x).all())
+    assert int(ws["sync"].max()) < 0  # still poisoned: the next launch cannot pass early either
+    ws["sync"].zero_()
+    gp.ws_err.zero_()
+    K.gru(gp, rows, T, out=o_x, X=Xd, ws=3)
+    torch.cuda.synchronize()
+    assert not gp.ws_failed() and int(ws["sync"].abs().sum()) == 0
     np.testing.assert_allclose(o_x.cpu().numpy(), o_bp.cpu().numpy(), rtol=0, atol=1e-5)
 
 

@@ -165,6 +165,7 @@ def main(argv=None) -> int:
     [t.join() for t in th]
     time.sleep(1.0)
     eng.acct.router.stats(3, True)
+    eng.core.stats(True)
     res = {}
     th = [threading.Thread(target=open_loop, args=(srv.port, "abuse", abuse_p, a.abuse_rate, a.seconds, a.clients, res)),
           threading.Thread(target=open_loop, args=(srv.port, "tx", tx_p, a.tx_rate, a.seconds, a.clients, res))]
@@ -172,6 +173,10 @@ def main(argv=None) -> int:
     mixed = batch_load(eng, payloads, a.threads, a.seconds, NOW0 + 600, rate=a.batch_rate)
     [t.join() for t in th]
     st = eng.acct.router.stats(3, False)
+    sv = dict(eng.core.stats(False))
+    ns = max(int(sv.get("steps", 1)), 1)
+    serve = {k: sv[k] for k in ("items", "rows", "steps", "unary", "max_step_rows") if k in sv}
+    serve.update({k[:-3] + "_us_per_step": round(sv[k] / ns / 1e3, 1) for k in sv if k.endswith("_ns")})
     fb = sum(int(d.driver.fallbacks) for d in dev) - fb0
     out = dict(metric="mixed traffic on one GPU: ScoreBatch load + open-loop CheckBonusAbuse + ScoreTransaction",
                n_gpus=1, seconds=a.seconds, data="synthetic (UUID ids over %d accounts, random-init cfg3/cfg4/cfg5 "
@@ -197,7 +202,7 @@ def main(argv=None) -> int:
                            scorebatch_offered_per_s=(a.batch_rate * 8192 if a.batch_rate > 0 else "closed loop"),
                            abuse_max_batch=a.abuse_max_batch, abuse_high_priority=bool(a.abuse_priority),
                            models="cfg3 GBDT(100,d7,128f)+MLP(32-256-1) fp32; cfg5 GRU 2x256 x 100 events fp32 split"),
-               server_stats=srv.stats())
+               server_stats=srv.stats(), serve_core_mixed=serve)
     srv.stop()
     eng.close()
     line = json.dumps(out)
