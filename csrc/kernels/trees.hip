@@ -1,9 +1,10 @@
 // K2 tree_ensemble: ONNX-ML TreeEnsemble{Classifier,Regressor} on the complete-tree layout
 // (csrc/runtime/trees.h). Semantics: CPU executor (csrc/runtime/trees.cpp).
 //
-// Block = 256 threads = 4 waves, 64 samples. The block's X tile ([64][F+1] f32; the +1 pad
-// makes the per-lane column reads conflict-free at the root) and its tree group's node table
-// (8 B/node) are staged in LDS. Traversal: lane = sample, the four waves split the group's
+// Block = 256 threads = 4 waves, 64 samples. The block's X tile and its tree group's node table
+// (8 B/node) are staged in LDS. The tile is feature-major, [F][64]: lane r reads sample r's
+// feature at [f][r], bank r whatever feature its traversal reached, so a wave's reads never
+// conflict (the row-major [64][F+1] tile put lane r's read in bank (r + f) % 32). Traversal: lane = sample, the four waves split the group's
 // trees, each lane keeps 4 traversals in flight (independent LDS chains hide ds_read latency).
 //  * K < 16: each lane accumulates its leaf values directly (4-32 B per visit).
 //  * K >= 16 (leaf vectors, e.g. stacked GBDT->MLP embeddings): traversal only records leaf
@@ -76,9 +77,8 @@ template <int K, bool LEQ, bool WT>
 __device__ __forceinline__ void tree_block(const TreeArgs& a, int trees_per_group, int feat_w, int nodes_in_lds,
                                            float* partial, char* smem) {
   constexpr bool TWO_PHASE = K >= 16;
-  const int xs = feat_w + 1;
-  float* sx = reinterpret_cast<float*>(smem);                       // [64][feat_w+1]
-  const size_t x_bytes = ((size_t)TR_ROWS * xs * 4 + 15) & ~size_t(15);
+  float* sx = reinterpret_cast<float*>(smem);                       // [feat_w][64]
+  const size_t x_bytes = ((size_t)TR_ROWS * feat_w * 4 + 15) & ~size_t(15);
   const size_t red_b = TWO_PHASE ? (size_t)TR_ROWS * K * 4 : (size_t)5 * TR_ROWS * K * 4;
   const size_t base_b = x_bytes > red_b ? x_bytes : red_b;
   float2* sn = reinterpret_cast<float2*>(smem + base_b);             // group node table
@@ -99,121 +99,107 @@ __device__ __forceinline__ void tree_block(const TreeArgs& a, int trees_per_grou
   if (trow) trow[k] = (int64_t)wall_clock64()
   TR_MARK(0);
 
-  // stage the X tile and the group's node table: the first chunk of both is loaded with every
-  // load of a thread in flight (one memory round trip instead of one per chunk), then stored
+  // stage the X tile and the group's node table: the node table's first chunk is loaded with
+  // the whole X tile in flight (one memory round trip), then both are stored. X is read one row
+  // per lane (lane r = sample r, its row's 16-B chunks cg, cg + 4, ...): the feature-major
+  // stores of a wave then hit 64 different banks as well
   const float2* gn = a.nodes + (size_t)t0 * n_int;
   {
-    constexpr int UX = 32, UN = 16;
-    const int xt = TR_ROWS * feat_w;
+    constexpr int UN = 32, UC = 8;
     const int ntot = nodes_in_lds ? nt * n_int : 0;
-    // X: 16-byte loads when rows are float4-aligned (the usual case), else element loads with
-    // (r, c) advanced incrementally; the tile is stored with a +1 column pad (conflict-free
-    // per-lane column reads at the root)
-    const bool vec = (feat_w & 3) == 0 && (a.x_stride & 3) == 0;
-    const int f4 = feat_w >> 2;
-    const int dr = 256 / feat_w, dc = 256 % feat_w;
-    for (int xb = 0, nb = 0; xb < xt || nb < ntot; xb += 256 * UX, nb += 256 * UN) {
-      float v[UX];
-      float2 w[UN];
-      int rr[UX], cc[UX];
-      if (vec) {
+    float2 w[UN];
 #pragma unroll
-        for (int u = 0; u < UX / 4; ++u) {
-          const int e4 = (xb >> 2) + u * 256 + tid;  // float4 index in the tile
-          const int r = e4 / f4, c = (e4 - r * f4) * 4;
-          const int row = row0 + r;
-          float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (r < TR_ROWS && row < a.n_rows) q = *reinterpret_cast<const float4*>(a.X + (size_t)row * a.x_stride + c);
-          v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
-          rr[4 * u] = r; cc[4 * u] = c;
-        }
-      } else {
-        int r = (xb + tid) / feat_w, c = (xb + tid) - r * feat_w;
-#pragma unroll
-        for (int u = 0; u < UX; ++u) {
-          rr[u] = r;
-          cc[u] = c;
-          r += dr;
-          c += dc;
-          if (c >= feat_w) { c -= feat_w; ++r; }
-        }
-#pragma unroll
-        for (int u = 0; u < UX; ++u) {
-          const int row = row0 + rr[u];
-          v[u] = (rr[u] < TR_ROWS && row < a.n_rows) ? a.X[(size_t)row * a.x_stride + cc[u]] : 0.f;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < UN; ++u) {
-        const int e = nb + u * 256 + tid;
-        w[u] = e < ntot ? gn[e] : make_float2(0.f, 0.f);
-      }
-      if (vec) {
-#pragma unroll
-        for (int u = 0; u < UX / 4; ++u)
-          if (rr[4 * u] < TR_ROWS) {
-            float* d = sx + rr[4 * u] * xs + cc[4 * u];
-            d[0] = v[4 * u]; d[1] = v[4 * u + 1]; d[2] = v[4 * u + 2]; d[3] = v[4 * u + 3];
-          }
-      } else {
-#pragma unroll
-        for (int u = 0; u < UX; ++u)
-          if (rr[u] < TR_ROWS) sx[rr[u] * xs + cc[u]] = v[u];
-      }
-#pragma unroll
-      for (int u = 0; u < UN; ++u) {
-        const int e = nb + u * 256 + tid;
-        if (e < ntot) sn[e] = w[u];
-      }
+    for (int u = 0; u < UN; ++u) {
+      const int e = u * 256 + tid;
+      w[u] = e < ntot ? gn[e] : make_float2(0.f, 0.f);
     }
+    const int r = lane, row = row0 + r;
+    const bool live = row < a.n_rows;
+    const float* xr = a.X + (size_t)(live ? row : 0) * a.x_stride;
+    if ((feat_w & 3) == 0 && (a.x_stride & 3) == 0) {  // 16-byte loads (the usual case)
+      const int f4 = feat_w >> 2;
+      for (int c0 = wave; c0 < f4; c0 += 4 * UC) {
+        float4 q[UC];
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+          const int ch = c0 + 4 * u;
+          q[u] = live && ch < f4 ? *reinterpret_cast<const float4*>(xr + 4 * ch) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+          const int ch = c0 + 4 * u;
+          if (ch < f4) {
+            float* d = sx + (4 * ch) * TR_ROWS + r;
+            d[0] = q[u].x; d[TR_ROWS] = q[u].y; d[2 * TR_ROWS] = q[u].z; d[3 * TR_ROWS] = q[u].w;
+          }
+        }
+      }
+    } else {
+      for (int c = wave; c < feat_w; c += 4) sx[c * TR_ROWS + r] = live ? xr[c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+      const int e = u * 256 + tid;
+      if (e < ntot) sn[e] = w[u];
+    }
+    for (int e = UN * 256 + tid; e < ntot; e += 256) sn[e] = gn[e];
   }
   __syncthreads();
   TR_MARK(1);
-  const float2* nodes = nodes_in_lds ? sn : gn;
-  const float* xrow = sx + lane * xs;
 
   float acc[TWO_PHASE ? 1 : K];
 #pragma unroll
   for (int k = 0; k < (TWO_PHASE ? 1 : K); ++k) acc[k] = 0.f;
 
-  for (int tb = t0 + wave; tb < t1; tb += 4 * TR_ILP) {
-    int idx[TR_ILP];
-    int tt[TR_ILP];
-#pragma unroll
-    for (int q = 0; q < TR_ILP; ++q) {
-      tt[q] = tb + 4 * q;
-      idx[q] = 0;
-    }
-    for (int d = 0; d < a.depth; ++d) {
+  // traversal: lane = sample, TR_ILP trees per wave in flight. The trees of a wave are uniform
+  // (scalar tree index), so a missing tree past the group end is a scalar condition, not an
+  // exec-masked branch; each level issues the TR_ILP node reads, then the TR_ILP feature reads
+  // (the node table from LDS - ds_read, not a flat load through the vector memory path - and
+  // the X tile, conflict-free), then the TR_ILP compares
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  auto traverse = [&](const float2* nodes) {
+    for (int tb = t0 + wv; tb < t1; tb += 4 * TR_ILP) {
+      int idx[TR_ILP], nb[TR_ILP];
 #pragma unroll
       for (int q = 0; q < TR_ILP; ++q) {
-        if (tt[q] < t1) {
-          const float2 nd = nodes[(tt[q] - t0) * n_int + idx[q]];
-          const int f = __float_as_uint(nd.y) & 0xffff;
-          idx[q] = tree_next<LEQ>(idx[q], xrow[f], nd);
-        }
+        const int tq = tb + 4 * q;
+        nb[q] = (tq < t1 ? tq - t0 : 0) * n_int;
+        idx[q] = 0;
       }
-    }
+      for (int d = 0; d < a.depth; ++d) {
+        float2 nd[TR_ILP];
+        float xv[TR_ILP];
 #pragma unroll
-    for (int q = 0; q < TR_ILP; ++q) {
-      if (tt[q] >= t1) continue;
-      if constexpr (TWO_PHASE) {
-        sleaf[lane * nt + (tt[q] - t0)] = (uint16_t)(idx[q] - n_int);
-      } else {
-        const float* lf = a.leaves + ((size_t)tt[q] * n_leaf + (idx[q] - n_int)) * K;
-        if constexpr (K % 4 == 0) {
+        for (int q = 0; q < TR_ILP; ++q) nd[q] = nodes[nb[q] + idx[q]];
 #pragma unroll
-          for (int k = 0; k < K; k += 4) {
-            const float4 v = *reinterpret_cast<const float4*>(lf + k);
-            acc[k] += v.x; acc[k + 1] += v.y; acc[k + 2] += v.z; acc[k + 3] += v.w;
-          }
+        for (int q = 0; q < TR_ILP; ++q) xv[q] = sx[(__float_as_uint(nd[q].y) & 0xffff) * TR_ROWS + lane];
+#pragma unroll
+        for (int q = 0; q < TR_ILP; ++q) idx[q] = tree_next<LEQ>(idx[q], xv[q], nd[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < TR_ILP; ++q) {
+        const int tq = tb + 4 * q;
+        if (tq >= t1) break;
+        if constexpr (TWO_PHASE) {
+          sleaf[lane * nt + (tq - t0)] = (uint16_t)(idx[q] - n_int);
         } else {
+          const float* lf = a.leaves + ((size_t)tq * n_leaf + (idx[q] - n_int)) * K;
+          if constexpr (K % 4 == 0) {
 #pragma unroll
-          for (int k = 0; k < K; ++k) acc[k] += lf[k];
+            for (int k = 0; k < K; k += 4) {
+              const float4 v = *reinterpret_cast<const float4*>(lf + k);
+              acc[k] += v.x; acc[k + 1] += v.y; acc[k + 2] += v.z; acc[k + 3] += v.w;
+            }
+          } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc[k] += lf[k];
+          }
         }
       }
     }
-  }
+  };
+  if (nodes_in_lds) traverse(sn);
+  else traverse(gn);
   TR_MARK(2);
   __syncthreads();
   TR_MARK(3);
@@ -572,7 +558,7 @@ static void launch_kl(const TreeArgs& a, int groups, float* partial, int no_fini
   const int tpg = (a.n_trees + groups - 1) / groups;
   const int feat_w = a.x_stride;
   const int n_int = (1 << a.depth) - 1;
-  const size_t x_bytes = ((size_t)TR_ROWS * (feat_w + 1) * 4 + 15) & ~size_t(15);
+  const size_t x_bytes = ((size_t)TR_ROWS * feat_w * 4 + 15) & ~size_t(15);
   const size_t red_bytes = K >= 16 ? (size_t)TR_ROWS * K * 4 : (size_t)5 * TR_ROWS * K * 4;
   const size_t node_bytes = ((size_t)tpg * n_int * 8 + 15) & ~size_t(15);
   const size_t leaf_bytes = K >= 16 ? (size_t)TR_ROWS * tpg * 2 : 0;
@@ -627,7 +613,7 @@ void launch_tree_head(const TreeArgs& a, const HeadArgs& h, int groups, float* p
   const int tpg = (a.n_trees + groups - 1) / groups;
   const int feat_w = a.x_stride;
   const int n_int = (1 << a.depth) - 1;
-  const size_t x_bytes = ((size_t)TR_ROWS * (feat_w + 1) * 4 + 15) & ~size_t(15);
+  const size_t x_bytes = ((size_t)TR_ROWS * feat_w * 4 + 15) & ~size_t(15);
   const size_t red_bytes = (size_t)TR_ROWS * 32 * 4;
   const size_t node_bytes = ((size_t)tpg * n_int * 8 + 15) & ~size_t(15);
   const size_t leaf_bytes = (size_t)TR_ROWS * tpg * 2;
