@@ -109,6 +109,7 @@ def parse():
         a.numerics = "fp32"
     if a.scope == "auto":  # cfg4 / cfg5: the account-RPC serving path, owner-routed over every rank
         a.scope = "serving"
+    a.depth_given = a.depth > 0
     if a.depth <= 0:
         a.depth = 3 if a.config in ("cfg4", "cfg5") else 4
     return a
@@ -209,6 +210,9 @@ def acct_dp_bench(a) -> None:
     if small and kind == "gpu":
         raise SystemExit("IGP_BENCH_SMALL_MODELS is for the CPU rehearsal only")
     cfg, lm, am = acct_models(a.numerics, small)
+    # the account devices' pipeline slots (--depth; default: cfg5 3, cfg4 2 - same-box sweep
+    # cfg5 1.66 / 1.84 / 1.63 M at 2 / 3 / 4, cfg4 4.28 / 1.58 M at 2 / 3, profiles/r6/n)
+    cfg.gpu.acct_depth = max(2, a.depth) if getattr(a, "depth_given", True) else (2 if a.config == "cfg4" else 3)
     n_acc = a.accounts
     if world == 1:
         from igaming_platform_amd.engine.risk_engine import RiskEngine
@@ -287,6 +291,7 @@ def acct_dp_bench(a) -> None:
         "config": {"model": c["desc"], "global_batch": per_step * world, "seq_len": 100 if a.config == "cfg5" else 1,
                    "parallelism": f"dp{world} (owner-routed: each call computed once, on its account's GPU)",
                    "calls_per_step_per_rank": per_step, "inflight_per_rank": a.inflight,
+                   "device_pipeline_depth": cfg.gpu.acct_depth,
                    "submit_threads_per_rank": a.drive_threads,
                    "device_micro_batch_max": max(cfg.gpu.buckets), "accounts_per_gpu": n_acc,
                    "account_spread": f"zipf({a.zipf})" if a.zipf > 1 else "uniform",

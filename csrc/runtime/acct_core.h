@@ -97,6 +97,16 @@ class AcctCore {
   // origin: -1 local call (tag back through the router's sink / poll queue), else the ingress rank
   void submit(uint8_t rpc, int32_t slot, std::string_view account, uint64_t tag, int origin, int64_t now,
               int64_t t0_ns, uint64_t link_ticket);
+  // several local calls under one queue-lock acquisition (AcctRouter::submit_many)
+  struct Call {
+    uint8_t rpc;
+    int32_t slot;
+    std::string_view account;
+    uint64_t tag;
+    int64_t now, t0;
+    uint64_t ticket;
+  };
+  void submit_many(const Call* calls, size_t n);
   void stop();
   // swap the device function table (hot model reload): blocks new steps, drains, swaps
   void set_device(const IgpModelOps* dev);
@@ -249,6 +259,10 @@ class AcctRouter {
   // through the sink (tags with kSinkTag) or poll()
   // now: the clock the account's features are read at (unix s; < 0: the wall clock)
   void submit(uint8_t rpc, const char* data, size_t n, uint64_t tag, int64_t t0_ns, int64_t now = -1);
+  // n calls of one RPC (a submitter's batch): each parsed and routed as submit(), the local ones
+  // queued on their core under one lock acquisition instead of one per call
+  void submit_many(uint8_t rpc, const std::string_view* data, const uint64_t* tags, const int64_t* t0_ns, size_t n,
+                   int64_t now = -1);
   void set_sink(Sink s);
   Sink sink() const;
   size_t poll(std::vector<Done>& out, size_t max, int64_t timeout_us);
