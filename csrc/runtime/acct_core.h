@@ -61,7 +61,7 @@ struct AbuseParams {
   // rest under overload, so links are best-effort there anyway; a long wait only adds latency:
   // 2 ms put ~0.4-1.3 ms of link waiting on every CheckBonusAbuse micro-batch under ScoreBatch
   // load (tools/bench_mixed.py abuse_finish_us_per_step, profiles/r6/j)
-  int64_t link_wait_us = 500;
+  int64_t link_wait_us = 200;
 };
 
 namespace acctwire {

@@ -185,7 +185,7 @@ class AbuseConfig:
     cluster_kernel: bool = True
     # longest wait of a CheckBonusAbuse micro-batch for the link inserts queued before its calls
     # (acct_core.h AbuseParams.link_wait_us)
-    link_wait_us: int = 500
+    link_wait_us: int = 200
 
 
 @dataclass

@@ -269,7 +269,7 @@ class NativeAcct:
                            finishers=int(g.serve_finishers))
         self.devices.append(device)
 
-    def set_abuse(self, scoring, threshold: float, link_wait_us: int = 500) -> None:
+    def set_abuse(self, scoring, threshold: float, link_wait_us: int = 200) -> None:
         self.router.set_abuse(int(scoring.max_devices_per_day), int(scoring.max_ips_per_day),
                               int(scoring.max_tx_per_minute), float(threshold),
                               [float(SIGNAL_WEIGHTS[k]) for k in SIGNAL_ORDER], link_wait_us=int(link_wait_us))

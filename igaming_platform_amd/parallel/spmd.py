@@ -104,7 +104,7 @@ class ShardRunner:
         self.ltv = ltv    # this rank's LTV shard (engine/ltv.py LtvService holding its own accounts)
         self.acct = None  # this rank's native account-RPC router (engine/acct.py NativeAcct)
         self.abuse_threshold = 0.7
-        self.abuse_link_wait_us = 500
+        self.abuse_link_wait_us = 200
         self.model_version = 1  # fraud-model reloads applied (audit stamp of the core's rows)
         self.snapshot_dir = None  # the directory of the last OP_SNAPSHOT (final snapshot on failure)
         self.used = [0] * comm.world  # slots in use per rank (the shared registry, via OP_PING)
@@ -471,7 +471,7 @@ class SpmdGroup:
 
 
 def run_worker(comm, backend, abuse_gpu=None, core=None, ltv=None, acct=None, abuse_threshold: float = 0.7,
-               abuse_link_wait_us: int = 500):
+               abuse_link_wait_us: int = 200):
     """Cold-op loop of ranks >= 1 until rank 0 sends STOP (the rank's serving core keeps
     ingesting and stepping on its own threads meanwhile). Returns (ops served, rows scored).
     When a collective fails (rank 0 or a peer died / the group was torn down), the shard
