@@ -94,6 +94,8 @@ def parse():
     ap.add_argument("--calls", type=int, default=65536, help="cfg4 / cfg5 serving: calls per rank per step")
     ap.add_argument("--inflight", type=int, default=16384, help="cfg4 / cfg5 serving: outstanding calls per rank")
     ap.add_argument("--drive-threads", type=int, default=1, help="cfg4 / cfg5 serving: threads submitting calls per rank")
+    ap.add_argument("--finishers", type=int, default=0,
+                    help="cfg4 / cfg5 serving: answer-writing threads per account device (0: the config's)")
     ap.add_argument("--check-out", default="", help="cfg4 / cfg5 serving: after the timed run every rank answers "
                     "the same fixed calls and writes them to <check-out>.<rank>.json (tests/test_bench_acct.py)")
     ap.add_argument("--seconds", type=float, default=5.0, help="cfg4 / cfg5 serving: seconds per offered-load level")
@@ -213,6 +215,8 @@ def acct_dp_bench(a) -> None:
     # the account devices' pipeline slots (--depth; default: cfg5 3, cfg4 2 - same-box sweep
     # cfg5 1.66 / 1.84 / 1.63 M at 2 / 3 / 4, cfg4 4.28 / 1.58 M at 2 / 3, profiles/r6/n)
     cfg.gpu.acct_depth = max(2, a.depth) if getattr(a, "depth_given", True) else (2 if a.config == "cfg4" else 3)
+    if a.finishers > 0:
+        cfg.gpu.serve_finishers = a.finishers
     n_acc = a.accounts
     if world == 1:
         from igaming_platform_amd.engine.risk_engine import RiskEngine
@@ -262,11 +266,31 @@ def acct_dp_bench(a) -> None:
     router.stats(3 if rpc_name == "abuse" else 1, True)  # the timed run's device steps only
     if comm is not None:
         comm.barrier()
+    # IGP_BENCH_THREADS_OUT=<path>: per-thread CPU over the timed run (rank 0), as in the cfg3
+    # serving bench - which of the router's threads (stepper, completion, finishers, mailbox) or
+    # the drive threads, if any, is saturated
+    threads_out = os.environ.get("IGP_BENCH_THREADS_OUT") if rank == 0 else None
+    if threads_out:
+        import host_profile
+        cpu0, proc0 = host_profile.thread_cpu(), os.times()
     t0 = time.perf_counter()
     r = router.drive(rpc, payloads, a.steps * per_step, a.inflight, now, a.drive_threads)
     if comm is not None:
         comm.barrier()
     elapsed = time.perf_counter() - t0
+    if threads_out:
+        cpu1, proc1 = host_profile.thread_cpu(), os.times()
+        busy, alive = {}, 0.0
+        for tid, (name, cpu) in cpu1.items():
+            d = cpu - cpu0.get(tid, (name, 0.0))[1]
+            alive += d
+            if d > 0:
+                busy.setdefault(name, []).append(round(d / elapsed, 3))
+        total = (proc1.user + proc1.system) - (proc0.user + proc0.system)
+        with open(threads_out, "w") as f:  # the drive threads exit with drive(): total minus the rest
+            json.dump({"elapsed_s": elapsed, "cpu_fraction_by_thread_name": busy,
+                       "drive_threads_cores": round(max(0.0, total - alive) / elapsed, 2),
+                       "process_cores": round(total / elapsed, 2)}, f, indent=1)
     lat = np.asarray(r["latency_ns"], np.float64)
     ok = lat[lat >= 0] / 1e6
     p99 = float(np.percentile(ok, 99)) if len(ok) else float("nan")
@@ -292,7 +316,7 @@ def acct_dp_bench(a) -> None:
                    "parallelism": f"dp{world} (owner-routed: each call computed once, on its account's GPU)",
                    "calls_per_step_per_rank": per_step, "inflight_per_rank": a.inflight,
                    "device_pipeline_depth": cfg.gpu.acct_depth,
-                   "submit_threads_per_rank": a.drive_threads,
+                   "submit_threads_per_rank": a.drive_threads, "finishers_per_device": cfg.gpu.serve_finishers,
                    "device_micro_batch_max": max(cfg.gpu.buckets), "accounts_per_gpu": n_acc,
                    "account_spread": f"zipf({a.zipf})" if a.zipf > 1 else "uniform",
                    "numerics": numerics_desc(a), "backend": kind,

@@ -487,21 +487,32 @@ __device__ __forceinline__ void feature_assemble_body(const AssembleArgs& a) {
       // A/B, cfg3 bench: 109.6 vs 106.1 M scores/s for the full-ring load)
       const int64_t* amp = a.ring_amt + (size_t)s * rs;
       const bool want_amt = !cfg.sum_compat;
+      // amounts as 16-byte pairs (entries 4 q + {0, 1} and {2, 3}: one load per pair with an
+      // in-hour entry, half the load instructions of one 8-byte load per entry when the whole
+      // ring is inside the hour - the serving bench's case)
+      typedef long long k1_ll2 __attribute__((ext_vector_type(2)));
       long long av[16];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t tv[4] = {tsv[i].x, tsv[i].y, tsv[i].z, tsv[i].w};
+        bool in1h[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int64_t t = (int64_t)tv[j];
           const bool v = t != 0 && ql + 16 * i < n4;  // rings < 256 entries: clamped lanes are copies
           c1 += v && t >= now - 60;
           c5 += v && t >= now - 300;
-          const bool in1h = v && t >= now - 3600;
-          c60 += in1h;
-          av[4 * i + j] = 0;
-          if (in1h && want_amt) av[4 * i + j] = amp[4 * (ql + 16 * i) + j];
+          in1h[j] = v && t >= now - 3600;
+          c60 += in1h[j];
         }
+        const k1_ll2* ap = reinterpret_cast<const k1_ll2*>(amp + 4 * (ql + 16 * i));
+        k1_ll2 p0 = {0, 0}, p1 = {0, 0};
+        if (want_amt && (in1h[0] || in1h[1])) p0 = ap[0];
+        if (want_amt && (in1h[2] || in1h[3])) p1 = ap[1];
+        av[4 * i + 0] = in1h[0] ? p0.x : 0;
+        av[4 * i + 1] = in1h[1] ? p0.y : 0;
+        av[4 * i + 2] = in1h[2] ? p1.x : 0;
+        av[4 * i + 3] = in1h[3] ? p1.y : 0;
       }
 #pragma unroll
       for (int k = 0; k < 16; ++k) s60 += av[k];
