@@ -332,6 +332,11 @@ def acct_dp_bench(a) -> None:
         "device_us_per_step_rank0": round(st.get("device_ns", 0) / max(int(st.get("steps", 1)), 1) / 1e3, 1),
         "queue_us_per_call_rank0": round(st.get("queue_ns", 0) / max(int(st.get("items", 1)), 1) / 1e3, 1),
         "max_step_rows_rank0": int(st.get("max_step_rows", 0)),
+        # the slot cycle (acct_core.h AcctStats): dev->submit, device done -> slot released, slot
+        # free -> next step on it; why each step was issued (full / idle device / queue head aged)
+        "slot_cycle_us_per_step_rank0": {k: round(st.get(k + "_ns", 0) / max(int(st.get("steps", 1)), 1) / 1e3, 1)
+                                         for k in ("submit", "turn", "free", "finish")},
+        "steps_by_reason_rank0": {k: int(st.get(k + "_steps", 0)) for k in ("full", "idle", "aged")},
         "cluster_fallbacks_rank0": sum(int(getattr(getattr(d, "driver", None), "fallbacks", 0) or 0)
                                        for d in getattr(acct, "devices", [])),
     }

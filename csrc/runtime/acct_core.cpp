@@ -197,6 +197,8 @@ bool AcctCore::issue(std::unique_lock<std::mutex>& lk) {
   st->failed = false;
   st->err.clear();
   const size_t n = std::min(queue_.size(), size_t(cap_));
+  const int why = queue_.size() >= size_t(cap_) ? 0 : inflight_ == 0 ? 1 : 2;
+  const int64_t t_free = st->t_release;
   st->items.reserve(n);
   int64_t now = 0;
   for (size_t k = 0; k < n; ++k) {
@@ -223,6 +225,9 @@ bool AcctCore::issue(std::unique_lock<std::mutex>& lk) {
     st_.steps += 1;
     st_.rows += int64_t(n);
     st_.max_step_rows = std::max<int64_t>(st_.max_step_rows, int64_t(n));
+    st_.submit_ns += st->t_submit - t1;
+    if (t_free > 0) st_.free_ns += t1 - t_free;
+    (why == 0 ? st_.full_steps : why == 1 ? st_.idle_steps : st_.aged_steps) += 1;
     for (const Item& it : st->items) st_.queue_ns += t1 - it.t_enq;
   }
   {
@@ -285,9 +290,10 @@ void AcctCore::completion_loop() {
         st_.wait_errors += 1;
       }
     }
+    st->t_done = mono_ns();
     {
       std::lock_guard<std::mutex> g(st_mu_);
-      st_.device_ns += mono_ns() - st->t_submit;
+      st_.device_ns += st->t_done - st->t_submit;
     }
     const size_t n = st->items.size();
     const size_t nf = size_t(std::max(1, opt_.finishers));
@@ -310,6 +316,12 @@ void AcctCore::completion_loop() {
 
 void AcctCore::release(Step* st) {
   if (st->refs.fetch_sub(1) != 1) return;
+  const int64_t t = mono_ns();
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    if (st->t_done > 0) st_.turn_ns += t - st->t_done;
+  }
+  st->t_release = t;
   {
     std::lock_guard<std::mutex> lk(q_mu_);
     free_slots_.push_back(st->slot);

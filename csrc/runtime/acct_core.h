@@ -77,6 +77,9 @@ void write_abuse(std::string& out, bool is_abuser, float score, const std::vecto
 struct AcctStats {
   int64_t items = 0, steps = 0, rows = 0, device_ns = 0, queue_ns = 0, finish_ns = 0, wait_errors = 0;
   int64_t max_step_rows = 0, remote_in = 0, unknown = 0;
+  // slot cycle: time in dev->submit, device done -> slot released (answers written), slot free ->
+  // next step issued on it; steps issued full / on an idle device / when the queue head aged out
+  int64_t submit_ns = 0, turn_ns = 0, free_ns = 0, full_steps = 0, idle_steps = 0, aged_steps = 0;
 };
 
 class AcctRouter;
@@ -130,7 +133,7 @@ class AcctCore {
   struct Step {
     int slot = 0;
     std::vector<Item> items;
-    int64_t t_submit = 0;
+    int64_t t_submit = 0, t_done = 0, t_release = 0;
     bool failed = false;
     std::string err;
     std::atomic<int> refs{0};

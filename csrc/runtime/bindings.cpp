@@ -113,6 +113,8 @@ py::dict acct_stats_dict(const AcctStats& t) {
   py::dict d;
   d["items"] = t.items; d["steps"] = t.steps; d["rows"] = t.rows; d["device_ns"] = t.device_ns;
   d["queue_ns"] = t.queue_ns; d["finish_ns"] = t.finish_ns; d["wait_errors"] = t.wait_errors;
+  d["submit_ns"] = t.submit_ns; d["turn_ns"] = t.turn_ns; d["free_ns"] = t.free_ns;
+  d["full_steps"] = t.full_steps; d["idle_steps"] = t.idle_steps; d["aged_steps"] = t.aged_steps;
   d["max_step_rows"] = t.max_step_rows;
   return d;
 }

@@ -188,6 +188,14 @@ class AbuseNativeDevice:
         wsx = self.gm is not None and any(gp.wsx_ok for gp in self.gm.packs)
         with torch.cuda.device(dev):
             for b in self.buckets:
+                # rows per workgroup of the batch-parallel split GRU, per bucket: 16-row tiles for
+                # the small steps of unary traffic, 32-row tiles (half the chip at 4096 rows) for
+                # the full steps, so a slot's step runs beside the next slot's as in the cfg5
+                # engine bench (one 16-row-tile step filled the chip: 1.7-1.8 vs 2.6 M checks/s,
+                # profiles/r6/s, round-4 sweep profiles/r4/m/gru_x3_sweep.json)
+                if self.gm is not None and self.gm.split and len(self.streams) > 1:
+                    for gp in self.gm.packs:
+                        gp.x3_rows = 32 if b >= 2048 else 16
                 for slot in range(self.depth):
                     self.driver.set_graph(b, slot, self._capture(slot, b))
                     if wsx:  # the same step on the batch-parallel kernel (the fallback body)
