@@ -92,8 +92,13 @@ def parse():
                          "level, open loop over the native gRPC server (e.g. 25000,50000,100000,200000); without it "
                          "the owner-routed DP bench (every rank's account router, closed loop)")
     ap.add_argument("--calls", type=int, default=65536, help="cfg4 / cfg5 serving: calls per rank per step")
-    ap.add_argument("--inflight", type=int, default=16384, help="cfg4 / cfg5 serving: outstanding calls per rank")
-    ap.add_argument("--drive-threads", type=int, default=1, help="cfg4 / cfg5 serving: threads submitting calls per rank")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="cfg4 / cfg5 serving: outstanding calls per rank (0: (depth + 3) x the device step, so a "
+                         "freed slot finds a full step queued while the answers of the step before it are still "
+                         "on their way back)")
+    ap.add_argument("--drive-threads", type=int, default=4,
+                    help="cfg4 / cfg5 serving: threads submitting calls per rank (one thread: the submit loop "
+                         "itself bounds the rate, profiles/r6/s)")
     ap.add_argument("--finishers", type=int, default=0,
                     help="cfg4 / cfg5 serving: answer-writing threads per account device (0: the config's)")
     ap.add_argument("--check-out", default="", help="cfg4 / cfg5 serving: after the timed run every rank answers "
@@ -217,6 +222,8 @@ def acct_dp_bench(a) -> None:
     cfg.gpu.acct_depth = max(2, a.depth) if getattr(a, "depth_given", True) else (2 if a.config == "cfg4" else 3)
     if a.finishers > 0:
         cfg.gpu.serve_finishers = a.finishers
+    if a.inflight <= 0:
+        a.inflight = (cfg.gpu.acct_depth + 3) * cfg.gpu.max_batch
     n_acc = a.accounts
     if world == 1:
         from igaming_platform_amd.engine.risk_engine import RiskEngine

@@ -296,7 +296,9 @@ __device__ __forceinline__ void write_fenc(const AssembleArgs& a, int row, int q
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      out[ql] = reinterpret_cast<const uint2*>(se)[ql];
+      // only the chunks holding the body and the length byte cross the host link (the reader
+      // takes [0, len) and byte 127: wire.cpp write_tx_body); a ~75-byte body is 11 of 16 chunks
+      if (8 * ql < total || ql == 15) out[ql] = reinterpret_cast<const uint2*>(se)[ql];
       return;
     }
   }
