@@ -207,7 +207,6 @@ bool AcctCore::issue(std::unique_lock<std::mutex>& lk) {
     queue_.pop_front();
   }
   ++inflight_;
-  st->refs.store(1);
   const IgpModelOps* dev = dev_;
   lk.unlock();
   int32_t* sl = dev->slots(dev->ctx, slot);
@@ -295,27 +294,58 @@ void AcctCore::completion_loop() {
       std::lock_guard<std::mutex> g(st_mu_);
       st_.device_ns += st->t_done - st->t_submit;
     }
-    const size_t n = st->items.size();
-    const size_t nf = size_t(std::max(1, opt_.finishers));
-    const size_t per = std::max<size_t>(32, (n + nf - 1) / nf);
+    // the calls and a copy of the outputs leave the slot; answers are written from the copy
+    Batch* bt = nullptr;
     {
       std::lock_guard<std::mutex> g(f_mu_);
-      for (size_t b = 0; b < n; b += per) {
-        st->refs.fetch_add(1);
-        ftasks_.push_back(FTask{st, b, std::min(n, b + per)});
+      if (!batch_pool_.empty()) {
+        bt = batch_pool_.back().release();
+        batch_pool_.pop_back();
       }
     }
-    f_cv_.notify_all();
+    if (!bt) bt = new Batch();
+    bt->items.swap(st->items);
+    st->items.clear();
+    bt->failed = st->failed;
+    bt->err = st->err;
+    bt->has_model = dev->has_model != 0;
+    const size_t n = bt->items.size();
+    const size_t s0 = kind_ == IGP_MODEL_LTV ? 6 * sizeof(float) : sizeof(float);
+    const size_t s1 = kind_ == IGP_MODEL_ABUSE ? sizeof(FeatRec) : 0;
+    if (!bt->failed) {
+      bt->o0.resize(n * s0);
+      if (n) std::memcpy(bt->o0.data(), dev->out0(dev->ctx, st->slot), n * s0);
+      bt->o1.resize(n * s1);
+      if (n && s1) std::memcpy(bt->o1.data(), dev->out1(dev->ctx, st->slot), n * s1);
+    }
     if (late) {  // the device may still write the slot's outputs: keep it until it drained
       char err[256] = {0};
       (void)dev->wait(dev->ctx, st->slot, -1, err, sizeof err);
     }
     release(st);
+    const size_t nf = size_t(std::max(1, opt_.finishers));
+    const size_t per = std::max<size_t>(32, (n + nf - 1) / nf);
+    {
+      std::lock_guard<std::mutex> g(f_mu_);
+      bt->refs.store(int((n + per - 1) / per));
+      if (n == 0) {
+        batch_pool_.emplace_back(bt);
+      } else {
+        for (size_t b = 0; b < n; b += per) ftasks_.push_back(FTask{bt, b, std::min(n, b + per)});
+      }
+    }
+    f_cv_.notify_all();
   }
 }
 
+void AcctCore::recycle(Batch* bt) {
+  if (bt->refs.fetch_sub(1) != 1) return;
+  bt->items.clear();
+  std::lock_guard<std::mutex> g(f_mu_);
+  batch_pool_.emplace_back(bt);
+}
+
 void AcctCore::release(Step* st) {
-  if (st->refs.fetch_sub(1) != 1) return;
   const int64_t t = mono_ns();
   {
     std::lock_guard<std::mutex> g(st_mu_);
@@ -331,13 +361,12 @@ void AcctCore::release(Step* st) {
   idle_cv_.notify_all();
 }
 
-void AcctCore::finish(Step& st, size_t b, size_t e) {
+void AcctCore::finish(Batch& st, size_t b, size_t e) {
   using Done = ServeCore::Done;
   std::vector<Done> local;
   std::vector<std::pair<int, Done>> remote;
-  const IgpModelOps* dev = dev_;
-  const void* o0 = st.failed ? nullptr : dev->out0(dev->ctx, st.slot);
-  const void* o1 = st.failed ? nullptr : dev->out1(dev->ctx, st.slot);
+  const void* o0 = st.failed ? nullptr : st.o0.data();
+  const void* o1 = st.failed ? nullptr : st.o1.data();
   int64_t sec = 0;
   int32_t nanos = 0;
   wall_now(sec, nanos);
@@ -402,7 +431,7 @@ void AcctCore::finish(Step& st, size_t b, size_t e) {
       }
       if (!linked.empty()) fire(6);
       score = std::min(1.0, score);
-      if (dev->has_model) {
+      if (st.has_model) {
         const double ms = double(static_cast<const float*>(o0)[i]);
         if (ms >= ap.threshold) sig.push_back(acctwire::kSignals[7]);
         score = std::max(score, ms);
@@ -431,13 +460,13 @@ void AcctCore::finisher_loop() {
       ftasks_.pop_front();
     }
     const int64_t t0 = mono_ns();
-    finish(*t.st, t.b, t.e);
+    finish(*t.bt, t.b, t.e);
     {
       std::lock_guard<std::mutex> g(st_mu_);
       st_.finish_ns += mono_ns() - t0;
       st_.items += int64_t(t.e - t.b);
     }
-    release(t.st);
+    recycle(t.bt);
   }
 }
 

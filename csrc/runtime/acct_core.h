@@ -136,14 +136,25 @@ class AcctCore {
     int64_t t_submit = 0, t_done = 0, t_release = 0;
     bool failed = false;
     std::string err;
+  };
+  // a completed step's calls and a copy of its outputs: the device slot is released as soon as
+  // the outputs are copied out of its host buffers, and the finishers write the answers from here
+  // (answer writing no longer holds the slot: cfg4 spent 364 us per step between the device
+  // finishing and the slot freeing, profiles/r6/s)
+  struct Batch {
+    std::vector<Item> items;
+    std::vector<char> o0, o1;
+    bool failed = false, has_model = false;
+    std::string err;
     std::atomic<int> refs{0};
   };
   void stepper_loop();
   void completion_loop();
   void finisher_loop();
   bool issue(std::unique_lock<std::mutex>& lk);
-  void finish(Step& st, size_t b, size_t e);
+  void finish(Batch& bt, size_t b, size_t e);
   void release(Step* st);
+  void recycle(Batch* bt);
 
   AcctRouter* router_;
   const IgpModelOps* dev_;
@@ -164,12 +175,13 @@ class AcctCore {
   bool c_stop_ = false;
 
   struct FTask {
-    Step* st;
+    Batch* bt;
     size_t b, e;
   };
   std::mutex f_mu_;
   std::condition_variable f_cv_;
   std::deque<FTask> ftasks_;
+  std::vector<std::unique_ptr<Batch>> batch_pool_;  // under f_mu_
   bool f_stop_ = false;
 
   std::mutex st_mu_;
