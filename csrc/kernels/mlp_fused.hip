@@ -43,6 +43,10 @@ __device__ __forceinline__ int mc_idx(int row, int col) {
   return row * MC_LDA + ((((col >> 3) ^ (row & 15))) << 3) + (col & 7);
 }
 constexpr int MC_PF = 5;  // k-steps of weight fragments prefetched ahead
+// the split chain's (hi + lo fragments: twice the registers per k-step): one k-step ahead. Two
+// ahead spilled 2 VGPRs at 2 waves per SIMD and ran slower (8192 rows: 120 -> 124-126 us alone,
+// cfg4 engine_only 137.6 -> 133.9 M, profiles/r6/z); three spilled 47
+constexpr int MC_PFS = 1;
 
 __device__ __forceinline__ float mc_act(float v, int act) {
   switch (act) {
@@ -64,8 +68,11 @@ __device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, c
                                              int colw, int NT, int lane, mc_f32x4 (&acc)[MT][JT]) {
   const int NTT = N >> 4;  // column tiles of the layer: a k-step's tiles are NTT x 1 KB contiguous
   if constexpr (SPLIT) {
-    // hi*hi + hi*lo + lo*hi per k-step; both weight halves prefetched one k-step ahead
-    mc_bf16x8 fh[2][JT], fl[2][JT];
+    // hi*hi + hi*lo + lo*hi per k-step; both weight halves prefetched PFD k-steps ahead (a ring
+    // of PFD + 1 fragment sets: 8 x 16 B per lane per k-step at JT = 4)
+    constexpr int PF = PFD < NKS ? PFD : NKS - 1;
+    constexpr int RING = PF + 1;
+    mc_bf16x8 fh[RING][JT], fl[RING][JT];
     const int kq = 8 * (lane >> 4);
     const size_t woff = (size_t)(colw >> 4) * 512 + lane * 8;
     int jt[JT];
@@ -78,10 +85,11 @@ __device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, c
         dl[j] = *reinterpret_cast<const mc_bf16x8*>(Wlo + woff + ((size_t)ks * NTT + jt[j]) * 512);
       }
     };
-    load(0, fh[0], fl[0]);
+#pragma unroll
+    for (int p = 0; p < PF; ++p) load(p, fh[p], fl[p]);
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      if (ks + 1 < NKS) load(ks + 1, fh[(ks + 1) & 1], fl[(ks + 1) & 1]);
+      if (ks + PF < NKS) load(ks + PF, fh[(ks + PF) % RING], fl[(ks + PF) % RING]);
       __builtin_amdgcn_sched_barrier(0);
       mc_bf16x8 ah[MT], al[MT];
 #pragma unroll
@@ -94,9 +102,9 @@ __device__ __forceinline__ void mc_layer_mma(const uint16_t* __restrict__ Hin, c
       for (int j = 0; j < JT; ++j)
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
-          acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[m], fh[ks & 1][j], acc[m][j], 0, 0, 0);
-          acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[m], fl[ks & 1][j], acc[m][j], 0, 0, 0);
-          acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[m], fh[ks & 1][j], acc[m][j], 0, 0, 0);
+          acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[m], fh[ks % RING][j], acc[m][j], 0, 0, 0);
+          acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[m], fl[ks % RING][j], acc[m][j], 0, 0, 0);
+          acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[m], fh[ks % RING][j], acc[m][j], 0, 0, 0);
         }
     }
     return;
@@ -300,11 +308,11 @@ void launch_mlp_chain(const MlpChainArgs& a, hipStream_t st) {
   const int r = a.rows_per_block;
   if (a.split) {  // f32-faithful: hi + lo tiles fill the LDS (64 rows: each tile once, NBUF = 1)
     if (a.waves == 8 && r == 64)
-      IGP_LAUNCH((mlp_chain_kernel<64, 8, true, MC_PF, 1>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
+      IGP_LAUNCH((mlp_chain_kernel<64, 8, true, MC_PFS, 1>), dim3((a.n_rows + 63) / 64), dim3(512), 0, st, a);
     else if (a.waves == 8)
-      IGP_LAUNCH((mlp_chain_kernel<32, 8, true>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
+      IGP_LAUNCH((mlp_chain_kernel<32, 8, true, MC_PFS>), dim3((a.n_rows + 31) / 32), dim3(512), 0, st, a);
     else
-      IGP_LAUNCH((mlp_chain_kernel<32, 4, true>), dim3((a.n_rows + 31) / 32), dim3(256), 0, st, a);
+      IGP_LAUNCH((mlp_chain_kernel<32, 4, true, MC_PFS>), dim3((a.n_rows + 31) / 32), dim3(256), 0, st, a);
     return;
   }
   if (a.waves == 8 && r == 64) {
