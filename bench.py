@@ -852,6 +852,10 @@ def serving_bench(a) -> None:
     barrier()
     sync()
     core.stats(True)
+    if spmd:  # the exchange driver's wait counters: the timed run only
+        xd0 = getattr(getattr(getattr(node, "local", None), "scorer", None), "xdriver", None)
+        if xd0 is not None:
+            xd0.stats()
     # IGP_BENCH_THREADS_OUT=<path>: per-thread CPU time over the timed run (rank 0; thread names
     # from csrc/runtime/thread_name.h) - which host thread, if any, is saturated
     threads_out = os.environ.get("IGP_BENCH_THREADS_OUT") if rank == 0 else None
@@ -935,6 +939,10 @@ def serving_bench(a) -> None:
         "host_stages_rank0": stages,
         "request_stage_ms_rank0": stage_tails,
     }
+    if spmd:  # the exchange driver's host waits per step (mean / worst): senders' rows, owners' results
+        xd = getattr(getattr(getattr(node, "local", None), "scorer", None), "xdriver", None)
+        if xd is not None:
+            out["exchange_waits_us_rank0"] = {k: round(float(v), 1) for k, v in xd.stats().items()}
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

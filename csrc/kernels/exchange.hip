@@ -489,7 +489,14 @@ class XchgDriver {
   int32_t wait_owners(int slot, int64_t timeout_us, char* err, int32_t errlen) {
     const int64_t g = gen_[size_t(slot)];
     owners_.publish(slot, g);
-    return owners_.wait(slot, g, timeout_us >= 0 ? timeout_us : owner_deadline_us_, wait_spin_us(), err, errlen);
+    // every step's results wait is a host barrier on the slowest owner: its time is accounted
+    // (mean and worst per stats() window) next to the senders' rows wait
+    const auto t0 = clk::now();
+    const int32_t rc = owners_.wait(slot, g, timeout_us >= 0 ? timeout_us : owner_deadline_us_, wait_spin_us(), err, errlen);
+    const double dt = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+    st_[5] += dt;
+    st_[6] = std::max(st_[6], dt);
+    return rc;
   }
 
   void submit_impl(int slot, int C, int seq, int64_t now, uintptr_t src, size_t nbytes, bool with_features) {
@@ -545,7 +552,9 @@ class XchgDriver {
       auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
       st_[0] += us(t0, t1);
       st_[1] += us(t2, clk::now());
-      st_[2] += us(t1, t2);  // the wait for the other senders' rows (host)
+      const double sw = us(t1, t2);  // the wait for the other senders' rows (host)
+      st_[2] += sw;
+      st_[7] = std::max(st_[7], sw);
       st_[3] += 1;
       done_recorded_[slot] = true;
       return;
@@ -654,8 +663,11 @@ class XchgDriver {
     d["submits"] = st_[3];
     d["rows_copy_us"] = st_[0] / n;
     d["launch_event_ops_us"] = st_[1] / n;
-    d["rccl_issue_us"] = st_[2] / n;
+    d[rows_ ? "sender_wait_us" : "rccl_issue_us"] = st_[2] / n;
     d["wait_us"] = st_[4] / n;
+    d["owner_wait_us"] = st_[5] / n;       // results region: wait for every owner's generation
+    d["owner_wait_max_us"] = st_[6];
+    d["sender_wait_max_us"] = st_[7];
     for (double& v : st_) v = 0;
     return d;
   }

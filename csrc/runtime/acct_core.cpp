@@ -74,10 +74,13 @@ void write_ltv(std::string& out, std::string_view account, const float* row, int
   w.i32(5, int32_t(double(row[2])));  // int(float): truncation
   w.f32(6, row[3]);
   w.str(7, kNbaCodes[nba_of(row[5])]);
-  pb::Writer ts;
+  // Timestamp sub-message sized first and written in place (no second buffer per answer)
+  pb::Sizer ts;
   ts.i64(1, sec);
   ts.i32(2, nanos);
-  w.msg(8, ts.buf);
+  w.msg_header(8, ts.n);
+  w.i64(1, sec);
+  w.i32(2, nanos);
   out = std::move(w.buf);
 }
 
@@ -364,6 +367,7 @@ void AcctCore::release(Step* st) {
 void AcctCore::finish(Batch& st, size_t b, size_t e) {
   using Done = ServeCore::Done;
   std::vector<Done> local;
+  local.reserve(e - b);
   std::vector<std::pair<int, Done>> remote;
   const void* o0 = st.failed ? nullptr : st.o0.data();
   const void* o1 = st.failed ? nullptr : st.o1.data();
