@@ -143,6 +143,15 @@ def maybe_launch_torchrun(a) -> None:
         sys.exit(subprocess.call(cmd))
 
 
+def gpu_index(local: int) -> int:
+    """One rank per GPU. More ranks than GPUs (the 1-GPU box's multi-rank rehearsal of the
+    node-shared exchange path, which opens no RCCL communicator) share them round-robin; RCCL
+    itself refuses two ranks on one device. device_count() does not initialise the HIP runtime."""
+    import torch
+    n = torch.cuda.device_count()
+    return local % n if 0 < n <= local else local
+
+
 def acct_serving_bench(a) -> None:
     """cfg4 / cfg5 offered-load curve, 1 GPU (--rates): unary PredictLTV / CheckBonusAbuse calls
     over the native HTTP/2 server (bytes in -> the native account router -> micro-batches on the
@@ -205,6 +214,7 @@ def acct_dp_bench(a) -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     kind = os.environ.get("IGP_BENCH_BACKEND", "gpu")
     if kind == "gpu":
+        local = gpu_index(local)
         torch.cuda.set_device(local)
     comm = None
     if world > 1:
@@ -738,6 +748,7 @@ def serving_bench(a) -> None:
     # IGP_BENCH_BACKEND=cpu: the same serving objects on CPU shards (protocol rehearsal without a GPU)
     kind = os.environ.get("IGP_BENCH_BACKEND", "gpu")
     if kind == "gpu":
+        local = gpu_index(local)
         torch.cuda.set_device(local)
 
     def sync():
@@ -781,9 +792,12 @@ def serving_bench(a) -> None:
         node = SpmdNode(cfg, comm, kind, n_acc + 4096, _load_onnx(fm), "onnx",
                         Blacklist(cfg.gpu.blacklist_capacity), IPIntel(cfg.gpu.blacklist_capacity))
         core, registry, backend = node.core, node.registry, node.local
-        mode = ("native serving core per rank, owner-routed RCCL exchange (every rank ingests), results via "
-                + ("per-GPU D2H into node-shared pinned memory" if node.results_mode == "d2h"
-                   else "the result all-to-all"))
+        from igaming_platform_amd.engine.dp import rows_mode
+        rows_shm = node.results_mode == "d2h" and rows_mode() == "shm"
+        mode = ("native serving core per rank, owner-routed exchange (every rank ingests): rows "
+                + ("through the node-shared pinned rows region" if rows_shm else "over an RCCL all-to-all")
+                + ", results " + ("written by each owner into node-shared pinned memory" if node.results_mode == "d2h"
+                                  else "over the result all-to-all"))
     if core is None:
         raise RuntimeError("no native serving core (IGP native driver disabled?)")
     # this rank's accounts: the global population is world x n_acc UUIDs; a rank loads the

@@ -373,3 +373,34 @@ def test_exchange_world1_same_accounts_in_one_step_follow_fifo_order():
             if e is not None:
                 e.close()
         dist.destroy_process_group()
+
+
+def test_two_rank_processes_serve_through_the_node_shared_exchange():
+    """The multi-rank serving path on real GPU processes: ``bench.py --gpus 2`` under
+    torch.distributed.run with both ranks on this box's one GPU (bench.py gpu_index: the
+    node-shared rows / results regions open no RCCL communicator, so two ranks may share a
+    device). Every rank ingests requests spread over both owners; the run must finish with both
+    ranks answering, the rows-region mode named in the line and the exchange waits accounted."""
+    import json
+    import subprocess
+    import sys
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "w2.json")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+               "--steps", "2", "--warmup", "1", "--threads", "4", "--rounds", "4", "--accounts", "65536",
+               "--json-out", out]
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        r = subprocess.run(cmd, cwd=root, env=env, timeout=110, capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout[-1500:] + r.stderr[-3000:]
+        with open(out) as f:
+            d = json.load(f)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["value"] > 0
+    assert "node-shared pinned rows region" in d["config"]["serving"]
+    w = d["exchange_waits_us_rank0"]
+    assert w["submits"] > 0 and w["owner_wait_max_us"] >= 0
