@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="per-GPU micro-batch (default: the config's)")
     ap.add_argument("--accounts", type=int, default=1 << 20, help="feature-store accounts per GPU")
     ap.add_argument("--depth", type=int, default=0,
-                    help="pipeline depth (batches in flight; up to 7, launch.h DEDUP_AHEAD); default 4 for the "
+                    help="pipeline depth (batches in flight; up to 7, launch.h DEDUP_AHEAD); default 6 for the "
                          "fraud configs, 3 for cfg4 / cfg5 (one stream per slot: a fourth slot stream plus the "
                          "default stream exceed the box's 4 hardware queues - same-box A/B cfg4 135.5 vs 105.7 M, "
                          "cfg5 2.62 vs 2.42 M, profiles/r6/a)")
@@ -118,7 +118,11 @@ def parse():
         a.scope = "serving"
     a.depth_given = a.depth > 0
     if a.depth <= 0:
-        a.depth = 3 if a.config in ("cfg4", "cfg5") else 4
+        # fraud configs: 6 slots - a serving slot stays held while its caller copies the step's
+        # results and feature images out (~72 us), so at 4 the stepper waited for a slot 1.2 times
+        # per step; same box, interleaved, 2 runs each: depth 4 / 5 / 6 / 7 = 116.8-121.0 /
+        # 118.8-120.3 / 122.7-127.4 / 123.1-128.4 M (profiles/r6/ad)
+        a.depth = 3 if a.config in ("cfg4", "cfg5") else 6
     return a
 
 

@@ -36,7 +36,8 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 
 
-def build(accounts: int, abuse_max_batch: int = 0, abuse_priority: bool = False, acct_depth: int = 2):
+def build(accounts: int, abuse_max_batch: int = 0, abuse_priority: bool = False, acct_depth: int = 2,
+          serve_depth: int = 0):
     """One engine: cfg3 fraud model (8192-row micro-batches), cfg4 LTV MLP, cfg5 abuse GRU; warehouse
     rows + ext rows for every account, profile rows for the LTV model, full event rings."""
     import bench_e2e as E
@@ -52,6 +53,8 @@ def build(accounts: int, abuse_max_batch: int = 0, abuse_priority: bool = False,
     cfg.abuse.max_batch = abuse_max_batch
     cfg.abuse.high_priority = abuse_priority
     cfg.gpu.acct_depth = acct_depth
+    if serve_depth > 0:
+        cfg.gpu.serve_depth = serve_depth
     eng = RiskEngine(cfg, backend="gpu", capacity=accounts + 4096, fraud_model=E.fraud_model_bytes("cfg3"),
                      ltv_model=builders.build("ltv_mlp", n_features=256, width=512, layers=4).SerializeToString(),
                      abuse_model=builders.build("gru", seq=100, in_dim=16, hidden=256).SerializeToString())
@@ -137,6 +140,7 @@ def main(argv=None) -> int:
     ap.add_argument("--abuse-max-batch", type=int, default=0, help="AbuseConfig.max_batch (0: the largest bucket)")
     ap.add_argument("--abuse-priority", type=int, default=0, help="AbuseConfig.high_priority")
     ap.add_argument("--acct-depth", type=int, default=2, help="GpuConfig.acct_depth (abuse device slots)")
+    ap.add_argument("--serve-depth", type=int, default=0, help="GpuConfig.serve_depth (scoring pipeline slots; 0: the config's)")
     ap.add_argument("--batch-rate", type=float, default=0.0,
                     help="ScoreBatch requests/s, paced open loop over --threads (0: closed loop)")
     ap.add_argument("--json-out", default="")
@@ -144,7 +148,7 @@ def main(argv=None) -> int:
     import bench_e2e as E
     from igaming_platform_amd.api.native_grpc import NativeRiskServer
     from igaming_platform_amd.utils.synth import NOW0
-    eng = build(a.accounts, a.abuse_max_batch, bool(a.abuse_priority), a.acct_depth)
+    eng = build(a.accounts, a.abuse_max_batch, bool(a.abuse_priority), a.acct_depth, a.serve_depth)
     srv = NativeRiskServer(eng, port=0, workers=a.server_workers, batching=True).start()
     payloads = E.spread_payloads(a.accounts, 64, 8192, seed=11)
     abuse_p = E.acct_payloads(a.accounts, "abuse", 1 << 16, 300)
@@ -203,7 +207,7 @@ def main(argv=None) -> int:
                config=dict(scorebatch_threads=a.threads, clients_per_rpc=a.clients, server_workers=a.server_workers,
                            scorebatch_offered_per_s=(a.batch_rate * 8192 if a.batch_rate > 0 else "closed loop"),
                            abuse_max_batch=a.abuse_max_batch, abuse_high_priority=bool(a.abuse_priority),
-                           acct_depth=a.acct_depth,
+                           acct_depth=a.acct_depth, serve_depth=eng.cfg.gpu.serve_depth,
                            models="cfg3 GBDT(100,d7,128f)+MLP(32-256-1) fp32; cfg5 GRU 2x256 x 100 events fp32 split"),
                server_stats=srv.stats(), serve_core_mixed=serve)
     srv.stop()
