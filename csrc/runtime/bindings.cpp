@@ -784,8 +784,9 @@ PYBIND11_MODULE(_native, m) {
   py::class_<PyServe, std::shared_ptr<PyServe>>(m, "ServeCore")
       .def(py::init([](std::vector<std::shared_ptr<AccountIndex>> idx, py::object dev, int rank,
                        std::shared_ptr<StepClock> clock, int max_wait_us, int64_t timeout_us, int finishers,
-                       bool features, int32_t seq0) {
+                       bool features, int32_t seq0, int unary_depth) {
              ServeCore::Options o;
+             o.unary_depth = unary_depth;
              o.max_wait_us = max_wait_us;
              o.timeout_us = timeout_us;
              o.finishers = finishers;
@@ -800,7 +801,7 @@ PYBIND11_MODULE(_native, m) {
            }),
            py::arg("indexes"), py::arg("device"), py::arg("rank") = 0, py::arg("clock") = nullptr,
            py::arg("max_wait_us") = 200, py::arg("timeout_us") = -1, py::arg("finishers") = 2,
-           py::arg("features") = true, py::arg("seq0") = 0)
+           py::arg("features") = true, py::arg("seq0") = 0, py::arg("unary_depth") = 0)
       .def("score_batch", [](PyServe& s, py::bytes data, int64_t now, int64_t t0_ns) {
         char* p; py::ssize_t n;
         PYBIND11_BYTES_AS_STRING_AND_SIZE(data.ptr(), &p, &n);

@@ -445,7 +445,7 @@ void ServeCore::submit_tx_many(const TxCall* calls, size_t n, int64_t now) {
   {
     std::lock_guard<std::mutex> lk(q_mu_);
     stopped = stopping_ || stopped_;
-    if (!stopped)
+    if (!stopped) {
       for (Item* it : items)
         if (it) {
           it->remaining = int64_t(it->n);
@@ -453,6 +453,8 @@ void ServeCore::submit_tx_many(const TxCall* calls, size_t n, int64_t now) {
           uqueue_.push_back(it);
           queued_rows_ += int64_t(it->n);
         }
+      last_unary_ns_ = t_enq;
+    }
   }
   if (stopped) {
     for (size_t k = 0; k < n; ++k)
@@ -521,7 +523,11 @@ int ServeCore::pending_items() {
 // region and generation flags by slot (with a free-slot stack, ranks released steps in
 // different orders and could run one step on different slots). Direct mode: any free slot.
 int ServeCore::next_slot_locked() const {
-  if (!exchange_) return free_slots_.empty() ? -1 : free_slots_.back();
+  if (!exchange_) {
+    if (free_slots_.empty()) return -1;
+    if (opt_.unary_depth > 0 && inflight_ >= opt_.unary_depth && now_ns() - last_unary_ns_ < kUnaryWindowNs) return -1;
+    return free_slots_.back();
+  }
   const int s = int(issued_.load() % int64_t(depth_));
   return std::find(free_slots_.begin(), free_slots_.end(), s) != free_slots_.end() ? s : -1;
 }

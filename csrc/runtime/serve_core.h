@@ -110,7 +110,14 @@ class ServeCore {
     bool features = true;        // responses carry the FeatureVector (risk.proto:73)
     int64_t stop_timeout_us = 30000000;
     int32_t seq0 = 0;            // batch sequence to continue from (dedup-ring rotation on device)
+    // steps in flight while unary calls arrived in the last kUnaryWindowNs (0: the full depth):
+    // deep pipelines serve bulk ScoreBatch traffic, but a unary call's step queues behind every
+    // step ahead of it on the device (mixed traffic at depth 6 vs 4: abuse / tx p99 2.8-7.5 /
+    // 2.4-16.6 vs 2.2-2.3 / 0.8-1.0 ms, profiles/r6/af). Direct (single-GPU) mode only: exchange
+    // ranks issue their steps in lockstep
+    int unary_depth = 0;
   };
+  static constexpr int64_t kUnaryWindowNs = 20000000;
 
   // indexes: one per owner (world entries); dev: the device function table (owned by the
   // device object, which must outlive the core or be swapped out while paused); clock:
@@ -248,6 +255,7 @@ class ServeCore {
   std::vector<int> free_slots_;
   std::vector<std::unique_ptr<Step>> steps_;  // by slot
   int inflight_ = 0;
+  int64_t last_unary_ns_ = 0;  // under q_mu_: the latest unary call's enqueue time
   bool stopping_ = false, stopped_ = false, paused_ = false, pause_req_ = false, aborting_ = false;
   int64_t hold_gen_ = 0;              // generation the stepper converges to (0: none)
   bool held_ = false;

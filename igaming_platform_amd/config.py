@@ -144,7 +144,8 @@ class GPUConfig:
     # native serving core (csrc/runtime/serve_core.cpp, engine/serving.py): request bytes ->
     # response bytes without Python on the hot path; the unary micro-batcher is its FIFO
     native_serving: bool = True
-    serve_depth: int = 4          # pipeline slots (batches in flight) of a shard's device (<= 7)
+    serve_depth: int = 6          # pipeline slots (batches in flight) of a shard's device (<= 7; profiles/r6/ad)
+    unary_depth: int = 4          # steps in flight while unary calls are arriving (ServeCore Options.unary_depth)
     serve_finishers: int = 2      # unary response threads
     exchange_timeout_s: float = 10.0  # multi-rank step deadline: a peer that misses it failed
     # native account RPCs (csrc/runtime/acct_core.cpp, engine/acct.py): PredictLTV,

@@ -53,7 +53,8 @@ def make_core(indexes: Sequence, device, cfg, rank: int = 0, clock=None, seq0: i
     g = cfg.gpu
     timeout_us = int(g.batch_timeout_ms * 1000) if g.batch_timeout_ms > 0 else -1
     return native().ServeCore(list(indexes), device, rank, clock, max_wait_us=int(g.wait_us), timeout_us=timeout_us,
-                               finishers=int(g.serve_finishers), features=features, seq0=int(seq0))
+                               finishers=int(g.serve_finishers), features=features, seq0=int(seq0),
+                               unary_depth=int(g.unary_depth))
 
 
 def shm_token() -> str:
