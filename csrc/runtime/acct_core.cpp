@@ -872,8 +872,17 @@ void AcctRouter::submit_many(uint8_t rpc, const std::string_view* data, const ui
     return;
   }
   const uint64_t ticket = links_ ? links_->ticket() : 0;
-  std::vector<AcctCore::Call> calls;
-  calls.reserve(n);
+  // parse every call, then resolve this rank's accounts in one batched index lookup (probe lines
+  // prefetched for the whole range: one overlapped round of cache misses, not one per call)
+  thread_local std::vector<std::string_view> acc;
+  thread_local std::vector<uint64_t> hs;
+  thread_local std::vector<uint8_t> mine;
+  thread_local std::vector<int32_t> slots;
+  acc.assign(n, std::string_view());
+  hs.assign(n, 0);
+  mine.assign(n, 0);
+  slots.assign(n, -1);
+  size_t n_mine = 0;
   for (size_t k = 0; k < n; ++k) {
     std::string_view account, bonus;
     try {
@@ -892,12 +901,22 @@ void AcctRouter::submit_many(uint8_t rpc, const std::string_view* data, const ui
       submit(rpc, data[k].data(), data[k].size(), tags[k], t0_ns[k], now);
       continue;
     }
-    const int32_t slot = idx_[size_t(owner)]->find(account, h);
+    acc[k] = account;
+    hs[k] = h;
+    mine[k] = 1;
+    ++n_mine;
+  }
+  if (n_mine) idx_[size_t(rank_)]->lookup_views(acc.data(), hs.data(), n, false, slots.data(), nullptr, mine.data());
+  std::vector<AcctCore::Call> calls;
+  calls.reserve(n_mine);
+  for (size_t k = 0; k < n; ++k) {
+    if (!mine[k]) continue;
+    const int32_t slot = slots[k];
     if (rpc == RPC_ABUSE && slot < 0) {  // as local(): an unknown account has nothing to check
       answer_now(-1, tags[k], std::string(), std::string());
       continue;
     }
-    calls.push_back(AcctCore::Call{rpc, slot, account, tags[k], now, t0_ns[k], ticket});
+    calls.push_back(AcctCore::Call{rpc, slot, acc[k], tags[k], now, t0_ns[k], ticket});
   }
   try {
     c->submit_many(calls.data(), calls.size());

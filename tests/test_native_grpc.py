@@ -168,3 +168,40 @@ def test_native_load_generator_against_the_native_server(nstack):
     r = native().grpc_load("127.0.0.1", srv.port, P.method_path("ScoreTransaction"), body, 1000.0, 1.0, 4, 512)
     assert r["errors"] == 0 and r["sent"] == 1000 and len(r["latency_ms"]) == 1000
     assert float(np.median(r["latency_ms"])) < 1000 and r["elapsed"] >= 1.0
+
+
+def test_unary_in_flight_cap_with_concurrent_batches():
+    """ServeCore Options.unary_depth (GpuConfig.unary_depth): while unary calls arrive the core
+    keeps at most that many steps in flight, the full serve_depth otherwise. With a cap of 1
+    under concurrent ScoreTransaction and ScoreBatch traffic every call is still answered, and a
+    batch's rows all see the account's 128 earlier rows (8 batches x 16) in their 1-minute window."""
+    cfg = Config()
+    cfg.gpu.serve_depth, cfg.gpu.unary_depth = 4, 1
+    eng = RiskEngine(cfg, backend="cpu", capacity=4000)
+    srv = NativeRiskServer(eng, port=0, workers=2).start()
+    addr = f"127.0.0.1:{srv.port}"
+    chans = [grpc.insecure_channel(addr) for _ in range(4)]
+    try:
+        tx = [c.unary_unary(P.method_path("ScoreTransaction")) for c in chans]
+        sb = chans[0].unary_unary(P.method_path("ScoreBatch"))
+        req = [P.ScoreTransactionRequest(account_id=f"ud-{i % 50}", amount=100 + i, transaction_type="bet")
+               .SerializeToString() for i in range(400)]
+        body = P.ScoreBatchRequest(transactions=[P.ScoreTransactionRequest(
+            account_id="ud-batch", amount=10, transaction_type="bet")] * 16).SerializeToString()
+
+        def one(i):
+            if i % 50 == 0:
+                return len(P.ScoreBatchResponse.FromString(sb(body, timeout=30)).results)
+            return P.ScoreTransactionResponse.FromString(tx[i % 4](req[i], timeout=30)).action
+        with ThreadPoolExecutor(16) as ex:
+            out = list(ex.map(one, range(400)))
+        assert all(o == 16 for i, o in enumerate(out) if i % 50 == 0)
+        assert all(1 <= o <= 3 for i, o in enumerate(out) if i % 50)
+        # the batch account's rows: 8 earlier batches x 16 rows, scored at the batch clock
+        last = P.ScoreBatchResponse.FromString(sb(body, timeout=30))
+        assert {r.features.tx_count_1m for r in last.results} == {8 * 16}
+    finally:
+        for c in chans:
+            c.close()
+        srv.stop()
+        eng.close()
