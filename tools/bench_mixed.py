@@ -80,7 +80,7 @@ def batch_load(eng, payloads, threads: int, seconds: float, t_base: int, rows_pe
     latency from the due time). Returns (rows/s, p50, p99 ms, requests)."""
     core = eng.core
     lock = threading.Lock()
-    lat, rows = [], [0]
+    lat, rows, starts = [], [0], []
     t_start = time.perf_counter()
     t_end = t_start + seconds
     counter = [0]
@@ -107,12 +107,14 @@ def batch_load(eng, payloads, threads: int, seconds: float, t_base: int, rows_pe
                 raise RuntimeError("empty ScoreBatch response")
             with lock:
                 lat.append(dt)
+                starts.append(t0 / 1e6 - t_start * 1e3)
                 rows[0] += rows_per_request
     th = [threading.Thread(target=worker, args=(w,)) for w in range(threads)]
     t0 = time.perf_counter()
     [t.start() for t in th]
     [t.join() for t in th]
     el = time.perf_counter() - t0
+    batch_load.stalls = stall_windows(np.asarray(starts), np.asarray(lat), 5.0)
     return rows[0] / el, float(np.percentile(lat, 50)), float(np.percentile(lat, 99)), counter[0]
 
 
@@ -125,7 +127,22 @@ def open_loop(port: int, rpc: str, payloads, rate: float, seconds: float, conns:
     out[rpc] = dict(offered_per_s=rate, achieved_per_s=round(len(lat) / float(r["elapsed"]), 1), calls=int(r["sent"]),
                     errors=int(r["errors"]),
                     p50_ms=round(float(np.percentile(lat, 50)), 3) if len(lat) else None,
-                    p99_ms=round(float(np.percentile(lat, 99)), 3) if len(lat) else None)
+                    p99_ms=round(float(np.percentile(lat, 99)), 3) if len(lat) else None,
+                    stall_windows=stall_windows(np.asarray(r["sched_ms"]), lat, 5.0))
+
+
+def stall_windows(t_ms, lat_ms, over_ms: float, bin_ms: float = 50.0, top: int = 12):
+    """Where a run's tail comes from: the 50-ms windows (by scheduled send / start time) whose
+    worst latency exceeds ``over_ms``, as [window start ms, calls in it, calls over, worst ms]."""
+    if len(t_ms) == 0 or len(t_ms) != len(lat_ms):
+        return []
+    b = (np.asarray(t_ms) // bin_ms).astype(np.int64)
+    out = []
+    for w in np.unique(b[lat_ms > over_ms]):
+        m = b == w
+        out.append([int(w * bin_ms), int(m.sum()), int((lat_ms[m] > over_ms).sum()), round(float(lat_ms[m].max()), 2)])
+    out.sort(key=lambda x: -x[3])
+    return sorted(out[:top])
 
 
 def main(argv=None) -> int:
@@ -190,7 +207,10 @@ def main(argv=None) -> int:
                scorebatch_alone=dict(scores_per_s=round(alone[0], 1), p50_ms=round(alone[1], 3), p99_ms=round(alone[2], 3),
                                      requests=alone[3]),
                scorebatch_mixed=dict(scores_per_s=round(mixed[0], 1), p50_ms=round(mixed[1], 3), p99_ms=round(mixed[2], 3),
-                                     requests=mixed[3]),
+                                     requests=mixed[3], stall_windows=batch_load.stalls),
+               stall_windows_what="[window start ms, calls, calls over 5 ms, worst ms] per 50-ms window with a call over "
+                                  "5 ms; ScoreBatch windows by request start, unary windows by scheduled send (the load "
+                                  "generator starts its schedule ~200 ms after the ScoreBatch threads)",
                scorebatch_loss_pct=round(100.0 * (1 - mixed[0] / alone[0]), 2),
                check_bonus_abuse=res.get("abuse"), score_transaction=res.get("tx"),
                unary_without_scorebatch=dict(check_bonus_abuse=solo.get("abuse"), score_transaction=solo.get("tx")),
