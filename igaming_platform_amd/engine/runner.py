@@ -19,16 +19,18 @@ from ..ops import kernels as K
 
 def tree_groups(step, bucket: int) -> int:
     """Split the trees of one ensemble into ``g`` groups so a small batch still fills the
-    256 CUs (>= 256 workgroups, one per CU), without shrinking a group below 8 trees. The
-    target was 512 workgroups until round 5: at 8192 rows, 2 groups instead of 4 leave more of
-    the chip to the K1 / dedup-insert kernels running beside the trees - engine_only 151 vs 139 M
-    scores/s, serving unchanged (5 interleaved pairs 117.7 vs 117.8 M); 1 group (128
-    workgroups) drops to 91 M (profiles/r5/eng/groups)."""
+    256 CUs, without shrinking a group below 8 trees: >= 384 workgroups (3 groups at 8192 rows).
+    Round 5 moved the target from 512 to 256 workgroups (at 8192 rows 2 groups instead of 4
+    left more of the chip to K1 / the dedup insert: engine_only 151 vs 139 M, profiles/r5/eng/
+    groups). After round 6's LDS traversal rework and at serving depth 6, 3 groups measured best
+    (same box, interleaved: 2 / 3 / 4 groups engine_only 149.4 / 151.0 / 147.5 M, serving
+    120.1 / 127.1 / 127.0 M, profiles/r6/al; 3 pairs 2 vs 3 groups: serving 119.7 / 122.8 / 122.7
+    vs 125.5 / 126.4 / 127.1 M, engine_only flat, profiles/r6/am); 1 group drops to 91 M."""
     forced = int(os.environ.get("IGP_TREE_GROUPS", "0"))  # same-box A/B override
     if forced > 0:
         return max(1, min(forced, step.n_trees))
     tiles = -(-bucket // 64)
-    return max(1, min(max(1, step.n_trees // 8), -(-256 // tiles)))
+    return max(1, min(max(1, step.n_trees // 8), -(-384 // tiles)))
 
 
 class GruModel:
