@@ -44,7 +44,7 @@ from ..layouts import REQREC
 from ..native import hipk
 from ..ops import kernels as K
 from ..parallel.exchange import FEAT_BYTES, RES_BYTES, build_chunks, gather_results, result_width
-from .scorer import HDR_BYTES, GpuScorer
+from .scorer import GpuScorer
 
 REQ = REQREC.itemsize
 
