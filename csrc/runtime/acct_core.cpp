@@ -202,16 +202,21 @@ bool AcctCore::issue(std::unique_lock<std::mutex>& lk) {
   const size_t n = std::min(queue_.size(), size_t(cap_));
   const int why = queue_.size() >= size_t(cap_) ? 0 : inflight_ == 0 ? 1 : 2;
   const int64_t t_free = st->t_release;
-  st->items.reserve(n);
   int64_t now = 0;
-  for (size_t k = 0; k < n; ++k) {
-    now = std::max(now, queue_.front().now);
-    st->items.push_back(std::move(queue_.front()));
-    queue_.pop_front();
+  const bool whole = queue_.head == 0 && n == queue_.v.size();
+  if (whole) {
+    st->items.swap(queue_.v);  // the step's old (cleared) vector becomes the queue's storage
+  } else {
+    st->items.reserve(n);
+    for (size_t k = 0; k < n; ++k) {
+      st->items.push_back(std::move(queue_.front()));
+      queue_.pop_front();
+    }
   }
   ++inflight_;
   const IgpModelOps* dev = dev_;
   lk.unlock();
+  for (const Item& it : st->items) now = std::max(now, it.now);
   int32_t* sl = dev->slots(dev->ctx, slot);
   for (size_t k = 0; k < n; ++k) sl[k] = st->items[k].slot;
   char err[256] = {0};

@@ -163,7 +163,27 @@ class AcctCore {
 
   std::mutex q_mu_;
   std::condition_variable q_cv_, idle_cv_;
-  std::deque<Item> queue_;
+  // FIFO of queued calls: a vector with a head index. A step that takes the whole queue swaps
+  // the storage with its item vector (O(1) under the queue lock, which the submitting threads
+  // also take); a partial take moves items and compacts once the consumed head passes half
+  struct ItemQueue {
+    std::vector<Item> v;
+    size_t head = 0;
+    bool empty() const { return head == v.size(); }
+    size_t size() const { return v.size() - head; }
+    Item& front() { return v[head]; }
+    void push_back(Item&& it) { v.push_back(std::move(it)); }
+    void pop_front() {
+      if (++head == v.size()) {
+        v.clear();
+        head = 0;
+      } else if (head >= 4096 && 2 * head >= v.size()) {
+        v.erase(v.begin(), v.begin() + std::ptrdiff_t(head));
+        head = 0;
+      }
+    }
+  };
+  ItemQueue queue_;
   std::vector<int> free_slots_;
   std::vector<std::unique_ptr<Step>> steps_;
   int inflight_ = 0;
